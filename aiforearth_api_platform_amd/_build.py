@@ -1,0 +1,108 @@
+"""In-tree native build: the C++ control-plane core and the gfx950 HIP kernel library.
+
+Both artefacts land inside the package directory so they travel with the repo snapshot to
+the GPU box (see README "Build"):
+
+* ``_ai4e_core<EXT_SUFFIX>`` — pybind11 module (task store + dispatch queue), g++ -O3.
+* ``_lib/libai4e_kernels.so`` — hand-written CDNA4 kernels (``csrc/kernels/*.hip``) built
+  with ``hipcc --offload-arch=gfx950`` and exposed through a plain C ABI consumed via ctypes
+  (no torch headers in the kernel TU => seconds per file, no JIT cache under ~/.cache).
+
+Rebuilds are incremental on source mtime.  ``python -m aiforearth_api_platform_amd._build``.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import os
+import shutil
+import subprocess
+import sys
+import sysconfig
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+ROOT = PKG.parent
+CSRC = ROOT / "csrc"
+LIBDIR = PKG / "_lib"
+OBJDIR = ROOT / "build" / "obj"
+ARCH = os.environ.get("AI4E_OFFLOAD_ARCH", "gfx950")
+
+CORE_SO = PKG / ("_ai4e_core" + sysconfig.get_config_var("EXT_SUFFIX"))
+KERNEL_SO = LIBDIR / "libai4e_kernels.so"
+
+
+def _hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if cand and Path(cand).exists():
+            return cand
+    raise RuntimeError("hipcc not found (ROCm toolchain required to build the gfx950 kernels)")
+
+
+def _stale(out: Path, deps) -> bool:
+    if not out.exists():
+        return True
+    t = out.stat().st_mtime
+    return any(Path(d).stat().st_mtime > t for d in deps)
+
+
+def _run(cmd, verbose):
+    if verbose:
+        print(" ".join(map(str, cmd)), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"build failed ({r.returncode}): {' '.join(map(str, cmd))}\n{r.stdout}\n{r.stderr}")
+    return r
+
+
+def build_core(verbose: bool = False, force: bool = False) -> Path:
+    src = sorted((CSRC / "core").glob("*.cpp"))
+    if not force and not _stale(CORE_SO, src):
+        return CORE_SO
+    import pybind11
+
+    cxx = os.environ.get("CXX", "g++")
+    cmd = [cxx, "-O3", "-std=c++17", "-shared", "-fPIC", "-fvisibility=hidden", "-Wall",
+           f"-I{sysconfig.get_paths()['include']}", f"-I{pybind11.get_include()}",
+           *map(str, src), "-o", str(CORE_SO), "-lpthread"]
+    extra = os.environ.get("AI4E_CORE_CXXFLAGS")  # e.g. "-fsanitize=thread -g" for the TSAN build
+    if extra:
+        cmd[1:1] = extra.split()
+    _run(cmd, verbose)
+    return CORE_SO
+
+
+def _kernel_sources():
+    return sorted((CSRC / "kernels").glob("*.hip"))
+
+
+def build_kernels(verbose: bool = False, force: bool = False, jobs: int = 8) -> Path:
+    srcs = _kernel_sources()
+    headers = sorted((CSRC / "kernels").glob("*.h"))
+    LIBDIR.mkdir(parents=True, exist_ok=True)
+    OBJDIR.mkdir(parents=True, exist_ok=True)
+    hipcc = _hipcc()
+    flags = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
+             "-Wno-unused-result", f"-I{CSRC / 'kernels'}"]
+
+    def one(src: Path) -> Path:
+        obj = OBJDIR / (src.stem + ".o")
+        if force or _stale(obj, [src, *headers]):
+            _run([hipcc, *flags, "-c", str(src), "-o", str(obj)], verbose)
+        return obj
+
+    with cf.ThreadPoolExecutor(max_workers=max(1, min(jobs, len(srcs) or 1))) as ex:
+        objs = list(ex.map(one, srcs))
+    if force or _stale(KERNEL_SO, objs):
+        _run([hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs), "-o", str(KERNEL_SO)],
+             verbose)
+    return KERNEL_SO
+
+
+def build_all(verbose: bool = False, force: bool = False) -> None:
+    build_core(verbose=verbose, force=force)
+    build_kernels(verbose=verbose, force=force)
+
+
+if __name__ == "__main__":
+    build_all(verbose=True, force="--force" in sys.argv)
+    print("built:", CORE_SO, KERNEL_SO)

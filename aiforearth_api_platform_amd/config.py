@@ -1,0 +1,137 @@
+"""Single configuration object for the platform.
+
+Collapses the reference's three string-env tiers into one dataclass
+(survey §5.6):
+
+1. platform flags of ``InfrastructureDeployment/setup_env.sh:3-82`` (transport type, retry delay,
+   max deliveries, Redis timeouts -> store/queue knobs),
+2. function-app settings (``deploy_cache_manager.sh:36-150``, ``deploy_backend_queue_function.sh``),
+3. container env of the Helm charts (``APIs/Charts/templates/async-gpu/templates/deployment.yaml:23-49``)
+   read by ``APIs/1.0/base-py/ai4e_service.py:19-22,51``.
+
+Precedence: explicit overrides (CLI flags) > environment variables > YAML file > defaults.
+The container env names are kept verbatim; GPU knobs use the ``AI4E_`` prefix.
+"""
+from __future__ import annotations
+
+import dataclasses
+import os
+from dataclasses import dataclass, field, fields
+from typing import Any, Dict, Optional
+
+
+def _as_bool(v: Any) -> bool:
+    if isinstance(v, bool):
+        return v
+    return str(v).strip().lower() in ("1", "true", "yes", "on", "y")
+
+
+@dataclass
+class Config:
+    # --- container runtime (ai4e_service.py / deployment.yaml) ---
+    api_prefix: str = field(default="", metadata={"env": "API_PREFIX"})
+    cache_connector_upsert_uri: str = field(default="", metadata={"env": "CACHE_CONNECTOR_UPSERT_URI"})
+    cache_connector_get_uri: str = field(default="", metadata={"env": "CACHE_CONNECTOR_GET_URI"})
+    current_processing_upsert_uri: str = field(default="", metadata={"env": "CURRENT_PROCESSING_UPSERT_URI"})
+    # Reference default 'True' (ai4e_service.py:19). Parsed as a real bool here (Appendix B #2 fix).
+    disable_current_request_metric: bool = field(default=True, metadata={"env": "DISABLE_CURRENT_REQUEST_METRIC"})
+    service_cluster: str = field(default="undefined", metadata={"env": "SERVICE_CLUSTER"})
+    service_owner: str = field(default="AI4E", metadata={"env": "SERVICE_OWNER"})
+    service_name: str = field(default="ai4e-mi355x", metadata={"env": "SERVICE_NAME"})
+    service_version: str = field(default="1.0", metadata={"env": "SERVICE_VERSION"})
+    service_model_name: str = field(default="", metadata={"env": "SERVICE_MODEL_NAME"})
+    service_model_framework: str = field(default="pytorch-rocm", metadata={"env": "SERVICE_MODEL_FRAMEWORK"})
+    service_model_framework_version: str = field(default="", metadata={"env": "SERVICE_MODEL_FRAMEOWRK_VERSION"})
+    service_model_version: str = field(default="", metadata={"env": "SERVICE_MODEL_VERSION"})
+    service_container_name: str = field(default="", metadata={"env": "SERVICE_CONTAINER_NAME"})
+    service_container_version: str = field(default="", metadata={"env": "SERVICE_CONTAINER_VERSION"})
+    next_api_name_in_pipeline: str = field(default="", metadata={"env": "NEXT_API_NAME_IN_PIPELINE"})
+    debug: bool = field(default=False, metadata={"env": "DEBUG"})
+    # --- transport / dispatcher (setup_env.sh:65-74, BackendQueueProcessor/host.json) ---
+    transport: str = field(default="inproc", metadata={"env": "AI4E_TRANSPORT"})  # inproc|queue|eventgrid
+    queue_retry_delay_ms: int = field(default=60000, metadata={"env": "QUEUE_RETRY_DELAY_MS"})
+    max_delivery_count: int = field(default=1440, metadata={"env": "SERVICEBUS_QUEUE_MAX_DELIVERY_COUNT"})
+    queue_lock_duration_s: float = field(default=300.0, metadata={"env": "AI4E_QUEUE_LOCK_DURATION_S"})
+    queue_max_size: int = field(default=0, metadata={"env": "AI4E_QUEUE_MAX_SIZE"})
+    dispatch_concurrency: int = field(default=1, metadata={"env": "AI4E_DISPATCH_CONCURRENCY"})
+    eventgrid_max_delivery_attempts: int = field(default=3, metadata={"env": "AI4E_EVENTGRID_MAX_ATTEMPTS"})
+    eventgrid_event_ttl_s: float = field(default=300.0, metadata={"env": "AI4E_EVENTGRID_TTL_S"})
+    # --- task store (Redis replacement) ---
+    store_backend: str = field(default="native", metadata={"env": "AI4E_STORE_BACKEND"})  # native|python
+    journal_path: str = field(default="", metadata={"env": "AI4E_JOURNAL"})
+    finished_task_ttl_s: float = field(default=3600.0, metadata={"env": "AI4E_FINISHED_TASK_TTL_S"})
+    # --- metrics timers (TaskQueueLogger.cs:20 / TaskProcessLogger.cs:22) ---
+    queue_logger_period_s: float = field(default=30.0, metadata={"env": "AI4E_QUEUE_LOGGER_PERIOD_S"})
+    process_logger_period_s: float = field(default=300.0, metadata={"env": "AI4E_PROCESS_LOGGER_PERIOD_S"})
+    # --- GPU worker pool / batcher ---
+    num_gpus: int = field(default=1, metadata={"env": "AI4E_NUM_GPUS"})
+    max_batch: int = field(default=256, metadata={"env": "AI4E_MAX_BATCH"})
+    max_batch_delay_ms: float = field(default=2.0, metadata={"env": "AI4E_MAX_BATCH_DELAY_MS"})
+    dtype: str = field(default="bf16", metadata={"env": "AI4E_DTYPE"})
+    kernel_backend: str = field(default="auto", metadata={"env": "AI4E_KERNEL_BACKEND"})  # auto|hip|torch
+    use_hip_graphs: bool = field(default=True, metadata={"env": "AI4E_HIP_GRAPHS"})
+    heartbeat_interval_s: float = field(default=1.0, metadata={"env": "AI4E_HEARTBEAT_S"})
+    heartbeat_timeout_s: float = field(default=30.0, metadata={"env": "AI4E_HEARTBEAT_TIMEOUT_S"})
+    max_batch_retries: int = field(default=3, metadata={"env": "AI4E_MAX_BATCH_RETRIES"})
+    fault_injection: str = field(default="", metadata={"env": "AI4E_FAULT_INJECTION"})
+    # --- gateway ---
+    host: str = field(default="127.0.0.1", metadata={"env": "AI4E_HOST"})
+    port: int = field(default=8080, metadata={"env": "AI4E_PORT"})
+    routes_file: str = field(default="", metadata={"env": "AI4E_ROUTES"})
+
+    @classmethod
+    def load(cls, yaml_path: Optional[str] = None, env: Optional[Dict[str, str]] = None,
+             **overrides: Any) -> "Config":
+        env = os.environ if env is None else env
+        values: Dict[str, Any] = {}
+        yaml_path = yaml_path or env.get("AI4E_CONFIG")
+        if yaml_path:
+            import yaml
+
+            with open(yaml_path) as f:
+                doc = yaml.safe_load(f) or {}
+            values.update({k: v for k, v in doc.items() if k in {f.name for f in fields(cls)}})
+        for f in fields(cls):
+            name = f.metadata.get("env")
+            if name and name in env:
+                values[f.name] = env[name]
+        values.update({k: v for k, v in overrides.items() if v is not None})
+        cfg = cls()
+        for f in fields(cls):
+            if f.name in values:
+                setattr(cfg, f.name, _coerce(f, values[f.name]))
+        return cfg
+
+    def replace(self, **kw: Any) -> "Config":
+        return dataclasses.replace(self, **kw)
+
+    def as_dict(self) -> Dict[str, Any]:
+        return dataclasses.asdict(self)
+
+
+def _coerce(f: dataclasses.Field, v: Any) -> Any:
+    t = f.type if isinstance(f.type, str) else getattr(f.type, "__name__", str(f.type))
+    if v is None:
+        return f.default
+    if t == "bool":
+        return _as_bool(v)
+    if t == "int":
+        return int(v)
+    if t == "float":
+        return float(v)
+    return str(v)
+
+
+_GLOBAL: Optional[Config] = None
+
+
+def get_config() -> Config:
+    global _GLOBAL
+    if _GLOBAL is None:
+        _GLOBAL = Config.load()
+    return _GLOBAL
+
+
+def set_config(cfg: Config) -> None:
+    global _GLOBAL
+    _GLOBAL = cfg

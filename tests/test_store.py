@@ -1,0 +1,156 @@
+"""Task store + dispatch queue: semantics of the reference's Redis/Service Bus usage, both backends."""
+import json
+import time
+
+import pytest
+
+from aiforearth_api_platform_amd.store import make_queue, make_store, pystore
+
+
+def test_upsert_insert_assigns_guid_and_indexes(backend):
+    s = make_store(backend=backend)
+    js, pub = s.upsert("", "created", "created", "http://10.1.2.3/v1/camera-trap/detect", '{"x": 1}', True)
+    t = json.loads(js)
+    assert list(t.keys()) == ["TaskId", "Timestamp", "Status", "BackendStatus", "Endpoint", "Body",
+                              "PublishToGrid", "EndpointPath"]
+    assert len(t["TaskId"]) == 36 and t["TaskId"][14] == "4"
+    assert t["Body"] is None and t["PublishToGrid"] is True
+    assert t["EndpointPath"] == "/v1/camera-trap/detect"
+    assert pub == '{"x": 1}'
+    assert s.get_orig_body(t["TaskId"]) == '{"x": 1}'
+    assert s.zcard("/v1/camera-trap/detect_created") == 1
+
+
+def test_state_transitions_move_index_membership(backend):
+    s = make_store(backend=backend)
+    tid = json.loads(s.upsert("", "created", "created", "http://h/v1/a", None, False)[0])["TaskId"]
+    s.upsert(tid, "running - 10%", "running", "http://h/v1/a")
+    assert s.zcard("/v1/a_created") == 0 and s.zcard("/v1/a_running") == 1
+    s.upsert(tid, "completed - result at x", "completed", "http://h/v1/a")
+    assert s.zcard("/v1/a_running") == 0 and s.zcard("/v1/a_completed") == 1
+    rec = json.loads(s.get(tid))
+    assert rec["Status"] == "completed - result at x" and rec["BackendStatus"] == "completed"
+    assert s.get("nope") is None
+
+
+def test_pipeline_publish_reuses_orig_body(backend):
+    s = make_store(backend=backend)
+    tid = json.loads(s.upsert("", "created", "created", "http://h/v1/o/a1", "BODY", True)[0])["TaskId"]
+    # subsequent pipeline call with empty body -> original body is published
+    js, pub = s.upsert(tid, "created", "created", "http://h/v1/o/a2", None, True)
+    assert pub == "BODY"
+    assert s.zcard("/v1/o/a2_created") == 1
+
+
+def test_create_many_and_transition_many_latency(backend):
+    s = make_store(backend=backend)
+    ids = s.create_many("http://h/v1/resnet", 10)
+    assert len(set(ids)) == 10 and s.zcard("/v1/resnet_created") == 10
+    assert s.transition_many(ids, "running", "running") == 10
+    assert s.zcard("/v1/resnet_created") == 0 and s.zcard("/v1/resnet_running") == 10
+    time.sleep(0.002)
+    s.transition_many(ids[:4], "completed", "completed")
+    s.transition_many(ids[4:], "failed", "Task failed - try again")
+    lat = s.latencies(ids)
+    assert len(lat) == 10 and all(x > 0 for x in lat)
+    assert s.keys_with_suffix("_failed") == ["/v1/resnet_failed"]
+    assert s.zrange("/v1/resnet_completed", 2) == s.zrange("/v1/resnet_completed")[:2]
+
+
+def test_counters_and_eviction(backend):
+    s = make_store(backend=backend)
+    assert s.incrby("CURRENT_REQUESTS/c/v1/x", 2) == 2
+    assert s.incrby("CURRENT_REQUESTS/c/v1/x", -1) == 1
+    assert s.get_counter("missing") is None
+    ids = s.create_many("/v1/e", 3)
+    s.transition_many(ids, "completed", "done")
+    assert s.evict_finished(0.0) == 3 and s.size() == 0 and s.zcard("/v1/e_completed") == 0
+
+
+def test_journal_replay(tmp_path, backend):
+    p = str(tmp_path / "journal.jsonl")
+    s = make_store(p, backend=backend)
+    tid = json.loads(s.upsert("", "created", "created", "http://h/v1/j", "B", True)[0])["TaskId"]
+    s.upsert(tid, "running", "running", "http://h/v1/j")
+    other = s.create_many("http://h/v1/j", 2)
+    s.flush()
+    del s
+    s2 = make_store(backend=backend)
+    assert s2.replay(p) == 4
+    assert json.loads(s2.get(tid))["BackendStatus"] == "running"
+    assert s2.zcard("/v1/j_running") == 1 and s2.zcard("/v1/j_created") == 2
+    assert s2.get_orig_body(tid) == "B"
+    assert set(s2.zrange("/v1/j_created")) == set(other)
+
+
+def test_timestamp_and_path_helpers():
+    from aiforearth_api_platform_amd.store import native
+    assert pystore.dotnet_timestamp(0) == "1/1/1970 12:00:00 AM"
+    assert pystore.dotnet_timestamp(13 * 3600 + 5 * 60 + 7) == "1/1/1970 1:05:07 PM"
+    assert native.dotnet_timestamp(13 * 3600 + 5 * 60 + 7) == "1/1/1970 1:05:07 PM"
+    for ep in ["http://a:80/v1/x?q=1", "https://h/v1/o/api", "http://h", "/v1/local", "v1/rel"]:
+        assert native.absolute_path(ep) == pystore.absolute_path(ep), ep
+
+
+def test_queue_peek_lock_complete_abandon_deadletter(backend):
+    q = make_queue("q", max_delivery_count=2, lock_duration_s=30.0, backend=backend)
+    assert q.send("t1", 7, "body")
+    m = q.receive(4, 0.1, 0.0)
+    assert len(m) == 1 and m[0].task_id == "t1" and m[0].ref == 7 and m[0].delivery_count == 1
+    assert bytes(m[0].body) == b"body"
+    assert q.abandon(m[0].seq, 0.0) == "requeued"
+    m2 = q.receive(4, 0.1, 0.0)
+    assert m2[0].delivery_count == 2
+    assert q.abandon(m2[0].seq, 0.0) == "deadlettered"
+    assert q.take_deadletters() == ["t1"]
+    assert q.receive(1, 0.0, 0.0) == []
+    q.send("t2")
+    m3 = q.receive(1, 0.1)
+    assert q.complete([m3[0].seq]) == 1 and q.stats()["inflight"] == 0
+
+
+def test_queue_delayed_redelivery_and_lock_expiry(backend):
+    q = make_queue("q", max_delivery_count=10, lock_duration_s=0.05, backend=backend)
+    q.send("a")
+    m = q.receive(1, 0.1)
+    q.abandon(m[0].seq, 0.15)
+    assert q.receive(1, 0.0) == []
+    t0 = time.monotonic()
+    m = q.receive(1, 1.0)
+    assert m and time.monotonic() - t0 >= 0.1
+    # lock expiry: do not complete -> redelivered
+    m2 = q.receive(1, 1.0)
+    assert m2 and m2[0].task_id == "a" and m2[0].delivery_count == 3
+
+
+def test_queue_batch_receive_linger_and_backpressure(backend):
+    q = make_queue("q", max_size=5, backend=backend)
+    assert q.send_many([f"t{i}" for i in range(8)], list(range(8))) == 5
+    assert not q.send("x")
+    got = q.receive(3, 0.1, 0.0)
+    assert [m.ref for m in got] == [0, 1, 2]
+    t0 = time.monotonic()
+    got = q.receive(8, 0.1, 0.05)  # only 2 left: linger until timeout
+    assert len(got) == 2 and time.monotonic() - t0 >= 0.04
+
+
+def test_native_threaded_throughput():
+    """Many producer threads + one batching consumer: no loss, no duplication."""
+    import threading
+    q = make_queue("q", backend="native")
+    s = make_store(backend="native")
+    N, P = 2000, 4
+    def prod():
+        ids = s.create_many("/v1/x", N // P)
+        q.send_many(ids, [])
+    ts = [threading.Thread(target=prod) for _ in range(P)]
+    [t.start() for t in ts]
+    seen = []
+    while len(seen) < N:
+        ms = q.receive(256, 1.0, 0.001)
+        assert ms
+        q.complete([m.seq for m in ms])
+        s.transition_many([m.task_id for m in ms], "completed", "ok")
+        seen += [m.task_id for m in ms]
+    [t.join() for t in ts]
+    assert len(set(seen)) == N and s.zcard("/v1/x_completed") == N
