@@ -1,0 +1,170 @@
+"""ResNet-50 (v1.5, torchvision layout) — the headline ResNet-50 224x224 classification API model.
+
+Two forms:
+
+* ``ResNet`` — a plain ``torch.nn`` NCHW definition (fp32), the numerics reference and the
+  weight source (``load_state_dict`` accepts torchvision-style keys; weights are random-init here
+  because no checkpoint is available offline).
+* ``FusedResNet`` — the serving form: BatchNorm folded into the convs, NHWC bf16 activations, every
+  conv (+bias +ReLU +residual add) one K1 HIP kernel, preprocess (K7), max-pool, global avg-pool
+  and the classifier (a 1x1 conv through K1) — 57 kernel launches per forward, capturable in a
+  HIP graph.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Tuple
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ..ops.conv import PackedConv, conv2d_nhwc, fold_bn, pack_conv
+from ..ops.pool import global_avgpool_nhwc, maxpool2d_nhwc, preprocess_u8
+
+
+class Bottleneck(nn.Module):
+    expansion = 4
+
+    def __init__(self, inplanes: int, planes: int, stride: int = 1, downsample: Optional[nn.Module] = None):
+        super().__init__()
+        self.conv1 = nn.Conv2d(inplanes, planes, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(planes)
+        self.conv2 = nn.Conv2d(planes, planes, 3, stride=stride, padding=1, bias=False)
+        self.bn2 = nn.BatchNorm2d(planes)
+        self.conv3 = nn.Conv2d(planes, planes * 4, 1, bias=False)
+        self.bn3 = nn.BatchNorm2d(planes * 4)
+        self.downsample = downsample
+
+    def forward(self, x):
+        idt = x if self.downsample is None else self.downsample(x)
+        out = F.relu(self.bn1(self.conv1(x)))
+        out = F.relu(self.bn2(self.conv2(out)))
+        out = self.bn3(self.conv3(out))
+        return F.relu(out + idt)
+
+
+class ResNet(nn.Module):
+    def __init__(self, layers=(3, 4, 6, 3), num_classes: int = 1000, in_ch: int = 3):
+        super().__init__()
+        self.inplanes = 64
+        self.conv1 = nn.Conv2d(in_ch, 64, 7, stride=2, padding=3, bias=False)
+        self.bn1 = nn.BatchNorm2d(64)
+        self.layer1 = self._make(64, layers[0], 1)
+        self.layer2 = self._make(128, layers[1], 2)
+        self.layer3 = self._make(256, layers[2], 2)
+        self.layer4 = self._make(512, layers[3], 2)
+        self.fc = nn.Linear(2048, num_classes)
+
+    def _make(self, planes, blocks, stride):
+        down = None
+        if stride != 1 or self.inplanes != planes * 4:
+            down = nn.Sequential(nn.Conv2d(self.inplanes, planes * 4, 1, stride=stride, bias=False),
+                                 nn.BatchNorm2d(planes * 4))
+        mods = [Bottleneck(self.inplanes, planes, stride, down)]
+        self.inplanes = planes * 4
+        mods += [Bottleneck(self.inplanes, planes) for _ in range(1, blocks)]
+        return nn.Sequential(*mods)
+
+    def features(self, x):
+        x = F.max_pool2d(F.relu(self.bn1(self.conv1(x))), 3, 2, 1)
+        return self.layer4(self.layer3(self.layer2(self.layer1(x))))
+
+    def forward(self, x):
+        return self.fc(torch.flatten(F.adaptive_avg_pool2d(self.features(x), 1), 1))
+
+
+def randomize_bn_(model: nn.Module, generator: Optional[torch.Generator] = None) -> nn.Module:
+    """Random-init weights with realistic inference BN statistics (so folding is exercised)."""
+    g = generator
+    for m in model.modules():
+        if isinstance(m, nn.Conv2d):
+            nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu", generator=g)
+        elif isinstance(m, nn.BatchNorm2d):
+            c = m.num_features
+            m.weight.data = 0.5 + 0.5 * torch.rand(c, generator=g)
+            m.bias.data = 0.1 * torch.randn(c, generator=g)
+            m.running_mean.data = 0.1 * torch.randn(c, generator=g)
+            m.running_var.data = 0.5 + torch.rand(c, generator=g)
+        elif isinstance(m, nn.Linear):
+            nn.init.normal_(m.weight, 0, 0.01, generator=g)
+            nn.init.zeros_(m.bias)
+    # keep the residual stream bounded through 16 blocks with random weights (zero-init-residual
+    # style damping of the last BN in every block)
+    for m in model.modules():
+        if isinstance(m, Bottleneck):
+            m.bn3.weight.data *= 0.2
+    return model.eval()
+
+
+def resnet50(num_classes: int = 1000, seed: int = 0) -> ResNet:
+    g = torch.Generator().manual_seed(seed)
+    return randomize_bn_(ResNet((3, 4, 6, 3), num_classes), g)
+
+
+def _fold(conv: nn.Conv2d, bn: nn.BatchNorm2d, cin_pad: Optional[int] = None) -> PackedConv:
+    w, b = fold_bn(conv.weight.data.float(), bn.weight.data.float(), bn.bias.data.float(), bn.running_mean.float(),
+                   bn.running_var.float(), bn.eps)
+    return pack_conv(w, b, stride=conv.stride[0], pad=conv.padding[0], cin_pad=cin_pad)
+
+
+class FusedResNet:
+    """Inference graph over packed, BN-folded layers (NHWC bf16)."""
+
+    def __init__(self, model: ResNet, device="cpu", in_ch: Optional[int] = None):
+        model = model.eval()
+        self.device = torch.device(device)
+        self.in_ch = in_ch or model.conv1.in_channels
+        self.stem = _fold(model.conv1, model.bn1, cin_pad=8).to(self.device)
+        self.blocks: List[Tuple[PackedConv, PackedConv, PackedConv, Optional[PackedConv]]] = []
+        for layer in (model.layer1, model.layer2, model.layer3, model.layer4):
+            for blk in layer:
+                down = None
+                if blk.downsample is not None:
+                    down = _fold(blk.downsample[0], blk.downsample[1]).to(self.device)
+                self.blocks.append((_fold(blk.conv1, blk.bn1).to(self.device), _fold(blk.conv2, blk.bn2).to(self.device),
+                                    _fold(blk.conv3, blk.bn3).to(self.device), down))
+        fcw = model.fc.weight.data.float().reshape(model.fc.out_features, -1, 1, 1)
+        self.fc = pack_conv(fcw, model.fc.bias.data.float()).to(self.device)
+        self.num_classes = model.fc.out_features
+
+    def layers(self) -> List[PackedConv]:
+        out = [self.stem]
+        for c1, c2, c3, d in self.blocks:
+            out += [c1, c2, c3] + ([d] if d is not None else [])
+        return out + [self.fc]
+
+    def flops(self, n: int, h: int = 224, w: int = 224) -> int:
+        from ..ops.conv import conv_flops
+
+        total = conv_flops(self.stem, n, h, w)
+        h, w = self.stem.out_hw(h, w)
+        h, w = (h + 1) // 2, (w + 1) // 2
+        for c1, c2, c3, d in self.blocks:
+            total += conv_flops(c1, n, h, w) + conv_flops(c2, n, h, w)
+            h2, w2 = c2.out_hw(h, w)
+            total += conv_flops(c3, n, h2, w2)
+            if d is not None:
+                total += conv_flops(d, n, h, w)
+            h, w = h2, w2
+        return total + conv_flops(self.fc, n, 1, 1)
+
+    def forward_features(self, x: torch.Tensor) -> torch.Tensor:
+        """x: NHWC [N,H,W,8] normalized (bf16 on GPU) -> [N,h,w,2048]."""
+        x = conv2d_nhwc(x, self.stem, relu=True)
+        x = maxpool2d_nhwc(x, 3, 2, 1)
+        for c1, c2, c3, down in self.blocks:
+            idt = x if down is None else conv2d_nhwc(x, down)
+            y = conv2d_nhwc(x, c1, relu=True)
+            y = conv2d_nhwc(y, c2, relu=True)
+            x = conv2d_nhwc(y, c3, residual=idt, relu=True)
+        return x
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        f = global_avgpool_nhwc(self.forward_features(x))
+        return conv2d_nhwc(f, self.fc).reshape(f.shape[0], -1).float()
+
+    def forward_u8(self, img_u8: torch.Tensor) -> torch.Tensor:
+        """uint8 NHWC images -> fp32 logits (preprocess fused into the first kernel launch)."""
+        return self.forward(preprocess_u8(img_u8))
+
+    __call__ = forward_u8

@@ -1,0 +1,98 @@
+"""Loader for the in-tree gfx950 kernel library (``_lib/libai4e_kernels.so``) via a plain C ABI.
+
+Every launcher takes raw device pointers plus the current HIP stream, so kernels compose with
+PyTorch's caching allocator, streams and HIP-graph capture (``torch.cuda.graph``) with no torch
+headers in the kernel translation units.
+
+Backend policy (``AI4E_KERNEL_BACKEND``): ``auto`` runs the HIP kernels for tensors on the GPU
+and the PyTorch reference ops on CPU; ``hip`` forces the kernels; ``torch`` forces the reference
+ops. A GPU tensor with the library missing is a hard error — never a silent fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+from typing import Optional
+
+import torch
+
+_LIB_PATH = Path(__file__).resolve().parent.parent / "_lib" / "libai4e_kernels.so"
+_lib: Optional[ctypes.CDLL] = None
+
+_c_int, _c_long, _c_float, _vp = ctypes.c_int, ctypes.c_long, ctypes.c_float, ctypes.c_void_p
+
+# name -> argtypes (all return int status)
+_SIGS = {
+    "ai4e_conv2d_fwd": [_vp, _vp, _vp, _vp, _vp] + [_c_int] * 20 + [_vp],
+    "ai4e_preprocess_u8": [_vp, _vp, _c_long, _c_int, _vp, _vp, _c_float, _vp],
+    "ai4e_maxpool2d": [_vp, _vp] + [_c_int] * 9 + [_vp],
+    "ai4e_global_avgpool": [_vp, _vp, _c_int, _c_int, _c_int, _vp],
+    "ai4e_groupnorm_nhwc": [_vp, _vp, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_float, _c_int, _c_int,
+                            _c_int, _vp],
+    "ai4e_upsample2x_bilinear": [_vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _vp],
+    "ai4e_nms_mask": [_vp, _c_int, _c_float, _vp, _vp],
+    "ai4e_nms_reduce": [_vp, _vp, _c_int, _c_int, _vp, _vp, _vp],
+    "ai4e_roi_align_nhwc": [_vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_float,
+                            _c_int, _c_int, _vp],
+    "ai4e_tile_stitch_accum": [_vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int,
+                               _c_int, _vp],
+    "ai4e_tile_stitch_finalize": [_vp, _vp, _vp, _vp, _c_int, _c_int, _c_int, _vp],
+    "ai4e_crop_resize_nhwc": [_vp, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _vp],
+    "ai4e_decode_boxes": [_vp, _vp, _vp, _c_int, _c_int, _c_float, _c_float, _c_float, _vp],
+}
+
+
+class KernelError(RuntimeError):
+    pass
+
+
+def library_path() -> Path:
+    return _LIB_PATH
+
+
+def available() -> bool:
+    return _LIB_PATH.exists()
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not _LIB_PATH.exists():
+            raise KernelError(f"HIP kernel library not built: {_LIB_PATH} (run python -m aiforearth_api_platform_amd._build)")
+        _lib = ctypes.CDLL(str(_LIB_PATH))
+        for name, args in _SIGS.items():
+            fn = getattr(_lib, name, None)
+            if fn is not None:
+                fn.argtypes = args
+                fn.restype = _c_int
+    return _lib
+
+
+def call(name: str, *args) -> None:
+    rc = getattr(lib(), name)(*args)
+    if rc != 0:
+        raise KernelError(f"{name} failed with status {rc}")
+
+
+def stream_ptr(device: Optional[torch.device] = None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def ptr(t: Optional[torch.Tensor]) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+def backend_for(t: torch.Tensor) -> str:
+    mode = os.environ.get("AI4E_KERNEL_BACKEND", "auto").lower()
+    if mode == "torch":
+        return "torch"
+    if mode == "hip":
+        if not t.is_cuda:
+            raise KernelError("AI4E_KERNEL_BACKEND=hip but tensor is on CPU")
+        lib()
+        return "hip"
+    if t.is_cuda:
+        lib()  # loud failure if the kernels are missing on a GPU box
+        return "hip"
+    return "torch"

@@ -1,0 +1,147 @@
+"""Fused NHWC conv2d (+folded BN bias, +residual, +ReLU) — HIP implicit-GEMM kernel K1.
+
+``PackedConv`` holds one layer's weights in the kernel layout ``[rows_pad, Kpad]`` bf16 with
+``k = (kh, kw, c)`` (c innermost, C padded to a multiple of 8, K to a multiple of 32, rows to the
+tile height) and an fp32 bias, plus the reference fp32 weights for the PyTorch path.
+
+``conv2d_nhwc(x, pc, residual=None, relu=False, out=None, out_coff=0)`` runs on NHWC tensors.
+``out``/``out_coff`` let a layer write a channel slice of a wider buffer (U-Net skip concat without
+a copy). ``x`` may itself be a channel slice view of a wider buffer.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+
+from . import _ext
+
+K_ALIGN = 32
+ROW_ALIGN = 256
+C_ALIGN = 8
+
+
+def _round_up(a: int, b: int) -> int:
+    return (a + b - 1) // b * b
+
+
+@dataclass
+class PackedConv:
+    w_ref: torch.Tensor      # [Cout, Cin, KH, KW] fp32 (BN folded)
+    b_ref: torch.Tensor      # [Cout] fp32
+    w_packed: torch.Tensor   # [rows_pad, Kpad] bf16
+    bias: torch.Tensor       # [rows_pad] fp32
+    cin: int
+    cin_pad: int
+    cout: int
+    kh: int
+    kw: int
+    stride: int
+    pad: int
+
+    @property
+    def kpad(self) -> int:
+        return self.w_packed.shape[1]
+
+    def to(self, device) -> "PackedConv":
+        return PackedConv(self.w_ref.to(device), self.b_ref.to(device), self.w_packed.to(device), self.bias.to(device),
+                          self.cin, self.cin_pad, self.cout, self.kh, self.kw, self.stride, self.pad)
+
+    def out_hw(self, h: int, w: int):
+        return ((h + 2 * self.pad - self.kh) // self.stride + 1, (w + 2 * self.pad - self.kw) // self.stride + 1)
+
+
+def pack_conv(weight: torch.Tensor, bias: Optional[torch.Tensor], stride: int = 1, pad: int = 0,
+              cin_pad: Optional[int] = None) -> PackedConv:
+    """Pack an OIHW fp32 weight (+bias) into the K1 layout."""
+    weight = weight.detach().float().cpu()
+    cout, cin, kh, kw = weight.shape
+    cin_pad = cin_pad or _round_up(cin, C_ALIGN)
+    w = torch.zeros(cout, kh, kw, cin_pad)
+    w[..., :cin] = weight.permute(0, 2, 3, 1)
+    k = kh * kw * cin_pad
+    kp = _round_up(k, K_ALIGN)
+    rows = _round_up(cout, ROW_ALIGN)
+    wp = torch.zeros(rows, kp, dtype=torch.bfloat16)
+    wp[:cout, :k] = w.reshape(cout, k).to(torch.bfloat16)
+    b = torch.zeros(rows, dtype=torch.float32)
+    bref = torch.zeros(cout) if bias is None else bias.detach().float().cpu()
+    b[:cout] = bref
+    return PackedConv(weight, bref, wp, b, cin, cin_pad, cout, kh, kw, stride, pad)
+
+
+def fold_bn(weight: torch.Tensor, bn_weight, bn_bias, running_mean, running_var, eps: float = 1e-5,
+            conv_bias: Optional[torch.Tensor] = None):
+    """Fold inference BatchNorm into the preceding conv: returns (w', b')."""
+    scale = bn_weight / torch.sqrt(running_var + eps)
+    w = weight * scale.reshape(-1, 1, 1, 1)
+    b = bn_bias - running_mean * scale
+    if conv_bias is not None:
+        b = b + conv_bias * scale
+    return w, b
+
+
+def conv2d_nhwc(x: torch.Tensor, pc: PackedConv, residual: Optional[torch.Tensor] = None, relu: bool = False,
+                out: Optional[torch.Tensor] = None, out_coff: int = 0, tile_cfg: int = 0) -> torch.Tensor:
+    n, h, w, c = x.shape
+    if c != pc.cin_pad:
+        raise ValueError(f"conv expects C={pc.cin_pad} (padded), got {c}")
+    oh, ow = pc.out_hw(h, w)
+    if out is None:
+        out = torch.empty(n, oh, ow, pc.cout, device=x.device, dtype=x.dtype)
+        out_coff = 0
+    if _ext.backend_for(x) == "hip":
+        _conv_hip(x, pc, residual, relu, out, out_coff, tile_cfg)
+    else:
+        y = _conv_torch(x, pc, residual, relu)
+        out[..., out_coff:out_coff + pc.cout] = y.to(out.dtype)
+    return out
+
+
+def _conv_hip(x, pc, residual, relu, out, out_coff, tile_cfg):
+    n, h, w, c = x.shape
+    oh, ow = pc.out_hw(h, w)
+    if x.dtype != torch.bfloat16 or out.dtype != torch.bfloat16:
+        raise TypeError("HIP conv path is bf16")
+    # x may be a channel-slice view of a wider NHWC buffer: rows stride = x.stride(2)
+    if x.stride(3) != 1 or x.stride(2) * w != x.stride(1) or x.stride(1) * h != x.stride(0):
+        raise ValueError("conv input must be an NHWC (possibly channel-sliced) dense tensor")
+    ldx = x.stride(2)
+    base = x.untyped_storage().data_ptr()
+    xoff = x.storage_offset()
+    if out.stride(3) != 1 or out.shape[1] != oh or out.shape[2] != ow:
+        raise ValueError("bad conv output buffer")
+    ldy = out.stride(2)
+    ldres = 0
+    if residual is not None:
+        if residual.shape != (n, oh, ow, pc.cout) or not residual.is_contiguous():
+            raise ValueError("residual must be contiguous [N,OH,OW,Cout]")
+        ldres = pc.cout
+    _ext.call("ai4e_conv2d_fwd", base + 2 * (xoff - xoff % ldx), pc.w_packed.data_ptr(), pc.bias.data_ptr(),
+              _ext.ptr(residual), out.data_ptr(), n, h, w, c, ldx, xoff % ldx, pc.kh, pc.kw, pc.stride, pc.pad,
+              oh, ow, pc.cout, pc.kpad, ldy, out_coff, ldres, int(relu), tile_cfg, _ext.stream_ptr(x.device))
+
+
+def _conv_torch(x, pc, residual, relu):
+    cdt = torch.float32 if not x.is_cuda else x.dtype
+    xin = x[..., :pc.cin].permute(0, 3, 1, 2).to(cdt)
+    y = F.conv2d(xin, pc.w_ref.to(x.device, cdt), pc.b_ref.to(x.device, cdt), stride=pc.stride, padding=pc.pad)
+    y = y.permute(0, 2, 3, 1)
+    if residual is not None:
+        y = y + residual.to(cdt)
+    if relu:
+        y = F.relu(y)
+    return y
+
+
+def conv_flops(pc: PackedConv, n: int, h: int, w: int) -> int:
+    oh, ow = pc.out_hw(h, w)
+    return 2 * n * oh * ow * pc.cout * pc.kh * pc.kw * pc.cin
+
+
+def kaiming_conv(cout: int, cin: int, k: int, generator: Optional[torch.Generator] = None) -> torch.Tensor:
+    std = math.sqrt(2.0 / (cin * k * k))
+    return torch.randn(cout, cin, k, k, generator=generator) * std

@@ -1,0 +1,63 @@
+"""Preprocess (K7), max-pool and global-avg-pool (K8 front half) on NHWC bf16."""
+from __future__ import annotations
+
+import ctypes
+from typing import Sequence
+
+import torch
+import torch.nn.functional as F
+
+from . import _ext
+
+IMAGENET_MEAN = (0.485, 0.456, 0.406)
+IMAGENET_STD = (0.229, 0.224, 0.225)
+
+
+def preprocess_u8(img: torch.Tensor, mean: Sequence[float] = IMAGENET_MEAN, std: Sequence[float] = IMAGENET_STD,
+                  scale: float = 1.0 / 255.0, out: torch.Tensor = None) -> torch.Tensor:
+    """uint8 NHWC [N,H,W,Cin<=8] -> normalized bf16 NHWC [N,H,W,8] (channels >= Cin are zero)."""
+    n, h, w, cin = img.shape
+    if img.dtype != torch.uint8 or cin > 8:
+        raise ValueError("preprocess expects uint8 NHWC with <= 8 channels")
+    m8 = list(mean) + [0.0] * (8 - len(mean))
+    s8 = list(std) + [1.0] * (8 - len(std))
+    if out is None:
+        out = torch.empty(n, h, w, 8, device=img.device, dtype=torch.bfloat16 if img.is_cuda else torch.float32)
+    if _ext.backend_for(img) == "hip":
+        mean_a, std_a = ctypes_floats(m8), ctypes_floats(s8)  # kept alive across the call
+        _ext.call("ai4e_preprocess_u8", img.data_ptr(), out.data_ptr(), n * h * w, cin, ctypes.addressof(mean_a),
+                  ctypes.addressof(std_a), scale, _ext.stream_ptr(img.device))
+    else:
+        x = img.float() * scale
+        x = (x - torch.tensor(m8[:cin], device=img.device)) / torch.tensor(s8[:cin], device=img.device)
+        out.zero_()
+        out[..., :cin] = x.to(out.dtype)
+    return out
+
+
+def ctypes_floats(vals):
+    return (ctypes.c_float * len(vals))(*vals)
+
+
+def maxpool2d_nhwc(x: torch.Tensor, k: int = 3, stride: int = 2, pad: int = 1) -> torch.Tensor:
+    n, h, w, c = x.shape
+    oh, ow = (h + 2 * pad - k) // stride + 1, (w + 2 * pad - k) // stride + 1
+    if _ext.backend_for(x) == "hip":
+        x = x.contiguous()
+        y = torch.empty(n, oh, ow, c, device=x.device, dtype=x.dtype)
+        _ext.call("ai4e_maxpool2d", x.data_ptr(), y.data_ptr(), n, h, w, c, oh, ow, k, stride, pad,
+                  _ext.stream_ptr(x.device))
+        return y
+    y = F.max_pool2d(x.permute(0, 3, 1, 2).float(), k, stride, pad)
+    return y.permute(0, 2, 3, 1).to(x.dtype).contiguous()
+
+
+def global_avgpool_nhwc(x: torch.Tensor) -> torch.Tensor:
+    """[N,H,W,C] -> [N,1,1,C] (kept 4-D so the classifier runs as a 1x1 conv)."""
+    n, h, w, c = x.shape
+    if _ext.backend_for(x) == "hip":
+        x = x.contiguous()
+        y = torch.empty(n, 1, 1, c, device=x.device, dtype=x.dtype)
+        _ext.call("ai4e_global_avgpool", x.data_ptr(), y.data_ptr(), n, h * w, c, _ext.stream_ptr(x.device))
+        return y
+    return x.float().mean(dim=(1, 2), keepdim=True).to(x.dtype)

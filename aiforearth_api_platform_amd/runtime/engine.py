@@ -1,0 +1,198 @@
+"""Per-GPU inference engine: static device buffers, HIP-graph-captured forward, overlapped H2D/D2H.
+
+One engine per MI355X (one process per GPU in the worker pool). The model forward (57 kernel
+launches for ResNet-50) is captured once per (batch bucket, buffer) into a HIP graph
+(``torch.cuda.CUDAGraph`` is hipGraph on ROCm), so a batch costs one graph launch instead of
+dozens of Python-side launches. Inputs arrive as uint8 images in a pinned host ring
+(:class:`PayloadRing`); contiguous slot runs are copied H2D on a dedicated copy stream while the
+previous batch computes; only the top-k result (a few bytes per image) is copied back.
+"""
+from __future__ import annotations
+
+import threading
+from dataclasses import dataclass
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
+
+import torch
+
+
+class PayloadRing:
+    """Pinned host ring of fixed-shape request payloads (e.g. decoded uint8 images).
+
+    ``alloc`` hands out slot indices in FIFO order so a batch received from the FIFO dispatch
+    queue is (almost always) one contiguous run -> one DMA.
+    """
+
+    def __init__(self, nslots: int, item_shape: Sequence[int], dtype=torch.uint8, pin: bool = True):
+        self.nslots = int(nslots)
+        self.item_shape = tuple(item_shape)
+        pin = pin and torch.cuda.is_available()
+        self.buf = torch.empty((self.nslots, *self.item_shape), dtype=dtype, pin_memory=pin)
+        self._head = 0
+        self._used = 0
+        self._free = [False] * self.nslots
+        self._mu = threading.Condition()
+
+    def alloc(self, n: int, timeout: Optional[float] = None) -> List[int]:
+        with self._mu:
+            if n > self.nslots:
+                raise ValueError("request larger than the ring")
+            if not self._mu.wait_for(lambda: self.nslots - self._used >= n, timeout):
+                raise TimeoutError("payload ring full")
+            start = (self._head + self._used) % self.nslots
+            self._used += n
+            return [(start + i) % self.nslots for i in range(n)]
+
+    def free(self, slots: Sequence[int]) -> None:
+        """Release slots; the ring head only advances over a contiguous freed prefix."""
+        with self._mu:
+            for s in slots:
+                self._free[s] = True
+            while self._used and self._free[self._head]:
+                self._free[self._head] = False
+                self._head = (self._head + 1) % self.nslots
+                self._used -= 1
+            self._mu.notify_all()
+
+    def write(self, slot: int, data) -> None:
+        self.buf[slot].copy_(torch.as_tensor(data))
+
+
+def contiguous_runs(slots: Sequence[int]) -> List[Tuple[int, int, int]]:
+    """[(dst_offset, src_start, length)] for runs of consecutive slot ids."""
+    runs = []
+    i = 0
+    n = len(slots)
+    while i < n:
+        j = i + 1
+        while j < n and slots[j] == slots[j - 1] + 1:
+            j += 1
+        runs.append((i, slots[i], j - i))
+        i = j
+    return runs
+
+
+class _DoneEvent:
+    def synchronize(self) -> None:
+        return None
+
+    def query(self) -> bool:
+        return True
+
+
+@dataclass
+class BatchResult:
+    top_idx: torch.Tensor    # [b, k] int32 (pinned host)
+    top_prob: torch.Tensor   # [b, k] fp32 (pinned host)
+    done: torch.cuda.Event
+    n: int
+
+
+class InferenceEngine:
+    """Runs ``model_fn(u8 [b,H,W,C] on device) -> logits [b, classes]`` with graphs + 2-deep buffering."""
+
+    def __init__(self, model_fn: Callable[[torch.Tensor], torch.Tensor], item_shape: Sequence[int], max_batch: int,
+                 device: Optional[torch.device] = None, topk: int = 5, use_graphs: bool = True, nbuf: int = 2,
+                 buckets: Optional[Sequence[int]] = None):
+        self.model_fn = model_fn
+        self.device = torch.device(device or "cuda")
+        self.item_shape = tuple(item_shape)
+        self.max_batch = max_batch
+        self.topk = topk
+        self.use_graphs = use_graphs and self.device.type == "cuda"
+        self.nbuf = nbuf
+        self.buckets = sorted(set(buckets or [max_batch]))
+        if self.buckets[-1] != max_batch:
+            self.buckets.append(max_batch)
+        self.copy_stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
+        self.compute_stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
+        self.inputs = [torch.empty((max_batch, *self.item_shape), dtype=torch.uint8, device=self.device)
+                       for _ in range(nbuf)]
+        pin = self.device.type == "cuda"
+        self.h_idx = [torch.empty((max_batch, topk), dtype=torch.int32, pin_memory=pin) for _ in range(nbuf)]
+        self.h_prob = [torch.empty((max_batch, topk), dtype=torch.float32, pin_memory=pin) for _ in range(nbuf)]
+        self.graphs: Dict[Tuple[int, int], torch.cuda.CUDAGraph] = {}
+        self._graph_out: Dict[Tuple[int, int], Tuple[torch.Tensor, torch.Tensor]] = {}
+        self.compute_done: List[Optional[torch.cuda.Event]] = [None] * nbuf
+        self._k = 0
+
+    # -------------------------------------------------------------- forward
+    def _forward_into(self, buf: int, b: int):
+        logits = self.model_fn(self.inputs[buf][:b])
+        prob = torch.softmax(logits.float(), dim=1)
+        p, i = torch.topk(prob, self.topk, dim=1)
+        return i.to(torch.int32), p
+
+    def bucket_for(self, n: int) -> int:
+        for b in self.buckets:
+            if b >= n:
+                return b
+        raise ValueError(f"batch {n} > max_batch {self.max_batch}")
+
+    def warmup(self) -> None:
+        """Run every (bucket, buffer) once eagerly (kernel load / allocator warm) then capture graphs."""
+        if self.device.type != "cuda":
+            return
+        with torch.cuda.stream(self.compute_stream):
+            for buf in range(self.nbuf):
+                self.inputs[buf].zero_()
+                for b in self.buckets:
+                    self._forward_into(buf, b)
+        torch.cuda.synchronize(self.device)
+        if not self.use_graphs:
+            return
+        for buf in range(self.nbuf):
+            for b in self.buckets:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, stream=self.compute_stream):
+                    i, p = self._forward_into(buf, b)
+                self.graphs[(buf, b)] = g
+                self._graph_out[(buf, b)] = (i, p)
+        torch.cuda.synchronize(self.device)
+
+    # -------------------------------------------------------------- submit
+    def submit(self, host_src: torch.Tensor, slots: Sequence[int]) -> BatchResult:
+        """Copy ``host_src[slots]`` to the next device buffer, run, and return an async result."""
+        n = len(slots)
+        if self.device.type != "cuda":  # CPU path (tests / CPU-only hosts): synchronous
+            idx, prob = self.run_sync(host_src[list(slots)])
+            return BatchResult(idx, prob, _DoneEvent(), n)
+        buf = self._k % self.nbuf
+        self._k += 1
+        b = self.bucket_for(n)
+        dev_in = self.inputs[buf]
+        cs = self.copy_stream
+        # the copy into `buf` must not overwrite an input the compute stream is still reading
+        # (only the batch that last used this buffer; the previous batch keeps computing)
+        if self.compute_done[buf] is not None:
+            cs.wait_event(self.compute_done[buf])
+        with torch.cuda.stream(cs):
+            for dst, src, ln in contiguous_runs(list(slots)):
+                dev_in[dst:dst + ln].copy_(host_src[src:src + ln], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(cs)
+        st = self.compute_stream
+        st.wait_event(ev)
+        with torch.cuda.stream(st):
+            if self.use_graphs and (buf, b) in self.graphs:
+                self.graphs[(buf, b)].replay()
+                i, p = self._graph_out[(buf, b)]
+            else:
+                i, p = self._forward_into(buf, b)
+            self.h_idx[buf][:n].copy_(i[:n], non_blocking=True)
+            self.h_prob[buf][:n].copy_(p[:n], non_blocking=True)
+            done = torch.cuda.Event()
+            done.record(st)
+        self.compute_done[buf] = done
+        return BatchResult(self.h_idx[buf][:n], self.h_prob[buf][:n], done, n)
+
+    def run_sync(self, images_u8: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        """Convenience (sync API / tests): images already on host or device."""
+        if self.device.type != "cuda":
+            logits = self.model_fn(images_u8)
+            p, i = torch.topk(torch.softmax(logits.float(), 1), self.topk, 1)
+            return i.to(torch.int32), p
+        host = images_u8.cpu().pin_memory() if not images_u8.is_pinned() else images_u8
+        res = self.submit(host, list(range(images_u8.shape[0])))
+        res.done.synchronize()
+        return res.top_idx.clone(), res.top_prob.clone()

@@ -1,0 +1,165 @@
+#!/usr/bin/env python
+"""Headline benchmark: ResNet-50 224x224 async classification API, bf16, images/s + p50 task latency.
+
+Metric and config from BASELINE.json ("images/sec (whole node) + p50 async-task latency,
+ResNet-50 API at 1/2/4/8 GPUs"). Every image goes through the full async serving path of one
+replica per GPU (one process per GPU, torch.distributed/RCCL only for the barrier and the
+cross-rank MAX of the timings):
+
+    create task (native task store, status "created")  ->  enqueue (native dispatch queue, payload =
+    pinned uint8 image slot)  ->  dynamic batcher (receive up to --batch, linger)  ->  "running"  ->
+    H2D on a copy stream  ->  HIP-graph replay of the fused ResNet-50 (preprocess + 53 conv kernels +
+    pools + classifier, hand-written gfx950 kernels)  ->  softmax/top-5  ->  D2H  ->  "completed".
+
+A step = one batch of --batch tasks per GPU submitted through the API; --inflight steps are kept
+outstanding (closed loop). Weak scaling: per-GPU work is fixed as N grows. Data is synthetic
+(random uint8 images), weights are random-init (no checkpoints offline).
+
+    python bench.py [--gpus N --steps K --warmup W]       (N>1: torchrun, one rank per GPU)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "images/sec (whole node) + p50 async-task latency, ResNet-50 API at 1/2/4/8 GPUs"
+BASELINE_VALUE = None  # the reference publishes no numbers
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--batch", type=int, default=256, help="images per step per GPU (= max dynamic batch)")
+    p.add_argument("--inflight", type=int, default=2, help="steps kept outstanding per GPU")
+    p.add_argument("--image-size", type=int, default=224)
+    p.add_argument("--backend", default="auto", choices=["auto", "hip", "torch"])
+    p.add_argument("--no-graphs", action="store_true")
+    p.add_argument("--device", default="cuda")
+    p.add_argument("--json-out", default="")
+    return p.parse_args()
+
+
+def main():
+    args = parse()
+    os.environ["AI4E_KERNEL_BACKEND"] = args.backend
+    from aiforearth_api_platform_amd import _build
+    from aiforearth_api_platform_amd.config import Config
+    from aiforearth_api_platform_amd.gateway.control import ControlPlane
+    from aiforearth_api_platform_amd.models.resnet import FusedResNet, resnet50
+    from aiforearth_api_platform_amd.runtime.engine import InferenceEngine, PayloadRing
+    from aiforearth_api_platform_amd.runtime.serving import GpuBatchWorker
+    from aiforearth_api_platform_amd.utils.metrics import percentile
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and args.gpus != world:
+        raise SystemExit(f"--gpus {args.gpus} != WORLD_SIZE {world}")
+    if rank == 0:
+        _build.build_all()
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        backend = "nccl" if args.device == "cuda" else "gloo"
+        if args.device == "cuda":
+            torch.cuda.set_device(local)
+        dist.init_process_group(backend, rank=rank, world_size=world)
+        dist.barrier()  # rank 0 finished building before anyone loads the libraries
+    device = torch.device(f"cuda:{local}" if args.device == "cuda" else "cpu")
+    if device.type == "cuda":
+        torch.cuda.set_device(device)
+
+    B, S = args.batch, args.image_size
+    model = FusedResNet(resnet50(seed=0), device=device)
+    engine = InferenceEngine(model.forward_u8, (S, S, 3), B, device=device, use_graphs=not args.no_graphs)
+    engine.warmup()
+
+    cfg = Config.load(env={}, max_batch=B, max_batch_delay_ms=0.0)
+    cp = ControlPlane(cfg)
+    endpoint = "http://127.0.0.1/v1/ai4e/resnet50/classify"
+    ring = PayloadRing(B * (args.inflight + 2), (S, S, 3))
+    g = torch.Generator().manual_seed(1234 + rank)
+    ring.buf.copy_(torch.randint(0, 256, ring.buf.shape, dtype=torch.uint8, generator=g))
+    worker = GpuBatchWorker(cp, endpoint, engine, ring, max_batch=B, max_delay_s=0.0005).start()
+    queue = cp.queue_for(endpoint)
+
+    def submit_step():
+        slots = ring.alloc(B, timeout=60)
+        ids = cp.store.create_many(endpoint, B)
+        queue.send_many(ids, slots)
+        return ids
+
+    def run(nsteps):
+        target = worker.images + nsteps * B
+        all_ids = []
+        submitted = 0
+        while submitted < min(args.inflight, nsteps):
+            all_ids += submit_step()
+            submitted += 1
+        while worker.images < target:
+            done_steps = (worker.images - (target - nsteps * B)) // B
+            while submitted < nsteps and submitted - done_steps < args.inflight:
+                all_ids += submit_step()
+                submitted += 1
+            time.sleep(0.0002)
+        return all_ids
+
+    def sync():
+        if device.type == "cuda":
+            torch.cuda.synchronize(device)
+        if dist is not None:
+            dist.barrier()
+
+    run(args.warmup)
+    sync()
+    t0 = time.perf_counter()
+    ids = run(args.steps)
+    sync()
+    dt = time.perf_counter() - t0
+    worker.stop()
+    lat = sorted(cp.store.latencies(ids))
+    p50, p99 = percentile(lat, 50) * 1e3, percentile(lat, 99) * 1e3
+    stats = torch.tensor([dt, p50, p99], dtype=torch.float64, device=device if world > 1 and device.type == "cuda" else "cpu")
+    if dist is not None:
+        dist.all_reduce(stats, op=dist.ReduceOp.MAX)
+    dt, p50, p99 = [float(x) for x in stats.cpu()]
+    images = args.steps * B * world
+    value = images / dt
+    gflop_img = model.flops(1, S, S) / 1e9
+    out = {
+        "metric": METRIC, "value": round(value, 2), "unit": "images/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None if BASELINE_VALUE is None else round(value / BASELINE_VALUE, 4),
+        "dtype": "bf16", "data": "synthetic uint8 images, random-init weights",
+        "p50_task_latency_ms": round(p50, 3), "p99_task_latency_ms": round(p99, 3),
+        "tflops_effective": round(value * gflop_img / 1e3, 2),
+        "config": {"model": "resnet50", "global_batch": B * world, "per_gpu_batch": B, "image_size": S,
+                   "seq_len": None, "parallelism": f"dp{world}", "api": "async", "inflight_steps": args.inflight,
+                   "hip_graphs": not args.no_graphs, "kernel_backend": args.backend},
+    }
+    if rank == 0:
+        line = json.dumps(out)
+        print(line, flush=True)
+        if args.json_out:
+            with open(args.json_out, "w") as f:
+                f.write(line + "\n")
+    cp.close()
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

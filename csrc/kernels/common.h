@@ -1,0 +1,44 @@
+// Shared helpers for the gfx950 (CDNA4, MI355X) kernels. Wave64 everywhere.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+typedef float f32x16_t __attribute__((ext_vector_type(16)));
+
+#define AI4E_API extern "C" __attribute__((visibility("default")))
+
+// Error codes returned by the C ABI launchers (0 = ok).
+enum { AI4E_OK = 0, AI4E_EINVAL = 1, AI4E_ELAUNCH = 2 };
+
+__device__ __forceinline__ float bf16_to_f32(uint16_t h) {
+  return __uint_as_float(static_cast<uint32_t>(h) << 16);
+}
+
+// Round-to-nearest-even float -> bf16 bits (NaN kept quiet).
+__device__ __forceinline__ uint16_t f32_to_bf16(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x007fffffu)) return 0x7fc0;
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return static_cast<uint16_t>(u >> 16);
+}
+
+__device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
+  return static_cast<uint32_t>(f32_to_bf16(lo)) | (static_cast<uint32_t>(f32_to_bf16(hi)) << 16);
+}
+
+__device__ __forceinline__ void unpack_bf16x2(uint32_t v, float& lo, float& hi) {
+  lo = __uint_as_float(v << 16);
+  hi = __uint_as_float(v & 0xffff0000u);
+}
+
+// Bijective XCD-aware remap of a linear workgroup id: the dispatcher places workgroup b on XCD
+// (b % 8); give each XCD a contiguous run of logical tiles so neighbouring tiles (which share an
+// operand panel) hit the same private L2 (cdna_hip_programming.md §5.5 T1).
+__device__ __forceinline__ int xcd_remap(int b, int nb) {
+  const int xcd = b & 7, q = nb >> 3, r = nb & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+}
+
+static inline int ai4e_cdiv(long a, long b) { return static_cast<int>((a + b - 1) / b); }

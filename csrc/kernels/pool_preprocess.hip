@@ -1,0 +1,112 @@
+// K7 preprocess, max-pool, global-avg-pool — memory-bound NHWC bf16 kernels, 16-B vectors per lane.
+#include "common.h"
+
+namespace {
+
+// uint8 [N,H,W,Cin] (Cin<=8, e.g. decoded RGB / RGB+NIR) -> bf16 [N,H,W,8], (x*scale - mean)/std,
+// channels >= Cin zero-filled so the stem conv sees C = 8 (one 16-B vector per pixel).
+__global__ __launch_bounds__(256) void preprocess_u8_kernel(const uint8_t* __restrict__ in, uint16_t* __restrict__ out,
+                                                            long npix, int cin, float4 mean_lo, float4 mean_hi,
+                                                            float4 istd_lo, float4 istd_hi, float scale) {
+  const float mean[8] = {mean_lo.x, mean_lo.y, mean_lo.z, mean_lo.w, mean_hi.x, mean_hi.y, mean_hi.z, mean_hi.w};
+  const float istd[8] = {istd_lo.x, istd_lo.y, istd_lo.z, istd_lo.w, istd_hi.x, istd_hi.y, istd_hi.z, istd_hi.w};
+  for (long p = blockIdx.x * 256L + threadIdx.x; p < npix; p += static_cast<long>(gridDim.x) * 256) {
+    float v[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) v[c] = c < cin ? (in[p * cin + c] * scale - mean[c]) * istd[c] : 0.f;
+    uint4 o = make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]),
+                         pack_bf16x2(v[6], v[7]));
+    reinterpret_cast<uint4*>(out)[p] = o;
+  }
+}
+
+// Max pool NHWC bf16; one lane = 8 channels of one output pixel. Padding ignored (= -inf).
+__global__ __launch_bounds__(256) void maxpool_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y, int N,
+                                                      int H, int W, int C, int OH, int OW, int k, int s, int pad) {
+  const int C8 = C >> 3;
+  const long total = static_cast<long>(N) * OH * OW * C8;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += static_cast<long>(gridDim.x) * 256) {
+    const int c8 = static_cast<int>(i % C8);
+    long pix = i / C8;
+    const int ow = static_cast<int>(pix % OW);
+    pix /= OW;
+    const int oh = static_cast<int>(pix % OH);
+    const int n = static_cast<int>(pix / OH);
+    float m[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) m[j] = -INFINITY;
+    for (int dh = 0; dh < k; ++dh) {
+      const int ih = oh * s - pad + dh;
+      if (ih < 0 || ih >= H) continue;
+      for (int dw = 0; dw < k; ++dw) {
+        const int iw = ow * s - pad + dw;
+        if (iw < 0 || iw >= W) continue;
+        const uint4 v = reinterpret_cast<const uint4*>(x)[((static_cast<long>(n) * H + ih) * W + iw) * C8 + c8];
+        float a, b;
+        unpack_bf16x2(v.x, a, b); m[0] = fmaxf(m[0], a); m[1] = fmaxf(m[1], b);
+        unpack_bf16x2(v.y, a, b); m[2] = fmaxf(m[2], a); m[3] = fmaxf(m[3], b);
+        unpack_bf16x2(v.z, a, b); m[4] = fmaxf(m[4], a); m[5] = fmaxf(m[5], b);
+        unpack_bf16x2(v.w, a, b); m[6] = fmaxf(m[6], a); m[7] = fmaxf(m[7], b);
+      }
+    }
+    reinterpret_cast<uint4*>(y)[i] =
+        make_uint4(pack_bf16x2(m[0], m[1]), pack_bf16x2(m[2], m[3]), pack_bf16x2(m[4], m[5]), pack_bf16x2(m[6], m[7]));
+  }
+}
+
+// Global average pool [N, HW, C] -> [N, C] (bf16 out, fp32 accumulate). One lane = 8 channels.
+__global__ __launch_bounds__(256) void avgpool_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y, int N,
+                                                      int HW, int C) {
+  const int C8 = C >> 3;
+  const long total = static_cast<long>(N) * C8;
+  const float inv = 1.f / HW;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += static_cast<long>(gridDim.x) * 256) {
+    const int c8 = static_cast<int>(i % C8);
+    const long n = i / C8;
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const uint4* p = reinterpret_cast<const uint4*>(x) + n * HW * C8 + c8;
+    for (int j = 0; j < HW; ++j) {
+      const uint4 v = p[static_cast<long>(j) * C8];
+      float a, b;
+      unpack_bf16x2(v.x, a, b); acc[0] += a; acc[1] += b;
+      unpack_bf16x2(v.y, a, b); acc[2] += a; acc[3] += b;
+      unpack_bf16x2(v.z, a, b); acc[4] += a; acc[5] += b;
+      unpack_bf16x2(v.w, a, b); acc[6] += a; acc[7] += b;
+    }
+    reinterpret_cast<uint4*>(y)[i] = make_uint4(pack_bf16x2(acc[0] * inv, acc[1] * inv), pack_bf16x2(acc[2] * inv, acc[3] * inv),
+                                                pack_bf16x2(acc[4] * inv, acc[5] * inv), pack_bf16x2(acc[6] * inv, acc[7] * inv));
+  }
+}
+
+inline int grid_for(long work) {
+  long g = (work + 255) / 256;
+  return static_cast<int>(g < 1 ? 1 : (g > 8192 ? 8192 : g));
+}
+
+}  // namespace
+
+AI4E_API int ai4e_preprocess_u8(const void* in, void* out, long npix, int cin, const float* mean8, const float* std8,
+                                float scale, hipStream_t s) {
+  if (cin < 1 || cin > 8) return AI4E_EINVAL;
+  float4 ml = make_float4(mean8[0], mean8[1], mean8[2], mean8[3]), mh = make_float4(mean8[4], mean8[5], mean8[6], mean8[7]);
+  float4 il = make_float4(1.f / std8[0], 1.f / std8[1], 1.f / std8[2], 1.f / std8[3]);
+  float4 ih = make_float4(1.f / std8[4], 1.f / std8[5], 1.f / std8[6], 1.f / std8[7]);
+  hipLaunchKernelGGL(preprocess_u8_kernel, dim3(grid_for(npix)), dim3(256), 0, s, static_cast<const uint8_t*>(in),
+                     static_cast<uint16_t*>(out), npix, cin, ml, mh, il, ih, scale);
+  return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
+}
+
+AI4E_API int ai4e_maxpool2d(const void* x, void* y, int N, int H, int W, int C, int OH, int OW, int k, int stride,
+                            int pad, hipStream_t s) {
+  if (C % 8) return AI4E_EINVAL;
+  hipLaunchKernelGGL(maxpool_kernel, dim3(grid_for(static_cast<long>(N) * OH * OW * (C / 8))), dim3(256), 0, s,
+                     static_cast<const uint16_t*>(x), static_cast<uint16_t*>(y), N, H, W, C, OH, OW, k, stride, pad);
+  return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
+}
+
+AI4E_API int ai4e_global_avgpool(const void* x, void* y, int N, int HW, int C, hipStream_t s) {
+  if (C % 8) return AI4E_EINVAL;
+  hipLaunchKernelGGL(avgpool_kernel, dim3(grid_for(static_cast<long>(N) * (C / 8))), dim3(256), 0, s,
+                     static_cast<const uint16_t*>(x), static_cast<uint16_t*>(y), N, HW, C);
+  return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
+}

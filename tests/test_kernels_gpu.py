@@ -1,0 +1,136 @@
+"""HIP kernel numerics vs PyTorch fp32 references (GPU box only)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+from aiforearth_api_platform_amd.ops import _ext
+from aiforearth_api_platform_amd.ops.conv import conv2d_nhwc, pack_conv
+from aiforearth_api_platform_amd.ops.pool import global_avgpool_nhwc, maxpool2d_nhwc, preprocess_u8
+
+DEV = "cuda"
+
+
+@pytest.fixture(autouse=True, scope="module")
+def _lib():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from aiforearth_api_platform_amd import _build
+    _build.build_kernels()
+    _ext.lib()
+
+
+def ref_conv(x, w, b, stride, pad, res=None, relu=False):
+    y = F.conv2d(x.float().permute(0, 3, 1, 2), w.float(), b.float(), stride=stride, padding=pad).permute(0, 2, 3, 1)
+    if res is not None:
+        y = y + res.float()
+    return F.relu(y) if relu else y
+
+
+CASES = [
+    # n, h, w, cin, cout, k, stride, pad
+    (2, 56, 56, 64, 64, 1, 1, 0),
+    (2, 56, 56, 64, 64, 3, 1, 1),
+    (2, 56, 56, 64, 256, 1, 1, 0),
+    (2, 56, 56, 128, 128, 3, 2, 1),
+    (3, 28, 28, 256, 512, 1, 2, 0),
+    (2, 7, 7, 512, 2048, 1, 1, 0),
+    (2, 112, 112, 3, 64, 7, 2, 3),      # stem (C padded to 8)
+    (5, 1, 1, 2048, 1000, 1, 1, 0),     # classifier, M tiny, Kout % 64 != 0
+    (1, 33, 17, 40, 96, 3, 1, 1),       # ragged M / C=40 (not multiple of 32)
+]
+
+
+@pytest.mark.parametrize("case", CASES)
+@pytest.mark.parametrize("epi", ["plain", "relu", "res_relu"])
+def test_conv_igemm(case, epi):
+    n, h, w, cin, cout, k, s, p = case
+    torch.manual_seed(0)
+    wt = torch.randn(cout, cin, k, k) / (cin * k * k) ** 0.5
+    b = torch.randn(cout) * 0.1
+    pc = pack_conv(wt, b, stride=s, pad=p).to(DEV)
+    x = torch.randn(n, h, w, pc.cin_pad, device=DEV).to(torch.bfloat16)
+    x[..., cin:] = 0
+    oh, ow = pc.out_hw(h, w)
+    res = torch.randn(n, oh, ow, cout, device=DEV).to(torch.bfloat16) if epi == "res_relu" else None
+    y = conv2d_nhwc(x, pc, residual=res, relu=epi != "plain")
+    torch.cuda.synchronize()
+    wq = pc.w_packed[:cout, :k * k * pc.cin_pad].float().reshape(cout, k, k, pc.cin_pad).permute(0, 3, 1, 2)
+    ref = ref_conv(x, wq, b.to(DEV), s, p, res, epi != "plain")
+    err = (y.float() - ref).abs().max().item()
+    assert err <= 0.02 * ref.abs().max().item() + 0.02, err
+
+
+@pytest.mark.parametrize("tile", [1, 2, 3, 4])
+def test_conv_tile_configs(tile):
+    torch.manual_seed(1)
+    wt = torch.randn(256, 64, 3, 3) / 24
+    pc = pack_conv(wt, torch.zeros(256), pad=1).to(DEV)
+    x = torch.randn(2, 20, 20, 64, device=DEV).to(torch.bfloat16)
+    y = conv2d_nhwc(x, pc, tile_cfg=tile)
+    ref = ref_conv(x, pc.w_packed[:256, :576].float().reshape(256, 3, 3, 64).permute(0, 3, 1, 2), torch.zeros(256, device=DEV), 1, 1)
+    assert (y.float() - ref).abs().max().item() < 0.02 * ref.abs().max().item() + 0.02
+
+
+def test_conv_channel_slices():
+    """Write into a channel slice of a concat buffer and read from a channel slice."""
+    torch.manual_seed(2)
+    pc = pack_conv(torch.randn(32, 16, 3, 3) / 12, torch.randn(32), pad=1).to(DEV)
+    big = torch.randn(1, 9, 9, 48, device=DEV).to(torch.bfloat16)
+    xin = big[..., 16:32]
+    out = torch.zeros(1, 9, 9, 64, device=DEV, dtype=torch.bfloat16)
+    conv2d_nhwc(xin, pc, out=out, out_coff=32)
+    ref = ref_conv(xin.contiguous(), pc.w_packed[:32, :144].float().reshape(32, 3, 3, 16).permute(0, 3, 1, 2),
+                   pc.bias[:32], 1, 1)
+    assert out[..., :32].abs().max().item() == 0
+    assert (out[..., 32:].float() - ref).abs().max().item() < 0.05
+
+
+def test_preprocess_maxpool_avgpool():
+    img = torch.randint(0, 256, (3, 31, 29, 3), dtype=torch.uint8, device=DEV)
+    y = preprocess_u8(img)
+    import os
+    os.environ["AI4E_KERNEL_BACKEND"] = "torch"
+    try:
+        ref = preprocess_u8(img.cpu())
+    finally:
+        os.environ["AI4E_KERNEL_BACKEND"] = "auto"
+    assert (y.float().cpu() - ref).abs().max().item() < 0.02
+    x = torch.randn(2, 57, 55, 64, device=DEV).to(torch.bfloat16)
+    mp = maxpool2d_nhwc(x)
+    mref = F.max_pool2d(x.float().permute(0, 3, 1, 2), 3, 2, 1).permute(0, 2, 3, 1)
+    assert torch.equal(mp.float(), mref)
+    ap = global_avgpool_nhwc(x)
+    aref = x.float().mean(dim=(1, 2), keepdim=True)
+    assert (ap.float() - aref).abs().max().item() < 0.01
+
+
+def test_resnet50_fused_matches_reference():
+    from aiforearth_api_platform_amd.models.resnet import FusedResNet, resnet50
+    torch.manual_seed(0)
+    m = resnet50(seed=3)
+    fused = FusedResNet(m, device=DEV)
+    img = torch.randint(0, 256, (4, 224, 224, 3), dtype=torch.uint8)
+    logits = fused(img.to(DEV)).cpu()
+    x = preprocess_u8(img)[..., :3].permute(0, 3, 1, 2).float()
+    with torch.no_grad():
+        ref = m(x)
+    rel = (logits - ref).norm() / ref.norm()
+    assert rel < 0.05, rel.item()
+    # top-1 agreement on most images
+    assert (logits.argmax(1) == ref.argmax(1)).float().mean() >= 0.75
+
+
+def test_engine_graph_replay_matches_eager():
+    from aiforearth_api_platform_amd.models.resnet import FusedResNet, resnet50
+    from aiforearth_api_platform_amd.runtime.engine import InferenceEngine
+    fused = FusedResNet(resnet50(seed=4), device=DEV)
+    eng = InferenceEngine(fused.forward_u8, (64, 64, 3), 8, device=torch.device(DEV), use_graphs=True, buckets=[4, 8])
+    eng.warmup()
+    img = torch.randint(0, 256, (6, 64, 64, 3), dtype=torch.uint8)
+    i_g, p_g = eng.run_sync(img)
+    logits = fused(img.to(DEV))
+    p, i = torch.topk(torch.softmax(logits.float(), 1), 5, 1)
+    assert torch.equal(i_g[:, 0], i[:, 0].int().cpu())
+    assert torch.allclose(p_g, p.cpu(), atol=1e-3)
