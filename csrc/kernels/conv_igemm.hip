@@ -15,13 +15,17 @@
 // * Operands are swapped (A = weights, B = activations) so each lane's accumulator holds 4
 //   consecutive output CHANNELS of one pixel: the epilogue stores 8 contiguous bytes per lane
 //   straight from registers (bias float4, residual 8-B loads) with no LDS round trip.
-// * A/B tiles (BK = 32) are register-staged into a 2-deep LDS ring with one barrier per K-step;
-//   the global loads of step k+1 are issued before the MFMAs of step k (cdna guide T14).
+// * A/B tiles (BK = 32) stream global -> LDS by LDS-DMA (global_load_lds_dwordx4, no VGPR staging)
+//   into a 4-deep ring: 3 K-steps stay in flight across the one raw s_barrier per step, retired by a
+//   counted vmcnt (cdna guide §5 "Pipelining across barriers", T3/T4) — one K-step of MFMA work is
+//   far shorter than an HBM round trip, so depth, not a 2-buffer swap, is what hides latency.
 //   Each 64-B LDS row (32 bf16) is XOR-swizzled per 16-B chunk with s = {0,2,3,1}[(row>>2)&3],
 //   which makes every ds_read_b128 fragment read conflict-free for the gfx950 lane groups
-//   {0-3,12-15,20-27},{4-11,16-19,28-31},... (MI355X_MICROARCH.md §LDS).
-// * The activation gather handles padding/stride/any KHxKW with 16-B loads per (pixel, tap,
-//   8-channel chunk); C must be a multiple of 8 (the stem is fed C=8 by the preprocess kernel).
+//   {0-3,12-15,20-27},{4-11,16-19,28-31},... (MI355X_MICROARCH.md §LDS). Since an LDS-DMA writes
+//   base + 16*lane, the swizzle is applied to the per-lane SOURCE address (rule 21).
+// * The activation gather handles padding/stride/any KHxKW with one 16-B DMA per (pixel, tap,
+//   8-channel chunk); padding taps read a zero chunk. C must be a multiple of 8 (the stem is fed C=8
+//   by the preprocess kernel). The residual tile is prefetched into registers before the K loop.
 // * XCD-aware tile order: tiles that share an activation panel (same m-tile, different n-tiles)
 //   land on one XCD's L2 (common.h xcd_remap).
 #include "common.h"
@@ -29,6 +33,9 @@
 namespace {
 
 constexpr int BK = 32;
+
+// Source of the zero 16-B chunks the DMA gather reads for padding / out-of-range taps.
+__device__ __attribute__((aligned(64))) uint16_t g_zero_chunk[32];
 
 struct ConvParams {
   const uint16_t* x;
@@ -48,19 +55,41 @@ struct ConvParams {
 
 __device__ __forceinline__ int swz(int row) { return (0x78 >> (2 * ((row >> 2) & 3))) & 3; }
 
-template <int WAVES_M, int WAVES_N>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, WAVES_N > 1 ? 2 : 3))) void conv_igemm_kernel(const ConvParams p) {
+// One 16-B LDS-DMA per lane: global -> LDS at (wave-uniform M0 base + 16*lane). Inline asm so hipcc
+// neither drains it with vmcnt(0) before every ds_read nor at barriers (cdna guide §5.7, §5 "Pipelining
+// across barriers"); completion is tracked by hand with counted vmcnt.
+__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_base) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds_base)
+      : "memory");
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int WAVES_M, int WAVES_N, int STAGES>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) void conv_igemm_kernel(const ConvParams p) {
+  static_assert(WAVES_M * WAVES_N == 4, "4 waves per workgroup");
   constexpr int BM = WAVES_M * 64;  // pixels per workgroup
   constexpr int BN = WAVES_N * 64;  // channels per workgroup
-  constexpr int CA = BM / 64;       // A (activation) 16-B chunks per thread per K-step
-  constexpr int CB = BN / 64;       // B (weight) chunks per thread per K-step
-  __shared__ __attribute__((aligned(16))) uint16_t smem[2 * (BM + BN) * BK];
-  uint16_t* const sX = smem;                // [2][BM][BK]
-  uint16_t* const sW = smem + 2 * BM * BK;  // [2][BN][BK]
+  constexpr int CA = BM / 64;       // A (activation) DMA instructions per wave per stage
+  constexpr int CB = BN / 64;       // B (weight) DMA instructions per wave per stage
+  constexpr int PER_STAGE = CA + CB;
+  constexpr int STAGE_ELEMS = (BM + BN) * BK;
+  __shared__ __attribute__((aligned(1024))) uint16_t smem[STAGES * STAGE_ELEMS];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
-  const int wave = tid >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave % WAVES_M;
   const int wn = wave / WAVES_M;
 
@@ -70,15 +99,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, WAVES_N 
   const int m0 = mt * BM;
   const int n0 = nt * BN;
 
-  // ---- per-thread load assignment: chunk column c fixed, rows (tid>>2) + 64*i
-  const int c = tid & 3;
-  const int r0 = tid >> 2;
+  // ---- residual prefetch (issued first: the first stage wait also retires it)
+  const int pm = m0 + wm * 64 + (lane & 15);
+  const int pn = n0 + wn * 64 + 4 * (lane >> 4);
+  uint2 rres[4][4];
+  if (p.res) {  // unconditional loads (clamped rows/cols) so hipcc keeps one counted wait for all 16
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = min(pm + 16 * i, p.M - 1), n = min(pn + 16 * j, p.Kout - 4);
+        rres[i][j] = *reinterpret_cast<const uint2*>(p.res + static_cast<long>(m) * p.ldres + n);
+      }
+  }
+
+  // ---- DMA lane mapping: lane writes LDS slot 16*lane of a 16-row x 64-B block, i.e. row lane>>2,
+  //      physical chunk lane&3, which holds logical k-chunk c = (lane&3) ^ swz(row).
+  const int rin = lane >> 2;
+  const int c = (lane & 3) ^ swz(rin);
   const int OHW = p.OH * p.OW;
   int ih0[CA], iw0[CA];
   long xbase[CA];
 #pragma unroll
   for (int i = 0; i < CA; ++i) {
-    const int m = m0 + r0 + 64 * i;
+    const int m = m0 + 16 * (wave + 4 * i) + rin;
     if (m < p.M) {
       const int img = m / OHW;
       const int rem = m - img * OHW;
@@ -88,12 +132,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, WAVES_N 
       iw0[i] = ow * p.stride - p.pad;
       xbase[i] = static_cast<long>(img) * p.H * p.W * p.ldx + p.xcoff;
     } else {
-      ih0[i] = -(1 << 28);  // forces the bounds check to fail -> zeros
+      ih0[i] = -(1 << 28);  // fails the bounds check -> zero page
       iw0[i] = 0;
       xbase[i] = 0;
     }
   }
-  // k-state of this thread's chunk: k = kt*BK + 8c  ->  (kh, kw, cc)
   int cc, kh, kw;
   {
     const int k = 8 * c;
@@ -102,46 +145,32 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, WAVES_N 
     kh = tap / p.KW;
     kw = tap - kh * p.KW;
   }
-  const uint16_t* const wbase = p.w + static_cast<long>(n0 + r0) * p.Kpad + 8 * c;
-  const long wstride64 = 64L * p.Kpad;
+  const uint16_t* const wsrc = p.w + static_cast<long>(n0 + 16 * wave + rin) * p.Kpad + 8 * c;
+  const long wstep = 64L * p.Kpad;  // rows 16*(wave+4i)
+  const uint32_t smem_base = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(smem));
 
-  uint4 ra[CA], rb[CB];
-  // Issue the global loads of K-tile kt into registers, then advance the k-state by BK.
-#define AI4E_LOAD_TILE(kt)                                                                                   \
-  do {                                                                                                       \
-    _Pragma("unroll") for (int i = 0; i < CA; ++i) {                                                         \
-      const int ih = ih0[i] + kh, iw = iw0[i] + kw;                                                          \
-      uint4 v = make_uint4(0, 0, 0, 0);                                                                      \
-      if (kh < p.KH && static_cast<unsigned>(ih) < static_cast<unsigned>(p.H) &&                             \
-          static_cast<unsigned>(iw) < static_cast<unsigned>(p.W))                                            \
-        v = *reinterpret_cast<const uint4*>(p.x + xbase[i] + (static_cast<long>(ih) * p.W + iw) * p.ldx + cc); \
-      ra[i] = v;                                                                                             \
-    }                                                                                                        \
-    _Pragma("unroll") for (int i = 0; i < CB; ++i) rb[i] =                                                   \
-        *reinterpret_cast<const uint4*>(wbase + i * wstride64 + (kt) * BK);                                  \
-    cc += BK;                                                                                                \
-    while (cc >= p.C) {                                                                                      \
-      cc -= p.C;                                                                                             \
-      if (++kw == p.KW) {                                                                                    \
-        kw = 0;                                                                                              \
-        ++kh;                                                                                                \
-      }                                                                                                      \
-    }                                                                                                        \
-  } while (0)
-  // Write the staged registers into LDS buffer `buf` (swizzled 16-B chunks).
-#define AI4E_STORE_TILE(buf)                                                                                 \
-  do {                                                                                                       \
-    uint16_t* sx_ = sX + (buf) * BM * BK;                                                                    \
-    uint16_t* sw_ = sW + (buf) * BN * BK;                                                                    \
-    _Pragma("unroll") for (int i = 0; i < CA; ++i) {                                                         \
-      const int row = r0 + 64 * i;                                                                           \
-      *reinterpret_cast<uint4*>(sx_ + row * BK + ((c ^ swz(row)) << 3)) = ra[i];                              \
-    }                                                                                                        \
-    _Pragma("unroll") for (int i = 0; i < CB; ++i) {                                                         \
-      const int row = r0 + 64 * i;                                                                           \
-      *reinterpret_cast<uint4*>(sw_ + row * BK + ((c ^ swz(row)) << 3)) = rb[i];                              \
-    }                                                                                                        \
-  } while (0)
+  auto issue_stage = [&](int kt) {
+    const uint32_t sbase = smem_base + (kt % STAGES) * STAGE_ELEMS * 2;
+#pragma unroll
+    for (int i = 0; i < CA; ++i) {
+      const int ih = ih0[i] + kh, iw = iw0[i] + kw;
+      const void* src = g_zero_chunk;
+      if (kh < p.KH && static_cast<unsigned>(ih) < static_cast<unsigned>(p.H) &&
+          static_cast<unsigned>(iw) < static_cast<unsigned>(p.W))
+        src = p.x + xbase[i] + (static_cast<long>(ih) * p.W + iw) * p.ldx + cc;
+      glds16(src, sbase + (16 * (wave + 4 * i)) * BK * 2);
+    }
+#pragma unroll
+    for (int i = 0; i < CB; ++i) glds16(wsrc + i * wstep + kt * BK, sbase + (BM + 16 * (wave + 4 * i)) * BK * 2);
+    cc += BK;
+    while (cc >= p.C) {
+      cc -= p.C;
+      if (++kw == p.KW) {
+        kw = 0;
+        ++kh;
+      }
+    }
+  };
 
   f32x4_t acc[4][4];
 #pragma unroll
@@ -149,19 +178,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, WAVES_N 
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  // fragment read offset (elements) inside a 16-row block: row = lane&15, chunk = lane>>4 swizzled
   const int frow = lane & 15;
   const int fofs = frow * BK + (((lane >> 4) ^ swz(frow)) << 3);
   const int nk = p.Kpad / BK;
 
-  AI4E_LOAD_TILE(0);
-  AI4E_STORE_TILE(0);
-  __syncthreads();
+#pragma unroll
+  for (int s = 0; s < STAGES - 1; ++s)
+    if (s < nk) issue_stage(s);
+
   for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) AI4E_LOAD_TILE(kt + 1);
-    const uint16_t* x = sX + cur * BM * BK + (wm * 64) * BK + fofs;
-    const uint16_t* w = sW + cur * BN * BK + (wn * 64) * BK + fofs;
+    // stage kt has landed once at most (younger stages in flight) * PER_STAGE DMAs are outstanding
+    const int younger = min(STAGES - 2, nk - 1 - kt);
+    if (younger >= 2) wait_vmcnt<2 * PER_STAGE>();
+    else if (younger == 1) wait_vmcnt<PER_STAGE>();
+    else wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();  // every wave's DMA for stage kt is in LDS; stage kt-1 fully read
+    if (kt + STAGES - 1 < nk) issue_stage(kt + STAGES - 1);
+    const uint16_t* st = smem + (kt % STAGES) * STAGE_ELEMS;
+    const uint16_t* x = st + (wm * 64) * BK + fofs;
+    const uint16_t* w = st + (BM + wn * 64) * BK + fofs;
     bf16x8_t bw[4], bx[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) bw[j] = *reinterpret_cast<const bf16x8_t*>(w + j * 16 * BK);
@@ -171,56 +206,64 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, WAVES_N 
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[j], bx[i], acc[i][j], 0, 0, 0);
-    if (kt + 1 < nk) AI4E_STORE_TILE(cur ^ 1);
-    __syncthreads();
   }
 
-#undef AI4E_LOAD_TILE
-#undef AI4E_STORE_TILE
-
-  // ---- fused epilogue: lane holds channels n..n+3 of pixel m for each (i, j) fragment
-  const int pm = m0 + wm * 64 + (lane & 15);
-  const int pn = n0 + wn * 64 + 4 * (lane >> 4);
+  // ---- fused epilogue: lane holds channels n..n+3 of pixel m for each (i, j) fragment.
+  // Phase 1 (no stores): bias + residual into the accumulators, so the residual registers are
+  // consumed behind ONE wait; phase 2: ReLU, pack, 8-B stores.
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float4 b = *reinterpret_cast<const float4*>(p.bias + min(pn + 16 * j, p.Kout - 4));
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      acc[i][j][0] += b.x; acc[i][j][1] += b.y; acc[i][j][2] += b.z; acc[i][j][3] += b.w;
+    }
+  }
+  if (p.res) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float a0, a1, a2, a3;
+        unpack_bf16x2(rres[i][j].x, a0, a1);
+        unpack_bf16x2(rres[i][j].y, a2, a3);
+        acc[i][j][0] += a0; acc[i][j][1] += a1; acc[i][j][2] += a2; acc[i][j][3] += a3;
+      }
+  }
+  const float lo = p.relu ? 0.f : -INFINITY;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int n = pn + 16 * j;
-    if (n >= p.Kout) continue;
-    const float4 b = *reinterpret_cast<const float4*>(p.bias + n);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int m = pm + 16 * i;
-      if (m >= p.M) continue;
-      float v0 = acc[i][j][0] + b.x, v1 = acc[i][j][1] + b.y, v2 = acc[i][j][2] + b.z, v3 = acc[i][j][3] + b.w;
-      if (p.res) {
-        const uint2 r = *reinterpret_cast<const uint2*>(p.res + static_cast<long>(m) * p.ldres + n);
-        float a0, a1, a2, a3;
-        unpack_bf16x2(r.x, a0, a1);
-        unpack_bf16x2(r.y, a2, a3);
-        v0 += a0; v1 += a1; v2 += a2; v3 += a3;
-      }
-      if (p.relu) {
-        v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
-      }
-      *reinterpret_cast<uint2*>(p.y + static_cast<long>(m) * p.ldy + p.ycoff + n) =
-          make_uint2(pack_bf16x2(v0, v1), pack_bf16x2(v2, v3));
+      if (m < p.M && n < p.Kout)
+        *reinterpret_cast<uint2*>(p.y + static_cast<long>(m) * p.ldy + p.ycoff + n) =
+            make_uint2(pack_bf16x2(fmaxf(acc[i][j][0], lo), fmaxf(acc[i][j][1], lo)),
+                       pack_bf16x2(fmaxf(acc[i][j][2], lo), fmaxf(acc[i][j][3], lo)));
     }
   }
 }
 
+}  // namespace
+
+namespace {
+
 template <int WM, int WN>
 int launch(const ConvParams& p0, hipStream_t s) {
+  constexpr int STAGES = 4;
   ConvParams p = p0;
   const int mt = ai4e_cdiv(p.M, WM * 64);
   p.ntiles_n = ai4e_cdiv(p.Kout, WN * 64);
   const int nb = mt * p.ntiles_n;
-  hipLaunchKernelGGL((conv_igemm_kernel<WM, WN>), dim3(nb), dim3(256), 0, s, p);
+  hipLaunchKernelGGL((conv_igemm_kernel<WM, WN, STAGES>), dim3(nb), dim3(256), 0, s, p);
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
 }
 
 }  // namespace
 
 // tile_cfg (pixels x channels per workgroup): 0 = auto, 1 = 128x128 (2x2 waves), 2 = 256x64 (4x1),
-// 3 = 64x256 (1x4), 4 = 128x64 (2x1).
+// 3 = 64x256 (1x4).
 AI4E_API int ai4e_conv2d_fwd(const void* x, const void* w, const void* bias, const void* res, void* y, int N, int H,
                              int W, int C, int ldx, int xcoff, int KH, int KW, int stride, int pad, int OH, int OW,
                              int Kout, int Kpad, int ldy, int ycoff, int ldres, int relu, int tile_cfg,
@@ -244,7 +287,6 @@ AI4E_API int ai4e_conv2d_fwd(const void* x, const void* w, const void* bias, con
     case 1: return launch<2, 2>(p, stream);
     case 2: return launch<4, 1>(p, stream);
     case 3: return launch<1, 4>(p, stream);
-    case 4: return launch<2, 1>(p, stream);
     default: return AI4E_EINVAL;
   }
 }
