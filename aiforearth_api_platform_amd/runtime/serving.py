@@ -80,20 +80,31 @@ class GpuBatchWorker:
         self.images = 0
         self._stop = threading.Event()
         self._thread: Optional[threading.Thread] = None
+        self.phase_s = collections.defaultdict(float)  # host time per worker phase (diagnostics)
+        self.finalize_times: Deque[float] = collections.deque(maxlen=4096)
         self._h_batch = REGISTRY.histogram(f"batch_size{endpoint}", buckets=(1, 8, 32, 64, 128, 256, 512, 1024))
         self._c_images = REGISTRY.counter(f"images_total{endpoint}")
 
     def step(self, timeout_s: Optional[float] = None) -> int:
         """Receive at most one batch, launch it, finalize older batches. Returns #images launched."""
-        msgs = self.queue.receive(self.max_batch, self.poll_s if timeout_s is None else timeout_s, self.max_delay_s)
+        t0 = time.perf_counter()
+        if timeout_s is None:
+            # never park in receive while a launched batch may be finishing: poll at 0.5 ms
+            timeout_s = 0.0005 if self.pending else self.poll_s
+        msgs = self.queue.receive(self.max_batch, timeout_s, self.max_delay_s)
         n = len(msgs)
+        t1 = time.perf_counter()
+        self.phase_s["receive"] += t1 - t0
         if n:
             ids = [m.task_id for m in msgs]
             slots = [m.ref for m in msgs]
             seqs = [m.seq for m in msgs]
             self.store.transition_many(ids, STATE_RUNNING, STATE_RUNNING)
+            t2 = time.perf_counter()
+            self.phase_s["unpack+running"] += t2 - t1
             try:
                 res = self.engine.submit(self.ring.buf, slots)
+                self.phase_s["submit"] += time.perf_counter() - t2
             except Exception as e:  # launch failure -> redeliver the whole batch
                 self.cp.log.log_error(f"batch launch failed: {e}", self.endpoint)
                 for s in seqs:
@@ -103,14 +114,19 @@ class GpuBatchWorker:
                 return 0
             self.pending.append((ids, seqs, slots, res))
             self._h_batch.observe(n)
-        keep = 1 if n else 0  # keep one batch in flight while the next is being formed
-        while len(self.pending) > keep:
+        # keep one batch in flight while the next is being formed; with no new work, retire a
+        # batch as soon as its completion event fires
+        keep = 1 if n else 0
+        while len(self.pending) > keep or (self.pending and self.pending[0][3].done.query()):
             self._finalize(self.pending.popleft())
         return n
 
     def _finalize(self, item) -> None:
         ids, seqs, slots, res = item
+        t0 = time.perf_counter()
         res.done.synchronize()
+        t1 = time.perf_counter()
+        self.phase_s["gpu_wait"] += t1 - t0
         self.ring.free(slots)
         self.results.put_batch(ids, res.top_idx.numpy().copy(), res.top_prob.numpy().copy())
         self.store.transition_many(ids, STATE_COMPLETED, STATE_COMPLETED)
@@ -118,6 +134,8 @@ class GpuBatchWorker:
         self.batches += 1
         self.images += len(ids)
         self._c_images.inc(len(ids))
+        self.phase_s["finalize"] += time.perf_counter() - t1
+        self.finalize_times.append(t1)
 
     def _fail_deadletters(self) -> None:
         dead = self.queue.take_deadletters()

@@ -57,6 +57,7 @@ def main():
     from aiforearth_api_platform_amd.gateway.control import ControlPlane
     from aiforearth_api_platform_amd.models.resnet import FusedResNet, resnet50
     from aiforearth_api_platform_amd.runtime.engine import InferenceEngine, PayloadRing
+    from aiforearth_api_platform_amd.runtime.hostperf import tune_gc
     from aiforearth_api_platform_amd.runtime.serving import GpuBatchWorker
     from aiforearth_api_platform_amd.utils.metrics import percentile
 
@@ -123,7 +124,10 @@ def main():
             dist.barrier()
 
     run(args.warmup)
+    tune_gc()
     sync()
+    worker.phase_s.clear()
+    worker.finalize_times.clear()
     t0 = time.perf_counter()
     ids = run(args.steps)
     sync()
@@ -149,6 +153,12 @@ def main():
                    "seq_len": None, "parallelism": f"dp{world}", "api": "async", "inflight_steps": args.inflight,
                    "hip_graphs": not args.no_graphs, "kernel_backend": args.backend},
     }
+    if os.environ.get("AI4E_BENCH_DEBUG"):
+        import numpy as np
+        ft = np.diff(np.array(worker.finalize_times)) * 1e3
+        print("worker phases (s):", {k: round(v, 4) for k, v in worker.phase_s.items()}, "batches", worker.batches,
+              "finalize interval ms: median %.3f min %.3f max %.3f" % (np.median(ft), ft.min(), ft.max()),
+              "first finalize after t0 %.3f ms" % ((worker.finalize_times[0] - t0) * 1e3), file=sys.stderr)
     if rank == 0:
         line = json.dumps(out)
         print(line, flush=True)
