@@ -1,0 +1,266 @@
+"""HTTP front end: the API Management gateway + Istio routing + Functions HTTP triggers, in one process.
+
+Routes (all served by one aiohttp application):
+
+* ``POST <route prefix>[/...]`` — per the route table (replaces the Istio VirtualService prefix match
+  + rewrite of ``APIs/Charts/templates/routing.yml:10-18`` and the APIM API definitions):
+  ``async`` routes create a task and return ``200`` + the task JSON immediately
+  (``APIManagement/request_policy.xml:5-28``; ``500 "Task insert failed."`` on failure); ``sync``
+  routes proxy to the backend and return its response (``request_backend_policy.xml``).
+* ``GET /v1/taskmanagement/task/{taskId}`` — task status, verbatim store JSON or ``204``
+  (``task_management_policy.xml`` -> ``CacheConnectorGet``); ``.../result`` returns the model output.
+* ``POST /v1/cache/upsert``, ``GET /v1/cache/get?taskId=`` — CacheConnectorUpsert / Get.
+* ``POST /v1/requests/upsert``, ``POST /v1/requests/get`` — RequestReporter (CURRENT_REQUESTS).
+* ``POST /v1/backend/webhook`` — BackendWebhook incl. the Event Grid validation handshake.
+* ``GET /metrics`` (Prometheus text), ``GET /v1/platform/stats`` (JSON), ``GET /`` health.
+
+Admission control per route mirrors ``APIService.before_request`` (429 busy, 503 draining,
+401 content type, 413 too large).
+"""
+from __future__ import annotations
+
+import asyncio
+import json
+import signal
+from dataclasses import dataclass, field
+from typing import Any, Callable, Dict, List, Optional, Union
+
+from aiohttp import ClientSession, web
+
+from ..store import APITask
+from ..store.pystore import absolute_path
+from ..utils.metrics import REGISTRY
+from .control import ControlPlane
+
+TASK_INSERT_FAILED = "Task insert failed."
+
+
+@dataclass
+class Route:
+    prefix: str
+    mode: str = "async"                      # async | sync
+    backend: Any = None                      # ModelEndpoint | callable(task_id, body, headers) | "http://..."
+    rewrite: Optional[str] = None            # VirtualService rewrite of the matched prefix
+    max_concurrent: Optional[int] = None
+    content_types: Optional[List[str]] = None
+    max_content_length: Optional[int] = None
+    inflight: int = field(default=0, repr=False)
+
+    def target_path(self, path: str) -> str:
+        if self.rewrite is None:
+            return path
+        return self.rewrite + path[len(self.prefix):]
+
+
+class RouteTable:
+    def __init__(self, routes: Optional[List[Route]] = None):
+        self.routes: List[Route] = list(routes or [])
+
+    def add(self, route: Route) -> Route:
+        self.routes.append(route)
+        self.routes.sort(key=lambda r: -len(r.prefix))  # longest prefix wins
+        return route
+
+    def match(self, path: str) -> Optional[Route]:
+        for r in self.routes:
+            if path == r.prefix or path.startswith(r.prefix.rstrip("/") + "/"):
+                return r
+        return None
+
+    @classmethod
+    def from_yaml(cls, path: str, backends: Dict[str, Any]) -> "RouteTable":
+        import yaml
+
+        with open(path) as f:
+            doc = yaml.safe_load(f) or {}
+        t = cls()
+        for r in doc.get("routes", []):
+            be = r.get("backend")
+            if isinstance(be, str) and be.startswith("inproc:"):
+                be = backends[be.split(":", 1)[1]]
+            t.add(Route(prefix=r["prefix"], mode=r.get("mode", "async"), backend=be, rewrite=r.get("rewrite"),
+                        max_concurrent=r.get("max_concurrent"), content_types=r.get("content_types"),
+                        max_content_length=r.get("max_content_length")))
+        return t
+
+
+class Gateway:
+    def __init__(self, control_plane: ControlPlane, routes: Optional[RouteTable] = None, webhook=None,
+                 base_url: str = "http://127.0.0.1"):
+        self.cp = control_plane
+        self.routes = routes or RouteTable()
+        self.webhook = webhook
+        self.base_url = base_url.rstrip("/")
+        self.is_terminating = False
+        self._session: Optional[ClientSession] = None
+        self.app = web.Application(client_max_size=1 << 30)
+        self.app.router.add_get("/", self.health)
+        self.app.router.add_get("/metrics", self.metrics)
+        self.app.router.add_get("/v1/platform/stats", self.stats)
+        self.app.router.add_get("/v1/taskmanagement/task/{taskId}", self.task_get)
+        self.app.router.add_get("/v1/taskmanagement/task/{taskId}/result", self.task_result)
+        self.app.router.add_post("/v1/cache/upsert", self.cache_upsert)
+        self.app.router.add_get("/v1/cache/get", self.cache_get)
+        self.app.router.add_post("/v1/requests/upsert", self.requests_upsert)
+        self.app.router.add_post("/v1/requests/get", self.requests_get)
+        self.app.router.add_post("/v1/backend/webhook", self.backend_webhook)
+        self.app.router.add_route("*", "/{tail:.*}", self.dispatch)
+        self.app.on_cleanup.append(self._cleanup)
+        self._c_req = REGISTRY.counter("gateway_requests_total")
+
+    # ------------------------------------------------------------------ platform routes
+    async def health(self, request):
+        if self.is_terminating:
+            return web.Response(status=503, text="Service is terminating")
+        return web.Response(text="Health check OK")
+
+    async def metrics(self, request):
+        for s in ("_created", "_running", "_completed", "_failed"):
+            self.cp.log_queue_lengths(s, adjust=0)
+        return web.Response(text=REGISTRY.prometheus_text(), content_type="text/plain")
+
+    async def stats(self, request):
+        return web.json_response({"control_plane": self.cp.stats(), "metrics": REGISTRY.snapshot()})
+
+    async def task_get(self, request):
+        code, body = self.cp.get(request.match_info["taskId"])
+        if code != 200:
+            return web.Response(status=code)
+        return web.Response(text=body, content_type="application/json")
+
+    async def task_result(self, request):
+        tid = request.match_info["taskId"]
+        for r in self.routes.routes:
+            res = getattr(r.backend, "result", None)
+            if callable(res):
+                out = res(tid)
+                if out is not None:
+                    return web.json_response({"TaskId": tid, "Result": out})
+        return web.Response(status=204)
+
+    async def cache_upsert(self, request):
+        code, body = self.cp.upsert(await request.read())
+        return web.Response(status=code, text=body or None, content_type="application/json" if body else None)
+
+    async def cache_get(self, request):
+        code, body = self.cp.get(request.query.get("taskId", ""))
+        if code != 200:
+            return web.Response(status=code)
+        return web.Response(text=body, content_type="application/json")
+
+    async def requests_upsert(self, request):
+        code, val = self.cp.current_processing_upsert(await request.read())
+        return web.Response(status=code)
+
+    async def requests_get(self, request):
+        d = json.loads(await request.read() or b"{}")
+        code, val = self.cp.current_processing_get(str(d.get("ServiceCluster", "")), str(d.get("ApiPath", "")))
+        return web.Response(status=code, text=None if val is None else str(val))
+
+    async def backend_webhook(self, request):
+        if self.webhook is None:
+            return web.Response(status=404)
+        events = json.loads(await request.read() or b"[]")
+        if isinstance(events, dict):
+            events = [events]
+        for ev in events:  # BackendWebhook.cs: "We should only have 1 event"
+            code, payload = await asyncio.get_running_loop().run_in_executor(None, self.webhook.handle_event, ev)
+            return web.json_response(payload, status=code) if payload is not None else web.Response(status=code)
+        return web.Response(status=200)
+
+    # ------------------------------------------------------------------ API routes
+    def _admit(self, route: Route, request) -> Optional[web.Response]:
+        if self.is_terminating:
+            return web.json_response({"message": "Service is terminating, please try again later."}, status=503)
+        if route.max_concurrent is not None and route.inflight + 1 > route.max_concurrent:
+            return web.json_response({"message": "Service is busy, please try again later."}, status=429)
+        if route.content_types and request.content_type not in route.content_types:
+            return web.json_response({"message": f"Content-type must be {route.content_types}"}, status=401)
+        if route.max_content_length and (request.content_length or 0) > route.max_content_length:
+            return web.json_response({"message": f"Request content too large ({request.content_length}). Must be "
+                                                 f"smaller than: {route.max_content_length}"}, status=413)
+        return None
+
+    async def dispatch(self, request):
+        route = self.routes.match(request.path)
+        if route is None or request.method not in ("POST", "PUT", "GET"):
+            return web.Response(status=404)
+        self._c_req.inc()
+        rej = self._admit(route, request)
+        if rej is not None:
+            return rej
+        route.inflight += 1
+        try:
+            body = await request.read()
+            if route.mode == "async":
+                return await self._async(route, request, body)
+            return await self._sync(route, request, body)
+        finally:
+            route.inflight -= 1
+
+    async def _async(self, route: Route, request, body: bytes):
+        loop = asyncio.get_running_loop()
+        target = route.target_path(request.path)
+        upstream_id = request.headers.get("taskId", "")
+        try:
+            if hasattr(route.backend, "submit"):
+                js = await loop.run_in_executor(None, route.backend.submit, body, request.content_type, upstream_id)
+            else:
+                js = await loop.run_in_executor(None, self.cp.create_async_task, self.base_url + target,
+                                                body.decode("utf-8", "replace"))
+        except Exception as e:
+            self.cp.log.log_error(f"{TASK_INSERT_FAILED} {e}", request.path)
+            return web.Response(status=500, text=TASK_INSERT_FAILED)
+        if "application/json" in request.headers.get("Accept", "application/json") or "*/*" in request.headers.get(
+                "Accept", ""):
+            return web.Response(text=js, content_type="application/json")
+        return web.Response(text="TaskId: " + json.loads(js)["TaskId"])
+
+    async def _sync(self, route: Route, request, body: bytes):
+        loop = asyncio.get_running_loop()
+        be = route.backend
+        if hasattr(be, "submit"):
+            fut = loop.create_future()
+
+            def done(tid, _f=fut):
+                loop.call_soon_threadsafe(lambda: _f.done() or _f.set_result(tid))
+
+            js = await loop.run_in_executor(None, lambda: be.submit(body, request.content_type, "", done))
+            tid = json.loads(js)["TaskId"]
+            await fut
+            rec = self.cp.get_dict(tid)
+            if rec is None or rec["BackendStatus"] != "completed":
+                return web.json_response(rec or {"TaskId": tid, "Status": "failed"}, status=500)
+            return web.json_response(be.result(tid))
+        if isinstance(be, str):
+            if self._session is None:
+                self._session = ClientSession()
+            url = be.rstrip("/") + route.target_path(request.path) if route.rewrite is not None else be
+            async with self._session.post(url, data=body, headers={"Content-Type": request.content_type or
+                                                                   "application/octet-stream"}) as r:
+                return web.Response(status=r.status, body=await r.read(), content_type=r.content_type)
+        if callable(be):
+            res = await loop.run_in_executor(None, be, "", body, dict(request.headers))
+            code, payload = (res if isinstance(res, tuple) else (200, res))
+            if isinstance(payload, (dict, list)):
+                return web.json_response(payload, status=code)
+            return web.Response(status=code, body=payload if isinstance(payload, bytes) else str(payload).encode())
+        return web.Response(status=502)
+
+    async def _cleanup(self, app):
+        if self._session is not None:
+            await self._session.close()
+
+    # ------------------------------------------------------------------ lifecycle
+    def install_signal_handlers(self) -> None:
+        def drain(*_):
+            self.is_terminating = True
+
+        for sig in (signal.SIGINT, signal.SIGTERM):
+            try:
+                signal.signal(sig, drain)
+            except ValueError:
+                pass
+
+    def run(self, host: str = "127.0.0.1", port: int = 8080) -> None:
+        web.run_app(self.app, host=host, port=port, handle_signals=False, print=None)

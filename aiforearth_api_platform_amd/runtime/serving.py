@@ -82,6 +82,7 @@ class GpuBatchWorker:
         self._thread: Optional[threading.Thread] = None
         self.phase_s = collections.defaultdict(float)  # host time per worker phase (diagnostics)
         self.finalize_times: Deque[float] = collections.deque(maxlen=4096)
+        self.on_batch_done = None  # optional callback(ids) after a batch is completed or failed
         self._h_batch = REGISTRY.histogram(f"batch_size{endpoint}", buckets=(1, 8, 32, 64, 128, 256, 512, 1024))
         self._c_images = REGISTRY.counter(f"images_total{endpoint}")
 
@@ -136,11 +137,15 @@ class GpuBatchWorker:
         self._c_images.inc(len(ids))
         self.phase_s["finalize"] += time.perf_counter() - t1
         self.finalize_times.append(t1)
+        if self.on_batch_done is not None:
+            self.on_batch_done(ids)
 
     def _fail_deadletters(self) -> None:
         dead = self.queue.take_deadletters()
         if dead:
             self.store.transition_many(dead, STATE_FAILED, "Task failed - maximum retries exceeded")
+            if self.on_batch_done is not None:
+                self.on_batch_done(dead)
 
     def flush(self) -> None:
         while self.pending:
