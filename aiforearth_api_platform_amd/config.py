@@ -81,9 +81,9 @@ class Config:
 
     @classmethod
     def load(cls, yaml_path: Optional[str] = None, env: Optional[Dict[str, str]] = None,
-             **overrides: Any) -> "Config":
+             yaml_values: Optional[Dict[str, Any]] = None, **overrides: Any) -> "Config":
         env = os.environ if env is None else env
-        values: Dict[str, Any] = {}
+        values: Dict[str, Any] = dict(yaml_values or {})
         yaml_path = yaml_path or env.get("AI4E_CONFIG")
         if yaml_path:
             import yaml

@@ -252,9 +252,26 @@ class Gateway:
             await self._session.close()
 
     # ------------------------------------------------------------------ lifecycle
-    def install_signal_handlers(self) -> None:
+    def idle(self) -> bool:
+        return all(r.inflight == 0 for r in self.routes.routes) and all(
+            q.depth() == 0 and q.stats()["inflight"] == 0 for q in self.cp.queues().values())
+
+    def install_signal_handlers(self, grace_s: float = 30.0) -> None:
+        """SIGINT/SIGTERM: stop admitting (503), finish queued + in-flight work, then exit."""
+        import _thread
+        import threading
+        import time
+
+        def wait_then_exit():
+            deadline = time.time() + grace_s
+            while time.time() < deadline and not self.idle():
+                time.sleep(0.05)
+            _thread.interrupt_main()
+
         def drain(*_):
-            self.is_terminating = True
+            if not self.is_terminating:
+                self.is_terminating = True
+                threading.Thread(target=wait_then_exit, daemon=True).start()
 
         for sig in (signal.SIGINT, signal.SIGTERM):
             try:

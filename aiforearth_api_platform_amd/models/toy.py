@@ -1,0 +1,32 @@
+"""Tiny models for plumbing tests and the CPU "echo" configuration (BASELINE config #1)."""
+from __future__ import annotations
+
+import torch
+
+
+class ChannelMeanClassifier:
+    """logits[b] = [mean(channel 0..C-1), 0, 0, 0]: deterministic, cheap, device-agnostic."""
+
+    def __init__(self, device="cpu", extra_classes: int = 3):
+        self.device = torch.device(device)
+        self.extra = extra_classes
+
+    def __call__(self, x_u8: torch.Tensor) -> torch.Tensor:
+        m = x_u8.float().mean(dim=(1, 2))
+        return torch.cat([m, torch.zeros(m.shape[0], self.extra, device=m.device)], dim=1)
+
+
+def tiny_classifier(device="cpu", **kw):
+    return ChannelMeanClassifier(device, **kw)
+
+
+def resnet50_fused(device="cuda", seed: int = 0, num_classes: int = 1000):
+    """Factory used by the worker pool for the headline ResNet-50 endpoint."""
+    from .resnet import FusedResNet, resnet50
+
+    return FusedResNet(resnet50(num_classes=num_classes, seed=seed), device=device).forward_u8
+
+
+def echo(task_id: str, body: bytes, headers=None):
+    """Sync echo backend (BASELINE config #1: plumbing, no GPU)."""
+    return 200, body

@@ -1,0 +1,135 @@
+"""Platform launcher: one command replaces the reference's deployment pipeline.
+
+``InfrastructureDeployment/deploy_infrastructure.sh:5-39`` provisions APIM, AKS + GPU node pools,
+Istio, Redis, Service Bus / Event Grid and five Function apps, then every API is a Helm release +
+VirtualService + APIM API. Here a single YAML file (``examples/platform.yaml``) declares the model
+endpoints (factory, input shape, batch, GPUs, in-process engine or per-GPU worker pool) and the
+route table, and::
+
+    python -m aiforearth_api_platform_amd.serve --config examples/platform.yaml [--port 8080]
+
+brings up the control plane, the GPU workers, the dispatchers and the HTTP gateway in one process
+tree. Env/flags precedence follows :mod:`config` (CLI > env > YAML > defaults).
+"""
+from __future__ import annotations
+
+import argparse
+import importlib
+import logging
+import os
+import sys
+from typing import Any, Dict
+
+import torch
+import yaml
+
+from .config import Config, set_config
+from .gateway.control import ControlPlane, set_control_plane
+from .gateway.server import Gateway, Route, RouteTable
+from .sched.dispatcher import QueueDispatcher, WebhookDispatcher, http_backend
+from .utils.logging import AI4ELogger
+
+
+def _load(path: str):
+    mod, fn = path.split(":")
+    return getattr(importlib.import_module(mod), fn)
+
+
+def _devices(spec) -> list:
+    if spec in (None, "all"):
+        n = torch.cuda.device_count() if torch.cuda.is_available() else 0
+        return [f"cuda:{i}" for i in range(n)] or ["cpu"]
+    return list(spec)
+
+
+def build_platform(doc: Dict[str, Any], cfg: Config):
+    """Build (control_plane, gateway, endpoints, dispatchers) from a platform YAML document."""
+    from .runtime.engine import InferenceEngine, PayloadRing
+    from .runtime.model_endpoint import ModelEndpoint
+    from .runtime.worker_pool import ModelSpec, WorkerPool
+
+    cp = ControlPlane(cfg, AI4ELogger(level=logging.DEBUG if cfg.debug else logging.INFO))
+    set_control_plane(cp)
+    base_url = f"http://{cfg.host}:{cfg.port}"
+    endpoints: Dict[str, Any] = {}
+    for name, e in (doc.get("endpoints") or {}).items():
+        shape = tuple(e["item_shape"])
+        mb = int(e.get("max_batch", cfg.max_batch))
+        devs = _devices(e.get("devices", "all"))
+        if e.get("mode", "pool") == "pool":
+            spec = ModelSpec(e["factory"], shape, mb, int(e.get("topk", 5)), dict(e.get("kwargs") or {}),
+                             bool(e.get("hip_graphs", cfg.use_hip_graphs)))
+            pool = WorkerPool(cp, base_url + e["path"], spec, devs, max_delay_s=cfg.max_batch_delay_ms / 1e3,
+                              heartbeat_interval_s=cfg.heartbeat_interval_s,
+                              heartbeat_timeout_s=cfg.heartbeat_timeout_s)
+            ep = ModelEndpoint(cp, e["path"], None, pool.ring, worker=pool, base_url=base_url)
+        else:
+            dev = torch.device(devs[0])
+            model = _load(e["factory"])(device=str(dev), **(e.get("kwargs") or {}))
+            eng = InferenceEngine(model, shape, mb, device=dev, topk=int(e.get("topk", 5)),
+                                  use_graphs=bool(e.get("hip_graphs", cfg.use_hip_graphs)))
+            eng.warmup()
+            ring = PayloadRing(mb * 4, shape)
+            ep = ModelEndpoint(cp, e["path"], eng, ring, base_url=base_url)
+        endpoints[name] = ep
+    table = RouteTable()
+    dispatchers = []
+    backends: Dict[str, Any] = {}
+    for r in doc.get("routes") or []:
+        be = r.get("backend")
+        if isinstance(be, str) and be.startswith("inproc:"):
+            be = endpoints[be.split(":", 1)[1]]
+        elif isinstance(be, str) and be.startswith("callable:"):
+            be = _load(be.split(":", 1)[1])
+        route = table.add(Route(prefix=r["prefix"], mode=r.get("mode", "async"), backend=be, rewrite=r.get("rewrite"),
+                                max_concurrent=r.get("max_concurrent"), content_types=r.get("content_types"),
+                                max_content_length=r.get("max_content_length")))
+        # async route to a generic backend: a queue dispatcher delivers each task (BackendQueueProcessor)
+        if route.mode == "async" and not hasattr(be, "submit") and be is not None:
+            target = base_url + (route.rewrite or route.prefix)
+            fn = http_backend(be) if isinstance(be, str) else be
+            backends[target] = fn
+            if cfg.transport != "eventgrid":
+                dispatchers.append(QueueDispatcher(cp, target, fn))
+    webhook = WebhookDispatcher(cp, backends)
+    if cfg.transport == "eventgrid":
+        cp.push_transport = webhook.deliver
+    gw = Gateway(cp, table, webhook=webhook, base_url=base_url)
+    return cp, gw, endpoints, dispatchers
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(description="AI4E MI355X serving platform")
+    ap.add_argument("--config", required=True, help="platform YAML (endpoints + routes + settings)")
+    ap.add_argument("--host")
+    ap.add_argument("--port", type=int)
+    ap.add_argument("--transport", choices=["inproc", "queue", "eventgrid"])
+    args = ap.parse_args(argv)
+    with open(args.config) as f:
+        doc = yaml.safe_load(f) or {}
+    settings = dict(doc.get("settings") or {})
+    cfg = Config.load(env=os.environ, yaml_values=settings, host=args.host, port=args.port,
+                      transport=args.transport)
+    set_config(cfg)
+    cp, gw, endpoints, dispatchers = build_platform(doc, cfg)
+    for ep in endpoints.values():
+        ep.start()
+    for d in dispatchers:
+        d.start()
+    cp.start_metric_timers()
+    gw.install_signal_handlers()
+    print(f"ai4e-mi355x gateway on http://{cfg.host}:{cfg.port} endpoints={list(endpoints)}", file=sys.stderr,
+          flush=True)
+    try:
+        gw.run(cfg.host, cfg.port)
+    finally:
+        for d in dispatchers:
+            d.stop()
+        for ep in endpoints.values():
+            ep.stop()
+        cp.close()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
