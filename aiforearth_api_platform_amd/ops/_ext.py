@@ -30,16 +30,12 @@ _SIGS = {
     "ai4e_global_avgpool": [_vp, _vp, _c_int, _c_int, _c_int, _vp],
     "ai4e_groupnorm_nhwc": [_vp, _vp, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_float, _c_int, _c_int,
                             _c_int, _vp],
-    "ai4e_upsample2x_bilinear": [_vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _vp],
-    "ai4e_nms_mask": [_vp, _c_int, _c_float, _vp, _vp],
-    "ai4e_nms_reduce": [_vp, _vp, _c_int, _c_int, _vp, _vp, _vp],
-    "ai4e_roi_align_nhwc": [_vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_float,
-                            _c_int, _c_int, _vp],
-    "ai4e_tile_stitch_accum": [_vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int,
-                               _c_int, _vp],
-    "ai4e_tile_stitch_finalize": [_vp, _vp, _vp, _vp, _c_int, _c_int, _c_int, _vp],
-    "ai4e_crop_resize_nhwc": [_vp, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _vp],
-    "ai4e_decode_boxes": [_vp, _vp, _vp, _c_int, _c_int, _c_float, _c_float, _c_float, _vp],
+    "ai4e_upsample2x_bilinear": [_vp, _vp] + [_c_int] * 7 + [_vp],
+    "ai4e_nms_mask": [_vp, _c_int, _c_int, _c_float, _vp, _vp],
+    "ai4e_nms_reduce": [_vp, _vp, _c_int, _c_int, _c_int, _vp, _vp, _vp],
+    "ai4e_roi_align_nhwc": [_vp, _vp, _vp] + [_c_int] * 7 + [_c_float, _c_int, _c_int, _vp],
+    "ai4e_crop_resize_nhwc": [_vp, _vp, _vp, _vp] + [_c_int] * 7 + [_vp],
+    "ai4e_tile_stitch": [_vp, _vp, _vp] + [_c_int] * 10 + [_vp],
 }
 
 

@@ -1,0 +1,235 @@
+"""Detection ops: NMS [K4], RoIAlign / multi-scale RoIAlign [K5], crop-and-resize, box coding.
+
+GPU tensors run the HIP kernels of ``csrc/kernels/detection.hip``; CPU tensors run the PyTorch
+reference implementations below (torchvision is not available in this image, so these references
+are written out here and the GPU tests compare the kernels against them).
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+from typing import List, Optional, Sequence, Tuple
+
+import torch
+
+from . import _ext
+from .pool import IMAGENET_MEAN, IMAGENET_STD
+
+
+# ---------------------------------------------------------------------------------------------- boxes
+def box_iou(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    area_a = (a[:, 2] - a[:, 0]).clamp(min=0) * (a[:, 3] - a[:, 1]).clamp(min=0)
+    area_b = (b[:, 2] - b[:, 0]).clamp(min=0) * (b[:, 3] - b[:, 1]).clamp(min=0)
+    lt = torch.max(a[:, None, :2], b[None, :, :2])
+    rb = torch.min(a[:, None, 2:], b[None, :, 2:])
+    wh = (rb - lt).clamp(min=0)
+    inter = wh[..., 0] * wh[..., 1]
+    union = area_a[:, None] + area_b[None, :] - inter
+    return torch.where(union > 0, inter / union, torch.zeros_like(inter))
+
+
+def decode_boxes(anchors: torch.Tensor, deltas: torch.Tensor, weights=(1.0, 1.0, 1.0, 1.0),
+                 clip: float = math.log(1000.0 / 16)) -> torch.Tensor:
+    """Faster-RCNN box decoding (anchors [..., 4] xyxy, deltas [..., 4] dx,dy,dw,dh)."""
+    wx, wy, ww, wh = weights
+    w = anchors[..., 2] - anchors[..., 0]
+    h = anchors[..., 3] - anchors[..., 1]
+    cx = anchors[..., 0] + 0.5 * w
+    cy = anchors[..., 1] + 0.5 * h
+    dx, dy = deltas[..., 0] / wx, deltas[..., 1] / wy
+    dw, dh = (deltas[..., 2] / ww).clamp(max=clip), (deltas[..., 3] / wh).clamp(max=clip)
+    pcx, pcy = dx * w + cx, dy * h + cy
+    pw, ph = torch.exp(dw) * w, torch.exp(dh) * h
+    return torch.stack([pcx - 0.5 * pw, pcy - 0.5 * ph, pcx + 0.5 * pw, pcy + 0.5 * ph], dim=-1)
+
+
+def clip_boxes(boxes: torch.Tensor, h: int, w: int) -> torch.Tensor:
+    return torch.stack([boxes[..., 0].clamp(0, w), boxes[..., 1].clamp(0, h), boxes[..., 2].clamp(0, w),
+                        boxes[..., 3].clamp(0, h)], dim=-1)
+
+
+# ---------------------------------------------------------------------------------------------- NMS
+def nms_reference(boxes: torch.Tensor, scores: torch.Tensor, thr: float) -> torch.Tensor:
+    """Greedy NMS (torchvision.ops.nms semantics): indices kept, in descending score order."""
+    order = torch.argsort(scores, descending=True, stable=True)
+    b = boxes[order]
+    keep = []
+    suppressed = torch.zeros(len(order), dtype=torch.bool)
+    iou = box_iou(b, b)
+    for i in range(len(order)):
+        if suppressed[i]:
+            continue
+        keep.append(i)
+        suppressed |= iou[i] > thr
+        suppressed[i] = True
+    return order[torch.tensor(keep, dtype=torch.long)] if keep else torch.zeros(0, dtype=torch.long)
+
+
+def nms_batched_sorted(boxes: torch.Tensor, thr: float, max_out: int, valid: Optional[torch.Tensor] = None
+                       ) -> Tuple[torch.Tensor, torch.Tensor]:
+    """NMS over B images at once. boxes [B, N, 4] already sorted by descending score per image.
+
+    Returns (keep [B, max_out] int32 indices into N (padded -1), count [B] int32).
+    """
+    B, N, _ = boxes.shape
+    if _ext.backend_for(boxes) == "hip":
+        boxes = boxes.float().contiguous()
+        words = (N + 63) // 64
+        mask = torch.empty(B, N, words, dtype=torch.int64, device=boxes.device)
+        keep = torch.full((B, max_out), -1, dtype=torch.int32, device=boxes.device)
+        count = torch.empty(B, dtype=torch.int32, device=boxes.device)
+        vptr = None if valid is None else valid.to(torch.int32).contiguous()
+        st = _ext.stream_ptr(boxes.device)
+        _ext.call("ai4e_nms_mask", boxes.data_ptr(), B, N, float(thr), mask.data_ptr(), st)
+        _ext.call("ai4e_nms_reduce", mask.data_ptr(), _ext.ptr(vptr), B, N, max_out, keep.data_ptr(), count.data_ptr(),
+                  st)
+        return keep, count
+    keep = torch.full((B, max_out), -1, dtype=torch.int32)
+    count = torch.zeros(B, dtype=torch.int32)
+    for b in range(B):
+        n = N if valid is None else int(valid[b])
+        scores = torch.arange(n, 0, -1, dtype=torch.float32)  # already sorted
+        k = nms_reference(boxes[b, :n].float().cpu(), scores, thr)[:max_out]
+        keep[b, :len(k)] = k.to(torch.int32)
+        count[b] = len(k)
+    return keep.to(boxes.device), count.to(boxes.device)
+
+
+def batched_nms(boxes: torch.Tensor, scores: torch.Tensor, idxs: torch.Tensor, thr: float,
+                max_out: int = 1000) -> torch.Tensor:
+    """Per-class NMS for one image (coordinate-offset trick); returns kept indices (desc score)."""
+    if boxes.numel() == 0:
+        return torch.zeros(0, dtype=torch.long, device=boxes.device)
+    off = idxs.to(boxes.dtype) * (boxes.max() + 1)
+    b = boxes + off[:, None]
+    order = torch.argsort(scores, descending=True)
+    keep, count = nms_batched_sorted(b[order][None], thr, max_out)
+    k = keep[0, :int(count[0])].long()
+    return order[k]
+
+
+# ---------------------------------------------------------------------------------------------- RoIAlign
+def roi_align_reference(feat: torch.Tensor, rois: torch.Tensor, out_hw: Tuple[int, int], scale: float,
+                        sampling: int = 2, aligned: bool = False) -> torch.Tensor:
+    """torchvision.ops.roi_align on NHWC features (fp32 math). rois [R, 5] = (img, x1, y1, x2, y2)."""
+    n, H, W, C = feat.shape
+    PH, PW = out_hw
+    f = feat.float()
+    out = torch.zeros(rois.shape[0], PH, PW, C)
+    off = 0.5 if aligned else 0.0
+    for r in range(rois.shape[0]):
+        img = int(rois[r, 0])
+        x1, y1 = float(rois[r, 1]) * scale - off, float(rois[r, 2]) * scale - off
+        rw, rh = float(rois[r, 3]) * scale - off - x1, float(rois[r, 4]) * scale - off - y1
+        if not aligned:
+            rw, rh = max(rw, 1.0), max(rh, 1.0)
+        bh, bw = rh / PH, rw / PW
+        gh = sampling if sampling > 0 else int(math.ceil(rh / PH))
+        gw = sampling if sampling > 0 else int(math.ceil(rw / PW))
+        cnt = max(gh * gw, 1)
+        ys = torch.tensor([y1 + ph * bh + (iy + 0.5) * bh / gh for ph in range(PH) for iy in range(gh)])
+        xs = torch.tensor([x1 + pw * bw + (ix + 0.5) * bw / gw for pw in range(PW) for ix in range(gw)])
+        yy, xx = torch.meshgrid(ys, xs, indexing="ij")
+        v = _bilinear(f[img], yy, xx)  # [PH*gh, PW*gw, C]
+        out[r] = v.reshape(PH, gh, PW, gw, C).sum(dim=(1, 3)) / cnt
+    return out
+
+
+def _bilinear(f: torch.Tensor, y: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
+    H, W, C = f.shape
+    valid = (y >= -1) & (y <= H) & (x >= -1) & (x <= W)
+    y = y.clamp(min=0)
+    x = x.clamp(min=0)
+    y0 = y.floor().long()
+    x0 = x.floor().long()
+    ytop = y0 >= H - 1
+    xtop = x0 >= W - 1
+    y0 = torch.where(ytop, torch.full_like(y0, H - 1), y0)
+    x0 = torch.where(xtop, torch.full_like(x0, W - 1), x0)
+    y = torch.where(ytop, y0.float(), y)
+    x = torch.where(xtop, x0.float(), x)
+    y1 = torch.where(ytop, y0, y0 + 1).clamp(max=H - 1)
+    x1 = torch.where(xtop, x0, x0 + 1).clamp(max=W - 1)
+    ly, lx = (y - y0)[..., None], (x - x0)[..., None]
+    v = (1 - ly) * (1 - lx) * f[y0, x0] + (1 - ly) * lx * f[y0, x1] + ly * (1 - lx) * f[y1, x0] + ly * lx * f[y1, x1]
+    return v * valid[..., None]
+
+
+def roi_align_nhwc(feat: torch.Tensor, rois: torch.Tensor, out_hw: Tuple[int, int], scale: float,
+                   sampling: int = 2, aligned: bool = False) -> torch.Tensor:
+    n, H, W, C = feat.shape
+    R = rois.shape[0]
+    if _ext.backend_for(feat) == "hip":
+        feat = feat.contiguous()
+        rois = rois.float().contiguous()
+        out = torch.empty(R, out_hw[0], out_hw[1], C, device=feat.device, dtype=feat.dtype)
+        _ext.call("ai4e_roi_align_nhwc", feat.data_ptr(), rois.data_ptr(), out.data_ptr(), H, W, C, R, out_hw[0],
+                  out_hw[1], sampling, float(scale), int(aligned), 0, _ext.stream_ptr(feat.device))
+        return out
+    return roi_align_reference(feat, rois.cpu(), out_hw, scale, sampling, aligned).to(feat.dtype)
+
+
+def map_levels(rois: torch.Tensor, k_min: int = 2, k_max: int = 5, canonical_scale: float = 224.0,
+               canonical_level: int = 4) -> torch.Tensor:
+    """FPN level assignment (Lin et al. eq. 1)."""
+    area = (rois[:, 3] - rois[:, 1]).clamp(min=0) * (rois[:, 4] - rois[:, 2]).clamp(min=0)
+    lvl = torch.floor(canonical_level + torch.log2(torch.sqrt(area) / canonical_scale + 1e-6))
+    return lvl.clamp(k_min, k_max).long() - k_min
+
+
+def multiscale_roi_align(feats: Sequence[torch.Tensor], scales: Sequence[float], rois: torch.Tensor,
+                         out_hw=(7, 7), sampling: int = 2) -> torch.Tensor:
+    levels = map_levels(rois, 2, 2 + len(feats) - 1)
+    C = feats[0].shape[-1]
+    out = torch.zeros(rois.shape[0], out_hw[0], out_hw[1], C, device=feats[0].device, dtype=feats[0].dtype)
+    for lv, (f, s) in enumerate(zip(feats, scales)):
+        idx = torch.nonzero(levels == lv).flatten()
+        if idx.numel():
+            out[idx] = roi_align_nhwc(f, rois[idx], out_hw, s, sampling)
+    return out
+
+
+# ---------------------------------------------------------------------------------------------- crops
+def crop_resize_reference(img_u8: torch.Tensor, boxes: torch.Tensor, out_hw: Tuple[int, int],
+                          mean=IMAGENET_MEAN, std=IMAGENET_STD) -> torch.Tensor:
+    n, H, W, C = img_u8.shape
+    OH, OW = out_hw
+    m8 = torch.tensor(list(mean) + [0.0] * (8 - len(mean)))
+    s8 = torch.tensor(list(std) + [1.0] * (8 - len(std)))
+    out = torch.zeros(boxes.shape[0], OH, OW, 8)
+    for r in range(boxes.shape[0]):
+        b = boxes[r].float()
+        i = int(b[0])
+        sx = (b[1] + (torch.arange(OW) + 0.5) * (b[3] - b[1]) / OW - 0.5).clamp(0, W - 1)
+        sy = (b[2] + (torch.arange(OH) + 0.5) * (b[4] - b[2]) / OH - 0.5).clamp(0, H - 1)
+        yy, xx = torch.meshgrid(sy, sx, indexing="ij")
+        y0, x0 = yy.floor().long(), xx.floor().long()
+        y1, x1 = (y0 + 1).clamp(max=H - 1), (x0 + 1).clamp(max=W - 1)
+        ly, lx = (yy - y0)[..., None], (xx - x0)[..., None]
+        f = img_u8[i].float()
+        pix = (1 - ly) * ((1 - lx) * f[y0, x0] + lx * f[y0, x1]) + ly * ((1 - lx) * f[y1, x0] + lx * f[y1, x1])
+        out[r, ..., :C] = (pix / 255.0 - m8[:C]) / s8[:C]
+    return out
+
+
+_NORM_CACHE = {}
+
+
+def crop_resize_nhwc(img_u8: torch.Tensor, boxes: torch.Tensor, out_hw=(224, 224), mean=IMAGENET_MEAN,
+                     std=IMAGENET_STD) -> torch.Tensor:
+    """Crop boxes [R,5]=(img,x1,y1,x2,y2) from uint8 NHWC images, resize bilinear, normalize ->
+    bf16 [R, OH, OW, 8] (ready for a classifier stem)."""
+    n, H, W, C = img_u8.shape
+    R = boxes.shape[0]
+    if _ext.backend_for(img_u8) == "hip":
+        key = (img_u8.device, tuple(mean), tuple(std))
+        norm = _NORM_CACHE.get(key)
+        if norm is None:
+            norm = torch.tensor(list(mean) + [0.0] * (8 - len(mean)) + list(std) + [1.0] * (8 - len(std)),
+                                dtype=torch.float32, device=img_u8.device)
+            _NORM_CACHE[key] = norm
+        out = torch.empty(R, out_hw[0], out_hw[1], 8, device=img_u8.device, dtype=torch.bfloat16)
+        _ext.call("ai4e_crop_resize_nhwc", img_u8.contiguous().data_ptr(), boxes.float().contiguous().data_ptr(),
+                  out.data_ptr(), norm.data_ptr(), H, W, C, R, out_hw[0], out_hw[1], 0, _ext.stream_ptr(img_u8.device))
+        return out
+    return crop_resize_reference(img_u8.cpu(), boxes.cpu(), out_hw, mean, std)

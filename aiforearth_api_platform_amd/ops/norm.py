@@ -1,0 +1,66 @@
+"""GroupNorm (+ReLU) [K2] and bilinear 2x upsample [K3] on NHWC tensors, with concat-slice outputs."""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+
+from . import _ext
+
+GN_PIX_PER_BLOCK = 1024
+
+
+def _nhwc_ld(t: torch.Tensor):
+    """(row stride in channels, channel offset) of an NHWC tensor that may be a channel slice."""
+    n, h, w, c = t.shape
+    if t.stride(3) != 1 or t.stride(1) != w * t.stride(2) or t.stride(0) != h * t.stride(1):
+        raise ValueError("expected an NHWC (possibly channel-sliced) dense tensor")
+    return t.stride(2), t.storage_offset() % t.stride(2)
+
+
+def _base_ptr(t: torch.Tensor) -> int:
+    ld, coff = _nhwc_ld(t)
+    return t.untyped_storage().data_ptr() + t.element_size() * (t.storage_offset() - coff)
+
+
+def group_norm_nhwc(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, groups: int = 32, eps: float = 1e-5,
+                    relu: bool = False, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    n, h, w, c = x.shape
+    if out is None:
+        out = torch.empty(n, h, w, c, device=x.device, dtype=x.dtype)
+    if _ext.backend_for(x) == "hip":
+        ldx, xcoff = _nhwc_ld(x)
+        ldy, ycoff = _nhwc_ld(out)
+        nchunks = (h * w + GN_PIX_PER_BLOCK - 1) // GN_PIX_PER_BLOCK
+        partials = torch.empty(n * nchunks * groups * 2, device=x.device, dtype=torch.float32)
+        g32 = gamma.to(x.device, torch.float32).contiguous()
+        b32 = beta.to(x.device, torch.float32).contiguous()
+        _ext.call("ai4e_groupnorm_nhwc", _base_ptr(x), _base_ptr(out), g32.data_ptr(), b32.data_ptr(),
+                  partials.data_ptr(), n, h * w, c, groups, eps, int(relu), ldx | (ldy << 16), xcoff | (ycoff << 16),
+                  _ext.stream_ptr(x.device))
+        return out
+    y = F.group_norm(x.permute(0, 3, 1, 2).float(), groups, gamma.float().to(x.device), beta.float().to(x.device), eps)
+    if relu:
+        y = F.relu(y)
+    out.copy_(y.permute(0, 2, 3, 1).to(out.dtype))
+    return out
+
+
+def upsample2x_nhwc(x: torch.Tensor, out: Optional[torch.Tensor] = None, out_coff: int = 0) -> torch.Tensor:
+    """Bilinear x2 (align_corners=False). ``out`` may be a wider concat buffer; writes channels
+    [out_coff, out_coff + C)."""
+    n, h, w, c = x.shape
+    if out is None:
+        out = torch.empty(n, 2 * h, 2 * w, c, device=x.device, dtype=x.dtype)
+        out_coff = 0
+    if _ext.backend_for(x) == "hip":
+        x = x.contiguous()
+        if out.stride(3) != 1:
+            raise ValueError("bad output buffer")
+        _ext.call("ai4e_upsample2x_bilinear", x.data_ptr(), out.data_ptr(), n, h, w, c, out.stride(2), out_coff, 0,
+                  _ext.stream_ptr(x.device))
+        return out
+    y = F.interpolate(x.permute(0, 3, 1, 2).float(), scale_factor=2, mode="bilinear", align_corners=False)
+    out[..., out_coff:out_coff + c] = y.permute(0, 2, 3, 1).to(out.dtype)
+    return out

@@ -1,0 +1,209 @@
+// K4 NMS (IoU bitmask + on-GPU greedy reduction), K5 RoIAlign (NHWC) and crop-and-resize
+// (detector -> classifier hand-off, preprocess fused) — the irregular detection ops.
+#include "common.h"
+
+namespace {
+
+constexpr int NMS_BLOCK = 64;  // one wave64 per 64x64 IoU tile; a 64-bit word per row
+
+__device__ __forceinline__ float iou(const float4 a, const float4 b) {
+  const float l = fmaxf(a.x, b.x), t = fmaxf(a.y, b.y), r = fminf(a.z, b.z), bo = fminf(a.w, b.w);
+  const float iw = fmaxf(r - l, 0.f), ih = fmaxf(bo - t, 0.f);
+  const float inter = iw * ih;
+  const float ua = (a.z - a.x) * (a.w - a.y) + (b.z - b.x) * (b.w - b.y) - inter;
+  return ua > 0.f ? inter / ua : 0.f;
+}
+
+// boxes [B, N, 4] (x1,y1,x2,y2), sorted by descending score per image.
+// mask [B, N, W] (W = ceil(N/64)): bit j of mask[b][i][jb] set <=> j = 64*jb+bit > i and IoU(i,j) > thr.
+__global__ __launch_bounds__(NMS_BLOCK) void nms_mask_kernel(const float4* __restrict__ boxes, int N, float thr,
+                                                            unsigned long long* __restrict__ mask) {
+  const int b = blockIdx.z;
+  const int ib = blockIdx.y, jb = blockIdx.x;
+  const int W = (N + NMS_BLOCK - 1) / NMS_BLOCK;
+  if (jb < ib) return;  // lower triangle never needed
+  __shared__ float4 sb[NMS_BLOCK];
+  const int t = threadIdx.x;
+  const int j = jb * NMS_BLOCK + t;
+  if (j < N) sb[t] = boxes[static_cast<long>(b) * N + j];
+  __syncthreads();
+  const int i = ib * NMS_BLOCK + t;
+  if (i >= N) return;
+  const float4 bi = boxes[static_cast<long>(b) * N + i];
+  unsigned long long bits = 0;
+  const int jn = min(NMS_BLOCK, N - jb * NMS_BLOCK);
+  for (int k = (ib == jb ? t + 1 : 0); k < jn; ++k)
+    if (iou(bi, sb[k]) > thr) bits |= 1ull << k;
+  mask[(static_cast<long>(b) * N + i) * W + jb] = bits;
+}
+
+// One wave per image: greedy scan in score order over the bitmask. valid[b] = number of real boxes
+// (the rest are padding). keep[b][0..count) = kept indices (<= max_out), count[b].
+__global__ __launch_bounds__(64) void nms_reduce_kernel(const unsigned long long* __restrict__ mask,
+                                                        const int* __restrict__ valid, int N, int max_out,
+                                                        int* __restrict__ keep, int* __restrict__ count) {
+  const int b = blockIdx.x;
+  const int W = (N + 63) / 64;
+  const int lane = threadIdx.x;
+  __shared__ unsigned long long removed[128];  // N <= 8192
+  for (int w = lane; w < W; w += 64) removed[w] = 0;
+  __syncthreads();
+  const int n = valid ? min(valid[b], N) : N;
+  int kept = 0;
+  for (int i = 0; i < n && kept < max_out; ++i) {
+    const bool dead = (removed[i >> 6] >> (i & 63)) & 1ull;
+    if (dead) continue;  // uniform across the wave (LDS broadcast)
+    if (lane == 0) keep[static_cast<long>(b) * max_out + kept] = i;
+    ++kept;
+    const unsigned long long* row = mask + (static_cast<long>(b) * N + i) * W;
+    for (int w = (i >> 6) + lane; w < W; w += 64) removed[w] |= row[w];
+    __syncthreads();
+  }
+  if (lane == 0) count[b] = kept;
+}
+
+__device__ __forceinline__ void bilinear_acc8(const uint16_t* __restrict__ feat, int H, int W, int C, float y, float x,
+                                              int c8, float w, float* acc) {
+  if (y < -1.f || y > H || x < -1.f || x > W) return;
+  y = fmaxf(y, 0.f);
+  x = fmaxf(x, 0.f);
+  int y0 = static_cast<int>(y), x0 = static_cast<int>(x), y1, x1;
+  if (y0 >= H - 1) { y1 = y0 = H - 1; y = static_cast<float>(y0); } else { y1 = y0 + 1; }
+  if (x0 >= W - 1) { x1 = x0 = W - 1; x = static_cast<float>(x0); } else { x1 = x0 + 1; }
+  const float ly = y - y0, lx = x - x0, hy = 1.f - ly, hx = 1.f - lx;
+  const float ws[4] = {hy * hx * w, hy * lx * w, ly * hx * w, ly * lx * w};
+  const long offs[4] = {(static_cast<long>(y0) * W + x0) * C, (static_cast<long>(y0) * W + x1) * C,
+                        (static_cast<long>(y1) * W + x0) * C, (static_cast<long>(y1) * W + x1) * C};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint4 v = *reinterpret_cast<const uint4*>(feat + offs[k] + 8 * c8);
+    float a, b;
+    unpack_bf16x2(v.x, a, b); acc[0] += ws[k] * a; acc[1] += ws[k] * b;
+    unpack_bf16x2(v.y, a, b); acc[2] += ws[k] * a; acc[3] += ws[k] * b;
+    unpack_bf16x2(v.z, a, b); acc[4] += ws[k] * a; acc[5] += ws[k] * b;
+    unpack_bf16x2(v.w, a, b); acc[6] += ws[k] * a; acc[7] += ws[k] * b;
+  }
+}
+
+// RoIAlign (torchvision semantics) on an NHWC bf16 feature map; rois [R, 5] = (img, x1, y1, x2, y2).
+__global__ __launch_bounds__(256) void roi_align_kernel(const uint16_t* __restrict__ feat, const float* __restrict__ rois,
+                                                        uint16_t* __restrict__ out, int H, int W, int C, int R, int PH,
+                                                        int PW, int sampling, float scale, int aligned) {
+  const int C8 = C >> 3;
+  const long total = static_cast<long>(R) * PH * PW * C8;
+  for (long idx = blockIdx.x * 256L + threadIdx.x; idx < total; idx += static_cast<long>(gridDim.x) * 256) {
+    const int c8 = static_cast<int>(idx % C8);
+    long t = idx / C8;
+    const int pw = static_cast<int>(t % PW);
+    t /= PW;
+    const int ph = static_cast<int>(t % PH);
+    const int r = static_cast<int>(t / PH);
+    const float* roi = rois + 5L * r;
+    const int img = static_cast<int>(roi[0]);
+    const float off = aligned ? 0.5f : 0.f;
+    const float x1 = roi[1] * scale - off, y1 = roi[2] * scale - off;
+    float rw = roi[3] * scale - off - x1, rh = roi[4] * scale - off - y1;
+    if (!aligned) {
+      rw = fmaxf(rw, 1.f);
+      rh = fmaxf(rh, 1.f);
+    }
+    const float bh = rh / PH, bw = rw / PW;
+    const int gh = sampling > 0 ? sampling : static_cast<int>(ceilf(rh / PH));
+    const int gw = sampling > 0 ? sampling : static_cast<int>(ceilf(rw / PW));
+    const float inv = 1.f / fmaxf(gh * gw, 1);
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const uint16_t* f = feat + static_cast<long>(img) * H * W * C;
+    for (int iy = 0; iy < gh; ++iy) {
+      const float y = y1 + ph * bh + (iy + 0.5f) * bh / gh;
+      for (int ix = 0; ix < gw; ++ix) {
+        const float x = x1 + pw * bw + (ix + 0.5f) * bw / gw;
+        bilinear_acc8(f, H, W, C, y, x, c8, inv, acc);
+      }
+    }
+    *reinterpret_cast<uint4*>(out + (((static_cast<long>(r) * PH + ph) * PW + pw) * C) + 8 * c8) =
+        make_uint4(pack_bf16x2(acc[0], acc[1]), pack_bf16x2(acc[2], acc[3]), pack_bf16x2(acc[4], acc[5]),
+                   pack_bf16x2(acc[6], acc[7]));
+  }
+}
+
+// Crop + bilinear resize + normalize: uint8 image [N, H, W, C<=8], boxes [R, 5] = (img, x1, y1, x2, y2)
+// in pixels -> bf16 [R, OH, OW, 8] normalized (classifier stem input). norm = mean[8] ++ std[8].
+__global__ __launch_bounds__(256) void crop_resize_kernel(const uint8_t* __restrict__ img, const float* __restrict__ boxes,
+                                                          uint16_t* __restrict__ out, const float* __restrict__ norm, int H,
+                                                          int W, int C, int R, int OH, int OW) {
+  const long total = static_cast<long>(R) * OH * OW;
+  for (long idx = blockIdx.x * 256L + threadIdx.x; idx < total; idx += static_cast<long>(gridDim.x) * 256) {
+    const int ox = static_cast<int>(idx % OW);
+    long t = idx / OW;
+    const int oy = static_cast<int>(t % OH);
+    const int r = static_cast<int>(t / OH);
+    const float* bx = boxes + 5L * r;
+    const int n = static_cast<int>(bx[0]);
+    const float sx = bx[1] + (ox + 0.5f) * (bx[3] - bx[1]) / OW - 0.5f;
+    const float sy = bx[2] + (oy + 0.5f) * (bx[4] - bx[2]) / OH - 0.5f;
+    const float cy = fminf(fmaxf(sy, 0.f), H - 1.f), cx = fminf(fmaxf(sx, 0.f), W - 1.f);
+    const int y0 = static_cast<int>(cy), x0 = static_cast<int>(cx);
+    const int y1 = min(y0 + 1, H - 1), x1 = min(x0 + 1, W - 1);
+    const float ly = cy - y0, lx = cx - x0;
+    const uint8_t* base = img + static_cast<long>(n) * H * W * C;
+    float v[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      if (c < C) {
+        const float a = base[(static_cast<long>(y0) * W + x0) * C + c], b = base[(static_cast<long>(y0) * W + x1) * C + c];
+        const float d = base[(static_cast<long>(y1) * W + x0) * C + c], e = base[(static_cast<long>(y1) * W + x1) * C + c];
+        const float pix = (1 - ly) * ((1 - lx) * a + lx * b) + ly * ((1 - lx) * d + lx * e);
+        v[c] = (pix * (1.f / 255.f) - norm[c]) / norm[8 + c];
+      } else {
+        v[c] = 0.f;
+      }
+    }
+    reinterpret_cast<uint4*>(out)[idx] =
+        make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]), pack_bf16x2(v[6], v[7]));
+  }
+}
+
+inline int grid_for(long work) {
+  long g = (work + 255) / 256;
+  return static_cast<int>(g < 1 ? 1 : (g > 8192 ? 8192 : g));
+}
+
+}  // namespace
+
+AI4E_API int ai4e_nms_mask(const void* boxes, int B, int N, float thr, void* mask, hipStream_t s) {
+  if (N <= 0) return AI4E_OK;
+  const int nb = (N + NMS_BLOCK - 1) / NMS_BLOCK;
+  hipLaunchKernelGGL(nms_mask_kernel, dim3(nb, nb, B), dim3(NMS_BLOCK), 0, s, static_cast<const float4*>(boxes), N, thr,
+                     static_cast<unsigned long long*>(mask));
+  return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
+}
+
+AI4E_API int ai4e_nms_reduce(const void* mask, const void* valid, int B, int N, int max_out, void* keep, void* count,
+                             hipStream_t s) {
+  if (N > 8192) return AI4E_EINVAL;
+  hipLaunchKernelGGL(nms_reduce_kernel, dim3(B), dim3(64), 0, s, static_cast<const unsigned long long*>(mask),
+                     static_cast<const int*>(valid), N, max_out, static_cast<int*>(keep), static_cast<int*>(count));
+  return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
+}
+
+AI4E_API int ai4e_roi_align_nhwc(const void* feat, const void* rois, void* out, int H, int W, int C, int R, int PH,
+                                 int PW, int sampling, float scale, int aligned, int unused, hipStream_t s) {
+  (void)unused;
+  if (C % 8) return AI4E_EINVAL;
+  if (R <= 0) return AI4E_OK;
+  hipLaunchKernelGGL(roi_align_kernel, dim3(grid_for(static_cast<long>(R) * PH * PW * (C / 8))), dim3(256), 0, s,
+                     static_cast<const uint16_t*>(feat), static_cast<const float*>(rois), static_cast<uint16_t*>(out), H,
+                     W, C, R, PH, PW, sampling, scale, aligned);
+  return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
+}
+
+AI4E_API int ai4e_crop_resize_nhwc(const void* img, const void* boxes, void* out, const void* norm, int H, int W, int C,
+                                   int R, int OH, int OW, int unused, hipStream_t s) {
+  (void)unused;
+  if (C > 8) return AI4E_EINVAL;
+  if (R <= 0) return AI4E_OK;
+  hipLaunchKernelGGL(crop_resize_kernel, dim3(grid_for(static_cast<long>(R) * OH * OW)), dim3(256), 0, s,
+                     static_cast<const uint8_t*>(img), static_cast<const float*>(boxes), static_cast<uint16_t*>(out),
+                     static_cast<const float*>(norm), H, W, C, R, OH, OW);
+  return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
+}

@@ -1,0 +1,181 @@
+// K2 GroupNorm (+ReLU) and K3 bilinear 2x upsample — NHWC bf16, memory-bound, 16-B vectors per lane.
+//
+// GroupNorm is two launches: (1) per-(image, pixel-chunk) partial sum / sum-of-squares per group,
+// reduced in-register then across the workgroup in LDS and written as fp32 partials (no global
+// atomics); (2) every normalize workgroup combines its image's partials (fp64), then applies
+// (x - mean) * rstd * gamma + beta (+ReLU) and writes bf16 — optionally into a channel slice of a
+// wider buffer (U-Net concat). The upsample writes straight into a concat slice as well, so the
+// decoder's "upsample + concat" never materialises a separate tensor.
+#include "common.h"
+
+namespace {
+
+constexpr int GN_PIX_PER_BLOCK = 1024;
+
+// x: [N, HW, C] (row stride ldx, channel offset xcoff); partials: [N, nchunks, G, 2]
+__global__ __launch_bounds__(256) void gn_stats_kernel(const uint16_t* __restrict__ x, float* __restrict__ partials,
+                                                       int HW, int C, int G, int ldx, int xcoff, int nchunks) {
+  const int n = blockIdx.y;
+  const int chunk = blockIdx.x;
+  const int C8 = C >> 3;
+  const int cg = C / G;  // channels per group (multiple of 8 or a divisor of 8)
+  // each lane owns one 8-channel vector column (c8) and strides over pixels
+  const int lanes_per_pix = C8;
+  const int pix_per_iter = 256 / lanes_per_pix;  // requires C8 <= 256 and 256 % C8 == 0 (host checks)
+  const int c8 = threadIdx.x % lanes_per_pix;
+  const int p0 = threadIdx.x / lanes_per_pix;
+  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0}, q[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const int pbeg = chunk * GN_PIX_PER_BLOCK, pend = min(HW, pbeg + GN_PIX_PER_BLOCK);
+  if (p0 < pix_per_iter) {
+    for (int p = pbeg + p0; p < pend; p += pix_per_iter) {
+      const uint4 v = *reinterpret_cast<const uint4*>(x + (static_cast<long>(n) * HW + p) * ldx + xcoff + 8 * c8);
+      float a, b;
+      unpack_bf16x2(v.x, a, b); s[0] += a; q[0] += a * a; s[1] += b; q[1] += b * b;
+      unpack_bf16x2(v.y, a, b); s[2] += a; q[2] += a * a; s[3] += b; q[3] += b * b;
+      unpack_bf16x2(v.z, a, b); s[4] += a; q[4] += a * a; s[5] += b; q[5] += b * b;
+      unpack_bf16x2(v.w, a, b); s[6] += a; q[6] += a * a; s[7] += b; q[7] += b * b;
+    }
+  }
+  // reduce each lane's 8 channels into its group(s), then across lanes holding the same group
+  __shared__ float gs[64], gq[64];
+  if (threadIdx.x < 64) {
+    gs[threadIdx.x] = 0.f;
+    gq[threadIdx.x] = 0.f;
+  }
+  __syncthreads();
+  if (p0 < pix_per_iter) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int g = (8 * c8 + j) / cg;
+      atomicAdd(&gs[g], s[j]);
+      atomicAdd(&gq[g], q[j]);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < G) {
+    float* o = partials + ((static_cast<long>(n) * nchunks + chunk) * G + threadIdx.x) * 2;
+    o[0] = gs[threadIdx.x];
+    o[1] = gq[threadIdx.x];
+  }
+}
+
+__global__ __launch_bounds__(256) void gn_apply_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
+                                                       const float* __restrict__ partials,
+                                                       const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                       int HW, int C, int G, float eps, int relu, int nchunks, int ldx,
+                                                       int xcoff, int ldy, int ycoff) {
+  const int n = blockIdx.y;
+  __shared__ float mean_s[64], rstd_s[64];
+  if (threadIdx.x < G) {
+    double s = 0, q = 0;
+    for (int k = 0; k < nchunks; ++k) {
+      const float* o = partials + ((static_cast<long>(n) * nchunks + k) * G + threadIdx.x) * 2;
+      s += o[0];
+      q += o[1];
+    }
+    const double cnt = static_cast<double>(HW) * (C / G);
+    const double mean = s / cnt;
+    const double var = fmax(q / cnt - mean * mean, 0.0);
+    mean_s[threadIdx.x] = static_cast<float>(mean);
+    rstd_s[threadIdx.x] = static_cast<float>(1.0 / sqrt(var + eps));
+  }
+  __syncthreads();
+  const int C8 = C >> 3;
+  const int cg = C / G;
+  const long total = static_cast<long>(HW) * C8;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += static_cast<long>(gridDim.x) * 256) {
+    const int c8 = static_cast<int>(i % C8);
+    const long p = i / C8;
+    const uint4 v = *reinterpret_cast<const uint4*>(x + (static_cast<long>(n) * HW + p) * ldx + xcoff + 8 * c8);
+    float f[8];
+    unpack_bf16x2(v.x, f[0], f[1]);
+    unpack_bf16x2(v.y, f[2], f[3]);
+    unpack_bf16x2(v.z, f[4], f[5]);
+    unpack_bf16x2(v.w, f[6], f[7]);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = 8 * c8 + j;
+      const int g = c / cg;
+      float t = (f[j] - mean_s[g]) * rstd_s[g] * gamma[c] + beta[c];
+      f[j] = relu ? fmaxf(t, 0.f) : t;
+    }
+    *reinterpret_cast<uint4*>(y + (static_cast<long>(n) * HW + p) * ldy + ycoff + 8 * c8) =
+        make_uint4(pack_bf16x2(f[0], f[1]), pack_bf16x2(f[2], f[3]), pack_bf16x2(f[4], f[5]), pack_bf16x2(f[6], f[7]));
+  }
+}
+
+// Bilinear 2x upsample, align_corners=False (PyTorch semantics): src = (dst + 0.5) / 2 - 0.5, clamped.
+__global__ __launch_bounds__(256) void upsample2x_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
+                                                         int N, int H, int W, int C, int ldy, int ycoff) {
+  const int C8 = C >> 3;
+  const int OH = 2 * H, OW = 2 * W;
+  const long total = static_cast<long>(N) * OH * OW * C8;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += static_cast<long>(gridDim.x) * 256) {
+    const int c8 = static_cast<int>(i % C8);
+    long pix = i / C8;
+    const int ox = static_cast<int>(pix % OW);
+    pix /= OW;
+    const int oy = static_cast<int>(pix % OH);
+    const int n = static_cast<int>(pix / OH);
+    const float sy = fmaxf((oy + 0.5f) * 0.5f - 0.5f, 0.f), sx = fmaxf((ox + 0.5f) * 0.5f - 0.5f, 0.f);
+    const int y0 = static_cast<int>(sy), x0 = static_cast<int>(sx);
+    const int y1 = min(y0 + 1, H - 1), x1 = min(x0 + 1, W - 1);
+    const float ly = sy - y0, lx = sx - x0;
+    const float w00 = (1 - ly) * (1 - lx), w01 = (1 - ly) * lx, w10 = ly * (1 - lx), w11 = ly * lx;
+    const uint4* base = reinterpret_cast<const uint4*>(x) + static_cast<long>(n) * H * W * C8 + c8;
+    const uint4 a = base[(static_cast<long>(y0) * W + x0) * C8], b = base[(static_cast<long>(y0) * W + x1) * C8];
+    const uint4 c = base[(static_cast<long>(y1) * W + x0) * C8], d = base[(static_cast<long>(y1) * W + x1) * C8];
+    uint32_t out[4];
+    const uint32_t* pa = &a.x;
+    const uint32_t* pb = &b.x;
+    const uint32_t* pc = &c.x;
+    const uint32_t* pd = &d.x;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float a0, a1, b0, b1, c0, c1, d0, d1;
+      unpack_bf16x2(pa[k], a0, a1);
+      unpack_bf16x2(pb[k], b0, b1);
+      unpack_bf16x2(pc[k], c0, c1);
+      unpack_bf16x2(pd[k], d0, d1);
+      out[k] = pack_bf16x2(w00 * a0 + w01 * b0 + w10 * c0 + w11 * d0, w00 * a1 + w01 * b1 + w10 * c1 + w11 * d1);
+    }
+    *reinterpret_cast<uint4*>(y + ((static_cast<long>(n) * OH + oy) * OW + ox) * ldy + ycoff + 8 * c8) =
+        make_uint4(out[0], out[1], out[2], out[3]);
+  }
+}
+
+inline int grid_for(long work) {
+  long g = (work + 255) / 256;
+  return static_cast<int>(g < 1 ? 1 : (g > 8192 ? 8192 : g));
+}
+
+}  // namespace
+
+// partials must hold N * ceil(HW / 1024) * G * 2 floats.
+AI4E_API int ai4e_groupnorm_nhwc(const void* x, void* y, const void* gamma, const void* beta, void* partials, int N,
+                                 int HW, int C, int G, float eps, int relu, int ldx_ldy_pack, int coff_pack,
+                                 hipStream_t s) {
+  // ldx_ldy_pack = ldx | (ldy << 16), coff_pack = xcoff | (ycoff << 16) (channel strides/offsets < 65536)
+  const int ldx = ldx_ldy_pack & 0xffff, ldy = (ldx_ldy_pack >> 16) & 0xffff;
+  const int xcoff = coff_pack & 0xffff, ycoff = (coff_pack >> 16) & 0xffff;
+  if (C % 8 || G > 64 || C % G || (C / 8) > 256 || 256 % (C / 8) || ldx % 8 || ldy % 8 || xcoff % 8 || ycoff % 8)
+    return AI4E_EINVAL;
+  if ((C / G) % 8 && 8 % (C / G)) return AI4E_EINVAL;
+  const int nchunks = (HW + GN_PIX_PER_BLOCK - 1) / GN_PIX_PER_BLOCK;
+  hipLaunchKernelGGL(gn_stats_kernel, dim3(nchunks, N), dim3(256), 0, s, static_cast<const uint16_t*>(x),
+                     static_cast<float*>(partials), HW, C, G, ldx, xcoff, nchunks);
+  const int gx = grid_for(static_cast<long>(HW) * (C / 8) / 4 + 1);
+  hipLaunchKernelGGL(gn_apply_kernel, dim3(gx, N), dim3(256), 0, s, static_cast<const uint16_t*>(x),
+                     static_cast<uint16_t*>(y), static_cast<const float*>(partials), static_cast<const float*>(gamma),
+                     static_cast<const float*>(beta), HW, C, G, eps, relu, nchunks, ldx, xcoff, ldy, ycoff);
+  return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
+}
+
+AI4E_API int ai4e_upsample2x_bilinear(const void* x, void* y, int N, int H, int W, int C, int ldy, int ycoff, int unused,
+                                      hipStream_t s) {
+  (void)unused;
+  if (C % 8 || ldy % 8 || ycoff % 8) return AI4E_EINVAL;
+  hipLaunchKernelGGL(upsample2x_kernel, dim3(grid_for(static_cast<long>(N) * 4 * H * W * (C / 8))), dim3(256), 0, s,
+                     static_cast<const uint16_t*>(x), static_cast<uint16_t*>(y), N, H, W, C, ldy, ycoff);
+  return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
+}

@@ -1,0 +1,116 @@
+"""HIP kernels K2-K6 vs the PyTorch references (GPU box only)."""
+import os
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+from aiforearth_api_platform_amd.ops import _ext
+from aiforearth_api_platform_amd.ops.detection import (crop_resize_nhwc, crop_resize_reference, nms_batched_sorted,
+                                                       nms_reference, roi_align_nhwc, roi_align_reference)
+from aiforearth_api_platform_amd.ops.norm import group_norm_nhwc, upsample2x_nhwc
+from aiforearth_api_platform_amd.ops.stitch import TileGrid, stitch_reference, tile_stitch
+
+DEV = "cuda"
+
+
+@pytest.fixture(autouse=True, scope="module")
+def _lib():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from aiforearth_api_platform_amd import _build
+    _build.build_kernels()
+    _ext.lib()
+
+
+@pytest.mark.parametrize("shape,groups", [((2, 33, 17, 64), 32), ((1, 64, 64, 256), 32), ((3, 9, 9, 32), 8),
+                                          ((2, 40, 40, 512), 32)])
+@pytest.mark.parametrize("relu", [False, True])
+def test_groupnorm(shape, groups, relu):
+    torch.manual_seed(0)
+    x = (torch.randn(*shape) * 2 + 0.5).to(DEV).bfloat16()
+    g, b = torch.rand(shape[-1]) + 0.5, torch.randn(shape[-1])
+    y = group_norm_nhwc(x, g, b, groups, relu=relu)
+    ref = F.group_norm(x.float().permute(0, 3, 1, 2), groups, g.to(DEV), b.to(DEV))
+    ref = (F.relu(ref) if relu else ref).permute(0, 2, 3, 1)
+    assert (y.float() - ref).abs().max().item() < 0.05
+
+
+def test_groupnorm_concat_slices():
+    x_big = torch.randn(1, 16, 16, 96, device=DEV).bfloat16()
+    x = x_big[..., 32:96]
+    out = torch.zeros(1, 16, 16, 128, device=DEV, dtype=torch.bfloat16)
+    g, b = torch.ones(64), torch.zeros(64)
+    group_norm_nhwc(x, g, b, 32, out=out[..., 64:])
+    ref = F.group_norm(x.float().permute(0, 3, 1, 2), 32).permute(0, 2, 3, 1)
+    assert out[..., :64].abs().max() == 0
+    assert (out[..., 64:].float() - ref).abs().max().item() < 0.05
+
+
+@pytest.mark.parametrize("shape", [(2, 16, 16, 64), (1, 7, 9, 32), (1, 64, 64, 128)])
+def test_upsample_into_concat(shape):
+    x = torch.randn(*shape, device=DEV).bfloat16()
+    n, h, w, c = shape
+    buf = torch.zeros(n, 2 * h, 2 * w, c + 16, device=DEV, dtype=torch.bfloat16)
+    upsample2x_nhwc(x, out=buf, out_coff=16)
+    ref = F.interpolate(x.float().permute(0, 3, 1, 2), scale_factor=2, mode="bilinear",
+                        align_corners=False).permute(0, 2, 3, 1)
+    assert (buf[..., 16:].float() - ref).abs().max().item() < 0.02
+    assert buf[..., :16].abs().max() == 0
+
+
+@pytest.mark.parametrize("N,thr", [(100, 0.5), (2000, 0.7), (777, 0.3)])
+def test_nms_matches_reference(N, thr):
+    g = torch.Generator().manual_seed(N)
+    B = 3
+    xy = torch.rand(B, N, 2, generator=g) * 500
+    wh = torch.rand(B, N, 2, generator=g) * 120 + 2
+    boxes = torch.cat([xy, xy + wh], -1)
+    valid = torch.tensor([N, N - 7, N // 2], dtype=torch.int32)
+    keep, cnt = nms_batched_sorted(boxes.to(DEV), thr, 1000, valid.to(DEV))
+    keep, cnt = keep.cpu(), cnt.cpu()
+    for b in range(B):
+        n = int(valid[b])
+        ref = nms_reference(boxes[b, :n], torch.arange(n, 0, -1).float(), thr)[:1000]
+        assert keep[b, :cnt[b]].long().tolist() == ref.tolist()
+
+
+@pytest.mark.parametrize("aligned", [False, True])
+def test_roi_align(aligned):
+    g = torch.Generator().manual_seed(0)
+    feat = torch.randn(2, 25, 38, 64, generator=g)
+    R = 40
+    x1 = torch.rand(R, generator=g) * 500
+    y1 = torch.rand(R, generator=g) * 350
+    rois = torch.stack([torch.randint(0, 2, (R,), generator=g).float(), x1, y1,
+                        x1 + torch.rand(R, generator=g) * 200 + 1, y1 + torch.rand(R, generator=g) * 150 + 1], 1)
+    ref = roi_align_reference(feat.bfloat16().float(), rois, (7, 7), 1 / 16, 2, aligned)
+    out = roi_align_nhwc(feat.to(DEV).bfloat16(), rois.to(DEV), (7, 7), 1 / 16, 2, aligned)
+    assert (out.float().cpu() - ref).abs().max().item() < 0.03
+
+
+def test_crop_resize():
+    img = torch.randint(0, 256, (2, 300, 400, 3), dtype=torch.uint8)
+    boxes = torch.tensor([[0, 10.5, 20, 200, 220], [1, 0, 0, 400, 300], [1, 350, 250, 399, 299]])
+    ref = crop_resize_reference(img, boxes, (224, 224))
+    out = crop_resize_nhwc(img.to(DEV), boxes.to(DEV), (224, 224))
+    assert (out.float().cpu() - ref).abs().max().item() < 0.03
+
+
+@pytest.mark.parametrize("with_prob", [False, True])
+def test_tile_stitch(with_prob):
+    grid = TileGrid(300, 260, 64, 48)
+    C = 7
+    g = torch.Generator().manual_seed(3)
+    tiles = torch.randn(grid.nty, grid.ntx, 64, 64, C, generator=g).bfloat16()
+    cls_ref, prob_ref = stitch_reference(tiles.float(), grid, with_prob=with_prob)
+    cls, prob = tile_stitch(tiles.to(DEV), grid, with_prob=with_prob)
+    agree = (cls.cpu() == cls_ref).float().mean().item()
+    assert agree > 0.995, agree  # ties / bf16 rounding at near-equal logits may flip a few pixels
+    if with_prob:
+        assert (prob.float().cpu() - prob_ref).abs().max().item() < 0.02
+    ty0, ty1 = grid.tile_rows_for(100, 180)
+    cls2, _ = tile_stitch(tiles[ty0:ty1].to(DEV), grid, row0=100, rows=80, ty0=ty0)
+    assert torch.equal(cls2.cpu(), cls.cpu()[100:180])
