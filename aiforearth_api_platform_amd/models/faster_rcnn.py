@@ -1,0 +1,234 @@
+"""MegaDetector-style Faster-RCNN R50-FPN (BASELINE config #3) on NHWC bf16 with the HIP kernels.
+
+The reference's camera-trap detection API (``APIs/Charts/camera-trap/detection-async``, TF 1.9
+MegaDetector) is re-built as a torchvision-layout Faster-RCNN: ResNet-50 backbone (BN folded, K1),
+FPN (lateral 1x1 convs whose epilogue adds the nearest-upsampled top-down path, 3x3 output convs,
+P6 by stride-2 max-pool), RPN (3x3 conv + one fused 1x1 objectness/box-delta conv), proposals
+(top-k per level, decode, clip, NMS 0.7 via the K4 bitmask kernel — batched over images and
+levels), multi-level RoIAlign (K5, level picked in-kernel), the TwoMLPHead + predictor as 1x1
+convs through K1, and batched per-class NMS post-processing.
+
+Every stage runs on fixed, padded shapes ([B, post_nms_top_n] proposals, [B, detections] outputs
++ counts), so one forward has no host synchronisation and can be captured in a HIP graph.
+Weights are random-init (no checkpoint offline); classes = background + animal, person, vehicle.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+import torch.nn as nn
+
+from ..ops.conv import PackedConv, conv2d_nhwc, pack_conv
+from ..ops.detection import clip_boxes, decode_boxes, nms_batched_sorted, roi_align_fpn
+from ..ops.pool import maxpool2d_nhwc, preprocess_u8
+from .resnet import FusedResNet, resnet50
+
+MEGADETECTOR_CLASSES = ("background", "animal", "person", "vehicle")
+
+
+@dataclass
+class DetectorConfig:
+    num_classes: int = 4
+    fpn_channels: int = 256
+    anchor_sizes: Tuple[int, ...] = (32, 64, 128, 256, 512)
+    aspect_ratios: Tuple[float, ...] = (0.5, 1.0, 2.0)
+    pre_nms_top_n: int = 1000
+    post_nms_top_n: int = 1000
+    rpn_nms_thresh: float = 0.7
+    rpn_min_size: float = 1e-3
+    box_score_thresh: float = 0.05
+    box_nms_thresh: float = 0.5
+    detections_per_img: int = 100
+    box_reg_weights: Tuple[float, ...] = (10.0, 10.0, 5.0, 5.0)
+    representation: int = 1024
+
+
+def _rand_conv(cout, cin, k, g, std=None):
+    std = std if std is not None else math.sqrt(2.0 / (cin * k * k))
+    return torch.randn(cout, cin, k, k, generator=g) * std
+
+
+def _nearest_up2(x: torch.Tensor, hw: Tuple[int, int]) -> torch.Tensor:
+    """Nearest-neighbour upsample of NHWC x to spatial size hw (FPN top-down path)."""
+    n, h, w, c = x.shape
+    ih = (torch.arange(hw[0], device=x.device) * h // hw[0])
+    iw = (torch.arange(hw[1], device=x.device) * w // hw[1])
+    return x[:, ih][:, :, iw].contiguous()
+
+
+class FasterRCNN:
+    def __init__(self, cfg: Optional[DetectorConfig] = None, seed: int = 0, device="cpu",
+                 backbone: Optional[nn.Module] = None):
+        self.cfg = cfg = cfg or DetectorConfig()
+        self.device = d = torch.device(device)
+        g = torch.Generator().manual_seed(seed)
+        self.backbone = FusedResNet(backbone if backbone is not None else resnet50(seed=seed), device=d)
+        stage_out = (256, 512, 1024, 2048)
+        C = cfg.fpn_channels
+        self.lateral = [pack_conv(_rand_conv(C, ci, 1, g), torch.zeros(C)).to(d) for ci in stage_out]
+        self.fpn_out = [pack_conv(_rand_conv(C, C, 3, g), torch.zeros(C), pad=1).to(d) for _ in stage_out]
+        A = len(cfg.aspect_ratios)
+        self.num_anchors = A
+        self.rpn_conv = pack_conv(_rand_conv(C, C, 3, g, 0.01), torch.zeros(C), pad=1).to(d)
+        head_out = (A + 4 * A + 3) // 4 * 4
+        w = torch.zeros(head_out, C, 1, 1)
+        w[: A + 4 * A] = torch.randn(A + 4 * A, C, 1, 1, generator=g) * 0.01
+        self.rpn_head = pack_conv(w, torch.zeros(head_out)).to(d)
+        rep = cfg.representation
+        self.fc6 = pack_conv(torch.randn(rep, C * 49, 1, 1, generator=g) * math.sqrt(1.0 / (C * 49)),
+                             torch.zeros(rep)).to(d)
+        self.fc7 = pack_conv(torch.randn(rep, rep, 1, 1, generator=g) * math.sqrt(1.0 / rep), torch.zeros(rep)).to(d)
+        nc = cfg.num_classes
+        pred_out = (nc + 4 * nc + 3) // 4 * 4
+        wp = torch.zeros(pred_out, rep, 1, 1)
+        wp[:nc] = torch.randn(nc, rep, 1, 1, generator=g) * 0.01
+        wp[nc: nc + 4 * nc] = torch.randn(4 * nc, rep, 1, 1, generator=g) * 0.001
+        self.predictor = pack_conv(wp, torch.zeros(pred_out)).to(d)
+        self._anchor_cache: Dict[Tuple, List[torch.Tensor]] = {}
+
+    # ------------------------------------------------------------------ backbone + FPN
+    def backbone_stages(self, x: torch.Tensor) -> List[torch.Tensor]:
+        bb = self.backbone
+        x = conv2d_nhwc(x, bb.stem, relu=True)
+        x = maxpool2d_nhwc(x, 3, 2, 1)
+        outs = []
+        ends = {2, 6, 12, 15}  # last block index of layer1..layer4 for (3, 4, 6, 3)
+        for i, (c1, c2, c3, down) in enumerate(bb.blocks):
+            idt = x if down is None else conv2d_nhwc(x, down)
+            y = conv2d_nhwc(conv2d_nhwc(x, c1, relu=True), c2, relu=True)
+            x = conv2d_nhwc(y, c3, residual=idt, relu=True)
+            if i in ends:
+                outs.append(x)
+        return outs
+
+    def fpn(self, feats: List[torch.Tensor]) -> List[torch.Tensor]:
+        inner = conv2d_nhwc(feats[-1], self.lateral[-1])
+        results = [conv2d_nhwc(inner, self.fpn_out[-1])]
+        for i in range(len(feats) - 2, -1, -1):
+            top = _nearest_up2(inner, feats[i].shape[1:3])
+            inner = conv2d_nhwc(feats[i], self.lateral[i], residual=top)  # lateral + top-down fused
+            results.insert(0, conv2d_nhwc(inner, self.fpn_out[i]))
+        results.append(maxpool2d_nhwc(results[-1], 1, 2, 0))  # P6
+        return results
+
+    # ------------------------------------------------------------------ anchors
+    def anchors(self, shapes: Sequence[Tuple[int, int]], strides: Sequence[int]) -> List[torch.Tensor]:
+        key = (tuple(shapes), tuple(strides))
+        if key not in self._anchor_cache:
+            out = []
+            for (h, w), s, size in zip(shapes, strides, self.cfg.anchor_sizes):
+                r = torch.tensor(self.cfg.aspect_ratios)
+                hr = torch.sqrt(r)
+                wr = 1 / hr
+                ws, hs = wr * size, hr * size
+                base = torch.round(torch.stack([-ws, -hs, ws, hs], 1) / 2)
+                sy, sx = torch.meshgrid(torch.arange(h) * s, torch.arange(w) * s, indexing="ij")
+                shifts = torch.stack([sx, sy, sx, sy], -1).reshape(-1, 1, 4).float()
+                out.append((shifts + base[None]).reshape(-1, 4).to(self.device))
+            self._anchor_cache[key] = out
+        return self._anchor_cache[key]
+
+    # ------------------------------------------------------------------ RPN + proposals
+    def proposals(self, P: List[torch.Tensor], img_hw: Tuple[int, int]) -> Tuple[torch.Tensor, torch.Tensor]:
+        cfg = self.cfg
+        A = self.num_anchors
+        B = P[0].shape[0]
+        shapes = [p.shape[1:3] for p in P]
+        strides = [img_hw[0] // s[0] for s in shapes]
+        anchors = self.anchors(shapes, strides)
+        boxes_l, scores_l, lvl_l = [], [], []
+        for li, p in enumerate(P):
+            t = conv2d_nhwc(p, self.rpn_conv, relu=True)
+            head = conv2d_nhwc(t, self.rpn_head).float()          # [B, h, w, 16]
+            obj = head[..., :A].reshape(B, -1)
+            deltas = head[..., A: 5 * A].reshape(B, -1, 4)
+            k = min(cfg.pre_nms_top_n, obj.shape[1])
+            sc, idx = obj.topk(k, dim=1)
+            d = torch.gather(deltas, 1, idx[..., None].expand(B, k, 4))
+            a = anchors[li][idx]
+            bx = clip_boxes(decode_boxes(a, d), img_hw[0], img_hw[1])
+            boxes_l.append(bx)
+            scores_l.append(torch.sigmoid(sc))
+            lvl_l.append(torch.full((B, k), li, device=bx.device, dtype=torch.float32))
+        boxes = torch.cat(boxes_l, 1)
+        scores = torch.cat(scores_l, 1)
+        lvl = torch.cat(lvl_l, 1)
+        wh = boxes[..., 2:] - boxes[..., :2]
+        small = (wh < cfg.rpn_min_size).any(-1)
+        scores = scores.masked_fill(small, -1.0)
+        # batched NMS across levels via coordinate offsets; invalid (small) boxes sort last
+        order = scores.argsort(dim=1, descending=True)
+        boxes_s = torch.gather(boxes, 1, order[..., None].expand_as(boxes))
+        scores_s = torch.gather(scores, 1, order)
+        off = torch.gather(lvl, 1, order)[..., None] * (max(img_hw) + 1.0)
+        valid = (scores_s >= 0).sum(1).to(torch.int32)
+        keep, count = nms_batched_sorted(boxes_s + off, cfg.rpn_nms_thresh, cfg.post_nms_top_n, valid)
+        keep_l = keep.clamp(min=0).long()
+        props = torch.gather(boxes_s, 1, keep_l[..., None].expand(B, keep.shape[1], 4))
+        pad = (keep < 0)[..., None]
+        props = props.masked_fill(pad, 0.0)
+        return props, count
+
+    # ------------------------------------------------------------------ box head + postprocess
+    def box_head(self, P: List[torch.Tensor], props: torch.Tensor, img_hw):
+        B, R, _ = props.shape
+        bidx = torch.arange(B, device=props.device, dtype=torch.float32)[:, None, None].expand(B, R, 1)
+        rois = torch.cat([bidx, props], -1).reshape(B * R, 5)
+        strides = [img_hw[0] // p.shape[1] for p in P[:4]]
+        feats = roi_align_fpn(P[:4], [1.0 / s for s in strides], rois, (7, 7), 2)  # [B*R, 7, 7, C]
+        x = feats.reshape(B * R, 1, 1, -1)
+        x = conv2d_nhwc(x, self.fc6, relu=True)
+        x = conv2d_nhwc(x, self.fc7, relu=True)
+        out = conv2d_nhwc(x, self.predictor).reshape(B, R, -1).float()
+        nc = self.cfg.num_classes
+        return out[..., :nc], out[..., nc: 5 * nc].reshape(B, R, nc, 4)
+
+    def postprocess(self, props, count, logits, deltas, img_hw):
+        cfg = self.cfg
+        B, R, nc = logits.shape
+        scores = torch.softmax(logits, -1)[..., 1:]                            # drop background
+        boxes = decode_boxes(props[:, :, None, :].expand(B, R, nc - 1, 4), deltas[:, :, 1:], cfg.box_reg_weights)
+        boxes = clip_boxes(boxes, img_hw[0], img_hw[1])
+        labels = torch.arange(1, nc, device=props.device).expand(B, R, nc - 1)
+        roi_valid = (torch.arange(R, device=props.device)[None] < count[:, None].long())[..., None]
+        wh = boxes[..., 2:] - boxes[..., :2]
+        ok = roi_valid & (scores > cfg.box_score_thresh) & (wh >= 1e-2).all(-1)
+        scores = scores.masked_fill(~ok, -1.0).reshape(B, -1)
+        boxes = boxes.reshape(B, -1, 4)
+        labels = labels.reshape(B, -1)
+        order = scores.argsort(1, descending=True)
+        s_s = torch.gather(scores, 1, order)
+        b_s = torch.gather(boxes, 1, order[..., None].expand_as(boxes))
+        l_s = torch.gather(labels, 1, order)
+        valid = (s_s >= 0).sum(1).to(torch.int32)
+        off = l_s[..., None].float() * (max(img_hw) + 1.0)
+        keep, ndet = nms_batched_sorted(b_s + off, cfg.box_nms_thresh, cfg.detections_per_img, valid)
+        k = keep.clamp(min=0).long()
+        det_boxes = torch.gather(b_s, 1, k[..., None].expand(B, k.shape[1], 4))
+        det_scores = torch.gather(s_s, 1, k)
+        det_labels = torch.gather(l_s, 1, k)
+        return det_boxes, det_scores, det_labels, ndet
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, x: torch.Tensor):
+        """x normalized NHWC [B, H, W, 8] (H, W multiples of 64). Returns padded detections:
+        boxes [B, D, 4], scores [B, D], labels [B, D], counts [B]."""
+        img_hw = (x.shape[1], x.shape[2])
+        P = self.fpn(self.backbone_stages(x))
+        props, count = self.proposals(P, img_hw)
+        logits, deltas = self.box_head(P, props, img_hw)
+        return self.postprocess(props, count, logits, deltas, img_hw)
+
+    def forward_u8(self, img_u8: torch.Tensor):
+        return self.forward(preprocess_u8(img_u8))
+
+    __call__ = forward_u8
+
+    @staticmethod
+    def to_list(dets) -> List[Dict[str, list]]:
+        boxes, scores, labels, n = [t.cpu() for t in dets]
+        return [{"boxes": boxes[i, : n[i]].tolist(), "scores": scores[i, : n[i]].tolist(),
+                 "labels": [MEGADETECTOR_CLASSES[int(c)] for c in labels[i, : n[i]]]} for i in range(len(n))]

@@ -26,7 +26,7 @@ _c_int, _c_long, _c_float, _vp = ctypes.c_int, ctypes.c_long, ctypes.c_float, ct
 _SIGS = {
     "ai4e_conv2d_fwd": [_vp, _vp, _vp, _vp, _vp] + [_c_int] * 19 + [_vp],
     "ai4e_preprocess_u8": [_vp, _vp, _c_long, _c_int, _vp, _vp, _c_float, _vp],
-    "ai4e_maxpool2d": [_vp, _vp] + [_c_int] * 9 + [_vp],
+    "ai4e_maxpool2d": [_vp, _vp] + [_c_int] * 10 + [_vp],
     "ai4e_global_avgpool": [_vp, _vp, _c_int, _c_int, _c_int, _vp],
     "ai4e_groupnorm_nhwc": [_vp, _vp, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_float, _c_int, _c_int,
                             _c_int, _vp],
@@ -34,6 +34,7 @@ _SIGS = {
     "ai4e_nms_mask": [_vp, _c_int, _c_int, _c_float, _vp, _vp],
     "ai4e_nms_reduce": [_vp, _vp, _c_int, _c_int, _c_int, _vp, _vp, _vp],
     "ai4e_roi_align_nhwc": [_vp, _vp, _vp] + [_c_int] * 7 + [_c_float, _c_int, _c_int, _vp],
+    "ai4e_roi_align_fpn_nhwc": [_vp] * 8 + [_c_int] * 6 + [_vp],
     "ai4e_crop_resize_nhwc": [_vp, _vp, _vp, _vp] + [_c_int] * 7 + [_vp],
     "ai4e_tile_stitch": [_vp, _vp, _vp] + [_c_int] * 10 + [_vp],
 }

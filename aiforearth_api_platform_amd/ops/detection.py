@@ -189,6 +189,26 @@ def multiscale_roi_align(feats: Sequence[torch.Tensor], scales: Sequence[float],
     return out
 
 
+def roi_align_fpn(feats: Sequence[torch.Tensor], scales: Sequence[float], rois: torch.Tensor, out_hw=(7, 7),
+                  sampling: int = 2, aligned: bool = False) -> torch.Tensor:
+    """Multi-level RoIAlign over P2..P5 with in-kernel level assignment (static shapes, graph-safe)."""
+    if len(feats) != 4:
+        raise ValueError("roi_align_fpn expects 4 levels (P2..P5)")
+    if _ext.backend_for(feats[0]) == "hip":
+        feats = [f.contiguous() for f in feats]
+        C = feats[0].shape[-1]
+        R = rois.shape[0]
+        hw = (ctypes.c_int * 8)(*[v for f in feats for v in (f.shape[1], f.shape[2])])
+        sc = (ctypes.c_float * 4)(*[float(s) for s in scales])
+        rois = rois.float().contiguous()
+        out = torch.empty(R, out_hw[0], out_hw[1], C, device=feats[0].device, dtype=feats[0].dtype)
+        _ext.call("ai4e_roi_align_fpn_nhwc", *[f.data_ptr() for f in feats], ctypes.addressof(hw), ctypes.addressof(sc),
+                  rois.data_ptr(), out.data_ptr(), C, R, out_hw[0], out_hw[1], sampling, int(aligned),
+                  _ext.stream_ptr(feats[0].device))
+        return out
+    return multiscale_roi_align(feats, scales, rois, out_hw, sampling)
+
+
 # ---------------------------------------------------------------------------------------------- crops
 def crop_resize_reference(img_u8: torch.Tensor, boxes: torch.Tensor, out_hw: Tuple[int, int],
                           mean=IMAGENET_MEAN, std=IMAGENET_STD) -> torch.Tensor:

@@ -43,9 +43,10 @@ def maxpool2d_nhwc(x: torch.Tensor, k: int = 3, stride: int = 2, pad: int = 1) -
     n, h, w, c = x.shape
     oh, ow = (h + 2 * pad - k) // stride + 1, (w + 2 * pad - k) // stride + 1
     if _ext.backend_for(x) == "hip":
-        x = x.contiguous()
+        if x.stride(3) != 1 or x.stride(1) != w * x.stride(2) or x.stride(0) != h * x.stride(1):
+            x = x.contiguous()  # channel slices of an NHWC buffer are read in place
         y = torch.empty(n, oh, ow, c, device=x.device, dtype=x.dtype)
-        _ext.call("ai4e_maxpool2d", x.data_ptr(), y.data_ptr(), n, h, w, c, oh, ow, k, stride, pad,
+        _ext.call("ai4e_maxpool2d", x.data_ptr(), y.data_ptr(), n, h, w, c, oh, ow, k, stride, pad, x.stride(2),
                   _ext.stream_ptr(x.device))
         return y
     y = F.max_pool2d(x.permute(0, 3, 1, 2).float(), k, stride, pad)

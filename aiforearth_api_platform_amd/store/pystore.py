@@ -137,6 +137,8 @@ class TaskStore:
             if r is None:
                 r = self._records[task_id] = _Record()
                 r.t_created = mnow
+            elif absolute_path(endpoint) != r.endpoint_path:
+                self._idx(f"{r.endpoint_path}_{r.backend_status}").rem(task_id)  # pipeline hop
             r.task_id = task_id
             r.timestamp = dotnet_timestamp(wnow)
             r.status, r.backend_status, r.endpoint = status, backend_status, endpoint

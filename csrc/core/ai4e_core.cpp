@@ -189,7 +189,14 @@ class TaskStore {
     if (task_id.find_first_not_of(" \t\r\n") == std::string::npos) task_id = uuid_.next();
     const double wnow = wall_now(), mnow = mono_now();
     TaskRecord& r = records_[task_id];
-    if (r.task_id.empty()) r.t_created = mnow;
+    if (r.task_id.empty()) {
+      r.t_created = mnow;
+    } else {
+      // Pipeline hop to another endpoint: the task leaves the previous endpoint's state index
+      // (the reference leaves it behind in "{old}_{state}", inflating that queue's depth metric).
+      const std::string new_path = absolute_path(endpoint);
+      if (new_path != r.endpoint_path) index_[r.endpoint_path + "_" + r.backend_status].rem(task_id);
+    }
     r.task_id = task_id;
     r.timestamp = dotnet_timestamp(wnow);
     r.status = status;

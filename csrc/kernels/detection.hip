@@ -126,6 +126,60 @@ __global__ __launch_bounds__(256) void roi_align_kernel(const uint16_t* __restri
   }
 }
 
+// Multi-level (FPN P2..P5) RoIAlign: the level of each RoI is picked in-kernel (Lin et al. eq. 1,
+// canonical size 224 at level 4, clamped to [2, 5]) so the whole box head has static shapes and is
+// HIP-graph capturable (no per-level nonzero/gather on the host).
+struct FpnLevels {
+  const uint16_t* f[4];
+  int h[4], w[4];
+  float scale[4];
+};
+
+__global__ __launch_bounds__(256) void roi_align_fpn_kernel(FpnLevels lv, const float* __restrict__ rois,
+                                                            uint16_t* __restrict__ out, int C, int R, int PH, int PW,
+                                                            int sampling, int aligned) {
+  const int C8 = C >> 3;
+  const long total = static_cast<long>(R) * PH * PW * C8;
+  for (long idx = blockIdx.x * 256L + threadIdx.x; idx < total; idx += static_cast<long>(gridDim.x) * 256) {
+    const int c8 = static_cast<int>(idx % C8);
+    long t = idx / C8;
+    const int pw = static_cast<int>(t % PW);
+    t /= PW;
+    const int ph = static_cast<int>(t % PH);
+    const int r = static_cast<int>(t / PH);
+    const float* roi = rois + 5L * r;
+    const float area = fmaxf(roi[3] - roi[1], 0.f) * fmaxf(roi[4] - roi[2], 0.f);
+    int l = static_cast<int>(floorf(4.f + log2f(sqrtf(area) / 224.f + 1e-6f)));
+    l = min(max(l, 2), 5) - 2;
+    const int H = lv.h[l], W = lv.w[l];
+    const float scale = lv.scale[l];
+    const int img = static_cast<int>(roi[0]);
+    const float off = aligned ? 0.5f : 0.f;
+    const float x1 = roi[1] * scale - off, y1 = roi[2] * scale - off;
+    float rw = roi[3] * scale - off - x1, rh = roi[4] * scale - off - y1;
+    if (!aligned) {
+      rw = fmaxf(rw, 1.f);
+      rh = fmaxf(rh, 1.f);
+    }
+    const float bh = rh / PH, bw = rw / PW;
+    const int gh = sampling > 0 ? sampling : static_cast<int>(ceilf(rh / PH));
+    const int gw = sampling > 0 ? sampling : static_cast<int>(ceilf(rw / PW));
+    const float inv = 1.f / fmaxf(gh * gw, 1);
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const uint16_t* f = lv.f[l] + static_cast<long>(img) * H * W * C;
+    for (int iy = 0; iy < gh; ++iy) {
+      const float y = y1 + ph * bh + (iy + 0.5f) * bh / gh;
+      for (int ix = 0; ix < gw; ++ix) {
+        const float x = x1 + pw * bw + (ix + 0.5f) * bw / gw;
+        bilinear_acc8(f, H, W, C, y, x, c8, inv, acc);
+      }
+    }
+    *reinterpret_cast<uint4*>(out + (((static_cast<long>(r) * PH + ph) * PW + pw) * C) + 8 * c8) =
+        make_uint4(pack_bf16x2(acc[0], acc[1]), pack_bf16x2(acc[2], acc[3]), pack_bf16x2(acc[4], acc[5]),
+                   pack_bf16x2(acc[6], acc[7]));
+  }
+}
+
 // Crop + bilinear resize + normalize: uint8 image [N, H, W, C<=8], boxes [R, 5] = (img, x1, y1, x2, y2)
 // in pixels -> bf16 [R, OH, OW, 8] normalized (classifier stem input). norm = mean[8] ++ std[8].
 __global__ __launch_bounds__(256) void crop_resize_kernel(const uint8_t* __restrict__ img, const float* __restrict__ boxes,
@@ -194,6 +248,25 @@ AI4E_API int ai4e_roi_align_nhwc(const void* feat, const void* rois, void* out, 
   hipLaunchKernelGGL(roi_align_kernel, dim3(grid_for(static_cast<long>(R) * PH * PW * (C / 8))), dim3(256), 0, s,
                      static_cast<const uint16_t*>(feat), static_cast<const float*>(rois), static_cast<uint16_t*>(out), H,
                      W, C, R, PH, PW, sampling, scale, aligned);
+  return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
+}
+
+// feats: 4 NHWC bf16 maps (P2..P5) of one batch; hw = {h0, w0, h1, w1, ...}; scales = 1/stride per level.
+AI4E_API int ai4e_roi_align_fpn_nhwc(const void* f0, const void* f1, const void* f2, const void* f3, const int* hw,
+                                     const float* scales, const void* rois, void* out, int C, int R, int PH, int PW,
+                                     int sampling, int aligned, hipStream_t s) {
+  if (C % 8) return AI4E_EINVAL;
+  if (R <= 0) return AI4E_OK;
+  FpnLevels lv;
+  const void* fs[4] = {f0, f1, f2, f3};
+  for (int i = 0; i < 4; ++i) {
+    lv.f[i] = static_cast<const uint16_t*>(fs[i]);
+    lv.h[i] = hw[2 * i];
+    lv.w[i] = hw[2 * i + 1];
+    lv.scale[i] = scales[i];
+  }
+  hipLaunchKernelGGL(roi_align_fpn_kernel, dim3(grid_for(static_cast<long>(R) * PH * PW * (C / 8))), dim3(256), 0, s,
+                     lv, static_cast<const float*>(rois), static_cast<uint16_t*>(out), C, R, PH, PW, sampling, aligned);
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
 }
 

@@ -22,7 +22,8 @@ __global__ __launch_bounds__(256) void preprocess_u8_kernel(const uint8_t* __res
 
 // Max pool NHWC bf16; one lane = 8 channels of one output pixel. Padding ignored (= -inf).
 __global__ __launch_bounds__(256) void maxpool_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y, int N,
-                                                      int H, int W, int C, int OH, int OW, int k, int s, int pad) {
+                                                      int H, int W, int C, int OH, int OW, int k, int s, int pad,
+                                                      int ldx8) {
   const int C8 = C >> 3;
   const long total = static_cast<long>(N) * OH * OW * C8;
   for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += static_cast<long>(gridDim.x) * 256) {
@@ -41,7 +42,7 @@ __global__ __launch_bounds__(256) void maxpool_kernel(const uint16_t* __restrict
       for (int dw = 0; dw < k; ++dw) {
         const int iw = ow * s - pad + dw;
         if (iw < 0 || iw >= W) continue;
-        const uint4 v = reinterpret_cast<const uint4*>(x)[((static_cast<long>(n) * H + ih) * W + iw) * C8 + c8];
+        const uint4 v = reinterpret_cast<const uint4*>(x)[((static_cast<long>(n) * H + ih) * W + iw) * ldx8 + c8];
         float a, b;
         unpack_bf16x2(v.x, a, b); m[0] = fmaxf(m[0], a); m[1] = fmaxf(m[1], b);
         unpack_bf16x2(v.y, a, b); m[2] = fmaxf(m[2], a); m[3] = fmaxf(m[3], b);
@@ -96,11 +97,13 @@ AI4E_API int ai4e_preprocess_u8(const void* in, void* out, long npix, int cin, c
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
 }
 
+// x may be a channel slice of a wider NHWC buffer: row stride ldx (elements), x points at the slice start.
 AI4E_API int ai4e_maxpool2d(const void* x, void* y, int N, int H, int W, int C, int OH, int OW, int k, int stride,
-                            int pad, hipStream_t s) {
-  if (C % 8) return AI4E_EINVAL;
+                            int pad, int ldx, hipStream_t s) {
+  if (C % 8 || ldx % 8 || ldx < C) return AI4E_EINVAL;
   hipLaunchKernelGGL(maxpool_kernel, dim3(grid_for(static_cast<long>(N) * OH * OW * (C / 8))), dim3(256), 0, s,
-                     static_cast<const uint16_t*>(x), static_cast<uint16_t*>(y), N, H, W, C, OH, OW, k, stride, pad);
+                     static_cast<const uint16_t*>(x), static_cast<uint16_t*>(y), N, H, W, C, OH, OW, k, stride, pad,
+                     ldx / 8);
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
 }
 

@@ -1,0 +1,37 @@
+"""Faster-RCNN R50-FPN plumbing on CPU (torch reference ops): shapes, padding, NMS invariants."""
+import torch
+
+from aiforearth_api_platform_amd.models.faster_rcnn import DetectorConfig, FasterRCNN
+from aiforearth_api_platform_amd.ops.detection import box_iou
+
+
+def test_detector_forward_shapes_and_invariants():
+    cfg = DetectorConfig(pre_nms_top_n=200, post_nms_top_n=100, detections_per_img=20, box_score_thresh=0.0)
+    det = FasterRCNN(cfg, seed=0)
+    img = torch.randint(0, 256, (2, 128, 128, 3), dtype=torch.uint8)
+    boxes, scores, labels, n = det(img)
+    assert boxes.shape == (2, 20, 4) and scores.shape == (2, 20) and n.shape == (2,)
+    for b in range(2):
+        k = int(n[b])
+        assert k > 0
+        bb, ss, ll = boxes[b, :k], scores[b, :k], labels[b, :k]
+        assert torch.all(ss[:-1] >= ss[1:])
+        assert torch.all((bb[:, 0] >= 0) & (bb[:, 2] <= 128) & (bb[:, 1] >= 0) & (bb[:, 3] <= 128))
+        assert torch.all((ll >= 1) & (ll <= 3))
+        for c in range(1, 4):  # per-class NMS: no same-class pair above the threshold
+            m = ll == c
+            if m.sum() > 1:
+                iou = box_iou(bb[m], bb[m])
+                iou.fill_diagonal_(0)
+                assert iou.max() <= cfg.box_nms_thresh + 1e-6
+    out = FasterRCNN.to_list((boxes, scores, labels, n))
+    assert len(out) == 2 and set(out[0]["labels"]) <= {"animal", "person", "vehicle"}
+
+
+def test_anchor_layout():
+    det = FasterRCNN(DetectorConfig(), seed=0)
+    a = det.anchors([(2, 2)], [16])[0]
+    assert a.shape == (12, 4)
+    # location (0,0) anchors are centred on the origin; location (0,1) shifted by the stride in x
+    assert torch.allclose((a[0, :2] + a[0, 2:]) / 2, torch.zeros(2))
+    assert torch.allclose(a[3] - a[0], torch.tensor([16.0, 0, 16.0, 0]))
