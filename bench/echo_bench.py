@@ -1,0 +1,126 @@
+"""BASELINE config #1: sync "echo" API on CPU (plumbing, no GPU) — this platform vs reference style.
+
+* ``platform``: the aiohttp gateway route -> in-process echo backend (admission control, metrics).
+* ``reference``: a Flask app with the ``APIService.api_sync_func`` decorator (the reference's
+  container runtime, ``APIs/1.0/base-py/ai4e_service.py``), served by werkzeug's threaded server.
+
+Drives each with an asyncio HTTP client at fixed concurrency; reports req/s and p50/p99 latency.
+
+    python bench/echo_bench.py [--requests 5000 --concurrency 64]
+"""
+import argparse
+import asyncio
+import json
+import os
+import socket
+import sys
+import threading
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def start_platform(port):
+    from aiohttp import web
+
+    from aiforearth_api_platform_amd.config import Config
+    from aiforearth_api_platform_amd.gateway.control import ControlPlane
+    from aiforearth_api_platform_amd.gateway.server import Gateway, Route, RouteTable
+    from aiforearth_api_platform_amd.models.toy import echo
+
+    t = RouteTable()
+    t.add(Route("/v1/echo", "sync", echo))
+    gw = Gateway(ControlPlane(Config.load(env={})), t)
+
+    def run():
+        loop = asyncio.new_event_loop()
+        asyncio.set_event_loop(loop)
+        runner = web.AppRunner(gw.app)
+        loop.run_until_complete(runner.setup())
+        loop.run_until_complete(web.TCPSite(runner, "127.0.0.1", port).start())
+        loop.run_forever()
+
+    threading.Thread(target=run, daemon=True).start()
+
+
+def start_reference(port):
+    from flask import Flask, request
+
+    from aiforearth_api_platform_amd.api import APIService, InProcTaskClient, TaskManager
+    from aiforearth_api_platform_amd.utils.logging import AI4ELogger
+
+    app = Flask("echo")
+    svc = APIService(app, AI4ELogger(stream=None), TaskManager(InProcTaskClient()), install_signal_handlers=False)
+
+    @svc.api_sync_func(api_path="/echo", methods=["POST"])
+    def echo(*args, **kwargs):
+        return request.get_data()
+
+    threading.Thread(target=lambda: app.run("127.0.0.1", port, threaded=True), daemon=True).start()
+
+
+async def drive(url, n, conc):
+    import aiohttp
+
+    lat = []
+    payload = json.dumps({"hello": "world"}).encode()
+    async with aiohttp.ClientSession(connector=aiohttp.TCPConnector(limit=conc)) as s:
+        for _ in range(200):
+            try:
+                async with s.post(url, data=payload) as r:
+                    await r.read()
+                    break
+            except aiohttp.ClientError:
+                await asyncio.sleep(0.05)
+        sem = asyncio.Semaphore(conc)
+
+        async def one():
+            async with sem:
+                t = time.perf_counter()
+                async with s.post(url, data=payload, headers={"Content-Type": "application/json"}) as r:
+                    assert r.status == 200, r.status
+                    await r.read()
+                lat.append(time.perf_counter() - t)
+
+        t0 = time.perf_counter()
+        await asyncio.gather(*[one() for _ in range(n)])
+        dt = time.perf_counter() - t0
+    lat.sort()
+    return n / dt, lat[len(lat) // 2] * 1e3, lat[int(len(lat) * 0.99)] * 1e3
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--requests", type=int, default=5000)
+    ap.add_argument("--concurrency", type=int, default=64)
+    ap.add_argument("--json-out", default="")
+    a = ap.parse_args()
+    pp, rp = _port(), _port()
+    start_platform(pp)
+    os.environ["API_PREFIX"] = "/v1"
+    from aiforearth_api_platform_amd import config as cfgmod
+    cfgmod.set_config(cfgmod.Config.load())
+    start_reference(rp)
+    res = {}
+    for name, url in (("platform", f"http://127.0.0.1:{pp}/v1/echo"), ("reference_style", f"http://127.0.0.1:{rp}/v1/echo")):
+        rps, p50, p99 = asyncio.run(drive(url, a.requests, a.concurrency))
+        res[name] = {"req_per_s": round(rps, 1), "p50_ms": round(p50, 3), "p99_ms": round(p99, 3)}
+    out = {"metric": "echo API req/s (CPU, sync)", "value": res["platform"]["req_per_s"], "unit": "req/s",
+           "vs_reference_style": round(res["platform"]["req_per_s"] / res["reference_style"]["req_per_s"], 3),
+           "results": res, "config": {"requests": a.requests, "concurrency": a.concurrency}}
+    print(json.dumps(out), flush=True)
+    if a.json_out:
+        with open(a.json_out, "w") as f:
+            f.write(json.dumps(out) + "\n")
+
+
+if __name__ == "__main__":
+    main()

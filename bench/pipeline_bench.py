@@ -1,0 +1,62 @@
+"""BASELINE config #5: detector -> classifier 2-stage ensemble, crops handed GPU->GPU over RCCL.
+
+Ranks pair up (2i detector, 2i+1 classifier); world 1 runs both stages on one GPU. Reports whole-node
+images/s (images through both stages) and crops/s.
+
+    torchrun --nproc-per-node 2 bench/pipeline_bench.py [--batch 8 --size 640 --steps 10]
+"""
+import argparse
+
+import torch
+
+from common import Dist, build_once
+
+
+def main():
+    import time
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=8)
+    ap.add_argument("--size", type=int, default=640)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--json-out", default="")
+    a = ap.parse_args()
+    d = Dist()
+    build_once(d)
+    from aiforearth_api_platform_amd.models.faster_rcnn import DetectorConfig, FasterRCNN
+    from aiforearth_api_platform_amd.models.resnet import FusedResNet, resnet50
+    from aiforearth_api_platform_amd.runtime.pipeline import DetectClassifyPipeline, PipelineConfig
+    det = FasterRCNN(DetectorConfig(), seed=0, device=d.device)
+    cls = FusedResNet(resnet50(num_classes=200, seed=1), device=d.device)
+    pcfg = PipelineConfig(score_thresh=0.0, class_id=None, max_crops_per_image=4)
+    p = DetectClassifyPipeline(det, cls.forward, d.device, pcfg)
+    g = torch.Generator().manual_seed(d.rank)
+    batches = [torch.randint(0, 256, (a.batch, a.size, a.size, 3), dtype=torch.uint8, generator=g).to(d.device)
+               for _ in range(2)]
+    crops = 0
+    if p.is_detector:
+        p.run_batches([batches[i % 2] for i in range(a.warmup)])
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        out = p.run_batches([batches[i % 2] for i in range(a.steps)])
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t
+        crops = sum(b.shape[0] for _, b, _ in out)
+        p.stop()
+    else:
+        p.serve_classifier()
+        dt = 0.0
+    dt, = d.max(dt)
+    pairs = max(1, d.world // 2)
+    imgs = a.steps * a.batch * pairs
+    d.emit({"metric": "detector->classifier ensemble images/sec (whole node)", "value": round(imgs / dt, 2),
+            "unit": "images/s", "n_gpus": d.world, "crops_per_s": round(crops * pairs / dt, 2),
+            "ms_per_batch": round(dt / a.steps * 1e3, 2), "dtype": "bf16",
+            "data": "synthetic uint8 images, random-init weights",
+            "config": {"per_pair_batch": a.batch, "image_size": a.size, "crop": 224,
+                       "parallelism": f"pipeline2x{pairs}" if d.world > 1 else "colocated"}}, a.json_out)
+    d.close()
+
+
+if __name__ == "__main__":
+    main()
