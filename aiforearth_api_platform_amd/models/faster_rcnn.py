@@ -23,7 +23,7 @@ import torch.nn as nn
 
 from ..ops.conv import PackedConv, conv2d_nhwc, pack_conv
 from ..ops.detection import clip_boxes, decode_boxes, nms_batched_sorted, roi_align_fpn
-from ..ops.pool import maxpool2d_nhwc, preprocess_u8
+from ..ops.pool import maxpool2d_nhwc, preprocess_s2d_u8, preprocess_u8
 from .resnet import FusedResNet, resnet50
 
 MEGADETECTOR_CLASSES = ("background", "animal", "person", "vehicle")
@@ -92,7 +92,7 @@ class FasterRCNN:
     # ------------------------------------------------------------------ backbone + FPN
     def backbone_stages(self, x: torch.Tensor) -> List[torch.Tensor]:
         bb = self.backbone
-        x = conv2d_nhwc(x, bb.stem, relu=True)
+        x = conv2d_nhwc(bb.stem_input(x), bb.stem, relu=True)
         x = maxpool2d_nhwc(x, 3, 2, 1)
         outs = []
         ends = {2, 6, 12, 15}  # last block index of layer1..layer4 for (3, 4, 6, 3)
@@ -216,14 +216,14 @@ class FasterRCNN:
     def forward(self, x: torch.Tensor):
         """x normalized NHWC [B, H, W, 8] (H, W multiples of 64). Returns padded detections:
         boxes [B, D, 4], scores [B, D], labels [B, D], counts [B]."""
-        img_hw = (x.shape[1], x.shape[2])
+        img_hw = (x.shape[1], x.shape[2]) if x.shape[-1] != 16 else (2 * x.shape[1], 2 * x.shape[2])
         P = self.fpn(self.backbone_stages(x))
         props, count = self.proposals(P, img_hw)
         logits, deltas = self.box_head(P, props, img_hw)
         return self.postprocess(props, count, logits, deltas, img_hw)
 
     def forward_u8(self, img_u8: torch.Tensor):
-        return self.forward(preprocess_u8(img_u8))
+        return self.forward(preprocess_s2d_u8(img_u8))
 
     __call__ = forward_u8
 

@@ -6,9 +6,9 @@ Two forms:
   weight source (``load_state_dict`` accepts torchvision-style keys; weights are random-init here
   because no checkpoint is available offline).
 * ``FusedResNet`` — the serving form: BatchNorm folded into the convs, NHWC bf16 activations, every
-  conv (+bias +ReLU +residual add) one K1 HIP kernel, preprocess (K7), max-pool, global avg-pool
-  and the classifier (a 1x1 conv through K1) — 57 kernel launches per forward, capturable in a
-  HIP graph.
+  conv (+bias +ReLU +residual add) one K1 HIP kernel, preprocess (K7, fused 2x2 space-to-depth so
+  the 7x7/2 stem runs as a dense 4x4/1 conv), max-pool, global avg-pool and the classifier (a 1x1
+  conv through K1) — 57 kernel launches per forward, capturable in a HIP graph.
 """
 from __future__ import annotations
 
@@ -18,8 +18,9 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ..ops.conv import PackedConv, conv2d_nhwc, fold_bn, pack_conv
-from ..ops.pool import global_avgpool_nhwc, maxpool2d_nhwc, preprocess_u8
+from ..ops.conv import PackedConv, conv2d_nhwc, fold_bn, pack_conv, pack_stem_s2d
+from ..ops.pool import (global_avgpool_nhwc, maxpool2d_nhwc, preprocess_s2d_u8, preprocess_u8,
+                        space_to_depth_shifted)
 
 
 class Bottleneck(nn.Module):
@@ -114,7 +115,9 @@ class FusedResNet:
         model = model.eval()
         self.device = torch.device(device)
         self.in_ch = in_ch or model.conv1.in_channels
-        self.stem = _fold(model.conv1, model.bn1, cin_pad=8).to(self.device)
+        w, b = fold_bn(model.conv1.weight.data.float(), model.bn1.weight.data.float(), model.bn1.bias.data.float(),
+                       model.bn1.running_mean.float(), model.bn1.running_var.float(), model.bn1.eps)
+        self.stem = pack_stem_s2d(w, b).to(self.device)  # 7x7/2 stem as a 4x4/1 conv on space-to-depth input
         self.blocks: List[Tuple[PackedConv, PackedConv, PackedConv, Optional[PackedConv]]] = []
         for layer in (model.layer1, model.layer2, model.layer3, model.layer4):
             for blk in layer:
@@ -136,8 +139,8 @@ class FusedResNet:
     def flops(self, n: int, h: int = 224, w: int = 224) -> int:
         from ..ops.conv import conv_flops
 
-        total = conv_flops(self.stem, n, h, w)
-        h, w = self.stem.out_hw(h, w)
+        total = 2 * n * (h // 2) * (w // 2) * 64 * 7 * 7 * self.in_ch  # true 7x7/2 stem FLOPs
+        h, w = h // 2, w // 2
         h, w = (h + 1) // 2, (w + 1) // 2
         for c1, c2, c3, d in self.blocks:
             total += conv_flops(c1, n, h, w) + conv_flops(c2, n, h, w)
@@ -148,9 +151,15 @@ class FusedResNet:
             h, w = h2, w2
         return total + conv_flops(self.fc, n, 1, 1)
 
+    def stem_input(self, x: torch.Tensor) -> torch.Tensor:
+        """Normalized NHWC input -> the s2d stem's [N,H/2,W/2,16] layout (no-op if already s2d)."""
+        if x.shape[-1] == 16:
+            return x
+        return space_to_depth_shifted(x[..., : self.in_ch])
+
     def forward_features(self, x: torch.Tensor) -> torch.Tensor:
-        """x: NHWC [N,H,W,8] normalized (bf16 on GPU) -> [N,h,w,2048]."""
-        x = conv2d_nhwc(x, self.stem, relu=True)
+        """x: normalized NHWC [N,H,W,8] (or already space-to-depth [N,H/2,W/2,16]) -> [N,h,w,2048]."""
+        x = conv2d_nhwc(self.stem_input(x), self.stem, relu=True)
         x = maxpool2d_nhwc(x, 3, 2, 1)
         for c1, c2, c3, down in self.blocks:
             idt = x if down is None else conv2d_nhwc(x, down)
@@ -165,6 +174,6 @@ class FusedResNet:
 
     def forward_u8(self, img_u8: torch.Tensor) -> torch.Tensor:
         """uint8 NHWC images -> fp32 logits (preprocess fused into the first kernel launch)."""
-        return self.forward(preprocess_u8(img_u8))
+        return self.forward(preprocess_s2d_u8(img_u8))
 
     __call__ = forward_u8

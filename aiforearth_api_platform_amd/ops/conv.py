@@ -41,6 +41,7 @@ class PackedConv:
     kw: int
     stride: int
     pad: int
+    pad_hi: Optional[int] = None   # bottom/right padding when it differs from the top/left `pad`
 
     @property
     def kpad(self) -> int:
@@ -48,10 +49,11 @@ class PackedConv:
 
     def to(self, device) -> "PackedConv":
         return PackedConv(self.w_ref.to(device), self.b_ref.to(device), self.w_packed.to(device), self.bias.to(device),
-                          self.cin, self.cin_pad, self.cout, self.kh, self.kw, self.stride, self.pad)
+                          self.cin, self.cin_pad, self.cout, self.kh, self.kw, self.stride, self.pad, self.pad_hi)
 
     def out_hw(self, h: int, w: int):
-        return ((h + 2 * self.pad - self.kh) // self.stride + 1, (w + 2 * self.pad - self.kw) // self.stride + 1)
+        hi = self.pad if self.pad_hi is None else self.pad_hi
+        return ((h + self.pad + hi - self.kh) // self.stride + 1, (w + self.pad + hi - self.kw) // self.stride + 1)
 
 
 def pack_conv(weight: torch.Tensor, bias: Optional[torch.Tensor], stride: int = 1, pad: int = 0,
@@ -128,13 +130,49 @@ def _conv_hip(x, pc, residual, relu, out, out_coff, tile_cfg):
 def _conv_torch(x, pc, residual, relu):
     cdt = torch.float32 if not x.is_cuda else x.dtype
     xin = x[..., :pc.cin].permute(0, 3, 1, 2).to(cdt)
-    y = F.conv2d(xin, pc.w_ref.to(x.device, cdt), pc.b_ref.to(x.device, cdt), stride=pc.stride, padding=pc.pad)
+    pad = pc.pad
+    if pc.pad_hi is not None and pc.pad_hi != pc.pad:
+        xin = F.pad(xin, (pc.pad, pc.pad_hi, pc.pad, pc.pad_hi))
+        pad = 0
+    y = F.conv2d(xin, pc.w_ref.to(x.device, cdt), pc.b_ref.to(x.device, cdt), stride=pc.stride, padding=pad)
     y = y.permute(0, 2, 3, 1)
     if residual is not None:
         y = y + residual.to(cdt)
     if relu:
         y = F.relu(y)
     return y
+
+
+def pack_stem_s2d(weight: torch.Tensor, bias: Optional[torch.Tensor]) -> PackedConv:
+    """7x7/2 pad-3 stem -> equivalent 4x4/1 conv on the 2x2 space-to-depth input.
+
+    With ``X'[i, j, (dy, dx, c)] = x[2i + dy - 1, 2j + dx - 1, c]`` (built by ``preprocess_s2d``),
+    ``conv7x7s2(x)[oh, ow] = sum_{a,b<4} W'[a, b] . X'[oh - 1 + a, ow - 1 + b]`` where
+    ``W'[a, b, dy, dx, c] = W[2a + dy, 2b + dx, c]`` (zero for taps beyond 6). The GEMM K drops from
+    49 taps x 8 padded channels (416) to 16 taps x 16 channels (256) and every tap is a contiguous
+    32-byte run, so the stem runs in 8 instead of 13 K-steps.
+    """
+    weight = weight.detach().float().cpu()
+    cout, cin, kh, kw = weight.shape
+    if (kh, kw) != (7, 7) or cin * 4 > 16:
+        raise ValueError("s2d stem expects a 7x7 kernel with <= 4 input channels")
+    w = torch.zeros(cout, 4, 4, 2, 2, cin)  # [cout, a, b, dy, dx, c]
+    wt = weight.permute(0, 2, 3, 1)          # [cout, kh, kw, c]
+    for a in range(4):
+        for dy in range(2):
+            r = 2 * a + dy
+            if r > 6:
+                continue
+            for b in range(4):
+                for dx in range(2):
+                    q = 2 * b + dx
+                    if q <= 6:
+                        w[:, a, b, dy, dx] = wt[:, r, q]
+    w16 = torch.zeros(cout, 4, 4, 16)
+    w16[..., : 4 * cin] = w.reshape(cout, 4, 4, 4 * cin)
+    pc = pack_conv(w16.permute(0, 3, 1, 2).contiguous(), bias, stride=1, pad=1, cin_pad=16)
+    pc.pad_hi = 2
+    return pc
 
 
 def conv_flops(pc: PackedConv, n: int, h: int, w: int) -> int:

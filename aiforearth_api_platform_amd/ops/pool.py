@@ -35,6 +35,35 @@ def preprocess_u8(img: torch.Tensor, mean: Sequence[float] = IMAGENET_MEAN, std:
     return out
 
 
+def preprocess_s2d_u8(img: torch.Tensor, mean: Sequence[float] = IMAGENET_MEAN, std: Sequence[float] = IMAGENET_STD,
+                      scale: float = 1.0 / 255.0) -> torch.Tensor:
+    """uint8 NHWC [N,H,W,cin<=4] -> normalized, 2x2 space-to-depth bf16 [N,H/2,W/2,16] for the s2d stem:
+    ``out[i, j, (dy*2+dx)*cin + c] = norm(x[2i+dy-1, 2j+dx-1, c])`` (zero outside the image)."""
+    n, h, w, cin = img.shape
+    if img.dtype != torch.uint8 or cin > 4 or h % 2 or w % 2:
+        raise ValueError("s2d preprocess expects uint8 NHWC, <= 4 channels, even H and W")
+    m4 = list(mean) + [0.0] * (4 - len(mean))
+    s4 = list(std) + [1.0] * (4 - len(std))
+    if _ext.backend_for(img) == "hip":
+        out = torch.empty(n, h // 2, w // 2, 16, device=img.device, dtype=torch.bfloat16)
+        ma, sa = ctypes_floats(m4), ctypes_floats(s4)
+        _ext.call("ai4e_preprocess_s2d_u8", img.data_ptr(), out.data_ptr(), n, h, w, cin, ctypes.addressof(ma),
+                  ctypes.addressof(sa), scale, _ext.stream_ptr(img.device))
+        return out
+    x = (img.float() * scale - torch.tensor(m4[:cin])) / torch.tensor(s4[:cin])
+    return space_to_depth_shifted(x)
+
+
+def space_to_depth_shifted(x: torch.Tensor) -> torch.Tensor:
+    """Normalized NHWC [N,H,W,C<=4] -> [N,H/2,W/2,16] with the -1 pixel shift of the s2d stem."""
+    n, h, w, c = x.shape
+    xp = torch.nn.functional.pad(x, (0, 0, 1, 1, 1, 1))[:, : h, : w]   # xp[y, x] = x[y-1, x-1]
+    blocks = xp.reshape(n, h // 2, 2, w // 2, 2, c).permute(0, 1, 3, 2, 4, 5).reshape(n, h // 2, w // 2, 4 * c)
+    out = torch.zeros(n, h // 2, w // 2, 16, dtype=x.dtype, device=x.device)
+    out[..., : 4 * c] = blocks
+    return out
+
+
 def ctypes_floats(vals):
     return (ctypes.c_float * len(vals))(*vals)
 

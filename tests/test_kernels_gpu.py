@@ -134,3 +134,13 @@ def test_engine_graph_replay_matches_eager():
     p, i = torch.topk(torch.softmax(logits.float(), 1), 5, 1)
     assert torch.equal(i_g[:, 0], i[:, 0].int().cpu())
     assert torch.allclose(p_g, p.cpu(), atol=1e-3)
+
+
+def test_preprocess_s2d_matches_torch():
+    from aiforearth_api_platform_amd.ops.pool import preprocess_s2d_u8, space_to_depth_shifted, IMAGENET_MEAN, IMAGENET_STD
+    img = torch.randint(0, 256, (2, 36, 44, 3), dtype=torch.uint8)
+    y = preprocess_s2d_u8(img.to(DEV)).float().cpu()
+    x = (img.float() / 255 - torch.tensor(IMAGENET_MEAN)) / torch.tensor(IMAGENET_STD)
+    ref = space_to_depth_shifted(x)
+    assert y.shape == (2, 18, 22, 16)
+    assert (y - ref).abs().max().item() < 0.02
