@@ -128,6 +128,30 @@ class ControlPlane:
         v = self.store.get_counter(current_requests_key(service_cluster, api_path))
         return (200, v) if v is not None else (204, None)
 
+    # ------------------------------------------------------------------ restart recovery
+    def recover(self, journal_path: Optional[str] = None) -> Dict[str, int]:
+        """Replay a task journal and re-enqueue unfinished work (survey §5.4).
+
+        Tasks that were ``created`` or ``running`` when the process died are re-published to their
+        endpoint queue with their original body (``{TaskId}_ORIG``), like a Service Bus redelivery;
+        finished tasks stay queryable. Returns counts.
+        """
+        path = journal_path or self.cfg.journal_path
+        n = self.store.replay(path) if path else 0
+        requeued = 0
+        for suffix in ("_created", "_running"):
+            for key in self.store.keys_with_suffix(suffix):
+                for tid in self.store.zrange(key):
+                    rec = self.store.get_record(tid)
+                    if rec is None or not rec["PublishToGrid"]:
+                        continue
+                    body = self.store.get_orig_body(tid) or ""
+                    self.store.upsert(tid, "created - requeued after restart", STATE_CREATED, rec["Endpoint"],
+                                      None, True)
+                    if self.queue_for(rec["Endpoint"]).send(tid, -1, body):
+                        requeued += 1
+        return {"replayed": n, "requeued": requeued}
+
     # ------------------------------------------------------------------ queue-depth metrics
     def log_queue_lengths(self, suffix: str, adjust: int = 0) -> Dict[str, int]:
         """QueueLogger.LogSetCount: KEYS *suffix -> ZCARD (+adjust) -> metric."""

@@ -112,6 +112,8 @@ def main(argv=None) -> int:
                       transport=args.transport)
     set_config(cfg)
     cp, gw, endpoints, dispatchers = build_platform(doc, cfg)
+    if cfg.journal_path and os.path.exists(cfg.journal_path):
+        print(f"recovered from journal: {cp.recover(cfg.journal_path)}", file=sys.stderr, flush=True)
     for ep in endpoints.values():
         ep.start()
     for d in dispatchers:

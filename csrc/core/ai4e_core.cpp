@@ -580,14 +580,14 @@ class DispatchQueue {
       double wake = deadline;
       if (!scheduled_.empty()) wake = std::min(wake, scheduled_.top().visible_at);
       if (!inflight_.empty()) wake = std::min(wake, now + 0.05);
-      cv_.wait_for(lk, std::chrono::duration<double>(std::max(0.0, wake - now)));
+      wait_s(lk, wake - now);
     }
     if (linger_s > 0 && ready_.size() < max_n && !closed_) {
       const double ldl = mono_now() + linger_s;
       while (ready_.size() < max_n && !closed_) {
         double now = mono_now();
         if (now >= ldl) break;
-        cv_.wait_for(lk, std::chrono::duration<double>(ldl - now));
+        wait_s(lk, ldl - now);
         promote_locked(mono_now());
       }
     }
@@ -689,6 +689,15 @@ class DispatchQueue {
         requeue_locked(std::move(m), 0);
       }
     }
+  }
+
+  // Timed wait on the system clock: pthread_cond_timedwait (the steady-clock overload maps to
+  // pthread_cond_clockwait, which ThreadSanitizer in this toolchain does not intercept and then
+  // reports as a double lock — tools/tsan_check.sh keeps this core race-clean).
+  void wait_s(std::unique_lock<std::mutex>& lk, double seconds) {
+    cv_.wait_until(lk, std::chrono::system_clock::now() +
+                           std::chrono::duration_cast<std::chrono::system_clock::duration>(
+                               std::chrono::duration<double>(std::max(0.0, seconds))));
   }
 
   std::string name_;

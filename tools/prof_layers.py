@@ -17,7 +17,7 @@ def main(path, batch=256, size=224):
     # replay shapes
     h = w = size
     shapes = []
-    h, w = m.stem.out_hw(h, w); shapes.append(("stem", m.stem, size, size)); h, w = (h + 1) // 2, (w + 1) // 2
+    h, w = m.stem.out_hw(h // 2, w // 2); shapes.append(("stem", m.stem, size // 2, size // 2)); h, w = (h + 1) // 2, (w + 1) // 2
     for bi, (c1, c2, c3, d) in enumerate(m.blocks):
         if d is not None:
             shapes.append((f"b{bi}.down", d, h, w))
