@@ -86,9 +86,34 @@ def fold_bn(weight: torch.Tensor, bn_weight, bn_bias, running_mean, running_var,
     return w, b
 
 
+_TILES = None
+
+
+def tile_key(pc: PackedConv, n: int, h: int, w: int, residual: bool) -> str:
+    return f"{pc.kh}x{pc.kw}s{pc.stride}p{pc.pad}c{pc.cin_pad}k{pc.cout}n{n}h{h}w{w}r{int(residual)}"
+
+
+def tuned_tile(pc: PackedConv, n: int, h: int, w: int, residual: bool) -> int:
+    """Measured per-shape tile config (bench/conv_tune.py -> ops/conv_tiles.json); 0 = kernel default."""
+    global _TILES
+    if _TILES is None:
+        import json
+        import os
+
+        path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "conv_tiles.json")
+        try:
+            with open(path) as f:
+                _TILES = json.load(f)
+        except (OSError, ValueError):
+            _TILES = {}
+    return int(_TILES.get(tile_key(pc, n, h, w, residual), 0))
+
+
 def conv2d_nhwc(x: torch.Tensor, pc: PackedConv, residual: Optional[torch.Tensor] = None, relu: bool = False,
-                out: Optional[torch.Tensor] = None, out_coff: int = 0, tile_cfg: int = 0) -> torch.Tensor:
+                out: Optional[torch.Tensor] = None, out_coff: int = 0, tile_cfg: int = -1) -> torch.Tensor:
     n, h, w, c = x.shape
+    if tile_cfg < 0:
+        tile_cfg = tuned_tile(pc, n, h, w, residual is not None)
     if c != pc.cin_pad:
         raise ValueError(f"conv expects C={pc.cin_pad} (padded), got {c}")
     oh, ow = pc.out_hw(h, w)

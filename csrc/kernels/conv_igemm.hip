@@ -51,6 +51,7 @@ struct ConvParams {
   int relu;
   int M;
   int ntiles_n;
+  const uint16_t* zero;  // >= 16 zero bytes: source of the DMA gather for padding taps
 };
 
 __device__ __forceinline__ int swz(int row) { return (0x78 >> (2 * ((row >> 2) & 3))) & 3; }
@@ -76,7 +77,7 @@ __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int WAVES_M, int WAVES_N, int STAGES>
+template <int WAVES_M, int WAVES_N, int STAGES, bool POINTWISE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) void conv_igemm_kernel(const ConvParams p) {
   static_assert(WAVES_M * WAVES_N == 4, "4 waves per workgroup");
   constexpr int BM = WAVES_M * 64;  // pixels per workgroup
@@ -120,6 +121,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
   const int OHW = p.OH * p.OW;
   int ih0[CA], iw0[CA];
   long xbase[CA];
+  const uint16_t* rowp[CA];  // POINTWISE: the pixel's channel row, nullptr past M
 #pragma unroll
   for (int i = 0; i < CA; ++i) {
     const int m = m0 + 16 * (wave + 4 * i) + rin;
@@ -131,10 +133,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
       ih0[i] = oh * p.stride - p.pad;
       iw0[i] = ow * p.stride - p.pad;
       xbase[i] = static_cast<long>(img) * p.H * p.W * p.ldx + p.xcoff;
+      rowp[i] = p.x + xbase[i] + (static_cast<long>(ih0[i]) * p.W + iw0[i]) * p.ldx;
     } else {
-      ih0[i] = -(1 << 28);  // fails the bounds check -> zero page
+      ih0[i] = -(1 << 28);  // fails the bounds check -> zero chunk
       iw0[i] = 0;
       xbase[i] = 0;
+      rowp[i] = nullptr;
     }
   }
   int cc, kh, kw;
@@ -148,26 +152,39 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
   const uint16_t* const wsrc = p.w + static_cast<long>(n0 + 16 * wave + rin) * p.Kpad + 8 * c;
   const long wstep = 64L * p.Kpad;  // rows 16*(wave+4i)
   const uint32_t smem_base = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(smem));
+  const uint16_t* const zero = p.zero;
 
   auto issue_stage = [&](int kt) {
     const uint32_t sbase = smem_base + (kt % STAGES) * STAGE_ELEMS * 2;
+    if constexpr (POINTWISE) {
+      // 1x1, pad 0: K is the channel axis of one input pixel -> pointer + offset, no gather math
+      const int k = kt * BK + 8 * c;
 #pragma unroll
-    for (int i = 0; i < CA; ++i) {
-      const int ih = ih0[i] + kh, iw = iw0[i] + kw;
-      const void* src = g_zero_chunk;
-      if (kh < p.KH && static_cast<unsigned>(ih) < static_cast<unsigned>(p.H) &&
-          static_cast<unsigned>(iw) < static_cast<unsigned>(p.W))
-        src = p.x + xbase[i] + (static_cast<long>(ih) * p.W + iw) * p.ldx + cc;
-      glds16(src, sbase + (16 * (wave + 4 * i)) * BK * 2);
+      for (int i = 0; i < CA; ++i) {
+        const void* src = (rowp[i] != nullptr && k < p.C) ? static_cast<const void*>(rowp[i] + k) : zero;
+        glds16(src, sbase + (16 * (wave + 4 * i)) * BK * 2);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < CA; ++i) {
+        const int ih = ih0[i] + kh, iw = iw0[i] + kw;
+        const void* src = zero;
+        if (kh < p.KH && static_cast<unsigned>(ih) < static_cast<unsigned>(p.H) &&
+            static_cast<unsigned>(iw) < static_cast<unsigned>(p.W))
+          src = p.x + xbase[i] + (static_cast<long>(ih) * p.W + iw) * p.ldx + cc;
+        glds16(src, sbase + (16 * (wave + 4 * i)) * BK * 2);
+      }
     }
 #pragma unroll
     for (int i = 0; i < CB; ++i) glds16(wsrc + i * wstep + kt * BK, sbase + (BM + 16 * (wave + 4 * i)) * BK * 2);
-    cc += BK;
-    while (cc >= p.C) {
-      cc -= p.C;
-      if (++kw == p.KW) {
-        kw = 0;
-        ++kh;
+    if constexpr (!POINTWISE) {
+      cc += BK;
+      while (cc >= p.C) {
+        cc -= p.C;
+        if (++kw == p.KW) {
+          kw = 0;
+          ++kh;
+        }
       }
     }
   };
@@ -249,6 +266,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
 
 namespace {
 
+const uint16_t* zero_chunk_ptr() {
+  static const uint16_t* ptr = nullptr;
+  if (!ptr) {
+    void* a = nullptr;
+    if (hipGetSymbolAddress(&a, HIP_SYMBOL(g_zero_chunk)) == hipSuccess) ptr = static_cast<const uint16_t*>(a);
+  }
+  return ptr;
+}
+
 template <int WM, int WN>
 int launch(const ConvParams& p0, hipStream_t s) {
   constexpr int STAGES = 4;
@@ -256,7 +282,12 @@ int launch(const ConvParams& p0, hipStream_t s) {
   const int mt = ai4e_cdiv(p.M, WM * 64);
   p.ntiles_n = ai4e_cdiv(p.Kout, WN * 64);
   const int nb = mt * p.ntiles_n;
-  hipLaunchKernelGGL((conv_igemm_kernel<WM, WN, STAGES>), dim3(nb), dim3(256), 0, s, p);
+  p.zero = zero_chunk_ptr();
+  if (!p.zero) return AI4E_ELAUNCH;
+  if (p.KH == 1 && p.KW == 1 && p.pad == 0)
+    hipLaunchKernelGGL((conv_igemm_kernel<WM, WN, STAGES, true>), dim3(nb), dim3(256), 0, s, p);
+  else
+    hipLaunchKernelGGL((conv_igemm_kernel<WM, WN, STAGES, false>), dim3(nb), dim3(256), 0, s, p);
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
 }
 
