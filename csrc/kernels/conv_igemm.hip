@@ -77,7 +77,7 @@ __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int WAVES_M, int WAVES_N, int STAGES, bool POINTWISE>
+template <int WAVES_M, int WAVES_N, int STAGES, bool POINTWISE, bool EPI_LDS>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) void conv_igemm_kernel(const ConvParams p) {
   static_assert(WAVES_M * WAVES_N == 4, "4 waves per workgroup");
   constexpr int BM = WAVES_M * 64;  // pixels per workgroup
@@ -103,15 +103,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
   // ---- residual prefetch (issued first: the first stage wait also retires it)
   const int pm = m0 + wm * 64 + (lane & 15);
   const int pn = n0 + wn * 64 + 4 * (lane >> 4);
+  // EPI_LDS layout: thread handles 16-B output chunks g = tid + 256*e of the row-major tile
+  constexpr int CPR = BN / 8;                 // 16-B chunks per tile row
+  constexpr int EPI_CHUNKS = BM * CPR / 256;  // chunks per thread
   uint2 rres[4][4];
-  if (p.res) {  // unconditional loads (clamped rows/cols) so hipcc keeps one counted wait for all 16
+  uint4 rres16[EPI_CHUNKS];
+  if (p.res) {  // unconditional loads (clamped rows/cols) so hipcc keeps one counted wait for all
+    if constexpr (EPI_LDS) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int m = min(pm + 16 * i, p.M - 1), n = min(pn + 16 * j, p.Kout - 4);
-        rres[i][j] = *reinterpret_cast<const uint2*>(p.res + static_cast<long>(m) * p.ldres + n);
+      for (int e = 0; e < EPI_CHUNKS; ++e) {
+        const int g = tid + 256 * e;
+        const int m = min(m0 + g / CPR, p.M - 1), n = min(n0 + 8 * (g % CPR), p.Kout - 8);
+        rres16[e] = *reinterpret_cast<const uint4*>(p.res + static_cast<long>(m) * p.ldres + n);
       }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int m = min(pm + 16 * i, p.M - 1), n = min(pn + 16 * j, p.Kout - 4);
+          rres[i][j] = *reinterpret_cast<const uint2*>(p.res + static_cast<long>(m) * p.ldres + n);
+        }
+    }
   }
 
   // ---- DMA lane mapping: lane writes LDS slot 16*lane of a 16-row x 64-B block, i.e. row lane>>2,
@@ -226,8 +239,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
   }
 
   // ---- fused epilogue: lane holds channels n..n+3 of pixel m for each (i, j) fragment.
-  // Phase 1 (no stores): bias + residual into the accumulators, so the residual registers are
-  // consumed behind ONE wait; phase 2: ReLU, pack, 8-B stores.
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const float4 b = *reinterpret_cast<const float4*>(p.bias + min(pn + 16 * j, p.Kout - 4));
@@ -236,28 +247,78 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
       acc[i][j][0] += b.x; acc[i][j][1] += b.y; acc[i][j][2] += b.z; acc[i][j][3] += b.w;
     }
   }
-  if (p.res) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        float a0, a1, a2, a3;
-        unpack_bf16x2(rres[i][j].x, a0, a1);
-        unpack_bf16x2(rres[i][j].y, a2, a3);
-        acc[i][j][0] += a0; acc[i][j][1] += a1; acc[i][j][2] += a2; acc[i][j][3] += a3;
-      }
-  }
   const float lo = p.relu ? 0.f : -INFINITY;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int n = pn + 16 * j;
+  if constexpr (EPI_LDS) {
+    // Stage the fp32 tile through LDS (the now idle stage ring: BM*BN*4 bytes) so every lane
+    // reads/writes 16 contiguous bytes: a wave instruction then covers whole 256-B+ pixel rows,
+    // halving store instructions and giving the residual read the same full-line shape.
+    // Row-major [BM][BN] fp32 with the 16-B chunk index XOR-swizzled by (row & 7): the 8-lane
+    // ds_write_b128 groups (8 rows, one column) hit 8 different bank quads.
+    static_assert(BM * BN * 4 <= STAGES * STAGE_ELEMS * 2, "epilogue tile must fit the stage ring");
+    float* tile = reinterpret_cast<float*>(smem);
+    __builtin_amdgcn_s_barrier();  // all waves finished reading the last stage
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int m = pm + 16 * i;
-      if (m < p.M && n < p.Kout)
-        *reinterpret_cast<uint2*>(p.y + static_cast<long>(m) * p.ldy + p.ycoff + n) =
-            make_uint2(pack_bf16x2(fmaxf(acc[i][j][0], lo), fmaxf(acc[i][j][1], lo)),
-                       pack_bf16x2(fmaxf(acc[i][j][2], lo), fmaxf(acc[i][j][3], lo)));
+      const int r = wm * 64 + 16 * i + (lane & 15);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int q = (wn * 64 + 16 * j + 4 * (lane >> 4)) >> 2;  // fp32 16-B chunk in the row
+        *reinterpret_cast<f32x4_t*>(tile + r * BN + 4 * (q ^ (r & 7))) = acc[i][j];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < EPI_CHUNKS; ++e) {
+      const int g = tid + 256 * e;
+      const int r = g / CPR, cq = g % CPR;
+      const int m = m0 + r, n = n0 + 8 * cq;
+      const float4 v0 = *reinterpret_cast<const float4*>(tile + r * BN + 4 * ((2 * cq) ^ (r & 7)));
+      const float4 v1 = *reinterpret_cast<const float4*>(tile + r * BN + 4 * ((2 * cq + 1) ^ (r & 7)));
+      float f[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+      if (p.res) {
+        float a[8];
+        unpack_bf16x2(rres16[e].x, a[0], a[1]);
+        unpack_bf16x2(rres16[e].y, a[2], a[3]);
+        unpack_bf16x2(rres16[e].z, a[4], a[5]);
+        unpack_bf16x2(rres16[e].w, a[6], a[7]);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) f[k] += a[k];
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) f[k] = fmaxf(f[k], lo);
+      if (m < p.M && n < p.Kout) {
+        uint16_t* dst = p.y + static_cast<long>(m) * p.ldy + p.ycoff + n;
+        const uint2 lo4 = make_uint2(pack_bf16x2(f[0], f[1]), pack_bf16x2(f[2], f[3]));
+        if (n + 8 <= p.Kout) {
+          *reinterpret_cast<uint4*>(dst) = make_uint4(lo4.x, lo4.y, pack_bf16x2(f[4], f[5]), pack_bf16x2(f[6], f[7]));
+        } else {
+          *reinterpret_cast<uint2*>(dst) = lo4;  // Kout % 8 == 4 tail
+        }
+      }
+    }
+  } else {
+    if (p.res) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float a0, a1, a2, a3;
+          unpack_bf16x2(rres[i][j].x, a0, a1);
+          unpack_bf16x2(rres[i][j].y, a2, a3);
+          acc[i][j][0] += a0; acc[i][j][1] += a1; acc[i][j][2] += a2; acc[i][j][3] += a3;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = pn + 16 * j;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = pm + 16 * i;
+        if (m < p.M && n < p.Kout)
+          *reinterpret_cast<uint2*>(p.y + static_cast<long>(m) * p.ldy + p.ycoff + n) =
+              make_uint2(pack_bf16x2(fmaxf(acc[i][j][0], lo), fmaxf(acc[i][j][1], lo)),
+                         pack_bf16x2(fmaxf(acc[i][j][2], lo), fmaxf(acc[i][j][3], lo)));
+      }
     }
   }
 }
@@ -284,10 +345,17 @@ int launch(const ConvParams& p0, hipStream_t s) {
   const int nb = mt * p.ntiles_n;
   p.zero = zero_chunk_ptr();
   if (!p.zero) return AI4E_ELAUNCH;
-  if (p.KH == 1 && p.KW == 1 && p.pad == 0)
-    hipLaunchKernelGGL((conv_igemm_kernel<WM, WN, STAGES, true>), dim3(nb), dim3(256), 0, s, p);
+  const bool pw = p.KH == 1 && p.KW == 1 && p.pad == 0;
+  // coalesced LDS epilogue needs 16-B aligned output/residual rows
+  const bool epi = !(p.ldy % 8 || p.ycoff % 8 || (p.res && p.ldres % 8) || p.Kout < 8);
+  if (pw && epi)
+    hipLaunchKernelGGL((conv_igemm_kernel<WM, WN, STAGES, true, true>), dim3(nb), dim3(256), 0, s, p);
+  else if (pw)
+    hipLaunchKernelGGL((conv_igemm_kernel<WM, WN, STAGES, true, false>), dim3(nb), dim3(256), 0, s, p);
+  else if (epi)
+    hipLaunchKernelGGL((conv_igemm_kernel<WM, WN, STAGES, false, true>), dim3(nb), dim3(256), 0, s, p);
   else
-    hipLaunchKernelGGL((conv_igemm_kernel<WM, WN, STAGES, false>), dim3(nb), dim3(256), 0, s, p);
+    hipLaunchKernelGGL((conv_igemm_kernel<WM, WN, STAGES, false, false>), dim3(nb), dim3(256), 0, s, p);
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
 }
 
