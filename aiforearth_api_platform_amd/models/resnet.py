@@ -12,6 +12,7 @@ Two forms:
 """
 from __future__ import annotations
 
+import os
 from typing import List, Optional, Tuple
 
 import torch
@@ -108,10 +109,25 @@ def _fold(conv: nn.Conv2d, bn: nn.BatchNorm2d, cin_pad: Optional[int] = None) ->
     return pack_conv(w, b, stride=conv.stride[0], pad=conv.padding[0], cin_pad=cin_pad)
 
 
+def _env_chunk() -> Optional[Tuple[int, int]]:
+    """``AI4E_RESNET_CHUNK=mb:nblocks`` (``0`` / ``off`` disables); default from ``DEFAULT_CHUNK``."""
+    v = os.environ.get("AI4E_RESNET_CHUNK")
+    if v is None:
+        return DEFAULT_CHUNK
+    if v in ("", "0", "off"):
+        return None
+    mb, nb = v.split(":")
+    return int(mb), int(nb)
+
+
+DEFAULT_CHUNK: Optional[Tuple[int, int]] = None
+
+
 class FusedResNet:
     """Inference graph over packed, BN-folded layers (NHWC bf16)."""
 
-    def __init__(self, model: ResNet, device="cpu", in_ch: Optional[int] = None):
+    def __init__(self, model: ResNet, device="cpu", in_ch: Optional[int] = None,
+                 chunk: Optional[Tuple[int, int]] = None):
         model = model.eval()
         self.device = torch.device(device)
         self.in_ch = in_ch or model.conv1.in_channels
@@ -129,6 +145,7 @@ class FusedResNet:
         fcw = model.fc.weight.data.float().reshape(model.fc.out_features, -1, 1, 1)
         self.fc = pack_conv(fcw, model.fc.bias.data.float()).to(self.device)
         self.num_classes = model.fc.out_features
+        self.chunk = chunk if chunk is not None else _env_chunk()
 
     def layers(self) -> List[PackedConv]:
         out = [self.stem]
@@ -157,23 +174,61 @@ class FusedResNet:
             return x
         return space_to_depth_shifted(x[..., : self.in_ch])
 
-    def forward_features(self, x: torch.Tensor) -> torch.Tensor:
-        """x: normalized NHWC [N,H,W,8] (or already space-to-depth [N,H/2,W/2,16]) -> [N,h,w,2048]."""
-        x = conv2d_nhwc(self.stem_input(x), self.stem, relu=True)
-        x = maxpool2d_nhwc(x, 3, 2, 1)
-        for c1, c2, c3, down in self.blocks:
-            idt = x if down is None else conv2d_nhwc(x, down)
-            y = conv2d_nhwc(x, c1, relu=True)
-            y = conv2d_nhwc(y, c2, relu=True)
-            x = conv2d_nhwc(y, c3, residual=idt, relu=True)
-        return x
+    def _stem(self, x: torch.Tensor) -> torch.Tensor:
+        return maxpool2d_nhwc(conv2d_nhwc(self.stem_input(x), self.stem, relu=True), 3, 2, 1)
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
-        f = global_avgpool_nhwc(self.forward_features(x))
+    @staticmethod
+    def _block(x: torch.Tensor, blk, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        c1, c2, c3, down = blk
+        idt = x if down is None else conv2d_nhwc(x, down)
+        y = conv2d_nhwc(x, c1, relu=True)
+        y = conv2d_nhwc(y, c2, relu=True)
+        return conv2d_nhwc(y, c3, residual=idt, relu=True, out=out)
+
+    def _prefix_shape(self, n: int, h: int, w: int, nblocks: int) -> Tuple[int, int, int, int]:
+        """Output shape after the stem, max-pool and the first ``nblocks`` bottlenecks."""
+        h, w = (h - 1) // 2 + 1, (w - 1) // 2 + 1  # maxpool 3/2/1 on the (H/2, W/2) stem output
+        c = self.stem.cout
+        for c1, c2, c3, d in self.blocks[:nblocks]:
+            h, w = c2.out_hw(h, w)
+            c = c3.cout
+        return n, h, w, c
+
+    def forward_features(self, x: torch.Tensor, preprocess=None) -> torch.Tensor:
+        """x: normalized NHWC [N,H,W,8] (or space-to-depth [N,H/2,W/2,16]; or uint8 images when
+        ``preprocess`` is given) -> [N,h,w,2048].
+
+        Cache-resident micro-batching: at batch 256 a layer1 activation is 411 MB, so every conv of
+        the high-resolution stages streams its input, residual and output through HBM. With
+        ``chunk = (mb, nblocks)`` the stem and the first ``nblocks`` bottlenecks run ``mb`` images
+        at a time (a layer1 tensor of 32 images is 51 MB, so producer -> consumer traffic stays in
+        the 256 MB Infinity Cache) and write their output straight into the full-batch buffer; the
+        low-resolution stages then run on the whole batch, where they need it to fill 256 CUs.
+        """
+        n = x.shape[0]
+        mb, nblocks = self.chunk if self.chunk else (n, 0)
+        pre = preprocess or (lambda t: t)
+        if mb < n and nblocks > 0:
+            s2d = preprocess is None and x.shape[-1] == 16
+            h, w = (x.shape[1], x.shape[2]) if s2d else (x.shape[1] // 2, x.shape[2] // 2)  # stem output
+            feats = torch.empty(self._prefix_shape(n, h, w, nblocks), device=x.device, dtype=torch.bfloat16)
+            for n0 in range(0, n, mb):
+                y = self._stem(pre(x[n0:n0 + mb]))
+                for i in range(nblocks):
+                    y = self._block(y, self.blocks[i], out=feats[n0:n0 + mb] if i == nblocks - 1 else None)
+            y = feats
+        else:
+            y, nblocks = self._stem(pre(x)), 0
+        for blk in self.blocks[nblocks:]:
+            y = self._block(y, blk)
+        return y
+
+    def forward(self, x: torch.Tensor, preprocess=None) -> torch.Tensor:
+        f = global_avgpool_nhwc(self.forward_features(x, preprocess))
         return conv2d_nhwc(f, self.fc).reshape(f.shape[0], -1).float()
 
     def forward_u8(self, img_u8: torch.Tensor) -> torch.Tensor:
         """uint8 NHWC images -> fp32 logits (preprocess fused into the first kernel launch)."""
-        return self.forward(preprocess_s2d_u8(img_u8))
+        return self.forward(img_u8, preprocess=preprocess_s2d_u8)
 
     __call__ = forward_u8

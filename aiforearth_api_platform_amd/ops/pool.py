@@ -50,8 +50,9 @@ def preprocess_s2d_u8(img: torch.Tensor, mean: Sequence[float] = IMAGENET_MEAN, 
         _ext.call("ai4e_preprocess_s2d_u8", img.data_ptr(), out.data_ptr(), n, h, w, cin, ctypes.addressof(ma),
                   ctypes.addressof(sa), scale, _ext.stream_ptr(img.device))
         return out
-    x = (img.float() * scale - torch.tensor(m4[:cin])) / torch.tensor(s4[:cin])
-    return space_to_depth_shifted(x)
+    x = (img.float() * scale - torch.tensor(m4[:cin], device=img.device)) / torch.tensor(s4[:cin], device=img.device)
+    y = space_to_depth_shifted(x)
+    return y.to(torch.bfloat16) if img.is_cuda else y
 
 
 def space_to_depth_shifted(x: torch.Tensor) -> torch.Tensor:

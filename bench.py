@@ -44,6 +44,7 @@ def parse():
     p.add_argument("--image-size", type=int, default=224)
     p.add_argument("--backend", default="auto", choices=["auto", "hip", "torch"])
     p.add_argument("--no-graphs", action="store_true")
+    p.add_argument("--chunk", default=None, help="ResNet micro-batching mb:nblocks for the high-res stages ('off' = none)")
     p.add_argument("--device", default="cuda")
     p.add_argument("--json-out", default="")
     return p.parse_args()
@@ -52,6 +53,8 @@ def parse():
 def main():
     args = parse()
     os.environ["AI4E_KERNEL_BACKEND"] = args.backend
+    if args.chunk is not None:
+        os.environ["AI4E_RESNET_CHUNK"] = args.chunk
     from aiforearth_api_platform_amd import _build
     from aiforearth_api_platform_amd.config import Config
     from aiforearth_api_platform_amd.gateway.control import ControlPlane
@@ -61,26 +64,14 @@ def main():
     from aiforearth_api_platform_amd.runtime.serving import GpuBatchWorker
     from aiforearth_api_platform_amd.utils.metrics import percentile
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    from aiforearth_api_platform_amd.parallel.dist import all_reduce_max, destroy, env_ranks, init_from_env, sync
+
+    _, world, _ = env_ranks()
     if world > 1 and args.gpus != world:
         raise SystemExit(f"--gpus {args.gpus} != WORLD_SIZE {world}")
-    if rank == 0:
-        _build.build_all()
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        backend = "nccl" if args.device == "cuda" else "gloo"
-        if args.device == "cuda":
-            torch.cuda.set_device(local)
-        dist.init_process_group(backend, rank=rank, world_size=world)
-        dist.barrier()  # rank 0 finished building before anyone loads the libraries
-    device = torch.device(f"cuda:{local}" if args.device == "cuda" else "cpu")
-    if device.type == "cuda":
-        torch.cuda.set_device(device)
+    # rank 0 builds the in-tree HIP/C++ libraries, then everyone joins (RCCL on GPU, gloo on CPU)
+    denv = init_from_env(args.device, build=_build.build_all)
+    rank, device = denv.rank, denv.device
 
     B, S = args.batch, args.image_size
     model = FusedResNet(resnet50(seed=0), device=device)
@@ -117,28 +108,22 @@ def main():
             time.sleep(0.0002)
         return all_ids
 
-    def sync():
-        if device.type == "cuda":
-            torch.cuda.synchronize(device)
-        if dist is not None:
-            dist.barrier()
+    def sync_all():
+        sync(denv)
 
     run(args.warmup)
     tune_gc()
-    sync()
+    sync_all()
     worker.phase_s.clear()
     worker.finalize_times.clear()
     t0 = time.perf_counter()
     ids = run(args.steps)
-    sync()
+    sync_all()
     dt = time.perf_counter() - t0
     worker.stop()
     lat = sorted(cp.store.latencies(ids))
     p50, p99 = percentile(lat, 50) * 1e3, percentile(lat, 99) * 1e3
-    stats = torch.tensor([dt, p50, p99], dtype=torch.float64, device=device if world > 1 and device.type == "cuda" else "cpu")
-    if dist is not None:
-        dist.all_reduce(stats, op=dist.ReduceOp.MAX)
-    dt, p50, p99 = [float(x) for x in stats.cpu()]
+    dt, p50, p99 = all_reduce_max([dt, p50, p99], denv)  # slowest rank defines the step time
     images = args.steps * B * world
     value = images / dt
     gflop_img = model.flops(1, S, S) / 1e9
@@ -151,7 +136,8 @@ def main():
         "tflops_effective": round(value * gflop_img / 1e3, 2),
         "config": {"model": "resnet50", "global_batch": B * world, "per_gpu_batch": B, "image_size": S,
                    "seq_len": None, "parallelism": f"dp{world}", "api": "async", "inflight_steps": args.inflight,
-                   "hip_graphs": not args.no_graphs, "kernel_backend": args.backend},
+                   "hip_graphs": not args.no_graphs, "kernel_backend": args.backend,
+                   "resnet_chunk": list(model.chunk) if model.chunk else None},
     }
     if os.environ.get("AI4E_BENCH_DEBUG"):
         import numpy as np
@@ -166,9 +152,8 @@ def main():
             with open(args.json_out, "w") as f:
                 f.write(line + "\n")
     cp.close()
-    if dist is not None:
-        dist.barrier()
-        dist.destroy_process_group()
+    sync(denv)
+    destroy(denv)
 
 
 if __name__ == "__main__":

@@ -1,0 +1,62 @@
+"""bench.py contract on CPU: one JSON line from rank 0, whole-job value, MAX-over-ranks timing.
+
+Runs the real serving path with a tiny shape on the CPU (gloo for world 2). The GPU numbers come
+from the same script on MI355X (profiles/).
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ARGS = ["--device", "cpu", "--batch", "2", "--image-size", "64", "--steps", "2", "--warmup", "1"]
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _json_lines(out):
+    return [json.loads(l) for l in out.splitlines() if l.startswith("{")]
+
+
+def _check(d, n):
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config"):
+        assert k in d, k
+    assert d["n_gpus"] == n and d["steps"] == 2 and d["warmup"] == 1
+    assert d["config"]["global_batch"] == 2 * n and d["config"]["parallelism"] == f"dp{n}"
+    assert d["value"] > 0 and d["higher_is_better"] is True and d["scaling"] == "weak"
+    # value is the whole-job aggregate derived from the (max-over-ranks) step time
+    assert abs(d["value"] - 2 * n * 1e3 / d["ms_per_step"]) / d["value"] < 0.01
+
+
+def _env():
+    env = dict(os.environ, AI4E_KERNEL_BACKEND="torch", MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="2")
+    env.pop("RANK", None)
+    env.pop("WORLD_SIZE", None)
+    return env
+
+
+def test_bench_single_process_cpu():
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "1"] + ARGS, cwd=ROOT, env=_env(),
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1
+    _check(lines[0], 1)
+
+
+def test_bench_torchrun_two_ranks_gloo():
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2"] + ARGS
+    r = subprocess.run(cmd, cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1, r.stdout  # rank 0 only
+    _check(lines[0], 2)

@@ -144,3 +144,13 @@ def test_preprocess_s2d_matches_torch():
     ref = space_to_depth_shifted(x)
     assert y.shape == (2, 18, 22, 16)
     assert (y - ref).abs().max().item() < 0.02
+
+
+def test_resnet_chunked_prefix_matches_full_batch_gpu():
+    from aiforearth_api_platform_amd.models.resnet import FusedResNet, resnet50
+    m = resnet50(seed=6)
+    img = torch.randint(0, 256, (12, 96, 96, 3), dtype=torch.uint8).to(DEV)
+    ref = FusedResNet(m, device=DEV, chunk=None).forward_u8(img)
+    for chunk in [(4, 3), (8, 7)]:
+        out = FusedResNet(m, device=DEV, chunk=chunk).forward_u8(img)
+        assert (out - ref).abs().max().item() < 2e-2, chunk

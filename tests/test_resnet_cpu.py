@@ -61,3 +61,14 @@ def test_flops_resnet50():
     fused = FusedResNet(resnet50())
     gf = fused.flops(1) / 1e9
     assert 8.0 < gf < 8.4  # ~4.1 GMAC / image
+
+
+def test_chunked_prefix_matches_full_batch():
+    """Cache-resident micro-batching of the high-resolution stages does not change the result."""
+    m = resnet50(seed=5)
+    img = torch.randint(0, 256, (6, 64, 64, 3), dtype=torch.uint8)
+    ref = FusedResNet(m, chunk=None).forward_u8(img)
+    for chunk in [(4, 3), (2, 7), (5, 16)]:
+        out = FusedResNet(m, chunk=chunk).forward_u8(img)
+        assert out.shape == ref.shape
+        assert (out - ref).abs().max().item() < 1e-2, chunk
