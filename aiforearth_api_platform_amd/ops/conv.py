@@ -19,7 +19,7 @@ import torch.nn.functional as F
 
 from . import _ext
 
-K_ALIGN = 32
+K_ALIGN = 64  # K steps of 32 come in pairs: the K1 main loop is unrolled by two
 ROW_ALIGN = 256
 C_ALIGN = 8
 

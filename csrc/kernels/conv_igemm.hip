@@ -13,8 +13,11 @@
 //   4 x 4 fragments of v_mfma_f32_16x16x32_bf16; workgroup tile = WAVES_M*64 x WAVES_N*64
 //   (128x128 for wide layers, 256x64 for Cout=64 layers).
 // * Operands are swapped (A = weights, B = activations) so each lane's accumulator holds 4
-//   consecutive output CHANNELS of one pixel: the epilogue stores 8 contiguous bytes per lane
-//   straight from registers (bias float4, residual 8-B loads) with no LDS round trip.
+//   consecutive output CHANNELS of one pixel. Epilogue (EPI_LDS, the default when the output and
+//   residual row strides are multiples of 8 channels): acc + bias is staged through the now idle
+//   LDS ring as an fp32 tile, then every thread reads back whole 16-B row chunks, adds the 16-B
+//   residual chunk, applies ReLU and writes 16 B — fully coalesced rows instead of 8-B fragments.
+//   The fallback (odd strides, Cout < 8) stores 8 B per lane straight from the accumulators.
 // * A/B tiles (BK = 32) stream global -> LDS by LDS-DMA (global_load_lds_dwordx4, no VGPR staging)
 //   into a 4-deep ring: 3 K-steps stay in flight across the one raw s_barrier per step, retired by a
 //   counted vmcnt (cdna guide §5 "Pipelining across barriers", T3/T4) — one K-step of MFMA work is
@@ -77,9 +80,15 @@ __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int WAVES_M, int WAVES_N, int STAGES, bool POINTWISE, bool EPI_LDS>
+// Gather modes of the activation operand.
+enum { GATHER_GENERAL = 0,  // any C % 8: a 32-wide K chunk may span taps -> per-lane tap walk
+       GATHER_POINTWISE = 1,  // 1x1, pad 0 (any stride): K is the channel axis of one input pixel
+       GATHER_TAP = 2 };      // C % 32 == 0: a K chunk lies in ONE tap -> the tap walk is wave-uniform (SGPRs)
+
+template <int WAVES_M, int WAVES_N, int STAGES, int GATHER, bool EPI_LDS>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) void conv_igemm_kernel(const ConvParams p) {
   static_assert(WAVES_M * WAVES_N == 4, "4 waves per workgroup");
+  static_assert(STAGES >= 3, "fragment prefetch needs >= 3 ring stages");
   constexpr int BM = WAVES_M * 64;  // pixels per workgroup
   constexpr int BN = WAVES_N * 64;  // channels per workgroup
   constexpr int CA = BM / 64;       // A (activation) DMA instructions per wave per stage
@@ -134,7 +143,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
   const int OHW = p.OH * p.OW;
   int ih0[CA], iw0[CA];
   long xbase[CA];
-  const uint16_t* rowp[CA];  // POINTWISE: the pixel's channel row, nullptr past M
+  const uint16_t* rowp[CA];  // the pixel's (ih0, iw0) channel row (+ the lane's 8-channel chunk for
+                             // GATHER_TAP), nullptr past M
 #pragma unroll
   for (int i = 0; i < CA; ++i) {
     const int m = m0 + 16 * (wave + 4 * i) + rin;
@@ -146,7 +156,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
       ih0[i] = oh * p.stride - p.pad;
       iw0[i] = ow * p.stride - p.pad;
       xbase[i] = static_cast<long>(img) * p.H * p.W * p.ldx + p.xcoff;
-      rowp[i] = p.x + xbase[i] + (static_cast<long>(ih0[i]) * p.W + iw0[i]) * p.ldx;
+      rowp[i] = p.x + xbase[i] + (static_cast<long>(ih0[i]) * p.W + iw0[i]) * p.ldx +
+                (GATHER == GATHER_TAP ? 8 * c : 0);
     } else {
       ih0[i] = -(1 << 28);  // fails the bounds check -> zero chunk
       iw0[i] = 0;
@@ -154,7 +165,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
       rowp[i] = nullptr;
     }
   }
-  int cc, kh, kw;
+  int cc, kh, kw;  // GATHER_GENERAL: per-lane tap walk
   {
     const int k = 8 * c;
     const int tap = k / p.C;
@@ -162,6 +173,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
     kh = tap / p.KW;
     kw = tap - kh * p.KW;
   }
+  int tkh = 0, tkw = 0, tcb = 0;  // GATHER_TAP: wave-uniform tap (kh, kw) and channel base
   const uint16_t* const wsrc = p.w + static_cast<long>(n0 + 16 * wave + rin) * p.Kpad + 8 * c;
   const long wstep = 64L * p.Kpad;  // rows 16*(wave+4i)
   const uint32_t smem_base = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(smem));
@@ -169,13 +181,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
 
   auto issue_stage = [&](int kt) {
     const uint32_t sbase = smem_base + (kt % STAGES) * STAGE_ELEMS * 2;
-    if constexpr (POINTWISE) {
-      // 1x1, pad 0: K is the channel axis of one input pixel -> pointer + offset, no gather math
+    if constexpr (GATHER == GATHER_POINTWISE) {
       const int k = kt * BK + 8 * c;
 #pragma unroll
       for (int i = 0; i < CA; ++i) {
         const void* src = (rowp[i] != nullptr && k < p.C) ? static_cast<const void*>(rowp[i] + k) : zero;
         glds16(src, sbase + (16 * (wave + 4 * i)) * BK * 2);
+      }
+    } else if constexpr (GATHER == GATHER_TAP) {
+      // one tap per K chunk: offset and the padding test's tap part are scalar; per lane only the
+      // two unsigned bounds compares and a pointer select remain
+      const long toff = (static_cast<long>(tkh) * p.W + tkw) * p.ldx + tcb;
+      const bool tap_ok = tkh < p.KH;
+#pragma unroll
+      for (int i = 0; i < CA; ++i) {
+        const bool ok = tap_ok && static_cast<unsigned>(ih0[i] + tkh) < static_cast<unsigned>(p.H) &&
+                        static_cast<unsigned>(iw0[i] + tkw) < static_cast<unsigned>(p.W);
+        glds16(ok ? static_cast<const void*>(rowp[i] + toff) : zero, sbase + (16 * (wave + 4 * i)) * BK * 2);
+      }
+      tcb += BK;
+      if (tcb == p.C) {
+        tcb = 0;
+        if (++tkw == p.KW) {
+          tkw = 0;
+          ++tkh;
+        }
       }
     } else {
 #pragma unroll
@@ -187,10 +217,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
           src = p.x + xbase[i] + (static_cast<long>(ih) * p.W + iw) * p.ldx + cc;
         glds16(src, sbase + (16 * (wave + 4 * i)) * BK * 2);
       }
-    }
-#pragma unroll
-    for (int i = 0; i < CB; ++i) glds16(wsrc + i * wstep + kt * BK, sbase + (BM + 16 * (wave + 4 * i)) * BK * 2);
-    if constexpr (!POINTWISE) {
       cc += BK;
       while (cc >= p.C) {
         cc -= p.C;
@@ -200,6 +226,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
         }
       }
     }
+#pragma unroll
+    for (int i = 0; i < CB; ++i) glds16(wsrc + i * wstep + kt * BK, sbase + (BM + 16 * (wave + 4 * i)) * BK * 2);
   };
 
   f32x4_t acc[4][4];
@@ -212,31 +240,59 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
   const int fofs = frow * BK + (((lane >> 4) ^ swz(frow)) << 3);
   const int nk = p.Kpad / BK;
 
+  // Wait until ring stage `kt` has landed for this wave: the stages issued after it (at most
+  // min(ahead, nk-1-kt) of them, PER_STAGE DMAs each) may stay in flight.
+  auto wait_stage = [&](int kt, int ahead) {
+    const int younger = min(ahead, nk - 1 - kt);
+    if (younger >= 3) wait_vmcnt<3 * PER_STAGE>();
+    else if (younger == 2) wait_vmcnt<2 * PER_STAGE>();
+    else if (younger == 1) wait_vmcnt<PER_STAGE>();
+    else wait_vmcnt<0>();
+  };
+
+  // Software pipeline, per K step kt (fragments of step kt already in registers):
+  //   wait stage kt+1 + barrier -> ds_read fragments of kt+1 (async) -> 16 MFMAs on step kt
+  //   (hide the LDS latency) -> DMA-issue stage kt+STAGES-1 into the slot of step kt-1, which every
+  //   wave finished reading before this step's barrier.
+  bf16x8_t fw0[4], fx0[4], fw1[4], fx1[4];
+#define K1_READ(FW, FX, KT)                                                                     \
+  {                                                                                             \
+    const uint16_t* st_ = smem + ((KT) % STAGES) * STAGE_ELEMS;                                 \
+    const uint16_t* x_ = st_ + (wm * 64) * BK + fofs;                                           \
+    const uint16_t* w_ = st_ + (BM + wn * 64) * BK + fofs;                                      \
+    _Pragma("unroll") for (int j = 0; j < 4; ++j) FW[j] = *reinterpret_cast<const bf16x8_t*>(w_ + j * 16 * BK); \
+    _Pragma("unroll") for (int i = 0; i < 4; ++i) FX[i] = *reinterpret_cast<const bf16x8_t*>(x_ + i * 16 * BK); \
+  }
+#define K1_STEP(KT, FWC, FXC, FWN, FXN)                                                         \
+  {                                                                                             \
+    const int kt_ = (KT);                                                                       \
+    if (kt_ + 1 < nk) {                                                                         \
+      wait_stage(kt_ + 1, STAGES - 3); /* issued so far: up to kt+STAGES-2 */                   \
+      __builtin_amdgcn_s_barrier();                                                             \
+      K1_READ(FWN, FXN, kt_ + 1)                                                                \
+    }                                                                                           \
+    _Pragma("unroll") for (int i = 0; i < 4; ++i)                                               \
+      _Pragma("unroll") for (int j = 0; j < 4; ++j)                                             \
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(FWC[j], FXC[i], acc[i][j], 0, 0, 0); \
+    if (kt_ + STAGES - 1 < nk) issue_stage(kt_ + STAGES - 1);                                   \
+  }
+
 #pragma unroll
   for (int s = 0; s < STAGES - 1; ++s)
     if (s < nk) issue_stage(s);
-
-  for (int kt = 0; kt < nk; ++kt) {
-    // stage kt has landed once at most (younger stages in flight) * PER_STAGE DMAs are outstanding
-    const int younger = min(STAGES - 2, nk - 1 - kt);
-    if (younger >= 2) wait_vmcnt<2 * PER_STAGE>();
-    else if (younger == 1) wait_vmcnt<PER_STAGE>();
-    else wait_vmcnt<0>();
-    __builtin_amdgcn_s_barrier();  // every wave's DMA for stage kt is in LDS; stage kt-1 fully read
-    if (kt + STAGES - 1 < nk) issue_stage(kt + STAGES - 1);
-    const uint16_t* st = smem + (kt % STAGES) * STAGE_ELEMS;
-    const uint16_t* x = st + (wm * 64) * BK + fofs;
-    const uint16_t* w = st + (BM + wn * 64) * BK + fofs;
-    bf16x8_t bw[4], bx[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) bw[j] = *reinterpret_cast<const bf16x8_t*>(w + j * 16 * BK);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) bx[i] = *reinterpret_cast<const bf16x8_t*>(x + i * 16 * BK);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[j], bx[i], acc[i][j], 0, 0, 0);
+  wait_stage(0, STAGES - 2);
+  __builtin_amdgcn_s_barrier();
+  K1_READ(fw0, fx0, 0)
+  // unrolled by two so the fragment buffers alternate without register copies; the MFMAs sit
+  // outside any branch (a conditional MFMA block makes hipcc shuttle the accumulators AGPR<->VGPR),
+  // hence K is padded to whole pairs of steps
+  // (nk is even: the host pads K to a multiple of 2*BK)
+  for (int kt = 0; kt < nk; kt += 2) {
+    K1_STEP(kt, fw0, fx0, fw1, fx1)
+    K1_STEP(kt + 1, fw1, fx1, fw0, fx0)
   }
+#undef K1_STEP
+#undef K1_READ
 
   // ---- fused epilogue: lane holds channels n..n+3 of pixel m for each (i, j) fragment.
 #pragma unroll
@@ -336,38 +392,42 @@ const uint16_t* zero_chunk_ptr() {
   return ptr;
 }
 
-template <int WM, int WN>
+template <int WM, int WN, int STAGES>
 int launch(const ConvParams& p0, hipStream_t s) {
-  constexpr int STAGES = 4;
   ConvParams p = p0;
   const int mt = ai4e_cdiv(p.M, WM * 64);
   p.ntiles_n = ai4e_cdiv(p.Kout, WN * 64);
   const int nb = mt * p.ntiles_n;
   p.zero = zero_chunk_ptr();
   if (!p.zero) return AI4E_ELAUNCH;
-  const bool pw = p.KH == 1 && p.KW == 1 && p.pad == 0;
+  const int g = (p.KH == 1 && p.KW == 1 && p.pad == 0) ? GATHER_POINTWISE
+                : (p.C % BK == 0)                          ? GATHER_TAP
+                                                           : GATHER_GENERAL;
   // coalesced LDS epilogue needs 16-B aligned output/residual rows
   const bool epi = !(p.ldy % 8 || p.ycoff % 8 || (p.res && p.ldres % 8) || p.Kout < 8);
-  if (pw && epi)
-    hipLaunchKernelGGL((conv_igemm_kernel<WM, WN, STAGES, true, true>), dim3(nb), dim3(256), 0, s, p);
-  else if (pw)
-    hipLaunchKernelGGL((conv_igemm_kernel<WM, WN, STAGES, true, false>), dim3(nb), dim3(256), 0, s, p);
-  else if (epi)
-    hipLaunchKernelGGL((conv_igemm_kernel<WM, WN, STAGES, false, true>), dim3(nb), dim3(256), 0, s, p);
-  else
-    hipLaunchKernelGGL((conv_igemm_kernel<WM, WN, STAGES, false, false>), dim3(nb), dim3(256), 0, s, p);
+#define K1_LAUNCH(G, E) \
+  hipLaunchKernelGGL((conv_igemm_kernel<WM, WN, STAGES, G, E>), dim3(nb), dim3(256), 0, s, p)
+  if (g == GATHER_POINTWISE) {
+    if (epi) K1_LAUNCH(GATHER_POINTWISE, true); else K1_LAUNCH(GATHER_POINTWISE, false);
+  } else if (g == GATHER_TAP) {
+    if (epi) K1_LAUNCH(GATHER_TAP, true); else K1_LAUNCH(GATHER_TAP, false);
+  } else {
+    if (epi) K1_LAUNCH(GATHER_GENERAL, true); else K1_LAUNCH(GATHER_GENERAL, false);
+  }
+#undef K1_LAUNCH
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
 }
 
 }  // namespace
 
-// tile_cfg (pixels x channels per workgroup): 0 = auto, 1 = 128x128 (2x2 waves), 2 = 256x64 (4x1),
-// 3 = 64x256 (1x4).
+// tile_cfg (pixels x channels per workgroup, LDS ring depth): 0 = auto, 1 = 128x128 (2x2 waves),
+// 2 = 256x64 (4x1), 3 = 64x256 (1x4) with 4 stages; 4 = 128x128 with 5 stages (80 KB: still two
+// workgroups per CU), 5 = 256x64 with 5 stages (100 KB: one workgroup per CU).
 AI4E_API int ai4e_conv2d_fwd(const void* x, const void* w, const void* bias, const void* res, void* y, int N, int H,
                              int W, int C, int ldx, int xcoff, int KH, int KW, int stride, int pad, int OH, int OW,
                              int Kout, int Kpad, int ldy, int ycoff, int ldres, int relu, int tile_cfg,
                              hipStream_t stream) {
-  if (C % 8 || ldx % 8 || xcoff % 8 || Kpad % BK || Kout % 4 || ldy % 4 || ycoff % 4 || (res && ldres % 4) ||
+  if (C % 8 || ldx % 8 || xcoff % 8 || Kpad % (2 * BK) || Kout % 4 || ldy % 4 || ycoff % 4 || (res && ldres % 4) ||
       Kpad < KH * KW * C)
     return AI4E_EINVAL;
   ConvParams p{};
@@ -383,9 +443,11 @@ AI4E_API int ai4e_conv2d_fwd(const void* x, const void* w, const void* bias, con
   if (p.M <= 0) return AI4E_OK;
   if (tile_cfg == 0) tile_cfg = Kout <= 64 ? 2 : 1;
   switch (tile_cfg) {
-    case 1: return launch<2, 2>(p, stream);
-    case 2: return launch<4, 1>(p, stream);
-    case 3: return launch<1, 4>(p, stream);
+    case 1: return launch<2, 2, 4>(p, stream);
+    case 2: return launch<4, 1, 4>(p, stream);
+    case 3: return launch<1, 4, 4>(p, stream);
+    case 4: return launch<2, 2, 5>(p, stream);
+    case 5: return launch<4, 1, 5>(p, stream);
     default: return AI4E_EINVAL;
   }
 }

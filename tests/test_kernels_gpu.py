@@ -62,7 +62,7 @@ def test_conv_igemm(case, epi):
     assert err <= 0.02 * ref.abs().max().item() + 0.02, err
 
 
-@pytest.mark.parametrize("tile", [1, 2, 3])
+@pytest.mark.parametrize("tile", [1, 2, 3, 4, 5])
 def test_conv_tile_configs(tile):
     torch.manual_seed(1)
     wt = torch.randn(256, 64, 3, 3) / 24
