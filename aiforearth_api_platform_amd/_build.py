@@ -81,8 +81,10 @@ def build_kernels(verbose: bool = False, force: bool = False, jobs: int = 8) -> 
     LIBDIR.mkdir(parents=True, exist_ok=True)
     OBJDIR.mkdir(parents=True, exist_ok=True)
     hipcc = _hipcc()
+    # -amdgpu-mfma-vgpr-form: MFMA accumulators in arch VGPRs (gfx950 has one unified 512-entry
+    # file per SIMD); with AGPR accumulators hipcc shuttled them AGPR<->VGPR inside the K1 loop.
     flags = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
-             "-Wno-unused-result", f"-I{CSRC / 'kernels'}"]
+             "-mllvm", "-amdgpu-mfma-vgpr-form=1", "-Wno-unused-result", f"-I{CSRC / 'kernels'}"]
 
     def one(src: Path) -> Path:
         obj = OBJDIR / (src.stem + ".o")

@@ -39,7 +39,11 @@ def main():
         oh, ow = pc.out_hw(hh, ww)
         r = torch.randn(B, oh, ow, pc.cout, device=dev).bfloat16() if res else None
         times = {}
-        for cfg in (1, 2, 3, 4, 5):
+        for cfg in (1, 2, 3, 4, 5, 6):
+            try:
+                conv2d_nhwc(x, pc, residual=r, relu=True, tile_cfg=cfg)
+            except RuntimeError:
+                continue  # config not valid for this shape
             for _ in range(3):
                 conv2d_nhwc(x, pc, residual=r, relu=True, tile_cfg=cfg)
             torch.cuda.synchronize()

@@ -80,6 +80,26 @@ __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+// Wave-uniform (SGPR) walk over the taps of a conv whose K tiles never straddle a tap
+// (C % step == 0): (kh, kw, channel base cb) and the element offset (kh*W + kw)*ldx + cb, kept up to
+// date with adds only (no per-step multiplies or divisions on the scalar unit).
+struct TapWalk {
+  int kh = 0, kw = 0, cb = 0, off = 0;
+  __device__ __forceinline__ void next(int step, int C, int KW, int ldx, int rowjump) {
+    cb += step;
+    off += step;
+    if (cb == C) {
+      cb = 0;
+      off += ldx - C;
+      if (++kw == KW) {
+        kw = 0;
+        ++kh;
+        off += rowjump;  // (W - KW) * ldx
+      }
+    }
+  }
+};
+
 // Gather modes of the activation operand.
 enum { GATHER_GENERAL = 0,  // any C % 8: a 32-wide K chunk may span taps -> per-lane tap walk
        GATHER_POINTWISE = 1,  // 1x1, pad 0 (any stride): K is the channel axis of one input pixel
@@ -173,11 +193,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
     kh = tap / p.KW;
     kw = tap - kh * p.KW;
   }
-  int tkh = 0, tkw = 0, tcb = 0;  // GATHER_TAP: wave-uniform tap (kh, kw) and channel base
+  TapWalk tw;  // GATHER_TAP: wave-uniform tap walk
+  const int rowjump = (p.W - p.KW) * p.ldx;
   const uint16_t* const wsrc = p.w + static_cast<long>(n0 + 16 * wave + rin) * p.Kpad + 8 * c;
   const long wstep = 64L * p.Kpad;  // rows 16*(wave+4i)
   const uint32_t smem_base = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(smem));
   const uint16_t* const zero = p.zero;
+  const int nk = p.Kpad / BK;
 
   auto issue_stage = [&](int kt) {
     const uint32_t sbase = smem_base + (kt % STAGES) * STAGE_ELEMS * 2;
@@ -191,22 +213,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
     } else if constexpr (GATHER == GATHER_TAP) {
       // one tap per K chunk: offset and the padding test's tap part are scalar; per lane only the
       // two unsigned bounds compares and a pointer select remain
-      const long toff = (static_cast<long>(tkh) * p.W + tkw) * p.ldx + tcb;
-      const bool tap_ok = tkh < p.KH;
+      const int toff = tw.off;
+      const bool tap_ok = tw.kh < p.KH;
 #pragma unroll
       for (int i = 0; i < CA; ++i) {
-        const bool ok = tap_ok && static_cast<unsigned>(ih0[i] + tkh) < static_cast<unsigned>(p.H) &&
-                        static_cast<unsigned>(iw0[i] + tkw) < static_cast<unsigned>(p.W);
+        const bool ok = tap_ok && static_cast<unsigned>(ih0[i] + tw.kh) < static_cast<unsigned>(p.H) &&
+                        static_cast<unsigned>(iw0[i] + tw.kw) < static_cast<unsigned>(p.W);
         glds16(ok ? static_cast<const void*>(rowp[i] + toff) : zero, sbase + (16 * (wave + 4 * i)) * BK * 2);
       }
-      tcb += BK;
-      if (tcb == p.C) {
-        tcb = 0;
-        if (++tkw == p.KW) {
-          tkw = 0;
-          ++tkh;
-        }
-      }
+      tw.next(BK, p.C, p.KW, p.ldx, rowjump);
     } else {
 #pragma unroll
       for (int i = 0; i < CA; ++i) {
@@ -226,8 +241,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
         }
       }
     }
+    // past the end of K (the stray stages of the unconditional loop) every source is the zero chunk
+    const bool live = kt < nk;
 #pragma unroll
-    for (int i = 0; i < CB; ++i) glds16(wsrc + i * wstep + kt * BK, sbase + (BM + 16 * (wave + 4 * i)) * BK * 2);
+    for (int i = 0; i < CB; ++i)
+      glds16(live ? static_cast<const void*>(wsrc + i * wstep + kt * BK) : zero,
+             sbase + (BM + 16 * (wave + 4 * i)) * BK * 2);
   };
 
   f32x4_t acc[4][4];
@@ -238,17 +257,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
 
   const int frow = lane & 15;
   const int fofs = frow * BK + (((lane >> 4) ^ swz(frow)) << 3);
-  const int nk = p.Kpad / BK;
-
-  // Wait until ring stage `kt` has landed for this wave: the stages issued after it (at most
-  // min(ahead, nk-1-kt) of them, PER_STAGE DMAs each) may stay in flight.
-  auto wait_stage = [&](int kt, int ahead) {
-    const int younger = min(ahead, nk - 1 - kt);
-    if (younger >= 3) wait_vmcnt<3 * PER_STAGE>();
-    else if (younger == 2) wait_vmcnt<2 * PER_STAGE>();
-    else if (younger == 1) wait_vmcnt<PER_STAGE>();
-    else wait_vmcnt<0>();
-  };
 
   // Software pipeline, per K step kt (fragments of step kt already in registers):
   //   wait stage kt+1 + barrier -> ds_read fragments of kt+1 (async) -> 16 MFMAs on step kt
@@ -263,24 +271,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
     _Pragma("unroll") for (int j = 0; j < 4; ++j) FW[j] = *reinterpret_cast<const bf16x8_t*>(w_ + j * 16 * BK); \
     _Pragma("unroll") for (int i = 0; i < 4; ++i) FX[i] = *reinterpret_cast<const bf16x8_t*>(x_ + i * 16 * BK); \
   }
+// Every step waits, reads the next stage and issues stage kt+STAGES-1 unconditionally: past the
+// end of K the DMA re-reads the last weight columns / the zero chunk into a ring slot nobody reads
+// again, which keeps the loop free of scalar tail checks (and of the AGPR<->VGPR accumulator
+// shuffling hipcc emits around a second, checked loop). The stray DMAs drain before the epilogue.
 #define K1_STEP(KT, FWC, FXC, FWN, FXN)                                                         \
   {                                                                                             \
     const int kt_ = (KT);                                                                       \
-    if (kt_ + 1 < nk) {                                                                         \
-      wait_stage(kt_ + 1, STAGES - 3); /* issued so far: up to kt+STAGES-2 */                   \
-      __builtin_amdgcn_s_barrier();                                                             \
-      K1_READ(FWN, FXN, kt_ + 1)                                                                \
-    }                                                                                           \
+    wait_vmcnt<(STAGES - 3) * PER_STAGE>();                                                     \
+    __builtin_amdgcn_s_barrier();                                                               \
+    K1_READ(FWN, FXN, kt_ + 1)                                                                  \
     _Pragma("unroll") for (int i = 0; i < 4; ++i)                                               \
       _Pragma("unroll") for (int j = 0; j < 4; ++j)                                             \
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(FWC[j], FXC[i], acc[i][j], 0, 0, 0); \
-    if (kt_ + STAGES - 1 < nk) issue_stage(kt_ + STAGES - 1);                                   \
+    issue_stage(kt_ + STAGES - 1);                                                              \
   }
 
 #pragma unroll
-  for (int s = 0; s < STAGES - 1; ++s)
-    if (s < nk) issue_stage(s);
-  wait_stage(0, STAGES - 2);
+  for (int s = 0; s < STAGES - 1; ++s) issue_stage(s);
+  wait_vmcnt<(STAGES - 2) * PER_STAGE>();
   __builtin_amdgcn_s_barrier();
   K1_READ(fw0, fx0, 0)
   // unrolled by two so the fragment buffers alternate without register copies; the MFMAs sit
@@ -291,6 +300,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
     K1_STEP(kt, fw0, fx0, fw1, fx1)
     K1_STEP(kt + 1, fw1, fx1, fw0, fx0)
   }
+  wait_vmcnt<0>();  // the stray tail DMAs land before any LDS reuse
 #undef K1_STEP
 #undef K1_READ
 
@@ -379,6 +389,286 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
   }
 }
 
+// ============================================================================================
+// K1 "256" variant: 256x256 workgroup tile, 8 waves (2 pixel groups x 4 channel groups, each wave
+// 128 pixels x 64 channels), BK = 64, LDS-DMA staging of 16-KB "units", and a ping-pong phase
+// schedule: the two wave groups are offset by one barrier, so on every SIMD one wave issues its
+// LDS reads / DMA while the other runs its 16-MFMA phase (cdna guide §5 "The 256² 8-phase
+// template": 8 waves, BK 64, counted vmcnt never 0 in the loop, raw s_barrier, setprio around the
+// MFMAs). One workgroup per CU (128 KB LDS).
+//
+// Units (128 rows x 128 B each; LDS = 2 buffers x 4 units):
+//   u0 XQ0: pixel rows {wr*128 + 0..63}     u3 XQ1: pixel rows {wr*128 + 64..127}   (wr = 0, 1)
+//   u1 WQ0: channel rows {wc*64 + 0..31}    u2 WQ1: channel rows {wc*64 + 32..63}   (wc = 0..3)
+// Per K tile (4 phases) a wave computes its 2x2 quadrants (mq = pixel half, nq = channel half):
+//   phase 1 (0,0): ds_read XQ0 + WQ0 | phase 2 (0,1): ds_read WQ1 | phase 3 (1,1): ds_read XQ1 |
+//   phase 4 (1,0): no reads (WQ0 fragments kept in registers since phase 1).
+// So within a tile u0/u1 are last read in phase 1, u2 in phase 2, u3 in phase 3.
+// Staging (one unit per phase g = 4t+p): phase g stages unit (g-3) mod 4 of tile (g-3) div 4 + 2
+// into the buffer of tile t: u0 at p=3, u1 at p=4, u2 at p=1 and u3 at p=2 of the NEXT tile — every
+// slot is overwritten >= 2 phases after its last read (WAR with the one-barrier stagger), and
+// read >= 4 phases after it was staged. At phase g each wave waits until its DMAs of phases <= g-3
+// have landed (vmcnt = loads of phases g-2..g, at most 6), before that phase's first barrier; the
+// readers of phase g+1 pass that barrier first (RAW).
+// ============================================================================================
+constexpr int U_ROWS = 128, U_BYTES = U_ROWS * 128;
+
+template <int GATHER>
+__global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) {
+  static_assert(GATHER == GATHER_TAP || GATHER == GATHER_POINTWISE, "256 tile needs C % 64 == 0");
+  __shared__ __attribute__((aligned(1024))) uint8_t smem[2 * 4 * U_BYTES];  // the only LDS object
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+
+  const int t = xcd_remap(blockIdx.x, gridDim.x);
+  const int mt = t / p.ntiles_n;
+  const int nt = t - mt * p.ntiles_n;
+  const int m0 = mt * 256;
+  const int n0 = nt * 256;
+  const int nk = p.Kpad / 64;
+  const uint32_t sbase = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(smem));
+
+  // ---- DMA sources. Lane writes unit row R_i = 16*wave + 8*i + (lane>>3), physical 16-B chunk
+  //      lane&7, holding logical chunk q_i = (lane&7) ^ ((R_i >> 1) & 7).
+  const int OHW = p.OH * p.OW;
+  const uint16_t* xrow[2][2];  // [i][xq] pixel row pointer (+ 8*q_i), nullptr past M
+  int ih0[2][2], iw0[2][2];
+  const uint16_t* wrow[2];     // [i] weight row pointer (+ 8*q_i) for WQ0; WQ1 = +32 rows
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int R = 16 * wave + 8 * i + (lane >> 3);
+    const int q = (lane & 7) ^ ((R >> 1) & 7);
+#pragma unroll
+    for (int xq = 0; xq < 2; ++xq) {
+      const int m = m0 + (R >> 6) * 128 + (R & 63) + 64 * xq;
+      if (m < p.M) {
+        const int img = m / OHW;
+        const int rem = m - img * OHW;
+        const int oh = rem / p.OW;
+        const int ow = rem - oh * p.OW;
+        ih0[i][xq] = oh * p.stride - p.pad;
+        iw0[i][xq] = ow * p.stride - p.pad;
+        xrow[i][xq] = p.x + static_cast<long>(img) * p.H * p.W * p.ldx + p.xcoff +
+                      (static_cast<long>(ih0[i][xq]) * p.W + iw0[i][xq]) * p.ldx + 8 * q;
+      } else {
+        ih0[i][xq] = -(1 << 28);
+        iw0[i][xq] = 0;
+        xrow[i][xq] = nullptr;
+      }
+    }
+    wrow[i] = p.w + static_cast<long>(n0 + (R >> 5) * 64 + (R & 31)) * p.Kpad + 8 * q;
+  }
+  const uint16_t* const zero = p.zero;
+  // X units are staged tile by tile (XQ0 and XQ1 at different phases): one tap walk per unit kind
+  TapWalk wx[2];
+  const int rowjump = (p.W - p.KW) * p.ldx;
+
+  // stage unit u of K tile kt into buffer kt&1 (2 DMAs per lane); X units must be staged in tile order
+
+  auto stage = [&](int kt, int u) {
+    const uint32_t ubase = sbase + ((kt & 1) * 4 + u) * U_BYTES + (16 * wave) * 128;
+    const int k0 = kt * 64;
+    if (u == 1 || u == 2) {
+      const long roff = (u == 2 ? 32L * p.Kpad : 0L) + k0;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) glds16(wrow[i] + roff, ubase + i * 8 * 128);
+    } else {
+      const int xq = u == 3 ? 1 : 0;
+      if constexpr (GATHER == GATHER_POINTWISE) {
+        const bool kok = k0 < p.C;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const void* src = (kok && xrow[i][xq] != nullptr) ? static_cast<const void*>(xrow[i][xq] + k0) : zero;
+          glds16(src, ubase + i * 8 * 128);
+        }
+      } else {
+        // a 64-wide K tile lies in one tap (C % 64 == 0): wave-uniform walk
+        TapWalk& tw = wx[xq];
+        const bool tok = tw.kh < p.KH;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const bool ok = tok && static_cast<unsigned>(ih0[i][xq] + tw.kh) < static_cast<unsigned>(p.H) &&
+                          static_cast<unsigned>(iw0[i][xq] + tw.kw) < static_cast<unsigned>(p.W);
+          glds16(ok ? static_cast<const void*>(xrow[i][xq] + tw.off) : zero, ubase + i * 8 * 128);
+        }
+        tw.next(64, p.C, p.KW, p.ldx, rowjump);
+      }
+    }
+  };
+  // phase g stages unit (g-3) mod 4 of tile (g-3) div 4 + 2 (g may be <= 0: the prologue)
+  auto phase_tile = [&](int g) { return ((g + 5) >> 2); };  // floor((g-3)/4)+2 for g >= -5
+  auto phase_unit = [&](int g) { return (g + 5) & 3; };
+  auto stage_phase = [&](int g) {
+    const int kt = phase_tile(g);
+    if (kt < nk) stage(kt, phase_unit(g));
+  };
+  auto loads_of = [&](int g) { return phase_tile(g) < nk ? 2 : 0; };
+  // wait until this wave's DMAs of phases <= g-3 have landed
+  auto wait_phase = [&](int g) {
+    const int n = loads_of(g - 2) + loads_of(g - 1) + loads_of(g);
+    if (n >= 6) wait_vmcnt<6>();
+    else if (n == 4) wait_vmcnt<4>();
+    else if (n == 2) wait_vmcnt<2>();
+    else wait_vmcnt<0>();
+  };
+
+  f32x4_t acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  // fragment read offsets: row (lane&15) of a 16-row block, logical chunk 4s + (lane>>4)
+  const int frow = lane & 15;
+  const int fsw = frow >> 1;
+  const uint32_t fofs0 = frow * 128 + (((lane >> 4) ^ fsw) << 4);        // s = 0
+  const uint32_t fofs1 = frow * 128 + (((4 + (lane >> 4)) ^ fsw) << 4);  // s = 1
+  bf16x8_t xr[4][2], w0r[2][2], w1r[2][2];
+
+#define K256_READ_X(XQ, KT)                                                                        \
+  {                                                                                                \
+    const uint8_t* b_ = smem + (((KT) & 1) * 4 + ((XQ) ? 3 : 0)) * U_BYTES + (wr * 64) * 128;       \
+    _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                                \
+      xr[i][0] = *reinterpret_cast<const bf16x8_t*>(b_ + i * 16 * 128 + fofs0);                    \
+      xr[i][1] = *reinterpret_cast<const bf16x8_t*>(b_ + i * 16 * 128 + fofs1);                    \
+    }                                                                                              \
+  }
+#define K256_READ_W(WR, NQ, KT)                                                                    \
+  {                                                                                                \
+    const uint8_t* b_ = smem + (((KT) & 1) * 4 + 1 + (NQ)) * U_BYTES + (wc * 32) * 128;            \
+    _Pragma("unroll") for (int j = 0; j < 2; ++j) {                                                \
+      WR[j][0] = *reinterpret_cast<const bf16x8_t*>(b_ + j * 16 * 128 + fofs0);                    \
+      WR[j][1] = *reinterpret_cast<const bf16x8_t*>(b_ + j * 16 * 128 + fofs1);                    \
+    }                                                                                              \
+  }
+#define K256_MFMA(MQ, NQ, WR)                                                                      \
+  {                                                                                                \
+    __builtin_amdgcn_s_setprio(1);                                                                 \
+    _Pragma("unroll") for (int s = 0; s < 2; ++s)                                                  \
+      _Pragma("unroll") for (int i = 0; i < 4; ++i)                                                \
+        _Pragma("unroll") for (int j = 0; j < 2; ++j)                                              \
+          acc[4 * (MQ) + i][2 * (NQ) + j] =                                                        \
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(WR[j][s], xr[i][s], acc[4 * (MQ) + i][2 * (NQ) + j], 0, 0, 0); \
+    __builtin_amdgcn_s_setprio(0);                                                                 \
+  }
+// CHECKED = 0: steady state (kt + 2 < nk): every phase stages a unit, 3 phases of DMAs in flight
+#define K256_SYNC_LOADS(G, CHECKED)                                                                \
+  if (CHECKED) {                                                                                   \
+    stage_phase(G);                                                                                \
+    wait_phase(G);                                                                                 \
+  } else {                                                                                         \
+    stage(phase_tile(G), phase_unit(G));                                                           \
+    wait_vmcnt<6>();                                                                               \
+  }                                                                                                \
+  __builtin_amdgcn_s_barrier();                                                                    \
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#define K256_TILE(KT, CHECKED)                                                                     \
+  {                                                                                                \
+    const int g = 4 * (KT);                                                                        \
+    /* phase 1: quadrant (0,0) */                                                                  \
+    K256_READ_W(w0r, 0, KT)                                                                        \
+    K256_READ_X(0, KT)                                                                             \
+    K256_SYNC_LOADS(g + 1, CHECKED)                                                                \
+    K256_MFMA(0, 0, w0r)                                                                           \
+    __builtin_amdgcn_s_barrier();                                                                  \
+    /* phase 2: quadrant (0,1) */                                                                  \
+    K256_READ_W(w1r, 1, KT)                                                                        \
+    K256_SYNC_LOADS(g + 2, CHECKED)                                                                \
+    K256_MFMA(0, 1, w1r)                                                                           \
+    __builtin_amdgcn_s_barrier();                                                                  \
+    /* phase 3: quadrant (1,1) */                                                                  \
+    K256_READ_X(1, KT)                                                                             \
+    K256_SYNC_LOADS(g + 3, CHECKED)                                                                \
+    K256_MFMA(1, 1, w1r)                                                                           \
+    __builtin_amdgcn_s_barrier();                                                                  \
+    /* phase 4: quadrant (1,0), fragments already in registers */                                  \
+    K256_SYNC_LOADS(g + 4, CHECKED)                                                                \
+    K256_MFMA(1, 0, w0r)                                                                           \
+    __builtin_amdgcn_s_barrier();                                                                  \
+  }
+
+  // ---- prologue: tile 0 (virtual phases -5..-2) and tile 1's u0, u1 (phases -1, 0)
+#pragma unroll
+  for (int g = -5; g <= 0; ++g) stage_phase(g);
+  if (loads_of(-1) + loads_of(0) == 4) wait_vmcnt<4>();
+  else wait_vmcnt<0>();
+  __builtin_amdgcn_s_barrier();
+  if (wr == 1) __builtin_amdgcn_s_barrier();  // the stagger: group 1 trails by one barrier
+
+  int kt = 0;
+  for (; kt + 2 < nk; ++kt) K256_TILE(kt, 0)
+  for (; kt < nk; ++kt) K256_TILE(kt, 1)
+#undef K256_TILE
+#undef K256_SYNC_LOADS
+#undef K256_MFMA
+#undef K256_READ_W
+#undef K256_READ_X
+  if (wr == 0) __builtin_amdgcn_s_barrier();  // re-align the two groups
+  wait_vmcnt<0>();
+  __syncthreads();
+
+  // ---- epilogue, one pixel group at a time: fp32 [128][256] tile in LDS (16-B chunk index
+  //      XOR (row & 7)), then every thread handles 16-B output chunks: + bias (+ residual), ReLU.
+  float* tile = reinterpret_cast<float*>(smem);
+  const float lo = p.relu ? 0.f : -INFINITY;
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+    if (wr == pass) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int r = 16 * i + (lane & 15);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int c4 = (wc * 64 + 16 * j) / 4 + (lane >> 4);
+          *reinterpret_cast<f32x4_t*>(tile + r * 256 + 4 * (c4 ^ (r & 7))) = acc[i][j];
+        }
+      }
+    }
+    __syncthreads();
+    uint4 rv[8];
+    if (p.res) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int g = tid + 512 * e;
+        const int m = min(m0 + 128 * pass + (g >> 5), p.M - 1), n = min(n0 + 8 * (g & 31), p.Kout - 8);
+        rv[e] = *reinterpret_cast<const uint4*>(p.res + static_cast<long>(m) * p.ldres + n);
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int g = tid + 512 * e;
+      const int r = g >> 5, c8 = g & 31;
+      const int m = m0 + 128 * pass + r, n = n0 + 8 * c8;
+      const float4 v0 = *reinterpret_cast<const float4*>(tile + r * 256 + 4 * ((2 * c8) ^ (r & 7)));
+      const float4 v1 = *reinterpret_cast<const float4*>(tile + r * 256 + 4 * ((2 * c8 + 1) ^ (r & 7)));
+      const int nb = min(n, p.Kout - 8);
+      const float4 b0 = *reinterpret_cast<const float4*>(p.bias + nb);
+      const float4 b1 = *reinterpret_cast<const float4*>(p.bias + nb + 4);
+      float f[8] = {v0.x + b0.x, v0.y + b0.y, v0.z + b0.z, v0.w + b0.w,
+                    v1.x + b1.x, v1.y + b1.y, v1.z + b1.z, v1.w + b1.w};
+      if (p.res) {
+        float a[8];
+        unpack_bf16x2(rv[e].x, a[0], a[1]);
+        unpack_bf16x2(rv[e].y, a[2], a[3]);
+        unpack_bf16x2(rv[e].z, a[4], a[5]);
+        unpack_bf16x2(rv[e].w, a[6], a[7]);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) f[k] += a[k];
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) f[k] = fmaxf(f[k], lo);
+      if (m < p.M && n < p.Kout)
+        *reinterpret_cast<uint4*>(p.y + static_cast<long>(m) * p.ldy + p.ycoff + n) =
+            make_uint4(pack_bf16x2(f[0], f[1]), pack_bf16x2(f[2], f[3]), pack_bf16x2(f[4], f[5]),
+                       pack_bf16x2(f[6], f[7]));
+    }
+    __syncthreads();
+  }
+}
+
 }  // namespace
 
 namespace {
@@ -418,11 +708,29 @@ int launch(const ConvParams& p0, hipStream_t s) {
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
 }
 
+int launch256(const ConvParams& p0, hipStream_t s) {
+  ConvParams p = p0;
+  // 256 tile: C % 64 (one tap per 64-wide K tile), 16-B output/residual rows, Kout % 8
+  if (p.C % 64 || p.Kpad % 64 || p.ldy % 8 || p.ycoff % 8 || (p.res && p.ldres % 8) || p.Kout % 8)
+    return AI4E_EINVAL;
+  const int mt = ai4e_cdiv(p.M, 256);
+  p.ntiles_n = ai4e_cdiv(p.Kout, 256);
+  const int nb = mt * p.ntiles_n;
+  p.zero = zero_chunk_ptr();
+  if (!p.zero) return AI4E_ELAUNCH;
+  if (p.KH == 1 && p.KW == 1 && p.pad == 0)
+    hipLaunchKernelGGL(conv_igemm256_kernel<GATHER_POINTWISE>, dim3(nb), dim3(512), 0, s, p);
+  else
+    hipLaunchKernelGGL(conv_igemm256_kernel<GATHER_TAP>, dim3(nb), dim3(512), 0, s, p);
+  return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
+}
+
 }  // namespace
 
 // tile_cfg (pixels x channels per workgroup, LDS ring depth): 0 = auto, 1 = 128x128 (2x2 waves),
 // 2 = 256x64 (4x1), 3 = 64x256 (1x4) with 4 stages; 4 = 128x128 with 5 stages (80 KB: still two
-// workgroups per CU), 5 = 256x64 with 5 stages (100 KB: one workgroup per CU).
+// workgroups per CU), 5 = 256x64 with 5 stages (100 KB: one workgroup per CU), 6 = 256x256, 8 waves,
+// ping-pong phases (needs C % 64 == 0, Kout % 8 == 0).
 AI4E_API int ai4e_conv2d_fwd(const void* x, const void* w, const void* bias, const void* res, void* y, int N, int H,
                              int W, int C, int ldx, int xcoff, int KH, int KW, int stride, int pad, int OH, int OW,
                              int Kout, int Kpad, int ldy, int ycoff, int ldres, int relu, int tile_cfg,
@@ -448,6 +756,7 @@ AI4E_API int ai4e_conv2d_fwd(const void* x, const void* w, const void* bias, con
     case 3: return launch<1, 4, 4>(p, stream);
     case 4: return launch<2, 2, 5>(p, stream);
     case 5: return launch<4, 1, 5>(p, stream);
+    case 6: return launch256(p, stream);
     default: return AI4E_EINVAL;
   }
 }

@@ -62,7 +62,7 @@ def test_conv_igemm(case, epi):
     assert err <= 0.02 * ref.abs().max().item() + 0.02, err
 
 
-@pytest.mark.parametrize("tile", [1, 2, 3, 4, 5])
+@pytest.mark.parametrize("tile", [1, 2, 3, 4, 5, 6])
 def test_conv_tile_configs(tile):
     torch.manual_seed(1)
     wt = torch.randn(256, 64, 3, 3) / 24
@@ -71,6 +71,36 @@ def test_conv_tile_configs(tile):
     y = conv2d_nhwc(x, pc, tile_cfg=tile)
     ref = ref_conv(x, pc.w_packed[:256, :576].float().reshape(256, 3, 3, 64).permute(0, 3, 1, 2), torch.zeros(256, device=DEV), 1, 1)
     assert (y.float() - ref).abs().max().item() < 0.02 * ref.abs().max().item() + 0.02
+
+
+CASES_256 = [
+    # n, h, w, cin, cout, k, stride, pad  (256x256 ping-pong tile: C % 64 == 0, Cout % 8 == 0)
+    (2, 56, 56, 64, 256, 1, 1, 0),      # one K tile (nk = 1)
+    (3, 28, 28, 256, 512, 1, 2, 0),     # strided pointwise
+    (2, 14, 14, 256, 256, 3, 1, 1),     # 3x3, 36 K tiles
+    (2, 28, 28, 128, 128, 3, 2, 1),     # Cout < 256: half the channel tile masked
+    (2, 7, 7, 512, 2048, 1, 1, 0),      # M = 98 < 256
+    (1, 33, 17, 64, 264, 3, 1, 1),      # ragged M, Cout = 256 + 8
+]
+
+
+@pytest.mark.parametrize("case", CASES_256)
+@pytest.mark.parametrize("epi", ["plain", "res_relu"])
+def test_conv_tile256(case, epi):
+    n, h, w, cin, cout, k, s, p = case
+    torch.manual_seed(3)
+    wt = torch.randn(cout, cin, k, k) / (cin * k * k) ** 0.5
+    b = torch.randn(cout) * 0.1
+    pc = pack_conv(wt, b, stride=s, pad=p).to(DEV)
+    x = torch.randn(n, h, w, pc.cin_pad, device=DEV).to(torch.bfloat16)
+    oh, ow = pc.out_hw(h, w)
+    res = torch.randn(n, oh, ow, cout, device=DEV).to(torch.bfloat16) if epi == "res_relu" else None
+    y = conv2d_nhwc(x, pc, residual=res, relu=epi != "plain", tile_cfg=6)
+    torch.cuda.synchronize()
+    wq = pc.w_packed[:cout, :k * k * pc.cin_pad].float().reshape(cout, k, k, pc.cin_pad).permute(0, 3, 1, 2)
+    ref = ref_conv(x, wq, b.to(DEV), s, p, res, epi != "plain")
+    err = (y.float() - ref).abs().max().item()
+    assert err <= 0.02 * ref.abs().max().item() + 0.02, err
 
 
 def test_conv_channel_slices():
