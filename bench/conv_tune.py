@@ -59,8 +59,9 @@ def main():
         print(json.dumps({"layer": name, "key": key, "us": {k: round(v, 1) for k, v in times.items()}, "best": best}),
               flush=True)
     if "--write" in sys.argv:
-        path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "aiforearth_api_platform_amd",
-                            "ops", "conv_tiles.json")
+        path = os.environ.get("TILES_OUT") or os.path.join(
+            os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "aiforearth_api_platform_amd", "ops",
+            "conv_tiles.json")
         with open(path, "w") as f:
             json.dump(table, f, indent=1, sort_keys=True)
         print("wrote", path)
