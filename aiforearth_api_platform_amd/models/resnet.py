@@ -19,7 +19,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ..ops.conv import PackedConv, conv2d_nhwc, fold_bn, pack_conv, pack_stem_s2d
+from ..ops.conv import PackedConv, conv2d_nhwc, conv_chain, fold_bn, pack_conv, pack_stem_s2d
 from ..ops.pool import (global_avgpool_nhwc, maxpool2d_nhwc, preprocess_s2d_u8, preprocess_u8,
                         space_to_depth_shifted)
 
@@ -123,6 +123,11 @@ def _env_chunk() -> Optional[Tuple[int, int]]:
 DEFAULT_CHUNK: Optional[Tuple[int, int]] = None
 
 
+def _env_chain() -> bool:
+    """``AI4E_RESNET_CHAIN=0`` runs every conv as its own K1 launch instead of the K1c bottleneck chains."""
+    return os.environ.get("AI4E_RESNET_CHAIN", "1") not in ("0", "off", "")
+
+
 class FusedResNet:
     """Inference graph over packed, BN-folded layers (NHWC bf16)."""
 
@@ -146,6 +151,13 @@ class FusedResNet:
         self.fc = pack_conv(fcw, model.fc.bias.data.float()).to(self.device)
         self.num_classes = model.fc.out_features
         self.chunk = chunk if chunk is not None else _env_chunk()
+        self.chain = _env_chain()
+        # stages: runs of blocks starting at a block with a downsample conv
+        self.stages: List[List[Tuple[PackedConv, PackedConv, PackedConv, Optional[PackedConv]]]] = []
+        for blk in self.blocks:
+            if blk[3] is not None or not self.stages:
+                self.stages.append([])
+            self.stages[-1].append(blk)
 
     def layers(self) -> List[PackedConv]:
         out = [self.stem]
@@ -185,6 +197,18 @@ class FusedResNet:
         y = conv2d_nhwc(y, c2, relu=True)
         return conv2d_nhwc(y, c3, residual=idt, relu=True, out=out)
 
+    @staticmethod
+    def _stage(x: torch.Tensor, blocks) -> torch.Tensor:
+        """One ResNet stage with the K1c chains: c1 and the downsample of the first block run as K1 convs,
+        then every block is ONE kernel (c2 -> c3 + residual -> the next block's c1), see conv_chain."""
+        c1, _, _, down = blocks[0]
+        idt = x if down is None else conv2d_nhwc(x, down)
+        t1 = conv2d_nhwc(x, c1, relu=True)
+        for i, (_, c2, c3, _) in enumerate(blocks):
+            nxt = blocks[i + 1][0] if i + 1 < len(blocks) else None
+            idt, t1 = conv_chain(t1, c2, c3, idt, c1n=nxt)
+        return idt
+
     def _prefix_shape(self, n: int, h: int, w: int, nblocks: int) -> Tuple[int, int, int, int]:
         """Output shape after the stem, max-pool and the first ``nblocks`` bottlenecks."""
         h, w = (h - 1) // 2 + 1, (w - 1) // 2 + 1  # maxpool 3/2/1 on the (H/2, W/2) stem output
@@ -219,6 +243,10 @@ class FusedResNet:
             y = feats
         else:
             y, nblocks = self._stem(pre(x)), 0
+        if self.chain and nblocks == 0:
+            for st in self.stages:
+                y = self._stage(y, st)
+            return y
         for blk in self.blocks[nblocks:]:
             y = self._block(y, blk)
         return y

@@ -152,6 +152,44 @@ def _conv_hip(x, pc, residual, relu, out, out_coff, tile_cfg):
               oh, ow, pc.cout, pc.kpad, ldy, out_coff, ldres, int(relu), tile_cfg, _ext.stream_ptr(x.device))
 
 
+def chain_supported(mid: int, has_next: bool) -> bool:
+    """Shapes the fused bottleneck-chain kernel K1c is built for (csrc/kernels/conv_chain.hip)."""
+    return mid == 64 or (not has_next and mid in (128, 256))
+
+
+def conv_chain(t1: torch.Tensor, c2: PackedConv, c3: PackedConv, residual: torch.Tensor,
+               c1n: Optional[PackedConv] = None, out: Optional[torch.Tensor] = None):
+    """Fused bottleneck tail (K1c): ``y = relu(c3(relu(c2(t1))) + residual)`` and, with ``c1n`` (the next
+    block's 1x1 reduce), ``t1n = relu(c1n(y))`` from the same kernel. Returns ``(y, t1n or None)``.
+
+    ``t1``: NHWC ``[N,H,W,mid]`` bf16 (c1's output), ``c2`` 3x3/pad 1 (stride 1 or 2) mid->mid, ``c3`` 1x1
+    mid->4*mid, ``residual`` ``[N,OH,OW,4*mid]``, ``c1n`` 1x1 4*mid->mid. Shapes the kernel does not cover
+    (``chain_supported``) and the PyTorch backend run the three convs separately.
+    """
+    n, h, w, mid = t1.shape
+    if (c2.kh, c2.kw, c2.pad, c2.cin_pad, c2.cout) != (3, 3, 1, mid, mid) or c3.kh != 1 or c3.cin_pad != mid \
+            or c3.cout != 4 * mid or (c1n is not None and (c1n.kh != 1 or c1n.cin_pad != 4 * mid or c1n.cout != mid)):
+        raise ValueError("conv_chain: layer shapes do not form a bottleneck chain")
+    oh, ow = c2.out_hw(h, w)
+    if out is None:
+        out = torch.empty(n, oh, ow, 4 * mid, device=t1.device, dtype=t1.dtype)
+    if _ext.backend_for(t1) != "hip" or not chain_supported(mid, c1n is not None):
+        y2 = conv2d_nhwc(t1, c2, relu=True)
+        conv2d_nhwc(y2, c3, residual=residual, relu=True, out=out)
+        return out, (conv2d_nhwc(out, c1n, relu=True) if c1n is not None else None)
+    if t1.dtype != torch.bfloat16 or not t1.is_contiguous() or not out.is_contiguous():
+        raise ValueError("conv_chain: contiguous bf16 NHWC tensors required")
+    if residual.shape != (n, oh, ow, 4 * mid) or not residual.is_contiguous():
+        raise ValueError("conv_chain: residual must be contiguous [N,OH,OW,4*mid]")
+    t1n = torch.empty(n, oh, ow, mid, device=t1.device, dtype=t1.dtype) if c1n is not None else None
+    _ext.call("ai4e_conv_chain_fwd", t1.data_ptr(), c2.w_packed.data_ptr(), c2.bias.data_ptr(),
+              c3.w_packed.data_ptr(), c3.bias.data_ptr(), residual.data_ptr(), out.data_ptr(),
+              _ext.ptr(c1n.w_packed if c1n is not None else None), _ext.ptr(c1n.bias if c1n is not None else None),
+              _ext.ptr(t1n), n, h, w, mid, mid, c2.stride, c2.kpad, c3.kpad, c1n.kpad if c1n is not None else 0,
+              _ext.stream_ptr(t1.device))
+    return out, t1n
+
+
 def _conv_torch(x, pc, residual, relu):
     cdt = torch.float32 if not x.is_cuda else x.dtype
     xin = x[..., :pc.cin].permute(0, 3, 1, 2).to(cdt)

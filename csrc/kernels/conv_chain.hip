@@ -1,0 +1,464 @@
+// K1c — fused ResNet bottleneck chain: 3x3 conv (c2) -> 1x1 expand (c3) + residual -> [next block's
+// 1x1 reduce (c1')], one kernel per pixel tile, intermediates kept in LDS.
+//
+//   T2  = relu(conv3x3_s(T1; W2) + b2)                    [BM x MID]   (LDS only)
+//   Y   = relu(T2 . W3^T + b3 + R)                        [BM x 4MID]  (HBM: next block's residual)
+//   T1' = relu(Y . W1'^T + b1')          (NEXT only)      [BM x MID]   (HBM: next block's c2 input)
+//
+// Why: at batch 256 a layer1 bottleneck moves 1.6 GB through HBM as three separate convs (c1 reads the
+// 256-channel input, c3 re-reads T2 and the residual). Chained, a block reads T1 (+3x3 halo, L2) and R
+// once and writes Y and T1' once: 1.0 GB for layer1, and c1 of every identity block disappears as a
+// launch. BatchNorm is folded into W/b on the host (ops/conv.py).
+//
+// Structure (4 wave64s, every wave a 64-pixel x 64-channel MFMA tile of v_mfma_f32_16x16x32_bf16,
+// workgroup tile BM x MID with BM = 16384 / MID, i.e. 256x64, 128x128, 64x256):
+// * phase A: the K1 implicit-GEMM main loop (LDS-DMA ring, counted vmcnt, fragment double-buffering)
+//   over the 9*MID-long K of the 3x3 conv; epilogue writes bf16 T2 into LDS in the K-blocked,
+//   chunk-swizzled layout the MFMA operand reads expect ([MID/32][BM][32], 64-B rows).
+// * phases B/C, four passes p over the 4*MID output channels of c3: the residual chunk R_p is DMA'd into
+//   the Y buffer (coalesced 16-B rows), B_p = T2 . W3[p]^T, the epilogue adds b3 + R_p, applies ReLU and
+//   writes bf16 Y_p in place, C_p accumulates Y_p . W1'[:, p]^T into the persistent T1' accumulators,
+//   and Y_p is copied out to HBM with 16-B stores. Weights of B/C stream through a weights-only LDS ring
+//   (one continuous DMA stream across passes); every wait is a counted vmcnt whose count is a constant
+//   after unrolling (the wave's own DMA/store bookkeeping below).
+// LDS: max(phase-A pixel ring, T2 + Y buffer) + weight ring = 80 KB for MID 64 (2 workgroups per CU);
+// biases come through scalar loads (no LDS, no vmcnt).
+#include <type_traits>
+
+#include "conv_common.h"
+
+namespace {
+
+using ai4e_conv::BK;
+using ai4e_conv::glds16;
+using ai4e_conv::swz;
+using ai4e_conv::TapWalk;
+using ai4e_conv::wait_vmcnt;
+using ai4e_conv::wait_vmcnt_n;
+
+__device__ __attribute__((aligned(64))) uint16_t g_chain_zero[32];
+// target of the masked-off tail stores: a row base (+ column offsets up to 4*256) must stay inside it
+__device__ __attribute__((aligned(64))) uint16_t g_chain_sink[1024 + 64];
+
+// LDS-ordering barrier: own LDS reads/writes retired, then s_barrier; an asm statement with a memory
+// clobber so hipcc moves no LDS access across it (the raw builtin is not a compiler memory barrier).
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// Bias of the 4 channels n0 + 4*(lane>>4) + 0..3 from a wave-uniform 16-float block: read through the
+// constant address space (s_load: lgkmcnt, outside the hand-counted vmcnt bookkeeping), then a
+// lane-group select on registers.
+typedef const float __attribute__((address_space(4)))* const_f32_ptr;
+__device__ __forceinline__ f32x4_t bias4(const float* blk, int g) {
+  const const_f32_ptr b = reinterpret_cast<const_f32_ptr>(reinterpret_cast<uintptr_t>(blk));
+  f32x4_t r;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    // readfirstlane pins each value to an SGPR so the selects below stay register selects (without it
+    // hipcc folds select(load, load) into a per-lane vector load)
+    const float v0 = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(b[q])));
+    const float v1 = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(b[4 + q])));
+    const float v2 = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(b[8 + q])));
+    const float v3 = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(b[12 + q])));
+    const float lo = g & 1 ? v1 : v0;
+    const float hi = g & 1 ? v3 : v2;
+    r[q] = g & 2 ? hi : lo;
+  }
+  return r;
+}
+
+struct ChainParams {
+  const uint16_t* x;  // T1 [N, H, W, ldx], MID channels at offset 0
+  const uint16_t* w2;
+  const float* b2;
+  const uint16_t* w3;
+  const float* b3;
+  const uint16_t* res;  // [M, 4*MID]
+  uint16_t* y;          // [M, 4*MID]
+  const uint16_t* w1n;  // [MID rows, kpad1n >= 4*MID]   (NEXT)
+  const float* b1n;
+  uint16_t* t1n;        // [M, MID]                      (NEXT)
+  const uint16_t* zero;
+  int H, W, ldx, stride, OH, OW, M;
+  int kpad2, kpad3, kpad1n;
+  uint16_t* sink;
+};
+
+template <int MID>
+struct ChainCfg {
+  static constexpr int WN = MID / 64;         // waves along channels
+  static constexpr int WM = 4 / WN;           // waves along pixels
+  static constexpr int BM = WM * 64;          // pixels per workgroup
+  static constexpr int STAGES = 4;
+  static constexpr int CA = BM / 64;          // pixel-row DMAs per wave per phase-A stage
+  static constexpr int CB = MID / 64;         // weight-row DMAs per wave per stage
+  static constexpr int PX_RING = STAGES * BM * 64;
+  static constexpr int TILE = BM * MID * 2;   // one [BM x MID] bf16 tile
+  static constexpr int PX_BYTES = PX_RING > 2 * TILE ? PX_RING : 2 * TILE;
+  static constexpr int CH_BYTES = STAGES * MID * 64;
+  static constexpr int LDS = PX_BYTES + CH_BYTES;
+  static constexpr int NB = MID / 32;         // K steps of one B or C segment
+  static constexpr int NR = TILE / 1024 / 4;  // residual-chunk DMAs per wave
+  static constexpr int NS = TILE / 16 / 256;  // 16-B copy-out stores per thread
+};
+
+// byte offset of the 8-byte group holding channels n..n+3 of row r in a K-blocked swizzled tile
+template <int BM>
+__device__ __forceinline__ uint32_t tile_off(int r, int n) {
+  const int kb = n >> 5, e = n & 31;
+  return kb * BM * 64 + r * 64 + ((((e >> 3) ^ swz(r)) << 4) | (((e >> 2) & 1) << 3));
+}
+
+template <int MID, bool NEXT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) void conv_chain_kernel(
+    const ChainParams p) {
+  using Cfg = ChainCfg<MID>;
+  constexpr int WM = Cfg::WM, BM = Cfg::BM, STAGES = Cfg::STAGES, CA = Cfg::CA, CB = Cfg::CB, NB = Cfg::NB;
+  constexpr int C4 = 4 * MID;
+  extern __shared__ __attribute__((aligned(1024))) uint8_t smem[];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave % WM;
+  const int wn = wave / WM;
+  const int m0 = xcd_remap(blockIdx.x, gridDim.x) * BM;
+  const uint32_t sb = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(smem));
+  const uint32_t PX = sb, CH = sb + Cfg::PX_BYTES;
+  uint8_t* const t2buf = smem;                      // [BM x MID] T2 (then T1' staging)
+  uint8_t* const ybuf = smem + Cfg::TILE;           // [BM x MID] residual chunk -> Y chunk
+  const uint16_t* const zero = p.zero;
+  const int lg = lane >> 4;
+
+  const int rin = lane >> 2;
+  const int c = (lane & 3) ^ swz(rin);
+  const int frow = lane & 15;
+  const uint32_t fofs = frow * 64 + ((((lane >> 4) ^ swz(frow)) << 4));  // fragment byte offset in a 16-row block
+
+  // ================= phase A: T2 = relu(conv3x3(T1) + b2), K1 main loop (GATHER_TAP) =================
+  f32x4_t acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  {
+    const int OHW = p.OH * p.OW;
+    int ih0[CA], iw0[CA];
+    const uint16_t* rowp[CA];
+#pragma unroll
+    for (int i = 0; i < CA; ++i) {
+      const int m = m0 + 16 * (wave + 4 * i) + rin;
+      if (m < p.M) {
+        const int img = m / OHW;
+        const int rem = m - img * OHW;
+        const int oh = rem / p.OW;
+        const int ow = rem - oh * p.OW;
+        ih0[i] = oh * p.stride - 1;
+        iw0[i] = ow * p.stride - 1;
+        rowp[i] = p.x + (static_cast<long>(img) * p.H * p.W + static_cast<long>(ih0[i]) * p.W + iw0[i]) * p.ldx +
+                  8 * c;
+      } else {
+        ih0[i] = -(1 << 28);
+        iw0[i] = 0;
+        rowp[i] = nullptr;
+      }
+    }
+    TapWalk tw;
+    const int rowjump = (p.W - 3) * p.ldx;
+    const uint16_t* const wsrc = p.w2 + static_cast<long>(16 * wave + rin) * p.kpad2 + 8 * c;
+    const long wstep = 64L * p.kpad2;
+    constexpr int NKA = 9 * MID / BK;  // even: MID % 64 == 0
+
+    auto issue_a = [&](int kt) {
+      const uint32_t xs = PX + (kt % STAGES) * BM * 64;
+      const uint32_t ws = CH + (kt % STAGES) * MID * 64;
+      const int toff = tw.off;
+      const bool tap_ok = tw.kh < 3;
+#pragma unroll
+      for (int i = 0; i < CA; ++i) {
+        const bool ok = tap_ok && static_cast<unsigned>(ih0[i] + tw.kh) < static_cast<unsigned>(p.H) &&
+                        static_cast<unsigned>(iw0[i] + tw.kw) < static_cast<unsigned>(p.W);
+        glds16(ok ? static_cast<const void*>(rowp[i] + toff) : zero, xs + 16 * (wave + 4 * i) * 64);
+      }
+      tw.next(BK, MID, 3, p.ldx, rowjump);
+      const bool live = kt < NKA;
+#pragma unroll
+      for (int i = 0; i < CB; ++i)
+        glds16(live ? static_cast<const void*>(wsrc + i * wstep + kt * BK) : zero, ws + 16 * (wave + 4 * i) * 64);
+    };
+
+    bf16x8_t fw0[4], fx0[4], fw1[4], fx1[4];
+#define KC_READ(FW, FX, KT)                                                                             \
+  {                                                                                                     \
+    const uint8_t* x_ = smem + ((KT) % STAGES) * BM * 64 + (wm * 64) * 64 + fofs;                       \
+    const uint8_t* w_ = smem + Cfg::PX_BYTES + ((KT) % STAGES) * MID * 64 + (wn * 64) * 64 + fofs;      \
+    _Pragma("unroll") for (int j = 0; j < 4; ++j) FW[j] = *reinterpret_cast<const bf16x8_t*>(w_ + j * 1024); \
+    _Pragma("unroll") for (int i = 0; i < 4; ++i) FX[i] = *reinterpret_cast<const bf16x8_t*>(x_ + i * 1024); \
+  }
+#define KC_STEP(KT, FWC, FXC, FWN, FXN)                                                                 \
+  {                                                                                                     \
+    const int kt_ = (KT);                                                                               \
+    wait_vmcnt<(STAGES - 3) * (CA + CB)>();                                                             \
+    lds_barrier();                                                                                      \
+    KC_READ(FWN, FXN, kt_ + 1)                                                                          \
+    _Pragma("unroll") for (int i = 0; i < 4; ++i)                                                       \
+      _Pragma("unroll") for (int j = 0; j < 4; ++j)                                                     \
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(FWC[j], FXC[i], acc[i][j], 0, 0, 0);        \
+    issue_a(kt_ + STAGES - 1);                                                                          \
+  }
+#pragma unroll
+    for (int s = 0; s < STAGES - 1; ++s) issue_a(s);
+    wait_vmcnt<(STAGES - 2) * (CA + CB)>();
+    lds_barrier();
+    KC_READ(fw0, fx0, 0)
+    for (int kt = 0; kt < NKA; kt += 2) {
+      KC_STEP(kt, fw0, fx0, fw1, fx1)
+      KC_STEP(kt + 1, fw1, fx1, fw0, fx0)
+    }
+    wait_vmcnt<0>();
+    lds_barrier();  // ring idle: every wave finished its reads, every DMA landed
+#undef KC_STEP
+#undef KC_READ
+  }
+
+  // ================= phases B / C: weights-only DMA stream =================
+  // step t: pass t / SP; within a pass NB steps of W3 rows [p*MID, +MID) (B), then NB steps of
+  // W1' columns [p*MID, +MID) (C).
+  constexpr int SP = NEXT ? 2 * NB : NB;
+  constexpr int NW = 4 * SP;
+  const int wrow = 16 * wave + rin;  // + 64*i
+  int ops = 0;                       // vector-memory ops this wave issued since the phase-A drain
+  int stage_end[NW];                 // ops count right after stage t was issued
+  auto issue_w = [&](int t) {
+    if (t >= NW) return;
+    const int pp = t / SP, r = t % SP;
+    const uint32_t ws = CH + (t % STAGES) * MID * 64;
+    if (r < NB) {
+      const uint16_t* src = p.w3 + static_cast<long>(pp * MID + wrow) * p.kpad3 + r * BK + 8 * c;
+#pragma unroll
+      for (int i = 0; i < CB; ++i) glds16(src + i * 64L * p.kpad3, ws + 16 * (wave + 4 * i) * 64);
+    } else {
+      const uint16_t* src = p.w1n + static_cast<long>(wrow) * p.kpad1n + pp * MID + (r - NB) * BK + 8 * c;
+#pragma unroll
+      for (int i = 0; i < CB; ++i) glds16(src + i * 64L * p.kpad1n, ws + 16 * (wave + 4 * i) * 64);
+    }
+    ops += CB;
+    stage_end[t] = ops;
+  };
+#pragma unroll
+  for (int t = 0; t < STAGES - 1; ++t) issue_w(t);
+
+  const float lo = 0.f;
+  // T2 epilogue: + b2, ReLU, bf16 -> t2buf
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = wm * 64 + 16 * i + (lane & 15);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = wn * 64 + 16 * j + 4 * (lane >> 4);
+      const f32x4_t b = bias4(p.b2 + wn * 64 + 16 * j, lg);
+      *reinterpret_cast<uint2*>(t2buf + tile_off<BM>(r, n)) =
+          make_uint2(pack_bf16x2(fmaxf(acc[i][j][0] + b[0], lo), fmaxf(acc[i][j][1] + b[1], lo)),
+                     pack_bf16x2(fmaxf(acc[i][j][2] + b[2], lo), fmaxf(acc[i][j][3] + b[3], lo)));
+    }
+  }
+
+  f32x4_t accn[4][4];  // T1' accumulators (NEXT), live across the four passes
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) accn[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  // one B or C segment: NB weight steps t0.., the pixel operand from a K-blocked tile in LDS. Per step:
+  // wait for the step's stage, barrier (which also orders the refill below: the DMA of step t goes into
+  // the slot of stage t-1, which every wave has finished reading), fragments, MFMAs. Single-buffered
+  // fragments (the register budget holds two 64x64 accumulator tiles); the second workgroup on the CU
+  // covers the LDS latency.
+  auto segment = [&](f32x4_t (&a)[4][4], const uint8_t* xt, int t0) {
+#pragma unroll
+    for (int kk = 0; kk < NB; ++kk) {
+      const int t = t0 + kk;
+      wait_vmcnt_n(ops - stage_end[t]);
+      lds_barrier();
+      bf16x8_t fw[4], fx[4];
+      const uint8_t* w_ = smem + Cfg::PX_BYTES + (t % STAGES) * MID * 64 + (wn * 64) * 64 + fofs;
+      const uint8_t* x_ = xt + kk * BM * 64 + (wm * 64) * 64 + fofs;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fw[j] = *reinterpret_cast<const bf16x8_t*>(w_ + j * 1024);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fx[i] = *reinterpret_cast<const bf16x8_t*>(x_ + i * 1024);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          a[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[j], fx[i], a[i][j], 0, 0, 0);
+      issue_w(t + STAGES - 1);
+    }
+  };
+
+  // 16-B copy-out of a [BM x MID] K-blocked tile to rows m0.. of a [M x ld] bf16 matrix. Every store is
+  // unconditional (tail rows go to the sink) so the wave's vmcnt bookkeeping stays exact; the row bases
+  // are computed once per matrix and each pass adds its column offset as an immediate.
+  constexpr int CPR = MID / 8;  // 16-B chunks per row
+  auto row_bases = [&](uint16_t* dst, int ld, uint16_t* (&base)[Cfg::NS]) {
+#pragma unroll
+    for (int e = 0; e < Cfg::NS; ++e) {
+      const int g = tid + 256 * e;
+      const int r = g / CPR, cq = g % CPR;
+      base[e] = m0 + r < p.M ? dst + static_cast<long>(m0 + r) * ld + 8 * cq : p.sink;
+    }
+  };
+  auto copy_out = [&](const uint8_t* tile, uint16_t* const (&base)[Cfg::NS], int coff) {
+#pragma unroll
+    for (int e = 0; e < Cfg::NS; ++e) {
+      const int g = tid + 256 * e;
+      const int r = g / CPR, cq = g % CPR;
+      const uint4 v = *reinterpret_cast<const uint4*>(tile + (cq >> 2) * BM * 64 + r * 64 + (((cq & 3) ^ swz(r)) << 4));
+      *reinterpret_cast<uint4*>(base[e] + coff) = v;
+    }
+    ops += Cfg::NS;
+  };
+  uint16_t* ybase[Cfg::NS];
+  row_bases(p.y, C4, ybase);
+
+  // the four passes, unrolled by hand (a generic lambda per compile-time pass index) so every vmcnt
+  // count and ring slot below is a constant
+  auto pass = [&](auto ppc) {
+    constexpr int pp = decltype(ppc)::value;
+    if constexpr (pp > 0) copy_out(ybuf, ybase, (pp - 1) * MID);
+    lds_barrier();  // T2 / previous Y chunk fully consumed (and T2 visible at pass 0)
+    // residual chunk R_pp -> ybuf (K-blocked swizzled layout, 16-B DMA rows)
+#pragma unroll
+    for (int s = 0; s < Cfg::NR; ++s) {
+      const int q = wave + 4 * s;
+      const int kb = q / (BM / 16), rb = q % (BM / 16);
+      const int row = rb * 16 + rin;
+      // rows past M re-read row M-1 (never stored): no pointer select, one base for all passes
+      const void* src = p.res + static_cast<long>(min(m0 + row, p.M - 1)) * C4 + pp * MID + kb * BK + 8 * c;
+      glds16(src, sb + Cfg::TILE + kb * BM * 64 + rb * 16 * 64);
+    }
+    ops += Cfg::NR;
+    const int r_end = ops;
+
+    f32x4_t accb[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) accb[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    segment(accb, t2buf, pp * SP);
+
+    wait_vmcnt_n(ops - r_end);
+    lds_barrier();  // residual chunk visible
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = wm * 64 + 16 * i + (lane & 15);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = wn * 64 + 16 * j + 4 * (lane >> 4);
+        const f32x4_t b = bias4(p.b3 + pp * MID + wn * 64 + 16 * j, lg);
+        uint2* yp = reinterpret_cast<uint2*>(ybuf + tile_off<BM>(r, n));
+        const uint2 rv = *yp;
+        float r0, r1, r2, r3;
+        unpack_bf16x2(rv.x, r0, r1);
+        unpack_bf16x2(rv.y, r2, r3);
+        *yp = make_uint2(pack_bf16x2(fmaxf(accb[i][j][0] + b[0] + r0, lo), fmaxf(accb[i][j][1] + b[1] + r1, lo)),
+                         pack_bf16x2(fmaxf(accb[i][j][2] + b[2] + r2, lo), fmaxf(accb[i][j][3] + b[3] + r3, lo)));
+      }
+    }
+    if constexpr (NEXT) {
+      segment(accn, ybuf, pp * SP + NB);  // its first barrier publishes the Y chunk
+    } else {
+      lds_barrier();
+    }
+  };
+  pass(std::integral_constant<int, 0>{});
+  pass(std::integral_constant<int, 1>{});
+  pass(std::integral_constant<int, 2>{});
+  pass(std::integral_constant<int, 3>{});
+  copy_out(ybuf, ybase, 3 * MID);
+
+  if constexpr (NEXT) {
+    // T1' epilogue through the (now idle) T2 buffer, then 16-B copy-out
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = wm * 64 + 16 * i + (lane & 15);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = wn * 64 + 16 * j + 4 * (lane >> 4);
+        const f32x4_t b = bias4(p.b1n + wn * 64 + 16 * j, lg);
+        *reinterpret_cast<uint2*>(t2buf + tile_off<BM>(r, n)) =
+            make_uint2(pack_bf16x2(fmaxf(accn[i][j][0] + b[0], lo), fmaxf(accn[i][j][1] + b[1], lo)),
+                       pack_bf16x2(fmaxf(accn[i][j][2] + b[2], lo), fmaxf(accn[i][j][3] + b[3], lo)));
+      }
+    }
+    lds_barrier();
+    uint16_t* tbase[Cfg::NS];
+    row_bases(p.t1n, MID, tbase);
+    copy_out(t2buf, tbase, 0);
+  }
+}
+
+template <int MID, bool NEXT>
+int launch_chain(const ChainParams& p, hipStream_t s) {
+  using Cfg = ChainCfg<MID>;
+  static bool attr = false;
+  if (!attr) {
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(conv_chain_kernel<MID, NEXT>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, Cfg::LDS) != hipSuccess)
+      return AI4E_ELAUNCH;
+    attr = true;
+  }
+  const int nb = ai4e_cdiv(p.M, Cfg::BM);
+  hipLaunchKernelGGL((conv_chain_kernel<MID, NEXT>), dim3(nb), dim3(256), Cfg::LDS, s, p);
+  return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
+}
+
+template <typename T>
+T* symbol_ptr(const void* sym) {
+  void* a = nullptr;
+  return hipGetSymbolAddress(&a, sym) == hipSuccess ? static_cast<T*>(a) : nullptr;
+}
+
+}  // namespace
+
+// Fused bottleneck chain (see header). x: T1 NHWC [N,H,W,ldx] bf16 (MID channels at offset 0);
+// w2 [>=MID rows, kpad2 >= 9*MID] (k = (kh, kw, c)); w3 [>=4*MID rows, kpad3 >= MID];
+// w1n [>=MID rows, kpad1n >= 4*MID] (nullptr: no next block, t1n unused); res, y [M, 4*MID];
+// t1n [M, MID]. 3x3, pad 1, stride 1 or 2. MID in {64, 128, 256}.
+AI4E_API int ai4e_conv_chain_fwd(const void* x, const void* w2, const void* b2, const void* w3, const void* b3,
+                                 const void* res, void* y, const void* w1n, const void* b1n, void* t1n, int N, int H,
+                                 int W, int ldx, int mid, int stride, int kpad2, int kpad3, int kpad1n,
+                                 hipStream_t stream) {
+  if ((mid != 64 && mid != 128 && mid != 256) || ldx % 8 || ldx < mid || kpad2 < 9 * mid || kpad2 % 64 ||
+      kpad3 < mid || kpad3 % 8 || (stride != 1 && stride != 2) || !x || !w2 || !b2 || !w3 || !b3 || !res || !y ||
+      (w1n && (!b1n || !t1n || kpad1n < 4 * mid || kpad1n % 8)))
+    return AI4E_EINVAL;
+  ChainParams p{};
+  p.x = static_cast<const uint16_t*>(x);
+  p.w2 = static_cast<const uint16_t*>(w2);
+  p.b2 = static_cast<const float*>(b2);
+  p.w3 = static_cast<const uint16_t*>(w3);
+  p.b3 = static_cast<const float*>(b3);
+  p.res = static_cast<const uint16_t*>(res);
+  p.y = static_cast<uint16_t*>(y);
+  p.w1n = static_cast<const uint16_t*>(w1n);
+  p.b1n = static_cast<const float*>(b1n);
+  p.t1n = static_cast<uint16_t*>(t1n);
+  static const uint16_t* zero_p = symbol_ptr<const uint16_t>(HIP_SYMBOL(g_chain_zero));
+  static uint16_t* sink_p = symbol_ptr<uint16_t>(HIP_SYMBOL(g_chain_sink));
+  p.zero = zero_p;
+  p.sink = sink_p;
+  if (!p.zero || !p.sink) return AI4E_ELAUNCH;
+  p.H = H; p.W = W; p.ldx = ldx; p.stride = stride;
+  p.OH = (H + 2 - 3) / stride + 1;
+  p.OW = (W + 2 - 3) / stride + 1;
+  p.M = N * p.OH * p.OW;
+  p.kpad2 = kpad2; p.kpad3 = kpad3; p.kpad1n = kpad1n;
+  if (p.M <= 0) return AI4E_OK;
+  const bool next = w1n != nullptr;
+  switch (mid) {
+    case 64: return next ? launch_chain<64, true>(p, stream) : launch_chain<64, false>(p, stream);
+    // MID 128/256 with the chained c1' exceed the 256-VGPR budget of two waves per SIMD: not built
+    case 128: return next ? AI4E_EINVAL : launch_chain<128, false>(p, stream);
+    default: return next ? AI4E_EINVAL : launch_chain<256, false>(p, stream);
+  }
+}

@@ -31,11 +31,15 @@
 //   by the preprocess kernel). The residual tile is prefetched into registers before the K loop.
 // * XCD-aware tile order: tiles that share an activation panel (same m-tile, different n-tiles)
 //   land on one XCD's L2 (common.h xcd_remap).
-#include "common.h"
+#include "conv_common.h"
 
 namespace {
 
-constexpr int BK = 32;
+constexpr int BK = ai4e_conv::BK;
+using ai4e_conv::glds16;
+using ai4e_conv::swz;
+using ai4e_conv::TapWalk;
+using ai4e_conv::wait_vmcnt;
 
 // Source of the zero 16-B chunks the DMA gather reads for padding / out-of-range taps.
 __device__ __attribute__((aligned(64))) uint16_t g_zero_chunk[32];
@@ -55,49 +59,6 @@ struct ConvParams {
   int M;
   int ntiles_n;
   const uint16_t* zero;  // >= 16 zero bytes: source of the DMA gather for padding taps
-};
-
-__device__ __forceinline__ int swz(int row) { return (0x78 >> (2 * ((row >> 2) & 3))) & 3; }
-
-// One 16-B LDS-DMA per lane: global -> LDS at (wave-uniform M0 base + 16*lane). Inline asm so hipcc
-// neither drains it with vmcnt(0) before every ds_read nor at barriers (cdna guide §5.7, §5 "Pipelining
-// across barriers"); completion is tracked by hand with counted vmcnt.
-__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_base) {
-  uint32_t keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %2\n\t"
-      "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, off\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(gsrc), "s"(lds_base)
-      : "memory");
-}
-
-template <int N>
-__device__ __forceinline__ void wait_vmcnt() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
-// Wave-uniform (SGPR) walk over the taps of a conv whose K tiles never straddle a tap
-// (C % step == 0): (kh, kw, channel base cb) and the element offset (kh*W + kw)*ldx + cb, kept up to
-// date with adds only (no per-step multiplies or divisions on the scalar unit).
-struct TapWalk {
-  int kh = 0, kw = 0, cb = 0, off = 0;
-  __device__ __forceinline__ void next(int step, int C, int KW, int ldx, int rowjump) {
-    cb += step;
-    off += step;
-    if (cb == C) {
-      cb = 0;
-      off += ldx - C;
-      if (++kw == KW) {
-        kw = 0;
-        ++kh;
-        off += rowjump;  // (W - KW) * ldx
-      }
-    }
-  }
 };
 
 // Gather modes of the activation operand.

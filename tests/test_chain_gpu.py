@@ -1,0 +1,83 @@
+"""K1c fused bottleneck chain (csrc/kernels/conv_chain.hip) vs a PyTorch fp32 reference of the same
+three convs (GPU box only). Intermediates are rounded to bf16 where the kernel rounds them (T2 in LDS,
+Y before the chained 1x1)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+from aiforearth_api_platform_amd.ops import _ext
+from aiforearth_api_platform_amd.ops.conv import chain_supported, conv_chain, pack_conv
+
+DEV = "cuda"
+
+
+@pytest.fixture(autouse=True, scope="module")
+def _lib():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    _ext.lib()
+
+
+def _wq(pc, k):
+    return pc.w_packed[:pc.cout, :k * k * pc.cin_pad].float().reshape(pc.cout, k, k, pc.cin_pad).permute(0, 3, 1, 2)
+
+
+def _conv(x, w, b, stride=1, pad=0):
+    return F.conv2d(x.float().permute(0, 3, 1, 2), w, b, stride=stride, padding=pad).permute(0, 2, 3, 1)
+
+
+CASES = [
+    # n, h, w, mid, stride, next
+    (2, 56, 56, 64, 1, True),
+    (2, 56, 56, 64, 1, False),
+    (1, 15, 13, 64, 1, True),     # M = 195: one partial tile
+    (3, 9, 11, 64, 2, True),      # strided 3x3, ragged
+    (2, 28, 28, 128, 1, False),
+    (2, 28, 28, 128, 2, False),
+    (2, 14, 14, 256, 1, False),
+    (1, 7, 9, 256, 2, False),
+]
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_conv_chain(case):
+    n, h, w, mid, s, nxt = case
+    assert chain_supported(mid, nxt)
+    torch.manual_seed(7)
+    c2 = pack_conv(torch.randn(mid, mid, 3, 3) / (9 * mid) ** 0.5, torch.randn(mid) * 0.1, stride=s, pad=1).to(DEV)
+    c3 = pack_conv(torch.randn(4 * mid, mid, 1, 1) / mid ** 0.5, torch.randn(4 * mid) * 0.1).to(DEV)
+    c1n = pack_conv(torch.randn(mid, 4 * mid, 1, 1) / (4 * mid) ** 0.5, torch.randn(mid) * 0.1).to(DEV) if nxt else None
+    t1 = torch.randn(n, h, w, mid, device=DEV).relu().to(torch.bfloat16)
+    oh, ow = c2.out_hw(h, w)
+    res = torch.randn(n, oh, ow, 4 * mid, device=DEV).to(torch.bfloat16)
+    y, t1n = conv_chain(t1, c2, c3, res, c1n=c1n)
+    torch.cuda.synchronize()
+
+    t2 = F.relu(_conv(t1, _wq(c2, 3), c2.bias[:mid], s, 1)).to(torch.bfloat16)
+    yr = F.relu(_conv(t2, _wq(c3, 1), c3.bias[:4 * mid]) + res.float())
+    err = (y.float() - yr).abs().max().item()
+    assert err <= 0.02 * yr.abs().max().item() + 0.03, err
+    if nxt:
+        tr = F.relu(_conv(y, _wq(c1n, 1), c1n.bias[:mid]))
+        err = (t1n.float() - tr).abs().max().item()
+        assert err <= 0.02 * tr.abs().max().item() + 0.03, err
+    else:
+        assert t1n is None
+
+
+def test_resnet_chain_matches_unfused(monkeypatch):
+    """FusedResNet with K1c chains == the per-conv K1 graph (same weights, same input)."""
+    from aiforearth_api_platform_amd.models.resnet import FusedResNet, resnet50
+
+    torch.manual_seed(0)
+    m = FusedResNet(resnet50(seed=1), device=DEV)
+    img = torch.randint(0, 256, (4, 224, 224, 3), dtype=torch.uint8, device=DEV)
+    m.chain = True
+    a = m.forward_u8(img)
+    m.chain = False
+    b = m.forward_u8(img)
+    torch.cuda.synchronize()
+    assert (a - b).abs().max().item() <= 0.05 * b.abs().max().item() + 1e-3
+    assert (a.argmax(1) == b.argmax(1)).float().mean().item() >= 0.75
