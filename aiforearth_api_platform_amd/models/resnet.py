@@ -19,7 +19,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ..ops.conv import PackedConv, conv2d_nhwc, conv_chain, fold_bn, pack_conv, pack_stem_s2d
+from ..ops.conv import PackedConv, conv2d_nhwc, conv_chain, fold_bn, pack_conv, pack_stem_s2d, stem_pool
 from ..ops.pool import (global_avgpool_nhwc, maxpool2d_nhwc, preprocess_s2d_u8, preprocess_u8,
                         space_to_depth_shifted)
 
@@ -187,7 +187,7 @@ class FusedResNet:
         return space_to_depth_shifted(x[..., : self.in_ch])
 
     def _stem(self, x: torch.Tensor) -> torch.Tensor:
-        return maxpool2d_nhwc(conv2d_nhwc(self.stem_input(x), self.stem, relu=True), 3, 2, 1)
+        return stem_pool(self.stem_input(x), self.stem)  # K1s: conv + bias + ReLU + 3x3/2 max-pool
 
     @staticmethod
     def _block(x: torch.Tensor, blk, out: Optional[torch.Tensor] = None) -> torch.Tensor:

@@ -152,19 +152,27 @@ def _conv_hip(x, pc, residual, relu, out, out_coff, tile_cfg):
               oh, ow, pc.cout, pc.kpad, ldy, out_coff, ldres, int(relu), tile_cfg, _ext.stream_ptr(x.device))
 
 
-def chain_supported(mid: int, has_next: bool) -> bool:
+def chain_kernel_builds(mid: int, has_next: bool) -> bool:
     """Shapes the fused bottleneck-chain kernel K1c is built for (csrc/kernels/conv_chain.hip)."""
     return mid == 64 or (not has_next and mid in (128, 256))
 
 
+def chain_supported(mid: int, has_next: bool) -> bool:
+    """Shapes ``conv_chain`` routes to K1c by default."""
+    # measured (profiles/r1_chain): only the 64-channel stage gains; the 128/256 variants (no chained c1',
+    # 1 workgroup per CU, weight re-streaming per 64-128-pixel tile) were slower than two K1 launches
+    return mid == 64
+
+
 def conv_chain(t1: torch.Tensor, c2: PackedConv, c3: PackedConv, residual: torch.Tensor,
-               c1n: Optional[PackedConv] = None, out: Optional[torch.Tensor] = None):
+               c1n: Optional[PackedConv] = None, out: Optional[torch.Tensor] = None, force: bool = False):
     """Fused bottleneck tail (K1c): ``y = relu(c3(relu(c2(t1))) + residual)`` and, with ``c1n`` (the next
     block's 1x1 reduce), ``t1n = relu(c1n(y))`` from the same kernel. Returns ``(y, t1n or None)``.
 
     ``t1``: NHWC ``[N,H,W,mid]`` bf16 (c1's output), ``c2`` 3x3/pad 1 (stride 1 or 2) mid->mid, ``c3`` 1x1
     mid->4*mid, ``residual`` ``[N,OH,OW,4*mid]``, ``c1n`` 1x1 4*mid->mid. Shapes the kernel does not cover
-    (``chain_supported``) and the PyTorch backend run the three convs separately.
+    (``chain_supported``; ``force`` = every shape the kernel builds) and the PyTorch backend run the
+    three convs separately.
     """
     n, h, w, mid = t1.shape
     if (c2.kh, c2.kw, c2.pad, c2.cin_pad, c2.cout) != (3, 3, 1, mid, mid) or c3.kh != 1 or c3.cin_pad != mid \
@@ -173,7 +181,8 @@ def conv_chain(t1: torch.Tensor, c2: PackedConv, c3: PackedConv, residual: torch
     oh, ow = c2.out_hw(h, w)
     if out is None:
         out = torch.empty(n, oh, ow, 4 * mid, device=t1.device, dtype=t1.dtype)
-    if _ext.backend_for(t1) != "hip" or not chain_supported(mid, c1n is not None):
+    ok = chain_kernel_builds if force else chain_supported
+    if _ext.backend_for(t1) != "hip" or not ok(mid, c1n is not None):
         y2 = conv2d_nhwc(t1, c2, relu=True)
         conv2d_nhwc(y2, c3, residual=residual, relu=True, out=out)
         return out, (conv2d_nhwc(out, c1n, relu=True) if c1n is not None else None)
@@ -188,6 +197,22 @@ def conv_chain(t1: torch.Tensor, c2: PackedConv, c3: PackedConv, residual: torch
               _ext.ptr(t1n), n, h, w, mid, mid, c2.stride, c2.kpad, c3.kpad, c1n.kpad if c1n is not None else 0,
               _ext.stream_ptr(t1.device))
     return out, t1n
+
+
+def stem_pool(x: torch.Tensor, pc: PackedConv) -> torch.Tensor:
+    """Fused s2d stem (K1s): ``maxpool3x3/2(relu(conv4x4(x) + b))`` in one kernel; ``x`` = the
+    ``[N,H,W,16]`` space-to-depth input, ``pc`` from ``pack_stem_s2d``. PyTorch backend: the two ops."""
+    from .pool import maxpool2d_nhwc
+
+    n, h, w, c = x.shape
+    if _ext.backend_for(x) != "hip" or pc.cout != 64 or c != 16 or (pc.kh, pc.kw, pc.pad, pc.pad_hi) != (4, 4, 1, 2):
+        return maxpool2d_nhwc(conv2d_nhwc(x, pc, relu=True), 3, 2, 1)
+    if x.dtype != torch.bfloat16 or not x.is_contiguous():
+        raise ValueError("stem_pool: contiguous bf16 [N,H,W,16] input required")
+    y = torch.empty(n, (h - 1) // 2 + 1, (w - 1) // 2 + 1, 64, device=x.device, dtype=x.dtype)
+    _ext.call("ai4e_stem_pool_fwd", x.data_ptr(), pc.w_packed.data_ptr(), pc.bias.data_ptr(), y.data_ptr(), n, h, w,
+              pc.kpad, _ext.stream_ptr(x.device))
+    return y
 
 
 def _conv_torch(x, pc, residual, relu):

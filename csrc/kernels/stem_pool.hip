@@ -1,0 +1,195 @@
+// K1s — ResNet stem: the space-to-depth 4x4/1 conv (BN folded, + bias, ReLU) fused with the 3x3/2 pad-1
+// max-pool that follows it. The 112x112x64 stem activation (411 MB at batch 256) never reaches HBM.
+//
+// Each workgroup owns a 7 x 8 tile of POOLED outputs of one image; the conv region that tile's pooling
+// windows cover is 15 x 17 = 255 conv pixels (recompute factor 255/224 = 1.14 over the unfused conv).
+// Those 255 (+1 idle) pixels are the M rows of one 256 x 64 implicit-GEMM tile on MFMA
+// (v_mfma_f32_16x16x32_bf16, 4 wave64s x 64 pixels, the K1 LDS-DMA ring with counted vmcnt). The
+// epilogue writes relu(acc + b) as bf16 into LDS (conv pixels outside the image write 0: post-ReLU
+// values are >= 0, so a 0 never wins a max over a window that always holds a real pixel), then every
+// thread max-reduces 3x3 windows of 16-B channel chunks (integer max on the bf16 bits: non-negative bf16
+// order like unsigned integers) and stores 16-B pooled chunks.
+//
+// Input: the s2d layout of preprocess_s2d (ops/pool.py) [N, H, W, 16] bf16, K = (kh, kw, c) = 4x4x16 = 256
+// padded top/left 1 (bottom/right 2: bounds-checked). Output [N, PH, PW, 64], PH = ceil(H/2).
+#include "conv_common.h"
+
+namespace {
+
+using ai4e_conv::BK;
+using ai4e_conv::glds16;
+using ai4e_conv::swz;
+using ai4e_conv::wait_vmcnt;
+
+__device__ __attribute__((aligned(64))) uint16_t g_stem_zero[32];
+
+constexpr int SP_TR = 7, SP_TC = 8;                        // pooled tile
+constexpr int SP_RR = 2 * SP_TR + 1, SP_RC = 2 * SP_TC + 1;  // conv region 15 x 17
+constexpr int SP_STAGES = 4;
+constexpr int SP_BM = 256, SP_BN = 64, SP_C = 16, SP_NK = 256 / BK;  // 8 K steps
+
+struct StemParams {
+  const uint16_t* x;   // [N, H, W, 16]
+  const uint16_t* w;   // [>= 64 rows, kpad >= 256]
+  const float* bias;   // [64]
+  uint16_t* y;         // [N, PH, PW, 64]
+  const uint16_t* zero;
+  int H, W, PH, PW, kpad, tiles_r, tiles_c;
+};
+
+__device__ __forceinline__ uint32_t max_bf16x2(uint32_t a, uint32_t b) {
+  // both halves non-negative bf16: unsigned 16-bit max per half
+  const uint32_t lo = max(a & 0xffffu, b & 0xffffu), hi = max(a >> 16, b >> 16);
+  return lo | (hi << 16);
+}
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) void stem_pool_kernel(const StemParams p) {
+  constexpr int STAGE_ELEMS = (SP_BM + SP_BN) * BK;
+  __shared__ __attribute__((aligned(1024))) uint16_t smem[SP_STAGES * STAGE_ELEMS];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int per_img = p.tiles_r * p.tiles_c;
+  const int t = xcd_remap(blockIdx.x, gridDim.x);
+  const int img = t / per_img;
+  const int tr = (t - img * per_img) / p.tiles_c;
+  const int tc = t - img * per_img - tr * p.tiles_c;
+  const int ph0 = tr * SP_TR, pw0 = tc * SP_TC;
+  const int oh0 = 2 * ph0 - 1, ow0 = 2 * pw0 - 1;  // conv region origin
+
+  // DMA lanes: row rin of a 16-row block, logical 8-element chunk c of the 32-wide K step
+  const int rin = lane >> 2;
+  const int c = (lane & 3) ^ swz(rin);
+  int ihb[4], iwb[4];
+  const uint16_t* const xi = p.x + static_cast<long>(img) * p.H * p.W * SP_C;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = 16 * (wave + 4 * i) + rin;
+    const int r = m / SP_RC, cc = m - r * SP_RC;
+    // conv pixel (oh0 + r, ow0 + cc); its tap (kh, kw) reads input (oh - 1 + kh, ow - 1 + kw)
+    const bool live = m < SP_RR * SP_RC && oh0 + r >= 0 && oh0 + r < p.H && ow0 + cc >= 0 && ow0 + cc < p.W;
+    ihb[i] = live ? oh0 + r - 1 : -(1 << 28);
+    iwb[i] = ow0 + cc - 1;
+  }
+  const uint16_t* const wsrc = p.w + static_cast<long>(16 * wave + rin) * p.kpad + 8 * c;
+  const uint32_t smem_base = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(smem));
+
+  // K step kt: kh = kt / 2, the chunk's tap kw = 2 * (kt % 2) + (c >> 1), channels 8 * (c & 1)
+  auto issue_stage = [&](int kt) {
+    const uint32_t sbase = smem_base + (kt % SP_STAGES) * STAGE_ELEMS * 2;
+    const int kh = kt >> 1, kw = 2 * (kt & 1) + (c >> 1);
+    const bool kt_ok = kt < SP_NK;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int ih = ihb[i] + kh, iw = iwb[i] + kw;
+      const bool ok = kt_ok && static_cast<unsigned>(ih) < static_cast<unsigned>(p.H) &&
+                      static_cast<unsigned>(iw) < static_cast<unsigned>(p.W);
+      glds16(ok ? static_cast<const void*>(xi + (static_cast<long>(ih) * p.W + iw) * SP_C + 8 * (c & 1)) : p.zero,
+             sbase + (16 * (wave + 4 * i)) * BK * 2);
+    }
+    glds16(kt_ok ? static_cast<const void*>(wsrc + kt * BK) : p.zero, sbase + (SP_BM + 16 * wave) * BK * 2);
+  };
+
+  f32x4_t acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const int frow = lane & 15;
+  const int fofs = frow * BK + (((lane >> 4) ^ swz(frow)) << 3);
+  constexpr int PER_STAGE = 5;
+
+#pragma unroll
+  for (int s = 0; s < SP_STAGES - 1; ++s) issue_stage(s);
+#pragma unroll
+  for (int kt = 0; kt < SP_NK; ++kt) {
+    // stage kt landed: the younger stages in flight are kt+1 .. min(kt+2, NK-1)
+    ai4e_conv::wait_vmcnt_n(PER_STAGE * min(SP_STAGES - 2, SP_NK - 1 - kt));
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    const uint16_t* st = smem + (kt % SP_STAGES) * STAGE_ELEMS;
+    bf16x8_t fw[4], fx[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) fw[j] = *reinterpret_cast<const bf16x8_t*>(st + (SP_BM + 16 * j) * BK + fofs);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) fx[i] = *reinterpret_cast<const bf16x8_t*>(st + (wave * 64 + 16 * i) * BK + fofs);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[j], fx[i], acc[i][j], 0, 0, 0);
+    if (kt + SP_STAGES - 1 < SP_NK) issue_stage(kt + SP_STAGES - 1);
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // ring idle
+
+  // ---- epilogue: bf16 relu(acc + b) -> LDS [256 px][64 ch] (128-B rows, 16-B chunk ^= px & 7)
+  uint8_t* const tile = reinterpret_cast<uint8_t*>(smem);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = wave * 64 + 16 * i + (lane & 15);
+    const int r = m / SP_RC, cc = m - r * SP_RC;
+    const bool live = m < SP_RR * SP_RC && oh0 + r >= 0 && oh0 + r < p.H && ow0 + cc >= 0 && ow0 + cc < p.W;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = 16 * j + 4 * (lane >> 4);
+      const float4 b = *reinterpret_cast<const float4*>(p.bias + n);
+      uint2 v = make_uint2(0u, 0u);
+      if (live)
+        v = make_uint2(pack_bf16x2(fmaxf(acc[i][j][0] + b.x, 0.f), fmaxf(acc[i][j][1] + b.y, 0.f)),
+                       pack_bf16x2(fmaxf(acc[i][j][2] + b.z, 0.f), fmaxf(acc[i][j][3] + b.w, 0.f)));
+      *reinterpret_cast<uint2*>(tile + m * 128 + ((((n >> 3) ^ (m & 7)) << 4) | (((n >> 2) & 1) << 3))) = v;
+    }
+  }
+  __syncthreads();
+  // ---- 3x3/2 max over the region: task = (pooled pixel q, 8-channel chunk k8)
+  for (int task = tid; task < SP_TR * SP_TC * 8; task += 256) {
+    const int q = task >> 3, k8 = task & 7;
+    const int py = q / SP_TC, px = q - py * SP_TC;
+    const int ph = ph0 + py, pw = pw0 + px;
+    if (ph >= p.PH || pw >= p.PW) continue;
+    uint4 mx = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+    for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+      for (int dx = 0; dx < 3; ++dx) {
+        const int m = (2 * py + dy) * SP_RC + 2 * px + dx;
+        const uint4 v = *reinterpret_cast<const uint4*>(tile + m * 128 + ((k8 ^ (m & 7)) << 4));
+        mx.x = max_bf16x2(mx.x, v.x);
+        mx.y = max_bf16x2(mx.y, v.y);
+        mx.z = max_bf16x2(mx.z, v.z);
+        mx.w = max_bf16x2(mx.w, v.w);
+      }
+    *reinterpret_cast<uint4*>(p.y + ((static_cast<long>(img) * p.PH + ph) * p.PW + pw) * SP_BN + 8 * k8) = mx;
+  }
+}
+
+}  // namespace
+
+// x: s2d stem input [N, H, W, 16] bf16; w: packed 4x4x16 stem weights [>= 64 rows, kpad >= 256] (pad 1/2,
+// ops/conv.py pack_stem_s2d); bias [>= 64] fp32; y: [N, ceil(H/2), ceil(W/2), 64] bf16.
+AI4E_API int ai4e_stem_pool_fwd(const void* x, const void* w, const void* bias, void* y, int N, int H, int W, int kpad,
+                                hipStream_t stream) {
+  if (!x || !w || !bias || !y || kpad < 256 || kpad % 8 || H <= 0 || W <= 0) return AI4E_EINVAL;
+  static const uint16_t* zero = nullptr;
+  if (!zero) {
+    void* a = nullptr;
+    if (hipGetSymbolAddress(&a, HIP_SYMBOL(g_stem_zero)) != hipSuccess) return AI4E_ELAUNCH;
+    zero = static_cast<const uint16_t*>(a);
+  }
+  StemParams p{};
+  p.x = static_cast<const uint16_t*>(x);
+  p.w = static_cast<const uint16_t*>(w);
+  p.bias = static_cast<const float*>(bias);
+  p.y = static_cast<uint16_t*>(y);
+  p.zero = zero;
+  p.H = H; p.W = W;
+  p.PH = (H - 1) / 2 + 1;
+  p.PW = (W - 1) / 2 + 1;
+  p.kpad = kpad;
+  p.tiles_r = ai4e_cdiv(p.PH, SP_TR);
+  p.tiles_c = ai4e_cdiv(p.PW, SP_TC);
+  const long nb = static_cast<long>(N) * p.tiles_r * p.tiles_c;
+  if (nb <= 0) return AI4E_OK;
+  hipLaunchKernelGGL(stem_pool_kernel, dim3(static_cast<unsigned>(nb)), dim3(256), 0, stream, p);
+  return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
+}

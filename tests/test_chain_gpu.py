@@ -8,7 +8,7 @@ import torch.nn.functional as F
 pytestmark = pytest.mark.gpu
 
 from aiforearth_api_platform_amd.ops import _ext
-from aiforearth_api_platform_amd.ops.conv import chain_supported, conv_chain, pack_conv
+from aiforearth_api_platform_amd.ops.conv import chain_kernel_builds, conv_chain, pack_conv
 
 DEV = "cuda"
 
@@ -44,7 +44,7 @@ CASES = [
 @pytest.mark.parametrize("case", CASES)
 def test_conv_chain(case):
     n, h, w, mid, s, nxt = case
-    assert chain_supported(mid, nxt)
+    assert chain_kernel_builds(mid, nxt)
     torch.manual_seed(7)
     c2 = pack_conv(torch.randn(mid, mid, 3, 3) / (9 * mid) ** 0.5, torch.randn(mid) * 0.1, stride=s, pad=1).to(DEV)
     c3 = pack_conv(torch.randn(4 * mid, mid, 1, 1) / mid ** 0.5, torch.randn(4 * mid) * 0.1).to(DEV)
@@ -52,7 +52,7 @@ def test_conv_chain(case):
     t1 = torch.randn(n, h, w, mid, device=DEV).relu().to(torch.bfloat16)
     oh, ow = c2.out_hw(h, w)
     res = torch.randn(n, oh, ow, 4 * mid, device=DEV).to(torch.bfloat16)
-    y, t1n = conv_chain(t1, c2, c3, res, c1n=c1n)
+    y, t1n = conv_chain(t1, c2, c3, res, c1n=c1n, force=True)
     torch.cuda.synchronize()
 
     t2 = F.relu(_conv(t1, _wq(c2, 3), c2.bias[:mid], s, 1)).to(torch.bfloat16)
@@ -81,3 +81,22 @@ def test_resnet_chain_matches_unfused(monkeypatch):
     torch.cuda.synchronize()
     assert (a - b).abs().max().item() <= 0.05 * b.abs().max().item() + 1e-3
     assert (a.argmax(1) == b.argmax(1)).float().mean().item() >= 0.75
+
+
+@pytest.mark.parametrize("shape", [(2, 112, 112), (3, 30, 26), (1, 17, 9)])
+def test_stem_pool(shape):
+    """K1s fused s2d stem conv + ReLU + 3x3/2 max-pool vs PyTorch fp32 (conv output rounded to bf16)."""
+    from aiforearth_api_platform_amd.ops.conv import pack_stem_s2d, stem_pool
+
+    n, h, w = shape
+    torch.manual_seed(5)
+    pc = pack_stem_s2d(torch.randn(64, 3, 7, 7) / 12, torch.randn(64) * 0.1).to(DEV)
+    x = torch.randn(n, h, w, 16, device=DEV).to(torch.bfloat16)
+    y = stem_pool(x, pc)
+    torch.cuda.synchronize()
+    xp = F.pad(x.float().permute(0, 3, 1, 2), (1, 2, 1, 2))
+    conv = F.relu(F.conv2d(xp, _wq(pc, 4), pc.bias[:64])).to(torch.bfloat16).float()
+    ref = F.max_pool2d(conv, 3, 2, 1).permute(0, 2, 3, 1)
+    assert y.shape == ref.shape
+    err = (y.float() - ref).abs().max().item()
+    assert err <= 0.02 * ref.abs().max().item() + 0.02, err
