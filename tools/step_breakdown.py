@@ -14,9 +14,9 @@ print("step span us %.1f, kernels %d" % (span, len(seg)))
 agg = collections.defaultdict(lambda: [0.0, 0])
 for r in seg:
     n = r["Kernel_Name"]
-    base = n.split("(")[0] if not n.startswith("void ") else n[5:].split("(")[0]
-    m = re.search(r"(\w+)<([^>]*)>", base)
-    k = (m.group(1) + "<" + m.group(2) + ">") if m else (base.split("::")[-1] or n.split("(")[0])
+    base = n.replace("(anonymous namespace)::", "")
+    base = base[5:] if base.startswith("void ") else base
+    k = base.split("(")[0]
     k = k.replace("(anonymous namespace)::", "")[:70]
     d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
     agg[k][0] += d
