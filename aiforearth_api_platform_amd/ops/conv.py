@@ -154,14 +154,12 @@ def _conv_hip(x, pc, residual, relu, out, out_coff, tile_cfg):
 
 def chain_kernel_builds(mid: int, has_next: bool) -> bool:
     """Shapes the fused bottleneck-chain kernel K1c is built for (csrc/kernels/conv_chain.hip)."""
-    return mid == 64 or (not has_next and mid in (128, 256))
+    return mid in (64, 128)
 
 
 def chain_supported(mid: int, has_next: bool) -> bool:
     """Shapes ``conv_chain`` routes to K1c by default."""
-    # measured (profiles/r1_chain): only the 64-channel stage gains; the 128/256 variants (no chained c1',
-    # 1 workgroup per CU, weight re-streaming per 64-128-pixel tile) were slower than two K1 launches
-    return mid == 64
+    return mid in (64, 128)
 
 
 def conv_chain(t1: torch.Tensor, c2: PackedConv, c3: PackedConv, residual: torch.Tensor,

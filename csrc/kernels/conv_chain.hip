@@ -37,8 +37,8 @@ using ai4e_conv::wait_vmcnt;
 using ai4e_conv::wait_vmcnt_n;
 
 __device__ __attribute__((aligned(64))) uint16_t g_chain_zero[32];
-// target of the masked-off tail stores: a row base (+ column offsets up to 4*256) must stay inside it
-__device__ __attribute__((aligned(64))) uint16_t g_chain_sink[1024 + 64];
+// target of the masked-off tail stores: a row base (+ column offsets up to 4*128) must stay inside it
+__device__ __attribute__((aligned(64))) uint16_t g_chain_sink[512 + 64];
 
 // LDS-ordering barrier: own LDS reads/writes retired, then s_barrier; an asm statement with a memory
 // clobber so hipcc moves no LDS access across it (the raw builtin is not a compiler memory barrier).
@@ -85,23 +85,32 @@ struct ChainParams {
 
 template <int MID>
 struct ChainCfg {
-  static constexpr int WN = MID / 64;         // waves along channels
-  static constexpr int WM = 4 / WN;           // waves along pixels
-  static constexpr int BM = WM * 64;          // pixels per workgroup
+  static constexpr int WN = MID / 64;         // phase A / C: waves along channels
+  static constexpr int WM = 4 / WN;           // phase A / C: waves along pixels
+  static constexpr int BM = WM * 64;          // pixels per workgroup (256 | 128)
   static constexpr int STAGES = 4;
-  static constexpr int CA = BM / 64;          // pixel-row DMAs per wave per phase-A stage
-  static constexpr int CB = MID / 64;         // weight-row DMAs per wave per stage
-  static constexpr int PX_RING = STAGES * BM * 64;
-  static constexpr int TILE = BM * MID * 2;   // one [BM x MID] bf16 tile
-  static constexpr int PX_BYTES = PX_RING > 2 * TILE ? PX_RING : 2 * TILE;
-  static constexpr int CH_BYTES = STAGES * MID * 64;
-  static constexpr int LDS = PX_BYTES + CH_BYTES;
-  static constexpr int NB = MID / 32;         // K steps of one B or C segment
-  static constexpr int NR = TILE / 1024 / 4;  // residual-chunk DMAs per wave
-  static constexpr int NS = TILE / 16 / 256;  // 16-B copy-out stores per thread
+  static constexpr int CA = BM / 64;          // phase A pixel-row DMAs per wave per stage
+  static constexpr int CB = MID / 64;         // phase A / C weight-row DMAs per wave per stage
+  static constexpr int A_PX = STAGES * BM * 64;           // phase A: pixel ring, then the weight ring
+  static constexpr int A_BYTES = A_PX + STAGES * MID * 64;
+  static constexpr int T2_BYTES = BM * MID * 2;           // T2 [BM x MID] (K-blocked), later T1' staging
+  static constexpr int Y_BYTES = BM * 64 * 2;             // one 64-channel chunk [BM x 64] of R -> Y
+  static constexpr int RING = T2_BYTES + Y_BYTES;         // B/C weight ring: STAGES x MID rows x 64 B
+  static constexpr int BC_BYTES = RING + STAGES * MID * 64;
+  static constexpr int LDS = A_BYTES > BC_BYTES ? A_BYTES : BC_BYTES;
+  static constexpr int NP = 4 * MID / 64;     // 64-channel passes over c3's output
+  static constexpr int NB = MID / 32;         // B steps (K = MID)
+  static constexpr int NC = 2;                // C steps (K = 64)
+  static constexpr int SP = NB + NC;
+  static constexpr int BPW = BM / 4;          // B: pixels per wave (all 64 channels of the chunk)
+  static constexpr int BFI = BPW / 16;        // B: pixel fragments per wave
+  static constexpr int NR = Y_BYTES / 1024 / 4;   // residual-chunk DMAs per wave
+  static constexpr int NS = Y_BYTES / 16 / 256;   // 16-B Y copy-out stores per thread
+  static constexpr int NT = T2_BYTES / 16 / 256;  // 16-B T1' copy-out stores per thread
+  static_assert(LDS <= 80 * 1024, "two workgroups per CU");
 };
 
-// byte offset of the 8-byte group holding channels n..n+3 of row r in a K-blocked swizzled tile
+// byte offset of the 8-byte group holding channels n..n+3 of row r in a K-blocked swizzled tile of BM rows
 template <int BM>
 __device__ __forceinline__ uint32_t tile_off(int r, int n) {
   const int kb = n >> 5, e = n & 31;
@@ -109,10 +118,11 @@ __device__ __forceinline__ uint32_t tile_off(int r, int n) {
 }
 
 template <int MID, bool NEXT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) void conv_chain_kernel(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv_chain_kernel(
     const ChainParams p) {
   using Cfg = ChainCfg<MID>;
-  constexpr int WM = Cfg::WM, BM = Cfg::BM, STAGES = Cfg::STAGES, CA = Cfg::CA, CB = Cfg::CB, NB = Cfg::NB;
+  constexpr int WM = Cfg::WM, BM = Cfg::BM, STAGES = Cfg::STAGES, CA = Cfg::CA, CB = Cfg::CB;
+  constexpr int NB = Cfg::NB, NC = Cfg::NC, SP = Cfg::SP, BFI = Cfg::BFI;
   constexpr int C4 = 4 * MID;
   extern __shared__ __attribute__((aligned(1024))) uint8_t smem[];
 
@@ -123,9 +133,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
   const int wn = wave / WM;
   const int m0 = xcd_remap(blockIdx.x, gridDim.x) * BM;
   const uint32_t sb = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(smem));
-  const uint32_t PX = sb, CH = sb + Cfg::PX_BYTES;
+  const uint32_t PX = sb;
   uint8_t* const t2buf = smem;                      // [BM x MID] T2 (then T1' staging)
-  uint8_t* const ybuf = smem + Cfg::TILE;           // [BM x MID] residual chunk -> Y chunk
+  uint8_t* const ybuf = smem + Cfg::T2_BYTES;       // [BM x 64] residual chunk -> Y chunk
+  const uint32_t RING = sb + Cfg::RING;
   const uint16_t* const zero = p.zero;
   const int lg = lane >> 4;
 
@@ -168,9 +179,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
     const long wstep = 64L * p.kpad2;
     constexpr int NKA = 9 * MID / BK;  // even: MID % 64 == 0
 
-    auto issue_a = [&](int kt) {
+    auto issue_a = [&](int kt) __attribute__((always_inline)) {
       const uint32_t xs = PX + (kt % STAGES) * BM * 64;
-      const uint32_t ws = CH + (kt % STAGES) * MID * 64;
+      const uint32_t ws = PX + Cfg::A_PX + (kt % STAGES) * MID * 64;
       const int toff = tw.off;
       const bool tap_ok = tw.kh < 3;
 #pragma unroll
@@ -190,7 +201,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
 #define KC_READ(FW, FX, KT)                                                                             \
   {                                                                                                     \
     const uint8_t* x_ = smem + ((KT) % STAGES) * BM * 64 + (wm * 64) * 64 + fofs;                       \
-    const uint8_t* w_ = smem + Cfg::PX_BYTES + ((KT) % STAGES) * MID * 64 + (wn * 64) * 64 + fofs;      \
+    const uint8_t* w_ = smem + Cfg::A_PX + ((KT) % STAGES) * MID * 64 + (wn * 64) * 64 + fofs;         \
     _Pragma("unroll") for (int j = 0; j < 4; ++j) FW[j] = *reinterpret_cast<const bf16x8_t*>(w_ + j * 1024); \
     _Pragma("unroll") for (int i = 0; i < 4; ++i) FX[i] = *reinterpret_cast<const bf16x8_t*>(x_ + i * 1024); \
   }
@@ -220,41 +231,39 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
 #undef KC_READ
   }
 
-  // ================= phases B / C: weights-only DMA stream =================
-  // step t: pass t / SP; within a pass NB steps of W3 rows [p*MID, +MID) (B), then NB steps of
-  // W1' columns [p*MID, +MID) (C).
-  constexpr int SP = NEXT ? 2 * NB : NB;
-  constexpr int NW = 4 * SP;
-  const int wrow = 16 * wave + rin;  // + 64*i
-  int ops = 0;                       // vector-memory ops this wave issued since the phase-A drain
-  int stage_end[NW];                 // ops count right after stage t was issued
-  auto issue_w = [&](int t) {
+  // ================= passes: B (c3 chunk), Y epilogue, C (c1' partial) =================
+  // Weight stream step t: pass t / SP; NB steps of W3 rows [64 pp, +64) (B, k = 32 kb of MID), then
+  // NC steps of W1' (all MID rows, k columns 64 pp + 32 kb) (C, NEXT only).
+  constexpr int SPW = NEXT ? SP : NB;
+  constexpr int NW = Cfg::NP * SPW;
+  int ops = 0;        // vector-memory ops this wave issued since the phase-A drain
+  int stage_end[NW];  // ops count right after stage t was issued (constants after unrolling)
+  auto issue_w = [&](int t) __attribute__((always_inline)) {
     if (t >= NW) return;
-    const int pp = t / SP, r = t % SP;
-    const uint32_t ws = CH + (t % STAGES) * MID * 64;
-    if (r < NB) {
-      const uint16_t* src = p.w3 + static_cast<long>(pp * MID + wrow) * p.kpad3 + r * BK + 8 * c;
-#pragma unroll
-      for (int i = 0; i < CB; ++i) glds16(src + i * 64L * p.kpad3, ws + 16 * (wave + 4 * i) * 64);
+    const int pp = t / SPW, r = t % SPW;
+    const uint32_t ws = RING + (t % STAGES) * MID * 64;
+    if (r < NB) {  // 64 rows: one DMA per wave
+      glds16(p.w3 + static_cast<long>(pp * 64 + 16 * wave + rin) * p.kpad3 + r * BK + 8 * c, ws + 16 * wave * 64);
+      ops += 1;
     } else {
-      const uint16_t* src = p.w1n + static_cast<long>(wrow) * p.kpad1n + pp * MID + (r - NB) * BK + 8 * c;
+      const uint16_t* src = p.w1n + static_cast<long>(16 * wave + rin) * p.kpad1n + pp * 64 + (r - NB) * BK + 8 * c;
 #pragma unroll
       for (int i = 0; i < CB; ++i) glds16(src + i * 64L * p.kpad1n, ws + 16 * (wave + 4 * i) * 64);
+      ops += CB;
     }
-    ops += CB;
     stage_end[t] = ops;
   };
 #pragma unroll
   for (int t = 0; t < STAGES - 1; ++t) issue_w(t);
 
   const float lo = 0.f;
-  // T2 epilogue: + b2, ReLU, bf16 -> t2buf
+  // T2 epilogue: + b2, ReLU, bf16 -> t2buf (phase A wave layout)
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int r = wm * 64 + 16 * i + (lane & 15);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int n = wn * 64 + 16 * j + 4 * (lane >> 4);
+      const int n = wn * 64 + 16 * j + 4 * lg;
       const f32x4_t b = bias4(p.b2 + wn * 64 + 16 * j, lg);
       *reinterpret_cast<uint2*>(t2buf + tile_off<BM>(r, n)) =
           make_uint2(pack_bf16x2(fmaxf(acc[i][j][0] + b[0], lo), fmaxf(acc[i][j][1] + b[1], lo)),
@@ -262,26 +271,49 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
     }
   }
 
-  f32x4_t accn[4][4];  // T1' accumulators (NEXT), live across the four passes
+  f32x4_t accn[4][4];  // T1' accumulators (NEXT), phase A wave layout, live across the passes
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) accn[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  // one B or C segment: NB weight steps t0.., the pixel operand from a K-blocked tile in LDS. Per step:
-  // wait for the step's stage, barrier (which also orders the refill below: the DMA of step t goes into
-  // the slot of stage t-1, which every wave has finished reading), fragments, MFMAs. Single-buffered
-  // fragments (the register budget holds two 64x64 accumulator tiles); the second workgroup on the CU
-  // covers the LDS latency.
-  auto segment = [&](f32x4_t (&a)[4][4], const uint8_t* xt, int t0) {
+  // Per weight step: wait for the step's stage, barrier (which also orders the refill at the end of
+  // the step: the DMA of step t goes into the slot of stage t-1, which every wave has finished reading),
+  // fragments, MFMAs. Single-buffered fragments; the second workgroup on the CU covers the LDS latency.
+  auto step_wait = [&](int t) __attribute__((always_inline)) {
+    wait_vmcnt_n(ops - stage_end[t]);
+    lds_barrier();
+  };
+  // B segment: this wave's BPW pixels x the 64 channels of chunk pp, K = MID from T2
+  auto seg_b = [&](f32x4_t (&a)[BFI][4], int t0) {
 #pragma unroll
     for (int kk = 0; kk < NB; ++kk) {
       const int t = t0 + kk;
-      wait_vmcnt_n(ops - stage_end[t]);
-      lds_barrier();
+      step_wait(t);
+      bf16x8_t fw[4], fx[BFI];
+      const uint8_t* w_ = smem + Cfg::RING + (t % STAGES) * MID * 64 + fofs;
+      const uint8_t* x_ = t2buf + kk * BM * 64 + (wave * Cfg::BPW) * 64 + fofs;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fw[j] = *reinterpret_cast<const bf16x8_t*>(w_ + j * 1024);
+#pragma unroll
+      for (int i = 0; i < BFI; ++i) fx[i] = *reinterpret_cast<const bf16x8_t*>(x_ + i * 1024);
+#pragma unroll
+      for (int i = 0; i < BFI; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          a[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[j], fx[i], a[i][j], 0, 0, 0);
+      issue_w(t + STAGES - 1);
+    }
+  };
+  // C segment: accn += Y chunk [BM x 64] . W1'[:, chunk]^T (phase A wave layout)
+  auto seg_c = [&](int t0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int kk = 0; kk < NC; ++kk) {
+      const int t = t0 + kk;
+      step_wait(t);
       bf16x8_t fw[4], fx[4];
-      const uint8_t* w_ = smem + Cfg::PX_BYTES + (t % STAGES) * MID * 64 + (wn * 64) * 64 + fofs;
-      const uint8_t* x_ = xt + kk * BM * 64 + (wm * 64) * 64 + fofs;
+      const uint8_t* w_ = smem + Cfg::RING + (t % STAGES) * MID * 64 + (wn * 64) * 64 + fofs;
+      const uint8_t* x_ = ybuf + kk * BM * 64 + (wm * 64) * 64 + fofs;
 #pragma unroll
       for (int j = 0; j < 4; ++j) fw[j] = *reinterpret_cast<const bf16x8_t*>(w_ + j * 1024);
 #pragma unroll
@@ -290,71 +322,74 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          a[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[j], fx[i], a[i][j], 0, 0, 0);
+          accn[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[j], fx[i], accn[i][j], 0, 0, 0);
       issue_w(t + STAGES - 1);
     }
   };
 
-  // 16-B copy-out of a [BM x MID] K-blocked tile to rows m0.. of a [M x ld] bf16 matrix. Every store is
-  // unconditional (tail rows go to the sink) so the wave's vmcnt bookkeeping stays exact; the row bases
-  // are computed once per matrix and each pass adds its column offset as an immediate.
-  constexpr int CPR = MID / 8;  // 16-B chunks per row
-  auto row_bases = [&](uint16_t* dst, int ld, uint16_t* (&base)[Cfg::NS]) {
+  // 16-B copy-out of a K-blocked [BM x W] tile (W = 64 or MID) to rows m0.. of a [M x ld] bf16 matrix.
+  // Every store is unconditional (tail rows go to the sink) so the wave's vmcnt bookkeeping stays exact;
+  // row bases are computed once per matrix and each pass adds its column offset as an immediate.
+  auto row_bases = [&](auto wc, uint16_t* dst, int ld, uint16_t** base) __attribute__((always_inline)) {
+    constexpr int CPR = decltype(wc)::value / 8;  // 16-B chunks per row
+    constexpr int N = BM * CPR / 256;
 #pragma unroll
-    for (int e = 0; e < Cfg::NS; ++e) {
+    for (int e = 0; e < N; ++e) {
       const int g = tid + 256 * e;
       const int r = g / CPR, cq = g % CPR;
       base[e] = m0 + r < p.M ? dst + static_cast<long>(m0 + r) * ld + 8 * cq : p.sink;
     }
   };
-  auto copy_out = [&](const uint8_t* tile, uint16_t* const (&base)[Cfg::NS], int coff) {
+  auto copy_out = [&](auto wc, const uint8_t* tile, uint16_t* const* base, int coff) __attribute__((always_inline)) {
+    constexpr int CPR = decltype(wc)::value / 8;
+    constexpr int N = BM * CPR / 256;
 #pragma unroll
-    for (int e = 0; e < Cfg::NS; ++e) {
+    for (int e = 0; e < N; ++e) {
       const int g = tid + 256 * e;
       const int r = g / CPR, cq = g % CPR;
       const uint4 v = *reinterpret_cast<const uint4*>(tile + (cq >> 2) * BM * 64 + r * 64 + (((cq & 3) ^ swz(r)) << 4));
       *reinterpret_cast<uint4*>(base[e] + coff) = v;
     }
-    ops += Cfg::NS;
+    ops += N;
   };
+  using W64 = std::integral_constant<int, 64>;
+  using WMID = std::integral_constant<int, MID>;
   uint16_t* ybase[Cfg::NS];
-  row_bases(p.y, C4, ybase);
+  row_bases(W64{}, p.y, C4, ybase);
 
-  // the four passes, unrolled by hand (a generic lambda per compile-time pass index) so every vmcnt
-  // count and ring slot below is a constant
-  auto pass = [&](auto ppc) {
+  auto pass = [&](auto ppc) __attribute__((always_inline)) {
     constexpr int pp = decltype(ppc)::value;
-    if constexpr (pp > 0) copy_out(ybuf, ybase, (pp - 1) * MID);
-    lds_barrier();  // T2 / previous Y chunk fully consumed (and T2 visible at pass 0)
-    // residual chunk R_pp -> ybuf (K-blocked swizzled layout, 16-B DMA rows)
+    if constexpr (pp > 0) copy_out(W64{}, ybuf, ybase, (pp - 1) * 64);
+    lds_barrier();  // previous Y chunk fully consumed (and T2 visible at pass 0)
+    // residual chunk R_pp -> ybuf (K-blocked swizzled [BM x 64], 16-B DMA rows; rows past M re-read
+    // row M-1, never stored)
 #pragma unroll
     for (int s = 0; s < Cfg::NR; ++s) {
       const int q = wave + 4 * s;
       const int kb = q / (BM / 16), rb = q % (BM / 16);
       const int row = rb * 16 + rin;
-      // rows past M re-read row M-1 (never stored): no pointer select, one base for all passes
-      const void* src = p.res + static_cast<long>(min(m0 + row, p.M - 1)) * C4 + pp * MID + kb * BK + 8 * c;
-      glds16(src, sb + Cfg::TILE + kb * BM * 64 + rb * 16 * 64);
+      glds16(p.res + static_cast<long>(min(m0 + row, p.M - 1)) * C4 + pp * 64 + kb * BK + 8 * c,
+             sb + Cfg::T2_BYTES + kb * BM * 64 + rb * 16 * 64);
     }
     ops += Cfg::NR;
     const int r_end = ops;
 
-    f32x4_t accb[4][4];
+    f32x4_t accb[BFI][4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < BFI; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) accb[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-    segment(accb, t2buf, pp * SP);
+    seg_b(accb, pp * SPW);
 
     wait_vmcnt_n(ops - r_end);
     lds_barrier();  // residual chunk visible
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int r = wm * 64 + 16 * i + (lane & 15);
+    for (int i = 0; i < BFI; ++i) {
+      const int r = wave * Cfg::BPW + 16 * i + (lane & 15);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int n = wn * 64 + 16 * j + 4 * (lane >> 4);
-        const f32x4_t b = bias4(p.b3 + pp * MID + wn * 64 + 16 * j, lg);
+        const int n = 16 * j + 4 * lg;
+        const f32x4_t b = bias4(p.b3 + pp * 64 + 16 * j, lg);
         uint2* yp = reinterpret_cast<uint2*>(ybuf + tile_off<BM>(r, n));
         const uint2 rv = *yp;
         float r0, r1, r2, r3;
@@ -365,25 +400,32 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
       }
     }
     if constexpr (NEXT) {
-      segment(accn, ybuf, pp * SP + NB);  // its first barrier publishes the Y chunk
+      seg_c(pp * SPW + NB);  // its first barrier publishes the Y chunk
     } else {
       lds_barrier();
     }
   };
+  static_assert(Cfg::NP == 4 || Cfg::NP == 8, "passes");
   pass(std::integral_constant<int, 0>{});
   pass(std::integral_constant<int, 1>{});
   pass(std::integral_constant<int, 2>{});
   pass(std::integral_constant<int, 3>{});
-  copy_out(ybuf, ybase, 3 * MID);
+  if constexpr (Cfg::NP == 8) {
+    pass(std::integral_constant<int, 4>{});
+    pass(std::integral_constant<int, 5>{});
+    pass(std::integral_constant<int, 6>{});
+    pass(std::integral_constant<int, 7>{});
+  }
+  copy_out(W64{}, ybuf, ybase, (Cfg::NP - 1) * 64);
 
   if constexpr (NEXT) {
-    // T1' epilogue through the (now idle) T2 buffer, then 16-B copy-out
+    // T1' epilogue through the (idle) T2 buffer, then 16-B copy-out
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int r = wm * 64 + 16 * i + (lane & 15);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int n = wn * 64 + 16 * j + 4 * (lane >> 4);
+        const int n = wn * 64 + 16 * j + 4 * lg;
         const f32x4_t b = bias4(p.b1n + wn * 64 + 16 * j, lg);
         *reinterpret_cast<uint2*>(t2buf + tile_off<BM>(r, n)) =
             make_uint2(pack_bf16x2(fmaxf(accn[i][j][0] + b[0], lo), fmaxf(accn[i][j][1] + b[1], lo)),
@@ -391,9 +433,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
       }
     }
     lds_barrier();
-    uint16_t* tbase[Cfg::NS];
-    row_bases(p.t1n, MID, tbase);
-    copy_out(t2buf, tbase, 0);
+    uint16_t* tbase[Cfg::NT];
+    row_bases(WMID{}, p.t1n, MID, tbase);
+    copy_out(WMID{}, t2buf, tbase, 0);
   }
 }
 
@@ -423,12 +465,12 @@ T* symbol_ptr(const void* sym) {
 // Fused bottleneck chain (see header). x: T1 NHWC [N,H,W,ldx] bf16 (MID channels at offset 0);
 // w2 [>=MID rows, kpad2 >= 9*MID] (k = (kh, kw, c)); w3 [>=4*MID rows, kpad3 >= MID];
 // w1n [>=MID rows, kpad1n >= 4*MID] (nullptr: no next block, t1n unused); res, y [M, 4*MID];
-// t1n [M, MID]. 3x3, pad 1, stride 1 or 2. MID in {64, 128, 256}.
+// t1n [M, MID]. 3x3, pad 1, stride 1 or 2. MID in {64, 128}.
 AI4E_API int ai4e_conv_chain_fwd(const void* x, const void* w2, const void* b2, const void* w3, const void* b3,
                                  const void* res, void* y, const void* w1n, const void* b1n, void* t1n, int N, int H,
                                  int W, int ldx, int mid, int stride, int kpad2, int kpad3, int kpad1n,
                                  hipStream_t stream) {
-  if ((mid != 64 && mid != 128 && mid != 256) || ldx % 8 || ldx < mid || kpad2 < 9 * mid || kpad2 % 64 ||
+  if ((mid != 64 && mid != 128) || ldx % 8 || ldx < mid || kpad2 < 9 * mid || kpad2 % 64 ||
       kpad3 < mid || kpad3 % 8 || (stride != 1 && stride != 2) || !x || !w2 || !b2 || !w3 || !b3 || !res || !y ||
       (w1n && (!b1n || !t1n || kpad1n < 4 * mid || kpad1n % 8)))
     return AI4E_EINVAL;
@@ -455,10 +497,6 @@ AI4E_API int ai4e_conv_chain_fwd(const void* x, const void* w2, const void* b2, 
   p.kpad2 = kpad2; p.kpad3 = kpad3; p.kpad1n = kpad1n;
   if (p.M <= 0) return AI4E_OK;
   const bool next = w1n != nullptr;
-  switch (mid) {
-    case 64: return next ? launch_chain<64, true>(p, stream) : launch_chain<64, false>(p, stream);
-    // MID 128/256 with the chained c1' exceed the 256-VGPR budget of two waves per SIMD: not built
-    case 128: return next ? AI4E_EINVAL : launch_chain<128, false>(p, stream);
-    default: return next ? AI4E_EINVAL : launch_chain<256, false>(p, stream);
-  }
+  if (mid == 64) return next ? launch_chain<64, true>(p, stream) : launch_chain<64, false>(p, stream);
+  return next ? launch_chain<128, true>(p, stream) : launch_chain<128, false>(p, stream);
 }

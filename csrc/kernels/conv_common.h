@@ -23,7 +23,7 @@ __device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_base) {
       "global_load_lds_dwordx4 %1, off\n\t"
       "s_mov_b32 m0, %0"
       : "=&s"(keep)
-      : "v"(gsrc), "s"(lds_base)
+      : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(lds_base))
       : "memory");
 }
 

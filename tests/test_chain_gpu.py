@@ -34,10 +34,10 @@ CASES = [
     (2, 56, 56, 64, 1, False),
     (1, 15, 13, 64, 1, True),     # M = 195: one partial tile
     (3, 9, 11, 64, 2, True),      # strided 3x3, ragged
+    (2, 28, 28, 128, 1, True),
     (2, 28, 28, 128, 1, False),
-    (2, 28, 28, 128, 2, False),
-    (2, 14, 14, 256, 1, False),
-    (1, 7, 9, 256, 2, False),
+    (2, 56, 56, 128, 2, True),    # layer2 block 0: strided c2 chained into block 1's c1
+    (1, 9, 13, 128, 1, True),     # M = 117 < one 128-pixel tile
 ]
 
 
