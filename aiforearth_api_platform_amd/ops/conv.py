@@ -163,7 +163,8 @@ def chain_supported(mid: int, has_next: bool) -> bool:
 
 
 def conv_chain(t1: torch.Tensor, c2: PackedConv, c3: PackedConv, residual: torch.Tensor,
-               c1n: Optional[PackedConv] = None, out: Optional[torch.Tensor] = None, force: bool = False):
+               c1n: Optional[PackedConv] = None, out: Optional[torch.Tensor] = None, force: bool = False,
+               tile_cfg: int = -1):
     """Fused bottleneck tail (K1c): ``y = relu(c3(relu(c2(t1))) + residual)`` and, with ``c1n`` (the next
     block's 1x1 reduce), ``t1n = relu(c1n(y))`` from the same kernel. Returns ``(y, t1n or None)``.
 
@@ -193,8 +194,12 @@ def conv_chain(t1: torch.Tensor, c2: PackedConv, c3: PackedConv, residual: torch
               c3.w_packed.data_ptr(), c3.bias.data_ptr(), residual.data_ptr(), out.data_ptr(),
               _ext.ptr(c1n.w_packed if c1n is not None else None), _ext.ptr(c1n.bias if c1n is not None else None),
               _ext.ptr(t1n), n, h, w, mid, mid, c2.stride, c2.kpad, c3.kpad, c1n.kpad if c1n is not None else 0,
-              _ext.stream_ptr(t1.device))
+              CHAIN_TILE.get(mid, 0) if tile_cfg < 0 else tile_cfg, _ext.stream_ptr(t1.device))
     return out, t1n
+
+
+# K1c workgroup tile per bottleneck width (bench/chain_tune.py): 0 = 16384/mid pixels, 1 = 128 pixels (mid 64)
+CHAIN_TILE = {64: int(__import__("os").environ.get("AI4E_CHAIN_TILE64", "1")), 128: 0}
 
 
 def stem_pool(x: torch.Tensor, pc: PackedConv) -> torch.Tensor:

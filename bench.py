@@ -37,8 +37,8 @@ BASELINE_VALUE = None  # the reference publishes no numbers
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--steps", type=int, default=100)
+    p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--batch", type=int, default=256, help="images per step per GPU (= max dynamic batch)")
     p.add_argument("--inflight", type=int, default=2, help="steps kept outstanding per GPU")
     p.add_argument("--image-size", type=int, default=224)

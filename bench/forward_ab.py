@@ -1,0 +1,67 @@
+"""Low-noise A/B of model-level variants: HIP-graph replay of the fused ResNet-50 forward (uint8 in, logits
+out), variants interleaved over several rounds on one GPU.
+
+    python bench/forward_ab.py chain64=0 chain64=1 [chain=0] [chain=1] ...
+A variant is ``key=value`` over: chain (K1c on/off), chain64 / chain128 (K1c tile config).
+"""
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from aiforearth_api_platform_amd.models.resnet import FusedResNet, resnet50  # noqa: E402
+from aiforearth_api_platform_amd.ops import conv as convmod  # noqa: E402
+
+
+def apply(m, variant):
+    for kv in variant.split(","):
+        k, v = kv.split("=")
+        if k == "chain":
+            m.chain = v == "1"
+        elif k.startswith("chain"):
+            convmod.CHAIN_TILE[int(k[5:])] = int(v)
+        else:
+            raise SystemExit(f"unknown variant key {k}")
+
+
+def main():
+    dev = torch.device("cuda:0")
+    B = int(os.environ.get("B", "256"))
+    variants = sys.argv[1:] or ["chain=1", "chain=0"]
+    m = FusedResNet(resnet50(seed=0), device=dev)
+    img = torch.randint(0, 256, (B, 224, 224, 3), dtype=torch.uint8, device=dev)
+    graphs = {}
+    for v in variants:
+        apply(m, v)
+        s0 = torch.cuda.Stream(device=dev)
+        s0.wait_stream(torch.cuda.current_stream())
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(s0):
+            m.forward_u8(img)
+            torch.cuda.synchronize()
+            with torch.cuda.graph(g, stream=s0):
+                m.forward_u8(img)
+        torch.cuda.synchronize()
+        graphs[v] = g
+    res = {v: [] for v in variants}
+    for _ in range(4):
+        for v in variants:
+            g = graphs[v]
+            for _ in range(5):
+                g.replay()
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            for _ in range(40):
+                g.replay()
+            torch.cuda.synchronize()
+            res[v].append((time.perf_counter() - t) / 40 * 1e3)
+    for v in variants:
+        r = sorted(res[v])
+        print(f"{v:30s} ms/fwd min {r[0]:.3f} median {r[len(r) // 2]:.3f}  ({B / r[len(r) // 2] * 1e3:.0f} img/s)",
+              flush=True)
+
+
+if __name__ == "__main__":
+    main()

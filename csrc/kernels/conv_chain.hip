@@ -83,11 +83,13 @@ struct ChainParams {
   uint16_t* sink;
 };
 
-template <int MID>
+template <int MID, int BM_>
 struct ChainCfg {
+  static constexpr int BM = BM_;              // pixels per workgroup
   static constexpr int WN = MID / 64;         // phase A / C: waves along channels
   static constexpr int WM = 4 / WN;           // phase A / C: waves along pixels
-  static constexpr int BM = WM * 64;          // pixels per workgroup (256 | 128)
+  static constexpr int WPX = BM / WM;         // phase A / C: pixels per wave
+  static constexpr int FI = WPX / 16;         // phase A / C: pixel fragments per wave
   static constexpr int STAGES = 4;
   static constexpr int CA = BM / 64;          // phase A pixel-row DMAs per wave per stage
   static constexpr int CB = MID / 64;         // phase A / C weight-row DMAs per wave per stage
@@ -107,7 +109,9 @@ struct ChainCfg {
   static constexpr int NR = Y_BYTES / 1024 / 4;   // residual-chunk DMAs per wave
   static constexpr int NS = Y_BYTES / 16 / 256;   // 16-B Y copy-out stores per thread
   static constexpr int NT = T2_BYTES / 16 / 256;  // 16-B T1' copy-out stores per thread
+  static constexpr int MINW = LDS <= 160 * 1024 / 3 ? 3 : 2;  // workgroups (= waves per SIMD) per CU
   static_assert(LDS <= 80 * 1024, "two workgroups per CU");
+  static_assert(FI >= 1 && FI <= 4 && BFI >= 1, "tile");
 };
 
 // byte offset of the 8-byte group holding channels n..n+3 of row r in a K-blocked swizzled tile of BM rows
@@ -117,11 +121,12 @@ __device__ __forceinline__ uint32_t tile_off(int r, int n) {
   return kb * BM * 64 + r * 64 + ((((e >> 3) ^ swz(r)) << 4) | (((e >> 2) & 1) << 3));
 }
 
-template <int MID, bool NEXT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv_chain_kernel(
-    const ChainParams p) {
-  using Cfg = ChainCfg<MID>;
+template <int MID, int BM_, bool NEXT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ChainCfg<MID, BM_>::MINW, ChainCfg<MID, BM_>::MINW)))
+void conv_chain_kernel(const ChainParams p) {
+  using Cfg = ChainCfg<MID, BM_>;
   constexpr int WM = Cfg::WM, BM = Cfg::BM, STAGES = Cfg::STAGES, CA = Cfg::CA, CB = Cfg::CB;
+  constexpr int FI = Cfg::FI, WPX = Cfg::WPX;
   constexpr int NB = Cfg::NB, NC = Cfg::NC, SP = Cfg::SP, BFI = Cfg::BFI;
   constexpr int C4 = 4 * MID;
   extern __shared__ __attribute__((aligned(1024))) uint8_t smem[];
@@ -146,9 +151,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const uint32_t fofs = frow * 64 + ((((lane >> 4) ^ swz(frow)) << 4));  // fragment byte offset in a 16-row block
 
   // ================= phase A: T2 = relu(conv3x3(T1) + b2), K1 main loop (GATHER_TAP) =================
-  f32x4_t acc[4][4];
+  f32x4_t acc[FI][4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < FI; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   {
@@ -197,13 +202,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         glds16(live ? static_cast<const void*>(wsrc + i * wstep + kt * BK) : zero, ws + 16 * (wave + 4 * i) * 64);
     };
 
-    bf16x8_t fw0[4], fx0[4], fw1[4], fx1[4];
+    bf16x8_t fw0[4], fx0[FI], fw1[4], fx1[FI];
 #define KC_READ(FW, FX, KT)                                                                             \
   {                                                                                                     \
-    const uint8_t* x_ = smem + ((KT) % STAGES) * BM * 64 + (wm * 64) * 64 + fofs;                       \
+    const uint8_t* x_ = smem + ((KT) % STAGES) * BM * 64 + (wm * WPX) * 64 + fofs;                      \
     const uint8_t* w_ = smem + Cfg::A_PX + ((KT) % STAGES) * MID * 64 + (wn * 64) * 64 + fofs;         \
     _Pragma("unroll") for (int j = 0; j < 4; ++j) FW[j] = *reinterpret_cast<const bf16x8_t*>(w_ + j * 1024); \
-    _Pragma("unroll") for (int i = 0; i < 4; ++i) FX[i] = *reinterpret_cast<const bf16x8_t*>(x_ + i * 1024); \
+    _Pragma("unroll") for (int i = 0; i < FI; ++i) FX[i] = *reinterpret_cast<const bf16x8_t*>(x_ + i * 1024); \
   }
 #define KC_STEP(KT, FWC, FXC, FWN, FXN)                                                                 \
   {                                                                                                     \
@@ -211,7 +216,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     wait_vmcnt<(STAGES - 3) * (CA + CB)>();                                                             \
     lds_barrier();                                                                                      \
     KC_READ(FWN, FXN, kt_ + 1)                                                                          \
-    _Pragma("unroll") for (int i = 0; i < 4; ++i)                                                       \
+    _Pragma("unroll") for (int i = 0; i < FI; ++i)                                                      \
       _Pragma("unroll") for (int j = 0; j < 4; ++j)                                                     \
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(FWC[j], FXC[i], acc[i][j], 0, 0, 0);        \
     issue_a(kt_ + STAGES - 1);                                                                          \
@@ -259,8 +264,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const float lo = 0.f;
   // T2 epilogue: + b2, ReLU, bf16 -> t2buf (phase A wave layout)
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int r = wm * 64 + 16 * i + (lane & 15);
+  for (int i = 0; i < FI; ++i) {
+    const int r = wm * WPX + 16 * i + (lane & 15);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int n = wn * 64 + 16 * j + 4 * lg;
@@ -271,9 +276,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     }
   }
 
-  f32x4_t accn[4][4];  // T1' accumulators (NEXT), phase A wave layout, live across the passes
+  f32x4_t accn[FI][4];  // T1' accumulators (NEXT), phase A wave layout, live across the passes
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < FI; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) accn[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
@@ -311,15 +316,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     for (int kk = 0; kk < NC; ++kk) {
       const int t = t0 + kk;
       step_wait(t);
-      bf16x8_t fw[4], fx[4];
+      bf16x8_t fw[4], fx[FI];
       const uint8_t* w_ = smem + Cfg::RING + (t % STAGES) * MID * 64 + (wn * 64) * 64 + fofs;
-      const uint8_t* x_ = ybuf + kk * BM * 64 + (wm * 64) * 64 + fofs;
+      const uint8_t* x_ = ybuf + kk * BM * 64 + (wm * WPX) * 64 + fofs;
 #pragma unroll
       for (int j = 0; j < 4; ++j) fw[j] = *reinterpret_cast<const bf16x8_t*>(w_ + j * 1024);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) fx[i] = *reinterpret_cast<const bf16x8_t*>(x_ + i * 1024);
+      for (int i = 0; i < FI; ++i) fx[i] = *reinterpret_cast<const bf16x8_t*>(x_ + i * 1024);
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < FI; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           accn[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[j], fx[i], accn[i][j], 0, 0, 0);
@@ -421,8 +426,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   if constexpr (NEXT) {
     // T1' epilogue through the (idle) T2 buffer, then 16-B copy-out
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int r = wm * 64 + 16 * i + (lane & 15);
+    for (int i = 0; i < FI; ++i) {
+      const int r = wm * WPX + 16 * i + (lane & 15);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int n = wn * 64 + 16 * j + 4 * lg;
@@ -439,18 +444,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   }
 }
 
-template <int MID, bool NEXT>
+template <int MID, int BM, bool NEXT>
 int launch_chain(const ChainParams& p, hipStream_t s) {
-  using Cfg = ChainCfg<MID>;
+  using Cfg = ChainCfg<MID, BM>;
   static bool attr = false;
   if (!attr) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(conv_chain_kernel<MID, NEXT>),
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(conv_chain_kernel<MID, BM, NEXT>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, Cfg::LDS) != hipSuccess)
       return AI4E_ELAUNCH;
     attr = true;
   }
   const int nb = ai4e_cdiv(p.M, Cfg::BM);
-  hipLaunchKernelGGL((conv_chain_kernel<MID, NEXT>), dim3(nb), dim3(256), Cfg::LDS, s, p);
+  hipLaunchKernelGGL((conv_chain_kernel<MID, BM, NEXT>), dim3(nb), dim3(256), Cfg::LDS, s, p);
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
 }
 
@@ -469,7 +474,7 @@ T* symbol_ptr(const void* sym) {
 AI4E_API int ai4e_conv_chain_fwd(const void* x, const void* w2, const void* b2, const void* w3, const void* b3,
                                  const void* res, void* y, const void* w1n, const void* b1n, void* t1n, int N, int H,
                                  int W, int ldx, int mid, int stride, int kpad2, int kpad3, int kpad1n,
-                                 hipStream_t stream) {
+                                 int tile_cfg, hipStream_t stream) {
   if ((mid != 64 && mid != 128) || ldx % 8 || ldx < mid || kpad2 < 9 * mid || kpad2 % 64 ||
       kpad3 < mid || kpad3 % 8 || (stride != 1 && stride != 2) || !x || !w2 || !b2 || !w3 || !b3 || !res || !y ||
       (w1n && (!b1n || !t1n || kpad1n < 4 * mid || kpad1n % 8)))
@@ -497,6 +502,10 @@ AI4E_API int ai4e_conv_chain_fwd(const void* x, const void* w2, const void* b2, 
   p.kpad2 = kpad2; p.kpad3 = kpad3; p.kpad1n = kpad1n;
   if (p.M <= 0) return AI4E_OK;
   const bool next = w1n != nullptr;
-  if (mid == 64) return next ? launch_chain<64, true>(p, stream) : launch_chain<64, false>(p, stream);
-  return next ? launch_chain<128, true>(p, stream) : launch_chain<128, false>(p, stream);
+  // tile_cfg: 0 = default (MID 64: 256 pixels, MID 128: 128), 1 = 128-pixel MID-64 tile (48 KB LDS, 3 per CU)
+  if (mid == 64) {
+    if (tile_cfg == 1) return next ? launch_chain<64, 128, true>(p, stream) : launch_chain<64, 128, false>(p, stream);
+    return next ? launch_chain<64, 256, true>(p, stream) : launch_chain<64, 256, false>(p, stream);
+  }
+  return next ? launch_chain<128, 128, true>(p, stream) : launch_chain<128, 128, false>(p, stream);
 }

@@ -42,8 +42,11 @@ CASES = [
 
 
 @pytest.mark.parametrize("case", CASES)
-def test_conv_chain(case):
+@pytest.mark.parametrize("tile", [0, 1])
+def test_conv_chain(case, tile):
     n, h, w, mid, s, nxt = case
+    if tile == 1 and mid != 64:
+        pytest.skip("128-pixel tile variant is MID 64 only")
     assert chain_kernel_builds(mid, nxt)
     torch.manual_seed(7)
     c2 = pack_conv(torch.randn(mid, mid, 3, 3) / (9 * mid) ** 0.5, torch.randn(mid) * 0.1, stride=s, pad=1).to(DEV)
@@ -52,7 +55,7 @@ def test_conv_chain(case):
     t1 = torch.randn(n, h, w, mid, device=DEV).relu().to(torch.bfloat16)
     oh, ow = c2.out_hw(h, w)
     res = torch.randn(n, oh, ow, 4 * mid, device=DEV).to(torch.bfloat16)
-    y, t1n = conv_chain(t1, c2, c3, res, c1n=c1n, force=True)
+    y, t1n = conv_chain(t1, c2, c3, res, c1n=c1n, force=True, tile_cfg=tile)
     torch.cuda.synchronize()
 
     t2 = F.relu(_conv(t1, _wq(c2, 3), c2.bias[:mid], s, 1)).to(torch.bfloat16)
