@@ -92,7 +92,7 @@ class InferenceEngine:
     """Runs ``model_fn(u8 [b,H,W,C] on device) -> logits [b, classes]`` with graphs + 2-deep buffering."""
 
     def __init__(self, model_fn: Callable[[torch.Tensor], torch.Tensor], item_shape: Sequence[int], max_batch: int,
-                 device: Optional[torch.device] = None, topk: int = 5, use_graphs: bool = True, nbuf: int = 2,
+                 device: Optional[torch.device] = None, topk: int = 5, use_graphs: bool = True, nbuf: int = 3,
                  buckets: Optional[Sequence[int]] = None):
         self.model_fn = model_fn
         self.device = torch.device(device or "cuda")

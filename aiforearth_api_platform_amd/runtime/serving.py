@@ -115,10 +115,13 @@ class GpuBatchWorker:
                 return 0
             self.pending.append((ids, seqs, slots, res))
             self._h_batch.observe(n)
-        # keep one batch in flight while the next is being formed; with no new work, retire a
-        # batch as soon as its completion event fires
-        keep = 1 if n else 0
-        while len(self.pending) > keep or (self.pending and self.pending[0][3].done.query()):
+        # keep one launched batch queued behind the running one while the next is being formed; retire
+        # a batch as soon as its completion event fires. Never block on the GPU while there is only one
+        # batch in flight: an empty receive must not turn into a synchronize, or the next batch (arriving
+        # a moment later) is launched only after the GPU has drained and the H2D copy stalls it. At most
+        # two batches stay pending, so the engine's third buffer set is never reused before its batch
+        # was finalized (InferenceEngine nbuf = 3).
+        while len(self.pending) > 2 or (self.pending and self.pending[0][3].done.query()):
             self._finalize(self.pending.popleft())
         return n
 
