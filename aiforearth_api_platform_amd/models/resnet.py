@@ -19,7 +19,8 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ..ops.conv import PackedConv, conv2d_nhwc, conv_chain, fold_bn, pack_conv, pack_stem_s2d, stem_pool
+from ..ops.conv import (PackedConv, chain_supported, conv2d_nhwc, conv_chain, fold_bn, pack_conv,
+                        pack_stem_s2d, stem_pool)
 from ..ops.pool import (global_avgpool_nhwc, maxpool2d_nhwc, preprocess_s2d_u8, preprocess_u8,
                         space_to_depth_shifted)
 
@@ -197,17 +198,29 @@ class FusedResNet:
         y = conv2d_nhwc(y, c2, relu=True)
         return conv2d_nhwc(y, c3, residual=idt, relu=True, out=out)
 
-    @staticmethod
-    def _stage(x: torch.Tensor, blocks) -> torch.Tensor:
-        """One ResNet stage with the K1c chains: c1 and the downsample of the first block run as K1 convs,
-        then every block is ONE kernel (c2 -> c3 + residual -> the next block's c1), see conv_chain."""
-        c1, _, _, down = blocks[0]
-        idt = x if down is None else conv2d_nhwc(x, down)
-        t1 = conv2d_nhwc(x, c1, relu=True)
-        for i, (_, c2, c3, _) in enumerate(blocks):
-            nxt = blocks[i + 1][0] if i + 1 < len(blocks) else None
-            idt, t1 = conv_chain(t1, c2, c3, idt, c1n=nxt)
-        return idt
+    def _stages_chained(self, y: torch.Tensor) -> torch.Tensor:
+        """All four stages with the K1c chains: the first block's downsample runs as a K1 conv, then every
+        block is ONE kernel (c2 -> c3 + residual -> the next block's c1, across stage boundaries too: the
+        last block of a stage computes the next stage's first c1). Shapes K1c does not build fall back to
+        separate K1 convs inside ``conv_chain``."""
+        t1 = None
+        for si, blocks in enumerate(self.stages):
+            c1, _, _, down = blocks[0]
+            idt = y if down is None else conv2d_nhwc(y, down)
+            if t1 is None:
+                t1 = conv2d_nhwc(y, c1, relu=True)
+            for i, (_, c2, c3, _) in enumerate(blocks):
+                if i + 1 < len(blocks):
+                    nxt = blocks[i + 1][0]
+                elif si + 1 < len(self.stages):
+                    nxt = self.stages[si + 1][0][0]
+                else:
+                    nxt = None
+                if nxt is not None and not chain_supported(c2.cout, nxt.cout) and chain_supported(c2.cout):
+                    nxt = None  # keep the chain, run the next c1 as its own K1 launch
+                idt, t1 = conv_chain(t1, c2, c3, idt, c1n=nxt)
+            y = idt
+        return y
 
     def _prefix_shape(self, n: int, h: int, w: int, nblocks: int) -> Tuple[int, int, int, int]:
         """Output shape after the stem, max-pool and the first ``nblocks`` bottlenecks."""
@@ -244,9 +257,7 @@ class FusedResNet:
         else:
             y, nblocks = self._stem(pre(x)), 0
         if self.chain and nblocks == 0:
-            for st in self.stages:
-                y = self._stage(y, st)
-            return y
+            return self._stages_chained(y)
         for blk in self.blocks[nblocks:]:
             y = self._block(y, blk)
         return y

@@ -152,14 +152,15 @@ def _conv_hip(x, pc, residual, relu, out, out_coff, tile_cfg):
               oh, ow, pc.cout, pc.kpad, ldy, out_coff, ldres, int(relu), tile_cfg, _ext.stream_ptr(x.device))
 
 
-def chain_kernel_builds(mid: int, has_next: bool) -> bool:
-    """Shapes the fused bottleneck-chain kernel K1c is built for (csrc/kernels/conv_chain.hip)."""
-    return mid in (64, 128)
+def chain_kernel_builds(mid: int, midn: int = 0) -> bool:
+    """Shapes the fused bottleneck-chain kernel K1c is built for (csrc/kernels/conv_chain.hip); ``midn`` is
+    the chained 1x1's output width (0 = no chained 1x1)."""
+    return (mid, midn) in ((64, 0), (64, 64), (64, 128), (128, 0), (128, 128))
 
 
-def chain_supported(mid: int, has_next: bool) -> bool:
+def chain_supported(mid: int, midn: int = 0) -> bool:
     """Shapes ``conv_chain`` routes to K1c by default."""
-    return mid in (64, 128)
+    return chain_kernel_builds(mid, midn)
 
 
 def conv_chain(t1: torch.Tensor, c2: PackedConv, c3: PackedConv, residual: torch.Tensor,
@@ -175,13 +176,14 @@ def conv_chain(t1: torch.Tensor, c2: PackedConv, c3: PackedConv, residual: torch
     """
     n, h, w, mid = t1.shape
     if (c2.kh, c2.kw, c2.pad, c2.cin_pad, c2.cout) != (3, 3, 1, mid, mid) or c3.kh != 1 or c3.cin_pad != mid \
-            or c3.cout != 4 * mid or (c1n is not None and (c1n.kh != 1 or c1n.cin_pad != 4 * mid or c1n.cout != mid)):
+            or c3.cout != 4 * mid or (c1n is not None and (c1n.kh != 1 or c1n.stride != 1 or c1n.cin_pad != 4 * mid)):
         raise ValueError("conv_chain: layer shapes do not form a bottleneck chain")
     oh, ow = c2.out_hw(h, w)
     if out is None:
         out = torch.empty(n, oh, ow, 4 * mid, device=t1.device, dtype=t1.dtype)
     ok = chain_kernel_builds if force else chain_supported
-    if _ext.backend_for(t1) != "hip" or not ok(mid, c1n is not None):
+    midn = c1n.cout if c1n is not None else 0
+    if _ext.backend_for(t1) != "hip" or not ok(mid, midn):
         y2 = conv2d_nhwc(t1, c2, relu=True)
         conv2d_nhwc(y2, c3, residual=residual, relu=True, out=out)
         return out, (conv2d_nhwc(out, c1n, relu=True) if c1n is not None else None)
@@ -189,11 +191,11 @@ def conv_chain(t1: torch.Tensor, c2: PackedConv, c3: PackedConv, residual: torch
         raise ValueError("conv_chain: contiguous bf16 NHWC tensors required")
     if residual.shape != (n, oh, ow, 4 * mid) or not residual.is_contiguous():
         raise ValueError("conv_chain: residual must be contiguous [N,OH,OW,4*mid]")
-    t1n = torch.empty(n, oh, ow, mid, device=t1.device, dtype=t1.dtype) if c1n is not None else None
+    t1n = torch.empty(n, oh, ow, midn, device=t1.device, dtype=t1.dtype) if c1n is not None else None
     _ext.call("ai4e_conv_chain_fwd", t1.data_ptr(), c2.w_packed.data_ptr(), c2.bias.data_ptr(),
               c3.w_packed.data_ptr(), c3.bias.data_ptr(), residual.data_ptr(), out.data_ptr(),
               _ext.ptr(c1n.w_packed if c1n is not None else None), _ext.ptr(c1n.bias if c1n is not None else None),
-              _ext.ptr(t1n), n, h, w, mid, mid, c2.stride, c2.kpad, c3.kpad, c1n.kpad if c1n is not None else 0,
+              _ext.ptr(t1n), n, h, w, mid, mid, midn, c2.stride, c2.kpad, c3.kpad, c1n.kpad if c1n is not None else 0,
               CHAIN_TILE.get(mid, 0) if tile_cfg < 0 else tile_cfg, _ext.stream_ptr(t1.device))
     return out, t1n
 

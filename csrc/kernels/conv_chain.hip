@@ -83,9 +83,10 @@ struct ChainParams {
   uint16_t* sink;
 };
 
-template <int MID, int BM_>
+template <int MID, int BM_, int MIDN = 0>
 struct ChainCfg {
   static constexpr int BM = BM_;              // pixels per workgroup
+  static constexpr bool NEXT = MIDN > 0;      // chained 1x1 c1' (output width MIDN)
   static constexpr int WN = MID / 64;         // phase A / C: waves along channels
   static constexpr int WM = 4 / WN;           // phase A / C: waves along pixels
   static constexpr int WPX = BM / WM;         // phase A / C: pixels per wave
@@ -97,8 +98,15 @@ struct ChainCfg {
   static constexpr int A_BYTES = A_PX + STAGES * MID * 64;
   static constexpr int T2_BYTES = BM * MID * 2;           // T2 [BM x MID] (K-blocked), later T1' staging
   static constexpr int Y_BYTES = BM * 64 * 2;             // one 64-channel chunk [BM x 64] of R -> Y
-  static constexpr int RING = T2_BYTES + Y_BYTES;         // B/C weight ring: STAGES x MID rows x 64 B
-  static constexpr int BC_BYTES = RING + STAGES * MID * 64;
+  static constexpr int RING = T2_BYTES + Y_BYTES;         // B/C weight ring: STAGES x SLOT rows x 64 B
+  static constexpr int SLOT = NEXT ? (MID > MIDN ? MID : MIDN) : MID;  // >= 64 (B) and MIDN (C) rows
+  static constexpr int BC_BYTES = RING + STAGES * SLOT * 64;
+  // phase C layout over the [BM x MIDN] T1' tile (4 waves, 64-channel wave columns)
+  static constexpr int WNC = NEXT ? MIDN / 64 : 1;
+  static constexpr int WMC = 4 / WNC;
+  static constexpr int WPXC = BM / WMC;
+  static constexpr int FIC = WPXC / 16;
+  static constexpr int CBC = NEXT ? MIDN / 64 : 1;  // C weight-row DMAs per wave per stage
   static constexpr int LDS = A_BYTES > BC_BYTES ? A_BYTES : BC_BYTES;
   static constexpr int NP = 4 * MID / 64;     // 64-channel passes over c3's output
   static constexpr int NB = MID / 32;         // B steps (K = MID)
@@ -108,10 +116,10 @@ struct ChainCfg {
   static constexpr int BFI = BPW / 16;        // B: pixel fragments per wave
   static constexpr int NR = Y_BYTES / 1024 / 4;   // residual-chunk DMAs per wave
   static constexpr int NS = Y_BYTES / 16 / 256;   // 16-B Y copy-out stores per thread
-  static constexpr int NT = T2_BYTES / 16 / 256;  // 16-B T1' copy-out stores per thread
+  static_assert(!NEXT || BM * MIDN * 2 <= RING, "T1' staging fits below the weight ring");
   static constexpr int MINW = LDS <= 160 * 1024 / 3 ? 3 : 2;  // workgroups (= waves per SIMD) per CU
   static_assert(LDS <= 80 * 1024, "two workgroups per CU");
-  static_assert(FI >= 1 && FI <= 4 && BFI >= 1, "tile");
+  static_assert(FI >= 1 && FI <= 4 && BFI >= 1 && FIC >= 1 && FIC <= 4, "tile");
 };
 
 // byte offset of the 8-byte group holding channels n..n+3 of row r in a K-blocked swizzled tile of BM rows
@@ -121,10 +129,13 @@ __device__ __forceinline__ uint32_t tile_off(int r, int n) {
   return kb * BM * 64 + r * 64 + ((((e >> 3) ^ swz(r)) << 4) | (((e >> 2) & 1) << 3));
 }
 
-template <int MID, int BM_, bool NEXT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ChainCfg<MID, BM_>::MINW, ChainCfg<MID, BM_>::MINW)))
+template <int MID, int BM_, int MIDN>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ChainCfg<MID, BM_, MIDN>::MINW,
+                                                                     ChainCfg<MID, BM_, MIDN>::MINW)))
 void conv_chain_kernel(const ChainParams p) {
-  using Cfg = ChainCfg<MID, BM_>;
+  using Cfg = ChainCfg<MID, BM_, MIDN>;
+  constexpr bool NEXT = Cfg::NEXT;
+  constexpr int FIC = Cfg::FIC, WPXC = Cfg::WPXC, CBC = Cfg::CBC;
   constexpr int WM = Cfg::WM, BM = Cfg::BM, STAGES = Cfg::STAGES, CA = Cfg::CA, CB = Cfg::CB;
   constexpr int FI = Cfg::FI, WPX = Cfg::WPX;
   constexpr int NB = Cfg::NB, NC = Cfg::NC, SP = Cfg::SP, BFI = Cfg::BFI;
@@ -238,7 +249,7 @@ void conv_chain_kernel(const ChainParams p) {
 
   // ================= passes: B (c3 chunk), Y epilogue, C (c1' partial) =================
   // Weight stream step t: pass t / SP; NB steps of W3 rows [64 pp, +64) (B, k = 32 kb of MID), then
-  // NC steps of W1' (all MID rows, k columns 64 pp + 32 kb) (C, NEXT only).
+  // NC steps of W1' (all MIDN rows, k columns 64 pp + 32 kb) (C, NEXT only).
   constexpr int SPW = NEXT ? SP : NB;
   constexpr int NW = Cfg::NP * SPW;
   int ops = 0;        // vector-memory ops this wave issued since the phase-A drain
@@ -246,15 +257,15 @@ void conv_chain_kernel(const ChainParams p) {
   auto issue_w = [&](int t) __attribute__((always_inline)) {
     if (t >= NW) return;
     const int pp = t / SPW, r = t % SPW;
-    const uint32_t ws = RING + (t % STAGES) * MID * 64;
+    const uint32_t ws = RING + (t % STAGES) * Cfg::SLOT * 64;
     if (r < NB) {  // 64 rows: one DMA per wave
       glds16(p.w3 + static_cast<long>(pp * 64 + 16 * wave + rin) * p.kpad3 + r * BK + 8 * c, ws + 16 * wave * 64);
       ops += 1;
     } else {
       const uint16_t* src = p.w1n + static_cast<long>(16 * wave + rin) * p.kpad1n + pp * 64 + (r - NB) * BK + 8 * c;
 #pragma unroll
-      for (int i = 0; i < CB; ++i) glds16(src + i * 64L * p.kpad1n, ws + 16 * (wave + 4 * i) * 64);
-      ops += CB;
+      for (int i = 0; i < CBC; ++i) glds16(src + i * 64L * p.kpad1n, ws + 16 * (wave + 4 * i) * 64);
+      ops += CBC;
     }
     stage_end[t] = ops;
   };
@@ -276,9 +287,10 @@ void conv_chain_kernel(const ChainParams p) {
     }
   }
 
-  f32x4_t accn[FI][4];  // T1' accumulators (NEXT), phase A wave layout, live across the passes
+  const int wmc = wave % Cfg::WMC, wnc = wave / Cfg::WMC;
+  f32x4_t accn[FIC][4];  // T1' accumulators (NEXT), phase C wave layout, live across the passes
 #pragma unroll
-  for (int i = 0; i < FI; ++i)
+  for (int i = 0; i < FIC; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) accn[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
@@ -296,7 +308,7 @@ void conv_chain_kernel(const ChainParams p) {
       const int t = t0 + kk;
       step_wait(t);
       bf16x8_t fw[4], fx[BFI];
-      const uint8_t* w_ = smem + Cfg::RING + (t % STAGES) * MID * 64 + fofs;
+      const uint8_t* w_ = smem + Cfg::RING + (t % STAGES) * Cfg::SLOT * 64 + fofs;
       const uint8_t* x_ = t2buf + kk * BM * 64 + (wave * Cfg::BPW) * 64 + fofs;
 #pragma unroll
       for (int j = 0; j < 4; ++j) fw[j] = *reinterpret_cast<const bf16x8_t*>(w_ + j * 1024);
@@ -316,15 +328,15 @@ void conv_chain_kernel(const ChainParams p) {
     for (int kk = 0; kk < NC; ++kk) {
       const int t = t0 + kk;
       step_wait(t);
-      bf16x8_t fw[4], fx[FI];
-      const uint8_t* w_ = smem + Cfg::RING + (t % STAGES) * MID * 64 + (wn * 64) * 64 + fofs;
-      const uint8_t* x_ = ybuf + kk * BM * 64 + (wm * WPX) * 64 + fofs;
+      bf16x8_t fw[4], fx[FIC];
+      const uint8_t* w_ = smem + Cfg::RING + (t % STAGES) * Cfg::SLOT * 64 + (wnc * 64) * 64 + fofs;
+      const uint8_t* x_ = ybuf + kk * BM * 64 + (wmc * WPXC) * 64 + fofs;
 #pragma unroll
       for (int j = 0; j < 4; ++j) fw[j] = *reinterpret_cast<const bf16x8_t*>(w_ + j * 1024);
 #pragma unroll
-      for (int i = 0; i < FI; ++i) fx[i] = *reinterpret_cast<const bf16x8_t*>(x_ + i * 1024);
+      for (int i = 0; i < FIC; ++i) fx[i] = *reinterpret_cast<const bf16x8_t*>(x_ + i * 1024);
 #pragma unroll
-      for (int i = 0; i < FI; ++i)
+      for (int i = 0; i < FIC; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           accn[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[j], fx[i], accn[i][j], 0, 0, 0);
@@ -358,7 +370,7 @@ void conv_chain_kernel(const ChainParams p) {
     ops += N;
   };
   using W64 = std::integral_constant<int, 64>;
-  using WMID = std::integral_constant<int, MID>;
+  using WMIDN = std::integral_constant<int, NEXT ? MIDN : 64>;
   uint16_t* ybase[Cfg::NS];
   row_bases(W64{}, p.y, C4, ybase);
 
@@ -424,38 +436,39 @@ void conv_chain_kernel(const ChainParams p) {
   copy_out(W64{}, ybuf, ybase, (Cfg::NP - 1) * 64);
 
   if constexpr (NEXT) {
-    // T1' epilogue through the (idle) T2 buffer, then 16-B copy-out
+    // T1' epilogue through the (idle) T2 (+ Y) buffer, then 16-B copy-out
+    if constexpr (MIDN > MID) lds_barrier();  // the staging overlaps the Y chunk the copy-out just read
 #pragma unroll
-    for (int i = 0; i < FI; ++i) {
-      const int r = wm * WPX + 16 * i + (lane & 15);
+    for (int i = 0; i < FIC; ++i) {
+      const int r = wmc * WPXC + 16 * i + (lane & 15);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int n = wn * 64 + 16 * j + 4 * lg;
-        const f32x4_t b = bias4(p.b1n + wn * 64 + 16 * j, lg);
+        const int n = wnc * 64 + 16 * j + 4 * lg;
+        const f32x4_t b = bias4(p.b1n + wnc * 64 + 16 * j, lg);
         *reinterpret_cast<uint2*>(t2buf + tile_off<BM>(r, n)) =
             make_uint2(pack_bf16x2(fmaxf(accn[i][j][0] + b[0], lo), fmaxf(accn[i][j][1] + b[1], lo)),
                        pack_bf16x2(fmaxf(accn[i][j][2] + b[2], lo), fmaxf(accn[i][j][3] + b[3], lo)));
       }
     }
     lds_barrier();
-    uint16_t* tbase[Cfg::NT];
-    row_bases(WMID{}, p.t1n, MID, tbase);
-    copy_out(WMID{}, t2buf, tbase, 0);
+    uint16_t* tbase[BM * MIDN / 8 / 256];
+    row_bases(WMIDN{}, p.t1n, MIDN, tbase);
+    copy_out(WMIDN{}, t2buf, tbase, 0);
   }
 }
 
-template <int MID, int BM, bool NEXT>
+template <int MID, int BM, int MIDN>
 int launch_chain(const ChainParams& p, hipStream_t s) {
-  using Cfg = ChainCfg<MID, BM>;
+  using Cfg = ChainCfg<MID, BM, MIDN>;
   static bool attr = false;
   if (!attr) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(conv_chain_kernel<MID, BM, NEXT>),
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(conv_chain_kernel<MID, BM, MIDN>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, Cfg::LDS) != hipSuccess)
       return AI4E_ELAUNCH;
     attr = true;
   }
   const int nb = ai4e_cdiv(p.M, Cfg::BM);
-  hipLaunchKernelGGL((conv_chain_kernel<MID, BM, NEXT>), dim3(nb), dim3(256), Cfg::LDS, s, p);
+  hipLaunchKernelGGL((conv_chain_kernel<MID, BM, MIDN>), dim3(nb), dim3(256), Cfg::LDS, s, p);
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
 }
 
@@ -469,13 +482,14 @@ T* symbol_ptr(const void* sym) {
 
 // Fused bottleneck chain (see header). x: T1 NHWC [N,H,W,ldx] bf16 (MID channels at offset 0);
 // w2 [>=MID rows, kpad2 >= 9*MID] (k = (kh, kw, c)); w3 [>=4*MID rows, kpad3 >= MID];
-// w1n [>=MID rows, kpad1n >= 4*MID] (nullptr: no next block, t1n unused); res, y [M, 4*MID];
-// t1n [M, MID]. 3x3, pad 1, stride 1 or 2. MID in {64, 128}.
+// w1n [>=MIDN rows, kpad1n >= 4*MID] (nullptr: no next block, t1n unused); res, y [M, 4*MID];
+// t1n [M, MIDN]. 3x3, pad 1, stride 1 or 2. (MID, MIDN) in {(64, 64), (64, 128), (128, 128)}; midn 0 = mid.
 AI4E_API int ai4e_conv_chain_fwd(const void* x, const void* w2, const void* b2, const void* w3, const void* b3,
                                  const void* res, void* y, const void* w1n, const void* b1n, void* t1n, int N, int H,
-                                 int W, int ldx, int mid, int stride, int kpad2, int kpad3, int kpad1n,
+                                 int W, int ldx, int mid, int midn, int stride, int kpad2, int kpad3, int kpad1n,
                                  int tile_cfg, hipStream_t stream) {
-  if ((mid != 64 && mid != 128) || ldx % 8 || ldx < mid || kpad2 < 9 * mid || kpad2 % 64 ||
+  if (midn == 0) midn = mid;
+  if ((mid != 64 && mid != 128) || (midn != mid && !(mid == 64 && midn == 128)) || ldx % 8 || ldx < mid || kpad2 < 9 * mid || kpad2 % 64 ||
       kpad3 < mid || kpad3 % 8 || (stride != 1 && stride != 2) || !x || !w2 || !b2 || !w3 || !b3 || !res || !y ||
       (w1n && (!b1n || !t1n || kpad1n < 4 * mid || kpad1n % 8)))
     return AI4E_EINVAL;
@@ -504,8 +518,9 @@ AI4E_API int ai4e_conv_chain_fwd(const void* x, const void* w2, const void* b2, 
   const bool next = w1n != nullptr;
   // tile_cfg: 0 = default (MID 64: 256 pixels, MID 128: 128), 1 = 128-pixel MID-64 tile (48 KB LDS, 3 per CU)
   if (mid == 64) {
-    if (tile_cfg == 1) return next ? launch_chain<64, 128, true>(p, stream) : launch_chain<64, 128, false>(p, stream);
-    return next ? launch_chain<64, 256, true>(p, stream) : launch_chain<64, 256, false>(p, stream);
+    if (next && midn == 128) return launch_chain<64, 128, 128>(p, stream);
+    if (tile_cfg == 1) return next ? launch_chain<64, 128, 64>(p, stream) : launch_chain<64, 128, 0>(p, stream);
+    return next ? launch_chain<64, 256, 64>(p, stream) : launch_chain<64, 256, 0>(p, stream);
   }
-  return next ? launch_chain<128, 128, true>(p, stream) : launch_chain<128, 128, false>(p, stream);
+  return next ? launch_chain<128, 128, 128>(p, stream) : launch_chain<128, 128, 0>(p, stream);
 }

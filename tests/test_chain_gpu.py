@@ -29,8 +29,10 @@ def _conv(x, w, b, stride=1, pad=0):
 
 
 CASES = [
-    # n, h, w, mid, stride, next
+    # n, h, w, mid, stride, next (True = same width, or the chained 1x1's output width)
     (2, 56, 56, 64, 1, True),
+    (2, 56, 56, 64, 1, 128),      # layer1 -> layer2 boundary
+    (1, 15, 13, 64, 1, 128),
     (2, 56, 56, 64, 1, False),
     (1, 15, 13, 64, 1, True),     # M = 195: one partial tile
     (3, 9, 11, 64, 2, True),      # strided 3x3, ragged
@@ -45,13 +47,14 @@ CASES = [
 @pytest.mark.parametrize("tile", [0, 1])
 def test_conv_chain(case, tile):
     n, h, w, mid, s, nxt = case
-    if tile == 1 and mid != 64:
-        pytest.skip("128-pixel tile variant is MID 64 only")
-    assert chain_kernel_builds(mid, nxt)
+    midn = 0 if not nxt else (mid if nxt is True else nxt)
+    if tile == 1 and (mid != 64 or midn == 128):
+        pytest.skip("tile config 1 is the MID-64, same-width variant")
+    assert chain_kernel_builds(mid, midn)
     torch.manual_seed(7)
     c2 = pack_conv(torch.randn(mid, mid, 3, 3) / (9 * mid) ** 0.5, torch.randn(mid) * 0.1, stride=s, pad=1).to(DEV)
     c3 = pack_conv(torch.randn(4 * mid, mid, 1, 1) / mid ** 0.5, torch.randn(4 * mid) * 0.1).to(DEV)
-    c1n = pack_conv(torch.randn(mid, 4 * mid, 1, 1) / (4 * mid) ** 0.5, torch.randn(mid) * 0.1).to(DEV) if nxt else None
+    c1n = pack_conv(torch.randn(midn, 4 * mid, 1, 1) / (4 * mid) ** 0.5, torch.randn(midn) * 0.1).to(DEV) if nxt else None
     t1 = torch.randn(n, h, w, mid, device=DEV).relu().to(torch.bfloat16)
     oh, ow = c2.out_hw(h, w)
     res = torch.randn(n, oh, ow, 4 * mid, device=DEV).to(torch.bfloat16)
@@ -63,7 +66,7 @@ def test_conv_chain(case, tile):
     err = (y.float() - yr).abs().max().item()
     assert err <= 0.02 * yr.abs().max().item() + 0.03, err
     if nxt:
-        tr = F.relu(_conv(y, _wq(c1n, 1), c1n.bias[:mid]))
+        tr = F.relu(_conv(y, _wq(c1n, 1), c1n.bias[:midn]))
         err = (t1n.float() - tr).abs().max().item()
         assert err <= 0.02 * tr.abs().max().item() + 0.03, err
     else:
