@@ -21,6 +21,7 @@ import torch.nn.functional as F
 
 from ..ops.conv import (PackedConv, chain_supported, conv2d_nhwc, conv_chain, fold_bn, pack_conv,
                         pack_stem_s2d, stem_pool)
+from ..ops.head import softmax_topk
 from ..ops.pool import (global_avgpool_nhwc, maxpool2d_nhwc, preprocess_s2d_u8, preprocess_u8,
                         space_to_depth_shifted)
 
@@ -262,9 +263,18 @@ class FusedResNet:
             y = self._block(y, blk)
         return y
 
-    def forward(self, x: torch.Tensor, preprocess=None) -> torch.Tensor:
+    def logits(self, x: torch.Tensor, preprocess=None) -> torch.Tensor:
+        """bf16 logits [N, classes]."""
         f = global_avgpool_nhwc(self.forward_features(x, preprocess))
-        return conv2d_nhwc(f, self.fc).reshape(f.shape[0], -1).float()
+        return conv2d_nhwc(f, self.fc).reshape(f.shape[0], -1)
+
+    def forward(self, x: torch.Tensor, preprocess=None) -> torch.Tensor:
+        return self.logits(x, preprocess).float()
+
+    def topk_u8(self, img_u8: torch.Tensor, k: int = 5):
+        """uint8 NHWC images -> (top-k class ids int32, probabilities fp32): the serving head, with softmax
+        and top-k fused into one kernel (ops/head.py)."""
+        return softmax_topk(self.logits(img_u8, preprocess=preprocess_s2d_u8), k)
 
     def forward_u8(self, img_u8: torch.Tensor) -> torch.Tensor:
         """uint8 NHWC images -> fp32 logits (preprocess fused into the first kernel launch)."""

@@ -93,8 +93,10 @@ class InferenceEngine:
 
     def __init__(self, model_fn: Callable[[torch.Tensor], torch.Tensor], item_shape: Sequence[int], max_batch: int,
                  device: Optional[torch.device] = None, topk: int = 5, use_graphs: bool = True, nbuf: int = 3,
-                 buckets: Optional[Sequence[int]] = None):
+                 buckets: Optional[Sequence[int]] = None,
+                 head_fn: Optional[Callable[[torch.Tensor, int], Tuple[torch.Tensor, torch.Tensor]]] = None):
         self.model_fn = model_fn
+        self.head_fn = head_fn  # optional images -> (top-k idx int32, prob fp32), e.g. FusedResNet.topk_u8
         self.device = torch.device(device or "cuda")
         self.item_shape = tuple(item_shape)
         self.max_batch = max_batch
@@ -118,6 +120,9 @@ class InferenceEngine:
 
     # -------------------------------------------------------------- forward
     def _forward_into(self, buf: int, b: int):
+        if self.head_fn is not None:
+            i, p = self.head_fn(self.inputs[buf][:b], self.topk)
+            return i, p
         logits = self.model_fn(self.inputs[buf][:b])
         prob = torch.softmax(logits.float(), dim=1)
         p, i = torch.topk(prob, self.topk, dim=1)

@@ -109,7 +109,7 @@ def _child_main(rank: int, device: str, spec: ModelSpec, shm_name: str, nslots: 
             registered = False
     model = _load_factory(spec.factory)(device=device, **spec.kwargs)
     engine = InferenceEngine(model, spec.item_shape, spec.max_batch, device=dev, topk=spec.topk,
-                             use_graphs=spec.use_graphs)
+                             use_graphs=spec.use_graphs, head_fn=getattr(model, "topk_u8", None))
     engine.warmup()
     fault = _parse_fault(rank)
     send_mu = threading.Lock()

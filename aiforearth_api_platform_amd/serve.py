@@ -67,7 +67,8 @@ def build_platform(doc: Dict[str, Any], cfg: Config):
             dev = torch.device(devs[0])
             model = _load(e["factory"])(device=str(dev), **(e.get("kwargs") or {}))
             eng = InferenceEngine(model, shape, mb, device=dev, topk=int(e.get("topk", 5)),
-                                  use_graphs=bool(e.get("hip_graphs", cfg.use_hip_graphs)))
+                                  use_graphs=bool(e.get("hip_graphs", cfg.use_hip_graphs)),
+                                  head_fn=getattr(model, "topk_u8", None))
             eng.warmup()
             ring = PayloadRing(mb * 4, shape)
             ep = ModelEndpoint(cp, e["path"], eng, ring, base_url=base_url)

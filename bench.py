@@ -75,7 +75,8 @@ def main():
 
     B, S = args.batch, args.image_size
     model = FusedResNet(resnet50(seed=0), device=device)
-    engine = InferenceEngine(model.forward_u8, (S, S, 3), B, device=device, use_graphs=not args.no_graphs)
+    engine = InferenceEngine(model.forward_u8, (S, S, 3), B, device=device, use_graphs=not args.no_graphs,
+                             head_fn=model.topk_u8)
     engine.warmup()
 
     cfg = Config.load(env={}, max_batch=B, max_batch_delay_ms=0.0)

@@ -106,3 +106,21 @@ def test_stem_pool(shape):
     assert y.shape == ref.shape
     err = (y.float() - ref).abs().max().item()
     assert err <= 0.02 * ref.abs().max().item() + 0.02, err
+
+
+@pytest.mark.parametrize("shape", [(256, 1000, 5), (3, 1000, 1), (7, 10, 10), (2, 2048, 5), (5, 1500, 3)])
+def test_softmax_topk(shape):
+    """Fused softmax + top-k head kernel vs torch.softmax + torch.topk on the same bf16 logits."""
+    from aiforearth_api_platform_amd.ops.head import softmax_topk
+
+    n, c, k = shape
+    torch.manual_seed(11)
+    logits = (torch.randn(n, c, device=DEV) * 3).to(torch.bfloat16)
+    idx, prob = softmax_topk(logits, k)
+    torch.cuda.synchronize()
+    rp, ri = torch.topk(torch.softmax(logits.float(), 1), k, 1)
+    assert idx.dtype == torch.int32 and prob.dtype == torch.float32
+    assert torch.allclose(prob, rp, rtol=1e-4, atol=1e-6)
+    # bf16 logits tie often: compare the probability of the chosen class, not the index
+    chosen = torch.softmax(logits.float(), 1).gather(1, idx.long())
+    assert torch.allclose(chosen, rp, rtol=1e-4, atol=1e-6)
