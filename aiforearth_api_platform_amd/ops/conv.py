@@ -204,7 +204,10 @@ def conv_chain(t1: torch.Tensor, c2: PackedConv, c3: PackedConv, residual: torch
 CHAIN_TILE = {64: int(__import__("os").environ.get("AI4E_CHAIN_TILE64", "1")), 128: 0}
 
 
-def stem_pool(x: torch.Tensor, pc: PackedConv) -> torch.Tensor:
+STEM_VARIANT = int(__import__("os").environ.get("AI4E_STEM_VARIANT", "0"))
+
+
+def stem_pool(x: torch.Tensor, pc: PackedConv, variant: int = -1) -> torch.Tensor:
     """Fused s2d stem (K1s): ``maxpool3x3/2(relu(conv4x4(x) + b))`` in one kernel; ``x`` = the
     ``[N,H,W,16]`` space-to-depth input, ``pc`` from ``pack_stem_s2d``. PyTorch backend: the two ops."""
     from .pool import maxpool2d_nhwc
@@ -216,7 +219,7 @@ def stem_pool(x: torch.Tensor, pc: PackedConv) -> torch.Tensor:
         raise ValueError("stem_pool: contiguous bf16 [N,H,W,16] input required")
     y = torch.empty(n, (h - 1) // 2 + 1, (w - 1) // 2 + 1, 64, device=x.device, dtype=x.dtype)
     _ext.call("ai4e_stem_pool_fwd", x.data_ptr(), pc.w_packed.data_ptr(), pc.bias.data_ptr(), y.data_ptr(), n, h, w,
-              pc.kpad, _ext.stream_ptr(x.device))
+              pc.kpad, STEM_VARIANT if variant < 0 else variant, _ext.stream_ptr(x.device))
     return y
 
 

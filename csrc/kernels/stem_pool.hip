@@ -163,12 +163,144 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
   }
 }
 
+
+// ---- v2: direct conv from the input footprint in LDS (persistent workgroups).
+// The 15x17 conv region of a tile reads an 18x20 input footprint (the 4x4 taps overlap 16-fold), so
+// instead of gathering 16 taps x 255 pixels through the DMA ring (128 KB per tile) the footprint is
+// DMA'd once (360 pixels x 32 B = 11.25 KB, zero outside the image) and every MFMA operand fragment is
+// read straight from it: the K step kt covers taps 2kt, 2kt+1 of filter row kt/2, a lane group g reads
+// the 8 channels 8(g&1) of tap 2kt + (g>>1) of its pixel. The footprint is stored as two channel planes
+// (channels 0-7 | 8-15, 16 B per pixel) so 16 lanes reading 16 consecutive pixels hit 16 distinct bank
+// quads. The 64 x 256 weights (32 KB) stay in LDS for the whole persistent loop, each 512-B row with its
+// 16-B chunk index XOR (row & 31) so the 16 rows of a fragment read hit distinct bank quads.
+constexpr int FP_R = SP_RR + 3, FP_C = SP_RC + 3, FP_PIX = FP_R * FP_C;  // 18 x 20 footprint
+constexpr int FP_SLOTS = 2 * FP_PIX;                                    // 720 16-B slots (2 planes)
+constexpr int FP_DMA = (FP_SLOTS + 255) / 256;                          // DMA instrs per wave (3)
+constexpr int D_W = 0, D_FP = 64 * 512, D_TILE = D_FP + FP_DMA * 4 * 1024, D_LDS = D_TILE + SP_BM * 128;
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
+void stem_pool_direct_kernel(const StemParams p, int ntiles) {
+  extern __shared__ __attribute__((aligned(1024))) uint8_t dsm[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const uint32_t sb = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(dsm));
+  // weights -> LDS once: row n (512 B), chunk q stored at chunk q ^ (n & 31)
+  for (int e = tid; e < 64 * 32; e += 256) {
+    const int n = e >> 5, q = e & 31;
+    *reinterpret_cast<uint4*>(dsm + D_W + n * 512 + ((q ^ (n & 31)) << 4)) =
+        *reinterpret_cast<const uint4*>(p.w + static_cast<long>(n) * p.kpad + 8 * q);
+  }
+  float4 bias[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) bias[j] = *reinterpret_cast<const float4*>(p.bias + 16 * j + 4 * (lane >> 4));
+  const int per_img = p.tiles_r * p.tiles_c;
+  const int g = lane >> 4;
+  // this lane's 4 pixels (one per fragment i): region coords and footprint base
+  int fpb[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = wave * 64 + 16 * i + (lane & 15);
+    const int r = m / SP_RC, cc = m - r * SP_RC;
+    fpb[i] = m < SP_RR * SP_RC ? r * FP_C + cc : 0;  // the idle 256th row reads pixel 0 (never pooled)
+  }
+  uint8_t* const tile = dsm + D_TILE;
+
+  for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const int img = t / per_img;
+    const int tr = (t - img * per_img) / p.tiles_c;
+    const int tc = t - img * per_img - tr * p.tiles_c;
+    const int ph0 = tr * SP_TR, pw0 = tc * SP_TC;
+    const int oh0 = 2 * ph0 - 1, ow0 = 2 * pw0 - 1;
+    const uint16_t* const xi = p.x + static_cast<long>(img) * p.H * p.W * SP_C;
+    // footprint DMA: slot s = plane * FP_PIX + pixel; footprint pixel (a, b) is input (oh0-1+a, ow0-1+b)
+#pragma unroll
+    for (int q = 0; q < FP_DMA; ++q) {
+      const int s = (wave + 4 * q) * 64 + lane;
+      const int h = s >= FP_PIX ? 1 : 0, pix = s - h * FP_PIX;
+      const int a = pix / FP_C, b = pix - a * FP_C;
+      const int ih = oh0 - 1 + a, iw = ow0 - 1 + b;
+      const bool ok = s < FP_SLOTS && static_cast<unsigned>(ih) < static_cast<unsigned>(p.H) &&
+                      static_cast<unsigned>(iw) < static_cast<unsigned>(p.W);
+      glds16(ok ? static_cast<const void*>(xi + (static_cast<long>(ih) * p.W + iw) * SP_C + 8 * h) : p.zero,
+             sb + D_FP + (wave + 4 * q) * 1024);
+    }
+    wait_vmcnt<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // footprint (and weights) visible
+
+    f32x4_t acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kt = 0; kt < SP_NK; ++kt) {
+      const int kh = kt >> 1, kw = 2 * (kt & 1) + (g >> 1);
+      const int plane = (g & 1) * FP_PIX * 16;
+      bf16x8_t fw[4], fx[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = 16 * j + (lane & 15);
+        fw[j] = *reinterpret_cast<const bf16x8_t*>(dsm + D_W + n * 512 + (((4 * kt + g) ^ (n & 31)) << 4));
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        fx[i] = *reinterpret_cast<const bf16x8_t*>(dsm + D_FP + plane + (fpb[i] + kh * FP_C + kw) * 16);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[j], fx[i], acc[i][j], 0, 0, 0);
+    }
+    // epilogue: bf16 relu(acc + b) -> tile [256 px][64 ch] (128-B rows, 16-B chunk ^= px & 7)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = wave * 64 + 16 * i + (lane & 15);
+      const int r = m / SP_RC, cc = m - r * SP_RC;
+      const bool live = m < SP_RR * SP_RC && oh0 + r >= 0 && oh0 + r < p.H && ow0 + cc >= 0 && ow0 + cc < p.W;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = 16 * j + 4 * (lane >> 4);
+        const float4 b = bias[j];
+        uint2 v = make_uint2(0u, 0u);
+        if (live)
+          v = make_uint2(pack_bf16x2(fmaxf(acc[i][j][0] + b.x, 0.f), fmaxf(acc[i][j][1] + b.y, 0.f)),
+                         pack_bf16x2(fmaxf(acc[i][j][2] + b.z, 0.f), fmaxf(acc[i][j][3] + b.w, 0.f)));
+        *reinterpret_cast<uint2*>(tile + m * 128 + ((((n >> 3) ^ (m & 7)) << 4) | (((n >> 2) & 1) << 3))) = v;
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    for (int task = tid; task < SP_TR * SP_TC * 8; task += 256) {
+      const int q = task >> 3, k8 = task & 7;
+      const int py = q / SP_TC, px = q - py * SP_TC;
+      const int ph = ph0 + py, pw = pw0 + px;
+      if (ph >= p.PH || pw >= p.PW) continue;
+      uint4 mx = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+      for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx) {
+          const int m = (2 * py + dy) * SP_RC + 2 * px + dx;
+          const uint4 v = *reinterpret_cast<const uint4*>(tile + m * 128 + ((k8 ^ (m & 7)) << 4));
+          mx.x = max_bf16x2(mx.x, v.x);
+          mx.y = max_bf16x2(mx.y, v.y);
+          mx.z = max_bf16x2(mx.z, v.z);
+          mx.w = max_bf16x2(mx.w, v.w);
+        }
+      *reinterpret_cast<uint4*>(p.y + ((static_cast<long>(img) * p.PH + ph) * p.PW + pw) * SP_BN + 8 * k8) = mx;
+    }
+    // the next tile's footprint DMA and epilogue overwrite what this tile's readers still use
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  }
+}
+
 }  // namespace
 
 // x: s2d stem input [N, H, W, 16] bf16; w: packed 4x4x16 stem weights [>= 64 rows, kpad >= 256] (pad 1/2,
 // ops/conv.py pack_stem_s2d); bias [>= 64] fp32; y: [N, ceil(H/2), ceil(W/2), 64] bf16.
+// variant: 0 = direct conv from the LDS input footprint (persistent, default), 1 = DMA-gather implicit GEMM.
 AI4E_API int ai4e_stem_pool_fwd(const void* x, const void* w, const void* bias, void* y, int N, int H, int W, int kpad,
-                                hipStream_t stream) {
+                                int variant, hipStream_t stream) {
   if (!x || !w || !bias || !y || kpad < 256 || kpad % 8 || H <= 0 || W <= 0) return AI4E_EINVAL;
   static const uint16_t* zero = nullptr;
   if (!zero) {
@@ -190,6 +322,21 @@ AI4E_API int ai4e_stem_pool_fwd(const void* x, const void* w, const void* bias, 
   p.tiles_c = ai4e_cdiv(p.PW, SP_TC);
   const long nb = static_cast<long>(N) * p.tiles_r * p.tiles_c;
   if (nb <= 0) return AI4E_OK;
+  if (variant == 0) {
+    static bool attr = false;
+    if (!attr) {
+      if (hipFuncSetAttribute(reinterpret_cast<const void*>(stem_pool_direct_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, D_LDS) != hipSuccess)
+        return AI4E_ELAUNCH;
+      attr = true;
+    }
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const long grid = nb < 2L * cus ? nb : 2L * cus;  // two persistent workgroups per CU
+    hipLaunchKernelGGL(stem_pool_direct_kernel, dim3(static_cast<unsigned>(grid)), dim3(256), D_LDS, stream, p,
+                       static_cast<int>(nb));
+    return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
+  }
   hipLaunchKernelGGL(stem_pool_kernel, dim3(static_cast<unsigned>(nb)), dim3(256), 0, stream, p);
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
 }

@@ -89,8 +89,9 @@ def test_resnet_chain_matches_unfused(monkeypatch):
     assert (a.argmax(1) == b.argmax(1)).float().mean().item() >= 0.75
 
 
-@pytest.mark.parametrize("shape", [(2, 112, 112), (3, 30, 26), (1, 17, 9)])
-def test_stem_pool(shape):
+@pytest.mark.parametrize("shape", [(2, 112, 112), (3, 30, 26), (1, 17, 9), (600, 16, 16)])
+@pytest.mark.parametrize("variant", [0, 1])
+def test_stem_pool(shape, variant):
     """K1s fused s2d stem conv + ReLU + 3x3/2 max-pool vs PyTorch fp32 (conv output rounded to bf16)."""
     from aiforearth_api_platform_amd.ops.conv import pack_stem_s2d, stem_pool
 
@@ -98,7 +99,7 @@ def test_stem_pool(shape):
     torch.manual_seed(5)
     pc = pack_stem_s2d(torch.randn(64, 3, 7, 7) / 12, torch.randn(64) * 0.1).to(DEV)
     x = torch.randn(n, h, w, 16, device=DEV).to(torch.bfloat16)
-    y = stem_pool(x, pc)
+    y = stem_pool(x, pc, variant=variant)
     torch.cuda.synchronize()
     xp = F.pad(x.float().permute(0, 3, 1, 2), (1, 2, 1, 2))
     conv = F.relu(F.conv2d(xp, _wq(pc, 4), pc.bias[:64])).to(torch.bfloat16).float()
