@@ -154,6 +154,7 @@ class FusedResNet:
         self.num_classes = model.fc.out_features
         self.chunk = chunk if chunk is not None else _env_chunk()
         self.chain = _env_chain()
+        self.fold_down = os.environ.get("AI4E_RESNET_FOLD_DOWN", "1") not in ("0", "off", "")
         # stages: runs of blocks starting at a block with a downsample conv
         self.stages: List[List[Tuple[PackedConv, PackedConv, PackedConv, Optional[PackedConv]]]] = []
         for blk in self.blocks:
@@ -207,9 +208,11 @@ class FusedResNet:
         t1 = None
         for si, blocks in enumerate(self.stages):
             c1, _, _, down = blocks[0]
-            idt = y if down is None else conv2d_nhwc(y, down)
             if t1 is None:
                 t1 = conv2d_nhwc(y, c1, relu=True)
+            # the first block's downsample: folded into the chain kernel where it can be (layer1), else a K1 conv
+            x0, dn = (y, down) if down is not None and down.stride == 1 and self.fold_down else (None, None)
+            idt = None if dn is not None else (y if down is None else conv2d_nhwc(y, down))
             for i, (_, c2, c3, _) in enumerate(blocks):
                 if i + 1 < len(blocks):
                     nxt = blocks[i + 1][0]
@@ -219,7 +222,8 @@ class FusedResNet:
                     nxt = None
                 if nxt is not None and not chain_supported(c2.cout, nxt.cout) and chain_supported(c2.cout):
                     nxt = None  # keep the chain, run the next c1 as its own K1 launch
-                idt, t1 = conv_chain(t1, c2, c3, idt, c1n=nxt)
+                idt, t1 = conv_chain(t1, c2, c3, idt, c1n=nxt, down=dn, x0=x0)
+                x0 = dn = None
             y = idt
         return y
 

@@ -12,7 +12,7 @@ from __future__ import annotations
 
 import math
 from dataclasses import dataclass
-from typing import Optional
+from typing import Optional, Tuple
 
 import torch
 import torch.nn.functional as F
@@ -163,18 +163,40 @@ def chain_supported(mid: int, midn: int = 0) -> bool:
     return chain_kernel_builds(mid, midn)
 
 
-def conv_chain(t1: torch.Tensor, c2: PackedConv, c3: PackedConv, residual: torch.Tensor,
+def _down_pack(c3: PackedConv, down: PackedConv) -> Tuple[torch.Tensor, torch.Tensor]:
+    """[W3 | Wd] along K and b3 + bd: the downsample 1x1 folded into c3 (K1c DOWN mode), cached on c3."""
+    cached = getattr(c3, "_down_pack", None)
+    if cached is not None and cached[0] is down:
+        return cached[1], cached[2]
+    k3, kd = c3.cin_pad, down.cin_pad
+    w = torch.cat([c3.w_packed[:, :k3], down.w_packed[:, :kd]], dim=1).contiguous()
+    b = (c3.bias + down.bias).contiguous()
+    c3._down_pack = (down, w, b)
+    return w, b
+
+
+def conv_chain(t1: torch.Tensor, c2: PackedConv, c3: PackedConv, residual: Optional[torch.Tensor],
                c1n: Optional[PackedConv] = None, out: Optional[torch.Tensor] = None, force: bool = False,
-               tile_cfg: int = -1):
+               tile_cfg: int = -1, down: Optional[PackedConv] = None, x0: Optional[torch.Tensor] = None):
     """Fused bottleneck tail (K1c): ``y = relu(c3(relu(c2(t1))) + residual)`` and, with ``c1n`` (the next
     block's 1x1 reduce), ``t1n = relu(c1n(y))`` from the same kernel. Returns ``(y, t1n or None)``.
 
     ``t1``: NHWC ``[N,H,W,mid]`` bf16 (c1's output), ``c2`` 3x3/pad 1 (stride 1 or 2) mid->mid, ``c3`` 1x1
-    mid->4*mid, ``residual`` ``[N,OH,OW,4*mid]``, ``c1n`` 1x1 4*mid->mid. Shapes the kernel does not cover
+    mid->4*mid, ``residual`` ``[N,OH,OW,4*mid]``, ``c1n`` 1x1 4*mid->mid. With ``residual=None`` and
+    ``down``/``x0`` the residual is ``down(x0)`` (a stage's first block); for mid 64, stride 1 and a chained
+    64-wide c1n the kernel folds that projection into c3's K (no residual tensor at all). Shapes the kernel does not cover
     (``chain_supported``; ``force`` = every shape the kernel builds) and the PyTorch backend run the
     three convs separately.
     """
     n, h, w, mid = t1.shape
+    if residual is None:
+        if down is None or x0 is None:
+            raise ValueError("conv_chain: residual or (down, x0) required")
+        dmode = (_ext.backend_for(t1) == "hip" and mid == 64 and c2.stride == 1 and c1n is not None
+                 and c1n.cout == 64 and down.kh == 1 and down.stride == 1 and down.cin_pad == 64
+                 and x0.is_contiguous() and x0.shape[:3] == t1.shape[:3])
+        if not dmode:
+            residual = conv2d_nhwc(x0, down)
     if (c2.kh, c2.kw, c2.pad, c2.cin_pad, c2.cout) != (3, 3, 1, mid, mid) or c3.kh != 1 or c3.cin_pad != mid \
             or c3.cout != 4 * mid or (c1n is not None and (c1n.kh != 1 or c1n.stride != 1 or c1n.cin_pad != 4 * mid)):
         raise ValueError("conv_chain: layer shapes do not form a bottleneck chain")
@@ -189,14 +211,19 @@ def conv_chain(t1: torch.Tensor, c2: PackedConv, c3: PackedConv, residual: torch
         return out, (conv2d_nhwc(out, c1n, relu=True) if c1n is not None else None)
     if t1.dtype != torch.bfloat16 or not t1.is_contiguous() or not out.is_contiguous():
         raise ValueError("conv_chain: contiguous bf16 NHWC tensors required")
-    if residual.shape != (n, oh, ow, 4 * mid) or not residual.is_contiguous():
+    if residual is not None and (residual.shape != (n, oh, ow, 4 * mid) or not residual.is_contiguous()):
         raise ValueError("conv_chain: residual must be contiguous [N,OH,OW,4*mid]")
+    w3, b3, kpad3 = c3.w_packed, c3.bias, c3.kpad
+    if residual is None:
+        w3, b3 = _down_pack(c3, down)
+        kpad3 = w3.shape[1]
     t1n = torch.empty(n, oh, ow, midn, device=t1.device, dtype=t1.dtype) if c1n is not None else None
     _ext.call("ai4e_conv_chain_fwd", t1.data_ptr(), c2.w_packed.data_ptr(), c2.bias.data_ptr(),
-              c3.w_packed.data_ptr(), c3.bias.data_ptr(), residual.data_ptr(), out.data_ptr(),
+              w3.data_ptr(), b3.data_ptr(), _ext.ptr(residual), out.data_ptr(),
               _ext.ptr(c1n.w_packed if c1n is not None else None), _ext.ptr(c1n.bias if c1n is not None else None),
-              _ext.ptr(t1n), n, h, w, mid, mid, midn, c2.stride, c2.kpad, c3.kpad, c1n.kpad if c1n is not None else 0,
-              CHAIN_TILE.get(mid, 0) if tile_cfg < 0 else tile_cfg, _ext.stream_ptr(t1.device))
+              _ext.ptr(t1n), n, h, w, mid, mid, midn, c2.stride, c2.kpad, kpad3, c1n.kpad if c1n is not None else 0,
+              CHAIN_TILE.get(mid, 0) if tile_cfg < 0 else tile_cfg, _ext.ptr(x0 if residual is None else None),
+              x0.shape[-1] if residual is None else 0, _ext.stream_ptr(t1.device))
     return out, t1n
 
 

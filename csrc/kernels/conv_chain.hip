@@ -81,9 +81,11 @@ struct ChainParams {
   int H, W, ldx, stride, OH, OW, M;
   int kpad2, kpad3, kpad1n;
   uint16_t* sink;
+  const uint16_t* x0;   // DOWN: the block input [M, ldx0] (64 channels) whose 1x1 projection is the residual
+  int ldx0;
 };
 
-template <int MID, int BM_, int MIDN = 0>
+template <int MID, int BM_, int MIDN = 0, bool DOWN = false>
 struct ChainCfg {
   static constexpr int BM = BM_;              // pixels per workgroup
   static constexpr bool NEXT = MIDN > 0;      // chained 1x1 c1' (output width MIDN)
@@ -96,7 +98,10 @@ struct ChainCfg {
   static constexpr int CB = MID / 64;         // phase A / C weight-row DMAs per wave per stage
   static constexpr int A_PX = STAGES * BM * 64;           // phase A: pixel ring, then the weight ring
   static constexpr int A_BYTES = A_PX + STAGES * MID * 64;
-  static constexpr int T2_BYTES = BM * MID * 2;           // T2 [BM x MID] (K-blocked), later T1' staging
+  // B operand [T2 | X0] [BM x KB] (K-blocked; X0 = the 64-channel block input in DOWN mode, where the
+  // downsample 1x1 is folded into c3 as extra K: W3' = [W3 | Wd], b3' = b3 + bd), later T1' staging
+  static constexpr int KB = MID + (DOWN ? 64 : 0);
+  static constexpr int T2_BYTES = BM * KB * 2;
   static constexpr int Y_BYTES = BM * 64 * 2;             // one 64-channel chunk [BM x 64] of R -> Y
   static constexpr int RING = T2_BYTES + Y_BYTES;         // B/C weight ring: STAGES x SLOT rows x 64 B
   static constexpr int SLOT = NEXT ? (MID > MIDN ? MID : MIDN) : MID;  // >= 64 (B) and MIDN (C) rows
@@ -109,7 +114,7 @@ struct ChainCfg {
   static constexpr int CBC = NEXT ? MIDN / 64 : 1;  // C weight-row DMAs per wave per stage
   static constexpr int LDS = A_BYTES > BC_BYTES ? A_BYTES : BC_BYTES;
   static constexpr int NP = 4 * MID / 64;     // 64-channel passes over c3's output
-  static constexpr int NB = MID / 32;         // B steps (K = MID)
+  static constexpr int NB = KB / 32;          // B steps
   static constexpr int NC = 2;                // C steps (K = 64)
   static constexpr int SP = NB + NC;
   static constexpr int BPW = BM / 4;          // B: pixels per wave (all 64 channels of the chunk)
@@ -129,11 +134,11 @@ __device__ __forceinline__ uint32_t tile_off(int r, int n) {
   return kb * BM * 64 + r * 64 + ((((e >> 3) ^ swz(r)) << 4) | (((e >> 2) & 1) << 3));
 }
 
-template <int MID, int BM_, int MIDN>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ChainCfg<MID, BM_, MIDN>::MINW,
-                                                                     ChainCfg<MID, BM_, MIDN>::MINW)))
+template <int MID, int BM_, int MIDN, bool DOWN>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ChainCfg<MID, BM_, MIDN, DOWN>::MINW,
+                                                                     ChainCfg<MID, BM_, MIDN, DOWN>::MINW)))
 void conv_chain_kernel(const ChainParams p) {
-  using Cfg = ChainCfg<MID, BM_, MIDN>;
+  using Cfg = ChainCfg<MID, BM_, MIDN, DOWN>;
   constexpr bool NEXT = Cfg::NEXT;
   constexpr int FIC = Cfg::FIC, WPXC = Cfg::WPXC, CBC = Cfg::CBC;
   constexpr int WM = Cfg::WM, BM = Cfg::BM, STAGES = Cfg::STAGES, CA = Cfg::CA, CB = Cfg::CB;
@@ -269,6 +274,19 @@ void conv_chain_kernel(const ChainParams p) {
     }
     stage_end[t] = ops;
   };
+  if constexpr (DOWN) {
+    // block input X0 -> K blocks MID/32.. of the B operand tile (before the weight prologue, so the first
+    // stage wait also retires it); rows past M re-read row M-1 (never stored)
+#pragma unroll
+    for (int s = 0; s < BM / 32; ++s) {
+      const int q = wave + 4 * s;
+      const int kb = q / (BM / 16), rb = q % (BM / 16);
+      const int row = rb * 16 + rin;
+      glds16(p.x0 + static_cast<long>(min(m0 + row, p.M - 1)) * p.ldx0 + kb * BK + 8 * c,
+             sb + (MID / 32 + kb) * BM * 64 + rb * 16 * 64);
+    }
+    ops += BM / 32;
+  }
 #pragma unroll
   for (int t = 0; t < STAGES - 1; ++t) issue_w(t);
 
@@ -379,16 +397,16 @@ void conv_chain_kernel(const ChainParams p) {
     if constexpr (pp > 0) copy_out(W64{}, ybuf, ybase, (pp - 1) * 64);
     lds_barrier();  // previous Y chunk fully consumed (and T2 visible at pass 0)
     // residual chunk R_pp -> ybuf (K-blocked swizzled [BM x 64], 16-B DMA rows; rows past M re-read
-    // row M-1, never stored)
+    // row M-1, never stored); none in DOWN mode (the projection is part of the B GEMM)
 #pragma unroll
-    for (int s = 0; s < Cfg::NR; ++s) {
+    for (int s = 0; s < (DOWN ? 0 : Cfg::NR); ++s) {
       const int q = wave + 4 * s;
       const int kb = q / (BM / 16), rb = q % (BM / 16);
       const int row = rb * 16 + rin;
       glds16(p.res + static_cast<long>(min(m0 + row, p.M - 1)) * C4 + pp * 64 + kb * BK + 8 * c,
              sb + Cfg::T2_BYTES + kb * BM * 64 + rb * 16 * 64);
     }
-    ops += Cfg::NR;
+    ops += DOWN ? 0 : Cfg::NR;
     const int r_end = ops;
 
     f32x4_t accb[BFI][4];
@@ -398,8 +416,10 @@ void conv_chain_kernel(const ChainParams p) {
       for (int j = 0; j < 4; ++j) accb[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
     seg_b(accb, pp * SPW);
 
-    wait_vmcnt_n(ops - r_end);
-    lds_barrier();  // residual chunk visible
+    if constexpr (!DOWN) {
+      wait_vmcnt_n(ops - r_end);
+      lds_barrier();  // residual chunk visible
+    }
 #pragma unroll
     for (int i = 0; i < BFI; ++i) {
       const int r = wave * Cfg::BPW + 16 * i + (lane & 15);
@@ -408,10 +428,12 @@ void conv_chain_kernel(const ChainParams p) {
         const int n = 16 * j + 4 * lg;
         const f32x4_t b = bias4(p.b3 + pp * 64 + 16 * j, lg);
         uint2* yp = reinterpret_cast<uint2*>(ybuf + tile_off<BM>(r, n));
-        const uint2 rv = *yp;
-        float r0, r1, r2, r3;
-        unpack_bf16x2(rv.x, r0, r1);
-        unpack_bf16x2(rv.y, r2, r3);
+        float r0 = 0.f, r1 = 0.f, r2 = 0.f, r3 = 0.f;
+        if constexpr (!DOWN) {
+          const uint2 rv = *yp;
+          unpack_bf16x2(rv.x, r0, r1);
+          unpack_bf16x2(rv.y, r2, r3);
+        }
         *yp = make_uint2(pack_bf16x2(fmaxf(accb[i][j][0] + b[0] + r0, lo), fmaxf(accb[i][j][1] + b[1] + r1, lo)),
                          pack_bf16x2(fmaxf(accb[i][j][2] + b[2] + r2, lo), fmaxf(accb[i][j][3] + b[3] + r3, lo)));
       }
@@ -457,18 +479,18 @@ void conv_chain_kernel(const ChainParams p) {
   }
 }
 
-template <int MID, int BM, int MIDN>
+template <int MID, int BM, int MIDN, bool DOWN = false>
 int launch_chain(const ChainParams& p, hipStream_t s) {
-  using Cfg = ChainCfg<MID, BM, MIDN>;
+  using Cfg = ChainCfg<MID, BM, MIDN, DOWN>;
   static bool attr = false;
   if (!attr) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(conv_chain_kernel<MID, BM, MIDN>),
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(conv_chain_kernel<MID, BM, MIDN, DOWN>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, Cfg::LDS) != hipSuccess)
       return AI4E_ELAUNCH;
     attr = true;
   }
   const int nb = ai4e_cdiv(p.M, Cfg::BM);
-  hipLaunchKernelGGL((conv_chain_kernel<MID, BM, MIDN>), dim3(nb), dim3(256), Cfg::LDS, s, p);
+  hipLaunchKernelGGL((conv_chain_kernel<MID, BM, MIDN, DOWN>), dim3(nb), dim3(256), Cfg::LDS, s, p);
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
 }
 
@@ -487,8 +509,14 @@ T* symbol_ptr(const void* sym) {
 AI4E_API int ai4e_conv_chain_fwd(const void* x, const void* w2, const void* b2, const void* w3, const void* b3,
                                  const void* res, void* y, const void* w1n, const void* b1n, void* t1n, int N, int H,
                                  int W, int ldx, int mid, int midn, int stride, int kpad2, int kpad3, int kpad1n,
-                                 int tile_cfg, hipStream_t stream) {
+                                 int tile_cfg, const void* x0, int ldx0, hipStream_t stream) {
   if (midn == 0) midn = mid;
+  // DOWN mode (x0 given, res null): the residual is the 1x1 projection of x0 [M, ldx0] (64 channels), folded
+  // into w3 = [W3 | Wd] (kpad3 >= mid + 64) and b3 = b3 + bd; MID 64, same-width chained c1', stride 1.
+  const bool down = x0 != nullptr;
+  if (down && (res || mid != 64 || midn != 64 || !w1n || stride != 1 || ldx0 % 8 || ldx0 < 64 || kpad3 < 128))
+    return AI4E_EINVAL;
+  if (down) res = x0;  // placeholder for the null checks below; never read
   if ((mid != 64 && mid != 128) || (midn != mid && !(mid == 64 && midn == 128)) || ldx % 8 || ldx < mid || kpad2 < 9 * mid || kpad2 % 64 ||
       kpad3 < mid || kpad3 % 8 || (stride != 1 && stride != 2) || !x || !w2 || !b2 || !w3 || !b3 || !res || !y ||
       (w1n && (!b1n || !t1n || kpad1n < 4 * mid || kpad1n % 8)))
@@ -514,9 +542,12 @@ AI4E_API int ai4e_conv_chain_fwd(const void* x, const void* w2, const void* b2, 
   p.OW = (W + 2 - 3) / stride + 1;
   p.M = N * p.OH * p.OW;
   p.kpad2 = kpad2; p.kpad3 = kpad3; p.kpad1n = kpad1n;
+  p.x0 = static_cast<const uint16_t*>(x0);
+  p.ldx0 = ldx0;
   if (p.M <= 0) return AI4E_OK;
   const bool next = w1n != nullptr;
   // tile_cfg: 0 = default (MID 64: 256 pixels, MID 128: 128), 1 = 128-pixel MID-64 tile (48 KB LDS, 3 per CU)
+  if (down) return launch_chain<64, 128, 64, true>(p, stream);
   if (mid == 64) {
     if (next && midn == 128) return launch_chain<64, 128, 128>(p, stream);
     if (tile_cfg == 1) return next ? launch_chain<64, 128, 64>(p, stream) : launch_chain<64, 128, 0>(p, stream);

@@ -125,3 +125,27 @@ def test_softmax_topk(shape):
     # bf16 logits tie often: compare the probability of the chosen class, not the index
     chosen = torch.softmax(logits.float(), 1).gather(1, idx.long())
     assert torch.allclose(chosen, rp, rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.parametrize("shape", [(2, 56, 56), (1, 15, 13)])
+def test_conv_chain_down(shape):
+    """K1c DOWN mode: the residual is the 1x1 projection of the block input, folded into c3's K."""
+    n, h, w = shape
+    mid = 64
+    torch.manual_seed(9)
+    c2 = pack_conv(torch.randn(mid, mid, 3, 3) / (9 * mid) ** 0.5, torch.randn(mid) * 0.1, pad=1).to(DEV)
+    c3 = pack_conv(torch.randn(4 * mid, mid, 1, 1) / mid ** 0.5, torch.randn(4 * mid) * 0.1).to(DEV)
+    dn = pack_conv(torch.randn(4 * mid, 64, 1, 1) / 8, torch.randn(4 * mid) * 0.1).to(DEV)
+    c1n = pack_conv(torch.randn(mid, 4 * mid, 1, 1) / (4 * mid) ** 0.5, torch.randn(mid) * 0.1).to(DEV)
+    t1 = torch.randn(n, h, w, mid, device=DEV).relu().to(torch.bfloat16)
+    x0 = torch.randn(n, h, w, 64, device=DEV).relu().to(torch.bfloat16)
+    y, t1n = conv_chain(t1, c2, c3, None, c1n=c1n, down=dn, x0=x0)
+    torch.cuda.synchronize()
+    t2 = F.relu(_conv(t1, _wq(c2, 3), c2.bias[:mid], 1, 1)).to(torch.bfloat16)
+    res = _conv(x0, _wq(dn, 1), dn.bias[:4 * mid])
+    yr = F.relu(_conv(t2, _wq(c3, 1), c3.bias[:4 * mid]) + res)
+    err = (y.float() - yr).abs().max().item()
+    assert err <= 0.02 * yr.abs().max().item() + 0.03, err
+    tr = F.relu(_conv(y, _wq(c1n, 1), c1n.bias[:mid]))
+    err = (t1n.float() - tr).abs().max().item()
+    assert err <= 0.02 * tr.abs().max().item() + 0.03, err
