@@ -11,6 +11,7 @@ a copy). ``x`` may itself be a channel slice view of a wider buffer.
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 from typing import Optional, Tuple
 
@@ -227,11 +228,11 @@ def conv_chain(t1: torch.Tensor, c2: PackedConv, c3: PackedConv, residual: Optio
     return out, t1n
 
 
-# K1c workgroup tile per bottleneck width (bench/chain_tune.py): 0 = 16384/mid pixels, 1 = 128 pixels (mid 64)
-CHAIN_TILE = {64: int(__import__("os").environ.get("AI4E_CHAIN_TILE64", "1")), 128: 0}
+# K1c tile config per bottleneck width (reserved: the kernel uses 128-pixel tiles for both widths)
+CHAIN_TILE = {64: int(os.environ.get("AI4E_CHAIN_TILE64", "1")), 128: 0}
 
-
-STEM_VARIANT = int(__import__("os").environ.get("AI4E_STEM_VARIANT", "0"))
+# K1s variant: 0 = direct conv from the LDS input footprint (default), 1 = DMA-gather implicit GEMM
+STEM_VARIANT = int(os.environ.get("AI4E_STEM_VARIANT", "0"))
 
 
 def stem_pool(x: torch.Tensor, pc: PackedConv, variant: int = -1) -> torch.Tensor:
