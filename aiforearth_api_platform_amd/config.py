@@ -17,7 +17,7 @@ from __future__ import annotations
 import dataclasses
 import os
 from dataclasses import dataclass, field, fields
-from typing import Any, Dict, Optional
+from typing import Any, Dict, List, Optional
 
 
 def _as_bool(v: Any) -> bool:
@@ -67,6 +67,8 @@ class Config:
     num_gpus: int = field(default=1, metadata={"env": "AI4E_NUM_GPUS"})
     max_batch: int = field(default=256, metadata={"env": "AI4E_MAX_BATCH"})
     max_batch_delay_ms: float = field(default=2.0, metadata={"env": "AI4E_MAX_BATCH_DELAY_MS"})
+    # graph-captured batch sizes below max_batch (low-load fast path: a batch of n runs the smallest bucket >= n)
+    batch_buckets: str = field(default="8,32,128", metadata={"env": "AI4E_BATCH_BUCKETS"})
     dtype: str = field(default="bf16", metadata={"env": "AI4E_DTYPE"})
     kernel_backend: str = field(default="auto", metadata={"env": "AI4E_KERNEL_BACKEND"})  # auto|hip|torch
     use_hip_graphs: bool = field(default=True, metadata={"env": "AI4E_HIP_GRAPHS"})
@@ -120,6 +122,20 @@ def _coerce(f: dataclasses.Field, v: Any) -> Any:
     if t == "float":
         return float(v)
     return str(v)
+
+
+def bucket_list(spec: Any, max_batch: int) -> List[int]:
+    """Batch-size buckets for an engine: the listed sizes below ``max_batch`` plus ``max_batch`` itself.
+
+    ``spec`` is a comma-separated string ("8,32,128") or a sequence of ints; empty = ``[max_batch]``.
+    Under low load the dynamic batcher hands the engine small batches, which then run the smallest captured
+    graph that fits instead of a full ``max_batch`` forward (survey §7.5 item 3).
+    """
+    if isinstance(spec, str):
+        items = [int(x) for x in spec.replace(" ", "").split(",") if x]
+    else:
+        items = [int(x) for x in (spec or [])]
+    return sorted({b for b in items if 0 < b < max_batch} | {int(max_batch)})
 
 
 _GLOBAL: Optional[Config] = None

@@ -42,6 +42,7 @@ class ModelSpec:
     topk: int = 5
     kwargs: Dict[str, Any] = field(default_factory=dict)
     use_graphs: bool = True
+    buckets: Tuple[int, ...] = ()      # captured batch sizes (config.bucket_list); () = max_batch only
 
 
 class SharedPayloadRing(PayloadRing):
@@ -109,7 +110,8 @@ def _child_main(rank: int, device: str, spec: ModelSpec, shm_name: str, nslots: 
             registered = False
     model = _load_factory(spec.factory)(device=device, **spec.kwargs)
     engine = InferenceEngine(model, spec.item_shape, spec.max_batch, device=dev, topk=spec.topk,
-                             use_graphs=spec.use_graphs, head_fn=getattr(model, "topk_u8", None))
+                             use_graphs=spec.use_graphs, head_fn=getattr(model, "topk_u8", None),
+                             buckets=list(spec.buckets) or None)
     engine.warmup()
     fault = _parse_fault(rank)
     send_mu = threading.Lock()

@@ -23,7 +23,7 @@ from typing import Any, Dict
 import torch
 import yaml
 
-from .config import Config, set_config
+from .config import Config, bucket_list, set_config
 from .gateway.control import ControlPlane, set_control_plane
 from .gateway.server import Gateway, Route, RouteTable
 from .sched.dispatcher import QueueDispatcher, WebhookDispatcher, http_backend
@@ -56,9 +56,10 @@ def build_platform(doc: Dict[str, Any], cfg: Config):
         shape = tuple(e["item_shape"])
         mb = int(e.get("max_batch", cfg.max_batch))
         devs = _devices(e.get("devices", "all"))
+        buckets = bucket_list(e.get("batch_buckets", cfg.batch_buckets), mb)
         if e.get("mode", "pool") == "pool":
             spec = ModelSpec(e["factory"], shape, mb, int(e.get("topk", 5)), dict(e.get("kwargs") or {}),
-                             bool(e.get("hip_graphs", cfg.use_hip_graphs)))
+                             bool(e.get("hip_graphs", cfg.use_hip_graphs)), tuple(buckets))
             pool = WorkerPool(cp, base_url + e["path"], spec, devs, max_delay_s=cfg.max_batch_delay_ms / 1e3,
                               heartbeat_interval_s=cfg.heartbeat_interval_s,
                               heartbeat_timeout_s=cfg.heartbeat_timeout_s)
@@ -68,7 +69,7 @@ def build_platform(doc: Dict[str, Any], cfg: Config):
             model = _load(e["factory"])(device=str(dev), **(e.get("kwargs") or {}))
             eng = InferenceEngine(model, shape, mb, device=dev, topk=int(e.get("topk", 5)),
                                   use_graphs=bool(e.get("hip_graphs", cfg.use_hip_graphs)),
-                                  head_fn=getattr(model, "topk_u8", None))
+                                  head_fn=getattr(model, "topk_u8", None), buckets=buckets)
             eng.warmup()
             ring = PayloadRing(mb * 4, shape)
             ep = ModelEndpoint(cp, e["path"], eng, ring, base_url=base_url)

@@ -95,3 +95,22 @@ def test_pipeline_and_spatial_single_gpu():
     seg = SpatialSegmenter(f.forward_u8, TileGrid(700, 600, 256, 224), 7, DEV, tile_batch=8)
     cls_map = seg.run(torch.randint(0, 256, (700, 600, 4), dtype=torch.uint8))
     assert cls_map.shape == (700, 600) and cls_map.max() < 7
+
+
+def test_engine_buckets_resnet_fused_head():
+    """Engine with batch buckets + the fused softmax/top-k head: a 5-image batch runs the 8-bucket graph and
+    matches the eager FusedResNet logits' top-5."""
+    from aiforearth_api_platform_amd.models.resnet import FusedResNet, resnet50
+    from aiforearth_api_platform_amd.runtime.engine import InferenceEngine
+
+    m = FusedResNet(resnet50(seed=2), device=DEV)
+    eng = InferenceEngine(m.forward_u8, (224, 224, 3), 32, device=DEV, head_fn=m.topk_u8, buckets=[8])
+    eng.warmup()
+    assert sorted({b for _, b in eng.graphs}) == [8, 32]
+    host = torch.randint(0, 256, (5, 224, 224, 3), dtype=torch.uint8).pin_memory()
+    res = eng.submit(host, list(range(5)))
+    res.done.synchronize()
+    ref = torch.topk(torch.softmax(m.forward_u8(host.to(DEV)).float(), 1), 5, 1)
+    torch.cuda.synchronize()
+    assert res.top_idx.shape == (5, 5)
+    assert torch.allclose(res.top_prob, ref.values.cpu(), rtol=2e-2, atol=1e-4)
