@@ -91,18 +91,9 @@ class FasterRCNN:
 
     # ------------------------------------------------------------------ backbone + FPN
     def backbone_stages(self, x: torch.Tensor) -> List[torch.Tensor]:
+        """C2..C5 of the ResNet-50 backbone: fused stem + max-pool (K1s) and the bottleneck chains (K1c)."""
         bb = self.backbone
-        x = conv2d_nhwc(bb.stem_input(x), bb.stem, relu=True)
-        x = maxpool2d_nhwc(x, 3, 2, 1)
-        outs = []
-        ends = {2, 6, 12, 15}  # last block index of layer1..layer4 for (3, 4, 6, 3)
-        for i, (c1, c2, c3, down) in enumerate(bb.blocks):
-            idt = x if down is None else conv2d_nhwc(x, down)
-            y = conv2d_nhwc(conv2d_nhwc(x, c1, relu=True), c2, relu=True)
-            x = conv2d_nhwc(y, c3, residual=idt, relu=True)
-            if i in ends:
-                outs.append(x)
-        return outs
+        return bb.stage_features(bb.stem_input(x))
 
     def fpn(self, feats: List[torch.Tensor]) -> List[torch.Tensor]:
         inner = conv2d_nhwc(feats[-1], self.lateral[-1])

@@ -200,12 +200,13 @@ class FusedResNet:
         y = conv2d_nhwc(y, c2, relu=True)
         return conv2d_nhwc(y, c3, residual=idt, relu=True, out=out)
 
-    def _stages_chained(self, y: torch.Tensor) -> torch.Tensor:
+    def _stages_chained(self, y: torch.Tensor, collect: bool = False):
         """All four stages with the K1c chains: the first block's downsample runs as a K1 conv, then every
         block is ONE kernel (c2 -> c3 + residual -> the next block's c1, across stage boundaries too: the
         last block of a stage computes the next stage's first c1). Shapes K1c does not build fall back to
-        separate K1 convs inside ``conv_chain``."""
+        separate K1 convs inside ``conv_chain``. ``collect`` returns every stage's output (FPN backbones)."""
         t1 = None
+        outs = []
         for si, blocks in enumerate(self.stages):
             c1, _, _, down = blocks[0]
             if t1 is None:
@@ -225,7 +226,24 @@ class FusedResNet:
                 idt, t1 = conv_chain(t1, c2, c3, idt, c1n=nxt, down=dn, x0=x0)
                 x0 = dn = None
             y = idt
-        return y
+            outs.append(y)
+        return outs if collect else y
+
+    def stage_features(self, x_s2d: torch.Tensor):
+        """Space-to-depth input -> the four stage outputs (C2..C5) through K1s + the K1c chains; the
+        per-conv K1 graph when chains are off."""
+        y = self._stem(x_s2d)
+        if self.chain:
+            return self._stages_chained(y, collect=True)
+        outs, ends, start = [], [], 0
+        for st in self.stages:
+            start += len(st)
+            ends.append(start - 1)
+        for i, blk in enumerate(self.blocks):
+            y = self._block(y, blk)
+            if i in ends:
+                outs.append(y)
+        return outs
 
     def _prefix_shape(self, n: int, h: int, w: int, nblocks: int) -> Tuple[int, int, int, int]:
         """Output shape after the stem, max-pool and the first ``nblocks`` bottlenecks."""
