@@ -2,7 +2,7 @@
 out), variants interleaved over several rounds on one GPU.
 
     python bench/forward_ab.py chain64=0 chain64=1 [chain=0] [chain=1] ...
-A variant is ``key=value`` over: chain (K1c on/off), chain64 / chain128 (K1c tile config).
+A variant is ``key=value`` over: chain (K1c on/off), stemu8 (preprocess fused into K1s), chain64 / chain128 (K1c tile config).
 """
 import os
 import sys
@@ -20,6 +20,8 @@ def apply(m, variant):
         k, v = kv.split("=")
         if k == "chain":
             m.chain = v == "1"
+        elif k == "stemu8":
+            m.stem_u8 = v == "1"
         elif k.startswith("chain"):
             convmod.CHAIN_TILE[int(k[5:])] = int(v)
         else:

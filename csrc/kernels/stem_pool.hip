@@ -35,6 +35,11 @@ struct StemParams {
   uint16_t* y;         // [N, PH, PW, 64]
   const uint16_t* zero;
   int H, W, PH, PW, kpad, tiles_r, tiles_c;
+  // fused preprocess (stem_pool_direct_kernel<true>): raw uint8 NHWC images [N, 2H, 2W, cin], normalized
+  // as (u8 * scale - mean[c]) * istd[c] while the s2d footprint is built (same math as preprocess_s2d)
+  const uint8_t* img;
+  int cin;
+  float mean[4], istd[4], scale;
 };
 
 __device__ __forceinline__ uint32_t max_bf16x2(uint32_t a, uint32_t b) {
@@ -178,6 +183,7 @@ constexpr int FP_SLOTS = 2 * FP_PIX;                                    // 720 1
 constexpr int FP_DMA = (FP_SLOTS + 255) / 256;                          // DMA instrs per wave (3)
 constexpr int D_W = 0, D_FP = 64 * 512, D_TILE = D_FP + FP_DMA * 4 * 1024, D_LDS = D_TILE + SP_BM * 128;
 
+template <bool U8>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void stem_pool_direct_kernel(const StemParams p, int ntiles) {
   extern __shared__ __attribute__((aligned(1024))) uint8_t dsm[];
@@ -213,6 +219,37 @@ void stem_pool_direct_kernel(const StemParams p, int ntiles) {
     const int ph0 = tr * SP_TR, pw0 = tc * SP_TC;
     const int oh0 = 2 * ph0 - 1, ow0 = 2 * pw0 - 1;
     const uint16_t* const xi = p.x + static_cast<long>(img) * p.H * p.W * SP_C;
+    if constexpr (U8) {
+      // fused preprocess: one thread per footprint pixel builds its 16 s2d channels
+      // ((dy*2+dx)*cin + c = norm(img[2ih+dy-1, 2iw+dx-1, c]), zero outside the image) and writes both planes
+      const int Hi = 2 * p.H, Wi = 2 * p.W;
+      const uint8_t* const ii = p.img + static_cast<long>(img) * Hi * Wi * p.cin;
+      for (int pix = tid; pix < FP_PIX; pix += 256) {
+        const int a = pix / FP_C, b = pix - a * FP_C;
+        const int ih = oh0 - 1 + a, iw = ow0 - 1 + b;
+        float v[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) v[k] = 0.f;
+        if (static_cast<unsigned>(ih) < static_cast<unsigned>(p.H) && static_cast<unsigned>(iw) < static_cast<unsigned>(p.W)) {
+#pragma unroll
+          for (int dy = 0; dy < 2; ++dy)
+#pragma unroll
+            for (int dx = 0; dx < 2; ++dx) {
+              const int yy = 2 * ih + dy - 1, xx = 2 * iw + dx - 1;
+              if (yy < 0 || yy >= Hi || xx < 0 || xx >= Wi) continue;
+              const uint8_t* src = ii + (static_cast<long>(yy) * Wi + xx) * p.cin;
+#pragma unroll
+              for (int c = 0; c < 4; ++c)
+                if (c < p.cin) v[(dy * 2 + dx) * p.cin + c] = (src[c] * p.scale - p.mean[c]) * p.istd[c];
+            }
+        }
+        uint4* d0 = reinterpret_cast<uint4*>(dsm + D_FP + pix * 16);
+        uint4* d1 = reinterpret_cast<uint4*>(dsm + D_FP + (FP_PIX + pix) * 16);
+        *d0 = make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]), pack_bf16x2(v[6], v[7]));
+        *d1 = make_uint4(pack_bf16x2(v[8], v[9]), pack_bf16x2(v[10], v[11]), pack_bf16x2(v[12], v[13]),
+                         pack_bf16x2(v[14], v[15]));
+      }
+    } else {
     // footprint DMA: slot s = plane * FP_PIX + pixel; footprint pixel (a, b) is input (oh0-1+a, ow0-1+b)
 #pragma unroll
     for (int q = 0; q < FP_DMA; ++q) {
@@ -224,6 +261,7 @@ void stem_pool_direct_kernel(const StemParams p, int ntiles) {
                       static_cast<unsigned>(iw) < static_cast<unsigned>(p.W);
       glds16(ok ? static_cast<const void*>(xi + (static_cast<long>(ih) * p.W + iw) * SP_C + 8 * h) : p.zero,
              sb + D_FP + (wave + 4 * q) * 1024);
+    }
     }
     wait_vmcnt<0>();
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // footprint (and weights) visible
@@ -294,7 +332,65 @@ void stem_pool_direct_kernel(const StemParams p, int ntiles) {
   }
 }
 
+template <bool U8>
+int launch_direct(const StemParams& p, long nb, hipStream_t stream) {
+  static bool attr = false;
+  if (!attr) {
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(stem_pool_direct_kernel<U8>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, D_LDS) != hipSuccess)
+      return AI4E_ELAUNCH;
+    attr = true;
+  }
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const long grid = nb < 2L * cus ? nb : 2L * cus;  // two persistent workgroups per CU
+  hipLaunchKernelGGL(stem_pool_direct_kernel<U8>, dim3(static_cast<unsigned>(grid)), dim3(256), D_LDS, stream, p,
+                     static_cast<int>(nb));
+  return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
+}
+
+const uint16_t* stem_zero_ptr() {
+  static const uint16_t* zero = nullptr;
+  if (!zero) {
+    void* a = nullptr;
+    if (hipGetSymbolAddress(&a, HIP_SYMBOL(g_stem_zero)) == hipSuccess) zero = static_cast<const uint16_t*>(a);
+  }
+  return zero;
+}
+
 }  // namespace
+
+// Fused preprocess + stem + max-pool: uint8 NHWC images [N, Hi, Wi, cin<=4] (Hi, Wi even) ->
+// [N, ceil(Hi/4), ceil(Wi/4), 64] bf16. mean4/std4 per channel (host arrays), value = (u8 * scale - mean) / std.
+AI4E_API int ai4e_stem_pool_u8_fwd(const void* img, const void* w, const void* bias, void* y, int N, int Hi, int Wi,
+                                   int cin, int kpad, const float* mean4, const float* std4, float scale,
+                                   hipStream_t stream) {
+  if (!img || !w || !bias || !y || !mean4 || !std4 || kpad < 256 || kpad % 8 || Hi <= 0 || Wi <= 0 || (Hi & 1) ||
+      (Wi & 1) || cin < 1 || cin > 4)
+    return AI4E_EINVAL;
+  StemParams p{};
+  p.w = static_cast<const uint16_t*>(w);
+  p.bias = static_cast<const float*>(bias);
+  p.y = static_cast<uint16_t*>(y);
+  p.zero = stem_zero_ptr();
+  if (!p.zero) return AI4E_ELAUNCH;
+  p.img = static_cast<const uint8_t*>(img);
+  p.cin = cin;
+  for (int c = 0; c < 4; ++c) {
+    p.mean[c] = c < cin ? mean4[c] : 0.f;
+    p.istd[c] = c < cin ? 1.f / std4[c] : 0.f;
+  }
+  p.scale = scale;
+  p.H = Hi / 2; p.W = Wi / 2;
+  p.PH = (p.H - 1) / 2 + 1;
+  p.PW = (p.W - 1) / 2 + 1;
+  p.kpad = kpad;
+  p.tiles_r = ai4e_cdiv(p.PH, SP_TR);
+  p.tiles_c = ai4e_cdiv(p.PW, SP_TC);
+  const long nb = static_cast<long>(N) * p.tiles_r * p.tiles_c;
+  if (nb <= 0) return AI4E_OK;
+  return launch_direct<true>(p, nb, stream);
+}
 
 // x: s2d stem input [N, H, W, 16] bf16; w: packed 4x4x16 stem weights [>= 64 rows, kpad >= 256] (pad 1/2,
 // ops/conv.py pack_stem_s2d); bias [>= 64] fp32; y: [N, ceil(H/2), ceil(W/2), 64] bf16.
@@ -322,21 +418,7 @@ AI4E_API int ai4e_stem_pool_fwd(const void* x, const void* w, const void* bias, 
   p.tiles_c = ai4e_cdiv(p.PW, SP_TC);
   const long nb = static_cast<long>(N) * p.tiles_r * p.tiles_c;
   if (nb <= 0) return AI4E_OK;
-  if (variant == 0) {
-    static bool attr = false;
-    if (!attr) {
-      if (hipFuncSetAttribute(reinterpret_cast<const void*>(stem_pool_direct_kernel),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, D_LDS) != hipSuccess)
-        return AI4E_ELAUNCH;
-      attr = true;
-    }
-    int dev = 0, cus = 256;
-    if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    const long grid = nb < 2L * cus ? nb : 2L * cus;  // two persistent workgroups per CU
-    hipLaunchKernelGGL(stem_pool_direct_kernel, dim3(static_cast<unsigned>(grid)), dim3(256), D_LDS, stream, p,
-                       static_cast<int>(nb));
-    return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
-  }
+  if (variant == 0) return launch_direct<false>(p, nb, stream);
   hipLaunchKernelGGL(stem_pool_kernel, dim3(static_cast<unsigned>(nb)), dim3(256), 0, stream, p);
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
 }
