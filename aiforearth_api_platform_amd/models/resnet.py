@@ -158,6 +158,9 @@ class FusedResNet:
         # uint8 preprocess fused into the stem kernel (AI4E_STEM_U8=1); off by default: measured 0.1 ms slower
         # per batch of 256 than the separate K7 preprocess + K1s (byte gathers serialize with the conv)
         self.stem_u8 = os.environ.get("AI4E_STEM_U8", "0") not in ("0", "off", "")
+        # chained micro-batching (AI4E_RESNET_CHAIN_MB=mb:nstages): stem + the first nstages run mb images at a time
+        cmb = os.environ.get("AI4E_RESNET_CHAIN_MB", "")
+        self.chain_mb: Optional[Tuple[int, int]] = tuple(int(v) for v in cmb.split(":")) if ":" in cmb else None
         # stages: runs of blocks starting at a block with a downsample conv
         self.stages: List[List[Tuple[PackedConv, PackedConv, PackedConv, Optional[PackedConv]]]] = []
         for blk in self.blocks:
@@ -203,14 +206,20 @@ class FusedResNet:
         y = conv2d_nhwc(y, c2, relu=True)
         return conv2d_nhwc(y, c3, residual=idt, relu=True, out=out)
 
-    def _stages_chained(self, y: torch.Tensor, collect: bool = False):
-        """All four stages with the K1c chains: the first block's downsample runs as a K1 conv, then every
+    def _stages_chained(self, y: torch.Tensor, collect: bool = False, t1: Optional[torch.Tensor] = None,
+                        s0: int = 0, s1: Optional[int] = None, y_out: Optional[torch.Tensor] = None,
+                        t1_out: Optional[torch.Tensor] = None):
+        """Stages ``s0 .. s1-1`` with the K1c chains: the first block's downsample runs as a K1 conv, then every
         block is ONE kernel (c2 -> c3 + residual -> the next block's c1, across stage boundaries too: the
         last block of a stage computes the next stage's first c1). Shapes K1c does not build fall back to
-        separate K1 convs inside ``conv_chain``. ``collect`` returns every stage's output (FPN backbones)."""
-        t1 = None
+        separate K1 convs inside ``conv_chain``. ``collect`` returns every stage's output (FPN backbones).
+        ``t1`` is stage ``s0``'s first c1 output when a previous call already computed it; with ``s1`` short
+        of the last stage the call returns ``(y, t1)`` for the next call, written into ``y_out`` / ``t1_out``
+        when given (micro-batch slices of the full-batch buffers)."""
+        s1 = len(self.stages) if s1 is None else s1
         outs = []
-        for si, blocks in enumerate(self.stages):
+        for si in range(s0, s1):
+            blocks = self.stages[si]
             c1, _, _, down = blocks[0]
             if t1 is None:
                 t1 = conv2d_nhwc(y, c1, relu=True)
@@ -226,11 +235,42 @@ class FusedResNet:
                     nxt = None
                 if nxt is not None and not chain_supported(c2.cout, nxt.cout) and chain_supported(c2.cout):
                     nxt = None  # keep the chain, run the next c1 as its own K1 launch
-                idt, t1 = conv_chain(t1, c2, c3, idt, c1n=nxt, down=dn, x0=x0)
+                last = si + 1 == s1 and i + 1 == len(blocks)
+                idt, t1 = conv_chain(t1, c2, c3, idt, c1n=nxt, down=dn, x0=x0, out=y_out if last else None,
+                                     t1n_out=t1_out if last and nxt is not None else None)
                 x0 = dn = None
             y = idt
             outs.append(y)
+        if s1 < len(self.stages):
+            return y, t1
         return outs if collect else y
+
+    def _chained_microbatched(self, x: torch.Tensor, pre, mb: int, nstages: int) -> torch.Tensor:
+        if not 0 < nstages < len(self.stages):
+            raise ValueError(f"chained micro-batching: nstages must be in 1..{len(self.stages) - 1}")
+        """Cache-resident micro-batching over the K1c chains: the stem and the first ``nstages`` stages run
+        ``mb`` images at a time (a layer1 activation of 32 images is 51 MB, so each chain's input comes
+        back from the 256 MB Infinity Cache instead of HBM), writing the stage output and the next stage's
+        first c1 straight into full-batch buffers; the later stages run on the whole batch."""
+        n = x.shape[0]
+        y_full = t1_full = None
+        for n0 in range(0, n, mb):
+            xs = x[n0:n0 + mb]
+            y = stem_pool_u8(xs, self.stem) if pre is preprocess_s2d_u8 and self.stem_u8 else self._stem(
+                pre(xs) if pre is not None else xs)
+            if y_full is None:
+                h, w = y.shape[1], y.shape[2]
+                for si in range(nstages):
+                    h, w = self.stages[si][0][1].out_hw(h, w)
+                c2, c3 = self.stages[nstages - 1][-1][1:3]
+                y_full = torch.empty(n, h, w, c3.cout, device=y.device, dtype=y.dtype)
+                nxt = self.stages[nstages][0][0]
+                if not (not chain_supported(c2.cout, nxt.cout) and chain_supported(c2.cout)):
+                    t1_full = torch.empty(n, h, w, nxt.cout, device=y.device, dtype=y.dtype)
+            m = y.shape[0]
+            self._stages_chained(y, s1=nstages, y_out=y_full[n0:n0 + m],
+                                 t1_out=None if t1_full is None else t1_full[n0:n0 + m])
+        return self._stages_chained(y_full, t1=t1_full, s0=nstages)
 
     def stage_features(self, x_s2d: torch.Tensor):
         """Space-to-depth input -> the four stage outputs (C2..C5) through K1s + the K1c chains; the
@@ -270,6 +310,8 @@ class FusedResNet:
         """
         n = x.shape[0]
         mb, nblocks = self.chunk if self.chunk else (n, 0)
+        if self.chain and self.chain_mb and self.chain_mb[0] < n:
+            return self._chained_microbatched(x, preprocess, *self.chain_mb)
         pre = preprocess or (lambda t: t)
         if mb < n and nblocks > 0:
             s2d = preprocess is None and x.shape[-1] == 16

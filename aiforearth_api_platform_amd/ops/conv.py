@@ -178,10 +178,12 @@ def _down_pack(c3: PackedConv, down: PackedConv) -> Tuple[torch.Tensor, torch.Te
 
 def conv_chain(t1: torch.Tensor, c2: PackedConv, c3: PackedConv, residual: Optional[torch.Tensor],
                c1n: Optional[PackedConv] = None, out: Optional[torch.Tensor] = None, force: bool = False,
-               tile_cfg: int = -1, down: Optional[PackedConv] = None, x0: Optional[torch.Tensor] = None):
+               tile_cfg: int = -1, down: Optional[PackedConv] = None, x0: Optional[torch.Tensor] = None,
+               t1n_out: Optional[torch.Tensor] = None):
     """Fused bottleneck tail (K1c): ``y = relu(c3(relu(c2(t1))) + residual)`` and, with ``c1n`` (the next
     block's 1x1 reduce), ``t1n = relu(c1n(y))`` from the same kernel. Returns ``(y, t1n or None)``.
 
+    ``out`` / ``t1n_out`` are optional preallocated outputs (micro-batch slices of full-batch buffers).
     ``t1``: NHWC ``[N,H,W,mid]`` bf16 (c1's output), ``c2`` 3x3/pad 1 (stride 1 or 2) mid->mid, ``c3`` 1x1
     mid->4*mid, ``residual`` ``[N,OH,OW,4*mid]``, ``c1n`` 1x1 4*mid->mid. With ``residual=None`` and
     ``down``/``x0`` the residual is ``down(x0)`` (a stage's first block); for mid 64, stride 1 and a chained
@@ -209,7 +211,7 @@ def conv_chain(t1: torch.Tensor, c2: PackedConv, c3: PackedConv, residual: Optio
     if _ext.backend_for(t1) != "hip" or not ok(mid, midn):
         y2 = conv2d_nhwc(t1, c2, relu=True)
         conv2d_nhwc(y2, c3, residual=residual, relu=True, out=out)
-        return out, (conv2d_nhwc(out, c1n, relu=True) if c1n is not None else None)
+        return out, (conv2d_nhwc(out, c1n, relu=True, out=t1n_out) if c1n is not None else None)
     if t1.dtype != torch.bfloat16 or not t1.is_contiguous() or not out.is_contiguous():
         raise ValueError("conv_chain: contiguous bf16 NHWC tensors required")
     if residual is not None and (residual.shape != (n, oh, ow, 4 * mid) or not residual.is_contiguous()):
@@ -218,7 +220,11 @@ def conv_chain(t1: torch.Tensor, c2: PackedConv, c3: PackedConv, residual: Optio
     if residual is None:
         w3, b3 = _down_pack(c3, down)
         kpad3 = w3.shape[1]
-    t1n = torch.empty(n, oh, ow, midn, device=t1.device, dtype=t1.dtype) if c1n is not None else None
+    t1n = None
+    if c1n is not None:
+        t1n = torch.empty(n, oh, ow, midn, device=t1.device, dtype=t1.dtype) if t1n_out is None else t1n_out
+        if t1n.shape != (n, oh, ow, midn) or not t1n.is_contiguous():
+            raise ValueError("conv_chain: bad t1n_out buffer")
     _ext.call("ai4e_conv_chain_fwd", t1.data_ptr(), c2.w_packed.data_ptr(), c2.bias.data_ptr(),
               w3.data_ptr(), b3.data_ptr(), _ext.ptr(residual), out.data_ptr(),
               _ext.ptr(c1n.w_packed if c1n is not None else None), _ext.ptr(c1n.bias if c1n is not None else None),

@@ -2,7 +2,7 @@
 out), variants interleaved over several rounds on one GPU.
 
     python bench/forward_ab.py chain64=0 chain64=1 [chain=0] [chain=1] ...
-A variant is ``key=value`` over: chain (K1c on/off), stemu8 (preprocess fused into K1s), chain64 / chain128 (K1c tile config).
+A variant is ``key=value[,key=value]`` over: t.<conv tile key> (tile config), chain (K1c on/off), stemu8 (preprocess fused into K1s), chain64 / chain128 (K1c tile config).
 """
 import os
 import sys
@@ -15,11 +15,25 @@ from aiforearth_api_platform_amd.models.resnet import FusedResNet, resnet50  # n
 from aiforearth_api_platform_amd.ops import conv as convmod  # noqa: E402
 
 
+_TILES0 = None
+
+
 def apply(m, variant):
+    global _TILES0
+    convmod.tuned_tile(m.stem, 1, 1, 1, False)  # load the measured table, then undo earlier variants' overrides
+    _TILES0 = dict(convmod._TILES) if _TILES0 is None else _TILES0
+    convmod._TILES = dict(_TILES0)
+    m.chain_mb = None
     for kv in variant.split(","):
+        if kv == "base":
+            continue
         k, v = kv.split("=")
         if k == "chain":
             m.chain = v == "1"
+        elif k.startswith("t."):  # t.<tile_key>=<cfg>: override one conv's tile config (ops/conv_tiles.json)
+            convmod._TILES[k[2:]] = int(v)
+        elif k == "mb":  # chained micro-batching mb:nstages (0 = off)
+            m.chain_mb = tuple(int(t) for t in v.split(":")) if ":" in v else None
         elif k == "stemu8":
             m.stem_u8 = v == "1"
         elif k.startswith("chain"):
