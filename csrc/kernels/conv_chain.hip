@@ -85,7 +85,7 @@ struct ChainParams {
   int ldx0;
 };
 
-template <int MID, int BM_, int MIDN = 0, bool DOWN = false>
+template <int MID, int BM_, int MIDN = 0, bool DOWN = false, int ST = 4>
 struct ChainCfg {
   static constexpr int BM = BM_;              // pixels per workgroup
   static constexpr bool NEXT = MIDN > 0;      // chained 1x1 c1' (output width MIDN)
@@ -93,7 +93,7 @@ struct ChainCfg {
   static constexpr int WM = 4 / WN;           // phase A / C: waves along pixels
   static constexpr int WPX = BM / WM;         // phase A / C: pixels per wave
   static constexpr int FI = WPX / 16;         // phase A / C: pixel fragments per wave
-  static constexpr int STAGES = 4;
+  static constexpr int STAGES = ST;           // DMA ring depth (phase A pixel/weight ring, B/C weight ring)
   static constexpr int CA = BM / 64;          // phase A pixel-row DMAs per wave per stage
   static constexpr int CB = MID / 64;         // phase A / C weight-row DMAs per wave per stage
   static constexpr int A_PX = STAGES * BM * 64;           // phase A: pixel ring, then the weight ring
@@ -134,11 +134,11 @@ __device__ __forceinline__ uint32_t tile_off(int r, int n) {
   return kb * BM * 64 + r * 64 + ((((e >> 3) ^ swz(r)) << 4) | (((e >> 2) & 1) << 3));
 }
 
-template <int MID, int BM_, int MIDN, bool DOWN>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ChainCfg<MID, BM_, MIDN, DOWN>::MINW,
-                                                                     ChainCfg<MID, BM_, MIDN, DOWN>::MINW)))
+template <int MID, int BM_, int MIDN, bool DOWN, int ST>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ChainCfg<MID, BM_, MIDN, DOWN, ST>::MINW,
+                                                                     ChainCfg<MID, BM_, MIDN, DOWN, ST>::MINW)))
 void conv_chain_kernel(const ChainParams p) {
-  using Cfg = ChainCfg<MID, BM_, MIDN, DOWN>;
+  using Cfg = ChainCfg<MID, BM_, MIDN, DOWN, ST>;
   constexpr bool NEXT = Cfg::NEXT;
   constexpr int FIC = Cfg::FIC, WPXC = Cfg::WPXC, CBC = Cfg::CBC;
   constexpr int WM = Cfg::WM, BM = Cfg::BM, STAGES = Cfg::STAGES, CA = Cfg::CA, CB = Cfg::CB;
@@ -479,19 +479,29 @@ void conv_chain_kernel(const ChainParams p) {
   }
 }
 
-template <int MID, int BM, int MIDN, bool DOWN = false>
+template <int MID, int BM, int MIDN, bool DOWN = false, int ST = 4>
 int launch_chain(const ChainParams& p, hipStream_t s) {
-  using Cfg = ChainCfg<MID, BM, MIDN, DOWN>;
+  using Cfg = ChainCfg<MID, BM, MIDN, DOWN, ST>;
   static bool attr = false;
   if (!attr) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(conv_chain_kernel<MID, BM, MIDN, DOWN>),
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(conv_chain_kernel<MID, BM, MIDN, DOWN, ST>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, Cfg::LDS) != hipSuccess)
       return AI4E_ELAUNCH;
     attr = true;
   }
   const int nb = ai4e_cdiv(p.M, Cfg::BM);
-  hipLaunchKernelGGL((conv_chain_kernel<MID, BM, MIDN, DOWN>), dim3(nb), dim3(256), Cfg::LDS, s, p);
+  hipLaunchKernelGGL((conv_chain_kernel<MID, BM, MIDN, DOWN, ST>), dim3(nb), dim3(256), Cfg::LDS, s, p);
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
+}
+
+template <int S>
+int launch_chain_st(const ChainParams& p, bool down, int mid, int midn, bool next, hipStream_t stream) {
+  if (down) return launch_chain<64, 128, 64, true, S>(p, stream);
+  if (mid == 64 && next && midn == 128) return launch_chain<64, 128, 128, false, S>(p, stream);
+  if (mid == 64) return next ? launch_chain<64, 128, 64, false, S>(p, stream) : launch_chain<64, 128, 0, false, S>(p, stream);
+  if constexpr (S <= 4)
+    return next ? launch_chain<128, 128, 128, false, S>(p, stream) : launch_chain<128, 128, 0, false, S>(p, stream);
+  return next ? launch_chain<128, 128, 128>(p, stream) : launch_chain<128, 128, 0>(p, stream);
 }
 
 template <typename T>
@@ -547,6 +557,11 @@ AI4E_API int ai4e_conv_chain_fwd(const void* x, const void* w2, const void* b2, 
   if (p.M <= 0) return AI4E_OK;
   const bool next = w1n != nullptr;
   // tile_cfg: 0 = default (MID 64: 256 pixels, MID 128: 128), 1 = 128-pixel MID-64 tile (48 KB LDS, 3 per CU)
+  // experimental ring depths: tile_cfg 13 / 15 / 16 = STAGES 3 / 5 / 6 for the 128-pixel tiles (MID 128: 3 only,
+  // deeper rings exceed 80 KB)
+  if (tile_cfg == 13) return launch_chain_st<3>(p, down, mid, midn, next, stream);
+  if (tile_cfg == 15) return launch_chain_st<5>(p, down, mid, midn, next, stream);
+  if (tile_cfg == 16) return launch_chain_st<6>(p, down, mid, midn, next, stream);
   if (down) return launch_chain<64, 128, 64, true>(p, stream);
   if (mid == 64) {
     if (next && midn == 128) return launch_chain<64, 128, 128>(p, stream);
