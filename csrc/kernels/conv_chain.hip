@@ -85,7 +85,7 @@ struct ChainParams {
   int ldx0;
 };
 
-template <int MID, int BM_, int MIDN = 0, bool DOWN = false, int ST = 4>
+template <int MID, int BM_, int MIDN = 0, bool DOWN = false, int ST = 4, bool BL = true>
 struct ChainCfg {
   static constexpr int BM = BM_;              // pixels per workgroup
   static constexpr bool NEXT = MIDN > 0;      // chained 1x1 c1' (output width MIDN)
@@ -113,6 +113,12 @@ struct ChainCfg {
   static constexpr int FIC = WPXC / 16;
   static constexpr int CBC = NEXT ? MIDN / 64 : 1;  // C weight-row DMAs per wave per stage
   static constexpr int LDS = A_BYTES > BC_BYTES ? A_BYTES : BC_BYTES;
+  // MID 64: the c3 / c1' biases are staged in LDS past everything else (<= 1.5 KB, same occupancy) and read
+  // back as one ds_read_b128 per 16-channel block: they seed the B accumulators (no epilogue add) and
+  // replace the SGPR lane-group select of bias4 (~20 VALU per block). MID 128 has no LDS to spare (80 KB).
+  static constexpr bool BIAS_LDS = BL && MID == 64 && LDS + (4 * MID + MIDN) * 4 <= 80 * 1024;
+  static constexpr int NBIAS = 4 * MID + (NEXT ? MIDN : 0);  // floats: b3 then b1'
+  static constexpr int LDS_ALL = LDS + (BIAS_LDS ? NBIAS * 4 : 0);
   static constexpr int NP = 4 * MID / 64;     // 64-channel passes over c3's output
   static constexpr int NB = KB / 32;          // B steps
   static constexpr int NC = 2;                // C steps (K = 64)
@@ -122,8 +128,9 @@ struct ChainCfg {
   static constexpr int NR = Y_BYTES / 1024 / 4;   // residual-chunk DMAs per wave
   static constexpr int NS = Y_BYTES / 16 / 256;   // 16-B Y copy-out stores per thread
   static_assert(!NEXT || BM * MIDN * 2 <= RING, "T1' staging fits below the weight ring");
-  static constexpr int MINW = LDS <= 160 * 1024 / 3 ? 3 : 2;  // workgroups (= waves per SIMD) per CU
-  static_assert(LDS <= 80 * 1024, "two workgroups per CU");
+  static constexpr int MINW = LDS_ALL <= 160 * 1024 / 3 ? 3 : 2;  // workgroups (= waves per SIMD) per CU
+  static_assert(LDS_ALL <= 80 * 1024, "two workgroups per CU");
+  static_assert(!BIAS_LDS || NBIAS <= 512, "bias staging: two values per thread");
   static_assert(FI >= 1 && FI <= 4 && BFI >= 1 && FIC >= 1 && FIC <= 4, "tile");
 };
 
@@ -134,11 +141,11 @@ __device__ __forceinline__ uint32_t tile_off(int r, int n) {
   return kb * BM * 64 + r * 64 + ((((e >> 3) ^ swz(r)) << 4) | (((e >> 2) & 1) << 3));
 }
 
-template <int MID, int BM_, int MIDN, bool DOWN, int ST>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ChainCfg<MID, BM_, MIDN, DOWN, ST>::MINW,
-                                                                     ChainCfg<MID, BM_, MIDN, DOWN, ST>::MINW)))
+template <int MID, int BM_, int MIDN, bool DOWN, int ST, bool BL>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ChainCfg<MID, BM_, MIDN, DOWN, ST, BL>::MINW,
+                                                                     ChainCfg<MID, BM_, MIDN, DOWN, ST, BL>::MINW)))
 void conv_chain_kernel(const ChainParams p) {
-  using Cfg = ChainCfg<MID, BM_, MIDN, DOWN, ST>;
+  using Cfg = ChainCfg<MID, BM_, MIDN, DOWN, ST, BL>;
   constexpr bool NEXT = Cfg::NEXT;
   constexpr int FIC = Cfg::FIC, WPXC = Cfg::WPXC, CBC = Cfg::CBC;
   constexpr int WM = Cfg::WM, BM = Cfg::BM, STAGES = Cfg::STAGES, CA = Cfg::CA, CB = Cfg::CB;
@@ -165,6 +172,17 @@ void conv_chain_kernel(const ChainParams p) {
   const int c = (lane & 3) ^ swz(rin);
   const int frow = lane & 15;
   const uint32_t fofs = frow * 64 + ((((lane >> 4) ^ swz(frow)) << 4));  // fragment byte offset in a 16-row block
+
+  // bias values this thread stages into LDS once phase A has drained (loaded now, ahead of the DMA asm)
+  float bstage[2] = {0.f, 0.f};
+  if constexpr (Cfg::BIAS_LDS) {
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int idx = tid + 256 * e;
+      if (idx < C4) bstage[e] = p.b3[idx];
+      else if (NEXT && idx < Cfg::NBIAS) bstage[e] = p.b1n[idx - C4];
+    }
+  }
 
   // ================= phase A: T2 = relu(conv3x3(T1) + b2), K1 main loop (GATHER_TAP) =================
   f32x4_t acc[FI][4];
@@ -250,6 +268,12 @@ void conv_chain_kernel(const ChainParams p) {
     lds_barrier();  // ring idle: every wave finished its reads, every DMA landed
 #undef KC_STEP
 #undef KC_READ
+  }
+  float* const bias_lds = reinterpret_cast<float*>(smem + Cfg::LDS);  // [NBIAS] (BIAS_LDS); visible after pass 0's barrier
+  if constexpr (Cfg::BIAS_LDS) {
+#pragma unroll
+    for (int e = 0; e < 2; ++e)
+      if (tid + 256 * e < Cfg::NBIAS) bias_lds[tid + 256 * e] = bstage[e];
   }
 
   // ================= passes: B (c3 chunk), Y epilogue, C (c1' partial) =================
@@ -411,9 +435,12 @@ void conv_chain_kernel(const ChainParams p) {
 
     f32x4_t accb[BFI][4];
 #pragma unroll
-    for (int i = 0; i < BFI; ++i)
+    for (int j = 0; j < 4; ++j) {
+      f32x4_t b0 = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      if constexpr (Cfg::BIAS_LDS) b0 = *reinterpret_cast<const f32x4_t*>(bias_lds + pp * 64 + 16 * j + 4 * lg);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) accb[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      for (int i = 0; i < BFI; ++i) accb[i][j] = b0;  // B accumulators start at the c3 bias
+    }
     seg_b(accb, pp * SPW);
 
     if constexpr (!DOWN) {
@@ -426,7 +453,7 @@ void conv_chain_kernel(const ChainParams p) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int n = 16 * j + 4 * lg;
-        const f32x4_t b = bias4(p.b3 + pp * 64 + 16 * j, lg);
+        const f32x4_t b = Cfg::BIAS_LDS ? f32x4_t{0.f, 0.f, 0.f, 0.f} : bias4(p.b3 + pp * 64 + 16 * j, lg);
         uint2* yp = reinterpret_cast<uint2*>(ybuf + tile_off<BM>(r, n));
         float r0 = 0.f, r1 = 0.f, r2 = 0.f, r3 = 0.f;
         if constexpr (!DOWN) {
@@ -434,8 +461,13 @@ void conv_chain_kernel(const ChainParams p) {
           unpack_bf16x2(rv.x, r0, r1);
           unpack_bf16x2(rv.y, r2, r3);
         }
-        *yp = make_uint2(pack_bf16x2(fmaxf(accb[i][j][0] + b[0] + r0, lo), fmaxf(accb[i][j][1] + b[1] + r1, lo)),
-                         pack_bf16x2(fmaxf(accb[i][j][2] + b[2] + r2, lo), fmaxf(accb[i][j][3] + b[3] + r3, lo)));
+        if constexpr (Cfg::BIAS_LDS) {  // bias already in the accumulators
+          *yp = make_uint2(pack_bf16x2(fmaxf(accb[i][j][0] + r0, lo), fmaxf(accb[i][j][1] + r1, lo)),
+                           pack_bf16x2(fmaxf(accb[i][j][2] + r2, lo), fmaxf(accb[i][j][3] + r3, lo)));
+        } else {
+          *yp = make_uint2(pack_bf16x2(fmaxf(accb[i][j][0] + b[0] + r0, lo), fmaxf(accb[i][j][1] + b[1] + r1, lo)),
+                           pack_bf16x2(fmaxf(accb[i][j][2] + b[2] + r2, lo), fmaxf(accb[i][j][3] + b[3] + r3, lo)));
+        }
       }
     }
     if constexpr (NEXT) {
@@ -466,7 +498,8 @@ void conv_chain_kernel(const ChainParams p) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int n = wnc * 64 + 16 * j + 4 * lg;
-        const f32x4_t b = bias4(p.b1n + wnc * 64 + 16 * j, lg);
+        const f32x4_t b = Cfg::BIAS_LDS ? *reinterpret_cast<const f32x4_t*>(bias_lds + C4 + wnc * 64 + 16 * j + 4 * lg)
+                                        : bias4(p.b1n + wnc * 64 + 16 * j, lg);
         *reinterpret_cast<uint2*>(t2buf + tile_off<BM>(r, n)) =
             make_uint2(pack_bf16x2(fmaxf(accn[i][j][0] + b[0], lo), fmaxf(accn[i][j][1] + b[1], lo)),
                        pack_bf16x2(fmaxf(accn[i][j][2] + b[2], lo), fmaxf(accn[i][j][3] + b[3], lo)));
@@ -479,29 +512,19 @@ void conv_chain_kernel(const ChainParams p) {
   }
 }
 
-template <int MID, int BM, int MIDN, bool DOWN = false, int ST = 4>
+template <int MID, int BM, int MIDN, bool DOWN = false, int ST = 4, bool BL = true>
 int launch_chain(const ChainParams& p, hipStream_t s) {
-  using Cfg = ChainCfg<MID, BM, MIDN, DOWN, ST>;
+  using Cfg = ChainCfg<MID, BM, MIDN, DOWN, ST, BL>;
   static bool attr = false;
   if (!attr) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(conv_chain_kernel<MID, BM, MIDN, DOWN, ST>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, Cfg::LDS) != hipSuccess)
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(conv_chain_kernel<MID, BM, MIDN, DOWN, ST, BL>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, Cfg::LDS_ALL) != hipSuccess)
       return AI4E_ELAUNCH;
     attr = true;
   }
   const int nb = ai4e_cdiv(p.M, Cfg::BM);
-  hipLaunchKernelGGL((conv_chain_kernel<MID, BM, MIDN, DOWN, ST>), dim3(nb), dim3(256), Cfg::LDS, s, p);
+  hipLaunchKernelGGL((conv_chain_kernel<MID, BM, MIDN, DOWN, ST, BL>), dim3(nb), dim3(256), Cfg::LDS_ALL, s, p);
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
-}
-
-template <int S>
-int launch_chain_st(const ChainParams& p, bool down, int mid, int midn, bool next, hipStream_t stream) {
-  if (down) return launch_chain<64, 128, 64, true, S>(p, stream);
-  if (mid == 64 && next && midn == 128) return launch_chain<64, 128, 128, false, S>(p, stream);
-  if (mid == 64) return next ? launch_chain<64, 128, 64, false, S>(p, stream) : launch_chain<64, 128, 0, false, S>(p, stream);
-  if constexpr (S <= 4)
-    return next ? launch_chain<128, 128, 128, false, S>(p, stream) : launch_chain<128, 128, 0, false, S>(p, stream);
-  return next ? launch_chain<128, 128, 128>(p, stream) : launch_chain<128, 128, 0>(p, stream);
 }
 
 template <typename T>
@@ -557,13 +580,13 @@ AI4E_API int ai4e_conv_chain_fwd(const void* x, const void* w2, const void* b2, 
   if (p.M <= 0) return AI4E_OK;
   const bool next = w1n != nullptr;
   // tile_cfg: 0 = default (MID 64: 256 pixels, MID 128: 128), 1 = 128-pixel MID-64 tile (48 KB LDS, 3 per CU)
-  // experimental ring depths: tile_cfg 13 / 15 / 16 = STAGES 3 / 5 / 6 for the 128-pixel tiles (MID 128: 3 only,
-  // deeper rings exceed 80 KB)
-  if (tile_cfg == 13) return launch_chain_st<3>(p, down, mid, midn, next, stream);
-  if (tile_cfg == 15) return launch_chain_st<5>(p, down, mid, midn, next, stream);
-  if (tile_cfg == 16) return launch_chain_st<6>(p, down, mid, midn, next, stream);
-  if (down) return launch_chain<64, 128, 64, true>(p, stream);
+  if (down) return tile_cfg == 2 ? launch_chain<64, 128, 64, true, 4, false>(p, stream)
+                                 : launch_chain<64, 128, 64, true>(p, stream);
   if (mid == 64) {
+    if (tile_cfg == 2) {  // A/B reference: the 128-pixel tile with the SGPR-select biases (no LDS staging)
+      if (next && midn == 128) return launch_chain<64, 128, 128, false, 4, false>(p, stream);
+      return next ? launch_chain<64, 128, 64, false, 4, false>(p, stream) : launch_chain<64, 128, 0, false, 4, false>(p, stream);
+    }
     if (next && midn == 128) return launch_chain<64, 128, 128>(p, stream);
     if (tile_cfg == 1) return next ? launch_chain<64, 128, 64>(p, stream) : launch_chain<64, 128, 0>(p, stream);
     return next ? launch_chain<64, 256, 64>(p, stream) : launch_chain<64, 256, 0>(p, stream);
