@@ -119,6 +119,10 @@ struct ChainCfg {
   static constexpr bool BIAS_LDS = BL && MID == 64 && LDS + (4 * MID + MIDN) * 4 <= 80 * 1024;
   static constexpr int NBIAS = 4 * MID + (NEXT ? MIDN : 0);  // floats: b3 then b1'
   static constexpr int LDS_ALL = LDS + (BIAS_LDS ? NBIAS * 4 : 0);
+  // Otherwise (MID 128), when a weight-ring slot has >= 128 rows: B steps fill only its first 64 rows, so the
+  // pass's c3 bias chunk (64 floats) rides in the free half of the pass's first B slot (one extra DMA per
+  // wave per pass) and seeds the accumulators the same way.
+  static constexpr bool BIAS_RING = !BIAS_LDS && BL && SLOT >= 128;
   static constexpr int NP = 4 * MID / 64;     // 64-channel passes over c3's output
   static constexpr int NB = KB / 32;          // B steps
   static constexpr int NC = 2;                // C steps (K = 64)
@@ -290,6 +294,11 @@ void conv_chain_kernel(const ChainParams p) {
     if (r < NB) {  // 64 rows: one DMA per wave
       glds16(p.w3 + static_cast<long>(pp * 64 + 16 * wave + rin) * p.kpad3 + r * BK + 8 * c, ws + 16 * wave * 64);
       ops += 1;
+      if (Cfg::BIAS_RING && r == 0) {  // bias chunk: wave w, lane l < 16 -> channels pp*64 + 16w + 4l .. +3
+        glds16(lane < 16 ? static_cast<const void*>(p.b3 + pp * 64 + 16 * wave + 4 * lane) : zero,
+               ws + 64 * 64 + wave * 1024);
+        ops += 1;
+      }
     } else {
       const uint16_t* src = p.w1n + static_cast<long>(16 * wave + rin) * p.kpad1n + pp * 64 + (r - NB) * BK + 8 * c;
 #pragma unroll
@@ -356,11 +365,22 @@ void conv_chain_kernel(const ChainParams p) {
       for (int j = 0; j < 4; ++j) fw[j] = *reinterpret_cast<const bf16x8_t*>(w_ + j * 1024);
 #pragma unroll
       for (int i = 0; i < BFI; ++i) fx[i] = *reinterpret_cast<const bf16x8_t*>(x_ + i * 1024);
+      if (Cfg::BIAS_RING && kk == 0) {  // the first MFMA of each accumulator starts from the ring-borne bias
+        const uint8_t* b_ = smem + Cfg::RING + (t % STAGES) * Cfg::SLOT * 64 + 64 * 64 + lg * 16;
+        f32x4_t bj[4];
 #pragma unroll
-      for (int i = 0; i < BFI; ++i)
+        for (int j = 0; j < 4; ++j) bj[j] = *reinterpret_cast<const f32x4_t*>(b_ + j * 1024);
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          a[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[j], fx[i], a[i][j], 0, 0, 0);
+        for (int i = 0; i < BFI; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) a[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[j], fx[i], bj[j], 0, 0, 0);
+      } else {
+#pragma unroll
+        for (int i = 0; i < BFI; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            a[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[j], fx[i], a[i][j], 0, 0, 0);
+      }
       issue_w(t + STAGES - 1);
     }
   };
@@ -453,7 +473,8 @@ void conv_chain_kernel(const ChainParams p) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int n = 16 * j + 4 * lg;
-        const f32x4_t b = Cfg::BIAS_LDS ? f32x4_t{0.f, 0.f, 0.f, 0.f} : bias4(p.b3 + pp * 64 + 16 * j, lg);
+        constexpr bool BSEED = Cfg::BIAS_LDS || Cfg::BIAS_RING;  // bias already in the accumulators
+        const f32x4_t b = BSEED ? f32x4_t{0.f, 0.f, 0.f, 0.f} : bias4(p.b3 + pp * 64 + 16 * j, lg);
         uint2* yp = reinterpret_cast<uint2*>(ybuf + tile_off<BM>(r, n));
         float r0 = 0.f, r1 = 0.f, r2 = 0.f, r3 = 0.f;
         if constexpr (!DOWN) {
@@ -461,7 +482,7 @@ void conv_chain_kernel(const ChainParams p) {
           unpack_bf16x2(rv.x, r0, r1);
           unpack_bf16x2(rv.y, r2, r3);
         }
-        if constexpr (Cfg::BIAS_LDS) {  // bias already in the accumulators
+        if constexpr (BSEED) {
           *yp = make_uint2(pack_bf16x2(fmaxf(accb[i][j][0] + r0, lo), fmaxf(accb[i][j][1] + r1, lo)),
                            pack_bf16x2(fmaxf(accb[i][j][2] + r2, lo), fmaxf(accb[i][j][3] + r3, lo)));
         } else {
@@ -579,7 +600,8 @@ AI4E_API int ai4e_conv_chain_fwd(const void* x, const void* w2, const void* b2, 
   p.ldx0 = ldx0;
   if (p.M <= 0) return AI4E_OK;
   const bool next = w1n != nullptr;
-  // tile_cfg: 0 = default (MID 64: 256 pixels, MID 128: 128), 1 = 128-pixel MID-64 tile (48 KB LDS, 3 per CU)
+  // tile_cfg: 0 = default (MID 64: 256 pixels, MID 128: 128), 1 = 128-pixel MID-64 tile (48 KB LDS, 3 per CU),
+  // 2 = the 128-pixel tiles with the SGPR lane-select biases (A/B reference for the LDS / ring-borne biases)
   if (down) return tile_cfg == 2 ? launch_chain<64, 128, 64, true, 4, false>(p, stream)
                                  : launch_chain<64, 128, 64, true>(p, stream);
   if (mid == 64) {
@@ -591,5 +613,8 @@ AI4E_API int ai4e_conv_chain_fwd(const void* x, const void* w2, const void* b2, 
     if (tile_cfg == 1) return next ? launch_chain<64, 128, 64>(p, stream) : launch_chain<64, 128, 0>(p, stream);
     return next ? launch_chain<64, 256, 64>(p, stream) : launch_chain<64, 256, 0>(p, stream);
   }
+  if (tile_cfg == 2)  // A/B reference: SGPR-select biases
+    return next ? launch_chain<128, 128, 128, false, 4, false>(p, stream)
+                : launch_chain<128, 128, 0, false, 4, false>(p, stream);
   return next ? launch_chain<128, 128, 128>(p, stream) : launch_chain<128, 128, 0>(p, stream);
 }
