@@ -29,6 +29,42 @@ __device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
   return __builtin_bit_cast(uint32_t, v);
 }
 
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+typedef short i16x2_t __attribute__((ext_vector_type(2)));
+
+// ReLU on two packed bf16 (sign bit set -> 0; relu(round(x)) == round(relu(x))): one v_pk_max_i16.
+__device__ __forceinline__ uint32_t relu_bf16x2(uint32_t v) {
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(i16x2_t, v), (i16x2_t){0, 0}));
+}
+
+// bf16x2(relu(lo, hi)): v_cvt_pk_bf16_f32 + v_pk_max_i16.
+__device__ __forceinline__ uint32_t pack_relu_bf16x2(float lo, float hi) {
+  const f32x2_t v = {lo, hi};
+  return relu_bf16x2(__builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2_t)));
+}
+
+// (a + r.lo, b + r.hi) for two packed bf16 r without unpacking: v_dot2c_f32_bf16 against (1, 0) / (0, 1).
+// The selector constants go through an opaque s_mov: hipcc otherwise encodes bf16x2 (1, 0) = 0x00003f80 as
+// the inline constant 1.0, which the hardware reads as 0x3f800000 = (0, 1) (measured: wrong half added).
+__device__ __forceinline__ uint32_t bf16_sel_lo() {
+  uint32_t v;
+  asm("s_mov_b32 %0, 0x3f80" : "=s"(v));
+  return v;
+}
+__device__ __forceinline__ uint32_t bf16_sel_hi() {
+  uint32_t v;
+  asm("s_mov_b32 %0, 0x3f800000" : "=s"(v));
+  return v;
+}
+__device__ __forceinline__ float add_bf16_lo(uint32_t r, float a) {
+  return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, r), __builtin_bit_cast(bf16x2_t, bf16_sel_lo()),
+                                         a, false);
+}
+__device__ __forceinline__ float add_bf16_hi(uint32_t r, float a) {
+  return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, r), __builtin_bit_cast(bf16x2_t, bf16_sel_hi()),
+                                         a, false);
+}
+
 __device__ __forceinline__ void unpack_bf16x2(uint32_t v, float& lo, float& hi) {
   lo = __uint_as_float(v << 16);
   hi = __uint_as_float(v & 0xffff0000u);

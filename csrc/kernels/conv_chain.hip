@@ -21,8 +21,10 @@
 //   and Y_p is copied out to HBM with 16-B stores. Weights of B/C stream through a weights-only LDS ring
 //   (one continuous DMA stream across passes); every wait is a counted vmcnt whose count is a constant
 //   after unrolling (the wave's own DMA/store bookkeeping below).
-// LDS: max(phase-A pixel ring, T2 + Y buffer) + weight ring = 80 KB for MID 64 (2 workgroups per CU);
-// biases come through scalar loads (no LDS, no vmcnt).
+// LDS: max(phase-A pixel ring, T2 + Y buffer) + weight ring (48 KB for the 128-pixel MID-64 tile: 3 workgroups
+// per CU; 80 KB for MID 128: 2). c3 biases seed the B accumulators (MID 64: staged in LDS; MID 128: carried in
+// the weight ring); the T2 bias comes through scalar loads. Epilogues add the residual from packed bf16 (dot2),
+// convert with v_cvt_pk_bf16_f32 and apply ReLU on the packed bf16 (v_pk_max_i16).
 #include <type_traits>
 
 #include "conv_common.h"
@@ -324,17 +326,21 @@ void conv_chain_kernel(const ChainParams p) {
   for (int t = 0; t < STAGES - 1; ++t) issue_w(t);
 
   const float lo = 0.f;
-  // T2 epilogue: + b2, ReLU, bf16 -> t2buf (phase A wave layout)
+  // T2 epilogue: + b2, ReLU, bf16 -> t2buf (phase A wave layout); the lane-group bias select once per j
+  // (readfirstlane is convergent: hipcc does not CSE it across the i loop)
+  f32x4_t b2v[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) b2v[j] = bias4(p.b2 + wn * 64 + 16 * j, lg);
 #pragma unroll
   for (int i = 0; i < FI; ++i) {
     const int r = wm * WPX + 16 * i + (lane & 15);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int n = wn * 64 + 16 * j + 4 * lg;
-      const f32x4_t b = bias4(p.b2 + wn * 64 + 16 * j, lg);
+      const f32x4_t b = b2v[j];
       *reinterpret_cast<uint2*>(t2buf + tile_off<BM>(r, n)) =
-          make_uint2(pack_bf16x2(fmaxf(acc[i][j][0] + b[0], lo), fmaxf(acc[i][j][1] + b[1], lo)),
-                     pack_bf16x2(fmaxf(acc[i][j][2] + b[2], lo), fmaxf(acc[i][j][3] + b[3], lo)));
+          make_uint2(pack_relu_bf16x2(acc[i][j][0] + b[0], acc[i][j][1] + b[1]),
+                     pack_relu_bf16x2(acc[i][j][2] + b[2], acc[i][j][3] + b[3]));
     }
   }
 
@@ -476,16 +482,23 @@ void conv_chain_kernel(const ChainParams p) {
         constexpr bool BSEED = Cfg::BIAS_LDS || Cfg::BIAS_RING;  // bias already in the accumulators
         const f32x4_t b = BSEED ? f32x4_t{0.f, 0.f, 0.f, 0.f} : bias4(p.b3 + pp * 64 + 16 * j, lg);
         uint2* yp = reinterpret_cast<uint2*>(ybuf + tile_off<BM>(r, n));
+        if constexpr (BSEED && DOWN) {
+          *yp = make_uint2(pack_relu_bf16x2(accb[i][j][0], accb[i][j][1]), pack_relu_bf16x2(accb[i][j][2], accb[i][j][3]));
+          continue;
+        }
+        if constexpr (BSEED) {  // residual added straight from its packed bf16 (dot2), ReLU on packed bf16
+          const uint2 rv = *yp;
+          *yp = make_uint2(pack_relu_bf16x2(add_bf16_lo(rv.x, accb[i][j][0]), add_bf16_hi(rv.x, accb[i][j][1])),
+                           pack_relu_bf16x2(add_bf16_lo(rv.y, accb[i][j][2]), add_bf16_hi(rv.y, accb[i][j][3])));
+          continue;
+        }
         float r0 = 0.f, r1 = 0.f, r2 = 0.f, r3 = 0.f;
         if constexpr (!DOWN) {
           const uint2 rv = *yp;
           unpack_bf16x2(rv.x, r0, r1);
           unpack_bf16x2(rv.y, r2, r3);
         }
-        if constexpr (BSEED) {
-          *yp = make_uint2(pack_bf16x2(fmaxf(accb[i][j][0] + r0, lo), fmaxf(accb[i][j][1] + r1, lo)),
-                           pack_bf16x2(fmaxf(accb[i][j][2] + r2, lo), fmaxf(accb[i][j][3] + r3, lo)));
-        } else {
+        {
           *yp = make_uint2(pack_bf16x2(fmaxf(accb[i][j][0] + b[0] + r0, lo), fmaxf(accb[i][j][1] + b[1] + r1, lo)),
                            pack_bf16x2(fmaxf(accb[i][j][2] + b[2] + r2, lo), fmaxf(accb[i][j][3] + b[3] + r3, lo)));
         }
@@ -513,17 +526,21 @@ void conv_chain_kernel(const ChainParams p) {
   if constexpr (NEXT) {
     // T1' epilogue through the (idle) T2 (+ Y) buffer, then 16-B copy-out
     if constexpr (MIDN > MID) lds_barrier();  // the staging overlaps the Y chunk the copy-out just read
+    f32x4_t b1v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      b1v[j] = Cfg::BIAS_LDS ? *reinterpret_cast<const f32x4_t*>(bias_lds + C4 + wnc * 64 + 16 * j + 4 * lg)
+                             : bias4(p.b1n + wnc * 64 + 16 * j, lg);
 #pragma unroll
     for (int i = 0; i < FIC; ++i) {
       const int r = wmc * WPXC + 16 * i + (lane & 15);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int n = wnc * 64 + 16 * j + 4 * lg;
-        const f32x4_t b = Cfg::BIAS_LDS ? *reinterpret_cast<const f32x4_t*>(bias_lds + C4 + wnc * 64 + 16 * j + 4 * lg)
-                                        : bias4(p.b1n + wnc * 64 + 16 * j, lg);
+        const f32x4_t b = b1v[j];
         *reinterpret_cast<uint2*>(t2buf + tile_off<BM>(r, n)) =
-            make_uint2(pack_bf16x2(fmaxf(accn[i][j][0] + b[0], lo), fmaxf(accn[i][j][1] + b[1], lo)),
-                       pack_bf16x2(fmaxf(accn[i][j][2] + b[2], lo), fmaxf(accn[i][j][3] + b[3], lo)));
+            make_uint2(pack_relu_bf16x2(accn[i][j][0] + b[0], accn[i][j][1] + b[1]),
+                       pack_relu_bf16x2(accn[i][j][2] + b[2], accn[i][j][3] + b[3]));
       }
     }
     lds_barrier();
