@@ -65,6 +65,31 @@ __device__ __forceinline__ float add_bf16_hi(uint32_t r, float a) {
                                          a, false);
 }
 
+// bf16x2 of two floats (v_cvt_pk_bf16_f32), no ReLU.
+__device__ __forceinline__ uint32_t cvt_bf16x2(float lo, float hi) {
+  const f32x2_t v = {lo, hi};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2_t));
+}
+
+// Conv epilogue for 8 consecutive channels: f (+ 8 packed-bf16 residual values) -> 8 bf16 (ReLU optional);
+// the residual is added from its packed form (dot2), ReLU runs on the packed result.
+__device__ __forceinline__ uint4 epilogue8_bf16(const float (&f)[8], bool has_res, const uint4& r, bool relu) {
+  float g[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) g[k] = f[k];
+  if (has_res) {
+    g[0] = add_bf16_lo(r.x, g[0]); g[1] = add_bf16_hi(r.x, g[1]);
+    g[2] = add_bf16_lo(r.y, g[2]); g[3] = add_bf16_hi(r.y, g[3]);
+    g[4] = add_bf16_lo(r.z, g[4]); g[5] = add_bf16_hi(r.z, g[5]);
+    g[6] = add_bf16_lo(r.w, g[6]); g[7] = add_bf16_hi(r.w, g[7]);
+  }
+  uint4 o = make_uint4(cvt_bf16x2(g[0], g[1]), cvt_bf16x2(g[2], g[3]), cvt_bf16x2(g[4], g[5]), cvt_bf16x2(g[6], g[7]));
+  if (relu) {
+    o.x = relu_bf16x2(o.x); o.y = relu_bf16x2(o.y); o.z = relu_bf16x2(o.z); o.w = relu_bf16x2(o.w);
+  }
+  return o;
+}
+
 __device__ __forceinline__ void unpack_bf16x2(uint32_t v, float& lo, float& hi) {
   lo = __uint_as_float(v << 16);
   hi = __uint_as_float(v & 0xffff0000u);

@@ -296,8 +296,8 @@ void conv_chain_kernel(const ChainParams p) {
     if (r < NB) {  // 64 rows: one DMA per wave
       glds16(p.w3 + static_cast<long>(pp * 64 + 16 * wave + rin) * p.kpad3 + r * BK + 8 * c, ws + 16 * wave * 64);
       ops += 1;
-      if (Cfg::BIAS_RING && r == 0) {  // bias chunk: wave w, lane l < 16 -> channels pp*64 + 16w + 4l .. +3
-        glds16(lane < 16 ? static_cast<const void*>(p.b3 + pp * 64 + 16 * wave + 4 * lane) : zero,
+      if (Cfg::BIAS_RING && r == 0) {  // bias chunk: wave w, lane l < 4 -> channels pp*64 + 16w + 4l .. +3
+        glds16(lane < 4 ? static_cast<const void*>(p.b3 + pp * 64 + 16 * wave + 4 * lane) : zero,
                ws + 64 * 64 + wave * 1024);
         ops += 1;
       }

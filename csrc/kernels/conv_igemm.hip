@@ -301,25 +301,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
       const int m = m0 + r, n = n0 + 8 * cq;
       const float4 v0 = *reinterpret_cast<const float4*>(tile + r * BN + 4 * ((2 * cq) ^ (r & 7)));
       const float4 v1 = *reinterpret_cast<const float4*>(tile + r * BN + 4 * ((2 * cq + 1) ^ (r & 7)));
-      float f[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-      if (p.res) {
-        float a[8];
-        unpack_bf16x2(rres16[e].x, a[0], a[1]);
-        unpack_bf16x2(rres16[e].y, a[2], a[3]);
-        unpack_bf16x2(rres16[e].z, a[4], a[5]);
-        unpack_bf16x2(rres16[e].w, a[6], a[7]);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) f[k] += a[k];
-      }
-#pragma unroll
-      for (int k = 0; k < 8; ++k) f[k] = fmaxf(f[k], lo);
+      const float f[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+      const uint4 o = epilogue8_bf16(f, p.res != nullptr, rres16[e], p.relu != 0);
       if (m < p.M && n < p.Kout) {
         uint16_t* dst = p.y + static_cast<long>(m) * p.ldy + p.ycoff + n;
-        const uint2 lo4 = make_uint2(pack_bf16x2(f[0], f[1]), pack_bf16x2(f[2], f[3]));
         if (n + 8 <= p.Kout) {
-          *reinterpret_cast<uint4*>(dst) = make_uint4(lo4.x, lo4.y, pack_bf16x2(f[4], f[5]), pack_bf16x2(f[6], f[7]));
+          *reinterpret_cast<uint4*>(dst) = o;
         } else {
-          *reinterpret_cast<uint2*>(dst) = lo4;  // Kout % 8 == 4 tail
+          *reinterpret_cast<uint2*>(dst) = make_uint2(o.x, o.y);  // Kout % 8 == 4 tail
         }
       }
     }
@@ -608,23 +597,10 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
       const int nb = min(n, p.Kout - 8);
       const float4 b0 = *reinterpret_cast<const float4*>(p.bias + nb);
       const float4 b1 = *reinterpret_cast<const float4*>(p.bias + nb + 4);
-      float f[8] = {v0.x + b0.x, v0.y + b0.y, v0.z + b0.z, v0.w + b0.w,
-                    v1.x + b1.x, v1.y + b1.y, v1.z + b1.z, v1.w + b1.w};
-      if (p.res) {
-        float a[8];
-        unpack_bf16x2(rv[e].x, a[0], a[1]);
-        unpack_bf16x2(rv[e].y, a[2], a[3]);
-        unpack_bf16x2(rv[e].z, a[4], a[5]);
-        unpack_bf16x2(rv[e].w, a[6], a[7]);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) f[k] += a[k];
-      }
-#pragma unroll
-      for (int k = 0; k < 8; ++k) f[k] = fmaxf(f[k], lo);
-      if (m < p.M && n < p.Kout)
-        *reinterpret_cast<uint4*>(p.y + static_cast<long>(m) * p.ldy + p.ycoff + n) =
-            make_uint4(pack_bf16x2(f[0], f[1]), pack_bf16x2(f[2], f[3]), pack_bf16x2(f[4], f[5]),
-                       pack_bf16x2(f[6], f[7]));
+      const float f[8] = {v0.x + b0.x, v0.y + b0.y, v0.z + b0.z, v0.w + b0.w,
+                          v1.x + b1.x, v1.y + b1.y, v1.z + b1.z, v1.w + b1.w};
+      const uint4 o = epilogue8_bf16(f, p.res != nullptr, rv[e], p.relu != 0);
+      if (m < p.M && n < p.Kout) *reinterpret_cast<uint4*>(p.y + static_cast<long>(m) * p.ldy + p.ycoff + n) = o;
     }
     __syncthreads();
   }
