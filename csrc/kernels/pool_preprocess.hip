@@ -23,18 +23,22 @@ __global__ __launch_bounds__(256) void preprocess_u8_kernel(const uint8_t* __res
 // Space-to-depth preprocess for the 7x7/2 stem (see ops/conv.py pack_stem_s2d):
 // uint8 [N,H,W,cin<=4] -> bf16 [N,H/2,W/2,16], out[i,j,(dy*2+dx)*cin+c] = norm(x[2i+dy-1, 2j+dx-1, c])
 // (zero outside the image = the conv's zero padding of the normalized input).
+// CIN > 0: channel count known at compile time (fully unrolled, the 16 outputs stay in registers) and
+// 32-bit pixel indexing (IDX = int when N*H/2*W/2 < 2^31); CIN = 0: runtime cin, 64-bit indexing.
+template <int CIN, typename IDX>
 __global__ __launch_bounds__(256) void preprocess_s2d_kernel(const uint8_t* __restrict__ in, uint16_t* __restrict__ out,
-                                                             int N, int H, int W, int cin, float4 mean, float4 istd,
+                                                             int N, int H, int W, int cin_rt, float4 mean, float4 istd,
                                                              float scale) {
+  const int cin = CIN > 0 ? CIN : cin_rt;
   const int OH = H >> 1, OW = W >> 1;
   const float m[4] = {mean.x, mean.y, mean.z, mean.w};
   const float is[4] = {istd.x, istd.y, istd.z, istd.w};
-  const long total = static_cast<long>(N) * OH * OW;
-  for (long p = blockIdx.x * 256L + threadIdx.x; p < total; p += static_cast<long>(gridDim.x) * 256) {
-    const int j = static_cast<int>(p % OW);
-    const long t = p / OW;
-    const int i = static_cast<int>(t % OH);
-    const int n = static_cast<int>(t / OH);
+  const IDX total = static_cast<IDX>(N) * OH * OW;
+  for (IDX p = static_cast<IDX>(blockIdx.x) * 256 + threadIdx.x; p < total; p += static_cast<IDX>(gridDim.x) * 256) {
+    const IDX t = p / OW;
+    const int j = static_cast<int>(p - t * OW);
+    const IDX n = t / OH;
+    const int i = static_cast<int>(t - n * OH);
     float v[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) v[k] = 0.f;
@@ -46,10 +50,12 @@ __global__ __launch_bounds__(256) void preprocess_s2d_kernel(const uint8_t* __re
         const int x = 2 * j + dx - 1;
         if (y < 0 || y >= H || x < 0 || x >= W) continue;
         const uint8_t* src = in + ((static_cast<long>(n) * H + y) * W + x) * cin;
-        for (int c = 0; c < cin; ++c) v[(dy * 2 + dx) * cin + c] = (src[c] * scale - m[c]) * is[c];
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          if (c < cin) v[(dy * 2 + dx) * cin + c] = (src[c] * scale - m[c]) * is[c];
       }
     }
-    uint4* o = reinterpret_cast<uint4*>(out) + 2 * p;
+    uint4* o = reinterpret_cast<uint4*>(out) + 2 * static_cast<long>(p);
     o[0] = make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]), pack_bf16x2(v[6], v[7]));
     o[1] = make_uint4(pack_bf16x2(v[8], v[9]), pack_bf16x2(v[10], v[11]), pack_bf16x2(v[12], v[13]),
                       pack_bf16x2(v[14], v[15]));
@@ -139,8 +145,18 @@ AI4E_API int ai4e_preprocess_s2d_u8(const void* in, void* out, int N, int H, int
   if (cin < 1 || cin > 4 || (H & 1) || (W & 1)) return AI4E_EINVAL;
   float4 m = make_float4(mean4[0], mean4[1], mean4[2], mean4[3]);
   float4 is = make_float4(1.f / std4[0], 1.f / std4[1], 1.f / std4[2], 1.f / std4[3]);
-  hipLaunchKernelGGL(preprocess_s2d_kernel, dim3(grid_for(static_cast<long>(N) * (H / 2) * (W / 2))), dim3(256), 0, s,
-                     static_cast<const uint8_t*>(in), static_cast<uint16_t*>(out), N, H, W, cin, m, is, scale);
+  const long total = static_cast<long>(N) * (H / 2) * (W / 2);
+  const dim3 grid(grid_for(total));
+  const uint8_t* i8 = static_cast<const uint8_t*>(in);
+  uint16_t* o16 = static_cast<uint16_t*>(out);
+  const bool small = total < (1L << 31) - 65536L * 256;
+  if (small && cin == 3) {
+    hipLaunchKernelGGL((preprocess_s2d_kernel<3, int>), grid, dim3(256), 0, s, i8, o16, N, H, W, cin, m, is, scale);
+  } else if (small && cin == 4) {
+    hipLaunchKernelGGL((preprocess_s2d_kernel<4, int>), grid, dim3(256), 0, s, i8, o16, N, H, W, cin, m, is, scale);
+  } else {
+    hipLaunchKernelGGL((preprocess_s2d_kernel<0, long>), grid, dim3(256), 0, s, i8, o16, N, H, W, cin, m, is, scale);
+  }
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
 }
 
