@@ -59,48 +59,83 @@ __global__ __launch_bounds__(256) void gn_stats_kernel(const uint16_t* __restric
   }
 }
 
-__global__ __launch_bounds__(256) void gn_apply_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
-                                                       const float* __restrict__ partials,
-                                                       const float* __restrict__ gamma, const float* __restrict__ beta,
-                                                       int HW, int C, int G, float eps, int relu, int nchunks, int ldx,
-                                                       int xcoff, int ldy, int ycoff) {
-  const int n = blockIdx.y;
+// One workgroup per image: combine the image's chunk partials (fp64) into per-group mean / rstd, then fold
+// gamma / beta into a per-channel affine: ss[n, c] = (a, b) with y = x * a + b, a = rstd_g * gamma_c,
+// b = beta_c - mean_g * a. (Done once per image instead of in every normalize workgroup.)
+__global__ __launch_bounds__(256) void gn_finalize_kernel(const float* __restrict__ partials,
+                                                          const float* __restrict__ gamma,
+                                                          const float* __restrict__ beta, float2* __restrict__ ss,
+                                                          int HW, int C, int G, float eps, int nchunks) {
+  const int n = blockIdx.x;
+  constexpr int LPG = 4;  // lanes per group (G <= 64)
+  __shared__ double red_s[256], red_q[256];
   __shared__ float mean_s[64], rstd_s[64];
-  if (threadIdx.x < G) {
-    double s = 0, q = 0;
-    for (int k = 0; k < nchunks; ++k) {
-      const float* o = partials + ((static_cast<long>(n) * nchunks + k) * G + threadIdx.x) * 2;
+  const int g = threadIdx.x / LPG, l = threadIdx.x % LPG;
+  double s = 0, q = 0;
+  if (g < G) {
+    for (int k = l; k < nchunks; k += LPG) {
+      const float* o = partials + ((static_cast<long>(n) * nchunks + k) * G + g) * 2;
       s += o[0];
       q += o[1];
+    }
+  }
+  red_s[threadIdx.x] = s;
+  red_q[threadIdx.x] = q;
+  __syncthreads();
+  if (l == 0 && g < G) {
+    for (int k = 1; k < LPG; ++k) {
+      s += red_s[threadIdx.x + k];
+      q += red_q[threadIdx.x + k];
     }
     const double cnt = static_cast<double>(HW) * (C / G);
     const double mean = s / cnt;
     const double var = fmax(q / cnt - mean * mean, 0.0);
-    mean_s[threadIdx.x] = static_cast<float>(mean);
-    rstd_s[threadIdx.x] = static_cast<float>(1.0 / sqrt(var + eps));
+    mean_s[g] = static_cast<float>(mean);
+    rstd_s[g] = static_cast<float>(1.0 / sqrt(var + eps));
   }
   __syncthreads();
-  const int C8 = C >> 3;
   const int cg = C / G;
-  const long total = static_cast<long>(HW) * C8;
-  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += static_cast<long>(gridDim.x) * 256) {
-    const int c8 = static_cast<int>(i % C8);
-    const long p = i / C8;
-    const uint4 v = *reinterpret_cast<const uint4*>(x + (static_cast<long>(n) * HW + p) * ldx + xcoff + 8 * c8);
+  for (int c = threadIdx.x; c < C; c += 256) {
+    const int gc = c / cg;
+    const float a = rstd_s[gc] * gamma[c];
+    ss[static_cast<long>(n) * C + c] = make_float2(a, beta[c] - mean_s[gc] * a);
+  }
+}
+
+// y = x * a_c + b_c (+ReLU), 16-B vectors. C8 = C/8 divides 256, so with a grid stride that is a multiple of
+// 256 every lane keeps one 8-channel column: its 8 affine pairs load once, the loop is unpack + FMA + cvt.
+__global__ __launch_bounds__(256) void gn_apply_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
+                                                       const float2* __restrict__ ss, int HW, int C, int relu, int ldx,
+                                                       int xcoff, int ldy, int ycoff) {
+  const int n = blockIdx.y;
+  const int C8 = C >> 3;
+  const int sh = __builtin_ctz(C8);  // C8 is a power of two (divides 256)
+  const int c8 = threadIdx.x & (C8 - 1);
+  float a[8], b[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float2 v = ss[static_cast<long>(n) * C + 8 * c8 + j];
+    a[j] = v.x;
+    b[j] = v.y;
+  }
+  const uint16_t* xn = x + static_cast<long>(n) * HW * ldx + xcoff + 8 * c8;
+  uint16_t* yn = y + static_cast<long>(n) * HW * ldy + ycoff + 8 * c8;
+  const int total = HW * C8;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+    const int p = i >> sh;
+    const uint4 v = *reinterpret_cast<const uint4*>(xn + static_cast<long>(p) * ldx);
     float f[8];
     unpack_bf16x2(v.x, f[0], f[1]);
     unpack_bf16x2(v.y, f[2], f[3]);
     unpack_bf16x2(v.z, f[4], f[5]);
     unpack_bf16x2(v.w, f[6], f[7]);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int c = 8 * c8 + j;
-      const int g = c / cg;
-      float t = (f[j] - mean_s[g]) * rstd_s[g] * gamma[c] + beta[c];
-      f[j] = relu ? fmaxf(t, 0.f) : t;
+    for (int j = 0; j < 8; ++j) f[j] = fmaf(f[j], a[j], b[j]);
+    uint4 o = make_uint4(cvt_bf16x2(f[0], f[1]), cvt_bf16x2(f[2], f[3]), cvt_bf16x2(f[4], f[5]), cvt_bf16x2(f[6], f[7]));
+    if (relu) {
+      o.x = relu_bf16x2(o.x); o.y = relu_bf16x2(o.y); o.z = relu_bf16x2(o.z); o.w = relu_bf16x2(o.w);
     }
-    *reinterpret_cast<uint4*>(y + (static_cast<long>(n) * HW + p) * ldy + ycoff + 8 * c8) =
-        make_uint4(pack_bf16x2(f[0], f[1]), pack_bf16x2(f[2], f[3]), pack_bf16x2(f[4], f[5]), pack_bf16x2(f[6], f[7]));
+    *reinterpret_cast<uint4*>(yn + static_cast<long>(p) * ldy) = o;
   }
 }
 
@@ -151,7 +186,8 @@ inline int grid_for(long work) {
 
 }  // namespace
 
-// partials must hold N * ceil(HW / 1024) * G * 2 floats.
+// partials (workspace) must hold N * ceil(HW / 1024) * G * 2 + N * C * 2 floats (chunk partials, then the
+// per-channel affine). HW * C / 8 < 2^31.
 AI4E_API int ai4e_groupnorm_nhwc(const void* x, void* y, const void* gamma, const void* beta, void* partials, int N,
                                  int HW, int C, int G, float eps, int relu, int ldx_ldy_pack, int coff_pack,
                                  hipStream_t s) {
@@ -161,13 +197,17 @@ AI4E_API int ai4e_groupnorm_nhwc(const void* x, void* y, const void* gamma, cons
   if (C % 8 || G > 64 || C % G || (C / 8) > 256 || 256 % (C / 8) || ldx % 8 || ldy % 8 || xcoff % 8 || ycoff % 8)
     return AI4E_EINVAL;
   if ((C / G) % 8 && 8 % (C / G)) return AI4E_EINVAL;
+  if (static_cast<long>(HW) * (C / 8) >= (1L << 31) - 8192L * 256) return AI4E_EINVAL;
   const int nchunks = (HW + GN_PIX_PER_BLOCK - 1) / GN_PIX_PER_BLOCK;
   hipLaunchKernelGGL(gn_stats_kernel, dim3(nchunks, N), dim3(256), 0, s, static_cast<const uint16_t*>(x),
                      static_cast<float*>(partials), HW, C, G, ldx, xcoff, nchunks);
+  float2* ss = reinterpret_cast<float2*>(static_cast<float*>(partials) + static_cast<long>(N) * nchunks * G * 2);
+  hipLaunchKernelGGL(gn_finalize_kernel, dim3(N), dim3(256), 0, s, static_cast<const float*>(partials),
+                     static_cast<const float*>(gamma), static_cast<const float*>(beta), ss, HW, C, G, eps, nchunks);
+  // ~4 vectors per lane; at most 8192 workgroups per image
   const int gx = grid_for(static_cast<long>(HW) * (C / 8) / 4 + 1);
   hipLaunchKernelGGL(gn_apply_kernel, dim3(gx, N), dim3(256), 0, s, static_cast<const uint16_t*>(x),
-                     static_cast<uint16_t*>(y), static_cast<const float*>(partials), static_cast<const float*>(gamma),
-                     static_cast<const float*>(beta), HW, C, G, eps, relu, nchunks, ldx, xcoff, ldy, ycoff);
+                     static_cast<uint16_t*>(y), ss, HW, C, relu, ldx, xcoff, ldy, ycoff);
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
 }
 
