@@ -1,0 +1,93 @@
+"""Per-shape K1 tile-config sweep for the convs one model forward actually runs (U-Net land-cover tiles,
+Faster-RCNN detector batches): records every ``tuned_tile`` lookup during a forward, times tile configs
+1-6 on each distinct shape in isolation and, with ``--write``, MERGES the winners into
+``aiforearth_api_platform_amd/ops/conv_tiles.json`` (existing keys of other shapes are kept).
+
+    python bench/conv_tune_model.py unet [--write]      # batch 16 x 512^2 x 4 (bench/landcover_bench.py)
+    python bench/conv_tune_model.py detector [--write]  # batch 8 x 640^2 x 3 (bench/detector_bench.py)
+"""
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from aiforearth_api_platform_amd.ops import conv as convmod  # noqa: E402
+
+TILES = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "aiforearth_api_platform_amd", "ops",
+                     "conv_tiles.json")
+
+
+def record(run):
+    seen = {}
+    orig = convmod.tuned_tile
+
+    def rec(pc, n, h, w, residual):
+        seen.setdefault(convmod.tile_key(pc, n, h, w, residual), (pc, n, h, w, residual))
+        return orig(pc, n, h, w, residual)
+
+    convmod.tuned_tile = rec
+    try:
+        run()
+        torch.cuda.synchronize()
+    finally:
+        convmod.tuned_tile = orig
+    return seen
+
+
+def time_cfg(pc, n, h, w, res, cfg, dev):
+    x = torch.randn(n, h, w, pc.cin_pad, device=dev).bfloat16()
+    oh, ow = pc.out_hw(h, w)
+    r = torch.randn(n, oh, ow, pc.cout, device=dev).bfloat16() if res else None
+    try:
+        convmod.conv2d_nhwc(x, pc, residual=r, relu=True, tile_cfg=cfg)
+    except RuntimeError:
+        return None  # config not valid for this shape
+    for _ in range(2):
+        convmod.conv2d_nhwc(x, pc, residual=r, relu=True, tile_cfg=cfg)
+    torch.cuda.synchronize()
+    st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    st.record()
+    for _ in range(5):
+        convmod.conv2d_nhwc(x, pc, residual=r, relu=True, tile_cfg=cfg)
+    en.record()
+    torch.cuda.synchronize()
+    return st.elapsed_time(en) / 5 * 1e3
+
+
+def main():
+    which = sys.argv[1] if len(sys.argv) > 1 else "unet"
+    dev = torch.device("cuda:0")
+    if which == "unet":
+        from aiforearth_api_platform_amd.models.unet import FusedUNet, unet_landcover
+        m = FusedUNet(unet_landcover(seed=0), device=dev)
+        img = torch.randint(0, 256, (16, 512, 512, 4), dtype=torch.uint8, device=dev)
+        shapes = record(lambda: m.forward_u8(img))
+    elif which == "detector":
+        from aiforearth_api_platform_amd.models.faster_rcnn import DetectorConfig, FasterRCNN
+        m = FasterRCNN(DetectorConfig(), seed=0, device=dev)
+        img = torch.randint(0, 256, (8, 640, 640, 3), dtype=torch.uint8, device=dev)
+        shapes = record(lambda: m.forward_u8(img))
+    else:
+        raise SystemExit(f"unknown model {which}")
+    table = {}
+    for key, (pc, n, h, w, res) in shapes.items():
+        times = {c: t for c in (1, 2, 3, 4, 5, 6) if (t := time_cfg(pc, n, h, w, res, c, dev)) is not None}
+        best = min(times, key=times.get)
+        table[key] = best
+        print(json.dumps({"key": key, "us": {k: round(v, 1) for k, v in times.items()}, "best": best}), flush=True)
+    if "--write" in sys.argv:
+        try:
+            with open(TILES) as f:
+                merged = json.load(f)
+        except (OSError, ValueError):
+            merged = {}
+        merged.update(table)
+        with open(TILES, "w") as f:
+            json.dump(merged, f, indent=1, sort_keys=True)
+        print("merged", len(table), "entries into", TILES, flush=True)
+
+
+if __name__ == "__main__":
+    main()
