@@ -37,29 +37,77 @@ __global__ __launch_bounds__(NMS_BLOCK) void nms_mask_kernel(const float4* __res
   mask[(static_cast<long>(b) * N + i) * W + jb] = bits;
 }
 
-// One wave per image: greedy scan in score order over the bitmask. valid[b] = number of real boxes
-// (the rest are padding). keep[b][0..count) = kept indices (<= max_out), count[b].
+// One wave per image: greedy scan in score order over the bitmask, 64 candidates (one mask word) at a
+// time. valid[b] = number of real boxes (the rest are padding). keep[b][0..count) = kept indices
+// (<= max_out), count[b].
+//  * the "removed" bitmap lives in registers: lane l owns words l and l + 64 (N <= 8192);
+//  * inside a 64-box block the greedy order is resolved on the block's own mask words (lane i holds box i's
+//    word for this block, one coalesced load; a scalar loop over the alive bits with lane reads);
+//  * the full rows of the block's kept boxes are OR-ed into the bitmap 8 rows per batch, so their loads are
+//    in flight together (one memory latency per 8 kept boxes instead of one per box).
+__device__ __forceinline__ unsigned long long readlane_u64(unsigned long long v, int l) {
+  const uint32_t lo = __builtin_amdgcn_readlane(static_cast<uint32_t>(v), l);
+  const uint32_t hi = __builtin_amdgcn_readlane(static_cast<uint32_t>(v >> 32), l);
+  return (static_cast<unsigned long long>(hi) << 32) | lo;
+}
+
 __global__ __launch_bounds__(64) void nms_reduce_kernel(const unsigned long long* __restrict__ mask,
                                                         const int* __restrict__ valid, int N, int max_out,
                                                         int* __restrict__ keep, int* __restrict__ count) {
   const int b = blockIdx.x;
   const int W = (N + 63) / 64;
   const int lane = threadIdx.x;
-  __shared__ unsigned long long removed[128];  // N <= 8192
-  for (int w = lane; w < W; w += 64) removed[w] = 0;
-  __syncthreads();
   const int n = valid ? min(valid[b], N) : N;
+  const unsigned long long* const mb = mask + static_cast<long>(b) * N * W;
+  unsigned long long rem0 = 0, rem1 = 0;  // removed bits of words lane, lane + 64
   int kept = 0;
-  for (int i = 0; i < n && kept < max_out; ++i) {
-    const bool dead = (removed[i >> 6] >> (i & 63)) & 1ull;
-    if (dead) continue;  // uniform across the wave (LDS broadcast)
-    if (lane == 0) keep[static_cast<long>(b) * max_out + kept] = i;
-    ++kept;
-    const unsigned long long* row = mask + (static_cast<long>(b) * N + i) * W;
-    for (int w = (i >> 6) + lane; w < W; w += 64) removed[w] |= row[w];
-    __syncthreads();
+  const int nblk = (n + 63) / 64;
+  for (int wb = 0; wb < nblk && kept < max_out; ++wb) {
+    const unsigned long long remw = wb < 64 ? readlane_u64(rem0, wb) : readlane_u64(rem1, wb - 64);
+    const int inblk = min(64, n - 64 * wb);
+    unsigned long long alive = ~remw & (inblk == 64 ? ~0ull : ((1ull << inblk) - 1));
+    const int i_l = 64 * wb + lane;
+    const unsigned long long mine = i_l < n ? mb[static_cast<long>(i_l) * W + wb] : 0ull;
+    unsigned long long keepbits = 0;
+    int kb = 0;
+    while (alive && kept + kb < max_out) {
+      const int i = __builtin_ctzll(alive);
+      keepbits |= 1ull << i;
+      ++kb;
+      alive &= ~(1ull << i);
+      alive &= ~readlane_u64(mine, i);  // box i suppresses the later boxes of this block
+    }
+    if ((keepbits >> lane) & 1ull)
+      keep[static_cast<long>(b) * max_out + kept + __builtin_popcountll(keepbits & ((1ull << lane) - 1))] = i_l;
+    kept += kb;
+    // OR the kept rows' later words into the bitmap, 8 rows per batch
+    const int w0 = lane, w1 = lane + 64;
+    const bool ok0 = w0 > wb && w0 < W, ok1 = w1 > wb && w1 < W;
+    while (keepbits && wb + 1 < W) {
+      long rows[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        if (keepbits) {
+          rows[u] = static_cast<long>(64 * wb + __builtin_ctzll(keepbits)) * W;
+          keepbits &= keepbits - 1;
+        } else {
+          rows[u] = -1;
+        }
+      }
+      unsigned long long r0[8], r1[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        r0[u] = rows[u] >= 0 && ok0 ? mb[rows[u] + w0] : 0ull;
+        r1[u] = rows[u] >= 0 && ok1 ? mb[rows[u] + w1] : 0ull;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        rem0 |= r0[u];
+        rem1 |= r1[u];
+      }
+    }
   }
-  if (lane == 0) count[b] = kept;
+  if (lane == 0) count[b] = min(kept, max_out);
 }
 
 __device__ __forceinline__ void bilinear_acc8(const uint16_t* __restrict__ feat, int H, int W, int C, float y, float x,
