@@ -22,7 +22,7 @@ import torch
 import torch.nn as nn
 
 from ..ops.conv import PackedConv, conv2d_nhwc, pack_conv
-from ..ops.detection import clip_boxes, decode_boxes, nms_batched_sorted, roi_align_fpn
+from ..ops.detection import clip_boxes, decode_boxes, nms_batched_sorted, roi_align_fpn, rpn_decode_into
 from ..ops.pool import maxpool2d_nhwc, preprocess_s2d_u8, preprocess_u8
 from .resnet import FusedResNet, resnet50
 
@@ -130,26 +130,19 @@ class FasterRCNN:
         shapes = [p.shape[1:3] for p in P]
         strides = [img_hw[0] // s[0] for s in shapes]
         anchors = self.anchors(shapes, strides)
-        boxes_l, scores_l, lvl_l = [], [], []
-        for li, p in enumerate(P):
+        ks = [min(cfg.pre_nms_top_n, p.shape[1] * p.shape[2] * A) for p in P]
+        KT = sum(ks)
+        boxes = torch.empty(B, KT, 4, device=P[0].device, dtype=torch.float32)
+        scores = torch.empty(B, KT, device=P[0].device, dtype=torch.float32)
+        lvl = torch.empty(B, KT, device=P[0].device, dtype=torch.float32)
+        off = 0
+        for li, (p, k) in enumerate(zip(P, ks)):
             t = conv2d_nhwc(p, self.rpn_conv, relu=True)
-            head = conv2d_nhwc(t, self.rpn_head).float()          # [B, h, w, 16]
-            obj = head[..., :A].reshape(B, -1)
-            deltas = head[..., A: 5 * A].reshape(B, -1, 4)
-            k = min(cfg.pre_nms_top_n, obj.shape[1])
-            sc, idx = obj.topk(k, dim=1)
-            d = torch.gather(deltas, 1, idx[..., None].expand(B, k, 4))
-            a = anchors[li][idx]
-            bx = clip_boxes(decode_boxes(a, d), img_hw[0], img_hw[1])
-            boxes_l.append(bx)
-            scores_l.append(torch.sigmoid(sc))
-            lvl_l.append(torch.full((B, k), li, device=bx.device, dtype=torch.float32))
-        boxes = torch.cat(boxes_l, 1)
-        scores = torch.cat(scores_l, 1)
-        lvl = torch.cat(lvl_l, 1)
-        wh = boxes[..., 2:] - boxes[..., :2]
-        small = (wh < cfg.rpn_min_size).any(-1)
-        scores = scores.masked_fill(small, -1.0)
+            head = conv2d_nhwc(t, self.rpn_head)                   # [B, h, w, 16]: A logits, 4A deltas
+            _, idx = head[..., :A].reshape(B, -1).topk(k, dim=1)  # per-level pre-NMS top-k
+            # decode + clip + sigmoid + min-size mask straight into the all-level buffers (one HIP launch)
+            rpn_decode_into(head, idx, anchors[li], A, boxes, scores, lvl, off, li, img_hw, cfg.rpn_min_size)
+            off += k
         # batched NMS across levels via coordinate offsets; invalid (small) boxes sort last
         order = scores.argsort(dim=1, descending=True)
         boxes_s = torch.gather(boxes, 1, order[..., None].expand_as(boxes))

@@ -48,6 +48,33 @@ def clip_boxes(boxes: torch.Tensor, h: int, w: int) -> torch.Tensor:
                         boxes[..., 3].clamp(0, h)], dim=-1)
 
 
+def rpn_decode_into(head: torch.Tensor, idx: torch.Tensor, anchors: torch.Tensor, num_anchors: int,
+                    boxes: torch.Tensor, scores: torch.Tensor, lvl: torch.Tensor, off: int, level: int,
+                    img_hw: Tuple[int, int], min_size: float, clip: float = math.log(1000.0 / 16)) -> None:
+    """One FPN level's RPN proposals into columns [off, off + k) of the all-level buffers: deltas and anchors
+    gathered by the top-k flat indices ``idx`` [B, k] (pos * A + a), decoded, clipped to the image; score =
+    sigmoid(objectness), -1 for boxes narrower or shorter than ``min_size``; lvl = level.
+    ``head`` [B, h, w, >= 5A] holds A objectness logits then 4A deltas per pixel."""
+    B, k = idx.shape
+    A = num_anchors
+    hw = head.shape[1] * head.shape[2]
+    if _ext.backend_for(head) == "hip" and head.dtype == torch.bfloat16 and head.is_contiguous():
+        _ext.call("ai4e_rpn_decode", head.data_ptr(), idx.contiguous().data_ptr(), anchors.data_ptr(), boxes.data_ptr(),
+                  scores.data_ptr(), lvl.data_ptr(), B, hw, head.shape[-1], A, k, boxes.shape[1], off, float(level),
+                  float(img_hw[0]), float(img_hw[1]), float(min_size), float(clip), _ext.stream_ptr(head.device))
+        return
+    hf = head.float().reshape(B, hw, -1)
+    obj = hf[..., :A].reshape(B, -1)
+    deltas = hf[..., A: 5 * A].reshape(B, -1, 4)
+    d = torch.gather(deltas, 1, idx[..., None].expand(B, k, 4))
+    bx = clip_boxes(decode_boxes(anchors[idx], d, clip=clip), img_hw[0], img_hw[1])
+    sc = torch.sigmoid(torch.gather(obj, 1, idx))
+    wh = bx[..., 2:] - bx[..., :2]
+    boxes[:, off:off + k] = bx
+    scores[:, off:off + k] = sc.masked_fill((wh < min_size).any(-1), -1.0)
+    lvl[:, off:off + k] = float(level)
+
+
 # ---------------------------------------------------------------------------------------------- NMS
 def nms_reference(boxes: torch.Tensor, scores: torch.Tensor, thr: float) -> torch.Tensor:
     """Greedy NMS (torchvision.ops.nms semantics): indices kept, in descending score order."""

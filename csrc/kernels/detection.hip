@@ -110,6 +110,37 @@ __global__ __launch_bounds__(64) void nms_reduce_kernel(const unsigned long long
   if (lane == 0) count[b] = min(kept, max_out);
 }
 
+// RPN proposals of one FPN level, decoded straight into the all-level buffers (replaces ~20 small PyTorch
+// launches per level: gather of deltas and anchors, box decode, clip, sigmoid, min-size mask, concat).
+// head: bf16 [B, HW, ldh] (A objectness logits, then 4A deltas per pixel); idx: int64 [B, k] top-k flat
+// indices pos * A + a; anchors fp32 [HW * A, 4]; outputs at columns [off, off + k) of boxes [B, KT, 4],
+// scores [B, KT] (sigmoid, -1 for boxes under min_size) and lvl [B, KT].
+__global__ __launch_bounds__(256) void rpn_decode_kernel(const uint16_t* __restrict__ head, const long* __restrict__ idx,
+                                                         const float4* __restrict__ anchors, float4* __restrict__ boxes,
+                                                         float* __restrict__ scores, float* __restrict__ lvl, int B,
+                                                         int HW, int ldh, int A, int k, int KT, int off, float level,
+                                                         float img_h, float img_w, float min_size, float clip) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= B * k) return;
+  const int b = t / k, j = t - b * k;
+  const long flat = idx[static_cast<long>(b) * k + j];
+  const int pos = static_cast<int>(flat / A), a = static_cast<int>(flat - static_cast<long>(pos) * A);
+  const uint16_t* hp = head + (static_cast<long>(b) * HW + pos) * ldh;
+  const float obj = bf16_to_f32(hp[a]);
+  const float dx = bf16_to_f32(hp[A + 4 * a]), dy = bf16_to_f32(hp[A + 4 * a + 1]);
+  const float dw = fminf(bf16_to_f32(hp[A + 4 * a + 2]), clip), dh = fminf(bf16_to_f32(hp[A + 4 * a + 3]), clip);
+  const float4 an = anchors[flat];
+  const float w = an.z - an.x, h = an.w - an.y;
+  const float cx = an.x + 0.5f * w, cy = an.y + 0.5f * h;
+  const float pcx = dx * w + cx, pcy = dy * h + cy, pw = expf(dw) * w, ph = expf(dh) * h;
+  const float x1 = fminf(fmaxf(pcx - 0.5f * pw, 0.f), img_w), y1 = fminf(fmaxf(pcy - 0.5f * ph, 0.f), img_h);
+  const float x2 = fminf(fmaxf(pcx + 0.5f * pw, 0.f), img_w), y2 = fminf(fmaxf(pcy + 0.5f * ph, 0.f), img_h);
+  const long o = static_cast<long>(b) * KT + off + j;
+  boxes[o] = make_float4(x1, y1, x2, y2);
+  scores[o] = (x2 - x1 < min_size || y2 - y1 < min_size) ? -1.f : 1.f / (1.f + expf(-obj));
+  lvl[o] = level;
+}
+
 __device__ __forceinline__ void bilinear_acc8(const uint16_t* __restrict__ feat, int H, int W, int C, float y, float x,
                                               int c8, float w, float* acc) {
   if (y < -1.f || y > H || x < -1.f || x > W) return;
@@ -285,6 +316,18 @@ AI4E_API int ai4e_nms_reduce(const void* mask, const void* valid, int B, int N, 
   if (N > 8192) return AI4E_EINVAL;
   hipLaunchKernelGGL(nms_reduce_kernel, dim3(B), dim3(64), 0, s, static_cast<const unsigned long long*>(mask),
                      static_cast<const int*>(valid), N, max_out, static_cast<int*>(keep), static_cast<int*>(count));
+  return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
+}
+
+AI4E_API int ai4e_rpn_decode(const void* head, const void* idx, const void* anchors, void* boxes, void* scores,
+                             void* lvl, int B, int HW, int ldh, int A, int k, int KT, int off, float level, float img_h,
+                             float img_w, float min_size, float clip, hipStream_t s) {
+  if (B <= 0 || k <= 0) return AI4E_OK;
+  if (!head || !idx || !anchors || !boxes || !scores || !lvl || A <= 0 || ldh < 5 * A || off + k > KT) return AI4E_EINVAL;
+  hipLaunchKernelGGL(rpn_decode_kernel, dim3((B * k + 255) / 256), dim3(256), 0, s, static_cast<const uint16_t*>(head),
+                     static_cast<const long*>(idx), static_cast<const float4*>(anchors), static_cast<float4*>(boxes),
+                     static_cast<float*>(scores), static_cast<float*>(lvl), B, HW, ldh, A, k, KT, off, level, img_h,
+                     img_w, min_size, clip);
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
 }
 

@@ -114,3 +114,33 @@ def test_tile_stitch(with_prob):
     ty0, ty1 = grid.tile_rows_for(100, 180)
     cls2, _ = tile_stitch(tiles[ty0:ty1].to(DEV), grid, row0=100, rows=80, ty0=ty0)
     assert torch.equal(cls2.cpu(), cls.cpu()[100:180])
+
+
+@pytest.mark.parametrize("B,h,w,k", [(2, 40, 40, 1000), (3, 10, 10, 300), (1, 5, 7, 105)])
+def test_rpn_decode_matches_reference(B, h, w, k):
+    """Fused RPN decode (gather + decode + clip + sigmoid + min-size mask into the all-level buffers) vs the
+    PyTorch formulation of the same op on the CPU."""
+    from aiforearth_api_platform_amd.ops.detection import rpn_decode_into
+
+    A = 3
+    torch.manual_seed(3)
+    head = (torch.randn(B, h, w, 16) * 2).to(torch.bfloat16)
+    head[..., A + 2: 5 * A: 4] *= 3  # some dw beyond the clip
+    anchors = torch.rand(h * w * A, 4) * 300
+    anchors[:, 2:] += anchors[:, :2] + torch.rand(h * w * A, 2) * 5  # includes tiny boxes
+    idx = head[..., :A].float().reshape(B, -1).topk(min(k, h * w * A), dim=1)[1]
+    k = idx.shape[1]
+    KT, off = k + 17, 9
+    outs = []
+    for dev in ("cpu", DEV):
+        hd = head.to(dev) if dev != "cpu" else head.float()
+        bx = torch.full((B, KT, 4), 7.0, device=dev)
+        sc = torch.full((B, KT), 7.0, device=dev)
+        lv = torch.full((B, KT), 7.0, device=dev)
+        rpn_decode_into(hd, idx.to(dev), anchors.to(dev), A, bx, sc, lv, off, 2, (320, 300), 1.0)
+        outs.append((bx.cpu(), sc.cpu(), lv.cpu()))
+    (b0, s0, l0), (b1, s1, l1) = outs
+    assert torch.allclose(b0, b1, rtol=1e-4, atol=1e-2)
+    assert torch.allclose(s0, s1, rtol=1e-4, atol=1e-5)
+    assert torch.equal(l0, l1)
+    assert (b1[:, :off] == 7.0).all() and (b1[:, off + k:] == 7.0).all()
