@@ -22,7 +22,7 @@ import torch
 import torch.nn as nn
 
 from ..ops.conv import PackedConv, conv2d_nhwc, pack_conv
-from ..ops.detection import clip_boxes, decode_boxes, nms_batched_sorted, roi_align_fpn, rpn_decode_into
+from ..ops.detection import det_decode, nms_batched_sorted, roi_align_fpn, rpn_decode_into
 from ..ops.pool import maxpool2d_nhwc, preprocess_s2d_u8, preprocess_u8
 from .resnet import FusedResNet, resnet50
 
@@ -166,23 +166,15 @@ class FasterRCNN:
         x = feats.reshape(B * R, 1, 1, -1)
         x = conv2d_nhwc(x, self.fc6, relu=True)
         x = conv2d_nhwc(x, self.fc7, relu=True)
-        out = conv2d_nhwc(x, self.predictor).reshape(B, R, -1).float()
-        nc = self.cfg.num_classes
-        return out[..., :nc], out[..., nc: 5 * nc].reshape(B, R, nc, 4)
+        # [B, R, >= 5 nc]: nc class logits, then 4 nc box deltas
+        return conv2d_nhwc(x, self.predictor).reshape(B, R, -1)
 
-    def postprocess(self, props, count, logits, deltas, img_hw):
+    def postprocess(self, props, count, pred, img_hw):
         cfg = self.cfg
-        B, R, nc = logits.shape
-        scores = torch.softmax(logits, -1)[..., 1:]                            # drop background
-        boxes = decode_boxes(props[:, :, None, :].expand(B, R, nc - 1, 4), deltas[:, :, 1:], cfg.box_reg_weights)
-        boxes = clip_boxes(boxes, img_hw[0], img_hw[1])
-        labels = torch.arange(1, nc, device=props.device).expand(B, R, nc - 1)
-        roi_valid = (torch.arange(R, device=props.device)[None] < count[:, None].long())[..., None]
-        wh = boxes[..., 2:] - boxes[..., :2]
-        ok = roi_valid & (scores > cfg.box_score_thresh) & (wh >= 1e-2).all(-1)
-        scores = scores.masked_fill(~ok, -1.0).reshape(B, -1)
-        boxes = boxes.reshape(B, -1, 4)
-        labels = labels.reshape(B, -1)
+        B = props.shape[0]
+        # softmax (background dropped) + per-class decode + clip + validity mask: one HIP launch
+        boxes, scores, labels = det_decode(pred, props, count, cfg.num_classes, cfg.box_reg_weights, img_hw,
+                                           cfg.box_score_thresh)
         order = scores.argsort(1, descending=True)
         s_s = torch.gather(scores, 1, order)
         b_s = torch.gather(boxes, 1, order[..., None].expand_as(boxes))
@@ -203,8 +195,7 @@ class FasterRCNN:
         img_hw = (x.shape[1], x.shape[2]) if x.shape[-1] != 16 else (2 * x.shape[1], 2 * x.shape[2])
         P = self.fpn(self.backbone_stages(x))
         props, count = self.proposals(P, img_hw)
-        logits, deltas = self.box_head(P, props, img_hw)
-        return self.postprocess(props, count, logits, deltas, img_hw)
+        return self.postprocess(props, count, self.box_head(P, props, img_hw), img_hw)
 
     def forward_u8(self, img_u8: torch.Tensor):
         return self.forward(preprocess_s2d_u8(img_u8))

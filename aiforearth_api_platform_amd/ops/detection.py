@@ -75,6 +75,40 @@ def rpn_decode_into(head: torch.Tensor, idx: torch.Tensor, anchors: torch.Tensor
     lvl[:, off:off + k] = float(level)
 
 
+def det_decode(pred: torch.Tensor, props: torch.Tensor, count: torch.Tensor, num_classes: int,
+               weights: Sequence[float], img_hw: Tuple[int, int], score_thresh: float,
+               clip: float = math.log(1000.0 / 16)) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """Box-head postprocess before the final NMS: softmax over the nc logits of each RoI, every foreground
+    class's box decoded from the RoI's proposal (regression ``weights``) and clipped; score -1 unless the RoI
+    is real (r < count[b]), the score clears ``score_thresh`` and the box is >= 1e-2 wide and high.
+    pred [B, R, >= 5 nc] (logits, then 4 nc deltas), props [B, R, 4], count [B] ->
+    boxes [B, R * (nc-1), 4], scores [B, R * (nc-1)], labels [B, R * (nc-1)] (int64, 1..nc-1)."""
+    B, R, ldp = pred.shape
+    nc = num_classes
+    if _ext.backend_for(pred) == "hip":
+        pred = pred.float().contiguous()
+        boxes = torch.empty(B, R * (nc - 1), 4, device=pred.device, dtype=torch.float32)
+        scores = torch.empty(B, R * (nc - 1), device=pred.device, dtype=torch.float32)
+        labels = torch.empty(B, R * (nc - 1), device=pred.device, dtype=torch.int64)
+        w4 = (ctypes.c_float * 4)(*[float(v) for v in weights])
+        _ext.call("ai4e_det_decode", pred.data_ptr(), props.float().contiguous().data_ptr(),
+                  count.to(torch.int32).contiguous().data_ptr(), boxes.data_ptr(), scores.data_ptr(), labels.data_ptr(),
+                  B, R, ldp, nc, ctypes.addressof(w4), float(img_hw[0]), float(img_hw[1]), float(score_thresh),
+                  float(clip), _ext.stream_ptr(pred.device))
+        return boxes, scores, labels
+    pred = pred.float()
+    logits, deltas = pred[..., :nc], pred[..., nc: 5 * nc].reshape(B, R, nc, 4)
+    scores = torch.softmax(logits, -1)[..., 1:]
+    boxes = decode_boxes(props[:, :, None, :].expand(B, R, nc - 1, 4), deltas[:, :, 1:], weights, clip)
+    boxes = clip_boxes(boxes, img_hw[0], img_hw[1])
+    labels = torch.arange(1, nc, device=props.device).expand(B, R, nc - 1)
+    roi_valid = (torch.arange(R, device=props.device)[None] < count[:, None].long())[..., None]
+    wh = boxes[..., 2:] - boxes[..., :2]
+    ok = roi_valid & (scores > score_thresh) & (wh >= 1e-2).all(-1)
+    scores = scores.masked_fill(~ok, -1.0).reshape(B, -1)
+    return boxes.reshape(B, -1, 4), scores, labels.reshape(B, -1)
+
+
 # ---------------------------------------------------------------------------------------------- NMS
 def nms_reference(boxes: torch.Tensor, scores: torch.Tensor, thr: float) -> torch.Tensor:
     """Greedy NMS (torchvision.ops.nms semantics): indices kept, in descending score order."""

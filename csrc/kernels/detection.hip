@@ -141,6 +141,42 @@ __global__ __launch_bounds__(256) void rpn_decode_kernel(const uint16_t* __restr
   lvl[o] = level;
 }
 
+// Box-head postprocess (one thread per (image, RoI, foreground class)): softmax over the RoI's nc logits,
+// the class's box decoded from its proposal with the regression weights, clipped; score -1 unless the RoI
+// is real (r < count[b]), the score clears thresh and the box is at least 1e-2 wide and high.
+// pred: fp32 [B, R, ldp] (nc logits, then 4 nc deltas); props fp32 [B, R, 4]; outputs [B, R * (nc - 1)].
+__global__ __launch_bounds__(256) void det_decode_kernel(const float* __restrict__ pred, const float4* __restrict__ props,
+                                                         const int* __restrict__ count, float4* __restrict__ boxes,
+                                                         float* __restrict__ scores, long* __restrict__ labels, int B,
+                                                         int R, int ldp, int nc, float4 wts, float img_h, float img_w,
+                                                         float thresh, float clip) {
+  const int ncf = nc - 1;
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= B * R * ncf) return;
+  const int b = t / (R * ncf);
+  const int rc = t - b * R * ncf;
+  const int r = rc / ncf, c = rc - r * ncf + 1;
+  const float* lp = pred + (static_cast<long>(b) * R + r) * ldp;
+  float mx = lp[0];
+  for (int q = 1; q < nc; ++q) mx = fmaxf(mx, lp[q]);
+  float den = 0.f;
+  for (int q = 0; q < nc; ++q) den += expf(lp[q] - mx);
+  const float sc = expf(lp[c] - mx) / den;
+  const float4 pr = props[static_cast<long>(b) * R + r];
+  const float* dp = lp + nc + 4 * c;
+  const float w = pr.z - pr.x, h = pr.w - pr.y;
+  const float cx = pr.x + 0.5f * w, cy = pr.y + 0.5f * h;
+  const float dx = dp[0] / wts.x, dy = dp[1] / wts.y;
+  const float dw = fminf(dp[2] / wts.z, clip), dh = fminf(dp[3] / wts.w, clip);
+  const float pcx = dx * w + cx, pcy = dy * h + cy, pw = expf(dw) * w, ph = expf(dh) * h;
+  const float x1 = fminf(fmaxf(pcx - 0.5f * pw, 0.f), img_w), y1 = fminf(fmaxf(pcy - 0.5f * ph, 0.f), img_h);
+  const float x2 = fminf(fmaxf(pcx + 0.5f * pw, 0.f), img_w), y2 = fminf(fmaxf(pcy + 0.5f * ph, 0.f), img_h);
+  const bool ok = r < count[b] && sc > thresh && x2 - x1 >= 1e-2f && y2 - y1 >= 1e-2f;
+  boxes[t] = make_float4(x1, y1, x2, y2);
+  scores[t] = ok ? sc : -1.f;
+  labels[t] = c;
+}
+
 __device__ __forceinline__ void bilinear_acc8(const uint16_t* __restrict__ feat, int H, int W, int C, float y, float x,
                                               int c8, float w, float* acc) {
   if (y < -1.f || y > H || x < -1.f || x > W) return;
@@ -328,6 +364,19 @@ AI4E_API int ai4e_rpn_decode(const void* head, const void* idx, const void* anch
                      static_cast<const long*>(idx), static_cast<const float4*>(anchors), static_cast<float4*>(boxes),
                      static_cast<float*>(scores), static_cast<float*>(lvl), B, HW, ldh, A, k, KT, off, level, img_h,
                      img_w, min_size, clip);
+  return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
+}
+
+AI4E_API int ai4e_det_decode(const void* pred, const void* props, const void* count, void* boxes, void* scores,
+                             void* labels, int B, int R, int ldp, int nc, const float* wts4, float img_h, float img_w,
+                             float thresh, float clip, hipStream_t s) {
+  if (B <= 0 || R <= 0) return AI4E_OK;
+  if (!pred || !props || !count || !boxes || !scores || !labels || !wts4 || nc < 2 || ldp < 5 * nc) return AI4E_EINVAL;
+  const long n = static_cast<long>(B) * R * (nc - 1);
+  hipLaunchKernelGGL(det_decode_kernel, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, s,
+                     static_cast<const float*>(pred), static_cast<const float4*>(props), static_cast<const int*>(count),
+                     static_cast<float4*>(boxes), static_cast<float*>(scores), static_cast<long*>(labels), B, R, ldp, nc,
+                     make_float4(wts4[0], wts4[1], wts4[2], wts4[3]), img_h, img_w, thresh, clip);
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
 }
 

@@ -144,3 +144,27 @@ def test_rpn_decode_matches_reference(B, h, w, k):
     assert torch.allclose(s0, s1, rtol=1e-4, atol=1e-5)
     assert torch.equal(l0, l1)
     assert (b1[:, :off] == 7.0).all() and (b1[:, off + k:] == 7.0).all()
+
+
+@pytest.mark.parametrize("B,R,nc", [(2, 1000, 4), (3, 37, 7)])
+def test_det_decode_matches_reference(B, R, nc):
+    """Fused box-head postprocess (softmax + per-class decode + clip + validity mask) vs its PyTorch form."""
+    from aiforearth_api_platform_amd.ops.detection import det_decode
+
+    torch.manual_seed(4)
+    ldp = (5 * nc + 3) // 4 * 4
+    pred = torch.randn(B, R, ldp) * 2
+    pred[..., nc:] *= 0.5
+    props = torch.rand(B, R, 4) * 200
+    props[..., 2:] += props[..., :2] + torch.rand(B, R, 2) * 100
+    count = torch.randint(R // 2, R + 1, (B,), dtype=torch.int32)
+    wts = (10.0, 10.0, 5.0, 5.0)
+    ref = det_decode(pred, props, count, nc, wts, (320, 300), 0.05)
+    got = det_decode(pred.to(DEV).bfloat16().float(), props.to(DEV), count.to(DEV), nc, wts, (320, 300), 0.05)
+    ref2 = det_decode(pred.bfloat16().float(), props, count, nc, wts, (320, 300), 0.05)
+    b0, s0, l0 = ref2
+    b1, s1, l1 = [t.cpu() for t in got]
+    assert torch.allclose(b0, b1, rtol=1e-4, atol=1e-2)
+    assert torch.allclose(s0, s1, rtol=1e-4, atol=1e-5)
+    assert torch.equal(l0, l1)
+    assert ref[0].shape == b1.shape
