@@ -99,8 +99,12 @@ class FasterRCNN:
         inner = conv2d_nhwc(feats[-1], self.lateral[-1])
         results = [conv2d_nhwc(inner, self.fpn_out[-1])]
         for i in range(len(feats) - 2, -1, -1):
-            top = _nearest_up2(inner, feats[i].shape[1:3])
-            inner = conv2d_nhwc(feats[i], self.lateral[i], residual=top)  # lateral + top-down fused
+            hw = tuple(feats[i].shape[1:3])
+            if hw == (2 * inner.shape[1], 2 * inner.shape[2]):
+                # lateral + nearest-2x top-down merge in one launch: the epilogue reads the coarse map directly
+                inner = conv2d_nhwc(feats[i], self.lateral[i], residual=inner, residual_up2=True)
+            else:
+                inner = conv2d_nhwc(feats[i], self.lateral[i], residual=_nearest_up2(inner, hw))
             results.insert(0, conv2d_nhwc(inner, self.fpn_out[i]))
         results.append(maxpool2d_nhwc(results[-1], 1, 2, 0))  # P6
         return results

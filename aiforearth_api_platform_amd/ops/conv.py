@@ -111,7 +111,10 @@ def tuned_tile(pc: PackedConv, n: int, h: int, w: int, residual: bool) -> int:
 
 
 def conv2d_nhwc(x: torch.Tensor, pc: PackedConv, residual: Optional[torch.Tensor] = None, relu: bool = False,
-                out: Optional[torch.Tensor] = None, out_coff: int = 0, tile_cfg: int = -1) -> torch.Tensor:
+                out: Optional[torch.Tensor] = None, out_coff: int = 0, tile_cfg: int = -1,
+                residual_up2: bool = False) -> torch.Tensor:
+    """``residual_up2``: ``residual`` is [N, OH/2, OW/2, Cout] and is added nearest-neighbour upsampled 2x
+    (the FPN top-down merge), read straight from the half-resolution tensor by the kernel epilogue."""
     n, h, w, c = x.shape
     if tile_cfg < 0:
         tile_cfg = tuned_tile(pc, n, h, w, residual is not None)
@@ -122,14 +125,16 @@ def conv2d_nhwc(x: torch.Tensor, pc: PackedConv, residual: Optional[torch.Tensor
         out = torch.empty(n, oh, ow, pc.cout, device=x.device, dtype=x.dtype)
         out_coff = 0
     if _ext.backend_for(x) == "hip":
-        _conv_hip(x, pc, residual, relu, out, out_coff, tile_cfg)
+        _conv_hip(x, pc, residual, relu, out, out_coff, tile_cfg, residual_up2)
     else:
+        if residual is not None and residual_up2:
+            residual = residual.repeat_interleave(2, dim=1).repeat_interleave(2, dim=2)
         y = _conv_torch(x, pc, residual, relu)
         out[..., out_coff:out_coff + pc.cout] = y.to(out.dtype)
     return out
 
 
-def _conv_hip(x, pc, residual, relu, out, out_coff, tile_cfg):
+def _conv_hip(x, pc, residual, relu, out, out_coff, tile_cfg, residual_up2=False):
     n, h, w, c = x.shape
     oh, ow = pc.out_hw(h, w)
     if x.dtype != torch.bfloat16 or out.dtype != torch.bfloat16:
@@ -145,12 +150,14 @@ def _conv_hip(x, pc, residual, relu, out, out_coff, tile_cfg):
     ldy = out.stride(2)
     ldres = 0
     if residual is not None:
-        if residual.shape != (n, oh, ow, pc.cout) or not residual.is_contiguous():
-            raise ValueError("residual must be contiguous [N,OH,OW,Cout]")
+        rshape = (n, oh // 2, ow // 2, pc.cout) if residual_up2 else (n, oh, ow, pc.cout)
+        if residual.shape != rshape or not residual.is_contiguous() or (residual_up2 and (oh % 2 or ow % 2)):
+            raise ValueError(f"residual must be contiguous {list(rshape)}")
         ldres = pc.cout
     _ext.call("ai4e_conv2d_fwd", base + 2 * (xoff - xoff % ldx), pc.w_packed.data_ptr(), pc.bias.data_ptr(),
               _ext.ptr(residual), out.data_ptr(), n, h, w, c, ldx, xoff % ldx, pc.kh, pc.kw, pc.stride, pc.pad,
-              oh, ow, pc.cout, pc.kpad, ldy, out_coff, ldres, int(relu), tile_cfg, _ext.stream_ptr(x.device))
+              oh, ow, pc.cout, pc.kpad, ldy, out_coff, ldres, int(relu) | (2 if residual_up2 else 0), tile_cfg,
+              _ext.stream_ptr(x.device))
 
 
 def chain_kernel_builds(mid: int, midn: int = 0) -> bool:

@@ -61,6 +61,17 @@ struct ConvParams {
   const uint16_t* zero;  // >= 16 zero bytes: source of the DMA gather for padding taps
 };
 
+// Row of the residual tensor for output pixel m: m itself, or (relu flag bit 1) the pixel (oh/2, ow/2) of a
+// half-resolution residual [N, OH/2, OW/2, ldres]: the FPN top-down nearest-neighbour 2x upsample fused into
+// the lateral conv's residual read (no upsampled tensor is materialized).
+__device__ __forceinline__ long res_row(const ConvParams& p, int m) {
+  if (!(p.relu & 2)) return m;
+  const int ohw = p.OH * p.OW;
+  const int img = m / ohw, rem = m - img * ohw;
+  const int oh = rem / p.OW, ow = rem - oh * p.OW;
+  return (static_cast<long>(img) * (p.OH >> 1) + (oh >> 1)) * (p.OW >> 1) + (ow >> 1);
+}
+
 // Gather modes of the activation operand.
 enum { GATHER_GENERAL = 0,  // any C % 8: a 32-wide K chunk may span taps -> per-lane tap walk
        GATHER_POINTWISE = 1,  // 1x1, pad 0 (any stride): K is the channel axis of one input pixel
@@ -104,7 +115,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
       for (int e = 0; e < EPI_CHUNKS; ++e) {
         const int g = tid + 256 * e;
         const int m = min(m0 + g / CPR, p.M - 1), n = min(n0 + 8 * (g % CPR), p.Kout - 8);
-        rres16[e] = *reinterpret_cast<const uint4*>(p.res + static_cast<long>(m) * p.ldres + n);
+        rres16[e] = *reinterpret_cast<const uint4*>(p.res + res_row(p, m) * p.ldres + n);
       }
     } else {
 #pragma unroll
@@ -112,7 +123,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int m = min(pm + 16 * i, p.M - 1), n = min(pn + 16 * j, p.Kout - 4);
-          rres[i][j] = *reinterpret_cast<const uint2*>(p.res + static_cast<long>(m) * p.ldres + n);
+          rres[i][j] = *reinterpret_cast<const uint2*>(p.res + res_row(p, m) * p.ldres + n);
         }
     }
   }
@@ -274,7 +285,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
       acc[i][j][0] += b.x; acc[i][j][1] += b.y; acc[i][j][2] += b.z; acc[i][j][3] += b.w;
     }
   }
-  const float lo = p.relu ? 0.f : -INFINITY;
+  const float lo = (p.relu & 1) ? 0.f : -INFINITY;
   if constexpr (EPI_LDS) {
     // Stage the fp32 tile through LDS (the now idle stage ring: BM*BN*4 bytes) so every lane
     // reads/writes 16 contiguous bytes: a wave instruction then covers whole 256-B+ pixel rows,
@@ -302,7 +313,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
       const float4 v0 = *reinterpret_cast<const float4*>(tile + r * BN + 4 * ((2 * cq) ^ (r & 7)));
       const float4 v1 = *reinterpret_cast<const float4*>(tile + r * BN + 4 * ((2 * cq + 1) ^ (r & 7)));
       const float f[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-      const uint4 o = epilogue8_bf16(f, p.res != nullptr, rres16[e], p.relu != 0);
+      const uint4 o = epilogue8_bf16(f, p.res != nullptr, rres16[e], (p.relu & 1) != 0);
       if (m < p.M && n < p.Kout) {
         uint16_t* dst = p.y + static_cast<long>(m) * p.ldy + p.ycoff + n;
         if (n + 8 <= p.Kout) {
@@ -563,7 +574,7 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
   // ---- epilogue, one pixel group at a time: fp32 [128][256] tile in LDS (16-B chunk index
   //      XOR (row & 7)), then every thread handles 16-B output chunks: + bias (+ residual), ReLU.
   float* tile = reinterpret_cast<float*>(smem);
-  const float lo = p.relu ? 0.f : -INFINITY;
+  const float lo = (p.relu & 1) ? 0.f : -INFINITY;
 #pragma unroll
   for (int pass = 0; pass < 2; ++pass) {
     if (wr == pass) {
@@ -584,7 +595,7 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
       for (int e = 0; e < 8; ++e) {
         const int g = tid + 512 * e;
         const int m = min(m0 + 128 * pass + (g >> 5), p.M - 1), n = min(n0 + 8 * (g & 31), p.Kout - 8);
-        rv[e] = *reinterpret_cast<const uint4*>(p.res + static_cast<long>(m) * p.ldres + n);
+        rv[e] = *reinterpret_cast<const uint4*>(p.res + res_row(p, m) * p.ldres + n);
       }
     }
 #pragma unroll
@@ -599,7 +610,7 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
       const float4 b1 = *reinterpret_cast<const float4*>(p.bias + nb + 4);
       const float f[8] = {v0.x + b0.x, v0.y + b0.y, v0.z + b0.z, v0.w + b0.w,
                           v1.x + b1.x, v1.y + b1.y, v1.z + b1.z, v1.w + b1.w};
-      const uint4 o = epilogue8_bf16(f, p.res != nullptr, rv[e], p.relu != 0);
+      const uint4 o = epilogue8_bf16(f, p.res != nullptr, rv[e], (p.relu & 1) != 0);
       if (m < p.M && n < p.Kout) *reinterpret_cast<uint4*>(p.y + static_cast<long>(m) * p.ldy + p.ycoff + n) = o;
     }
     __syncthreads();
@@ -668,6 +679,8 @@ int launch256(const ConvParams& p0, hipStream_t s) {
 // 2 = 256x64 (4x1), 3 = 64x256 (1x4) with 4 stages; 4 = 128x128 with 5 stages (80 KB: still two
 // workgroups per CU), 5 = 256x64 with 5 stages (100 KB: one workgroup per CU), 6 = 256x256, 8 waves,
 // ping-pong phases (needs C % 64 == 0, Kout % 8 == 0).
+// relu: bit 0 = ReLU; bit 1 = `res` is on the half-resolution grid [N, OH/2, OW/2, ldres] (nearest 2x
+// upsample of the residual, OH and OW even).
 AI4E_API int ai4e_conv2d_fwd(const void* x, const void* w, const void* bias, const void* res, void* y, int N, int H,
                              int W, int C, int ldx, int xcoff, int KH, int KW, int stride, int pad, int OH, int OW,
                              int Kout, int Kpad, int ldy, int ycoff, int ldres, int relu, int tile_cfg,
@@ -685,6 +698,7 @@ AI4E_API int ai4e_conv2d_fwd(const void* x, const void* w, const void* bias, con
   p.KH = KH; p.KW = KW; p.stride = stride; p.pad = pad; p.OH = OH; p.OW = OW;
   p.Kout = Kout; p.Kpad = Kpad; p.ldy = ldy; p.ycoff = ycoff; p.ldres = ldres; p.relu = relu;
   p.M = N * OH * OW;
+  if ((relu & 2) && (!res || (OH & 1) || (OW & 1))) return AI4E_EINVAL;  // half-resolution residual grid
   if (p.M <= 0) return AI4E_OK;
   if (tile_cfg == 0) tile_cfg = Kout <= 64 ? 2 : 1;
   switch (tile_cfg) {

@@ -184,3 +184,22 @@ def test_resnet_chunked_prefix_matches_full_batch_gpu():
     for chunk in [(4, 3), (8, 7)]:
         out = FusedResNet(m, device=DEV, chunk=chunk).forward_u8(img)
         assert (out - ref).abs().max().item() < 2e-2, chunk
+
+
+@pytest.mark.parametrize("tile", [1, 2, 4, 6])
+@pytest.mark.parametrize("shape", [(2, 40, 40, 256, 256), (3, 10, 14, 512, 256), (1, 6, 2, 64, 68)])
+def test_conv_residual_upsampled2x(tile, shape):
+    """FPN top-down merge fused into the lateral 1x1: the epilogue reads the residual from the half-resolution
+    map at (oh/2, ow/2) (nearest 2x upsample) == conv + explicitly upsampled residual."""
+    n, h, w, cin, cout = shape
+    if tile == 6 and cout % 8:
+        pytest.skip("256 tile needs Cout % 8 == 0")
+    torch.manual_seed(2)
+    pc = pack_conv(torch.randn(cout, cin, 1, 1) / cin ** 0.5, torch.randn(cout) * 0.1).to(DEV)
+    x = torch.randn(n, h, w, cin, device=DEV).to(torch.bfloat16)
+    coarse = torch.randn(n, h // 2, w // 2, cout, device=DEV).to(torch.bfloat16)
+    y = conv2d_nhwc(x, pc, residual=coarse, residual_up2=True, tile_cfg=tile)
+    up = coarse.repeat_interleave(2, dim=1).repeat_interleave(2, dim=2).contiguous()
+    ref = conv2d_nhwc(x, pc, residual=up, tile_cfg=tile)
+    torch.cuda.synchronize()
+    assert torch.equal(y, ref)
