@@ -140,18 +140,20 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const uint16_t* __restric
 }
 
 // Bilinear 2x upsample, align_corners=False (PyTorch semantics): src = (dst + 0.5) / 2 - 0.5, clamped.
+// IDX = int when the element count fits (32-bit index math instead of a 64-bit div/mod chain per vector)
+template <typename IDX>
 __global__ __launch_bounds__(256) void upsample2x_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
                                                          int N, int H, int W, int C, int ldy, int ycoff) {
   const int C8 = C >> 3;
   const int OH = 2 * H, OW = 2 * W;
-  const long total = static_cast<long>(N) * OH * OW * C8;
-  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += static_cast<long>(gridDim.x) * 256) {
-    const int c8 = static_cast<int>(i % C8);
-    long pix = i / C8;
-    const int ox = static_cast<int>(pix % OW);
-    pix /= OW;
-    const int oy = static_cast<int>(pix % OH);
-    const int n = static_cast<int>(pix / OH);
+  const IDX total = static_cast<IDX>(N) * OH * OW * C8;
+  for (IDX i = static_cast<IDX>(blockIdx.x) * 256 + threadIdx.x; i < total; i += static_cast<IDX>(gridDim.x) * 256) {
+    const IDX pix0 = i / C8;
+    const int c8 = static_cast<int>(i - pix0 * C8);
+    const IDX pix1 = pix0 / OW;
+    const int ox = static_cast<int>(pix0 - pix1 * OW);
+    const int n = static_cast<int>(pix1 / OH);
+    const int oy = static_cast<int>(pix1 - static_cast<IDX>(n) * OH);
     const float sy = fmaxf((oy + 0.5f) * 0.5f - 0.5f, 0.f), sx = fmaxf((ox + 0.5f) * 0.5f - 0.5f, 0.f);
     const int y0 = static_cast<int>(sy), x0 = static_cast<int>(sx);
     const int y1 = min(y0 + 1, H - 1), x1 = min(x0 + 1, W - 1);
@@ -215,7 +217,12 @@ AI4E_API int ai4e_upsample2x_bilinear(const void* x, void* y, int N, int H, int 
                                       hipStream_t s) {
   (void)unused;
   if (C % 8 || ldy % 8 || ycoff % 8) return AI4E_EINVAL;
-  hipLaunchKernelGGL(upsample2x_kernel, dim3(grid_for(static_cast<long>(N) * 4 * H * W * (C / 8))), dim3(256), 0, s,
-                     static_cast<const uint16_t*>(x), static_cast<uint16_t*>(y), N, H, W, C, ldy, ycoff);
+  const long total = static_cast<long>(N) * 4 * H * W * (C / 8);
+  if (total < (1L << 31) - 8192L * 256)
+    hipLaunchKernelGGL(upsample2x_kernel<int>, dim3(grid_for(total)), dim3(256), 0, s, static_cast<const uint16_t*>(x),
+                       static_cast<uint16_t*>(y), N, H, W, C, ldy, ycoff);
+  else
+    hipLaunchKernelGGL(upsample2x_kernel<long>, dim3(grid_for(total)), dim3(256), 0, s, static_cast<const uint16_t*>(x),
+                       static_cast<uint16_t*>(y), N, H, W, C, ldy, ycoff);
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
 }

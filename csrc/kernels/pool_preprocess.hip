@@ -63,18 +63,20 @@ __global__ __launch_bounds__(256) void preprocess_s2d_kernel(const uint8_t* __re
 }
 
 // Max pool NHWC bf16; one lane = 8 channels of one output pixel. Padding ignored (= -inf).
+// IDX = int when the element count fits (32-bit index math: the 64-bit div/mod chain cost more than the loads)
+template <typename IDX>
 __global__ __launch_bounds__(256) void maxpool_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y, int N,
                                                       int H, int W, int C, int OH, int OW, int k, int s, int pad,
                                                       int ldx8) {
   const int C8 = C >> 3;
-  const long total = static_cast<long>(N) * OH * OW * C8;
-  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += static_cast<long>(gridDim.x) * 256) {
-    const int c8 = static_cast<int>(i % C8);
-    long pix = i / C8;
-    const int ow = static_cast<int>(pix % OW);
-    pix /= OW;
-    const int oh = static_cast<int>(pix % OH);
-    const int n = static_cast<int>(pix / OH);
+  const IDX total = static_cast<IDX>(N) * OH * OW * C8;
+  for (IDX i = static_cast<IDX>(blockIdx.x) * 256 + threadIdx.x; i < total; i += static_cast<IDX>(gridDim.x) * 256) {
+    const IDX pix0 = i / C8;
+    const int c8 = static_cast<int>(i - pix0 * C8);
+    const IDX pix1 = pix0 / OW;
+    const int ow = static_cast<int>(pix0 - pix1 * OW);
+    const int n = static_cast<int>(pix1 / OH);
+    const int oh = static_cast<int>(pix1 - static_cast<IDX>(n) * OH);
     float m[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) m[j] = -INFINITY;
@@ -163,9 +165,13 @@ AI4E_API int ai4e_preprocess_s2d_u8(const void* in, void* out, int N, int H, int
 AI4E_API int ai4e_maxpool2d(const void* x, void* y, int N, int H, int W, int C, int OH, int OW, int k, int stride,
                             int pad, int ldx, hipStream_t s) {
   if (C % 8 || ldx % 8 || ldx < C) return AI4E_EINVAL;
-  hipLaunchKernelGGL(maxpool_kernel, dim3(grid_for(static_cast<long>(N) * OH * OW * (C / 8))), dim3(256), 0, s,
-                     static_cast<const uint16_t*>(x), static_cast<uint16_t*>(y), N, H, W, C, OH, OW, k, stride, pad,
-                     ldx / 8);
+  const long total = static_cast<long>(N) * OH * OW * (C / 8);
+  if (total < (1L << 31) - 8192L * 256)
+    hipLaunchKernelGGL(maxpool_kernel<int>, dim3(grid_for(total)), dim3(256), 0, s, static_cast<const uint16_t*>(x),
+                       static_cast<uint16_t*>(y), N, H, W, C, OH, OW, k, stride, pad, ldx / 8);
+  else
+    hipLaunchKernelGGL(maxpool_kernel<long>, dim3(grid_for(total)), dim3(256), 0, s, static_cast<const uint16_t*>(x),
+                       static_cast<uint16_t*>(y), N, H, W, C, OH, OW, k, stride, pad, ldx / 8);
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
 }
 
