@@ -27,14 +27,24 @@ __global__ __launch_bounds__(256) void gn_stats_kernel(const uint16_t* __restric
   float s[8] = {0, 0, 0, 0, 0, 0, 0, 0}, q[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   const int pbeg = chunk * GN_PIX_PER_BLOCK, pend = min(HW, pbeg + GN_PIX_PER_BLOCK);
   if (p0 < pix_per_iter) {
-    for (int p = pbeg + p0; p < pend; p += pix_per_iter) {
-      const uint4 v = *reinterpret_cast<const uint4*>(x + (static_cast<long>(n) * HW + p) * ldx + xcoff + 8 * c8);
+    const uint16_t* const xb = x + static_cast<long>(n) * HW * ldx + xcoff + 8 * c8;
+    auto acc = [&](const uint4& v) __attribute__((always_inline)) {
       float a, b;
       unpack_bf16x2(v.x, a, b); s[0] += a; q[0] += a * a; s[1] += b; q[1] += b * b;
       unpack_bf16x2(v.y, a, b); s[2] += a; q[2] += a * a; s[3] += b; q[3] += b * b;
       unpack_bf16x2(v.z, a, b); s[4] += a; q[4] += a * a; s[5] += b; q[5] += b * b;
       unpack_bf16x2(v.w, a, b); s[6] += a; q[6] += a * a; s[7] += b; q[7] += b * b;
+    };
+    int p = pbeg + p0;
+    // four independent 16-B loads in flight per lane, then the accumulation
+    for (; p + 3 * pix_per_iter < pend; p += 4 * pix_per_iter) {
+      uint4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const uint4*>(xb + static_cast<long>(p + u * pix_per_iter) * ldx);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc(v[u]);
     }
+    for (; p < pend; p += pix_per_iter) acc(*reinterpret_cast<const uint4*>(xb + static_cast<long>(p) * ldx));
   }
   // reduce each lane's 8 channels into its group(s), then across lanes holding the same group
   __shared__ float gs[64], gq[64];
