@@ -158,6 +158,9 @@ class FusedResNet:
         # uint8 preprocess fused into the stem kernel (AI4E_STEM_U8=1); off by default: measured 0.1 ms slower
         # per batch of 256 than the separate K7 preprocess + K1s (byte gathers serialize with the conv)
         self.stem_u8 = os.environ.get("AI4E_STEM_U8", "0") not in ("0", "off", "")
+        # classifier FC through hipBLASLt (AI4E_FC_BLAS=0: the K1 conv kernel)
+        self.fc_blas = os.environ.get("AI4E_FC_BLAS", "1") not in ("0", "off", "")
+        self._fc_lin = None
         # chained micro-batching (AI4E_RESNET_CHAIN_MB=mb:nstages): stem + the first nstages run mb images at a time
         cmb = os.environ.get("AI4E_RESNET_CHAIN_MB", "")
         self.chain_mb: Optional[Tuple[int, int]] = tuple(int(v) for v in cmb.split(":")) if ":" in cmb else None
@@ -335,6 +338,14 @@ class FusedResNet:
     def logits(self, x: torch.Tensor, preprocess=None) -> torch.Tensor:
         """bf16 logits [N, classes]."""
         f = global_avgpool_nhwc(self.forward_features(x, preprocess))
+        if self.fc_blas and f.is_cuda:
+            # [N, 2048] x [2048, classes]: a plain library GEMM (hipBLASLt picks split-K); the K1 tile grid
+            # has only 16 workgroups at N = 256
+            if self._fc_lin is None:
+                k = self.fc.cin_pad
+                self._fc_lin = (self.fc.w_packed[:self.fc.cout, :k].contiguous(),
+                                self.fc.bias[:self.fc.cout].to(torch.bfloat16))
+            return F.linear(f.reshape(f.shape[0], -1), *self._fc_lin)
         return conv2d_nhwc(f, self.fc).reshape(f.shape[0], -1)
 
     def forward(self, x: torch.Tensor, preprocess=None) -> torch.Tensor:

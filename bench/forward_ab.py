@@ -24,6 +24,7 @@ def apply(m, variant):
     _TILES0 = dict(convmod._TILES) if _TILES0 is None else _TILES0
     convmod._TILES = dict(_TILES0)
     m.chain_mb = None
+    m.fc_blas = True
     for kv in variant.split(","):
         if kv == "base":
             continue
@@ -34,6 +35,8 @@ def apply(m, variant):
             convmod._TILES[k[2:]] = int(v)
         elif k == "mb":  # chained micro-batching mb:nstages (0 = off)
             m.chain_mb = tuple(int(t) for t in v.split(":")) if ":" in v else None
+        elif k == "fcblas":
+            m.fc_blas = v == "1"
         elif k == "stemu8":
             m.stem_u8 = v == "1"
         elif k.startswith("chain"):
