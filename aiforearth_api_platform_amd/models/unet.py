@@ -22,7 +22,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ..ops.conv import PackedConv, conv2d_nhwc, pack_conv
+from ..ops.conv import PackedConv, conv2d_gn_nhwc, conv2d_nhwc, pack_conv
 from ..ops.norm import group_norm_nhwc, upsample2x_nhwc
 from ..ops.pool import maxpool2d_nhwc, preprocess_u8
 
@@ -96,10 +96,12 @@ class _FusedDouble:
         self.g2 = (dc.n2.weight.data.float().to(device), dc.n2.bias.data.float().to(device), dc.n2.num_groups)
 
     def __call__(self, x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-        y = conv2d_nhwc(x, self.c1)
-        y = group_norm_nhwc(y, *self.g1[:2], groups=self.g1[2], relu=True, out=y)
-        z = conv2d_nhwc(y, self.c2)
-        return group_norm_nhwc(z, *self.g2[:2], groups=self.g2[2], relu=True, out=out if out is not None else z)
+        # GroupNorm statistics come out of the conv epilogues (conv2d_gn_nhwc) where the tile allows
+        y, st = conv2d_gn_nhwc(x, self.c1, self.g1[2])
+        y = group_norm_nhwc(y, *self.g1[:2], groups=self.g1[2], relu=True, out=y, stats=st)
+        z, st = conv2d_gn_nhwc(y, self.c2, self.g2[2])
+        return group_norm_nhwc(z, *self.g2[:2], groups=self.g2[2], relu=True, out=out if out is not None else z,
+                               stats=st)
 
 
 class FusedUNet:

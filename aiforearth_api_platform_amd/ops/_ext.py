@@ -25,6 +25,7 @@ _c_int, _c_long, _c_float, _vp = ctypes.c_int, ctypes.c_long, ctypes.c_float, ct
 # name -> argtypes (all return int status)
 _SIGS = {
     "ai4e_conv2d_fwd": [_vp, _vp, _vp, _vp, _vp] + [_c_int] * 19 + [_vp],
+    "ai4e_conv2d_gn_fwd": [_vp, _vp, _vp, _vp, _vp] + [_c_int] * 19 + [_vp, _c_int, _vp],
     "ai4e_conv_chain_fwd": [_vp] * 10 + [_c_int] * 11 + [_vp, _c_int, _vp],
     "ai4e_stem_pool_fwd": [_vp] * 4 + [_c_int] * 5 + [_vp],
     "ai4e_stem_pool_u8_fwd": [_vp] * 4 + [_c_int] * 5 + [_vp, _vp, _c_float, _vp],
@@ -35,6 +36,8 @@ _SIGS = {
     "ai4e_global_avgpool": [_vp, _vp, _c_int, _c_int, _c_int, _vp],
     "ai4e_groupnorm_nhwc": [_vp, _vp, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_float, _c_int, _c_int,
                             _c_int, _vp],
+    "ai4e_groupnorm_apply_nhwc": [_vp, _vp, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_float, _c_int, _c_int,
+                                  _c_int, _c_int, _vp],
     "ai4e_upsample2x_bilinear": [_vp, _vp] + [_c_int] * 7 + [_vp],
     "ai4e_nms_mask": [_vp, _c_int, _c_int, _c_float, _vp, _vp],
     "ai4e_nms_reduce": [_vp, _vp, _c_int, _c_int, _c_int, _vp, _vp, _vp],

@@ -134,7 +134,7 @@ def conv2d_nhwc(x: torch.Tensor, pc: PackedConv, residual: Optional[torch.Tensor
     return out
 
 
-def _conv_hip(x, pc, residual, relu, out, out_coff, tile_cfg, residual_up2=False):
+def _conv_hip(x, pc, residual, relu, out, out_coff, tile_cfg, residual_up2=False, gn=None):
     n, h, w, c = x.shape
     oh, ow = pc.out_hw(h, w)
     if x.dtype != torch.bfloat16 or out.dtype != torch.bfloat16:
@@ -154,10 +154,39 @@ def _conv_hip(x, pc, residual, relu, out, out_coff, tile_cfg, residual_up2=False
         if residual.shape != rshape or not residual.is_contiguous() or (residual_up2 and (oh % 2 or ow % 2)):
             raise ValueError(f"residual must be contiguous {list(rshape)}")
         ldres = pc.cout
-    _ext.call("ai4e_conv2d_fwd", base + 2 * (xoff - xoff % ldx), pc.w_packed.data_ptr(), pc.bias.data_ptr(),
-              _ext.ptr(residual), out.data_ptr(), n, h, w, c, ldx, xoff % ldx, pc.kh, pc.kw, pc.stride, pc.pad,
-              oh, ow, pc.cout, pc.kpad, ldy, out_coff, ldres, int(relu) | (2 if residual_up2 else 0), tile_cfg,
-              _ext.stream_ptr(x.device))
+    args = (base + 2 * (xoff - xoff % ldx), pc.w_packed.data_ptr(), pc.bias.data_ptr(), _ext.ptr(residual),
+            out.data_ptr(), n, h, w, c, ldx, xoff % ldx, pc.kh, pc.kw, pc.stride, pc.pad, oh, ow, pc.cout, pc.kpad, ldy,
+            out_coff, ldres, int(relu) | (2 if residual_up2 else 0), tile_cfg)
+    if gn is None:
+        _ext.call("ai4e_conv2d_fwd", *args, _ext.stream_ptr(x.device))
+    else:
+        _ext.call("ai4e_conv2d_gn_fwd", *args, gn[0].data_ptr(), gn[1], _ext.stream_ptr(x.device))
+
+
+def conv2d_gn_nhwc(x: torch.Tensor, pc: PackedConv, groups: int, out: Optional[torch.Tensor] = None,
+                   out_coff: int = 0):
+    """``conv2d_nhwc(x, pc)`` that also produces the GroupNorm statistics of its output from the same epilogue
+    (per image, tile-row chunk and group: sum and sum of squares of the stored bf16 values), so the norm that
+    follows skips its statistics pass over the tensor. Returns ``(y, stats)``; ``stats`` = ``(partials,
+    nchunks)`` for ``group_norm_nhwc(..., stats=stats)``, or ``None`` when the shape or the tuned tile cannot
+    fuse (then the norm computes its own statistics)."""
+    n, h, w, c = x.shape
+    oh, ow = pc.out_hw(h, w)
+    cfg = tuned_tile(pc, n, h, w, False) or (2 if pc.cout <= 64 else 1)
+    bm, bn = (256, 64) if cfg in (2, 5) else (128, 128)
+    ok = (_ext.backend_for(x) == "hip" and cfg in (1, 2, 4, 5) and groups > 0 and pc.cout % groups == 0
+          and (oh * ow) % bm == 0 and pc.cout % 8 == 0 and bn % (pc.cout // groups) == 0 and out_coff % 8 == 0
+          and (out is None or out.stride(2) % 8 == 0) and x.dtype == torch.bfloat16 and c == pc.cin_pad)
+    if not ok:
+        return conv2d_nhwc(x, pc, out=out, out_coff=out_coff), None
+    if out is None:
+        out = torch.empty(n, oh, ow, pc.cout, device=x.device, dtype=x.dtype)
+        out_coff = 0
+    nchunks = oh * ow // bm
+    # chunk sums, then room for the per-channel affine the norm's finalize launch writes
+    partials = torch.empty(n * nchunks * groups * 2 + n * pc.cout * 2, device=x.device, dtype=torch.float32)
+    _conv_hip(x, pc, None, False, out, out_coff, cfg, gn=(partials, groups))
+    return out, (partials, nchunks)
 
 
 def chain_kernel_builds(mid: int, midn: int = 0) -> bool:

@@ -25,13 +25,23 @@ def _base_ptr(t: torch.Tensor) -> int:
 
 
 def group_norm_nhwc(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, groups: int = 32, eps: float = 1e-5,
-                    relu: bool = False, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                    relu: bool = False, out: Optional[torch.Tensor] = None, stats=None) -> torch.Tensor:
+    """``stats``: ``(partials, nchunks)`` from ``conv2d_gn_nhwc`` (the producing conv's epilogue already summed
+    the groups), which skips the statistics pass."""
     n, h, w, c = x.shape
     if out is None:
         out = torch.empty(n, h, w, c, device=x.device, dtype=x.dtype)
     if _ext.backend_for(x) == "hip":
         ldx, xcoff = _nhwc_ld(x)
         ldy, ycoff = _nhwc_ld(out)
+        if stats is not None:
+            partials, nchunks = stats
+            g32 = gamma.to(x.device, torch.float32).contiguous()
+            b32 = beta.to(x.device, torch.float32).contiguous()
+            _ext.call("ai4e_groupnorm_apply_nhwc", _base_ptr(x), _base_ptr(out), g32.data_ptr(), b32.data_ptr(),
+                      partials.data_ptr(), n, h * w, c, groups, eps, int(relu), ldx | (ldy << 16),
+                      xcoff | (ycoff << 16), nchunks, _ext.stream_ptr(x.device))
+            return out
         nchunks = (h * w + GN_PIX_PER_BLOCK - 1) // GN_PIX_PER_BLOCK
         # chunk partials, then the per-channel affine (scale, shift) the finalize launch writes
         partials = torch.empty(n * nchunks * groups * 2 + n * c * 2, device=x.device, dtype=torch.float32)

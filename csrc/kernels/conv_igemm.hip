@@ -31,6 +31,8 @@
 //   by the preprocess kernel). The residual tile is prefetched into registers before the K loop.
 // * XCD-aware tile order: tiles that share an activation panel (same m-tile, different n-tiles)
 //   land on one XCD's L2 (common.h xcd_remap).
+#include <type_traits>
+
 #include "conv_common.h"
 
 namespace {
@@ -59,6 +61,10 @@ struct ConvParams {
   int M;
   int ntiles_n;
   const uint16_t* zero;  // >= 16 zero bytes: source of the DMA gather for padding taps
+  // GroupNorm statistics of the stored (bf16) output, fused into the EPI_LDS epilogue (null = off): per
+  // (image, BM-pixel chunk, group) sum and sum of squares -> gnp[((img * (OH*OW/BM) + chunk) * gn_groups + g) * 2]
+  float* gnp;
+  int gn_groups;
 };
 
 // Row of the residual tensor for output pixel m: m itself, or (relu flag bit 1) the pixel (oh/2, ow/2) of a
@@ -294,6 +300,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
     // ds_write_b128 groups (8 rows, one column) hit 8 different bank quads.
     static_assert(BM * BN * 4 <= STAGES * STAGE_ELEMS * 2, "epilogue tile must fit the stage ring");
     float* tile = reinterpret_cast<float*>(smem);
+    float gs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, gq[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     __builtin_amdgcn_s_barrier();  // all waves finished reading the last stage
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -314,6 +321,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
       const float4 v1 = *reinterpret_cast<const float4*>(tile + r * BN + 4 * ((2 * cq + 1) ^ (r & 7)));
       const float f[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
       const uint4 o = epilogue8_bf16(f, p.res != nullptr, rres16[e], (p.relu & 1) != 0);
+      if (p.gnp && m < p.M && n < p.Kout) {  // GN statistics of the values as stored (bf16)
+        const uint32_t ow[4] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          float a, b;
+          unpack_bf16x2(ow[q], a, b);
+          gs[2 * q] += a; gq[2 * q] += a * a;
+          gs[2 * q + 1] += b; gq[2 * q + 1] += b * b;
+        }
+      }
       if (m < p.M && n < p.Kout) {
         uint16_t* dst = p.y + static_cast<long>(m) * p.ldy + p.ycoff + n;
         if (n + 8 <= p.Kout) {
@@ -321,6 +338,62 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
         } else {
           *reinterpret_cast<uint2*>(dst) = make_uint2(o.x, o.y);  // Kout % 8 == 4 tail
         }
+      }
+    }
+    if (p.gnp) {
+      // (1) in-thread: fold this lane's 8 channels into their groups (cgm = min(channels per group, 8) adjacent
+      // channels per slot); (2) lanes sharing the 8-channel column (lane % CPR) reduce by xor shuffles; (3) the
+      // 4 waves and each group's slots meet in LDS (the staged tile is dead by then)
+      const int cg = p.Kout / p.gn_groups;
+      const int cgm = cg < 8 ? cg : 8;
+      auto reduce = [&](auto cgc) __attribute__((always_inline)) {
+        constexpr int CG = decltype(cgc)::value;
+#pragma unroll
+        for (int w = 1; w < CG; w <<= 1)
+#pragma unroll
+          for (int k = 0; k < 8; k += 2 * w) {
+            gs[k] += gs[k + w];
+            gq[k] += gq[k + w];
+          }
+#pragma unroll
+        for (int off = CPR; off < 64; off <<= 1)
+#pragma unroll
+          for (int k = 0; k < 8; k += CG) {
+            gs[k] += __shfl_xor(gs[k], off);
+            gq[k] += __shfl_xor(gq[k], off);
+          }
+      };
+      switch (cgm) {
+        case 1: reduce(std::integral_constant<int, 1>{}); break;
+        case 2: reduce(std::integral_constant<int, 2>{}); break;
+        case 4: reduce(std::integral_constant<int, 4>{}); break;
+        default: reduce(std::integral_constant<int, 8>{}); break;
+      }
+      __syncthreads();
+      float* red = tile;  // [4 waves][BN channel slots][2]; slot c holds channels c .. c + cgm - 1
+      if (lane < CPR) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          if (k % cgm == 0) {
+            red[(wave * BN + lane * 8 + k) * 2] = gs[k];
+            red[(wave * BN + lane * 8 + k) * 2 + 1] = gq[k];
+          }
+        }
+      }
+      __syncthreads();
+      const int ng = min(BN, p.Kout - n0) / cg;  // host: BN % cg == 0, Kout % cg == 0
+      if (tid < ng) {
+        float S = 0.f, Q = 0.f;
+        for (int w = 0; w < 4; ++w)
+          for (int c = 0; c < cg; c += cgm) {
+            S += red[(w * BN + tid * cg + c) * 2];
+            Q += red[(w * BN + tid * cg + c) * 2 + 1];
+          }
+        const int ohw = p.OH * p.OW;  // host: ohw % BM == 0, so a tile never straddles images
+        const int img = m0 / ohw, chunk = (m0 - img * ohw) / BM;
+        float* o = p.gnp + ((static_cast<long>(img) * (ohw / BM) + chunk) * p.gn_groups + n0 / cg + tid) * 2;
+        o[0] = S;
+        o[1] = Q;
       }
     }
   } else {
@@ -681,10 +754,10 @@ int launch256(const ConvParams& p0, hipStream_t s) {
 // ping-pong phases (needs C % 64 == 0, Kout % 8 == 0).
 // relu: bit 0 = ReLU; bit 1 = `res` is on the half-resolution grid [N, OH/2, OW/2, ldres] (nearest 2x
 // upsample of the residual, OH and OW even).
-AI4E_API int ai4e_conv2d_fwd(const void* x, const void* w, const void* bias, const void* res, void* y, int N, int H,
-                             int W, int C, int ldx, int xcoff, int KH, int KW, int stride, int pad, int OH, int OW,
-                             int Kout, int Kpad, int ldy, int ycoff, int ldres, int relu, int tile_cfg,
-                             hipStream_t stream) {
+namespace {
+int conv2d_impl(const void* x, const void* w, const void* bias, const void* res, void* y, int N, int H, int W, int C,
+                int ldx, int xcoff, int KH, int KW, int stride, int pad, int OH, int OW, int Kout, int Kpad, int ldy,
+                int ycoff, int ldres, int relu, int tile_cfg, float* gnp, int gn_groups, hipStream_t stream) {
   if (C % 8 || ldx % 8 || xcoff % 8 || Kpad % (2 * BK) || Kout % 4 || ldy % 4 || ycoff % 4 || (res && ldres % 4) ||
       Kpad < KH * KW * C)
     return AI4E_EINVAL;
@@ -701,6 +774,16 @@ AI4E_API int ai4e_conv2d_fwd(const void* x, const void* w, const void* bias, con
   if ((relu & 2) && (!res || (OH & 1) || (OW & 1))) return AI4E_EINVAL;  // half-resolution residual grid
   if (p.M <= 0) return AI4E_OK;
   if (tile_cfg == 0) tile_cfg = Kout <= 64 ? 2 : 1;
+  if (gnp) {
+    // fused GroupNorm statistics: 128-wide LDS-epilogue tiles only (configs 1, 2, 4, 5), whole groups per
+    // channel tile, tiles that never straddle images, full 16-B output rows
+    const int bm = (tile_cfg == 2 || tile_cfg == 5) ? 256 : 128, bn = (tile_cfg == 2 || tile_cfg == 5) ? 64 : 128;
+    if (tile_cfg == 3 || tile_cfg == 6 || gn_groups <= 0 || Kout % gn_groups || (OH * OW) % bm || Kout % 8 ||
+        ldy % 8 || ycoff % 8 || (res && ldres % 8) || bn % (Kout / gn_groups))
+      return AI4E_EINVAL;
+    p.gnp = gnp;
+    p.gn_groups = gn_groups;
+  }
   switch (tile_cfg) {
     case 1: return launch<2, 2, 4>(p, stream);
     case 2: return launch<4, 1, 4>(p, stream);
@@ -710,6 +793,29 @@ AI4E_API int ai4e_conv2d_fwd(const void* x, const void* w, const void* bias, con
     case 6: return launch256(p, stream);
     default: return AI4E_EINVAL;
   }
+}
+
+}  // namespace
+
+AI4E_API int ai4e_conv2d_fwd(const void* x, const void* w, const void* bias, const void* res, void* y, int N, int H,
+                             int W, int C, int ldx, int xcoff, int KH, int KW, int stride, int pad, int OH, int OW,
+                             int Kout, int Kpad, int ldy, int ycoff, int ldres, int relu, int tile_cfg,
+                             hipStream_t stream) {
+  return conv2d_impl(x, w, bias, res, y, N, H, W, C, ldx, xcoff, KH, KW, stride, pad, OH, OW, Kout, Kpad, ldy, ycoff,
+                     ldres, relu, tile_cfg, nullptr, 0, stream);
+}
+
+// Same conv, plus the GroupNorm statistics of its output (gn_groups groups over Kout channels) written as
+// per-(image, tile-row chunk, group) partial sum / sum of squares into gn_partials
+// [N, OH*OW / BM, gn_groups, 2] fp32 (BM = 256 for tile configs 2 and 5, else 128). Configs 3 and 6 and
+// shapes whose tiles would straddle images are refused (EINVAL) before anything is launched.
+AI4E_API int ai4e_conv2d_gn_fwd(const void* x, const void* w, const void* bias, const void* res, void* y, int N,
+                                int H, int W, int C, int ldx, int xcoff, int KH, int KW, int stride, int pad, int OH,
+                                int OW, int Kout, int Kpad, int ldy, int ycoff, int ldres, int relu, int tile_cfg,
+                                void* gn_partials, int gn_groups, hipStream_t stream) {
+  if (!gn_partials) return AI4E_EINVAL;
+  return conv2d_impl(x, w, bias, res, y, N, H, W, C, ldx, xcoff, KH, KW, stride, pad, OH, OW, Kout, Kpad, ldy, ycoff,
+                     ldres, relu, tile_cfg, static_cast<float*>(gn_partials), gn_groups, stream);
 }
 
 // Weight rows must be padded to this multiple (tile height in the channel dimension).

@@ -77,31 +77,39 @@ __global__ __launch_bounds__(256) void gn_finalize_kernel(const float* __restric
                                                           const float* __restrict__ beta, float2* __restrict__ ss,
                                                           int HW, int C, int G, float eps, int nchunks) {
   const int n = blockIdx.x;
-  constexpr int LPG = 4;  // lanes per group (G <= 64)
+  // thread t owns group t % G and every (256/G)-th chunk from t / G: each iteration the block reads one
+  // contiguous 2 KB run of (chunk, group) float2 partials; two fp64 accumulator pairs per thread
   __shared__ double red_s[256], red_q[256];
   __shared__ float mean_s[64], rstd_s[64];
-  const int g = threadIdx.x / LPG, l = threadIdx.x % LPG;
-  double s = 0, q = 0;
-  if (g < G) {
-    for (int k = l; k < nchunks; k += LPG) {
-      const float* o = partials + ((static_cast<long>(n) * nchunks + k) * G + g) * 2;
-      s += o[0];
-      q += o[1];
+  const int lpg = 256 / G;  // threads per group (G <= 64 divides 256 only when a power of two; else some idle)
+  const int g = threadIdx.x % G, l = threadIdx.x / G;
+  double s0 = 0, q0 = 0, s1 = 0, q1 = 0;
+  if (l < lpg) {
+    const float2* pp = reinterpret_cast<const float2*>(partials) + static_cast<long>(n) * nchunks * G + g;
+    int k = l;
+    for (; k + lpg < nchunks; k += 2 * lpg) {
+      const float2 a = pp[static_cast<long>(k) * G], b = pp[static_cast<long>(k + lpg) * G];
+      s0 += a.x; q0 += a.y; s1 += b.x; q1 += b.y;
+    }
+    if (k < nchunks) {
+      const float2 a = pp[static_cast<long>(k) * G];
+      s0 += a.x; q0 += a.y;
     }
   }
-  red_s[threadIdx.x] = s;
-  red_q[threadIdx.x] = q;
+  red_s[threadIdx.x] = s0 + s1;
+  red_q[threadIdx.x] = q0 + q1;
   __syncthreads();
-  if (l == 0 && g < G) {
-    for (int k = 1; k < LPG; ++k) {
-      s += red_s[threadIdx.x + k];
-      q += red_q[threadIdx.x + k];
+  if (threadIdx.x < G) {
+    double s = 0, q = 0;
+    for (int k = 0; k < lpg; ++k) {
+      s += red_s[k * G + threadIdx.x];
+      q += red_q[k * G + threadIdx.x];
     }
     const double cnt = static_cast<double>(HW) * (C / G);
     const double mean = s / cnt;
     const double var = fmax(q / cnt - mean * mean, 0.0);
-    mean_s[g] = static_cast<float>(mean);
-    rstd_s[g] = static_cast<float>(1.0 / sqrt(var + eps));
+    mean_s[threadIdx.x] = static_cast<float>(mean);
+    rstd_s[threadIdx.x] = static_cast<float>(1.0 / sqrt(var + eps));
   }
   __syncthreads();
   const int cg = C / G;
@@ -217,6 +225,26 @@ AI4E_API int ai4e_groupnorm_nhwc(const void* x, void* y, const void* gamma, cons
   hipLaunchKernelGGL(gn_finalize_kernel, dim3(N), dim3(256), 0, s, static_cast<const float*>(partials),
                      static_cast<const float*>(gamma), static_cast<const float*>(beta), ss, HW, C, G, eps, nchunks);
   // ~4 vectors per lane; at most 8192 workgroups per image
+  const int gx = grid_for(static_cast<long>(HW) * (C / 8) / 4 + 1);
+  hipLaunchKernelGGL(gn_apply_kernel, dim3(gx, N), dim3(256), 0, s, static_cast<const uint16_t*>(x),
+                     static_cast<uint16_t*>(y), ss, HW, C, relu, ldx, xcoff, ldy, ycoff);
+  return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
+}
+
+// GroupNorm when the statistics were already produced (e.g. by the conv epilogue, ai4e_conv2d_gn_fwd):
+// partials [N, nchunks, G, 2] chunk sums, followed by room for the per-channel affine (N * C * 2 floats).
+AI4E_API int ai4e_groupnorm_apply_nhwc(const void* x, void* y, const void* gamma, const void* beta, void* partials,
+                                       int N, int HW, int C, int G, float eps, int relu, int ldx_ldy_pack,
+                                       int coff_pack, int nchunks, hipStream_t s) {
+  const int ldx = ldx_ldy_pack & 0xffff, ldy = (ldx_ldy_pack >> 16) & 0xffff;
+  const int xcoff = coff_pack & 0xffff, ycoff = (coff_pack >> 16) & 0xffff;
+  if (C % 8 || G > 64 || C % G || (C / 8) > 256 || 256 % (C / 8) || ldx % 8 || ldy % 8 || xcoff % 8 || ycoff % 8 ||
+      nchunks <= 0)
+    return AI4E_EINVAL;
+  if (static_cast<long>(HW) * (C / 8) >= (1L << 31) - 8192L * 256) return AI4E_EINVAL;
+  float2* ss = reinterpret_cast<float2*>(static_cast<float*>(partials) + static_cast<long>(N) * nchunks * G * 2);
+  hipLaunchKernelGGL(gn_finalize_kernel, dim3(N), dim3(256), 0, s, static_cast<const float*>(partials),
+                     static_cast<const float*>(gamma), static_cast<const float*>(beta), ss, HW, C, G, eps, nchunks);
   const int gx = grid_for(static_cast<long>(HW) * (C / 8) / 4 + 1);
   hipLaunchKernelGGL(gn_apply_kernel, dim3(gx, N), dim3(256), 0, s, static_cast<const uint16_t*>(x),
                      static_cast<uint16_t*>(y), ss, HW, C, relu, ldx, xcoff, ldy, ycoff);
