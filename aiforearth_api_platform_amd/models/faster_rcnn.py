@@ -15,13 +15,14 @@ Weights are random-init (no checkpoint offline); classes = background + animal, 
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
 import torch.nn as nn
 
-from ..ops.conv import PackedConv, conv2d_nhwc, pack_conv
+from ..ops.conv import PackedConv, conv2d_nhwc, linear_nhwc, pack_conv
 from ..ops.detection import det_decode, nms_batched_sorted, roi_align_fpn, rpn_decode_into
 from ..ops.pool import maxpool2d_nhwc, preprocess_s2d_u8, preprocess_u8
 from .resnet import FusedResNet, resnet50
@@ -88,6 +89,7 @@ class FasterRCNN:
         wp[nc: nc + 4 * nc] = torch.randn(4 * nc, rep, 1, 1, generator=g) * 0.001
         self.predictor = pack_conv(wp, torch.zeros(pred_out)).to(d)
         self._anchor_cache: Dict[Tuple, List[torch.Tensor]] = {}
+        self.fc_blas = os.environ.get("AI4E_DET_FC_BLAS", "1") not in ("0", "off", "")
 
     # ------------------------------------------------------------------ backbone + FPN
     def backbone_stages(self, x: torch.Tensor) -> List[torch.Tensor]:
@@ -168,8 +170,9 @@ class FasterRCNN:
         strides = [img_hw[0] // p.shape[1] for p in P[:4]]
         feats = roi_align_fpn(P[:4], [1.0 / s for s in strides], rois, (7, 7), 2)  # [B*R, 7, 7, C]
         x = feats.reshape(B * R, 1, 1, -1)
-        x = conv2d_nhwc(x, self.fc6, relu=True)
-        x = conv2d_nhwc(x, self.fc7, relu=True)
+        fc = linear_nhwc if self.fc_blas else conv2d_nhwc  # FCs as library GEMMs (AI4E_DET_FC_BLAS=0: K1)
+        x = fc(x, self.fc6, relu=True)
+        x = fc(x, self.fc7, relu=True)
         # [B, R, >= 5 nc]: nc class logits, then 4 nc box deltas
         return conv2d_nhwc(x, self.predictor).reshape(B, R, -1)
 

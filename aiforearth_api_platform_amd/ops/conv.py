@@ -189,6 +189,23 @@ def conv2d_gn_nhwc(x: torch.Tensor, pc: PackedConv, groups: int, out: Optional[t
     return out, (partials, nchunks)
 
 
+def linear_nhwc(x: torch.Tensor, pc: PackedConv, relu: bool = False) -> torch.Tensor:
+    """A 1x1 conv on [M, 1, 1, C] rows (a fully connected layer) as a plain library GEMM (hipBLASLt via
+    ``F.linear``) on the GPU: large-K FCs (the detector's box head, K = 12544) where the library's split-K /
+    stream-K tilings beat K1's fixed tile grid. Returns [M, 1, 1, Cout] bf16; other backends use K1."""
+    if not (x.is_cuda and _ext.backend_for(x) == "hip" and x.dtype == torch.bfloat16 and pc.kh == 1 and pc.kw == 1
+            and x.shape[1] == 1 and x.shape[2] == 1 and x.shape[-1] == pc.cin_pad):
+        return conv2d_nhwc(x, pc, relu=relu)
+    lin = getattr(pc, "_linear", None)
+    if lin is None:
+        lin = (pc.w_packed[:pc.cout, :pc.cin_pad].contiguous(), pc.bias[:pc.cout].to(torch.bfloat16))
+        pc._linear = lin
+    y = F.linear(x.reshape(x.shape[0], -1), *lin)
+    if relu:
+        y = torch.relu_(y)
+    return y.reshape(x.shape[0], 1, 1, pc.cout)
+
+
 def chain_kernel_builds(mid: int, midn: int = 0) -> bool:
     """Shapes the fused bottleneck-chain kernel K1c is built for (csrc/kernels/conv_chain.hip); ``midn`` is
     the chained 1x1's output width (0 = no chained 1x1)."""
