@@ -18,6 +18,8 @@ from typing import Optional
 import torch
 
 _LIB_PATH = Path(__file__).resolve().parent.parent / "_lib" / "libai4e_kernels.so"
+if os.environ.get("AI4E_KERNEL_LIB"):  # A/B of two builds of the kernel library on one GPU box
+    _LIB_PATH = Path(os.environ["AI4E_KERNEL_LIB"])
 _lib: Optional[ctypes.CDLL] = None
 
 _c_int, _c_long, _c_float, _vp = ctypes.c_int, ctypes.c_long, ctypes.c_float, ctypes.c_void_p
