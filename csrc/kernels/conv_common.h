@@ -14,16 +14,19 @@ __device__ __forceinline__ int swz(int row) { return (0x78 >> (2 * ((row >> 2) &
 // One 16-B LDS-DMA per lane: global -> LDS at (wave-uniform M0 base + 16*lane). Inline asm so hipcc
 // neither drains it with vmcnt(0) before every ds_read nor at barriers (cdna guide §5.7); completion is
 // tracked by hand with counted vmcnt. The swizzle is applied to the per-lane SOURCE address.
-// M0 is declared clobbered (instead of saved and restored around the DMA): hipcc re-materializes M0 itself
-// if it ever holds something live, and the DMA costs 2 SALU instead of 4.
+// M0 is saved and restored around the DMA: hipcc treats M0 as a reserved register and ignores it in a clobber
+// list (-Winline-asm), so a live M0 of its own (s_movrel indexing) would otherwise be corrupted silently.
 __device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_base) {
+  uint32_t keep;
   asm volatile(
-      "s_mov_b32 m0, %1\n\t"
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
       "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %0, off"
-      :
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
       : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(lds_base))
-      : "memory", "m0");
+      : "memory");
 }
 
 template <int N>

@@ -647,7 +647,6 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
   // ---- epilogue, one pixel group at a time: fp32 [128][256] tile in LDS (16-B chunk index
   //      XOR (row & 7)), then every thread handles 16-B output chunks: + bias (+ residual), ReLU.
   float* tile = reinterpret_cast<float*>(smem);
-  const float lo = (p.relu & 1) ? 0.f : -INFINITY;
 #pragma unroll
   for (int pass = 0; pass < 2; ++pass) {
     if (wr == pass) {

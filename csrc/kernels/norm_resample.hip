@@ -62,7 +62,7 @@ __global__ __launch_bounds__(256) void gn_stats_kernel(const uint16_t* __restric
     }
   }
   __syncthreads();
-  if (threadIdx.x < G) {
+  if (static_cast<int>(threadIdx.x) < G) {
     float* o = partials + ((static_cast<long>(n) * nchunks + chunk) * G + threadIdx.x) * 2;
     o[0] = gs[threadIdx.x];
     o[1] = gq[threadIdx.x];
@@ -99,7 +99,7 @@ __global__ __launch_bounds__(256) void gn_finalize_kernel(const float* __restric
   red_s[threadIdx.x] = s0 + s1;
   red_q[threadIdx.x] = q0 + q1;
   __syncthreads();
-  if (threadIdx.x < G) {
+  if (static_cast<int>(threadIdx.x) < G) {
     double s = 0, q = 0;
     for (int k = 0; k < lpg; ++k) {
       s += red_s[k * G + threadIdx.x];

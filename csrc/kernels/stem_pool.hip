@@ -342,7 +342,8 @@ int launch_direct(const StemParams& p, long nb, hipStream_t stream) {
     attr = true;
   }
   int dev = 0, cus = 256;
-  if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    cus = 256;
   const long grid = nb < 2L * cus ? nb : 2L * cus;  // two persistent workgroups per CU
   hipLaunchKernelGGL(stem_pool_direct_kernel<U8>, dim3(static_cast<unsigned>(grid)), dim3(256), D_LDS, stream, p,
                      static_cast<int>(nb));
