@@ -121,6 +121,10 @@ def conv2d_nhwc(x: torch.Tensor, pc: PackedConv, residual: Optional[torch.Tensor
     if c != pc.cin_pad:
         raise ValueError(f"conv expects C={pc.cin_pad} (padded), got {c}")
     oh, ow = pc.out_hw(h, w)
+    if (out is None and residual is None and BLAS_1X1 and pc.kh == 1 and pc.kw == 1 and pc.stride == 1 and pc.pad == 0
+            and pc.cin_pad >= 512 and pc.cout >= 256 and x.is_contiguous() and tile_cfg <= 0
+            and _ext.backend_for(x) == "hip" and x.dtype == torch.bfloat16):
+        return _pointwise_blas(x, pc, relu)
     if out is None:
         out = torch.empty(n, oh, ow, pc.cout, device=x.device, dtype=x.dtype)
         out_coff = 0
@@ -132,6 +136,24 @@ def conv2d_nhwc(x: torch.Tensor, pc: PackedConv, residual: Optional[torch.Tensor
         y = _conv_torch(x, pc, residual, relu)
         out[..., out_coff:out_coff + pc.cout] = y.to(out.dtype)
     return out
+
+
+# Wide-K pointwise convs without a residual (ResNet layer3/4 c1: 512/1024/2048 -> 256/512) as hipBLASLt GEMMs with
+# the bias + ReLU epilogue (AI4E_BLAS_1X1=1). In isolation they are 7-14 us faster per launch than K1 at batch
+# 256 (bench/blas_vs_k1.py), but inside the captured ResNet forward the A/B is flat (3.797 vs 3.797 ms), so K1
+# stays the default; the residual convs never route (K1's fused residual epilogue beats addmm + ReLU).
+BLAS_1X1 = os.environ.get("AI4E_BLAS_1X1", "0") not in ("0", "off", "")
+
+
+def _pointwise_blas(x, pc, relu):
+    n, h, w, c = x.shape
+    lin = getattr(pc, "_linear", None)
+    if lin is None:
+        lin = (pc.w_packed[:pc.cout, :pc.cin_pad].contiguous(), pc.bias[:pc.cout].to(torch.bfloat16))
+        pc._linear = lin
+    x2 = x.reshape(-1, c)
+    y = torch._addmm_activation(lin[1], x2, lin[0].t()) if relu else torch.addmm(lin[1], x2, lin[0].t())
+    return y.reshape(n, h, w, pc.cout)
 
 
 def _conv_hip(x, pc, residual, relu, out, out_coff, tile_cfg, residual_up2=False, gn=None):
@@ -196,14 +218,7 @@ def linear_nhwc(x: torch.Tensor, pc: PackedConv, relu: bool = False) -> torch.Te
     if not (x.is_cuda and _ext.backend_for(x) == "hip" and x.dtype == torch.bfloat16 and pc.kh == 1 and pc.kw == 1
             and x.shape[1] == 1 and x.shape[2] == 1 and x.shape[-1] == pc.cin_pad):
         return conv2d_nhwc(x, pc, relu=relu)
-    lin = getattr(pc, "_linear", None)
-    if lin is None:
-        lin = (pc.w_packed[:pc.cout, :pc.cin_pad].contiguous(), pc.bias[:pc.cout].to(torch.bfloat16))
-        pc._linear = lin
-    y = F.linear(x.reshape(x.shape[0], -1), *lin)
-    if relu:
-        y = torch.relu_(y)
-    return y.reshape(x.shape[0], 1, 1, pc.cout)
+    return _pointwise_blas(x.contiguous(), pc, relu)
 
 
 def chain_kernel_builds(mid: int, midn: int = 0) -> bool:

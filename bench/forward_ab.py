@@ -25,6 +25,7 @@ def apply(m, variant):
     convmod._TILES = dict(_TILES0)
     m.chain_mb = None
     m.fc_blas = True
+    convmod.BLAS_1X1 = False
     for kv in variant.split(","):
         if kv == "base":
             continue
@@ -35,6 +36,8 @@ def apply(m, variant):
             convmod._TILES[k[2:]] = int(v)
         elif k == "mb":  # chained micro-batching mb:nstages (0 = off)
             m.chain_mb = tuple(int(t) for t in v.split(":")) if ":" in v else None
+        elif k == "blas1x1":
+            convmod.BLAS_1X1 = v == "1"
         elif k == "fcblas":
             m.fc_blas = v == "1"
         elif k == "stemu8":
