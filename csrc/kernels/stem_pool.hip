@@ -179,7 +179,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
 // quads. The 64 x 256 weights (32 KB) stay in LDS for the whole persistent loop, each 512-B row with its
 // 16-B chunk index XOR (row & 31) so the 16 rows of a fragment read hit distinct bank quads.
 constexpr int FP_R = SP_RR + 3, FP_C = SP_RC + 3, FP_PIX = FP_R * FP_C;  // 18 x 20 footprint
-constexpr int FP_SLOTS = 2 * FP_PIX;                                    // 720 16-B slots (2 planes)
+// plane stride padded to a multiple of 16 slots (360 -> 368): a ds_read_b128 lane group {0-3, 12-15, 20-27}
+// reads lanes of both planes, and with a stride of 360 = 8 (mod 16) slots lanes 12-15 of plane 0 and 20-23 of
+// plane 1 hit the same bank quads (the 50 % LDS-conflict share in profiles/r1_pmc); at 368 the group's 16
+// chunks are distinct mod 16.
+constexpr int FP_STRIDE = (FP_PIX + 15) / 16 * 16;                      // 368
+constexpr int FP_SLOTS = 2 * FP_STRIDE;                                 // 736 16-B slots (2 planes + pad)
 constexpr int FP_DMA = (FP_SLOTS + 255) / 256;                          // DMA instrs per wave (3)
 constexpr int D_W = 0, D_FP = 64 * 512, D_TILE = D_FP + FP_DMA * 4 * 1024, D_LDS = D_TILE + SP_BM * 128;
 
@@ -244,20 +249,21 @@ void stem_pool_direct_kernel(const StemParams p, int ntiles) {
             }
         }
         uint4* d0 = reinterpret_cast<uint4*>(dsm + D_FP + pix * 16);
-        uint4* d1 = reinterpret_cast<uint4*>(dsm + D_FP + (FP_PIX + pix) * 16);
+        uint4* d1 = reinterpret_cast<uint4*>(dsm + D_FP + (FP_STRIDE + pix) * 16);
         *d0 = make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]), pack_bf16x2(v[6], v[7]));
         *d1 = make_uint4(pack_bf16x2(v[8], v[9]), pack_bf16x2(v[10], v[11]), pack_bf16x2(v[12], v[13]),
                          pack_bf16x2(v[14], v[15]));
       }
     } else {
-    // footprint DMA: slot s = plane * FP_PIX + pixel; footprint pixel (a, b) is input (oh0-1+a, ow0-1+b)
+    // footprint DMA: slot s = plane * FP_STRIDE + pixel (pixels >= FP_PIX are padding, zero-filled);
+    // footprint pixel (a, b) is input (oh0-1+a, ow0-1+b)
 #pragma unroll
     for (int q = 0; q < FP_DMA; ++q) {
       const int s = (wave + 4 * q) * 64 + lane;
-      const int h = s >= FP_PIX ? 1 : 0, pix = s - h * FP_PIX;
+      const int h = s >= FP_STRIDE ? 1 : 0, pix = s - h * FP_STRIDE;
       const int a = pix / FP_C, b = pix - a * FP_C;
       const int ih = oh0 - 1 + a, iw = ow0 - 1 + b;
-      const bool ok = s < FP_SLOTS && static_cast<unsigned>(ih) < static_cast<unsigned>(p.H) &&
+      const bool ok = s < FP_SLOTS && pix < FP_PIX && static_cast<unsigned>(ih) < static_cast<unsigned>(p.H) &&
                       static_cast<unsigned>(iw) < static_cast<unsigned>(p.W);
       glds16(ok ? static_cast<const void*>(xi + (static_cast<long>(ih) * p.W + iw) * SP_C + 8 * h) : p.zero,
              sb + D_FP + (wave + 4 * q) * 1024);
@@ -274,7 +280,7 @@ void stem_pool_direct_kernel(const StemParams p, int ntiles) {
 #pragma unroll
     for (int kt = 0; kt < SP_NK; ++kt) {
       const int kh = kt >> 1, kw = 2 * (kt & 1) + (g >> 1);
-      const int plane = (g & 1) * FP_PIX * 16;
+      const int plane = (g & 1) * FP_STRIDE * 16;
       bf16x8_t fw[4], fx[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
