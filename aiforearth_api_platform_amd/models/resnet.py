@@ -171,6 +171,15 @@ class FusedResNet:
                 self.stages.append([])
             self.stages[-1].append(blk)
 
+    def tensors(self) -> List[torch.Tensor]:
+        """Every weight tensor of the packed model (for ``parallel.dist.broadcast_tensors``: load on one rank,
+        replicate over xGMI). Call before the first forward: derived caches (folded downsample weights, the
+        library-GEMM FC views) are built lazily from these."""
+        out = []
+        for pc in self.layers():
+            out += [pc.w_packed, pc.bias, pc.w_ref, pc.b_ref]
+        return out
+
     def layers(self) -> List[PackedConv]:
         out = [self.stem]
         for c1, c2, c3, d in self.blocks:

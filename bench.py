@@ -64,7 +64,8 @@ def main():
     from aiforearth_api_platform_amd.runtime.serving import GpuBatchWorker
     from aiforearth_api_platform_amd.utils.metrics import percentile
 
-    from aiforearth_api_platform_amd.parallel.dist import all_reduce_max, destroy, env_ranks, init_from_env, sync
+    from aiforearth_api_platform_amd.parallel.dist import (all_reduce_max, broadcast_tensors, destroy, env_ranks,
+                                                           init_from_env, sync)
 
     _, world, _ = env_ranks()
     if world > 1 and args.gpus != world:
@@ -75,6 +76,8 @@ def main():
 
     B, S = args.batch, args.image_size
     model = FusedResNet(resnet50(seed=0), device=device)
+    if world > 1:  # weights as if loaded once on rank 0: one bucketed RCCL broadcast over xGMI (survey C1)
+        broadcast_tensors(model.tensors(), src=0)
     engine = InferenceEngine(model.forward_u8, (S, S, 3), B, device=device, use_graphs=not args.no_graphs,
                              head_fn=model.topk_u8)
     engine.warmup()
