@@ -39,6 +39,9 @@ class PipelineConfig:
     score_thresh: float = 0.5
     class_id: Optional[int] = 1    # MegaDetector "animal"; None = every class
     max_crops_per_image: int = 8
+    # dtype of the crops on the RCCL wire between detector and classifier GPUs (BASELINE config #5: fp16);
+    # the classifier computes in bf16 and converts on receipt. CPU ranks (gloo) keep fp32.
+    wire_dtype: str = "float16"
 
 
 def select_crops(dets, cfg: PipelineConfig) -> torch.Tensor:
@@ -77,7 +80,8 @@ class DetectClassifyPipeline:
         self.peer = self.rank + 1 if self.rank % 2 == 0 else self.rank - 1
         if self.world > 1 and self.peer >= self.world:
             raise ValueError("pipeline needs an even number of ranks (detector/classifier pairs)")
-        self.crop_dtype = torch.bfloat16 if device.type == "cuda" else torch.float32
+        self.crop_dtype = torch.bfloat16 if device.type == "cuda" else torch.float32  # classifier compute dtype
+        self.wire_dtype = getattr(torch, self.cfg.wire_dtype) if device.type == "cuda" else torch.float32
 
     # ------------------------------------------------------------ classifier stage
     def classify(self, crops: torch.Tensor) -> torch.Tensor:
@@ -97,10 +101,10 @@ class DetectClassifyPipeline:
             n = int(hdr.item())
             if n == STOP:
                 return total
-            crops = torch.empty(n, h, w, 8, dtype=self.crop_dtype, device=self.device)
+            crops = torch.empty(n, h, w, 8, dtype=self.wire_dtype, device=self.device)
             if n:
                 dist.recv(crops, self.peer, group=self.group)
-            res = self.classify(crops)
+            res = self.classify(crops.to(self.crop_dtype))
             if n:
                 dist.send(res.contiguous(), self.peer, group=self.group)
             total += n
@@ -137,11 +141,12 @@ class DetectClassifyPipeline:
                 dets, boxes, crops = self._detect_and_crop(imgs)
                 out.append((dets, boxes, self.classify(crops)))
             return out
+        # only the hand-off goes through wire_dtype (fp16 on GPUs): one conversion each side of the RCCL send
         pending = None
         inflight: list = []
         for imgs in batches:
             dets, boxes, crops = self._detect_and_crop(imgs)
-            works = self._send(crops)               # hand batch i to the classifier ...
+            works = self._send(crops.to(self.wire_dtype))  # hand batch i to the classifier ...
             if pending is not None:                 # ... then collect batch i-1 while it works
                 pd, pb = pending
                 out.append((pd, pb, self._recv_results(pb.shape[0])))

@@ -52,6 +52,7 @@ def main():
     d.emit({"metric": "detector->classifier ensemble images/sec (whole node)", "value": round(imgs / dt, 2),
             "unit": "images/s", "n_gpus": d.world, "crops_per_s": round(crops * pairs / dt, 2),
             "ms_per_batch": round(dt / a.steps * 1e3, 2), "dtype": "bf16",
+            "wire_dtype": pcfg.wire_dtype if d.world > 1 else None,
             "data": "synthetic uint8 images, random-init weights",
             "config": {"per_pair_batch": a.batch, "image_size": a.size, "crop": 224,
                        "parallelism": f"pipeline2x{pairs}" if d.world > 1 else "colocated"}}, a.json_out)
