@@ -3,7 +3,7 @@ Faster-RCNN detector batches): records every ``tuned_tile`` lookup during a forw
 1-6 on each distinct shape in isolation and, with ``--write``, MERGES the winners into
 ``aiforearth_api_platform_amd/ops/conv_tiles.json`` (existing keys of other shapes are kept).
 
-    python bench/conv_tune_model.py unet [--write]      # batch 16 x 512^2 x 4 (bench/landcover_bench.py)
+    [B=16] python bench/conv_tune_model.py unet [--write]   # B tiles x 512^2 x 4 (bench/landcover_bench.py)
     python bench/conv_tune_model.py detector [--write]  # batch 8 x 640^2 x 3 (bench/detector_bench.py)
 """
 import json
@@ -62,7 +62,8 @@ def main():
     if which == "unet":
         from aiforearth_api_platform_amd.models.unet import FusedUNet, unet_landcover
         m = FusedUNet(unet_landcover(seed=0), device=dev)
-        img = torch.randint(0, 256, (16, 512, 512, 4), dtype=torch.uint8, device=dev)
+        nb = int(os.environ.get("B", "16"))  # tiles per forward (bench/landcover_bench.py --tile-batch)
+        img = torch.randint(0, 256, (nb, 512, 512, 4), dtype=torch.uint8, device=dev)
         shapes = record(lambda: m.forward_u8(img))
     elif which == "detector":
         from aiforearth_api_platform_amd.models.faster_rcnn import DetectorConfig, FasterRCNN
