@@ -110,14 +110,22 @@ __global__ __launch_bounds__(256) void avgpool_kernel(const uint16_t* __restrict
     const long n = i / C8;
     float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     const uint4* p = reinterpret_cast<const uint4*>(x) + n * HW * C8 + c8;
-    for (int j = 0; j < HW; ++j) {
-      const uint4 v = p[static_cast<long>(j) * C8];
+    auto add = [&](const uint4& v) __attribute__((always_inline)) {
       float a, b;
       unpack_bf16x2(v.x, a, b); acc[0] += a; acc[1] += b;
       unpack_bf16x2(v.y, a, b); acc[2] += a; acc[3] += b;
       unpack_bf16x2(v.z, a, b); acc[4] += a; acc[5] += b;
       unpack_bf16x2(v.w, a, b); acc[6] += a; acc[7] += b;
+    };
+    int j = 0;
+    for (; j + 7 <= HW; j += 7) {  // seven independent 16-B loads in flight (7x7 maps: one batch per row)
+      uint4 v[7];
+#pragma unroll
+      for (int u = 0; u < 7; ++u) v[u] = p[static_cast<long>(j + u) * C8];
+#pragma unroll
+      for (int u = 0; u < 7; ++u) add(v[u]);
     }
+    for (; j < HW; ++j) add(p[static_cast<long>(j) * C8]);
     reinterpret_cast<uint4*>(y)[i] = make_uint4(pack_bf16x2(acc[0] * inv, acc[1] * inv), pack_bf16x2(acc[2] * inv, acc[3] * inv),
                                                 pack_bf16x2(acc[4] * inv, acc[5] * inv), pack_bf16x2(acc[6] * inv, acc[7] * inv));
   }
