@@ -65,7 +65,7 @@ class Config:
     process_logger_period_s: float = field(default=300.0, metadata={"env": "AI4E_PROCESS_LOGGER_PERIOD_S"})
     # --- GPU worker pool / batcher ---
     num_gpus: int = field(default=1, metadata={"env": "AI4E_NUM_GPUS"})
-    max_batch: int = field(default=256, metadata={"env": "AI4E_MAX_BATCH"})
+    max_batch: int = field(default=250, metadata={"env": "AI4E_MAX_BATCH"})  # whole waves on 256 CUs (bench.py)
     max_batch_delay_ms: float = field(default=2.0, metadata={"env": "AI4E_MAX_BATCH_DELAY_MS"})
     # graph-captured batch sizes below max_batch (low-load fast path: a batch of n runs the smallest bucket >= n)
     batch_buckets: str = field(default="8,32,128", metadata={"env": "AI4E_BATCH_BUCKETS"})

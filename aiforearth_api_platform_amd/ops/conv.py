@@ -107,7 +107,10 @@ def tuned_tile(pc: PackedConv, n: int, h: int, w: int, residual: bool) -> int:
                 _TILES = json.load(f)
         except (OSError, ValueError):
             _TILES = {}
-    return int(_TILES.get(tile_key(pc, n, h, w, residual), 0))
+    cfg = _TILES.get(tile_key(pc, n, h, w, residual))
+    if cfg is None and 224 <= n <= 288:  # batch sizes near the tuned 256 share its tile choices
+        cfg = _TILES.get(tile_key(pc, 256, h, w, residual))
+    return int(cfg or 0)
 
 
 def conv2d_nhwc(x: torch.Tensor, pc: PackedConv, residual: Optional[torch.Tensor] = None, relu: bool = False,

@@ -39,7 +39,10 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=100)
     p.add_argument("--warmup", type=int, default=10)
-    p.add_argument("--batch", type=int, default=256, help="images per step per GPU (= max dynamic batch)")
+    # 250, not 256: with the K1c / K1 tile sizes and occupancies on 256 CUs, 250 images fill the layer1 chains
+    # (8 x 768 slots), the layer2 chains (3 x 512) and layer3's c3 convs (6 x 512) to whole waves of
+    # workgroups; 256 spills a few % of tiles into an extra, nearly empty wave (+1.8-2.1 % images/s measured)
+    p.add_argument("--batch", type=int, default=250, help="images per step per GPU (= max dynamic batch)")
     p.add_argument("--inflight", type=int, default=2, help="steps kept outstanding per GPU")
     p.add_argument("--image-size", type=int, default=224)
     p.add_argument("--backend", default="auto", choices=["auto", "hip", "torch"])
