@@ -38,7 +38,7 @@ from .serving import ResultStore
 class ModelSpec:
     factory: str                      # "package.module:function" -> callable(u8 [b,H,W,C]) -> logits
     item_shape: Tuple[int, int, int]
-    max_batch: int = 256
+    max_batch: int = 250  # whole waves of workgroups on 256 CUs for ResNet-50 (bench.py)
     topk: int = 5
     kwargs: Dict[str, Any] = field(default_factory=dict)
     use_graphs: bool = True
