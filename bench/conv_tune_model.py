@@ -4,7 +4,7 @@ Faster-RCNN detector batches): records every ``tuned_tile`` lookup during a forw
 ``aiforearth_api_platform_amd/ops/conv_tiles.json`` (existing keys of other shapes are kept).
 
     [B=16] python bench/conv_tune_model.py unet [--write]   # B tiles x 512^2 x 4 (bench/landcover_bench.py)
-    python bench/conv_tune_model.py detector [--write]  # batch 8 x 640^2 x 3 (bench/detector_bench.py)
+    [B=32] python bench/conv_tune_model.py detector [--write]  # B x 640^2 x 3 (bench/detector_bench.py)
 """
 import json
 import os
@@ -68,7 +68,7 @@ def main():
     elif which == "detector":
         from aiforearth_api_platform_amd.models.faster_rcnn import DetectorConfig, FasterRCNN
         m = FasterRCNN(DetectorConfig(), seed=0, device=dev)
-        img = torch.randint(0, 256, (8, 640, 640, 3), dtype=torch.uint8, device=dev)
+        img = torch.randint(0, 256, (int(os.environ.get("B", "32")), 640, 640, 3), dtype=torch.uint8, device=dev)
         shapes = record(lambda: m.forward_u8(img))
     else:
         raise SystemExit(f"unknown model {which}")
