@@ -20,7 +20,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops.conv import (PackedConv, chain_supported, conv2d_nhwc, conv_chain, fold_bn, pack_conv,
-                        pack_stem_s2d, stem_pool, stem_pool_u8)
+                        pack_stem_s2d, stem_pool, stem_pool_c1, stem_pool_u8)
 from ..ops.head import softmax_topk
 from ..ops.pool import (global_avgpool_nhwc, maxpool2d_nhwc, preprocess_s2d_u8, preprocess_u8,
                         space_to_depth_shifted)
@@ -158,6 +158,8 @@ class FusedResNet:
         # uint8 preprocess fused into the stem kernel (AI4E_STEM_U8=1); off by default: measured 0.1 ms slower
         # per batch of 256 than the separate K7 preprocess + K1s (byte gathers serialize with the conv)
         self.stem_u8 = os.environ.get("AI4E_STEM_U8", "0") not in ("0", "off", "")
+        # the first bottleneck's 1x1 c1 fused into the stem kernel (computed from the pooled tile in LDS)
+        self.stem_c1 = os.environ.get("AI4E_STEM_C1", "1") not in ("0", "off", "")
         # classifier FC through hipBLASLt (AI4E_FC_BLAS=0: the K1 conv kernel)
         self.fc_blas = os.environ.get("AI4E_FC_BLAS", "1") not in ("0", "off", "")
         self._fc_lin = None
@@ -209,6 +211,12 @@ class FusedResNet:
 
     def _stem(self, x: torch.Tensor) -> torch.Tensor:
         return stem_pool(self.stem_input(x), self.stem)  # K1s: conv + bias + ReLU + 3x3/2 max-pool
+
+    def _stem_t1(self, x: torch.Tensor):
+        """(stem output, first bottleneck's c1 output): one K1s launch with the 1x1 fused (AI4E_STEM_C1=0: two)."""
+        if self.stem_c1:
+            return stem_pool_c1(self.stem_input(x), self.stem, self.stages[0][0][0])
+        return self._stem(x), None
 
     @staticmethod
     def _block(x: torch.Tensor, blk, out: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -287,9 +295,10 @@ class FusedResNet:
     def stage_features(self, x_s2d: torch.Tensor):
         """Space-to-depth input -> the four stage outputs (C2..C5) through K1s + the K1c chains; the
         per-conv K1 graph when chains are off."""
-        y = self._stem(x_s2d)
         if self.chain:
-            return self._stages_chained(y, collect=True)
+            y, t1 = self._stem_t1(x_s2d)
+            return self._stages_chained(y, collect=True, t1=t1)
+        y = self._stem(x_s2d)
         outs, ends, start = [], [], 0
         for st in self.stages:
             start += len(st)
@@ -336,6 +345,9 @@ class FusedResNet:
             y = feats
         elif preprocess is preprocess_s2d_u8 and self.stem_u8:
             y, nblocks = stem_pool_u8(x, self.stem), 0  # K7 preprocess fused into the stem kernel
+        elif self.chain:
+            y, t1 = self._stem_t1(pre(x))
+            return self._stages_chained(y, t1=t1)
         else:
             y, nblocks = self._stem(pre(x)), 0
         if self.chain and nblocks == 0:

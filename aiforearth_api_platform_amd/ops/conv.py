@@ -328,6 +328,25 @@ def stem_pool(x: torch.Tensor, pc: PackedConv, variant: int = -1) -> torch.Tenso
     return y
 
 
+def stem_pool_c1(x: torch.Tensor, pc: PackedConv, c1: PackedConv):
+    """K1s followed by the first bottleneck's 1x1 c1 (64 -> 64, + bias, ReLU) computed from the pooled tile
+    while it is still in LDS: returns ``(y, relu(c1(y)))`` from ONE launch (no re-read of y). Other backends /
+    shapes: ``stem_pool`` then a K1 conv."""
+    n, h, w, c = x.shape
+    if (_ext.backend_for(x) != "hip" or pc.cout != 64 or c != 16 or (pc.kh, pc.kw, pc.pad, pc.pad_hi) != (4, 4, 1, 2)
+            or (c1.kh, c1.kw, c1.stride, c1.pad, c1.cin_pad, c1.cout) != (1, 1, 1, 0, 64, 64) or STEM_VARIANT != 0
+            or x.dtype != torch.bfloat16 or not x.is_contiguous()):
+        y = stem_pool(x, pc)
+        return y, conv2d_nhwc(y, c1, relu=True)
+    ph, pw = (h - 1) // 2 + 1, (w - 1) // 2 + 1
+    y = torch.empty(n, ph, pw, 64, device=x.device, dtype=x.dtype)
+    t1 = torch.empty(n, ph, pw, 64, device=x.device, dtype=x.dtype)
+    _ext.call("ai4e_stem_pool_c1_fwd", x.data_ptr(), pc.w_packed.data_ptr(), pc.bias.data_ptr(), y.data_ptr(),
+              c1.w_packed.data_ptr(), c1.bias.data_ptr(), t1.data_ptr(), c1.kpad, n, h, w, pc.kpad,
+              _ext.stream_ptr(x.device))
+    return y, t1
+
+
 def stem_pool_u8(img: torch.Tensor, pc: PackedConv, mean=None, std=None, scale: float = 1.0 / 255.0) -> torch.Tensor:
     """uint8 NHWC images -> pooled stem output: the s2d preprocess (K7) fused into K1s, so the normalized
     space-to-depth image (103 MB at batch 256) is never written. Same math as

@@ -24,6 +24,7 @@ def apply(m, variant):
     _TILES0 = dict(convmod._TILES) if _TILES0 is None else _TILES0
     convmod._TILES = dict(_TILES0)
     m.chain_mb = None
+    m.stem_c1 = True
     m.fc_blas = True
     convmod.BLAS_1X1 = False
     for kv in variant.split(","):
@@ -40,6 +41,8 @@ def apply(m, variant):
             convmod.BLAS_1X1 = v == "1"
         elif k == "fcblas":
             m.fc_blas = v == "1"
+        elif k == "stemc1":
+            m.stem_c1 = v == "1"
         elif k == "stemu8":
             m.stem_u8 = v == "1"
         elif k.startswith("chain"):

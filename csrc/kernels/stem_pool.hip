@@ -40,6 +40,12 @@ struct StemParams {
   const uint8_t* img;
   int cin;
   float mean[4], istd[4], scale;
+  // fused next 1x1 (the first bottleneck's c1, 64 -> 64, + bias, ReLU) on the pooled tile (null = off):
+  // t1 [N, PH, PW, 64] = relu(y . W1^T + b1), W1 [>= 64 rows, kpad1 >= 64]
+  const uint16_t* w1;
+  const float* b1;
+  uint16_t* t1;
+  int kpad1;
 };
 
 __device__ __forceinline__ uint32_t max_bf16x2(uint32_t a, uint32_t b) {
@@ -188,7 +194,7 @@ constexpr int FP_SLOTS = 2 * FP_STRIDE;                                 // 736 1
 constexpr int FP_DMA = (FP_SLOTS + 255) / 256;                          // DMA instrs per wave (3)
 constexpr int D_W = 0, D_FP = 64 * 512, D_TILE = D_FP + FP_DMA * 4 * 1024, D_LDS = D_TILE + SP_BM * 128;
 
-template <bool U8>
+template <bool U8, bool C1 = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void stem_pool_direct_kernel(const StemParams p, int ntiles) {
   extern __shared__ __attribute__((aligned(1024))) uint8_t dsm[];
@@ -314,6 +320,20 @@ void stem_pool_direct_kernel(const StemParams p, int ntiles) {
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    // fused c1 operands, issued now so the L2 latency hides under the pooling: W1 fragments (output-channel
+    // rows 16j + lane&15, k-chunk lane>>4 of k-step ks; 8 KB, L2-resident) and the bias
+    bf16x8_t w1f[4][2];
+    float4 b1v[4];
+    if constexpr (C1) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+          w1f[j][ks] = *reinterpret_cast<const bf16x8_t*>(p.w1 + static_cast<long>(16 * j + (lane & 15)) * p.kpad1 +
+                                                          32 * ks + 8 * (lane >> 4));
+        b1v[j] = *reinterpret_cast<const float4*>(p.b1 + 16 * j + 4 * (lane >> 4));
+      }
+    }
     for (int task = tid; task < SP_TR * SP_TC * 8; task += 256) {
       const int q = task >> 3, k8 = task & 7;
       const int py = q / SP_TC, px = q - py * SP_TC;
@@ -332,17 +352,44 @@ void stem_pool_direct_kernel(const StemParams p, int ntiles) {
           mx.w = max_bf16x2(mx.w, v.w);
         }
       *reinterpret_cast<uint4*>(p.y + ((static_cast<long>(img) * p.PH + ph) * p.PW + pw) * SP_BN + 8 * k8) = mx;
+      if constexpr (C1)  // pooled row q as the c1 B operand: [k-block k8/4][64 rows][4 x 16-B chunks ^ swz(q)]
+        *reinterpret_cast<uint4*>(dsm + D_FP + (k8 >> 2) * 64 * 64 + q * 64 + (((k8 & 3) ^ swz(q)) << 4)) = mx;
     }
     // the next tile's footprint DMA and epilogue overwrite what this tile's readers still use
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if constexpr (C1) {
+      // t1 = relu(W1 . pooled + b1) for the tile's 56 pooled pixels (wave w: rows 16w..16w+15; rows >= 56 and
+      // pooled pixels outside the image are computed from stale LDS and never stored)
+      const int r = 16 * wave + (lane & 15);
+      f32x4_t a1[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) a1[j] = f32x4_t{b1v[j].x, b1v[j].y, b1v[j].z, b1v[j].w};
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const bf16x8_t fx = *reinterpret_cast<const bf16x8_t*>(dsm + D_FP + ks * 64 * 64 + r * 64 +
+                                                               (((lane >> 4) ^ swz(r)) << 4));
+#pragma unroll
+        for (int j = 0; j < 4; ++j) a1[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1f[j][ks], fx, a1[j], 0, 0, 0);
+      }
+      const int py = r / SP_TC, px = r - py * SP_TC;
+      const int ph = ph0 + py, pw = pw0 + px;
+      if (r < SP_TR * SP_TC && ph < p.PH && pw < p.PW) {
+        uint16_t* dst = p.t1 + ((static_cast<long>(img) * p.PH + ph) * p.PW + pw) * 64 + 4 * (lane >> 4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          *reinterpret_cast<uint2*>(dst + 16 * j) =
+              make_uint2(pack_relu_bf16x2(a1[j][0], a1[j][1]), pack_relu_bf16x2(a1[j][2], a1[j][3]));
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // pooled rows read before the next DMA
+    }
   }
 }
 
-template <bool U8>
+template <bool U8, bool C1 = false>
 int launch_direct(const StemParams& p, long nb, hipStream_t stream) {
   static bool attr = false;
   if (!attr) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(stem_pool_direct_kernel<U8>),
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(stem_pool_direct_kernel<U8, C1>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, D_LDS) != hipSuccess)
       return AI4E_ELAUNCH;
     attr = true;
@@ -351,7 +398,7 @@ int launch_direct(const StemParams& p, long nb, hipStream_t stream) {
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     cus = 256;
   const long grid = nb < 2L * cus ? nb : 2L * cus;  // two persistent workgroups per CU
-  hipLaunchKernelGGL(stem_pool_direct_kernel<U8>, dim3(static_cast<unsigned>(grid)), dim3(256), D_LDS, stream, p,
+  hipLaunchKernelGGL((stem_pool_direct_kernel<U8, C1>), dim3(static_cast<unsigned>(grid)), dim3(256), D_LDS, stream, p,
                      static_cast<int>(nb));
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
 }
@@ -397,6 +444,37 @@ AI4E_API int ai4e_stem_pool_u8_fwd(const void* img, const void* w, const void* b
   const long nb = static_cast<long>(N) * p.tiles_r * p.tiles_c;
   if (nb <= 0) return AI4E_OK;
   return launch_direct<true>(p, nb, stream);
+}
+
+// Stem + pool + the first bottleneck's 1x1 c1 (64 -> 64, bias, ReLU) in one launch: y as ai4e_stem_pool_fwd,
+// plus t1 [N, PH, PW, 64] = relu(y . W1^T + b1) (w1 [>= 64 rows, kpad1 >= 64] bf16, b1 [>= 64] fp32), computed
+// from the pooled tile while it is still in LDS (no re-read of y, no separate launch).
+AI4E_API int ai4e_stem_pool_c1_fwd(const void* x, const void* w, const void* bias, void* y, const void* w1,
+                                   const void* b1, void* t1, int kpad1, int N, int H, int W, int kpad,
+                                   hipStream_t stream) {
+  if (!x || !w || !bias || !y || !w1 || !b1 || !t1 || kpad < 256 || kpad % 8 || kpad1 < 64 || kpad1 % 8 || H <= 0 ||
+      W <= 0)
+    return AI4E_EINVAL;
+  StemParams p{};
+  p.x = static_cast<const uint16_t*>(x);
+  p.w = static_cast<const uint16_t*>(w);
+  p.bias = static_cast<const float*>(bias);
+  p.y = static_cast<uint16_t*>(y);
+  p.zero = stem_zero_ptr();
+  if (!p.zero) return AI4E_ELAUNCH;
+  p.w1 = static_cast<const uint16_t*>(w1);
+  p.b1 = static_cast<const float*>(b1);
+  p.t1 = static_cast<uint16_t*>(t1);
+  p.kpad1 = kpad1;
+  p.H = H; p.W = W;
+  p.PH = (H - 1) / 2 + 1;
+  p.PW = (W - 1) / 2 + 1;
+  p.kpad = kpad;
+  p.tiles_r = ai4e_cdiv(p.PH, SP_TR);
+  p.tiles_c = ai4e_cdiv(p.PW, SP_TC);
+  const long nb = static_cast<long>(N) * p.tiles_r * p.tiles_c;
+  if (nb <= 0) return AI4E_OK;
+  return launch_direct<false, true>(p, nb, stream);
 }
 
 // x: s2d stem input [N, H, W, 16] bf16; w: packed 4x4x16 stem weights [>= 64 rows, kpad >= 256] (pad 1/2,

@@ -167,3 +167,21 @@ def test_stem_pool_u8_fused_preprocess(shape):
     torch.cuda.synchronize()
     assert a.shape == b.shape
     assert (a.float() - b.float()).abs().max().item() <= 1e-2 * b.float().abs().max().item() + 1e-3
+
+
+@pytest.mark.parametrize("shape", [(3, 112, 112), (2, 31, 25), (1, 17, 9)])
+def test_stem_pool_fused_c1(shape):
+    """K1s with the first bottleneck's 1x1 fused (t1 from the pooled tile in LDS) == K1s + a K1 conv."""
+    from aiforearth_api_platform_amd.ops.conv import conv2d_nhwc, pack_stem_s2d, stem_pool, stem_pool_c1
+
+    n, h, w = shape
+    torch.manual_seed(8)
+    pc = pack_stem_s2d(torch.randn(64, 3, 7, 7) / 12, torch.randn(64) * 0.1).to(DEV)
+    c1 = pack_conv(torch.randn(64, 64, 1, 1) / 8, torch.randn(64) * 0.1).to(DEV)
+    x = torch.randn(n, h, w, 16, device=DEV).to(torch.bfloat16)
+    y, t1 = stem_pool_c1(x, pc, c1)
+    yr = stem_pool(x, pc)
+    tr = conv2d_nhwc(yr, c1, relu=True)
+    torch.cuda.synchronize()
+    assert torch.equal(y, yr)
+    assert (t1.float() - tr.float()).abs().max().item() <= 0.02 * tr.float().abs().max().item() + 0.02
