@@ -16,6 +16,8 @@ bf16 built from the hand-written kernels, arranged so that skip-concat costs no 
 """
 from __future__ import annotations
 
+import os
+
 from typing import List, Optional, Tuple
 
 import torch
@@ -95,13 +97,14 @@ class _FusedDouble:
         self.g1 = (dc.n1.weight.data.float().to(device), dc.n1.bias.data.float().to(device), dc.n1.num_groups)
         self.g2 = (dc.n2.weight.data.float().to(device), dc.n2.bias.data.float().to(device), dc.n2.num_groups)
 
-    def __call__(self, x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    def __call__(self, x: torch.Tensor, out: Optional[torch.Tensor] = None,
+                 pool_out: Optional[torch.Tensor] = None) -> torch.Tensor:
         # GroupNorm statistics come out of the conv epilogues (conv2d_gn_nhwc) where the tile allows
         y, st = conv2d_gn_nhwc(x, self.c1, self.g1[2])
         y = group_norm_nhwc(y, *self.g1[:2], groups=self.g1[2], relu=True, out=y, stats=st)
         z, st = conv2d_gn_nhwc(y, self.c2, self.g2[2])
         return group_norm_nhwc(z, *self.g2[:2], groups=self.g2[2], relu=True, out=out if out is not None else z,
-                               stats=st)
+                               stats=st, pool_out=pool_out)
 
 
 class FusedUNet:
@@ -120,6 +123,7 @@ class FusedUNet:
         b[: model.n_classes] = model.outc.bias.data
         self.outc = pack_conv(w, b).to(d)
         self.out_channels = kout
+        self.fused_pool = os.environ.get("AI4E_UNET_FUSED_POOL", "1") != "0"
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         """x: normalized NHWC [N,H,W,8] (H, W multiples of 16) -> logits NHWC [N,H,W,kout]."""
@@ -130,6 +134,27 @@ class FusedUNet:
         for lvl in range(4):
             s = 2 ** lvl
             cat.append(torch.empty(n, h // s, w // s, enc_c[lvl] + up_c[3 - lvl], device=x.device, dtype=x.dtype))
+        # each encoder level's GN apply also writes the 2x2 max-pool the next level reads (no pool pass)
+        if not self.fused_pool:
+            return self._forward_unfused(x, cat, enc_c)
+        pooled = torch.empty(n, h // 2, w // 2, enc_c[0], device=x.device, dtype=x.dtype)
+        self.inc(x, out=cat[0][..., : enc_c[0]], pool_out=pooled)
+        for lvl in range(1, 5):
+            if lvl < 4:
+                s = 2 ** (lvl + 1)
+                nxt = torch.empty(n, h // s, w // s, enc_c[lvl], device=x.device, dtype=x.dtype)
+                self.down[lvl - 1](pooled, out=cat[lvl][..., : enc_c[lvl]], pool_out=nxt)
+                pooled = nxt
+            else:
+                y = self.down[3](pooled)
+        for i, lvl in enumerate((3, 2, 1, 0)):
+            buf = cat[lvl]
+            upsample2x_nhwc(y, out=buf, out_coff=enc_c[lvl])
+            y = self.up[i](buf)
+        return conv2d_nhwc(y, self.outc)
+
+    def _forward_unfused(self, x, cat, enc_c):
+        """Encoder with a separate max-pool pass (AI4E_UNET_FUSED_POOL=0, for A/B)."""
         skip = self.inc(x, out=cat[0][..., : enc_c[0]])
         for lvl in range(1, 5):
             pooled = maxpool2d_nhwc(skip, 2, 2, 0)

@@ -25,15 +25,33 @@ def _base_ptr(t: torch.Tensor) -> int:
 
 
 def group_norm_nhwc(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, groups: int = 32, eps: float = 1e-5,
-                    relu: bool = False, out: Optional[torch.Tensor] = None, stats=None) -> torch.Tensor:
+                    relu: bool = False, out: Optional[torch.Tensor] = None, stats=None,
+                    pool_out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """``stats``: ``(partials, nchunks)`` from ``conv2d_gn_nhwc`` (the producing conv's epilogue already summed
-    the groups), which skips the statistics pass."""
+    the groups), which skips the statistics pass. ``pool_out``: contiguous [N, H/2, W/2, C] that also receives the
+    2x2/2 max-pool of the result (from the same pass when ``stats`` is given)."""
     n, h, w, c = x.shape
     if out is None:
         out = torch.empty(n, h, w, c, device=x.device, dtype=x.dtype)
     if _ext.backend_for(x) == "hip":
         ldx, xcoff = _nhwc_ld(x)
         ldy, ycoff = _nhwc_ld(out)
+        c8 = c // 8
+        if (stats is not None and pool_out is not None and h % 2 == 0 and w % 2 == 0 and c % 8 == 0
+                and c8 <= 256 and 256 % c8 == 0 and pool_out.is_contiguous()
+                and tuple(pool_out.shape) == (n, h // 2, w // 2, c)):
+            partials, nchunks = stats
+            g32 = gamma.to(x.device, torch.float32).contiguous()
+            b32 = beta.to(x.device, torch.float32).contiguous()
+            _ext.call("ai4e_groupnorm_apply_pool_nhwc", _base_ptr(x), _base_ptr(out), g32.data_ptr(),
+                      b32.data_ptr(), partials.data_ptr(), pool_out.data_ptr(), n, h, w, c, groups, eps, int(relu),
+                      ldx | (ldy << 16), xcoff | (ycoff << 16), nchunks, _ext.stream_ptr(x.device))
+            return out
+        if pool_out is not None:
+            group_norm_nhwc(x, gamma, beta, groups, eps, relu, out, stats)
+            from .pool import maxpool2d_nhwc
+            pool_out.copy_(maxpool2d_nhwc(out, 2, 2, 0))
+            return out
         if stats is not None:
             partials, nchunks = stats
             g32 = gamma.to(x.device, torch.float32).contiguous()
@@ -55,6 +73,8 @@ def group_norm_nhwc(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, gr
     if relu:
         y = F.relu(y)
     out.copy_(y.permute(0, 2, 3, 1).to(out.dtype))
+    if pool_out is not None:
+        pool_out.copy_(F.max_pool2d(out.permute(0, 3, 1, 2).float(), 2, 2).permute(0, 2, 3, 1).to(pool_out.dtype))
     return out
 
 

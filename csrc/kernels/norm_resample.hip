@@ -157,6 +157,59 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const uint16_t* __restric
   }
 }
 
+// GN apply (+ReLU) that also emits the 2x2/2 max-pool of its output (the U-Net encoder's skip tensor and the
+// next level's input from one pass: the pool never re-reads the skip). One lane = one 8-channel column of a
+// 2x2 pixel quad; H, W even; pooled [N, H/2, W/2, C] contiguous.
+__global__ __launch_bounds__(256) void gn_apply_pool_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
+                                                            uint16_t* __restrict__ pooled, const float2* __restrict__ ss,
+                                                            int H, int W, int C, int relu, int ldx, int xcoff, int ldy,
+                                                            int ycoff) {
+  const int n = blockIdx.y;
+  const int C8 = C >> 3;
+  const int sh = __builtin_ctz(C8);
+  const int c8 = threadIdx.x & (C8 - 1);
+  float a[8], b[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float2 v = ss[static_cast<long>(n) * C + 8 * c8 + j];
+    a[j] = v.x;
+    b[j] = v.y;
+  }
+  const int PW = W >> 1, PH = H >> 1;
+  const uint16_t* xn = x + static_cast<long>(n) * H * W * ldx + xcoff + 8 * c8;
+  uint16_t* yn = y + static_cast<long>(n) * H * W * ldy + ycoff + 8 * c8;
+  uint16_t* pn = pooled + static_cast<long>(n) * PH * PW * C + 8 * c8;
+  const int total = PH * PW * C8;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+    const int q = i >> sh;
+    const int qh = q / PW, qw = q - qh * PW;
+    uint4 v[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+      v[d] = *reinterpret_cast<const uint4*>(xn + static_cast<long>((2 * qh + (d >> 1)) * W + 2 * qw + (d & 1)) * ldx);
+    float m[8];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      float f[8];
+      unpack_bf16x2(v[d].x, f[0], f[1]);
+      unpack_bf16x2(v[d].y, f[2], f[3]);
+      unpack_bf16x2(v[d].z, f[4], f[5]);
+      unpack_bf16x2(v[d].w, f[6], f[7]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        f[j] = fmaf(f[j], a[j], b[j]);
+        if (relu) f[j] = fmaxf(f[j], 0.f);
+        m[j] = d == 0 ? f[j] : fmaxf(m[j], f[j]);
+      }
+      *reinterpret_cast<uint4*>(yn + static_cast<long>((2 * qh + (d >> 1)) * W + 2 * qw + (d & 1)) * ldy) =
+          make_uint4(cvt_bf16x2(f[0], f[1]), cvt_bf16x2(f[2], f[3]), cvt_bf16x2(f[4], f[5]), cvt_bf16x2(f[6], f[7]));
+    }
+    // max of the rounded values == rounded max (rounding is monotonic)
+    *reinterpret_cast<uint4*>(pn + static_cast<long>(q) * C) =
+        make_uint4(cvt_bf16x2(m[0], m[1]), cvt_bf16x2(m[2], m[3]), cvt_bf16x2(m[4], m[5]), cvt_bf16x2(m[6], m[7]));
+  }
+}
+
 // Bilinear 2x upsample, align_corners=False (PyTorch semantics): src = (dst + 0.5) / 2 - 0.5, clamped.
 // IDX = int when the element count fits (32-bit index math instead of a 64-bit div/mod chain per vector)
 template <typename IDX>
@@ -248,6 +301,28 @@ AI4E_API int ai4e_groupnorm_apply_nhwc(const void* x, void* y, const void* gamma
   const int gx = grid_for(static_cast<long>(HW) * (C / 8) / 4 + 1);
   hipLaunchKernelGGL(gn_apply_kernel, dim3(gx, N), dim3(256), 0, s, static_cast<const uint16_t*>(x),
                      static_cast<uint16_t*>(y), ss, HW, C, relu, ldx, xcoff, ldy, ycoff);
+  return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
+}
+
+// GN (precomputed statistics, as ai4e_groupnorm_apply_nhwc) that also writes the 2x2/2 max-pool of its output
+// into pooled [N, H/2, W/2, C] (contiguous); H and W even.
+AI4E_API int ai4e_groupnorm_apply_pool_nhwc(const void* x, void* y, const void* gamma, const void* beta, void* partials,
+                                            void* pooled, int N, int H, int W, int C, int G, float eps, int relu,
+                                            int ldx_ldy_pack, int coff_pack, int nchunks, hipStream_t s) {
+  const int ldx = ldx_ldy_pack & 0xffff, ldy = (ldx_ldy_pack >> 16) & 0xffff;
+  const int xcoff = coff_pack & 0xffff, ycoff = (coff_pack >> 16) & 0xffff;
+  if (!pooled || (H & 1) || (W & 1) || C % 8 || G > 64 || C % G || (C / 8) > 256 || 256 % (C / 8) || ldx % 8 ||
+      ldy % 8 || xcoff % 8 || ycoff % 8 || nchunks <= 0)
+    return AI4E_EINVAL;
+  const int HW = H * W;
+  if (static_cast<long>(HW) * (C / 8) >= (1L << 31) - 8192L * 256) return AI4E_EINVAL;
+  float2* ss = reinterpret_cast<float2*>(static_cast<float*>(partials) + static_cast<long>(N) * nchunks * G * 2);
+  hipLaunchKernelGGL(gn_finalize_kernel, dim3(N), dim3(256), 0, s, static_cast<const float*>(partials),
+                     static_cast<const float*>(gamma), static_cast<const float*>(beta), ss, HW, C, G, eps, nchunks);
+  const int gx = grid_for(static_cast<long>(HW / 4) * (C / 8) / 2 + 1);
+  hipLaunchKernelGGL(gn_apply_pool_kernel, dim3(gx, N), dim3(256), 0, s, static_cast<const uint16_t*>(x),
+                     static_cast<uint16_t*>(y), static_cast<uint16_t*>(pooled), ss, H, W, C, relu, ldx, xcoff, ldy,
+                     ycoff);
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
 }
 

@@ -190,3 +190,29 @@ def test_conv_fused_groupnorm_stats(cfg, shape, monkeypatch):
     b = group_norm_nhwc(y, gamma, beta, groups=g, relu=True)
     torch.cuda.synchronize()
     assert (a.float() - b.float()).abs().max().item() <= 0.02
+
+
+@pytest.mark.parametrize("shape", [(2, 32, 32, 64, 64, 32), (1, 16, 24, 128, 256, 16)])
+def test_groupnorm_apply_fused_maxpool(shape, monkeypatch):
+    """GN apply + ReLU that also writes the 2x2/2 max-pool (the U-Net encoder's skip + next input) == GN then
+    max-pool, with the GN output in a channel slice of a wider concat buffer."""
+    from aiforearth_api_platform_amd.ops import conv as convmod
+    from aiforearth_api_platform_amd.ops.conv import conv2d_gn_nhwc, pack_conv
+
+    n, h, w, cin, cout, g = shape
+    monkeypatch.setattr(convmod, "tuned_tile", lambda *a: 1)
+    torch.manual_seed(6)
+    pc = pack_conv(torch.randn(cout, cin, 3, 3) / (9 * cin) ** 0.5, torch.randn(cout) * 0.3, pad=1).to(DEV)
+    x = torch.randn(n, h, w, cin, device=DEV).to(torch.bfloat16)
+    gamma, beta = torch.rand(cout, device=DEV) + 0.5, torch.randn(cout, device=DEV) * 0.3
+    y, st = conv2d_gn_nhwc(x, pc, g)
+    assert st is not None
+    cat = torch.full((n, h, w, cout + 64), 7.0, device=DEV, dtype=torch.bfloat16)
+    pooled = torch.empty(n, h // 2, w // 2, cout, device=DEV, dtype=torch.bfloat16)
+    a = group_norm_nhwc(y, gamma, beta, groups=g, relu=True, stats=st, out=cat[..., :cout], pool_out=pooled)
+    b = group_norm_nhwc(y, gamma, beta, groups=g, relu=True, stats=st)
+    ref_pool = F.max_pool2d(b.permute(0, 3, 1, 2).float(), 2, 2).permute(0, 2, 3, 1)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+    assert (cat[..., cout:] == 7.0).all()
+    assert torch.equal(pooled.float(), ref_pool)
