@@ -5,6 +5,7 @@ Faster-RCNN detector batches): records every ``tuned_tile`` lookup during a forw
 
     [B=16] python bench/conv_tune_model.py unet [--write]   # B tiles x 512^2 x 4 (bench/landcover_bench.py)
     [B=32] python bench/conv_tune_model.py detector [--write]  # B x 640^2 x 3 (bench/detector_bench.py)
+    [B=250] python bench/conv_tune_model.py resnet [--write]   # B x 224^2 x 3 (bench.py serving batch)
 """
 import json
 import os
@@ -69,6 +70,11 @@ def main():
         from aiforearth_api_platform_amd.models.faster_rcnn import DetectorConfig, FasterRCNN
         m = FasterRCNN(DetectorConfig(), seed=0, device=dev)
         img = torch.randint(0, 256, (int(os.environ.get("B", "32")), 640, 640, 3), dtype=torch.uint8, device=dev)
+        shapes = record(lambda: m.forward_u8(img))
+    elif which == "resnet":
+        from aiforearth_api_platform_amd.models.resnet import FusedResNet, resnet50
+        m = FusedResNet(resnet50(seed=0), device=dev)
+        img = torch.randint(0, 256, (int(os.environ.get("B", "250")), 224, 224, 3), dtype=torch.uint8, device=dev)
         shapes = record(lambda: m.forward_u8(img))
     else:
         raise SystemExit(f"unknown model {which}")
