@@ -152,6 +152,22 @@ def test_resnet50_fused_matches_reference():
     assert (logits.argmax(1) == ref.argmax(1)).float().mean() >= 0.75
 
 
+def test_resnet50_serving_batch_matches_reference():
+    """At the serving batch (250) the forward takes the batch-250 tile-table entries, the whole-wave K1c chain
+    grids and the 256x256 K1 tile: all of it against the fp32 PyTorch model on the same GPU."""
+    from aiforearth_api_platform_amd.models.resnet import FusedResNet, resnet50
+    m = resnet50(seed=5)
+    fused = FusedResNet(m, device=DEV)
+    img = torch.randint(0, 256, (250, 224, 224, 3), dtype=torch.uint8, generator=torch.Generator().manual_seed(5))
+    logits = fused(img.to(DEV)).float()
+    x = preprocess_u8(img)[..., :3].permute(0, 3, 1, 2).float().to(DEV)
+    with torch.no_grad():
+        ref = m.to(DEV).float()(x)
+    rel = (logits - ref).norm() / ref.norm()
+    assert rel < 0.05, rel.item()
+    assert (logits.argmax(1) == ref.argmax(1)).float().mean() >= 0.75
+
+
 def test_engine_graph_replay_matches_eager():
     from aiforearth_api_platform_amd.models.resnet import FusedResNet, resnet50
     from aiforearth_api_platform_amd.runtime.engine import InferenceEngine
