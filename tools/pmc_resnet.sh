@@ -12,7 +12,7 @@ for set in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTI
            "FETCH_SIZE TCC_HIT_sum" \
            "WRITE_SIZE TCC_MISS_sum"; do
   i=$((i+1))
-  timeout -s KILL 120 rocprofv3 --pmc $set --output-format csv -d gpurun_out/pmc -o pass$i -- python bench/profile_resnet.py 256 2 > gpurun_out/pmc/pass$i.log 2>&1
+  timeout -s KILL 120 rocprofv3 --pmc $set --output-format csv -d gpurun_out/pmc -o pass$i -- python bench/profile_resnet.py ${B:-250} 2 > gpurun_out/pmc/pass$i.log 2>&1
   rc=$?; echo "pass $i rc=$rc"; if [ $rc -ne 0 ]; then tail -5 gpurun_out/pmc/pass$i.log; exit $rc; fi
 done
 ls gpurun_out/pmc
