@@ -250,38 +250,38 @@ struct FpnLevels {
   float scale[4];
 };
 
+// One workgroup per (RoI, output row): the RoI's level, scale and bin geometry are workgroup-uniform
+// (scalar loads, computed once per lane instead of once per 8-channel output), and lanes walk (pw, c8)
+// with 32-bit index math — the flat grid-stride form spent ~6 64-bit div/mods per output.
 __global__ __launch_bounds__(256) void roi_align_fpn_kernel(FpnLevels lv, const float* __restrict__ rois,
                                                             uint16_t* __restrict__ out, int C, int R, int PH, int PW,
                                                             int sampling, int aligned) {
   const int C8 = C >> 3;
-  const long total = static_cast<long>(R) * PH * PW * C8;
-  for (long idx = blockIdx.x * 256L + threadIdx.x; idx < total; idx += static_cast<long>(gridDim.x) * 256) {
-    const int c8 = static_cast<int>(idx % C8);
-    long t = idx / C8;
-    const int pw = static_cast<int>(t % PW);
-    t /= PW;
-    const int ph = static_cast<int>(t % PH);
-    const int r = static_cast<int>(t / PH);
-    const float* roi = rois + 5L * r;
-    const float area = fmaxf(roi[3] - roi[1], 0.f) * fmaxf(roi[4] - roi[2], 0.f);
-    int l = static_cast<int>(floorf(4.f + log2f(sqrtf(area) / 224.f + 1e-6f)));
-    l = min(max(l, 2), 5) - 2;
-    const int H = lv.h[l], W = lv.w[l];
-    const float scale = lv.scale[l];
-    const int img = static_cast<int>(roi[0]);
-    const float off = aligned ? 0.5f : 0.f;
-    const float x1 = roi[1] * scale - off, y1 = roi[2] * scale - off;
-    float rw = roi[3] * scale - off - x1, rh = roi[4] * scale - off - y1;
-    if (!aligned) {
-      rw = fmaxf(rw, 1.f);
-      rh = fmaxf(rh, 1.f);
-    }
-    const float bh = rh / PH, bw = rw / PW;
-    const int gh = sampling > 0 ? sampling : static_cast<int>(ceilf(rh / PH));
-    const int gw = sampling > 0 ? sampling : static_cast<int>(ceilf(rw / PW));
-    const float inv = 1.f / fmaxf(gh * gw, 1);
+  const int r = blockIdx.x / PH;
+  const int ph = blockIdx.x - r * PH;
+  const float* roi = rois + 5L * r;
+  const float area = fmaxf(roi[3] - roi[1], 0.f) * fmaxf(roi[4] - roi[2], 0.f);
+  int l = static_cast<int>(floorf(4.f + log2f(sqrtf(area) / 224.f + 1e-6f)));
+  l = min(max(l, 2), 5) - 2;
+  const int H = lv.h[l], W = lv.w[l];
+  const float scale = lv.scale[l];
+  const int img = static_cast<int>(roi[0]);
+  const float off = aligned ? 0.5f : 0.f;
+  const float x1 = roi[1] * scale - off, y1 = roi[2] * scale - off;
+  float rw = roi[3] * scale - off - x1, rh = roi[4] * scale - off - y1;
+  if (!aligned) {
+    rw = fmaxf(rw, 1.f);
+    rh = fmaxf(rh, 1.f);
+  }
+  const float bh = rh / PH, bw = rw / PW;
+  const int gh = sampling > 0 ? sampling : static_cast<int>(ceilf(rh / PH));
+  const int gw = sampling > 0 ? sampling : static_cast<int>(ceilf(rw / PW));
+  const float inv = 1.f / fmaxf(gh * gw, 1);
+  const uint16_t* f = lv.f[l] + static_cast<long>(img) * H * W * C;
+  uint16_t* o = out + (static_cast<long>(r) * PH + ph) * PW * C;
+  for (int e = threadIdx.x; e < PW * C8; e += 256) {
+    const int pw = e / C8, c8 = e - pw * C8;
     float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    const uint16_t* f = lv.f[l] + static_cast<long>(img) * H * W * C;
     for (int iy = 0; iy < gh; ++iy) {
       const float y = y1 + ph * bh + (iy + 0.5f) * bh / gh;
       for (int ix = 0; ix < gw; ++ix) {
@@ -289,7 +289,7 @@ __global__ __launch_bounds__(256) void roi_align_fpn_kernel(FpnLevels lv, const 
         bilinear_acc8(f, H, W, C, y, x, c8, inv, acc);
       }
     }
-    *reinterpret_cast<uint4*>(out + (((static_cast<long>(r) * PH + ph) * PW + pw) * C) + 8 * c8) =
+    *reinterpret_cast<uint4*>(o + static_cast<long>(pw) * C + 8 * c8) =
         make_uint4(pack_bf16x2(acc[0], acc[1]), pack_bf16x2(acc[2], acc[3]), pack_bf16x2(acc[4], acc[5]),
                    pack_bf16x2(acc[6], acc[7]));
   }
@@ -405,7 +405,8 @@ AI4E_API int ai4e_roi_align_fpn_nhwc(const void* f0, const void* f1, const void*
     lv.w[i] = hw[2 * i + 1];
     lv.scale[i] = scales[i];
   }
-  hipLaunchKernelGGL(roi_align_fpn_kernel, dim3(grid_for(static_cast<long>(R) * PH * PW * (C / 8))), dim3(256), 0, s,
+  if (static_cast<long>(R) * PH >= (1L << 31)) return AI4E_EINVAL;
+  hipLaunchKernelGGL(roi_align_fpn_kernel, dim3(static_cast<unsigned>(R * PH)), dim3(256), 0, s,
                      lv, static_cast<const float*>(rois), static_cast<uint16_t*>(out), C, R, PH, PW, sampling, aligned);
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
 }

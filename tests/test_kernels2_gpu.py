@@ -91,6 +91,24 @@ def test_roi_align(aligned):
     assert (out.float().cpu() - ref).abs().max().item() < 0.03
 
 
+@pytest.mark.parametrize("C", [256, 64, 24])
+def test_roi_align_fpn_matches_per_level_reference(C):
+    """In-kernel FPN level assignment (one workgroup per RoI row) == map_levels + per-level reference RoIAlign."""
+    from aiforearth_api_platform_amd.ops.detection import multiscale_roi_align, roi_align_fpn
+    g = torch.Generator().manual_seed(1)
+    feats = [torch.randn(2, 160 // s, 160 // s, C, generator=g).bfloat16() for s in (1, 2, 4, 8)]
+    scales = [1 / 4, 1 / 8, 1 / 16, 1 / 32]
+    R = 300
+    x1 = torch.rand(R, generator=g) * 600
+    y1 = torch.rand(R, generator=g) * 600
+    wh = torch.rand(R, 2, generator=g) ** 2 * 600 + 1  # small boxes (P2) through large ones (P5)
+    rois = torch.stack([torch.randint(0, 2, (R,), generator=g).float(), x1, y1, x1 + wh[:, 0], y1 + wh[:, 1]], 1)
+    ref = multiscale_roi_align([f.float() for f in feats], scales, rois, (7, 7), 2)
+    out = roi_align_fpn([f.to(DEV) for f in feats], scales, rois.to(DEV), (7, 7), 2)
+    assert out.shape == (R, 7, 7, C)
+    assert (out.float().cpu() - ref).abs().max().item() < 0.03
+
+
 def test_crop_resize():
     img = torch.randint(0, 256, (2, 300, 400, 3), dtype=torch.uint8)
     boxes = torch.tensor([[0, 10.5, 20, 200, 220], [1, 0, 0, 400, 300], [1, 350, 250, 399, 299]])
