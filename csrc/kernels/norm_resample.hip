@@ -77,7 +77,7 @@ __global__ __launch_bounds__(256) void gn_finalize_kernel(const float* __restric
                                                           const float* __restrict__ beta, float2* __restrict__ ss,
                                                           int HW, int C, int G, float eps, int nchunks) {
   const int n = blockIdx.x;
-  // thread t owns group t % G and every (256/G)-th chunk from t / G: each iteration the block reads one
+  // thread t owns group t % G and every (256/G)-th chunk from t / G: each load step the block reads one
   // contiguous 2 KB run of (chunk, group) float2 partials; two fp64 accumulator pairs per thread
   __shared__ double red_s[256], red_q[256];
   __shared__ float mean_s[64], rstd_s[64];
@@ -86,12 +86,18 @@ __global__ __launch_bounds__(256) void gn_finalize_kernel(const float* __restric
   double s0 = 0, q0 = 0, s1 = 0, q1 = 0;
   if (l < lpg) {
     const float2* pp = reinterpret_cast<const float2*>(partials) + static_cast<long>(n) * nchunks * G + g;
+    // 8 independent loads in flight per lane: with one workgroup per image the pass is latency-bound
     int k = l;
-    for (; k + lpg < nchunks; k += 2 * lpg) {
-      const float2 a = pp[static_cast<long>(k) * G], b = pp[static_cast<long>(k + lpg) * G];
-      s0 += a.x; q0 += a.y; s1 += b.x; q1 += b.y;
+    for (; k + 7 * lpg < nchunks; k += 8 * lpg) {
+      float2 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = pp[static_cast<long>(k + u * lpg) * G];
+#pragma unroll
+      for (int u = 0; u < 8; u += 2) {
+        s0 += v[u].x; q0 += v[u].y; s1 += v[u + 1].x; q1 += v[u + 1].y;
+      }
     }
-    if (k < nchunks) {
+    for (; k < nchunks; k += lpg) {
       const float2 a = pp[static_cast<long>(k) * G];
       s0 += a.x; q0 += a.y;
     }
