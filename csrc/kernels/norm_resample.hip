@@ -145,21 +145,33 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const uint16_t* __restric
   const uint16_t* xn = x + static_cast<long>(n) * HW * ldx + xcoff + 8 * c8;
   uint16_t* yn = y + static_cast<long>(n) * HW * ldy + ycoff + 8 * c8;
   const int total = HW * C8;
-  for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
-    const int p = i >> sh;
-    const uint4 v = *reinterpret_cast<const uint4*>(xn + static_cast<long>(p) * ldx);
-    float f[8];
-    unpack_bf16x2(v.x, f[0], f[1]);
-    unpack_bf16x2(v.y, f[2], f[3]);
-    unpack_bf16x2(v.z, f[4], f[5]);
-    unpack_bf16x2(v.w, f[6], f[7]);
+  const int S = gridDim.x * 256;
+  // the launch gives each lane ~4 vectors: issue their 4 loads together, then normalize and store
+  for (int i0 = blockIdx.x * 256 + threadIdx.x; i0 < total; i0 += 4 * S) {
+    uint4 v[4];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) f[j] = fmaf(f[j], a[j], b[j]);
-    uint4 o = make_uint4(cvt_bf16x2(f[0], f[1]), cvt_bf16x2(f[2], f[3]), cvt_bf16x2(f[4], f[5]), cvt_bf16x2(f[6], f[7]));
-    if (relu) {
-      o.x = relu_bf16x2(o.x); o.y = relu_bf16x2(o.y); o.z = relu_bf16x2(o.z); o.w = relu_bf16x2(o.w);
+    for (int u = 0; u < 4; ++u) {
+      const int i = i0 + u * S;
+      if (i < total) v[u] = *reinterpret_cast<const uint4*>(xn + static_cast<long>(i >> sh) * ldx);
     }
-    *reinterpret_cast<uint4*>(yn + static_cast<long>(p) * ldy) = o;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = i0 + u * S;
+      if (i >= total) break;
+      float f[8];
+      unpack_bf16x2(v[u].x, f[0], f[1]);
+      unpack_bf16x2(v[u].y, f[2], f[3]);
+      unpack_bf16x2(v[u].z, f[4], f[5]);
+      unpack_bf16x2(v[u].w, f[6], f[7]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] = fmaf(f[j], a[j], b[j]);
+      uint4 o = make_uint4(cvt_bf16x2(f[0], f[1]), cvt_bf16x2(f[2], f[3]), cvt_bf16x2(f[4], f[5]),
+                           cvt_bf16x2(f[6], f[7]));
+      if (relu) {
+        o.x = relu_bf16x2(o.x); o.y = relu_bf16x2(o.y); o.z = relu_bf16x2(o.z); o.w = relu_bf16x2(o.w);
+      }
+      *reinterpret_cast<uint4*>(yn + static_cast<long>(i >> sh) * ldy) = o;
+    }
   }
 }
 
@@ -276,7 +288,7 @@ AI4E_API int ai4e_groupnorm_nhwc(const void* x, void* y, const void* gamma, cons
   if (C % 8 || G > 64 || C % G || (C / 8) > 256 || 256 % (C / 8) || ldx % 8 || ldy % 8 || xcoff % 8 || ycoff % 8)
     return AI4E_EINVAL;
   if ((C / G) % 8 && 8 % (C / G)) return AI4E_EINVAL;
-  if (static_cast<long>(HW) * (C / 8) >= (1L << 31) - 8192L * 256) return AI4E_EINVAL;
+  if (static_cast<long>(HW) * (C / 8) >= (1L << 31) - 4 * 8192L * 256) return AI4E_EINVAL;
   const int nchunks = (HW + GN_PIX_PER_BLOCK - 1) / GN_PIX_PER_BLOCK;
   hipLaunchKernelGGL(gn_stats_kernel, dim3(nchunks, N), dim3(256), 0, s, static_cast<const uint16_t*>(x),
                      static_cast<float*>(partials), HW, C, G, ldx, xcoff, nchunks);
@@ -300,7 +312,7 @@ AI4E_API int ai4e_groupnorm_apply_nhwc(const void* x, void* y, const void* gamma
   if (C % 8 || G > 64 || C % G || (C / 8) > 256 || 256 % (C / 8) || ldx % 8 || ldy % 8 || xcoff % 8 || ycoff % 8 ||
       nchunks <= 0)
     return AI4E_EINVAL;
-  if (static_cast<long>(HW) * (C / 8) >= (1L << 31) - 8192L * 256) return AI4E_EINVAL;
+  if (static_cast<long>(HW) * (C / 8) >= (1L << 31) - 4 * 8192L * 256) return AI4E_EINVAL;
   float2* ss = reinterpret_cast<float2*>(static_cast<float*>(partials) + static_cast<long>(N) * nchunks * G * 2);
   hipLaunchKernelGGL(gn_finalize_kernel, dim3(N), dim3(256), 0, s, static_cast<const float*>(partials),
                      static_cast<const float*>(gamma), static_cast<const float*>(beta), ss, HW, C, G, eps, nchunks);
@@ -321,7 +333,7 @@ AI4E_API int ai4e_groupnorm_apply_pool_nhwc(const void* x, void* y, const void* 
       ldy % 8 || xcoff % 8 || ycoff % 8 || nchunks <= 0)
     return AI4E_EINVAL;
   const int HW = H * W;
-  if (static_cast<long>(HW) * (C / 8) >= (1L << 31) - 8192L * 256) return AI4E_EINVAL;
+  if (static_cast<long>(HW) * (C / 8) >= (1L << 31) - 4 * 8192L * 256) return AI4E_EINVAL;
   float2* ss = reinterpret_cast<float2*>(static_cast<float*>(partials) + static_cast<long>(N) * nchunks * G * 2);
   hipLaunchKernelGGL(gn_finalize_kernel, dim3(N), dim3(256), 0, s, static_cast<const float*>(partials),
                      static_cast<const float*>(gamma), static_cast<const float*>(beta), ss, HW, C, G, eps, nchunks);
@@ -337,7 +349,7 @@ AI4E_API int ai4e_upsample2x_bilinear(const void* x, void* y, int N, int H, int 
   (void)unused;
   if (C % 8 || ldy % 8 || ycoff % 8) return AI4E_EINVAL;
   const long total = static_cast<long>(N) * 4 * H * W * (C / 8);
-  if (total < (1L << 31) - 8192L * 256)
+  if (total < (1L << 31) - 4 * 8192L * 256)
     hipLaunchKernelGGL(upsample2x_kernel<int>, dim3(grid_for(total)), dim3(256), 0, s, static_cast<const uint16_t*>(x),
                        static_cast<uint16_t*>(y), N, H, W, C, ldy, ycoff);
   else
