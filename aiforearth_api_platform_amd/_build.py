@@ -56,7 +56,8 @@ def _run(cmd, verbose):
 
 def build_core(verbose: bool = False, force: bool = False) -> Path:
     src = sorted((CSRC / "core").glob("*.cpp"))
-    if not force and not _stale(CORE_SO, src):
+    headers = sorted((CSRC / "core").glob("*.h"))
+    if not force and not _stale(CORE_SO, [*src, *headers]):
         return CORE_SO
     import pybind11
 

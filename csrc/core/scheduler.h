@@ -1,0 +1,712 @@
+// NodeScheduler — the node's dispatch loop in native code: dispatch queue -> dynamic batch ->
+// per-GPU worker process -> results + task-state transitions, with no Python (and no GIL) on the
+// per-batch path.
+//
+// It is the single-node replacement for the reference's per-endpoint BackendQueueProcessor
+// (ProcessManager/BackendQueueProcessor/BackendQueueProcessor.cs:27-81: receive -> POST ->
+// complete / abandon on 429) *and* for its replica scaling (APIs/Charts/templates/async-gpu/
+// autoscaler.yaml, routing.yml ROUND_ROBIN): every GPU worker process owns one connection; for
+// each connection a dispatcher thread pulls up to max_batch peek-locked messages when its GPU has
+// a free pipeline slot (least-loaded placement by construction) and a reader thread retires the
+// worker's results. Messages on a connection use multiprocessing.Connection framing (4-byte
+// big-endian length + payload), so the Python side of a worker is plain Connection.send_bytes /
+// recv_bytes. Payload = u32 type + fields (little-endian):
+//
+//   READY  (w->s) i32 rank, i32 pinned, utf-8 JSON info
+//   HB     (w->s) f64 t, u64 hbm_used, u64 hbm_total, f64 gpu_busy_ms, u64 batches
+//   DONE   (w->s) u64 bid, u32 n, u32 row_bytes, f64 stage[5], u8 status[n] (padded to 8), rows
+//   BATCH  (s->w) u64 bid, u32 n, u32 0, i64 slots[n]
+//   STOP   (s->w)
+//   SUBMIT (w->s) u32 n, u32 0, i64 slots[n]      (a remote ingest shard enqueued n payloads)
+//   FREE   (s->w) u32 n, u32 0, i64 slots[n]      (slots of that shard's partition are free again)
+//   STAGE  (w->s) u64 bid, u32 stage, u32 0        (ensemble hop: AddPipelineTask for the batch)
+//
+// Item status in DONE: 0 ok, 1 invalid payload (failed, not retried), 2 model error (failed,
+// "Task failed - try again" as ai4e_service.py:208-211), 3 retry (abandoned with the retry delay;
+// dead-lettered after max delivery -> failed with a reason).
+// Failure detection (survey §5.3): a closed connection or a heartbeat older than hb_timeout marks
+// the worker dead; its in-flight batches go back to the queue and the rank is reported to Python
+// (`wait_failed`) which restarts or removes the process.
+#pragma once
+
+#include <arpa/inet.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <cerrno>
+#include <condition_variable>
+#include <cstring>
+#include <deque>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "dispatch_queue.h"
+#include "slot_ring.h"
+#include "task_store.h"
+
+namespace ai4e {
+
+// Timed condition waits on the system clock (see DispatchQueue::wait_s: TSAN-interceptable).
+template <class Pred>
+inline bool cv_wait_s(std::condition_variable& cv, std::unique_lock<std::mutex>& lk, double seconds, Pred pred) {
+  return cv.wait_until(lk,
+                       std::chrono::system_clock::now() + std::chrono::duration_cast<std::chrono::system_clock::duration>(
+                                                              std::chrono::duration<double>(std::max(0.0, seconds))),
+                       pred);
+}
+
+enum : uint32_t { F_READY = 1, F_HB = 2, F_DONE = 3, F_BATCH = 4, F_STOP = 5, F_SUBMIT = 6, F_FREE = 7, F_STAGE = 8 };
+enum : uint8_t { IT_OK = 0, IT_INVALID = 1, IT_ERROR = 2, IT_RETRY = 3 };
+
+static const char* kFailInvalid = "Task failed - invalid payload";
+static const char* kFailError = "Task failed - try again";
+static const char* kFailMaxRetries = "Task failed - maximum retries exceeded";
+static const char* kRequeued = "Awaiting service availability. Worker failed; requeued.";
+static const char* kPublishFailed = "Failed - unable to send to backend service.";
+
+struct SchedConfig {
+  size_t max_batch = 250;
+  double linger_s = 0.0005;
+  int depth = 2;               // batches in flight per worker
+  double retry_delay_s = 1.0;  // abandon delay for IT_RETRY items
+  double hb_timeout_s = 10.0;
+  double poll_s = 0.02;        // queue wait per dispatcher iteration
+};
+
+struct WorkerStats {
+  int rank = -1;
+  bool ready = false, alive = false, pinned = false;
+  uint64_t batches = 0, images = 0, failed_items = 0, retried_items = 0;
+  size_t outstanding = 0;
+  double last_hb_age_s = 0, gpu_busy_ms = 0;
+  uint64_t hbm_used = 0, hbm_total = 0;
+  std::string info;
+};
+
+class NodeScheduler {
+ public:
+  NodeScheduler(std::shared_ptr<TaskStore> store, std::shared_ptr<DispatchQueue> queue, std::string endpoint,
+                int64_t ring_slots, SchedConfig cfg)
+      : store_(std::move(store)), queue_(std::move(queue)), endpoint_(std::move(endpoint)), ring_slots_(ring_slots),
+        cfg_(cfg), hist_(12, 0) {}
+  ~NodeScheduler() { stop(); }
+
+  // Partition of the payload ring freed in this process (the ingest ring of the gateway).
+  void add_local_ring(std::shared_ptr<SlotRing> ring) {
+    std::lock_guard<std::mutex> g(mu_);
+    local_rings_.push_back(std::move(ring));
+  }
+  // Partition [base, base+len) is owned by the ingest shard on `rank`'s connection.
+  void add_remote_partition(int64_t base, int64_t len, int rank) {
+    std::lock_guard<std::mutex> g(mu_);
+    remote_parts_.push_back({base, len, rank});
+  }
+  // Ensemble stages: STAGE k from a worker moves the batch's tasks to stage_endpoints[k].
+  void set_stage_endpoints(std::vector<std::string> eps, std::vector<std::string> statuses) {
+    std::lock_guard<std::mutex> g(mu_);
+    stage_eps_ = std::move(eps);
+    stage_status_ = std::move(statuses);
+  }
+  void enable_completion_feed(bool on) {
+    std::lock_guard<std::mutex> g(feed_mu_);
+    feed_on_ = on;
+  }
+
+  // Takes ownership of `fd` (a connected stream socket). dispatch=false: ingest-only connection.
+  void attach(int rank, int fd, bool dispatch) {
+    std::unique_ptr<Worker> old;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      auto it = workers_.find(rank);
+      if (it != workers_.end()) old = std::move(it->second);
+      workers_.erase(rank);
+    }
+    if (old) join_worker(*old);
+    auto w = std::make_unique<Worker>();
+    w->rank = rank;
+    w->fd = fd;
+    w->dispatch = dispatch;
+    w->alive = true;
+    w->last_hb = mono_now();
+    Worker* raw = w.get();
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      workers_[rank] = std::move(w);
+    }
+    raw->reader = std::thread([this, raw] { reader_loop(*raw); });
+    if (dispatch) raw->dispatcher = std::thread([this, raw] { dispatch_loop(*raw); });
+  }
+
+  // Graceful retire: stop dispatching to `rank`, wait (<= timeout) for its batches, send STOP.
+  void detach(int rank, double timeout_s) {
+    Worker* w = nullptr;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      auto it = workers_.find(rank);
+      if (it == workers_.end()) return;
+      w = it->second.get();
+    }
+    {
+      std::unique_lock<std::mutex> lk(w->mu);
+      w->draining = true;
+      w->cv.notify_all();
+      cv_wait_s(w->cv, lk, timeout_s, [&] { return w->out.empty() || !w->alive; });
+    }
+    send_simple(*w, F_STOP);
+    mark_dead(*w, "retired", false);
+    std::unique_ptr<Worker> own;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      auto it = workers_.find(rank);
+      if (it != workers_.end()) own = std::move(it->second);
+      workers_.erase(rank);
+    }
+    if (own) join_worker(*own);
+  }
+
+  // Ranks whose worker died since the last call (blocks up to timeout_s for the first one).
+  std::vector<int> wait_failed(double timeout_s) {
+    std::unique_lock<std::mutex> lk(fail_mu_);
+    cv_wait_s(fail_cv_, lk, timeout_s, [&] { return !failed_.empty() || stopped_; });
+    std::vector<int> out(failed_.begin(), failed_.end());
+    failed_.clear();
+    return out;
+  }
+
+  // In-process ingest (gateway): create tasks for payloads already written to `slots`.
+  std::vector<std::string> submit(const std::vector<int64_t>& slots, const std::string& trace) {
+    return enqueue(slots, trace);
+  }
+
+  std::vector<std::string> wait_completed(double timeout_s) {
+    std::unique_lock<std::mutex> lk(feed_mu_);
+    cv_wait_s(feed_cv_, lk, timeout_s, [&] { return !feed_.empty() || stopped_; });
+    std::vector<std::string> out(std::make_move_iterator(feed_.begin()), std::make_move_iterator(feed_.end()));
+    feed_.clear();
+    return out;
+  }
+
+  std::vector<WorkerStats> worker_stats() {
+    std::vector<WorkerStats> out;
+    std::lock_guard<std::mutex> g(mu_);
+    const double now = mono_now();
+    for (auto& kv : workers_) {
+      Worker& w = *kv.second;
+      std::lock_guard<std::mutex> wg(w.mu);
+      WorkerStats s;
+      s.rank = w.rank;
+      s.ready = w.ready;
+      s.alive = w.alive;
+      s.pinned = w.pinned;
+      s.batches = w.batches;
+      s.images = w.images;
+      s.failed_items = w.failed_items;
+      s.retried_items = w.retried_items;
+      s.outstanding = w.out.size();
+      s.last_hb_age_s = now - w.last_hb;
+      s.gpu_busy_ms = w.gpu_busy_ms;
+      s.hbm_used = w.hbm_used;
+      s.hbm_total = w.hbm_total;
+      s.info = w.info;
+      out.push_back(s);
+    }
+    return out;
+  }
+
+  // Batch-size histogram: bucket i counts batches of size in (2^(i-1), 2^i].
+  std::vector<uint64_t> batch_histogram() {
+    std::lock_guard<std::mutex> g(hist_mu_);
+    return hist_;
+  }
+  uint64_t images_done() const { return images_done_.load(); }
+
+  void stop() {
+    {
+      std::lock_guard<std::mutex> g(fail_mu_);
+      if (stopped_) return;
+      stopped_ = true;
+    }
+    fail_cv_.notify_all();
+    feed_cv_.notify_all();
+    std::vector<std::unique_ptr<Worker>> ws;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      for (auto& kv : workers_) ws.push_back(std::move(kv.second));
+      workers_.clear();
+    }
+    for (auto& w : ws) {
+      send_simple(*w, F_STOP);
+      mark_dead(*w, "stopped", false);
+    }
+    queue_->kick();
+    for (auto& w : ws) join_worker(*w);
+  }
+
+ private:
+  struct Outstanding {
+    std::vector<std::string> ids;
+    std::vector<uint64_t> seqs;
+    std::vector<int64_t> slots;
+  };
+  struct Worker {
+    int rank = -1;
+    int fd = -1;
+    bool dispatch = true;
+    std::thread reader, dispatcher;
+    std::mutex send_mu;
+    std::mutex mu;  // guards everything below
+    std::condition_variable cv;
+    std::atomic<bool> alive{false};
+    bool ready = false, draining = false, pinned = false;
+    double last_hb = 0;
+    std::unordered_map<uint64_t, Outstanding> out;
+    uint64_t batches = 0, images = 0, failed_items = 0, retried_items = 0;
+    double gpu_busy_ms = 0;
+    uint64_t hbm_used = 0, hbm_total = 0;
+    std::string info;
+  };
+  struct RemotePart {
+    int64_t base, len;
+    int rank;
+  };
+
+  // ------------------------------------------------------------------ framing
+  static bool read_exact(int fd, void* buf, size_t n) {
+    char* p = static_cast<char*>(buf);
+    while (n) {
+      ssize_t k = ::recv(fd, p, n, 0);
+      if (k == 0) return false;
+      if (k < 0) {
+        if (errno == EINTR) continue;
+        return false;
+      }
+      p += k;
+      n -= static_cast<size_t>(k);
+    }
+    return true;
+  }
+  static bool write_all(int fd, const void* buf, size_t n) {
+    const char* p = static_cast<const char*>(buf);
+    while (n) {
+      ssize_t k = ::send(fd, p, n, MSG_NOSIGNAL);
+      if (k < 0) {
+        if (errno == EINTR) continue;
+        return false;
+      }
+      p += k;
+      n -= static_cast<size_t>(k);
+    }
+    return true;
+  }
+  static bool read_frame(int fd, std::string& out) {
+    int32_t be;
+    if (!read_exact(fd, &be, 4)) return false;
+    int64_t len = static_cast<int32_t>(ntohl(static_cast<uint32_t>(be)));
+    if (len == -1) {  // multiprocessing's >2 GiB form: 8-byte big-endian length follows
+      uint64_t be8;
+      if (!read_exact(fd, &be8, 8)) return false;
+      len = static_cast<int64_t>(be64toh(be8));
+    }
+    if (len < 4) return false;
+    out.resize(static_cast<size_t>(len));
+    return read_exact(fd, out.data(), out.size());
+  }
+  bool send_frame(Worker& w, const std::string& payload) {
+    std::lock_guard<std::mutex> g(w.send_mu);
+    if (w.fd < 0) return false;
+    const uint32_t be = htonl(static_cast<uint32_t>(payload.size()));
+    return write_all(w.fd, &be, 4) && write_all(w.fd, payload.data(), payload.size());
+  }
+  bool send_simple(Worker& w, uint32_t type) {
+    std::string p(4, '\0');
+    std::memcpy(p.data(), &type, 4);
+    return send_frame(w, p);
+  }
+  bool send_slots(Worker& w, uint32_t type, uint64_t bid, const std::vector<int64_t>& slots, bool with_bid) {
+    std::string p;
+    p.resize(4 + (with_bid ? 8 : 0) + 8 + slots.size() * 8);
+    char* q = p.data();
+    std::memcpy(q, &type, 4);
+    q += 4;
+    if (with_bid) {
+      std::memcpy(q, &bid, 8);
+      q += 8;
+    }
+    const uint32_t n = static_cast<uint32_t>(slots.size()), z = 0;
+    std::memcpy(q, &n, 4);
+    std::memcpy(q + 4, &z, 4);
+    q += 8;
+    if (!slots.empty()) std::memcpy(q, slots.data(), slots.size() * 8);
+    return send_frame(w, p);
+  }
+
+  // ------------------------------------------------------------------ slots / tasks
+  void free_slots(const std::vector<int64_t>& slots) {
+    if (slots.empty()) return;
+    std::vector<std::shared_ptr<SlotRing>> locals;
+    std::vector<RemotePart> parts;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      locals = local_rings_;
+      parts = remote_parts_;
+    }
+    for (auto& r : locals) r->free(slots);
+    for (const auto& p : parts) {
+      std::vector<int64_t> mine;
+      for (int64_t s : slots)
+        if (s >= p.base && s < p.base + p.len) mine.push_back(s);
+      if (mine.empty()) continue;
+      std::lock_guard<std::mutex> g(mu_);  // keeps the worker alive while its FREE frame is sent
+      auto it = workers_.find(p.rank);
+      if (it != workers_.end()) send_slots(*it->second, F_FREE, 0, mine, false);
+    }
+  }
+
+  std::vector<std::string> enqueue(const std::vector<int64_t>& slots, const std::string& trace) {
+    auto ids = store_->create_many(endpoint_, slots.size(), "created", trace);
+    const size_t sent = queue_->send_many(ids, slots);
+    if (sent < ids.size()) {  // backpressure / closed: CacheConnectorUpsert.cs:181-199
+      std::vector<std::string> rest(ids.begin() + static_cast<long>(sent), ids.end());
+      std::vector<int64_t> rs(slots.begin() + static_cast<long>(sent), slots.end());
+      store_->transition_many(rest, "failed", kPublishFailed);
+      free_slots(rs);
+      feed(rest);
+    }
+    return ids;
+  }
+
+  void feed(const std::vector<std::string>& ids) {
+    {
+      std::lock_guard<std::mutex> g(feed_mu_);
+      if (!feed_on_) return;
+      feed_.insert(feed_.end(), ids.begin(), ids.end());
+    }
+    feed_cv_.notify_all();
+  }
+
+  // Requeue (or dead-letter) items; returns ids that were dead-lettered (already failed).
+  void requeue(const std::vector<std::string>& ids, const std::vector<uint64_t>& seqs,
+               const std::vector<int64_t>& slots, double delay_s, const char* status) {
+    if (ids.empty()) return;
+    store_->transition_many(ids, "created", status);
+    std::vector<std::string> dead;
+    std::vector<int64_t> dead_slots;
+    for (size_t i = 0; i < seqs.size(); ++i) {
+      if (queue_->abandon(seqs[i], delay_s) == "deadlettered") {
+        dead.push_back(ids[i]);
+        dead_slots.push_back(slots[i]);
+      }
+    }
+    queue_->take_deadletters();  // drained here: the scheduler fails them itself
+    if (!dead.empty()) {
+      store_->transition_many(dead, "failed", kFailMaxRetries);
+      free_slots(dead_slots);
+      feed(dead);
+    }
+  }
+
+  void mark_dead(Worker& w, const char* why, bool report) {
+    if (!w.alive.exchange(false)) return;
+    std::unordered_map<uint64_t, Outstanding> out;
+    {
+      std::lock_guard<std::mutex> g(w.mu);
+      out.swap(w.out);
+      w.cv.notify_all();
+    }
+    for (auto& kv : out) requeue(kv.second.ids, kv.second.seqs, kv.second.slots, 0.0, kRequeued);
+    {
+      std::lock_guard<std::mutex> g(w.send_mu);
+      if (w.fd >= 0) ::shutdown(w.fd, SHUT_RDWR);
+    }
+    if (report) {
+      {
+        std::lock_guard<std::mutex> g(fail_mu_);
+        failed_.push_back(w.rank);
+        fail_reasons_.push_back(why);
+      }
+      fail_cv_.notify_all();
+    }
+  }
+
+  void join_worker(Worker& w) {
+    mark_dead(w, "joined", false);
+    if (w.dispatcher.joinable()) w.dispatcher.join();
+    if (w.reader.joinable()) w.reader.join();
+    std::lock_guard<std::mutex> g(w.send_mu);
+    if (w.fd >= 0) ::close(w.fd);
+    w.fd = -1;
+  }
+
+  // ------------------------------------------------------------------ threads
+  void dispatch_loop(Worker& w) {
+    while (w.alive) {
+      {
+        std::unique_lock<std::mutex> lk(w.mu);
+        cv_wait_s(w.cv, lk, 0.05, [&] {
+          return !w.alive || (w.ready && !w.draining && w.out.size() < static_cast<size_t>(cfg_.depth));
+        });
+        if (!w.alive) break;
+        if (w.ready && mono_now() - w.last_hb > cfg_.hb_timeout_s) {
+          lk.unlock();
+          mark_dead(w, "heartbeat timeout", true);
+          break;
+        }
+        if (!w.ready || w.draining || w.out.size() >= static_cast<size_t>(cfg_.depth)) continue;
+      }
+      if (queue_->closed()) {
+        std::this_thread::sleep_for(std::chrono::milliseconds(20));
+        continue;
+      }
+      auto msgs = queue_->receive(cfg_.max_batch, cfg_.poll_s, cfg_.linger_s);
+      if (msgs.empty()) continue;
+      Outstanding o;
+      std::vector<std::string> bad;
+      std::vector<uint64_t> bad_seqs;
+      o.ids.reserve(msgs.size());
+      o.seqs.reserve(msgs.size());
+      o.slots.reserve(msgs.size());
+      for (auto& m : msgs) {
+        // poison guard: a message without a valid payload slot (e.g. recovered after a restart
+        // with its ring slot gone) fails on its own instead of poisoning the batch
+        if (m.ref < 0 || m.ref >= ring_slots_) {
+          bad.push_back(m.task_id);
+          bad_seqs.push_back(m.seq);
+          continue;
+        }
+        o.ids.push_back(std::move(m.task_id));
+        o.seqs.push_back(m.seq);
+        o.slots.push_back(m.ref);
+      }
+      if (!bad.empty()) {
+        store_->transition_many(bad, "failed", kFailInvalid);
+        queue_->complete(bad_seqs);
+        feed(bad);
+      }
+      if (o.ids.empty()) continue;
+      store_->transition_many(o.ids, "running", "running");
+      {
+        std::lock_guard<std::mutex> g(hist_mu_);
+        size_t b = 0;
+        while ((size_t{1} << b) < o.ids.size() && b + 1 < hist_.size()) ++b;
+        ++hist_[b];
+      }
+      const uint64_t bid = next_bid_.fetch_add(1);
+      std::vector<int64_t> slots = o.slots;
+      bool died = false;
+      {
+        std::lock_guard<std::mutex> g(w.mu);
+        died = !w.alive;
+        if (!died) w.out.emplace(bid, std::move(o));
+      }
+      if (died) {  // died while we were receiving: hand the batch straight back
+        requeue(o.ids, o.seqs, o.slots, 0.0, kRequeued);
+        break;
+      }
+      if (!send_slots(w, F_BATCH, bid, slots, true)) {
+        mark_dead(w, "send failed", true);
+        break;
+      }
+    }
+  }
+
+  void reader_loop(Worker& w) {
+    std::string f;
+    while (true) {
+      if (!read_frame(w.fd, f)) {
+        if (w.alive) mark_dead(w, "connection lost", true);
+        return;
+      }
+      uint32_t type;
+      std::memcpy(&type, f.data(), 4);
+      const char* p = f.data() + 4;
+      const size_t len = f.size() - 4;
+      switch (type) {
+        case F_READY: {
+          std::lock_guard<std::mutex> g(w.mu);
+          if (len >= 8) {
+            int32_t pinned;
+            std::memcpy(&pinned, p + 4, 4);
+            w.pinned = pinned != 0;
+            w.info.assign(p + 8, len - 8);
+          }
+          w.ready = true;
+          w.last_hb = mono_now();
+          w.cv.notify_all();
+          break;
+        }
+        case F_HB: {
+          std::lock_guard<std::mutex> g(w.mu);
+          w.last_hb = mono_now();
+          if (len >= 40) {
+            std::memcpy(&w.hbm_used, p + 8, 8);
+            std::memcpy(&w.hbm_total, p + 16, 8);
+            std::memcpy(&w.gpu_busy_ms, p + 24, 8);
+          }
+          break;
+        }
+        case F_DONE:
+          on_done(w, p, len);
+          break;
+        case F_SUBMIT: {
+          uint32_t n;
+          std::memcpy(&n, p, 4);
+          std::vector<int64_t> slots(n);
+          if (n) std::memcpy(slots.data(), p + 8, n * 8ull);
+          enqueue(slots, std::string());
+          break;
+        }
+        case F_STAGE: {
+          uint64_t bid;
+          uint32_t stage;
+          std::memcpy(&bid, p, 8);
+          std::memcpy(&stage, p + 8, 4);
+          on_stage(w, bid, stage);
+          break;
+        }
+        default:
+          break;
+      }
+    }
+  }
+
+  void on_stage(Worker& w, uint64_t bid, uint32_t stage) {
+    std::vector<std::string> ids;
+    {
+      std::lock_guard<std::mutex> g(w.mu);
+      auto it = w.out.find(bid);
+      if (it == w.out.end()) return;
+      ids = it->second.ids;
+    }
+    std::string ep, st;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      if (stage >= stage_eps_.size()) return;
+      ep = stage_eps_[stage];
+      st = stage_status_[stage];
+    }
+    store_->retarget_many(ids, ep, st);
+  }
+
+  void on_done(Worker& w, const char* p, size_t len) {
+    if (len < 16 + 40) return;
+    uint64_t bid;
+    uint32_t n, row_bytes;
+    std::memcpy(&bid, p, 8);
+    std::memcpy(&n, p + 8, 4);
+    std::memcpy(&row_bytes, p + 12, 4);
+    auto res = std::make_shared<ResultBatch>();
+    std::memcpy(res->stage, p + 16, 40);
+    res->row_bytes = row_bytes;
+    res->worker = w.rank;
+    const char* status = p + 56;
+    const size_t spad = (static_cast<size_t>(n) + 7) / 8 * 8;
+    const size_t need = 56 + spad + static_cast<size_t>(n) * row_bytes;
+    Outstanding o;
+    {
+      std::lock_guard<std::mutex> g(w.mu);
+      auto it = w.out.find(bid);
+      if (it == w.out.end()) return;  // batch was already requeued (worker declared dead)
+      o = std::move(it->second);
+      w.out.erase(it);
+    }
+    if (len < need || n != o.ids.size()) {  // malformed: treat the batch as a model error
+      std::vector<uint8_t> none(o.ids.size(), 0);
+      store_->finish_many(o.ids, nullptr, none, "completed", kFailError);
+      queue_->complete(o.seqs);
+      free_slots(o.slots);
+      feed(o.ids);
+    } else {
+      res->data.assign(status + spad, static_cast<size_t>(n) * row_bytes);
+      std::vector<uint8_t> ok(n);
+      std::vector<std::string> done_ids, invalid, retry;
+      std::vector<uint64_t> done_seqs, retry_seqs;
+      std::vector<int64_t> free_s, retry_slots;
+      bool any_err = false;
+      for (uint32_t i = 0; i < n; ++i) {
+        const uint8_t s = static_cast<uint8_t>(status[i]);
+        if (s == IT_RETRY) {
+          retry.push_back(o.ids[i]);
+          retry_seqs.push_back(o.seqs[i]);
+          retry_slots.push_back(o.slots[i]);
+          continue;
+        }
+        ok[i] = s == IT_OK;
+        if (s == IT_INVALID) invalid.push_back(o.ids[i]);
+        if (s == IT_ERROR) any_err = true;
+        done_seqs.push_back(o.seqs[i]);
+        free_s.push_back(o.slots[i]);
+      }
+      std::shared_ptr<const ResultBatch> cres = res;
+      if (retry.empty()) {
+        store_->finish_many(o.ids, cres, ok, "completed", kFailError);
+      } else {  // finish only the non-retried items (retried ones keep their slot and message)
+        std::vector<std::string> fin;
+        std::vector<uint8_t> fok;
+        std::shared_ptr<ResultBatch> sub = std::make_shared<ResultBatch>();
+        *sub = *res;
+        sub->data.clear();
+        for (uint32_t i = 0; i < n; ++i) {
+          if (static_cast<uint8_t>(status[i]) == IT_RETRY) continue;
+          fin.push_back(o.ids[i]);
+          fok.push_back(ok[i]);
+          sub->data.append(res->data, static_cast<size_t>(i) * row_bytes, row_bytes);
+        }
+        store_->finish_many(fin, sub, fok, "completed", kFailError);
+      }
+      if (!invalid.empty()) store_->transition_many(invalid, "failed", kFailInvalid);
+      queue_->complete(done_seqs);
+      free_slots(free_s);
+      if (!retry.empty()) requeue(retry, retry_seqs, retry_slots, cfg_.retry_delay_s,
+                                  "Awaiting service availability. Batch failed; retrying.");
+      size_t nfail = 0;
+      for (uint32_t i = 0; i < n; ++i) nfail += status[i] == IT_INVALID || status[i] == IT_ERROR;
+      (void)any_err;
+      {
+        std::lock_guard<std::mutex> g(w.mu);
+        w.batches += 1;
+        w.images += n - retry.size() - nfail;
+        w.failed_items += nfail;
+        w.retried_items += retry.size();
+      }
+      images_done_.fetch_add(n - retry.size());
+      std::vector<std::string> fed;
+      fed.reserve(n);
+      for (uint32_t i = 0; i < n; ++i)
+        if (static_cast<uint8_t>(status[i]) != IT_RETRY) fed.push_back(o.ids[i]);
+      feed(fed);
+    }
+    w.cv.notify_all();
+  }
+
+  std::shared_ptr<TaskStore> store_;
+  std::shared_ptr<DispatchQueue> queue_;
+  std::string endpoint_;
+  int64_t ring_slots_;
+  SchedConfig cfg_;
+  std::mutex mu_;
+  std::map<int, std::unique_ptr<Worker>> workers_;
+  std::vector<std::shared_ptr<SlotRing>> local_rings_;
+  std::vector<RemotePart> remote_parts_;
+  std::vector<std::string> stage_eps_, stage_status_;
+  std::atomic<uint64_t> next_bid_{1};
+  std::atomic<uint64_t> images_done_{0};
+  std::mutex fail_mu_;
+  std::condition_variable fail_cv_;
+  std::vector<int> failed_;
+  std::vector<std::string> fail_reasons_;
+  bool stopped_ = false;
+  std::mutex feed_mu_;
+  std::condition_variable feed_cv_;
+  std::deque<std::string> feed_;
+  bool feed_on_ = false;
+  std::mutex hist_mu_;
+  std::vector<uint64_t> hist_;
+};
+
+}  // namespace ai4e
