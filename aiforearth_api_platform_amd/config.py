@@ -60,6 +60,9 @@ class Config:
     store_backend: str = field(default="native", metadata={"env": "AI4E_STORE_BACKEND"})  # native|python
     journal_path: str = field(default="", metadata={"env": "AI4E_JOURNAL"})
     finished_task_ttl_s: float = field(default=3600.0, metadata={"env": "AI4E_FINISHED_TASK_TTL_S"})
+    evict_period_s: float = field(default=10.0, metadata={"env": "AI4E_EVICT_PERIOD_S"})
+    # request bodies up to this size are journaled as the task's _ORIG body (replayed after a restart)
+    journal_payload_max_bytes: int = field(default=1 << 20, metadata={"env": "AI4E_JOURNAL_PAYLOAD_MAX_BYTES"})
     # --- metrics timers (TaskQueueLogger.cs:20 / TaskProcessLogger.cs:22) ---
     queue_logger_period_s: float = field(default=30.0, metadata={"env": "AI4E_QUEUE_LOGGER_PERIOD_S"})
     process_logger_period_s: float = field(default=300.0, metadata={"env": "AI4E_PROCESS_LOGGER_PERIOD_S"})
@@ -80,6 +83,12 @@ class Config:
     host: str = field(default="127.0.0.1", metadata={"env": "AI4E_HOST"})
     port: int = field(default=8080, metadata={"env": "AI4E_PORT"})
     routes_file: str = field(default="", metadata={"env": "AI4E_ROUTES"})
+    sync_timeout_s: float = field(default=120.0, metadata={"env": "AI4E_SYNC_TIMEOUT_S"})
+    # --- autoscaler (HPA analogue, autoscaler.yaml: min/max replicas, target CURRENT_REQUESTS per replica) ---
+    autoscale: bool = field(default=False, metadata={"env": "AI4E_AUTOSCALE"})
+    autoscale_min_workers: int = field(default=1, metadata={"env": "AI4E_AUTOSCALE_MIN"})
+    autoscale_target_per_worker: float = field(default=2.0, metadata={"env": "AI4E_AUTOSCALE_TARGET"})
+    autoscale_period_s: float = field(default=5.0, metadata={"env": "AI4E_AUTOSCALE_PERIOD_S"})
 
     @classmethod
     def load(cls, yaml_path: Optional[str] = None, env: Optional[Dict[str, str]] = None,

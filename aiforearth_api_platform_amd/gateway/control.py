@@ -40,6 +40,8 @@ class ControlPlane:
         self.push_transport: Optional[Callable[[str, str, str], bool]] = None
         self._timers: list = []
         self._stop = threading.Event()
+        # endpoint path -> fn(task_id, orig_body) that re-ingests a GPU task's payload after a restart
+        self._replayers: Dict[str, Callable[[str, Optional[str]], bool]] = {}
 
     # ------------------------------------------------------------------ queues
     def queue_for(self, endpoint: str):
@@ -129,28 +131,42 @@ class ControlPlane:
         return (200, v) if v is not None else (204, None)
 
     # ------------------------------------------------------------------ restart recovery
+    def register_replayer(self, endpoint: str, fn: Callable[[str, Optional[str]], bool]) -> None:
+        """A GPU model endpoint's payloads live in the payload ring, which does not survive a restart:
+        its tasks are recovered by re-ingesting the journaled ``_ORIG`` body (``fn``)."""
+        self._replayers[APITask(Endpoint=endpoint).EndpointPath] = fn
+
     def recover(self, journal_path: Optional[str] = None) -> Dict[str, int]:
         """Replay a task journal and re-enqueue unfinished work (survey §5.4).
 
-        Tasks that were ``created`` or ``running`` when the process died are re-published to their
-        endpoint queue with their original body (``{TaskId}_ORIG``), like a Service Bus redelivery;
-        finished tasks stay queryable. Returns counts.
+        Tasks that were ``created`` or ``running`` when the process died are re-published with their
+        original body (``{TaskId}_ORIG``), like a Service Bus redelivery. For GPU model endpoints the
+        body is re-ingested into a fresh payload-ring slot by the endpoint's replayer; a task whose
+        payload was not journaled is failed with a reason ("Task failed - payload lost on restart"),
+        never requeued without a payload. Finished tasks stay queryable. Returns counts.
         """
         path = journal_path or self.cfg.journal_path
         n = self.store.replay(path) if path else 0
-        requeued = 0
+        requeued = failed = 0
         for suffix in ("_created", "_running"):
             for key in self.store.keys_with_suffix(suffix):
                 for tid in self.store.zrange(key):
                     rec = self.store.get_record(tid)
                     if rec is None or not rec["PublishToGrid"]:
                         continue
-                    body = self.store.get_orig_body(tid) or ""
+                    body = self.store.get_orig_body(tid)
+                    replay = self._replayers.get(rec["EndpointPath"])
+                    if replay is not None:
+                        if replay(tid, body):
+                            requeued += 1
+                        else:
+                            failed += 1
+                        continue
                     self.store.upsert(tid, "created - requeued after restart", STATE_CREATED, rec["Endpoint"],
                                       None, True)
-                    if self.queue_for(rec["Endpoint"]).send(tid, -1, body):
+                    if self.queue_for(rec["Endpoint"]).send(tid, -1, body or ""):
                         requeued += 1
-        return {"replayed": n, "requeued": requeued}
+        return {"replayed": n, "requeued": requeued, "failed": failed}
 
     # ------------------------------------------------------------------ queue-depth metrics
     def log_queue_lengths(self, suffix: str, adjust: int = 0) -> Dict[str, int]:
@@ -179,7 +195,13 @@ class ControlPlane:
             for s in ("_completed", "_running", "_failed"):
                 self.log_queue_lengths(s)
 
-        for period, fn in ((self.cfg.queue_logger_period_s, created), (self.cfg.process_logger_period_s, processed)):
+        def evict():  # bounded store: finished tasks older than the TTL (and their results) are dropped
+            n = self.store.evict_finished(self.cfg.finished_task_ttl_s)
+            if n:
+                REGISTRY.counter("tasks_evicted_total").inc(n)
+
+        for period, fn in ((self.cfg.queue_logger_period_s, created), (self.cfg.process_logger_period_s, processed),
+                           (self.cfg.evict_period_s, evict)):
             t = threading.Thread(target=loop, args=(period, fn), daemon=True, name="ai4e-metric-timer")
             t.start()
             self._timers.append(t)

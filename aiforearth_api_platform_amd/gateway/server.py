@@ -8,14 +8,20 @@ Routes (all served by one aiohttp application):
   (``APIManagement/request_policy.xml:5-28``; ``500 "Task insert failed."`` on failure); ``sync``
   routes proxy to the backend and return its response (``request_backend_policy.xml``).
 * ``GET /v1/taskmanagement/task/{taskId}`` — task status, verbatim store JSON or ``204``
-  (``task_management_policy.xml`` -> ``CacheConnectorGet``); ``.../result`` returns the model output.
+  (``task_management_policy.xml`` -> ``CacheConnectorGet``); ``.../result`` returns the model output,
+  ``.../trace`` the per-stage timeline (accept -> batch -> worker -> GPU -> complete) + B3 ids.
+* Binary batch ingest: an async model route accepts ``Content-Type: application/x-ai4e-batch`` with
+  ``n`` raw uint8 payloads back to back and answers ``{"TaskIds": [...]}`` (one copy per request into
+  the payload ring; the high-rate client path).
 * ``POST /v1/cache/upsert``, ``GET /v1/cache/get?taskId=`` — CacheConnectorUpsert / Get.
 * ``POST /v1/requests/upsert``, ``POST /v1/requests/get`` — RequestReporter (CURRENT_REQUESTS).
 * ``POST /v1/backend/webhook`` — BackendWebhook incl. the Event Grid validation handshake.
 * ``GET /metrics`` (Prometheus text), ``GET /v1/platform/stats`` (JSON), ``GET /`` health.
 
 Admission control per route mirrors ``APIService.before_request`` (429 busy, 503 draining,
-401 content type, 413 too large).
+401 content type, 413 too large); undecodable payloads get 400 (415 for unknown media types) and
+no task; a sync request that outlives ``sync_timeout_s`` gets 504. B3 headers
+(``x-b3-traceid``/``spanid``) are read or created, stored with the task and echoed back.
 """
 from __future__ import annotations
 
@@ -30,9 +36,11 @@ from aiohttp import ClientSession, web
 from ..store import APITask
 from ..store.pystore import absolute_path
 from ..utils.metrics import REGISTRY
+from ..utils.tracing import StageClock, b3_from_headers, b3_pack, b3_unpack
 from .control import ControlPlane
 
 TASK_INSERT_FAILED = "Task insert failed."
+BATCH_CONTENT_TYPE = "application/x-ai4e-batch"
 
 
 @dataclass
@@ -99,6 +107,7 @@ class Gateway:
         self.app.router.add_get("/v1/platform/stats", self.stats)
         self.app.router.add_get("/v1/taskmanagement/task/{taskId}", self.task_get)
         self.app.router.add_get("/v1/taskmanagement/task/{taskId}/result", self.task_result)
+        self.app.router.add_get("/v1/taskmanagement/task/{taskId}/trace", self.task_trace)
         self.app.router.add_post("/v1/cache/upsert", self.cache_upsert)
         self.app.router.add_get("/v1/cache/get", self.cache_get)
         self.app.router.add_post("/v1/requests/upsert", self.requests_upsert)
@@ -117,10 +126,43 @@ class Gateway:
     async def metrics(self, request):
         for s in ("_created", "_running", "_completed", "_failed"):
             self.cp.log_queue_lengths(s, adjust=0)
+        self.collect_backend_metrics()
         return web.Response(text=REGISTRY.prometheus_text(), content_type="text/plain")
 
     async def stats(self, request):
-        return web.json_response({"control_plane": self.cp.stats(), "metrics": REGISTRY.snapshot()})
+        self.collect_backend_metrics()
+        return web.json_response({"control_plane": self.cp.stats(), "metrics": REGISTRY.snapshot(),
+                                  "backends": self.backend_stats()})
+
+    def _backends(self):
+        seen = []
+        for r in self.routes.routes:
+            if r.backend is not None and hasattr(r.backend, "submit") and r.backend not in seen:
+                seen.append(r.backend)
+        return seen
+
+    def backend_stats(self) -> dict:
+        out = {}
+        for be in self._backends():
+            st = getattr(getattr(be, "worker", None), "stats", None)
+            if callable(st):
+                out[be.path] = st()
+        return out
+
+    def collect_backend_metrics(self) -> None:
+        """Per-GPU gauges from the worker pools' heartbeats (survey §5.5): HBM used/total, GPU busy ms,
+        images, batches, in-flight batches; the batch-size histogram comes from the native scheduler."""
+        for path, st in self.backend_stats().items():
+            for w in st.get("workers", []):
+                tag = f"{path}/gpu{w.get('rank')}"
+                for k in ("hbm_used", "hbm_total", "gpu_busy_ms", "images", "batches", "outstanding",
+                          "failed_items", "retried_items"):
+                    if k in w:
+                        REGISTRY.gauge(f"{k}{tag}").set(float(w[k]))
+            for i, c in enumerate(st.get("batch_histogram", [])):
+                REGISTRY.gauge(f"batch_size_le_{1 << i}{path}").set(float(c))
+            for k, v in (st.get("xgmi") or {}).items():
+                REGISTRY.gauge(f"xgmi_{k}{path}").set(float(v))
 
     async def task_get(self, request):
         code, body = self.cp.get(request.match_info["taskId"])
@@ -128,15 +170,32 @@ class Gateway:
             return web.Response(status=code)
         return web.Response(text=body, content_type="application/json")
 
+    def _backend_for_task(self, tid: str):
+        rec = self.cp.get_dict(tid)
+        if rec is None:
+            return None, None
+        for be in self._backends():
+            if getattr(be, "path", None) == rec["EndpointPath"] or getattr(be, "endpoint", None) == rec["Endpoint"]:
+                return rec, be
+        return rec, None
+
     async def task_result(self, request):
         tid = request.match_info["taskId"]
-        for r in self.routes.routes:
-            res = getattr(r.backend, "result", None)
-            if callable(res):
-                out = res(tid)
-                if out is not None:
-                    return web.json_response({"TaskId": tid, "Result": out})
+        rec, be = self._backend_for_task(tid)
+        if be is not None:
+            out = await asyncio.get_running_loop().run_in_executor(None, be.result, tid)
+            if out is not None:
+                return web.json_response({"TaskId": tid, "Result": out})
         return web.Response(status=204)
+
+    async def task_trace(self, request):
+        tid = request.match_info["taskId"]
+        tr = self.cp.store.trace(tid)
+        if tr is None:
+            return web.Response(status=204)
+        out = dict(tr, **StageClock.from_trace(tr).to_dict())
+        out.update(b3_unpack(tr.get("trace", "")))
+        return web.json_response(out)
 
     async def cache_upsert(self, request):
         code, body = self.cp.upsert(await request.read())
@@ -198,23 +257,41 @@ class Gateway:
         finally:
             route.inflight -= 1
 
+    @staticmethod
+    def _payload_error(e: Exception) -> Optional[web.Response]:
+        from ..runtime.model_endpoint import PayloadError
+
+        if isinstance(e, PayloadError):
+            return web.json_response({"message": str(e)}, status=getattr(e, "status", 400))
+        return None
+
     async def _async(self, route: Route, request, body: bytes):
         loop = asyncio.get_running_loop()
         target = route.target_path(request.path)
         upstream_id = request.headers.get("taskId", "")
+        b3 = b3_from_headers(request.headers)
+        trace = b3_pack(b3)
         try:
             if hasattr(route.backend, "submit"):
-                js = await loop.run_in_executor(None, route.backend.submit, body, request.content_type, upstream_id)
+                if request.content_type == BATCH_CONTENT_TYPE:
+                    ids = await loop.run_in_executor(None, route.backend.submit_raw_batch, body, trace)
+                    return web.json_response({"TaskIds": ids}, headers=b3)
+                js = await loop.run_in_executor(
+                    None, lambda: route.backend.submit(body, request.content_type, upstream_id, None, trace))
             else:
                 js = await loop.run_in_executor(None, self.cp.create_async_task, self.base_url + target,
                                                 body.decode("utf-8", "replace"))
+                self.cp.store.set_trace(json.loads(js)["TaskId"], trace)
         except Exception as e:
+            rej = self._payload_error(e)
+            if rej is not None:
+                return rej
             self.cp.log.log_error(f"{TASK_INSERT_FAILED} {e}", request.path)
             return web.Response(status=500, text=TASK_INSERT_FAILED)
         if "application/json" in request.headers.get("Accept", "application/json") or "*/*" in request.headers.get(
                 "Accept", ""):
-            return web.Response(text=js, content_type="application/json")
-        return web.Response(text="TaskId: " + json.loads(js)["TaskId"])
+            return web.Response(text=js, content_type="application/json", headers=b3)
+        return web.Response(text="TaskId: " + json.loads(js)["TaskId"], headers=b3)
 
     async def _sync(self, route: Route, request, body: bytes):
         loop = asyncio.get_running_loop()
@@ -225,9 +302,20 @@ class Gateway:
             def done(tid, _f=fut):
                 loop.call_soon_threadsafe(lambda: _f.done() or _f.set_result(tid))
 
-            js = await loop.run_in_executor(None, lambda: be.submit(body, request.content_type, "", done))
+            trace = b3_pack(b3_from_headers(request.headers))
+            try:
+                js = await loop.run_in_executor(None, lambda: be.submit(body, request.content_type, "", done, trace))
+            except Exception as e:
+                rej = self._payload_error(e)
+                if rej is not None:
+                    return rej
+                raise
             tid = json.loads(js)["TaskId"]
-            await fut
+            try:
+                await asyncio.wait_for(fut, timeout=self.cp.cfg.sync_timeout_s)
+            except asyncio.TimeoutError:
+                return web.json_response({"TaskId": tid, "message": "Task did not finish in time; poll "
+                                          f"/v1/taskmanagement/task/{tid}"}, status=504)
             rec = self.cp.get_dict(tid)
             if rec is None or rec["BackendStatus"] != "completed":
                 return web.json_response(rec or {"TaskId": tid, "Status": "failed"}, status=500)

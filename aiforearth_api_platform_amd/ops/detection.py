@@ -314,3 +314,44 @@ def crop_resize_nhwc(img_u8: torch.Tensor, boxes: torch.Tensor, out_hw=(224, 224
                   out.data_ptr(), norm.data_ptr(), H, W, C, R, out_hw[0], out_hw[1], 0, _ext.stream_ptr(img_u8.device))
         return out
     return crop_resize_reference(img_u8.cpu(), boxes.cpu(), out_hw, mean, std)
+
+
+def crop_resize_u8_reference(img_u8: torch.Tensor, boxes: torch.Tensor, out_hw: Tuple[int, int]) -> torch.Tensor:
+    """fp32 reference of :func:`crop_resize_u8` (same sampling grid as the normalized variant)."""
+    n, H, W, C = img_u8.shape
+    OH, OW = out_hw
+    out = torch.zeros(boxes.shape[0], OH, OW, C, dtype=torch.uint8)
+    for r in range(boxes.shape[0]):
+        b = boxes[r].float().cpu()
+        i = int(b[0])
+        sx = (b[1] + (torch.arange(OW) + 0.5) * (b[3] - b[1]) / OW - 0.5).clamp(0, W - 1)
+        sy = (b[2] + (torch.arange(OH) + 0.5) * (b[4] - b[2]) / OH - 0.5).clamp(0, H - 1)
+        yy, xx = torch.meshgrid(sy, sx, indexing="ij")
+        y0, x0 = yy.floor().long(), xx.floor().long()
+        y1, x1 = (y0 + 1).clamp(max=H - 1), (x0 + 1).clamp(max=W - 1)
+        ly, lx = (yy - y0)[..., None], (xx - x0)[..., None]
+        f = img_u8[i].float().cpu()
+        pix = (1 - ly) * ((1 - lx) * f[y0, x0] + lx * f[y0, x1]) + ly * ((1 - lx) * f[y1, x0] + lx * f[y1, x1])
+        out[r] = (pix + 0.5).clamp(0, 255).to(torch.uint8)
+    return out
+
+
+def crop_resize_u8(img_u8: torch.Tensor, boxes: torch.Tensor, out_hw=(224, 224)) -> torch.Tensor:
+    """Crop boxes [R,5]=(img,x1,y1,x2,y2) from uint8 NHWC images and bilinear-resize -> uint8
+    [R, OH, OW, C] (K5/K7). The ensemble's detector->classifier wire format: 3 bytes per pixel."""
+    n, H, W, C = img_u8.shape
+    R = boxes.shape[0]
+    if _ext.backend_for(img_u8) == "hip":
+        out = torch.empty(R, out_hw[0], out_hw[1], C, device=img_u8.device, dtype=torch.uint8)
+        _ext.call("ai4e_crop_resize_nhwc", img_u8.contiguous().data_ptr(), boxes.float().contiguous().data_ptr(),
+                  out.data_ptr(), 0, H, W, C, R, out_hw[0], out_hw[1], 1, _ext.stream_ptr(img_u8.device))
+        return out
+    return crop_resize_u8_reference(img_u8, boxes, out_hw).to(img_u8.device)
+
+
+def resize_u8(img_u8: torch.Tensor, out_hw: Tuple[int, int]) -> torch.Tensor:
+    """Bilinear resize of uint8 NHWC images on the GPU (K7): one whole-image box per image."""
+    n, H, W, _ = img_u8.shape
+    boxes = torch.tensor([[i, 0.0, 0.0, float(W), float(H)] for i in range(n)], dtype=torch.float32,
+                         device=img_u8.device)
+    return crop_resize_u8(img_u8, boxes, out_hw)

@@ -10,6 +10,7 @@ previous batch computes; only the top-k result (a few bytes per image) is copied
 from __future__ import annotations
 
 import threading
+import time
 from dataclasses import dataclass
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
@@ -82,50 +83,72 @@ class _DoneEvent:
 
 @dataclass
 class BatchResult:
-    top_idx: torch.Tensor    # [b, k] int32 (pinned host)
-    top_prob: torch.Tensor   # [b, k] fp32 (pinned host)
-    done: torch.cuda.Event
+    outputs: List[torch.Tensor]  # per output: [n, ...] (pinned host views, valid after done)
+    done: "torch.cuda.Event"
     n: int
+    t_launch: float = 0.0        # host CLOCK_MONOTONIC at launch
+    ev_copy0: Optional["torch.cuda.Event"] = None
+    ev_copy1: Optional["torch.cuda.Event"] = None
+
+    @property
+    def top_idx(self) -> torch.Tensor:
+        return self.outputs[0]
+
+    @property
+    def top_prob(self) -> torch.Tensor:
+        return self.outputs[1]
+
+    def gpu_ms(self) -> Tuple[float, float]:
+        """(H2D copy ms, copy-end -> outputs-ready ms) once ``done`` has fired (0, 0 without timing)."""
+        if self.ev_copy0 is None:
+            return 0.0, 0.0
+        return self.ev_copy0.elapsed_time(self.ev_copy1), self.ev_copy1.elapsed_time(self.done)
 
 
 class InferenceEngine:
-    """Runs ``model_fn(u8 [b,H,W,C] on device) -> logits [b, classes]`` with graphs + 2-deep buffering."""
+    """Runs ``output_fn(u8 [b,H,W,C] on device) -> tuple of [b, ...] tensors`` with HIP graphs and
+    3-deep buffering. Without ``output_fn`` the engine is a classifier: ``head_fn`` (a fused top-k,
+    e.g. ``FusedResNet.topk_u8``) or softmax/top-k over ``model_fn``'s logits."""
 
-    def __init__(self, model_fn: Callable[[torch.Tensor], torch.Tensor], item_shape: Sequence[int], max_batch: int,
-                 device: Optional[torch.device] = None, topk: int = 5, use_graphs: bool = True, nbuf: int = 3,
-                 buckets: Optional[Sequence[int]] = None,
-                 head_fn: Optional[Callable[[torch.Tensor, int], Tuple[torch.Tensor, torch.Tensor]]] = None):
+    def __init__(self, model_fn: Optional[Callable[[torch.Tensor], torch.Tensor]], item_shape: Sequence[int],
+                 max_batch: int, device: Optional[torch.device] = None, topk: int = 5, use_graphs: bool = True,
+                 nbuf: int = 3, buckets: Optional[Sequence[int]] = None,
+                 head_fn: Optional[Callable[[torch.Tensor, int], Tuple[torch.Tensor, torch.Tensor]]] = None,
+                 output_fn: Optional[Callable[[torch.Tensor], Sequence[torch.Tensor]]] = None, timing: bool = False):
         self.model_fn = model_fn
-        self.head_fn = head_fn  # optional images -> (top-k idx int32, prob fp32), e.g. FusedResNet.topk_u8
+        self.head_fn = head_fn
+        self.output_fn = output_fn
         self.device = torch.device(device or "cuda")
         self.item_shape = tuple(item_shape)
         self.max_batch = max_batch
         self.topk = topk
         self.use_graphs = use_graphs and self.device.type == "cuda"
+        self.timing = timing and self.device.type == "cuda"
         self.nbuf = nbuf
         self.buckets = sorted(set(buckets or [max_batch]))
         if self.buckets[-1] != max_batch:
             self.buckets.append(max_batch)
-        self.copy_stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
-        self.compute_stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
+        cuda = self.device.type == "cuda"
+        self.copy_stream = torch.cuda.Stream(self.device) if cuda else None
+        self.compute_stream = torch.cuda.Stream(self.device) if cuda else None
         self.inputs = [torch.empty((max_batch, *self.item_shape), dtype=torch.uint8, device=self.device)
                        for _ in range(nbuf)]
-        pin = self.device.type == "cuda"
-        self.h_idx = [torch.empty((max_batch, topk), dtype=torch.int32, pin_memory=pin) for _ in range(nbuf)]
-        self.h_prob = [torch.empty((max_batch, topk), dtype=torch.float32, pin_memory=pin) for _ in range(nbuf)]
+        self.host_out: List[List[torch.Tensor]] = [[] for _ in range(nbuf)]  # allocated at warmup
         self.graphs: Dict[Tuple[int, int], torch.cuda.CUDAGraph] = {}
-        self._graph_out: Dict[Tuple[int, int], Tuple[torch.Tensor, torch.Tensor]] = {}
+        self._graph_out: Dict[Tuple[int, int], Tuple[torch.Tensor, ...]] = {}
         self.compute_done: List[Optional[torch.cuda.Event]] = [None] * nbuf
         self._k = 0
 
     # -------------------------------------------------------------- forward
-    def _forward_into(self, buf: int, b: int):
+    def _forward_into(self, buf: int, b: int) -> Tuple[torch.Tensor, ...]:
+        x = self.inputs[buf][:b]
+        if self.output_fn is not None:
+            return tuple(self.output_fn(x))
         if self.head_fn is not None:
-            i, p = self.head_fn(self.inputs[buf][:b], self.topk)
+            i, p = self.head_fn(x, self.topk)
             return i, p
-        logits = self.model_fn(self.inputs[buf][:b])
-        prob = torch.softmax(logits.float(), dim=1)
-        p, i = torch.topk(prob, self.topk, dim=1)
+        logits = self.model_fn(x)
+        p, i = torch.topk(torch.softmax(logits.float(), dim=1), self.topk, dim=1)
         return i.to(torch.int32), p
 
     def bucket_for(self, n: int) -> int:
@@ -133,6 +156,12 @@ class InferenceEngine:
             if b >= n:
                 return b
         raise ValueError(f"batch {n} > max_batch {self.max_batch}")
+
+    def _alloc_host(self, outs: Sequence[torch.Tensor]) -> None:
+        pin = self.device.type == "cuda"
+        for buf in range(self.nbuf):
+            self.host_out[buf] = [torch.empty((self.max_batch, *o.shape[1:]), dtype=o.dtype, pin_memory=pin)
+                                  for o in outs]
 
     def warmup(self) -> None:
         """Run every (bucket, buffer) once eagerly (kernel load / allocator warm) then capture graphs."""
@@ -142,26 +171,30 @@ class InferenceEngine:
             for buf in range(self.nbuf):
                 self.inputs[buf].zero_()
                 for b in self.buckets:
-                    self._forward_into(buf, b)
+                    outs = self._forward_into(buf, b)
         torch.cuda.synchronize(self.device)
+        self._alloc_host(outs)
         if not self.use_graphs:
             return
         for buf in range(self.nbuf):
             for b in self.buckets:
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g, stream=self.compute_stream):
-                    i, p = self._forward_into(buf, b)
+                    outs = self._forward_into(buf, b)
                 self.graphs[(buf, b)] = g
-                self._graph_out[(buf, b)] = (i, p)
+                self._graph_out[(buf, b)] = outs
         torch.cuda.synchronize(self.device)
 
     # -------------------------------------------------------------- submit
     def submit(self, host_src: torch.Tensor, slots: Sequence[int]) -> BatchResult:
         """Copy ``host_src[slots]`` to the next device buffer, run, and return an async result."""
         n = len(slots)
+        t_launch = time.monotonic()
         if self.device.type != "cuda":  # CPU path (tests / CPU-only hosts): synchronous
-            idx, prob = self.run_sync(host_src[list(slots)])
-            return BatchResult(idx, prob, _DoneEvent(), n)
+            outs = self.run_sync(host_src[list(slots)])
+            return BatchResult(list(outs), _DoneEvent(), n, t_launch)
+        if not self.host_out[0]:
+            raise RuntimeError("InferenceEngine.warmup() must run before submit() on a GPU")
         buf = self._k % self.nbuf
         self._k += 1
         b = self.bucket_for(n)
@@ -171,33 +204,39 @@ class InferenceEngine:
         # (only the batch that last used this buffer; the previous batch keeps computing)
         if self.compute_done[buf] is not None:
             cs.wait_event(self.compute_done[buf])
+        ev0 = ev1 = None
+        if self.timing:
+            ev0 = torch.cuda.Event(enable_timing=True)
+            ev0.record(cs)
         with torch.cuda.stream(cs):
             for dst, src, ln in contiguous_runs(list(slots)):
                 dev_in[dst:dst + ln].copy_(host_src[src:src + ln], non_blocking=True)
-        ev = torch.cuda.Event()
+        ev = torch.cuda.Event(enable_timing=self.timing)
         ev.record(cs)
+        if self.timing:
+            ev1 = ev
         st = self.compute_stream
         st.wait_event(ev)
         with torch.cuda.stream(st):
             if self.use_graphs and (buf, b) in self.graphs:
                 self.graphs[(buf, b)].replay()
-                i, p = self._graph_out[(buf, b)]
+                outs = self._graph_out[(buf, b)]
             else:
-                i, p = self._forward_into(buf, b)
-            self.h_idx[buf][:n].copy_(i[:n], non_blocking=True)
-            self.h_prob[buf][:n].copy_(p[:n], non_blocking=True)
-            done = torch.cuda.Event()
+                outs = self._forward_into(buf, b)
+            host = self.host_out[buf]
+            for h, o in zip(host, outs):
+                h[:n].copy_(o[:n], non_blocking=True)
+            done = torch.cuda.Event(enable_timing=self.timing)
             done.record(st)
         self.compute_done[buf] = done
-        return BatchResult(self.h_idx[buf][:n], self.h_prob[buf][:n], done, n)
+        return BatchResult([h[:n] for h in self.host_out[buf]], done, n, t_launch, ev0, ev1)
 
-    def run_sync(self, images_u8: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    def run_sync(self, images_u8: torch.Tensor) -> Tuple[torch.Tensor, ...]:
         """Convenience (sync API / tests): images already on host or device."""
         if self.device.type != "cuda":
-            logits = self.model_fn(images_u8)
-            p, i = torch.topk(torch.softmax(logits.float(), 1), self.topk, 1)
-            return i.to(torch.int32), p
+            self.inputs[0][: images_u8.shape[0]].copy_(images_u8)
+            return tuple(o.cpu() for o in self._forward_into(0, images_u8.shape[0]))
         host = images_u8.cpu().pin_memory() if not images_u8.is_pinned() else images_u8
         res = self.submit(host, list(range(images_u8.shape[0])))
         res.done.synchronize()
-        return res.top_idx.clone(), res.top_prob.clone()
+        return tuple(o.clone() for o in res.outputs)

@@ -1,0 +1,293 @@
+"""GPU worker process body: one process per MI355X, driven by the native NodeScheduler.
+
+Replaces the reference's model container behind ``BackendQueueProcessor``
+(``APIs/1.0/base-py/ai4e_service.py:180-213`` thread-per-request execution, fed by
+``BackendQueueProcessor.cs:48-52`` HTTP POSTs): the worker maps the node's shared payload ring,
+registers it as pinned host memory (``hipHostRegister``) so the H2D DMA reads request bytes where
+the ingest wrote them, captures the model once per batch bucket in HIP graphs, and then only
+executes BATCH frames (slot lists) and answers with DONE frames (item-major result rows).
+
+Per-item isolation (survey §5.3, poison messages): slots outside the ring fail as invalid payloads
+on their own; if a batch launch raises, the worker re-runs its items one by one, so only the items
+that fail on their own are reported failed — the rest of the batch completes.
+
+Fault injection (``AI4E_FAULT_INJECTION``, comma list, ``key=value[@rank]``):
+``exit_after=<batches>``, ``hang_after=<batches>``, ``delay_ms=<ms>``, ``fail_batch=<batch index>``
+(the launch of that batch raises; drives the isolation path), ``fail_item=<slot>`` (the isolated run
+of that slot raises -> that item fails).
+"""
+from __future__ import annotations
+
+import importlib
+import os
+import queue
+import threading
+import time
+from dataclasses import dataclass, field
+from typing import Any, Dict, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from . import protocol as P
+from .servable import as_servable, encode_rows, row_bytes
+
+
+@dataclass
+class ModelSpec:
+    factory: str                      # "package.module:function" -> Servable or logits model
+    item_shape: Tuple[int, ...]
+    max_batch: int = 250  # whole waves of workgroups on 256 CUs for ResNet-50 (bench.py)
+    topk: int = 5
+    kwargs: Dict[str, Any] = field(default_factory=dict)
+    use_graphs: bool = True
+    buckets: Tuple[int, ...] = ()      # captured batch sizes (config.bucket_list); () = max_batch only
+
+
+def load_factory(path: str):
+    mod, fn = path.split(":")
+    return getattr(importlib.import_module(mod), fn)
+
+
+def parse_fault(rank: int) -> Dict[str, int]:
+    out = {}
+    for item in filter(None, os.environ.get("AI4E_FAULT_INJECTION", "").split(",")):
+        k, v = item.split("=")
+        tgt = None
+        if "@" in v:
+            v, tgt = v.split("@")
+        if tgt is None or int(tgt) == rank:
+            out[k.strip()] = int(v)
+    return out
+
+
+def attach_ring(shm_name: str, nslots: int, item_shape: Sequence[int], untrack: bool = False):
+    """Map the node's payload ring. Processes with their own resource tracker (torchrun ranks) must
+    ``untrack`` it, or their tracker unlinks the owner's segment when they exit; spawned children
+    share the owner's tracker and must not."""
+    from multiprocessing import resource_tracker, shared_memory
+
+    shm = shared_memory.SharedMemory(name=shm_name)
+    if untrack:
+        try:
+            resource_tracker.unregister(shm._name, "shared_memory")  # type: ignore[attr-defined]
+        except Exception:
+            pass
+    nbytes = int(nslots) * int(np.prod(item_shape))
+    buf = torch.frombuffer(shm.buf, dtype=torch.uint8, count=nbytes).view(int(nslots), *item_shape)
+    return shm, buf
+
+
+def pin_host(buf: torch.Tensor) -> bool:
+    """Register the mapped ring as pinned host memory for direct DMA (hipHostRegister)."""
+    try:
+        rc = torch.cuda.cudart().cudaHostRegister(buf.data_ptr(), buf.numel(), 0)
+        return (int(rc[0]) if isinstance(rc, tuple) else int(rc)) == 0
+    except Exception:
+        return False
+
+
+class _Pending:
+    __slots__ = ("bid", "n", "valid", "res", "t_recv", "status")
+
+    def __init__(self, bid, n, valid, res, t_recv, status):
+        self.bid, self.n, self.valid, self.res, self.t_recv, self.status = bid, n, valid, res, t_recv, status
+
+
+class GpuWorker:
+    """The loop of one worker process (also usable in a thread for tests)."""
+
+    def __init__(self, conn: P.FrameConn, rank: int, device: str, spec: ModelSpec, ring_buf: torch.Tensor,
+                 local_ring=None, hb_interval: float = 0.5, depth: int = 2):
+        self.conn = conn
+        self.rank = rank
+        self.device = torch.device(device)
+        self.spec = spec
+        self.buf = ring_buf
+        self.nslots = ring_buf.shape[0]
+        self.local_ring = local_ring  # native SlotRing of this process's ingest partition (FREE frames)
+        self.hb_interval = hb_interval
+        self.depth = depth
+        self.fault = parse_fault(rank)
+        self.servable = as_servable(load_factory(spec.factory)(device=device, **spec.kwargs), spec.topk)
+        from .engine import InferenceEngine
+
+        self.engine = InferenceEngine(None, spec.item_shape, spec.max_batch, device=self.device,
+                                      use_graphs=spec.use_graphs, buckets=list(spec.buckets) or None,
+                                      output_fn=self.servable, timing=self.device.type == "cuda")
+        self.engine.warmup()
+        self.row_bytes = row_bytes(self.servable.outputs)
+        self.batches = 0
+        self.busy_ms = 0.0
+        self.alive = threading.Event()
+        self.alive.set()
+
+    # ------------------------------------------------------------------ lifecycle
+    def info(self) -> dict:
+        d = self.servable.describe()
+        d.update(device=str(self.device), max_batch=self.spec.max_batch, buckets=list(self.engine.buckets),
+                 pid=os.getpid())
+        if self.device.type == "cuda":
+            d["gpu"] = torch.cuda.get_device_name(self.device)
+        return d
+
+    def _heartbeat(self) -> None:
+        while self.alive.is_set():
+            used = total = 0
+            if self.device.type == "cuda":
+                try:
+                    free, total = torch.cuda.mem_get_info(self.device)
+                    used = total - free
+                except Exception:
+                    pass
+            try:
+                self.conn.heartbeat(time.monotonic(), used, total, self.busy_ms, self.batches)
+            except (BrokenPipeError, EOFError, OSError):
+                return
+            time.sleep(self.hb_interval)
+
+    def serve(self, pinned: bool = False) -> None:
+        """Main thread: read frames and launch batches; a completion thread retires them in order
+        (blocking event waits, no polling), so a DONE frame leaves as soon as its GPU work ends."""
+        threading.Thread(target=self._heartbeat, daemon=True, name=f"ai4e-hb-{self.rank}").start()
+        self._done_q: "queue.Queue[Optional[_Pending]]" = queue.Queue()
+        self._idle = threading.Condition()
+        self._inflight = 0
+        fin = threading.Thread(target=self._completion_loop, daemon=True, name=f"ai4e-done-{self.rank}")
+        fin.start()
+        self.conn.ready(self.rank, pinned, self.info())
+        try:
+            while True:
+                try:
+                    buf = self.conn.recv()
+                except (EOFError, OSError):
+                    break
+                t = P.frame_type(buf)
+                if t == P.F_BATCH:
+                    self._on_batch(buf)
+                elif t == P.F_FREE:
+                    if self.local_ring is not None:
+                        self.local_ring.free(P.parse_slots(buf).tolist())
+                elif t == P.F_STOP:
+                    break
+        finally:
+            self._done_q.put(None)
+            fin.join(60)
+            self.alive.clear()
+
+    def _completion_loop(self) -> None:
+        while True:
+            p = self._done_q.get()
+            if p is None:
+                return
+            try:
+                self._finalize(p)
+            except (BrokenPipeError, EOFError, OSError):
+                pass
+            with self._idle:
+                self._inflight -= 1
+                self._idle.notify_all()
+
+    def _drain(self) -> None:
+        with self._idle:
+            self._idle.wait_for(lambda: self._inflight == 0, timeout=120)
+
+    # ------------------------------------------------------------------ batches
+    def _on_batch(self, buf: bytes) -> None:
+        t_recv = time.monotonic()
+        bid, slots = P.parse_batch(buf)
+        n = slots.shape[0]
+        self.batches += 1
+        f = self.fault
+        if "exit_after" in f and self.batches > f["exit_after"]:
+            os._exit(17)
+        if "hang_after" in f and self.batches > f["hang_after"]:
+            self.alive.clear()  # heartbeats stop too
+            time.sleep(3600)
+        if f.get("delay_ms"):
+            time.sleep(f["delay_ms"] / 1e3)
+        status = np.zeros(n, np.uint8)
+        valid = (slots >= 0) & (slots < self.nslots)
+        status[~valid] = P.IT_INVALID
+        vslots = slots[valid].tolist()
+        if not vslots:
+            self.conn.done(bid, status, bytes(n * self.row_bytes), self.row_bytes, (t_recv, t_recv, t_recv, 0, 0))
+            return
+        # the engine has 3 buffer sets: never launch a 3rd batch over one not yet retired
+        with self._idle:
+            self._idle.wait_for(lambda: self._inflight < self.engine.nbuf, timeout=120)
+        try:
+            if f.get("fail_batch") == self.batches:
+                raise RuntimeError("injected batch launch failure")
+            res = self.engine.submit(self.buf, vslots)
+        except Exception:
+            self._drain()
+            self._isolate(bid, slots, valid, status, t_recv)
+            return
+        with self._idle:
+            self._inflight += 1
+        self._done_q.put(_Pending(bid, n, valid, res, t_recv, status))
+
+    def _rows(self, n: int, valid: np.ndarray, outputs) -> bytes:
+        nv = int(valid.sum())
+        enc = encode_rows([o.numpy() if isinstance(o, torch.Tensor) else o for o in outputs], nv)
+        if nv == n:
+            return enc
+        rows = np.zeros((n, self.row_bytes), np.uint8)
+        rows[valid] = np.frombuffer(enc, np.uint8).reshape(nv, self.row_bytes)
+        return rows.tobytes()
+
+    def _finalize(self, p: _Pending) -> None:
+        p.res.done.synchronize()
+        t_done = time.monotonic()
+        h2d_ms, comp_ms = p.res.gpu_ms()
+        self.busy_ms += h2d_ms + comp_ms
+        rows = self._rows(p.n, p.valid, p.res.outputs)
+        self.conn.done(p.bid, p.status, rows, self.row_bytes, (p.t_recv, p.res.t_launch, t_done, h2d_ms, comp_ms))
+
+    def _isolate(self, bid: int, slots: np.ndarray, valid: np.ndarray, status: np.ndarray, t_recv: float) -> None:
+        """Batch launch failed (pipeline already drained): run each valid item alone."""
+        if self.device.type == "cuda":
+            try:
+                torch.cuda.synchronize(self.device)
+            except Exception:
+                pass
+        n = slots.shape[0]
+        rows = np.zeros((n, self.row_bytes), np.uint8)
+        t_launch = time.monotonic()
+        for i in np.nonzero(valid)[0].tolist():
+            try:
+                if self.fault.get("fail_item") == int(slots[i]):
+                    raise RuntimeError("injected item failure")
+                outs = self.engine.run_sync(self.buf[int(slots[i]): int(slots[i]) + 1])
+                rows[i] = np.frombuffer(encode_rows([o.numpy() for o in outs], 1), np.uint8)
+            except Exception:
+                status[i] = P.IT_ERROR
+        self.conn.done(bid, status, rows.tobytes(), self.row_bytes, (t_recv, t_launch, time.monotonic(), 0, 0))
+
+
+def worker_main(conn, rank: int, device: str, spec: ModelSpec, shm_name: str, nslots: int, hb_interval: float,
+                partition: Optional[Tuple[int, int]] = None, untrack: bool = False, local_ring=None) -> None:
+    """Entry point of a spawned worker process (and of ``torchrun`` worker ranks, which pass their
+    ingest partition's ``local_ring`` and ``untrack=True``)."""
+    dev = torch.device(device)
+    if dev.type == "cuda":
+        torch.cuda.set_device(dev)
+    shm, buf = attach_ring(shm_name, nslots, spec.item_shape, untrack=untrack)
+    pinned = pin_host(buf) if dev.type == "cuda" else False
+    if local_ring is None and partition is not None:
+        from ..store import native
+
+        local_ring = native.SlotRing(partition[1], partition[0])
+    fc = P.FrameConn(conn)
+    w = GpuWorker(fc, rank, device, spec, buf, local_ring=local_ring, hb_interval=hb_interval)
+    try:
+        w.serve(pinned)
+    finally:
+        if pinned:
+            try:
+                torch.cuda.cudart().cudaHostUnregister(buf.data_ptr())
+            except Exception:
+                pass
+        del buf
+        shm.close()

@@ -1,10 +1,17 @@
-"""A GPU model exposed as an API endpoint: payload decode -> pinned ring slot -> task -> batch worker.
+"""A GPU model exposed as an API endpoint: payload decode -> payload-ring slot -> task -> batch worker.
 
 This is the "drop-in model" container of the reference (``APIs/Charts/templates/async-gpu``,
 ``APIs/1.0/base-py/ai4e_service.py``) collapsed into the node process: request bodies are decoded
-once on the CPU straight into a slot of the pinned payload ring, the task record is created in the
-native store and the slot index travels through the dispatch queue, so the GPU worker's H2D copy
-reads the request bytes exactly where the front end put them.
+once on the CPU straight into a slot of the payload ring, the task record is created in the native
+store and the slot index travels through the dispatch queue, so the GPU worker's H2D copy reads the
+request bytes exactly where the front end put them. The backend is either the per-GPU
+:class:`WorkerPool` (native scheduler, one process per GPU) or an in-process
+:class:`GpuBatchWorker` (single GPU / CPU tests).
+
+Durability (survey §5.4, the reference's ``{TaskId}_ORIG`` replay, ``CacheConnectorUpsert.cs:150-176``):
+with a journal configured, request bodies up to ``journal_payload_max_bytes`` are journaled as the
+task's ``_ORIG`` body, and :meth:`replay` re-ingests them after a restart; tasks whose payload was
+not journaled are failed with a reason instead of being requeued without a payload.
 """
 from __future__ import annotations
 
@@ -17,12 +24,20 @@ from typing import Callable, Dict, List, Optional, Sequence, Tuple
 import numpy as np
 import torch
 
-from ..store import STATE_CREATED, STATE_FAILED, APITask
-from .serving import GpuBatchWorker, ResultStore
+from ..store import STATE_CREATED, STATE_FAILED
+from .serving import GpuBatchWorker
+
+PAYLOAD_LOST = "Task failed - payload lost on restart"
+PUBLISH_FAILED = "Failed - unable to send to backend service."
+_ORIG_PREFIX = "ai4e-b64:"
 
 
 class PayloadError(ValueError):
-    pass
+    """A request body that cannot be decoded into the endpoint's input (HTTP 400 / 415)."""
+
+    def __init__(self, msg: str, status: int = 400):
+        super().__init__(msg)
+        self.status = status
 
 
 def decode_image(body: bytes, content_type: str, shape: Tuple[int, int, int]) -> np.ndarray:
@@ -34,31 +49,38 @@ def decode_image(body: bytes, content_type: str, shape: Tuple[int, int, int]) ->
     """
     h, w, c = shape
     ct = (content_type or "").split(";")[0].strip().lower()
-    if ct in ("application/json", "text/json"):
-        d = json.loads(body or b"{}")
-        raw = base64.b64decode(d["image_b64"])
-        shp = tuple(d.get("shape", shape))
-        arr = np.frombuffer(raw, dtype=np.uint8).reshape(shp)
-    elif ct == "application/x-npy":
-        arr = np.load(io.BytesIO(body), allow_pickle=False)
-    elif ct.startswith("image/"):
-        from PIL import Image
+    try:
+        if ct in ("application/json", "text/json"):
+            d = json.loads(body or b"{}")
+            raw = base64.b64decode(d["image_b64"])
+            shp = tuple(d.get("shape", shape))
+            arr = np.frombuffer(raw, dtype=np.uint8).reshape(shp)
+        elif ct == "application/x-npy":
+            arr = np.load(io.BytesIO(body), allow_pickle=False)
+        elif ct.startswith("image/"):
+            from PIL import Image
 
-        im = Image.open(io.BytesIO(body))
-        im = im.convert("RGB" if c == 3 else ("L" if c == 1 else "RGBA"))
-        if im.size != (w, h):
-            im = im.resize((w, h), Image.BILINEAR)
-        arr = np.asarray(im, dtype=np.uint8)
-    else:
-        if len(body) != h * w * c:
-            raise PayloadError(f"raw payload must be {h * w * c} bytes (uint8 {h}x{w}x{c}), got {len(body)}")
-        arr = np.frombuffer(body, dtype=np.uint8).reshape(h, w, c)
+            im = Image.open(io.BytesIO(body))
+            im = im.convert("RGB" if c == 3 else ("L" if c == 1 else "RGBA"))
+            if im.size != (w, h):
+                im = im.resize((w, h), Image.BILINEAR)
+            arr = np.asarray(im, dtype=np.uint8)
+        elif ct in ("", "application/octet-stream"):
+            if len(body) != h * w * c:
+                raise PayloadError(f"raw payload must be {h * w * c} bytes (uint8 {h}x{w}x{c}), got {len(body)}")
+            arr = np.frombuffer(body, dtype=np.uint8).reshape(h, w, c)
+        else:
+            raise PayloadError(f"unsupported content type {ct!r}", 415)
+    except PayloadError:
+        raise
+    except Exception as e:  # malformed JSON / base64 / npy / image bytes
+        raise PayloadError(f"cannot decode payload: {e}") from e
     if arr.dtype != np.uint8:
         arr = np.clip(arr, 0, 255).astype(np.uint8)
     if arr.ndim == 2:
         arr = arr[..., None]
-    if arr.shape[2] != c:
-        raise PayloadError(f"expected {c} channels, got {arr.shape[2]}")
+    if arr.ndim != 3 or arr.shape[2] != c:
+        raise PayloadError(f"expected {c} channels, got shape {arr.shape}")
     if arr.shape[:2] != (h, w):
         t = torch.from_numpy(np.ascontiguousarray(arr)).permute(2, 0, 1)[None].float()
         t = torch.nn.functional.interpolate(t, size=(h, w), mode="bilinear", align_corners=False)
@@ -67,57 +89,155 @@ def decode_image(body: bytes, content_type: str, shape: Tuple[int, int, int]) ->
 
 
 class ModelEndpoint:
-    def __init__(self, control_plane, path: str, engine, ring, worker: Optional[GpuBatchWorker] = None,
-                 decode: Optional[Callable[[bytes, str], np.ndarray]] = None, base_url: str = "http://127.0.0.1"):
+    def __init__(self, control_plane, path: str, engine=None, ring=None, worker=None,
+                 decode: Optional[Callable[[bytes, str], np.ndarray]] = None, base_url: str = "http://127.0.0.1",
+                 journal_payload_max_bytes: Optional[int] = None):
         self.cp = control_plane
         self.path = path
         self.endpoint = base_url.rstrip("/") + path
-        self.engine = engine
-        self.ring = ring
-        self.results: ResultStore = worker.results if worker is not None else ResultStore()
-        self.worker = worker or GpuBatchWorker(control_plane, self.endpoint, engine, ring, results=self.results)
-        self.worker.on_batch_done = self._on_done
-        self.decode = decode or (lambda body, ct: decode_image(body, ct, ring.item_shape))
+        self.worker = worker if worker is not None else GpuBatchWorker(control_plane, self.endpoint, engine, ring)
+        self.ring = self.worker.ring
+        self.is_pool = hasattr(self.worker, "submit_slots")
+        self.decode = decode or (lambda body, ct: decode_image(body, ct, self.ring.item_shape))
         self.queue = control_plane.queue_for(self.endpoint)
         self._waiters: Dict[str, Callable[[str], None]] = {}
         self._wmu = threading.Lock()
+        if not self.is_pool:
+            self.worker.on_batch_done = self._on_done
+        cap = getattr(control_plane.cfg, "journal_payload_max_bytes", 0) if journal_payload_max_bytes is None \
+            else journal_payload_max_bytes
+        self.journal_cap = int(cap) if control_plane.cfg.journal_path else 0
+        control_plane.register_replayer(self.endpoint, self.replay)
+
+    @property
+    def item_shape(self) -> Tuple[int, ...]:
+        return tuple(self.ring.item_shape)
 
     # ------------------------------------------------------------- ingest
-    def ingest(self, body: bytes, content_type: str) -> int:
-        arr = self.decode(body, content_type)
-        slot = self.ring.alloc(1, timeout=30)[0]
-        self.ring.buf[slot].copy_(torch.from_numpy(np.require(arr, requirements=["C", "W"])))
-        return slot
+    def _enqueue(self, slots: List[int], trace: str = "") -> List[str]:
+        if self.is_pool:
+            return self.worker.submit_slots(slots, trace)
+        ids = self.cp.store.create_many(self.endpoint, len(slots), trace=trace)
+        sent = self.queue.send_many(ids, slots)
+        if sent < len(ids):
+            self.cp.store.transition_many(ids[sent:], STATE_FAILED, PUBLISH_FAILED)
+            self.ring.free(slots[sent:])
+        return ids
+
+    def _write(self, slots: Sequence[int], images_u8: np.ndarray) -> None:
+        if self.is_pool:  # SharedPayloadRing: one copy per contiguous run of slots
+            self.ring.write(slots, images_u8)
+            return
+        src = torch.from_numpy(np.require(images_u8, np.uint8, ["C", "W"]))
+        for i, s in enumerate(slots):
+            self.ring.buf[s].copy_(src[i])
 
     def submit(self, body: bytes, content_type: str = "application/octet-stream", task_id: str = "",
-               on_done: Optional[Callable[[str], None]] = None) -> str:
-        """Async API: decode, create task (or adopt an upstream ``taskId``), enqueue. Returns task JSON."""
-        slot = self.ingest(body, content_type)
-        serialized, _ = self.cp.store.upsert(task_id, STATE_CREATED, STATE_CREATED, self.endpoint, None, True)
-        tid = json.loads(serialized)["TaskId"]
+               on_done: Optional[Callable[[str], None]] = None, trace: str = "") -> str:
+        """Async API: decode, create task (or adopt an upstream ``taskId``), enqueue. Returns task JSON.
+
+        Raises :class:`PayloadError` (-> HTTP 400/415) before any task exists for undecodable bodies."""
+        arr = self.decode(body, content_type)
+        slot = self.ring.alloc(1, timeout=30)[0]
+        self._write([slot], arr[None])
+        orig = self._orig(body, content_type)
+        if task_id or orig is not None:
+            # upstream TaskId (header taskId, api_task.py:12-20) or a journaled payload: explicit upsert
+            serialized, _ = self.cp.store.upsert(task_id, STATE_CREATED, STATE_CREATED, self.endpoint, orig, True)
+            tid = json.loads(serialized)["TaskId"]
+            if trace:
+                self.cp.store.set_trace(tid, trace)
+            if on_done is not None:
+                self._add_waiter(tid, on_done)
+            if not self.queue.send(tid, slot, ""):
+                self.ring.free([slot])
+                serialized, _ = self.cp.store.upsert(tid, PUBLISH_FAILED, STATE_FAILED, self.endpoint, None, True)
+                self._fire(tid)
+            return serialized
+        if on_done is not None and self.is_pool:
+            self.worker.enable_completion_feed()
         if on_done is not None:
-            with self._wmu:
-                self._waiters[tid] = on_done
-        if not self.queue.send(tid, slot, ""):
-            self.ring.free([slot])
-            serialized, _ = self.cp.store.upsert(tid, "Failed - unable to send to backend service.", STATE_FAILED,
-                                                 self.endpoint, None, True)
-            with self._wmu:
-                self._waiters.pop(tid, None)
+            # register before enqueueing: the batch may complete before submit returns
+            tid_box: List[str] = []
+            ids = self._enqueue_with_waiter([slot], trace, on_done, tid_box)
+        else:
+            ids = self._enqueue([slot], trace)
+        serialized = self.cp.store.get(ids[0])
+        rec = json.loads(serialized)
+        if rec["BackendStatus"] == STATE_FAILED:
+            self._fire(ids[0])
         return serialized
 
-    def submit_many(self, images_u8: np.ndarray) -> List[str]:
+    def _enqueue_with_waiter(self, slots, trace, on_done, box) -> List[str]:
+        # the id is only known after creation; completions that race ahead are caught by checking the
+        # record state right after registration
+        ids = self._enqueue(slots, trace)
+        self._add_waiter(ids[0], on_done)
+        rec = self.cp.store.get_record(ids[0])
+        if rec is not None and rec["BackendStatus"] in ("completed", "failed"):
+            self._fire(ids[0])
+        return ids
+
+    def submit_many(self, images_u8: np.ndarray, trace: str = "") -> List[str]:
         """Bulk async submit of already-decoded images (batch clients / benchmarks)."""
         n = images_u8.shape[0]
         slots = self.ring.alloc(n, timeout=60)
-        for i, s in enumerate(slots):
-            self.ring.buf[s].copy_(torch.from_numpy(images_u8[i]))
-        ids = self.cp.store.create_many(self.endpoint, n)
-        self.queue.send_many(ids, slots)
-        return ids
+        self._write(slots, images_u8)
+        return self._enqueue(slots, trace)
 
+    def submit_raw_batch(self, body: bytes, trace: str = "") -> List[str]:
+        """Binary batch ingest: ``n * prod(item_shape)`` raw uint8 bytes -> n tasks (one copy per run)."""
+        item = int(np.prod(self.item_shape))
+        if len(body) == 0 or len(body) % item:
+            raise PayloadError(f"batch payload must be a multiple of {item} bytes (uint8 {self.item_shape})")
+        arr = np.frombuffer(body, dtype=np.uint8).reshape(-1, *self.item_shape)
+        return self.submit_many(arr, trace)
+
+    def _orig(self, body: bytes, content_type: str) -> Optional[str]:
+        if not self.journal_cap or len(body) > self.journal_cap:
+            return None
+        return _ORIG_PREFIX + (content_type or "") + ";" + base64.b64encode(body).decode()
+
+    def replay(self, task_id: str, orig: Optional[str]) -> bool:
+        """Restart recovery of one unfinished task: re-ingest its journaled payload, or fail it."""
+        if not orig or not orig.startswith(_ORIG_PREFIX):
+            self.cp.store.upsert(task_id, PAYLOAD_LOST, STATE_FAILED, self.endpoint, None, True)
+            return False
+        ct, b64 = orig[len(_ORIG_PREFIX):].split(";", 1)
+        try:
+            arr = self.decode(base64.b64decode(b64), ct)
+        except PayloadError:
+            self.cp.store.upsert(task_id, "Task failed - invalid payload", STATE_FAILED, self.endpoint, None, True)
+            return False
+        slot = self.ring.alloc(1, timeout=30)[0]
+        self._write([slot], arr[None])
+        self.cp.store.upsert(task_id, "created - requeued after restart", STATE_CREATED, self.endpoint, None, True)
+        if not self.queue.send(task_id, slot, ""):
+            self.ring.free([slot])
+            self.cp.store.upsert(task_id, PUBLISH_FAILED, STATE_FAILED, self.endpoint, None, True)
+            return False
+        return True
+
+    # ------------------------------------------------------------- results / completion
     def result(self, task_id: str) -> Optional[dict]:
-        return self.results.get(task_id)
+        return self.worker.result(task_id)
+
+    def _add_waiter(self, tid: str, cb: Callable[[str], None]) -> None:
+        if self.is_pool:
+            self.worker.enable_completion_feed()
+            self.worker.add_waiter(tid, cb)
+        else:
+            with self._wmu:
+                self._waiters[tid] = cb
+
+    def _fire(self, tid: str) -> None:
+        if self.is_pool:
+            cb = self.worker.pop_waiter(tid)
+        else:
+            with self._wmu:
+                cb = self._waiters.pop(tid, None)
+        if cb is not None:
+            cb(tid)
 
     def _on_done(self, ids: Sequence[str]) -> None:
         if not self._waiters:

@@ -5,16 +5,18 @@ The reference chains APIs by re-publishing the same TaskId to the next endpoint
 ``CacheConnectorUpsert.cs:144-176``): every hop is queue -> HTTP -> JSON. Here the stages are
 GPU ranks of one node and the hand-off is a tensor over xGMI:
 
-* detector ranks run Faster-RCNN on a batch, pick the animal boxes, crop + resize + normalise them
-  on the GPU (``crop_resize_nhwc``, K5) and ``send`` a count header then the bf16 crops
-  ``[N, 224, 224, 8]`` (≈0.8 MiB per crop) to their paired classifier rank over RCCL;
-* classifier ranks ``recv`` the count, the crops, run the crop classifier (fused ResNet-50 on
-  K1) and send back ``[N, 2]`` (class, probability);
+* detector ranks run Faster-RCNN on a batch, pick the confident animal boxes, crop + bilinear-resize
+  them on the GPU to uint8 ``[N, 224, 224, 3]`` (``crop_resize_u8``, K5/K7: 147 KiB per crop, the
+  classifier's own input format, half the bytes of fp16 and a sixth of a bf16x8 stem tensor) and
+  ``send`` a count header then the crops to their paired classifier rank over RCCL;
+* classifier ranks ``recv`` the count, the crops, run the crop classifier (fused ResNet-50 on K1,
+  the headline model's uint8 entry point) and send back ``[N, 2]`` (class, probability);
 * the detector side keeps one batch in flight: it sends batch i, starts detecting batch i+1, then
   collects batch i's classifications — compute and transfer overlap; message order is fixed
   (header, payload, results) so the pairing can never deadlock;
-* the task record keeps one TaskId across both stages (``stage_transition``): created@detector ->
-  running -> created@classifier ("AddPipelineTask") -> running -> completed.
+* the task record keeps one TaskId across both stages (``stage_transition`` /
+  ``TaskStore.retarget_many``): created@detector -> running -> created@classifier
+  ("AddPipelineTask") -> running -> completed.
 
 Pairing: with ``world`` ranks, rank 2i (detector) talks to rank 2i+1 (classifier). ``world == 1``
 runs both stages on one GPU with a local hand-off (no RCCL), same code path otherwise.
@@ -27,7 +29,7 @@ from typing import Callable, List, Optional, Sequence, Tuple
 import torch
 import torch.distributed as dist
 
-from ..ops.detection import crop_resize_nhwc
+from ..ops.detection import crop_resize_u8
 from ..store import STATE_COMPLETED, STATE_CREATED, STATE_RUNNING
 
 STOP = -1
@@ -39,13 +41,14 @@ class PipelineConfig:
     score_thresh: float = 0.5
     class_id: Optional[int] = 1    # MegaDetector "animal"; None = every class
     max_crops_per_image: int = 8
-    # dtype of the crops on the RCCL wire between detector and classifier GPUs (BASELINE config #5: fp16);
-    # the classifier computes in bf16 and converts on receipt. CPU ranks (gloo) keep fp32.
-    wire_dtype: str = "float16"
+    # crops on the RCCL wire between detector and classifier GPUs: "uint8" (3 B/px, exact classifier
+    # input) or "float16" (6 B/px, rounded back to uint8 on receipt)
+    wire_dtype: str = "uint8"
 
 
 def select_crops(dets, cfg: PipelineConfig) -> torch.Tensor:
-    """Padded detections -> boxes [N, 5] (img, x1, y1, x2, y2) of confident target-class boxes."""
+    """Padded detections -> [N, 6] (img, x1, y1, x2, y2, score) of confident target-class boxes,
+    grouped by image in score order."""
     boxes, scores, labels, n = dets
     B, D = scores.shape
     rank = torch.arange(D, device=scores.device)[None].expand(B, D)
@@ -55,7 +58,7 @@ def select_crops(dets, cfg: PipelineConfig) -> torch.Tensor:
     # cap per image (detections are score-sorted)
     ok &= torch.cumsum(ok.int(), 1) <= cfg.max_crops_per_image
     img = torch.arange(B, device=scores.device, dtype=torch.float32)[:, None].expand(B, D)
-    sel = torch.cat([img[..., None], boxes], -1)[ok]
+    sel = torch.cat([img[..., None], boxes.float(), scores.float()[..., None]], -1)[ok]
     return sel
 
 
@@ -70,7 +73,7 @@ class DetectClassifyPipeline:
     def __init__(self, detector: Callable, classifier: Callable[[torch.Tensor], torch.Tensor], device: torch.device,
                  cfg: Optional[PipelineConfig] = None, group=None):
         self.detector = detector        # uint8 NHWC images -> padded detections tuple
-        self.classifier = classifier    # normalized bf16 crops [N, h, w, 8] -> logits [N, K]
+        self.classifier = classifier    # uint8 crops [N, h, w, 3] -> logits [N, K]
         self.device = device
         self.cfg = cfg or PipelineConfig()
         self.group = group
@@ -80,8 +83,9 @@ class DetectClassifyPipeline:
         self.peer = self.rank + 1 if self.rank % 2 == 0 else self.rank - 1
         if self.world > 1 and self.peer >= self.world:
             raise ValueError("pipeline needs an even number of ranks (detector/classifier pairs)")
-        self.crop_dtype = torch.bfloat16 if device.type == "cuda" else torch.float32  # classifier compute dtype
-        self.wire_dtype = getattr(torch, self.cfg.wire_dtype) if device.type == "cuda" else torch.float32
+        self.wire_dtype = getattr(torch, self.cfg.wire_dtype)
+        self.bytes_sent = 0       # xGMI payload bytes (crops + headers), for the metrics registry
+        self.bytes_received = 0
 
     # ------------------------------------------------------------ classifier stage
     def classify(self, crops: torch.Tensor) -> torch.Tensor:
@@ -101,19 +105,28 @@ class DetectClassifyPipeline:
             n = int(hdr.item())
             if n == STOP:
                 return total
-            crops = torch.empty(n, h, w, 8, dtype=self.wire_dtype, device=self.device)
+            crops = torch.empty(n, h, w, 3, dtype=self.wire_dtype, device=self.device)
             if n:
                 dist.recv(crops, self.peer, group=self.group)
-            res = self.classify(crops.to(self.crop_dtype))
+                self.bytes_received += crops.numel() * crops.element_size()
+            res = self.classify(self._from_wire(crops))
             if n:
                 dist.send(res.contiguous(), self.peer, group=self.group)
+                self.bytes_sent += res.numel() * res.element_size()
             total += n
 
     # ------------------------------------------------------------ detector stage
+    def _to_wire(self, crops_u8: torch.Tensor) -> torch.Tensor:
+        return crops_u8 if self.wire_dtype == torch.uint8 else crops_u8.to(self.wire_dtype)
+
+    def _from_wire(self, crops: torch.Tensor) -> torch.Tensor:
+        return crops if crops.dtype == torch.uint8 else crops.round().clamp(0, 255).to(torch.uint8)
+
     def _detect_and_crop(self, images: torch.Tensor):
         dets = self.detector(images)
         boxes = select_crops(dets, self.cfg)
-        crops = crop_resize_nhwc(images, boxes, self.cfg.crop_hw).to(self.crop_dtype)
+        crops = crop_resize_u8(images[..., :3].contiguous() if images.shape[-1] != 3 else images, boxes[:, :5],
+                               self.cfg.crop_hw)
         return dets, boxes, crops
 
     def _send(self, crops: torch.Tensor) -> list:
@@ -121,15 +134,18 @@ class DetectClassifyPipeline:
         while these bytes move, or both sides block in send (rendezvous) and deadlock."""
         n = torch.tensor([crops.shape[0]], dtype=torch.int64, device=self.device)
         works = [(dist.isend(n, self.peer, group=self.group), n)]
+        self.bytes_sent += 8
         if crops.shape[0]:
             c = crops.contiguous()
             works.append((dist.isend(c, self.peer, group=self.group), c))
+            self.bytes_sent += c.numel() * c.element_size()
         return works
 
     def _recv_results(self, n: int) -> torch.Tensor:
         res = torch.empty(n, 2, device=self.device)
         if n:
             dist.recv(res, self.peer, group=self.group)
+            self.bytes_received += res.numel() * res.element_size()
         return res
 
     def run_batches(self, batches: Sequence[torch.Tensor]) -> List[Tuple]:
@@ -141,12 +157,11 @@ class DetectClassifyPipeline:
                 dets, boxes, crops = self._detect_and_crop(imgs)
                 out.append((dets, boxes, self.classify(crops)))
             return out
-        # only the hand-off goes through wire_dtype (fp16 on GPUs): one conversion each side of the RCCL send
         pending = None
         inflight: list = []
         for imgs in batches:
             dets, boxes, crops = self._detect_and_crop(imgs)
-            works = self._send(crops.to(self.wire_dtype))  # hand batch i to the classifier ...
+            works = self._send(self._to_wire(crops))  # hand batch i to the classifier ...
             if pending is not None:                 # ... then collect batch i-1 while it works
                 pd, pb = pending
                 out.append((pd, pb, self._recv_results(pb.shape[0])))

@@ -1,72 +1,79 @@
-"""Per-GPU worker pool: one process per MI355X, heartbeats, fail-over requeue, elastic resize.
+"""Per-GPU worker pool: one process per MI355X behind the native NodeScheduler.
 
 Replaces the reference's replica scaling (``APIs/Charts/templates/async-gpu/autoscaler.yaml`` HPA
 1..10 replicas, ``routing.yml`` ROUND_ROBIN, ``deploy_aks.sh`` cluster autoscaler) with a fixed
-node: the gateway process owns the task store, the dispatch queue and a shared-memory payload ring;
-each GPU worker process (``HIP_VISIBLE_DEVICES``-style pinning via ``cuda:<i>``) maps the ring,
-registers it as pinned host memory, and runs batches handed to it over a pipe. Placement is
-least-loaded by construction: each worker's dispatcher thread pulls the next batch from the shared
-endpoint queue only when its GPU has a free pipeline slot.
+node. The gateway process owns the task store, the endpoint's dispatch queue, the shared-memory
+payload ring and the native scheduler; each GPU worker process (spawned here, or a ``torchrun``
+rank that connects over TCP — :meth:`attach_remote`) maps the ring, registers it as pinned host
+memory and executes batches the scheduler hands it. Placement is least-loaded by construction: a
+worker's dispatcher thread pulls the next batch only when its GPU has a free pipeline slot. All
+per-batch work (receive, running/completed transitions, result attachment, slot release) is C++.
 
 Failure handling (survey §5.3): a worker that exits, or whose heartbeat stops for
-``heartbeat_timeout_s``, has its in-flight batches abandoned back to the queue (redelivered to the
-surviving workers, bounded by the queue's max delivery count -> task failed with a reason), and is
-restarted up to ``max_restarts`` times; ``resize(n)`` grows or shrinks the active GPU set without
-losing queued tasks. ``AI4E_FAULT_INJECTION`` drives the failure tests:
-``exit_after=<batches>[@<rank>]``, ``hang_after=<batches>[@<rank>]``, ``delay_ms=<ms>``.
+``heartbeat_timeout_s``, has its in-flight batches requeued (redelivered to the surviving workers,
+bounded by the queue's max delivery count -> task failed with a reason) and is restarted up to
+``max_restarts`` times. ``resize(n)`` grows or shrinks the active GPU set without losing queued
+tasks; :class:`runtime.autoscale.QueueDepthAutoscaler` drives it from queue depth (the HPA analogue).
+Fault injection: ``AI4E_FAULT_INJECTION`` (see :mod:`runtime.gpu_worker`).
 """
 from __future__ import annotations
 
-import importlib
+import json
 import multiprocessing as mp
 import os
 import threading
 import time
-from dataclasses import dataclass, field
 from multiprocessing import shared_memory
-from typing import Any, Dict, List, Optional, Sequence, Tuple
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
 
-from ..store import STATE_COMPLETED, STATE_FAILED, STATE_RUNNING
-from .engine import PayloadRing
-from .serving import ResultStore
+from ..store import native
+from .gpu_worker import ModelSpec, worker_main  # noqa: F401  (ModelSpec re-exported)
+from .servable import format_result
+
+__all__ = ["ModelSpec", "SharedPayloadRing", "WorkerPool"]
 
 
-@dataclass
-class ModelSpec:
-    factory: str                      # "package.module:function" -> callable(u8 [b,H,W,C]) -> logits
-    item_shape: Tuple[int, int, int]
-    max_batch: int = 250  # whole waves of workgroups on 256 CUs for ResNet-50 (bench.py)
-    topk: int = 5
-    kwargs: Dict[str, Any] = field(default_factory=dict)
-    use_graphs: bool = True
-    buckets: Tuple[int, ...] = ()      # captured batch sizes (config.bucket_list); () = max_batch only
+class SharedPayloadRing:
+    """The node's payload ring in POSIX shared memory + the native slot allocator of this process's
+    ingest partition ``[0, local_slots)``; slots beyond belong to remote ingest shards."""
 
-
-class SharedPayloadRing(PayloadRing):
-    """PayloadRing whose buffer lives in POSIX shared memory (children map it read-only by name)."""
-
-    def __init__(self, nslots: int, item_shape: Sequence[int]):
+    def __init__(self, nslots: int, item_shape: Sequence[int], local_slots: Optional[int] = None):
         self.nslots = int(nslots)
-        self.item_shape = tuple(item_shape)
+        self.item_shape = tuple(int(x) for x in item_shape)
         nbytes = self.nslots * int(np.prod(self.item_shape))
         self.shm = shared_memory.SharedMemory(create=True, size=max(nbytes, 1))
         self.buf = torch.frombuffer(self.shm.buf, dtype=torch.uint8, count=nbytes).view(self.nslots, *self.item_shape)
-        self._head = 0
-        self._used = 0
-        self._free = [False] * self.nslots
-        self._mu = threading.Condition()
+        self.slots = native.SlotRing(int(local_slots or self.nslots), 0)
 
-    @staticmethod
-    def attach(name: str, nslots: int, item_shape: Sequence[int]):
-        shm = shared_memory.SharedMemory(name=name)
-        nbytes = nslots * int(np.prod(item_shape))
-        buf = torch.frombuffer(shm.buf, dtype=torch.uint8, count=nbytes).view(nslots, *item_shape)
-        return shm, buf
+    @property
+    def name(self) -> str:
+        return self.shm.name
+
+    def alloc(self, n: int, timeout: Optional[float] = None) -> List[int]:
+        s = self.slots.alloc(int(n), -1.0 if timeout is None else float(timeout))
+        if not s:
+            raise TimeoutError("payload ring full")
+        return s
+
+    def free(self, slots: Sequence[int]) -> None:
+        self.slots.free(list(slots))
+
+    def write(self, slots: Sequence[int], images_u8: np.ndarray) -> None:
+        """Copy decoded payloads into their slots (one copy per contiguous run of slots)."""
+        src = torch.from_numpy(np.require(images_u8, np.uint8, ["C", "W"]))
+        i, n = 0, len(slots)
+        while i < n:
+            j = i + 1
+            while j < n and slots[j] == slots[j - 1] + 1:
+                j += 1
+            self.buf[slots[i]:slots[i] + (j - i)].copy_(src[i:j])
+            i = j
 
     def close(self) -> None:
+        self.slots.close()
         del self.buf
         try:
             self.shm.close()
@@ -75,160 +82,142 @@ class SharedPayloadRing(PayloadRing):
             pass
 
 
-def _load_factory(path: str):
-    mod, fn = path.split(":")
-    return getattr(importlib.import_module(mod), fn)
-
-
-def _parse_fault(rank: int) -> Dict[str, int]:
-    out = {}
-    spec = os.environ.get("AI4E_FAULT_INJECTION", "")
-    for item in filter(None, spec.split(",")):
-        k, v = item.split("=")
-        tgt = None
-        if "@" in v:
-            v, tgt = v.split("@")
-        if tgt is None or int(tgt) == rank:
-            out[k.strip()] = int(v)
-    return out
-
-
-def _child_main(rank: int, device: str, spec: ModelSpec, shm_name: str, nslots: int, conn, hb_interval: float):
-    """GPU worker process body."""
-    from .engine import InferenceEngine
-
-    dev = torch.device(device)
-    if dev.type == "cuda":
-        torch.cuda.set_device(dev)
-    shm, buf = SharedPayloadRing.attach(shm_name, nslots, spec.item_shape)
-    registered = False
-    if dev.type == "cuda":
-        try:  # pin the shared ring in place so H2D DMA reads it directly
-            rc = torch.cuda.cudart().cudaHostRegister(buf.data_ptr(), buf.numel(), 0)
-            registered = int(rc) == 0 if not isinstance(rc, tuple) else int(rc[0]) == 0
-        except Exception:
-            registered = False
-    model = _load_factory(spec.factory)(device=device, **spec.kwargs)
-    engine = InferenceEngine(model, spec.item_shape, spec.max_batch, device=dev, topk=spec.topk,
-                             use_graphs=spec.use_graphs, head_fn=getattr(model, "topk_u8", None),
-                             buckets=list(spec.buckets) or None)
-    engine.warmup()
-    fault = _parse_fault(rank)
-    send_mu = threading.Lock()
-    alive = threading.Event()
-    alive.set()
-
-    def send(msg):
-        with send_mu:
-            conn.send(msg)
-
-    def heartbeat():
-        while alive.is_set():
-            try:
-                send(("hb", rank, time.time()))
-            except (BrokenPipeError, EOFError, OSError):
-                return
-            time.sleep(hb_interval)
-
-    threading.Thread(target=heartbeat, daemon=True).start()
-    send(("ready", rank, registered))
-    pending: List[Tuple[int, Any]] = []
-    nbatches = 0
-    while True:
-        # retire finished batches in order (the parent keeps at most `depth` outstanding)
-        while pending and (pending[0][1].done.query() or len(pending) > 2):
-            bid, res = pending.pop(0)
-            res.done.synchronize()
-            send(("done", bid, res.top_idx.numpy().copy(), res.top_prob.numpy().copy()))
-        if not conn.poll(0.0005 if pending else 0.05):
-            continue
-        msg = conn.recv()
-        if msg[0] == "stop":
-            break
-        if msg[0] == "batch":
-            _, bid, slots = msg
-            nbatches += 1
-            if "exit_after" in fault and nbatches > fault["exit_after"]:
-                os._exit(17)
-            if "hang_after" in fault and nbatches > fault["hang_after"]:
-                alive.clear()
-                time.sleep(3600)
-            if fault.get("delay_ms"):
-                time.sleep(fault["delay_ms"] / 1e3)
-            pending.append((bid, engine.submit(buf, slots)))
-    alive.clear()
-    for bid, res in pending:
-        res.done.synchronize()
-    del buf
-    shm.close()
-
-
 class _WorkerHandle:
     def __init__(self, rank: int, device: str):
         self.rank = rank
         self.device = device
         self.proc: Optional[mp.Process] = None
-        self.conn = None
-        self.last_hb = 0.0
-        self.ready = False
-        self.outstanding: Dict[int, Tuple[List[str], List[int], List[int]]] = {}
         self.restarts = 0
-        self.thread: Optional[threading.Thread] = None
         self.stop = threading.Event()
-        self.batches = 0
-        self.images = 0
+        self.remote = False
+        self.stats: dict = {}
+
+    @property
+    def ready(self) -> bool:
+        return bool(self.stats.get("ready")) and bool(self.stats.get("alive"))
+
+    @property
+    def batches(self) -> int:
+        return int(self.stats.get("batches", 0))
+
+    @property
+    def images(self) -> int:
+        return int(self.stats.get("images", 0))
 
 
 class WorkerPool:
     def __init__(self, control_plane, endpoint: str, spec: ModelSpec, devices: Sequence[str], ring_slots: int = 0,
                  max_delay_s: float = 0.0005, heartbeat_interval_s: float = 0.5, heartbeat_timeout_s: float = 10.0,
-                 max_restarts: int = 2, pipeline_depth: int = 2, results: Optional[ResultStore] = None):
+                 max_restarts: int = 2, pipeline_depth: int = 2, retry_delay_s: float = 1.0,
+                 remote_partitions: Sequence[Tuple[int, int, int]] = (), completion_feed: bool = False,
+                 poll_s: float = 0.02):
+        if native is None:
+            raise RuntimeError("the worker pool needs the native core (_ai4e_core)")
         self.cp = control_plane
         self.endpoint = endpoint
         self.queue = control_plane.queue_for(endpoint)
         self.store = control_plane.store
+        if not isinstance(self.store, native.TaskStore) or not isinstance(self.queue, native.DispatchQueue):
+            raise RuntimeError("the worker pool needs the native store/queue backend (AI4E_STORE_BACKEND=native)")
         self.spec = spec
         self.devices = list(devices)
-        self.ring = SharedPayloadRing(ring_slots or spec.max_batch * (pipeline_depth + 2) * max(1, len(devices)),
-                                      spec.item_shape)
-        self.max_delay_s = max_delay_s
+        local = ring_slots or spec.max_batch * (pipeline_depth + 2) * max(1, len(self.devices))
+        self.remote_partitions = [tuple(int(v) for v in p) for p in remote_partitions]  # (base, len, rank)
+        total = max([local] + [b + n for b, n, _ in self.remote_partitions])
+        self.ring = SharedPayloadRing(total, spec.item_shape, local_slots=local)
         self.hb_interval = heartbeat_interval_s
-        self.hb_timeout = heartbeat_timeout_s
         self.max_restarts = max_restarts
-        self.depth = pipeline_depth
-        self.results = results or ResultStore()
+        self.sched = native.NodeScheduler(self.store, self.queue, endpoint, total, max_batch=spec.max_batch,
+                                          linger_s=max_delay_s, depth=pipeline_depth, retry_delay_s=retry_delay_s,
+                                          hb_timeout_s=heartbeat_timeout_s, poll_s=poll_s)
+        self.sched.add_local_ring(self.ring.slots)
+        for base, n, rank in self.remote_partitions:
+            self.sched.add_remote_partition(base, n, rank)
         self.workers: List[_WorkerHandle] = []
         self.events: List[Tuple[float, str, int]] = []  # (time, event, rank) for tests/ops
         self._ctx = mp.get_context("spawn")
-        self._bid = 0
-        self._bmu = threading.Lock()
-        self.on_batch_done = None
+        self._mu = threading.Lock()
+        self._stop = threading.Event()
+        self._monitor: Optional[threading.Thread] = None
+        self._feed: Optional[threading.Thread] = None
+        self._waiters: Dict[str, Callable[[str], None]] = {}
+        self._wmu = threading.Lock()
+        self.describe: dict = {}
+        if completion_feed:
+            self.enable_completion_feed()
 
     # ------------------------------------------------------------ lifecycle
-    def start(self, wait_ready_s: float = 300.0) -> "WorkerPool":
+    def start(self, wait_ready_s: float = 600.0) -> "WorkerPool":
+        if self._monitor is not None:  # already started
+            return self
         for i, dev in enumerate(self.devices):
             self._spawn(_WorkerHandle(i, dev))
-        deadline = time.time() + wait_ready_s
-        while time.time() < deadline and not all(w.ready for w in self.workers):
-            time.sleep(0.01)
+        self._monitor = threading.Thread(target=self._monitor_loop, daemon=True, name="ai4e-pool-monitor")
+        self._monitor.start()
+        self.wait_ready(wait_ready_s)
         return self
 
+    def wait_ready(self, timeout_s: float = 600.0, n: Optional[int] = None) -> bool:
+        deadline = time.time() + timeout_s
+        while time.time() < deadline:
+            self.refresh()
+            active = [w for w in self.workers if not w.stop.is_set()]
+            want = len(active) if n is None else n
+            if sum(w.ready for w in active) >= want:
+                return True
+            if all(w.proc is not None and not w.proc.is_alive() for w in active if not w.remote) and active and \
+                    not any(w.remote for w in active):
+                return False
+            time.sleep(0.02)
+        return False
+
     def _spawn(self, w: _WorkerHandle) -> None:
-        parent, child = self._ctx.Pipe()
-        w.conn = parent
-        w.ready = False
-        w.last_hb = time.time()
-        w.proc = self._ctx.Process(target=_child_main, args=(w.rank, w.device, self.spec, self.ring.shm.name,
-                                                             self.ring.nslots, child, self.hb_interval), daemon=True)
+        parent, child = self._ctx.Pipe(duplex=True)
+        w.proc = self._ctx.Process(target=worker_main, args=(child, w.rank, w.device, self.spec, self.ring.name,
+                                                             self.ring.nslots, self.hb_interval), daemon=True,
+                                   name=f"ai4e-gpu-worker-{w.rank}")
         w.proc.start()
         child.close()
+        fd = os.dup(parent.fileno())
+        parent.close()
         w.stop.clear()
-        if w not in self.workers:
-            self.workers.append(w)
-        w.thread = threading.Thread(target=self._dispatch_loop, args=(w,), daemon=True,
-                                    name=f"ai4e-pool-dispatch-{w.rank}")
-        w.thread.start()
+        w.stats = {}
+        with self._mu:
+            if w not in self.workers:
+                self.workers.append(w)
+        self.sched.attach(w.rank, fd, True)
         self.events.append((time.time(), "spawn", w.rank))
+
+    def attach_remote(self, rank: int, conn, device: str = "remote") -> None:
+        """A worker process started elsewhere (a torchrun rank) that connected to this node scheduler."""
+        w = _WorkerHandle(rank, device)
+        w.remote = True
+        fd = os.dup(conn.fileno())
+        conn.close()
+        with self._mu:
+            self.workers.append(w)
+        self.sched.attach(rank, fd, True)
+        self.events.append((time.time(), "attach", rank))
+
+    def _monitor_loop(self) -> None:
+        while not self._stop.is_set():
+            failed = self.sched.wait_failed(0.2)
+            self.refresh()
+            for rank in failed:
+                w = next((x for x in self.workers if x.rank == rank), None)
+                if w is None or w.stop.is_set():
+                    continue
+                self.events.append((time.time(), "worker_failed", rank))
+                if w.proc is not None and w.proc.is_alive():
+                    w.proc.kill()
+                    w.proc.join(10)
+                if not w.remote and w.restarts < self.max_restarts and not self._stop.is_set():
+                    w.restarts += 1
+                    self.events.append((time.time(), "restart", rank))
+                    self._spawn(w)
+                else:
+                    w.stop.set()
+                    self.events.append((time.time(), "removed", rank))
 
     def resize(self, n: int, devices: Optional[Sequence[str]] = None) -> None:
         """Elastic: grow to / shrink to n active workers (queued tasks are never lost)."""
@@ -236,19 +225,17 @@ class WorkerPool:
         if n > len(active):
             devs = list(devices or self.devices)
             for i in range(len(active), n):
-                self._spawn(_WorkerHandle(len(self.workers), devs[i % len(devs)]))
+                self._spawn(_WorkerHandle(max((w.rank for w in self.workers), default=-1) + 1, devs[i % len(devs)]))
         else:
             for w in active[n:]:
                 self._retire(w)
 
+    def active(self) -> int:
+        return sum(1 for w in self.workers if not w.stop.is_set())
+
     def _retire(self, w: _WorkerHandle) -> None:
         w.stop.set()
-        if w.thread is not None:
-            w.thread.join(30)
-        try:
-            w.conn.send(("stop",))
-        except (BrokenPipeError, OSError):
-            pass
+        self.sched.detach(w.rank, 30.0)
         if w.proc is not None:
             w.proc.join(30)
             if w.proc.is_alive():
@@ -256,98 +243,86 @@ class WorkerPool:
         self.events.append((time.time(), "retire", w.rank))
 
     def stop(self) -> None:
+        self._stop.set()
         for w in self.workers:
             if not w.stop.is_set():
-                self._retire(w)
+                w.stop.set()
+        self.sched.stop()
+        for w in self.workers:
+            if w.proc is not None:
+                w.proc.join(30)
+                if w.proc.is_alive():
+                    w.proc.kill()
+        if self._monitor is not None:
+            self._monitor.join(5)
+        if self._feed is not None:
+            self._feed.join(5)
         self.ring.close()
 
-    # ------------------------------------------------------------ submission (ModelEndpoint-compatible)
-    def submit_many(self, images_u8: np.ndarray) -> List[str]:
-        n = images_u8.shape[0]
-        slots = self.ring.alloc(n, timeout=60)
-        for i, s in enumerate(slots):
-            self.ring.buf[s].copy_(torch.from_numpy(np.require(images_u8[i], requirements=["C", "W"])))
-        ids = self.store.create_many(self.endpoint, n)
-        self.queue.send_many(ids, slots)
-        return ids
+    # ------------------------------------------------------------ ingest (ModelEndpoint backend)
+    def submit_slots(self, slots: Sequence[int], trace: str = "") -> List[str]:
+        return self.sched.submit(list(slots), trace)
 
-    def result(self, task_id: str):
-        return self.results.get(task_id)
+    def submit_many(self, images_u8: np.ndarray) -> List[str]:
+        slots = self.ring.alloc(images_u8.shape[0], timeout=60)
+        self.ring.write(slots, images_u8)
+        return self.submit_slots(slots)
+
+    # ------------------------------------------------------------ completion feed (sync routes)
+    def enable_completion_feed(self) -> None:
+        if self._feed is None:
+            self.sched.enable_completion_feed(True)
+            self._feed = threading.Thread(target=self._feed_loop, daemon=True, name="ai4e-pool-feed")
+            self._feed.start()
+
+    def add_waiter(self, task_id: str, cb: Callable[[str], None]) -> None:
+        with self._wmu:
+            self._waiters[task_id] = cb
+
+    def pop_waiter(self, task_id: str) -> Optional[Callable[[str], None]]:
+        with self._wmu:
+            return self._waiters.pop(task_id, None)
+
+    def _feed_loop(self) -> None:
+        while not self._stop.is_set():
+            ids = self.sched.wait_completed(0.2)
+            if not ids or not self._waiters:
+                continue
+            with self._wmu:
+                cbs = [(t, self._waiters.pop(t)) for t in ids if t in self._waiters]
+            for t, cb in cbs:
+                try:
+                    cb(t)
+                except Exception:
+                    pass
+
+    # ------------------------------------------------------------ results / stats
+    def refresh(self) -> None:
+        stats = {s["rank"]: s for s in self.sched.worker_stats()}
+        for w in self.workers:
+            s = stats.get(w.rank)
+            if s is not None:
+                w.stats = s
+                if not self.describe and s.get("info"):
+                    try:
+                        self.describe = json.loads(s["info"])
+                    except ValueError:
+                        pass
+
+    def result(self, task_id: str) -> Optional[dict]:
+        if not self.describe:
+            self.refresh()
+        row = self.store.result(task_id)
+        if row is None or not self.describe:
+            return None
+        return format_result(self.describe.get("kind", "raw"), self.describe.get("outputs", []), row)
 
     @property
     def images(self) -> int:
-        return sum(w.images for w in self.workers)
+        return int(self.sched.images_done())
 
-    # ------------------------------------------------------------ per-worker dispatcher
-    def _dispatch_loop(self, w: _WorkerHandle) -> None:
-        while not w.stop.is_set():
-            # drain worker messages
-            try:
-                while w.conn.poll(0):
-                    self._on_msg(w, w.conn.recv())
-            except (EOFError, OSError):
-                pass
-            if not w.proc.is_alive() or (w.ready and time.time() - w.last_hb > self.hb_timeout):
-                self._fail_over(w)
-                return
-            if not w.ready or len(w.outstanding) >= self.depth:
-                w.conn.poll(0.0005)
-                continue
-            msgs = self.queue.receive(self.spec.max_batch, 0.0005 if w.outstanding else 0.02, self.max_delay_s)
-            if not msgs:
-                continue
-            ids = [m.task_id for m in msgs]
-            seqs = [m.seq for m in msgs]
-            slots = [m.ref for m in msgs]
-            self.store.transition_many(ids, STATE_RUNNING, STATE_RUNNING)
-            with self._bmu:
-                bid = self._bid
-                self._bid += 1
-            w.outstanding[bid] = (ids, seqs, slots)
-            try:
-                w.conn.send(("batch", bid, slots))
-            except (BrokenPipeError, OSError):
-                self._fail_over(w)
-                return
-
-    def _on_msg(self, w: _WorkerHandle, msg) -> None:
-        kind = msg[0]
-        if kind == "hb":
-            w.last_hb = time.time()
-        elif kind == "ready":
-            w.ready = True
-            w.last_hb = time.time()
-            self.events.append((time.time(), "ready", w.rank))
-        elif kind == "done":
-            _, bid, idx, prob = msg
-            ids, seqs, slots = w.outstanding.pop(bid)
-            self.ring.free(slots)
-            self.results.put_batch(ids, idx, prob)
-            self.store.transition_many(ids, STATE_COMPLETED, STATE_COMPLETED)
-            self.queue.complete(seqs)
-            w.batches += 1
-            w.images += len(ids)
-            if self.on_batch_done is not None:
-                self.on_batch_done(ids)
-
-    def _fail_over(self, w: _WorkerHandle) -> None:
-        """Requeue the dead/hung worker's in-flight batches and restart it (bounded)."""
-        self.events.append((time.time(), "worker_failed", w.rank))
-        for bid, (ids, seqs, slots) in list(w.outstanding.items()):
-            self.store.transition_many(ids, "created", "Awaiting service availability. Worker failed; requeued.")
-            for s in seqs:
-                self.queue.abandon(s, 0.0)
-        w.outstanding.clear()
-        dead = self.queue.take_deadletters()
-        if dead:
-            self.store.transition_many(dead, STATE_FAILED, "Task failed - maximum retries exceeded")
-        if w.proc is not None and w.proc.is_alive():
-            w.proc.kill()
-            w.proc.join(10)
-        if w.restarts < self.max_restarts and not w.stop.is_set():
-            w.restarts += 1
-            self.events.append((time.time(), "restart", w.rank))
-            self._spawn(w)
-        else:
-            w.stop.set()
-            self.events.append((time.time(), "removed", w.rank))
+    def stats(self) -> dict:
+        self.refresh()
+        return {"workers": [dict(w.stats, device=w.device, restarts=w.restarts) for w in self.workers],
+                "batch_histogram": self.sched.batch_histogram(), "images": self.images,
+                "ring": {"slots": self.ring.nslots, "local_used": self.ring.slots.used()}}

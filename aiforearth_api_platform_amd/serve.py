@@ -46,6 +46,8 @@ def build_platform(doc: Dict[str, Any], cfg: Config):
     """Build (control_plane, gateway, endpoints, dispatchers) from a platform YAML document."""
     from .runtime.engine import InferenceEngine, PayloadRing
     from .runtime.model_endpoint import ModelEndpoint
+    from .runtime.servable import as_servable
+    from .runtime.serving import GpuBatchWorker
     from .runtime.worker_pool import ModelSpec, WorkerPool
 
     cp = ControlPlane(cfg, AI4ELogger(level=logging.DEBUG if cfg.debug else logging.INFO))
@@ -57,22 +59,25 @@ def build_platform(doc: Dict[str, Any], cfg: Config):
         mb = int(e.get("max_batch", cfg.max_batch))
         devs = _devices(e.get("devices", "all"))
         buckets = bucket_list(e.get("batch_buckets", cfg.batch_buckets), mb)
+        graphs = bool(e.get("hip_graphs", cfg.use_hip_graphs))
         if e.get("mode", "pool") == "pool":
-            spec = ModelSpec(e["factory"], shape, mb, int(e.get("topk", 5)), dict(e.get("kwargs") or {}),
-                             bool(e.get("hip_graphs", cfg.use_hip_graphs)), tuple(buckets))
+            spec = ModelSpec(e["factory"], shape, mb, int(e.get("topk", 5)), dict(e.get("kwargs") or {}), graphs,
+                             tuple(buckets))
             pool = WorkerPool(cp, base_url + e["path"], spec, devs, max_delay_s=cfg.max_batch_delay_ms / 1e3,
                               heartbeat_interval_s=cfg.heartbeat_interval_s,
-                              heartbeat_timeout_s=cfg.heartbeat_timeout_s)
-            ep = ModelEndpoint(cp, e["path"], None, pool.ring, worker=pool, base_url=base_url)
+                              heartbeat_timeout_s=cfg.heartbeat_timeout_s,
+                              ring_slots=int(e.get("ring_slots", 0)))
+            ep = ModelEndpoint(cp, e["path"], worker=pool, base_url=base_url)
         else:
             dev = torch.device(devs[0])
-            model = _load(e["factory"])(device=str(dev), **(e.get("kwargs") or {}))
-            eng = InferenceEngine(model, shape, mb, device=dev, topk=int(e.get("topk", 5)),
-                                  use_graphs=bool(e.get("hip_graphs", cfg.use_hip_graphs)),
-                                  head_fn=getattr(model, "topk_u8", None), buckets=buckets)
+            servable = as_servable(_load(e["factory"])(device=str(dev), **(e.get("kwargs") or {})),
+                                   int(e.get("topk", 5)))
+            eng = InferenceEngine(None, shape, mb, device=dev, use_graphs=graphs, buckets=buckets,
+                                  output_fn=servable, timing=dev.type == "cuda")
             eng.warmup()
-            ring = PayloadRing(mb * 4, shape)
-            ep = ModelEndpoint(cp, e["path"], eng, ring, base_url=base_url)
+            ring = PayloadRing(int(e.get("ring_slots", 0)) or mb * 4, shape)
+            worker = GpuBatchWorker(cp, base_url + e["path"], eng, ring, kind=servable.kind, outputs=servable.outputs)
+            ep = ModelEndpoint(cp, e["path"], worker=worker, base_url=base_url)
         endpoints[name] = ep
     table = RouteTable()
     dispatchers = []
@@ -121,12 +126,23 @@ def main(argv=None) -> int:
     for d in dispatchers:
         d.start()
     cp.start_metric_timers()
+    scalers = []
+    if cfg.autoscale:
+        from .runtime.autoscale import QueueDepthAutoscaler
+
+        for ep in endpoints.values():
+            if getattr(ep, "is_pool", False):
+                scalers.append(QueueDepthAutoscaler(ep.worker, min_workers=cfg.autoscale_min_workers,
+                                                    target_per_worker=cfg.autoscale_target_per_worker,
+                                                    period_s=cfg.autoscale_period_s).start())
     gw.install_signal_handlers()
     print(f"ai4e-mi355x gateway on http://{cfg.host}:{cfg.port} endpoints={list(endpoints)}", file=sys.stderr,
           flush=True)
     try:
         gw.run(cfg.host, cfg.port)
     finally:
+        for sc in scalers:
+            sc.stop()
         for d in dispatchers:
             d.stop()
         for ep in endpoints.values():

@@ -68,13 +68,16 @@ class _SortedSet:
 
 class _Record:
     __slots__ = ("task_id", "timestamp", "status", "backend_status", "endpoint", "endpoint_path",
-                 "publish_to_grid", "t_created", "t_running", "t_finished")
+                 "publish_to_grid", "t_created", "t_running", "t_finished", "result", "stage", "trace")
 
     def __init__(self):
         self.task_id = ""
         self.timestamp = self.status = self.backend_status = self.endpoint = self.endpoint_path = ""
         self.publish_to_grid = False
         self.t_created = self.t_running = self.t_finished = 0.0
+        self.result = None
+        self.stage = None
+        self.trace = ""
 
     def as_dict(self) -> dict:
         return {"TaskId": self.task_id, "Timestamp": self.timestamp, "Status": self.status,
@@ -155,7 +158,7 @@ class TaskStore:
             self._journal_write(r, body if (publish_to_grid and body) else None)
             return self._serialize(r), publish_body
 
-    def create_many(self, endpoint: str, n: int, status: str = "created") -> List[str]:
+    def create_many(self, endpoint: str, n: int, status: str = "created", trace: str = "") -> List[str]:
         with self._mu:
             wnow, mnow = time.time(), time.monotonic()
             ts, path = dotnet_timestamp(wnow), absolute_path(endpoint)
@@ -166,6 +169,7 @@ class TaskStore:
                 r.task_id = uuid4()
                 r.timestamp, r.status, r.backend_status = ts, status, "created"
                 r.endpoint, r.endpoint_path, r.publish_to_grid, r.t_created = endpoint, path, True, mnow
+                r.trace = trace
                 self._records[r.task_id] = r
                 created.add(r.task_id, float(int(wnow)))
                 self._journal_write(r, None)
@@ -186,6 +190,66 @@ class TaskStore:
                 self._journal_write(r, None)
                 n += 1
             return n
+
+    def retarget_many(self, ids, endpoint: str, status: str) -> int:
+        """Pipeline hop (AddPipelineTask): same TaskIds -> created@next endpoint -> running there."""
+        n = 0
+        for tid in ids:
+            if tid in self._records:
+                self.upsert(tid, status, "created", endpoint, None, self._records[tid].publish_to_grid)
+                n += 1
+        self.transition_many(ids, "running", status)
+        return n
+
+    def finish_batch(self, ids, rows: bytes, row_bytes: int, ok=(), stage=(), worker: int = -1,
+                     status_ok: str = "completed", status_fail: str = "Task failed - try again") -> None:
+        ok = list(ok)
+        with self._mu:
+            wnow, mnow = time.time(), time.monotonic()
+            ts = dotnet_timestamp(wnow)
+            for i, tid in enumerate(ids):
+                r = self._records.get(tid)
+                if r is None:
+                    continue
+                good = not ok or bool(ok[i])
+                r.timestamp, r.status = ts, status_ok if good else status_fail
+                r.backend_status = "completed" if good else "failed"
+                if good:
+                    r.result = bytes(rows[i * row_bytes:(i + 1) * row_bytes])
+                    r.stage = (list(stage) + [0.0] * 5)[:5] + [worker]
+                self._apply_index(r, wnow, mnow)
+                self._journal_write(r, None)
+
+    def result(self, task_id: str) -> Optional[bytes]:
+        with self._mu:
+            r = self._records.get(task_id)
+            return r.result if r is not None and r.backend_status == "completed" else None
+
+    def set_trace(self, task_id: str, trace: str) -> bool:
+        with self._mu:
+            r = self._records.get(task_id)
+            if r is None:
+                return False
+            r.trace = trace
+            return True
+
+    def trace(self, task_id: str) -> Optional[dict]:
+        with self._mu:
+            r = self._records.get(task_id)
+            if r is None:
+                return None
+            d = {"TaskId": r.task_id, "BackendStatus": r.backend_status, "trace": r.trace, "t_created": r.t_created,
+                 "t_running": r.t_running, "t_finished": r.t_finished}
+            if r.stage is not None:
+                d.update(worker=r.stage[5], t_worker_recv=r.stage[0], t_worker_launch=r.stage[1],
+                         t_worker_done=r.stage[2], gpu_h2d_ms=r.stage[3], gpu_compute_ms=r.stage[4])
+            return d
+
+    def latencies_window(self, path: str, t0: float, t1: float) -> List[float]:
+        with self._mu:
+            return [r.t_finished - r.t_created for r in self._records.values()
+                    if r.endpoint_path == path and r.backend_status in ("completed", "failed")
+                    and t0 <= r.t_finished <= t1]
 
     def set_status_text(self, task_id: str, status: str) -> bool:
         with self._mu:
@@ -292,6 +356,7 @@ class TaskStore:
                 r = self._records.get(tid)
                 if r is None:
                     r = self._records[tid] = _Record()
+                    r.t_created = time.monotonic()
                 elif r.backend_status:
                     self._idx(f"{r.endpoint_path}_{r.backend_status}").rem(tid)
                 r.task_id, r.timestamp, r.status = tid, d["Timestamp"], d["Status"]
@@ -301,6 +366,8 @@ class TaskStore:
                 self._idx(f"{r.endpoint_path}_{r.backend_status}").add(tid, float(d["_score"]))
                 if d.get("_orig") is not None:
                     self._orig[tid] = d["_orig"]
+                # finished records get a finish time, so TTL eviction applies to them too
+                r.t_finished = time.monotonic() if r.backend_status in ("completed", "failed") else 0.0
                 n += 1
             self._journal = saved
         return n
@@ -417,6 +484,10 @@ class DispatchQueue:
                 self._inflight[m.seq] = m
                 out.append(m)
         return out
+
+    def receive_batch(self, max_n: int = 1, timeout_s: float = 0.0, linger_s: float = 0.0):
+        ms = self.receive(max_n, timeout_s, linger_s)
+        return [m.task_id for m in ms], [m.ref for m in ms], [m.seq for m in ms]
 
     def complete(self, seqs) -> int:
         with self._cv:

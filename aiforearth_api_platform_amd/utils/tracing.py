@@ -6,7 +6,8 @@ via an OpenCensus tracer; mesh-level B3 spans go to App Insights
 (``Cluster/monitoring/application-insights-istio-adapter/configuration.yaml``).  Here a ``Tracer``
 offers the same ``span(name=...)`` context manager, propagates B3-style ids
 (``x-b3-traceid``/``x-b3-spanid``) and records the task pipeline stages
-(accept -> enqueue -> batch-form -> h2d -> compute -> d2h -> complete).  When running on the GPU it
+(accept -> batch-form -> worker -> h2d -> compute -> complete, :class:`StageClock` over the native
+task record).  When running on the GPU it
 also pushes ``roctx`` ranges so rocprofv3 kernel traces line up with request spans.
 """
 from __future__ import annotations
@@ -132,10 +133,44 @@ def get_tracer() -> Tracer:
     return _TRACER
 
 
-class StageClock:
-    """Per-task stage timestamps (monotonic) — the new framework's hot-path trace record."""
+# ---------------------------------------------------------------------------- B3 propagation
+B3_HEADERS = ("x-b3-traceid", "x-b3-spanid", "x-b3-parentspanid", "x-b3-sampled")
 
-    STAGES = ("accept", "enqueue", "batch_form", "h2d", "compute", "d2h", "complete")
+
+def b3_from_headers(headers) -> Dict[str, str]:
+    """Incoming B3 context (the Istio mesh headers the reference's adapter reads,
+    ``application-insights-istio-adapter/configuration.yaml``); a fresh trace when absent. The gateway
+    is the next hop, so it opens a child span of the caller's span."""
+    get = (lambda k: headers.get(k) or headers.get(k.upper()) or "") if headers is not None else (lambda k: "")
+    trace_id = get("x-b3-traceid") or _hexid(128)
+    parent = get("x-b3-spanid")
+    return {"x-b3-traceid": trace_id, "x-b3-spanid": _hexid(64), "x-b3-parentspanid": parent,
+            "x-b3-sampled": get("x-b3-sampled") or "1"}
+
+
+def b3_pack(ctx: Dict[str, str]) -> str:
+    """Compact form stored in the native task record: traceid/spanid/parentspanid."""
+    return f"{ctx['x-b3-traceid']}/{ctx['x-b3-spanid']}/{ctx.get('x-b3-parentspanid', '')}"
+
+
+def b3_unpack(s: str) -> Dict[str, str]:
+    parts = (s or "").split("/")
+    parts += [""] * (3 - len(parts))
+    return {"x-b3-traceid": parts[0], "x-b3-spanid": parts[1], "x-b3-parentspanid": parts[2]}
+
+
+# ---------------------------------------------------------------------------- per-task stages
+class StageClock:
+    """Per-task stage timestamps (CLOCK_MONOTONIC) of the hot path.
+
+    The native store keeps accept (``t_created``), dispatch (``t_running``) and finish times per task;
+    the GPU worker reports, per batch, when it received and launched the batch, when the GPU results
+    were ready and the GPU-side H2D / compute durations (``TaskStore.trace``). ``from_trace`` turns one
+    such record into the stage sequence accept -> enqueue(d) -> batch_form -> h2d -> compute -> d2h ->
+    complete, which ``GET /v1/taskmanagement/task/{id}/trace`` returns.
+    """
+
+    STAGES = ("accept", "batch_form", "worker_recv", "launch", "h2d_done", "gpu_done", "complete")
 
     def __init__(self):
         self.t: Dict[str, float] = {}
@@ -143,12 +178,36 @@ class StageClock:
     def mark(self, stage: str, t: Optional[float] = None) -> None:
         self.t[stage] = time.monotonic() if t is None else t
 
+    @classmethod
+    def from_trace(cls, tr: dict) -> "StageClock":
+        c = cls()
+        if tr.get("t_created"):
+            c.mark("accept", tr["t_created"])
+        if tr.get("t_running"):
+            c.mark("batch_form", tr["t_running"])
+        if tr.get("t_worker_recv"):
+            c.mark("worker_recv", tr["t_worker_recv"])
+        if tr.get("t_worker_launch"):
+            c.mark("launch", tr["t_worker_launch"])
+            if tr.get("gpu_h2d_ms"):
+                c.mark("h2d_done", tr["t_worker_launch"] + tr["gpu_h2d_ms"] / 1e3)
+        if tr.get("t_worker_done"):
+            c.mark("gpu_done", tr["t_worker_done"])
+        if tr.get("t_finished"):
+            c.mark("complete", tr["t_finished"])
+        return c
+
     def durations_ms(self) -> Dict[str, float]:
         out = {}
         prev = None
         for s in self.STAGES:
             if s in self.t:
                 if prev is not None:
-                    out[f"{prev}->{s}"] = (self.t[s] - self.t[prev]) * 1e3
+                    out[f"{prev}->{s}"] = round((self.t[s] - self.t[prev]) * 1e3, 4)
                 prev = s
         return out
+
+    def to_dict(self) -> dict:
+        base = min(self.t.values()) if self.t else 0.0
+        return {"stages_ms_from_accept": {k: round((v - base) * 1e3, 4) for k, v in self.t.items()},
+                "durations_ms": self.durations_ms()}

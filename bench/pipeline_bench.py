@@ -29,7 +29,7 @@ def main():
     det = FasterRCNN(DetectorConfig(), seed=0, device=d.device)
     cls = FusedResNet(resnet50(num_classes=200, seed=1), device=d.device)
     pcfg = PipelineConfig(score_thresh=0.0, class_id=None, max_crops_per_image=4)
-    p = DetectClassifyPipeline(det, cls.forward, d.device, pcfg)
+    p = DetectClassifyPipeline(det, cls.forward_u8, d.device, pcfg)
     g = torch.Generator().manual_seed(d.rank)
     batches = [torch.randint(0, 256, (a.batch, a.size, a.size, 3), dtype=torch.uint8, generator=g).to(d.device)
                for _ in range(2)]

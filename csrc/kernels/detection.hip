@@ -332,6 +332,37 @@ __global__ __launch_bounds__(256) void crop_resize_kernel(const uint8_t* __restr
   }
 }
 
+// Crop + bilinear resize to uint8 [R, OH, OW, C] (no normalization): the detector -> classifier
+// wire format of the ensemble (3 bytes per pixel instead of 16 for bf16x8; the classifier stem
+// normalizes on its side) and the GPU resize of K7 (a whole-image box).
+__global__ __launch_bounds__(256) void crop_resize_u8_kernel(const uint8_t* __restrict__ img,
+                                                             const float* __restrict__ boxes, uint8_t* __restrict__ out,
+                                                             int H, int W, int C, int R, int OH, int OW) {
+  const long total = static_cast<long>(R) * OH * OW;
+  for (long idx = blockIdx.x * 256L + threadIdx.x; idx < total; idx += static_cast<long>(gridDim.x) * 256) {
+    const int ox = static_cast<int>(idx % OW);
+    long t = idx / OW;
+    const int oy = static_cast<int>(t % OH);
+    const int r = static_cast<int>(t / OH);
+    const float* bx = boxes + 5L * r;
+    const int n = static_cast<int>(bx[0]);
+    const float sx = bx[1] + (ox + 0.5f) * (bx[3] - bx[1]) / OW - 0.5f;
+    const float sy = bx[2] + (oy + 0.5f) * (bx[4] - bx[2]) / OH - 0.5f;
+    const float cy = fminf(fmaxf(sy, 0.f), H - 1.f), cx = fminf(fmaxf(sx, 0.f), W - 1.f);
+    const int y0 = static_cast<int>(cy), x0 = static_cast<int>(cx);
+    const int y1 = min(y0 + 1, H - 1), x1 = min(x0 + 1, W - 1);
+    const float ly = cy - y0, lx = cx - x0;
+    const uint8_t* base = img + static_cast<long>(n) * H * W * C;
+    uint8_t* o = out + idx * C;
+    for (int c = 0; c < C; ++c) {
+      const float a = base[(static_cast<long>(y0) * W + x0) * C + c], b = base[(static_cast<long>(y0) * W + x1) * C + c];
+      const float d = base[(static_cast<long>(y1) * W + x0) * C + c], e = base[(static_cast<long>(y1) * W + x1) * C + c];
+      const float pix = (1 - ly) * ((1 - lx) * a + lx * b) + ly * ((1 - lx) * d + lx * e);
+      o[c] = static_cast<uint8_t>(fminf(fmaxf(pix + 0.5f, 0.f), 255.f));
+    }
+  }
+}
+
 inline int grid_for(long work) {
   long g = (work + 255) / 256;
   return static_cast<int>(g < 1 ? 1 : (g > 8192 ? 8192 : g));
@@ -411,11 +442,17 @@ AI4E_API int ai4e_roi_align_fpn_nhwc(const void* f0, const void* f1, const void*
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
 }
 
+// mode 0: normalized bf16 [R, OH, OW, 8]; mode 1: uint8 [R, OH, OW, C] (norm unused).
 AI4E_API int ai4e_crop_resize_nhwc(const void* img, const void* boxes, void* out, const void* norm, int H, int W, int C,
-                                   int R, int OH, int OW, int unused, hipStream_t s) {
-  (void)unused;
-  if (C > 8) return AI4E_EINVAL;
+                                   int R, int OH, int OW, int mode, hipStream_t s) {
+  if (C > 8 || C < 1) return AI4E_EINVAL;
   if (R <= 0) return AI4E_OK;
+  if (mode == 1) {
+    hipLaunchKernelGGL(crop_resize_u8_kernel, dim3(grid_for(static_cast<long>(R) * OH * OW)), dim3(256), 0, s,
+                       static_cast<const uint8_t*>(img), static_cast<const float*>(boxes), static_cast<uint8_t*>(out), H,
+                       W, C, R, OH, OW);
+    return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
+  }
   hipLaunchKernelGGL(crop_resize_kernel, dim3(grid_for(static_cast<long>(R) * OH * OW)), dim3(256), 0, s,
                      static_cast<const uint8_t*>(img), static_cast<const float*>(boxes), static_cast<uint16_t*>(out),
                      static_cast<const float*>(norm), H, W, C, R, OH, OW);

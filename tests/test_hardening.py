@@ -1,0 +1,240 @@
+"""Poison messages, per-item isolation, restart recovery of GPU-endpoint tasks, 400/415 payloads,
+binary batch ingest, B3 trace propagation and the queue-depth autoscaler (CPU)."""
+import asyncio
+import json
+import time
+
+import numpy as np
+import pytest
+import torch
+from aiohttp.test_utils import TestClient, TestServer
+
+from aiforearth_api_platform_amd.config import Config
+from aiforearth_api_platform_amd.gateway.control import ControlPlane
+from aiforearth_api_platform_amd.gateway.server import BATCH_CONTENT_TYPE, Gateway, Route, RouteTable
+from aiforearth_api_platform_amd.runtime.autoscale import QueueDepthAutoscaler
+from aiforearth_api_platform_amd.runtime.engine import InferenceEngine, PayloadRing
+from aiforearth_api_platform_amd.runtime.model_endpoint import PAYLOAD_LOST, ModelEndpoint
+from aiforearth_api_platform_amd.runtime.serving import GpuBatchWorker
+from aiforearth_api_platform_amd.runtime.worker_pool import ModelSpec, WorkerPool
+
+SHAPE = (4, 4, 3)
+SPEC = ModelSpec("aiforearth_api_platform_amd.models.toy:tiny_classifier", SHAPE, max_batch=8, topk=2,
+                 use_graphs=False)
+PATH = "/v1/ai4e/tiny/classify"
+EP = "http://127.0.0.1" + PATH
+
+
+def tiny_model(x_u8):
+    m = x_u8.float().mean(dim=(1, 2))
+    return torch.cat([m, torch.zeros(m.shape[0], 3)], dim=1)
+
+
+def _imgs(n):
+    a = np.zeros((n, *SHAPE), np.uint8)
+    a[np.arange(n), :, :, np.arange(n) % 3] = 100
+    return a
+
+
+def _wait(cond, t=60):
+    d = time.time() + t
+    while time.time() < d:
+        if cond():
+            return True
+        time.sleep(0.02)
+    return False
+
+
+def _local_endpoint(cp):
+    eng = InferenceEngine(tiny_model, SHAPE, 8, device=torch.device("cpu"), topk=2)
+    ring = PayloadRing(32, SHAPE)
+    w = GpuBatchWorker(cp, EP, eng, ring, max_delay_s=0.05)
+    return ModelEndpoint(cp, PATH, worker=w)
+
+
+def test_poison_message_fails_alone_local():
+    cp = ControlPlane(Config.load(env={}))
+    ep = _local_endpoint(cp)
+    q = cp.queue_for(EP)
+    bad = cp.store.create_many(EP, 1)
+    q.send_many(bad, [-1])  # e.g. recovered after a restart without its ring slot
+    good = ep.submit_many(_imgs(7))
+    ep.worker.step(1.0)
+    ep.worker.flush()
+    assert cp.get_dict(bad[0])["BackendStatus"] == "failed"
+    assert all(cp.get_dict(t)["BackendStatus"] == "completed" for t in good)
+    assert q.stats()["ready"] == 0 and q.stats()["scheduled"] == 0  # no redelivery storm
+    cp.close()
+
+
+def test_poison_message_fails_alone_pool():
+    cp = ControlPlane(Config.load(env={}))
+    pool = WorkerPool(cp, EP, SPEC, ["cpu"], heartbeat_interval_s=0.1, max_delay_s=0.05).start()
+    try:
+        bad = cp.store.create_many(EP, 1)
+        cp.queue_for(EP).send_many(bad, [10 ** 9])
+        good = pool.submit_many(_imgs(7))
+        assert _wait(lambda: cp.store.zcard(PATH + "_completed") == 7 and cp.store.zcard(PATH + "_failed") == 1)
+        assert cp.get_dict(bad[0])["Status"] == "Task failed - invalid payload"
+        pool.refresh()
+        assert all(w.ready for w in pool.workers)  # the pool survived
+        assert pool.result(good[3])["classes"][0] == 0
+    finally:
+        pool.stop()
+        cp.close()
+
+
+def test_batch_failure_isolates_the_bad_item(monkeypatch):
+    # batch 1 raises at launch -> items re-run one by one; slot 2's isolated run raises -> only it fails
+    monkeypatch.setenv("AI4E_FAULT_INJECTION", "fail_batch=1,fail_item=2")
+    cp = ControlPlane(Config.load(env={}))
+    pool = WorkerPool(cp, EP, SPEC, ["cpu"], heartbeat_interval_s=0.1, max_delay_s=0.2).start()
+    try:
+        ids = pool.submit_many(_imgs(8))
+        assert _wait(lambda: cp.store.zcard(PATH + "_completed") + cp.store.zcard(PATH + "_failed") == 8)
+        st = [cp.get_dict(t)["BackendStatus"] for t in ids]
+        assert st.count("failed") == 1 and st[2] == "failed"
+        assert pool.result(ids[5])["classes"][0] == 2
+    finally:
+        pool.stop()
+        cp.close()
+
+
+@pytest.mark.parametrize("journal_body", [True, False])
+def test_recover_model_endpoint_tasks(tmp_path, journal_body):
+    j = str(tmp_path / "j.jsonl")
+    cap = 1 << 20 if journal_body else 0
+    cp = ControlPlane(Config.load(env={}, journal_path=j))
+    ep = _local_endpoint(cp)
+    ep.journal_cap = cap
+    img = _imgs(3)[2]
+    tid = json.loads(ep.submit(img.tobytes(), "application/octet-stream"))["TaskId"]
+    cp.close()  # "crash" before the worker ran: the task is still created, its ring slot is gone
+    cp2 = ControlPlane(Config.load(env={}, journal_path=str(tmp_path / "j2.jsonl")))
+    ep2 = _local_endpoint(cp2)
+    out = cp2.recover(j)
+    assert out["replayed"] >= 1
+    if journal_body:
+        assert out["requeued"] == 1
+        ep2.worker.step(1.0)
+        ep2.worker.flush()
+        assert cp2.get_dict(tid)["BackendStatus"] == "completed"
+        assert ep2.result(tid)["classes"][0] == 2
+    else:
+        assert out["failed"] == 1
+        rec = cp2.get_dict(tid)
+        assert rec["BackendStatus"] == "failed" and rec["Status"] == PAYLOAD_LOST
+        assert cp2.queue_for(EP).depth() == 0
+    cp2.close()
+
+
+def test_evict_finished_applies_to_replayed_records(tmp_path):
+    j = str(tmp_path / "j.jsonl")
+    cp = ControlPlane(Config.load(env={}, journal_path=j))
+    ids = cp.store.create_many(EP, 3)
+    cp.store.transition_many(ids, "completed", "done")
+    cp.close()
+    cp2 = ControlPlane(Config.load(env={}))
+    cp2.recover(j)
+    assert cp2.store.size() == 3 and cp2.store.evict_finished(0.0) == 3 and cp2.store.size() == 0
+
+
+def _run(coro):
+    return asyncio.new_event_loop().run_until_complete(coro)
+
+
+def test_http_payload_errors_batch_ingest_and_b3_trace():
+    cp = ControlPlane(Config.load(env={}))
+    ep = _local_endpoint(cp).start()
+    table = RouteTable()
+    table.add(Route("/v1/tiny/async", "async", ep))
+    table.add(Route("/v1/tiny/sync", "sync", ep))
+    gw = Gateway(cp, table)
+
+    async def go():
+        c = TestClient(TestServer(gw.app))
+        await c.start_server()
+        try:
+            r = await c.post("/v1/tiny/async", data=b"\x00" * 7, headers={"Content-Type": "application/octet-stream"})
+            assert r.status == 400
+            r = await c.post("/v1/tiny/async", data=b"xx", headers={"Content-Type": "text/csv"})
+            assert r.status == 415
+            r = await c.post("/v1/tiny/async", data=b"{not json", headers={"Content-Type": "application/json"})
+            assert r.status == 400
+            assert cp.store.size() == 0  # no task for rejected payloads
+            r = await c.post("/v1/tiny/async", data=_imgs(5).tobytes(), headers={"Content-Type": BATCH_CONTENT_TYPE})
+            assert r.status == 200
+            ids = (await r.json())["TaskIds"]
+            assert len(ids) == 5
+            tid = "0af7651916cd43dd8448eb211c80319c"
+            r = await c.post("/v1/tiny/async", data=_imgs(1).tobytes(),
+                             headers={"Content-Type": "application/octet-stream", "x-b3-traceid": tid,
+                                      "x-b3-spanid": "b7ad6b7169203331"})
+            assert r.headers["x-b3-traceid"] == tid and r.headers["x-b3-parentspanid"] == "b7ad6b7169203331"
+            one = (await r.json())["TaskId"]
+            for _ in range(200):
+                rec = await (await c.get(f"/v1/taskmanagement/task/{one}")).json()
+                if rec["BackendStatus"] == "completed":
+                    break
+                await asyncio.sleep(0.02)
+            tr = await (await c.get(f"/v1/taskmanagement/task/{one}/trace")).json()
+            assert tr["x-b3-traceid"] == tid and tr["t_finished"] >= tr["t_running"] >= tr["t_created"] > 0
+            assert "accept->batch_form" in tr["durations_ms"]
+            res = await (await c.get(f"/v1/taskmanagement/task/{ids[4]}/result")).json()
+            assert res["Result"]["classes"][0] == 1
+            r = await c.post("/v1/tiny/sync", data=b"\x01\x02", headers={"Content-Type": "application/octet-stream"})
+            assert r.status == 400
+        finally:
+            await c.close()
+
+    try:
+        _run(go())
+    finally:
+        ep.stop()
+        cp.close()
+
+
+class _FakeQueue:
+    def __init__(self):
+        self.depth = 0
+
+    def stats(self):
+        return {"ready": self.depth, "scheduled": 0, "inflight": 0}
+
+
+class _FakeWorker:
+    def __init__(self):
+        from threading import Event
+        self.stop = Event()
+        self.stats = {"outstanding": 0}
+
+
+class _FakePool:
+    endpoint = "/v1/fake"
+
+    def __init__(self, n=1, devices=8):
+        self.devices = [f"cuda:{i}" for i in range(devices)]
+        self.spec = SPEC
+        self.queue = _FakeQueue()
+        self.workers = [_FakeWorker() for _ in range(n)]
+
+    def active(self):
+        return sum(1 for w in self.workers if not w.stop.is_set())
+
+    def resize(self, n):
+        while self.active() < n:
+            self.workers.append(_FakeWorker())
+        for w in [w for w in self.workers if not w.stop.is_set()][n:]:
+            w.stop.set()
+
+
+def test_autoscaler_scales_on_queue_depth_with_stabilized_scale_down():
+    pool = _FakePool(1)
+    sc = QueueDepthAutoscaler(pool, min_workers=1, target_per_worker=2.0, down_stabilization=3)
+    pool.queue.depth = 8 * 9  # 9 full batches waiting -> ceil(9/2) = 5 workers
+    assert sc.step() == 5 and pool.active() == 5
+    pool.queue.depth = 8 * 100  # capped at the node's 8 GPUs
+    assert sc.step() == 8 and pool.active() == 8
+    pool.queue.depth = 0
+    assert sc.step() == 8 and sc.step() == 8  # stabilization window
+    assert sc.step() == 1 and pool.active() == 1

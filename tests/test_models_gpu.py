@@ -87,7 +87,7 @@ def test_pipeline_and_spatial_single_gpu():
     from aiforearth_api_platform_amd.runtime.spatial import SpatialSegmenter
     det = FasterRCNN(DetectorConfig(box_score_thresh=0.0), seed=0, device=DEV)
     cls = FusedResNet(resnet50(num_classes=20, seed=1), device=DEV)
-    p = DetectClassifyPipeline(det, cls.forward, DEV, PipelineConfig(score_thresh=0.0, class_id=None))
+    p = DetectClassifyPipeline(det, cls.forward_u8, DEV, PipelineConfig(score_thresh=0.0, class_id=None))
     out = p.run_batches([torch.randint(0, 256, (2, 256, 256, 3), dtype=torch.uint8, device=DEV)])
     dets, boxes, res = out[0]
     assert boxes.shape[0] == res.shape[0] > 0 and torch.all((res[:, 0] >= 0) & (res[:, 0] < 20))

@@ -44,6 +44,7 @@ def test_pool_two_workers_complete_all(cp):
         assert _wait(lambda: cp.store.zcard("/v1/ai4e/tiny/classify_completed") == 40)
         for i, t in enumerate(ids):
             assert pool.result(t)["classes"][0] == i % 3
+        pool.refresh()
         assert sum(1 for w in pool.workers if w.batches > 0) >= 1
     finally:
         pool.stop()
