@@ -279,7 +279,7 @@ def worker_main(conn, rank: int, device: str, spec: ModelSpec, shm_name: str, ns
         from ..store import native
 
         local_ring = native.SlotRing(partition[1], partition[0])
-    fc = P.FrameConn(conn)
+    fc = conn if isinstance(conn, P.FrameConn) else P.FrameConn(conn)
     w = GpuWorker(fc, rank, device, spec, buf, local_ring=local_ring, hb_interval=hb_interval)
     try:
         w.serve(pinned)

@@ -120,6 +120,13 @@ class NodeScheduler {
 
   // Takes ownership of `fd` (a connected stream socket). dispatch=false: ingest-only connection.
   void attach(int rank, int fd, bool dispatch) {
+    {
+      std::lock_guard<std::mutex> g(fail_mu_);
+      if (stopped_) {  // shutting down: never start threads nobody will join
+        ::close(fd);
+        return;
+      }
+    }
     std::unique_ptr<Worker> old;
     {
       std::lock_guard<std::mutex> g(mu_);
@@ -229,23 +236,25 @@ class NodeScheduler {
   void stop() {
     {
       std::lock_guard<std::mutex> g(fail_mu_);
-      if (stopped_) return;
       stopped_ = true;
     }
     fail_cv_.notify_all();
     feed_cv_.notify_all();
-    std::vector<std::unique_ptr<Worker>> ws;
-    {
-      std::lock_guard<std::mutex> g(mu_);
-      for (auto& kv : workers_) ws.push_back(std::move(kv.second));
-      workers_.clear();
+    for (;;) {  // until no worker is left (an attach racing with stop is refused after stopped_)
+      std::vector<std::unique_ptr<Worker>> ws;
+      {
+        std::lock_guard<std::mutex> g(mu_);
+        for (auto& kv : workers_) ws.push_back(std::move(kv.second));
+        workers_.clear();
+      }
+      if (ws.empty()) break;
+      for (auto& w : ws) {
+        send_simple(*w, F_STOP);
+        mark_dead(*w, "stopped", false);
+      }
+      queue_->kick();
+      for (auto& w : ws) join_worker(*w);
     }
-    for (auto& w : ws) {
-      send_simple(*w, F_STOP);
-      mark_dead(*w, "stopped", false);
-    }
-    queue_->kick();
-    for (auto& w : ws) join_worker(*w);
   }
 
  private:
