@@ -1,0 +1,122 @@
+"""Servable factories of the platform's model families (``ModelSpec.factory`` / platform YAML).
+
+The reference deploys each model as its own container behind an API route: the camera-trap
+detector (``APIs/Charts/camera-trap/detection-{async,sync}``, MegaDetector on TF 1.9) and the
+land-cover service (``APIManagement/create_sync_api_management_api.sh:9-92``: classify /
+classifybyextent / tile / tilebyextent), chained with ``AddPipelineTask`` for ensembles
+(``APIs/1.0/Common/task_management/distributed_api_task.py:67-100``). Here each factory returns a
+:class:`runtime.servable.Servable` that a GPU worker process runs on fixed-shape batches:
+
+* :func:`resnet50_classifier` — the headline classifier (fused ResNet-50 + fused top-k head);
+* :func:`megadetector` — Faster-RCNN R50-FPN (K1 convs, K4 NMS, K5 RoIAlign) -> detections;
+* :func:`landcover` — U-Net over a tiled mosaic (K2 GroupNorm, K3 upsample, K6 stitch) -> class map;
+* :func:`camera_trap_ensemble` — detector -> crop classifier on one GPU with static shapes (the whole
+  two-stage batch is one HIP graph); the two-GPU RCCL form is :mod:`runtime.pipeline`.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from ..runtime.servable import (ClassifierServable, DetectorServable, EnsembleServable, SegmenterServable,
+                                OutputField)
+
+
+def resnet50_classifier(device="cuda", seed: int = 0, num_classes: int = 1000, topk: int = 5):
+    from .resnet import FusedResNet, resnet50
+
+    m = FusedResNet(resnet50(num_classes=num_classes, seed=seed), device=device)
+    return ClassifierServable(m, topk, head=m.topk_u8)
+
+
+def megadetector(device="cuda", seed: int = 0, max_dets: Optional[int] = None, **cfg):
+    from .faster_rcnn import DetectorConfig, FasterRCNN
+
+    det = FasterRCNN(DetectorConfig(**cfg), seed=seed, device=device)
+    return DetectorServable(det, max_dets)
+
+
+def landcover(device="cuda", height: int = 4096, width: int = 4096, tile: int = 512, stride: int = 448,
+              tile_batch: int = 16, n_classes: int = 7, seed: int = 0):
+    from ..ops.stitch import TileGrid
+    from ..runtime.spatial import SpatialSegmenter
+    from .unet import FusedUNet, unet_landcover
+
+    f = FusedUNet(unet_landcover(n_classes=n_classes, seed=seed), device=device)
+    seg = SpatialSegmenter(f.forward_u8, TileGrid(height, width, tile, stride), f.n_classes, torch.device(device),
+                           tile_batch=tile_batch, local=True)
+    return SegmenterServable(seg.run, height, width, f.n_classes)
+
+
+def select_crops_padded(dets, max_crops: int, score_thresh: float, class_id: Optional[int]):
+    """Static-shape crop selection: the first ``max_crops`` confident detections of each image
+    (score order) -> boxes [B, M, 4], scores [B, M], valid [B, M] (no host sync, graph-capturable)."""
+    boxes, scores, labels, n = dets
+    B, D = scores.shape
+    M = max_crops
+    rank = torch.arange(D, device=scores.device)[None].expand(B, D)
+    ok = (rank < n[:, None].long()) & (scores > score_thresh)
+    if class_id is not None:
+        ok &= labels == class_id
+    pos = torch.cumsum(ok.int(), 1) - 1
+    keep = ok & (pos < M)
+    dst = torch.where(keep, pos, torch.full_like(pos, M)).long()  # slot M = discard
+    sel_b = torch.zeros(B, M + 1, 4, device=boxes.device)
+    sel_s = torch.zeros(B, M + 1, device=boxes.device)
+    sel_b.scatter_(1, dst[..., None].expand(B, D, 4), boxes.float())
+    sel_s.scatter_(1, dst, scores.float())
+    valid = torch.arange(M, device=boxes.device)[None] < keep.sum(1, keepdim=True)
+    return sel_b[:, :M], sel_s[:, :M], valid
+
+
+class StaticEnsemble:
+    """Detector -> crop + resize (uint8, K5/K7) -> crop classifier, all static shapes."""
+
+    def __init__(self, detector, classifier, max_crops: int, score_thresh: float, class_id: Optional[int],
+                 crop_hw=(224, 224)):
+        self.detector, self.classifier = detector, classifier
+        self.max_crops, self.score_thresh, self.class_id, self.crop_hw = max_crops, score_thresh, class_id, crop_hw
+
+    def __call__(self, images_u8: torch.Tensor):
+        from ..ops.detection import crop_resize_u8
+
+        B = images_u8.shape[0]
+        M = self.max_crops
+        dets = self.detector(images_u8)
+        boxes, scores, valid = select_crops_padded(dets, M, self.score_thresh, self.class_id)
+        img = torch.arange(B, device=boxes.device, dtype=torch.float32)[:, None, None].expand(B, M, 1)
+        flat = torch.cat([img, boxes], -1).reshape(B * M, 5)
+        crops = crop_resize_u8(images_u8[..., :3].contiguous(), flat, self.crop_hw)
+        prob = torch.softmax(self.classifier(crops).float(), 1)
+        p, c = prob.max(1)
+        species = torch.where(valid, c.reshape(B, M).to(torch.int32), torch.full((B, M), -1, dtype=torch.int32,
+                                                                                  device=c.device))
+        sp_prob = torch.where(valid, p.reshape(B, M), torch.zeros_like(p.reshape(B, M)))
+        count = valid.sum(1, keepdim=True).to(torch.int32)
+        return boxes.contiguous(), (scores * valid).contiguous(), species, sp_prob, count
+
+
+class _EnsembleServable(EnsembleServable):
+    stages = 1  # the worker reports the detector -> classifier hop (AddPipelineTask) per batch
+
+    def __init__(self, model: StaticEnsemble):
+        super().__init__(None, model.max_crops)
+        self.model = model
+
+    def __call__(self, images_u8):
+        return self.model(images_u8)
+
+
+def camera_trap_ensemble(device="cuda", seed: int = 0, max_crops: int = 4, score_thresh: float = 0.5,
+                         class_id: Optional[int] = 1, num_species: int = 200, **det_cfg):
+    from .faster_rcnn import DetectorConfig, FasterRCNN
+    from .resnet import FusedResNet, resnet50
+
+    det = FasterRCNN(DetectorConfig(**det_cfg), seed=seed, device=device)
+    cls = FusedResNet(resnet50(num_classes=num_species, seed=seed + 1), device=device)
+    return _EnsembleServable(StaticEnsemble(det, cls.forward_u8, max_crops, score_thresh, class_id))
+
+
+__all__ = ["resnet50_classifier", "megadetector", "landcover", "camera_trap_ensemble", "select_crops_padded",
+           "StaticEnsemble", "OutputField"]

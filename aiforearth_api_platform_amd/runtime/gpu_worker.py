@@ -42,6 +42,8 @@ class ModelSpec:
     kwargs: Dict[str, Any] = field(default_factory=dict)
     use_graphs: bool = True
     buckets: Tuple[int, ...] = ()      # captured batch sizes (config.bucket_list); () = max_batch only
+    # ensemble stages: endpoint of each later stage (the scheduler re-targets the batch's tasks there)
+    stage_endpoints: Tuple[str, ...] = ()
 
 
 def load_factory(path: str):
@@ -243,6 +245,8 @@ class GpuWorker:
         h2d_ms, comp_ms = p.res.gpu_ms()
         self.busy_ms += h2d_ms + comp_ms
         rows = self._rows(p.n, p.valid, p.res.outputs)
+        if getattr(self.servable, "stages", 0):  # ensemble hop (AddPipelineTask) for this batch's tasks
+            self.conn.stage(p.bid, 0)
         self.conn.done(p.bid, p.status, rows, self.row_bytes, (p.t_recv, p.res.t_launch, t_done, h2d_ms, comp_ms))
 
     def _isolate(self, bid: int, slots: np.ndarray, valid: np.ndarray, status: np.ndarray, t_recv: float) -> None:

@@ -50,16 +50,18 @@ def owned_rows(grid: TileGrid, ranges: List[Tuple[int, int]], r: int) -> Tuple[i
 
 class SpatialSegmenter:
     def __init__(self, model_fn: Callable[[torch.Tensor], torch.Tensor], grid: TileGrid, n_out: int,
-                 device: torch.device, tile_batch: int = 16, group=None):
-        """model_fn: uint8 tiles [b, ts, ts, C_in] -> logits NHWC [b, ts, ts, n_out]."""
+                 device: torch.device, tile_batch: int = 16, group=None, local: bool = False):
+        """model_fn: uint8 tiles [b, ts, ts, C_in] -> logits NHWC [b, ts, ts, n_out].
+        ``local``: one-GPU segmentation even inside an initialized process group (a pool worker)."""
         self.model_fn = model_fn
         self.grid = grid
         self.n_out = n_out
         self.device = device
         self.tile_batch = tile_batch
         self.group = group
-        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
-        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        dist_on = dist.is_initialized() and not local
+        self.rank = dist.get_rank(group) if dist_on else 0
+        self.world = dist.get_world_size(group) if dist_on else 1
         if grid.ts >= 2 * grid.stride:
             raise ValueError("tile overlap must be < 50% (a halo of one tile row per boundary)")
         if grid.nty < self.world:

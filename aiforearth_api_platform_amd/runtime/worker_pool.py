@@ -131,6 +131,9 @@ class WorkerPool:
                                           linger_s=max_delay_s, depth=pipeline_depth, retry_delay_s=retry_delay_s,
                                           hb_timeout_s=heartbeat_timeout_s, poll_s=poll_s)
         self.sched.add_local_ring(self.ring.slots)
+        if spec.stage_endpoints:
+            self.sched.set_stage_endpoints(list(spec.stage_endpoints),
+                                           ["running - stage %d" % (i + 2) for i in range(len(spec.stage_endpoints))])
         for base, n, rank in self.remote_partitions:
             self.sched.add_remote_partition(base, n, rank)
         self.workers: List[_WorkerHandle] = []
