@@ -175,7 +175,8 @@ class Gateway:
         if rec is None:
             return None, None
         for be in self._backends():
-            if getattr(be, "path", None) == rec["EndpointPath"] or getattr(be, "endpoint", None) == rec["Endpoint"]:
+            paths = getattr(be, "paths", None) or [getattr(be, "path", None)]
+            if rec["EndpointPath"] in paths or getattr(be, "endpoint", None) == rec["Endpoint"]:
                 return rec, be
         return rec, None
 

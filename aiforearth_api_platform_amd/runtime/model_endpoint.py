@@ -110,6 +110,14 @@ class ModelEndpoint:
         control_plane.register_replayer(self.endpoint, self.replay)
 
     @property
+    def paths(self) -> List[str]:
+        """Endpoint paths whose tasks this endpoint owns: its own + later ensemble stages."""
+        from ..store.pystore import absolute_path
+
+        stages = getattr(getattr(self.worker, "spec", None), "stage_endpoints", ()) or ()
+        return [self.path] + [absolute_path(e) for e in stages]
+
+    @property
     def item_shape(self) -> Tuple[int, ...]:
         return tuple(self.ring.item_shape)
 
