@@ -58,7 +58,7 @@ def parse():
     # (8 x 768 slots), the layer2 chains (3 x 512) and layer3's c3 convs (6 x 512) to whole waves of
     # workgroups; 256 spills a few % of tiles into an extra, nearly empty wave (+1.8-2.1 % images/s measured)
     p.add_argument("--batch", type=int, default=250, help="images per step per GPU (= max dynamic batch)")
-    p.add_argument("--inflight", type=int, default=3, help="steps of ring slots per ingest shard")
+    p.add_argument("--inflight", type=int, default=2, help="steps of ring slots per ingest shard (+1)")
     p.add_argument("--image-size", type=int, default=224)
     p.add_argument("--backend", default="auto", choices=["auto", "hip", "torch"])
     p.add_argument("--no-graphs", action="store_true")
