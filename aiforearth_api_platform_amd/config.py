@@ -61,6 +61,8 @@ class Config:
     journal_path: str = field(default="", metadata={"env": "AI4E_JOURNAL"})
     finished_task_ttl_s: float = field(default=3600.0, metadata={"env": "AI4E_FINISHED_TASK_TTL_S"})
     evict_period_s: float = field(default=10.0, metadata={"env": "AI4E_EVICT_PERIOD_S"})
+    # finished tasks (and their results) kept per endpoint and state regardless of age
+    max_finished_tasks: int = field(default=4_000_000, metadata={"env": "AI4E_MAX_FINISHED_TASKS"})
     # request bodies up to this size are journaled as the task's _ORIG body (replayed after a restart)
     journal_payload_max_bytes: int = field(default=1 << 20, metadata={"env": "AI4E_JOURNAL_PAYLOAD_MAX_BYTES"})
     # --- metrics timers (TaskQueueLogger.cs:20 / TaskProcessLogger.cs:22) ---

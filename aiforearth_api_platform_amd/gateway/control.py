@@ -196,7 +196,7 @@ class ControlPlane:
                 self.log_queue_lengths(s)
 
         def evict():  # bounded store: finished tasks older than the TTL (and their results) are dropped
-            n = self.store.evict_finished(self.cfg.finished_task_ttl_s)
+            n = self.store.evict_finished(self.cfg.finished_task_ttl_s, self.cfg.max_finished_tasks)
             if n:
                 REGISTRY.counter("tasks_evicted_total").inc(n)
 

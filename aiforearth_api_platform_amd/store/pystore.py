@@ -317,10 +317,16 @@ class TaskStore:
         with self._mu:
             return dict(sorted(self._counters.items()))
 
-    def evict_finished(self, max_age_s: float) -> int:
+    def evict_finished(self, max_age_s: float, max_finished: Optional[int] = None) -> int:
         with self._mu:
             cutoff = time.monotonic() - max_age_s
             dead = [tid for tid, r in self._records.items() if 0 < r.t_finished <= cutoff]
+            if max_finished is not None:
+                dset = set(dead)
+                for key, idx in self._index.items():
+                    if key.endswith(("_completed", "_failed")):
+                        live = [t for t in idx.score if t not in dset]  # insertion (= finish) order
+                        dead += live[: max(0, len(live) - max_finished)]
             for tid in dead:
                 r = self._records.pop(tid)
                 self._idx(f"{r.endpoint_path}_{r.backend_status}").rem(tid)

@@ -151,7 +151,8 @@ PYBIND11_MODULE(_ai4e_core, m) {
       .def("incrby", &TaskStore::incrby)
       .def("get_counter", &TaskStore::get_counter)
       .def("counters", &TaskStore::counters)
-      .def("evict_finished", &TaskStore::evict_finished, py::call_guard<py::gil_scoped_release>())
+      .def("evict_finished", &TaskStore::evict_finished, py::arg("max_age_s"),
+           py::arg("max_finished") = static_cast<size_t>(SIZE_MAX), py::call_guard<py::gil_scoped_release>())
       .def("size", &TaskStore::size)
       .def("flush", &TaskStore::flush)
       .def("replay", [](TaskStore& s, const std::string& path) {

@@ -60,8 +60,9 @@ struct ResultBatch {
 };
 
 struct TaskRec {
-  std::string id;
-  std::string endpoint;
+  const std::string* idp = nullptr;               // the record's key in the map (node-stable)
+  std::shared_ptr<const std::string> endpoint;    // shared by every task of a batch
+  const std::string& id() const { return *idp; }
   PathIndex* pidx = nullptr;
   IndexList* list = nullptr;
   TaskRec* prev = nullptr;
@@ -81,6 +82,7 @@ class TaskStore {
  public:
   explicit TaskStore(std::string journal_path = "") : journal_path_(std::move(journal_path)) {
     for (const char* s : {"created", "running", "completed", "failed"}) state_id(s);
+    recs_.reserve(1 << 20);  // a node's worth of in-flight + TTL-retained tasks without rehash stalls
     if (!journal_path_.empty()) {
       journal_ = std::fopen(journal_path_.c_str(), "a");
       if (!journal_) throw std::runtime_error("cannot open journal " + journal_path_);
@@ -105,11 +107,11 @@ class TaskStore {
     auto ins = recs_.try_emplace(task_id);
     TaskRec& r = ins.first->second;
     if (ins.second) {
-      r.id = task_id;
+      r.idp = &ins.first->first;
       r.t_created = mnow;
     }
     PathIndex* p = path_index(absolute_path(endpoint));
-    r.endpoint = endpoint;
+    r.endpoint = shared_endpoint(endpoint);
     r.status = std::make_shared<const std::string>(status);
     r.pub = publish_to_grid;
     r.wall = wnow;
@@ -137,6 +139,7 @@ class TaskStore {
     const double wnow = wall_now(), mnow = mono_now();
     PathIndex* p = path_index(absolute_path(endpoint));
     auto st = std::make_shared<const std::string>(status);
+    auto ep = shared_endpoint(endpoint);
     for (size_t i = 0; i < n; ++i) {
       std::string id = uuid_.next();
       auto ins = recs_.try_emplace(id);
@@ -145,8 +148,8 @@ class TaskStore {
         continue;
       }
       TaskRec& r = ins.first->second;
-      r.id = id;
-      r.endpoint = endpoint;
+      r.idp = &ins.first->first;
+      r.endpoint = ep;
       r.status = st;
       r.pub = true;
       r.wall = wnow;
@@ -187,12 +190,13 @@ class TaskStore {
     const double wnow = wall_now(), mnow = mono_now();
     PathIndex* p = path_index(absolute_path(endpoint));
     auto st = std::make_shared<const std::string>(status);
+    auto ep = shared_endpoint(endpoint);
     size_t n = 0;
     for (const auto& id : ids) {
       auto it = recs_.find(id);
       if (it == recs_.end()) continue;
       TaskRec& r = it->second;
-      r.endpoint = endpoint;
+      r.endpoint = ep;
       r.status = st;
       r.wall = wnow;
       move_to(r, p, ST_CREATED, wnow, mnow);
@@ -268,11 +272,11 @@ class TaskStore {
     if (it == recs_.end()) return std::nullopt;
     const TaskRec& r = it->second;
     View v;
-    v.id = r.id;
+    v.id = r.id();
     v.timestamp = dotnet_timestamp(r.wall);
     v.status = r.status ? *r.status : std::string();
     v.backend_status = state_names_[r.state];
-    v.endpoint = r.endpoint;
+    v.endpoint = *r.endpoint;
     v.path = r.pidx->path;
     v.trace = r.trace;
     v.pub = r.pub;
@@ -331,7 +335,7 @@ class TaskStore {
     std::vector<std::string> out;
     const IndexList* l = find_list(key);
     if (!l) return out;
-    for (TaskRec* r = l->head; r && out.size() < limit; r = r->next) out.push_back(r->id);
+    for (TaskRec* r = l->head; r && out.size() < limit; r = r->next) out.push_back(r->id());
     return out;
   }
 
@@ -369,19 +373,20 @@ class TaskStore {
 
   // Drop completed/failed records finished more than max_age_s ago, oldest first: the finished
   // lists are in finish order, so this costs O(evicted), not O(store).
-  size_t evict_finished(double max_age_s) {
+  // `max_finished` caps the finished records kept per (path, state) regardless of age (a node at
+  // ~550k tasks/s cannot keep an hour of results): the oldest beyond the cap go first.
+  size_t evict_finished(double max_age_s, size_t max_finished = SIZE_MAX) {
     std::lock_guard<std::mutex> g(mu_);
     const double cutoff = mono_now() - max_age_s;
     size_t n = 0;
     for (auto& kv : paths_) {
       for (int s : {ST_COMPLETED, ST_FAILED}) {
         IndexList& l = kv.second->lists[s];
-        while (l.head && l.head->t_finished > 0 && l.head->t_finished <= cutoff) {
+        while (l.head && l.head->t_finished > 0 && (l.head->t_finished <= cutoff || l.n > max_finished)) {
           TaskRec* r = l.head;
           unlink(*r);
-          orig_.erase(r->id);
-          std::string id = r->id;  // r dies with the erase
-          recs_.erase(id);
+          orig_.erase(r->id());
+          recs_.erase(recs_.find(r->id()));  // by iterator: the key lives in the node being erased
           ++n;
         }
       }
@@ -424,10 +429,10 @@ class TaskStore {
       auto ins = recs_.try_emplace(jl.id);
       TaskRec& r = ins.first->second;
       if (ins.second) {
-        r.id = jl.id;
+        r.idp = &ins.first->first;
         r.t_created = mnow;
       }
-      r.endpoint = jl.endpoint;
+      r.endpoint = shared_endpoint(jl.endpoint);
       r.status = std::make_shared<const std::string>(jl.status);
       r.pub = jl.pub;
       r.wall = jl.score;
@@ -440,7 +445,7 @@ class TaskStore {
       link_tail(r, &p->lists[sid]);
       // finished records get a finish time, so TTL eviction applies to them too
       r.t_finished = (sid == ST_COMPLETED || sid == ST_FAILED) ? mnow : 0;
-      if (jl.orig) orig_[r.id] = *jl.orig;
+      if (jl.orig) orig_[r.id()] = *jl.orig;
       ++n;
     }
     journal_ = saved;
@@ -450,6 +455,15 @@ class TaskStore {
   const std::string& state_name(int s) const { return state_names_[s]; }
 
  private:
+  // Endpoint strings are interned: a batch of tasks shares one allocation.
+  std::shared_ptr<const std::string> shared_endpoint(const std::string& e) {
+    auto it = endpoints_.find(e);
+    if (it != endpoints_.end()) return it->second;
+    auto p = std::make_shared<const std::string>(e);
+    if (endpoints_.size() < 65536) endpoints_.emplace(e, p);
+    return p;
+  }
+
   int state_id(const std::string& s) {
     auto it = state_ids_.find(s);
     if (it != state_ids_.end()) return it->second;
@@ -523,7 +537,7 @@ class TaskStore {
     std::string out;
     out.reserve(256);
     out += "{\"TaskId\":";
-    json_escape_into(out, r.id);
+    json_escape_into(out, r.id());
     out += ",\"Timestamp\":";
     json_escape_into(out, dotnet_timestamp(r.wall));
     out += ",\"Status\":";
@@ -531,7 +545,7 @@ class TaskStore {
     out += ",\"BackendStatus\":";
     json_escape_into(out, state_names_[r.state]);
     out += ",\"Endpoint\":";
-    json_escape_into(out, r.endpoint);
+    json_escape_into(out, *r.endpoint);
     out += ",\"Body\":null,\"PublishToGrid\":";
     out += r.pub ? "true" : "false";
     out += ",\"EndpointPath\":";
@@ -556,6 +570,7 @@ class TaskStore {
   std::mutex mu_;
   Uuid4 uuid_;
   std::unordered_map<std::string, TaskRec> recs_;  // node-based: record addresses are stable
+  std::unordered_map<std::string, std::shared_ptr<const std::string>> endpoints_;
   std::unordered_map<std::string, std::unique_ptr<PathIndex>> paths_;
   std::unordered_map<std::string, int> state_ids_;
   std::vector<std::string> state_names_;

@@ -154,3 +154,11 @@ def test_native_threaded_throughput():
         seen += [m.task_id for m in ms]
     [t.join() for t in ts]
     assert len(set(seen)) == N and s.zcard("/v1/x_completed") == N
+
+
+def test_evict_caps_finished_records(backend):
+    s = make_store(backend=backend)
+    ids = s.create_many("/v1/cap", 10)
+    s.transition_many(ids, "completed", "done")
+    assert s.evict_finished(3600.0, 4) == 6 and s.zcard("/v1/cap_completed") == 4
+    assert s.get(ids[-1]) is not None and s.get(ids[0]) is None  # oldest go first

@@ -1,0 +1,132 @@
+"""Node-scale load test of the control plane, CPU only (no model): how many tasks/s can ONE node
+scheduler create, dispatch, complete and attach results for, with N worker processes?
+
+Each fake worker speaks the real wire protocol (runtime/protocol.py) and answers every BATCH with a
+DONE of top-5 rows immediately, so the measured ceiling is the host path the 8-GPU bench exercises:
+native create + enqueue (ingest), dispatcher receive + running transition + BATCH frame, reader
+DONE parse + result attach + completed transition + queue complete + slot release. Target: 8 GPUs x
+~70k images/s = 560k tasks/s.
+
+    python tools/cp_loadtest.py [--workers 8 --batch 250 --seconds 5 --ingest-threads 4]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import multiprocessing as mp
+import os
+import sys
+import threading
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def fake_worker(conn, rank: int, row_bytes: int):
+    import numpy as np
+
+    from aiforearth_api_platform_amd.runtime import protocol as P
+
+    fc = P.FrameConn(conn)
+    fc.ready(rank, False, {"kind": "classifier", "outputs": [["classes", "int32", [5]], ["probabilities", "float32",
+                                                                                         [5]]]})
+    zeros = bytes(row_bytes * 1024)
+    while True:
+        try:
+            buf = fc.recv()
+        except (EOFError, OSError):
+            return
+        t = P.frame_type(buf)
+        if t == P.F_BATCH:
+            bid, slots = P.parse_batch(buf)
+            n = slots.shape[0]
+            now = time.monotonic()
+            fc.done(bid, np.zeros(n, np.uint8), zeros[: n * row_bytes], row_bytes, (now, now, now, 0.0, 0.0))
+        elif t == P.F_STOP:
+            return
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workers", type=int, default=8)
+    ap.add_argument("--batch", type=int, default=250)
+    ap.add_argument("--seconds", type=float, default=5.0)
+    ap.add_argument("--ingest-threads", type=int, default=4)
+    ap.add_argument("--json-out", default="")
+    a = ap.parse_args()
+    from aiforearth_api_platform_amd.config import Config
+    from aiforearth_api_platform_amd.gateway.control import ControlPlane
+    from aiforearth_api_platform_amd.store import native
+    from aiforearth_api_platform_amd.utils.metrics import percentile
+
+    cp = ControlPlane(Config.load(env={}))
+    path = "/v1/ai4e/resnet50/classify"
+    q = cp.queue_for("http://127.0.0.1" + path)
+    B = a.batch
+    per_thread = B * 4
+    nslots = per_thread * a.ingest_threads
+    sched = native.NodeScheduler(cp.store, q, "http://127.0.0.1" + path, nslots, max_batch=B, linger_s=0.0005,
+                                 depth=2, hb_timeout_s=60.0, poll_s=0.005)
+    rings = [native.SlotRing(per_thread, i * per_thread) for i in range(a.ingest_threads)]
+    for r in rings:
+        sched.add_local_ring(r)
+    ctx = mp.get_context("spawn")
+    procs = []
+    for r in range(a.workers):
+        parent, child = ctx.Pipe()
+        p = ctx.Process(target=fake_worker, args=(child, r, 40), daemon=True)
+        p.start()
+        child.close()
+        sched.attach(r, os.dup(parent.fileno()), True)
+        parent.close()
+        procs.append(p)
+    while sum(1 for w in sched.worker_stats() if w["ready"]) < a.workers:
+        time.sleep(0.01)
+    stop = threading.Event()
+
+    def ingest(ring):
+        while not stop.is_set():
+            s = ring.alloc(B, 1.0)
+            if s:
+                sched.submit(s, "")
+
+    evict_stop = threading.Event()
+
+    def evictor():  # the serving process's TTL timer, at a short TTL so the store stays bounded
+        while not evict_stop.wait(0.5):
+            cp.store.evict_finished(2.0)
+
+    ths = [threading.Thread(target=ingest, args=(r,), daemon=True) for r in rings]
+    ev = threading.Thread(target=evictor, daemon=True)
+    ev.start()
+    for t in ths:
+        t.start()
+    time.sleep(1.0)  # warm
+    n0, t0, m0 = sched.images_done(), time.perf_counter(), time.monotonic()
+    time.sleep(a.seconds)
+    n1, t1, m1 = sched.images_done(), time.perf_counter(), time.monotonic()
+    stop.set()
+    for t in ths:
+        t.join(5)
+    lat = sorted(cp.store.latencies_window(path, m0, m1))
+    evict_stop.set()
+    rate = (n1 - n0) / (t1 - t0)
+    out = {"metric": "control-plane tasks/s (create + dispatch + complete + result attach), no model",
+           "value": round(rate), "unit": "tasks/s", "workers": a.workers, "batch": B, "ingest_threads": a.ingest_threads,
+           "seconds": a.seconds, "p50_task_latency_ms": round(percentile(lat, 50) * 1e3, 3) if lat else None,
+           "store_size_end": cp.store.size(), "cpu_count": os.cpu_count(),
+           "batch_histogram": sched.batch_histogram()}
+    sched.stop()
+    for p in procs:
+        p.join(5)
+    cp.close()
+    line = json.dumps(out)
+    print(line)
+    if a.json_out:
+        with open(a.json_out, "w") as f:
+            f.write(line + "\n")
+
+
+if __name__ == "__main__":
+    main()
