@@ -31,14 +31,8 @@ Data is synthetic (random uint8 images), weights are random-init (no checkpoints
 from __future__ import annotations
 
 import argparse
-import json
 import os
 import sys
-import threading
-import time
-
-import numpy as np
-import torch
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
@@ -69,293 +63,23 @@ def parse():
     return p.parse_args()
 
 
-class Client:
-    """Synthetic clients of one ingest shard: per submission, write --batch images into this shard's
-    ring partition (one copy per contiguous slot run) and enqueue them."""
-
-    def __init__(self, ring_buf: torch.Tensor, alloc, submit, batch: int, seed: int):
-        self.buf, self.alloc, self.submit, self.batch = ring_buf, alloc, submit, batch
-        g = torch.Generator().manual_seed(1234 + seed)
-        self.src = torch.randint(0, 256, (2 * batch, *ring_buf.shape[1:]), dtype=torch.uint8, generator=g)
-        self.k = 0
-
-    def step(self) -> None:
-        slots = self.alloc(self.batch)
-        src = self.src[(self.k % 2) * self.batch:(self.k % 2 + 1) * self.batch]
-        self.k += 1
-        i, n = 0, len(slots)
-        while i < n:
-            j = i + 1
-            while j < n and slots[j] == slots[j - 1] + 1:
-                j += 1
-            self.buf[slots[i]:slots[i] + (j - i)].copy_(src[i:j])
-            i = j
-        self.submit(slots)
-
-    def run(self, steps: int) -> None:
-        for _ in range(steps):
-            self.step()
-
-
-def http_phase(cp, pool, seconds: float, batch: int, image_size: int) -> dict:
-    """REST ingest on this node: aiohttp gateway + binary batch route, then single-image requests."""
-    import asyncio
-
-    import aiohttp
-    from aiohttp import web
-
-    from aiforearth_api_platform_amd.gateway.server import BATCH_CONTENT_TYPE, Gateway, Route, RouteTable
-    from aiforearth_api_platform_amd.runtime.model_endpoint import ModelEndpoint
-    from aiforearth_api_platform_amd.utils.metrics import percentile
-
-    ep = ModelEndpoint(cp, PATH, worker=pool)
-    table = RouteTable()
-    table.add(Route("/v1/camera-trap/classify-async", "async", ep))
-    gw = Gateway(cp, table)
-    ready = threading.Event()
-    box = {}
-
-    def serve():
-        loop = asyncio.new_event_loop()
-        asyncio.set_event_loop(loop)
-        runner = web.AppRunner(gw.app, access_log=None)
-        loop.run_until_complete(runner.setup())
-        site = web.TCPSite(runner, "127.0.0.1", 0)
-        loop.run_until_complete(site.start())
-        box["port"] = site._server.sockets[0].getsockname()[1]
-        box["loop"], box["runner"] = loop, runner
-        ready.set()
-        loop.run_forever()
-        loop.run_until_complete(runner.cleanup())
-
-    th = threading.Thread(target=serve, daemon=True)
-    th.start()
-    ready.wait(30)
-    url = f"http://127.0.0.1:{box['port']}/v1/camera-trap/classify-async"
-    rng = np.random.default_rng(7)
-    img = rng.integers(0, 256, (image_size, image_size, 3), dtype=np.uint8)
-    batch_body = np.broadcast_to(img, (batch, *img.shape)).tobytes()
-
-    async def batches(conc: int):
-        ids, n = [], 0
-        t_end = time.perf_counter() + seconds / 2
-
-        async def one(s):
-            nonlocal n
-            while time.perf_counter() < t_end:
-                async with s.post(url, data=batch_body, headers={"Content-Type": BATCH_CONTENT_TYPE}) as r:
-                    ids.extend((await r.json())["TaskIds"])
-                    n += batch
-
-        async with aiohttp.ClientSession() as s:
-            t0 = time.perf_counter()
-            await asyncio.gather(*(one(s) for _ in range(conc)))
-        return ids, n, t0
-
-    async def singles(conc: int):
-        ids = []
-        t_end = time.perf_counter() + seconds / 2
-        body = img.tobytes()
-
-        async def one(s):
-            while time.perf_counter() < t_end:
-                async with s.post(url, data=body, headers={"Content-Type": "application/octet-stream"}) as r:
-                    ids.append((await r.json())["TaskId"])
-
-        async with aiohttp.ClientSession() as s:
-            t0 = time.perf_counter()
-            await asyncio.gather(*(one(s) for _ in range(conc)))
-        return ids, t0
-
-    def wait_done(ids, timeout=60):
-        deadline = time.time() + timeout
-        while time.time() < deadline:
-            lat = cp.store.latencies(ids)
-            if len(lat) >= len(ids):
-                return sorted(lat)
-            time.sleep(0.01)
-        return sorted(cp.store.latencies(ids))
-
-    out = {}
-    ids, n, t0 = asyncio.run(batches(4))
-    lat = wait_done(ids)
-    dt = time.perf_counter() - t0
-    out["batch_route"] = {"images": n, "images_per_s": round(n / dt, 1), "request_images": batch, "connections": 4,
-                          "p50_task_latency_ms": round(percentile(lat, 50) * 1e3, 3),
-                          "p99_task_latency_ms": round(percentile(lat, 99) * 1e3, 3)}
-    ids, t0 = asyncio.run(singles(64))
-    lat = wait_done(ids)
-    dt = time.perf_counter() - t0
-    out["single_image_route"] = {"requests": len(ids), "images_per_s": round(len(ids) / dt, 1), "connections": 64,
-                                 "p50_task_latency_ms": round(percentile(lat, 50) * 1e3, 3),
-                                 "p99_task_latency_ms": round(percentile(lat, 99) * 1e3, 3)}
-    box["loop"].call_soon_threadsafe(box["loop"].stop)
-    th.join(10)
-    return out
-
-
 def main():
     args = parse()
     os.environ["AI4E_KERNEL_BACKEND"] = args.backend
-    from aiforearth_api_platform_amd import _build
-    from aiforearth_api_platform_amd.config import Config
-    from aiforearth_api_platform_amd.gateway.control import ControlPlane
     from aiforearth_api_platform_amd.models.resnet import FusedResNet, resnet50
-    from aiforearth_api_platform_amd.parallel.dist import all_reduce_max, destroy, env_ranks, init_from_env, sync
-    from aiforearth_api_platform_amd.runtime import protocol as P
-    from aiforearth_api_platform_amd.runtime.hostperf import tune_gc
-    from aiforearth_api_platform_amd.runtime.worker_pool import ModelSpec, WorkerPool
-    from aiforearth_api_platform_amd.utils.metrics import percentile
+    from aiforearth_api_platform_amd.runtime.node_bench import run_node_bench
+    from aiforearth_api_platform_amd.runtime.worker_pool import ModelSpec
 
-    _, world, _ = env_ranks()
-    if world > 1 and args.gpus != world:
-        raise SystemExit(f"--gpus {args.gpus} != WORLD_SIZE {world}")
-    # rank 0 builds the in-tree HIP/C++ libraries, then everyone joins (RCCL on GPU, gloo on CPU)
-    denv = init_from_env(args.device, build=_build.build_all)
-    rank, device = denv.rank, denv.device
     B, S = args.batch, args.image_size
     # small captured buckets = the low-load fast path of the REST phase (a batch of n runs the smallest graph >= n)
     buckets = tuple(b for b in (8, 32, 128) if b < B)
-    spec = ModelSpec("aiforearth_api_platform_amd.models.toy:resnet50_fused", (S, S, 3), B, 5, {},
+    spec = ModelSpec("aiforearth_api_platform_amd.models.zoo:resnet50_classifier", (S, S, 3), B, 5, {},
                      not args.no_graphs, buckets)
-    part = B * (args.inflight + 1)  # ring slots per ingest shard
-    hb = 0.5
-    total_images = (args.warmup + args.steps) * B * world
-
-    if rank == 0:
-        cfg = Config.load(env={}, max_batch=B, max_batch_delay_ms=0.0)
-        cp = ControlPlane(cfg)
-        remote = [(part * r, part, r) for r in range(1, world)]
-        pool = WorkerPool(cp, ENDPOINT, spec, [f"{args.device}:{denv.local_rank}" if args.device == "cuda" else "cpu"],
-                          ring_slots=part, max_delay_s=0.0005, heartbeat_interval_s=hb, heartbeat_timeout_s=120.0,
-                          remote_partitions=remote, pipeline_depth=2, poll_s=0.005)
-        info = None
-        listener = None
-        if world > 1:
-            import secrets
-            from multiprocessing.connection import Listener
-
-            key = secrets.token_bytes(16)
-            listener = Listener(("127.0.0.1", 0), authkey=key)
-            info = {"shm": pool.ring.name, "nslots": pool.ring.nslots, "addr": listener.address, "key": key.hex()}
-        objs = [info]
-        if world > 1:
-            import torch.distributed as dist
-
-            dist.broadcast_object_list(objs, src=0)
-
-            def accept():
-                for _ in range(world - 1):
-                    c = listener.accept()
-                    r = int(c.recv_bytes().decode())
-                    pool.attach_remote(r, c, device=f"cuda:{r}")
-
-            acc = threading.Thread(target=accept, daemon=True)
-            acc.start()
-        pool.start(wait_ready_s=900)
-        if world > 1:
-            acc.join(900)
-            pool.wait_ready(900)
-        client = Client(pool.ring.buf, lambda n: pool.ring.alloc(n, timeout=600), pool.submit_slots, B, rank)
-    else:
-        import torch.distributed as dist
-        from multiprocessing.connection import Client as MPClient
-
-        from aiforearth_api_platform_amd.runtime.gpu_worker import attach_ring, worker_main
-        from aiforearth_api_platform_amd.store import native
-
-        objs = [None]
-        dist.broadcast_object_list(objs, src=0)
-        info = objs[0]
-        conn = MPClient(tuple(info["addr"]), authkey=bytes.fromhex(info["key"]))
-        conn.send_bytes(str(rank).encode())
-        fc = P.FrameConn(conn)
-        local_ring = native.SlotRing(part, part * rank)
-        shm, ring_buf = attach_ring(info["shm"], info["nslots"], spec.item_shape, untrack=True)
-
-        def alloc(n):
-            s = local_ring.alloc(n, 600.0)
-            if not s:
-                raise TimeoutError("ingest partition full")
-            return s
-
-        client = Client(ring_buf, alloc, fc.submit, B, rank)
-        wth = threading.Thread(target=worker_main, args=(fc, rank, str(device), spec, info["shm"], info["nslots"], hb),
-                               kwargs={"untrack": True, "local_ring": local_ring}, daemon=True)
-        wth.start()
-
-    def wait_images(target: int) -> None:
-        while pool.images < target:
-            time.sleep(0.0002)
-
-    # ---------------------------------------------------------------- warmup (untimed)
-    sync(denv)
-    wth_c = threading.Thread(target=client.run, args=(args.warmup,), daemon=True)
-    wth_c.start()
-    wth_c.join()
-    if rank == 0:
-        wait_images(args.warmup * B * world)
-    tune_gc()
-    sync(denv)
-    # ---------------------------------------------------------------- timed region
-    t0 = time.perf_counter()
-    tm0 = time.monotonic()
-    cth = threading.Thread(target=client.run, args=(args.steps,), daemon=True)
-    cth.start()
-    if rank == 0:
-        wait_images(total_images)
-    cth.join()
-    sync(denv)
-    dt = time.perf_counter() - t0
-    tm1 = time.monotonic()
-    p50 = p99 = 0.0
-    stats = {}
-    if rank == 0:
-        lat = sorted(cp.store.latencies_window(PATH, tm0, tm1))
-        p50, p99 = percentile(lat, 50) * 1e3, percentile(lat, 99) * 1e3
-        stats = pool.stats()
-    dt, p50, p99 = all_reduce_max([dt, p50, p99], denv)  # slowest rank defines the step time
-    images = args.steps * B * world
-    value = images / dt
-    if rank == 0:
-        http = None
-        if args.http and args.device == "cuda":
-            try:
-                http = http_phase(cp, pool, args.http_seconds, B, S)
-            except Exception as e:  # the headline number stands on its own
-                http = {"error": repr(e)}
-        gflop_img = FusedResNet(resnet50(seed=0), device="cpu").flops(1, S, S) / 1e9
-        workers = [{k: w.get(k) for k in ("rank", "images", "batches", "pinned", "hbm_used", "gpu_busy_ms")}
-                   for w in stats.get("workers", [])]
-        out = {
-            "metric": METRIC, "value": round(value, 2), "unit": "images/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None if BASELINE_VALUE is None else round(value / BASELINE_VALUE, 4),
-            "dtype": "bf16", "data": "synthetic uint8 images (written into the payload ring per submission), "
-                                     "random-init weights",
-            "p50_task_latency_ms": round(p50, 3), "p99_task_latency_ms": round(p99, 3),
-            "tflops_effective": round(value * gflop_img / 1e3, 2),
-            "config": {"model": "resnet50", "global_batch": B * world, "per_gpu_batch": B, "image_size": S,
-                       "seq_len": None, "parallelism": f"dp{world}", "api": "async",
-                       "serving_path": "node scheduler (native) + 1 GPU worker process per GPU",
-                       "ingest_shards": world, "ring_slots_per_shard": part, "hip_graphs": not args.no_graphs,
-                       "kernel_backend": args.backend},
-            "workers": workers, "batch_histogram": stats.get("batch_histogram"), "http": http,
-        }
-        line = json.dumps(out)
-        print(line, flush=True)
-        if args.json_out:
-            with open(args.json_out, "w") as f:
-                f.write(line + "\n")
-    sync(denv)
-    if rank == 0:
-        pool.stop()
-        cp.close()
-    else:
-        wth.join(60)
-        del ring_buf
-        shm.close()
-    destroy(denv)
+    flops = FusedResNet(resnet50(seed=0), device="cpu").flops(1, S, S)
+    run_node_bench(args, spec, PATH, METRIC, "images/s",
+                   config={"model": "resnet50", "image_size": S, "seq_len": None, "api": "async",
+                           "kernel_backend": args.backend},
+                   flops_per_item=flops, baseline=BASELINE_VALUE)
 
 
 if __name__ == "__main__":
