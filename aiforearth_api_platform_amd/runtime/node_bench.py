@@ -259,7 +259,10 @@ def run_node_bench(args, spec, path: str, metric: str, unit: str = "images/s", c
     p50 = p99 = 0.0
     stats = {}
     if rank == 0:
-        lat = sorted(cp.store.latencies_window(path, tm0, tm1))
+        from ..store.pystore import absolute_path
+
+        lat = sorted(x for pth in [path] + [absolute_path(e) for e in spec.stage_endpoints]
+                     for x in cp.store.latencies_window(pth, tm0, tm1))  # ensembles finish at the last stage
         p50, p99 = percentile(lat, 50) * 1e3, percentile(lat, 99) * 1e3
         stats = pool.stats()
     dt, p50, p99 = all_reduce_max([dt, p50, p99], denv)  # slowest rank defines the step time
