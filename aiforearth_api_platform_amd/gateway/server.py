@@ -156,7 +156,7 @@ class Gateway:
             for w in st.get("workers", []):
                 tag = f"{path}/gpu{w.get('rank')}"
                 for k in ("hbm_used", "hbm_total", "gpu_busy_ms", "images", "batches", "outstanding",
-                          "failed_items", "retried_items"):
+                          "failed_items", "retried_items", "xgmi_tx_bytes", "xgmi_rx_bytes"):
                     if k in w:
                         REGISTRY.gauge(f"{k}{tag}").set(float(w[k]))
             for i, c in enumerate(st.get("batch_histogram", [])):

@@ -44,6 +44,10 @@ class ModelSpec:
     buckets: Tuple[int, ...] = ()      # captured batch sizes (config.bucket_list); () = max_batch only
     # ensemble stages: endpoint of each later stage (the scheduler re-targets the batch's tasks there)
     stage_endpoints: Tuple[str, ...] = ()
+    # worker group: each pool worker is `group_size` processes on consecutive devices joined in one
+    # process group (RCCL on GPUs, gloo on CPU) — the leader talks to the scheduler, the followers serve
+    # it (detector -> classifier pair over xGMI, spatial-parallel mosaic segmentation)
+    group_size: int = 1
 
 
 def load_factory(path: str):
@@ -100,7 +104,7 @@ class GpuWorker:
     """The loop of one worker process (also usable in a thread for tests)."""
 
     def __init__(self, conn: P.FrameConn, rank: int, device: str, spec: ModelSpec, ring_buf: torch.Tensor,
-                 local_ring=None, hb_interval: float = 0.5, depth: int = 2):
+                 local_ring=None, hb_interval: float = 0.5, depth: int = 2, group_kwargs: Optional[dict] = None):
         self.conn = conn
         self.rank = rank
         self.device = torch.device(device)
@@ -111,7 +115,8 @@ class GpuWorker:
         self.hb_interval = hb_interval
         self.depth = depth
         self.fault = parse_fault(rank)
-        self.servable = as_servable(load_factory(spec.factory)(device=device, **spec.kwargs), spec.topk)
+        self.servable = as_servable(load_factory(spec.factory)(device=device, **spec.kwargs, **(group_kwargs or {})),
+                                    spec.topk)
         from .engine import InferenceEngine
 
         self.engine = InferenceEngine(None, spec.item_shape, spec.max_batch, device=self.device,
@@ -142,8 +147,13 @@ class GpuWorker:
                     used = total - free
                 except Exception:
                     pass
+            xg = getattr(self.servable, "xgmi_bytes", None)
+            tx = rx = 0
+            if callable(xg):
+                b = xg()
+                tx, rx = int(b.get("sent", 0)), int(b.get("received", 0))
             try:
-                self.conn.heartbeat(time.monotonic(), used, total, self.busy_ms, self.batches)
+                self.conn.heartbeat(time.monotonic(), used, total, self.busy_ms, self.batches, tx, rx)
             except (BrokenPipeError, EOFError, OSError):
                 return
             time.sleep(self.hb_interval)
@@ -176,6 +186,9 @@ class GpuWorker:
             self._done_q.put(None)
             fin.join(60)
             self.alive.clear()
+            close = getattr(self.servable, "close", None)  # e.g. release the group's followers
+            if callable(close):
+                close()
 
     def _completion_loop(self) -> None:
         while True:
@@ -270,13 +283,47 @@ class GpuWorker:
         self.conn.done(bid, status, rows.tobytes(), self.row_bytes, (t_recv, t_launch, time.monotonic(), 0, 0))
 
 
-def worker_main(conn, rank: int, device: str, spec: ModelSpec, shm_name: str, nslots: int, hb_interval: float,
-                partition: Optional[Tuple[int, int]] = None, untrack: bool = False, local_ring=None) -> None:
-    """Entry point of a spawned worker process (and of ``torchrun`` worker ranks, which pass their
-    ingest partition's ``local_ring`` and ``untrack=True``)."""
+def join_group(device: str, group_rank: int, group_size: int, port: int):
+    """Process group of one worker group (RCCL over xGMI between its GPUs; gloo on CPU)."""
+    import datetime
+
+    import torch.distributed as dist
+
+    dev = torch.device(device)
+    backend = "nccl" if dev.type == "cuda" else "gloo"
+    kw = {"device_id": dev} if backend == "nccl" else {}
+    dist.init_process_group(backend, init_method=f"tcp://127.0.0.1:{port}", rank=group_rank, world_size=group_size,
+                            timeout=datetime.timedelta(seconds=600), **kw)
+    return {"group": dist.group.WORLD, "role": "leader" if group_rank == 0 else "follower"}
+
+
+def follower_main(device: str, spec: ModelSpec, group_rank: int, group_size: int, port: int) -> None:
+    """A non-leader process of a worker group: builds its part of the model and serves the leader
+    (``servable.serve_follower()`` returns when the leader releases the group)."""
     dev = torch.device(device)
     if dev.type == "cuda":
         torch.cuda.set_device(dev)
+    gk = join_group(device, group_rank, group_size, port)
+    part = load_factory(spec.factory)(device=device, **spec.kwargs, **gk)
+    try:
+        part.serve_follower()
+    finally:
+        import torch.distributed as dist
+
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def worker_main(conn, rank: int, device: str, spec: ModelSpec, shm_name: str, nslots: int, hb_interval: float,
+                partition: Optional[Tuple[int, int]] = None, untrack: bool = False, local_ring=None,
+                group_port: int = 0) -> None:
+    """Entry point of a spawned worker process (and of ``torchrun`` worker ranks, which pass their
+    ingest partition's ``local_ring`` and ``untrack=True``). With ``spec.group_size > 1`` this is the
+    leader of a worker group (rendezvous on ``group_port``)."""
+    dev = torch.device(device)
+    if dev.type == "cuda":
+        torch.cuda.set_device(dev)
+    group_kwargs = join_group(device, 0, spec.group_size, group_port) if spec.group_size > 1 else None
     shm, buf = attach_ring(shm_name, nslots, spec.item_shape, untrack=untrack)
     pinned = pin_host(buf) if dev.type == "cuda" else False
     if local_ring is None and partition is not None:
@@ -284,7 +331,7 @@ def worker_main(conn, rank: int, device: str, spec: ModelSpec, shm_name: str, ns
 
         local_ring = native.SlotRing(partition[1], partition[0])
     fc = conn if isinstance(conn, P.FrameConn) else P.FrameConn(conn)
-    w = GpuWorker(fc, rank, device, spec, buf, local_ring=local_ring, hb_interval=hb_interval)
+    w = GpuWorker(fc, rank, device, spec, buf, local_ring=local_ring, hb_interval=hb_interval, group_kwargs=group_kwargs)
     try:
         w.serve(pinned)
     finally:
@@ -295,3 +342,8 @@ def worker_main(conn, rank: int, device: str, spec: ModelSpec, shm_name: str, ns
                 pass
         del buf
         shm.close()
+        if group_kwargs is not None:
+            import torch.distributed as dist
+
+            if dist.is_initialized():
+                dist.destroy_process_group()

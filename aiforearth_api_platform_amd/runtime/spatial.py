@@ -62,6 +62,8 @@ class SpatialSegmenter:
         dist_on = dist.is_initialized() and not local
         self.rank = dist.get_rank(group) if dist_on else 0
         self.world = dist.get_world_size(group) if dist_on else 1
+        self.bytes_sent = 0      # P2P / broadcast payload bytes over the group (xGMI on the GPU node)
+        self.bytes_received = 0
         if grid.ts >= 2 * grid.stride:
             raise ValueError("tile overlap must be < 50% (a halo of one tile row per boundary)")
         if grid.nty < self.world:
@@ -97,6 +99,8 @@ class SpatialSegmenter:
         if world > 1:
             shape = torch.tensor(list(mosaic.shape) if r == 0 else [0, 0, 0], dtype=torch.int64, device=self.device)
             dist.broadcast(shape, 0, group=self.group)
+            if int(shape[0]) < 0:  # the leader released the group (stop())
+                return None
             if r != 0:
                 mosaic = torch.empty(*shape.tolist(), dtype=torch.uint8, device=self.device)
             else:
@@ -104,6 +108,11 @@ class SpatialSegmenter:
             dist.broadcast(mosaic, 0, group=self.group)
         else:
             mosaic = mosaic.to(self.device)
+        return self._segment(mosaic)
+
+    def _segment(self, mosaic: torch.Tensor) -> Optional[torch.Tensor]:
+        g = self.grid
+        r, world = self.rank, self.world
         ranges = split_tile_rows(g.nty, world)
         ty0, ty1 = ranges[r]
         row0, row1 = owned_rows(g, ranges, r)
@@ -114,6 +123,7 @@ class SpatialSegmenter:
             last = self._infer(tiles[-1:])
             if r + 1 < world:
                 send_req = dist.isend(last.contiguous(), r + 1, group=self.group)
+                self.bytes_sent += last.numel() * last.element_size()
             rest = self._infer(tiles[:-1]) if ty1 - ty0 > 1 else last[:0]
             logits = torch.cat([rest, last])
         else:
@@ -122,6 +132,7 @@ class SpatialSegmenter:
         if r > 0:  # halo: previous rank's last tile row
             halo = torch.empty(1, g.ntx, g.ts, g.ts, self.n_out, dtype=logits.dtype, device=self.device)
             dist.recv(halo, r - 1, group=self.group)
+            self.bytes_received += halo.numel() * halo.element_size()
             logits = torch.cat([halo, logits])
             lt0 = ty0 - 1
         cls, _ = tile_stitch(logits, g, row0=row0, rows=row1 - row0, ty0=lt0)
@@ -131,11 +142,36 @@ class SpatialSegmenter:
             return cls
         if r != 0:
             dist.send(cls.contiguous(), 0, group=self.group)
+            self.bytes_sent += cls.numel()
             return None
         bands = [cls]
         for src in range(1, world):
             a, b = owned_rows(g, ranges, src)
             buf = torch.empty(b - a, g.width, dtype=torch.uint8, device=self.device)
             dist.recv(buf, src, group=self.group)
+            self.bytes_received += buf.numel()
             bands.append(buf)
         return torch.cat(bands)
+
+    # ------------------------------------------------------------ API worker group (leader + followers)
+    def serve_follower(self) -> int:
+        """Non-zero ranks of a land-cover worker group: segment every mosaic the leader broadcasts
+        until it calls :meth:`stop`. Returns the number of mosaics served."""
+        n = 0
+        while True:
+            shape = torch.zeros(3, dtype=torch.int64, device=self.device)
+            dist.broadcast(shape, 0, group=self.group)
+            if int(shape[0]) < 0:
+                return n
+            self._run_follower(tuple(int(v) for v in shape.tolist()))
+            n += 1
+
+    def _run_follower(self, shape) -> None:
+        # same collective sequence as run() on a non-zero rank, after the shape broadcast
+        mosaic = torch.empty(*shape, dtype=torch.uint8, device=self.device)
+        dist.broadcast(mosaic, 0, group=self.group)
+        self._segment(mosaic)
+
+    def stop(self) -> None:
+        if self.world > 1 and self.rank == 0:
+            dist.broadcast(torch.full((3,), -1, dtype=torch.int64, device=self.device), 0, group=self.group)

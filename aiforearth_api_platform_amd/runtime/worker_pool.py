@@ -30,10 +30,18 @@ import numpy as np
 import torch
 
 from ..store import native
-from .gpu_worker import ModelSpec, worker_main  # noqa: F401  (ModelSpec re-exported)
+from .gpu_worker import ModelSpec, follower_main, worker_main  # noqa: F401  (ModelSpec re-exported)
 from .servable import format_result
 
 __all__ = ["ModelSpec", "SharedPayloadRing", "WorkerPool"]
+
+
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
 
 
 class SharedPayloadRing:
@@ -87,6 +95,8 @@ class _WorkerHandle:
         self.rank = rank
         self.device = device
         self.proc: Optional[mp.Process] = None
+        self.followers: List[mp.Process] = []  # the rest of a worker group
+        self.group_devices: List[str] = [device]
         self.restarts = 0
         self.stop = threading.Event()
         self.remote = False
@@ -153,8 +163,13 @@ class WorkerPool:
     def start(self, wait_ready_s: float = 600.0) -> "WorkerPool":
         if self._monitor is not None:  # already started
             return self
-        for i, dev in enumerate(self.devices):
-            self._spawn(_WorkerHandle(i, dev))
+        k = max(1, self.spec.group_size)
+        if len(self.devices) % k:
+            raise ValueError(f"{len(self.devices)} devices cannot form worker groups of {k}")
+        for i in range(len(self.devices) // k):
+            w = _WorkerHandle(i, self.devices[i * k])
+            w.group_devices = self.devices[i * k:(i + 1) * k]
+            self._spawn(w)
         self._monitor = threading.Thread(target=self._monitor_loop, daemon=True, name="ai4e-pool-monitor")
         self._monitor.start()
         self.wait_ready(wait_ready_s)
@@ -176,10 +191,17 @@ class WorkerPool:
 
     def _spawn(self, w: _WorkerHandle) -> None:
         parent, child = self._ctx.Pipe(duplex=True)
+        port = _free_port() if self.spec.group_size > 1 else 0
+        self._kill_followers(w)
         w.proc = self._ctx.Process(target=worker_main, args=(child, w.rank, w.device, self.spec, self.ring.name,
-                                                             self.ring.nslots, self.hb_interval), daemon=True,
-                                   name=f"ai4e-gpu-worker-{w.rank}")
+                                                             self.ring.nslots, self.hb_interval),
+                                   kwargs={"group_port": port}, daemon=True, name=f"ai4e-gpu-worker-{w.rank}")
         w.proc.start()
+        for g, dev in enumerate(w.group_devices[1:], start=1):
+            f = self._ctx.Process(target=follower_main, args=(dev, self.spec, g, self.spec.group_size, port),
+                                  daemon=True, name=f"ai4e-gpu-worker-{w.rank}.{g}")
+            f.start()
+            w.followers.append(f)
         child.close()
         fd = os.dup(parent.fileno())
         parent.close()
@@ -190,6 +212,15 @@ class WorkerPool:
                 self.workers.append(w)
         self.sched.attach(w.rank, fd, True)
         self.events.append((time.time(), "spawn", w.rank))
+
+    @staticmethod
+    def _kill_followers(w: _WorkerHandle, grace_s: float = 0.0) -> None:
+        for f in w.followers:
+            f.join(grace_s)
+            if f.is_alive():
+                f.kill()
+                f.join(10)
+        w.followers = []
 
     def attach_remote(self, rank: int, conn, device: str = "remote") -> None:
         """A worker process started elsewhere (a torchrun rank) that connected to this node scheduler."""
@@ -214,6 +245,7 @@ class WorkerPool:
                 if w.proc is not None and w.proc.is_alive():
                     w.proc.kill()
                     w.proc.join(10)
+                self._kill_followers(w)
                 if not w.remote and w.restarts < self.max_restarts and not self._stop.is_set():
                     w.restarts += 1
                     self.events.append((time.time(), "restart", rank))
@@ -227,8 +259,11 @@ class WorkerPool:
         active = [w for w in self.workers if not w.stop.is_set()]
         if n > len(active):
             devs = list(devices or self.devices)
+            k = max(1, self.spec.group_size)
             for i in range(len(active), n):
-                self._spawn(_WorkerHandle(max((w.rank for w in self.workers), default=-1) + 1, devs[i % len(devs)]))
+                w = _WorkerHandle(max((w.rank for w in self.workers), default=-1) + 1, devs[(i * k) % len(devs)])
+                w.group_devices = [devs[(i * k + j) % len(devs)] for j in range(k)]
+                self._spawn(w)
         else:
             for w in active[n:]:
                 self._retire(w)
@@ -243,6 +278,7 @@ class WorkerPool:
             w.proc.join(30)
             if w.proc.is_alive():
                 w.proc.kill()
+        self._kill_followers(w, 30.0)
         self.events.append((time.time(), "retire", w.rank))
 
     def stop(self) -> None:
@@ -256,6 +292,7 @@ class WorkerPool:
                 w.proc.join(30)
                 if w.proc.is_alive():
                     w.proc.kill()
+            self._kill_followers(w, 30.0)
         if self._monitor is not None:
             self._monitor.join(5)
         if self._feed is not None:

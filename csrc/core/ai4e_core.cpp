@@ -300,6 +300,8 @@ PYBIND11_MODULE(_ai4e_core, m) {
                d["gpu_busy_ms"] = w.gpu_busy_ms;
                d["hbm_used"] = w.hbm_used;
                d["hbm_total"] = w.hbm_total;
+               d["xgmi_tx_bytes"] = w.xgmi_tx;
+               d["xgmi_rx_bytes"] = w.xgmi_rx;
                d["info"] = w.info;
                out.append(d);
              }

@@ -13,7 +13,7 @@
 // recv_bytes. Payload = u32 type + fields (little-endian):
 //
 //   READY  (w->s) i32 rank, i32 pinned, utf-8 JSON info
-//   HB     (w->s) f64 t, u64 hbm_used, u64 hbm_total, f64 gpu_busy_ms, u64 batches
+//   HB     (w->s) f64 t, u64 hbm_used, u64 hbm_total, f64 gpu_busy_ms, u64 batches, u64 xgmi_tx, u64 xgmi_rx
 //   DONE   (w->s) u64 bid, u32 n, u32 row_bytes, f64 stage[5], u8 status[n] (padded to 8), rows
 //   BATCH  (s->w) u64 bid, u32 n, u32 0, i64 slots[n]
 //   STOP   (s->w)
@@ -85,7 +85,7 @@ struct WorkerStats {
   uint64_t batches = 0, images = 0, failed_items = 0, retried_items = 0;
   size_t outstanding = 0;
   double last_hb_age_s = 0, gpu_busy_ms = 0;
-  uint64_t hbm_used = 0, hbm_total = 0;
+  uint64_t hbm_used = 0, hbm_total = 0, xgmi_tx = 0, xgmi_rx = 0;
   std::string info;
 };
 
@@ -220,6 +220,8 @@ class NodeScheduler {
       s.gpu_busy_ms = w.gpu_busy_ms;
       s.hbm_used = w.hbm_used;
       s.hbm_total = w.hbm_total;
+      s.xgmi_tx = w.xgmi_tx;
+      s.xgmi_rx = w.xgmi_rx;
       s.info = w.info;
       out.push_back(s);
     }
@@ -277,7 +279,7 @@ class NodeScheduler {
     std::unordered_map<uint64_t, Outstanding> out;
     uint64_t batches = 0, images = 0, failed_items = 0, retried_items = 0;
     double gpu_busy_ms = 0;
-    uint64_t hbm_used = 0, hbm_total = 0;
+    uint64_t hbm_used = 0, hbm_total = 0, xgmi_tx = 0, xgmi_rx = 0;
     std::string info;
   };
   struct RemotePart {
@@ -556,6 +558,10 @@ class NodeScheduler {
             std::memcpy(&w.hbm_used, p + 8, 8);
             std::memcpy(&w.hbm_total, p + 16, 8);
             std::memcpy(&w.gpu_busy_ms, p + 24, 8);
+          }
+          if (len >= 56) {
+            std::memcpy(&w.xgmi_tx, p + 40, 8);
+            std::memcpy(&w.xgmi_rx, p + 48, 8);
           }
           break;
         }

@@ -69,3 +69,53 @@ def test_worker_pool_two_gpus_share_the_queue():
     imgs, got, stats, _ = _run_pool(["cuda:0", "cuda:1"], 256)
     assert torch.equal(got, _reference_top1(imgs))
     assert all(w["images"] > 0 for w in stats["workers"])
+
+
+@pytest.mark.skipif(torch.cuda.device_count() < 2, reason="needs two GPUs (RCCL detector -> classifier pair)")
+def test_ensemble_pair_over_rccl_matches_single_gpu():
+    from aiforearth_api_platform_amd.models import zoo
+    kw = dict(max_crops=4, score_thresh=0.0, class_id=None, num_species=20, box_score_thresh=0.0)
+    imgs = np.random.default_rng(2).integers(0, 256, (4, 256, 256, 3), dtype=np.uint8)
+    spec = ModelSpec("aiforearth_api_platform_amd.models.zoo:camera_trap_ensemble_pair", (256, 256, 3), 4, 5, kw,
+                     False, (), ("http://127.0.0.1/v1/pair/classify",), 2)
+    cp = ControlPlane(Config.load(env={}))
+    pool = WorkerPool(cp, "http://127.0.0.1/v1/pair/detect", spec, ["cuda:0", "cuda:1"],
+                      heartbeat_interval_s=0.2).start(wait_ready_s=600)
+    try:
+        ids = pool.submit_many(imgs)
+        assert _wait(lambda: cp.store.zcard("/v1/pair/classify_completed") == 4)
+        got = [pool.result(t) for t in ids]
+    finally:
+        pool.stop()
+        cp.close()
+    local = zoo.camera_trap_ensemble("cuda:0", **kw)
+    outs = local(torch.from_numpy(imgs).cuda())
+    for i in range(4):
+        assert [a["species"] for a in got[i]["animals"]] == outs[2][i][: int(outs[4][i, 0])].tolist()
+
+
+@pytest.mark.skipif(torch.cuda.device_count() < 2, reason="needs two GPUs (RCCL halo exchange)")
+def test_spatial_landcover_over_rccl_matches_single_gpu():
+    import base64
+    import io
+
+    from PIL import Image
+
+    from aiforearth_api_platform_amd.models import zoo
+    kw = dict(height=1024, width=1024, tile=512, stride=448, tile_batch=8)
+    mosaic = np.random.default_rng(4).integers(0, 256, (1, 1024, 1024, 4), dtype=np.uint8)
+    spec = ModelSpec("aiforearth_api_platform_amd.models.zoo:landcover_spatial", (1024, 1024, 4), 1, 5, kw, False,
+                     (), (), 2)
+    cp = ControlPlane(Config.load(env={}))
+    pool = WorkerPool(cp, "http://127.0.0.1/v1/lc/spatial", spec, ["cuda:0", "cuda:1"],
+                      heartbeat_interval_s=0.2).start(wait_ready_s=600)
+    try:
+        ids = pool.submit_many(mosaic)
+        assert _wait(lambda: cp.store.zcard("/v1/lc/spatial_completed") == 1)
+        got = pool.result(ids[0])
+    finally:
+        pool.stop()
+        cp.close()
+    cls = np.asarray(Image.open(io.BytesIO(base64.b64decode(got["class_map"]))))
+    ref = zoo.landcover("cuda:0", **kw)(torch.from_numpy(mosaic).cuda())[0][0].cpu().numpy()
+    assert (cls != ref).mean() < 1e-3  # bf16 tile logits: a handful of argmax ties may flip

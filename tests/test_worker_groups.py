@@ -1,0 +1,79 @@
+"""Multi-GPU API forms as worker groups, on CPU ranks (gloo stands in for RCCL):
+
+* config 5: detector -> classifier pair (leader = detector process, follower = classifier process,
+  crops and results over P2P) served through the pool == the single-process ensemble;
+* config 4: spatial-parallel land-cover over a 3-process group (tile rows split, halo rows over P2P,
+  bands gathered on the leader) == the single-process segmentation.
+"""
+import time
+
+import numpy as np
+import torch
+
+from aiforearth_api_platform_amd.config import Config
+from aiforearth_api_platform_amd.gateway.control import ControlPlane
+from aiforearth_api_platform_amd.runtime.worker_pool import ModelSpec, WorkerPool
+
+DET = dict(box_score_thresh=0.0, pre_nms_top_n=100, post_nms_top_n=50, detections_per_img=10)
+ENS = dict(max_crops=3, score_thresh=0.0, class_id=None, num_species=10, **DET)
+
+
+def _wait(cond, t=300):
+    d = time.time() + t
+    while time.time() < d:
+        if cond():
+            return True
+        time.sleep(0.05)
+    return False
+
+
+def _serve(spec, devices, payloads, done_path):
+    cp = ControlPlane(Config.load(env={}))
+    pool = WorkerPool(cp, "http://127.0.0.1/v1/group/in", spec, devices, heartbeat_interval_s=0.2,
+                      heartbeat_timeout_s=120, max_delay_s=0.2).start(wait_ready_s=300)
+    try:
+        ids = pool.submit_many(payloads)
+        assert _wait(lambda: cp.store.zcard(done_path + "_completed") == len(ids))
+        time.sleep(0.6)  # one more heartbeat carries the transfer counters
+        pool.refresh()
+        return [pool.result(t) for t in ids], pool.stats()
+    finally:
+        pool.stop()
+        cp.close()
+
+
+def test_ensemble_pair_group_matches_single_process():
+    from aiforearth_api_platform_amd.models import zoo
+    from aiforearth_api_platform_amd.runtime.servable import decode_row, encode_rows
+    imgs = np.random.default_rng(5).integers(0, 256, (2, 128, 128, 3), dtype=np.uint8)
+    spec = ModelSpec("aiforearth_api_platform_amd.models.zoo:camera_trap_ensemble_pair", (128, 128, 3), 2, 5, ENS,
+                     False, (), ("http://127.0.0.1/v1/group/classify",), 2)
+    got, stats = _serve(spec, ["cpu", "cpu"], imgs, "/v1/group/classify")
+    local = zoo.camera_trap_ensemble("cpu", **ENS)
+    outs = [o.numpy() for o in local(torch.from_numpy(imgs))]
+    rb = sum(f.nbytes for f in local.outputs)
+    rows = encode_rows(outs, 2)
+    for i in range(2):
+        ref = local.format(decode_row(rows[i * rb:(i + 1) * rb], local.outputs))
+        assert [a["species"] for a in got[i]["animals"]] == [a["species"] for a in ref["animals"]]
+        assert [a["bbox"] for a in got[i]["animals"]] == [a["bbox"] for a in ref["animals"]]
+    w = stats["workers"][0]
+    assert w["xgmi_tx_bytes"] > 0 and w["xgmi_rx_bytes"] > 0  # crops out, classifications back
+
+
+def test_spatial_landcover_group_matches_single_process():
+    import base64
+    import io
+
+    from PIL import Image
+
+    from aiforearth_api_platform_amd.models import zoo
+    kw = dict(height=256, width=256, tile=128, stride=112, tile_batch=4)
+    mosaic = np.random.default_rng(6).integers(0, 256, (1, 256, 256, 4), dtype=np.uint8)
+    spec = ModelSpec("aiforearth_api_platform_amd.models.zoo:landcover_spatial", (256, 256, 4), 1, 5, kw, False,
+                     (), (), 3)
+    got, stats = _serve(spec, ["cpu", "cpu", "cpu"], mosaic, "/v1/group/in")
+    cls = np.asarray(Image.open(io.BytesIO(base64.b64decode(got[0]["class_map"]))))
+    ref = zoo.landcover("cpu", **kw)(torch.from_numpy(mosaic))[0][0].numpy()
+    assert np.array_equal(cls, ref)
+    assert stats["workers"][0]["xgmi_rx_bytes"] > 0
