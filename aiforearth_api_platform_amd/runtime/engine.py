@@ -9,6 +9,7 @@ previous batch computes; only the top-k result (a few bytes per image) is copied
 """
 from __future__ import annotations
 
+import os
 import threading
 import time
 from dataclasses import dataclass
@@ -131,6 +132,10 @@ class InferenceEngine:
         cuda = self.device.type == "cuda"
         self.copy_stream = torch.cuda.Stream(self.device) if cuda else None
         self.compute_stream = torch.cuda.Stream(self.device) if cuda else None
+        # AI4E_ENGINE_STREAMS=2: consecutive batches replay on alternating compute streams, so the tail of
+        # batch i (layer3/4 grids smaller than the 256-CU machine) can overlap the head of batch i+1
+        ns = int(os.environ.get("AI4E_ENGINE_STREAMS", "1")) if cuda else 1
+        self.compute_streams = [self.compute_stream] + [torch.cuda.Stream(self.device) for _ in range(ns - 1)]
         self.inputs = [torch.empty((max_batch, *self.item_shape), dtype=torch.uint8, device=self.device)
                        for _ in range(nbuf)]
         self.host_out: List[List[torch.Tensor]] = [[] for _ in range(nbuf)]  # allocated at warmup
@@ -215,7 +220,7 @@ class InferenceEngine:
         ev.record(cs)
         if self.timing:
             ev1 = ev
-        st = self.compute_stream
+        st = self.compute_streams[buf % len(self.compute_streams)]
         st.wait_event(ev)
         with torch.cuda.stream(st):
             if self.use_graphs and (buf, b) in self.graphs:
