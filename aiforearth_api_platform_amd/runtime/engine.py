@@ -132,9 +132,10 @@ class InferenceEngine:
         cuda = self.device.type == "cuda"
         self.copy_stream = torch.cuda.Stream(self.device) if cuda else None
         self.compute_stream = torch.cuda.Stream(self.device) if cuda else None
-        # AI4E_ENGINE_STREAMS=2: consecutive batches replay on alternating compute streams, so the tail of
+        # AI4E_ENGINE_STREAMS (default 2): consecutive batches replay on alternating compute streams, so the tail of
         # batch i (layer3/4 grids smaller than the 256-CU machine) can overlap the head of batch i+1
-        ns = int(os.environ.get("AI4E_ENGINE_STREAMS", "1")) if cuda else 1
+        # (ResNet-50 @250: +1.5-1.9 % images/s same-box A/B, p99 14.1 -> 10.9 ms; profiles/r2_pool/)
+        ns = int(os.environ.get("AI4E_ENGINE_STREAMS", "2")) if cuda else 1
         self.compute_streams = [self.compute_stream] + [torch.cuda.Stream(self.device) for _ in range(ns - 1)]
         self.inputs = [torch.empty((max_batch, *self.item_shape), dtype=torch.uint8, device=self.device)
                        for _ in range(nbuf)]

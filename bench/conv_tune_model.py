@@ -1,6 +1,6 @@
 """Per-shape K1 tile-config sweep for the convs one model forward actually runs (U-Net land-cover tiles,
 Faster-RCNN detector batches): records every ``tuned_tile`` lookup during a forward, times tile configs
-1-6 on each distinct shape in isolation and, with ``--write``, MERGES the winners into
+1-8 on each distinct shape in isolation and, with ``--write``, MERGES the winners into
 ``aiforearth_api_platform_amd/ops/conv_tiles.json`` (existing keys of other shapes are kept).
 
     [B=16] python bench/conv_tune_model.py unet [--write]   # B tiles x 512^2 x 4 (bench/landcover_bench.py)
@@ -80,7 +80,7 @@ def main():
         raise SystemExit(f"unknown model {which}")
     table = {}
     for key, (pc, n, h, w, res) in shapes.items():
-        times = {c: t for c in (1, 2, 3, 4, 5, 6) if (t := time_cfg(pc, n, h, w, res, c, dev)) is not None}
+        times = {c: t for c in (1, 2, 3, 4, 5, 6, 7, 8) if (t := time_cfg(pc, n, h, w, res, c, dev)) is not None}
         best = min(times, key=times.get)
         table[key] = best
         print(json.dumps({"key": key, "us": {k: round(v, 1) for k, v in times.items()}, "best": best}), flush=True)

@@ -83,8 +83,11 @@ enum { GATHER_GENERAL = 0,  // any C % 8: a 32-wide K chunk may span taps -> per
        GATHER_POINTWISE = 1,  // 1x1, pad 0 (any stride): K is the channel axis of one input pixel
        GATHER_TAP = 2 };      // C % 32 == 0: a K chunk lies in ONE tap -> the tap walk is wave-uniform (SGPRs)
 
-template <int WAVES_M, int WAVES_N, int STAGES, int GATHER, bool EPI_LDS>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) void conv_igemm_kernel(const ConvParams p) {
+// OCC = workgroups per CU the config is built for (waves per SIMD): 2 for the 4-stage ring (64 KB of
+// LDS), 3 for the 3-stage ring (48 KB) — the register budget (<= 512/OCC VGPRs) must let that many
+// resident, which is what lets a 766-tile layer3 grid run as ONE balanced round on 256 CUs.
+template <int WAVES_M, int WAVES_N, int STAGES, int GATHER, bool EPI_LDS, int OCC = 2>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC > 2 ? OCC : 1, OCC))) void conv_igemm_kernel(const ConvParams p) {
   static_assert(WAVES_M * WAVES_N == 4, "4 waves per workgroup");
   static_assert(STAGES >= 3, "fragment prefetch needs >= 3 ring stages");
   constexpr int BM = WAVES_M * 64;  // pixels per workgroup
@@ -115,13 +118,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
   constexpr int EPI_CHUNKS = BM * CPR / 256;  // chunks per thread
   uint2 rres[4][4];
   uint4 rres16[EPI_CHUNKS];
+  // occupancy-3 configs cannot hold the residual tile in registers across the K loop (168-VGPR budget):
+  // they load it per epilogue pass instead, with the other resident workgroups covering the latency
+  constexpr bool EARLY_RES = OCC <= 2;
   if (p.res) {  // unconditional loads (clamped rows/cols) so hipcc keeps one counted wait for all
     if constexpr (EPI_LDS) {
+      if constexpr (EARLY_RES) {
 #pragma unroll
-      for (int e = 0; e < EPI_CHUNKS; ++e) {
-        const int g = tid + 256 * e;
-        const int m = min(m0 + g / CPR, p.M - 1), n = min(n0 + 8 * (g % CPR), p.Kout - 8);
-        rres16[e] = *reinterpret_cast<const uint4*>(p.res + res_row(p, m) * p.ldres + n);
+        for (int e = 0; e < EPI_CHUNKS; ++e) {
+          const int g = tid + 256 * e;
+          const int m = min(m0 + g / CPR, p.M - 1), n = min(n0 + 8 * (g % CPR), p.Kout - 8);
+          rres16[e] = *reinterpret_cast<const uint4*>(p.res + res_row(p, m) * p.ldres + n);
+        }
       }
     } else {
 #pragma unroll
@@ -298,29 +306,53 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
     // halving store instructions and giving the residual read the same full-line shape.
     // Row-major [BM][BN] fp32 with the 16-B chunk index XOR-swizzled by (row & 7): the 8-lane
     // ds_write_b128 groups (8 rows, one column) hit 8 different bank quads.
-    static_assert(BM * BN * 4 <= STAGES * STAGE_ELEMS * 2, "epilogue tile must fit the stage ring");
+    // A ring smaller than the fp32 tile (the 3-stage configs) stages it in two row halves: the waves
+    // owning rows [0, BM/2) write first, every thread stores those rows, then the other half.
+    constexpr int EPI_PASSES = (BM * BN * 4 <= STAGES * STAGE_ELEMS * 2) ? 1 : 2;
+    static_assert(EPI_PASSES == 1 || (WAVES_M % 2 == 0 && BM * BN * 2 <= STAGES * STAGE_ELEMS * 2),
+                  "epilogue tile (or half of it) must fit the stage ring");
+    constexpr int PASS_ROWS = BM / EPI_PASSES;
     float* tile = reinterpret_cast<float*>(smem);
     float gs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, gq[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     __builtin_amdgcn_s_barrier();  // all waves finished reading the last stage
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int r = wm * 64 + 16 * i + (lane & 15);
+    for (int pass = 0; pass < EPI_PASSES; ++pass) {
+    if (pass) __syncthreads();  // the first half is stored before the second overwrites it
+    constexpr int PC = EPI_CHUNKS / EPI_PASSES;
+    uint4 rlate[PC];
+    if constexpr (!EARLY_RES) {
+      if (p.res) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int q = (wn * 64 + 16 * j + 4 * (lane >> 4)) >> 2;  // fp32 16-B chunk in the row
-        *reinterpret_cast<f32x4_t*>(tile + r * BN + 4 * (q ^ (r & 7))) = acc[i][j];
+        for (int k = 0; k < PC; ++k) {
+          const int g = tid + 256 * (pass * PC + k);
+          const int m = min(m0 + g / CPR, p.M - 1), n = min(n0 + 8 * (g % CPR), p.Kout - 8);
+          rlate[k] = *reinterpret_cast<const uint4*>(p.res + res_row(p, m) * p.ldres + n);
+        }
+      }
+    }
+    if (wm * 64 / PASS_ROWS == pass) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = wm * 64 + 16 * i + (lane & 15) - pass * PASS_ROWS;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int q = (wn * 64 + 16 * j + 4 * (lane >> 4)) >> 2;  // fp32 16-B chunk in the row
+          *reinterpret_cast<f32x4_t*>(tile + r * BN + 4 * (q ^ (r & 7))) = acc[i][j];
+        }
       }
     }
     __syncthreads();
 #pragma unroll
-    for (int e = 0; e < EPI_CHUNKS; ++e) {
+    for (int e = pass * EPI_CHUNKS / EPI_PASSES; e < (pass + 1) * EPI_CHUNKS / EPI_PASSES; ++e) {
       const int g = tid + 256 * e;
       const int r = g / CPR, cq = g % CPR;
       const int m = m0 + r, n = n0 + 8 * cq;
-      const float4 v0 = *reinterpret_cast<const float4*>(tile + r * BN + 4 * ((2 * cq) ^ (r & 7)));
-      const float4 v1 = *reinterpret_cast<const float4*>(tile + r * BN + 4 * ((2 * cq + 1) ^ (r & 7)));
+      const int rl = r - pass * PASS_ROWS;  // row within the staged half
+      const float4 v0 = *reinterpret_cast<const float4*>(tile + rl * BN + 4 * ((2 * cq) ^ (rl & 7)));
+      const float4 v1 = *reinterpret_cast<const float4*>(tile + rl * BN + 4 * ((2 * cq + 1) ^ (rl & 7)));
       const float f[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-      const uint4 o = epilogue8_bf16(f, p.res != nullptr, rres16[e], (p.relu & 1) != 0);
+      const uint4 o = epilogue8_bf16(f, p.res != nullptr, EARLY_RES ? rres16[e] : rlate[e - pass * PC],
+                                     (p.relu & 1) != 0);
       if (p.gnp && m < p.M && n < p.Kout) {  // GN statistics of the values as stored (bf16)
         const uint32_t ow[4] = {o.x, o.y, o.z, o.w};
 #pragma unroll
@@ -340,6 +372,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
         }
       }
     }
+    }  // pass
     if (p.gnp) {
       // (1) in-thread: fold this lane's 8 channels into their groups (cgm = min(channels per group, 8) adjacent
       // channels per slot); (2) lanes sharing the 8-channel column (lane % CPR) reduce by xor shuffles; (3) the
@@ -702,7 +735,7 @@ const uint16_t* zero_chunk_ptr() {
   return ptr;
 }
 
-template <int WM, int WN, int STAGES>
+template <int WM, int WN, int STAGES, int OCC = 2>
 int launch(const ConvParams& p0, hipStream_t s) {
   ConvParams p = p0;
   const int mt = ai4e_cdiv(p.M, WM * 64);
@@ -716,7 +749,7 @@ int launch(const ConvParams& p0, hipStream_t s) {
   // coalesced LDS epilogue needs 16-B aligned output/residual rows
   const bool epi = !(p.ldy % 8 || p.ycoff % 8 || (p.res && p.ldres % 8) || p.Kout < 8);
 #define K1_LAUNCH(G, E) \
-  hipLaunchKernelGGL((conv_igemm_kernel<WM, WN, STAGES, G, E>), dim3(nb), dim3(256), 0, s, p)
+  hipLaunchKernelGGL((conv_igemm_kernel<WM, WN, STAGES, G, E, OCC>), dim3(nb), dim3(256), 0, s, p)
   if (g == GATHER_POINTWISE) {
     if (epi) K1_LAUNCH(GATHER_POINTWISE, true); else K1_LAUNCH(GATHER_POINTWISE, false);
   } else if (g == GATHER_TAP) {
@@ -750,7 +783,8 @@ int launch256(const ConvParams& p0, hipStream_t s) {
 // tile_cfg (pixels x channels per workgroup, LDS ring depth): 0 = auto, 1 = 128x128 (2x2 waves),
 // 2 = 256x64 (4x1), 3 = 64x256 (1x4) with 4 stages; 4 = 128x128 with 5 stages (80 KB: still two
 // workgroups per CU), 5 = 256x64 with 5 stages (100 KB: one workgroup per CU), 6 = 256x256, 8 waves,
-// ping-pong phases (needs C % 64 == 0, Kout % 8 == 0).
+// ping-pong phases (needs C % 64 == 0, Kout % 8 == 0); 7/8 = the 128x128 / 256x64 tiles with a 3-stage
+// ring (48 KB, two-pass LDS epilogue) built for three workgroups per CU.
 // relu: bit 0 = ReLU; bit 1 = `res` is on the half-resolution grid [N, OH/2, OW/2, ldres] (nearest 2x
 // upsample of the residual, OH and OW even).
 namespace {
@@ -776,7 +810,8 @@ int conv2d_impl(const void* x, const void* w, const void* bias, const void* res,
   if (gnp) {
     // fused GroupNorm statistics: 128-wide LDS-epilogue tiles only (configs 1, 2, 4, 5), whole groups per
     // channel tile, tiles that never straddle images, full 16-B output rows
-    const int bm = (tile_cfg == 2 || tile_cfg == 5) ? 256 : 128, bn = (tile_cfg == 2 || tile_cfg == 5) ? 64 : 128;
+    const bool tall = tile_cfg == 2 || tile_cfg == 5 || tile_cfg == 8;
+    const int bm = tall ? 256 : 128, bn = tall ? 64 : 128;
     if (tile_cfg == 3 || tile_cfg == 6 || gn_groups <= 0 || Kout % gn_groups || (OH * OW) % bm || Kout % 8 ||
         ldy % 8 || ycoff % 8 || (res && ldres % 8) || bn % (Kout / gn_groups))
       return AI4E_EINVAL;
@@ -790,6 +825,8 @@ int conv2d_impl(const void* x, const void* w, const void* bias, const void* res,
     case 4: return launch<2, 2, 5>(p, stream);
     case 5: return launch<4, 1, 5>(p, stream);
     case 6: return launch256(p, stream);
+    case 7: return launch<2, 2, 3, 3>(p, stream);
+    case 8: return launch<4, 1, 3, 3>(p, stream);
     default: return AI4E_EINVAL;
   }
 }

@@ -62,7 +62,7 @@ def test_conv_igemm(case, epi):
     assert err <= 0.02 * ref.abs().max().item() + 0.02, err
 
 
-@pytest.mark.parametrize("tile", [1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("tile", [1, 2, 3, 4, 5, 6, 7, 8])
 def test_conv_tile_configs(tile):
     torch.manual_seed(1)
     wt = torch.randn(256, 64, 3, 3) / 24
@@ -71,6 +71,25 @@ def test_conv_tile_configs(tile):
     y = conv2d_nhwc(x, pc, tile_cfg=tile)
     ref = ref_conv(x, pc.w_packed[:256, :576].float().reshape(256, 3, 3, 64).permute(0, 3, 1, 2), torch.zeros(256, device=DEV), 1, 1)
     assert (y.float() - ref).abs().max().item() < 0.02 * ref.abs().max().item() + 0.02
+
+
+@pytest.mark.parametrize("tile", [7, 8])
+@pytest.mark.parametrize("shape", [(3, 14, 14, 256, 256, 3, 1, 1), (2, 7, 7, 512, 512, 3, 1, 1),
+                                   (5, 14, 14, 256, 1024, 1, 1, 0), (1, 9, 11, 64, 136, 1, 1, 0)])
+def test_conv_occupancy3_configs_residual(tile, shape):
+    """3-stage ring (two-pass LDS epilogue, residual loaded per pass): ragged M, residual + ReLU."""
+    n, h, w, cin, cout, k, st, pd = shape
+    torch.manual_seed(7)
+    wt = torch.randn(cout, cin, k, k) / (cin * k * k) ** 0.5
+    b = torch.randn(cout) * 0.1
+    pc = pack_conv(wt, b, stride=st, pad=pd).to(DEV)
+    x = torch.randn(n, h, w, cin, device=DEV).to(torch.bfloat16)
+    oh, ow = pc.out_hw(h, w)
+    res = torch.randn(n, oh, ow, cout, device=DEV).to(torch.bfloat16)
+    y = conv2d_nhwc(x, pc, residual=res, relu=True, tile_cfg=tile)
+    wq = pc.w_packed[:cout, :k * k * cin].float().reshape(cout, k, k, cin).permute(0, 3, 1, 2)
+    ref = ref_conv(x, wq, b.to(DEV), st, pd, res, True)
+    assert (y.float() - ref).abs().max().item() <= 0.02 * ref.abs().max().item() + 0.02
 
 
 CASES_256 = [
