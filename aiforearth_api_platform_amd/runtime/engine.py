@@ -125,7 +125,7 @@ class InferenceEngine:
         self.topk = topk
         self.use_graphs = use_graphs and self.device.type == "cuda"
         self.timing = timing and self.device.type == "cuda"
-        self.nbuf = nbuf
+        self.nbuf = max(nbuf, int(os.environ.get("AI4E_ENGINE_NBUF", "0")))
         self.buckets = sorted(set(buckets or [max_batch]))
         if self.buckets[-1] != max_batch:
             self.buckets.append(max_batch)
