@@ -138,11 +138,11 @@ class InferenceEngine:
         ns = int(os.environ.get("AI4E_ENGINE_STREAMS", "2")) if cuda else 1
         self.compute_streams = [self.compute_stream] + [torch.cuda.Stream(self.device) for _ in range(ns - 1)]
         self.inputs = [torch.empty((max_batch, *self.item_shape), dtype=torch.uint8, device=self.device)
-                       for _ in range(nbuf)]
-        self.host_out: List[List[torch.Tensor]] = [[] for _ in range(nbuf)]  # allocated at warmup
+                       for _ in range(self.nbuf)]
+        self.host_out: List[List[torch.Tensor]] = [[] for _ in range(self.nbuf)]  # allocated at warmup
         self.graphs: Dict[Tuple[int, int], torch.cuda.CUDAGraph] = {}
         self._graph_out: Dict[Tuple[int, int], Tuple[torch.Tensor, ...]] = {}
-        self.compute_done: List[Optional[torch.cuda.Event]] = [None] * nbuf
+        self.compute_done: List[Optional[torch.cuda.Event]] = [None] * self.nbuf
         self._k = 0
 
     # -------------------------------------------------------------- forward
