@@ -113,7 +113,7 @@ class InferenceEngine:
 
     def __init__(self, model_fn: Optional[Callable[[torch.Tensor], torch.Tensor]], item_shape: Sequence[int],
                  max_batch: int, device: Optional[torch.device] = None, topk: int = 5, use_graphs: bool = True,
-                 nbuf: int = 3, buckets: Optional[Sequence[int]] = None,
+                 nbuf: int = 4, buckets: Optional[Sequence[int]] = None,
                  head_fn: Optional[Callable[[torch.Tensor, int], Tuple[torch.Tensor, torch.Tensor]]] = None,
                  output_fn: Optional[Callable[[torch.Tensor], Sequence[torch.Tensor]]] = None, timing: bool = False):
         self.model_fn = model_fn

@@ -177,7 +177,7 @@ def run_node_bench(args, spec, path: str, metric: str, unit: str = "images/s", c
         remote = [(part * r, part, r) for r in range(1, world)]
         pool = WorkerPool(cp, endpoint, spec, [f"{args.device}:{denv.local_rank}" if args.device == "cuda" else "cpu"],
                           ring_slots=part, max_delay_s=0.0005, heartbeat_interval_s=hb, heartbeat_timeout_s=120.0,
-                          remote_partitions=remote, pipeline_depth=int(os.environ.get("AI4E_PIPELINE_DEPTH", "2")),
+                          remote_partitions=remote, pipeline_depth=int(os.environ.get("AI4E_PIPELINE_DEPTH", "3")),
                           poll_s=0.005)
         info = None
         listener = None

@@ -118,7 +118,7 @@ class _WorkerHandle:
 class WorkerPool:
     def __init__(self, control_plane, endpoint: str, spec: ModelSpec, devices: Sequence[str], ring_slots: int = 0,
                  max_delay_s: float = 0.0005, heartbeat_interval_s: float = 0.5, heartbeat_timeout_s: float = 10.0,
-                 max_restarts: int = 2, pipeline_depth: int = 2, retry_delay_s: float = 1.0,
+                 max_restarts: int = 2, pipeline_depth: int = 3, retry_delay_s: float = 1.0,
                  remote_partitions: Sequence[Tuple[int, int, int]] = (), completion_feed: bool = False,
                  poll_s: float = 0.02):
         if native is None:
@@ -131,6 +131,9 @@ class WorkerPool:
             raise RuntimeError("the worker pool needs the native store/queue backend (AI4E_STORE_BACKEND=native)")
         self.spec = spec
         self.devices = list(devices)
+        # 3 batches in flight per worker: two overlap on the GPU's two compute streams while the third is
+        # already copied in, so a finishing batch never leaves the GPU waiting for the next H2D
+        # (ResNet-50 @250: 67.4-69.5k -> 75.7-77.7k images/s, p50 10.6 -> 9.1-9.4 ms; profiles/r2_pool/)
         local = ring_slots or spec.max_batch * (pipeline_depth + 2) * max(1, len(self.devices))
         self.remote_partitions = [tuple(int(v) for v in p) for p in remote_partitions]  # (base, len, rank)
         total = max([local] + [b + n for b, n, _ in self.remote_partitions])
