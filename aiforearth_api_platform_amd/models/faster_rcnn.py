@@ -89,7 +89,8 @@ class FasterRCNN:
         wp[nc: nc + 4 * nc] = torch.randn(4 * nc, rep, 1, 1, generator=g) * 0.001
         self.predictor = pack_conv(wp, torch.zeros(pred_out)).to(d)
         self._anchor_cache: Dict[Tuple, List[torch.Tensor]] = {}
-        self.fc_blas = os.environ.get("AI4E_DET_FC_BLAS", "1") not in ("0", "off", "")
+        # box-head FCs on K1 (the 256x256 tile, tuned per batch in conv_tiles.json); AI4E_DET_FC_BLAS=1: hipBLASLt
+        self.fc_blas = os.environ.get("AI4E_DET_FC_BLAS", "0") not in ("0", "off", "")
 
     # ------------------------------------------------------------------ backbone + FPN
     def backbone_stages(self, x: torch.Tensor) -> List[torch.Tensor]:
