@@ -19,22 +19,29 @@ from typing import Optional
 
 import torch
 
-from ..runtime.servable import (ClassifierServable, DetectorServable, EnsembleServable, SegmenterServable,
-                                OutputField)
+from ..runtime.servable import (ClassifierServable, DetectorServable, EnsembleServable, OutputField,
+                                ResizingServable, SegmenterServable)
 
 
-def resnet50_classifier(device="cuda", seed: int = 0, num_classes: int = 1000, topk: int = 5):
+def resnet50_classifier(device="cuda", seed: int = 0, num_classes: int = 1000, topk: int = 5,
+                        resize_from_gpu: bool = False):
+    """``resize_from_gpu``: payloads of any fixed frame size (the endpoint's item_shape) are resized
+    to 224x224 on the GPU inside the graph (K7) instead of by the CPU decoder."""
     from .resnet import FusedResNet, resnet50
 
     m = FusedResNet(resnet50(num_classes=num_classes, seed=seed), device=device)
-    return ClassifierServable(m, topk, head=m.topk_u8)
+    s = ClassifierServable(m, topk, head=m.topk_u8)
+    return ResizingServable(s, (224, 224)) if resize_from_gpu else s
 
 
-def megadetector(device="cuda", seed: int = 0, max_dets: Optional[int] = None, **cfg):
+def megadetector(device="cuda", seed: int = 0, max_dets: Optional[int] = None, model_hw=None, **cfg):
+    """``model_hw``: detector resolution when the payload slots hold native camera frames (e.g. 1536x2048):
+    the frames are resized on the GPU in the graph (K7) and boxes come back in frame coordinates."""
     from .faster_rcnn import DetectorConfig, FasterRCNN
 
     det = FasterRCNN(DetectorConfig(**cfg), seed=seed, device=device)
-    return DetectorServable(det, max_dets)
+    s = DetectorServable(det, max_dets)
+    return ResizingServable(s, tuple(model_hw), ("boxes",)) if model_hw else s
 
 
 def landcover(device="cuda", height: int = 4096, width: int = 4096, tile: int = 512, stride: int = 448,

@@ -226,6 +226,49 @@ def pack_ensemble(b: int, sel: torch.Tensor, cls: torch.Tensor, max_crops: int):
     return boxes, scores, species, prob, count
 
 
+class ResizingServable(Servable):
+    """K7 on the GPU: the endpoint's payload slots hold frames of the camera's native size and the
+    bilinear uint8 resize to the model resolution runs inside the same captured graph (``resize_u8``,
+    one whole-image crop-resize per frame) — the data-prep stage of the reference diagram
+    (``Assets/platform_diagram.jpeg``: API1 data prep -> API2 inference) fused into the inference call.
+    Box outputs are scaled back to native-frame coordinates."""
+
+    def __init__(self, inner: Servable, model_hw: Tuple[int, int], box_fields: Sequence[str] = ()):
+        self.inner = inner
+        self.model_hw = tuple(model_hw)
+        self.kind = inner.kind
+        self.outputs = inner.outputs
+        self.box_fields = tuple(box_fields)
+        for k in ("stages",):
+            if hasattr(inner, k):
+                setattr(self, k, getattr(inner, k))
+
+    def __call__(self, images_u8):
+        from ..ops.detection import resize_u8
+
+        h, w = images_u8.shape[1:3]
+        x = images_u8 if (h, w) == self.model_hw else resize_u8(images_u8, self.model_hw)
+        outs = list(self.inner(x))
+        if self.box_fields and (h, w) != self.model_hw:
+            sx, sy = w / self.model_hw[1], h / self.model_hw[0]
+            scale = torch.tensor([sx, sy, sx, sy], device=outs[0].device, dtype=torch.float32)
+            for i, f in enumerate(self.outputs):
+                if f.name in self.box_fields:
+                    outs[i] = outs[i] * scale
+        return tuple(outs)
+
+    def format(self, fields):
+        return self.inner.format(fields)
+
+    def describe(self) -> dict:
+        return self.inner.describe()
+
+    def close(self) -> None:
+        close = getattr(self.inner, "close", None)
+        if callable(close):
+            close()
+
+
 KINDS = {c.kind: c for c in (Servable, ClassifierServable, DetectorServable, SegmenterServable, EnsembleServable)}
 
 

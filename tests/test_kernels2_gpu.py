@@ -234,3 +234,31 @@ def test_groupnorm_apply_fused_maxpool(shape, monkeypatch):
     assert torch.equal(a, b)
     assert (cat[..., cout:] == 7.0).all()
     assert torch.equal(pooled.float(), ref_pool)
+
+
+def test_crop_resize_u8_and_gpu_resize_match_fp32_reference():
+    """K5/K7 uint8 crop-resize (ensemble wire format) and whole-frame GPU resize vs the fp32 reference."""
+    from aiforearth_api_platform_amd.ops.detection import crop_resize_u8, crop_resize_u8_reference, resize_u8
+    torch.manual_seed(3)
+    img = torch.randint(0, 256, (2, 150, 190, 3), dtype=torch.uint8)
+    boxes = torch.tensor([[0, 10.0, 5.0, 120.0, 140.0], [1, 0.0, 0.0, 190.0, 150.0], [0, 50.5, 60.2, 51.0, 61.0]])
+    ref = crop_resize_u8_reference(img, boxes, (64, 48))
+    out = crop_resize_u8(img.to(DEV), boxes.to(DEV), (64, 48)).cpu()
+    assert out.shape == ref.shape and (out.int() - ref.int()).abs().max().item() <= 1
+    frames = torch.randint(0, 256, (3, 480, 640, 3), dtype=torch.uint8)
+    full = torch.tensor([[i, 0.0, 0.0, 640.0, 480.0] for i in range(3)])
+    r = resize_u8(frames.to(DEV), (224, 224)).cpu()
+    assert (r.int() - crop_resize_u8_reference(frames, full, (224, 224)).int()).abs().max().item() <= 1
+
+
+def test_resizing_servable_scales_boxes_to_frame_coordinates():
+    from aiforearth_api_platform_amd.models import zoo
+    frames = torch.randint(0, 256, (2, 480, 640, 3), dtype=torch.uint8, device=DEV)
+    s = zoo.megadetector(DEV, model_hw=(256, 256), box_score_thresh=0.0)
+    boxes, scores, labels, count = s(frames)
+    plain = zoo.megadetector(DEV, box_score_thresh=0.0)
+    from aiforearth_api_platform_amd.ops.detection import resize_u8
+    b2, _, _, c2 = plain(resize_u8(frames, (256, 256)))
+    assert torch.equal(count, c2)
+    k = int(count[0, 0])
+    assert torch.allclose(boxes[0, :k], b2[0, :k] * torch.tensor([2.5, 1.875, 2.5, 1.875], device=DEV), atol=1e-3)
