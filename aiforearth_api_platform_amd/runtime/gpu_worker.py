@@ -125,6 +125,7 @@ class GpuWorker:
         self.engine.warmup()
         self.row_bytes = row_bytes(self.servable.outputs)
         self.batches = 0
+        self.isolated_batches = 0
         self.busy_ms = 0.0
         self.alive = threading.Event()
         self.alive.set()
@@ -235,7 +236,12 @@ class GpuWorker:
             if f.get("fail_batch") == self.batches:
                 raise RuntimeError("injected batch launch failure")
             res = self.engine.submit(self.buf, vslots)
-        except Exception:
+        except Exception as e:
+            import sys
+
+            print(f"[ai4e worker {self.rank}] batch {bid} launch failed ({e!r}); re-running its {len(vslots)} items "
+                  "one by one", file=sys.stderr, flush=True)
+            self.isolated_batches += 1
             self._drain()
             self._isolate(bid, slots, valid, status, t_recv)
             return

@@ -23,6 +23,7 @@ runs both stages on one GPU with a local hand-off (no RCCL), same code path othe
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 from typing import Callable, List, Optional, Sequence, Tuple
 
@@ -86,6 +87,14 @@ class DetectClassifyPipeline:
         self.wire_dtype = getattr(torch, self.cfg.wire_dtype)
         self.bytes_sent = 0       # xGMI payload bytes (crops + headers), for the metrics registry
         self.bytes_received = 0
+        # fault injection (survey §5.3): AI4E_FAULT_INJECTION=xgmi_fail_batch=<k> makes the k-th hand-off of
+        # this detector fail before anything is on the wire (a lost / refused P2P transfer)
+        self._handoffs = 0
+        self._fail_at = 0
+        for item in filter(None, os.environ.get("AI4E_FAULT_INJECTION", "").split(",")):
+            k, _, v = item.partition("=")
+            if k.strip() == "xgmi_fail_batch":
+                self._fail_at = int(v.split("@")[0])
 
     # ------------------------------------------------------------ classifier stage
     def classify(self, crops: torch.Tensor) -> torch.Tensor:
@@ -132,6 +141,9 @@ class DetectClassifyPipeline:
     def _send(self, crops: torch.Tensor) -> list:
         """Non-blocking: the detector must be free to post the recv of the previous batch's results
         while these bytes move, or both sides block in send (rendezvous) and deadlock."""
+        self._handoffs += 1
+        if self._fail_at and self._handoffs == self._fail_at:
+            raise RuntimeError(f"injected xGMI hand-off failure (batch {self._handoffs})")
         n = torch.tensor([crops.shape[0]], dtype=torch.int64, device=self.device)
         works = [(dist.isend(n, self.peer, group=self.group), n)]
         self.bytes_sent += 8

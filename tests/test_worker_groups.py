@@ -77,3 +77,15 @@ def test_spatial_landcover_group_matches_single_process():
     ref = zoo.landcover("cpu", **kw)(torch.from_numpy(mosaic))[0][0].numpy()
     assert np.array_equal(cls, ref)
     assert stats["workers"][0]["xgmi_rx_bytes"] > 0
+
+
+def test_ensemble_pair_recovers_from_failed_xgmi_handoff(monkeypatch):
+    """A hand-off that fails before anything is on the wire fails the batch launch; the worker re-runs
+    the batch's items one by one and every task completes (survey §5.3 fault injection)."""
+    # CPU engines skip the warmup pass, so hand-off 1 is the first real batch
+    monkeypatch.setenv("AI4E_FAULT_INJECTION", "xgmi_fail_batch=1")
+    imgs = np.random.default_rng(8).integers(0, 256, (2, 128, 128, 3), dtype=np.uint8)
+    spec = ModelSpec("aiforearth_api_platform_amd.models.zoo:camera_trap_ensemble_pair", (128, 128, 3), 2, 5, ENS,
+                     False, (), ("http://127.0.0.1/v1/group/classify",), 2)
+    got, stats = _serve(spec, ["cpu", "cpu"], imgs, "/v1/group/classify")
+    assert all(g is not None and "animals" in g for g in got)
