@@ -284,8 +284,13 @@ class GpuWorker:
                     raise RuntimeError("injected item failure")
                 outs = self.engine.run_sync(self.buf[int(slots[i]): int(slots[i]) + 1])
                 rows[i] = np.frombuffer(encode_rows([o.numpy() for o in outs], 1), np.uint8)
-            except Exception:
+            except Exception as e:  # this item fails on its own
+                import sys
+                print(f"[ai4e worker {self.rank}] item (slot {int(slots[i])}) failed alone: {e!r}", file=sys.stderr,
+                      flush=True)
                 status[i] = P.IT_ERROR
+        if getattr(self.servable, "stages", 0):
+            self.conn.stage(bid, 0)
         self.conn.done(bid, status, rows.tobytes(), self.row_bytes, (t_recv, t_launch, time.monotonic(), 0, 0))
 
 
