@@ -64,7 +64,8 @@ PYBIND11_MODULE(_ai4e_core, m) {
   m.def("mono_now", &mono_now);
 
   py::class_<TaskStore, std::shared_ptr<TaskStore>>(m, "TaskStore")
-      .def(py::init<std::string>(), py::arg("journal_path") = "")
+      .def(py::init<std::string, size_t>(), py::arg("journal_path") = "", py::arg("nshards") = 8)
+      .def_property_readonly("nshards", &TaskStore::nshards)
       .def("upsert", &TaskStore::upsert, py::arg("task_id"), py::arg("status"), py::arg("backend_status"),
            py::arg("endpoint"), py::arg("body") = std::nullopt, py::arg("publish_to_grid") = false,
            py::call_guard<py::gil_scoped_release>())

@@ -17,6 +17,7 @@
 #pragma once
 
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <deque>
 #include <fstream>
@@ -78,21 +79,48 @@ struct TaskRec {
   uint32_t row = 0;
 };
 
-class TaskStore {
+// Append-only journal shared by the shards (its own lock; taken while a shard lock is held).
+struct Journal {
+  FILE* f = nullptr;
+  bool paused = false;
+  std::mutex mu;
+  void write(const std::string& line) {
+    std::lock_guard<std::mutex> g(mu);
+    if (f && !paused) std::fwrite(line.data(), 1, line.size(), f);
+  }
+};
+
+// Which shard owns a task id: its last character (hex digit value, else the byte) modulo the shard
+// count. Ids minted by the store carry their shard in that digit; upstream ids spread by it.
+inline size_t shard_of(const std::string& id, size_t nshards) {
+  if (id.empty() || nshards <= 1) return 0;
+  const unsigned char c = static_cast<unsigned char>(id.back());
+  const unsigned v = (c >= '0' && c <= '9') ? c - '0' : (c >= 'a' && c <= 'f') ? c - 'a' + 10
+                     : (c >= 'A' && c <= 'F') ? c - 'A' + 10 : c;
+  return v % nshards;
+}
+
+// One lock domain of the task store: records, per-(path, state) indexes, _ORIG bodies.
+class StoreShard {
  public:
-  explicit TaskStore(std::string journal_path = "") : journal_path_(std::move(journal_path)) {
+  StoreShard(size_t shard = 0, size_t nshards = 1, Journal* journal = nullptr)
+      : shard_(shard), nshards_(nshards), journal_(journal) {
     for (const char* s : {"created", "running", "completed", "failed"}) state_id(s);
-    recs_.reserve(1 << 20);  // a node's worth of in-flight + TTL-retained tasks without rehash stalls
-    if (!journal_path_.empty()) {
-      journal_ = std::fopen(journal_path_.c_str(), "a");
-      if (!journal_) throw std::runtime_error("cannot open journal " + journal_path_);
+    recs_.reserve((1 << 20) / nshards);  // a node's worth of in-flight + retained tasks without rehash stalls
+  }
+  StoreShard(const StoreShard&) = delete;
+  StoreShard& operator=(const StoreShard&) = delete;
+
+  // A fresh UUID whose last hex digit routes to this shard.
+  std::string mint_id() {
+    std::string id = uuid_.next();
+    if (nshards_ > 1) {
+      static const char* hex = "0123456789abcdef";
+      const unsigned d = static_cast<unsigned>(shard_) + static_cast<unsigned>(nshards_) * (uuid_rnd_++ & 1);
+      id.back() = hex[d & 15];
     }
+    return id;
   }
-  ~TaskStore() {
-    if (journal_) std::fclose(journal_);
-  }
-  TaskStore(const TaskStore&) = delete;
-  TaskStore& operator=(const TaskStore&) = delete;
 
   // CacheConnectorUpsert (CacheConnectorUpsert.cs:92-176): returns the serialized task (Body
   // nulled) and the body to publish (the original "{TaskId}_ORIG" body on a pipeline re-publish).
@@ -102,7 +130,7 @@ class TaskStore {
                                                             const std::optional<std::string>& body,
                                                             bool publish_to_grid) {
     std::lock_guard<std::mutex> g(mu_);
-    if (task_id.find_first_not_of(" \t\r\n") == std::string::npos) task_id = uuid_.next();
+    if (task_id.find_first_not_of(" \t\r\n") == std::string::npos) task_id = mint_id();
     const double wnow = wall_now(), mnow = mono_now();
     auto ins = recs_.try_emplace(task_id);
     TaskRec& r = ins.first->second;
@@ -141,7 +169,7 @@ class TaskStore {
     auto st = std::make_shared<const std::string>(status);
     auto ep = shared_endpoint(endpoint);
     for (size_t i = 0; i < n; ++i) {
-      std::string id = uuid_.next();
+      std::string id = mint_id();
       auto ins = recs_.try_emplace(id);
       if (!ins.second) {  // 2^-122 collision: draw again
         --i;
@@ -211,7 +239,8 @@ class TaskStore {
   // Finish a batch: attach results (row r of `res` to ids[r]) and set per-task final states.
   // ok[r] != 0 -> completed with `status_ok`, else failed with `status_fail`.
   void finish_many(const std::vector<std::string>& ids, const std::shared_ptr<const ResultBatch>& res,
-                   const std::vector<uint8_t>& ok, const std::string& status_ok, const std::string& status_fail) {
+                   const std::vector<uint8_t>& ok, const std::string& status_ok, const std::string& status_fail,
+                   const std::vector<uint32_t>* rows = nullptr) {
     std::lock_guard<std::mutex> g(mu_);
     const double wnow = wall_now(), mnow = mono_now();
     auto sok = std::make_shared<const std::string>(status_ok);
@@ -220,12 +249,12 @@ class TaskStore {
       auto it = recs_.find(ids[i]);
       if (it == recs_.end()) continue;
       TaskRec& r = it->second;
-      const bool good = ok.empty() || ok[i];
+      const bool good = ok.empty() || ok[rows ? (*rows)[i] : i];
       r.status = good ? sok : sfail;
       r.wall = wnow;
       if (good && res) {
         r.res = res;
-        r.row = static_cast<uint32_t>(i);
+        r.row = rows ? (*rows)[i] : static_cast<uint32_t>(i);
       }
       move_to(r, r.pidx, good ? ST_COMPLETED : ST_FAILED, wnow, mnow);
       journal_write(r, nullptr);
@@ -330,12 +359,12 @@ class TaskStore {
     return l ? l->n : 0;
   }
 
-  std::vector<std::string> zrange(const std::string& key, size_t limit) {
+  std::vector<std::pair<double, std::string>> zrange_scored(const std::string& key, size_t limit) {
     std::lock_guard<std::mutex> g(mu_);
-    std::vector<std::string> out;
+    std::vector<std::pair<double, std::string>> out;
     const IndexList* l = find_list(key);
     if (!l) return out;
-    for (TaskRec* r = l->head; r && out.size() < limit; r = r->next) out.push_back(r->id());
+    for (TaskRec* r = l->head; r && out.size() < limit; r = r->next) out.emplace_back(r->score, r->id());
     return out;
   }
 
@@ -354,21 +383,6 @@ class TaskStore {
     }
     std::sort(out.begin(), out.end());
     return out;
-  }
-
-  int64_t incrby(const std::string& key, int64_t delta) {
-    std::lock_guard<std::mutex> g(mu_);
-    return counters_[key] += delta;
-  }
-  std::optional<int64_t> get_counter(const std::string& key) {
-    std::lock_guard<std::mutex> g(mu_);
-    auto it = counters_.find(key);
-    if (it == counters_.end()) return std::nullopt;
-    return it->second;
-  }
-  std::map<std::string, int64_t> counters() {
-    std::lock_guard<std::mutex> g(mu_);
-    return {counters_.begin(), counters_.end()};
   }
 
   // Drop completed/failed records finished more than max_age_s ago, oldest first: the finished
@@ -399,11 +413,6 @@ class TaskStore {
     return recs_.size();
   }
 
-  void flush() {
-    std::lock_guard<std::mutex> g(mu_);
-    if (journal_) std::fflush(journal_);
-  }
-
   // Journal replay: each line is a full record image (+ optional _ORIG body). `parse` turns one
   // JSON line into fields (bindings supply the Python json module; the core stays JSON-free).
   struct JournalLine {
@@ -412,44 +421,29 @@ class TaskStore {
     double score = 0;
     std::optional<std::string> orig;
   };
-  template <class Parse>
-  size_t replay(const std::string& path, Parse parse) {
-    std::ifstream in(path);
-    if (!in) return 0;
-    std::string line;
-    size_t n = 0;
+  // Apply one journal line (replay; the journal is paused by the caller).
+  void replay_line(const JournalLine& jl, double mnow) {
     std::lock_guard<std::mutex> g(mu_);
-    FILE* saved = journal_;
-    journal_ = nullptr;  // do not re-journal while replaying
-    const double mnow = mono_now();
-    while (std::getline(in, line)) {
-      if (line.empty()) continue;
-      JournalLine jl;
-      if (!parse(line, jl)) continue;  // torn tail line after a crash
-      auto ins = recs_.try_emplace(jl.id);
-      TaskRec& r = ins.first->second;
-      if (ins.second) {
-        r.idp = &ins.first->first;
-        r.t_created = mnow;
-      }
-      r.endpoint = shared_endpoint(jl.endpoint);
-      r.status = std::make_shared<const std::string>(jl.status);
-      r.pub = jl.pub;
-      r.wall = jl.score;
-      const int sid = state_id(jl.backend_status);
-      PathIndex* p = path_index(absolute_path(jl.endpoint));
-      if (r.list) unlink(r);
-      r.pidx = p;
-      r.state = sid;
-      r.score = jl.score;
-      link_tail(r, &p->lists[sid]);
-      // finished records get a finish time, so TTL eviction applies to them too
-      r.t_finished = (sid == ST_COMPLETED || sid == ST_FAILED) ? mnow : 0;
-      if (jl.orig) orig_[r.id()] = *jl.orig;
-      ++n;
+    auto ins = recs_.try_emplace(jl.id);
+    TaskRec& r = ins.first->second;
+    if (ins.second) {
+      r.idp = &ins.first->first;
+      r.t_created = mnow;
     }
-    journal_ = saved;
-    return n;
+    r.endpoint = shared_endpoint(jl.endpoint);
+    r.status = std::make_shared<const std::string>(jl.status);
+    r.pub = jl.pub;
+    r.wall = jl.score;
+    const int sid = state_id(jl.backend_status);
+    PathIndex* p = path_index(absolute_path(jl.endpoint));
+    if (r.list) unlink(r);
+    r.pidx = p;
+    r.state = sid;
+    r.score = jl.score;
+    link_tail(r, &p->lists[sid]);
+    // finished records get a finish time, so TTL eviction applies to them too
+    r.t_finished = (sid == ST_COMPLETED || sid == ST_FAILED) ? mnow : 0;
+    if (jl.orig) orig_[r.id()] = *jl.orig;
   }
 
   const std::string& state_name(int s) const { return state_names_[s]; }
@@ -555,7 +549,7 @@ class TaskStore {
   }
 
   void journal_write(const TaskRec& r, const std::string* orig) {
-    if (!journal_) return;
+    if (!journal_ || !journal_->f) return;
     std::string line = serialize(r);
     line.pop_back();
     line += ",\"_score\":" + std::to_string(static_cast<int64_t>(r.score));
@@ -564,20 +558,233 @@ class TaskStore {
       json_escape_into(line, *orig);
     }
     line += "}\n";
-    std::fwrite(line.data(), 1, line.size(), journal_);
+    journal_->write(line);
   }
 
   std::mutex mu_;
+  size_t shard_, nshards_;
+  Journal* journal_;
   Uuid4 uuid_;
+  uint32_t uuid_rnd_ = 0;
   std::unordered_map<std::string, TaskRec> recs_;  // node-based: record addresses are stable
   std::unordered_map<std::string, std::shared_ptr<const std::string>> endpoints_;
   std::unordered_map<std::string, std::unique_ptr<PathIndex>> paths_;
   std::unordered_map<std::string, int> state_ids_;
   std::vector<std::string> state_names_;
   std::unordered_map<std::string, std::string> orig_;
+};
+
+// JournalLine is declared inside StoreShard's public section (replay parser output).
+using JournalLine = StoreShard::JournalLine;
+
+// TaskStore — the sharded store: ids route to one of S lock domains (shard_of), batches minted by
+// create_many live in one shard (round-robin per call), so a node's ingest, dispatcher and reader
+// threads contend on different locks; index queries (ZCARD, ZRANGE, KEYS) merge the shards.
+class TaskStore {
+ public:
+  using View = StoreShard::View;
+  using JournalLine = StoreShard::JournalLine;
+
+  explicit TaskStore(std::string journal_path = "", size_t nshards = 8) : nshards_(std::max<size_t>(1, nshards)) {
+    if (!journal_path.empty()) {
+      journal_.f = std::fopen(journal_path.c_str(), "a");
+      if (!journal_.f) throw std::runtime_error("cannot open journal " + journal_path);
+    }
+    for (size_t i = 0; i < nshards_; ++i) shards_.push_back(std::make_unique<StoreShard>(i, nshards_, &journal_));
+  }
+  ~TaskStore() {
+    if (journal_.f) std::fclose(journal_.f);
+  }
+  TaskStore(const TaskStore&) = delete;
+  TaskStore& operator=(const TaskStore&) = delete;
+
+  size_t nshards() const { return nshards_; }
+  StoreShard& shard_for(const std::string& id) { return *shards_[shard_of(id, nshards_)]; }
+
+  std::pair<std::string, std::optional<std::string>> upsert(std::string task_id, const std::string& status,
+                                                            const std::string& backend_status,
+                                                            const std::string& endpoint,
+                                                            const std::optional<std::string>& body,
+                                                            bool publish_to_grid) {
+    StoreShard& sh = task_id.find_first_not_of(" \t\r\n") == std::string::npos ? next_shard() : shard_for(task_id);
+    return sh.upsert(std::move(task_id), status, backend_status, endpoint, body, publish_to_grid);
+  }
+
+  std::vector<std::string> create_many(const std::string& endpoint, size_t n, const std::string& status,
+                                       const std::string& trace = std::string()) {
+    return next_shard().create_many(endpoint, n, status, trace);
+  }
+
+  size_t transition_many(const std::vector<std::string>& ids, const std::string& backend_status,
+                         const std::string& status) {
+    size_t n = 0;
+    for_groups(ids, [&](StoreShard& sh, const std::vector<std::string>& g, const std::vector<uint32_t>*) {
+      n += sh.transition_many(g, backend_status, status);
+    });
+    return n;
+  }
+
+  size_t retarget_many(const std::vector<std::string>& ids, const std::string& endpoint, const std::string& status) {
+    size_t n = 0;
+    for_groups(ids, [&](StoreShard& sh, const std::vector<std::string>& g, const std::vector<uint32_t>*) {
+      n += sh.retarget_many(g, endpoint, status);
+    });
+    return n;
+  }
+
+  void finish_many(const std::vector<std::string>& ids, const std::shared_ptr<const ResultBatch>& res,
+                   const std::vector<uint8_t>& ok, const std::string& status_ok, const std::string& status_fail) {
+    for_groups(ids, [&](StoreShard& sh, const std::vector<std::string>& g, const std::vector<uint32_t>* rows) {
+      sh.finish_many(g, res, ok, status_ok, status_fail, rows);
+    });
+  }
+
+  bool set_status_text(const std::string& id, const std::string& status) {
+    return shard_for(id).set_status_text(id, status);
+  }
+  bool set_trace(const std::string& id, const std::string& trace) { return shard_for(id).set_trace(id, trace); }
+  std::optional<std::string> get(const std::string& id) { return shard_for(id).get(id); }
+  std::optional<StoreShard::View> view(const std::string& id) { return shard_for(id).view(id); }
+  std::optional<std::string> get_orig_body(const std::string& id) { return shard_for(id).get_orig_body(id); }
+
+  std::vector<double> latencies(const std::vector<std::string>& ids, bool to_running) {
+    std::vector<double> out;
+    out.reserve(ids.size());
+    for_groups(ids, [&](StoreShard& sh, const std::vector<std::string>& g, const std::vector<uint32_t>*) {
+      auto v = sh.latencies(g, to_running);
+      out.insert(out.end(), v.begin(), v.end());
+    });
+    return out;
+  }
+  std::vector<double> latencies_window(const std::string& path, double t0, double t1) {
+    std::vector<double> out;
+    for (auto& sh : shards_) {
+      auto v = sh->latencies_window(path, t0, t1);
+      out.insert(out.end(), v.begin(), v.end());
+    }
+    return out;
+  }
+
+  size_t zcard(const std::string& key) {
+    size_t n = 0;
+    for (auto& sh : shards_) n += sh->zcard(key);
+    return n;
+  }
+  // ZRANGE over the shards: merged by score (the wall-clock second of the last mutation).
+  std::vector<std::string> zrange(const std::string& key, size_t limit) {
+    std::vector<std::pair<double, std::string>> all;
+    for (auto& sh : shards_) {
+      auto v = sh->zrange_scored(key, limit);
+      all.insert(all.end(), std::make_move_iterator(v.begin()), std::make_move_iterator(v.end()));
+    }
+    std::stable_sort(all.begin(), all.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+    std::vector<std::string> out;
+    for (auto& e : all) {
+      if (out.size() >= limit) break;
+      out.push_back(std::move(e.second));
+    }
+    return out;
+  }
+  std::vector<std::string> keys_with_suffix(const std::string& suffix) {
+    std::vector<std::string> out;
+    for (auto& sh : shards_) {
+      auto v = sh->keys_with_suffix(suffix);
+      out.insert(out.end(), v.begin(), v.end());
+    }
+    std::sort(out.begin(), out.end());
+    out.erase(std::unique(out.begin(), out.end()), out.end());
+    return out;
+  }
+
+  int64_t incrby(const std::string& key, int64_t delta) {
+    std::lock_guard<std::mutex> g(cmu_);
+    return counters_[key] += delta;
+  }
+  std::optional<int64_t> get_counter(const std::string& key) {
+    std::lock_guard<std::mutex> g(cmu_);
+    auto it = counters_.find(key);
+    if (it == counters_.end()) return std::nullopt;
+    return it->second;
+  }
+  std::map<std::string, int64_t> counters() {
+    std::lock_guard<std::mutex> g(cmu_);
+    return {counters_.begin(), counters_.end()};
+  }
+
+  size_t evict_finished(double max_age_s, size_t max_finished = SIZE_MAX) {
+    size_t n = 0;
+    const size_t per = max_finished == SIZE_MAX ? SIZE_MAX : (max_finished + nshards_ - 1) / nshards_;
+    for (auto& sh : shards_) n += sh->evict_finished(max_age_s, per);
+    return n;
+  }
+  size_t size() {
+    size_t n = 0;
+    for (auto& sh : shards_) n += sh->size();
+    return n;
+  }
+  void flush() {
+    std::lock_guard<std::mutex> g(journal_.mu);
+    if (journal_.f) std::fflush(journal_.f);
+  }
+
+  template <class Parse>
+  size_t replay(const std::string& path, Parse parse) {
+    std::ifstream in(path);
+    if (!in) return 0;
+    {
+      std::lock_guard<std::mutex> g(journal_.mu);
+      journal_.paused = true;  // do not re-journal while replaying
+    }
+    std::string line;
+    size_t n = 0;
+    const double mnow = mono_now();
+    while (std::getline(in, line)) {
+      if (line.empty()) continue;
+      JournalLine jl;
+      if (!parse(line, jl)) continue;  // torn tail line after a crash
+      shard_for(jl.id).replay_line(jl, mnow);
+      ++n;
+    }
+    std::lock_guard<std::mutex> g(journal_.mu);
+    journal_.paused = false;
+    return n;
+  }
+
+ private:
+  StoreShard& next_shard() { return *shards_[rr_.fetch_add(1, std::memory_order_relaxed) % nshards_]; }
+
+  // Calls fn(shard, ids of that shard, original positions or null) once per shard touched, in order.
+  template <class Fn>
+  void for_groups(const std::vector<std::string>& ids, Fn fn) {
+    if (ids.empty()) return;
+    const size_t s0 = shard_of(ids[0], nshards_);
+    bool one = true;
+    for (const auto& id : ids)
+      if (shard_of(id, nshards_) != s0) {
+        one = false;
+        break;
+      }
+    if (one) {  // the common case: a batch minted by one create_many call
+      fn(*shards_[s0], ids, nullptr);
+      return;
+    }
+    std::vector<std::vector<std::string>> g(nshards_);
+    std::vector<std::vector<uint32_t>> pos(nshards_);
+    for (size_t i = 0; i < ids.size(); ++i) {
+      const size_t s = shard_of(ids[i], nshards_);
+      g[s].push_back(ids[i]);
+      pos[s].push_back(static_cast<uint32_t>(i));
+    }
+    for (size_t s = 0; s < nshards_; ++s)
+      if (!g[s].empty()) fn(*shards_[s], g[s], &pos[s]);
+  }
+
+  size_t nshards_;
+  Journal journal_;
+  std::vector<std::unique_ptr<StoreShard>> shards_;
+  std::atomic<size_t> rr_{0};
+  std::mutex cmu_;
   std::unordered_map<std::string, int64_t> counters_;
-  std::string journal_path_;
-  FILE* journal_ = nullptr;
 };
 
 }  // namespace ai4e

