@@ -327,7 +327,7 @@ def follower_main(device: str, spec: ModelSpec, group_rank: int, group_size: int
 
 def worker_main(conn, rank: int, device: str, spec: ModelSpec, shm_name: str, nslots: int, hb_interval: float,
                 partition: Optional[Tuple[int, int]] = None, untrack: bool = False, local_ring=None,
-                group_port: int = 0) -> None:
+                group_port: int = 0, ready_event: Optional[threading.Event] = None) -> None:
     """Entry point of a spawned worker process (and of ``torchrun`` worker ranks, which pass their
     ingest partition's ``local_ring`` and ``untrack=True``). With ``spec.group_size > 1`` this is the
     leader of a worker group (rendezvous on ``group_port``)."""
@@ -343,6 +343,8 @@ def worker_main(conn, rank: int, device: str, spec: ModelSpec, shm_name: str, ns
         local_ring = native.SlotRing(partition[1], partition[0])
     fc = conn if isinstance(conn, P.FrameConn) else P.FrameConn(conn)
     w = GpuWorker(fc, rank, device, spec, buf, local_ring=local_ring, hb_interval=hb_interval, group_kwargs=group_kwargs)
+    if ready_event is not None:  # graphs are captured: the hosting process may use the device again
+        ready_event.set()
     try:
         w.serve(pinned)
     finally:

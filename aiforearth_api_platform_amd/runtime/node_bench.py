@@ -230,9 +230,14 @@ def run_node_bench(args, spec, path: str, metric: str, unit: str = "images/s", c
             return s
 
         client = Client(ring_buf, alloc, fc.submit, B, rank)
+        ready = threading.Event()
         wth = threading.Thread(target=worker_main, args=(fc, rank, str(device), spec, info["shm"], info["nslots"], hb),
-                               kwargs={"untrack": True, "local_ring": local_ring}, daemon=True)
+                               kwargs={"untrack": True, "local_ring": local_ring, "ready_event": ready}, daemon=True)
         wth.start()
+        # the worker thread captures HIP graphs in global capture mode: this thread must not touch the device
+        # (synchronize, RCCL barrier) until the capture is over
+        if not ready.wait(1800):
+            raise SystemExit(f"rank {rank}: GPU worker did not come up")
 
     def wait_images(target: int) -> None:
         while pool.images < target:
