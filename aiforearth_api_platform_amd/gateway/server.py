@@ -52,6 +52,7 @@ class Route:
     max_concurrent: Optional[int] = None
     content_types: Optional[List[str]] = None
     max_content_length: Optional[int] = None
+    inline: bool = False                     # sync callable cheap enough to run on the event loop (no thread hop)
     inflight: int = field(default=0, repr=False)
 
     def target_path(self, path: str) -> str:
@@ -88,7 +89,7 @@ class RouteTable:
                 be = backends[be.split(":", 1)[1]]
             t.add(Route(prefix=r["prefix"], mode=r.get("mode", "async"), backend=be, rewrite=r.get("rewrite"),
                         max_concurrent=r.get("max_concurrent"), content_types=r.get("content_types"),
-                        max_content_length=r.get("max_content_length")))
+                        max_content_length=r.get("max_content_length"), inline=bool(r.get("inline", False))))
         return t
 
 
@@ -329,7 +330,8 @@ class Gateway:
                                                                    "application/octet-stream"}) as r:
                 return web.Response(status=r.status, body=await r.read(), content_type=r.content_type)
         if callable(be):
-            res = await loop.run_in_executor(None, be, "", body, dict(request.headers))
+            hdrs = dict(request.headers)
+            res = be("", body, hdrs) if route.inline else await loop.run_in_executor(None, be, "", body, hdrs)
             code, payload = (res if isinstance(res, tuple) else (200, res))
             if isinstance(payload, (dict, list)):
                 return web.json_response(payload, status=code)

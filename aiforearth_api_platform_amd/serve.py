@@ -91,7 +91,7 @@ def build_platform(doc: Dict[str, Any], cfg: Config):
             be = _load(be.split(":", 1)[1])
         route = table.add(Route(prefix=r["prefix"], mode=r.get("mode", "async"), backend=be, rewrite=r.get("rewrite"),
                                 max_concurrent=r.get("max_concurrent"), content_types=r.get("content_types"),
-                                max_content_length=r.get("max_content_length")))
+                                max_content_length=r.get("max_content_length"), inline=bool(r.get("inline", False))))
         # async route to a generic backend: a queue dispatcher delivers each task (BackendQueueProcessor)
         if route.mode == "async" and not hasattr(be, "submit") and be is not None:
             target = base_url + (route.rewrite or route.prefix)

@@ -4,7 +4,8 @@
 * ``reference``: a Flask app with the ``APIService.api_sync_func`` decorator (the reference's
   container runtime, ``APIs/1.0/base-py/ai4e_service.py``), served by werkzeug's threaded server.
 
-Drives each with an asyncio HTTP client at fixed concurrency; reports req/s and p50/p99 latency.
+Each server runs in its own process (its own GIL, like a deployed service); the asyncio HTTP client
+drives it at fixed concurrency from this process and reports req/s and p50/p99 latency.
 
     python bench/echo_bench.py [--requests 5000 --concurrency 64]
 """
@@ -28,7 +29,7 @@ def _port():
     return p
 
 
-def start_platform(port):
+def start_platform(port, ready=None):
     from aiohttp import web
 
     from aiforearth_api_platform_amd.config import Config
@@ -36,22 +37,17 @@ def start_platform(port):
     from aiforearth_api_platform_amd.gateway.server import Gateway, Route, RouteTable
     from aiforearth_api_platform_amd.models.toy import echo
 
+    from aiforearth_api_platform_amd.runtime.hostperf import tune_gc
+
     t = RouteTable()
-    t.add(Route("/v1/echo", "sync", echo))
+    t.add(Route("/v1/echo", "sync", echo, inline=True))
     gw = Gateway(ControlPlane(Config.load(env={})), t)
-
-    def run():
-        loop = asyncio.new_event_loop()
-        asyncio.set_event_loop(loop)
-        runner = web.AppRunner(gw.app)
-        loop.run_until_complete(runner.setup())
-        loop.run_until_complete(web.TCPSite(runner, "127.0.0.1", port).start())
-        loop.run_forever()
-
-    threading.Thread(target=run, daemon=True).start()
+    tune_gc()
+    web.run_app(gw.app, host="127.0.0.1", port=port, access_log=None, print=None)
 
 
 def start_reference(port):
+    os.environ["API_PREFIX"] = "/v1"
     from flask import Flask, request
 
     from aiforearth_api_platform_amd.api import APIService, InProcTaskClient, TaskManager
@@ -64,7 +60,7 @@ def start_reference(port):
     def echo(*args, **kwargs):
         return request.get_data()
 
-    threading.Thread(target=lambda: app.run("127.0.0.1", port, threaded=True), daemon=True).start()
+    app.run("127.0.0.1", port, threaded=True)
 
 
 async def drive(url, n, conc):
@@ -103,12 +99,14 @@ def main():
     ap.add_argument("--concurrency", type=int, default=64)
     ap.add_argument("--json-out", default="")
     a = ap.parse_args()
+    import multiprocessing as mp
+
     pp, rp = _port(), _port()
-    start_platform(pp)
-    os.environ["API_PREFIX"] = "/v1"
-    from aiforearth_api_platform_amd import config as cfgmod
-    cfgmod.set_config(cfgmod.Config.load())
-    start_reference(rp)
+    ctx = mp.get_context("spawn")
+    procs = [ctx.Process(target=start_platform, args=(pp,), daemon=True),
+             ctx.Process(target=start_reference, args=(rp,), daemon=True)]
+    for p in procs:
+        p.start()
     res = {}
     for name, url in (("platform", f"http://127.0.0.1:{pp}/v1/echo"), ("reference_style", f"http://127.0.0.1:{rp}/v1/echo")):
         rps, p50, p99 = asyncio.run(drive(url, a.requests, a.concurrency))
@@ -116,6 +114,8 @@ def main():
     out = {"metric": "echo API req/s (CPU, sync)", "value": res["platform"]["req_per_s"], "unit": "req/s",
            "vs_reference_style": round(res["platform"]["req_per_s"] / res["reference_style"]["req_per_s"], 3),
            "results": res, "config": {"requests": a.requests, "concurrency": a.concurrency}}
+    for p in procs:
+        p.terminate()
     print(json.dumps(out), flush=True)
     if a.json_out:
         with open(a.json_out, "w") as f:
