@@ -252,6 +252,9 @@ class Gateway:
             return rej
         route.inflight += 1
         try:
+            if (route.mode == "async" and request.content_type == BATCH_CONTENT_TYPE and request.content_length
+                    and hasattr(route.backend, "begin_stream_batch")):
+                return await self._async_stream_batch(route, request)
             body = await request.read()
             if route.mode == "async":
                 return await self._async(route, request, body)
@@ -266,6 +269,27 @@ class Gateway:
         if isinstance(e, PayloadError):
             return web.json_response({"message": str(e)}, status=getattr(e, "status", 400))
         return None
+
+    async def _async_stream_batch(self, route: Route, request):
+        """Binary batch ingest: the body streams chunk by chunk into ring slots (no buffered copy)."""
+        b3 = b3_from_headers(request.headers)
+        sb = None
+        try:
+            sb = route.backend.begin_stream_batch(request.content_length, b3_pack(b3))
+            if not sb.try_alloc():
+                await asyncio.get_running_loop().run_in_executor(None, sb.alloc)
+            async for chunk in request.content.iter_any():
+                sb.feed(chunk)
+            ids = sb.finish()
+        except Exception as e:
+            if sb is not None:
+                sb.abort()
+            rej = self._payload_error(e)
+            if rej is not None:
+                return rej
+            self.cp.log.log_error(f"{TASK_INSERT_FAILED} {e}", request.path)
+            return web.Response(status=500, text=TASK_INSERT_FAILED)
+        return web.json_response({"TaskIds": ids}, headers=b3)
 
     async def _async(self, route: Route, request, body: bytes):
         loop = asyncio.get_running_loop()

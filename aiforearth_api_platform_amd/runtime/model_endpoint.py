@@ -88,6 +88,64 @@ def decode_image(body: bytes, content_type: str, shape: Tuple[int, int, int]) ->
     return arr
 
 
+class StreamedBatch:
+    """Ring slots of one streamed batch request; bytes land in slot order (one copy per chunk piece)."""
+
+    def __init__(self, ep: "ModelEndpoint", n: int, item: int, trace: str):
+        self.ep, self.n, self.item, self.trace = ep, n, item, trace
+        self.slots: List[int] = []
+        self.pos = 0
+        self._flat = ep.ring.buf.view(-1).numpy()
+
+    def try_alloc(self) -> bool:
+        """Non-blocking slot allocation (the event loop's fast path)."""
+        s = self.ep.ring.slots.alloc(self.n, 0.0) if hasattr(self.ep.ring, "slots") else None
+        if s:
+            self._set(s)
+        return bool(s)
+
+    def alloc(self, timeout: float = 60.0) -> None:
+        self._set(self.ep.ring.alloc(self.n, timeout=timeout))
+
+    def _set(self, slots: List[int]) -> None:
+        self.slots = list(slots)
+        # contiguous slot runs: (first logical byte, ring byte offset, bytes)
+        self.runs, i = [], 0
+        while i < self.n:
+            j = i + 1
+            while j < self.n and self.slots[j] == self.slots[j - 1] + 1:
+                j += 1
+            self.runs.append((i * self.item, self.slots[i] * self.item, (j - i) * self.item))
+            i = j
+        self._run = 0
+
+    def feed(self, chunk: bytes) -> None:
+        src = np.frombuffer(chunk, np.uint8)
+        off, m = 0, src.shape[0]
+        if self.pos + m > self.n * self.item:
+            raise PayloadError("batch payload longer than its Content-Length")
+        while off < m:
+            lo, ring_off, nb = self.runs[self._run]
+            k = min(m - off, lo + nb - self.pos)
+            dst = ring_off + self.pos - lo
+            self._flat[dst:dst + k] = src[off:off + k]
+            off += k
+            self.pos += k
+            if self.pos == lo + nb:
+                self._run += 1
+
+    def finish(self) -> List[str]:
+        if self.pos != self.n * self.item:
+            raise PayloadError(f"batch payload truncated ({self.pos} of {self.n * self.item} bytes)")
+        slots, self.slots = self.slots, []
+        return self.ep._enqueue(slots, self.trace)
+
+    def abort(self) -> None:
+        if self.slots:
+            self.ep.ring.free(self.slots)
+            self.slots = []
+
+
 class ModelEndpoint:
     def __init__(self, control_plane, path: str, engine=None, ring=None, worker=None,
                  decode: Optional[Callable[[bytes, str], np.ndarray]] = None, base_url: str = "http://127.0.0.1",
@@ -200,6 +258,17 @@ class ModelEndpoint:
             raise PayloadError(f"batch payload must be a multiple of {item} bytes (uint8 {self.item_shape})")
         arr = np.frombuffer(body, dtype=np.uint8).reshape(-1, *self.item_shape)
         return self.submit_many(arr, trace)
+
+    def begin_stream_batch(self, nbytes: int, trace: str = "") -> "StreamedBatch":
+        """Binary batch ingest without buffering the body: ``nbytes`` (a multiple of the item size) are
+        fed chunk by chunk straight into ring slots allocated up front, then enqueued (``finish``)."""
+        item = int(np.prod(self.item_shape))
+        if nbytes <= 0 or nbytes % item:
+            raise PayloadError(f"batch payload must be a multiple of {item} bytes (uint8 {self.item_shape})")
+        n = nbytes // item
+        if n > self.ring.nslots:
+            raise PayloadError(f"batch of {n} items exceeds the payload ring ({self.ring.nslots} slots)", 413)
+        return StreamedBatch(self, n, item, trace)
 
     def _orig(self, body: bytes, content_type: str) -> Optional[str]:
         if not self.journal_cap or len(body) > self.journal_cap:

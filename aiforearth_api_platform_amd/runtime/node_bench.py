@@ -49,14 +49,15 @@ class Client:
 
 
 def http_phase(cp, pool, seconds: float, batch: int, item_shape, path: str) -> dict:
-    """REST ingest on this node: aiohttp gateway + binary batch route, then single-image requests."""
+    """REST ingest on this node: aiohttp gateway (this process) + binary batch route (streamed into the
+    payload ring), then single-image requests; the clients run in separate processes."""
     import asyncio
 
-    import aiohttp
     from aiohttp import web
 
     from ..gateway.server import BATCH_CONTENT_TYPE, Gateway, Route, RouteTable
     from ..utils.metrics import percentile
+    from .http_load import run_clients
     from .model_endpoint import ModelEndpoint
 
     ep = ModelEndpoint(cp, path, worker=pool)
@@ -87,37 +88,6 @@ def http_phase(cp, pool, seconds: float, batch: int, item_shape, path: str) -> d
     img = rng.integers(0, 256, tuple(item_shape), dtype=np.uint8)
     batch_body = np.broadcast_to(img, (batch, *img.shape)).tobytes()
 
-    async def batches(conc: int):
-        ids, n = [], 0
-        t_end = time.perf_counter() + seconds / 2
-
-        async def one(s):
-            nonlocal n
-            while time.perf_counter() < t_end:
-                async with s.post(url, data=batch_body, headers={"Content-Type": BATCH_CONTENT_TYPE}) as r:
-                    ids.extend((await r.json())["TaskIds"])
-                    n += batch
-
-        async with aiohttp.ClientSession() as s:
-            t0 = time.perf_counter()
-            await asyncio.gather(*(one(s) for _ in range(conc)))
-        return ids, n, t0
-
-    async def singles(conc: int):
-        ids = []
-        t_end = time.perf_counter() + seconds / 2
-        body = img.tobytes()
-
-        async def one(s):
-            while time.perf_counter() < t_end:
-                async with s.post(url, data=body, headers={"Content-Type": "application/octet-stream"}) as r:
-                    ids.append((await r.json())["TaskId"])
-
-        async with aiohttp.ClientSession() as s:
-            t0 = time.perf_counter()
-            await asyncio.gather(*(one(s) for _ in range(conc)))
-        return ids, t0
-
     def wait_done(ids, timeout=60):
         deadline = time.time() + timeout
         while time.time() < deadline:
@@ -127,19 +97,20 @@ def http_phase(cp, pool, seconds: float, batch: int, item_shape, path: str) -> d
             time.sleep(0.01)
         return sorted(cp.store.latencies(ids))
 
+    # load generators in their own processes (the server keeps this interpreter to itself)
     out = {}
-    ids, n, t0 = asyncio.run(batches(4))
-    lat = wait_done(ids)
-    dt = time.perf_counter() - t0
-    out["batch_route"] = {"images": n, "images_per_s": round(n / dt, 1), "request_images": batch, "connections": 4,
-                          "p50_task_latency_ms": round(percentile(lat, 50) * 1e3, 3),
-                          "p99_task_latency_ms": round(percentile(lat, 99) * 1e3, 3)}
-    ids, t0 = asyncio.run(singles(64))
-    lat = wait_done(ids)
-    dt = time.perf_counter() - t0
-    out["single_image_route"] = {"requests": len(ids), "images_per_s": round(len(ids) / dt, 1), "connections": 64,
-                                 "p50_task_latency_ms": round(percentile(lat, 50) * 1e3, 3),
-                                 "p99_task_latency_ms": round(percentile(lat, 99) * 1e3, 3)}
+    for name, body, ctype, is_batch, procs, conc in (
+            ("batch_route", batch_body, BATCH_CONTENT_TYPE, True, 2, 2),
+            ("single_image_route", img.tobytes(), "application/octet-stream", False, 3, 32)):
+        ids, t0, _, errors = run_clients(url, seconds / 2, conc, body, ctype, is_batch, procs=procs)
+        lat = wait_done(ids)
+        dt = time.time() - t0
+        out[name] = {"images": len(ids), "images_per_s": round(len(ids) / dt, 1), "connections": procs * conc,
+                     "client_processes": procs, "errors": errors,
+                     "p50_task_latency_ms": round(percentile(lat, 50) * 1e3, 3),
+                     "p99_task_latency_ms": round(percentile(lat, 99) * 1e3, 3)}
+        if is_batch:
+            out[name]["request_images"] = batch
     box["loop"].call_soon_threadsafe(box["loop"].stop)
     th.join(10)
     return out

@@ -80,7 +80,7 @@ def main():
         raise SystemExit(f"unknown model {which}")
     table = {}
     for key, (pc, n, h, w, res) in shapes.items():
-        times = {c: t for c in (1, 2, 3, 4, 5, 6, 7, 8) if (t := time_cfg(pc, n, h, w, res, c, dev)) is not None}
+        times = {c: t for c in (1, 2, 3, 4, 5, 6, 7, 8, 9) if (t := time_cfg(pc, n, h, w, res, c, dev)) is not None}
         best = min(times, key=times.get)
         table[key] = best
         print(json.dumps({"key": key, "us": {k: round(v, 1) for k, v in times.items()}, "best": best}), flush=True)

@@ -42,6 +42,7 @@ using ai4e_conv::glds16;
 using ai4e_conv::swz;
 using ai4e_conv::TapWalk;
 using ai4e_conv::wait_vmcnt;
+using ai4e_conv::wait_vmcnt_n;
 
 // Source of the zero 16-B chunks the DMA gather reads for padding / out-of-range taps.
 __device__ __attribute__((aligned(64))) uint16_t g_zero_chunk[32];
@@ -480,9 +481,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC > 2 ? O
 // ============================================================================================
 constexpr int U_ROWS = 128, U_BYTES = U_ROWS * 128;
 
-template <int GATHER>
+// BM = 192 (tile config 9) keeps the schedule with 96-pixel wave groups: u0 holds pixel rows
+// {wr*96 + 0..63} (still 128 unit rows), u3 only {wr*96 + 64..95} (64 rows: one DMA per lane, two
+// fragments, 8-MFMA phases 3 and 4). A 14x14 layer of 250 images (M = 49000) is then 256 tiles —
+// one per CU — instead of 192 256-row tiles that leave a quarter of the chip idle.
+template <int GATHER, int BM>
 __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) {
   static_assert(GATHER == GATHER_TAP || GATHER == GATHER_POINTWISE, "256 tile needs C % 64 == 0");
+  static_assert(BM == 256 || BM == 192, "wave groups of 128 or 96 pixels");
+  constexpr int WROWS = BM / 2;    // pixels per wave group
+  constexpr int X1 = WROWS - 64;   // u3 rows per wave group
+  constexpr int L3 = X1 / 32;      // DMAs per lane for u3
+  constexpr int MF1 = X1 / 16;     // u3 fragments per wave
+  constexpr int MFR = 4 + MF1;     // accumulator rows
   __shared__ __attribute__((aligned(1024))) uint8_t smem[2 * 4 * U_BYTES];  // the only LDS object
 
   const int tid = threadIdx.x;
@@ -493,13 +504,13 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
   const int t = xcd_remap(blockIdx.x, gridDim.x);
   const int mt = t / p.ntiles_n;
   const int nt = t - mt * p.ntiles_n;
-  const int m0 = mt * 256;
+  const int m0 = mt * BM;
   const int n0 = nt * 256;
   const int nk = p.Kpad / 64;
   const uint32_t sbase = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(smem));
 
-  // ---- DMA sources. Lane writes unit row R_i = 16*wave + 8*i + (lane>>3), physical 16-B chunk
-  //      lane&7, holding logical chunk q_i = (lane&7) ^ ((R_i >> 1) & 7).
+  // ---- DMA sources. Lane writes unit row R_i = 16*wave + 8*i + (lane>>3) (u3 of BM 192: 8*wave +
+  //      (lane>>3)), physical 16-B chunk lane&7, holding logical chunk q_i = (lane&7) ^ ((R_i >> 1) & 7).
   const int OHW = p.OH * p.OW;
   const uint16_t* xrow[2][2];  // [i][xq] pixel row pointer (+ 8*q_i), nullptr past M
   int ih0[2][2], iw0[2][2];
@@ -510,8 +521,11 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
     const int q = (lane & 7) ^ ((R >> 1) & 7);
 #pragma unroll
     for (int xq = 0; xq < 2; ++xq) {
-      const int m = m0 + (R >> 6) * 128 + (R & 63) + 64 * xq;
-      if (m < p.M) {
+      const int RG = xq ? X1 : 64;  // unit rows per wave group
+      const int Rx = (xq && L3 == 1) ? 8 * wave + (lane >> 3) : R;
+      const int qx = (lane & 7) ^ ((Rx >> 1) & 7);
+      const int m = m0 + (Rx / RG) * WROWS + (xq ? 64 : 0) + (Rx % RG);
+      if (m < p.M && !(xq && L3 == 1 && i == 1)) {
         const int img = m / OHW;
         const int rem = m - img * OHW;
         const int oh = rem / p.OW;
@@ -519,7 +533,7 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
         ih0[i][xq] = oh * p.stride - p.pad;
         iw0[i][xq] = ow * p.stride - p.pad;
         xrow[i][xq] = p.x + static_cast<long>(img) * p.H * p.W * p.ldx + p.xcoff +
-                      (static_cast<long>(ih0[i][xq]) * p.W + iw0[i][xq]) * p.ldx + 8 * q;
+                      (static_cast<long>(ih0[i][xq]) * p.W + iw0[i][xq]) * p.ldx + 8 * qx;
       } else {
         ih0[i][xq] = -(1 << 28);
         iw0[i][xq] = 0;
@@ -535,6 +549,31 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
 
   // stage unit u of K tile kt into buffer kt&1 (2 DMAs per lane); X units must be staged in tile order
 
+  // X unit xq (compile-time, so each tap walk stays in registers) of the K tile at k0
+  auto stage_x = [&](auto XQ, uint32_t ubase, int k0) {
+    constexpr int xq = decltype(XQ)::value;
+    constexpr int nl = xq ? L3 : 2;
+    const uint32_t xb = (xq && L3 == 1) ? ubase - (8 * wave) * 128 : ubase;
+    if constexpr (GATHER == GATHER_POINTWISE) {
+      const bool kok = k0 < p.C;
+#pragma unroll
+      for (int i = 0; i < nl; ++i) {
+        const void* src = (kok && xrow[i][xq] != nullptr) ? static_cast<const void*>(xrow[i][xq] + k0) : zero;
+        glds16(src, xb + i * 8 * 128);
+      }
+    } else {
+      // a 64-wide K tile lies in one tap (C % 64 == 0): wave-uniform walk
+      TapWalk& tw = wx[xq];
+      const bool tok = tw.kh < p.KH;
+#pragma unroll
+      for (int i = 0; i < nl; ++i) {
+        const bool ok = tok && static_cast<unsigned>(ih0[i][xq] + tw.kh) < static_cast<unsigned>(p.H) &&
+                        static_cast<unsigned>(iw0[i][xq] + tw.kw) < static_cast<unsigned>(p.W);
+        glds16(ok ? static_cast<const void*>(xrow[i][xq] + tw.off) : zero, xb + i * 8 * 128);
+      }
+      tw.next(64, p.C, p.KW, p.ldx, rowjump);
+    }
+  };
   auto stage = [&](int kt, int u) {
     const uint32_t ubase = sbase + ((kt & 1) * 4 + u) * U_BYTES + (16 * wave) * 128;
     const int k0 = kt * 64;
@@ -542,27 +581,10 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
       const long roff = (u == 2 ? 32L * p.Kpad : 0L) + k0;
 #pragma unroll
       for (int i = 0; i < 2; ++i) glds16(wrow[i] + roff, ubase + i * 8 * 128);
+    } else if (u == 3) {
+      stage_x(std::integral_constant<int, 1>{}, ubase, k0);
     } else {
-      const int xq = u == 3 ? 1 : 0;
-      if constexpr (GATHER == GATHER_POINTWISE) {
-        const bool kok = k0 < p.C;
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          const void* src = (kok && xrow[i][xq] != nullptr) ? static_cast<const void*>(xrow[i][xq] + k0) : zero;
-          glds16(src, ubase + i * 8 * 128);
-        }
-      } else {
-        // a 64-wide K tile lies in one tap (C % 64 == 0): wave-uniform walk
-        TapWalk& tw = wx[xq];
-        const bool tok = tw.kh < p.KH;
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          const bool ok = tok && static_cast<unsigned>(ih0[i][xq] + tw.kh) < static_cast<unsigned>(p.H) &&
-                          static_cast<unsigned>(iw0[i][xq] + tw.kw) < static_cast<unsigned>(p.W);
-          glds16(ok ? static_cast<const void*>(xrow[i][xq] + tw.off) : zero, ubase + i * 8 * 128);
-        }
-        tw.next(64, p.C, p.KW, p.ldx, rowjump);
-      }
+      stage_x(std::integral_constant<int, 0>{}, ubase, k0);
     }
   };
   // phase g stages unit (g-3) mod 4 of tile (g-3) div 4 + 2 (g may be <= 0: the prologue)
@@ -572,19 +594,13 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
     const int kt = phase_tile(g);
     if (kt < nk) stage(kt, phase_unit(g));
   };
-  auto loads_of = [&](int g) { return phase_tile(g) < nk ? 2 : 0; };
+  auto loads_of = [&](int g) { return phase_tile(g) < nk ? (phase_unit(g) == 3 ? L3 : 2) : 0; };
   // wait until this wave's DMAs of phases <= g-3 have landed
-  auto wait_phase = [&](int g) {
-    const int n = loads_of(g - 2) + loads_of(g - 1) + loads_of(g);
-    if (n >= 6) wait_vmcnt<6>();
-    else if (n == 4) wait_vmcnt<4>();
-    else if (n == 2) wait_vmcnt<2>();
-    else wait_vmcnt<0>();
-  };
+  auto wait_phase = [&](int g) { wait_vmcnt_n(loads_of(g - 2) + loads_of(g - 1) + loads_of(g)); };
 
-  f32x4_t acc[8][4];
+  f32x4_t acc[MFR][4];
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < MFR; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
@@ -597,8 +613,8 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
 
 #define K256_READ_X(XQ, KT)                                                                        \
   {                                                                                                \
-    const uint8_t* b_ = smem + (((KT) & 1) * 4 + ((XQ) ? 3 : 0)) * U_BYTES + (wr * 64) * 128;       \
-    _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                                \
+    const uint8_t* b_ = smem + (((KT) & 1) * 4 + ((XQ) ? 3 : 0)) * U_BYTES + (wr * ((XQ) ? X1 : 64)) * 128; \
+    _Pragma("unroll") for (int i = 0; i < ((XQ) ? MF1 : 4); ++i) {                                 \
       xr[i][0] = *reinterpret_cast<const bf16x8_t*>(b_ + i * 16 * 128 + fofs0);                    \
       xr[i][1] = *reinterpret_cast<const bf16x8_t*>(b_ + i * 16 * 128 + fofs1);                    \
     }                                                                                              \
@@ -615,20 +631,21 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
   {                                                                                                \
     __builtin_amdgcn_s_setprio(1);                                                                 \
     _Pragma("unroll") for (int s = 0; s < 2; ++s)                                                  \
-      _Pragma("unroll") for (int i = 0; i < 4; ++i)                                                \
+      _Pragma("unroll") for (int i = 0; i < ((MQ) ? MF1 : 4); ++i)                                 \
         _Pragma("unroll") for (int j = 0; j < 2; ++j)                                              \
           acc[4 * (MQ) + i][2 * (NQ) + j] =                                                        \
               __builtin_amdgcn_mfma_f32_16x16x32_bf16(WR[j][s], xr[i][s], acc[4 * (MQ) + i][2 * (NQ) + j], 0, 0, 0); \
     __builtin_amdgcn_s_setprio(0);                                                                 \
   }
 // CHECKED = 0: steady state (kt + 2 < nk): every phase stages a unit, 3 phases of DMAs in flight
-#define K256_SYNC_LOADS(G, CHECKED)                                                                \
+// (NS = this wave's DMAs of those 3 phases: 6 at phase 1, 4 + L3 at phases 2-4, which stage u3 or follow it)
+#define K256_SYNC_LOADS(G, CHECKED, NS)                                                            \
   if (CHECKED) {                                                                                   \
     stage_phase(G);                                                                                \
     wait_phase(G);                                                                                 \
   } else {                                                                                         \
     stage(phase_tile(G), phase_unit(G));                                                           \
-    wait_vmcnt<6>();                                                                               \
+    wait_vmcnt<NS>();                                                                              \
   }                                                                                                \
   __builtin_amdgcn_s_barrier();                                                                    \
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -638,21 +655,21 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
     /* phase 1: quadrant (0,0) */                                                                  \
     K256_READ_W(w0r, 0, KT)                                                                        \
     K256_READ_X(0, KT)                                                                             \
-    K256_SYNC_LOADS(g + 1, CHECKED)                                                                \
+    K256_SYNC_LOADS(g + 1, CHECKED, 6)                                                                \
     K256_MFMA(0, 0, w0r)                                                                           \
     __builtin_amdgcn_s_barrier();                                                                  \
     /* phase 2: quadrant (0,1) */                                                                  \
     K256_READ_W(w1r, 1, KT)                                                                        \
-    K256_SYNC_LOADS(g + 2, CHECKED)                                                                \
+    K256_SYNC_LOADS(g + 2, CHECKED, 4 + L3)                                                                \
     K256_MFMA(0, 1, w1r)                                                                           \
     __builtin_amdgcn_s_barrier();                                                                  \
     /* phase 3: quadrant (1,1) */                                                                  \
     K256_READ_X(1, KT)                                                                             \
-    K256_SYNC_LOADS(g + 3, CHECKED)                                                                \
+    K256_SYNC_LOADS(g + 3, CHECKED, 4 + L3)                                                                \
     K256_MFMA(1, 1, w1r)                                                                           \
     __builtin_amdgcn_s_barrier();                                                                  \
     /* phase 4: quadrant (1,0), fragments already in registers */                                  \
-    K256_SYNC_LOADS(g + 4, CHECKED)                                                                \
+    K256_SYNC_LOADS(g + 4, CHECKED, 4 + L3)                                                                \
     K256_MFMA(1, 0, w0r)                                                                           \
     __builtin_amdgcn_s_barrier();                                                                  \
   }
@@ -677,14 +694,14 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
   wait_vmcnt<0>();
   __syncthreads();
 
-  // ---- epilogue, one pixel group at a time: fp32 [128][256] tile in LDS (16-B chunk index
+  // ---- epilogue, one pixel group at a time: fp32 [WROWS][256] tile in LDS (16-B chunk index
   //      XOR (row & 7)), then every thread handles 16-B output chunks: + bias (+ residual), ReLU.
   float* tile = reinterpret_cast<float*>(smem);
 #pragma unroll
   for (int pass = 0; pass < 2; ++pass) {
     if (wr == pass) {
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
+      for (int i = 0; i < MFR; ++i) {
         const int r = 16 * i + (lane & 15);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -694,20 +711,21 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
       }
     }
     __syncthreads();
-    uint4 rv[8];
+    constexpr int EP = WROWS / 16;  // 16-B output chunks per thread and pass
+    uint4 rv[EP];
     if (p.res) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
+      for (int e = 0; e < EP; ++e) {
         const int g = tid + 512 * e;
-        const int m = min(m0 + 128 * pass + (g >> 5), p.M - 1), n = min(n0 + 8 * (g & 31), p.Kout - 8);
+        const int m = min(m0 + WROWS * pass + (g >> 5), p.M - 1), n = min(n0 + 8 * (g & 31), p.Kout - 8);
         rv[e] = *reinterpret_cast<const uint4*>(p.res + res_row(p, m) * p.ldres + n);
       }
     }
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
+    for (int e = 0; e < EP; ++e) {
       const int g = tid + 512 * e;
       const int r = g >> 5, c8 = g & 31;
-      const int m = m0 + 128 * pass + r, n = n0 + 8 * c8;
+      const int m = m0 + WROWS * pass + r, n = n0 + 8 * c8;
       const float4 v0 = *reinterpret_cast<const float4*>(tile + r * 256 + 4 * ((2 * c8) ^ (r & 7)));
       const float4 v1 = *reinterpret_cast<const float4*>(tile + r * 256 + 4 * ((2 * c8 + 1) ^ (r & 7)));
       const int nb = min(n, p.Kout - 8);
@@ -761,20 +779,21 @@ int launch(const ConvParams& p0, hipStream_t s) {
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
 }
 
+template <int BM>
 int launch256(const ConvParams& p0, hipStream_t s) {
   ConvParams p = p0;
   // 256 tile: C % 64 (one tap per 64-wide K tile), 16-B output/residual rows, Kout % 8
   if (p.C % 64 || p.Kpad % 64 || p.ldy % 8 || p.ycoff % 8 || (p.res && p.ldres % 8) || p.Kout % 8)
     return AI4E_EINVAL;
-  const int mt = ai4e_cdiv(p.M, 256);
+  const int mt = ai4e_cdiv(p.M, BM);
   p.ntiles_n = ai4e_cdiv(p.Kout, 256);
   const int nb = mt * p.ntiles_n;
   p.zero = zero_chunk_ptr();
   if (!p.zero) return AI4E_ELAUNCH;
   if (p.KH == 1 && p.KW == 1 && p.pad == 0)
-    hipLaunchKernelGGL(conv_igemm256_kernel<GATHER_POINTWISE>, dim3(nb), dim3(512), 0, s, p);
+    hipLaunchKernelGGL((conv_igemm256_kernel<GATHER_POINTWISE, BM>), dim3(nb), dim3(512), 0, s, p);
   else
-    hipLaunchKernelGGL(conv_igemm256_kernel<GATHER_TAP>, dim3(nb), dim3(512), 0, s, p);
+    hipLaunchKernelGGL((conv_igemm256_kernel<GATHER_TAP, BM>), dim3(nb), dim3(512), 0, s, p);
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
 }
 
@@ -784,7 +803,8 @@ int launch256(const ConvParams& p0, hipStream_t s) {
 // 2 = 256x64 (4x1), 3 = 64x256 (1x4) with 4 stages; 4 = 128x128 with 5 stages (80 KB: still two
 // workgroups per CU), 5 = 256x64 with 5 stages (100 KB: one workgroup per CU), 6 = 256x256, 8 waves,
 // ping-pong phases (needs C % 64 == 0, Kout % 8 == 0); 7/8 = the 128x128 / 256x64 tiles with a 3-stage
-// ring (48 KB, two-pass LDS epilogue) built for three workgroups per CU.
+// ring (48 KB, two-pass LDS epilogue) built for three workgroups per CU; 9 = the 256x256 schedule with
+// 192-pixel tiles (one tile per CU for 250-image 14x14 layers).
 // relu: bit 0 = ReLU; bit 1 = `res` is on the half-resolution grid [N, OH/2, OW/2, ldres] (nearest 2x
 // upsample of the residual, OH and OW even).
 namespace {
@@ -812,7 +832,7 @@ int conv2d_impl(const void* x, const void* w, const void* bias, const void* res,
     // channel tile, tiles that never straddle images, full 16-B output rows
     const bool tall = tile_cfg == 2 || tile_cfg == 5 || tile_cfg == 8;
     const int bm = tall ? 256 : 128, bn = tall ? 64 : 128;
-    if (tile_cfg == 3 || tile_cfg == 6 || gn_groups <= 0 || Kout % gn_groups || (OH * OW) % bm || Kout % 8 ||
+    if (tile_cfg == 3 || tile_cfg == 6 || tile_cfg == 9 || gn_groups <= 0 || Kout % gn_groups || (OH * OW) % bm || Kout % 8 ||
         ldy % 8 || ycoff % 8 || (res && ldres % 8) || bn % (Kout / gn_groups))
       return AI4E_EINVAL;
     p.gnp = gnp;
@@ -824,9 +844,10 @@ int conv2d_impl(const void* x, const void* w, const void* bias, const void* res,
     case 3: return launch<1, 4, 4>(p, stream);
     case 4: return launch<2, 2, 5>(p, stream);
     case 5: return launch<4, 1, 5>(p, stream);
-    case 6: return launch256(p, stream);
+    case 6: return launch256<256>(p, stream);
     case 7: return launch<2, 2, 3, 3>(p, stream);
     case 8: return launch<4, 1, 3, 3>(p, stream);
+    case 9: return launch256<192>(p, stream);
     default: return AI4E_EINVAL;
   }
 }

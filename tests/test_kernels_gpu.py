@@ -62,7 +62,7 @@ def test_conv_igemm(case, epi):
     assert err <= 0.02 * ref.abs().max().item() + 0.02, err
 
 
-@pytest.mark.parametrize("tile", [1, 2, 3, 4, 5, 6, 7, 8])
+@pytest.mark.parametrize("tile", [1, 2, 3, 4, 5, 6, 7, 8, 9])
 def test_conv_tile_configs(tile):
     torch.manual_seed(1)
     wt = torch.randn(256, 64, 3, 3) / 24
@@ -103,9 +103,10 @@ CASES_256 = [
 ]
 
 
+@pytest.mark.parametrize("tile", [6, 9])  # 9: the same schedule with 192-pixel tiles
 @pytest.mark.parametrize("case", CASES_256)
 @pytest.mark.parametrize("epi", ["plain", "res_relu"])
-def test_conv_tile256(case, epi):
+def test_conv_tile256(case, epi, tile):
     n, h, w, cin, cout, k, s, p = case
     torch.manual_seed(3)
     wt = torch.randn(cout, cin, k, k) / (cin * k * k) ** 0.5
@@ -114,7 +115,7 @@ def test_conv_tile256(case, epi):
     x = torch.randn(n, h, w, pc.cin_pad, device=DEV).to(torch.bfloat16)
     oh, ow = pc.out_hw(h, w)
     res = torch.randn(n, oh, ow, cout, device=DEV).to(torch.bfloat16) if epi == "res_relu" else None
-    y = conv2d_nhwc(x, pc, residual=res, relu=epi != "plain", tile_cfg=6)
+    y = conv2d_nhwc(x, pc, residual=res, relu=epi != "plain", tile_cfg=tile)
     torch.cuda.synchronize()
     wq = pc.w_packed[:cout, :k * k * pc.cin_pad].float().reshape(cout, k, k, pc.cin_pad).permute(0, 3, 1, 2)
     ref = ref_conv(x, wq, b.to(DEV), s, p, res, epi != "plain")
