@@ -95,13 +95,15 @@ def tile_key(pc: PackedConv, n: int, h: int, w: int, residual: bool) -> str:
 
 
 def tuned_tile(pc: PackedConv, n: int, h: int, w: int, residual: bool) -> int:
-    """Measured per-shape tile config (bench/conv_tune.py -> ops/conv_tiles.json); 0 = kernel default."""
+    """Measured per-shape tile config (bench/conv_tune.py -> ops/conv_tiles.json, or the table named by
+    ``AI4E_CONV_TILES`` for A/B runs); 0 = kernel default."""
     global _TILES
     if _TILES is None:
         import json
         import os
 
-        path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "conv_tiles.json")
+        path = os.environ.get("AI4E_CONV_TILES") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                                                 "conv_tiles.json")
         try:
             with open(path) as f:
                 _TILES = json.load(f)
