@@ -65,6 +65,9 @@ class Config:
     max_finished_tasks: int = field(default=4_000_000, metadata={"env": "AI4E_MAX_FINISHED_TASKS"})
     # request bodies up to this size are journaled as the task's _ORIG body (replayed after a restart)
     journal_payload_max_bytes: int = field(default=1 << 20, metadata={"env": "AI4E_JOURNAL_PAYLOAD_MAX_BYTES"})
+    # image endpoints: processes that decode JPEG/PNG/npy/JSON bodies straight into the shared payload ring
+    # (0 = decode on the gateway's executor threads); per endpoint: `decode_processes` in the platform YAML
+    decode_processes: int = field(default=0, metadata={"env": "AI4E_DECODE_PROCESSES"})
     # --- metrics timers (TaskQueueLogger.cs:20 / TaskProcessLogger.cs:22) ---
     queue_logger_period_s: float = field(default=30.0, metadata={"env": "AI4E_QUEUE_LOGGER_PERIOD_S"})
     process_logger_period_s: float = field(default=300.0, metadata={"env": "AI4E_PROCESS_LOGGER_PERIOD_S"})

@@ -25,67 +25,12 @@ import numpy as np
 import torch
 
 from ..store import STATE_CREATED, STATE_FAILED
+from .decode import PayloadError, decode_image  # noqa: F401  (re-exported: the endpoint's payload API)
 from .serving import GpuBatchWorker
 
 PAYLOAD_LOST = "Task failed - payload lost on restart"
 PUBLISH_FAILED = "Failed - unable to send to backend service."
 _ORIG_PREFIX = "ai4e-b64:"
-
-
-class PayloadError(ValueError):
-    """A request body that cannot be decoded into the endpoint's input (HTTP 400 / 415)."""
-
-    def __init__(self, msg: str, status: int = 400):
-        super().__init__(msg)
-        self.status = status
-
-
-def decode_image(body: bytes, content_type: str, shape: Tuple[int, int, int]) -> np.ndarray:
-    """Decode a request body to uint8 HxWxC of ``shape`` (resizing if needed).
-
-    Accepted: raw ``application/octet-stream`` (exactly H*W*C bytes), ``application/x-npy``
-    (``numpy.load(allow_pickle=False)``), ``image/jpeg``/``image/png``/``image/tiff`` (PIL), and JSON
-    ``{"image_b64": ..., "shape": [H, W, C]}`` with raw bytes.
-    """
-    h, w, c = shape
-    ct = (content_type or "").split(";")[0].strip().lower()
-    try:
-        if ct in ("application/json", "text/json"):
-            d = json.loads(body or b"{}")
-            raw = base64.b64decode(d["image_b64"])
-            shp = tuple(d.get("shape", shape))
-            arr = np.frombuffer(raw, dtype=np.uint8).reshape(shp)
-        elif ct == "application/x-npy":
-            arr = np.load(io.BytesIO(body), allow_pickle=False)
-        elif ct.startswith("image/"):
-            from PIL import Image
-
-            im = Image.open(io.BytesIO(body))
-            im = im.convert("RGB" if c == 3 else ("L" if c == 1 else "RGBA"))
-            if im.size != (w, h):
-                im = im.resize((w, h), Image.BILINEAR)
-            arr = np.asarray(im, dtype=np.uint8)
-        elif ct in ("", "application/octet-stream"):
-            if len(body) != h * w * c:
-                raise PayloadError(f"raw payload must be {h * w * c} bytes (uint8 {h}x{w}x{c}), got {len(body)}")
-            arr = np.frombuffer(body, dtype=np.uint8).reshape(h, w, c)
-        else:
-            raise PayloadError(f"unsupported content type {ct!r}", 415)
-    except PayloadError:
-        raise
-    except Exception as e:  # malformed JSON / base64 / npy / image bytes
-        raise PayloadError(f"cannot decode payload: {e}") from e
-    if arr.dtype != np.uint8:
-        arr = np.clip(arr, 0, 255).astype(np.uint8)
-    if arr.ndim == 2:
-        arr = arr[..., None]
-    if arr.ndim != 3 or arr.shape[2] != c:
-        raise PayloadError(f"expected {c} channels, got shape {arr.shape}")
-    if arr.shape[:2] != (h, w):
-        t = torch.from_numpy(np.ascontiguousarray(arr)).permute(2, 0, 1)[None].float()
-        t = torch.nn.functional.interpolate(t, size=(h, w), mode="bilinear", align_corners=False)
-        arr = t[0].permute(1, 2, 0).round().clamp(0, 255).to(torch.uint8).numpy()
-    return arr
 
 
 class StreamedBatch:
@@ -149,7 +94,7 @@ class StreamedBatch:
 class ModelEndpoint:
     def __init__(self, control_plane, path: str, engine=None, ring=None, worker=None,
                  decode: Optional[Callable[[bytes, str], np.ndarray]] = None, base_url: str = "http://127.0.0.1",
-                 journal_payload_max_bytes: Optional[int] = None):
+                 journal_payload_max_bytes: Optional[int] = None, decode_processes: int = 0):
         self.cp = control_plane
         self.path = path
         self.endpoint = base_url.rstrip("/") + path
@@ -157,6 +102,12 @@ class ModelEndpoint:
         self.ring = self.worker.ring
         self.is_pool = hasattr(self.worker, "submit_slots")
         self.decode = decode or (lambda body, ct: decode_image(body, ct, self.ring.item_shape))
+        # decode worker processes writing into the shared ring (pool backends: the ring is shared memory)
+        self.decode_pool = None
+        if decode_processes > 0 and decode is None and hasattr(self.ring, "name"):
+            from .decode_pool import DecodePool
+
+            self.decode_pool = DecodePool(decode_processes, self.ring.name, self.ring.nslots, self.ring.item_shape)
         self.queue = control_plane.queue_for(self.endpoint)
         self._waiters: Dict[str, Callable[[str], None]] = {}
         self._wmu = threading.Lock()
@@ -203,9 +154,18 @@ class ModelEndpoint:
         """Async API: decode, create task (or adopt an upstream ``taskId``), enqueue. Returns task JSON.
 
         Raises :class:`PayloadError` (-> HTTP 400/415) before any task exists for undecodable bodies."""
-        arr = self.decode(body, content_type)
-        slot = self.ring.alloc(1, timeout=30)[0]
-        self._write([slot], arr[None])
+        ct = (content_type or "").split(";")[0].strip().lower()
+        if self.decode_pool is not None and ct not in ("", "application/octet-stream"):
+            slot = self.ring.alloc(1, timeout=30)[0]
+            try:
+                self.decode_pool.decode_into(slot, body, content_type)
+            except BaseException:
+                self.ring.free([slot])
+                raise
+        else:
+            arr = self.decode(body, content_type)
+            slot = self.ring.alloc(1, timeout=30)[0]
+            self._write([slot], arr[None])
         orig = self._orig(body, content_type)
         if task_id or orig is not None:
             # upstream TaskId (header taskId, api_task.py:12-20) or a journaled payload: explicit upsert
@@ -329,4 +289,7 @@ class ModelEndpoint:
         return self
 
     def stop(self) -> None:
+        if self.decode_pool is not None:
+            self.decode_pool.close()
+            self.decode_pool = None
         self.worker.stop()

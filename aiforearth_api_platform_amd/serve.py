@@ -68,7 +68,8 @@ def build_platform(doc: Dict[str, Any], cfg: Config):
                               heartbeat_interval_s=cfg.heartbeat_interval_s,
                               heartbeat_timeout_s=cfg.heartbeat_timeout_s,
                               ring_slots=int(e.get("ring_slots", 0)))
-            ep = ModelEndpoint(cp, e["path"], worker=pool, base_url=base_url)
+            ep = ModelEndpoint(cp, e["path"], worker=pool, base_url=base_url,
+                               decode_processes=int(e.get("decode_processes", cfg.decode_processes)))
         else:
             dev = torch.device(devs[0])
             servable = as_servable(_load(e["factory"])(device=str(dev), **(e.get("kwargs") or {})),
