@@ -211,7 +211,7 @@ def conv2d_gn_nhwc(x: torch.Tensor, pc: PackedConv, groups: int, out: Optional[t
         out_coff = 0
     nchunks = oh * ow // bm
     # chunk sums, then room for the per-channel affine the norm's finalize launch writes
-    partials = torch.empty(n * nchunks * groups * 2 + n * pc.cout * 2, device=x.device, dtype=torch.float32)
+    partials = torch.empty(n * nchunks * groups * 4 + n * pc.cout * 2, device=x.device, dtype=torch.float32)
     _conv_hip(x, pc, None, False, out, out_coff, cfg, gn=(partials, groups))
     return out, (partials, nchunks)
 

@@ -62,7 +62,7 @@ def group_norm_nhwc(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, gr
             return out
         nchunks = (h * w + GN_PIX_PER_BLOCK - 1) // GN_PIX_PER_BLOCK
         # chunk partials, then the per-channel affine (scale, shift) the finalize launch writes
-        partials = torch.empty(n * nchunks * groups * 2 + n * c * 2, device=x.device, dtype=torch.float32)
+        partials = torch.empty(n * nchunks * groups * 4 + n * c * 2, device=x.device, dtype=torch.float32)
         g32 = gamma.to(x.device, torch.float32).contiguous()
         b32 = beta.to(x.device, torch.float32).contiguous()
         _ext.call("ai4e_groupnorm_nhwc", _base_ptr(x), _base_ptr(out), g32.data_ptr(), b32.data_ptr(),

@@ -63,7 +63,8 @@ struct ConvParams {
   int ntiles_n;
   const uint16_t* zero;  // >= 16 zero bytes: source of the DMA gather for padding taps
   // GroupNorm statistics of the stored (bf16) output, fused into the EPI_LDS epilogue (null = off): per
-  // (image, BM-pixel chunk, group) sum and sum of squares -> gnp[((img * (OH*OW/BM) + chunk) * gn_groups + g) * 2]
+  // (image, BM-pixel chunk, group) shifted sum, sum of squares and the shift (norm_resample.hip) ->
+  // gnp[((img * (OH*OW/BM) + chunk) * gn_groups + g) * 4 + {0, 1, 2}]
   float* gnp;
   int gn_groups;
 };
@@ -315,6 +316,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC > 2 ? O
     constexpr int PASS_ROWS = BM / EPI_PASSES;
     float* tile = reinterpret_cast<float*>(smem);
     float gs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, gq[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    float gk[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, kout = 0.f;  // GN shifts (norm_resample.hip)
     __builtin_amdgcn_s_barrier();  // all waves finished reading the last stage
 #pragma unroll
     for (int pass = 0; pass < EPI_PASSES; ++pass) {
@@ -343,6 +345,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC > 2 ? O
       }
     }
     __syncthreads();
+    if (p.gnp && pass == 0) {
+      // GN shift per channel slot: the tile's first pixel (row 0, unswizzled) at the group's first channel
+      const int cg = p.Kout / p.gn_groups;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) gk[k] = fmaxf(tile[(8 * (tid % CPR) + k) / cg * cg], lo);
+      if (tid < BN / cg) kout = fmaxf(tile[tid * cg], lo);
+    }
 #pragma unroll
     for (int e = pass * EPI_CHUNKS / EPI_PASSES; e < (pass + 1) * EPI_CHUNKS / EPI_PASSES; ++e) {
       const int g = tid + 256 * e;
@@ -360,6 +369,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC > 2 ? O
         for (int q = 0; q < 4; ++q) {
           float a, b;
           unpack_bf16x2(ow[q], a, b);
+          a -= gk[2 * q];
+          b -= gk[2 * q + 1];
           gs[2 * q] += a; gq[2 * q] += a * a;
           gs[2 * q + 1] += b; gq[2 * q + 1] += b * b;
         }
@@ -425,9 +436,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC > 2 ? O
           }
         const int ohw = p.OH * p.OW;  // host: ohw % BM == 0, so a tile never straddles images
         const int img = m0 / ohw, chunk = (m0 - img * ohw) / BM;
-        float* o = p.gnp + ((static_cast<long>(img) * (ohw / BM) + chunk) * p.gn_groups + n0 / cg + tid) * 2;
-        o[0] = S;
-        o[1] = Q;
+        float* o = p.gnp + ((static_cast<long>(img) * (ohw / BM) + chunk) * p.gn_groups + n0 / cg + tid) * 4;
+        *reinterpret_cast<float4*>(o) = make_float4(S, Q, kout, 0.f);  // shifted sums, shift
       }
     }
   } else {
@@ -863,8 +873,8 @@ AI4E_API int ai4e_conv2d_fwd(const void* x, const void* w, const void* bias, con
 }
 
 // Same conv, plus the GroupNorm statistics of its output (gn_groups groups over Kout channels) written as
-// per-(image, tile-row chunk, group) partial sum / sum of squares into gn_partials
-// [N, OH*OW / BM, gn_groups, 2] fp32 (BM = 256 for tile configs 2 and 5, else 128). Configs 3 and 6 and
+// per-(image, tile-row chunk, group) shifted partial sums (sum(x - K), sum((x - K)^2), K, pad) into gn_partials
+// [N, OH*OW / BM, gn_groups, 4] fp32 (BM = 256 for tile configs 2 and 5, else 128). Configs 3 and 6 and
 // shapes whose tiles would straddle images are refused (EINVAL) before anything is launched.
 AI4E_API int ai4e_conv2d_gn_fwd(const void* x, const void* w, const void* bias, const void* res, void* y, int N,
                                 int H, int W, int C, int ldx, int xcoff, int KH, int KW, int stride, int pad, int OH,

@@ -1,16 +1,22 @@
 // K2 GroupNorm (+ReLU) and K3 bilinear 2x upsample — NHWC bf16, memory-bound, 16-B vectors per lane.
 //
-// GroupNorm is two launches: (1) per-(image, pixel-chunk) partial sum / sum-of-squares per group,
-// reduced in-register then across the workgroup in LDS and written as fp32 partials (no global
-// atomics); (2) every normalize workgroup combines its image's partials (fp64), then applies
+// GroupNorm is two launches: (1) per-(image, pixel-chunk) partial sums per group, reduced in-register
+// then across the workgroup in LDS and written as fp32 partials (no global atomics); (2) a finalize
+// workgroup per image combines the partials (fp64) into mean / rstd, then the normalize pass applies
 // (x - mean) * rstd * gamma + beta (+ReLU) and writes bf16 — optionally into a channel slice of a
-// wider buffer (U-Net concat). The upsample writes straight into a concat slice as well, so the
-// decoder's "upsample + concat" never materialises a separate tensor.
+// wider buffer (U-Net concat).
+// Partials are SHIFTED sums: chunk k of group g stores (S, Q, K) = (sum(x - K), sum((x - K)^2), K) with
+// K one of the chunk's own values of that group, so a group whose mean is far from 0 relative to its
+// spread (e.g. 50 + 0.05 * noise) does not cancel in E[x^2] - mean^2; the finalize re-bases every chunk
+// on chunk 0's K in fp64 (GN_PARTIAL floats per (chunk, group); the conv epilogue writes the same form).
+// The upsample writes straight into a concat slice as well, so the decoder's "upsample + concat" never
+// materialises a separate tensor.
 #include "common.h"
 
 namespace {
 
 constexpr int GN_PIX_PER_BLOCK = 1024;
+constexpr int GN_PARTIAL = 4;  // floats per (chunk, group) partial: S, Q, K, pad
 
 // x: [N, HW, C] (row stride ldx, channel offset xcoff); partials: [N, nchunks, G, 2]
 __global__ __launch_bounds__(256) void gn_stats_kernel(const uint16_t* __restrict__ x, float* __restrict__ partials,
@@ -26,14 +32,32 @@ __global__ __launch_bounds__(256) void gn_stats_kernel(const uint16_t* __restric
   const int p0 = threadIdx.x / lanes_per_pix;
   float s[8] = {0, 0, 0, 0, 0, 0, 0, 0}, q[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   const int pbeg = chunk * GN_PIX_PER_BLOCK, pend = min(HW, pbeg + GN_PIX_PER_BLOCK);
+  // the chunk's shift per group: its first pixel's value of the group's first channel
+  __shared__ float gs[64], gq[64], gk[64];
+  if (static_cast<int>(threadIdx.x) < G) {
+    const uint16_t v = x[static_cast<long>(n) * HW * ldx + xcoff + static_cast<long>(pbeg) * ldx + threadIdx.x * cg];
+    gk[threadIdx.x] = __uint_as_float(static_cast<uint32_t>(v) << 16);
+  }
+  if (threadIdx.x < 64) {
+    gs[threadIdx.x] = 0.f;
+    gq[threadIdx.x] = 0.f;
+  }
+  __syncthreads();
+  float k[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) k[j] = gk[min((8 * c8 + j) / cg, G - 1)];
   if (p0 < pix_per_iter) {
     const uint16_t* const xb = x + static_cast<long>(n) * HW * ldx + xcoff + 8 * c8;
     auto acc = [&](const uint4& v) __attribute__((always_inline)) {
       float a, b;
-      unpack_bf16x2(v.x, a, b); s[0] += a; q[0] += a * a; s[1] += b; q[1] += b * b;
-      unpack_bf16x2(v.y, a, b); s[2] += a; q[2] += a * a; s[3] += b; q[3] += b * b;
-      unpack_bf16x2(v.z, a, b); s[4] += a; q[4] += a * a; s[5] += b; q[5] += b * b;
-      unpack_bf16x2(v.w, a, b); s[6] += a; q[6] += a * a; s[7] += b; q[7] += b * b;
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int h = 0; h < 4; ++h) {
+        unpack_bf16x2(w[h], a, b);
+        a -= k[2 * h];
+        b -= k[2 * h + 1];
+        s[2 * h] += a; q[2 * h] += a * a; s[2 * h + 1] += b; q[2 * h + 1] += b * b;
+      }
     };
     int p = pbeg + p0;
     // four independent 16-B loads in flight per lane, then the accumulation
@@ -47,12 +71,6 @@ __global__ __launch_bounds__(256) void gn_stats_kernel(const uint16_t* __restric
     for (; p < pend; p += pix_per_iter) acc(*reinterpret_cast<const uint4*>(xb + static_cast<long>(p) * ldx));
   }
   // reduce each lane's 8 channels into its group(s), then across lanes holding the same group
-  __shared__ float gs[64], gq[64];
-  if (threadIdx.x < 64) {
-    gs[threadIdx.x] = 0.f;
-    gq[threadIdx.x] = 0.f;
-  }
-  __syncthreads();
   if (p0 < pix_per_iter) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -63,47 +81,50 @@ __global__ __launch_bounds__(256) void gn_stats_kernel(const uint16_t* __restric
   }
   __syncthreads();
   if (static_cast<int>(threadIdx.x) < G) {
-    float* o = partials + ((static_cast<long>(n) * nchunks + chunk) * G + threadIdx.x) * 2;
-    o[0] = gs[threadIdx.x];
-    o[1] = gq[threadIdx.x];
+    float* o = partials + ((static_cast<long>(n) * nchunks + chunk) * G + threadIdx.x) * GN_PARTIAL;
+    *reinterpret_cast<float4*>(o) = make_float4(gs[threadIdx.x], gq[threadIdx.x], gk[threadIdx.x], 0.f);
   }
 }
 
 // One workgroup per image: combine the image's chunk partials (fp64) into per-group mean / rstd, then fold
 // gamma / beta into a per-channel affine: ss[n, c] = (a, b) with y = x * a + b, a = rstd_g * gamma_c,
-// b = beta_c - mean_g * a. (Done once per image instead of in every normalize workgroup.)
+// b = beta_c - mean_g * a. (Done once per image instead of in every normalize workgroup.) Chunk k holds
+// chunk_px pixels (the last one possibly fewer); its shifted sums are re-based on chunk 0's shift K0:
+// sum(x - K0) = S + n d, sum((x - K0)^2) = Q + 2 d S + n d^2 with d = K - K0.
 __global__ __launch_bounds__(256) void gn_finalize_kernel(const float* __restrict__ partials,
                                                           const float* __restrict__ gamma,
                                                           const float* __restrict__ beta, float2* __restrict__ ss,
-                                                          int HW, int C, int G, float eps, int nchunks) {
+                                                          int HW, int C, int G, float eps, int nchunks, int chunk_px) {
   const int n = blockIdx.x;
-  // thread t owns group t % G and every (256/G)-th chunk from t / G: each load step the block reads one
-  // contiguous 2 KB run of (chunk, group) float2 partials; two fp64 accumulator pairs per thread
+  // thread t owns group t % G and every (256/G)-th chunk from t / G
   __shared__ double red_s[256], red_q[256];
   __shared__ float mean_s[64], rstd_s[64];
   const int lpg = 256 / G;  // threads per group (G <= 64 divides 256 only when a power of two; else some idle)
   const int g = threadIdx.x % G, l = threadIdx.x / G;
-  double s0 = 0, q0 = 0, s1 = 0, q1 = 0;
+  const int cg = C / G;
+  const float4* pp = reinterpret_cast<const float4*>(partials) + static_cast<long>(n) * nchunks * G + g;
+  const double k0 = pp[0].z;
+  double s0 = 0, q0 = 0;
   if (l < lpg) {
-    const float2* pp = reinterpret_cast<const float2*>(partials) + static_cast<long>(n) * nchunks * G + g;
-    // 8 independent loads in flight per lane: with one workgroup per image the pass is latency-bound
-    int k = l;
-    for (; k + 7 * lpg < nchunks; k += 8 * lpg) {
-      float2 v[8];
+    // 4 independent loads in flight per lane: with one workgroup per image the pass is latency-bound
+    for (int k = l; k < nchunks; k += 4 * lpg) {
+      float4 v[4];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = pp[static_cast<long>(k + u * lpg) * G];
+      for (int u = 0; u < 4; ++u)
+        if (k + u * lpg < nchunks) v[u] = pp[static_cast<long>(k + u * lpg) * G];
 #pragma unroll
-      for (int u = 0; u < 8; u += 2) {
-        s0 += v[u].x; q0 += v[u].y; s1 += v[u + 1].x; q1 += v[u + 1].y;
+      for (int u = 0; u < 4; ++u) {
+        const int kk = k + u * lpg;
+        if (kk >= nchunks) break;
+        const double cnt = static_cast<double>(min(chunk_px, HW - kk * chunk_px)) * cg;
+        const double d = static_cast<double>(v[u].z) - k0;
+        s0 += v[u].x + cnt * d;
+        q0 += v[u].y + 2.0 * d * v[u].x + cnt * d * d;
       }
     }
-    for (; k < nchunks; k += lpg) {
-      const float2 a = pp[static_cast<long>(k) * G];
-      s0 += a.x; q0 += a.y;
-    }
   }
-  red_s[threadIdx.x] = s0 + s1;
-  red_q[threadIdx.x] = q0 + q1;
+  red_s[threadIdx.x] = s0;
+  red_q[threadIdx.x] = q0;
   __syncthreads();
   if (static_cast<int>(threadIdx.x) < G) {
     double s = 0, q = 0;
@@ -111,14 +132,13 @@ __global__ __launch_bounds__(256) void gn_finalize_kernel(const float* __restric
       s += red_s[k * G + threadIdx.x];
       q += red_q[k * G + threadIdx.x];
     }
-    const double cnt = static_cast<double>(HW) * (C / G);
-    const double mean = s / cnt;
-    const double var = fmax(q / cnt - mean * mean, 0.0);
-    mean_s[threadIdx.x] = static_cast<float>(mean);
+    const double cnt = static_cast<double>(HW) * cg;
+    const double m = s / cnt;  // mean relative to K0
+    const double var = fmax(q / cnt - m * m, 0.0);
+    mean_s[threadIdx.x] = static_cast<float>(pp[0].z + m);
     rstd_s[threadIdx.x] = static_cast<float>(1.0 / sqrt(var + eps));
   }
   __syncthreads();
-  const int cg = C / G;
   for (int c = threadIdx.x; c < C; c += 256) {
     const int gc = c / cg;
     const float a = rstd_s[gc] * gamma[c];
@@ -277,7 +297,7 @@ inline int grid_for(long work) {
 
 }  // namespace
 
-// partials (workspace) must hold N * ceil(HW / 1024) * G * 2 + N * C * 2 floats (chunk partials, then the
+// partials (workspace) must hold N * ceil(HW / 1024) * G * 4 + N * C * 2 floats (chunk partials, then the
 // per-channel affine). HW * C / 8 < 2^31.
 AI4E_API int ai4e_groupnorm_nhwc(const void* x, void* y, const void* gamma, const void* beta, void* partials, int N,
                                  int HW, int C, int G, float eps, int relu, int ldx_ldy_pack, int coff_pack,
@@ -292,9 +312,11 @@ AI4E_API int ai4e_groupnorm_nhwc(const void* x, void* y, const void* gamma, cons
   const int nchunks = (HW + GN_PIX_PER_BLOCK - 1) / GN_PIX_PER_BLOCK;
   hipLaunchKernelGGL(gn_stats_kernel, dim3(nchunks, N), dim3(256), 0, s, static_cast<const uint16_t*>(x),
                      static_cast<float*>(partials), HW, C, G, ldx, xcoff, nchunks);
-  float2* ss = reinterpret_cast<float2*>(static_cast<float*>(partials) + static_cast<long>(N) * nchunks * G * 2);
+  float2* ss =
+      reinterpret_cast<float2*>(static_cast<float*>(partials) + static_cast<long>(N) * nchunks * G * GN_PARTIAL);
   hipLaunchKernelGGL(gn_finalize_kernel, dim3(N), dim3(256), 0, s, static_cast<const float*>(partials),
-                     static_cast<const float*>(gamma), static_cast<const float*>(beta), ss, HW, C, G, eps, nchunks);
+                     static_cast<const float*>(gamma), static_cast<const float*>(beta), ss, HW, C, G, eps, nchunks,
+                     GN_PIX_PER_BLOCK);
   // ~4 vectors per lane; at most 8192 workgroups per image
   const int gx = grid_for(static_cast<long>(HW) * (C / 8) / 4 + 1);
   hipLaunchKernelGGL(gn_apply_kernel, dim3(gx, N), dim3(256), 0, s, static_cast<const uint16_t*>(x),
@@ -303,7 +325,8 @@ AI4E_API int ai4e_groupnorm_nhwc(const void* x, void* y, const void* gamma, cons
 }
 
 // GroupNorm when the statistics were already produced (e.g. by the conv epilogue, ai4e_conv2d_gn_fwd):
-// partials [N, nchunks, G, 2] chunk sums, followed by room for the per-channel affine (N * C * 2 floats).
+// partials [N, nchunks, G, 4] shifted chunk sums (HW / nchunks pixels per chunk), followed by room for the
+// per-channel affine (N * C * 2 floats).
 AI4E_API int ai4e_groupnorm_apply_nhwc(const void* x, void* y, const void* gamma, const void* beta, void* partials,
                                        int N, int HW, int C, int G, float eps, int relu, int ldx_ldy_pack,
                                        int coff_pack, int nchunks, hipStream_t s) {
@@ -313,9 +336,12 @@ AI4E_API int ai4e_groupnorm_apply_nhwc(const void* x, void* y, const void* gamma
       nchunks <= 0)
     return AI4E_EINVAL;
   if (static_cast<long>(HW) * (C / 8) >= (1L << 31) - 4 * 8192L * 256) return AI4E_EINVAL;
-  float2* ss = reinterpret_cast<float2*>(static_cast<float*>(partials) + static_cast<long>(N) * nchunks * G * 2);
+  if (HW % nchunks) return AI4E_EINVAL;  // conv-epilogue partials: whole tiles per image
+  float2* ss =
+      reinterpret_cast<float2*>(static_cast<float*>(partials) + static_cast<long>(N) * nchunks * G * GN_PARTIAL);
   hipLaunchKernelGGL(gn_finalize_kernel, dim3(N), dim3(256), 0, s, static_cast<const float*>(partials),
-                     static_cast<const float*>(gamma), static_cast<const float*>(beta), ss, HW, C, G, eps, nchunks);
+                     static_cast<const float*>(gamma), static_cast<const float*>(beta), ss, HW, C, G, eps, nchunks,
+                     HW / nchunks);
   const int gx = grid_for(static_cast<long>(HW) * (C / 8) / 4 + 1);
   hipLaunchKernelGGL(gn_apply_kernel, dim3(gx, N), dim3(256), 0, s, static_cast<const uint16_t*>(x),
                      static_cast<uint16_t*>(y), ss, HW, C, relu, ldx, xcoff, ldy, ycoff);
@@ -334,9 +360,12 @@ AI4E_API int ai4e_groupnorm_apply_pool_nhwc(const void* x, void* y, const void* 
     return AI4E_EINVAL;
   const int HW = H * W;
   if (static_cast<long>(HW) * (C / 8) >= (1L << 31) - 4 * 8192L * 256) return AI4E_EINVAL;
-  float2* ss = reinterpret_cast<float2*>(static_cast<float*>(partials) + static_cast<long>(N) * nchunks * G * 2);
+  if (HW % nchunks) return AI4E_EINVAL;  // conv-epilogue partials: whole tiles per image
+  float2* ss =
+      reinterpret_cast<float2*>(static_cast<float*>(partials) + static_cast<long>(N) * nchunks * G * GN_PARTIAL);
   hipLaunchKernelGGL(gn_finalize_kernel, dim3(N), dim3(256), 0, s, static_cast<const float*>(partials),
-                     static_cast<const float*>(gamma), static_cast<const float*>(beta), ss, HW, C, G, eps, nchunks);
+                     static_cast<const float*>(gamma), static_cast<const float*>(beta), ss, HW, C, G, eps, nchunks,
+                     HW / nchunks);
   const int gx = grid_for(static_cast<long>(HW / 4) * (C / 8) / 2 + 1);
   hipLaunchKernelGGL(gn_apply_pool_kernel, dim3(gx, N), dim3(256), 0, s, static_cast<const uint16_t*>(x),
                      static_cast<uint16_t*>(y), static_cast<uint16_t*>(pooled), ss, H, W, C, relu, ldx, xcoff, ldy,

@@ -38,6 +38,36 @@ def test_groupnorm(shape, groups, relu):
     assert (y.float() - ref).abs().max().item() < 0.05
 
 
+@pytest.mark.parametrize("dc,std", [(50.0, 0.5), (300.0, 2.0)])
+def test_groupnorm_large_dc_offset(dc, std):
+    """A group whose mean is far from 0 relative to its spread: the shifted chunk sums keep E[x^2] - mean^2
+    from cancelling (reference: torch fp32 GroupNorm of the same bf16 input)."""
+    torch.manual_seed(3)
+    x = (dc + std * torch.randn(2, 48, 64, 64)).to(DEV).bfloat16()  # 3072 pixels: 3 chunks per image
+    g, b = torch.rand(64) + 0.5, torch.randn(64)
+    y = group_norm_nhwc(x, g, b, 32)
+    ref = F.group_norm(x.float().permute(0, 3, 1, 2), 32, g.to(DEV), b.to(DEV)).permute(0, 2, 3, 1)
+    assert (y.float() - ref).abs().max().item() < 0.03
+
+
+def test_conv_fused_groupnorm_stats_dc_offset(monkeypatch):
+    """Conv-epilogue GroupNorm statistics on an output with a large DC offset (bias 40): same as the fp32
+    reference GroupNorm of the stored conv output."""
+    from aiforearth_api_platform_amd.ops import conv as convmod
+    from aiforearth_api_platform_amd.ops.conv import conv2d_gn_nhwc, pack_conv
+
+    monkeypatch.setattr(convmod, "tuned_tile", lambda *a: 1)
+    torch.manual_seed(9)
+    pc = pack_conv(torch.randn(64, 64, 3, 3) / (9 * 64) ** 0.5 * 0.2, torch.full((64,), 40.0), pad=1).to(DEV)
+    x = torch.randn(2, 32, 32, 64, device=DEV).to(torch.bfloat16)
+    y, st = conv2d_gn_nhwc(x, pc, 32)
+    assert st is not None
+    gamma, beta = torch.rand(64, device=DEV) + 0.5, torch.randn(64, device=DEV) * 0.1
+    a = group_norm_nhwc(y, gamma, beta, groups=32, stats=st)
+    ref = F.group_norm(y.float().permute(0, 3, 1, 2), 32, gamma, beta).permute(0, 2, 3, 1)
+    assert (a.float() - ref).abs().max().item() < 0.03
+
+
 def test_groupnorm_concat_slices():
     x_big = torch.randn(1, 16, 16, 96, device=DEV).bfloat16()
     x = x_big[..., 32:96]
