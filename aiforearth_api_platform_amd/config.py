@@ -68,6 +68,10 @@ class Config:
     # image endpoints: processes that decode JPEG/PNG/npy/JSON bodies straight into the shared payload ring
     # (0 = decode on the gateway's executor threads); per endpoint: `decode_processes` in the platform YAML
     decode_processes: int = field(default=0, metadata={"env": "AI4E_DECODE_PROCESSES"})
+    # ingest front-end processes sharing the public port (SO_REUSEPORT) with the serving process
+    # (runtime/frontend.py); each gets `frontend_ring_slots` payload slots per GPU endpoint (0 = 4 batches)
+    frontend_processes: int = field(default=0, metadata={"env": "AI4E_FRONTEND_PROCESSES"})
+    frontend_ring_slots: int = field(default=0, metadata={"env": "AI4E_FRONTEND_RING_SLOTS"})
     # --- metrics timers (TaskQueueLogger.cs:20 / TaskProcessLogger.cs:22) ---
     queue_logger_period_s: float = field(default=30.0, metadata={"env": "AI4E_QUEUE_LOGGER_PERIOD_S"})
     process_logger_period_s: float = field(default=300.0, metadata={"env": "AI4E_PROCESS_LOGGER_PERIOD_S"})

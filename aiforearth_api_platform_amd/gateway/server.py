@@ -394,5 +394,12 @@ class Gateway:
             except ValueError:
                 pass
 
-    def run(self, host: str = "127.0.0.1", port: int = 8080) -> None:
-        web.run_app(self.app, host=host, port=port, handle_signals=False, print=None)
+    def run(self, host: str = "127.0.0.1", port: int = 8080, socks=None) -> None:
+        """Serve on (host, port), or on the given listening sockets (public SO_REUSEPORT socket shared with
+        the ingest front-ends + the internal socket they proxy to: serve.open_listeners)."""
+        # the drain (install_signal_handlers) already waited for in-flight work: do not hold the exit on idle
+        # keep-alive connections (e.g. the front-ends' proxy sessions) for aiohttp's default 60 s
+        if socks:
+            web.run_app(self.app, sock=socks, handle_signals=False, print=None, shutdown_timeout=2.0)
+        else:
+            web.run_app(self.app, host=host, port=port, handle_signals=False, print=None, shutdown_timeout=2.0)

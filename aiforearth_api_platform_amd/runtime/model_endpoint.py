@@ -26,69 +26,12 @@ import torch
 
 from ..store import STATE_CREATED, STATE_FAILED
 from .decode import PayloadError, decode_image  # noqa: F401  (re-exported: the endpoint's payload API)
+from .ingest import StreamedBatch
 from .serving import GpuBatchWorker
 
 PAYLOAD_LOST = "Task failed - payload lost on restart"
 PUBLISH_FAILED = "Failed - unable to send to backend service."
 _ORIG_PREFIX = "ai4e-b64:"
-
-
-class StreamedBatch:
-    """Ring slots of one streamed batch request; bytes land in slot order (one copy per chunk piece)."""
-
-    def __init__(self, ep: "ModelEndpoint", n: int, item: int, trace: str):
-        self.ep, self.n, self.item, self.trace = ep, n, item, trace
-        self.slots: List[int] = []
-        self.pos = 0
-        self._flat = ep.ring.buf.view(-1).numpy()
-
-    def try_alloc(self) -> bool:
-        """Non-blocking slot allocation (the event loop's fast path)."""
-        s = self.ep.ring.slots.alloc(self.n, 0.0) if hasattr(self.ep.ring, "slots") else None
-        if s:
-            self._set(s)
-        return bool(s)
-
-    def alloc(self, timeout: float = 60.0) -> None:
-        self._set(self.ep.ring.alloc(self.n, timeout=timeout))
-
-    def _set(self, slots: List[int]) -> None:
-        self.slots = list(slots)
-        # contiguous slot runs: (first logical byte, ring byte offset, bytes)
-        self.runs, i = [], 0
-        while i < self.n:
-            j = i + 1
-            while j < self.n and self.slots[j] == self.slots[j - 1] + 1:
-                j += 1
-            self.runs.append((i * self.item, self.slots[i] * self.item, (j - i) * self.item))
-            i = j
-        self._run = 0
-
-    def feed(self, chunk: bytes) -> None:
-        src = np.frombuffer(chunk, np.uint8)
-        off, m = 0, src.shape[0]
-        if self.pos + m > self.n * self.item:
-            raise PayloadError("batch payload longer than its Content-Length")
-        while off < m:
-            lo, ring_off, nb = self.runs[self._run]
-            k = min(m - off, lo + nb - self.pos)
-            dst = ring_off + self.pos - lo
-            self._flat[dst:dst + k] = src[off:off + k]
-            off += k
-            self.pos += k
-            if self.pos == lo + nb:
-                self._run += 1
-
-    def finish(self) -> List[str]:
-        if self.pos != self.n * self.item:
-            raise PayloadError(f"batch payload truncated ({self.pos} of {self.n * self.item} bytes)")
-        slots, self.slots = self.slots, []
-        return self.ep._enqueue(slots, self.trace)
-
-    def abort(self) -> None:
-        if self.slots:
-            self.ep.ring.free(self.slots)
-            self.slots = []
 
 
 class ModelEndpoint:

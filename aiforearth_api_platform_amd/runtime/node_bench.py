@@ -48,9 +48,10 @@ class Client:
             self.step()
 
 
-def http_phase(cp, pool, seconds: float, batch: int, item_shape, path: str) -> dict:
+def http_phase(cp, pool, seconds: float, batch: int, item_shape, path: str, frontends: int = 0) -> dict:
     """REST ingest on this node: aiohttp gateway (this process) + binary batch route (streamed into the
-    payload ring), then single-image requests; the clients run in separate processes."""
+    payload ring), then single-image requests; the clients run in separate processes. ``frontends``:
+    ingest front-end processes sharing the port (runtime/frontend.py; the pool needs as many partitions)."""
     import asyncio
 
     from aiohttp import web
@@ -67,14 +68,22 @@ def http_phase(cp, pool, seconds: float, batch: int, item_shape, path: str) -> d
     ready = threading.Event()
     box = {}
 
+    from .frontend import open_listeners, spawn_frontends
+
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    socks = open_listeners("127.0.0.1", port, shared=frontends > 0)
+
     def serve():
         loop = asyncio.new_event_loop()
         asyncio.set_event_loop(loop)
         runner = web.AppRunner(gw.app, access_log=None)
         loop.run_until_complete(runner.setup())
-        site = web.TCPSite(runner, "127.0.0.1", 0)
-        loop.run_until_complete(site.start())
-        box["port"] = site._server.sockets[0].getsockname()[1]
+        for sk in socks:
+            loop.run_until_complete(web.SockSite(runner, sk).start())
         box["loop"], box["runner"] = loop, runner
         ready.set()
         loop.run_forever()
@@ -83,7 +92,12 @@ def http_phase(cp, pool, seconds: float, batch: int, item_shape, path: str) -> d
     th = threading.Thread(target=serve, daemon=True)
     th.start()
     ready.wait(30)
-    url = f"http://127.0.0.1:{box['port']}/v1/bench/async"
+    fe = spawn_frontends(frontends, {"bench": ep}, [{"prefix": "/v1/bench/async", "mode": "async",
+                                                    "endpoint": "bench"}], "127.0.0.1", port,
+                         f"http://127.0.0.1:{socks[1].getsockname()[1]}") if frontends else []
+    if fe:
+        time.sleep(5.0)  # their interpreters start and bind the shared port
+    url = f"http://127.0.0.1:{port}/v1/bench/async"
     rng = np.random.default_rng(7)
     img = rng.integers(0, 256, tuple(item_shape), dtype=np.uint8)
     batch_body = np.broadcast_to(img, (batch, *img.shape)).tobytes()
@@ -106,11 +120,15 @@ def http_phase(cp, pool, seconds: float, batch: int, item_shape, path: str) -> d
         lat = wait_done(ids)
         dt = time.time() - t0
         out[name] = {"images": len(ids), "images_per_s": round(len(ids) / dt, 1), "connections": procs * conc,
-                     "client_processes": procs, "errors": errors,
+                     "client_processes": procs, "ingest_frontends": len(fe), "errors": errors,
                      "p50_task_latency_ms": round(percentile(lat, 50) * 1e3, 3),
                      "p99_task_latency_ms": round(percentile(lat, 99) * 1e3, 3)}
         if is_batch:
             out[name]["request_images"] = batch
+    for p in fe:
+        p.terminate()
+    for p in fe:
+        p.join(10)
     box["loop"].call_soon_threadsafe(box["loop"].stop)
     th.join(10)
     return out
@@ -149,7 +167,7 @@ def run_node_bench(args, spec, path: str, metric: str, unit: str = "images/s", c
         pool = WorkerPool(cp, endpoint, spec, [f"{args.device}:{denv.local_rank}" if args.device == "cuda" else "cpu"],
                           ring_slots=part, max_delay_s=0.0005, heartbeat_interval_s=hb, heartbeat_timeout_s=120.0,
                           remote_partitions=remote, pipeline_depth=int(os.environ.get("AI4E_PIPELINE_DEPTH", "3")),
-                          poll_s=0.005)
+                          poll_s=0.005, frontends=getattr(args, "http_frontends", 0) if args.http else 0)
         info = None
         listener = None
         if world > 1:
@@ -252,6 +270,9 @@ def run_node_bench(args, spec, path: str, metric: str, unit: str = "images/s", c
         if args.http and args.device == "cuda":
             try:
                 http = http_phase(cp, pool, args.http_seconds, B, spec.item_shape, path)
+                nfe = getattr(args, "http_frontends", 0)
+                if nfe:
+                    http["with_frontends"] = http_phase(cp, pool, args.http_seconds, B, spec.item_shape, path, nfe)
             except Exception as e:  # the headline number stands on its own
                 http = {"error": repr(e)}
         workers = [{k: w.get(k) for k in ("rank", "images", "batches", "pinned", "hbm_used", "gpu_busy_ms")}

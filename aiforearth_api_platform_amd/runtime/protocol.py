@@ -13,7 +13,7 @@ from typing import List, Sequence, Tuple
 
 import numpy as np
 
-F_READY, F_HB, F_DONE, F_BATCH, F_STOP, F_SUBMIT, F_FREE, F_STAGE = 1, 2, 3, 4, 5, 6, 7, 8
+F_READY, F_HB, F_DONE, F_BATCH, F_STOP, F_SUBMIT, F_FREE, F_STAGE, F_SUBMIT_IDS, F_SUBMITTED = range(1, 11)
 IT_OK, IT_INVALID, IT_ERROR, IT_RETRY = 0, 1, 2, 3
 
 _U32 = struct.Struct("<I")
@@ -23,6 +23,8 @@ _DONE_HDR = struct.Struct("<IQII5d")
 _BATCH_HDR = struct.Struct("<IQII")
 _SLOTS_HDR = struct.Struct("<III")
 _STAGE = struct.Struct("<IQII")
+_SUBMIT_IDS_HDR = struct.Struct("<IIIIIQ")
+_SUBMITTED = struct.Struct("<IQII")
 
 
 class FrameConn:
@@ -70,6 +72,15 @@ class FrameConn:
     def stage(self, bid: int, stage: int) -> None:
         self.send(_STAGE.pack(F_STAGE, bid, stage, 0))
 
+    def submit_ids(self, slots: Sequence[int], ids: Sequence[str], trace: str = "", token: int = 0,
+                   ack: bool = True) -> None:
+        """Ingest front-end: enqueue payloads under task ids minted here (all ids the same length)."""
+        a = np.asarray(slots, dtype=np.int64)
+        il = len(ids[0]) if ids else 0
+        tb = trace.encode()
+        self.send(b"".join((_SUBMIT_IDS_HDR.pack(F_SUBMIT_IDS, a.shape[0], len(tb), il, int(ack), token),
+                            a.tobytes(), "".join(ids).encode(), tb)))
+
 
 def frame_type(buf: bytes) -> int:
     return _U32.unpack_from(buf, 0)[0]
@@ -83,6 +94,12 @@ def parse_batch(buf: bytes) -> Tuple[int, np.ndarray]:
 def parse_slots(buf: bytes) -> np.ndarray:
     _, n, _ = _SLOTS_HDR.unpack_from(buf, 0)
     return np.frombuffer(buf, dtype=np.int64, count=n, offset=_SLOTS_HDR.size)
+
+
+def parse_submitted(buf: bytes) -> Tuple[int, int]:
+    """SUBMITTED -> (token, tasks created)."""
+    _, token, n, _ = _SUBMITTED.unpack_from(buf, 0)
+    return token, n
 
 
 def parse_ready_info(buf: bytes) -> dict:

@@ -115,12 +115,15 @@ class _WorkerHandle:
         return int(self.stats.get("images", 0))
 
 
+FRONTEND_RANK0 = 1 << 20  # scheduler connection ids of ingest front-ends (GPU worker ranks stay below)
+
+
 class WorkerPool:
     def __init__(self, control_plane, endpoint: str, spec: ModelSpec, devices: Sequence[str], ring_slots: int = 0,
                  max_delay_s: float = 0.0005, heartbeat_interval_s: float = 0.5, heartbeat_timeout_s: float = 10.0,
                  max_restarts: int = 2, pipeline_depth: int = 3, retry_delay_s: float = 1.0,
                  remote_partitions: Sequence[Tuple[int, int, int]] = (), completion_feed: bool = False,
-                 poll_s: float = 0.02):
+                 poll_s: float = 0.02, frontends: int = 0, frontend_slots: int = 0):
         if native is None:
             raise RuntimeError("the worker pool needs the native core (_ai4e_core)")
         self.cp = control_plane
@@ -136,6 +139,11 @@ class WorkerPool:
         # (ResNet-50 @250: 67.4-69.5k -> 75.7-77.7k images/s, p50 10.6 -> 9.1-9.4 ms; profiles/r2_pool/)
         local = ring_slots or spec.max_batch * (pipeline_depth + 2) * max(1, len(self.devices))
         self.remote_partitions = [tuple(int(v) for v in p) for p in remote_partitions]  # (base, len, rank)
+        # ingest front-end processes (runtime/frontend.py): one ring partition each, after everything else
+        end = max([local] + [b + n for b, n, _ in self.remote_partitions])
+        fs = frontend_slots or spec.max_batch * 4
+        self.frontend_partitions = [(end + i * fs, fs, FRONTEND_RANK0 + i) for i in range(int(frontends))]
+        self.remote_partitions += self.frontend_partitions
         total = max([local] + [b + n for b, n, _ in self.remote_partitions])
         self.ring = SharedPayloadRing(total, spec.item_shape, local_slots=local)
         self.hb_interval = heartbeat_interval_s
@@ -235,6 +243,14 @@ class WorkerPool:
             self.workers.append(w)
         self.sched.attach(rank, fd, True)
         self.events.append((time.time(), "attach", rank))
+
+    def attach_ingest(self, rank: int, conn) -> None:
+        """An ingest front-end process (its ring partition declared via ``frontends``): SUBMIT_IDS in,
+        SUBMITTED / FREE out; never given batches."""
+        fd = os.dup(conn.fileno())
+        conn.close()
+        self.sched.attach(rank, fd, False)
+        self.events.append((time.time(), "attach-ingest", rank))
 
     def _monitor_loop(self) -> None:
         while not self._stop.is_set():

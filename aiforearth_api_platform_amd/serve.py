@@ -42,6 +42,30 @@ def _devices(spec) -> list:
     return list(spec)
 
 
+from .runtime.frontend import open_listeners  # noqa: E402  (re-exported for the CLI)
+
+
+def frontend_count(cfg: Config) -> int:
+    """Ingest front-end processes to run (none while payloads are journaled: the journal is written by the
+    serving process's store, so those endpoints must ingest there)."""
+    return 0 if cfg.journal_path else max(0, int(cfg.frontend_processes))
+
+
+def start_frontends(cfg: Config, doc: Dict[str, Any], endpoints: Dict[str, Any], port: int, internal_port: int):
+    """Spawn the ingest front-end processes (runtime/frontend.py) for the platform's pool endpoints."""
+    from .runtime.frontend import spawn_frontends
+
+    pools = {name: ep for name, ep in endpoints.items() if getattr(ep, "is_pool", False)}
+    routes = []
+    for r in doc.get("routes") or []:
+        be = r.get("backend")
+        name = be.split(":", 1)[1] if isinstance(be, str) and be.startswith("inproc:") else None
+        routes.append({"prefix": r["prefix"], "rewrite": r.get("rewrite"), "mode": r.get("mode", "async"),
+                       "endpoint": name if name in pools else None, "content_types": r.get("content_types"),
+                       "max_content_length": r.get("max_content_length")})
+    return spawn_frontends(frontend_count(cfg), pools, routes, cfg.host, port, f"http://127.0.0.1:{internal_port}")
+
+
 def build_platform(doc: Dict[str, Any], cfg: Config):
     """Build (control_plane, gateway, endpoints, dispatchers) from a platform YAML document."""
     from .runtime.engine import InferenceEngine, PayloadRing
@@ -67,7 +91,8 @@ def build_platform(doc: Dict[str, Any], cfg: Config):
             pool = WorkerPool(cp, base_url + e["path"], spec, devs, max_delay_s=cfg.max_batch_delay_ms / 1e3,
                               heartbeat_interval_s=cfg.heartbeat_interval_s,
                               heartbeat_timeout_s=cfg.heartbeat_timeout_s,
-                              ring_slots=int(e.get("ring_slots", 0)))
+                              ring_slots=int(e.get("ring_slots", 0)), frontends=frontend_count(cfg),
+                              frontend_slots=int(e.get("frontend_ring_slots", cfg.frontend_ring_slots)))
             ep = ModelEndpoint(cp, e["path"], worker=pool, base_url=base_url,
                                decode_processes=int(e.get("decode_processes", cfg.decode_processes)))
         else:
@@ -138,11 +163,16 @@ def main(argv=None) -> int:
                                                     target_per_worker=cfg.autoscale_target_per_worker,
                                                     period_s=cfg.autoscale_period_s).start())
     gw.install_signal_handlers()
-    print(f"ai4e-mi355x gateway on http://{cfg.host}:{cfg.port} endpoints={list(endpoints)}", file=sys.stderr,
-          flush=True)
+    nfe = frontend_count(cfg)
+    socks = open_listeners(cfg.host, cfg.port, shared=nfe > 0)
+    frontends = start_frontends(cfg, doc, endpoints, cfg.port, socks[1].getsockname()[1]) if nfe else []
+    print(f"ai4e-mi355x gateway on http://{cfg.host}:{cfg.port} endpoints={list(endpoints)} "
+          f"ingest_frontends={len(frontends)}", file=sys.stderr, flush=True)
     try:
-        gw.run(cfg.host, cfg.port)
+        gw.run(cfg.host, cfg.port, socks=socks)
     finally:
+        for p in frontends:
+            p.terminate()
         for sc in scalers:
             sc.stop()
         for d in dispatchers:

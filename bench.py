@@ -59,6 +59,8 @@ def parse():
     p.add_argument("--device", default="cuda")
     p.add_argument("--http", type=int, default=1, help="also measure the REST ingest path (rank 0)")
     p.add_argument("--http-seconds", type=float, default=6.0)
+    p.add_argument("--http-frontends", type=int, default=4,
+                   help="also measure the REST ingest with this many ingest front-end processes (0 = skip)")
     p.add_argument("--json-out", default="")
     return p.parse_args()
 

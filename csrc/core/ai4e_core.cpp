@@ -71,6 +71,8 @@ PYBIND11_MODULE(_ai4e_core, m) {
            py::call_guard<py::gil_scoped_release>())
       .def("create_many", &TaskStore::create_many, py::arg("endpoint"), py::arg("n"), py::arg("status") = "created",
            py::arg("trace") = "", py::call_guard<py::gil_scoped_release>())
+      .def("create_ids", &TaskStore::create_ids, py::arg("endpoint"), py::arg("ids"), py::arg("status") = "created",
+           py::arg("trace") = "", py::call_guard<py::gil_scoped_release>())
       .def("transition_many", &TaskStore::transition_many, py::arg("ids"), py::arg("backend_status"),
            py::arg("status"), py::call_guard<py::gil_scoped_release>())
       .def("retarget_many", &TaskStore::retarget_many, py::arg("ids"), py::arg("endpoint"), py::arg("status"),

@@ -19,6 +19,10 @@
 //   STOP   (s->w)
 //   SUBMIT (w->s) u32 n, u32 0, i64 slots[n]      (a remote ingest shard enqueued n payloads)
 //   FREE   (s->w) u32 n, u32 0, i64 slots[n]      (slots of that shard's partition are free again)
+//   SUBMIT_IDS (w->s) u32 n, u32 trace_len, u32 id_len, u32 flags, u64 token, i64 slots[n],
+//          char ids[n][id_len], trace   (an ingest front-end process enqueued n payloads under task ids it
+//          minted; flags bit 0: answer with SUBMITTED once the tasks exist, so its HTTP reply never races them)
+//   SUBMITTED (s->w) u64 token, u32 n_created, u32 0
 //   STAGE  (w->s) u64 bid, u32 stage, u32 0        (ensemble hop: AddPipelineTask for the batch)
 //
 // Item status in DONE: 0 ok, 1 invalid payload (failed, not retried), 2 model error (failed,
@@ -61,7 +65,10 @@ inline bool cv_wait_s(std::condition_variable& cv, std::unique_lock<std::mutex>&
                        pred);
 }
 
-enum : uint32_t { F_READY = 1, F_HB = 2, F_DONE = 3, F_BATCH = 4, F_STOP = 5, F_SUBMIT = 6, F_FREE = 7, F_STAGE = 8 };
+enum : uint32_t {
+  F_READY = 1, F_HB = 2, F_DONE = 3, F_BATCH = 4, F_STOP = 5, F_SUBMIT = 6, F_FREE = 7, F_STAGE = 8, F_SUBMIT_IDS = 9,
+  F_SUBMITTED = 10
+};
 enum : uint8_t { IT_OK = 0, IT_INVALID = 1, IT_ERROR = 2, IT_RETRY = 3 };
 
 static const char* kFailInvalid = "Task failed - invalid payload";
@@ -392,6 +399,37 @@ class NodeScheduler {
     return ids;
   }
 
+  // SUBMIT_IDS: the front-end already answered its clients with these ids; a payload whose id could not be
+  // created (duplicate) or queued is dropped and its slot freed.
+  size_t enqueue_ids(std::vector<int64_t> slots, std::vector<std::string> ids, const std::string& trace) {
+    auto ok = store_->create_ids(endpoint_, ids, "created", trace);
+    std::vector<int64_t> drop;
+    size_t k = 0;
+    for (size_t i = 0; i < ids.size(); ++i) {
+      if (!ok[i]) {
+        drop.push_back(slots[i]);
+        continue;
+      }
+      if (k != i) {  // (a self move-assignment would empty the string)
+        ids[k] = std::move(ids[i]);
+        slots[k] = slots[i];
+      }
+      ++k;
+    }
+    ids.resize(k);
+    slots.resize(k);
+    free_slots(drop);
+    const size_t sent = queue_->send_many(ids, slots);
+    if (sent < ids.size()) {
+      std::vector<std::string> rest(ids.begin() + static_cast<long>(sent), ids.end());
+      std::vector<int64_t> rs(slots.begin() + static_cast<long>(sent), slots.end());
+      store_->transition_many(rest, "failed", kPublishFailed);
+      free_slots(rs);
+      feed(rest);
+    }
+    return ids.size();
+  }
+
   void feed(const std::vector<std::string>& ids) {
     {
       std::lock_guard<std::mutex> g(feed_mu_);
@@ -574,6 +612,34 @@ class NodeScheduler {
           std::vector<int64_t> slots(n);
           if (n) std::memcpy(slots.data(), p + 8, n * 8ull);
           enqueue(slots, std::string());
+          break;
+        }
+        case F_SUBMIT_IDS: {
+          if (len < 24) break;
+          uint32_t n, tl, il, flags;
+          uint64_t token;
+          std::memcpy(&n, p, 4);
+          std::memcpy(&tl, p + 4, 4);
+          std::memcpy(&il, p + 8, 4);
+          std::memcpy(&flags, p + 12, 4);
+          std::memcpy(&token, p + 16, 8);
+          if (len < 24 + n * (8ull + il) + tl) break;  // malformed: ignore
+          std::vector<int64_t> slots(n);
+          if (n) std::memcpy(slots.data(), p + 24, n * 8ull);
+          std::vector<std::string> ids(n);
+          const char* q = p + 24 + n * 8ull;
+          for (uint32_t i = 0; i < n; ++i) ids[i].assign(q + i * static_cast<size_t>(il), il);
+          const uint32_t created = static_cast<uint32_t>(
+              enqueue_ids(std::move(slots), std::move(ids), std::string(q + n * static_cast<size_t>(il), tl)));
+          if (flags & 1u) {
+            std::string ack(20, '\0');
+            const uint32_t t = F_SUBMITTED, z = 0;
+            std::memcpy(&ack[0], &t, 4);
+            std::memcpy(&ack[4], &token, 8);
+            std::memcpy(&ack[12], &created, 4);
+            std::memcpy(&ack[16], &z, 4);
+            send_frame(w, ack);
+          }
           break;
         }
         case F_STAGE: {

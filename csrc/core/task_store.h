@@ -190,6 +190,34 @@ class StoreShard {
     return ids;
   }
 
+  // create_many with ids minted by the caller (an ingest front-end process); an id already present is
+  // left untouched and reported as not created (ok[i] = 0).
+  std::vector<uint8_t> create_ids(const std::string& endpoint, const std::vector<std::string>& ids,
+                                  const std::string& status, const std::string& trace = std::string()) {
+    std::vector<uint8_t> ok(ids.size(), 0);
+    std::lock_guard<std::mutex> g(mu_);
+    const double wnow = wall_now(), mnow = mono_now();
+    PathIndex* p = path_index(absolute_path(endpoint));
+    auto st = std::make_shared<const std::string>(status);
+    auto ep = shared_endpoint(endpoint);
+    for (size_t i = 0; i < ids.size(); ++i) {
+      auto ins = recs_.try_emplace(ids[i]);
+      if (!ins.second) continue;
+      TaskRec& r = ins.first->second;
+      r.idp = &ins.first->first;
+      r.endpoint = ep;
+      r.status = st;
+      r.pub = true;
+      r.wall = wnow;
+      r.t_created = mnow;
+      r.trace = trace;
+      move_to(r, p, ST_CREATED, wnow, mnow);
+      journal_write(r, nullptr);
+      ok[i] = 1;
+    }
+    return ok;
+  }
+
   // Hot path: move tasks to running / completed / failed (any backend state) in one lock.
   size_t transition_many(const std::vector<std::string>& ids, const std::string& backend_status,
                          const std::string& status) {
@@ -613,6 +641,16 @@ class TaskStore {
   std::vector<std::string> create_many(const std::string& endpoint, size_t n, const std::string& status,
                                        const std::string& trace = std::string()) {
     return next_shard().create_many(endpoint, n, status, trace);
+  }
+
+  std::vector<uint8_t> create_ids(const std::string& endpoint, const std::vector<std::string>& ids,
+                                  const std::string& status, const std::string& trace = std::string()) {
+    std::vector<uint8_t> ok(ids.size(), 0);
+    for_groups(ids, [&](StoreShard& sh, const std::vector<std::string>& g, const std::vector<uint32_t>* pos) {
+      auto r = sh.create_ids(endpoint, g, status, trace);
+      for (size_t i = 0; i < r.size(); ++i) ok[pos ? (*pos)[i] : i] = r[i];
+    });
+    return ok;
   }
 
   size_t transition_many(const std::vector<std::string>& ids, const std::string& backend_status,

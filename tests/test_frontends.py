@@ -1,0 +1,81 @@
+"""Ingest front-end processes (runtime/frontend.py): the platform CLI with AI4E_FRONTEND_PROCESSES=2 —
+async POSTs over fresh connections land on the serving process or on a front-end (SO_REUSEPORT), every
+task completes and is visible through the task API (proxied to the serving process), batch ingest and
+sync routes work through any listener."""
+import os
+import subprocess
+import sys
+import time
+
+import numpy as np
+import requests
+
+from test_serve_e2e import ROOT, _port
+
+
+def test_frontend_processes_end_to_end():
+    port = _port()
+    env = dict(os.environ, PYTHONPATH=ROOT, AI4E_FRONTEND_PROCESSES="2")
+    proc = subprocess.Popen([sys.executable, "-m", "aiforearth_api_platform_amd.serve", "--config",
+                             os.path.join(ROOT, "examples", "platform_cpu.yaml"), "--port", str(port)],
+                            cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+    base = f"http://127.0.0.1:{port}"
+    try:
+        for _ in range(600):
+            try:
+                if requests.get(base + "/", timeout=1).status_code == 200:
+                    break
+            except requests.ConnectionError:
+                time.sleep(0.1)
+        else:
+            raise AssertionError("server did not come up")
+        time.sleep(3.0)  # the front-ends finish starting (they listen once their interpreters are up)
+        img = np.zeros((4, 4, 3), np.uint8)
+        img[..., 1] = 60
+        ids = []
+        for _ in range(60):  # a new connection per request: the kernel spreads them over the listeners
+            r = requests.post(base + "/v1/tiny/async", data=img.tobytes(),
+                              headers={"Content-Type": "application/octet-stream", "Connection": "close"})
+            assert r.status_code == 200, r.text
+            rec = r.json()
+            assert rec["BackendStatus"] == "created" and rec["EndpointPath"] == "/v1/ai4e/tiny/classify"
+            ids.append(rec["TaskId"])
+        batch = np.repeat(img[None], 5, axis=0)
+        r = requests.post(base + "/v1/tiny/async", data=batch.tobytes(),
+                          headers={"Content-Type": "application/x-ai4e-batch", "Connection": "close"})
+        assert r.status_code == 200
+        ids += r.json()["TaskIds"]
+        r = requests.post(base + "/v1/tiny/async", data=b"\x00" * 7, headers={"Content-Type": "application/octet-stream"})
+        assert r.status_code == 400
+        deadline = time.time() + 90
+        done = set()
+        while time.time() < deadline and len(done) < len(ids):
+            for t in ids:
+                if t not in done and requests.get(f"{base}/v1/taskmanagement/task/{t}").json()["BackendStatus"] == \
+                        "completed":
+                    done.add(t)
+            time.sleep(0.05)
+        assert len(done) == len(ids)
+        res = requests.get(f"{base}/v1/taskmanagement/task/{ids[-1]}/result").json()["Result"]
+        assert res["classes"][0] == 1
+        r = requests.post(base + "/v1/tiny/sync", data=img.tobytes(), headers={"Connection": "close"})
+        assert r.status_code == 200 and r.json()["classes"][0] == 1
+        assert "ingest_frontends=2" in _drain(proc)
+    finally:
+        proc.terminate()
+        try:
+            proc.wait(20)
+        except subprocess.TimeoutExpired:
+            proc.kill()
+
+
+def _drain(proc) -> str:
+    import select
+
+    out = b""
+    while select.select([proc.stdout], [], [], 0.1)[0]:
+        chunk = os.read(proc.stdout.fileno(), 65536)
+        if not chunk:
+            break
+        out += chunk
+    return out.decode(errors="replace")
