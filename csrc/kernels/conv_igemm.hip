@@ -348,8 +348,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC > 2 ? O
     if (p.gnp && pass == 0) {
       // GN shift per channel slot: the tile's first pixel (row 0, unswizzled) at the group's first channel
       const int cg = p.Kout / p.gn_groups;
+      const int c8 = 8 * (tid % CPR);
+      if ((cg & (cg - 1)) == 0) {  // power-of-two group width (every model here): mask, no division
 #pragma unroll
-      for (int k = 0; k < 8; ++k) gk[k] = fmaxf(tile[(8 * (tid % CPR) + k) / cg * cg], lo);
+        for (int k = 0; k < 8; ++k) gk[k] = fmaxf(tile[(c8 + k) & -cg], lo);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) gk[k] = fmaxf(tile[(c8 + k) / cg * cg], lo);
+      }
       if (tid < BN / cg) kout = fmaxf(tile[tid * cg], lo);
     }
 #pragma unroll

@@ -91,60 +91,69 @@ __global__ __launch_bounds__(256) void gn_stats_kernel(const uint16_t* __restric
 // b = beta_c - mean_g * a. (Done once per image instead of in every normalize workgroup.) Chunk k holds
 // chunk_px pixels (the last one possibly fewer); its shifted sums are re-based on chunk 0's shift K0:
 // sum(x - K0) = S + n d, sum((x - K0)^2) = Q + 2 d S + n d^2 with d = K - K0.
-__global__ __launch_bounds__(256) void gn_finalize_kernel(const float* __restrict__ partials,
-                                                          const float* __restrict__ gamma,
-                                                          const float* __restrict__ beta, float2* __restrict__ ss,
-                                                          int HW, int C, int G, float eps, int nchunks, int chunk_px) {
+constexpr int GN_FIN_THREADS = 512;
+constexpr int GN_FIN_GROUPS = 8;  // groups per finalize workgroup (gridDim.y = G / 8 when it divides)
+
+// One workgroup per (image, slice of GL groups): reading an image's partials is per-CU-bandwidth bound, so the
+// groups of an image are spread over several workgroups (groups are independent).
+__global__ __launch_bounds__(GN_FIN_THREADS) void gn_finalize_kernel(const float* __restrict__ partials,
+                                                                     const float* __restrict__ gamma,
+                                                                     const float* __restrict__ beta,
+                                                                     float2* __restrict__ ss, int HW, int C, int G,
+                                                                     float eps, int nchunks, int chunk_px) {
   const int n = blockIdx.x;
-  // thread t owns group t % G and every (256/G)-th chunk from t / G
-  __shared__ double red_s[256], red_q[256];
+  const int GL = G / gridDim.y;      // groups of this workgroup
+  const int g0 = blockIdx.y * GL;
+  __shared__ double red_s[GN_FIN_THREADS], red_q[GN_FIN_THREADS];
   __shared__ float mean_s[64], rstd_s[64];
-  const int lpg = 256 / G;  // threads per group (G <= 64 divides 256 only when a power of two; else some idle)
-  const int g = threadIdx.x % G, l = threadIdx.x / G;
+  const int lpg = GN_FIN_THREADS / GL;  // threads per group (GL <= 64; a GL that does not divide leaves some idle)
+  const int gl = threadIdx.x % GL, l = threadIdx.x / GL;
   const int cg = C / G;
-  const float4* pp = reinterpret_cast<const float4*>(partials) + static_cast<long>(n) * nchunks * G + g;
+  const float4* pp = reinterpret_cast<const float4*>(partials) + static_cast<long>(n) * nchunks * G + g0 + gl;
   const double k0 = pp[0].z;
   double s0 = 0, q0 = 0;
   if (l < lpg) {
-    // 4 independent loads in flight per lane: with one workgroup per image the pass is latency-bound
-    for (int k = l; k < nchunks; k += 4 * lpg) {
-      float4 v[4];
+    // 8 independent loads in flight per lane
+    for (int k = l; k < nchunks; k += 8 * lpg) {
+      float4 v[8];
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
+      for (int u = 0; u < 8; ++u)
         if (k + u * lpg < nchunks) v[u] = pp[static_cast<long>(k + u * lpg) * G];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < 8; ++u) {
         const int kk = k + u * lpg;
         if (kk >= nchunks) break;
         const double cnt = static_cast<double>(min(chunk_px, HW - kk * chunk_px)) * cg;
         const double d = static_cast<double>(v[u].z) - k0;
         s0 += v[u].x + cnt * d;
-        q0 += v[u].y + 2.0 * d * v[u].x + cnt * d * d;
+        q0 += v[u].y + (2.0 * v[u].x + cnt * d) * d;
       }
     }
   }
   red_s[threadIdx.x] = s0;
   red_q[threadIdx.x] = q0;
   __syncthreads();
-  if (static_cast<int>(threadIdx.x) < G) {
+  if (static_cast<int>(threadIdx.x) < GL) {
     double s = 0, q = 0;
     for (int k = 0; k < lpg; ++k) {
-      s += red_s[k * G + threadIdx.x];
-      q += red_q[k * G + threadIdx.x];
+      s += red_s[k * GL + threadIdx.x];
+      q += red_q[k * GL + threadIdx.x];
     }
     const double cnt = static_cast<double>(HW) * cg;
     const double m = s / cnt;  // mean relative to K0
     const double var = fmax(q / cnt - m * m, 0.0);
-    mean_s[threadIdx.x] = static_cast<float>(pp[0].z + m);
+    mean_s[threadIdx.x] = static_cast<float>(k0 + m);
     rstd_s[threadIdx.x] = static_cast<float>(1.0 / sqrt(var + eps));
   }
   __syncthreads();
-  for (int c = threadIdx.x; c < C; c += 256) {
-    const int gc = c / cg;
-    const float a = rstd_s[gc] * gamma[c];
-    ss[static_cast<long>(n) * C + c] = make_float2(a, beta[c] - mean_s[gc] * a);
+  for (int c = threadIdx.x; c < GL * cg; c += GN_FIN_THREADS) {
+    const int cc = g0 * cg + c;
+    const float a = rstd_s[c / cg] * gamma[cc];
+    ss[static_cast<long>(n) * C + cc] = make_float2(a, beta[cc] - mean_s[c / cg] * a);
   }
 }
+
+inline dim3 gn_finalize_grid(int N, int G) { return dim3(N, G % GN_FIN_GROUPS == 0 ? G / GN_FIN_GROUPS : 1); }
 
 // y = x * a_c + b_c (+ReLU), 16-B vectors. C8 = C/8 divides 256, so with a grid stride that is a multiple of
 // 256 every lane keeps one 8-channel column: its 8 affine pairs load once, the loop is unpack + FMA + cvt.
@@ -314,7 +323,7 @@ AI4E_API int ai4e_groupnorm_nhwc(const void* x, void* y, const void* gamma, cons
                      static_cast<float*>(partials), HW, C, G, ldx, xcoff, nchunks);
   float2* ss =
       reinterpret_cast<float2*>(static_cast<float*>(partials) + static_cast<long>(N) * nchunks * G * GN_PARTIAL);
-  hipLaunchKernelGGL(gn_finalize_kernel, dim3(N), dim3(256), 0, s, static_cast<const float*>(partials),
+  hipLaunchKernelGGL(gn_finalize_kernel, gn_finalize_grid(N, G), dim3(GN_FIN_THREADS), 0, s, static_cast<const float*>(partials),
                      static_cast<const float*>(gamma), static_cast<const float*>(beta), ss, HW, C, G, eps, nchunks,
                      GN_PIX_PER_BLOCK);
   // ~4 vectors per lane; at most 8192 workgroups per image
@@ -339,7 +348,7 @@ AI4E_API int ai4e_groupnorm_apply_nhwc(const void* x, void* y, const void* gamma
   if (HW % nchunks) return AI4E_EINVAL;  // conv-epilogue partials: whole tiles per image
   float2* ss =
       reinterpret_cast<float2*>(static_cast<float*>(partials) + static_cast<long>(N) * nchunks * G * GN_PARTIAL);
-  hipLaunchKernelGGL(gn_finalize_kernel, dim3(N), dim3(256), 0, s, static_cast<const float*>(partials),
+  hipLaunchKernelGGL(gn_finalize_kernel, gn_finalize_grid(N, G), dim3(GN_FIN_THREADS), 0, s, static_cast<const float*>(partials),
                      static_cast<const float*>(gamma), static_cast<const float*>(beta), ss, HW, C, G, eps, nchunks,
                      HW / nchunks);
   const int gx = grid_for(static_cast<long>(HW) * (C / 8) / 4 + 1);
@@ -363,7 +372,7 @@ AI4E_API int ai4e_groupnorm_apply_pool_nhwc(const void* x, void* y, const void* 
   if (HW % nchunks) return AI4E_EINVAL;  // conv-epilogue partials: whole tiles per image
   float2* ss =
       reinterpret_cast<float2*>(static_cast<float*>(partials) + static_cast<long>(N) * nchunks * G * GN_PARTIAL);
-  hipLaunchKernelGGL(gn_finalize_kernel, dim3(N), dim3(256), 0, s, static_cast<const float*>(partials),
+  hipLaunchKernelGGL(gn_finalize_kernel, gn_finalize_grid(N, G), dim3(GN_FIN_THREADS), 0, s, static_cast<const float*>(partials),
                      static_cast<const float*>(gamma), static_cast<const float*>(beta), ss, HW, C, G, eps, nchunks,
                      HW / nchunks);
   const int gx = grid_for(static_cast<long>(HW / 4) * (C / 8) / 2 + 1);
