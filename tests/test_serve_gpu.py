@@ -111,3 +111,85 @@ def test_classify_detect_landcover_ensemble_over_http(platform):
     # per-task stage trace from the worker process
     tr = out["trace"]
     assert tr["t_worker_done"] >= tr["t_worker_launch"] > 0 and "durations_ms" in tr
+
+
+def test_ingest_frontends_gpu():
+    """Ingest front-end processes (runtime/frontend.py) in front of a GPU pool endpoint: POSTs over fresh
+    connections are spread over the serving process and 2 front-ends (SO_REUSEPORT); every task completes
+    on the GPU with the same top-5 as the serving process's own ingest path."""
+    import socket
+    import threading
+    import time
+
+    import requests
+    from aiohttp import web
+
+    from aiforearth_api_platform_amd.config import Config
+    from aiforearth_api_platform_amd.runtime.frontend import open_listeners
+    from aiforearth_api_platform_amd.serve import build_platform, start_frontends
+
+    with open(os.path.join(ROOT, "examples", "platform_gpu_small.yaml")) as f:
+        full = yaml.safe_load(f)
+    doc = {"settings": dict(full.get("settings") or {}, frontend_processes=2),
+           "endpoints": {"resnet50": full["endpoints"]["resnet50"]},
+           "routes": [r for r in full["routes"] if r.get("backend") == "inproc:resnet50"]}
+    cfg = Config.load(env={}, yaml_values=doc["settings"])
+    cp, gw, endpoints, _ = build_platform(doc, cfg)
+    for ep in endpoints.values():
+        ep.start()
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    socks = open_listeners("127.0.0.1", port, shared=True)
+    box = {}
+
+    def serve():
+        loop = asyncio.new_event_loop()
+        runner = web.AppRunner(gw.app, access_log=None)
+        loop.run_until_complete(runner.setup())
+        for sk in socks:
+            loop.run_until_complete(web.SockSite(runner, sk).start())
+        box["loop"] = loop
+        loop.run_forever()
+        loop.run_until_complete(runner.cleanup())
+
+    th = threading.Thread(target=serve, daemon=True)
+    th.start()
+    cfg.host = "127.0.0.1"
+    fe = start_frontends(cfg, doc, endpoints, port, socks[1].getsockname()[1])
+    try:
+        assert len(fe) == 2
+        time.sleep(8.0)  # front-end interpreters start and bind
+        route = next(r["prefix"] for r in doc["routes"] if r.get("mode", "async") == "async")
+        img = np.random.default_rng(3).integers(0, 256, (224, 224, 3), dtype=np.uint8)
+        ids = []
+        for _ in range(24):
+            r = requests.post(f"http://127.0.0.1:{port}{route}", data=img.tobytes(),
+                              headers={"Content-Type": "application/octet-stream", "Connection": "close"}, timeout=60)
+            assert r.status_code == 200, r.text
+            ids.append(r.json()["TaskId"])
+        deadline = time.time() + 120
+        results = {}
+        while time.time() < deadline and len(results) < len(ids):
+            for t in ids:
+                if t in results:
+                    continue
+                rec = requests.get(f"http://127.0.0.1:{port}/v1/taskmanagement/task/{t}", timeout=30).json()
+                if rec["BackendStatus"] == "completed":
+                    results[t] = requests.get(f"http://127.0.0.1:{port}/v1/taskmanagement/task/{t}/result",
+                                              timeout=30).json()["Result"]
+            time.sleep(0.05)
+        assert len(results) == len(ids)
+        classes = {tuple(r["classes"]) for r in results.values()}
+        assert len(classes) == 1  # the same image -> the same top-5 whichever process ingested it
+    finally:
+        for p in fe:
+            p.terminate()
+        for p in fe:
+            p.join(10)
+        if "loop" in box:
+            box["loop"].call_soon_threadsafe(box["loop"].stop)
+        th.join(10)
+        for ep in endpoints.values():
+            ep.stop()
+        cp.close()
