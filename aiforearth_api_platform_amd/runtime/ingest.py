@@ -108,6 +108,7 @@ class IngestShard:
         self._amu = threading.Lock()
         self._shard = itertools.count()
         self._on_close = on_close  # called once the scheduler connection is gone (the serving process exited)
+        self._closing = False
         self.ring = self  # StreamedBatch's view of an endpoint
         self._reader = threading.Thread(target=self._read_loop, daemon=True, name="ai4e-ingest-reader")
         self._reader.start()
@@ -150,8 +151,8 @@ class IngestShard:
         while True:
             try:
                 buf = self.fc.recv()
-            except (EOFError, OSError):
-                if self._on_close is not None:
+            except (EOFError, OSError, TypeError, ValueError):  # (the last two: closed under us by close())
+                if self._on_close is not None and not self._closing:
                     self._on_close()
                 return
             t = P.frame_type(buf)
@@ -167,6 +168,7 @@ class IngestShard:
                 return
 
     def close(self) -> None:
+        self._closing = True
         self.fc.close()
         self.slots.close()
         del self.buf

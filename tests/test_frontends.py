@@ -79,3 +79,46 @@ def _drain(proc) -> str:
             break
         out += chunk
     return out.decode(errors="replace")
+
+
+def test_submit_ids_protocol_in_process():
+    """SUBMIT_IDS over an ingest connection (the front-end side run in-process): tasks are created under the
+    caller's ids and acknowledged with the created count, a duplicate id is dropped with its slot, and every
+    slot of the partition comes back (FREE) once the tasks finish."""
+    import multiprocessing as mp
+
+    from aiforearth_api_platform_amd.config import Config
+    from aiforearth_api_platform_amd.gateway.control import ControlPlane
+    from aiforearth_api_platform_amd.runtime.ingest import IngestShard
+    from aiforearth_api_platform_amd.runtime.worker_pool import ModelSpec, WorkerPool
+
+    shape = (4, 4, 3)
+    spec = ModelSpec("aiforearth_api_platform_amd.models.toy:tiny_classifier", shape, max_batch=8, topk=2,
+                     use_graphs=False)
+    cp = ControlPlane(Config.load(env={}))
+    ep = "http://127.0.0.1/v1/fe/classify"
+    pool = WorkerPool(cp, ep, spec, ["cpu"], max_delay_s=0.001, frontends=1, frontend_slots=16).start(120)
+    base, length, rank = pool.frontend_partitions[0]
+    a, b = mp.Pipe(duplex=True)
+    pool.attach_ingest(rank, a)
+    shard = IngestShard(b, ep, pool.ring.name, pool.ring.nslots, shape, base, length)
+    try:
+        slots = shard.alloc(5)
+        assert all(base <= s < base + length for s in slots)
+        for i, s in enumerate(slots):
+            img = np.zeros(shape, np.uint8)
+            img[..., i % 3] = 80
+            shard.write(s, img)
+        ids = shard.mint_ids(4)
+        ids.append(ids[0])  # duplicate: dropped by the scheduler, its slot freed
+        assert shard.submit_ids(slots, ids, "").wait(30) == 4
+        deadline = time.time() + 60
+        while time.time() < deadline and (cp.store.zcard("/v1/fe/classify_completed") < 4 or shard.slots.used()):
+            time.sleep(0.05)
+        assert cp.store.zcard("/v1/fe/classify_completed") == 4
+        assert shard.slots.used() == 0  # FREE frames returned every slot of the partition
+        assert [pool.result(t)["classes"][0] for t in ids[:3]] == [0, 1, 2]
+    finally:
+        shard.close()
+        pool.stop()
+        cp.close()
