@@ -295,6 +295,52 @@ __global__ __launch_bounds__(256) void roi_align_fpn_kernel(FpnLevels lv, const 
   }
 }
 
+// Same op, one workgroup per RoI (PW * C/8 <= 256 lanes, one (pw, 8-channel chunk) each) walking the output
+// rows in order: the sample rows of bin row ph and ph+1 share feature rows, and with the whole RoI on one CU
+// those re-reads hit its L1 instead of going to L2 from 7 different CUs (the per-row grid's pattern).
+__global__ __launch_bounds__(256) void roi_align_fpn_roi_kernel(FpnLevels lv, const float* __restrict__ rois,
+                                                                uint16_t* __restrict__ out, int C, int R, int PH,
+                                                                int PW, int sampling, int aligned) {
+  const int C8 = C >> 3;
+  const int r = blockIdx.x;
+  const float* roi = rois + 5L * r;
+  const float area = fmaxf(roi[3] - roi[1], 0.f) * fmaxf(roi[4] - roi[2], 0.f);
+  int l = static_cast<int>(floorf(4.f + log2f(sqrtf(area) / 224.f + 1e-6f)));
+  l = min(max(l, 2), 5) - 2;
+  const int H = lv.h[l], W = lv.w[l];
+  const float scale = lv.scale[l];
+  const int img = static_cast<int>(roi[0]);
+  const float off = aligned ? 0.5f : 0.f;
+  const float x1 = roi[1] * scale - off, y1 = roi[2] * scale - off;
+  float rw = roi[3] * scale - off - x1, rh = roi[4] * scale - off - y1;
+  if (!aligned) {
+    rw = fmaxf(rw, 1.f);
+    rh = fmaxf(rh, 1.f);
+  }
+  const float bh = rh / PH, bw = rw / PW;
+  const int gh = sampling > 0 ? sampling : static_cast<int>(ceilf(rh / PH));
+  const int gw = sampling > 0 ? sampling : static_cast<int>(ceilf(rw / PW));
+  const float inv = 1.f / fmaxf(gh * gw, 1);
+  const uint16_t* f = lv.f[l] + static_cast<long>(img) * H * W * C;
+  const int t = threadIdx.x;
+  if (t >= PW * C8) return;
+  const int pw = t / C8, c8 = t - pw * C8;
+  uint16_t* o = out + static_cast<long>(r) * PH * PW * C + static_cast<long>(pw) * C + 8 * c8;
+  for (int ph = 0; ph < PH; ++ph) {
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int iy = 0; iy < gh; ++iy) {
+      const float y = y1 + ph * bh + (iy + 0.5f) * bh / gh;
+      for (int ix = 0; ix < gw; ++ix) {
+        const float x = x1 + pw * bw + (ix + 0.5f) * bw / gw;
+        bilinear_acc8(f, H, W, C, y, x, c8, inv, acc);
+      }
+    }
+    *reinterpret_cast<uint4*>(o + static_cast<long>(ph) * PW * C) =
+        make_uint4(pack_bf16x2(acc[0], acc[1]), pack_bf16x2(acc[2], acc[3]), pack_bf16x2(acc[4], acc[5]),
+                   pack_bf16x2(acc[6], acc[7]));
+  }
+}
+
 // Crop + bilinear resize + normalize: uint8 image [N, H, W, C<=8], boxes [R, 5] = (img, x1, y1, x2, y2)
 // in pixels -> bf16 [R, OH, OW, 8] normalized (classifier stem input). norm = mean[8] ++ std[8].
 __global__ __launch_bounds__(256) void crop_resize_kernel(const uint8_t* __restrict__ img, const float* __restrict__ boxes,
@@ -437,8 +483,16 @@ AI4E_API int ai4e_roi_align_fpn_nhwc(const void* f0, const void* f1, const void*
     lv.scale[i] = scales[i];
   }
   if (static_cast<long>(R) * PH >= (1L << 31)) return AI4E_EINVAL;
-  hipLaunchKernelGGL(roi_align_fpn_kernel, dim3(static_cast<unsigned>(R * PH)), dim3(256), 0, s,
-                     lv, static_cast<const float*>(rois), static_cast<uint16_t*>(out), C, R, PH, PW, sampling, aligned);
+  static const int per_roi = [] {
+    const char* e = getenv("AI4E_ROI_PER_ROI");  // A/B switch: 0 = one workgroup per (RoI, output row)
+    return e ? atoi(e) : 1;
+  }();
+  if (per_roi && PW * (C / 8) <= 256)
+    hipLaunchKernelGGL(roi_align_fpn_roi_kernel, dim3(static_cast<unsigned>(R)), dim3(256), 0, s, lv,
+                       static_cast<const float*>(rois), static_cast<uint16_t*>(out), C, R, PH, PW, sampling, aligned);
+  else
+    hipLaunchKernelGGL(roi_align_fpn_kernel, dim3(static_cast<unsigned>(R * PH)), dim3(256), 0, s,
+                       lv, static_cast<const float*>(rois), static_cast<uint16_t*>(out), C, R, PH, PW, sampling, aligned);
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
 }
 
