@@ -29,12 +29,10 @@ import asyncio
 import json
 import signal
 from dataclasses import dataclass, field
-from typing import Any, Callable, Dict, List, Optional, Union
+from typing import Any, Dict, List, Optional
 
 from aiohttp import ClientSession, web
 
-from ..store import APITask
-from ..store.pystore import absolute_path
 from ..utils.metrics import REGISTRY
 from ..utils.tracing import StageClock, b3_from_headers, b3_pack, b3_unpack
 from .control import ControlPlane

@@ -16,7 +16,6 @@ not journaled are failed with a reason instead of being requeued without a paylo
 from __future__ import annotations
 
 import base64
-import io
 import json
 import threading
 from typing import Callable, Dict, List, Optional, Sequence, Tuple

@@ -15,7 +15,7 @@ import json
 import os
 import threading
 import time
-from typing import Callable, Optional
+from typing import Optional
 
 import numpy as np
 import torch
