@@ -167,7 +167,8 @@ def run_node_bench(args, spec, path: str, metric: str, unit: str = "images/s", c
         pool = WorkerPool(cp, endpoint, spec, [f"{args.device}:{denv.local_rank}" if args.device == "cuda" else "cpu"],
                           ring_slots=part, max_delay_s=0.0005, heartbeat_interval_s=hb, heartbeat_timeout_s=120.0,
                           remote_partitions=remote, pipeline_depth=int(os.environ.get("AI4E_PIPELINE_DEPTH", "3")),
-                          poll_s=0.005, frontends=getattr(args, "http_frontends", 0) if args.http else 0)
+                          poll_s=0.005, frontends=getattr(args, "http_frontends", 0) if args.http else 0,
+                          frontend_slots=2 * B)  # (REST phase only: keep the pinned ring small)
         info = None
         listener = None
         if world > 1:
