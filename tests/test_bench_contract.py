@@ -52,11 +52,16 @@ def test_bench_single_process_cpu():
     _check(lines[0], 1)
 
 
-def test_bench_torchrun_two_ranks_gloo():
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
-           "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2"] + ARGS
-    r = subprocess.run(cmd, cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=300)
+@pytest.mark.parametrize("world", [2, 4])
+def test_bench_torchrun_ranks_gloo(world):
+    """The driver's multi-GPU launch shape (torchrun, one rank per device; rank 0 = node scheduler, the other
+    ranks attach as workers + ingest shards) with gloo on CPU ranks."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", str(world)] + ARGS
+    env = dict(_env(), OMP_NUM_THREADS="1")
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = _json_lines(r.stdout)
     assert len(lines) == 1, r.stdout  # rank 0 only
-    _check(lines[0], 2)
+    _check(lines[0], world)
+    assert len(lines[0]["workers"]) == world and sum(w["images"] for w in lines[0]["workers"]) == 2 * world * 3
