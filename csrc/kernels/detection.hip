@@ -326,6 +326,62 @@ __global__ __launch_bounds__(256) void roi_align_fpn_roi_kernel(FpnLevels lv, co
   if (t >= PW * C8) return;
   const int pw = t / C8, c8 = t - pw * C8;
   uint16_t* o = out + static_cast<long>(r) * PH * PW * C + static_cast<long>(pw) * C + 8 * c8;
+  if (gh == 2 && gw == 2) {
+    // sampling 2 (the box head's setting): per output row, the 4 samples' 16 corner offsets and weights first
+    // (out-of-range samples get weight 0 instead of a branch), then all 16 loads in flight, then the FMAs
+    int xo[2][2];
+    float xw[2][2];
+    bool xok[2];
+#pragma unroll
+    for (int ix = 0; ix < 2; ++ix) {
+      float x = x1 + pw * bw + (ix + 0.5f) * bw * 0.5f;
+      xok[ix] = !(x < -1.f || x > W);
+      x = fmaxf(x, 0.f);
+      int x0 = static_cast<int>(x), x1i;
+      if (x0 >= W - 1) { x1i = x0 = W - 1; x = static_cast<float>(x0); } else { x1i = x0 + 1; }
+      const float lx = x - x0;
+      xo[ix][0] = x0 * C + 8 * c8;
+      xo[ix][1] = x1i * C + 8 * c8;
+      xw[ix][0] = 1.f - lx;
+      xw[ix][1] = lx;
+    }
+    for (int ph = 0; ph < PH; ++ph) {
+      long ro[2][2];
+      float yw[2][2];
+#pragma unroll
+      for (int iy = 0; iy < 2; ++iy) {
+        float y = y1 + ph * bh + (iy + 0.5f) * bh * 0.5f;
+        const bool yok = !(y < -1.f || y > H);
+        y = fmaxf(y, 0.f);
+        int y0 = static_cast<int>(y), y1i;
+        if (y0 >= H - 1) { y1i = y0 = H - 1; y = static_cast<float>(y0); } else { y1i = y0 + 1; }
+        const float ly = y - y0;
+        ro[iy][0] = static_cast<long>(y0) * W * C;
+        ro[iy][1] = static_cast<long>(y1i) * W * C;
+        yw[iy][0] = yok ? (1.f - ly) * inv : 0.f;
+        yw[iy][1] = yok ? ly * inv : 0.f;
+      }
+      uint4 v[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q)  // q = ((iy * 2 + ix) * 2 + cy) * 2 + cx
+        v[q] = *reinterpret_cast<const uint4*>(f + ro[q >> 3][(q >> 1) & 1] + xo[(q >> 2) & 1][q & 1]);
+      float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int iy = q >> 3, ix = (q >> 2) & 1, cy = (q >> 1) & 1, cx = q & 1;
+        const float w = xok[ix] ? yw[iy][cy] * xw[ix][cx] : 0.f;
+        float a, b;
+        unpack_bf16x2(v[q].x, a, b); acc[0] += w * a; acc[1] += w * b;
+        unpack_bf16x2(v[q].y, a, b); acc[2] += w * a; acc[3] += w * b;
+        unpack_bf16x2(v[q].z, a, b); acc[4] += w * a; acc[5] += w * b;
+        unpack_bf16x2(v[q].w, a, b); acc[6] += w * a; acc[7] += w * b;
+      }
+      *reinterpret_cast<uint4*>(o + static_cast<long>(ph) * PW * C) =
+          make_uint4(pack_bf16x2(acc[0], acc[1]), pack_bf16x2(acc[2], acc[3]), pack_bf16x2(acc[4], acc[5]),
+                     pack_bf16x2(acc[6], acc[7]));
+    }
+    return;
+  }
   for (int ph = 0; ph < PH; ++ph) {
     float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (int iy = 0; iy < gh; ++iy) {
