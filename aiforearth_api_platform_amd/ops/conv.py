@@ -200,8 +200,8 @@ def conv2d_gn_nhwc(x: torch.Tensor, pc: PackedConv, groups: int, out: Optional[t
     n, h, w, c = x.shape
     oh, ow = pc.out_hw(h, w)
     cfg = tuned_tile(pc, n, h, w, False) or (2 if pc.cout <= 64 else 1)
-    bm, bn = (256, 64) if cfg in (2, 5) else (128, 128)
-    ok = (_ext.backend_for(x) == "hip" and cfg in (1, 2, 4, 5) and groups > 0 and pc.cout % groups == 0
+    bm, bn = (256, 64) if cfg in (2, 5, 8) else (128, 128)
+    ok = (_ext.backend_for(x) == "hip" and cfg in (1, 2, 4, 5, 7, 8) and groups > 0 and pc.cout % groups == 0
           and (oh * ow) % bm == 0 and pc.cout % 8 == 0 and bn % (pc.cout // groups) == 0 and out_coff % 8 == 0
           and (out is None or out.stride(2) % 8 == 0) and x.dtype == torch.bfloat16 and c == pc.cin_pad)
     if not ok:

@@ -880,7 +880,7 @@ AI4E_API int ai4e_conv2d_fwd(const void* x, const void* w, const void* bias, con
 
 // Same conv, plus the GroupNorm statistics of its output (gn_groups groups over Kout channels) written as
 // per-(image, tile-row chunk, group) shifted partial sums (sum(x - K), sum((x - K)^2), K, pad) into gn_partials
-// [N, OH*OW / BM, gn_groups, 4] fp32 (BM = 256 for tile configs 2 and 5, else 128). Configs 3 and 6 and
+// [N, OH*OW / BM, gn_groups, 4] fp32 (BM = 256 for tile configs 2, 5 and 8, else 128). Configs 3, 6 and 9 and
 // shapes whose tiles would straddle images are refused (EINVAL) before anything is launched.
 AI4E_API int ai4e_conv2d_gn_fwd(const void* x, const void* w, const void* bias, const void* res, void* y, int N,
                                 int H, int W, int C, int ldx, int xcoff, int KH, int KW, int stride, int pad, int OH,

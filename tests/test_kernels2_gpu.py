@@ -218,7 +218,7 @@ def test_det_decode_matches_reference(B, R, nc):
     assert ref[0].shape == b1.shape
 
 
-@pytest.mark.parametrize("cfg", [1, 2, 4, 5])
+@pytest.mark.parametrize("cfg", [1, 2, 4, 5, 7, 8])
 @pytest.mark.parametrize("shape", [(2, 32, 32, 64, 64, 32), (3, 16, 16, 64, 128, 32), (1, 16, 32, 128, 256, 16)])
 def test_conv_fused_groupnorm_stats(cfg, shape, monkeypatch):
     """GroupNorm statistics from the conv epilogue (conv2d_gn_nhwc -> group_norm_nhwc(stats=...)) == the
