@@ -29,7 +29,7 @@ import asyncio
 import json
 import signal
 from dataclasses import dataclass, field
-from typing import Any, Dict, List, Optional
+from typing import Any, Callable, Dict, List, Optional
 
 from aiohttp import ClientSession, web
 
@@ -99,6 +99,7 @@ class Gateway:
         self.webhook = webhook
         self.base_url = base_url.rstrip("/")
         self.is_terminating = False
+        self.on_drain: List[Callable[[], None]] = []
         self._session: Optional[ClientSession] = None
         self.app = web.Application(client_max_size=1 << 30)
         self.app.router.add_get("/", self.health)
@@ -384,6 +385,11 @@ class Gateway:
         def drain(*_):
             if not self.is_terminating:
                 self.is_terminating = True
+                for hook in self.on_drain:  # e.g. stop the ingest front-ends so no new tasks arrive
+                    try:
+                        hook()
+                    except Exception as e:  # draining must go on
+                        self.cp.log.log_error(f"drain hook failed: {e}")
                 threading.Thread(target=wait_then_exit, daemon=True).start()
 
         for sig in (signal.SIGINT, signal.SIGTERM):

@@ -166,6 +166,8 @@ def main(argv=None) -> int:
     nfe = frontend_count(cfg)
     socks = open_listeners(cfg.host, cfg.port, shared=nfe > 0)
     frontends = start_frontends(cfg, doc, endpoints, cfg.port, socks[1].getsockname()[1]) if nfe else []
+    # SIGTERM drain: the front-ends stop first (their own graceful shutdown), so no new tasks arrive meanwhile
+    gw.on_drain.append(lambda: [p.terminate() for p in frontends])
     print(f"ai4e-mi355x gateway on http://{cfg.host}:{cfg.port} endpoints={list(endpoints)} "
           f"ingest_frontends={len(frontends)}", file=sys.stderr, flush=True)
     try:
