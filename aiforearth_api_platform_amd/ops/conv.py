@@ -283,6 +283,9 @@ def conv_chain(t1: torch.Tensor, c2: PackedConv, c3: PackedConv, residual: Optio
     midn = c1n.cout if c1n is not None else 0
     if _ext.backend_for(t1) != "hip" or not ok(mid, midn):
         y2 = conv2d_nhwc(t1, c2, relu=True)
+        if (c1n is not None and PAIR and _ext.backend_for(t1) == "hip" and residual is not None
+                and pair_supported(mid, c3.cout, midn) and (mid == 256 or PAIR_L4)):
+            return conv_pair(y2, c3, residual, c1n, out=out, t1n_out=t1n_out)  # K1p: c3 + residual + next c1
         conv2d_nhwc(y2, c3, residual=residual, relu=True, out=out)
         return out, (conv2d_nhwc(out, c1n, relu=True, out=t1n_out) if c1n is not None else None)
     if t1.dtype != torch.bfloat16 or not t1.is_contiguous() or not out.is_contiguous():
@@ -305,6 +308,64 @@ def conv_chain(t1: torch.Tensor, c2: PackedConv, c3: PackedConv, residual: Optio
               CHAIN_TILE.get(mid, 0) if tile_cfg < 0 else tile_cfg, _ext.ptr(x0 if residual is None else None),
               x0.shape[-1] if residual is None else 0, _ext.stream_ptr(t1.device))
     return out, t1n
+
+
+def pack_mfma_frags(w: torch.Tensor) -> torch.Tensor:
+    """[R, K] bf16 (R % 16 == 0, K % 32 == 0) -> the MFMA fragment order the K1p pair kernel streams:
+    [R/16][K/32][64 lanes][8], lane l holding row 16 rb + (l & 15), K elements 32 ks + 8 (l >> 4) .. +8
+    (the B-operand fragment of v_mfma_f32_16x16x32_bf16), so each fragment is one contiguous 1-KB wave load."""
+    r, k = w.shape
+    if r % 16 or k % 32:
+        raise ValueError(f"pack_mfma_frags: [{r}, {k}] is not a whole number of 16x32 fragments")
+    return w.reshape(r // 16, 16, k // 32, 4, 8).permute(0, 2, 3, 1, 4).contiguous().reshape(r // 16, k // 32, 64, 8)
+
+
+def pair_supported(mid: int, c4: int, midn: int) -> bool:
+    """Shapes the fused 1x1 pair kernel K1p (csrc/kernels/conv_pair.hip) is built for."""
+    return (mid, c4, midn) in ((256, 1024, 256), (512, 2048, 512))
+
+
+def _pair_pack(c3: PackedConv, c1n: PackedConv):
+    cached = getattr(c3, "_pair_pack", None)
+    if cached is not None and cached[0] is c1n:
+        return cached[1], cached[2]
+    w3p = pack_mfma_frags(c3.w_packed[:c3.cout, :c3.cin_pad])
+    w1p = pack_mfma_frags(c1n.w_packed[:c1n.cout, :c1n.cin_pad])
+    c3._pair_pack = (c1n, w3p, w1p)
+    return w3p, w1p
+
+
+def conv_pair(t2: torch.Tensor, c3: PackedConv, residual: torch.Tensor, c1n: PackedConv,
+              out: Optional[torch.Tensor] = None, t1n_out: Optional[torch.Tensor] = None, tile_cfg: int = -1):
+    """K1p: ``y = relu(c3(t2) + residual)`` and the next block's ``t1n = relu(c1n(y))`` in one launch (c3, c1n
+    1x1 convs; ``t2`` [N,H,W,mid], ``residual`` [N,H,W,4*mid]); Y is read back from LDS instead of HBM.
+    Returns ``(y, t1n)``. Other backends/shapes: the two K1 convs."""
+    n, h, w, mid = t2.shape
+    c4, midn = c3.cout, c1n.cout
+    if out is None:
+        out = torch.empty(n, h, w, c4, device=t2.device, dtype=t2.dtype)
+    t1n = torch.empty(n, h, w, midn, device=t2.device, dtype=t2.dtype) if t1n_out is None else t1n_out
+    ok = (_ext.backend_for(t2) == "hip" and pair_supported(mid, c4, midn) and c3.kh == 1 and c3.stride == 1
+          and c1n.kh == 1 and c1n.stride == 1 and c3.cin_pad == mid and c1n.cin_pad == c4 and t2.is_contiguous()
+          and residual.is_contiguous() and residual.shape == (n, h, w, c4) and out.is_contiguous()
+          and t1n.is_contiguous() and t1n.shape == (n, h, w, midn) and t2.dtype == torch.bfloat16)
+    if not ok:
+        conv2d_nhwc(t2, c3, residual=residual, relu=True, out=out)
+        conv2d_nhwc(out, c1n, relu=True, out=t1n)
+        return out, t1n
+    w3p, w1p = _pair_pack(c3, c1n)
+    _ext.call("ai4e_conv_pair_fwd", t2.data_ptr(), w3p.data_ptr(), c3.bias.data_ptr(), residual.data_ptr(),
+              out.data_ptr(), w1p.data_ptr(), c1n.bias.data_ptr(), t1n.data_ptr(), n * h * w, mid, c4, midn,
+              PAIR_TILE if tile_cfg < 0 else tile_cfg, _ext.stream_ptr(t2.device))
+    return out, t1n
+
+
+# K1p: on by default for the ResNet layer3 pairs (AI4E_PAIR=0 runs c3 + residual and the next c1 as two K1
+# launches); AI4E_PAIR_TILE picks the tile height (0 = kernel default)
+PAIR = os.environ.get("AI4E_PAIR", "1") not in ("0", "off", "")
+PAIR_TILE = int(os.environ.get("AI4E_PAIR_TILE", "0"))
+# layer4 (mid 512): a 32-pixel tile streams 4 MB of weights per tile through L2, so it stays opt-in (AI4E_PAIR_L4=1)
+PAIR_L4 = os.environ.get("AI4E_PAIR_L4", "0") not in ("0", "off", "")
 
 
 # K1c tile config per bottleneck width (reserved: the kernel uses 128-pixel tiles for both widths)

@@ -1,0 +1,310 @@
+// K1p — fused 1x1 pair of consecutive wide bottlenecks (ResNet layer3/4): block i's expand conv c3 with
+// its residual and ReLU, and block i+1's reduce conv c1', in one launch:
+//
+//   Y   = relu(T2 . W3^T + b3 + R)        [BM x C4]    (HBM: block i+1's residual)
+//   T1' = relu(Y . W1'^T + b1')           [BM x MIDN]  (HBM: block i+1's 3x3 input)
+//
+// Why: unfused, layer3 runs c3+res (reads T2 25 MB + R 100 MB, writes Y 100 MB at batch 250) and then the
+// next c1 re-reads all of Y; both are short-K GEMMs whose tile grids leave HBM at 2-3 TB/s
+// (profiles/r2_final/pmc_summary.txt: 58-70 us + 36-39 us per block). Fused, Y is read back from LDS.
+//
+// Structure: one 512-thread workgroup (8 wave64s) per BM-pixel tile; LDS holds the T2 tile [BM x MID] for
+// the whole launch plus a double-buffered Y chunk [BM x CH]. The C4 output channels of c3 go in NP = C4/CH
+// passes of CH = 128 channels:
+//   B  accb[BM x 16 per wave] = b3 + T2 . W3[chunk rows]^T   (K = MID, v_mfma_f32_16x16x32_bf16)
+//   epilogue: + residual (registers, prefetched a pass ahead), ReLU, bf16 -> Y chunk in LDS, one barrier
+//   C  accn[BM x MIDN/8 per wave] += Y chunk . W1'[:, chunk]^T (persistent accumulators, seeded with b1')
+//   copy-out of the Y chunk with 16-B row stores.
+// Weights are pre-packed on the host into MFMA fragment order ([16-row block][32-wide K step][64 lanes][8]),
+// so every weight fragment is ONE contiguous 1-KB wave load straight into registers: each wave streams only
+// the rows it owns (no LDS ring, no per-step barriers), C fragments a B phase ahead, B fragments a C phase
+// ahead. The residual is read in the accumulator layout (4 channels per lane), so the epilogue never
+// shuffles. T1' leaves through the (then idle) T2 region with 16-B row stores.
+#include "common.h"
+
+namespace {
+
+constexpr int PR_CH = 128;     // c3 output channels per pass (Y chunk width)
+constexpr int PR_WAVES = 8;
+
+// swizzled 16-B chunk within a 64-B LDS row (same rotation as the K1/K1c operand tiles)
+__device__ __forceinline__ int pswz(int row) { return (0x78 >> (2 * ((row >> 2) & 3))) & 3; }
+
+// K-blocked tiles: [K/32 blocks][BM rows][64 B], the blocks padded by 64 B so that the same row of
+// consecutive blocks falls in different LDS banks (BM * 64 is a multiple of the 256-B bank row: unpadded, the
+// 16-B row-chunk copy-outs, whose 16-lane groups span four blocks, conflict four ways)
+template <int BM>
+constexpr int kbs() { return BM * 64 + 64; }
+
+// byte offset of the 8-byte group holding channels n..n+3 of row r in a K-blocked swizzled tile of BM rows
+template <int BM>
+__device__ __forceinline__ uint32_t poff(int r, int n) {
+  const int kb = n >> 5, e = n & 31;
+  return kb * kbs<BM>() + r * 64 + ((((e >> 3) ^ pswz(r)) << 4) | (((e >> 2) & 1) << 3));
+}
+
+// bias of the 4 channels blk[4 g .. 4 g + 3] (g = lane >> 4) from a wave-uniform 16-float block: scalar loads
+// (lgkmcnt, outside the vector-memory waits) and a lane-group select on registers
+typedef const float __attribute__((address_space(4)))* pconst_f32_ptr;
+__device__ __forceinline__ f32x4_t pbias4(const float* blk, int g) {
+  const pconst_f32_ptr b = reinterpret_cast<pconst_f32_ptr>(reinterpret_cast<uintptr_t>(blk));
+  f32x4_t r;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float v0 = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(b[q])));
+    const float v1 = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(b[4 + q])));
+    const float v2 = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(b[8 + q])));
+    const float v3 = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(b[12 + q])));
+    const float lo = g & 1 ? v1 : v0;
+    const float hi = g & 1 ? v3 : v2;
+    r[q] = g & 2 ? hi : lo;
+  }
+  return r;
+}
+
+__device__ __forceinline__ void pbarrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+struct PairParams {
+  const uint16_t* t2;   // [M, MID]
+  const uint16_t* w3p;  // packed [C4/16][MID/32][64][8]
+  const float* b3;      // [C4]
+  const uint16_t* res;  // [M, C4]
+  uint16_t* y;          // [M, C4]
+  const uint16_t* w1p;  // packed [MIDN/16][C4/32][64][8]
+  const float* b1n;     // [MIDN]
+  uint16_t* t1n;        // [M, MIDN]
+  int M;
+};
+
+template <int MID, int C4, int MIDN, int BM>
+__global__ __launch_bounds__(512) void conv_pair_kernel(const PairParams p) {
+  constexpr int FI = BM / 16;            // pixel fragments
+  constexpr int NKB = MID / 32;          // B K steps
+  constexpr int NKC = PR_CH / 32;        // C K steps per pass
+  constexpr int NP = C4 / PR_CH;         // passes
+  constexpr int JC = MIDN / 16 / PR_WAVES;  // C weight fragments (16-channel blocks) per wave
+  constexpr int KBS = kbs<BM>();
+  constexpr int T2_BYTES = MID / 32 * KBS;
+  constexpr int Y_BYTES = PR_CH / 32 * KBS;
+  static_assert(PR_CH == 16 * PR_WAVES, "B: one 16-channel block per wave");
+  static_assert(JC >= 1 && MIDN == 16 * PR_WAVES * JC, "C: whole 16-channel blocks per wave");
+  static_assert(MID >= MIDN, "T1' staging fits the T2 region");
+  extern __shared__ __attribute__((aligned(1024))) uint8_t smem[];
+  uint8_t* const t2s = smem;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lg = lane >> 4;
+  const int m0 = xcd_remap(blockIdx.x, gridDim.x) * BM;
+  const int frow = lane & 15;
+  const uint32_t fofs = frow * 64 + (((lg ^ pswz(frow)) << 4));
+
+  // ---- T2 tile -> LDS (K-blocked, swizzled); 16-B loads, rows past M re-read row M-1 (never stored)
+  {
+    constexpr int N = BM * MID / 8 / 512;
+    uint4 v[N];
+#pragma unroll
+    for (int e = 0; e < N; ++e) {
+      const int g = tid + 512 * e;
+      const int r = g / (MID / 8), cq = g % (MID / 8);
+      v[e] = *reinterpret_cast<const uint4*>(p.t2 + static_cast<long>(min(m0 + r, p.M - 1)) * MID + 8 * cq);
+    }
+#pragma unroll
+    for (int e = 0; e < N; ++e) {
+      const int g = tid + 512 * e;
+      const int r = g / (MID / 8), cq = g % (MID / 8);
+      *reinterpret_cast<uint4*>(t2s + (cq >> 2) * KBS + r * 64 + (((cq & 3) ^ pswz(r)) << 4)) = v[e];
+    }
+  }
+
+  // per-lane fragment pointers (elements): fragment (rb, ks) of a packed matrix with NK K steps is at
+  // ((rb * NK + ks) * 64 + lane) * 8
+  const uint16_t* const w3l = p.w3p + lane * 8;
+  const uint16_t* const w1l = p.w1p + lane * 8;
+  auto w3frag = [&](int pass, int ks) -> bf16x8_t {
+    return *reinterpret_cast<const bf16x8_t*>(w3l + (static_cast<long>((pass * PR_WAVES + w) * NKB + ks) << 9));
+  };
+  auto w1frag = [&](int pass, int kc, int j) -> bf16x8_t {
+    return *reinterpret_cast<const bf16x8_t*>(w1l + (static_cast<long>((w * JC + j) * (C4 / 32) + pass * NKC + kc) << 9));
+  };
+  // residual of pass `pass` in the accumulator layout: pixel 16i + frow, channels 128 pass + 16 w + 4 lg .. +3
+  const uint16_t* resl[FI];
+#pragma unroll
+  for (int i = 0; i < FI; ++i)
+    resl[i] = p.res + static_cast<long>(min(m0 + 16 * i + frow, p.M - 1)) * C4 + 16 * w + 4 * lg;
+
+  // T1' accumulators seeded with b1'
+  f32x4_t accn[FI][JC];
+#pragma unroll
+  for (int j = 0; j < JC; ++j) {
+    const f32x4_t b = pbias4(p.b1n + (w * JC + j) * 16, lg);
+#pragma unroll
+    for (int i = 0; i < FI; ++i) accn[i][j] = b;
+  }
+
+  // pass-0 operands
+  f32x4_t b3v = pbias4(p.b3 + 16 * w, lg);
+  bf16x8_t wb[NKB];
+#pragma unroll
+  for (int k = 0; k < NKB; ++k) wb[k] = w3frag(0, k);
+  uint2 rr[FI];
+#pragma unroll
+  for (int i = 0; i < FI; ++i) rr[i] = *reinterpret_cast<const uint2*>(resl[i]);
+
+  pbarrier();  // T2 tile visible
+
+  constexpr int NS = BM * PR_CH / 8 / 512;  // Y copy-out: thread g -> (row g / 16, 16-B chunk g % 16)
+
+#pragma unroll 1
+  for (int pass = 0; pass < NP; ++pass) {
+    uint8_t* const ybuf = smem + T2_BYTES + (pass & 1) * Y_BYTES;
+    // C fragments of this pass (consumed after the B phase)
+    bf16x8_t wc[NKC][JC];
+#pragma unroll
+    for (int k = 0; k < NKC; ++k)
+#pragma unroll
+      for (int j = 0; j < JC; ++j) wc[k][j] = w1frag(pass, k, j);
+    __builtin_amdgcn_sched_barrier(0);  // keep these loads here, a whole B phase ahead of their use
+    // ---- B: accb = b3 + T2 . W3[rows 128 pass + 16 w ..]^T; the pixel fragments of step k+1 are read from
+    // LDS before the MFMAs of step k (the scheduler otherwise pairs each read with its MFMA)
+    f32x4_t accb[FI];
+#pragma unroll
+    for (int i = 0; i < FI; ++i) accb[i] = b3v;
+    bf16x8_t fx[2][FI];
+#pragma unroll
+    for (int i = 0; i < FI; ++i) fx[0][i] = *reinterpret_cast<const bf16x8_t*>(t2s + fofs + i * 1024);
+#pragma unroll
+    for (int k = 0; k < NKB; ++k) {
+      if (k + 1 < NKB) {
+        const uint8_t* x_ = t2s + (k + 1) * KBS + fofs;
+#pragma unroll
+        for (int i = 0; i < FI; ++i) fx[(k + 1) & 1][i] = *reinterpret_cast<const bf16x8_t*>(x_ + i * 1024);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < FI; ++i) accb[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[k], fx[k & 1][i], accb[i], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+
+    // ---- epilogue: + residual (registers), ReLU, bf16 -> Y chunk (LDS)
+#pragma unroll
+    for (int i = 0; i < FI; ++i) {
+      const uint2 rv = rr[i];
+      *reinterpret_cast<uint2*>(ybuf + poff<BM>(16 * i + frow, 16 * w + 4 * lg)) =
+          make_uint2(pack_relu_bf16x2(add_bf16_lo(rv.x, accb[i][0]), add_bf16_hi(rv.x, accb[i][1])),
+                     pack_relu_bf16x2(add_bf16_lo(rv.y, accb[i][2]), add_bf16_hi(rv.y, accb[i][3])));
+    }
+    pbarrier();  // Y chunk visible (and every wave is past the chunk buffer's previous readers)
+
+    // next pass's bias and B fragments (waited for at the next B phase) and residual (waited for at the next
+    // epilogue), issued in that order and ahead of this pass's Y stores: every wait is then a count of younger
+    // operations that never has to drain the stores or, for the B phase, the residual loads
+    const int pn = pass + 1 < NP ? pass + 1 : pass;
+    b3v = pbias4(p.b3 + pn * PR_CH + 16 * w, lg);
+#pragma unroll
+    for (int k = 0; k < NKB; ++k) wb[k] = w3frag(pn, k);
+#pragma unroll
+    for (int i = 0; i < FI; ++i) rr[i] = *reinterpret_cast<const uint2*>(resl[i] + pn * PR_CH);
+    __builtin_amdgcn_sched_barrier(0);
+    // ---- Y chunk -> HBM (16-B row stores)
+#pragma unroll
+    for (int e = 0; e < NS; ++e) {
+      const int g = tid + 512 * e;
+      const int r = g >> 4, cq = g & 15;
+      const uint4 v = *reinterpret_cast<const uint4*>(ybuf + (cq >> 2) * KBS + r * 64 + (((cq & 3) ^ pswz(r)) << 4));
+      if (m0 + r < p.M) *reinterpret_cast<uint4*>(p.y + static_cast<long>(m0 + r) * C4 + pass * PR_CH + 8 * cq) = v;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+
+    // ---- C: accn += Y chunk . W1'[:, chunk]^T (pixel fragments one K step ahead, as in B)
+    bf16x8_t fy[2][FI];
+#pragma unroll
+    for (int i = 0; i < FI; ++i) fy[0][i] = *reinterpret_cast<const bf16x8_t*>(ybuf + fofs + i * 1024);
+#pragma unroll
+    for (int k = 0; k < NKC; ++k) {
+      if (k + 1 < NKC) {
+        const uint8_t* x_ = ybuf + (k + 1) * KBS + fofs;
+#pragma unroll
+        for (int i = 0; i < FI; ++i) fy[(k + 1) & 1][i] = *reinterpret_cast<const bf16x8_t*>(x_ + i * 1024);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < FI; ++i)
+#pragma unroll
+        for (int j = 0; j < JC; ++j)
+          accn[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wc[k][j], fy[k & 1][i], accn[i][j], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+
+  // ---- T1' epilogue through the T2 region (every wave finished its last B phase before the last barrier)
+#pragma unroll
+  for (int i = 0; i < FI; ++i)
+#pragma unroll
+    for (int j = 0; j < JC; ++j)
+      *reinterpret_cast<uint2*>(t2s + poff<BM>(16 * i + frow, (w * JC + j) * 16 + 4 * lg)) =
+          make_uint2(pack_relu_bf16x2(accn[i][j][0], accn[i][j][1]), pack_relu_bf16x2(accn[i][j][2], accn[i][j][3]));
+  pbarrier();
+  constexpr int NT = BM * MIDN / 8 / 512;
+#pragma unroll
+  for (int e = 0; e < NT; ++e) {
+    const int g = tid + 512 * e;
+    const int r = g / (MIDN / 8), cq = g % (MIDN / 8);
+    const uint4 v = *reinterpret_cast<const uint4*>(t2s + (cq >> 2) * KBS + r * 64 + (((cq & 3) ^ pswz(r)) << 4));
+    if (m0 + r < p.M) *reinterpret_cast<uint4*>(p.t1n + static_cast<long>(m0 + r) * MIDN + 8 * cq) = v;
+  }
+}
+
+template <int MID, int C4, int MIDN, int BM>
+int launch_pair(const PairParams& p, hipStream_t s) {
+  constexpr int LDS = (MID / 32 + 2 * PR_CH / 32) * kbs<BM>();
+  static bool attr = false;
+  if (!attr) {
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(conv_pair_kernel<MID, C4, MIDN, BM>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, LDS) != hipSuccess)
+      return AI4E_ELAUNCH;
+    attr = true;
+  }
+  hipLaunchKernelGGL((conv_pair_kernel<MID, C4, MIDN, BM>), dim3(ai4e_cdiv(p.M, BM)), dim3(512), LDS, s, p);
+  return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
+}
+
+}  // namespace
+
+// Fused 1x1 pair (see header). t2 [M, mid], res / y [M, c4], t1n [M, midn] bf16 row-major (contiguous);
+// w3p / w1p packed by ops/conv.py pack_pair_weights; b3 [c4], b1n [midn] fp32.
+// (mid, c4, midn) = (256, 1024, 256) (layer3) or (512, 2048, 512) (layer4). bm_cfg: 0 = default tile,
+// else the tile height in pixels (64 or 96 for layer3, 32 for layer4; taller tiles spill at 256 VGPRs).
+AI4E_API int ai4e_conv_pair_fwd(const void* t2, const void* w3p, const void* b3, const void* res, void* y,
+                                const void* w1p, const void* b1n, void* t1n, int M, int mid, int c4, int midn,
+                                int bm_cfg, hipStream_t stream) {
+  if (!t2 || !w3p || !b3 || !res || !y || !w1p || !b1n || !t1n || M < 0) return AI4E_EINVAL;
+  PairParams p{};
+  p.t2 = static_cast<const uint16_t*>(t2);
+  p.w3p = static_cast<const uint16_t*>(w3p);
+  p.b3 = static_cast<const float*>(b3);
+  p.res = static_cast<const uint16_t*>(res);
+  p.y = static_cast<uint16_t*>(y);
+  p.w1p = static_cast<const uint16_t*>(w1p);
+  p.b1n = static_cast<const float*>(b1n);
+  p.t1n = static_cast<uint16_t*>(t1n);
+  p.M = M;
+  if (M == 0) return AI4E_OK;
+  if (mid == 256 && c4 == 1024 && midn == 256) {
+    switch (bm_cfg) {
+      case 0:
+      case 96: return launch_pair<256, 1024, 256, 96>(p, stream);
+      case 64: return launch_pair<256, 1024, 256, 64>(p, stream);
+      default: return AI4E_EINVAL;
+    }
+  }
+  if (mid == 512 && c4 == 2048 && midn == 512) {
+    switch (bm_cfg) {
+      case 0:
+      case 32: return launch_pair<512, 2048, 512, 32>(p, stream);
+      default: return AI4E_EINVAL;
+    }
+  }
+  return AI4E_EINVAL;
+}

@@ -102,3 +102,31 @@ def test_tile_grid_and_stitch_reference():
     ty0, ty1 = grid.tile_rows_for(40, 70)
     cls2, _ = tile_stitch(tiles[ty0:ty1], grid, row0=40, rows=30, ty0=ty0)
     assert torch.equal(cls2, cls[40:70])
+
+
+def test_pack_mfma_frags_layout():
+    """K1p weight packing: fragment (rb, ks), lane l holds row 16 rb + (l & 15), K 32 ks + 8 (l >> 4) .. +8."""
+    from aiforearth_api_platform_amd.ops.conv import pack_mfma_frags
+
+    w = torch.arange(64 * 96, dtype=torch.float32).reshape(64, 96)
+    p = pack_mfma_frags(w)
+    assert p.shape == (4, 3, 64, 8)
+    for rb in range(4):
+        for ks in range(3):
+            for lane in (0, 5, 16, 37, 63):
+                r, k0 = 16 * rb + (lane & 15), 32 * ks + 8 * (lane >> 4)
+                assert torch.equal(p[rb, ks, lane], w[r, k0:k0 + 8])
+
+
+def test_conv_pair_cpu_fallback_matches_two_convs():
+    from aiforearth_api_platform_amd.ops.conv import conv2d_nhwc, conv_pair, pack_conv
+
+    torch.manual_seed(3)
+    c3 = pack_conv(torch.randn(1024, 256, 1, 1) / 16, torch.randn(1024) * 0.1)
+    c1n = pack_conv(torch.randn(256, 1024, 1, 1) / 32, torch.randn(256) * 0.1)
+    t2 = torch.randn(1, 3, 4, 256).relu()
+    res = torch.randn(1, 3, 4, 1024)
+    y, t1n = conv_pair(t2, c3, res, c1n)
+    y_ref = conv2d_nhwc(t2, c3, residual=res, relu=True)
+    assert torch.allclose(y, y_ref)
+    assert torch.allclose(t1n, conv2d_nhwc(y_ref, c1n, relu=True))

@@ -1,0 +1,71 @@
+"""K1p fused 1x1 pair (csrc/kernels/conv_pair.hip): block i's c3 + residual + ReLU and block i+1's c1 in
+one launch, vs a PyTorch fp32 reference of the two convs (GPU box only). Y is rounded to bf16 before the
+chained 1x1, where the kernel rounds it (the Y chunk in LDS)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from aiforearth_api_platform_amd.ops import _ext
+from aiforearth_api_platform_amd.ops.conv import conv_pair, pack_conv, pair_supported
+
+DEV = "cuda"
+
+
+@pytest.fixture(autouse=True, scope="module")
+def _lib():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    _ext.lib()
+
+
+def _w(pc):
+    return pc.w_packed[:pc.cout, :pc.cin_pad].float()
+
+
+CASES = [
+    # n, h, w, mid, tile
+    (2, 14, 14, 256, 0),      # layer3 shape, M = 392 (partial last tile)
+    (2, 14, 14, 256, 64),
+    (1, 5, 7, 256, 0),        # M = 35 < one tile
+    (8, 14, 14, 256, 96),     # M = 1568: 17 tiles
+    (2, 7, 7, 512, 0),        # layer4 shape
+    (1, 3, 5, 512, 32),
+]
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_conv_pair(case):
+    n, h, w, mid, tile = case
+    c4 = 4 * mid
+    assert pair_supported(mid, c4, mid)
+    torch.manual_seed(11)
+    c3 = pack_conv(torch.randn(c4, mid, 1, 1) / mid ** 0.5, torch.randn(c4) * 0.1).to(DEV)
+    c1n = pack_conv(torch.randn(mid, c4, 1, 1) / c4 ** 0.5, torch.randn(mid) * 0.1).to(DEV)
+    t2 = torch.randn(n, h, w, mid, device=DEV).relu().to(torch.bfloat16)
+    res = torch.randn(n, h, w, c4, device=DEV).to(torch.bfloat16)
+    y, t1n = conv_pair(t2, c3, res, c1n, tile_cfg=tile)
+    torch.cuda.synchronize()
+    y_ref = (t2.float().reshape(-1, mid) @ _w(c3).t() + c3.b_ref.to(DEV) + res.float().reshape(-1, c4)).relu()
+    t_ref = (y_ref.to(torch.bfloat16).float() @ _w(c1n).t() + c1n.b_ref.to(DEV)).relu()
+    y_err = (y.float().reshape(-1, c4) - y_ref).abs().max().item()
+    t_err = (t1n.float().reshape(-1, mid) - t_ref).abs().max().item()
+    assert y_err <= 0.02 * y_ref.abs().max().item() + 1e-2, y_err
+    assert t_err <= 0.02 * t_ref.abs().max().item() + 1e-2, t_err
+
+
+def test_conv_pair_in_resnet_layer3_matches_unfused(monkeypatch):
+    """The fused forward with K1p in layer3 equals the same forward with the pair split into two K1 convs."""
+    from aiforearth_api_platform_amd.models.resnet import FusedResNet, resnet50
+    from aiforearth_api_platform_amd.ops import conv as convmod
+
+    torch.manual_seed(0)
+    fused = FusedResNet(resnet50(), device=DEV)
+    x = torch.randint(0, 256, (4, 224, 224, 3), dtype=torch.uint8, device=DEV)
+    with torch.no_grad():
+        monkeypatch.setattr(convmod, "PAIR", True)
+        a = fused.forward_u8(x)
+        monkeypatch.setattr(convmod, "PAIR", False)
+        b = fused.forward_u8(x)
+    torch.cuda.synchronize()
+    assert (a - b).abs().max().item() <= 0.05 * b.abs().max().item() + 1e-2
