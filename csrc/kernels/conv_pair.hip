@@ -144,7 +144,7 @@ __global__ __launch_bounds__(512) void conv_pair_kernel(const PairParams p) {
   }
 
   // pass-0 operands
-  f32x4_t b3v = pbias4(p.b3 + 16 * w, lg);
+  f32x4_t b3v = *reinterpret_cast<const f32x4_t*>(p.b3 + 16 * w + 4 * lg);
   bf16x8_t wb[NKB];
 #pragma unroll
   for (int k = 0; k < NKB; ++k) wb[k] = w3frag(0, k);
@@ -201,7 +201,7 @@ __global__ __launch_bounds__(512) void conv_pair_kernel(const PairParams p) {
     // epilogue), issued in that order and ahead of this pass's Y stores: every wait is then a count of younger
     // operations that never has to drain the stores or, for the B phase, the residual loads
     const int pn = pass + 1 < NP ? pass + 1 : pass;
-    b3v = pbias4(p.b3 + pn * PR_CH + 16 * w, lg);
+    b3v = *reinterpret_cast<const f32x4_t*>(p.b3 + pn * PR_CH + 16 * w + 4 * lg);
 #pragma unroll
     for (int k = 0; k < NKB; ++k) wb[k] = w3frag(pn, k);
 #pragma unroll
