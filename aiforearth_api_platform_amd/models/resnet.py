@@ -19,7 +19,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ..ops.conv import (PackedConv, chain_supported, conv2d_nhwc, conv_chain, fold_bn, pack_conv,
+from ..ops.conv import (PackedConv, chain_supported, conv2d_nhwc, conv_chain, fold_bn, pack_conv, pair_supported,
                         pack_stem_s2d, stem_pool, stem_pool_c1, stem_pool_u8)
 from ..ops.head import softmax_topk
 from ..ops.pool import (global_avgpool_nhwc, maxpool2d_nhwc, preprocess_s2d_u8, preprocess_u8,
@@ -168,6 +168,15 @@ class FusedResNet:
         # chained micro-batching (AI4E_RESNET_CHAIN_MB=mb:nstages): stem + the first nstages run mb images at a time
         cmb = os.environ.get("AI4E_RESNET_CHAIN_MB", "")
         self.chain_mb: Optional[Tuple[int, int]] = tuple(int(v) for v in cmb.split(":")) if ":" in cmb else None
+        # stage entry: the downsample projection on a side stream, concurrent with the stage's first c1 (both read
+        # the previous stage's output, both are latency-bound short-K GEMMs); forked and joined inside the caller's
+        # stream, so a captured HIP graph holds the two as parallel branches. Opt-in (AI4E_PAR_DOWN=1): -27 us on a
+        # lone forward but -2.2 % images/s in the serving worker, whose two compute streams already fill the chip
+        # (profiles/r2_pair/README.md)
+        self.par_down = os.environ.get("AI4E_PAR_DOWN", "0") not in ("0", "off", "")
+        self._side: dict = {}
+        self._side_pool = ([torch.cuda.Stream(device=self.device) for _ in range(4)]
+                           if self.device.type == "cuda" and torch.cuda.is_available() else [])
         # stages: runs of blocks starting at a block with a downsample conv
         self.stages: List[List[Tuple[PackedConv, PackedConv, PackedConv, Optional[PackedConv]]]] = []
         for blk in self.blocks:
@@ -243,11 +252,14 @@ class FusedResNet:
         for si in range(s0, s1):
             blocks = self.stages[si]
             c1, _, _, down = blocks[0]
-            if t1 is None:
-                t1 = conv2d_nhwc(y, c1, relu=True)
             # the first block's downsample: folded into the chain kernel where it can be (layer1), else a K1 conv
             x0, dn = (y, down) if down is not None and down.stride == 1 and self.fold_down else (None, None)
-            idt = None if dn is not None else (y if down is None else conv2d_nhwc(y, down))
+            if t1 is None and dn is None and down is not None and self._side_ok(y):
+                t1, idt = self._c1_down_parallel(y, c1, down)
+            else:
+                if t1 is None:
+                    t1 = conv2d_nhwc(y, c1, relu=True)
+                idt = None if dn is not None else (y if down is None else conv2d_nhwc(y, down))
             for i, (_, c2, c3, _) in enumerate(blocks):
                 if i + 1 < len(blocks):
                     nxt = blocks[i + 1][0]
@@ -257,6 +269,9 @@ class FusedResNet:
                     nxt = None
                 if nxt is not None and not chain_supported(c2.cout, nxt.cout) and chain_supported(c2.cout):
                     nxt = None  # keep the chain, run the next c1 as its own K1 launch
+                if (nxt is not None and i + 1 == len(blocks) and not chain_supported(c2.cout, nxt.cout)
+                        and not pair_supported(c2.cout, c3.cout, nxt.cout) and self._side_ok(t1)):
+                    nxt = None  # the next stage's c1 runs at its entry, beside its downsample
                 last = si + 1 == s1 and i + 1 == len(blocks)
                 idt, t1 = conv_chain(t1, c2, c3, idt, c1n=nxt, down=dn, x0=x0, out=y_out if last else None,
                                      t1n_out=t1_out if last and nxt is not None else None)
@@ -266,6 +281,23 @@ class FusedResNet:
         if s1 < len(self.stages):
             return y, t1
         return outs if collect else y
+
+    def _side_ok(self, t: torch.Tensor) -> bool:
+        return self.par_down and bool(self._side_pool) and t.is_cuda
+
+    def _c1_down_parallel(self, y: torch.Tensor, c1: PackedConv, down: PackedConv):
+        """(relu(c1(y)), down(y)) with the downsample forked onto a side stream of the current stream."""
+        main = torch.cuda.current_stream(y.device)
+        side = self._side.get(main.cuda_stream)
+        if side is None:  # pre-created streams only: no stream creation inside a graph capture
+            side = self._side[main.cuda_stream] = self._side_pool[len(self._side) % len(self._side_pool)]
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            idt = conv2d_nhwc(y, down)
+        t1 = conv2d_nhwc(y, c1, relu=True)
+        main.wait_stream(side)
+        idt.record_stream(main)
+        return t1, idt
 
     def _chained_microbatched(self, x: torch.Tensor, pre, mb: int, nstages: int) -> torch.Tensor:
         if not 0 < nstages < len(self.stages):

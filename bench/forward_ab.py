@@ -3,7 +3,7 @@ out), variants interleaved over several rounds on one GPU.
 
     python bench/forward_ab.py chain64=0 chain64=1 [chain=0] [chain=1] ...
 A variant is ``key=value[,key=value]`` over: t.<conv tile key> (tile config), chain (K1c on/off), stemu8 (preprocess fused into K1s), chain64 / chain128 (K1c tile config),
-pair / pairtile / pairl4 (K1p fused 1x1 pair on/off, tile height, layer4 too).
+pair / pairtile / pairl4 (K1p fused 1x1 pair on/off, tile height, layer4 too), pardown (side-stream downsample).
 """
 import os
 import sys
@@ -29,6 +29,7 @@ def apply(m, variant):
     m.fc_blas = True
     convmod.BLAS_1X1 = False
     convmod.PAIR, convmod.PAIR_TILE, convmod.PAIR_L4 = True, 0, False
+    m.par_down = False
     for kv in variant.split(","):
         if kv == "base":
             continue
@@ -49,6 +50,8 @@ def apply(m, variant):
             m.stem_u8 = v == "1"
         elif k == "pair":  # K1p fused c3 + residual + next c1 (layer3; pairl4=1 adds layer4)
             convmod.PAIR = v == "1"
+        elif k == "pardown":  # stage-entry downsample on a side stream beside the first c1
+            m.par_down = v == "1"
         elif k == "pairtile":
             convmod.PAIR_TILE = int(v)
         elif k == "pairl4":

@@ -69,3 +69,26 @@ def test_conv_pair_in_resnet_layer3_matches_unfused(monkeypatch):
         b = fused.forward_u8(x)
     torch.cuda.synchronize()
     assert (a - b).abs().max().item() <= 0.05 * b.abs().max().item() + 1e-2
+
+
+def test_side_stream_downsample_matches_serial():
+    """Stage-entry downsample forked onto a side stream (captured in a HIP graph) == the serial forward."""
+    from aiforearth_api_platform_amd.models.resnet import FusedResNet, resnet50
+
+    torch.manual_seed(0)
+    fused = FusedResNet(resnet50(), device=DEV)
+    x = torch.randint(0, 256, (8, 224, 224, 3), dtype=torch.uint8, device=DEV)
+    with torch.no_grad():
+        fused.par_down = False
+        ref = fused.forward_u8(x)
+        fused.par_down = True
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            fused.forward_u8(x)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=s):
+                out = fused.forward_u8(x)
+        g.replay()
+        torch.cuda.synchronize()
+    assert torch.equal(out, ref)

@@ -16,7 +16,7 @@ run() {  # name timeout cmd...
 python -c "import __graft_entry__ as g; g.build()" > gpurun_out/build.log 2>&1 || { tail gpurun_out/build.log; exit 3; }
 run pair_tests 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread -p no:cacheprovider tests/test_pair_gpu.py
 run pair_micro 200 python -u bench/pair_micro.py 250
-run pair_ab 400 env B=250 python -u bench/forward_ab.py pair=0 pair=1 pair=1,pairtile=64 ${AB_EXTRA:-}
+run pair_ab 400 env B=250 python -u bench/forward_ab.py ${AB_VARIANTS:-pair=0 pair=1 pair=1,pairtile=64}
 if [ -n "${BENCH:-}" ]; then
   run bench 400 python -u bench.py --steps 200 --warmup 10 --http 0 --json-out gpurun_out/bench.json
 fi
