@@ -38,7 +38,7 @@ def main():
     B = int(sys.argv[1]) if len(sys.argv) > 1 else 250
     dev = "cuda"
     out = {}
-    for mid, hw, tiles in ((256, 14, (96, 64)), (512, 7, (32,))):
+    for mid, hw, tiles in ((256, 14, tuple(int(t) for t in os.environ.get("PAIR_TILES", "96,64").split(","))), (512, 7, (32,))):
         c4 = 4 * mid
         torch.manual_seed(0)
         c3 = pack_conv(torch.randn(c4, mid, 1, 1) / mid ** 0.5, torch.randn(c4) * 0.1).to(dev)

@@ -76,7 +76,7 @@ struct PairParams {
   int M;
 };
 
-template <int MID, int C4, int MIDN, int BM>
+template <int MID, int C4, int MIDN, int BM, bool KF = true>
 __global__ __launch_bounds__(512) void conv_pair_kernel(const PairParams p) {
   constexpr int FI = BM / 16;            // pixel fragments
   constexpr int NKB = MID / 32;          // B K steps
@@ -181,10 +181,10 @@ __global__ __launch_bounds__(512) void conv_pair_kernel(const PairParams p) {
 #pragma unroll
         for (int i = 0; i < FI; ++i) fx[(k + 1) & 1][i] = *reinterpret_cast<const bf16x8_t*>(x_ + i * 1024);
       }
-      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (KF) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int i = 0; i < FI; ++i) accb[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[k], fx[k & 1][i], accb[i], 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (KF) __builtin_amdgcn_sched_barrier(0);
     }
 
     // ---- epilogue: + residual (registers), ReLU, bf16 -> Y chunk (LDS)
@@ -228,13 +228,13 @@ __global__ __launch_bounds__(512) void conv_pair_kernel(const PairParams p) {
 #pragma unroll
         for (int i = 0; i < FI; ++i) fy[(k + 1) & 1][i] = *reinterpret_cast<const bf16x8_t*>(x_ + i * 1024);
       }
-      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (KF) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int i = 0; i < FI; ++i)
 #pragma unroll
         for (int j = 0; j < JC; ++j)
           accn[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wc[k][j], fy[k & 1][i], accn[i][j], 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (KF) __builtin_amdgcn_sched_barrier(0);
     }
   }
 
@@ -256,17 +256,17 @@ __global__ __launch_bounds__(512) void conv_pair_kernel(const PairParams p) {
   }
 }
 
-template <int MID, int C4, int MIDN, int BM>
+template <int MID, int C4, int MIDN, int BM, bool KF = true>
 int launch_pair(const PairParams& p, hipStream_t s) {
   constexpr int LDS = (MID / 32 + 2 * PR_CH / 32) * kbs<BM>();
   static bool attr = false;
   if (!attr) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(conv_pair_kernel<MID, C4, MIDN, BM>),
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(conv_pair_kernel<MID, C4, MIDN, BM, KF>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, LDS) != hipSuccess)
       return AI4E_ELAUNCH;
     attr = true;
   }
-  hipLaunchKernelGGL((conv_pair_kernel<MID, C4, MIDN, BM>), dim3(ai4e_cdiv(p.M, BM)), dim3(512), LDS, s, p);
+  hipLaunchKernelGGL((conv_pair_kernel<MID, C4, MIDN, BM, KF>), dim3(ai4e_cdiv(p.M, BM)), dim3(512), LDS, s, p);
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
 }
 
@@ -296,6 +296,7 @@ AI4E_API int ai4e_conv_pair_fwd(const void* t2, const void* w3p, const void* b3,
       case 0:
       case 96: return launch_pair<256, 1024, 256, 96>(p, stream);
       case 64: return launch_pair<256, 1024, 256, 64>(p, stream);
+      case 97: return launch_pair<256, 1024, 256, 96, false>(p, stream);  // A/B: scheduler-placed fragment reads
       default: return AI4E_EINVAL;
     }
   }
