@@ -35,3 +35,17 @@ def test_anchor_layout():
     # location (0,0) anchors are centred on the origin; location (0,1) shifted by the stride in x
     assert torch.allclose((a[0, :2] + a[0, 2:]) / 2, torch.zeros(2))
     assert torch.allclose(a[3] - a[0], torch.tensor([16.0, 0, 16.0, 0]))
+
+
+def test_nms_reference_hand_computed():
+    """Pins the greedy NMS reference the GPU kernel is tested against (torchvision is absent here):
+    boxes 0/1 overlap with IoU 64/136 = 0.47, boxes 0/2 with IoU 81/100 = 0.81, box 3 is disjoint."""
+    from aiforearth_api_platform_amd.ops.detection import nms_reference
+
+    boxes = torch.tensor([[0., 0., 10., 10.], [2., 2., 12., 12.], [0., 0., 9., 9.], [50., 50., 60., 60.]])
+    scores = torch.tensor([0.9, 0.8, 0.95, 0.1])
+    assert abs(float(box_iou(boxes[:1], boxes[1:2])) - 64 / 136) < 1e-6
+    # thr 0.5: box 2 (best) suppresses box 0 (IoU 0.81 > 0.5); box 1 vs box 2: IoU 49/151 = 0.32 -> kept
+    assert nms_reference(boxes, scores, 0.5).tolist() == [2, 1, 3]
+    # thr 0.9: nothing overlaps that much
+    assert nms_reference(boxes, scores, 0.9).tolist() == [2, 0, 1, 3]

@@ -93,6 +93,9 @@ def test_upsample_into_concat(shape):
 
 @pytest.mark.parametrize("N,thr", [(100, 0.5), (2000, 0.7), (777, 0.3)])
 def test_nms_matches_reference(N, thr):
+    """Parity unpinned against torchvision.ops.nms (not installed in this image): the kernel is compared with the
+    greedy reference ``ops.detection.nms_reference``, whose semantics are pinned by a hand-computed case in
+    tests/test_detector_cpu.py::test_nms_reference_hand_computed."""
     g = torch.Generator().manual_seed(N)
     B = 3
     xy = torch.rand(B, N, 2, generator=g) * 500
