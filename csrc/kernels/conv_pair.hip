@@ -30,11 +30,12 @@ constexpr int PR_WAVES = 8;
 // swizzled 16-B chunk within a 64-B LDS row (same rotation as the K1/K1c operand tiles)
 __device__ __forceinline__ int pswz(int row) { return (0x78 >> (2 * ((row >> 2) & 3))) & 3; }
 
-// K-blocked tiles: [K/32 blocks][BM rows][64 B], the blocks padded by 64 B so that the same row of
-// consecutive blocks falls in different LDS banks (BM * 64 is a multiple of the 256-B bank row: unpadded, the
-// 16-B row-chunk copy-outs, whose 16-lane groups span four blocks, conflict four ways)
+// K-blocked tiles: [K/32 blocks][BM rows][64 B], the blocks padded by 128 B: BM * 64 is a multiple of the 256-B
+// bank row, so unpadded the 16-B row-chunk copy-out reads conflict (a ds_read_b128 lane group {0-3, 12-15,
+// 20-27} reads blocks 0 and 3 of row r and blocks 1-2 of row r+1); with block offsets of 128 B mod 256 the
+// group's 16 chunks fall in distinct bank quads
 template <int BM>
-constexpr int kbs() { return BM * 64 + 64; }
+constexpr int kbs() { return BM * 64 + 128; }
 
 // byte offset of the 8-byte group holding channels n..n+3 of row r in a K-blocked swizzled tile of BM rows
 template <int BM>
