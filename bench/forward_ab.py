@@ -28,7 +28,7 @@ def apply(m, variant):
     m.stem_c1 = True
     m.fc_blas = True
     convmod.BLAS_1X1 = False
-    convmod.PAIR, convmod.PAIR_TILE, convmod.PAIR_L4 = True, 0, False
+    convmod.PAIR, convmod.PAIR_TILE, convmod.PAIR_L4, convmod.PAIR_X = True, 0, False, False
     m.par_down = False
     for kv in variant.split(","):
         if kv == "base":
@@ -54,6 +54,8 @@ def apply(m, variant):
             m.par_down = v == "1"
         elif k == "pairtile":
             convmod.PAIR_TILE = int(v)
+        elif k == "pairx":  # the layer3 -> layer4 pair (512-wide c1)
+            convmod.PAIR_X = v == "1"
         elif k == "pairl4":
             convmod.PAIR_L4 = v == "1"
         elif k.startswith("chain"):

@@ -38,15 +38,16 @@ def main():
     B = int(sys.argv[1]) if len(sys.argv) > 1 else 250
     dev = "cuda"
     out = {}
-    for mid, hw, tiles in ((256, 14, tuple(int(t) for t in os.environ.get("PAIR_TILES", "96,64").split(","))), (512, 7, (32,))):
+    for mid, hw, tiles, midn in ((256, 14, tuple(int(t) for t in os.environ.get("PAIR_TILES", "96,64").split(",")), 256),
+                                 (256, 14, (64,), 512), (512, 7, (32,), 512)):
         c4 = 4 * mid
         torch.manual_seed(0)
         c3 = pack_conv(torch.randn(c4, mid, 1, 1) / mid ** 0.5, torch.randn(c4) * 0.1).to(dev)
-        c1n = pack_conv(torch.randn(mid, c4, 1, 1) / c4 ** 0.5, torch.randn(mid) * 0.1).to(dev)
+        c1n = pack_conv(torch.randn(midn, c4, 1, 1) / c4 ** 0.5, torch.randn(midn) * 0.1).to(dev)
         t2 = torch.randn(B, hw, hw, mid, device=dev).relu().to(torch.bfloat16)
         res = torch.randn(B, hw, hw, c4, device=dev).to(torch.bfloat16)
         y = torch.empty(B, hw, hw, c4, device=dev, dtype=torch.bfloat16)
-        t1 = torch.empty(B, hw, hw, mid, device=dev, dtype=torch.bfloat16)
+        t1 = torch.empty(B, hw, hw, midn, device=dev, dtype=torch.bfloat16)
 
         def unfused():
             conv2d_nhwc(t2, c3, residual=res, relu=True, out=y)
@@ -57,8 +58,8 @@ def main():
              "c1_us": round(timed(lambda: conv2d_nhwc(y, c1n, relu=True, out=t1)), 2)}
         for t in tiles:
             r[f"pair_bm{t}_us"] = round(timed(lambda t=t: conv_pair(t2, c3, res, c1n, out=y, t1n_out=t1, tile_cfg=t)), 2)
-        out[f"mid{mid}"] = r
-        print(json.dumps({f"mid{mid}": r}), flush=True)
+        out[f"mid{mid}_{midn}"] = r
+        print(json.dumps({f"mid{mid}_{midn}": r}), flush=True)
     print(json.dumps({"batch": B, **out}))
 
 

@@ -89,7 +89,7 @@ __global__ __launch_bounds__(512) void conv_pair_kernel(const PairParams p) {
   constexpr int Y_BYTES = PR_CH / 32 * KBS;
   static_assert(PR_CH == 16 * PR_WAVES, "B: one 16-channel block per wave");
   static_assert(JC >= 1 && MIDN == 16 * PR_WAVES * JC, "C: whole 16-channel blocks per wave");
-  static_assert(MID >= MIDN, "T1' staging fits the T2 region");
+  static_assert(T2_BYTES + 2 * Y_BYTES >= MIDN / 32 * KBS, "T1' staging fits the T2 + Y regions");
   extern __shared__ __attribute__((aligned(1024))) uint8_t smem[];
   uint8_t* const t2s = smem;
 
@@ -239,7 +239,9 @@ __global__ __launch_bounds__(512) void conv_pair_kernel(const PairParams p) {
     }
   }
 
-  // ---- T1' epilogue through the T2 region (every wave finished its last B phase before the last barrier)
+  // ---- T1' epilogue through the T2 region (every wave finished its last B phase before the last barrier);
+  // a T1' wider than T2 (layer3 -> layer4's 512-wide c1) also spans the Y buffers: wait for every wave's C phase
+  if constexpr (MIDN / 32 * KBS > T2_BYTES) pbarrier();
 #pragma unroll
   for (int i = 0; i < FI; ++i)
 #pragma unroll
@@ -259,7 +261,7 @@ __global__ __launch_bounds__(512) void conv_pair_kernel(const PairParams p) {
 
 template <int MID, int C4, int MIDN, int BM, bool KF = true>
 int launch_pair(const PairParams& p, hipStream_t s) {
-  constexpr int LDS = (MID / 32 + 2 * PR_CH / 32) * kbs<BM>();
+  constexpr int LDS = (MID / 32 + 2 * PR_CH / 32 > MIDN / 32 ? MID / 32 + 2 * PR_CH / 32 : MIDN / 32) * kbs<BM>();
   static bool attr = false;
   if (!attr) {
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(conv_pair_kernel<MID, C4, MIDN, BM, KF>),
@@ -275,7 +277,7 @@ int launch_pair(const PairParams& p, hipStream_t s) {
 
 // Fused 1x1 pair (see header). t2 [M, mid], res / y [M, c4], t1n [M, midn] bf16 row-major (contiguous);
 // w3p / w1p packed by ops/conv.py pack_pair_weights; b3 [c4], b1n [midn] fp32.
-// (mid, c4, midn) = (256, 1024, 256) (layer3) or (512, 2048, 512) (layer4). bm_cfg: 0 = default tile,
+// (mid, c4, midn) = (256, 1024, 256) (layer3), (256, 1024, 512) (layer3 -> layer4) or (512, 2048, 512) (layer4). bm_cfg: 0 = default tile,
 // else the tile height in pixels (64 or 96 for layer3, 32 for layer4; taller tiles spill at 256 VGPRs).
 AI4E_API int ai4e_conv_pair_fwd(const void* t2, const void* w3p, const void* b3, const void* res, void* y,
                                 const void* w1p, const void* b1n, void* t1n, int M, int mid, int c4, int midn,
@@ -298,6 +300,13 @@ AI4E_API int ai4e_conv_pair_fwd(const void* t2, const void* w3p, const void* b3,
       case 96: return launch_pair<256, 1024, 256, 96>(p, stream);
       case 64: return launch_pair<256, 1024, 256, 64>(p, stream);
       case 97: return launch_pair<256, 1024, 256, 96, false>(p, stream);  // A/B: scheduler-placed fragment reads
+      default: return AI4E_EINVAL;
+    }
+  }
+  if (mid == 256 && c4 == 1024 && midn == 512) {  // last layer3 block -> layer4's first c1 (BM 64: 241 VGPRs at 96)
+    switch (bm_cfg) {
+      case 0:
+      case 64: return launch_pair<256, 1024, 512, 64>(p, stream);
       default: return AI4E_EINVAL;
     }
   }

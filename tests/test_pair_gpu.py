@@ -24,8 +24,10 @@ def _w(pc):
 
 
 CASES = [
-    # n, h, w, mid, tile
+    # n, h, w, mid, tile[, midn]
     (2, 14, 14, 256, 0),      # layer3 shape, M = 392 (partial last tile)
+    (2, 14, 14, 256, 0, 512),  # last layer3 block -> layer4's 512-wide c1
+    (1, 5, 7, 256, 64, 512),
     (2, 14, 14, 256, 64),
     (1, 5, 7, 256, 0),        # M = 35 < one tile
     (8, 14, 14, 256, 96),     # M = 1568: 17 tiles
@@ -36,12 +38,13 @@ CASES = [
 
 @pytest.mark.parametrize("case", CASES)
 def test_conv_pair(case):
-    n, h, w, mid, tile = case
+    n, h, w, mid, tile = case[:5]
+    midn = case[5] if len(case) > 5 else mid
     c4 = 4 * mid
-    assert pair_supported(mid, c4, mid)
+    assert pair_supported(mid, c4, midn)
     torch.manual_seed(11)
     c3 = pack_conv(torch.randn(c4, mid, 1, 1) / mid ** 0.5, torch.randn(c4) * 0.1).to(DEV)
-    c1n = pack_conv(torch.randn(mid, c4, 1, 1) / c4 ** 0.5, torch.randn(mid) * 0.1).to(DEV)
+    c1n = pack_conv(torch.randn(midn, c4, 1, 1) / c4 ** 0.5, torch.randn(midn) * 0.1).to(DEV)
     t2 = torch.randn(n, h, w, mid, device=DEV).relu().to(torch.bfloat16)
     res = torch.randn(n, h, w, c4, device=DEV).to(torch.bfloat16)
     y, t1n = conv_pair(t2, c3, res, c1n, tile_cfg=tile)
@@ -49,7 +52,7 @@ def test_conv_pair(case):
     y_ref = (t2.float().reshape(-1, mid) @ _w(c3).t() + c3.b_ref.to(DEV) + res.float().reshape(-1, c4)).relu()
     t_ref = (y_ref.to(torch.bfloat16).float() @ _w(c1n).t() + c1n.b_ref.to(DEV)).relu()
     y_err = (y.float().reshape(-1, c4) - y_ref).abs().max().item()
-    t_err = (t1n.float().reshape(-1, mid) - t_ref).abs().max().item()
+    t_err = (t1n.float().reshape(-1, midn) - t_ref).abs().max().item()
     assert y_err <= 0.02 * y_ref.abs().max().item() + 1e-2, y_err
     assert t_err <= 0.02 * t_ref.abs().max().item() + 1e-2, t_err
 
