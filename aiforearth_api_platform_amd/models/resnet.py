@@ -19,8 +19,8 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ..ops.conv import (PackedConv, chain_supported, conv2d_nhwc, conv_chain, fold_bn, pack_conv, pair_supported,
-                        pack_stem_s2d, stem_pool, stem_pool_c1, stem_pool_u8)
+from ..ops.conv import (PackedConv, chain_supported, conv2d_nhwc, conv_chain, fold_bn, pack_conv, pack_stem_s2d,
+                        pair_route, pair_supported, stem_pool, stem_pool_c1, stem_pool_u8)
 from ..ops.head import softmax_topk
 from ..ops.pool import (global_avgpool_nhwc, maxpool2d_nhwc, preprocess_s2d_u8, preprocess_u8,
                         space_to_depth_shifted)
@@ -267,7 +267,8 @@ class FusedResNet:
                     nxt = self.stages[si + 1][0][0]
                 else:
                     nxt = None
-                if nxt is not None and not chain_supported(c2.cout, nxt.cout) and chain_supported(c2.cout):
+                if (nxt is not None and not chain_supported(c2.cout, nxt.cout) and chain_supported(c2.cout)
+                        and not pair_route(c2.cout, c3.cout, nxt.cout)):
                     nxt = None  # keep the chain, run the next c1 as its own K1 launch
                 if (nxt is not None and i + 1 == len(blocks) and not chain_supported(c2.cout, nxt.cout)
                         and not pair_supported(c2.cout, c3.cout, nxt.cout) and self._side_ok(t1)):

@@ -283,8 +283,7 @@ def conv_chain(t1: torch.Tensor, c2: PackedConv, c3: PackedConv, residual: Optio
     midn = c1n.cout if c1n is not None else 0
     if _ext.backend_for(t1) != "hip" or not ok(mid, midn):
         y2 = conv2d_nhwc(t1, c2, relu=True)
-        if (c1n is not None and PAIR and _ext.backend_for(t1) == "hip" and residual is not None
-                and pair_supported(mid, c3.cout, midn) and (mid == 256 or PAIR_L4) and (midn == mid or PAIR_X)):
+        if c1n is not None and _ext.backend_for(t1) == "hip" and residual is not None and pair_route(mid, c3.cout, midn):
             return conv_pair(y2, c3, residual, c1n, out=out, t1n_out=t1n_out)  # K1p: c3 + residual + next c1
         conv2d_nhwc(y2, c3, residual=residual, relu=True, out=out)
         return out, (conv2d_nhwc(out, c1n, relu=True, out=t1n_out) if c1n is not None else None)
@@ -322,7 +321,18 @@ def pack_mfma_frags(w: torch.Tensor) -> torch.Tensor:
 
 def pair_supported(mid: int, c4: int, midn: int) -> bool:
     """Shapes the fused 1x1 pair kernel K1p (csrc/kernels/conv_pair.hip) is built for."""
-    return (mid, c4, midn) in ((256, 1024, 256), (256, 1024, 512), (512, 2048, 512))
+    return (mid, c4, midn) in ((256, 1024, 256), (128, 512, 256), (256, 1024, 512), (512, 2048, 512))
+
+
+def pair_route(mid: int, c4: int, midn: int) -> bool:
+    """Whether ``conv_chain`` runs this c3 + residual + next-c1 shape as K1p by default (env switches below)."""
+    if not PAIR or not pair_supported(mid, c4, midn):
+        return False
+    if mid == 128:
+        return PAIR_B
+    if mid == 512:
+        return PAIR_L4
+    return midn == mid or PAIR_X
 
 
 def _pair_pack(c3: PackedConv, c1n: PackedConv):
@@ -356,7 +366,7 @@ def conv_pair(t2: torch.Tensor, c3: PackedConv, residual: torch.Tensor, c1n: Pac
     w3p, w1p = _pair_pack(c3, c1n)
     _ext.call("ai4e_conv_pair_fwd", t2.data_ptr(), w3p.data_ptr(), c3.bias.data_ptr(), residual.data_ptr(),
               out.data_ptr(), w1p.data_ptr(), c1n.bias.data_ptr(), t1n.data_ptr(), n * h * w, mid, c4, midn,
-              (PAIR_TILE if midn == mid else 0) if tile_cfg < 0 else tile_cfg, _ext.stream_ptr(t2.device))
+              (PAIR_TILE if (mid, midn) == (256, 256) else 0) if tile_cfg < 0 else tile_cfg, _ext.stream_ptr(t2.device))
     return out, t1n
 
 
@@ -369,6 +379,9 @@ PAIR_L4 = os.environ.get("AI4E_PAIR_L4", "0") not in ("0", "off", "")
 # the last layer3 block's c3 + residual with layer4's first (512-wide) c1, opt-in (AI4E_PAIR_X=1): 110 vs 124 us in
 # isolation, but -1 to -7 % images/s in the serving worker (profiles/r2_pair/README.md)
 PAIR_X = os.environ.get("AI4E_PAIR_X", "0") not in ("0", "off", "")
+# the last layer2 block as a K1 3x3 + K1p (c3 + residual + layer3's first c1) instead of the K1c chain + a K1 c1
+# (AI4E_PAIR_B=1)
+PAIR_B = os.environ.get("AI4E_PAIR_B", "0") not in ("0", "off", "")
 
 
 # K1c tile config per bottleneck width (reserved: the kernel uses 128-pixel tiles for both widths)

@@ -28,7 +28,7 @@ def apply(m, variant):
     m.stem_c1 = True
     m.fc_blas = True
     convmod.BLAS_1X1 = False
-    convmod.PAIR, convmod.PAIR_TILE, convmod.PAIR_L4, convmod.PAIR_X = True, 0, False, False
+    convmod.PAIR, convmod.PAIR_TILE, convmod.PAIR_L4, convmod.PAIR_X, convmod.PAIR_B = True, 0, False, False, False
     m.par_down = False
     for kv in variant.split(","):
         if kv == "base":
@@ -54,6 +54,8 @@ def apply(m, variant):
             m.par_down = v == "1"
         elif k == "pairtile":
             convmod.PAIR_TILE = int(v)
+        elif k == "pairb":  # the layer2 -> layer3 boundary as K1 3x3 + K1p
+            convmod.PAIR_B = v == "1"
         elif k == "pairx":  # the layer3 -> layer4 pair (512-wide c1)
             convmod.PAIR_X = v == "1"
         elif k == "pairl4":

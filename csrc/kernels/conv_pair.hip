@@ -277,7 +277,8 @@ int launch_pair(const PairParams& p, hipStream_t s) {
 
 // Fused 1x1 pair (see header). t2 [M, mid], res / y [M, c4], t1n [M, midn] bf16 row-major (contiguous);
 // w3p / w1p packed by ops/conv.py pack_pair_weights; b3 [c4], b1n [midn] fp32.
-// (mid, c4, midn) = (256, 1024, 256) (layer3), (256, 1024, 512) (layer3 -> layer4) or (512, 2048, 512) (layer4). bm_cfg: 0 = default tile,
+// (mid, c4, midn) = (256, 1024, 256) (layer3), (128, 512, 256) (layer2 -> layer3), (256, 1024, 512) (layer3 -> layer4)
+// or (512, 2048, 512) (layer4). bm_cfg: 0 = default tile,
 // else the tile height in pixels (64 or 96 for layer3, 32 for layer4; taller tiles spill at 256 VGPRs).
 AI4E_API int ai4e_conv_pair_fwd(const void* t2, const void* w3p, const void* b3, const void* res, void* y,
                                 const void* w1p, const void* b1n, void* t1n, int M, int mid, int c4, int midn,
@@ -300,6 +301,14 @@ AI4E_API int ai4e_conv_pair_fwd(const void* t2, const void* w3p, const void* b3,
       case 96: return launch_pair<256, 1024, 256, 96>(p, stream);
       case 64: return launch_pair<256, 1024, 256, 64>(p, stream);
       case 97: return launch_pair<256, 1024, 256, 96, false>(p, stream);  // A/B: scheduler-placed fragment reads
+      default: return AI4E_EINVAL;
+    }
+  }
+  if (mid == 128 && c4 == 512 && midn == 256) {  // last layer2 block -> layer3's first c1
+    switch (bm_cfg) {
+      case 0:
+      case 96: return launch_pair<128, 512, 256, 96>(p, stream);
+      case 64: return launch_pair<128, 512, 256, 64>(p, stream);
       default: return AI4E_EINVAL;
     }
   }

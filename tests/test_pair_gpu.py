@@ -28,6 +28,8 @@ CASES = [
     (2, 14, 14, 256, 0),      # layer3 shape, M = 392 (partial last tile)
     (2, 14, 14, 256, 0, 512),  # last layer3 block -> layer4's 512-wide c1
     (1, 5, 7, 256, 64, 512),
+    (2, 28, 28, 128, 0, 256),  # last layer2 block -> layer3's first c1
+    (1, 5, 9, 128, 64, 256),
     (2, 14, 14, 256, 64),
     (1, 5, 7, 256, 0),        # M = 35 < one tile
     (8, 14, 14, 256, 96),     # M = 1568: 17 tiles
