@@ -12,6 +12,8 @@
 //
 // Input: the s2d layout of preprocess_s2d (ops/pool.py) [N, H, W, 16] bf16, K = (kh, kw, c) = 4x4x16 = 256
 // padded top/left 1 (bottom/right 2: bounds-checked). Output [N, PH, PW, 64], PH = ceil(H/2).
+#include <cstdlib>
+
 #include "conv_common.h"
 
 namespace {
@@ -397,7 +399,14 @@ int launch_direct(const StemParams& p, long nb, hipStream_t stream) {
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     cus = 256;
-  const long grid = nb < 2L * cus ? nb : 2L * cus;  // two persistent workgroups per CU
+  // persistent workgroups per CU (AI4E_STEM_WPC, default 2): each strides over the tiles, so a workgroup that
+  // starts late (CUs held by the other serving stream's kernels) delays the whole launch by its full share
+  static const long wpc = [] {
+    const char* e = getenv("AI4E_STEM_WPC");
+    const long v = e ? atol(e) : 2;
+    return v < 1 ? 1L : v;
+  }();
+  const long grid = nb < wpc * cus ? nb : wpc * cus;
   hipLaunchKernelGGL((stem_pool_direct_kernel<U8, C1>), dim3(static_cast<unsigned>(grid)), dim3(256), D_LDS, stream, p,
                      static_cast<int>(nb));
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
