@@ -175,8 +175,7 @@ class FusedResNet:
         # (profiles/r2_pair/README.md)
         self.par_down = os.environ.get("AI4E_PAR_DOWN", "0") not in ("0", "off", "")
         self._side: dict = {}
-        self._side_pool = ([torch.cuda.Stream(device=self.device) for _ in range(4)]
-                           if self.device.type == "cuda" and torch.cuda.is_available() else [])
+        self._side_pool: List[torch.cuda.Stream] = []  # created on first use outside a graph capture
         # stages: runs of blocks starting at a block with a downsample conv
         self.stages: List[List[Tuple[PackedConv, PackedConv, PackedConv, Optional[PackedConv]]]] = []
         for blk in self.blocks:
@@ -284,7 +283,11 @@ class FusedResNet:
         return outs if collect else y
 
     def _side_ok(self, t: torch.Tensor) -> bool:
-        return self.par_down and bool(self._side_pool) and t.is_cuda
+        if not (self.par_down and t.is_cuda):
+            return False
+        if not self._side_pool and not torch.cuda.is_current_stream_capturing():
+            self._side_pool = [torch.cuda.Stream(device=t.device) for _ in range(4)]
+        return bool(self._side_pool)
 
     def _c1_down_parallel(self, y: torch.Tensor, c1: PackedConv, down: PackedConv):
         """(relu(c1(y)), down(y)) with the downsample forked onto a side stream of the current stream."""
