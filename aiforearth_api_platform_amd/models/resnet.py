@@ -396,7 +396,26 @@ class FusedResNet:
 
     def logits(self, x: torch.Tensor, preprocess=None) -> torch.Tensor:
         """bf16 logits [N, classes]."""
-        f = global_avgpool_nhwc(self.forward_features(x, preprocess))
+        return self._head_logits(self.forward_features(x, preprocess))
+
+    # Two-part serving forward (runtime/engine.py ``split``): stem .. layer2 | layer3 .. top-k. The serving engine
+    # captures each part as its own graph and starts batch k+1's front part only once batch k's has finished, so
+    # the two compute streams run an HBM-heavy front (stem, layer1/2 chains) beside a back (layer3/4, head).
+    SPLIT_STAGE = 2
+
+    def can_split(self) -> bool:
+        return self.chain and not self.chain_mb and not self.chunk and len(self.stages) > self.SPLIT_STAGE
+
+    def front_u8(self, img_u8: torch.Tensor) -> Tuple[torch.Tensor, ...]:
+        y, t1 = self._stem_t1(preprocess_s2d_u8(img_u8))
+        y, t1 = self._stages_chained(y, t1=t1, s1=self.SPLIT_STAGE)
+        return (y,) if t1 is None else (y, t1)
+
+    def back_topk(self, y: torch.Tensor, t1: Optional[torch.Tensor] = None, k: int = 5):
+        return softmax_topk(self._head_logits(self._stages_chained(y, t1=t1, s0=self.SPLIT_STAGE)), k)
+
+    def _head_logits(self, feats: torch.Tensor) -> torch.Tensor:
+        f = global_avgpool_nhwc(feats)
         if self.fc_blas and f.is_cuda:
             # [N, 2048] x [2048, classes]: a plain library GEMM (hipBLASLt picks split-K); the K1 tile grid
             # has only 16 workgroups at N = 256

@@ -144,6 +144,13 @@ class InferenceEngine:
         self._graph_out: Dict[Tuple[int, int], Tuple[torch.Tensor, ...]] = {}
         self.compute_done: List[Optional[torch.cuda.Event]] = [None] * self.nbuf
         self._k = 0
+        # phase-offset split (AI4E_ENGINE_SPLIT=1, output_fn.split = (front, back)): two graphs per (buffer, bucket);
+        # batch k+1's front waits for batch k's front, so the compute streams pair a front with a back
+        sp = getattr(output_fn, "split", None) if cuda and len(self.compute_streams) > 1 else None
+        self.split = sp if sp is not None and os.environ.get("AI4E_ENGINE_SPLIT", "0") not in ("0", "off", "") else None
+        self.graphs2: Dict[Tuple[int, int], torch.cuda.CUDAGraph] = {}
+        self._mid: Dict[Tuple[int, int], Tuple[torch.Tensor, ...]] = {}
+        self._front_done: Optional[torch.cuda.Event] = None
 
     # -------------------------------------------------------------- forward
     def _forward_into(self, buf: int, b: int) -> Tuple[torch.Tensor, ...]:
@@ -185,8 +192,18 @@ class InferenceEngine:
         for buf in range(self.nbuf):
             for b in self.buckets:
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, stream=self.compute_stream):
-                    outs = self._forward_into(buf, b)
+                if self.split is not None:
+                    front, back = self.split
+                    with torch.cuda.graph(g, stream=self.compute_stream):
+                        mid = tuple(front(self.inputs[buf][:b]))
+                    g2 = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g2, stream=self.compute_stream):
+                        outs = tuple(back(*mid))
+                    self._mid[(buf, b)] = mid  # keeps the front graph's outputs alive for the back graph
+                    self.graphs2[(buf, b)] = g2
+                else:
+                    with torch.cuda.graph(g, stream=self.compute_stream):
+                        outs = self._forward_into(buf, b)
                 self.graphs[(buf, b)] = g
                 self._graph_out[(buf, b)] = outs
         torch.cuda.synchronize(self.device)
@@ -224,7 +241,15 @@ class InferenceEngine:
         st = self.compute_streams[buf % len(self.compute_streams)]
         st.wait_event(ev)
         with torch.cuda.stream(st):
-            if self.use_graphs and (buf, b) in self.graphs:
+            if self.use_graphs and (buf, b) in self.graphs2:
+                if self._front_done is not None:
+                    st.wait_event(self._front_done)
+                self.graphs[(buf, b)].replay()
+                self._front_done = torch.cuda.Event()
+                self._front_done.record(st)
+                self.graphs2[(buf, b)].replay()
+                outs = self._graph_out[(buf, b)]
+            elif self.use_graphs and (buf, b) in self.graphs:
                 self.graphs[(buf, b)].replay()
                 outs = self._graph_out[(buf, b)]
             else:
