@@ -50,10 +50,10 @@ struct StemParams {
   int kpad1;
 };
 
+typedef unsigned short u16x2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t max_bf16x2(uint32_t a, uint32_t b) {
-  // both halves non-negative bf16: unsigned 16-bit max per half
-  const uint32_t lo = max(a & 0xffffu, b & 0xffffu), hi = max(a >> 16, b >> 16);
-  return lo | (hi << 16);
+  // both halves non-negative bf16: unsigned 16-bit max per half, one v_pk_max_u16
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(u16x2_t, a), __builtin_bit_cast(u16x2_t, b)));
 }
 
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) void stem_pool_kernel(const StemParams p) {
