@@ -243,6 +243,12 @@ def run_node_bench(args, spec, path: str, metric: str, unit: str = "images/s", c
     tune_gc()
     sync(denv)
     # ---------------------------------------------------------------- timed region
+    tel = None
+    if rank == 0 and args.device == "cuda":
+        from ..utils.gpu_telemetry import GpuTelemetry
+
+        tel = GpuTelemetry(denv.local_rank)  # clocks / power / hotspot sampled every 200 ms (fail-soft)
+        tel.start()
     t0 = time.perf_counter()
     tm0 = time.monotonic()
     cth = threading.Thread(target=client.run, args=(args.steps,), daemon=True)
@@ -253,6 +259,7 @@ def run_node_bench(args, spec, path: str, metric: str, unit: str = "images/s", c
     sync(denv)
     dt = time.perf_counter() - t0
     tm1 = time.monotonic()
+    telemetry = tel.stop() if tel is not None else {}
     p50 = p99 = 0.0
     stats = {}
     if rank == 0:
@@ -292,6 +299,8 @@ def run_node_bench(args, spec, path: str, metric: str, unit: str = "images/s", c
         }
         if flops_per_item:
             out["tflops_effective"] = round(value * flops_per_item / 1e12, 2)
+        if telemetry:
+            out["gpu_telemetry"] = telemetry  # rank 0's GPU during the timed region
         line = json.dumps(out)
         print(line, flush=True)
         if args.json_out:

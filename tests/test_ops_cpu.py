@@ -130,3 +130,15 @@ def test_conv_pair_cpu_fallback_matches_two_convs():
     y_ref = conv2d_nhwc(t2, c3, residual=res, relu=True)
     assert torch.allclose(y, y_ref)
     assert torch.allclose(t1n, conv2d_nhwc(y_ref, c1n, relu=True))
+
+
+def test_gpu_telemetry_fail_soft_and_summary():
+    from aiforearth_api_platform_amd.utils.gpu_telemetry import GpuTelemetry, summarize
+
+    t = GpuTelemetry(0)  # no GPU driver in the CPU container: empty, never raises
+    t.start(0.01)
+    s = t.stop()
+    assert isinstance(s, dict)
+    out = summarize([{"gfx_mhz": 2000.0, "power_w": 900.0}, {"gfx_mhz": 2400.0}])
+    assert out["gfx_mhz"] == {"min": 2000.0, "mean": 2200.0, "max": 2400.0, "n": 2}
+    assert out["power_w"]["n"] == 1
