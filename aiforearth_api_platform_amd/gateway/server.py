@@ -151,12 +151,13 @@ class Gateway:
 
     def collect_backend_metrics(self) -> None:
         """Per-GPU gauges from the worker pools' heartbeats (survey §5.5): HBM used/total, GPU busy ms,
-        images, batches, in-flight batches; the batch-size histogram comes from the native scheduler."""
+        images, batches, in-flight batches, GFX clock and board power; the batch-size histogram comes from the
+        native scheduler."""
         for path, st in self.backend_stats().items():
             for w in st.get("workers", []):
                 tag = f"{path}/gpu{w.get('rank')}"
                 for k in ("hbm_used", "hbm_total", "gpu_busy_ms", "images", "batches", "outstanding",
-                          "failed_items", "retried_items", "xgmi_tx_bytes", "xgmi_rx_bytes"):
+                          "failed_items", "retried_items", "xgmi_tx_bytes", "xgmi_rx_bytes", "gfx_mhz", "power_w"):
                     if k in w:
                         REGISTRY.gauge(f"{k}{tag}").set(float(w[k]))
             for i, c in enumerate(st.get("batch_histogram", [])):

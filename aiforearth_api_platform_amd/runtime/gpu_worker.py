@@ -140,6 +140,11 @@ class GpuWorker:
         return d
 
     def _heartbeat(self) -> None:
+        tel = None
+        if self.device.type == "cuda":
+            from ..utils.gpu_telemetry import GpuTelemetry
+
+            tel = GpuTelemetry(self.device.index or 0)  # GFX clock and power per heartbeat (fail-soft)
         while self.alive.is_set():
             used = total = 0
             if self.device.type == "cuda":
@@ -153,8 +158,10 @@ class GpuWorker:
             if callable(xg):
                 b = xg()
                 tx, rx = int(b.get("sent", 0)), int(b.get("received", 0))
+            smp = tel.sample() if tel is not None else {}
             try:
-                self.conn.heartbeat(time.monotonic(), used, total, self.busy_ms, self.batches, tx, rx)
+                self.conn.heartbeat(time.monotonic(), used, total, self.busy_ms, self.batches, tx, rx,
+                                    smp.get("gfx_mhz", 0.0), smp.get("power_w", 0.0))
             except (BrokenPipeError, EOFError, OSError):
                 return
             time.sleep(self.hb_interval)

@@ -283,7 +283,8 @@ def run_node_bench(args, spec, path: str, metric: str, unit: str = "images/s", c
                     http["with_frontends"] = http_phase(cp, pool, args.http_seconds, B, spec.item_shape, path, nfe)
             except Exception as e:  # the headline number stands on its own
                 http = {"error": repr(e)}
-        workers = [{k: w.get(k) for k in ("rank", "images", "batches", "pinned", "hbm_used", "gpu_busy_ms")}
+        workers = [{k: w.get(k) for k in ("rank", "images", "batches", "pinned", "hbm_used", "gpu_busy_ms", "gfx_mhz",
+                                          "power_w")}
                    for w in stats.get("workers", [])]
         out = {
             "metric": metric, "value": round(value, 2), "unit": unit, "n_gpus": world, "steps": args.steps,

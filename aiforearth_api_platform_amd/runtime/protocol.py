@@ -18,7 +18,7 @@ IT_OK, IT_INVALID, IT_ERROR, IT_RETRY = 0, 1, 2, 3
 
 _U32 = struct.Struct("<I")
 _READY = struct.Struct("<Iii")
-_HB = struct.Struct("<IdQQdQQQ")
+_HB = struct.Struct("<IdQQdQQQdd")
 _DONE_HDR = struct.Struct("<IQII5d")
 _BATCH_HDR = struct.Struct("<IQII")
 _SLOTS_HDR = struct.Struct("<III")
@@ -55,8 +55,8 @@ class FrameConn:
         self.send(_READY.pack(F_READY, rank, int(pinned)) + json.dumps(info).encode())
 
     def heartbeat(self, t: float, hbm_used: int, hbm_total: int, busy_ms: float, batches: int, xgmi_tx: int = 0,
-                  xgmi_rx: int = 0) -> None:
-        self.send(_HB.pack(F_HB, t, hbm_used, hbm_total, busy_ms, batches, xgmi_tx, xgmi_rx))
+                  xgmi_rx: int = 0, gfx_mhz: float = 0.0, power_w: float = 0.0) -> None:
+        self.send(_HB.pack(F_HB, t, hbm_used, hbm_total, busy_ms, batches, xgmi_tx, xgmi_rx, gfx_mhz, power_w))
 
     def done(self, bid: int, status: np.ndarray, rows: bytes, row_bytes: int, stage: Sequence[float]) -> None:
         n = int(status.shape[0])

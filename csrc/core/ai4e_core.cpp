@@ -305,6 +305,8 @@ PYBIND11_MODULE(_ai4e_core, m) {
                d["hbm_total"] = w.hbm_total;
                d["xgmi_tx_bytes"] = w.xgmi_tx;
                d["xgmi_rx_bytes"] = w.xgmi_rx;
+               d["gfx_mhz"] = w.gfx_mhz;
+               d["power_w"] = w.power_w;
                d["info"] = w.info;
                out.append(d);
              }

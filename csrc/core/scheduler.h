@@ -13,7 +13,8 @@
 // recv_bytes. Payload = u32 type + fields (little-endian):
 //
 //   READY  (w->s) i32 rank, i32 pinned, utf-8 JSON info
-//   HB     (w->s) f64 t, u64 hbm_used, u64 hbm_total, f64 gpu_busy_ms, u64 batches, u64 xgmi_tx, u64 xgmi_rx
+//   HB     (w->s) f64 t, u64 hbm_used, u64 hbm_total, f64 gpu_busy_ms, u64 batches, u64 xgmi_tx, u64 xgmi_rx,
+//                 f64 gfx_mhz, f64 power_w (GPU telemetry; 0 = unavailable)
 //   DONE   (w->s) u64 bid, u32 n, u32 row_bytes, f64 stage[5], u8 status[n] (padded to 8), rows
 //   BATCH  (s->w) u64 bid, u32 n, u32 0, i64 slots[n]
 //   STOP   (s->w)
@@ -91,7 +92,7 @@ struct WorkerStats {
   bool ready = false, alive = false, pinned = false;
   uint64_t batches = 0, images = 0, failed_items = 0, retried_items = 0;
   size_t outstanding = 0;
-  double last_hb_age_s = 0, gpu_busy_ms = 0;
+  double last_hb_age_s = 0, gpu_busy_ms = 0, gfx_mhz = 0, power_w = 0;
   uint64_t hbm_used = 0, hbm_total = 0, xgmi_tx = 0, xgmi_rx = 0;
   std::string info;
 };
@@ -229,6 +230,8 @@ class NodeScheduler {
       s.hbm_total = w.hbm_total;
       s.xgmi_tx = w.xgmi_tx;
       s.xgmi_rx = w.xgmi_rx;
+      s.gfx_mhz = w.gfx_mhz;
+      s.power_w = w.power_w;
       s.info = w.info;
       out.push_back(s);
     }
@@ -285,7 +288,7 @@ class NodeScheduler {
     double last_hb = 0;
     std::unordered_map<uint64_t, Outstanding> out;
     uint64_t batches = 0, images = 0, failed_items = 0, retried_items = 0;
-    double gpu_busy_ms = 0;
+    double gpu_busy_ms = 0, gfx_mhz = 0, power_w = 0;
     uint64_t hbm_used = 0, hbm_total = 0, xgmi_tx = 0, xgmi_rx = 0;
     std::string info;
   };
@@ -600,6 +603,10 @@ class NodeScheduler {
           if (len >= 56) {
             std::memcpy(&w.xgmi_tx, p + 40, 8);
             std::memcpy(&w.xgmi_rx, p + 48, 8);
+          }
+          if (len >= 72) {
+            std::memcpy(&w.gfx_mhz, p + 56, 8);
+            std::memcpy(&w.power_w, p + 64, 8);
           }
           break;
         }
