@@ -127,6 +127,7 @@ class GpuWorker:
         self.batches = 0
         self.isolated_batches = 0
         self.busy_ms = 0.0
+        self._ready_sent = threading.Event()
         self.alive = threading.Event()
         self.alive.set()
 
@@ -141,11 +142,13 @@ class GpuWorker:
 
     def _heartbeat(self) -> None:
         tel = None
-        if self.device.type == "cuda":
-            from ..utils.gpu_telemetry import GpuTelemetry
-
-            tel = GpuTelemetry(self.device.index or 0)  # GFX clock and power per heartbeat (fail-soft)
         while self.alive.is_set():
+            # GFX clock and power per heartbeat (fail-soft); amdsmi is initialised only once READY has gone out,
+            # never concurrently with the main thread's HIP calls (an amdsmi_init racing them broke device lookup)
+            if tel is None and self.device.type == "cuda" and self._ready_sent.is_set():
+                from ..utils.gpu_telemetry import GpuTelemetry
+
+                tel = GpuTelemetry(self.device.index or 0)
             used = total = 0
             if self.device.type == "cuda":
                 try:
@@ -176,6 +179,7 @@ class GpuWorker:
         fin = threading.Thread(target=self._completion_loop, daemon=True, name=f"ai4e-done-{self.rank}")
         fin.start()
         self.conn.ready(self.rank, pinned, self.info())
+        self._ready_sent.set()
         try:
             while True:
                 try:
