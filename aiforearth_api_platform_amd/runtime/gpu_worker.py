@@ -14,7 +14,8 @@ that fail on their own are reported failed — the rest of the batch completes.
 Fault injection (``AI4E_FAULT_INJECTION``, comma list, ``key=value[@rank]``):
 ``exit_after=<batches>``, ``hang_after=<batches>``, ``delay_ms=<ms>``, ``fail_batch=<batch index>``
 (the launch of that batch raises; drives the isolation path), ``fail_item=<slot>`` (the isolated run
-of that slot raises -> that item fails).
+of that slot raises -> that item fails), ``fail_finalize=<n>`` (the n-th batch retirement raises -> its
+items are returned for another delivery).
 """
 from __future__ import annotations
 
@@ -211,9 +212,40 @@ class GpuWorker:
                 self._finalize(p)
             except (BrokenPipeError, EOFError, OSError):
                 pass
-            with self._idle:
-                self._inflight -= 1
-                self._idle.notify_all()
+            except Exception as e:  # never let the retire thread die: answer the batch, keep the count right
+                self._fail_pending(p, e)
+            finally:
+                with self._idle:
+                    self._inflight -= 1
+                    self._idle.notify_all()
+
+    def _fail_pending(self, p: _Pending, err: Exception) -> None:
+        """A batch whose completion raised (device fault in the sync, an encode error): its valid items go
+        back to the queue (IT_RETRY: another delivery, bounded by max-delivery) so no task stays 'running'
+        until a lock expires. A device error is sticky (every later sync raises too): then the worker also
+        stops heartbeating and exits, so the scheduler marks it dead and its restart path runs."""
+        import sys
+
+        print(f"[ai4e worker {self.rank}] batch {p.bid} completion failed ({err!r}); returning its items for retry",
+              file=sys.stderr, flush=True)
+        status = p.status.copy()
+        status[p.valid] = P.IT_RETRY
+        try:
+            now = time.monotonic()
+            self.conn.done(p.bid, status, bytes(p.n * self.row_bytes), self.row_bytes, (p.t_recv, now, now, 0, 0))
+        except Exception:
+            pass
+        if self.device.type == "cuda" and not self._device_ok():
+            self.alive.clear()
+            print(f"[ai4e worker {self.rank}] device error is sticky; exiting", file=sys.stderr, flush=True)
+            os._exit(19)
+
+    def _device_ok(self) -> bool:
+        try:
+            torch.cuda.synchronize(self.device)
+            return True
+        except Exception:
+            return False
 
     def _drain(self) -> None:
         with self._idle:
@@ -270,6 +302,9 @@ class GpuWorker:
         return rows.tobytes()
 
     def _finalize(self, p: _Pending) -> None:
+        self._finalized = getattr(self, "_finalized", 0) + 1
+        if self.fault.get("fail_finalize") == self._finalized:
+            raise RuntimeError("injected completion failure")
         p.res.done.synchronize()
         t_done = time.monotonic()
         h2d_ms, comp_ms = p.res.gpu_ms()

@@ -233,32 +233,41 @@ def run_node_bench(args, spec, path: str, metric: str, unit: str = "images/s", c
         while pool.images < target:
             time.sleep(0.0002)
 
-    # ---------------------------------------------------------------- warmup (untimed)
+    # ---------------------------------------------------------------- steady-state window
+    # The clients submit warmup + steps + tail steps back to back and never stop between warmup and the
+    # timed steps, so the serving pipeline never drains and refills inside the window. The window is
+    # defined by completion counts on the scheduler (rank 0): t0 when warmup*B*world images have
+    # completed, t1 when (warmup+steps)*B*world have; exactly steps*B*world images complete inside it.
+    # The tail keeps the pipeline full up to t1 (its images are served, not counted). The barrier +
+    # device drain bracket the whole run on every rank.
+    tail = max(1, args.inflight + 1)
+    warm_n = args.warmup * B * world
     sync(denv)
-    wth_c = threading.Thread(target=client.run, args=(args.warmup,), daemon=True)
-    wth_c.start()
-    wth_c.join()
-    if rank == 0:
-        wait_images(args.warmup * B * world)
     tune_gc()
-    sync(denv)
-    # ---------------------------------------------------------------- timed region
     tel = None
     if rank == 0 and args.device == "cuda":
         from ..utils.gpu_telemetry import GpuTelemetry
 
         tel = GpuTelemetry(denv.local_rank)  # clocks / power / hotspot sampled every 200 ms (fail-soft)
         tel.start()
-    t0 = time.perf_counter()
-    tm0 = time.monotonic()
-    cth = threading.Thread(target=client.run, args=(args.steps,), daemon=True)
+    t_start = time.perf_counter()
+    cth = threading.Thread(target=client.run, args=(args.warmup + args.steps + tail,), daemon=True)
     cth.start()
+    dt, ramp_s, drain_s = 0.0, 0.0, 0.0
+    tm0 = tm1 = time.monotonic()
     if rank == 0:
+        if warm_n:  # (no warmup: the window starts at the first submission, fill included)
+            wait_images(warm_n)
+            t0, tm0 = time.perf_counter(), time.monotonic()
+        else:
+            t0 = t_start
         wait_images(total_images)
+        t1, tm1 = time.perf_counter(), time.monotonic()
+        dt, ramp_s = t1 - t0, t0 - t_start
+        wait_images(total_images + tail * B * world)
+        drain_s = time.perf_counter() - t1
     cth.join()
     sync(denv)
-    dt = time.perf_counter() - t0
-    tm1 = time.monotonic()
     telemetry = tel.stop() if tel is not None else {}
     p50 = p99 = 0.0
     stats = {}
@@ -293,6 +302,10 @@ def run_node_bench(args, spec, path: str, metric: str, unit: str = "images/s", c
             "dtype": "bf16", "data": "synthetic uint8 payloads (written into the payload ring per submission), "
                                      "random-init weights",
             "p50_task_latency_ms": round(p50, 3), "p99_task_latency_ms": round(p99, 3),
+            "window": {"kind": "steady-state, by completion count on the scheduler",
+                       "first_counted_image": args.warmup * B * world, "counted_images": images,
+                       "warmup_ramp_ms": round(ramp_s * 1e3, 3), "tail_drain_ms": round(drain_s * 1e3, 3),
+                       "tail_steps_uncounted": tail},
             "config": dict(config or {}, global_batch=B * world, per_gpu_batch=B, parallelism=f"dp{world}",
                            serving_path="node scheduler (native) + 1 GPU worker process per GPU",
                            ingest_shards=world, ring_slots_per_shard=part, hip_graphs=spec.use_graphs),

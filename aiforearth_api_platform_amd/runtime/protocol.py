@@ -76,10 +76,13 @@ class FrameConn:
                    ack: bool = True) -> None:
         """Ingest front-end: enqueue payloads under task ids minted here (all ids the same length)."""
         a = np.asarray(slots, dtype=np.int64)
-        il = len(ids[0]) if ids else 0
+        enc = [i.encode("ascii") for i in ids]  # ids are validated ASCII (frontend.valid_task_id)
+        il = len(enc[0]) if enc else 0
+        if any(len(e) != il for e in enc):
+            raise ValueError("submit_ids: all task ids must have the same byte length")
         tb = trace.encode()
         self.send(b"".join((_SUBMIT_IDS_HDR.pack(F_SUBMIT_IDS, a.shape[0], len(tb), il, int(ack), token),
-                            a.tobytes(), "".join(ids).encode(), tb)))
+                            a.tobytes(), b"".join(enc), tb)))
 
 
 def frame_type(buf: bytes) -> int:

@@ -132,6 +132,9 @@ class WorkerPool:
         self.store = control_plane.store
         if not isinstance(self.store, native.TaskStore) or not isinstance(self.queue, native.DispatchQueue):
             raise RuntimeError("the worker pool needs the native store/queue backend (AI4E_STORE_BACKEND=native)")
+        # dead workers are found by heartbeat and their batches requeued by the scheduler; a peek-lock expiry
+        # redelivery would give a batch's ring slots to a second worker while the first still holds them
+        self.queue.set_lock_duration(0.0)
         self.spec = spec
         self.devices = list(devices)
         # 3 batches in flight per worker: two overlap on the GPU's two compute streams while the third is

@@ -525,3 +525,15 @@ class DispatchQueue:
     def depth(self) -> int:
         with self._cv:
             return len(self._ready) + len(self._scheduled)
+
+    def set_lock_duration(self, seconds: float) -> None:
+        """<= 0 disables lock expiry (queues drained by the NodeScheduler: dispatch_queue.h)."""
+        with self._cv:
+            self._lock_s = seconds
+            now = time.monotonic()
+            for m in self._inflight.values():
+                m.lock_until = now + seconds if seconds > 0 else 0.0
+
+    @property
+    def lock_duration(self) -> float:
+        return self._lock_s

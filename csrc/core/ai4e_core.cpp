@@ -236,7 +236,9 @@ PYBIND11_MODULE(_ai4e_core, m) {
              d["sent"] = s.sent;
              return d;
            })
-      .def("depth", &DispatchQueue::depth);
+      .def("depth", &DispatchQueue::depth)
+      .def("set_lock_duration", &DispatchQueue::set_lock_duration, py::arg("seconds"))
+      .def_property_readonly("lock_duration", &DispatchQueue::lock_duration);
 
   py::class_<SlotRing, std::shared_ptr<SlotRing>>(m, "SlotRing")
       .def(py::init<int64_t, int64_t>(), py::arg("nslots"), py::arg("base") = 0)

@@ -164,6 +164,20 @@ class DispatchQueue {
   // Wake every blocked receiver (scheduler shutdown).
   void kick() { cv_.notify_all(); }
 
+  // Lock duration for later receives; <= 0 disables lock expiry. A queue drained by the NodeScheduler
+  // runs with expiry off: the scheduler detects dead workers by heartbeat and requeues their batches
+  // itself, and an expiry-redelivery of a batch the first worker still holds would hand its ring
+  // slots to a second worker while the first may still complete them.
+  void set_lock_duration(double s) {
+    std::lock_guard<std::mutex> g(mu_);
+    lock_s_ = s;
+    for (auto& kv : inflight_) kv.second.lock_until = s > 0 ? mono_now() + s : 0;
+  }
+  double lock_duration() {
+    std::lock_guard<std::mutex> g(mu_);
+    return lock_s_;
+  }
+
  private:
   struct Later {
     bool operator()(const Message& a, const Message& b) const { return a.visible_at > b.visible_at; }

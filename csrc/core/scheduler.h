@@ -433,6 +433,19 @@ class NodeScheduler {
     return ids.size();
   }
 
+  // A connection with a declared ring partition (torchrun rank, ingest front-end) may only submit slots of
+  // that partition; connections without one (spawned local workers do not submit) are not restricted.
+  bool in_partition(int rank, const std::vector<int64_t>& slots) {
+    std::lock_guard<std::mutex> g(mu_);
+    for (const auto& pt : remote_parts_) {
+      if (pt.rank != rank) continue;
+      for (int64_t s : slots)
+        if (s < pt.base || s >= pt.base + pt.len) return false;
+      return true;
+    }
+    return true;
+  }
+
   void feed(const std::vector<std::string>& ids) {
     {
       std::lock_guard<std::mutex> g(feed_mu_);
@@ -614,10 +627,13 @@ class NodeScheduler {
           on_done(w, p, len);
           break;
         case F_SUBMIT: {
+          if (len < 8) break;  // malformed: ignore
           uint32_t n;
           std::memcpy(&n, p, 4);
+          if (len < 8 + n * 8ull) break;
           std::vector<int64_t> slots(n);
           if (n) std::memcpy(slots.data(), p + 8, n * 8ull);
+          if (!in_partition(w.rank, slots)) break;  // slots outside the sender's ring partition
           enqueue(slots, std::string());
           break;
         }
@@ -633,6 +649,7 @@ class NodeScheduler {
           if (len < 24 + n * (8ull + il) + tl) break;  // malformed: ignore
           std::vector<int64_t> slots(n);
           if (n) std::memcpy(slots.data(), p + 24, n * 8ull);
+          if (!in_partition(w.rank, slots)) break;
           std::vector<std::string> ids(n);
           const char* q = p + 24 + n * 8ull;
           for (uint32_t i = 0; i < n; ++i) ids[i].assign(q + i * static_cast<size_t>(il), il);
@@ -650,6 +667,7 @@ class NodeScheduler {
           break;
         }
         case F_STAGE: {
+          if (len < 12) break;  // malformed: ignore
           uint64_t bid;
           uint32_t stage;
           std::memcpy(&bid, p, 8);

@@ -42,13 +42,17 @@ class SlotRing {
     return out;
   }
 
-  // Returns the number of slots that belonged to this ring.
+  // Returns the number of slots freed. Slots outside this ring, slots not currently allocated (outside
+  // [head, head + used)) and slots already freed are ignored: a stale or duplicated free can never
+  // latch a mark that would later let the head run over a live slot.
   size_t free(const std::vector<int64_t>& slots) {
     std::lock_guard<std::mutex> g(mu_);
     size_t k = 0;
     for (int64_t s : slots) {
       const int64_t i = s - base_;
       if (i < 0 || i >= n_) continue;
+      if ((i - head_ + n_) % n_ >= used_) continue;  // not allocated
+      if (freed_[static_cast<size_t>(i)]) continue;   // double free
       freed_[static_cast<size_t>(i)] = 1;
       ++k;
     }

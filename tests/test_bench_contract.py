@@ -64,4 +64,8 @@ def test_bench_torchrun_ranks_gloo(world):
     lines = _json_lines(r.stdout)
     assert len(lines) == 1, r.stdout  # rank 0 only
     _check(lines[0], world)
-    assert len(lines[0]["workers"]) == world and sum(w["images"] for w in lines[0]["workers"]) == 2 * world * 3
+    # warmup 1 + steps 2 + the uncounted tail (inflight 2 + 1 steps) that keeps the pipeline full past t1
+    w = lines[0]["window"]
+    assert w["counted_images"] == 2 * world * 2 and w["first_counted_image"] == 2 * world
+    assert len(lines[0]["workers"]) == world
+    assert sum(x["images"] for x in lines[0]["workers"]) == 2 * world * (3 + w["tail_steps_uncounted"])

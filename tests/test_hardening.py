@@ -100,6 +100,39 @@ def test_batch_failure_isolates_the_bad_item(monkeypatch):
         cp.close()
 
 
+def test_completion_failure_retries_the_batch(monkeypatch):
+    """The retire thread of a worker raising (e.g. a device error in the event sync) answers the batch with
+    IT_RETRY items: they are redelivered and complete; the worker keeps serving."""
+    monkeypatch.setenv("AI4E_FAULT_INJECTION", "fail_finalize=1")
+    cp = ControlPlane(Config.load(env={}))
+    pool = WorkerPool(cp, EP, SPEC, ["cpu"], heartbeat_interval_s=0.1, max_delay_s=0.2, retry_delay_s=0.05).start()
+    try:
+        assert pool.queue.lock_duration == 0.0  # scheduler-drained queue: no peek-lock expiry redelivery
+        ids = pool.submit_many(_imgs(8))
+        assert _wait(lambda: cp.store.zcard(PATH + "_completed") == 8)
+        assert pool.result(ids[4])["classes"][0] == 1
+        pool.refresh()
+        assert pool.workers[0].ready and pool.stats()["workers"][0]["retried_items"] >= 1
+    finally:
+        pool.stop()
+        cp.close()
+
+
+def test_slot_ring_ignores_stale_and_double_frees():
+    from aiforearth_api_platform_amd.store import native
+
+    r = native.SlotRing(8, 100)
+    a = r.alloc(4, 1.0)
+    assert a == [100, 101, 102, 103]
+    assert r.free([105]) == 0           # never allocated
+    assert r.free([101]) == 1 and r.free([101]) == 0  # double free ignored
+    assert r.free([100]) == 1 and r.used() == 2
+    b = r.alloc(6, 1.0)                 # wraps: 104..107, 100, 101
+    assert b == [104, 105, 106, 107, 100, 101]
+    assert r.free([101]) == 1           # freed out of order: head stays on 102
+    assert r.free([101]) == 0 and r.used() == 8
+
+
 @pytest.mark.parametrize("journal_body", [True, False])
 def test_recover_model_endpoint_tasks(tmp_path, journal_body):
     j = str(tmp_path / "j.jsonl")
