@@ -384,8 +384,10 @@ PAIR_X = os.environ.get("AI4E_PAIR_X", "0") not in ("0", "off", "")
 PAIR_B = os.environ.get("AI4E_PAIR_B", "0") not in ("0", "off", "")
 
 
-# K1c tile config per bottleneck width (reserved: the kernel uses 128-pixel tiles for both widths)
-CHAIN_TILE = {64: int(os.environ.get("AI4E_CHAIN_TILE64", "1")), 128: 0}
+# K1c tile config per bottleneck width: 3 = 128-pixel tiles with phase A from the LDS input patch wherever the
+# shape allows it (stride 1, patch fits), else the LDS-DMA ring (bench/chain_patch_ab.py: layer1 chains 14-17 %,
+# layer2 6 % faster at batch 250); AI4E_CHAIN_TILE64 / AI4E_CHAIN_TILE128 = 1 / 0 for the ring everywhere
+CHAIN_TILE = {64: int(os.environ.get("AI4E_CHAIN_TILE64", "3")), 128: int(os.environ.get("AI4E_CHAIN_TILE128", "3"))}
 
 # K1s variant: 0 = direct conv from the LDS input footprint (default), 1 = DMA-gather implicit GEMM
 STEM_VARIANT = int(os.environ.get("AI4E_STEM_VARIANT", "0"))

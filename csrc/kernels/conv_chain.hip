@@ -87,6 +87,22 @@ struct ChainParams {
   int ldx0;
 };
 
+// Phase A "patch" mode (PATCH, stride 1): instead of gathering every 3x3 tap of every pixel through the
+// LDS-DMA ring (nine 16-B gathers per pixel and channel chunk, 18-36 short dependent K steps), the workgroup
+// DMAs the input rows its BM pixels touch, plus one halo row above and below, ONCE into LDS as a padded
+// patch [rows][W + 2 slots][MID] (a zero slot at each row end = the left/right padding), waits once, and
+// then runs the nine taps as pure LDS-read + MFMA steps: tap (kh, kw) of pixel (r, ow) is slot
+// (r - r_lo + kh) * (W + 2) + ow + kw. A tap above / below the image (the row belongs to the neighbouring
+// image in the flattened row order, or lies outside the tensor) reads the zero slot instead. The 16-B
+// chunks of a slot are XOR-swizzled by the slot index (psw) so the 16 consecutive pixels of a fragment
+// read conflict-free. Weights come straight from global memory (L2-resident, 4 K steps prefetched in
+// registers). The 4 waves split the channels. The patch lives in the same LDS as phases B/C
+// (the host only picks this mode when the patch fits the config's LDS).
+template <int MID>
+__device__ __forceinline__ int psw(int slot) {
+  return MID == 64 ? ((slot >> 1) & 3) << 1 : (slot & 7) << 1;
+}
+
 template <int MID, int BM_, int MIDN = 0, bool DOWN = false, int ST = 4, bool BL = true>
 struct ChainCfg {
   static constexpr int BM = BM_;              // pixels per workgroup
@@ -147,11 +163,12 @@ __device__ __forceinline__ uint32_t tile_off(int r, int n) {
   return kb * BM * 64 + r * 64 + ((((e >> 3) ^ swz(r)) << 4) | (((e >> 2) & 1) << 3));
 }
 
-template <int MID, int BM_, int MIDN, bool DOWN, int ST, bool BL>
+template <int MID, int BM_, int MIDN, bool DOWN, int ST, bool BL, bool PATCH>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ChainCfg<MID, BM_, MIDN, DOWN, ST, BL>::MINW,
                                                                      ChainCfg<MID, BM_, MIDN, DOWN, ST, BL>::MINW)))
 void conv_chain_kernel(const ChainParams p) {
   using Cfg = ChainCfg<MID, BM_, MIDN, DOWN, ST, BL>;
+  static_assert(!PATCH || BM_ == 128, "patch mode: 128-pixel tiles (2 x 2 waves of 64 pixels)");
   constexpr bool NEXT = Cfg::NEXT;
   constexpr int FIC = Cfg::FIC, WPXC = Cfg::WPXC, CBC = Cfg::CBC;
   constexpr int WM = Cfg::WM, BM = Cfg::BM, STAGES = Cfg::STAGES, CA = Cfg::CA, CB = Cfg::CB;
@@ -196,7 +213,106 @@ void conv_chain_kernel(const ChainParams p) {
   for (int i = 0; i < FI; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  {
+  // patch mode: the 4 waves split the channels (each all BM pixels = PFI fragments x MID/4 channels = CF
+  // fragments), so every weight element is loaded by exactly one wave
+  constexpr int PWN = 4, PWM = 1;
+  constexpr int PFI = PATCH ? BM_ / 16 / PWM : 1, CF = PATCH ? MID / 16 / PWN : 1;
+  const int pwm = wave % PWM, pwn = wave / PWM;
+  f32x4_t pacc[PFI][CF];
+#pragma unroll
+  for (int i = 0; i < PFI; ++i)
+#pragma unroll
+    for (int j = 0; j < CF; ++j) pacc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  if constexpr (PATCH) {
+    constexpr int RB = MID * 2;    // bytes per pixel slot
+    constexpr int CPS = RB / 16;   // 16-B chunks per slot
+    const int W = p.W, W2 = p.W + 2;
+    const int r_lo = m0 / W;                          // flattened (image, row) index of the first pixel
+    const int r_hi = (min(m0 + BM, p.M) - 1) / W;
+    const int prows = r_hi - r_lo + 3;                // + one halo row above and below
+    const int nrows = p.M / W;                        // N * H
+    const int ipr = W * RB / 1024;                    // 1-KB DMA pieces per patch row (host: W * RB % 1024 == 0)
+    // the patch: row j = flattened row r_lo - 1 + j, data in slots 1..W (one contiguous 1-KB piece per wave DMA)
+    for (int I = wave; I < prows * ipr; I += 4) {
+      const int j = I / ipr, piece = I - j * ipr;
+      const int R = r_lo - 1 + j;
+      const int o = piece * 1024 + 16 * lane;
+      const int s1 = o / RB;                          // data slot in the row (0-based)
+      const int slot = j * W2 + 1 + s1;
+      const int q = ((o % RB) >> 4) ^ psw<MID>(slot);  // logical chunk that belongs at this physical chunk
+      const bool ok = R >= 0 && R < nrows;
+      glds16(ok ? static_cast<const void*>(p.x + (static_cast<long>(R) * W + s1) * p.ldx + 8 * q) : zero,
+             sb + (j * W2 + 1) * RB + piece * 1024);
+    }
+    // zero pad slots (left / right of every row; slot 0 doubles as the zero source of masked taps)
+    for (int g = tid; g < prows * 2 * CPS; g += 256) {
+      const int j = g / (2 * CPS), e = g - j * 2 * CPS;
+      const int slot = j * W2 + (e >= CPS ? W + 1 : 0);
+      *reinterpret_cast<uint4*>(smem + slot * RB + (e % CPS) * 16) = make_uint4(0u, 0u, 0u, 0u);
+    }
+    // per pixel fragment: slot of tap (0, 0) and the row-validity bits of kh = 0, 1, 2
+    int sbase[PFI], vmask[PFI];
+#pragma unroll
+    for (int i = 0; i < PFI; ++i) {
+      const int m = m0 + pwm * (BM / PWM) + 16 * i + (lane & 15);
+      if (m < p.M) {
+        const int r = m / W, ow = m - r * W;
+        const int oh = r % p.H;
+        sbase[i] = (r - r_lo) * W2 + ow;
+        vmask[i] = 2 | (oh > 0 ? 1 : 0) | (oh < p.H - 1 ? 4 : 0);
+      } else {
+        sbase[i] = 0;
+        vmask[i] = 0;
+      }
+    }
+    constexpr int SPT = MID / 32;   // K steps per tap
+    constexpr int NKA = 9 * SPT;
+    constexpr int PD = 4;           // weight K steps prefetched into registers
+    const uint16_t* const wp = p.w2 + static_cast<long>(pwn * (MID / PWN) + (lane & 15)) * p.kpad2 + 8 * lg;
+    bf16x8_t wr[PD][CF];
+#pragma unroll
+    for (int s = 0; s < PD; ++s)
+#pragma unroll
+      for (int j = 0; j < CF; ++j) wr[s][j] = *reinterpret_cast<const bf16x8_t*>(wp + j * 16L * p.kpad2 + s * 32);
+    wait_vmcnt<0>();  // the patch landed (the weight loads above retire with it)
+    lds_barrier();
+    bf16x8_t fx[2][PFI];
+    int soff[PFI], sws[PFI];
+    auto tap_slots = [&](int t) __attribute__((always_inline)) {
+      const int kh = t / 3, kw = t - 3 * (t / 3);
+#pragma unroll
+      for (int i = 0; i < PFI; ++i) {
+        const int slot = (vmask[i] >> kh) & 1 ? sbase[i] + kh * W2 + kw : 0;
+        soff[i] = slot * RB;
+        sws[i] = psw<MID>(slot);
+      }
+    };
+    auto read_px = [&](int s, bf16x8_t (&f)[PFI]) __attribute__((always_inline)) {
+      const int q = (s % SPT) * 4 + lg;
+#pragma unroll
+      for (int i = 0; i < PFI; ++i) f[i] = *reinterpret_cast<const bf16x8_t*>(smem + soff[i] + ((q ^ sws[i]) << 4));
+    };
+    tap_slots(0);
+    read_px(0, fx[0]);
+#pragma unroll
+    for (int s = 0; s < NKA; ++s) {
+      if (s + 1 < NKA) {
+        if ((s + 1) % SPT == 0) tap_slots((s + 1) / SPT);
+        read_px(s + 1, fx[(s + 1) & 1]);
+      }
+#pragma unroll
+      for (int i = 0; i < PFI; ++i)
+#pragma unroll
+        for (int j = 0; j < CF; ++j)
+          pacc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wr[s % PD][j], fx[s & 1][i], pacc[i][j], 0, 0, 0);
+      if (s + PD < NKA) {
+#pragma unroll
+        for (int j = 0; j < CF; ++j)
+          wr[s % PD][j] = *reinterpret_cast<const bf16x8_t*>(wp + j * 16L * p.kpad2 + (s + PD) * 32);
+      }
+    }
+    lds_barrier();  // every wave finished reading the patch before phases B/C reuse the LDS
+  } else {
     const int OHW = p.OH * p.OW;
     int ih0[CA], iw0[CA];
     const uint16_t* rowp[CA];
@@ -328,11 +444,25 @@ void conv_chain_kernel(const ChainParams p) {
   const float lo = 0.f;
   // T2 epilogue: + b2, ReLU, bf16 -> t2buf (phase A wave layout); the lane-group bias select once per j
   // (readfirstlane is convergent: hipcc does not CSE it across the i loop)
+  if constexpr (PATCH) {
+#pragma unroll
+    for (int j = 0; j < CF; ++j) {
+      const f32x4_t b = bias4(p.b2 + pwn * (MID / PWN) + 16 * j, lg);
+#pragma unroll
+      for (int i = 0; i < PFI; ++i) {
+        const int r = pwm * (BM / PWM) + 16 * i + (lane & 15);
+        const int n = pwn * (MID / PWN) + 16 * j + 4 * lg;
+        *reinterpret_cast<uint2*>(t2buf + tile_off<BM>(r, n)) =
+            make_uint2(pack_relu_bf16x2(pacc[i][j][0] + b[0], pacc[i][j][1] + b[1]),
+                       pack_relu_bf16x2(pacc[i][j][2] + b[2], pacc[i][j][3] + b[3]));
+      }
+    }
+  }
   f32x4_t b2v[4];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) b2v[j] = bias4(p.b2 + wn * 64 + 16 * j, lg);
+  for (int j = 0; j < 4; ++j) b2v[j] = PATCH ? f32x4_t{0.f, 0.f, 0.f, 0.f} : bias4(p.b2 + wn * 64 + 16 * j, lg);
 #pragma unroll
-  for (int i = 0; i < FI; ++i) {
+  for (int i = 0; i < (PATCH ? 0 : FI); ++i) {
     const int r = wm * WPX + 16 * i + (lane & 15);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -550,18 +680,39 @@ void conv_chain_kernel(const ChainParams p) {
   }
 }
 
+// Patch mode (phase A from an LDS patch of the input rows) applies to stride 1, an input row of whole 1-KB
+// DMA pieces, a dense [N, H, W, MID] input, 128-pixel tiles and a patch that fits the config's LDS.
+template <int MID, int BM>
+bool patch_fits(const ChainParams& p, int lds_bytes) {
+  if (BM != 128 || p.stride != 1 || p.ldx != MID || (p.W * MID * 2) % 1024) return false;
+  const int rows = (BM - 1 + p.W - 1) / p.W + 1 + 2;  // most rows BM consecutive pixels touch, + 2 halo rows
+  return static_cast<long>(rows) * (p.W + 2) * MID * 2 <= lds_bytes;
+}
+
 template <int MID, int BM, int MIDN, bool DOWN = false, int ST = 4, bool BL = true>
-int launch_chain(const ChainParams& p, hipStream_t s) {
+int launch_chain(const ChainParams& p, hipStream_t s, bool patch = false) {
   using Cfg = ChainCfg<MID, BM, MIDN, DOWN, ST, BL>;
   static bool attr = false;
   if (!attr) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(conv_chain_kernel<MID, BM, MIDN, DOWN, ST, BL>),
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(conv_chain_kernel<MID, BM, MIDN, DOWN, ST, BL, false>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, Cfg::LDS_ALL) != hipSuccess)
       return AI4E_ELAUNCH;
+    if constexpr (BM == 128) {
+      if (hipFuncSetAttribute(reinterpret_cast<const void*>(conv_chain_kernel<MID, BM, MIDN, DOWN, ST, BL, true>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, Cfg::LDS_ALL) != hipSuccess)
+        return AI4E_ELAUNCH;
+    }
     attr = true;
   }
   const int nb = ai4e_cdiv(p.M, Cfg::BM);
-  hipLaunchKernelGGL((conv_chain_kernel<MID, BM, MIDN, DOWN, ST, BL>), dim3(nb), dim3(256), Cfg::LDS_ALL, s, p);
+  if constexpr (BM == 128) {
+    if (patch && patch_fits<MID, BM>(p, Cfg::LDS)) {
+      hipLaunchKernelGGL((conv_chain_kernel<MID, BM, MIDN, DOWN, ST, BL, true>), dim3(nb), dim3(256), Cfg::LDS_ALL, s,
+                         p);
+      return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
+    }
+  }
+  hipLaunchKernelGGL((conv_chain_kernel<MID, BM, MIDN, DOWN, ST, BL, false>), dim3(nb), dim3(256), Cfg::LDS_ALL, s, p);
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
 }
 
@@ -618,20 +769,23 @@ AI4E_API int ai4e_conv_chain_fwd(const void* x, const void* w2, const void* b2, 
   if (p.M <= 0) return AI4E_OK;
   const bool next = w1n != nullptr;
   // tile_cfg: 0 = default (MID 64: 256 pixels, MID 128: 128), 1 = 128-pixel MID-64 tile (48 KB LDS, 3 per CU),
-  // 2 = the 128-pixel tiles with the SGPR lane-select biases (A/B reference for the LDS / ring-borne biases)
+  // 2 = the 128-pixel tiles with the SGPR lane-select biases (A/B reference for the LDS / ring-borne biases),
+  // 3 = the 128-pixel tiles with phase A in patch mode where the shape allows it (else the ring, as 1)
+  const bool patch = tile_cfg == 3;
   if (down) return tile_cfg == 2 ? launch_chain<64, 128, 64, true, 4, false>(p, stream)
-                                 : launch_chain<64, 128, 64, true>(p, stream);
+                                 : launch_chain<64, 128, 64, true>(p, stream, patch);
   if (mid == 64) {
     if (tile_cfg == 2) {  // A/B reference: the 128-pixel tile with the SGPR-select biases (no LDS staging)
       if (next && midn == 128) return launch_chain<64, 128, 128, false, 4, false>(p, stream);
       return next ? launch_chain<64, 128, 64, false, 4, false>(p, stream) : launch_chain<64, 128, 0, false, 4, false>(p, stream);
     }
-    if (next && midn == 128) return launch_chain<64, 128, 128>(p, stream);
-    if (tile_cfg == 1) return next ? launch_chain<64, 128, 64>(p, stream) : launch_chain<64, 128, 0>(p, stream);
+    if (next && midn == 128) return launch_chain<64, 128, 128>(p, stream, patch);
+    if (tile_cfg == 1 || patch)
+      return next ? launch_chain<64, 128, 64>(p, stream, patch) : launch_chain<64, 128, 0>(p, stream, patch);
     return next ? launch_chain<64, 256, 64>(p, stream) : launch_chain<64, 256, 0>(p, stream);
   }
   if (tile_cfg == 2)  // A/B reference: SGPR-select biases
     return next ? launch_chain<128, 128, 128, false, 4, false>(p, stream)
                 : launch_chain<128, 128, 0, false, 4, false>(p, stream);
-  return next ? launch_chain<128, 128, 128>(p, stream) : launch_chain<128, 128, 0>(p, stream);
+  return next ? launch_chain<128, 128, 128>(p, stream, patch) : launch_chain<128, 128, 0>(p, stream, patch);
 }

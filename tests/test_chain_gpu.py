@@ -40,12 +40,17 @@ CASES = [
     (2, 28, 28, 128, 1, False),
     (2, 56, 56, 128, 2, True),    # layer2 block 0: strided c2 chained into block 1's c1
     (1, 9, 13, 128, 1, True),     # M = 117 < one 128-pixel tile
+    (3, 12, 8, 64, 1, True),      # patch mode: tiles straddle image boundaries (96-pixel images)
+    (3, 12, 4, 128, 1, True),     # patch mode, MID 128: 35-row patch, tiles straddle images
+    (5, 7, 8, 64, 1, 128),        # patch mode, ragged last tile
 ]
 
 
 @pytest.mark.parametrize("case", CASES)
-@pytest.mark.parametrize("tile", [0, 1])
+@pytest.mark.parametrize("tile", [0, 1, 3])
 def test_conv_chain(case, tile):
+    """tile 3 = phase A from the LDS input patch (stride 1 and a patch that fits; other shapes fall back to the
+    ring, which the same comparison then covers)."""
     n, h, w, mid, s, nxt = case
     midn = 0 if not nxt else (mid if nxt is True else nxt)
     if tile == 1 and (mid != 64 or midn == 128):
@@ -127,8 +132,9 @@ def test_softmax_topk(shape):
     assert torch.allclose(chosen, rp, rtol=1e-4, atol=1e-6)
 
 
-@pytest.mark.parametrize("shape", [(2, 56, 56), (1, 15, 13)])
-def test_conv_chain_down(shape):
+@pytest.mark.parametrize("shape", [(2, 56, 56), (1, 15, 13), (3, 12, 8)])
+@pytest.mark.parametrize("tile", [-1, 3])
+def test_conv_chain_down(shape, tile):
     """K1c DOWN mode: the residual is the 1x1 projection of the block input, folded into c3's K."""
     n, h, w = shape
     mid = 64
@@ -139,7 +145,7 @@ def test_conv_chain_down(shape):
     c1n = pack_conv(torch.randn(mid, 4 * mid, 1, 1) / (4 * mid) ** 0.5, torch.randn(mid) * 0.1).to(DEV)
     t1 = torch.randn(n, h, w, mid, device=DEV).relu().to(torch.bfloat16)
     x0 = torch.randn(n, h, w, 64, device=DEV).relu().to(torch.bfloat16)
-    y, t1n = conv_chain(t1, c2, c3, None, c1n=c1n, down=dn, x0=x0)
+    y, t1n = conv_chain(t1, c2, c3, None, c1n=c1n, down=dn, x0=x0, tile_cfg=tile)
     torch.cuda.synchronize()
     t2 = F.relu(_conv(t1, _wq(c2, 3), c2.bias[:mid], 1, 1)).to(torch.bfloat16)
     res = _conv(x0, _wq(dn, 1), dn.bias[:4 * mid])
