@@ -93,6 +93,14 @@ class Config:
     port: int = field(default=8080, metadata={"env": "AI4E_PORT"})
     routes_file: str = field(default="", metadata={"env": "AI4E_ROUTES"})
     sync_timeout_s: float = field(default=120.0, metadata={"env": "AI4E_SYNC_TIMEOUT_S"})
+    # HTTPS listener (the Istio gateway's :443 with a mounted cert, Cluster/networking/secure_routing_base.yml):
+    # PEM certificate chain + private key; both empty = plain HTTP
+    tls_cert: str = field(default="", metadata={"env": "AI4E_TLS_CERT"})
+    tls_key: str = field(default="", metadata={"env": "AI4E_TLS_KEY"})
+    # APIM-style subscription keys (comma list) accepted on every API and task-management route, in the
+    # Ocp-Apim-Subscription-Key header or the subscription-key query parameter; routes may add keys of their own
+    # (`keys:` in the route table). Empty and no route keys = open access.
+    subscription_keys: str = field(default="", metadata={"env": "AI4E_SUBSCRIPTION_KEYS"})
     # --- autoscaler (HPA analogue, autoscaler.yaml: min/max replicas, target CURRENT_REQUESTS per replica) ---
     autoscale: bool = field(default=False, metadata={"env": "AI4E_AUTOSCALE"})
     autoscale_min_workers: int = field(default=1, metadata={"env": "AI4E_AUTOSCALE_MIN"})

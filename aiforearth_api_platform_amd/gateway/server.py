@@ -16,7 +16,13 @@ Routes (all served by one aiohttp application):
 * ``POST /v1/cache/upsert``, ``GET /v1/cache/get?taskId=`` — CacheConnectorUpsert / Get.
 * ``POST /v1/requests/upsert``, ``POST /v1/requests/get`` — RequestReporter (CURRENT_REQUESTS).
 * ``POST /v1/backend/webhook`` — BackendWebhook incl. the Event Grid validation handshake.
-* ``GET /metrics`` (Prometheus text), ``GET /v1/platform/stats`` (JSON), ``GET /`` health.
+* ``GET /metrics`` (Prometheus text), ``GET /v1/platform/stats`` (JSON), ``GET /`` health,
+  ``GET /openapi.json`` (OpenAPI 3.0 description of the route table, gateway/security.py).
+
+Security (gateway/security.py): APIM-style subscription keys (``Ocp-Apim-Subscription-Key`` header or
+``subscription-key`` query) on every API, task-management and control route when keys are configured (global
+``AI4E_SUBSCRIPTION_KEYS`` and/or per-route ``keys``; 401 otherwise; health and the OpenAPI document stay open),
+and an HTTPS listener when ``AI4E_TLS_CERT`` / ``AI4E_TLS_KEY`` name a PEM certificate and key.
 
 Admission control per route mirrors ``APIService.before_request`` (429 busy, 503 draining,
 401 content type, 413 too large); undecodable payloads get 400 (415 for unknown media types) and
@@ -28,6 +34,7 @@ from __future__ import annotations
 import asyncio
 import json
 import signal
+import threading
 from dataclasses import dataclass, field
 from typing import Any, Callable, Dict, List, Optional
 
@@ -36,8 +43,15 @@ from aiohttp import ClientSession, web
 from ..utils.metrics import REGISTRY
 from ..utils.tracing import StageClock, b3_from_headers, b3_pack, b3_unpack
 from .control import ControlPlane
+from .security import KeyAuth, openapi_document, parse_keys, server_ssl_context
 
 TASK_INSERT_FAILED = "Task insert failed."
+
+
+def valid_task_id(tid: str) -> bool:
+    """An upstream task id (``taskId`` header) the store and the scheduler wire format accept: 1-128 printable
+    ASCII characters (the wire carries ids as fixed-length byte strings, runtime/protocol.py)."""
+    return 0 < len(tid) <= 128 and tid.isascii() and tid.isprintable()
 BATCH_CONTENT_TYPE = "application/x-ai4e-batch"
 
 
@@ -51,6 +65,7 @@ class Route:
     content_types: Optional[List[str]] = None
     max_content_length: Optional[int] = None
     inline: bool = False                     # sync callable cheap enough to run on the event loop (no thread hop)
+    keys: Optional[List[str]] = None         # subscription keys valid on this route (besides the global ones)
     inflight: int = field(default=0, repr=False)
 
     def target_path(self, path: str) -> str:
@@ -87,22 +102,26 @@ class RouteTable:
                 be = backends[be.split(":", 1)[1]]
             t.add(Route(prefix=r["prefix"], mode=r.get("mode", "async"), backend=be, rewrite=r.get("rewrite"),
                         max_concurrent=r.get("max_concurrent"), content_types=r.get("content_types"),
-                        max_content_length=r.get("max_content_length"), inline=bool(r.get("inline", False))))
+                        max_content_length=r.get("max_content_length"), inline=bool(r.get("inline", False)),
+                        keys=parse_keys(r.get("keys")) or None))
         return t
 
 
 class Gateway:
     def __init__(self, control_plane: ControlPlane, routes: Optional[RouteTable] = None, webhook=None,
-                 base_url: str = "http://127.0.0.1"):
+                 base_url: str = "http://127.0.0.1", auth: Optional[KeyAuth] = None):
         self.cp = control_plane
+        self.auth = auth if auth is not None else KeyAuth(parse_keys(getattr(control_plane.cfg, "subscription_keys", "")))
         self.routes = routes or RouteTable()
         self.webhook = webhook
         self.base_url = base_url.rstrip("/")
         self.is_terminating = False
         self.on_drain: List[Callable[[], None]] = []
+        self._stopped = threading.Event()
         self._session: Optional[ClientSession] = None
-        self.app = web.Application(client_max_size=1 << 30)
+        self.app = web.Application(client_max_size=1 << 30, middlewares=[self._key_middleware])
         self.app.router.add_get("/", self.health)
+        self.app.router.add_get("/openapi.json", self.openapi)
         self.app.router.add_get("/metrics", self.metrics)
         self.app.router.add_get("/v1/platform/stats", self.stats)
         self.app.router.add_get("/v1/taskmanagement/task/{taskId}", self.task_get)
@@ -116,6 +135,24 @@ class Gateway:
         self.app.router.add_route("*", "/{tail:.*}", self.dispatch)
         self.app.on_cleanup.append(self._cleanup)
         self._c_req = REGISTRY.counter("gateway_requests_total")
+
+    # ------------------------------------------------------------------ security
+    OPEN_PATHS = ("/", "/openapi.json")
+
+    @web.middleware
+    async def _key_middleware(self, request, handler):
+        """Subscription-key check ahead of every handler: API routes accept the global keys and their own; the
+        task-management and control routes the global keys; health and the OpenAPI document are open."""
+        if request.path not in self.OPEN_PATHS:
+            route = self.routes.match(request.path)
+            rej = self.auth.check(request.headers, request.query, route.keys if route is not None else None)
+            if rej is not None:
+                return web.json_response(rej[1], status=rej[0])
+        return await handler(request)
+
+    async def openapi(self, request):
+        return web.json_response(openapi_document(self.routes.routes, keys_required=self.auth.enabled,
+                                                  servers=[self.base_url]))
 
     # ------------------------------------------------------------------ platform routes
     async def health(self, request):
@@ -295,6 +332,8 @@ class Gateway:
         loop = asyncio.get_running_loop()
         target = route.target_path(request.path)
         upstream_id = request.headers.get("taskId", "")
+        if upstream_id and not valid_task_id(upstream_id):
+            return web.json_response({"message": "taskId header must be 1-128 printable ASCII characters"}, status=400)
         b3 = b3_from_headers(request.headers)
         trace = b3_pack(b3)
         try:
@@ -373,15 +412,13 @@ class Gateway:
 
     def install_signal_handlers(self, grace_s: float = 30.0) -> None:
         """SIGINT/SIGTERM: stop admitting (503), finish queued + in-flight work, then exit."""
-        import _thread
-        import threading
         import time
 
         def wait_then_exit():
             deadline = time.time() + grace_s
             while time.time() < deadline and not self.idle():
                 time.sleep(0.05)
-            _thread.interrupt_main()
+            self._stopped.set()  # run() returns
 
         def drain(*_):
             if not self.is_terminating:
@@ -399,12 +436,33 @@ class Gateway:
             except ValueError:
                 pass
 
-    def run(self, host: str = "127.0.0.1", port: int = 8080, socks=None) -> None:
+    def run(self, host: str = "127.0.0.1", port: int = 8080, socks=None, ssl_context=None) -> None:
         """Serve on (host, port), or on the given listening sockets (public SO_REUSEPORT socket shared with
-        the ingest front-ends + the internal socket they proxy to: serve.open_listeners)."""
-        # the drain (install_signal_handlers) already waited for in-flight work: do not hold the exit on idle
-        # keep-alive connections (e.g. the front-ends' proxy sessions) for aiohttp's default 60 s
-        if socks:
-            web.run_app(self.app, sock=socks, handle_signals=False, print=None, shutdown_timeout=2.0)
-        else:
-            web.run_app(self.app, host=host, port=port, handle_signals=False, print=None, shutdown_timeout=2.0)
+        the ingest front-ends + the internal socket they proxy to: serve.open_listeners), until the drain
+        (install_signal_handlers) has finished. ``ssl_context`` (default: from the config's TLS cert/key) makes the
+        public listener HTTPS; the front-ends' internal loopback listener (the second socket) stays plain HTTP."""
+        if ssl_context is None:
+            ssl_context = server_ssl_context(self.cp.cfg.tls_cert, self.cp.cfg.tls_key)
+
+        async def serve():
+            # the drain already waited for in-flight work: do not hold the exit on idle keep-alive connections
+            # (e.g. the front-ends' proxy sessions) for aiohttp's default 60 s
+            runner = web.AppRunner(self.app, handle_signals=False, access_log=None, shutdown_timeout=2.0)
+            await runner.setup()
+            if socks:
+                sites = [web.SockSite(runner, sk, ssl_context=ssl_context if i == 0 else None)
+                         for i, sk in enumerate(socks)]
+            else:
+                sites = [web.TCPSite(runner, host, port, ssl_context=ssl_context)]
+            for site in sites:
+                await site.start()
+            try:
+                while not self._stopped.is_set():
+                    await asyncio.sleep(0.1)
+            finally:
+                await runner.cleanup()
+
+        try:
+            asyncio.run(serve())
+        except KeyboardInterrupt:
+            pass

@@ -12,8 +12,15 @@ endpoints itself:
   acknowledged once the tasks exist) and answers the client — the same JSON the gateway answers;
 * slots come back (FREE) when the tasks finish.
 
-Everything else (task status / result / trace queries, sync routes, metrics, generic backends) is
-proxied to the serving process's internal listener, where the task store lives. The reference scales
+Everything else (task status / result / trace queries, sync routes, metrics, generic backends, and async
+requests that carry an upstream ``taskId`` header, which the gateway adopts as the reference's
+``TaskManager.AddTask`` does) is proxied to the serving process's internal listener, where the task store lives.
+
+Admission matches the gateway's (``gateway/server.py``): subscription keys (401), the route's
+``max_concurrent`` per process (429), draining after SIGTERM (503), content type (401) and length (413); the
+listener is HTTPS when the platform has a TLS certificate. When the scheduler's acknowledgement does not come in
+time the tasks may already exist, so the minted ids are returned with 202 (not a 503 that invites a duplicate
+retry). The reference scales
 its front door with APIM + Istio in front of one Flask container per model
 (``APIs/1.0/base-py/ai4e_service.py``); here the ingest path itself scales across cores.
 """
@@ -30,11 +37,17 @@ _HOP = {"connection", "keep-alive", "proxy-authenticate", "proxy-authorization",
 
 
 def frontend_main(index: int, host: str, port: int, internal_url: str, endpoints: Dict[str, dict],
-                  routes: List[dict], conns: Dict[str, object], ack_timeout_s: float = 30.0) -> None:
+                  routes: List[dict], conns: Dict[str, object], ack_timeout_s: float = 30.0,
+                  security: Optional[dict] = None) -> None:
     """Process entry point. ``endpoints``: name -> {endpoint, shm, nslots, item_shape, base, len};
-    ``routes``: [{prefix, rewrite, mode, endpoint (name or None), content_types, max_content_length}];
-    ``conns``: name -> the Connection to that endpoint's node scheduler."""
+    ``routes``: [{prefix, rewrite, mode, endpoint (name or None), content_types, max_content_length,
+    max_concurrent, keys}]; ``conns``: name -> the Connection to that endpoint's node scheduler;
+    ``security``: {keys (global subscription keys), tls_cert, tls_key}."""
+    import signal
+
     from aiohttp import ClientSession, web
+
+    from ..gateway.security import KeyAuth, server_ssl_context
 
     from ..store.pystore import absolute_path, dotnet_timestamp
     from ..utils.tracing import b3_from_headers, b3_pack
@@ -48,7 +61,18 @@ def frontend_main(index: int, host: str, port: int, internal_url: str, endpoints
     shards = {name: IngestShard(conns[name], e["endpoint"], e["shm"], e["nslots"], e["item_shape"], e["base"],
                                 e["len"], on_close=lambda: os._exit(0)) for name, e in endpoints.items()}
     table = sorted(routes, key=lambda r: -len(r["prefix"]))
-    state: Dict[str, Optional[ClientSession]] = {"session": None}
+    state: Dict[str, object] = {"session": None, "draining": False}
+    sec = security or {}
+    auth = KeyAuth(sec.get("keys") or [])
+    inflight: Dict[str, int] = {}
+
+    def on_term(*_):  # drain: refuse new ingest (503), let in-flight requests finish, then exit
+        state["draining"] = True
+        import threading
+
+        threading.Timer(5.0, lambda: os._exit(0)).start()
+
+    signal.signal(signal.SIGTERM, on_term)
 
     def match(path: str) -> Optional[dict]:
         for r in table:
@@ -73,6 +97,18 @@ def frontend_main(index: int, host: str, port: int, internal_url: str, endpoints
             return web.Response(status=r.status, body=data, headers=out)
 
     async def ingest(request, route: dict, shard: IngestShard):
+        if state["draining"]:
+            return web.json_response({"message": "Service is terminating, please try again later."}, status=503)
+        mc = route.get("max_concurrent")
+        if mc is not None and inflight.get(route["prefix"], 0) + 1 > mc:
+            return web.json_response({"message": "Service is busy, please try again later."}, status=429)
+        inflight[route["prefix"]] = inflight.get(route["prefix"], 0) + 1
+        try:
+            return await _ingest(request, route, shard)
+        finally:
+            inflight[route["prefix"]] -= 1
+
+    async def _ingest(request, route: dict, shard: IngestShard):
         if route.get("content_types") and request.content_type not in route["content_types"]:
             return web.json_response({"message": f"Content-type must be {route['content_types']}"}, status=401)
         mcl = route.get("max_content_length")
@@ -95,20 +131,28 @@ def frontend_main(index: int, host: str, port: int, internal_url: str, endpoints
                     sb.abort()
                     raise
                 ids = shard.mint_ids(len(slots))
-                await shard.submit_ids(slots, ids, trace).wait_async(ack_timeout_s)
+                try:
+                    await shard.submit_ids(slots, ids, trace).wait_async(ack_timeout_s)
+                except (TimeoutError, asyncio.TimeoutError):  # submitted, not yet acknowledged: do not invite a retry
+                    return web.json_response({"TaskIds": ids, "message": "accepted, not yet acknowledged"},
+                                             status=202, headers=b3)
                 return web.json_response({"TaskIds": ids}, headers=b3)
             body = await request.read()
             arr = await loop.run_in_executor(None, decode_image, body, request.content_type, shard.item_shape)
             slot = shard.slots.alloc(1, 0.0) or await loop.run_in_executor(None, shard.alloc, 1)
             shard.write(slot[0], arr)
-            tid = request.headers.get("taskId") or shard.mint_ids(1)[0]
-            n = await shard.submit_ids(slot, [tid], trace).wait_async(ack_timeout_s)
-            if n != 1:  # an upstream taskId that already exists: the scheduler dropped the payload
-                return web.json_response({"message": f"task {tid} already exists"}, status=409)
+            tid = shard.mint_ids(1)[0]
+            try:
+                n = await shard.submit_ids(slot, [tid], trace).wait_async(ack_timeout_s)
+            except (TimeoutError, asyncio.TimeoutError):
+                return web.Response(text=task_json(tid, shard.endpoint), status=202, content_type="application/json",
+                                    headers=b3)
+            if n != 1:  # (minted ids are unique: only a scheduler that refused the payload gets here)
+                return web.json_response({"message": "Task insert failed."}, status=500)
         except PayloadError as e:
             return web.json_response({"message": str(e)}, status=e.status)
-        except (TimeoutError, asyncio.TimeoutError):
-            return web.json_response({"message": "Service is busy, please try again later."}, status=503)
+        except (TimeoutError, asyncio.TimeoutError):  # no ring slot in time: nothing was created
+            return web.json_response({"message": "Service is busy, please try again later."}, status=429)
         js = task_json(tid, shard.endpoint)
         accept = request.headers.get("Accept", "application/json")
         if "application/json" in accept or "*/*" in accept:
@@ -117,7 +161,12 @@ def frontend_main(index: int, host: str, port: int, internal_url: str, endpoints
 
     async def handle(request):
         r = match(request.path)
-        if r is not None and r["mode"] == "async" and r.get("endpoint") in shards and request.method in ("POST", "PUT"):
+        if request.path not in ("/", "/openapi.json"):
+            rej = auth.check(request.headers, request.query, r.get("keys") if r is not None else None)
+            if rej is not None:
+                return web.json_response(rej[1], status=rej[0])
+        if (r is not None and r["mode"] == "async" and r.get("endpoint") in shards and request.method in ("POST", "PUT")
+                and not request.headers.get("taskId")):
             return await ingest(request, r, shards[r["endpoint"]])
         return await proxy(request)
 
@@ -130,7 +179,8 @@ def frontend_main(index: int, host: str, port: int, internal_url: str, endpoints
 
     app.on_cleanup.append(close_session)
     try:
-        web.run_app(app, host=host, port=port, reuse_port=True, access_log=None, print=None)
+        web.run_app(app, host=host, port=port, reuse_port=True, access_log=None, print=None, handle_signals=False,
+                    ssl_context=server_ssl_context(sec.get("tls_cert", ""), sec.get("tls_key", "")))
     finally:
         for s in shards.values():
             s.close()
@@ -157,7 +207,7 @@ def open_listeners(host: str, port: int, shared: bool) -> list:
 
 
 def spawn_frontends(n: int, pools: Dict[str, object], routes: List[dict], host: str, port: int,
-                    internal_url: str) -> list:
+                    internal_url: str, security: Optional[dict] = None) -> list:
     """Start ``n`` front-end processes on (host, port) for the pool-backed ``ModelEndpoint``s in ``pools``
     (name -> endpoint; each WorkerPool built with ``frontends >= n``), attached to every endpoint's node
     scheduler over their own connection. ``routes``: as :func:`frontend_main`."""
@@ -176,8 +226,8 @@ def spawn_frontends(n: int, pools: Dict[str, object], routes: List[dict], host: 
             conns[name] = child
             eps[name] = {"endpoint": ep.endpoint, "shm": ep.ring.name, "nslots": ep.ring.nslots,
                          "item_shape": list(ep.item_shape), "base": base, "len": length}
-        p = ctx.Process(target=frontend_main, args=(i, host, port, internal_url, eps, routes, conns), daemon=True,
-                        name=f"ai4e-frontend-{i}")
+        p = ctx.Process(target=frontend_main, args=(i, host, port, internal_url, eps, routes, conns),
+                        kwargs={"security": security}, daemon=True, name=f"ai4e-frontend-{i}")
         p.start()
         for c in conns.values():
             c.close()

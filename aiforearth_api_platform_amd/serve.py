@@ -25,6 +25,7 @@ import yaml
 
 from .config import Config, bucket_list, set_config
 from .gateway.control import ControlPlane, set_control_plane
+from .gateway.security import parse_keys
 from .gateway.server import Gateway, Route, RouteTable
 from .sched.dispatcher import QueueDispatcher, WebhookDispatcher, http_backend
 from .utils.logging import AI4ELogger
@@ -62,8 +63,11 @@ def start_frontends(cfg: Config, doc: Dict[str, Any], endpoints: Dict[str, Any],
         name = be.split(":", 1)[1] if isinstance(be, str) and be.startswith("inproc:") else None
         routes.append({"prefix": r["prefix"], "rewrite": r.get("rewrite"), "mode": r.get("mode", "async"),
                        "endpoint": name if name in pools else None, "content_types": r.get("content_types"),
-                       "max_content_length": r.get("max_content_length")})
-    return spawn_frontends(frontend_count(cfg), pools, routes, cfg.host, port, f"http://127.0.0.1:{internal_port}")
+                       "max_content_length": r.get("max_content_length"), "max_concurrent": r.get("max_concurrent"),
+                       "keys": parse_keys(r.get("keys"))})
+    return spawn_frontends(frontend_count(cfg), pools, routes, cfg.host, port, f"http://127.0.0.1:{internal_port}",
+                           security={"keys": parse_keys(cfg.subscription_keys), "tls_cert": cfg.tls_cert,
+                                     "tls_key": cfg.tls_key})
 
 
 def build_platform(doc: Dict[str, Any], cfg: Config):
@@ -76,7 +80,7 @@ def build_platform(doc: Dict[str, Any], cfg: Config):
 
     cp = ControlPlane(cfg, AI4ELogger(level=logging.DEBUG if cfg.debug else logging.INFO))
     set_control_plane(cp)
-    base_url = f"http://{cfg.host}:{cfg.port}"
+    base_url = f"{'https' if cfg.tls_cert else 'http'}://{cfg.host}:{cfg.port}"
     endpoints: Dict[str, Any] = {}
     for name, e in (doc.get("endpoints") or {}).items():
         shape = tuple(e["item_shape"])
@@ -117,7 +121,8 @@ def build_platform(doc: Dict[str, Any], cfg: Config):
             be = _load(be.split(":", 1)[1])
         route = table.add(Route(prefix=r["prefix"], mode=r.get("mode", "async"), backend=be, rewrite=r.get("rewrite"),
                                 max_concurrent=r.get("max_concurrent"), content_types=r.get("content_types"),
-                                max_content_length=r.get("max_content_length"), inline=bool(r.get("inline", False))))
+                                max_content_length=r.get("max_content_length"), inline=bool(r.get("inline", False)),
+                                keys=parse_keys(r.get("keys")) or None))
         # async route to a generic backend: a queue dispatcher delivers each task (BackendQueueProcessor)
         if route.mode == "async" and not hasattr(be, "submit") and be is not None:
             target = base_url + (route.rewrite or route.prefix)
@@ -168,7 +173,7 @@ def main(argv=None) -> int:
     frontends = start_frontends(cfg, doc, endpoints, cfg.port, socks[1].getsockname()[1]) if nfe else []
     # SIGTERM drain: the front-ends stop first (their own graceful shutdown), so no new tasks arrive meanwhile
     gw.on_drain.append(lambda: [p.terminate() for p in frontends])
-    print(f"ai4e-mi355x gateway on http://{cfg.host}:{cfg.port} endpoints={list(endpoints)} "
+    print(f"ai4e-mi355x gateway on {'https' if cfg.tls_cert else 'http'}://{cfg.host}:{cfg.port} endpoints={list(endpoints)} "
           f"ingest_frontends={len(frontends)}", file=sys.stderr, flush=True)
     try:
         gw.run(cfg.host, cfg.port, socks=socks)

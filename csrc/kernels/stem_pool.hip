@@ -186,12 +186,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
 // (channels 0-7 | 8-15, 16 B per pixel) so 16 lanes reading 16 consecutive pixels hit 16 distinct bank
 // quads. The 64 x 256 weights (32 KB) stay in LDS for the whole persistent loop, each 512-B row with its
 // 16-B chunk index XOR (row & 31) so the 16 rows of a fragment read hit distinct bank quads.
-constexpr int FP_R = SP_RR + 3, FP_C = SP_RC + 3, FP_PIX = FP_R * FP_C;  // 18 x 20 footprint
-// plane stride padded to a multiple of 16 slots (360 -> 368): a ds_read_b128 lane group {0-3, 12-15, 20-27}
-// reads lanes of both planes, and with a stride of 360 = 8 (mod 16) slots lanes 12-15 of plane 0 and 20-23 of
-// plane 1 hit the same bank quads (the 50 % LDS-conflict share in profiles/r1_pmc); at 368 the group's 16
-// chunks are distinct mod 16.
-constexpr int FP_STRIDE = (FP_PIX + 15) / 16 * 16;                      // 368
+// Footprint 18 x 20 pixels stored with a row stride of FP_C = 21 slots (column 20 unused). The MFMA fragments
+// cover the 15 x 17 conv region as 15 row fragments (row r, columns 0..15: 16 consecutive slots) plus one column
+// fragment (column 16 of rows 0..14: slots 21 r, and 21 = 5 (mod 16) is odd, so 16 rows hit 16 distinct bank
+// quads). Every fragment read of the main loop is then conflict-free for the gfx950 ds_read_b128 lane groups
+// (round 2's row-major fragments of 16 consecutive region pixels crossed a region row almost every time and
+// jumped 3 slots there: 42.5 % SQ_LDS_BANK_CONFLICT, profiles/r2_final/pmc_summary.txt).
+constexpr int FP_R = SP_RR + 3, FP_C = SP_RC + 4, FP_PIX = FP_R * FP_C;  // 18 x 21 slots
+// plane stride padded to a multiple of 16 slots: a ds_read_b128 lane group {0-3, 12-15, 20-27} reads lanes of
+// both planes, which must then sit at the same bank offset
+constexpr int FP_STRIDE = (FP_PIX + 15) / 16 * 16;                      // 384
+// Epilogue tile [256 px][64 ch] bf16 for the pooling (direct kernel): pixels 2t and 2t+1 share one 256-B bank row,
+// pixel m in half h(m) = (m ^ m >> 1) & 1 (so pooled neighbours px, px+1 -- whose window pixels differ by 2 --
+// always sit in opposite halves), 16-B chunk k at k ^ (m & 7) within the half, and the two 8-B halves of a chunk
+// swapped when bit 3 of m is set (the 16 consecutive pixels of an epilogue ds_write_b64 group then cover all 32
+// banks). Byte address of chunk k of pixel m:
+__device__ __forceinline__ int ptile(int m, int k) {
+  return (m >> 1) * 256 + ((((m ^ (m >> 1)) & 1) << 3) | (k ^ (m & 7))) * 16;
+}
 constexpr int FP_SLOTS = 2 * FP_STRIDE;                                 // 736 16-B slots (2 planes + pad)
 constexpr int FP_DMA = (FP_SLOTS + 255) / 256;                          // DMA instrs per wave (3)
 constexpr int D_W = 0, D_FP = 64 * 512, D_TILE = D_FP + FP_DMA * 4 * 1024, D_LDS = D_TILE + SP_BM * 128;
@@ -215,15 +227,44 @@ void stem_pool_direct_kernel(const StemParams p, int ntiles) {
   for (int j = 0; j < 4; ++j) bias[j] = *reinterpret_cast<const float4*>(p.bias + 16 * j + 4 * (lane >> 4));
   const int per_img = p.tiles_r * p.tiles_c;
   const int g = lane >> 4;
-  // this lane's 4 pixels (one per fragment i): region coords and footprint base
-  int fpb[4];
+  // this lane's 4 pixels (one per fragment f = 4 wave + i): row fragments f < 15 hold region row f, columns
+  // lane&15; fragment 15 holds column 16 of rows lane&15 (lane 15 idle: reads footprint slot 0, writes tile row 255,
+  // which no pooling window covers). rm = the pixel's region index r * 17 + cc (the epilogue tile row).
+  int fpb[4], rmi[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int m = wave * 64 + 16 * i + (lane & 15);
-    const int r = m / SP_RC, cc = m - r * SP_RC;
-    fpb[i] = m < SP_RR * SP_RC ? r * FP_C + cc : 0;  // the idle 256th row reads pixel 0 (never pooled)
+    const int f = 4 * wave + i;
+    const int r = f < SP_RR ? f : (lane & 15), cc = f < SP_RR ? (lane & 15) : SP_RC - 1;
+    const bool v = r < SP_RR;
+    fpb[i] = v ? r * FP_C + cc : 0;
+    rmi[i] = v ? r * SP_RC + cc : SP_BM - 1;
   }
   uint8_t* const tile = dsm + D_TILE;
+
+  // footprint DMA of tile t: slot s = plane * FP_STRIDE + pixel (pixels >= FP_PIX are padding, zero-filled);
+  // footprint pixel (a, b) is input (oh0-1+a, ow0-1+b). Issued one tile ahead: the next tile's footprint lands
+  // while this tile's epilogue, pooling and fused c1 run (the MFMA loop is the footprint's only reader).
+  auto issue_fp = [&](int tt) __attribute__((always_inline)) {
+    const int im = tt / per_img;
+    const int r0 = (tt - im * per_img) / p.tiles_c;
+    const int c0 = tt - im * per_img - r0 * p.tiles_c;
+    const int oh = 2 * r0 * SP_TR - 1, ow = 2 * c0 * SP_TC - 1;
+    const uint16_t* const xs = p.x + static_cast<long>(im) * p.H * p.W * SP_C;
+#pragma unroll
+    for (int q = 0; q < FP_DMA; ++q) {
+      const int s = (wave + 4 * q) * 64 + lane;
+      const int h = s >= FP_STRIDE ? 1 : 0, pix = s - h * FP_STRIDE;
+      const int a = pix / FP_C, b = pix - a * FP_C;
+      const int ih = oh - 1 + a, iw = ow - 1 + b;
+      const bool ok = s < FP_SLOTS && pix < FP_PIX && b < SP_RC + 3 && static_cast<unsigned>(ih) < static_cast<unsigned>(p.H) &&
+                      static_cast<unsigned>(iw) < static_cast<unsigned>(p.W);
+      glds16(ok ? static_cast<const void*>(xs + (static_cast<long>(ih) * p.W + iw) * SP_C + 8 * h) : p.zero,
+             sb + D_FP + (wave + 4 * q) * 1024);
+    }
+  };
+  if constexpr (!U8) {
+    if (static_cast<int>(blockIdx.x) < ntiles) issue_fp(blockIdx.x);
+  }
 
   for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
     const int img = t / per_img;
@@ -231,7 +272,6 @@ void stem_pool_direct_kernel(const StemParams p, int ntiles) {
     const int tc = t - img * per_img - tr * p.tiles_c;
     const int ph0 = tr * SP_TR, pw0 = tc * SP_TC;
     const int oh0 = 2 * ph0 - 1, ow0 = 2 * pw0 - 1;
-    const uint16_t* const xi = p.x + static_cast<long>(img) * p.H * p.W * SP_C;
     if constexpr (U8) {
       // fused preprocess: one thread per footprint pixel builds its 16 s2d channels
       // ((dy*2+dx)*cin + c = norm(img[2ih+dy-1, 2iw+dx-1, c]), zero outside the image) and writes both planes
@@ -262,22 +302,8 @@ void stem_pool_direct_kernel(const StemParams p, int ntiles) {
         *d1 = make_uint4(pack_bf16x2(v[8], v[9]), pack_bf16x2(v[10], v[11]), pack_bf16x2(v[12], v[13]),
                          pack_bf16x2(v[14], v[15]));
       }
-    } else {
-    // footprint DMA: slot s = plane * FP_STRIDE + pixel (pixels >= FP_PIX are padding, zero-filled);
-    // footprint pixel (a, b) is input (oh0-1+a, ow0-1+b)
-#pragma unroll
-    for (int q = 0; q < FP_DMA; ++q) {
-      const int s = (wave + 4 * q) * 64 + lane;
-      const int h = s >= FP_STRIDE ? 1 : 0, pix = s - h * FP_STRIDE;
-      const int a = pix / FP_C, b = pix - a * FP_C;
-      const int ih = oh0 - 1 + a, iw = ow0 - 1 + b;
-      const bool ok = s < FP_SLOTS && pix < FP_PIX && static_cast<unsigned>(ih) < static_cast<unsigned>(p.H) &&
-                      static_cast<unsigned>(iw) < static_cast<unsigned>(p.W);
-      glds16(ok ? static_cast<const void*>(xi + (static_cast<long>(ih) * p.W + iw) * SP_C + 8 * h) : p.zero,
-             sb + D_FP + (wave + 4 * q) * 1024);
     }
-    }
-    wait_vmcnt<0>();
+    wait_vmcnt<0>();  // this tile's footprint landed (and the previous tile's stores retired)
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // footprint (and weights) visible
 
     f32x4_t acc[4][4];
@@ -304,10 +330,14 @@ void stem_pool_direct_kernel(const StemParams p, int ntiles) {
         for (int j = 0; j < 4; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[j], fx[i], acc[i][j], 0, 0, 0);
     }
-    // epilogue: bf16 relu(acc + b) -> tile [256 px][64 ch] (128-B rows, 16-B chunk ^= px & 7)
+    if constexpr (!U8) {
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // every wave finished reading the footprint
+      if (t + static_cast<int>(gridDim.x) < ntiles) issue_fp(t + gridDim.x);
+    }
+    // epilogue: bf16 relu(acc + b) -> tile [256 px][64 ch] (ptile layout)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int m = wave * 64 + 16 * i + (lane & 15);
+      const int m = rmi[i];
       const int r = m / SP_RC, cc = m - r * SP_RC;
       const bool live = m < SP_RR * SP_RC && oh0 + r >= 0 && oh0 + r < p.H && ow0 + cc >= 0 && ow0 + cc < p.W;
 #pragma unroll
@@ -318,7 +348,7 @@ void stem_pool_direct_kernel(const StemParams p, int ntiles) {
         if (live)
           v = make_uint2(pack_bf16x2(fmaxf(acc[i][j][0] + b.x, 0.f), fmaxf(acc[i][j][1] + b.y, 0.f)),
                          pack_bf16x2(fmaxf(acc[i][j][2] + b.z, 0.f), fmaxf(acc[i][j][3] + b.w, 0.f)));
-        *reinterpret_cast<uint2*>(tile + m * 128 + ((((n >> 3) ^ (m & 7)) << 4) | (((n >> 2) & 1) << 3))) = v;
+        *reinterpret_cast<uint2*>(tile + ptile(m, n >> 3) + ((((n >> 2) ^ (m >> 3)) & 1) << 3)) = v;
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -336,9 +366,18 @@ void stem_pool_direct_kernel(const StemParams p, int ntiles) {
         b1v[j] = *reinterpret_cast<const float4*>(p.b1 + 16 * j + 4 * (lane >> 4));
       }
     }
-    for (int task = tid; task < SP_TR * SP_TC * 8; task += 256) {
-      const int q = task >> 3, k8 = task & 7;
-      const int py = q / SP_TC, px = q - py * SP_TC;
+    // one pooled row (8 pixels x 8 chunks) per wave instruction; the lanes of each ds_read_b128 group
+    // {0-3,12-15,20-27}, {4-11,16-19,28-31} (+32) read the 8 chunks of two neighbouring pooled pixels, which
+    // ptile puts in opposite bank-row halves: conflict-free for every window offset
+    const int sub = lane & 31;
+    const int pxl = sub < 4 ? 0 : sub < 12 ? 2 : sub < 16 ? 0 : sub < 20 ? 3 : sub < 28 ? 1 : 3;
+    const int k8 = sub < 4 ? sub : sub < 12 ? sub - 4 : sub < 16 ? sub - 8 : sub < 20 ? sub - 16 : sub < 28 ? sub - 20 : sub - 24;
+    const int px = pxl + 4 * (lane >> 5);
+    uint4 mxs[2] = {make_uint4(0u, 0u, 0u, 0u), make_uint4(0u, 0u, 0u, 0u)};  // pooled rows wave, wave + 4 (c1)
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int py = wave + 4 * e;
+      if (py >= SP_TR) break;
       const int ph = ph0 + py, pw = pw0 + px;
       if (ph >= p.PH || pw >= p.PW) continue;
       uint4 mx = make_uint4(0u, 0u, 0u, 0u);
@@ -347,17 +386,28 @@ void stem_pool_direct_kernel(const StemParams p, int ntiles) {
 #pragma unroll
         for (int dx = 0; dx < 3; ++dx) {
           const int m = (2 * py + dy) * SP_RC + 2 * px + dx;
-          const uint4 v = *reinterpret_cast<const uint4*>(tile + m * 128 + ((k8 ^ (m & 7)) << 4));
+          uint4 v = *reinterpret_cast<const uint4*>(tile + ptile(m, k8));
+          if ((m >> 3) & 1) v = make_uint4(v.z, v.w, v.x, v.y);  // the chunk's 8-B halves are stored swapped
           mx.x = max_bf16x2(mx.x, v.x);
           mx.y = max_bf16x2(mx.y, v.y);
           mx.z = max_bf16x2(mx.z, v.z);
           mx.w = max_bf16x2(mx.w, v.w);
         }
       *reinterpret_cast<uint4*>(p.y + ((static_cast<long>(img) * p.PH + ph) * p.PW + pw) * SP_BN + 8 * k8) = mx;
-      if constexpr (C1)  // pooled row q as the c1 B operand: [k-block k8/4][64 rows][4 x 16-B chunks ^ swz(q)]
-        *reinterpret_cast<uint4*>(dsm + D_FP + (k8 >> 2) * 64 * 64 + q * 64 + (((k8 & 3) ^ swz(q)) << 4)) = mx;
+      mxs[e] = mx;
     }
-    // the next tile's footprint DMA and epilogue overwrite what this tile's readers still use
+    if constexpr (C1) {
+      // pooled rows q as the c1 B operand [k-block k8/4][64 rows][4 x 16-B chunks ^ swz(q)], staged in the tile
+      // region once every wave has finished pooling from it (the footprint region holds the next tile's DMA)
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int q = (wave + 4 * e) * SP_TC + px;
+        if (wave + 4 * e < SP_TR)
+          *reinterpret_cast<uint4*>(tile + (k8 >> 2) * 64 * 64 + q * 64 + (((k8 & 3) ^ swz(q)) << 4)) = mxs[e];
+      }
+    }
+    // the next tile's epilogue overwrites what this tile's readers still use
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     if constexpr (C1) {
       // t1 = relu(W1 . pooled + b1) for the tile's 56 pooled pixels (wave w: rows 16w..16w+15; rows >= 56 and
@@ -368,7 +418,7 @@ void stem_pool_direct_kernel(const StemParams p, int ntiles) {
       for (int j = 0; j < 4; ++j) a1[j] = f32x4_t{b1v[j].x, b1v[j].y, b1v[j].z, b1v[j].w};
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
-        const bf16x8_t fx = *reinterpret_cast<const bf16x8_t*>(dsm + D_FP + ks * 64 * 64 + r * 64 +
+        const bf16x8_t fx = *reinterpret_cast<const bf16x8_t*>(tile + ks * 64 * 64 + r * 64 +
                                                                (((lane >> 4) ^ swz(r)) << 4));
 #pragma unroll
         for (int j = 0; j < 4; ++j) a1[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1f[j][ks], fx, a1[j], 0, 0, 0);
@@ -382,7 +432,7 @@ void stem_pool_direct_kernel(const StemParams p, int ntiles) {
           *reinterpret_cast<uint2*>(dst + 16 * j) =
               make_uint2(pack_relu_bf16x2(a1[j][0], a1[j][1]), pack_relu_bf16x2(a1[j][2], a1[j][3]));
       }
-      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // pooled rows read before the next DMA
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // pooled rows read before the next epilogue
     }
   }
 }
