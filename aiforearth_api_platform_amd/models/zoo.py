@@ -45,15 +45,30 @@ def megadetector(device="cuda", seed: int = 0, max_dets: Optional[int] = None, m
 
 
 def landcover(device="cuda", height: int = 4096, width: int = 4096, tile: int = 512, stride: int = 448,
-              tile_batch: int = 16, n_classes: int = 7, seed: int = 0):
+              tile_batch: int = 16, n_classes: int = 7, seed: int = 0, unet_width: int = 64):
     from ..ops.stitch import TileGrid
     from ..runtime.spatial import SpatialSegmenter
     from .unet import FusedUNet, unet_landcover
 
-    f = FusedUNet(unet_landcover(n_classes=n_classes, seed=seed), device=device)
+    f = FusedUNet(unet_landcover(n_classes=n_classes, seed=seed, width=unet_width), device=device)
     seg = SpatialSegmenter(f.forward_u8, TileGrid(height, width, tile, stride), f.n_classes, torch.device(device),
                            tile_batch=tile_batch, local=True)
     return SegmenterServable(seg.run, height, width, f.n_classes)
+
+
+def landcover_extent(device="cuda", mosaics=None, tile: int = 512, stride: int = 448, max_extent=(2048, 2048),
+                     tile_batch: int = 16, n_classes: int = 7, seed: int = 0, unet_width: int = 64):
+    """``/v2/landcover/classifybyextent`` and ``tilebyextent`` (create_sync_api_management_api.sh:52-92): the
+    registered ``mosaics`` (name -> {height, width, channels, geotransform, path | seed}) stay resident in this
+    worker's HBM; each task is a 64-byte extent record (runtime/extent.py) and returns the window's class map,
+    identical to that window of the full-mosaic ``classify`` with the same tile grid."""
+    from ..runtime.extent import ExtentSegmenter, ExtentServable, MosaicSpec
+    from .unet import FusedUNet, unet_landcover
+
+    f = FusedUNet(unet_landcover(n_classes=n_classes, seed=seed, width=unet_width), device=device)
+    seg = ExtentSegmenter(f.forward_u8, MosaicSpec.parse(mosaics or {}), tile, stride, f.n_classes, device,
+                          tile_batch=tile_batch)
+    return ExtentServable(seg, tuple(max_extent), f.n_classes)
 
 
 def select_crops_padded(dets, max_crops: int, score_thresh: float, class_id: Optional[int]):
@@ -202,5 +217,6 @@ def landcover_spatial(device="cuda", group=None, role: str = "leader", height: i
     return _Follower(seg.serve_follower)
 
 
-__all__ = ["resnet50_classifier", "camera_trap_ensemble_pair", "landcover_spatial", "megadetector", "landcover", "camera_trap_ensemble", "select_crops_padded",
+__all__ = ["resnet50_classifier", "camera_trap_ensemble_pair", "landcover_spatial", "megadetector", "landcover",
+           "landcover_extent", "camera_trap_ensemble", "select_crops_padded",
            "StaticEnsemble", "OutputField"]

@@ -44,6 +44,7 @@ class ModelEndpoint:
         self.ring = self.worker.ring
         self.is_pool = hasattr(self.worker, "submit_slots")
         self.decode = decode or (lambda body, ct: decode_image(body, ct, self.ring.item_shape))
+        self.custom_decode = decode is not None  # (not an image endpoint: the ingest front-ends leave it alone)
         # decode worker processes writing into the shared ring (pool backends: the ring is shared memory)
         self.decode_pool = None
         if decode_processes > 0 and decode is None and hasattr(self.ring, "name"):

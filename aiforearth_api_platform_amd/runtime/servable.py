@@ -284,6 +284,8 @@ def format_result(kind: str, fields_json: Sequence, row: Optional[bytes]) -> Opt
     if row is None:
         return None
     fields = [OutputField.from_json(f) for f in fields_json]
+    if kind not in KINDS and kind == "extent_segmenter":
+        from . import extent  # noqa: F401  (registers its kind)
     return KINDS.get(kind, Servable).format(decode_row(row, fields))
 
 

@@ -56,7 +56,9 @@ def start_frontends(cfg: Config, doc: Dict[str, Any], endpoints: Dict[str, Any],
     """Spawn the ingest front-end processes (runtime/frontend.py) for the platform's pool endpoints."""
     from .runtime.frontend import spawn_frontends
 
-    pools = {name: ep for name, ep in endpoints.items() if getattr(ep, "is_pool", False)}
+    # image endpoints only: requests of endpoints with their own decoder (extent records) go to the gateway
+    pools = {name: ep for name, ep in endpoints.items() if getattr(ep, "is_pool", False)
+             and not getattr(ep, "custom_decode", False)}
     routes = []
     for r in doc.get("routes") or []:
         be = r.get("backend")
@@ -68,6 +70,19 @@ def start_frontends(cfg: Config, doc: Dict[str, Any], endpoints: Dict[str, Any],
     return spawn_frontends(frontend_count(cfg), pools, routes, cfg.host, port, f"http://127.0.0.1:{internal_port}",
                            security={"keys": parse_keys(cfg.subscription_keys), "tls_cert": cfg.tls_cert,
                                      "tls_key": cfg.tls_key})
+
+
+def _request_decoder(e: Dict[str, Any]):
+    """Endpoints whose requests are not images: ``request: extent`` = land-cover classifybyextent /
+    tilebyextent (``extent_op: classify | tile``), JSON extents encoded into 64-byte records (runtime/extent.py)."""
+    if e.get("request") != "extent":
+        return None
+    from .runtime.extent import OP_CLASSIFY, OP_TILE, MosaicSpec, request_decoder
+
+    kw = e.get("kwargs") or {}
+    return request_decoder(MosaicSpec.parse(kw.get("mosaics") or {}), OP_TILE if e.get("extent_op") == "tile"
+                           else OP_CLASSIFY, tuple(kw.get("max_extent", (2048, 2048))), int(kw.get("tile", 512)),
+                           int(kw.get("stride", 448)))
 
 
 def build_platform(doc: Dict[str, Any], cfg: Config):
@@ -97,8 +112,9 @@ def build_platform(doc: Dict[str, Any], cfg: Config):
                               heartbeat_timeout_s=cfg.heartbeat_timeout_s,
                               ring_slots=int(e.get("ring_slots", 0)), frontends=frontend_count(cfg),
                               frontend_slots=int(e.get("frontend_ring_slots", cfg.frontend_ring_slots)))
-            ep = ModelEndpoint(cp, e["path"], worker=pool, base_url=base_url,
-                               decode_processes=int(e.get("decode_processes", cfg.decode_processes)))
+            decode = _request_decoder(e)
+            ep = ModelEndpoint(cp, e["path"], worker=pool, base_url=base_url, decode=decode,
+                               decode_processes=0 if decode else int(e.get("decode_processes", cfg.decode_processes)))
         else:
             dev = torch.device(devs[0])
             servable = as_servable(_load(e["factory"])(device=str(dev), **(e.get("kwargs") or {})),

@@ -303,7 +303,14 @@ void stem_pool_direct_kernel(const StemParams p, int ntiles) {
                          pack_bf16x2(v[14], v[15]));
       }
     }
-    wait_vmcnt<0>();  // this tile's footprint landed (and the previous tile's stores retired)
+    // this tile's footprint landed. From the second tile on (C1) the DMA is already complete: the previous
+    // iteration waited for its c1 weight loads, issued after the DMA (vmcnt retires in issue order), so only the
+    // previous tile's stores can be outstanding (<= 2 pooled-row + 4 t1 stores per wave): they may stay in flight
+    if (C1 && !U8 && t != static_cast<int>(blockIdx.x)) {
+      wait_vmcnt<6>();
+    } else {
+      wait_vmcnt<0>();
+    }
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // footprint (and weights) visible
 
     f32x4_t acc[4][4];
