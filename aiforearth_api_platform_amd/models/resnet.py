@@ -134,9 +134,12 @@ class FusedResNet:
     """Inference graph over packed, BN-folded layers (NHWC bf16)."""
 
     def __init__(self, model: ResNet, device="cpu", in_ch: Optional[int] = None,
-                 chunk: Optional[Tuple[int, int]] = None):
+                 chunk: Optional[Tuple[int, int]] = None, dtype: torch.dtype = torch.bfloat16):
+        """``dtype``: bf16 (the fused serving graph: K1s stem, K1c chains, K1p pairs) or fp16 (every conv one K1
+        launch on f16 MFMA, weights re-rounded from fp32 — the ensemble's crop classifier)."""
         model = model.eval()
         self.device = torch.device(device)
+        self.dtype = dtype
         self.in_ch = in_ch or model.conv1.in_channels
         w, b = fold_bn(model.conv1.weight.data.float(), model.bn1.weight.data.float(), model.bn1.bias.data.float(),
                        model.bn1.running_mean.float(), model.bn1.running_var.float(), model.bn1.eps)
@@ -154,6 +157,13 @@ class FusedResNet:
         self.num_classes = model.fc.out_features
         self.chunk = chunk if chunk is not None else _env_chunk()
         self.chain = _env_chain()
+        if dtype == torch.float16:  # the K1 path is the one built for both element types
+            self.stem = self.stem.cast(dtype)
+            self.blocks = [tuple(c.cast(dtype) if c is not None else None for c in blk) for blk in self.blocks]
+            self.fc = self.fc.cast(dtype)
+            self.chain, self.chunk = False, None
+        elif dtype != torch.bfloat16:
+            raise ValueError(f"FusedResNet dtype must be bf16 or fp16, got {dtype}")
         self.fold_down = os.environ.get("AI4E_RESNET_FOLD_DOWN", "1") not in ("0", "off", "")
         # uint8 preprocess fused into the stem kernel (AI4E_STEM_U8=1); off by default: measured 0.1 ms slower
         # per batch of 256 than the separate K7 preprocess + K1s (byte gathers serialize with the conv)
@@ -220,6 +230,8 @@ class FusedResNet:
         return space_to_depth_shifted(x[..., : self.in_ch])
 
     def _stem(self, x: torch.Tensor) -> torch.Tensor:
+        if self.dtype == torch.float16:  # K1 s2d conv + the max-pool kernel (K1s is bf16-only)
+            return maxpool2d_nhwc(conv2d_nhwc(self.stem_input(x), self.stem, relu=True))
         return stem_pool(self.stem_input(x), self.stem)  # K1s: conv + bias + ReLU + 3x3/2 max-pool
 
     def _stem_t1(self, x: torch.Tensor):
@@ -395,7 +407,7 @@ class FusedResNet:
         return y
 
     def logits(self, x: torch.Tensor, preprocess=None) -> torch.Tensor:
-        """bf16 logits [N, classes]."""
+        """Logits [N, classes] in the model dtype (bf16 / fp16)."""
         return self._head_logits(self.forward_features(x, preprocess))
 
     # Two-part serving forward (runtime/engine.py ``split``): stem .. layer2 | layer3 .. top-k. The serving engine
@@ -422,7 +434,7 @@ class FusedResNet:
             if self._fc_lin is None:
                 k = self.fc.cin_pad
                 self._fc_lin = (self.fc.w_packed[:self.fc.cout, :k].contiguous(),
-                                self.fc.bias[:self.fc.cout].to(torch.bfloat16))
+                                self.fc.bias[:self.fc.cout].to(self.dtype))
             return F.linear(f.reshape(f.shape[0], -1), *self._fc_lin)
         return conv2d_nhwc(f, self.fc).reshape(f.shape[0], -1)
 
@@ -432,10 +444,15 @@ class FusedResNet:
     def topk_u8(self, img_u8: torch.Tensor, k: int = 5):
         """uint8 NHWC images -> (top-k class ids int32, probabilities fp32): the serving head, with softmax
         and top-k fused into one kernel (ops/head.py)."""
-        return softmax_topk(self.logits(img_u8, preprocess=preprocess_s2d_u8), k)
+        return softmax_topk(self.logits(img_u8, preprocess=self._pre()), k)
+
+    def _pre(self):
+        if self.dtype == torch.float16:
+            return lambda img: preprocess_s2d_u8(img, dtype=torch.float16)
+        return preprocess_s2d_u8
 
     def forward_u8(self, img_u8: torch.Tensor) -> torch.Tensor:
         """uint8 NHWC images -> fp32 logits (preprocess fused into the first kernel launch)."""
-        return self.forward(img_u8, preprocess=preprocess_s2d_u8)
+        return self.forward(img_u8, preprocess=self._pre())
 
     __call__ = forward_u8

@@ -20,16 +20,6 @@ def tiny_classifier(device="cpu", **kw):
     return ChannelMeanClassifier(device, **kw)
 
 
-def resnet50_fused(device="cuda", seed: int = 0, num_classes: int = 1000, topk: int = 5):
-    """Factory used by the worker pool for the headline ResNet-50 endpoint: the fused HIP model with
-    its fused softmax/top-k head (``FusedResNet.topk_u8``)."""
-    from ..runtime.servable import ClassifierServable
-    from .resnet import FusedResNet, resnet50
-
-    m = FusedResNet(resnet50(num_classes=num_classes, seed=seed), device=device)
-    return ClassifierServable(m, topk, head=m.topk_u8)
-
-
 def echo(task_id: str, body: bytes, headers=None):
     """Sync echo backend (BASELINE config #1: plumbing, no GPU)."""
     return 200, body

@@ -189,6 +189,67 @@ def camera_trap_ensemble_pair(device="cuda", group=None, role: str = "leader", s
     return _Follower(DetectClassifyPipeline(None, cls.forward_u8, dev, cfg, group=group).serve_classifier)
 
 
+class _StageGraphEnsembleServable(EnsembleServable):
+    """One detector leader of an N:M stage graph (runtime/pipeline.py StageGraphPipeline): detection + crops in
+    this process's HIP graph, classification on the group's classifier GPU over RCCL P2P."""
+
+    stages = 1
+
+    def __call__(self, images_u8):
+        boxes, scores, valid, res = self.pipeline.run_batches([images_u8])[0]
+        b, m = valid.shape
+        flat = valid.reshape(-1)
+        species = torch.full((b * m,), -1, dtype=torch.int32, device=valid.device)
+        prob = torch.zeros(b * m, device=valid.device)
+        n = res.shape[0]
+        if n:
+            pos = torch.nonzero(flat).reshape(-1)[:n]  # the valid slots, in the order the crops were packed
+            species[pos] = res[:, 0].to(torch.int32)
+            prob[pos] = res[:, 1].float()
+        count = valid.sum(1, keepdim=True).to(torch.int32)
+        return (boxes.float().contiguous(), (scores * valid).float().contiguous(), species.reshape(b, m),
+                prob.reshape(b, m), count)
+
+    def xgmi_bytes(self) -> dict:
+        return {"sent": self.pipeline.bytes_sent, "received": self.pipeline.bytes_received}
+
+    def close(self) -> None:
+        self.pipeline.stop()
+
+
+def camera_trap_ensemble_group(device="cuda", group=None, role: str = "leader", group_rank: int = 0,
+                               n_leaders: int = 1, seed: int = 0, max_crops: int = 4, score_thresh: float = 0.5,
+                               class_id: Optional[int] = 1, num_species: int = 200, wire_dtype: str = "uint8",
+                               classifier_dtype: str = "bf16", **det_cfg):
+    """Config 5 as an N:M stage graph (``ModelSpec.group_size`` = N + M, ``group_leaders`` = N): every leader is
+    a detector GPU taking its own batches from the scheduler, the followers classify the crops of the detectors
+    assigned to them (``runtime.pipeline.stage_assignment``), each stage in HIP graphs. ``classifier_dtype``:
+    "bf16" (the fused ResNet-50 chains) or "fp16" (the per-conv K1 graph with f16 MFMA, ops/conv.py)."""
+    from ..runtime.pipeline import PipelineConfig, StageGraphPipeline
+
+    cfg = PipelineConfig(score_thresh=score_thresh, class_id=class_id, max_crops_per_image=max_crops,
+                         wire_dtype=wire_dtype)
+    dev = torch.device(device)
+    if role == "leader":
+        from .faster_rcnn import DetectorConfig, FasterRCNN
+
+        det = FasterRCNN(DetectorConfig(**det_cfg), seed=seed, device=device)
+        pipe = StageGraphPipeline(det.forward_u8, None, dev, cfg, group=group, n_leaders=n_leaders)
+        return _StageGraphEnsembleServable(pipe, max_crops)
+    cls = crop_classifier(device, num_species, seed + 1, classifier_dtype)
+    pipe = StageGraphPipeline(None, cls, dev, cfg, group=group, n_leaders=n_leaders)
+    return _Follower(pipe.serve)
+
+
+def crop_classifier(device, num_species: int, seed: int, dtype: str = "bf16"):
+    """uint8 crops [N, 224, 224, 3] -> logits: the fused ResNet-50 (bf16), or its per-conv K1 graph in fp16."""
+    from .resnet import FusedResNet, resnet50
+
+    m = FusedResNet(resnet50(num_classes=num_species, seed=seed), device=device,
+                    dtype=torch.float16 if dtype in ("fp16", "float16") else torch.bfloat16)
+    return m.forward_u8
+
+
 class _SpatialSegmenterServable(SegmenterServable):
     def __init__(self, seg, height, width, n_classes):
         super().__init__(seg.run, height, width, n_classes)
@@ -218,5 +279,6 @@ def landcover_spatial(device="cuda", group=None, role: str = "leader", height: i
 
 
 __all__ = ["resnet50_classifier", "camera_trap_ensemble_pair", "landcover_spatial", "megadetector", "landcover",
-           "landcover_extent", "camera_trap_ensemble", "select_crops_padded",
+           "landcover_extent", "camera_trap_ensemble", "camera_trap_ensemble_group", "crop_classifier",
+           "select_crops_padded",
            "StaticEnsemble", "OutputField"]

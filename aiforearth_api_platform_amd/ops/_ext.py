@@ -27,6 +27,7 @@ _c_int, _c_long, _c_float, _vp = ctypes.c_int, ctypes.c_long, ctypes.c_float, ct
 # name -> argtypes (all return int status)
 _SIGS = {
     "ai4e_conv2d_fwd": [_vp, _vp, _vp, _vp, _vp] + [_c_int] * 19 + [_vp],
+    "ai4e_conv2d_f16_fwd": [_vp, _vp, _vp, _vp, _vp] + [_c_int] * 19 + [_vp],
     "ai4e_conv2d_gn_fwd": [_vp, _vp, _vp, _vp, _vp] + [_c_int] * 19 + [_vp, _c_int, _vp],
     "ai4e_conv_chain_fwd": [_vp] * 10 + [_c_int] * 11 + [_vp, _c_int, _vp],
     "ai4e_conv_pair_fwd": [_vp] * 8 + [_c_int] * 5 + [_vp],
@@ -36,8 +37,11 @@ _SIGS = {
     "ai4e_softmax_topk": [_vp, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp],
     "ai4e_preprocess_u8": [_vp, _vp, _c_long, _c_int, _vp, _vp, _c_float, _vp],
     "ai4e_preprocess_s2d_u8": [_vp, _vp, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _c_float, _vp],
+    "ai4e_preprocess_s2d_u8_dt": [_vp, _vp, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _c_float, _c_int, _vp],
     "ai4e_maxpool2d": [_vp, _vp] + [_c_int] * 10 + [_vp],
+    "ai4e_maxpool2d_dt": [_vp, _vp] + [_c_int] * 11 + [_vp],
     "ai4e_global_avgpool": [_vp, _vp, _c_int, _c_int, _c_int, _vp],
+    "ai4e_global_avgpool_dt": [_vp, _vp, _c_int, _c_int, _c_int, _c_int, _vp],
     "ai4e_groupnorm_nhwc": [_vp, _vp, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_float, _c_int, _c_int,
                             _c_int, _vp],
     "ai4e_groupnorm_apply_nhwc": [_vp, _vp, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_float, _c_int, _c_int,
@@ -82,6 +86,8 @@ def lib() -> ctypes.CDLL:
 
 
 def call(name: str, *args) -> None:
+    if name not in _SIGS:  # an untyped ctypes call would truncate pointers and streams to 32-bit ints
+        raise KernelError(f"{name}: no argument signature registered in ops/_ext.py _SIGS")
     rc = getattr(lib(), name)(*args)
     if rc != 0:
         raise KernelError(f"{name} failed with status {rc}")

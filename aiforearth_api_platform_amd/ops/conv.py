@@ -52,6 +52,19 @@ class PackedConv:
         return PackedConv(self.w_ref.to(device), self.b_ref.to(device), self.w_packed.to(device), self.bias.to(device),
                           self.cin, self.cin_pad, self.cout, self.kh, self.kw, self.stride, self.pad, self.pad_hi)
 
+    def cast(self, dtype: torch.dtype) -> "PackedConv":
+        """The same layer with its packed weights in ``dtype`` (fp16 for the f16 K1 path), re-rounded from the
+        fp32 weights (``w_ref``; the packed layout is [Cout, (kh, kw, c)] with zero padding, as pack_conv)."""
+        if dtype == self.w_packed.dtype:
+            return self
+        w = torch.zeros(self.cout, self.kh, self.kw, self.cin_pad, device=self.w_ref.device)
+        w[..., :self.w_ref.shape[1]] = self.w_ref.float().permute(0, 2, 3, 1)
+        k = self.kh * self.kw * self.cin_pad
+        wp = torch.zeros_like(self.w_packed, dtype=dtype)
+        wp[:self.cout, :k] = w.reshape(self.cout, k).to(dtype)
+        return PackedConv(self.w_ref, self.b_ref, wp, self.bias, self.cin, self.cin_pad, self.cout, self.kh, self.kw,
+                          self.stride, self.pad, self.pad_hi)
+
     def out_hw(self, h: int, w: int):
         hi = self.pad if self.pad_hi is None else self.pad_hi
         return ((h + self.pad + hi - self.kh) // self.stride + 1, (w + self.pad + hi - self.kw) // self.stride + 1)
@@ -164,8 +177,10 @@ def _pointwise_blas(x, pc, relu):
 def _conv_hip(x, pc, residual, relu, out, out_coff, tile_cfg, residual_up2=False, gn=None):
     n, h, w, c = x.shape
     oh, ow = pc.out_hw(h, w)
-    if x.dtype != torch.bfloat16 or out.dtype != torch.bfloat16:
-        raise TypeError("HIP conv path is bf16")
+    f16 = x.dtype == torch.float16
+    if x.dtype not in (torch.bfloat16, torch.float16) or out.dtype != x.dtype or pc.w_packed.dtype != x.dtype or \
+            (residual is not None and residual.dtype != x.dtype) or (f16 and gn is not None):
+        raise TypeError("HIP conv path: bf16 or fp16 activations, weights (PackedConv.cast) and residual alike")
     # x may be a channel-slice view of a wider NHWC buffer: rows stride = x.stride(2)
     if x.stride(3) != 1 or x.stride(2) * w != x.stride(1) or x.stride(1) * h != x.stride(0):
         raise ValueError("conv input must be an NHWC (possibly channel-sliced) dense tensor")
@@ -185,7 +200,7 @@ def _conv_hip(x, pc, residual, relu, out, out_coff, tile_cfg, residual_up2=False
             out.data_ptr(), n, h, w, c, ldx, xoff % ldx, pc.kh, pc.kw, pc.stride, pc.pad, oh, ow, pc.cout, pc.kpad, ldy,
             out_coff, ldres, int(relu) | (2 if residual_up2 else 0), tile_cfg)
     if gn is None:
-        _ext.call("ai4e_conv2d_fwd", *args, _ext.stream_ptr(x.device))
+        _ext.call("ai4e_conv2d_f16_fwd" if f16 else "ai4e_conv2d_fwd", *args, _ext.stream_ptr(x.device))
     else:
         _ext.call("ai4e_conv2d_gn_fwd", *args, gn[0].data_ptr(), gn[1], _ext.stream_ptr(x.device))
 

@@ -36,23 +36,23 @@ def preprocess_u8(img: torch.Tensor, mean: Sequence[float] = IMAGENET_MEAN, std:
 
 
 def preprocess_s2d_u8(img: torch.Tensor, mean: Sequence[float] = IMAGENET_MEAN, std: Sequence[float] = IMAGENET_STD,
-                      scale: float = 1.0 / 255.0) -> torch.Tensor:
-    """uint8 NHWC [N,H,W,cin<=4] -> normalized, 2x2 space-to-depth bf16 [N,H/2,W/2,16] for the s2d stem:
-    ``out[i, j, (dy*2+dx)*cin + c] = norm(x[2i+dy-1, 2j+dx-1, c])`` (zero outside the image)."""
+                      scale: float = 1.0 / 255.0, dtype: torch.dtype = torch.bfloat16) -> torch.Tensor:
+    """uint8 NHWC [N,H,W,cin<=4] -> normalized, 2x2 space-to-depth [N,H/2,W/2,16] (bf16, or fp16) for the s2d
+    stem: ``out[i, j, (dy*2+dx)*cin + c] = norm(x[2i+dy-1, 2j+dx-1, c])`` (zero outside the image)."""
     n, h, w, cin = img.shape
     if img.dtype != torch.uint8 or cin > 4 or h % 2 or w % 2:
         raise ValueError("s2d preprocess expects uint8 NHWC, <= 4 channels, even H and W")
     m4 = list(mean) + [0.0] * (4 - len(mean))
     s4 = list(std) + [1.0] * (4 - len(std))
     if _ext.backend_for(img) == "hip":
-        out = torch.empty(n, h // 2, w // 2, 16, device=img.device, dtype=torch.bfloat16)
+        out = torch.empty(n, h // 2, w // 2, 16, device=img.device, dtype=dtype)
         ma, sa = ctypes_floats(m4), ctypes_floats(s4)
-        _ext.call("ai4e_preprocess_s2d_u8", img.data_ptr(), out.data_ptr(), n, h, w, cin, ctypes.addressof(ma),
-                  ctypes.addressof(sa), scale, _ext.stream_ptr(img.device))
+        _ext.call("ai4e_preprocess_s2d_u8_dt", img.data_ptr(), out.data_ptr(), n, h, w, cin, ctypes.addressof(ma),
+                  ctypes.addressof(sa), scale, int(dtype == torch.float16), _ext.stream_ptr(img.device))
         return out
     x = (img.float() * scale - torch.tensor(m4[:cin], device=img.device)) / torch.tensor(s4[:cin], device=img.device)
     y = space_to_depth_shifted(x)
-    return y.to(torch.bfloat16) if img.is_cuda else y
+    return y.to(dtype) if img.is_cuda else y
 
 
 def space_to_depth_shifted(x: torch.Tensor) -> torch.Tensor:
@@ -76,8 +76,8 @@ def maxpool2d_nhwc(x: torch.Tensor, k: int = 3, stride: int = 2, pad: int = 1) -
         if x.stride(3) != 1 or x.stride(1) != w * x.stride(2) or x.stride(0) != h * x.stride(1):
             x = x.contiguous()  # channel slices of an NHWC buffer are read in place
         y = torch.empty(n, oh, ow, c, device=x.device, dtype=x.dtype)
-        _ext.call("ai4e_maxpool2d", x.data_ptr(), y.data_ptr(), n, h, w, c, oh, ow, k, stride, pad, x.stride(2),
-                  _ext.stream_ptr(x.device))
+        _ext.call("ai4e_maxpool2d_dt", x.data_ptr(), y.data_ptr(), n, h, w, c, oh, ow, k, stride, pad, x.stride(2),
+                  int(x.dtype == torch.float16), _ext.stream_ptr(x.device))
         return y
     y = F.max_pool2d(x.permute(0, 3, 1, 2).float(), k, stride, pad)
     return y.permute(0, 2, 3, 1).to(x.dtype).contiguous()
@@ -89,6 +89,7 @@ def global_avgpool_nhwc(x: torch.Tensor) -> torch.Tensor:
     if _ext.backend_for(x) == "hip":
         x = x.contiguous()
         y = torch.empty(n, 1, 1, c, device=x.device, dtype=x.dtype)
-        _ext.call("ai4e_global_avgpool", x.data_ptr(), y.data_ptr(), n, h * w, c, _ext.stream_ptr(x.device))
+        _ext.call("ai4e_global_avgpool_dt", x.data_ptr(), y.data_ptr(), n, h * w, c, int(x.dtype == torch.float16),
+                  _ext.stream_ptr(x.device))
         return y
     return x.float().mean(dim=(1, 2), keepdim=True).to(x.dtype)

@@ -49,6 +49,9 @@ class ModelSpec:
     # process group (RCCL on GPUs, gloo on CPU) — the leader talks to the scheduler, the followers serve
     # it (detector -> classifier pair over xGMI, spatial-parallel mosaic segmentation)
     group_size: int = 1
+    # stage graph: the first `group_leaders` processes of a group each take batches from the scheduler (e.g. 7
+    # detector GPUs), the rest serve them (e.g. 1 classifier GPU); 1 = one leader + followers
+    group_leaders: int = 1
 
 
 def load_factory(path: str):
@@ -340,8 +343,9 @@ class GpuWorker:
         self.conn.done(bid, status, rows.tobytes(), self.row_bytes, (t_recv, t_launch, time.monotonic(), 0, 0))
 
 
-def join_group(device: str, group_rank: int, group_size: int, port: int):
-    """Process group of one worker group (RCCL over xGMI between its GPUs; gloo on CPU)."""
+def join_group(device: str, group_rank: int, group_size: int, port: int, n_leaders: int = 1):
+    """Process group of one worker group (RCCL over xGMI between its GPUs; gloo on CPU). Stage-graph groups
+    (``n_leaders`` > 1) also tell the factory its group rank and the number of leaders."""
     import datetime
 
     import torch.distributed as dist
@@ -351,7 +355,10 @@ def join_group(device: str, group_rank: int, group_size: int, port: int):
     kw = {"device_id": dev} if backend == "nccl" else {}
     dist.init_process_group(backend, init_method=f"tcp://127.0.0.1:{port}", rank=group_rank, world_size=group_size,
                             timeout=datetime.timedelta(seconds=600), **kw)
-    return {"group": dist.group.WORLD, "role": "leader" if group_rank == 0 else "follower"}
+    kw = {"group": dist.group.WORLD, "role": "leader" if group_rank < n_leaders else "follower"}
+    if n_leaders > 1:
+        kw.update(group_rank=group_rank, n_leaders=n_leaders)
+    return kw
 
 
 def follower_main(device: str, spec: ModelSpec, group_rank: int, group_size: int, port: int) -> None:
@@ -360,7 +367,7 @@ def follower_main(device: str, spec: ModelSpec, group_rank: int, group_size: int
     dev = torch.device(device)
     if dev.type == "cuda":
         torch.cuda.set_device(dev)
-    gk = join_group(device, group_rank, group_size, port)
+    gk = join_group(device, group_rank, group_size, port, spec.group_leaders)
     part = load_factory(spec.factory)(device=device, **spec.kwargs, **gk)
     try:
         part.serve_follower()
@@ -373,14 +380,15 @@ def follower_main(device: str, spec: ModelSpec, group_rank: int, group_size: int
 
 def worker_main(conn, rank: int, device: str, spec: ModelSpec, shm_name: str, nslots: int, hb_interval: float,
                 partition: Optional[Tuple[int, int]] = None, untrack: bool = False, local_ring=None,
-                group_port: int = 0, ready_event: Optional[threading.Event] = None) -> None:
+                group_port: int = 0, ready_event: Optional[threading.Event] = None, group_rank: int = 0) -> None:
     """Entry point of a spawned worker process (and of ``torchrun`` worker ranks, which pass their
     ingest partition's ``local_ring`` and ``untrack=True``). With ``spec.group_size > 1`` this is the
     leader of a worker group (rendezvous on ``group_port``)."""
     dev = torch.device(device)
     if dev.type == "cuda":
         torch.cuda.set_device(dev)
-    group_kwargs = join_group(device, 0, spec.group_size, group_port) if spec.group_size > 1 else None
+    group_kwargs = (join_group(device, group_rank, spec.group_size, group_port, spec.group_leaders)
+                    if spec.group_size > 1 else None)
     shm, buf = attach_ring(shm_name, nslots, spec.item_shape, untrack=untrack)
     pinned = pin_host(buf) if dev.type == "cuda" else False
     if local_ring is None and partition is not None:

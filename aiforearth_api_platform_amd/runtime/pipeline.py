@@ -24,6 +24,7 @@ runs both stages on one GPU with a local hand-off (no RCCL), same code path othe
 from __future__ import annotations
 
 import os
+import time
 from dataclasses import dataclass
 from typing import Callable, List, Optional, Sequence, Tuple
 
@@ -110,17 +111,17 @@ class DetectClassifyPipeline:
         h, w = self.cfg.crop_hw
         hdr = torch.zeros(1, dtype=torch.int64, device=self.device)
         while True:
-            dist.recv(hdr, self.peer, group=self.group)
+            dist.recv(hdr, group_src=self.peer, group=self.group)
             n = int(hdr.item())
             if n == STOP:
                 return total
             crops = torch.empty(n, h, w, 3, dtype=self.wire_dtype, device=self.device)
             if n:
-                dist.recv(crops, self.peer, group=self.group)
+                dist.recv(crops, group_src=self.peer, group=self.group)
                 self.bytes_received += crops.numel() * crops.element_size()
             res = self.classify(self._from_wire(crops))
             if n:
-                dist.send(res.contiguous(), self.peer, group=self.group)
+                dist.send(res.contiguous(), group_dst=self.peer, group=self.group)
                 self.bytes_sent += res.numel() * res.element_size()
             total += n
 
@@ -145,18 +146,18 @@ class DetectClassifyPipeline:
         if self._fail_at and self._handoffs == self._fail_at:
             raise RuntimeError(f"injected xGMI hand-off failure (batch {self._handoffs})")
         n = torch.tensor([crops.shape[0]], dtype=torch.int64, device=self.device)
-        works = [(dist.isend(n, self.peer, group=self.group), n)]
+        works = [(dist.isend(n, group_dst=self.peer, group=self.group), n)]
         self.bytes_sent += 8
         if crops.shape[0]:
             c = crops.contiguous()
-            works.append((dist.isend(c, self.peer, group=self.group), c))
+            works.append((dist.isend(c, group_dst=self.peer, group=self.group), c))
             self.bytes_sent += c.numel() * c.element_size()
         return works
 
     def _recv_results(self, n: int) -> torch.Tensor:
         res = torch.empty(n, 2, device=self.device)
         if n:
-            dist.recv(res, self.peer, group=self.group)
+            dist.recv(res, group_src=self.peer, group=self.group)
             self.bytes_received += res.numel() * res.element_size()
         return res
 
@@ -190,4 +191,212 @@ class DetectClassifyPipeline:
 
     def stop(self) -> None:
         if self.world > 1 and self.is_detector:
-            dist.send(torch.tensor([STOP], dtype=torch.int64, device=self.device), self.peer, group=self.group)
+            dist.send(torch.tensor([STOP], dtype=torch.int64, device=self.device), group_dst=self.peer, group=self.group)
+
+
+# ----------------------------------------------------------------------------------------------------------
+# N:M stage graph (config 5 at node scale): L detector GPUs feed M classifier GPUs of one RCCL group.
+# ----------------------------------------------------------------------------------------------------------
+def stage_assignment(n_leaders: int, world: int) -> List[List[int]]:
+    """Classifier c (group rank n_leaders + c) serves detectors d with d % M == c (M = world - n_leaders):
+    a fixed map, so each detector always talks to one classifier and the P2P pairs (and RCCL's per-pair
+    communicators) never change. Ratio: sized by measured stage rates, e.g. 7:1 on an 8-GPU node when one
+    GPU classifies the crops of seven detectors (bench/api_bench.py --model ensemble_group)."""
+    m = world - n_leaders
+    if n_leaders < 1 or m < 1:
+        raise ValueError(f"stage graph needs >= 1 detector and >= 1 classifier rank, got {n_leaders}:{m}")
+    return [[d for d in range(n_leaders) if d % m == c] for c in range(m)]
+
+
+class _GraphRunner:
+    """One static-shape callable captured per input size in HIP graphs (CUDA graphs on ROCm); eager on CPU."""
+
+    def __init__(self, fn: Callable, device: torch.device, warmup: int = 2):
+        self.fn, self.device, self.warmup = fn, device, warmup
+        self.graphs: dict = {}
+
+    def __call__(self, x: torch.Tensor):
+        if self.device.type != "cuda":
+            return self.fn(x)
+        key = tuple(x.shape)
+        g = self.graphs.get(key)
+        if g is None:
+            static_in = x.clone()
+            s = torch.cuda.Stream(device=self.device)
+            s.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(s):
+                for _ in range(self.warmup):
+                    self.fn(static_in)
+            torch.cuda.current_stream(self.device).wait_stream(s)
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                static_out = self.fn(static_in)
+            g = self.graphs[key] = (graph, static_in, static_out)
+        graph, static_in, static_out = g
+        static_in.copy_(x)
+        graph.replay()
+        return static_out
+
+
+class StageGraphPipeline:
+    """Group ranks [0, L) detect + crop, ranks [L, L + M) classify crops (stage_assignment).
+
+    Detector rank: ``run_batches`` per image batch — a captured graph does detection, crop selection
+    (``models.zoo.select_crops_padded``: the first ``max_crops`` confident boxes per image), the uint8 224^2
+    crop-resize (K5/K7) and the compaction of the valid crops to a prefix; the count comes back to the host,
+    ``n`` and the ``n`` crops go to the rank's classifier over RCCL P2P (xGMI), one batch in flight.
+    Classifier rank: ``serve`` posts a header ``irecv`` for every detector it serves and handles whichever
+    arrives first (no head-of-line blocking behind an idle detector), runs the classifier on the crops in a
+    graph captured per bucket size and sends back ``[n, 2]`` (class, probability). A detector's STOP header
+    retires it; the classifier returns when all of its detectors have stopped.
+    """
+
+    BUCKETS = (8, 16, 32, 64, 128, 256, 512, 1024)
+
+    def __init__(self, detector: Optional[Callable], classifier: Optional[Callable], device: torch.device,
+                 cfg: PipelineConfig, group=None, n_leaders: int = 1, crop_dtype: torch.dtype = torch.uint8):
+        self.detector, self.classifier, self.device, self.cfg, self.group = detector, classifier, device, cfg, group
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.n_leaders = n_leaders
+        self.is_detector = self.rank < n_leaders
+        if self.world == 1:  # both stages in this process (no wire)
+            self.assign, self.peer, self.serves = [], None, []
+        else:
+            self.assign = stage_assignment(n_leaders, self.world)
+            m = self.world - n_leaders
+            self.peer = n_leaders + self.rank % m if self.is_detector else None
+            self.serves = self.assign[self.rank - n_leaders] if not self.is_detector else []
+        self.wire_dtype = getattr(torch, cfg.wire_dtype)
+        self.bytes_sent = self.bytes_received = 0
+        self._det_graph = _GraphRunner(self._detect_crop_compact, device) if self.is_detector else None
+        self._cls_graph = _GraphRunner(self._classify_static, device) if classifier is not None else None
+
+    # ------------------------------------------------------------ detector stage
+    def _detect_crop_compact(self, images: torch.Tensor):
+        from ..models.zoo import select_crops_padded
+
+        b, m = images.shape[0], self.cfg.max_crops_per_image
+        dets = self.detector(images)
+        boxes, scores, valid = select_crops_padded(dets, m, self.cfg.score_thresh, self.cfg.class_id)
+        img = torch.arange(b, device=boxes.device, dtype=torch.float32)[:, None, None].expand(b, m, 1)
+        crops = crop_resize_u8(images[..., :3].contiguous() if images.shape[-1] != 3 else images,
+                               torch.cat([img, boxes], -1).reshape(b * m, 5), self.cfg.crop_hw)
+        flat = valid.reshape(-1)
+        dst = torch.where(flat, torch.cumsum(flat.int(), 0) - 1, torch.full_like(flat, b * m, dtype=torch.int32))
+        h, w = self.cfg.crop_hw
+        packed = torch.zeros(b * m + 1, h, w, 3, dtype=torch.uint8, device=crops.device)
+        packed.index_copy_(0, dst.long(), crops)           # valid crops first, in (image, score) order
+        count = flat.sum().reshape(1).to(torch.int64)
+        return dets, boxes, scores, valid, packed[: b * m].to(self.wire_dtype), count
+
+    def _send(self, crops: torch.Tensor, n: int) -> list:
+        hdr = torch.tensor([n], dtype=torch.int64, device=self.device)
+        works = [(dist.isend(hdr, group_dst=self.peer, group=self.group), hdr)]
+        self.bytes_sent += 8
+        if n:
+            c = crops[:n].contiguous()
+            works.append((dist.isend(c, group_dst=self.peer, group=self.group), c))
+            self.bytes_sent += c.numel() * c.element_size()
+        return works
+
+    def _recv_results(self, n: int) -> torch.Tensor:
+        res = torch.empty(n, 2, device=self.device)
+        if n:
+            dist.recv(res, group_src=self.peer, group=self.group)
+            self.bytes_received += res.numel() * res.element_size()
+        return res
+
+    def run_batches(self, batches: Sequence[torch.Tensor]) -> List[Tuple]:
+        """Detector rank: per batch (boxes [B, M, 4], det scores [B, M], valid [B, M], classes [n, 2] for the
+        valid crops in (image, score) order), one batch's crops on the wire while the next one is detected."""
+        out, pending, inflight = [], None, []
+        for imgs in batches:
+            _, boxes, scores, valid, crops, count = self._det_graph(imgs)
+            boxes, scores, valid = boxes.clone(), scores.clone(), valid.clone()  # (graph outputs are reused)
+            n = int(count.item())
+            if self.world == 1:
+                out.append((boxes, scores, valid, self.classify(crops[:n])))
+                continue
+            works = self._send(crops, n)
+            if pending is not None:
+                out.append(pending[:3] + (self._recv_results(pending[3]),))
+            for w, _ in inflight:
+                w.wait()
+            inflight, pending = works, (boxes, scores, valid, n)
+        if pending is not None:
+            out.append(pending[:3] + (self._recv_results(pending[3]),))
+        for w, _ in inflight:
+            w.wait()
+        return out
+
+    def stop(self) -> None:
+        if self.world > 1 and self.is_detector:
+            dist.send(torch.tensor([STOP], dtype=torch.int64, device=self.device), group_dst=self.peer, group=self.group)
+
+    # ------------------------------------------------------------ classifier stage
+    def _classify_static(self, crops_u8: torch.Tensor) -> torch.Tensor:
+        p = torch.softmax(self.classifier(crops_u8).float(), 1)
+        prob, cls = p.max(1)
+        return torch.stack([cls.float(), prob], 1)
+
+    def classify(self, crops: torch.Tensor) -> torch.Tensor:
+        n = crops.shape[0]
+        if n == 0:
+            return torch.zeros(0, 2, device=self.device)
+        crops = crops if crops.dtype == torch.uint8 else crops.round().clamp(0, 255).to(torch.uint8)
+        bucket = next((b for b in self.BUCKETS if b >= n), None)
+        if bucket is None:  # (more crops than the largest captured bucket: in bucket-sized chunks)
+            return torch.cat([self.classify(crops[i:i + self.BUCKETS[-1]]) for i in range(0, n, self.BUCKETS[-1])])
+        if bucket != n:
+            pad = torch.zeros(bucket, *crops.shape[1:], dtype=crops.dtype, device=crops.device)
+            pad[:n] = crops
+            crops = pad
+        return self._cls_graph(crops)[:n].clone()
+
+    def _headers(self):
+        """Yield (detector, n) as headers arrive from the detectors this rank serves. RCCL: one posted ``irecv``
+        per detector, polled with ``is_completed`` (an event query), so an idle detector never blocks a busy
+        one. gloo (CPU tests) only marks a receive complete inside ``wait``, so there one any-source receive
+        is posted instead — the sender's FIFO order keeps the next unmatched message of every peer a header."""
+        alive = set(self.serves)
+        if dist.get_backend(self.group) == "gloo":
+            hdr = torch.zeros(1, dtype=torch.int64, device=self.device)
+            while alive:
+                wk = dist.irecv(hdr, group=self.group)
+                wk.wait()
+                d = wk._source_rank()
+                n = int(hdr.item())
+                if n == STOP:
+                    alive.discard(d)
+                yield d, n
+            return
+        hdrs = {d: torch.zeros(1, dtype=torch.int64, device=self.device) for d in alive}
+        posted = {d: dist.irecv(hdrs[d], group_src=d, group=self.group) for d in alive}
+        while posted:
+            ready = [d for d, wk in posted.items() if wk.is_completed()]
+            if not ready:
+                time.sleep(0.0002)
+                continue
+            for d in ready:
+                posted.pop(d).wait()
+                n = int(hdrs[d].item())
+                yield d, n  # (the crops are received before this detector's next header is posted)
+                if n != STOP:
+                    posted[d] = dist.irecv(hdrs[d], group_src=d, group=self.group)
+
+    def serve(self) -> int:
+        """Classifier rank loop; returns the number of crops classified."""
+        h, w = self.cfg.crop_hw
+        total = 0
+        for d, n in self._headers():
+            if n == STOP or n == 0:
+                continue
+            crops = torch.empty(n, h, w, 3, dtype=self.wire_dtype, device=self.device)
+            dist.recv(crops, group_src=d, group=self.group)
+            self.bytes_received += crops.numel() * crops.element_size()
+            res = self.classify(crops)
+            dist.send(res.contiguous(), group_dst=d, group=self.group)
+            self.bytes_sent += res.numel() * res.element_size()
+            total += n
+        return total

@@ -5,14 +5,15 @@ The reference's land-cover API only offers caller-side tiling (``classify`` / ``
 4096x4096 (or larger) RGB+NIR mosaic is segmented by all ranks at once — the imagery analogue of
 context parallelism (survey §5.7):
 
-1. rank 0 owns the request; the mosaic is broadcast over RCCL (64 MiB for 4096^2 x 4 uint8);
-2. the regular tile grid (``TileGrid``: tile ``ts``, ``stride``, overlap ``ts - stride``) is cut by
-   whole tile rows, balanced over ranks; each rank runs the fused U-Net on its own tiles only
-   (no redundant compute);
-3. **halo exchange**: mosaic rows in the overlap band between two ranks need the neighbour's
-   boundary tile row, so every rank ``isend``s its *last* tile row of logits to rank+1 (issued as
-   soon as that row is computed, overlapped with the rest of its tiles) — one P2P transfer over
-   one xGMI link per boundary;
+1. the regular tile grid (``TileGrid``: tile ``ts``, ``stride``, overlap ``ts - stride``) is split by
+   TILES (row-major flat ranges, at most one tile apart between ranks); each rank runs the fused
+   U-Net on its own tiles only (no redundant compute);
+2. rank 0 owns the request and sends each rank only the mosaic rows its tiles cover (one P2P
+   message per rank over its own xGMI link, instead of broadcasting the whole 64 MiB mosaic);
+3. **halo exchange**: stitching is by tile rows (a rank blends the mosaic rows from its first tile
+   row's origin to the next rank's), so a rank needs the logits of its tile rows plus the row above;
+   the tiles of those rows computed elsewhere come over in one ``batch_isend_irecv`` — contiguous
+   slices, mostly from the two neighbouring ranks;
 4. each rank blends + argmaxes its own mosaic rows with the gather-form stitch kernel (K6);
 5. the per-rank class bands are sent to rank 0 (P2P) and concatenated.
 
@@ -69,86 +70,131 @@ class SpatialSegmenter:
         if grid.nty < self.world:
             raise ValueError(f"{grid.nty} tile rows cannot be split over {self.world} ranks")
 
-    def _tiles_for(self, mosaic: torch.Tensor, ty0: int, ty1: int) -> torch.Tensor:
+    # ------------------------------------------------------------ plan (a pure function of grid and world)
+    def _plan(self):
+        """(computed flat tile ranges, stitched tile-row ranges, needed flat tile ranges, mosaic row bands).
+
+        Compute is balanced by TILES (row-major flat index; ranks differ by at most one tile: 4096^2 with
+        512/448 tiles is 81 tiles -> 10-11 per rank on 8 GPUs, where whole tile rows gave 2 to rank 0 and 1
+        to the rest). Stitching stays by tile rows (a rank blends the mosaic rows from its first tile row's
+        origin to the next rank's), so a rank needs the logits of its tile rows plus the row above — flat
+        ranges too, so every logits transfer between two ranks is ONE contiguous slice."""
+        g, world = self.grid, self.world
+        comp = split_tile_rows(g.nty * g.ntx, world)
+        own = split_tile_rows(g.nty, world)
+        need = [(max(0, a - 1) * g.ntx, b * g.ntx) for a, b in own]
+        bands = []
+        for a, b in comp:  # padded-mosaic rows [y0, y1) that rank r's tiles cover
+            bands.append((a // g.ntx * g.stride, (b - 1) // g.ntx * g.stride + g.ts) if b > a else (0, 0))
+        return comp, own, need, bands
+
+    def _tiles_range(self, band: torch.Tensor, y0: int, a: int, b: int) -> torch.Tensor:
+        """Tiles with flat indices [a, b) cut from ``band`` (mosaic rows from padded row ``y0``; zero padding
+        below / right of the mosaic) -> [b - a, ts, ts, c]."""
         g = self.grid
         hp, wp = g.padded_hw()
-        h, w, c = mosaic.shape
-        if (hp, wp) != (h, w):
-            pad = torch.zeros(hp, wp, c, dtype=mosaic.dtype, device=mosaic.device)
-            pad[:h, :w] = mosaic
-            mosaic = pad
-        rows = []
-        for ty in range(ty0, ty1):
-            y = ty * g.stride
-            band = mosaic[y:y + g.ts]                                   # [ts, wp, c]
-            rows.append(band.unfold(1, g.ts, g.stride).permute(1, 0, 3, 2))  # [ntx, ts, ts, c]
-        return torch.stack(rows) if rows else torch.zeros(0, g.ntx, g.ts, g.ts, c, dtype=mosaic.dtype,
-                                                          device=mosaic.device)
+        rows, c = band.shape[0], band.shape[2]
+        need_h = (b - 1) // g.ntx * g.stride + g.ts - y0
+        if rows < need_h or band.shape[1] < wp:
+            pad = torch.zeros(need_h, wp, c, dtype=band.dtype, device=band.device)
+            pad[:rows, :band.shape[1]] = band[:need_h]
+            band = pad
+        out = []
+        for ty in range(a // g.ntx, (b - 1) // g.ntx + 1):
+            t0, t1 = max(a, ty * g.ntx) - ty * g.ntx, min(b, (ty + 1) * g.ntx) - ty * g.ntx
+            y = ty * g.stride - y0
+            row = band[y:y + g.ts, :wp].unfold(1, g.ts, g.stride).permute(1, 0, 3, 2)  # [ntx, ts, ts, c]
+            out.append(row[t0:t1])
+        return torch.cat(out)
 
     def _infer(self, tiles: torch.Tensor) -> torch.Tensor:
-        """tiles [nrows, ntx, ts, ts, c] uint8 -> logits [nrows, ntx, ts, ts, n_out]."""
-        nr, ntx = tiles.shape[:2]
-        flat = tiles.reshape(nr * ntx, *tiles.shape[2:]).contiguous()
+        """tiles [n, ts, ts, c] uint8 -> logits [n, ts, ts, n_out]."""
+        flat = tiles.contiguous()
         outs = [self.model_fn(flat[i:i + self.tile_batch]) for i in range(0, flat.shape[0], self.tile_batch)]
-        return torch.cat(outs).reshape(nr, ntx, *outs[0].shape[1:])[..., : self.n_out]
+        return torch.cat(outs)[..., : self.n_out].contiguous()
 
     def run(self, mosaic: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
         """mosaic [H, W, C] uint8 on rank 0 (ignored elsewhere). Returns the class map on rank 0."""
-        g = self.grid
-        r, world = self.rank, self.world
-        if world > 1:
-            shape = torch.tensor(list(mosaic.shape) if r == 0 else [0, 0, 0], dtype=torch.int64, device=self.device)
-            dist.broadcast(shape, 0, group=self.group)
-            if int(shape[0]) < 0:  # the leader released the group (stop())
-                return None
-            if r != 0:
-                mosaic = torch.empty(*shape.tolist(), dtype=torch.uint8, device=self.device)
-            else:
-                mosaic = mosaic.to(self.device)
-            dist.broadcast(mosaic, 0, group=self.group)
-        else:
-            mosaic = mosaic.to(self.device)
-        return self._segment(mosaic)
+        if self.world == 1:
+            return self._segment(mosaic.to(self.device), 0)
+        shape = torch.tensor(list(mosaic.shape) if self.rank == 0 else [0, 0, 0], dtype=torch.int64,
+                             device=self.device)
+        dist.broadcast(shape, group_src=0, group=self.group)
+        if int(shape[0]) < 0:  # the leader released the group (stop())
+            return None
+        return self._scatter_and_segment(mosaic, tuple(int(v) for v in shape.tolist()))
 
-    def _segment(self, mosaic: torch.Tensor) -> Optional[torch.Tensor]:
+    def _scatter_and_segment(self, mosaic: Optional[torch.Tensor], shape) -> Optional[torch.Tensor]:
+        """Rank 0 sends every rank only the mosaic rows its tiles cover (one P2P message per rank, ~1/world of
+        the mosaic plus one tile overlap, instead of a 64 MiB broadcast to all)."""
+        h, w, c = shape
+        _, _, _, bands = self._plan()
+        if self.rank == 0:
+            mosaic = mosaic.to(self.device)
+            ops = []
+            for s in range(1, self.world):
+                y0, y1 = bands[s]
+                part = mosaic[min(y0, h):min(y1, h)].contiguous()
+                if part.numel():
+                    ops.append(dist.P2POp(dist.isend, part, group=self.group, group_peer=s))
+                    self.bytes_sent += part.numel()
+            for wk in dist.batch_isend_irecv(ops) if ops else []:
+                wk.wait()
+            return self._segment(mosaic[:bands[0][1]], bands[0][0])
+        y0, y1 = bands[self.rank]
+        band = torch.empty(max(0, min(y1, h) - min(y0, h)), w, c, dtype=torch.uint8, device=self.device)
+        if band.numel():
+            for wk in dist.batch_isend_irecv([dist.P2POp(dist.irecv, band, group=self.group, group_peer=0)]):
+                wk.wait()
+            self.bytes_received += band.numel()
+        return self._segment(band, y0)
+
+    def _segment(self, band: torch.Tensor, y0: int) -> Optional[torch.Tensor]:
         g = self.grid
         r, world = self.rank, self.world
-        ranges = split_tile_rows(g.nty, world)
-        ty0, ty1 = ranges[r]
-        row0, row1 = owned_rows(g, ranges, r)
-        tiles = self._tiles_for(mosaic, ty0, ty1)
-        send_req = None
-        # last tile row first, so the halo for rank+1 is on the wire while the rest computes
-        if ty1 > ty0:
-            last = self._infer(tiles[-1:])
-            if r + 1 < world:
-                send_req = dist.isend(last.contiguous(), r + 1, group=self.group)
-                self.bytes_sent += last.numel() * last.element_size()
-            rest = self._infer(tiles[:-1]) if ty1 - ty0 > 1 else last[:0]
-            logits = torch.cat([rest, last])
+        comp, own, need, _ = self._plan()
+        a, b = comp[r]
+        logits = self._infer(self._tiles_range(band, y0, a, b))       # [b - a, ts, ts, n_out]
+        na, nb = need[r]
+        if world == 1:
+            full = logits
         else:
-            logits = torch.zeros(0, g.ntx, g.ts, g.ts, self.n_out, device=self.device, dtype=torch.bfloat16)
-        lt0 = ty0
-        if r > 0:  # halo: previous rank's last tile row
-            halo = torch.empty(1, g.ntx, g.ts, g.ts, self.n_out, dtype=logits.dtype, device=self.device)
-            dist.recv(halo, r - 1, group=self.group)
-            self.bytes_received += halo.numel() * halo.element_size()
-            logits = torch.cat([halo, logits])
-            lt0 = ty0 - 1
-        cls, _ = tile_stitch(logits, g, row0=row0, rows=row1 - row0, ty0=lt0)
-        if send_req is not None:
-            send_req.wait()
+            # halo exchange: each rank sends every other rank the slice of its computed tiles that rank stitches
+            # over (contiguous flat ranges: typically the neighbours' boundary tiles), all in one batch
+            full = torch.empty(nb - na, *logits.shape[1:], dtype=logits.dtype, device=self.device)
+            ops = []
+            for s in range(world):
+                if s == r:
+                    continue
+                lo, hi = max(a, need[s][0]), min(b, need[s][1])
+                if hi > lo:
+                    t = logits[lo - a:hi - a]
+                    ops.append(dist.P2POp(dist.isend, t, group=self.group, group_peer=s))
+                    self.bytes_sent += t.numel() * t.element_size()
+                lo, hi = max(comp[s][0], na), min(comp[s][1], nb)
+                if hi > lo:
+                    ops.append(dist.P2POp(dist.irecv, full[lo - na:hi - na], group=self.group, group_peer=s))
+                    self.bytes_received += (hi - lo) * logits[0].numel() * logits.element_size()
+            lo, hi = max(a, na), min(b, nb)
+            if hi > lo:
+                full[lo - na:hi - na] = logits[lo - a:hi - a]
+            for wk in dist.batch_isend_irecv(ops) if ops else []:
+                wk.wait()
+        ty0, ty1 = own[r]
+        row0, row1 = owned_rows(g, own, r)
+        cls, _ = tile_stitch(full.reshape(-1, g.ntx, *full.shape[1:]), g, row0=row0, rows=row1 - row0,
+                             ty0=na // g.ntx)
         if world == 1:
             return cls
         if r != 0:
-            dist.send(cls.contiguous(), 0, group=self.group)
+            dist.send(cls.contiguous(), group_dst=0, group=self.group)
             self.bytes_sent += cls.numel()
             return None
         bands = [cls]
         for src in range(1, world):
-            a, b = owned_rows(g, ranges, src)
-            buf = torch.empty(b - a, g.width, dtype=torch.uint8, device=self.device)
-            dist.recv(buf, src, group=self.group)
+            lo, hi = owned_rows(g, own, src)
+            buf = torch.empty(hi - lo, g.width, dtype=torch.uint8, device=self.device)
+            dist.recv(buf, group_src=src, group=self.group)
             self.bytes_received += buf.numel()
             bands.append(buf)
         return torch.cat(bands)
@@ -160,18 +206,16 @@ class SpatialSegmenter:
         n = 0
         while True:
             shape = torch.zeros(3, dtype=torch.int64, device=self.device)
-            dist.broadcast(shape, 0, group=self.group)
+            dist.broadcast(shape, group_src=0, group=self.group)
             if int(shape[0]) < 0:
                 return n
             self._run_follower(tuple(int(v) for v in shape.tolist()))
             n += 1
 
     def _run_follower(self, shape) -> None:
-        # same collective sequence as run() on a non-zero rank, after the shape broadcast
-        mosaic = torch.empty(*shape, dtype=torch.uint8, device=self.device)
-        dist.broadcast(mosaic, 0, group=self.group)
-        self._segment(mosaic)
+        # same P2P sequence as run() on a non-zero rank, after the shape broadcast
+        self._scatter_and_segment(None, shape)
 
     def stop(self) -> None:
         if self.world > 1 and self.rank == 0:
-            dist.broadcast(torch.full((3,), -1, dtype=torch.int64, device=self.device), 0, group=self.group)
+            dist.broadcast(torch.full((3,), -1, dtype=torch.int64, device=self.device), group_src=0, group=self.group)

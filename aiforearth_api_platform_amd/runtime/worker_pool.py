@@ -97,6 +97,8 @@ class _WorkerHandle:
         self.proc: Optional[mp.Process] = None
         self.followers: List[mp.Process] = []  # the rest of a worker group
         self.group_devices: List[str] = [device]
+        self.co: List["_WorkerHandle"] = []     # stage graph: the group's other leaders (spawned by this handle)
+        self.owner: Optional["_WorkerHandle"] = None  # stage graph: the handle that spawns this leader's group
         self.restarts = 0
         self.stop = threading.Event()
         self.remote = False
@@ -178,11 +180,19 @@ class WorkerPool:
         if self._monitor is not None:  # already started
             return self
         k = max(1, self.spec.group_size)
+        nl = max(1, self.spec.group_leaders)
         if len(self.devices) % k:
             raise ValueError(f"{len(self.devices)} devices cannot form worker groups of {k}")
+        if nl > 1 and nl >= k:
+            raise ValueError(f"a stage graph of {k} GPUs needs fewer than {k} leaders, got {nl}")
         for i in range(len(self.devices) // k):
-            w = _WorkerHandle(i, self.devices[i * k])
-            w.group_devices = self.devices[i * k:(i + 1) * k]
+            devs = self.devices[i * k:(i + 1) * k]
+            w = _WorkerHandle(i * nl, devs[0])
+            w.group_devices = devs
+            for j in range(1, nl if k > 1 else 1):  # the group's other leaders: own scheduler connections
+                c = _WorkerHandle(i * nl + j, devs[j])
+                c.owner = w
+                w.co.append(c)
             self._spawn(w)
         self._monitor = threading.Thread(target=self._monitor_loop, daemon=True, name="ai4e-pool-monitor")
         self._monitor.start()
@@ -204,28 +214,37 @@ class WorkerPool:
         return False
 
     def _spawn(self, w: _WorkerHandle) -> None:
-        parent, child = self._ctx.Pipe(duplex=True)
+        """Start a worker (or a whole worker group: its leaders, each with a scheduler connection, and its
+        followers, all joined in one process group)."""
         port = _free_port() if self.spec.group_size > 1 else 0
         self._kill_followers(w)
-        w.proc = self._ctx.Process(target=worker_main, args=(child, w.rank, w.device, self.spec, self.ring.name,
-                                                             self.ring.nslots, self.hb_interval),
-                                   kwargs={"group_port": port}, daemon=True, name=f"ai4e-gpu-worker-{w.rank}")
-        w.proc.start()
-        for g, dev in enumerate(w.group_devices[1:], start=1):
+        leaders = [w] + w.co
+        conns = []
+        for gr, h in enumerate(leaders):
+            parent, child = self._ctx.Pipe(duplex=True)
+            h.proc = self._ctx.Process(target=worker_main, args=(child, h.rank, h.device, self.spec, self.ring.name,
+                                                                 self.ring.nslots, self.hb_interval),
+                                       kwargs={"group_port": port, "group_rank": gr}, daemon=True,
+                                       name=f"ai4e-gpu-worker-{h.rank}")
+            h.proc.start()
+            child.close()
+            conns.append(parent)
+        for g, dev in enumerate(w.group_devices[len(leaders):], start=len(leaders)):
             f = self._ctx.Process(target=follower_main, args=(dev, self.spec, g, self.spec.group_size, port),
                                   daemon=True, name=f"ai4e-gpu-worker-{w.rank}.{g}")
             f.start()
             w.followers.append(f)
-        child.close()
-        fd = os.dup(parent.fileno())
-        parent.close()
-        w.stop.clear()
-        w.stats = {}
-        with self._mu:
-            if w not in self.workers:
-                self.workers.append(w)
-        self.sched.attach(w.rank, fd, True)
-        self.events.append((time.time(), "spawn", w.rank))
+        for h, parent in zip(leaders, conns):
+            fd = os.dup(parent.fileno())
+            parent.close()
+            h.stop.clear()
+            h.stats = {}
+            h.spawned_at = time.time()
+            with self._mu:
+                if h not in self.workers:
+                    self.workers.append(h)
+            self.sched.attach(h.rank, fd, True)
+            self.events.append((time.time(), "spawn", h.rank))
 
     @staticmethod
     def _kill_followers(w: _WorkerHandle, grace_s: float = 0.0) -> None:
@@ -256,28 +275,45 @@ class WorkerPool:
         self.events.append((time.time(), "attach-ingest", rank))
 
     def _monitor_loop(self) -> None:
+        suppress: Dict[int, float] = {}  # leaders killed by a group restart: their connection loss is expected
         while not self._stop.is_set():
             failed = self.sched.wait_failed(0.2)
             self.refresh()
+            now = time.time()
+            # a dead follower (no scheduler connection of its own) takes its group down too
+            for w in list(self.workers):
+                if w.owner is None and not w.stop.is_set() and any(f.exitcode is not None for f in w.followers):
+                    failed.append(w.rank)
             for rank in failed:
+                if suppress.get(rank, 0.0) > now:
+                    suppress.pop(rank, None)
+                    continue
                 w = next((x for x in self.workers if x.rank == rank), None)
+                if w is not None and w.owner is not None:
+                    w = w.owner  # a stage-graph group restarts as a whole
                 if w is None or w.stop.is_set():
                     continue
                 self.events.append((time.time(), "worker_failed", rank))
-                if w.proc is not None and w.proc.is_alive():
-                    w.proc.kill()
-                    w.proc.join(10)
+                for h in [w] + w.co:
+                    if h.proc is not None and h.proc.is_alive():
+                        h.proc.kill()
+                        h.proc.join(10)
+                    if h.rank != rank:
+                        suppress[h.rank] = now + 10.0
                 self._kill_followers(w)
                 if not w.remote and w.restarts < self.max_restarts and not self._stop.is_set():
                     w.restarts += 1
                     self.events.append((time.time(), "restart", rank))
                     self._spawn(w)
                 else:
-                    w.stop.set()
+                    for h in [w] + w.co:
+                        h.stop.set()
                     self.events.append((time.time(), "removed", rank))
 
     def resize(self, n: int, devices: Optional[Sequence[str]] = None) -> None:
         """Elastic: grow to / shrink to n active workers (queued tasks are never lost)."""
+        if self.spec.group_leaders > 1:
+            raise NotImplementedError("resize a stage-graph pool by whole groups (restart it with other devices)")
         active = [w for w in self.workers if not w.stop.is_set()]
         if n > len(active):
             devs = list(devices or self.devices)
@@ -294,12 +330,14 @@ class WorkerPool:
         return sum(1 for w in self.workers if not w.stop.is_set())
 
     def _retire(self, w: _WorkerHandle) -> None:
-        w.stop.set()
-        self.sched.detach(w.rank, 30.0)
-        if w.proc is not None:
-            w.proc.join(30)
-            if w.proc.is_alive():
-                w.proc.kill()
+        for h in [w] + w.co:  # (a stage-graph group retires as a whole)
+            h.stop.set()
+            self.sched.detach(h.rank, 30.0)
+        for h in [w] + w.co:
+            if h.proc is not None:
+                h.proc.join(30)
+                if h.proc.is_alive():
+                    h.proc.kill()
         self._kill_followers(w, 30.0)
         self.events.append((time.time(), "retire", w.rank))
 

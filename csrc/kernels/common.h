@@ -95,6 +95,82 @@ __device__ __forceinline__ void unpack_bf16x2(uint32_t v, float& lo, float& hi) 
   hi = __uint_as_float(v & 0xffff0000u);
 }
 
+// ---- element-type traits of the K1 path: bf16 (default) or fp16 (F16 = true) activations and weights.
+// Both feed the same-rate gfx950 MFMA (v_mfma_f32_16x16x32_bf16 / _f16, fp32 accumulate); fp16 keeps 10
+// mantissa bits against bf16's 7 (the detector -> classifier ensemble runs its classifier in fp16).
+typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2_t __attribute__((ext_vector_type(2)));
+
+template <bool F16>
+__device__ __forceinline__ f32x4_t mfma_16x16x32(const bf16x8_t& a, const bf16x8_t& b, const f32x4_t& c) {
+  if constexpr (F16)
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8_t, a), __builtin_bit_cast(f16x8_t, b), c, 0,
+                                                  0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+template <bool F16>
+__device__ __forceinline__ uint32_t pack2(float lo, float hi) {
+  if constexpr (F16) {
+    const f32x2_t v = {lo, hi};
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, f16x2_t));
+  } else {
+    return pack_bf16x2(lo, hi);
+  }
+}
+
+template <bool F16>
+__device__ __forceinline__ void unpack2(uint32_t v, float& lo, float& hi) {
+  if constexpr (F16) {
+    const f16x2_t h = __builtin_bit_cast(f16x2_t, v);
+    lo = static_cast<float>(h[0]);
+    hi = static_cast<float>(h[1]);
+  } else {
+    unpack_bf16x2(v, lo, hi);
+  }
+}
+
+// f16 twins of add_bf16_lo/hi: (a + r.lo / r.hi) through v_dot2_f32_f16 against (1, 0) / (0, 1) (selectors
+// through an opaque s_mov, as for bf16: hipcc would encode 0x3c00 as an inline float constant)
+__device__ __forceinline__ uint32_t f16_sel_lo() {
+  uint32_t v;
+  asm("s_mov_b32 %0, 0x3c00" : "=s"(v));
+  return v;
+}
+__device__ __forceinline__ uint32_t f16_sel_hi() {
+  uint32_t v;
+  asm("s_mov_b32 %0, 0x3c000000" : "=s"(v));
+  return v;
+}
+
+template <bool F16>
+__device__ __forceinline__ uint4 epilogue8(const float (&f)[8], bool has_res, const uint4& r, bool relu) {
+  if constexpr (!F16) {
+    return epilogue8_bf16(f, has_res, r, relu);
+  } else {
+    float g[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) g[k] = f[k];
+    if (has_res) {
+      const uint32_t rr[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        g[2 * q] = __builtin_amdgcn_fdot2(__builtin_bit_cast(f16x2_t, rr[q]), __builtin_bit_cast(f16x2_t, f16_sel_lo()),
+                                          g[2 * q], false);
+        g[2 * q + 1] = __builtin_amdgcn_fdot2(__builtin_bit_cast(f16x2_t, rr[q]),
+                                              __builtin_bit_cast(f16x2_t, f16_sel_hi()), g[2 * q + 1], false);
+      }
+    }
+    uint4 o = make_uint4(pack2<true>(g[0], g[1]), pack2<true>(g[2], g[3]), pack2<true>(g[4], g[5]),
+                         pack2<true>(g[6], g[7]));
+    if (relu) {  // sign bit set -> 0, as for bf16 (v_pk_max_i16)
+      o.x = relu_bf16x2(o.x); o.y = relu_bf16x2(o.y); o.z = relu_bf16x2(o.z); o.w = relu_bf16x2(o.w);
+    }
+    return o;
+  }
+}
+
 // Bijective XCD-aware remap of a linear workgroup id: the dispatcher places workgroup b on XCD
 // (b % 8); give each XCD a contiguous run of logical tiles so neighbouring tiles (which share an
 // operand panel) hit the same private L2 (cdna_hip_programming.md §5.5 T1).

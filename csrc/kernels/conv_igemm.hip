@@ -88,7 +88,7 @@ enum { GATHER_GENERAL = 0,  // any C % 8: a 32-wide K chunk may span taps -> per
 // OCC = workgroups per CU the config is built for (waves per SIMD): 2 for the 4-stage ring (64 KB of
 // LDS), 3 for the 3-stage ring (48 KB) — the register budget (<= 512/OCC VGPRs) must let that many
 // resident, which is what lets a 766-tile layer3 grid run as ONE balanced round on 256 CUs.
-template <int WAVES_M, int WAVES_N, int STAGES, int GATHER, bool EPI_LDS, int OCC = 2>
+template <int WAVES_M, int WAVES_N, int STAGES, int GATHER, bool EPI_LDS, int OCC = 2, bool F16 = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC > 2 ? OCC : 1, OCC))) void conv_igemm_kernel(const ConvParams p) {
   static_assert(WAVES_M * WAVES_N == 4, "4 waves per workgroup");
   static_assert(STAGES >= 3, "fragment prefetch needs >= 3 ring stages");
@@ -271,7 +271,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC > 2 ? O
     K1_READ(FWN, FXN, kt_ + 1)                                                                  \
     _Pragma("unroll") for (int i = 0; i < 4; ++i)                                               \
       _Pragma("unroll") for (int j = 0; j < 4; ++j)                                             \
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(FWC[j], FXC[i], acc[i][j], 0, 0, 0); \
+        acc[i][j] = mfma_16x16x32<F16>(FWC[j], FXC[i], acc[i][j]);                                \
     issue_stage(kt_ + STAGES - 1);                                                              \
   }
 
@@ -367,14 +367,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC > 2 ? O
       const float4 v0 = *reinterpret_cast<const float4*>(tile + rl * BN + 4 * ((2 * cq) ^ (rl & 7)));
       const float4 v1 = *reinterpret_cast<const float4*>(tile + rl * BN + 4 * ((2 * cq + 1) ^ (rl & 7)));
       const float f[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-      const uint4 o = epilogue8_bf16(f, p.res != nullptr, EARLY_RES ? rres16[e] : rlate[e - pass * PC],
+      const uint4 o = epilogue8<F16>(f, p.res != nullptr, EARLY_RES ? rres16[e] : rlate[e - pass * PC],
                                      (p.relu & 1) != 0);
       if (p.gnp && m < p.M && n < p.Kout) {  // GN statistics of the values as stored (bf16)
         const uint32_t ow[4] = {o.x, o.y, o.z, o.w};
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           float a, b;
-          unpack_bf16x2(ow[q], a, b);
+          unpack2<F16>(ow[q], a, b);
           a -= gk[2 * q];
           b -= gk[2 * q + 1];
           gs[2 * q] += a; gq[2 * q] += a * a;
@@ -453,8 +453,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC > 2 ? O
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           float a0, a1, a2, a3;
-          unpack_bf16x2(rres[i][j].x, a0, a1);
-          unpack_bf16x2(rres[i][j].y, a2, a3);
+          unpack2<F16>(rres[i][j].x, a0, a1);
+          unpack2<F16>(rres[i][j].y, a2, a3);
           acc[i][j][0] += a0; acc[i][j][1] += a1; acc[i][j][2] += a2; acc[i][j][3] += a3;
         }
     }
@@ -466,8 +466,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC > 2 ? O
         const int m = pm + 16 * i;
         if (m < p.M && n < p.Kout)
           *reinterpret_cast<uint2*>(p.y + static_cast<long>(m) * p.ldy + p.ycoff + n) =
-              make_uint2(pack_bf16x2(fmaxf(acc[i][j][0], lo), fmaxf(acc[i][j][1], lo)),
-                         pack_bf16x2(fmaxf(acc[i][j][2], lo), fmaxf(acc[i][j][3], lo)));
+              make_uint2(pack2<F16>(fmaxf(acc[i][j][0], lo), fmaxf(acc[i][j][1], lo)),
+                         pack2<F16>(fmaxf(acc[i][j][2], lo), fmaxf(acc[i][j][3], lo)));
       }
     }
   }
@@ -501,7 +501,7 @@ constexpr int U_ROWS = 128, U_BYTES = U_ROWS * 128;
 // {wr*96 + 0..63} (still 128 unit rows), u3 only {wr*96 + 64..95} (64 rows: one DMA per lane, two
 // fragments, 8-MFMA phases 3 and 4). A 14x14 layer of 250 images (M = 49000) is then 256 tiles —
 // one per CU — instead of 192 256-row tiles that leave a quarter of the chip idle.
-template <int GATHER, int BM>
+template <int GATHER, int BM, bool F16 = false>
 __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) {
   static_assert(GATHER == GATHER_TAP || GATHER == GATHER_POINTWISE, "256 tile needs C % 64 == 0");
   static_assert(BM == 256 || BM == 192, "wave groups of 128 or 96 pixels");
@@ -650,7 +650,7 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
       _Pragma("unroll") for (int i = 0; i < ((MQ) ? MF1 : 4); ++i)                                 \
         _Pragma("unroll") for (int j = 0; j < 2; ++j)                                              \
           acc[4 * (MQ) + i][2 * (NQ) + j] =                                                        \
-              __builtin_amdgcn_mfma_f32_16x16x32_bf16(WR[j][s], xr[i][s], acc[4 * (MQ) + i][2 * (NQ) + j], 0, 0, 0); \
+              mfma_16x16x32<F16>(WR[j][s], xr[i][s], acc[4 * (MQ) + i][2 * (NQ) + j]);             \
     __builtin_amdgcn_s_setprio(0);                                                                 \
   }
 // CHECKED = 0: steady state (kt + 2 < nk): every phase stages a unit, 3 phases of DMAs in flight
@@ -749,7 +749,7 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
       const float4 b1 = *reinterpret_cast<const float4*>(p.bias + nb + 4);
       const float f[8] = {v0.x + b0.x, v0.y + b0.y, v0.z + b0.z, v0.w + b0.w,
                           v1.x + b1.x, v1.y + b1.y, v1.z + b1.z, v1.w + b1.w};
-      const uint4 o = epilogue8_bf16(f, p.res != nullptr, rv[e], (p.relu & 1) != 0);
+      const uint4 o = epilogue8<F16>(f, p.res != nullptr, rv[e], (p.relu & 1) != 0);
       if (m < p.M && n < p.Kout) *reinterpret_cast<uint4*>(p.y + static_cast<long>(m) * p.ldy + p.ycoff + n) = o;
     }
     __syncthreads();
@@ -769,7 +769,7 @@ const uint16_t* zero_chunk_ptr() {
   return ptr;
 }
 
-template <int WM, int WN, int STAGES, int OCC = 2>
+template <int WM, int WN, int STAGES, int OCC = 2, bool F16 = false>
 int launch(const ConvParams& p0, hipStream_t s) {
   ConvParams p = p0;
   const int mt = ai4e_cdiv(p.M, WM * 64);
@@ -783,7 +783,7 @@ int launch(const ConvParams& p0, hipStream_t s) {
   // coalesced LDS epilogue needs 16-B aligned output/residual rows
   const bool epi = !(p.ldy % 8 || p.ycoff % 8 || (p.res && p.ldres % 8) || p.Kout < 8);
 #define K1_LAUNCH(G, E) \
-  hipLaunchKernelGGL((conv_igemm_kernel<WM, WN, STAGES, G, E, OCC>), dim3(nb), dim3(256), 0, s, p)
+  hipLaunchKernelGGL((conv_igemm_kernel<WM, WN, STAGES, G, E, OCC, F16>), dim3(nb), dim3(256), 0, s, p)
   if (g == GATHER_POINTWISE) {
     if (epi) K1_LAUNCH(GATHER_POINTWISE, true); else K1_LAUNCH(GATHER_POINTWISE, false);
   } else if (g == GATHER_TAP) {
@@ -795,7 +795,7 @@ int launch(const ConvParams& p0, hipStream_t s) {
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
 }
 
-template <int BM>
+template <int BM, bool F16 = false>
 int launch256(const ConvParams& p0, hipStream_t s) {
   ConvParams p = p0;
   // 256 tile: C % 64 (one tap per 64-wide K tile), 16-B output/residual rows, Kout % 8
@@ -807,9 +807,9 @@ int launch256(const ConvParams& p0, hipStream_t s) {
   p.zero = zero_chunk_ptr();
   if (!p.zero) return AI4E_ELAUNCH;
   if (p.KH == 1 && p.KW == 1 && p.pad == 0)
-    hipLaunchKernelGGL((conv_igemm256_kernel<GATHER_POINTWISE, BM>), dim3(nb), dim3(512), 0, s, p);
+    hipLaunchKernelGGL((conv_igemm256_kernel<GATHER_POINTWISE, BM, F16>), dim3(nb), dim3(512), 0, s, p);
   else
-    hipLaunchKernelGGL((conv_igemm256_kernel<GATHER_TAP, BM>), dim3(nb), dim3(512), 0, s, p);
+    hipLaunchKernelGGL((conv_igemm256_kernel<GATHER_TAP, BM, F16>), dim3(nb), dim3(512), 0, s, p);
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
 }
 
@@ -824,6 +824,7 @@ int launch256(const ConvParams& p0, hipStream_t s) {
 // relu: bit 0 = ReLU; bit 1 = `res` is on the half-resolution grid [N, OH/2, OW/2, ldres] (nearest 2x
 // upsample of the residual, OH and OW even).
 namespace {
+template <bool F16>
 int conv2d_impl(const void* x, const void* w, const void* bias, const void* res, void* y, int N, int H, int W, int C,
                 int ldx, int xcoff, int KH, int KW, int stride, int pad, int OH, int OW, int Kout, int Kpad, int ldy,
                 int ycoff, int ldres, int relu, int tile_cfg, float* gnp, int gn_groups, hipStream_t stream) {
@@ -855,15 +856,15 @@ int conv2d_impl(const void* x, const void* w, const void* bias, const void* res,
     p.gn_groups = gn_groups;
   }
   switch (tile_cfg) {
-    case 1: return launch<2, 2, 4>(p, stream);
-    case 2: return launch<4, 1, 4>(p, stream);
-    case 3: return launch<1, 4, 4>(p, stream);
-    case 4: return launch<2, 2, 5>(p, stream);
-    case 5: return launch<4, 1, 5>(p, stream);
-    case 6: return launch256<256>(p, stream);
-    case 7: return launch<2, 2, 3, 3>(p, stream);
-    case 8: return launch<4, 1, 3, 3>(p, stream);
-    case 9: return launch256<192>(p, stream);
+    case 1: return launch<2, 2, 4, 2, F16>(p, stream);
+    case 2: return launch<4, 1, 4, 2, F16>(p, stream);
+    case 3: return launch<1, 4, 4, 2, F16>(p, stream);
+    case 4: return launch<2, 2, 5, 2, F16>(p, stream);
+    case 5: return launch<4, 1, 5, 2, F16>(p, stream);
+    case 6: return launch256<256, F16>(p, stream);
+    case 7: return launch<2, 2, 3, 3, F16>(p, stream);
+    case 8: return launch<4, 1, 3, 3, F16>(p, stream);
+    case 9: return launch256<192, F16>(p, stream);
     default: return AI4E_EINVAL;
   }
 }
@@ -874,8 +875,17 @@ AI4E_API int ai4e_conv2d_fwd(const void* x, const void* w, const void* bias, con
                              int W, int C, int ldx, int xcoff, int KH, int KW, int stride, int pad, int OH, int OW,
                              int Kout, int Kpad, int ldy, int ycoff, int ldres, int relu, int tile_cfg,
                              hipStream_t stream) {
-  return conv2d_impl(x, w, bias, res, y, N, H, W, C, ldx, xcoff, KH, KW, stride, pad, OH, OW, Kout, Kpad, ldy, ycoff,
-                     ldres, relu, tile_cfg, nullptr, 0, stream);
+  return conv2d_impl<false>(x, w, bias, res, y, N, H, W, C, ldx, xcoff, KH, KW, stride, pad, OH, OW, Kout, Kpad, ldy,
+                            ycoff, ldres, relu, tile_cfg, nullptr, 0, stream);
+}
+
+// The same conv on fp16 activations and weights (f16 MFMA, fp32 accumulate; bias fp32).
+AI4E_API int ai4e_conv2d_f16_fwd(const void* x, const void* w, const void* bias, const void* res, void* y, int N, int H,
+                                 int W, int C, int ldx, int xcoff, int KH, int KW, int stride, int pad, int OH, int OW,
+                                 int Kout, int Kpad, int ldy, int ycoff, int ldres, int relu, int tile_cfg,
+                                 hipStream_t stream) {
+  return conv2d_impl<true>(x, w, bias, res, y, N, H, W, C, ldx, xcoff, KH, KW, stride, pad, OH, OW, Kout, Kpad, ldy,
+                           ycoff, ldres, relu, tile_cfg, nullptr, 0, stream);
 }
 
 // Same conv, plus the GroupNorm statistics of its output (gn_groups groups over Kout channels) written as
@@ -887,8 +897,8 @@ AI4E_API int ai4e_conv2d_gn_fwd(const void* x, const void* w, const void* bias, 
                                 int OW, int Kout, int Kpad, int ldy, int ycoff, int ldres, int relu, int tile_cfg,
                                 void* gn_partials, int gn_groups, hipStream_t stream) {
   if (!gn_partials) return AI4E_EINVAL;
-  return conv2d_impl(x, w, bias, res, y, N, H, W, C, ldx, xcoff, KH, KW, stride, pad, OH, OW, Kout, Kpad, ldy, ycoff,
-                     ldres, relu, tile_cfg, static_cast<float*>(gn_partials), gn_groups, stream);
+  return conv2d_impl<false>(x, w, bias, res, y, N, H, W, C, ldx, xcoff, KH, KW, stride, pad, OH, OW, Kout, Kpad, ldy,
+                            ycoff, ldres, relu, tile_cfg, static_cast<float*>(gn_partials), gn_groups, stream);
 }
 
 // Weight rows must be padded to this multiple (tile height in the channel dimension).

@@ -1,4 +1,4 @@
-// K7 preprocess, max-pool, global-avg-pool — memory-bound NHWC bf16 kernels, 16-B vectors per lane.
+// K7 preprocess, max-pool, global-avg-pool — memory-bound NHWC bf16 (or fp16: F16) kernels, 16-B vectors per lane.
 #include "common.h"
 
 namespace {
@@ -25,7 +25,7 @@ __global__ __launch_bounds__(256) void preprocess_u8_kernel(const uint8_t* __res
 // (zero outside the image = the conv's zero padding of the normalized input).
 // CIN > 0: channel count known at compile time (fully unrolled, the 16 outputs stay in registers) and
 // 32-bit pixel indexing (IDX = int when N*H/2*W/2 < 2^31); CIN = 0: runtime cin, 64-bit indexing.
-template <int CIN, typename IDX>
+template <int CIN, typename IDX, bool F16 = false>
 __global__ __launch_bounds__(256) void preprocess_s2d_kernel(const uint8_t* __restrict__ in, uint16_t* __restrict__ out,
                                                              int N, int H, int W, int cin_rt, float4 mean, float4 istd,
                                                              float scale) {
@@ -56,15 +56,15 @@ __global__ __launch_bounds__(256) void preprocess_s2d_kernel(const uint8_t* __re
       }
     }
     uint4* o = reinterpret_cast<uint4*>(out) + 2 * static_cast<long>(p);
-    o[0] = make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]), pack_bf16x2(v[6], v[7]));
-    o[1] = make_uint4(pack_bf16x2(v[8], v[9]), pack_bf16x2(v[10], v[11]), pack_bf16x2(v[12], v[13]),
-                      pack_bf16x2(v[14], v[15]));
+    o[0] = make_uint4(pack2<F16>(v[0], v[1]), pack2<F16>(v[2], v[3]), pack2<F16>(v[4], v[5]), pack2<F16>(v[6], v[7]));
+    o[1] = make_uint4(pack2<F16>(v[8], v[9]), pack2<F16>(v[10], v[11]), pack2<F16>(v[12], v[13]),
+                      pack2<F16>(v[14], v[15]));
   }
 }
 
 // Max pool NHWC bf16; one lane = 8 channels of one output pixel. Padding ignored (= -inf).
 // IDX = int when the element count fits (32-bit index math: the 64-bit div/mod chain cost more than the loads)
-template <typename IDX>
+template <typename IDX, bool F16 = false>
 __global__ __launch_bounds__(256) void maxpool_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y, int N,
                                                       int H, int W, int C, int OH, int OW, int k, int s, int pad,
                                                       int ldx8) {
@@ -88,18 +88,19 @@ __global__ __launch_bounds__(256) void maxpool_kernel(const uint16_t* __restrict
         if (iw < 0 || iw >= W) continue;
         const uint4 v = reinterpret_cast<const uint4*>(x)[((static_cast<long>(n) * H + ih) * W + iw) * ldx8 + c8];
         float a, b;
-        unpack_bf16x2(v.x, a, b); m[0] = fmaxf(m[0], a); m[1] = fmaxf(m[1], b);
-        unpack_bf16x2(v.y, a, b); m[2] = fmaxf(m[2], a); m[3] = fmaxf(m[3], b);
-        unpack_bf16x2(v.z, a, b); m[4] = fmaxf(m[4], a); m[5] = fmaxf(m[5], b);
-        unpack_bf16x2(v.w, a, b); m[6] = fmaxf(m[6], a); m[7] = fmaxf(m[7], b);
+        unpack2<F16>(v.x, a, b); m[0] = fmaxf(m[0], a); m[1] = fmaxf(m[1], b);
+        unpack2<F16>(v.y, a, b); m[2] = fmaxf(m[2], a); m[3] = fmaxf(m[3], b);
+        unpack2<F16>(v.z, a, b); m[4] = fmaxf(m[4], a); m[5] = fmaxf(m[5], b);
+        unpack2<F16>(v.w, a, b); m[6] = fmaxf(m[6], a); m[7] = fmaxf(m[7], b);
       }
     }
     reinterpret_cast<uint4*>(y)[i] =
-        make_uint4(pack_bf16x2(m[0], m[1]), pack_bf16x2(m[2], m[3]), pack_bf16x2(m[4], m[5]), pack_bf16x2(m[6], m[7]));
+        make_uint4(pack2<F16>(m[0], m[1]), pack2<F16>(m[2], m[3]), pack2<F16>(m[4], m[5]), pack2<F16>(m[6], m[7]));
   }
 }
 
 // Global average pool [N, HW, C] -> [N, C] (bf16 out, fp32 accumulate). One lane = 8 channels.
+template <bool F16 = false>
 __global__ __launch_bounds__(256) void avgpool_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y, int N,
                                                       int HW, int C) {
   const int C8 = C >> 3;
@@ -112,10 +113,10 @@ __global__ __launch_bounds__(256) void avgpool_kernel(const uint16_t* __restrict
     const uint4* p = reinterpret_cast<const uint4*>(x) + n * HW * C8 + c8;
     auto add = [&](const uint4& v) __attribute__((always_inline)) {
       float a, b;
-      unpack_bf16x2(v.x, a, b); acc[0] += a; acc[1] += b;
-      unpack_bf16x2(v.y, a, b); acc[2] += a; acc[3] += b;
-      unpack_bf16x2(v.z, a, b); acc[4] += a; acc[5] += b;
-      unpack_bf16x2(v.w, a, b); acc[6] += a; acc[7] += b;
+      unpack2<F16>(v.x, a, b); acc[0] += a; acc[1] += b;
+      unpack2<F16>(v.y, a, b); acc[2] += a; acc[3] += b;
+      unpack2<F16>(v.z, a, b); acc[4] += a; acc[5] += b;
+      unpack2<F16>(v.w, a, b); acc[6] += a; acc[7] += b;
     };
     int j = 0;
     for (; j + 7 <= HW; j += 7) {  // seven independent 16-B loads in flight (7x7 maps: one batch per row)
@@ -126,8 +127,8 @@ __global__ __launch_bounds__(256) void avgpool_kernel(const uint16_t* __restrict
       for (int u = 0; u < 7; ++u) add(v[u]);
     }
     for (; j < HW; ++j) add(p[static_cast<long>(j) * C8]);
-    reinterpret_cast<uint4*>(y)[i] = make_uint4(pack_bf16x2(acc[0] * inv, acc[1] * inv), pack_bf16x2(acc[2] * inv, acc[3] * inv),
-                                                pack_bf16x2(acc[4] * inv, acc[5] * inv), pack_bf16x2(acc[6] * inv, acc[7] * inv));
+    reinterpret_cast<uint4*>(y)[i] = make_uint4(pack2<F16>(acc[0] * inv, acc[1] * inv), pack2<F16>(acc[2] * inv, acc[3] * inv),
+                                                pack2<F16>(acc[4] * inv, acc[5] * inv), pack2<F16>(acc[6] * inv, acc[7] * inv));
   }
 }
 
@@ -149,9 +150,11 @@ AI4E_API int ai4e_preprocess_u8(const void* in, void* out, long npix, int cin, c
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
 }
 
-// x may be a channel slice of a wider NHWC buffer: row stride ldx (elements), x points at the slice start.
-AI4E_API int ai4e_preprocess_s2d_u8(const void* in, void* out, int N, int H, int W, int cin, const float* mean4,
-                                    const float* std4, float scale, hipStream_t s) {
+namespace {
+
+template <bool F16>
+int preprocess_s2d_impl(const void* in, void* out, int N, int H, int W, int cin, const float* mean4, const float* std4,
+                        float scale, hipStream_t s) {
   if (cin < 1 || cin > 4 || (H & 1) || (W & 1)) return AI4E_EINVAL;
   float4 m = make_float4(mean4[0], mean4[1], mean4[2], mean4[3]);
   float4 is = make_float4(1.f / std4[0], 1.f / std4[1], 1.f / std4[2], 1.f / std4[3]);
@@ -161,31 +164,66 @@ AI4E_API int ai4e_preprocess_s2d_u8(const void* in, void* out, int N, int H, int
   uint16_t* o16 = static_cast<uint16_t*>(out);
   const bool small = total < (1L << 31) - 65536L * 256;
   if (small && cin == 3) {
-    hipLaunchKernelGGL((preprocess_s2d_kernel<3, int>), grid, dim3(256), 0, s, i8, o16, N, H, W, cin, m, is, scale);
+    hipLaunchKernelGGL((preprocess_s2d_kernel<3, int, F16>), grid, dim3(256), 0, s, i8, o16, N, H, W, cin, m, is, scale);
   } else if (small && cin == 4) {
-    hipLaunchKernelGGL((preprocess_s2d_kernel<4, int>), grid, dim3(256), 0, s, i8, o16, N, H, W, cin, m, is, scale);
+    hipLaunchKernelGGL((preprocess_s2d_kernel<4, int, F16>), grid, dim3(256), 0, s, i8, o16, N, H, W, cin, m, is, scale);
   } else {
-    hipLaunchKernelGGL((preprocess_s2d_kernel<0, long>), grid, dim3(256), 0, s, i8, o16, N, H, W, cin, m, is, scale);
+    hipLaunchKernelGGL((preprocess_s2d_kernel<0, long, F16>), grid, dim3(256), 0, s, i8, o16, N, H, W, cin, m, is, scale);
   }
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
 }
 
-AI4E_API int ai4e_maxpool2d(const void* x, void* y, int N, int H, int W, int C, int OH, int OW, int k, int stride,
-                            int pad, int ldx, hipStream_t s) {
+template <bool F16>
+int maxpool_impl(const void* x, void* y, int N, int H, int W, int C, int OH, int OW, int k, int stride, int pad, int ldx,
+                 hipStream_t s) {
   if (C % 8 || ldx % 8 || ldx < C) return AI4E_EINVAL;
   const long total = static_cast<long>(N) * OH * OW * (C / 8);
   if (total < (1L << 31) - 8192L * 256)
-    hipLaunchKernelGGL(maxpool_kernel<int>, dim3(grid_for(total)), dim3(256), 0, s, static_cast<const uint16_t*>(x),
-                       static_cast<uint16_t*>(y), N, H, W, C, OH, OW, k, stride, pad, ldx / 8);
+    hipLaunchKernelGGL((maxpool_kernel<int, F16>), dim3(grid_for(total)), dim3(256), 0, s,
+                       static_cast<const uint16_t*>(x), static_cast<uint16_t*>(y), N, H, W, C, OH, OW, k, stride, pad,
+                       ldx / 8);
   else
-    hipLaunchKernelGGL(maxpool_kernel<long>, dim3(grid_for(total)), dim3(256), 0, s, static_cast<const uint16_t*>(x),
-                       static_cast<uint16_t*>(y), N, H, W, C, OH, OW, k, stride, pad, ldx / 8);
+    hipLaunchKernelGGL((maxpool_kernel<long, F16>), dim3(grid_for(total)), dim3(256), 0, s,
+                       static_cast<const uint16_t*>(x), static_cast<uint16_t*>(y), N, H, W, C, OH, OW, k, stride, pad,
+                       ldx / 8);
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
 }
 
-AI4E_API int ai4e_global_avgpool(const void* x, void* y, int N, int HW, int C, hipStream_t s) {
+template <bool F16>
+int avgpool_impl(const void* x, void* y, int N, int HW, int C, hipStream_t s) {
   if (C % 8) return AI4E_EINVAL;
-  hipLaunchKernelGGL(avgpool_kernel, dim3(grid_for(static_cast<long>(N) * (C / 8))), dim3(256), 0, s,
+  hipLaunchKernelGGL((avgpool_kernel<F16>), dim3(grid_for(static_cast<long>(N) * (C / 8))), dim3(256), 0, s,
                      static_cast<const uint16_t*>(x), static_cast<uint16_t*>(y), N, HW, C);
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
+}
+
+}  // namespace
+
+// uint8 [N,H,W,cin<=4] -> s2d [N,H/2,W/2,16] bf16 (f16 != 0: fp16).
+AI4E_API int ai4e_preprocess_s2d_u8(const void* in, void* out, int N, int H, int W, int cin, const float* mean4,
+                                    const float* std4, float scale, hipStream_t s) {
+  return preprocess_s2d_impl<false>(in, out, N, H, W, cin, mean4, std4, scale, s);
+}
+AI4E_API int ai4e_preprocess_s2d_u8_dt(const void* in, void* out, int N, int H, int W, int cin, const float* mean4,
+                                       const float* std4, float scale, int f16, hipStream_t s) {
+  return f16 ? preprocess_s2d_impl<true>(in, out, N, H, W, cin, mean4, std4, scale, s)
+             : preprocess_s2d_impl<false>(in, out, N, H, W, cin, mean4, std4, scale, s);
+}
+
+// x may be a channel slice of a wider NHWC buffer: row stride ldx (elements), x points at the slice start.
+AI4E_API int ai4e_maxpool2d(const void* x, void* y, int N, int H, int W, int C, int OH, int OW, int k, int stride,
+                            int pad, int ldx, hipStream_t s) {
+  return maxpool_impl<false>(x, y, N, H, W, C, OH, OW, k, stride, pad, ldx, s);
+}
+AI4E_API int ai4e_maxpool2d_dt(const void* x, void* y, int N, int H, int W, int C, int OH, int OW, int k, int stride,
+                               int pad, int ldx, int f16, hipStream_t s) {
+  return f16 ? maxpool_impl<true>(x, y, N, H, W, C, OH, OW, k, stride, pad, ldx, s)
+             : maxpool_impl<false>(x, y, N, H, W, C, OH, OW, k, stride, pad, ldx, s);
+}
+
+AI4E_API int ai4e_global_avgpool(const void* x, void* y, int N, int HW, int C, hipStream_t s) {
+  return avgpool_impl<false>(x, y, N, HW, C, s);
+}
+AI4E_API int ai4e_global_avgpool_dt(const void* x, void* y, int N, int HW, int C, int f16, hipStream_t s) {
+  return f16 ? avgpool_impl<true>(x, y, N, HW, C, s) : avgpool_impl<false>(x, y, N, HW, C, s);
 }

@@ -17,7 +17,7 @@ from aiforearth_api_platform_amd.runtime.worker_pool import ModelSpec, WorkerPoo
 pytestmark = pytest.mark.gpu
 PATH = "/v1/ai4e/resnet50/classify"
 EP = "http://127.0.0.1" + PATH
-SPEC = ModelSpec("aiforearth_api_platform_amd.models.toy:resnet50_fused", (224, 224, 3), 32, 5, {}, True, (8,))
+SPEC = ModelSpec("aiforearth_api_platform_amd.models.zoo:resnet50_classifier", (224, 224, 3), 32, 5, {}, True, (8,))
 
 
 def _wait(cond, t=180):
@@ -92,6 +92,50 @@ def test_ensemble_pair_over_rccl_matches_single_gpu():
     outs = local(torch.from_numpy(imgs).cuda())
     for i in range(4):
         assert [a["species"] for a in got[i]["animals"]] == outs[2][i][: int(outs[4][i, 0])].tolist()
+
+
+@pytest.mark.skipif(torch.cuda.device_count() < 2, reason="needs two GPUs (RCCL stage graph)")
+@pytest.mark.parametrize("dtype", ["bf16", "fp16"])
+def test_ensemble_stage_graph_over_rccl_matches_single_gpu(dtype):
+    """Config 5 as an N:M stage graph through the pool (here 1 detector : 1 classifier on two GPUs; 7:1 on a
+    node): both stages in HIP graphs, crops over RCCL P2P, the classifier in bf16 or fp16."""
+    from aiforearth_api_platform_amd.models import zoo
+    kw = dict(max_crops=4, score_thresh=0.0, class_id=None, num_species=20, box_score_thresh=0.0,
+              classifier_dtype=dtype)
+    imgs = np.random.default_rng(3).integers(0, 256, (6, 256, 256, 3), dtype=np.uint8)
+    spec = ModelSpec("aiforearth_api_platform_amd.models.zoo:camera_trap_ensemble_group", (256, 256, 3), 4, 5, kw,
+                     False, (), ("http://127.0.0.1/v1/sg/classify",), 2, 1)
+    cp = ControlPlane(Config.load(env={}))
+    pool = WorkerPool(cp, "http://127.0.0.1/v1/sg/detect", spec, ["cuda:0", "cuda:1"],
+                      heartbeat_interval_s=0.2).start(wait_ready_s=600)
+    try:
+        ids = pool.submit_many(imgs)
+        assert _wait(lambda: cp.store.zcard("/v1/sg/classify_completed") == 6)
+        got = [pool.result(t) for t in ids]
+    finally:
+        pool.stop()
+        cp.close()
+    from aiforearth_api_platform_amd.models.faster_rcnn import DetectorConfig, FasterRCNN
+    from aiforearth_api_platform_amd.runtime.pipeline import PipelineConfig, StageGraphPipeline
+    det = FasterRCNN(DetectorConfig(box_score_thresh=0.0), seed=0, device="cuda:0")
+    cfg = PipelineConfig(score_thresh=0.0, class_id=None, max_crops_per_image=4)
+    local = StageGraphPipeline(det.forward_u8, zoo.crop_classifier("cuda:0", 20, 1, dtype), torch.device("cuda:0"),
+                               cfg)
+    n_same = n_all = 0
+    for i0 in range(0, 6, 4):
+        boxes, scores, valid, res = local.run_batches([torch.from_numpy(imgs[i0:i0 + 4]).cuda()])[0]
+        k = 0
+        for b in range(valid.shape[0]):
+            want = []
+            for j in range(valid.shape[1]):
+                if valid[b, j]:
+                    want.append(int(res[k, 0]))
+                    k += 1
+            have = [a["species"] for a in got[i0 + b]["animals"]]
+            n_all += len(want)
+            n_same += sum(int(x == y) for x, y in zip(have, want))
+            assert len(have) == len(want)
+    assert n_same >= 0.95 * n_all  # batch composition differs (4 vs 2 images): rare argmax ties may flip
 
 
 @pytest.mark.skipif(torch.cuda.device_count() < 2, reason="needs two GPUs (RCCL halo exchange)")

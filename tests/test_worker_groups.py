@@ -7,6 +7,8 @@
 """
 import time
 
+import pytest
+
 import numpy as np
 import torch
 
@@ -89,3 +91,36 @@ def test_ensemble_pair_recovers_from_failed_xgmi_handoff(monkeypatch):
                      False, (), ("http://127.0.0.1/v1/group/classify",), 2)
     got, stats = _serve(spec, ["cpu", "cpu"], imgs, "/v1/group/classify")
     assert all(g is not None and "animals" in g for g in got)
+
+
+def test_stage_graph_3_to_1_matches_single_process():
+    """Config 5 as an N:M stage graph: 3 detector leaders (each its own scheduler connection and batches) feed
+    1 classifier process over P2P; every task equals the single-process ensemble."""
+    from aiforearth_api_platform_amd.models import zoo
+    from aiforearth_api_platform_amd.runtime.servable import decode_row, encode_rows
+
+    imgs = np.random.default_rng(11).integers(0, 256, (9, 128, 128, 3), dtype=np.uint8)
+    spec = ModelSpec("aiforearth_api_platform_amd.models.zoo:camera_trap_ensemble_group", (128, 128, 3), 2, 5, ENS,
+                     False, (), ("http://127.0.0.1/v1/group/classify",), 4, 3)
+    got, stats = _serve(spec, ["cpu"] * 4, imgs, "/v1/group/classify")
+    assert len(stats["workers"]) == 3 and sum(w["images"] for w in stats["workers"]) == 9
+    local = zoo.camera_trap_ensemble("cpu", **ENS)
+    outs = [o.numpy() for o in local(torch.from_numpy(imgs))]
+    rb = sum(f.nbytes for f in local.outputs)
+    rows = encode_rows(outs, 9)
+    for i in range(9):
+        ref = local.format(decode_row(rows[i * rb:(i + 1) * rb], local.outputs))
+        assert [a["species"] for a in got[i]["animals"]] == [a["species"] for a in ref["animals"]]
+        assert [a["bbox"] for a in got[i]["animals"]] == [a["bbox"] for a in ref["animals"]]
+        assert [a["species_probability"] for a in got[i]["animals"]] == pytest.approx(
+            [a["species_probability"] for a in ref["animals"]], abs=1e-4)
+    assert sum(w["xgmi_tx_bytes"] for w in stats["workers"]) > 0
+
+
+def test_stage_assignment():
+    from aiforearth_api_platform_amd.runtime.pipeline import stage_assignment
+
+    assert stage_assignment(7, 8) == [[0, 1, 2, 3, 4, 5, 6]]
+    assert stage_assignment(6, 8) == [[0, 2, 4], [1, 3, 5]]
+    with pytest.raises(ValueError):
+        stage_assignment(4, 4)
