@@ -125,6 +125,15 @@ class FusedUNet:
         self.out_channels = kout
         self.fused_pool = os.environ.get("AI4E_UNET_FUSED_POOL", "1") != "0"
 
+    def tensors(self) -> List[torch.Tensor]:
+        """Every weight tensor (packed convs + GroupNorm affine), for ``parallel.dist.broadcast_tensors``."""
+        out = []
+        for dc in [self.inc] + self.down + self.up:
+            for pc in (dc.c1, dc.c2):
+                out += [pc.w_packed, pc.bias, pc.w_ref]
+            out += [dc.g1[0], dc.g1[1], dc.g2[0], dc.g2[1]]
+        return out + [self.outc.w_packed, self.outc.bias, self.outc.w_ref, self.outc.b_ref]
+
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         """x: normalized NHWC [N,H,W,8] (H, W multiples of 16) -> logits NHWC [N,H,W,kout]."""
         n, h, w, _ = x.shape

@@ -264,13 +264,19 @@ class _SpatialSegmenterServable(SegmenterServable):
 
 def landcover_spatial(device="cuda", group=None, role: str = "leader", height: int = 4096, width: int = 4096,
                       tile: int = 512, stride: int = 448, tile_batch: int = 16, n_classes: int = 7, seed: int = 0):
-    """Worker group of k GPUs segmenting ONE mosaic together (tile rows split over the group, halo rows
-    over RCCL P2P, bands gathered on the leader) — BASELINE config #4 (spatial parallel) as an API."""
+    """Worker group of k GPUs segmenting ONE mosaic together (tiles split evenly over the group, mosaic bands
+    scattered from the leader, halo logits over RCCL P2P, class bands gathered on the leader) — BASELINE
+    config #4 (spatial parallel) as an API."""
     from ..ops.stitch import TileGrid
     from ..runtime.spatial import SpatialSegmenter
     from .unet import FusedUNet, unet_landcover
 
+    from ..parallel.dist import broadcast_tensors
+
     f = FusedUNet(unet_landcover(n_classes=n_classes, seed=seed), device=device)
+    # weights are the leader's: loaded once there, replicated over the group's links in one bucketed
+    # broadcast per dtype (survey C1) instead of every GPU loading its own copy
+    broadcast_tensors(f.tensors(), src=0, group=group)
     seg = SpatialSegmenter(f.forward_u8, TileGrid(height, width, tile, stride), f.n_classes, torch.device(device),
                            tile_batch=tile_batch, group=group)
     if role == "leader":

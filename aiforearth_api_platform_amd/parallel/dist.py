@@ -125,7 +125,7 @@ def wait_all(works: list) -> None:
 
 def broadcast_tensors(tensors: Sequence[torch.Tensor], src: int = 0, group=None,
                       bucket_bytes: int = 256 << 20) -> None:
-    """Replicate ``tensors`` from rank ``src`` to every rank in place (survey C1: weights loaded once, then
+    """Replicate ``tensors`` from group rank ``src`` to every rank in place (survey C1: weights loaded once, then
     broadcast over xGMI). Tensors of one dtype are packed into flat buckets of up to ``bucket_bytes`` so a
     ResNet-50 (51 MB bf16) is ONE collective instead of ~160 small ones; every rank must pass tensors of the
     same shapes and order. No-op without an initialized process group."""
@@ -143,7 +143,7 @@ def broadcast_tensors(tensors: Sequence[torch.Tensor], src: int = 0, group=None,
                 size += t.numel() * t.element_size()
                 continue
             flat = torch.cat([b.reshape(-1) for b in bucket])
-            dist.broadcast(flat, src, group=group)
+            dist.broadcast(flat, group_src=src, group=group)
             off = 0
             for b in bucket:
                 b.copy_(flat[off:off + b.numel()].view_as(b))

@@ -135,7 +135,8 @@ def http_phase(cp, pool, seconds: float, batch: int, item_shape, path: str, fron
 
 
 def run_node_bench(args, spec, path: str, metric: str, unit: str = "images/s", config: Optional[dict] = None,
-                   flops_per_item: Optional[float] = None, baseline: Optional[float] = None) -> Optional[dict]:
+                   flops_per_item: Optional[float] = None, baseline: Optional[float] = None,
+                   dtype: str = "bf16") -> Optional[dict]:
     """Warm up, time exactly ``args.steps`` steps, return rank 0's JSON record (None elsewhere).
 
     ``args`` needs: steps, warmup, batch, inflight, device, http, http_seconds, json_out."""
@@ -152,6 +153,11 @@ def run_node_bench(args, spec, path: str, metric: str, unit: str = "images/s", c
     _, world, _ = env_ranks()
     if world > 1 and args.gpus != world:
         raise SystemExit(f"--gpus {args.gpus} != WORLD_SIZE {world}")
+    # worker-group forms (spec.group_size > 1: spatial segmentation, the N:M stage graph) run from ONE process:
+    # the pool spawns the group's processes, one per GPU, joined over RCCL
+    group = spec.group_size
+    if group > 1 and world > 1:
+        raise SystemExit("worker-group benches run in one process (the pool spawns one process per group GPU)")
     # rank 0 builds the in-tree HIP/C++ libraries, then everyone joins (RCCL on GPU, gloo on CPU)
     denv = init_from_env(args.device, build=_build.build_all)
     rank, device = denv.rank, denv.device
@@ -164,7 +170,11 @@ def run_node_bench(args, spec, path: str, metric: str, unit: str = "images/s", c
         cfg = Config.load(env={}, max_batch=B, max_batch_delay_ms=0.0)
         cp = ControlPlane(cfg)
         remote = [(part * r, part, r) for r in range(1, world)]
-        pool = WorkerPool(cp, endpoint, spec, [f"{args.device}:{denv.local_rank}" if args.device == "cuda" else "cpu"],
+        if group > 1:
+            devices = [f"cuda:{i}" for i in range(group)] if args.device == "cuda" else ["cpu"] * group
+        else:
+            devices = [f"{args.device}:{denv.local_rank}" if args.device == "cuda" else "cpu"]
+        pool = WorkerPool(cp, endpoint, spec, devices,
                           ring_slots=part, max_delay_s=0.0005, heartbeat_interval_s=hb, heartbeat_timeout_s=120.0,
                           remote_partitions=remote, pipeline_depth=int(os.environ.get("AI4E_PIPELINE_DEPTH", "3")),
                           poll_s=0.005, frontends=getattr(args, "http_frontends", 0) if args.http else 0,
@@ -296,17 +306,18 @@ def run_node_bench(args, spec, path: str, metric: str, unit: str = "images/s", c
                                           "power_w")}
                    for w in stats.get("workers", [])]
         out = {
-            "metric": metric, "value": round(value, 2), "unit": unit, "n_gpus": world, "steps": args.steps,
+            "metric": metric, "value": round(value, 2), "unit": unit, "n_gpus": world * group, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None if baseline is None else round(value / baseline, 4),
-            "dtype": "bf16", "data": "synthetic uint8 payloads (written into the payload ring per submission), "
+            "dtype": dtype, "data": "synthetic uint8 payloads (written into the payload ring per submission), "
                                      "random-init weights",
             "p50_task_latency_ms": round(p50, 3), "p99_task_latency_ms": round(p99, 3),
             "window": {"kind": "steady-state, by completion count on the scheduler",
                        "first_counted_image": args.warmup * B * world, "counted_images": images,
                        "warmup_ramp_ms": round(ramp_s * 1e3, 3), "tail_drain_ms": round(drain_s * 1e3, 3),
                        "tail_steps_uncounted": tail},
-            "config": dict(config or {}, global_batch=B * world, per_gpu_batch=B, parallelism=f"dp{world}",
+            "config": dict(config or {}, global_batch=B * world, per_gpu_batch=B,
+                           parallelism=(config or {}).get("parallelism", f"dp{world}"),
                            serving_path="node scheduler (native) + 1 GPU worker process per GPU",
                            ingest_shards=world, ring_slots_per_shard=part, hip_graphs=spec.use_graphs),
             "workers": workers, "batch_histogram": stats.get("batch_histogram"), "http": http,

@@ -7,6 +7,13 @@ one GPU worker process per GPU, per-submission payload writes, torchrun for N > 
   (mosaics/s + p50; the spatial-parallel single-mosaic form is bench/landcover_bench.py);
 * ``--model ensemble``  — config 5 as an API: detector -> species classifier under one TaskId (the
   AddPipelineTask hop), both stages in one HIP graph per GPU; images/s + p50.
+* ``--model ensemble_group --group 8 --classifiers 1`` — config 5 as an N:M stage graph over RCCL: N = group -
+  classifiers detector GPUs take batches from the scheduler, the classifier GPU(s) classify their crops
+  (``--classifier-dtype fp16`` by default, ``--wire uint8``); ``parallelism: pipeline{N}:{M}``.
+* ``--model landcover_spatial --group k`` — config 4 in its spatial form: each 4096^2 mosaic segmented by k GPUs
+  together (tiles split evenly, bands scattered, halo logits over P2P); ``parallelism: spatial{k}``.
+
+Worker-group models run from ONE process (the pool spawns one worker process per group GPU); no torchrun.
 
     python bench/api_bench.py --model detector [--batch 32 --size 640 --steps 20]
     torchrun --nproc-per-node 8 bench/api_bench.py --model detector --gpus 8
@@ -26,6 +33,11 @@ MODELS = {
                   lambda s: (s, s, 4), "mosaics/s", "land-cover API mosaics/sec (whole node) + p50"),
     "ensemble": ("aiforearth_api_platform_amd.models.zoo:camera_trap_ensemble", "/v1/camera-trap/ensemble/detect", 32,
                  lambda s: (s, s, 3), "images/s", "detector->classifier ensemble API images/sec (whole node) + p50"),
+    "ensemble_group": ("aiforearth_api_platform_amd.models.zoo:camera_trap_ensemble_group",
+                       "/v1/camera-trap/ensemble-group/detect", 32, lambda s: (s, s, 3), "images/s",
+                       "detector->classifier ensemble API images/sec (N:M stage graph over RCCL) + p50"),
+    "landcover_spatial": ("aiforearth_api_platform_amd.models.zoo:landcover_spatial", "/v1/landcover/spatial", 1,
+                          lambda s: (s, s, 4), "mosaics/s", "land-cover API mosaics/sec (spatial over k GPUs) + p50"),
 }
 
 
@@ -43,24 +55,43 @@ def main():
     ap.add_argument("--http", type=int, default=0)
     ap.add_argument("--http-seconds", type=float, default=6.0)
     ap.add_argument("--json-out", default="")
+    ap.add_argument("--group", type=int, default=2, help="GPUs per worker group (ensemble_group, landcover_spatial)")
+    ap.add_argument("--classifiers", type=int, default=1, help="classifier GPUs of an ensemble_group")
+    ap.add_argument("--classifier-dtype", default="fp16", choices=["bf16", "fp16"])
+    ap.add_argument("--wire", default="uint8", choices=["uint8", "float16"])
+    ap.add_argument("--tile", type=int, default=512)
+    ap.add_argument("--stride", type=int, default=448)
     a = ap.parse_args()
     from aiforearth_api_platform_amd.runtime.node_bench import run_node_bench
     from aiforearth_api_platform_amd.runtime.worker_pool import ModelSpec
 
     factory, path, batch, shape, unit, metric = MODELS[a.model]
     a.batch = a.batch or batch
-    size = a.size or (4096 if a.model == "landcover" else 640)
-    kwargs, graphs, stages = {}, not a.no_graphs, ()
-    if a.model == "landcover":
-        kwargs = {"height": size, "width": size, "tile": 512, "stride": 448, "tile_batch": 16}
+    size = a.size or (4096 if a.model.startswith("landcover") else 640)
+    kwargs, graphs, stages, group, leaders = {}, not a.no_graphs, (), 1, 1
+    extra, dtype = {}, "bf16"
+    if a.model.startswith("landcover"):
+        kwargs = {"height": size, "width": size, "tile": a.tile, "stride": a.stride, "tile_batch": 16}
         graphs = False
-    if a.model == "ensemble":
+    if a.model == "landcover_spatial":
+        group = a.group
+        extra["parallelism"] = f"spatial{group}"
+    if a.model.startswith("ensemble"):
         kwargs = {"max_crops": 4, "score_thresh": 0.0, "class_id": None}  # random weights: keep crops flowing
-        stages = ("http://127.0.0.1/v1/camera-trap/ensemble/classify",)
-    spec = ModelSpec(factory, shape(size), a.batch, 5, kwargs, graphs, (), stages)
-    run_node_bench(a, spec, path, metric, unit,
-                   config={"model": a.model, "image_size": size, "api": "async", **{k: v for k, v in kwargs.items()
-                                                                                      if k != "score_thresh"}})
+        stages = ("http://127.0.0.1" + path.replace("/detect", "/classify"),)
+    if a.model == "ensemble_group":
+        if not 1 <= a.classifiers < a.group:
+            raise SystemExit("--classifiers must leave at least one detector GPU in --group")
+        group, leaders = a.group, a.group - a.classifiers
+        kwargs.update(classifier_dtype=a.classifier_dtype, wire_dtype=a.wire)
+        graphs = False  # each stage captures its own HIP graphs (runtime/pipeline.py StageGraphPipeline)
+        extra.update(parallelism=f"pipeline{leaders}:{a.classifiers}", wire_dtype=a.wire,
+                     stage_dtypes={"detector": "bf16", "classifier": a.classifier_dtype})
+        dtype = a.classifier_dtype if a.classifier_dtype == "bf16" else "bf16 detector / fp16 classifier"
+    spec = ModelSpec(factory, shape(size), a.batch, 5, kwargs, graphs, (), stages, group, leaders)
+    run_node_bench(a, spec, path, metric, unit, dtype=dtype,
+                   config={"model": a.model, "image_size": size, "api": "async", **extra,
+                           **{k: v for k, v in kwargs.items() if k != "score_thresh"}})
 
 
 if __name__ == "__main__":

@@ -69,3 +69,21 @@ def test_bench_torchrun_ranks_gloo(world):
     assert w["counted_images"] == 2 * world * 2 and w["first_counted_image"] == 2 * world
     assert len(lines[0]["workers"]) == world
     assert sum(x["images"] for x in lines[0]["workers"]) == 2 * world * (3 + w["tail_steps_uncounted"])
+
+
+@pytest.mark.parametrize("model,extra,par", [
+    ("landcover_spatial", ["--group", "3", "--size", "128", "--tile", "32", "--stride", "24"], "spatial3"),
+    ("ensemble_group", ["--group", "3", "--classifiers", "1", "--size", "64", "--batch", "2"], "pipeline2:1"),
+])
+def test_api_bench_worker_group_forms_cpu(model, extra, par):
+    """bench/api_bench.py runs configs 4 and 5 in their multi-GPU forms through the task path (one process; the
+    pool spawns the group, gloo on CPU here, RCCL on the node) and labels the parallelism."""
+    cmd = [sys.executable, "bench/api_bench.py", "--model", model, "--device", "cpu", "--steps", "2", "--warmup", "1",
+           "--inflight", "1"] + extra
+    r = subprocess.run(cmd, cwd=ROOT, env=dict(_env(), OMP_NUM_THREADS="1"), capture_output=True, text=True,
+                       timeout=900)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _json_lines(r.stdout)[-1]
+    assert d["config"]["parallelism"] == par and d["n_gpus"] == 3 and d["value"] > 0
+    if model == "ensemble_group":
+        assert d["config"]["wire_dtype"] == "uint8" and d["config"]["stage_dtypes"]["classifier"] == "fp16"
