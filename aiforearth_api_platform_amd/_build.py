@@ -7,6 +7,8 @@ the GPU box (see README "Build"):
 * ``_lib/libai4e_kernels.so`` — hand-written CDNA4 kernels (``csrc/kernels/*.hip``) built
   with ``hipcc --offload-arch=gfx950`` and exposed through a plain C ABI consumed via ctypes
   (no torch headers in the kernel TU => seconds per file, no JIT cache under ~/.cache).
+* ``_lib/ai4e_ingestd`` / ``_lib/ai4e_http_load`` — the native ingest front-end and the REST load
+  generator (``csrc/ingest/*.cpp``), g++ -O2.
 
 Rebuilds are incremental on source mtime.  ``python -m aiforearth_api_platform_amd._build``.
 """
@@ -101,11 +103,26 @@ def build_kernels(verbose: bool = False, force: bool = False, jobs: int = 8) -> 
     return KERNEL_SO
 
 
+INGESTD = LIBDIR / "ai4e_ingestd"
+HTTP_LOAD = LIBDIR / "ai4e_http_load"
+
+
+def build_tools(verbose: bool = False, force: bool = False) -> None:
+    """The native executables of the ingest path (``csrc/ingest``)."""
+    LIBDIR.mkdir(parents=True, exist_ok=True)
+    cxx = os.environ.get("CXX", "g++")
+    headers = sorted((CSRC / "core").glob("*.h"))
+    for src, out in ((CSRC / "ingest" / "ingestd.cpp", INGESTD), (CSRC / "ingest" / "http_load.cpp", HTTP_LOAD)):
+        if force or _stale(out, [src, *headers]):
+            _run([cxx, "-O2", "-std=c++17", "-Wall", "-pthread", str(src), "-o", str(out), "-lrt"], verbose)
+
+
 def build_all(verbose: bool = False, force: bool = False) -> None:
     build_core(verbose=verbose, force=force)
     build_kernels(verbose=verbose, force=force)
+    build_tools(verbose=verbose, force=force)
 
 
 if __name__ == "__main__":
     build_all(verbose=True, force="--force" in sys.argv)
-    print("built:", CORE_SO, KERNEL_SO)
+    print("built:", CORE_SO, KERNEL_SO, INGESTD, HTTP_LOAD)

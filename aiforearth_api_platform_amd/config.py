@@ -72,6 +72,9 @@ class Config:
     # (runtime/frontend.py); each gets `frontend_ring_slots` payload slots per GPU endpoint (0 = 4 batches)
     frontend_processes: int = field(default=0, metadata={"env": "AI4E_FRONTEND_PROCESSES"})
     frontend_ring_slots: int = field(default=0, metadata={"env": "AI4E_FRONTEND_RING_SLOTS"})
+    # "native": the C++ front-end (csrc/ingest/ingestd.cpp: bodies recv()'d straight into ring slots);
+    # "python": runtime/frontend.py (aiohttp). TLS listeners always use the Python front-ends.
+    frontend_impl: str = field(default="native", metadata={"env": "AI4E_FRONTEND_IMPL"})
     # --- metrics timers (TaskQueueLogger.cs:20 / TaskProcessLogger.cs:22) ---
     queue_logger_period_s: float = field(default=30.0, metadata={"env": "AI4E_QUEUE_LOGGER_PERIOD_S"})
     process_logger_period_s: float = field(default=300.0, metadata={"env": "AI4E_PROCESS_LOGGER_PERIOD_S"})

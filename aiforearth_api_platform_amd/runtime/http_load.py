@@ -1,9 +1,10 @@
 """HTTP load generator processes for the REST benchmarks (no torch import).
 
-The clients run in their own spawned processes so the server under test does not share an
-interpreter (and a GIL) with its load: ``run_clients`` starts ``procs`` processes, each driving
-``conc`` keep-alive connections for ``seconds``, and returns every TaskId the server handed out
-plus the wall-clock window the requests covered.
+The clients run in their own processes so the server under test does not share an interpreter (and a GIL)
+with its load. ``run_native_clients`` (the default of the benchmarks) starts ``procs`` processes of the C++
+generator ``_lib/ai4e_http_load`` (csrc/ingest/http_load.cpp: one thread per keep-alive connection, one
+writev per request), which report their own CPU time; ``run_clients`` is the aiohttp form. Both return every
+TaskId the server handed out plus the wall-clock window the requests covered.
 """
 from __future__ import annotations
 
@@ -77,3 +78,48 @@ def run_clients(url: str, seconds: float, conc: int, body: bytes, content_type: 
     for p in ps:
         p.join(30)
     return ids, t0, t1, errors
+
+
+def run_native_clients(url: str, seconds: float, conc: int, body: bytes, content_type: str, procs: int = 2,
+                       headers=()) -> dict:
+    """``procs`` C++ load processes x ``conc`` connections each. Returns {ids, t0, t1, errors, requests,
+    bytes_sent, client_cpu_s (user + system, all client processes), client_processes, connections}."""
+    import json
+    import os
+    import subprocess
+    import tempfile
+    from urllib.parse import urlparse
+
+    from .. import _build
+
+    _build.build_tools()
+    u = urlparse(url)
+    tmp = tempfile.mkdtemp(prefix="ai4e_load_")
+    body_path = os.path.join(tmp, "body.bin")
+    with open(body_path, "wb") as f:
+        f.write(body)
+    start_at = time.time() + 1.0
+    ps = []
+    for i in range(procs):
+        cmd = [str(_build.HTTP_LOAD), u.hostname, str(u.port), u.path + (("?" + u.query) if u.query else ""),
+               content_type, body_path, str(conc), str(seconds), f"{start_at:.6f}", os.path.join(tmp, f"ids{i}.txt"),
+               *headers]
+        ps.append(subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    out = {"ids": [], "t0": float("inf"), "t1": 0.0, "errors": 0, "requests": 0, "bytes_sent": 0.0,
+           "client_cpu_s": 0.0, "client_processes": procs, "connections": procs * conc}
+    for i, p in enumerate(ps):
+        so, se = p.communicate(timeout=seconds + 120)
+        if p.returncode != 0:
+            raise RuntimeError(f"ai4e_http_load failed ({p.returncode}): {se[-500:]}")
+        st = json.loads(so.strip().splitlines()[-1])
+        out["t0"], out["t1"] = min(out["t0"], st["t0"]), max(out["t1"], st["t1"])
+        out["errors"] += st["errors"]
+        out["requests"] += st["requests"]
+        out["bytes_sent"] += st["bytes_sent"]
+        out["client_cpu_s"] += st["cpu_user_s"] + st["cpu_sys_s"]
+        with open(os.path.join(tmp, f"ids{i}.txt")) as f:
+            out["ids"] += [l.strip() for l in f if l.strip()]
+    for name in os.listdir(tmp):
+        os.unlink(os.path.join(tmp, name))
+    os.rmdir(tmp)
+    return out

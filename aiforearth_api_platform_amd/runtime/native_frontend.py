@@ -1,0 +1,118 @@
+"""Launcher of the native ingest front-ends (``csrc/ingest/ingestd.cpp``, built to ``_lib/ai4e_ingestd``).
+
+Same role and same admission rules as the Python front-ends of :mod:`runtime.frontend` — a process on the
+public port beside the serving process (SO_REUSEPORT), its own partition of every pool endpoint's payload
+ring, SUBMIT_IDS / SUBMITTED / FREE with the node scheduler over its own ingest connection — but written in
+C++: a binary batch or a raw single payload is ``recv()``'d straight into ring slots (one kernel->ring copy,
+no interpreter on the path), one thread per client connection. Requests it does not ingest itself (encoded
+images, task API, sync routes, upstream ``taskId`` requests, chunked bodies) are proxied to the serving
+process. TLS is not terminated there: with a certificate configured the platform starts the Python front-ends.
+
+The scheduler connection is the socket end of a ``multiprocessing.Pipe`` (a socketpair) inherited by the
+child; the config is a small line-oriented file (``ingestd.cpp`` ``parse_config``).
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import tempfile
+from typing import Dict, List, Optional
+
+from .. import _build
+
+
+class NativeFrontend:
+    """Handle of one ``ai4e_ingestd`` process (``terminate`` / ``join`` / ``is_alive`` like a Process)."""
+
+    def __init__(self, proc: subprocess.Popen, cfg_path: str):
+        self.proc, self.cfg_path = proc, cfg_path
+        self.pid = proc.pid
+
+    def terminate(self) -> None:
+        if self.proc.poll() is None:
+            self.proc.terminate()
+
+    def kill(self) -> None:
+        if self.proc.poll() is None:
+            self.proc.kill()
+
+    def join(self, timeout: Optional[float] = None) -> None:
+        try:
+            self.proc.wait(timeout)
+        except subprocess.TimeoutExpired:
+            pass
+        if self.proc.poll() is not None and os.path.exists(self.cfg_path):
+            os.unlink(self.cfg_path)
+
+    def is_alive(self) -> bool:
+        return self.proc.poll() is None
+
+    @property
+    def exitcode(self) -> Optional[int]:
+        return self.proc.poll()
+
+
+def available() -> bool:
+    try:
+        _build.build_tools()
+    except Exception:
+        return False
+    return _build.INGESTD.exists()
+
+
+def _token(v) -> str:
+    s = str(v)
+    if not s or any(c.isspace() for c in s):
+        raise ValueError(f"native front-end config value must be a non-empty token without spaces: {s!r}")
+    return s
+
+
+def spawn_native_frontends(n: int, pools: Dict[str, object], routes: List[dict], host: str, port: int,
+                           internal_url: str, security: Optional[dict] = None,
+                           ack_timeout_s: float = 30.0) -> List[NativeFrontend]:
+    """Start ``n`` native front-ends; arguments as :func:`runtime.frontend.spawn_frontends`."""
+    import multiprocessing as mp
+
+    if not n or not pools:
+        return []
+    sec = security or {}
+    if sec.get("tls_cert"):
+        raise ValueError("the native front-end does not terminate TLS; use the Python front-ends")
+    _build.build_tools()
+    ihost, iport = internal_url.split("://", 1)[1].rsplit(":", 1)
+    names = list(pools)
+    procs = []
+    for i in range(n):
+        lines = [f"listen {_token(host)} {int(port)}", f"internal {_token(ihost)} {int(iport)}",
+                 f"ack_timeout {float(ack_timeout_s)}"]
+        lines += [f"key {_token(k)}" for k in sec.get("keys") or []]
+        child_ends, fds = [], []
+        for si, name in enumerate(names):
+            ep = pools[name]
+            base, length, rank = ep.worker.frontend_partitions[i]
+            parent, child = mp.Pipe(duplex=True)
+            ep.worker.attach_ingest(rank, parent)
+            child_ends.append(child)
+            fds.append(child.fileno())
+            item = 1
+            for v in ep.item_shape:
+                item *= int(v)
+            shape = "(" + ",".join(str(int(v)) for v in ep.item_shape) + ")"
+            lines.append(f"shard {si} {child.fileno()} {_token(ep.ring.name)} {int(ep.ring.nslots)} {item} "
+                         f"{int(base)} {int(length)} {_token(ep.endpoint)} {shape}")
+        for r in routes:
+            si = names.index(r["endpoint"]) if r.get("endpoint") in pools else -1
+            types = ",".join(_token(t) for t in r.get("content_types") or []) or "-"
+            keys = ",".join(_token(k) for k in r.get("keys") or []) or "-"
+            mc = r.get("max_concurrent")
+            lines.append(f"route {_token(r['prefix'])} {_token(r.get('mode', 'async'))} {si} "
+                         f"{int(r.get('max_content_length') or 0)} {-1 if mc is None else int(mc)} {types} {keys}")
+        fd, cfg_path = tempfile.mkstemp(prefix="ai4e_ingestd_", suffix=".conf")
+        with os.fdopen(fd, "w") as f:
+            f.write("\n".join(lines) + "\n")
+        os.chmod(cfg_path, 0o600)  # (subscription keys)
+        p = subprocess.Popen([str(_build.INGESTD), cfg_path], pass_fds=fds, close_fds=True)
+        for c in child_ends:
+            c.close()
+        procs.append(NativeFrontend(p, cfg_path))
+    return procs

@@ -50,15 +50,18 @@ class Client:
 
 def http_phase(cp, pool, seconds: float, batch: int, item_shape, path: str, frontends: int = 0) -> dict:
     """REST ingest on this node: aiohttp gateway (this process) + binary batch route (streamed into the
-    payload ring), then single-image requests; the clients run in separate processes. ``frontends``:
-    ingest front-end processes sharing the port (runtime/frontend.py; the pool needs as many partitions)."""
+    payload ring), then single-image requests. ``frontends``: ingest front-end processes sharing the port
+    (native C++ ``ai4e_ingestd`` by default, AI4E_FRONTEND_IMPL=python for runtime/frontend.py; the pool needs
+    as many partitions). Load: the C++ generator (runtime/http_load.py ``run_native_clients``) in separate
+    processes; the record carries the client and server CPU seconds, so a reader can see which side was
+    the ceiling."""
     import asyncio
 
     from aiohttp import web
 
     from ..gateway.server import BATCH_CONTENT_TYPE, Gateway, Route, RouteTable
     from ..utils.metrics import percentile
-    from .http_load import run_clients
+    from .http_load import run_clients, run_native_clients
     from .model_endpoint import ModelEndpoint
 
     ep = ModelEndpoint(cp, path, worker=pool)
@@ -92,11 +95,14 @@ def http_phase(cp, pool, seconds: float, batch: int, item_shape, path: str, fron
     th = threading.Thread(target=serve, daemon=True)
     th.start()
     ready.wait(30)
-    fe = spawn_frontends(frontends, {"bench": ep}, [{"prefix": "/v1/bench/async", "mode": "async",
-                                                    "endpoint": "bench"}], "127.0.0.1", port,
-                         f"http://127.0.0.1:{socks[1].getsockname()[1]}") if frontends else []
+    impl = os.environ.get("AI4E_FRONTEND_IMPL", "native")
+    spawn = spawn_frontends
+    if impl == "native":
+        from .native_frontend import spawn_native_frontends as spawn
+    fe = spawn(frontends, {"bench": ep}, [{"prefix": "/v1/bench/async", "mode": "async", "endpoint": "bench"}],
+               "127.0.0.1", port, f"http://127.0.0.1:{socks[1].getsockname()[1]}") if frontends else []
     if fe:
-        time.sleep(5.0)  # their interpreters start and bind the shared port
+        time.sleep(5.0 if impl != "native" else 1.0)  # they start and bind the shared port
     url = f"http://127.0.0.1:{port}/v1/bench/async"
     rng = np.random.default_rng(7)
     img = rng.integers(0, 256, tuple(item_shape), dtype=np.uint8)
@@ -112,17 +118,43 @@ def http_phase(cp, pool, seconds: float, batch: int, item_shape, path: str, fron
         return sorted(cp.store.latencies(ids))
 
     # load generators in their own processes (the server keeps this interpreter to itself)
+    import psutil
+
+    server_procs = [psutil.Process(os.getpid())] + [psutil.Process(p.pid) for p in fe]
+
+    def server_cpu() -> float:
+        tot = 0.0
+        for p in server_procs:
+            try:
+                c = p.cpu_times()
+                tot += c.user + c.system
+            except psutil.Error:
+                pass
+        return tot
+
+    native = os.environ.get("AI4E_HTTP_CLIENT", "native") == "native"
     out = {}
     for name, body, ctype, is_batch, procs, conc in (
-            ("batch_route", batch_body, BATCH_CONTENT_TYPE, True, 2, 2),
-            ("single_image_route", img.tobytes(), "application/octet-stream", False, 3, 32)):
-        ids, t0, _, errors = run_clients(url, seconds / 2, conc, body, ctype, is_batch, procs=procs)
+            ("batch_route", batch_body, BATCH_CONTENT_TYPE, True, 4, 4),
+            ("single_image_route", img.tobytes(), "application/octet-stream", False, 4, 32)):
+        c0 = server_cpu()
+        if native:
+            res = run_native_clients(url, seconds / 2, conc, body, ctype, procs=procs)
+            ids, t0, errors = res["ids"], res["t0"], res["errors"]
+        else:
+            ids, t0, _, errors = run_clients(url, seconds / 2, conc, body, ctype, is_batch, procs=procs)
+            res = {}
         lat = wait_done(ids)
         dt = time.time() - t0
         out[name] = {"images": len(ids), "images_per_s": round(len(ids) / dt, 1), "connections": procs * conc,
-                     "client_processes": procs, "ingest_frontends": len(fe), "errors": errors,
+                     "client_processes": procs, "client": "c++ ai4e_http_load" if native else "python aiohttp",
+                     "ingest_frontends": len(fe), "frontend_impl": impl if fe else None, "errors": errors,
                      "p50_task_latency_ms": round(percentile(lat, 50) * 1e3, 3),
-                     "p99_task_latency_ms": round(percentile(lat, 99) * 1e3, 3)}
+                     "p99_task_latency_ms": round(percentile(lat, 99) * 1e3, 3),
+                     "server_cpu_s": round(server_cpu() - c0, 3), "window_s": round(dt, 3)}
+        if res:
+            out[name]["client_cpu_s"] = round(res["client_cpu_s"], 3)
+            out[name]["request_gbytes_per_s"] = round(res["bytes_sent"] / max(1e-9, res["t1"] - res["t0"]) / 1e9, 3)
         if is_batch:
             out[name]["request_images"] = batch
     for p in fe:
@@ -178,7 +210,7 @@ def run_node_bench(args, spec, path: str, metric: str, unit: str = "images/s", c
                           ring_slots=part, max_delay_s=0.0005, heartbeat_interval_s=hb, heartbeat_timeout_s=120.0,
                           remote_partitions=remote, pipeline_depth=int(os.environ.get("AI4E_PIPELINE_DEPTH", "3")),
                           poll_s=0.005, frontends=getattr(args, "http_frontends", 0) if args.http else 0,
-                          frontend_slots=2 * B)  # (REST phase only: keep the pinned ring small)
+                          frontend_slots=3 * B)  # (REST phase only: keep the pinned ring small)
         info = None
         listener = None
         if world > 1:

@@ -53,7 +53,8 @@ def frontend_count(cfg: Config) -> int:
 
 
 def start_frontends(cfg: Config, doc: Dict[str, Any], endpoints: Dict[str, Any], port: int, internal_port: int):
-    """Spawn the ingest front-end processes (runtime/frontend.py) for the platform's pool endpoints."""
+    """Spawn the ingest front-end processes for the platform's pool endpoints: native (runtime/native_frontend.py,
+    the default) or Python (runtime/frontend.py; always with TLS)."""
     from .runtime.frontend import spawn_frontends
 
     # image endpoints only: requests of endpoints with their own decoder (extent records) go to the gateway
@@ -67,9 +68,14 @@ def start_frontends(cfg: Config, doc: Dict[str, Any], endpoints: Dict[str, Any],
                        "endpoint": name if name in pools else None, "content_types": r.get("content_types"),
                        "max_content_length": r.get("max_content_length"), "max_concurrent": r.get("max_concurrent"),
                        "keys": parse_keys(r.get("keys"))})
+    security = {"keys": parse_keys(cfg.subscription_keys), "tls_cert": cfg.tls_cert, "tls_key": cfg.tls_key}
+    if cfg.frontend_impl == "native" and not cfg.tls_cert:
+        from .runtime.native_frontend import spawn_native_frontends
+
+        return spawn_native_frontends(frontend_count(cfg), pools, routes, cfg.host, port,
+                                      f"http://127.0.0.1:{internal_port}", security=security)
     return spawn_frontends(frontend_count(cfg), pools, routes, cfg.host, port, f"http://127.0.0.1:{internal_port}",
-                           security={"keys": parse_keys(cfg.subscription_keys), "tls_cert": cfg.tls_cert,
-                                     "tls_key": cfg.tls_key})
+                           security=security)
 
 
 def _request_decoder(e: Dict[str, Any]):

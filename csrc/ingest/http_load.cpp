@@ -1,0 +1,210 @@
+// ai4e_http_load — HTTP/1.1 keep-alive load generator for the REST benchmarks (runtime/node_bench.py
+// http_phase). A Python client tops out near the rate it is supposed to measure (one aiohttp process moves
+// ~1-2 GB/s of request bodies); this one sends a prebuilt request (headers + body, one writev) per
+// round trip from one thread per connection, parses the status line / Content-Length of the answer and
+// collects the task ids it hands back, so the server side is what the benchmark measures. It reports its
+// own CPU time (user + system) so a reader can tell whether the client was the ceiling.
+//
+//   ai4e_http_load HOST PORT PATH CONTENT_TYPE BODY_FILE CONNS SECONDS START_AT_EPOCH IDS_OUT [HEADER...]
+//
+// Prints one JSON line: requests, ok, errors, t0, t1 (epoch s), bytes_sent, cpu_user_s, cpu_sys_s.
+// IDS_OUT receives one task id per line (TaskId / TaskIds of every 2xx answer).
+#include <arpa/inet.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <sys/resource.h>
+#include <sys/socket.h>
+#include <sys/uio.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <cerrno>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <mutex>
+#include <sstream>
+#include <string>
+#include <thread>
+#include <vector>
+
+namespace {
+
+double now() {
+  return std::chrono::duration<double>(std::chrono::system_clock::now().time_since_epoch()).count();
+}
+
+struct Result {
+  long requests = 0, ok = 0, errors = 0;
+  double bytes = 0;
+  std::vector<std::string> ids;
+};
+
+bool send_all(int fd, const struct iovec* iov0, int cnt) {
+  std::vector<struct iovec> iov(iov0, iov0 + cnt);
+  size_t idx = 0;
+  while (idx < iov.size()) {
+    ssize_t k = ::writev(fd, iov.data() + idx, static_cast<int>(iov.size() - idx));
+    if (k < 0) {
+      if (errno == EINTR) continue;
+      return false;
+    }
+    size_t kk = static_cast<size_t>(k);
+    while (idx < iov.size() && kk >= iov[idx].iov_len) kk -= iov[idx++].iov_len;
+    if (idx < iov.size()) {
+      iov[idx].iov_base = static_cast<char*>(iov[idx].iov_base) + kk;
+      iov[idx].iov_len -= kk;
+    }
+  }
+  return true;
+}
+
+// Reads one response; returns the status (0 on a broken connection) and its body.
+int read_response(int fd, std::string& buf, std::string& body) {
+  size_t hend;
+  while ((hend = buf.find("\r\n\r\n")) == std::string::npos) {
+    char tmp[65536];
+    ssize_t k = ::recv(fd, tmp, sizeof(tmp), 0);
+    if (k <= 0) return 0;
+    buf.append(tmp, static_cast<size_t>(k));
+  }
+  int status = std::atoi(buf.c_str() + 9);
+  size_t clen = 0;
+  std::string head = buf.substr(0, hend);
+  for (auto& ch : head) ch = static_cast<char>(std::tolower(static_cast<unsigned char>(ch)));
+  auto p = head.find("content-length:");
+  if (p != std::string::npos) clen = std::strtoull(head.c_str() + p + 15, nullptr, 10);
+  while (buf.size() < hend + 4 + clen) {
+    char tmp[65536];
+    ssize_t k = ::recv(fd, tmp, sizeof(tmp), 0);
+    if (k <= 0) return 0;
+    buf.append(tmp, static_cast<size_t>(k));
+  }
+  body = buf.substr(hend + 4, clen);
+  buf.erase(0, hend + 4 + clen);
+  return status;
+}
+
+void extract_ids(const std::string& body, std::vector<std::string>& out) {
+  // {"TaskIds":["a","b",...]} or {"TaskId":"a",...}
+  auto p = body.find("\"TaskIds\"");
+  if (p != std::string::npos) {
+    size_t e = body.find(']', p);
+    size_t q = body.find('[', p);
+    while (q != std::string::npos && q < e) {
+      size_t a = body.find('"', q + 1);
+      if (a == std::string::npos || a > e) break;
+      size_t b = body.find('"', a + 1);
+      out.emplace_back(body.substr(a + 1, b - a - 1));
+      q = b;
+    }
+    return;
+  }
+  p = body.find("\"TaskId\"");
+  if (p != std::string::npos) {
+    size_t a = body.find('"', body.find(':', p) + 1);
+    size_t b = body.find('"', a + 1);
+    out.emplace_back(body.substr(a + 1, b - a - 1));
+  }
+}
+
+int dial(const char* host, int port) {
+  int fd = ::socket(AF_INET, SOCK_STREAM, 0);
+  sockaddr_in a{};
+  a.sin_family = AF_INET;
+  a.sin_port = htons(static_cast<uint16_t>(port));
+  inet_pton(AF_INET, host, &a.sin_addr);
+  if (::connect(fd, reinterpret_cast<sockaddr*>(&a), sizeof(a)) != 0) {
+    ::close(fd);
+    return -1;
+  }
+  int one = 1, snd = 4 << 20;
+  setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+  setsockopt(fd, SOL_SOCKET, SO_SNDBUF, &snd, sizeof(snd));
+  return fd;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  if (argc < 10) {
+    std::fprintf(stderr,
+                 "usage: ai4e_http_load HOST PORT PATH CONTENT_TYPE BODY_FILE CONNS SECONDS START_AT IDS_OUT "
+                 "[HEADER...]\n");
+    return 2;
+  }
+  const char* host = argv[1];
+  const int port = std::atoi(argv[2]);
+  const std::string path = argv[3], ctype = argv[4];
+  std::ifstream bf(argv[5], std::ios::binary);
+  std::string body((std::istreambuf_iterator<char>(bf)), std::istreambuf_iterator<char>());
+  const int conns = std::atoi(argv[6]);
+  const double seconds = std::atof(argv[7]), start_at = std::atof(argv[8]);
+  const char* ids_out = argv[9];
+  std::string head = "POST " + path + " HTTP/1.1\r\nHost: " + std::string(host) + ":" + std::to_string(port) +
+                     "\r\nContent-Type: " + ctype + "\r\nContent-Length: " + std::to_string(body.size()) + "\r\n";
+  for (int i = 10; i < argc; ++i) head += std::string(argv[i]) + "\r\n";
+  head += "\r\n";
+
+  std::vector<Result> res(static_cast<size_t>(conns));
+  while (now() < start_at) std::this_thread::sleep_for(std::chrono::microseconds(200));
+  const double t0 = now(), t_end = t0 + seconds;
+  std::vector<std::thread> th;
+  for (int c = 0; c < conns; ++c) {
+    th.emplace_back([&, c] {
+      Result& r = res[static_cast<size_t>(c)];
+      int fd = dial(host, port);
+      std::string buf, rbody;
+      struct iovec iov[2] = {{const_cast<char*>(head.data()), head.size()},
+                             {const_cast<char*>(body.data()), body.size()}};
+      while (fd >= 0 && now() < t_end) {
+        if (!send_all(fd, iov, 2)) {
+          ::close(fd);
+          fd = dial(host, port);
+          ++r.errors;
+          continue;
+        }
+        ++r.requests;
+        r.bytes += static_cast<double>(head.size() + body.size());
+        int st = read_response(fd, buf, rbody);
+        if (st == 0) {
+          ::close(fd);
+          buf.clear();
+          fd = dial(host, port);
+          ++r.errors;
+          continue;
+        }
+        if (st >= 200 && st < 300) {
+          ++r.ok;
+          extract_ids(rbody, r.ids);
+        } else {
+          ++r.errors;
+        }
+      }
+      if (fd >= 0) ::close(fd);
+    });
+  }
+  for (auto& t : th) t.join();
+  const double t1 = now();
+  Result tot;
+  FILE* f = std::fopen(ids_out, "w");
+  for (auto& r : res) {
+    tot.requests += r.requests;
+    tot.ok += r.ok;
+    tot.errors += r.errors;
+    tot.bytes += r.bytes;
+    if (f)
+      for (auto& id : r.ids) std::fprintf(f, "%s\n", id.c_str());
+  }
+  if (f) std::fclose(f);
+  struct rusage ru {};
+  getrusage(RUSAGE_SELF, &ru);
+  std::printf(
+      "{\"requests\": %ld, \"ok\": %ld, \"errors\": %ld, \"t0\": %.6f, \"t1\": %.6f, \"bytes_sent\": %.0f, "
+      "\"cpu_user_s\": %.3f, \"cpu_sys_s\": %.3f, \"connections\": %d}\n",
+      tot.requests, tot.ok, tot.errors, t0, t1, tot.bytes, ru.ru_utime.tv_sec + ru.ru_utime.tv_usec * 1e-6,
+      ru.ru_stime.tv_sec + ru.ru_stime.tv_usec * 1e-6, conns);
+  return 0;
+}

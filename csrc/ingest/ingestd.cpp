@@ -1,0 +1,841 @@
+// ai4e_ingestd — native ingest front-end of the gateway (the C++ form of runtime/frontend.py).
+//
+// One process listens on the public port beside the serving process (SO_REUSEPORT: the kernel spreads
+// connections over every listener) and takes the async POSTs of the GPU endpoints itself:
+//
+//   * binary batches (application/x-ai4e-batch, n x item bytes) and raw single payloads
+//     (application/octet-stream of exactly one item) are recv()'d STRAIGHT into slots of this process's
+//     partition of the endpoint's shared payload ring — one kernel->ring copy, no parse, no decode;
+//   * task ids are minted here (uuid4, last hex digit = store shard, as ingest.IngestShard.mint_ids) and handed
+//     to the node scheduler with the slots (SUBMIT_IDS over the ingest connection, acknowledged with
+//     SUBMITTED once the tasks exist); slots come back with FREE when the tasks finish;
+//   * everything else (task status / result / trace, sync routes, encoded images, requests carrying an
+//     upstream taskId, chunked bodies) is proxied to the serving process's internal listener.
+//
+// Admission matches the gateway (gateway/server.py, gateway/security.py): subscription keys (401), the
+// route's max_concurrent (429), draining after SIGTERM (503), content type (401), length (413). TLS is not
+// terminated here: with a certificate configured the platform runs the Python front-ends instead.
+//
+// Threads: one acceptor, one thread per client connection (blocking I/O, keep-alive), one reader per
+// scheduler connection. The process exits when a scheduler connection closes (the serving process is gone)
+// or 5 s after SIGTERM.
+//
+// Config: a line-oriented file written by runtime/native_frontend.py (see parse_config).
+#include <arpa/inet.h>
+#include <fcntl.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <signal.h>
+#include <sys/mman.h>
+#include <sys/socket.h>
+#include <sys/stat.h>
+#include <sys/uio.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cerrno>
+#include <condition_variable>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <sstream>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "../core/common.h"
+#include "../core/slot_ring.h"
+
+namespace {
+
+constexpr uint32_t F_STOP = 5, F_FREE = 7, F_SUBMIT_IDS = 9, F_SUBMITTED = 10;
+const char* kBatchType = "application/x-ai4e-batch";
+const char* kRawType = "application/octet-stream";
+const char* kKeyHeader = "ocp-apim-subscription-key";
+const char* kMissingKey =
+    "Access denied due to missing subscription key. Make sure to include subscription key when making requests "
+    "to an API.";
+const char* kInvalidKey =
+    "Access denied due to invalid subscription key. Make sure to provide a valid key for an active subscription.";
+
+std::atomic<bool> g_draining{false};
+
+// ------------------------------------------------------------------ socket helpers
+bool write_all(int fd, const void* p, size_t n) {
+  const char* c = static_cast<const char*>(p);
+  while (n) {
+    ssize_t k = ::send(fd, c, n, MSG_NOSIGNAL);
+    if (k < 0) {
+      if (errno == EINTR) continue;
+      return false;
+    }
+    c += k;
+    n -= static_cast<size_t>(k);
+  }
+  return true;
+}
+
+bool read_exact(int fd, void* p, size_t n) {
+  char* c = static_cast<char*>(p);
+  while (n) {
+    ssize_t k = ::recv(fd, c, n, 0);
+    if (k == 0) return false;
+    if (k < 0) {
+      if (errno == EINTR) continue;
+      return false;
+    }
+    c += k;
+    n -= static_cast<size_t>(k);
+  }
+  return true;
+}
+
+std::string lower(std::string s) {
+  for (auto& ch : s) ch = static_cast<char>(std::tolower(static_cast<unsigned char>(ch)));
+  return s;
+}
+
+std::string trim(const std::string& s) {
+  size_t a = s.find_first_not_of(" \t"), b = s.find_last_not_of(" \t\r");
+  return a == std::string::npos ? std::string() : s.substr(a, b - a + 1);
+}
+
+std::vector<std::string> split(const std::string& s, char sep) {
+  std::vector<std::string> out;
+  std::string cur;
+  for (char ch : s) {
+    if (ch == sep) {
+      out.push_back(cur);
+      cur.clear();
+    } else {
+      cur.push_back(ch);
+    }
+  }
+  out.push_back(cur);
+  return out;
+}
+
+std::string hexid(std::mt19937_64& rng, int bits) {
+  static const char* hx = "0123456789abcdef";
+  std::string s;
+  for (int i = 0; i < bits / 64; ++i) {
+    uint64_t v = rng();
+    for (int k = 15; k >= 0; --k) s.push_back(hx[(v >> (4 * k)) & 0xF]);
+  }
+  return s;
+}
+
+// ------------------------------------------------------------------ scheduler connection (one per endpoint)
+// multiprocessing.Connection framing on a socketpair: 4-byte big-endian length, then the frame.
+struct Ack {
+  bool done = false;
+  uint32_t n = 0;
+};
+
+struct Shard {
+  int idx = 0, fd = -1;
+  std::string endpoint, endpoint_path, shape_str;
+  int64_t nslots = 0, item = 0, base = 0, len = 0;
+  uint8_t* ring = nullptr;
+  std::unique_ptr<ai4e::SlotRing> slots;
+  std::mutex send_mu, ack_mu;
+  std::condition_variable ack_cv;
+  std::unordered_map<uint64_t, Ack> acks;
+  std::atomic<uint64_t> token{1}, shard_ctr{0};
+  std::mutex id_mu;
+  ai4e::Uuid4 uuid;
+
+  bool send_frame(const std::string& payload) {
+    uint32_t be = htonl(static_cast<uint32_t>(payload.size()));
+    std::lock_guard<std::mutex> g(send_mu);
+    return write_all(fd, &be, 4) && write_all(fd, payload.data(), payload.size());
+  }
+
+  std::vector<std::string> mint(size_t n) {
+    static const char* hx = "0123456789abcdef";
+    const char d = hx[shard_ctr.fetch_add(1) % 8];
+    std::vector<std::string> ids(n);
+    std::lock_guard<std::mutex> g(id_mu);
+    for (auto& s : ids) {
+      s = uuid.next();
+      s.back() = d;
+    }
+    return ids;
+  }
+
+  // SUBMIT_IDS: u32 type, u32 n, u32 trace_len, u32 id_len, u32 ack, u64 token | i64 slots[n] | ids | trace
+  uint64_t submit(const std::vector<int64_t>& sl, const std::vector<std::string>& ids, const std::string& trace) {
+    const uint64_t tok = token.fetch_add(1);
+    {
+      std::lock_guard<std::mutex> g(ack_mu);
+      acks[tok] = Ack{};
+    }
+    const uint32_t n = static_cast<uint32_t>(sl.size()), tl = static_cast<uint32_t>(trace.size()),
+                   il = ids.empty() ? 0 : static_cast<uint32_t>(ids[0].size()), ack = 1;
+    std::string f;
+    f.reserve(28 + 8 * n + il * n + tl);
+    auto put32 = [&](uint32_t v) { f.append(reinterpret_cast<const char*>(&v), 4); };
+    put32(F_SUBMIT_IDS);
+    put32(n);
+    put32(tl);
+    put32(il);
+    put32(ack);
+    f.append(reinterpret_cast<const char*>(&tok), 8);
+    f.append(reinterpret_cast<const char*>(sl.data()), 8 * sl.size());
+    for (auto& s : ids) f += s;
+    f += trace;
+    if (!send_frame(f)) std::_Exit(0);  // the serving process is gone
+    return tok;
+  }
+
+  // -1: timed out (the tasks may still be created), else tasks created
+  int64_t wait_ack(uint64_t tok, double timeout_s) {
+    std::unique_lock<std::mutex> lk(ack_mu);
+    bool ok = ack_cv.wait_for(lk, std::chrono::duration<double>(timeout_s), [&] { return acks[tok].done; });
+    int64_t n = ok ? acks[tok].n : -1;
+    acks.erase(tok);
+    return n;
+  }
+
+  void reader() {
+    std::vector<char> buf;
+    while (true) {
+      uint32_t be;
+      if (!read_exact(fd, &be, 4)) break;
+      int32_t n = static_cast<int32_t>(ntohl(be));
+      uint64_t len = static_cast<uint64_t>(n);
+      if (n == -1) {
+        uint64_t be8;
+        if (!read_exact(fd, &be8, 8)) break;
+        len = be64toh(be8);
+      }
+      buf.resize(len);
+      if (len && !read_exact(fd, buf.data(), len)) break;
+      if (len < 4) continue;
+      uint32_t type;
+      std::memcpy(&type, buf.data(), 4);
+      if (type == F_FREE && len >= 12) {  // u32 type, u32 n, u32 pad, i64 slots[n]
+        uint32_t cnt;
+        std::memcpy(&cnt, buf.data() + 4, 4);
+        std::vector<int64_t> s(cnt);
+        if (12 + 8ull * cnt <= len) {
+          std::memcpy(s.data(), buf.data() + 12, 8ull * cnt);
+          slots->free(s);
+        }
+      } else if (type == F_SUBMITTED && len >= 20) {  // u32 type, u64 token, u32 n, u32 pad
+        uint64_t tok;
+        uint32_t cnt;
+        std::memcpy(&tok, buf.data() + 4, 8);
+        std::memcpy(&cnt, buf.data() + 12, 4);
+        std::lock_guard<std::mutex> g(ack_mu);
+        auto it = acks.find(tok);
+        if (it != acks.end()) {
+          it->second.done = true;
+          it->second.n = cnt;
+        }
+        ack_cv.notify_all();
+      } else if (type == F_STOP) {
+        break;
+      }
+    }
+    std::_Exit(0);  // scheduler connection closed: nothing left to serve
+  }
+};
+
+struct Route {
+  std::string prefix, mode;
+  int shard = -1;
+  int64_t max_content_length = 0, max_concurrent = -1;
+  std::vector<std::string> content_types, keys;
+  std::atomic<int64_t> inflight{0};
+};
+
+struct Config {
+  std::string host = "127.0.0.1";
+  int port = 0;
+  std::string internal_host = "127.0.0.1";
+  int internal_port = 0;
+  double ack_timeout = 30.0, alloc_timeout = 60.0;
+  std::vector<std::string> keys;
+  std::vector<std::unique_ptr<Shard>> shards;
+  std::vector<std::unique_ptr<Route>> routes;  // longest prefix first
+};
+
+Config g_cfg;
+
+// "listen H P" | "internal H P" | "key K" | "ack_timeout S" | "alloc_timeout S"
+// "shard IDX FD SHM NSLOTS ITEM BASE LEN ENDPOINT SHAPE" | "route PREFIX MODE SHARD MCL MC TYPES|- KEYS|-"
+void parse_config(const char* path) {
+  std::ifstream in(path);
+  if (!in) {
+    std::fprintf(stderr, "ai4e_ingestd: cannot read %s\n", path);
+    std::exit(2);
+  }
+  std::string line;
+  while (std::getline(in, line)) {
+    std::istringstream ls(line);
+    std::string kw;
+    ls >> kw;
+    if (kw == "listen") {
+      ls >> g_cfg.host >> g_cfg.port;
+    } else if (kw == "internal") {
+      ls >> g_cfg.internal_host >> g_cfg.internal_port;
+    } else if (kw == "key") {
+      std::string k;
+      ls >> k;
+      g_cfg.keys.push_back(k);
+    } else if (kw == "ack_timeout") {
+      ls >> g_cfg.ack_timeout;
+    } else if (kw == "alloc_timeout") {
+      ls >> g_cfg.alloc_timeout;
+    } else if (kw == "shard") {
+      auto s = std::make_unique<Shard>();
+      std::string shm;
+      ls >> s->idx >> s->fd >> shm >> s->nslots >> s->item >> s->base >> s->len >> s->endpoint >> s->shape_str;
+      s->endpoint_path = ai4e::absolute_path(s->endpoint);
+      int mfd = shm_open(("/" + shm).c_str(), O_RDWR, 0);
+      if (mfd < 0) {
+        std::perror("ai4e_ingestd: shm_open");
+        std::exit(2);
+      }
+      void* p = mmap(nullptr, static_cast<size_t>(s->nslots * s->item), PROT_READ | PROT_WRITE, MAP_SHARED, mfd, 0);
+      ::close(mfd);
+      if (p == MAP_FAILED) {
+        std::perror("ai4e_ingestd: mmap");
+        std::exit(2);
+      }
+      s->ring = static_cast<uint8_t*>(p);
+      s->slots = std::make_unique<ai4e::SlotRing>(s->len, s->base);
+      g_cfg.shards.push_back(std::move(s));
+    } else if (kw == "route") {
+      auto r = std::make_unique<Route>();
+      std::string types, keys;
+      ls >> r->prefix >> r->mode >> r->shard >> r->max_content_length >> r->max_concurrent >> types >> keys;
+      if (types != "-")
+        for (auto& t : split(types, ',')) r->content_types.push_back(t);
+      if (keys != "-")
+        for (auto& k : split(keys, ',')) r->keys.push_back(k);
+      g_cfg.routes.push_back(std::move(r));
+    }
+  }
+  std::sort(g_cfg.routes.begin(), g_cfg.routes.end(),
+            [](const std::unique_ptr<Route>& a, const std::unique_ptr<Route>& b) {
+              return a->prefix.size() > b->prefix.size();
+            });
+}
+
+// ------------------------------------------------------------------ HTTP
+struct Request {
+  std::string method, target, path, query, version;
+  std::vector<std::pair<std::string, std::string>> headers;  // original case, in order
+  std::map<std::string, std::string> h;                       // lower-case name -> value
+  int64_t content_length = -1;
+  bool chunked = false, keep_alive = true;
+  std::string get(const char* k) const {
+    auto it = h.find(k);
+    return it == h.end() ? std::string() : it->second;
+  }
+};
+
+struct Conn {
+  int fd;
+  std::vector<char> buf;  // bytes received past the current parse point
+  size_t pos = 0, end = 0;
+  int upstream = -1;      // keep-alive connection to the internal listener
+  std::mt19937_64 rng{std::random_device{}()};
+
+  explicit Conn(int f) : fd(f), buf(1 << 16) {}
+  ~Conn() {
+    if (upstream >= 0) ::close(upstream);
+  }
+  size_t avail() const { return end - pos; }
+  bool fill() {
+    if (pos == end) pos = end = 0;
+    if (end == buf.size()) {
+      if (pos > 0) {
+        std::memmove(buf.data(), buf.data() + pos, end - pos);
+        end -= pos;
+        pos = 0;
+      } else {
+        buf.resize(buf.size() * 2);
+      }
+    }
+    ssize_t k;
+    do {
+      k = ::recv(fd, buf.data() + end, buf.size() - end, 0);
+    } while (k < 0 && errno == EINTR);
+    if (k <= 0) return false;
+    end += static_cast<size_t>(k);
+    return true;
+  }
+  // read exactly n body bytes into dst (buffered bytes first, then straight from the socket)
+  bool body_into(uint8_t* dst, size_t n) {
+    size_t take = std::min(n, avail());
+    if (take) {
+      std::memcpy(dst, buf.data() + pos, take);
+      pos += take;
+      dst += take;
+      n -= take;
+    }
+    return n == 0 || read_exact(fd, dst, n);
+  }
+  bool discard(size_t n) {
+    std::vector<char> tmp(1 << 16);
+    size_t take = std::min(n, avail());
+    pos += take;
+    n -= take;
+    while (n) {
+      size_t k = std::min(n, tmp.size());
+      if (!read_exact(fd, tmp.data(), k)) return false;
+      n -= k;
+    }
+    return true;
+  }
+  bool line(std::string& out) {  // one CRLF line (for chunked bodies)
+    while (true) {
+      char* b = buf.data() + pos;
+      char* e = static_cast<char*>(std::memchr(b, '\n', avail()));
+      if (e) {
+        out.assign(b, e);
+        if (!out.empty() && out.back() == '\r') out.pop_back();
+        pos += static_cast<size_t>(e - b) + 1;
+        return true;
+      }
+      if (!fill()) return false;
+    }
+  }
+};
+
+bool read_head(Conn& c, Request& r) {
+  size_t scanned = 0;
+  while (true) {
+    const char* b = c.buf.data() + c.pos;
+    size_t n = c.avail();
+    for (size_t i = scanned ? scanned - 3 : 0; i + 3 < n; ++i) {
+      if (b[i] == '\r' && b[i + 1] == '\n' && b[i + 2] == '\r' && b[i + 3] == '\n') {
+        std::string head(b, i);
+        c.pos += i + 4;
+        std::istringstream hs(head);
+        std::string l;
+        std::getline(hs, l);
+        if (!l.empty() && l.back() == '\r') l.pop_back();
+        std::istringstream rl(l);
+        rl >> r.method >> r.target >> r.version;
+        if (r.method.empty() || r.target.empty()) return false;
+        auto q = r.target.find('?');
+        r.path = q == std::string::npos ? r.target : r.target.substr(0, q);
+        r.query = q == std::string::npos ? "" : r.target.substr(q + 1);
+        while (std::getline(hs, l)) {
+          if (!l.empty() && l.back() == '\r') l.pop_back();
+          auto colon = l.find(':');
+          if (colon == std::string::npos) continue;
+          std::string k = trim(l.substr(0, colon)), v = trim(l.substr(colon + 1));
+          r.headers.emplace_back(k, v);
+          r.h[lower(k)] = v;
+        }
+        std::string cl = r.get("content-length");
+        if (!cl.empty()) r.content_length = std::strtoll(cl.c_str(), nullptr, 10);
+        r.chunked = lower(r.get("transfer-encoding")).find("chunked") != std::string::npos;
+        std::string conn = lower(r.get("connection"));
+        r.keep_alive = r.version == "HTTP/1.1" ? conn.find("close") == std::string::npos
+                                               : conn.find("keep-alive") != std::string::npos;
+        return true;
+      }
+    }
+    scanned = n;
+    if (n > (1 << 20)) return false;  // header too large
+    if (!c.fill()) return false;
+  }
+}
+
+const char* reason(int code) {
+  switch (code) {
+    case 200: return "OK";
+    case 202: return "Accepted";
+    case 204: return "No Content";
+    case 400: return "Bad Request";
+    case 401: return "Unauthorized";
+    case 404: return "Not Found";
+    case 411: return "Length Required";
+    case 413: return "Request Entity Too Large";
+    case 429: return "Too Many Requests";
+    case 500: return "Internal Server Error";
+    case 502: return "Bad Gateway";
+    case 503: return "Service Unavailable";
+    default: return "Status";
+  }
+}
+
+bool respond(Conn& c, int code, const std::string& ctype, const std::string& body, bool keep_alive,
+             const std::string& extra_headers = "") {
+  std::string h = "HTTP/1.1 " + std::to_string(code) + " " + reason(code) + "\r\nContent-Type: " + ctype +
+                  "\r\nContent-Length: " + std::to_string(body.size()) + "\r\n" + extra_headers +
+                  (keep_alive ? "" : "Connection: close\r\n") + "Server: ai4e-ingestd\r\n\r\n";
+  struct iovec iov[2] = {{const_cast<char*>(h.data()), h.size()}, {const_cast<char*>(body.data()), body.size()}};
+  size_t total = h.size() + body.size(), sent = 0;
+  int idx = 0;
+  while (sent < total) {
+    ssize_t k = ::writev(c.fd, iov + idx, 2 - idx);
+    if (k < 0) {
+      if (errno == EINTR) continue;
+      return false;
+    }
+    sent += static_cast<size_t>(k);
+    size_t kk = static_cast<size_t>(k);
+    while (idx < 2 && kk >= iov[idx].iov_len) {
+      kk -= iov[idx].iov_len;
+      ++idx;
+    }
+    if (idx < 2) {
+      iov[idx].iov_base = static_cast<char*>(iov[idx].iov_base) + kk;
+      iov[idx].iov_len -= kk;
+    }
+  }
+  return true;
+}
+
+std::string message_json(const std::string& m) {
+  std::string out = "{\"message\":";
+  ai4e::json_escape_into(out, m);
+  return out + "}";
+}
+
+std::string query_param(const std::string& q, const std::string& name) {
+  for (auto& kv : split(q, '&')) {
+    auto eq = kv.find('=');
+    if (eq != std::string::npos && kv.substr(0, eq) == name) return kv.substr(eq + 1);
+  }
+  return "";
+}
+
+bool ct_equal(const std::string& a, const std::string& b) {  // constant time per candidate
+  if (a.size() != b.size()) return false;
+  unsigned char d = 0;
+  for (size_t i = 0; i < a.size(); ++i) d |= static_cast<unsigned char>(a[i] ^ b[i]);
+  return d == 0;
+}
+
+// nullptr = allowed, else the APIM-style 401 message
+const char* check_key(const Request& r, const Route* route) {
+  std::vector<const std::string*> allowed;
+  for (auto& k : g_cfg.keys) allowed.push_back(&k);
+  if (route)
+    for (auto& k : route->keys) allowed.push_back(&k);
+  if (allowed.empty()) return nullptr;
+  std::string key = r.get(kKeyHeader);
+  if (key.empty()) key = query_param(r.query, "subscription-key");
+  if (key.empty()) return kMissingKey;
+  bool ok = false;
+  for (auto* a : allowed) ok |= ct_equal(key, *a);
+  return ok ? nullptr : kInvalidKey;
+}
+
+Route* match(const std::string& path) {
+  for (auto& r : g_cfg.routes) {
+    const std::string& p = r->prefix;
+    std::string pre = p;
+    while (!pre.empty() && pre.back() == '/') pre.pop_back();
+    if (path == p || path.compare(0, pre.size() + 1, pre + "/") == 0) return r.get();
+  }
+  return nullptr;
+}
+
+// ------------------------------------------------------------------ proxy to the serving process
+int connect_internal() {
+  int fd = ::socket(AF_INET, SOCK_STREAM, 0);
+  sockaddr_in a{};
+  a.sin_family = AF_INET;
+  a.sin_port = htons(static_cast<uint16_t>(g_cfg.internal_port));
+  inet_pton(AF_INET, g_cfg.internal_host.c_str(), &a.sin_addr);
+  if (::connect(fd, reinterpret_cast<sockaddr*>(&a), sizeof(a)) != 0) {
+    ::close(fd);
+    return -1;
+  }
+  int one = 1;
+  setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+  return fd;
+}
+
+bool read_body(Conn& c, const Request& r, std::string& body) {
+  if (r.chunked) {
+    while (true) {
+      std::string l;
+      if (!c.line(l)) return false;
+      size_t n = std::strtoull(l.c_str(), nullptr, 16);
+      if (n == 0) {
+        do {
+          if (!c.line(l)) return false;
+        } while (!l.empty());
+        return true;
+      }
+      size_t off = body.size();
+      body.resize(off + n);
+      if (!c.body_into(reinterpret_cast<uint8_t*>(&body[off]), n)) return false;
+      if (!c.line(l)) return false;
+    }
+  }
+  if (r.content_length > 0) {
+    body.resize(static_cast<size_t>(r.content_length));
+    return c.body_into(reinterpret_cast<uint8_t*>(&body[0]), body.size());
+  }
+  return true;
+}
+
+bool is_hop(const std::string& k) {
+  static const char* hop[] = {"connection", "keep-alive", "proxy-authenticate", "proxy-authorization", "te",
+                              "trailers", "transfer-encoding", "upgrade", "content-length"};
+  std::string l = lower(k);
+  for (auto* h : hop)
+    if (l == h) return true;
+  return false;
+}
+
+bool proxy(Conn& c, const Request& r) {
+  std::string body;
+  if (!read_body(c, r, body)) return false;
+  std::string req = r.method + " " + r.target + " HTTP/1.1\r\n";
+  for (auto& kv : r.headers)
+    if (!is_hop(kv.first)) req += kv.first + ": " + kv.second + "\r\n";
+  req += "Content-Length: " + std::to_string(body.size()) + "\r\nConnection: keep-alive\r\n\r\n";
+  for (int attempt = 0; attempt < 2; ++attempt) {  // a kept-alive upstream may have been closed meanwhile
+    if (c.upstream < 0 && (c.upstream = connect_internal()) < 0) break;
+    if (!write_all(c.upstream, req.data(), req.size()) || !write_all(c.upstream, body.data(), body.size())) {
+      ::close(c.upstream);
+      c.upstream = -1;
+      continue;
+    }
+    Conn up(c.upstream);
+    Request resp;
+    // (the upstream's status line parses with method = version, target = code)
+    if (!read_head(up, resp)) {
+      ::close(c.upstream);
+      c.upstream = -1;
+      up.fd = -1;
+      if (attempt == 0) continue;
+      break;
+    }
+    std::string rbody;
+    bool ok;
+    const int status = std::atoi(resp.target.c_str());
+    if (status < 200 || status == 204 || status == 304 || r.method == "HEAD") {
+      ok = true;  // no body by definition
+    } else if (resp.chunked || resp.content_length >= 0) {
+      ok = read_body(up, resp, rbody);
+    } else {  // no length: until the upstream closes
+      rbody.assign(up.buf.data() + up.pos, up.avail());
+      up.pos = up.end;
+      while (up.fill()) {
+        rbody.append(up.buf.data() + up.pos, up.avail());
+        up.pos = up.end;
+      }
+      ok = true;
+      ::close(c.upstream);
+      c.upstream = -1;
+    }
+    up.fd = -1;  // (the Conn wrapper does not own the upstream socket)
+    if (!ok) {
+      if (c.upstream >= 0) ::close(c.upstream);
+      c.upstream = -1;
+      break;
+    }
+    if (lower(resp.get("connection")).find("close") != std::string::npos && c.upstream >= 0) {
+      ::close(c.upstream);
+      c.upstream = -1;
+    }
+    const int code = status;
+    std::string extra, ctype = "application/octet-stream";
+    for (auto& kv : resp.headers) {
+      std::string l = lower(kv.first);
+      if (is_hop(kv.first) || l == "content-encoding" || l == "server" || l == "date") continue;
+      if (l == "content-type") {
+        ctype = kv.second;
+        continue;
+      }
+      extra += kv.first + ": " + kv.second + "\r\n";
+    }
+    return respond(c, code, ctype, rbody, r.keep_alive, extra);
+  }
+  return respond(c, 502, "application/json", message_json("gateway unreachable"), false) && false;
+}
+
+// ------------------------------------------------------------------ ingest
+std::string task_json(const std::string& tid, const Shard& s) {
+  std::string out = "{\"TaskId\":\"" + tid + "\",\"Timestamp\":";
+  ai4e::json_escape_into(out, ai4e::dotnet_timestamp(ai4e::wall_now()));
+  out += ",\"Status\":\"created\",\"BackendStatus\":\"created\",\"Endpoint\":";
+  ai4e::json_escape_into(out, s.endpoint);
+  out += ",\"Body\":null,\"PublishToGrid\":true,\"EndpointPath\":";
+  ai4e::json_escape_into(out, s.endpoint_path);
+  return out + "}";
+}
+
+std::string py_list(const std::vector<std::string>& v) {  // Python's repr of a list of str
+  std::string out = "[";
+  for (size_t i = 0; i < v.size(); ++i) out += (i ? ", '" : "'") + v[i] + "'";
+  return out + "]";
+}
+
+bool ingest(Conn& c, const Request& r, Route& route, Shard& s, bool batch) {
+  const int64_t nbytes = r.content_length;
+  const bool ka = r.keep_alive;
+  auto reject = [&](int code, const std::string& msg) {  // answer without reading the body: close after
+    respond(c, code, "application/json", message_json(msg), false);
+    return false;
+  };
+  if (g_draining.load()) return reject(503, "Service is terminating, please try again later.");
+  if (route.max_concurrent >= 0 && route.inflight.load() + 1 > route.max_concurrent)
+    return reject(429, "Service is busy, please try again later.");
+  struct Guard {
+    std::atomic<int64_t>& v;
+    explicit Guard(std::atomic<int64_t>& x) : v(x) { v.fetch_add(1); }
+    ~Guard() { v.fetch_sub(1); }
+  } guard(route.inflight);
+  std::string ctype = lower(trim(split(r.get("content-type"), ';')[0]));
+  if (!route.content_types.empty() &&
+      std::find(route.content_types.begin(), route.content_types.end(), ctype) == route.content_types.end())
+    return reject(401, "Content-type must be " + py_list(route.content_types));
+  if (route.max_content_length > 0 && nbytes > route.max_content_length)
+    return reject(413, "Request content too large (" + std::to_string(nbytes) +
+                           "). Must be smaller than: " + std::to_string(route.max_content_length));
+  if (nbytes <= 0 || nbytes % s.item)
+    return reject(400, "batch payload must be a multiple of " + std::to_string(s.item) + " bytes (uint8 " +
+                           s.shape_str + ")");
+  const int64_t n = nbytes / s.item;
+  if (n > s.len)
+    return reject(413, "batch of " + std::to_string(n) + " items exceeds the ingest partition (" +
+                           std::to_string(s.len) + " slots)");
+  if (lower(r.get("expect")) == "100-continue" && !write_all(c.fd, "HTTP/1.1 100 Continue\r\n\r\n", 25)) return false;
+  std::vector<int64_t> sl = s.slots->alloc(n, g_cfg.alloc_timeout);
+  if (sl.empty()) {  // no ring slot in time: nothing was created
+    if (!c.discard(static_cast<size_t>(nbytes))) return false;
+    return respond(c, 429, "application/json", message_json("Service is busy, please try again later."), ka);
+  }
+  // body -> ring: one recv per contiguous slot run
+  for (size_t i = 0; i < sl.size();) {
+    size_t j = i + 1;
+    while (j < sl.size() && sl[j] == sl[j - 1] + 1) ++j;
+    if (!c.body_into(s.ring + sl[i] * s.item, static_cast<size_t>((j - i) * s.item))) {
+      s.slots->free(sl);
+      return false;
+    }
+    i = j;
+  }
+  // B3: a child span of the caller's (utils/tracing.py b3_from_headers / b3_pack)
+  std::string trace_id = r.get("x-b3-traceid"), parent = r.get("x-b3-spanid"), sampled = r.get("x-b3-sampled");
+  if (trace_id.empty()) trace_id = hexid(c.rng, 128);
+  std::string span = hexid(c.rng, 64);
+  if (sampled.empty()) sampled = "1";
+  std::string b3 = "x-b3-traceid: " + trace_id + "\r\nx-b3-spanid: " + span + "\r\nx-b3-parentspanid: " + parent +
+                   "\r\nx-b3-sampled: " + sampled + "\r\n";
+  std::vector<std::string> ids = s.mint(static_cast<size_t>(n));
+  const uint64_t tok = s.submit(sl, ids, trace_id + "/" + span + "/" + parent);
+  const int64_t created = s.wait_ack(tok, g_cfg.ack_timeout);
+  if (batch) {
+    std::string body = "{\"TaskIds\":[";
+    for (size_t i = 0; i < ids.size(); ++i) body += (i ? ",\"" : "\"") + ids[i] + "\"";
+    body += "]";
+    if (created < 0) body += ",\"message\":\"accepted, not yet acknowledged\"";
+    body += "}";
+    return respond(c, created < 0 ? 202 : 200, "application/json", body, ka, b3);
+  }
+  if (created == 0)
+    return respond(c, 500, "application/json", message_json("Task insert failed."), ka, b3);
+  std::string accept = r.get("accept");
+  if (accept.empty() || accept.find("application/json") != std::string::npos ||
+      accept.find("*/*") != std::string::npos)
+    return respond(c, created < 0 ? 202 : 200, "application/json", task_json(ids[0], s), ka, b3);
+  return respond(c, created < 0 ? 202 : 200, "text/plain; charset=utf-8", "TaskId: " + ids[0], ka, b3);
+}
+
+void serve_conn(int fd) {
+  int one = 1;
+  setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+  int rcv = 4 << 20;
+  setsockopt(fd, SOL_SOCKET, SO_RCVBUF, &rcv, sizeof(rcv));
+  Conn c(fd);
+  while (true) {
+    Request r;
+    if (!read_head(c, r)) break;
+    Route* route = match(r.path);
+    if (r.path != "/" && r.path != "/openapi.json") {
+      if (const char* msg = check_key(r, route)) {
+        std::string body = "{\"statusCode\":401,\"message\":";
+        ai4e::json_escape_into(body, msg);
+        body += "}";
+        bool drained = r.chunked ? false : c.discard(static_cast<size_t>(std::max<int64_t>(0, r.content_length)));
+        if (!respond(c, 401, "application/json", body, r.keep_alive && drained) || !r.keep_alive || !drained) break;
+        continue;
+      }
+    }
+    bool ok;
+    std::string ctype = lower(trim(split(r.get("content-type"), ';')[0]));
+    Shard* s = route && route->shard >= 0 ? g_cfg.shards[static_cast<size_t>(route->shard)].get() : nullptr;
+    const bool ingestible = s && route->mode == "async" && (r.method == "POST" || r.method == "PUT") &&
+                            r.get("taskid").empty() && !r.chunked && r.content_length >= 0;
+    if (ingestible && ctype == kBatchType && r.content_length > 0) {
+      ok = ingest(c, r, *route, *s, true);
+    } else if (ingestible && ctype == kRawType && r.content_length == s->item) {
+      ok = ingest(c, r, *route, *s, false);
+    } else {
+      ok = proxy(c, r);  // encoded images, task API, sync routes, ... -> the serving process
+    }
+    if (!ok || !r.keep_alive) break;
+  }
+  ::close(fd);
+}
+
+int listen_on(const std::string& host, int port) {
+  int fd = ::socket(AF_INET, SOCK_STREAM, 0);
+  int one = 1;
+  setsockopt(fd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
+  setsockopt(fd, SOL_SOCKET, SO_REUSEPORT, &one, sizeof(one));
+  sockaddr_in a{};
+  a.sin_family = AF_INET;
+  a.sin_port = htons(static_cast<uint16_t>(port));
+  if (inet_pton(AF_INET, host == "0.0.0.0" || host.empty() ? "0.0.0.0" : host.c_str(), &a.sin_addr) != 1)
+    a.sin_addr.s_addr = htonl(INADDR_ANY);
+  if (::bind(fd, reinterpret_cast<sockaddr*>(&a), sizeof(a)) != 0 || ::listen(fd, 1024) != 0) {
+    std::perror("ai4e_ingestd: bind/listen");
+    std::exit(3);
+  }
+  return fd;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  if (argc < 2) {
+    std::fprintf(stderr, "usage: ai4e_ingestd CONFIG\n");
+    return 2;
+  }
+  signal(SIGPIPE, SIG_IGN);
+  parse_config(argv[1]);
+  struct sigaction sa{};
+  sa.sa_handler = [](int) {  // drain: refuse new ingest (503), let in-flight requests finish, then exit
+    g_draining.store(true);
+    alarm(5);
+  };
+  sigaction(SIGTERM, &sa, nullptr);
+  struct sigaction al{};
+  al.sa_handler = [](int) { std::_Exit(0); };
+  sigaction(SIGALRM, &al, nullptr);
+  for (auto& s : g_cfg.shards) std::thread([p = s.get()] { p->reader(); }).detach();
+  int lfd = listen_on(g_cfg.host, g_cfg.port);
+  std::fprintf(stderr, "ai4e_ingestd pid %d on %s:%d (%zu endpoints, %zu routes)\n", getpid(), g_cfg.host.c_str(),
+               g_cfg.port, g_cfg.shards.size(), g_cfg.routes.size());
+  while (true) {
+    int fd = ::accept(lfd, nullptr, nullptr);
+    if (fd < 0) {
+      if (errno == EINTR) continue;
+      continue;
+    }
+    std::thread(serve_conn, fd).detach();
+  }
+}

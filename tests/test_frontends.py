@@ -1,21 +1,26 @@
-"""Ingest front-end processes (runtime/frontend.py): the platform CLI with AI4E_FRONTEND_PROCESSES=2 —
-async POSTs over fresh connections land on the serving process or on a front-end (SO_REUSEPORT), every
-task completes and is visible through the task API (proxied to the serving process), batch ingest and
-sync routes work through any listener."""
+"""Ingest front-end processes — native (csrc/ingest/ingestd.cpp, runtime/native_frontend.py) and Python
+(runtime/frontend.py): the platform CLI with AI4E_FRONTEND_PROCESSES=2 — async POSTs over fresh connections
+land on the serving process or on a front-end (SO_REUSEPORT), every task completes and is visible through the
+task API (proxied to the serving process), batch ingest and sync routes work through any listener; admission
+(keys, content type, length) answers the same whichever process accepts the connection."""
+import json
 import os
 import subprocess
 import sys
 import time
 
 import numpy as np
+import pytest
 import requests
+import yaml
 
 from test_serve_e2e import ROOT, _port
 
 
-def test_frontend_processes_end_to_end():
+@pytest.mark.parametrize("impl", ["native", "python"])
+def test_frontend_processes_end_to_end(impl):
     port = _port()
-    env = dict(os.environ, PYTHONPATH=ROOT, AI4E_FRONTEND_PROCESSES="2")
+    env = dict(os.environ, PYTHONPATH=ROOT, AI4E_FRONTEND_PROCESSES="2", AI4E_FRONTEND_IMPL=impl)
     proc = subprocess.Popen([sys.executable, "-m", "aiforearth_api_platform_amd.serve", "--config",
                              os.path.join(ROOT, "examples", "platform_cpu.yaml"), "--port", str(port)],
                             cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
@@ -60,7 +65,101 @@ def test_frontend_processes_end_to_end():
         assert res["classes"][0] == 1
         r = requests.post(base + "/v1/tiny/sync", data=img.tobytes(), headers={"Connection": "close"})
         assert r.status_code == 200 and r.json()["classes"][0] == 1
-        assert "ingest_frontends=2" in _drain(proc)
+        out = _drain(proc)
+        assert "ingest_frontends=2" in out
+        assert ("ai4e_ingestd pid" in out) == (impl == "native")
+    finally:
+        proc.terminate()
+        try:
+            proc.wait(20)
+        except subprocess.TimeoutExpired:
+            proc.kill()
+
+
+def test_native_frontend_admission_parity(tmp_path):
+    """Subscription keys (global + per route), content type, length and payload-size errors through a native
+    front-end and the serving process: every request class gets the same status on both paths, the ids it
+    mints are real tasks, and encoded / odd-sized payloads fall through to the serving process."""
+    from aiforearth_api_platform_amd.gateway.security import KEY_HEADER
+
+    doc = yaml.safe_load(open(os.path.join(ROOT, "examples", "platform_cpu.yaml")))
+    doc["routes"] = [
+        {"prefix": "/v1/tiny/async", "mode": "async", "backend": "inproc:tiny", "max_content_length": 4096},
+        {"prefix": "/v1/tiny/keyed", "mode": "async", "backend": "inproc:tiny", "keys": ["tiny-key"],
+         "content_types": ["application/octet-stream"]},
+        {"prefix": "/v1/tiny/sync", "mode": "sync", "backend": "inproc:tiny"},
+    ]
+    cfgp = tmp_path / "platform.yaml"
+    cfgp.write_text(yaml.safe_dump(doc))
+    port = _port()
+    env = dict(os.environ, PYTHONPATH=ROOT, AI4E_FRONTEND_PROCESSES="2", AI4E_FRONTEND_IMPL="native",
+               AI4E_SUBSCRIPTION_KEYS="gk")
+    proc = subprocess.Popen([sys.executable, "-m", "aiforearth_api_platform_amd.serve", "--config", str(cfgp),
+                             "--port", str(port)], cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+    base = f"http://127.0.0.1:{port}"
+    s = requests.Session()
+    s.trust_env = False
+    try:
+        for _ in range(600):
+            try:
+                if s.get(base + "/", timeout=1).status_code == 200:
+                    break
+            except requests.ConnectionError:
+                time.sleep(0.1)
+        else:
+            raise AssertionError("server did not come up")
+        time.sleep(2.0)
+        img = np.zeros((4, 4, 3), np.uint8)
+        img[..., 2] = 90
+        ob = {"Content-Type": "application/octet-stream", "Connection": "close"}
+        bt = {"Content-Type": "application/x-ai4e-batch", "Connection": "close"}
+        cases = [  # (path, headers, body, expected status)
+            ("/v1/tiny/async", ob, img.tobytes(), 401),
+            ("/v1/tiny/async", dict(ob, **{KEY_HEADER: "wrong"}), img.tobytes(), 401),
+            ("/v1/tiny/async", dict(ob, **{KEY_HEADER: "gk"}), img.tobytes(), 200),
+            ("/v1/tiny/async?subscription-key=gk", ob, img.tobytes(), 200),
+            ("/v1/tiny/async", dict(bt, **{KEY_HEADER: "gk"}), np.repeat(img[None], 3, 0).tobytes(), 200),
+            ("/v1/tiny/async", dict(bt, **{KEY_HEADER: "gk"}), b"\x00" * 50, 400),   # not a multiple of the item
+            ("/v1/tiny/async", dict(ob, **{KEY_HEADER: "gk"}), b"\x00" * 5000, 413),
+            ("/v1/tiny/async", dict(ob, **{KEY_HEADER: "gk"}), b"\x00" * 7, 400),    # odd size: decoded upstream
+            ("/v1/tiny/keyed", dict(ob, **{KEY_HEADER: "tiny-key"}), img.tobytes(), 200),
+            ("/v1/tiny/keyed", dict(bt, **{KEY_HEADER: "tiny-key"}), img.tobytes(), 401),  # type not accepted
+            ("/v1/tiny/keyed", dict(ob, **{KEY_HEADER: "gk", "Content-Type": "image/png"}), img.tobytes(), 401),
+        ]
+        ids, servers = [], set()
+        for _ in range(8):  # fresh connections: the kernel spreads them over the three listeners
+            for path, hdr, body, want in cases:
+                r = s.post(base + path, data=body, headers=hdr)
+                assert r.status_code == want, (path, hdr, r.status_code, r.text)
+                servers.add(r.headers.get("Server", "").startswith("ai4e-ingestd"))
+                if want == 200:
+                    js = r.json()
+                    ids += js["TaskIds"] if "TaskIds" in js else [js["TaskId"]]
+                    assert r.headers.get("x-b3-traceid")
+        assert servers == {True, False}  # both the native front-ends and the serving process answered
+        # keep-alive: several requests on one connection, batch + proxied task queries interleaved
+        ka = requests.Session()
+        ka.trust_env = False
+        for _ in range(10):
+            r = ka.post(base + "/v1/tiny/async", data=img.tobytes(),
+                        headers={"Content-Type": "application/octet-stream", KEY_HEADER: "gk"})
+            assert r.status_code == 200
+            ids.append(r.json()["TaskId"])
+            assert ka.get(f"{base}/v1/taskmanagement/task/{ids[-1]}", headers={KEY_HEADER: "gk"}).status_code == 200
+        deadline = time.time() + 60
+        pending = set(ids)
+        while pending and time.time() < deadline:
+            for t in list(pending):
+                r = s.get(f"{base}/v1/taskmanagement/task/{t}", headers={KEY_HEADER: "gk", "Connection": "close"})
+                if r.status_code == 200 and r.json()["BackendStatus"] == "completed":
+                    pending.discard(t)
+            time.sleep(0.05)
+        assert not pending
+        r = s.get(f"{base}/v1/taskmanagement/task/{ids[0]}/result", headers={KEY_HEADER: "gk"})
+        assert r.json()["Result"]["classes"][0] == 2
+        assert s.get(f"{base}/v1/taskmanagement/task/nope", headers={KEY_HEADER: "gk"}).status_code == 204
+        assert json.loads(s.get(base + "/openapi.json").text)["openapi"].startswith("3.")
+        assert "ai4e_ingestd pid" in _drain(proc)
     finally:
         proc.terminate()
         try:
