@@ -78,29 +78,34 @@ def _kernel_sources():
     return sorted((CSRC / "kernels").glob("*.hip"))
 
 
-def build_kernels(verbose: bool = False, force: bool = False, jobs: int = 8) -> Path:
+def build_kernels(verbose: bool = False, force: bool = False, jobs: int = 8, defines=(), variant: str = "") -> Path:
+    """``defines`` + ``variant``: an A/B build of the library (``_lib/libai4e_kernels_<variant>.so``, objects in
+    their own directory), loaded with AI4E_KERNEL_LIB=<path> (ops/_ext.py)."""
     srcs = _kernel_sources()
     headers = sorted((CSRC / "kernels").glob("*.h"))
+    objdir = OBJDIR if not variant else OBJDIR.parent / f"obj_{variant}"
+    out_so = KERNEL_SO if not variant else LIBDIR / f"libai4e_kernels_{variant}.so"
     LIBDIR.mkdir(parents=True, exist_ok=True)
-    OBJDIR.mkdir(parents=True, exist_ok=True)
+    objdir.mkdir(parents=True, exist_ok=True)
     hipcc = _hipcc()
     # -amdgpu-mfma-vgpr-form: MFMA accumulators in arch VGPRs (gfx950 has one unified 512-entry
     # file per SIMD); with AGPR accumulators hipcc shuttled them AGPR<->VGPR inside the K1 loop.
     flags = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
-             "-mllvm", "-amdgpu-mfma-vgpr-form=1", "-Wno-unused-result", f"-I{CSRC / 'kernels'}"]
+             "-mllvm", "-amdgpu-mfma-vgpr-form=1", "-Wno-unused-result", f"-I{CSRC / 'kernels'}",
+             *[f"-D{d}" for d in defines]]
 
     def one(src: Path) -> Path:
-        obj = OBJDIR / (src.stem + ".o")
+        obj = objdir / (src.stem + ".o")
         if force or _stale(obj, [src, *headers]):
             _run([hipcc, *flags, "-c", str(src), "-o", str(obj)], verbose)
         return obj
 
     with cf.ThreadPoolExecutor(max_workers=max(1, min(jobs, len(srcs) or 1))) as ex:
         objs = list(ex.map(one, srcs))
-    if force or _stale(KERNEL_SO, objs):
-        _run([hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs), "-o", str(KERNEL_SO)],
+    if force or _stale(out_so, objs):
+        _run([hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs), "-o", str(out_so)],
              verbose)
-    return KERNEL_SO
+    return out_so
 
 
 INGESTD = LIBDIR / "ai4e_ingestd"

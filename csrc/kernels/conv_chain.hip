@@ -563,7 +563,7 @@ void conv_chain_kernel(const ChainParams p) {
       const int g = tid + 256 * e;
       const int r = g / CPR, cq = g % CPR;
       const uint4 v = *reinterpret_cast<const uint4*>(tile + (cq >> 2) * BM * 64 + r * 64 + (((cq & 3) ^ swz(r)) << 4));
-      *reinterpret_cast<uint4*>(base[e] + coff) = v;
+      ai4e_conv::st16_stream(base[e] + coff, v);
     }
     ops += N;
   };
@@ -583,7 +583,7 @@ void conv_chain_kernel(const ChainParams p) {
       const int q = wave + 4 * s;
       const int kb = q / (BM / 16), rb = q % (BM / 16);
       const int row = rb * 16 + rin;
-      glds16(p.res + static_cast<long>(min(m0 + row, p.M - 1)) * C4 + pp * 64 + kb * BK + 8 * c,
+      ai4e_conv::glds16_stream(p.res + static_cast<long>(min(m0 + row, p.M - 1)) * C4 + pp * 64 + kb * BK + 8 * c,
              sb + Cfg::T2_BYTES + kb * BM * 64 + rb * 16 * 64);
     }
     ops += DOWN ? 0 : Cfg::NR;

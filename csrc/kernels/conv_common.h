@@ -16,6 +16,37 @@ __device__ __forceinline__ int swz(int row) { return (0x78 >> (2 * ((row >> 2) &
 // tracked by hand with counted vmcnt. The swizzle is applied to the per-lane SOURCE address.
 // M0 is saved and restored around the DMA: hipcc treats M0 as a reserved register and ignores it in a clobber
 // list (-Winline-asm), so a live M0 of its own (s_movrel indexing) would otherwise be corrupted silently.
+// Streaming-hint variants (AI4E_STREAM_HINTS=1 builds): activations that are read or written exactly once
+// carry the non-temporal policy so they do not evict the weights every workgroup re-reads from L2.
+#ifndef AI4E_STREAM_HINTS
+#define AI4E_STREAM_HINTS 0
+#endif
+__device__ __forceinline__ void glds16_stream(const void* gsrc, uint32_t lds_base) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+#if AI4E_STREAM_HINTS
+      "global_load_lds_dwordx4 %1, off nt\n\t"
+#else
+      "global_load_lds_dwordx4 %1, off\n\t"
+#endif
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(lds_base))
+      : "memory");
+}
+
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st16_stream(void* dst, const uint4& v) {
+#if AI4E_STREAM_HINTS
+  __builtin_nontemporal_store(u32x4_t{v.x, v.y, v.z, v.w}, reinterpret_cast<u32x4_t*>(dst));
+#else
+  *reinterpret_cast<uint4*>(dst) = v;
+#endif
+}
+
 __device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_base) {
   uint32_t keep;
   asm volatile(
