@@ -1,5 +1,6 @@
 #!/bin/bash
-# Round-3 GPU session: focused tests, smoke, benches at several step counts, optional full suite + profile.
+# Round-3 GPU session: smoke, benches at several step counts, extra command, focused tests, optional full
+# suite + profile.
 # Each GPU step has its own time limit; any failure/fault/timeout stops the session.
 #   TESTS="tests/x.py"   focused pytest
 #   SMOKE=1              __graft_entry__.smoke()
@@ -21,9 +22,6 @@ run() {  # name timeout cmd...
   if [ $rc -ne 0 ]; then echo "STOP after $name"; exit $rc; fi
 }
 python -c "import __graft_entry__ as g; g.build()" > gpurun_out/build.log 2>&1 || { tail gpurun_out/build.log; exit 3; }
-if [ -n "${TESTS:-}" ]; then
-  run focus 400 python -u -m pytest -x -v --timeout 240 --timeout-method thread -p no:cacheprovider $TESTS
-fi
 if [ -n "${SMOKE:-}" ]; then
   run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()"
 fi
@@ -34,6 +32,9 @@ for sw in ${BENCHES:-}; do
 done
 if [ -n "${EXTRA:-}" ]; then
   run extra 400 $EXTRA
+fi
+if [ -n "${TESTS:-}" ]; then
+  run focus 400 python -u -m pytest -x -v --timeout 240 --timeout-method thread -p no:cacheprovider $TESTS
 fi
 if [ -n "${FULL:-}" ]; then
   run pytest_gpu 900 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread -p no:cacheprovider
