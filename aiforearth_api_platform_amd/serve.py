@@ -112,7 +112,7 @@ def build_platform(doc: Dict[str, Any], cfg: Config):
         if e.get("mode", "pool") == "pool":
             spec = ModelSpec(e["factory"], shape, mb, int(e.get("topk", 5)), dict(e.get("kwargs") or {}), graphs,
                              tuple(buckets), tuple(base_url + p for p in e.get("stage_paths", [])),
-                             int(e.get("group_size", 1)))
+                             int(e.get("group_size", 1)), int(e.get("group_leaders", 1)))
             pool = WorkerPool(cp, base_url + e["path"], spec, devs, max_delay_s=cfg.max_batch_delay_ms / 1e3,
                               heartbeat_interval_s=cfg.heartbeat_interval_s,
                               heartbeat_timeout_s=cfg.heartbeat_timeout_s,

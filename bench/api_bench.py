@@ -52,6 +52,8 @@ def main():
     ap.add_argument("--inflight", type=int, default=2)
     ap.add_argument("--device", default="cuda")
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--graphs", default="auto", choices=["auto", "on", "off"],
+                    help="capture the whole servable per batch bucket in HIP graphs (auto: the model's default)")
     ap.add_argument("--http", type=int, default=0)
     ap.add_argument("--http-seconds", type=float, default=6.0)
     ap.add_argument("--json-out", default="")
@@ -88,6 +90,8 @@ def main():
         extra.update(parallelism=f"pipeline{leaders}:{a.classifiers}", wire_dtype=a.wire,
                      stage_dtypes={"detector": "bf16", "classifier": a.classifier_dtype})
         dtype = a.classifier_dtype if a.classifier_dtype == "bf16" else "bf16 detector / fp16 classifier"
+    if a.graphs != "auto":
+        graphs = a.graphs == "on"
     spec = ModelSpec(factory, shape(size), a.batch, 5, kwargs, graphs, (), stages, group, leaders)
     run_node_bench(a, spec, path, metric, unit, dtype=dtype,
                    config={"model": a.model, "image_size": size, "api": "async", **extra,
