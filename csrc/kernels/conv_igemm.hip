@@ -384,7 +384,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC > 2 ? O
       if (m < p.M && n < p.Kout) {
         uint16_t* dst = p.y + static_cast<long>(m) * p.ldy + p.ycoff + n;
         if (n + 8 <= p.Kout) {
-          *reinterpret_cast<uint4*>(dst) = o;
+          ai4e_conv::st16_stream(dst, o);
         } else {
           *reinterpret_cast<uint2*>(dst) = make_uint2(o.x, o.y);  // Kout % 8 == 4 tail
         }
@@ -750,7 +750,7 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
       const float f[8] = {v0.x + b0.x, v0.y + b0.y, v0.z + b0.z, v0.w + b0.w,
                           v1.x + b1.x, v1.y + b1.y, v1.z + b1.z, v1.w + b1.w};
       const uint4 o = epilogue8<F16>(f, p.res != nullptr, rv[e], (p.relu & 1) != 0);
-      if (m < p.M && n < p.Kout) *reinterpret_cast<uint4*>(p.y + static_cast<long>(m) * p.ldy + p.ycoff + n) = o;
+      if (m < p.M && n < p.Kout) ai4e_conv::st16_stream(p.y + static_cast<long>(m) * p.ldy + p.ycoff + n, o);
     }
     __syncthreads();
   }

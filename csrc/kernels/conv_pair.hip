@@ -21,6 +21,7 @@
 // ahead. The residual is read in the accumulator layout (4 channels per lane), so the epilogue never
 // shuffles. T1' leaves through the (then idle) T2 region with 16-B row stores.
 #include "common.h"
+#include "conv_common.h"
 
 namespace {
 
@@ -214,7 +215,7 @@ __global__ __launch_bounds__(512) void conv_pair_kernel(const PairParams p) {
       const int g = tid + 512 * e;
       const int r = g >> 4, cq = g & 15;
       const uint4 v = *reinterpret_cast<const uint4*>(ybuf + (cq >> 2) * KBS + r * 64 + (((cq & 3) ^ pswz(r)) << 4));
-      if (m0 + r < p.M) *reinterpret_cast<uint4*>(p.y + static_cast<long>(m0 + r) * C4 + pass * PR_CH + 8 * cq) = v;
+      if (m0 + r < p.M) ai4e_conv::st16_stream(p.y + static_cast<long>(m0 + r) * C4 + pass * PR_CH + 8 * cq, v);
     }
     __builtin_amdgcn_sched_barrier(0);
 
@@ -255,7 +256,7 @@ __global__ __launch_bounds__(512) void conv_pair_kernel(const PairParams p) {
     const int g = tid + 512 * e;
     const int r = g / (MIDN / 8), cq = g % (MIDN / 8);
     const uint4 v = *reinterpret_cast<const uint4*>(t2s + (cq >> 2) * KBS + r * 64 + (((cq & 3) ^ pswz(r)) << 4));
-    if (m0 + r < p.M) *reinterpret_cast<uint4*>(p.t1n + static_cast<long>(m0 + r) * MIDN + 8 * cq) = v;
+    if (m0 + r < p.M) ai4e_conv::st16_stream(p.t1n + static_cast<long>(m0 + r) * MIDN + 8 * cq, v);
   }
 }
 

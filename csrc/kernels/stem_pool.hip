@@ -172,7 +172,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
         mx.z = max_bf16x2(mx.z, v.z);
         mx.w = max_bf16x2(mx.w, v.w);
       }
-    *reinterpret_cast<uint4*>(p.y + ((static_cast<long>(img) * p.PH + ph) * p.PW + pw) * SP_BN + 8 * k8) = mx;
+    ai4e_conv::st16_stream(p.y + ((static_cast<long>(img) * p.PH + ph) * p.PW + pw) * SP_BN + 8 * k8, mx);
   }
 }
 
@@ -400,7 +400,7 @@ void stem_pool_direct_kernel(const StemParams p, int ntiles) {
           mx.z = max_bf16x2(mx.z, v.z);
           mx.w = max_bf16x2(mx.w, v.w);
         }
-      *reinterpret_cast<uint4*>(p.y + ((static_cast<long>(img) * p.PH + ph) * p.PW + pw) * SP_BN + 8 * k8) = mx;
+      ai4e_conv::st16_stream(p.y + ((static_cast<long>(img) * p.PH + ph) * p.PW + pw) * SP_BN + 8 * k8, mx);
       mxs[e] = mx;
     }
     if constexpr (C1) {
