@@ -170,8 +170,10 @@ class SegmenterServable(Servable):
     def __call__(self, images_u8):
         maps = [self.segmenter(images_u8[i]) for i in range(images_u8.shape[0])]
         cls = torch.stack(maps)
-        hist = torch.stack([torch.bincount(m.reshape(-1).long(), minlength=self.n_classes)[: self.n_classes]
-                            for m in maps])
+        # per-class pixel counts without a host sync (bincount sizes its output from the data), so the whole
+        # servable can be captured in a HIP graph
+        classes = torch.arange(self.n_classes, device=cls.device, dtype=cls.dtype)
+        hist = (cls.reshape(cls.shape[0], 1, -1) == classes[None, :, None]).sum(-1)
         return cls, hist
 
     @staticmethod
