@@ -208,9 +208,36 @@ constexpr int FP_SLOTS = 2 * FP_STRIDE;                                 // 736 1
 constexpr int FP_DMA = (FP_SLOTS + 255) / 256;                          // DMA instrs per wave (3)
 constexpr int D_W = 0, D_FP = 64 * 512, D_TILE = D_FP + FP_DMA * 4 * 1024, D_LDS = D_TILE + SP_BM * 128;
 
+// Diagnostic build (AI4E_STEM_STAMPS=1): s_memtime stamps between the loop's phases, summed per wave and
+// written once per wave to g_stem_stamps (read by ai4e_stem_stamps_read). Never used for timing: read SHARES.
+#ifndef AI4E_STEM_STAMPS
+#define AI4E_STEM_STAMPS 0
+#endif
+constexpr int STEM_NSEG = 8;
+#if AI4E_STEM_STAMPS
+__device__ unsigned long long g_stem_stamps[2048 * 4 * STEM_NSEG];
+#define STEM_STAMP(k)                                                                          \
+  do {                                                                                         \
+    __builtin_amdgcn_sched_barrier(0);                                                         \
+    unsigned long long _t;                                                                     \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");               \
+    __builtin_amdgcn_sched_barrier(0);                                                         \
+    st_sum[k] += _t - st_last;                                                                 \
+    st_last = _t;                                                                              \
+  } while (0)
+#else
+#define STEM_STAMP(k) \
+  do {                \
+  } while (0)
+#endif
+
 template <bool U8, bool C1 = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void stem_pool_direct_kernel(const StemParams p, int ntiles) {
+#if AI4E_STEM_STAMPS
+  unsigned long long st_sum[STEM_NSEG] = {0, 0, 0, 0, 0, 0, 0, 0}, st_last;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_last)::"memory");
+#endif
   extern __shared__ __attribute__((aligned(1024))) uint8_t dsm[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -306,12 +333,14 @@ void stem_pool_direct_kernel(const StemParams p, int ntiles) {
     // this tile's footprint landed. From the second tile on (C1) the DMA is already complete: the previous
     // iteration waited for its c1 weight loads, issued after the DMA (vmcnt retires in issue order), so only the
     // previous tile's stores can be outstanding (<= 2 pooled-row + 4 t1 stores per wave): they may stay in flight
+    STEM_STAMP(7);  // (U8 preprocess / loop overhead)
     if (C1 && !U8 && t != static_cast<int>(blockIdx.x)) {
       wait_vmcnt<6>();
     } else {
       wait_vmcnt<0>();
     }
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // footprint (and weights) visible
+    STEM_STAMP(0);  // footprint wait + barrier
 
     f32x4_t acc[4][4];
 #pragma unroll
@@ -337,10 +366,12 @@ void stem_pool_direct_kernel(const StemParams p, int ntiles) {
         for (int j = 0; j < 4; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[j], fx[i], acc[i][j], 0, 0, 0);
     }
+    STEM_STAMP(1);  // MFMA loop
     if constexpr (!U8) {
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // every wave finished reading the footprint
       if (t + static_cast<int>(gridDim.x) < ntiles) issue_fp(t + gridDim.x);
     }
+    STEM_STAMP(2);  // barrier + next footprint DMA issue
     // epilogue: bf16 relu(acc + b) -> tile [256 px][64 ch] (ptile layout)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -359,6 +390,7 @@ void stem_pool_direct_kernel(const StemParams p, int ntiles) {
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    STEM_STAMP(3);  // epilogue tile writes + barrier
     // fused c1 operands, issued now so the L2 latency hides under the pooling: W1 fragments (output-channel
     // rows 16j + lane&15, k-chunk lane>>4 of k-step ks; 8 KB, L2-resident) and the bias
     bf16x8_t w1f[4][2];
@@ -403,6 +435,7 @@ void stem_pool_direct_kernel(const StemParams p, int ntiles) {
       ai4e_conv::st16_stream(p.y + ((static_cast<long>(img) * p.PH + ph) * p.PW + pw) * SP_BN + 8 * k8, mx);
       mxs[e] = mx;
     }
+    STEM_STAMP(4);  // c1 operand loads issue + pooling + pooled stores
     if constexpr (C1) {
       // pooled rows q as the c1 B operand [k-block k8/4][64 rows][4 x 16-B chunks ^ swz(q)], staged in the tile
       // region once every wave has finished pooling from it (the footprint region holds the next tile's DMA)
@@ -416,6 +449,7 @@ void stem_pool_direct_kernel(const StemParams p, int ntiles) {
     }
     // the next tile's epilogue overwrites what this tile's readers still use
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    STEM_STAMP(5);  // c1 operand staging + barriers
     if constexpr (C1) {
       // t1 = relu(W1 . pooled + b1) for the tile's 56 pooled pixels (wave w: rows 16w..16w+15; rows >= 56 and
       // pooled pixels outside the image are computed from stale LDS and never stored)
@@ -441,7 +475,15 @@ void stem_pool_direct_kernel(const StemParams p, int ntiles) {
       }
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // pooled rows read before the next epilogue
     }
+    STEM_STAMP(6);  // c1 MFMA + t1 stores + barrier
   }
+#if AI4E_STEM_STAMPS
+  if (lane == 0 && blockIdx.x < 2048) {
+    const int w = static_cast<int>(blockIdx.x) * 4 + wave;
+#pragma unroll
+    for (int k = 0; k < STEM_NSEG; ++k) g_stem_stamps[w * STEM_NSEG + k] = st_sum[k];
+  }
+#endif
 }
 
 template <bool U8, bool C1 = false>
@@ -573,3 +615,11 @@ AI4E_API int ai4e_stem_pool_fwd(const void* x, const void* w, const void* bias, 
   hipLaunchKernelGGL(stem_pool_kernel, dim3(static_cast<unsigned>(nb)), dim3(256), 0, stream, p);
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
 }
+
+#if AI4E_STEM_STAMPS
+// Diagnostic build only: per-wave phase cycle sums of the last direct-stem launch (2048 x 4 waves x 8).
+AI4E_API int ai4e_stem_stamps_read(void* host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stem_stamps), sizeof(g_stem_stamps)) == hipSuccess ? AI4E_OK
+                                                                                                    : AI4E_ELAUNCH;
+}
+#endif
