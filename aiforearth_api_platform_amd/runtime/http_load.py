@@ -108,7 +108,12 @@ def run_native_clients(url: str, seconds: float, conc: int, body: bytes, content
     out = {"ids": [], "t0": float("inf"), "t1": 0.0, "errors": 0, "requests": 0, "bytes_sent": 0.0,
            "client_cpu_s": 0.0, "client_processes": procs, "connections": procs * conc}
     for i, p in enumerate(ps):
-        so, se = p.communicate(timeout=seconds + 120)
+        try:
+            so, se = p.communicate(timeout=seconds + 90)
+        except subprocess.TimeoutExpired:
+            for q in ps:
+                q.kill()
+            raise
         if p.returncode != 0:
             raise RuntimeError(f"ai4e_http_load failed ({p.returncode}): {se[-500:]}")
         st = json.loads(so.strip().splitlines()[-1])

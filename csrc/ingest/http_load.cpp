@@ -123,6 +123,9 @@ int dial(const char* host, int port) {
   int one = 1, snd = 4 << 20;
   setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
   setsockopt(fd, SOL_SOCKET, SO_SNDBUF, &snd, sizeof(snd));
+  struct timeval tv {30, 0};  // a stalled server ends the run with errors instead of hanging it
+  setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
+  setsockopt(fd, SOL_SOCKET, SO_SNDTIMEO, &tv, sizeof(tv));
   return fd;
 }
 
