@@ -1,5 +1,5 @@
 #!/bin/bash
-# Same-box A/B session: each "label|env assignments|command" line of $AB_FILE runs under its own time limit,
+# Same-box A/B session: each "label|env assignments|seconds|command" line of $AB_FILE runs under its own time limit,
 # writes gpurun_out/ab_<label>.log, and the session stops at the first failure (no retries on the GPU).
 #   AB_FILE=tools/ab_r3.txt bash tools/gpu_ab_r3.sh
 set -u
@@ -7,11 +7,11 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 python -c "import __graft_entry__ as g; g.build()" > gpurun_out/build.log 2>&1 || { tail gpurun_out/build.log; exit 3; }
-while IFS='|' read -r label envs cmd; do
+while IFS='|' read -r label envs secs cmd; do
   [ -z "$label" ] && continue
   case "$label" in \#*) continue ;; esac
   echo "=== $label: $envs $cmd"
-  env $envs timeout -k 10 420 $cmd > "gpurun_out/ab_${label}.log" 2>&1
+  env $envs timeout -k 10 "$secs" $cmd > "gpurun_out/ab_${label}.log" 2>&1
   rc=$?
   grep '^{' "gpurun_out/ab_${label}.log" | tail -1 | cut -c1-400
   echo "=== $label rc=$rc"
