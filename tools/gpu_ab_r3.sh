@@ -11,7 +11,7 @@ while IFS='|' read -r label envs secs cmd; do
   [ -z "$label" ] && continue
   case "$label" in \#*) continue ;; esac
   echo "=== $label: $envs $cmd"
-  env $envs timeout -k 10 "$secs" $cmd > "gpurun_out/ab_${label}.log" 2>&1
+  env $envs timeout -k 10 "$secs" $cmd < /dev/null > "gpurun_out/ab_${label}.log" 2>&1
   rc=$?
   grep '^{' "gpurun_out/ab_${label}.log" | tail -1 | cut -c1-400
   echo "=== $label rc=$rc"
