@@ -213,6 +213,11 @@ constexpr int D_W = 0, D_FP = 64 * 512, D_TILE = D_FP + FP_DMA * 4 * 1024, D_LDS
 #ifndef AI4E_STEM_STAMPS
 #define AI4E_STEM_STAMPS 0
 #endif
+// One barrier after the MFMA loop instead of two: the epilogue barrier also releases the footprint for the
+// next tile's DMA (stamps: the post-MFMA barrier + DMA issue held 9 % of the loop).
+#ifndef AI4E_STEM_ONE_BARRIER
+#define AI4E_STEM_ONE_BARRIER 0
+#endif
 constexpr int STEM_NSEG = 8;
 #if AI4E_STEM_STAMPS
 __device__ unsigned long long g_stem_stamps[2048 * 4 * STEM_NSEG];
@@ -367,10 +372,12 @@ void stem_pool_direct_kernel(const StemParams p, int ntiles) {
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[j], fx[i], acc[i][j], 0, 0, 0);
     }
     STEM_STAMP(1);  // MFMA loop
+#if !AI4E_STEM_ONE_BARRIER
     if constexpr (!U8) {
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // every wave finished reading the footprint
       if (t + static_cast<int>(gridDim.x) < ntiles) issue_fp(t + gridDim.x);
     }
+#endif
     STEM_STAMP(2);  // barrier + next footprint DMA issue
     // epilogue: bf16 relu(acc + b) -> tile [256 px][64 ch] (ptile layout)
 #pragma unroll
@@ -390,6 +397,13 @@ void stem_pool_direct_kernel(const StemParams p, int ntiles) {
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#if AI4E_STEM_ONE_BARRIER
+    // this barrier also means every wave has finished reading the footprint: the next tile's DMA goes now
+    // (still ahead of the c1 operand loads, so the loop-top vmcnt bookkeeping is unchanged)
+    if constexpr (!U8) {
+      if (t + static_cast<int>(gridDim.x) < ntiles) issue_fp(t + gridDim.x);
+    }
+#endif
     STEM_STAMP(3);  // epilogue tile writes + barrier
     // fused c1 operands, issued now so the L2 latency hides under the pooling: W1 fragments (output-channel
     // rows 16j + lane&15, k-chunk lane>>4 of k-step ks; 8 KB, L2-resident) and the bias
