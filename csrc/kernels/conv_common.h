@@ -16,10 +16,10 @@ __device__ __forceinline__ int swz(int row) { return (0x78 >> (2 * ((row >> 2) &
 // tracked by hand with counted vmcnt. The swizzle is applied to the per-lane SOURCE address.
 // M0 is saved and restored around the DMA: hipcc treats M0 as a reserved register and ignores it in a clobber
 // list (-Winline-asm), so a live M0 of its own (s_movrel indexing) would otherwise be corrupted silently.
-// Streaming-hint variants (AI4E_STREAM_HINTS=1 builds): activations that are read or written exactly once
+// Streaming hints (default on; AI4E_STREAM_HINTS=0 builds the plain forms): activations read or written exactly once
 // carry the non-temporal policy so they do not evict the weights every workgroup re-reads from L2.
 #ifndef AI4E_STREAM_HINTS
-#define AI4E_STREAM_HINTS 0
+#define AI4E_STREAM_HINTS 1
 #endif
 __device__ __forceinline__ void glds16_stream(const void* gsrc, uint32_t lds_base) {
   uint32_t keep;
