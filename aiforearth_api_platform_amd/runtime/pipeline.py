@@ -221,16 +221,19 @@ class _GraphRunner:
         key = tuple(x.shape)
         g = self.graphs.get(key)
         if g is None:
+            # the engine's capture pattern (runtime/engine.py warmup): eager warmup on the capture stream
+            # itself, the device drained, then the capture on that same stream
             static_in = x.clone()
             s = torch.cuda.Stream(device=self.device)
             s.wait_stream(torch.cuda.current_stream(self.device))
             with torch.cuda.stream(s):
                 for _ in range(self.warmup):
                     self.fn(static_in)
-            torch.cuda.current_stream(self.device).wait_stream(s)
+            torch.cuda.synchronize(self.device)
             graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph):
+            with torch.cuda.graph(graph, stream=s):
                 static_out = self.fn(static_in)
+            torch.cuda.synchronize(self.device)
             g = self.graphs[key] = (graph, static_in, static_out)
         graph, static_in, static_out = g
         static_in.copy_(x)
