@@ -46,6 +46,29 @@ __device__ __attribute__((aligned(64))) uint16_t g_chain_sink[512 + 64];
 // clobber so hipcc moves no LDS access across it (the raw builtin is not a compiler memory barrier).
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+// Diagnostic build (AI4E_CHAIN_STAMPS=1): s_memtime stamps at the phase boundaries (phase A, B/C setup + T2
+// epilogue, the passes, the T1' epilogue + copy-out), per wave, written to g_chain_stamps (read SHARES only).
+#ifndef AI4E_CHAIN_STAMPS
+#define AI4E_CHAIN_STAMPS 0
+#endif
+constexpr int CHAIN_NSEG = 4, CHAIN_MAXW = 65536;
+#if AI4E_CHAIN_STAMPS
+__device__ unsigned long long g_chain_stamps[CHAIN_MAXW * CHAIN_NSEG];
+#define CHAIN_STAMP(k)                                                             \
+  do {                                                                             \
+    __builtin_amdgcn_sched_barrier(0);                                             \
+    unsigned long long _t;                                                         \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");  \
+    __builtin_amdgcn_sched_barrier(0);                                             \
+    ch_sum[k] += _t - ch_last;                                                     \
+    ch_last = _t;                                                                  \
+  } while (0)
+#else
+#define CHAIN_STAMP(k) \
+  do {                 \
+  } while (0)
+#endif
+
 // Bias of the 4 channels n0 + 4*(lane>>4) + 0..3 from a wave-uniform 16-float block: read through the
 // constant address space (s_load: lgkmcnt, outside the hand-counted vmcnt bookkeeping), then a
 // lane-group select on registers.
@@ -180,6 +203,10 @@ void conv_chain_kernel(const ChainParams p) {
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+#if AI4E_CHAIN_STAMPS
+  unsigned long long ch_sum[CHAIN_NSEG] = {0, 0, 0, 0}, ch_last;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(ch_last)::"memory");
+#endif
   const int wm = wave % WM;
   const int wn = wave / WM;
   const int m0 = xcd_remap(blockIdx.x, gridDim.x) * BM;
@@ -391,6 +418,7 @@ void conv_chain_kernel(const ChainParams p) {
 #undef KC_STEP
 #undef KC_READ
   }
+  CHAIN_STAMP(0);  // phase A (3x3 main loop, patch or ring)
   float* const bias_lds = reinterpret_cast<float*>(smem + Cfg::LDS);  // [NBIAS] (BIAS_LDS); visible after pass 0's barrier
   if constexpr (Cfg::BIAS_LDS) {
 #pragma unroll
@@ -641,6 +669,7 @@ void conv_chain_kernel(const ChainParams p) {
     }
   };
   static_assert(Cfg::NP == 4 || Cfg::NP == 8, "passes");
+  CHAIN_STAMP(1);  // B/C weight prologue + T2 epilogue
   pass(std::integral_constant<int, 0>{});
   pass(std::integral_constant<int, 1>{});
   pass(std::integral_constant<int, 2>{});
@@ -651,6 +680,7 @@ void conv_chain_kernel(const ChainParams p) {
     pass(std::integral_constant<int, 6>{});
     pass(std::integral_constant<int, 7>{});
   }
+  CHAIN_STAMP(2);  // passes (B, Y epilogue + residual, C)
   copy_out(W64{}, ybuf, ybase, (Cfg::NP - 1) * 64);
 
   if constexpr (NEXT) {
@@ -678,6 +708,14 @@ void conv_chain_kernel(const ChainParams p) {
     row_bases(WMIDN{}, p.t1n, MIDN, tbase);
     copy_out(WMIDN{}, t2buf, tbase, 0);
   }
+#if AI4E_CHAIN_STAMPS
+  wait_vmcnt<0>();
+  CHAIN_STAMP(3);  // last Y chunk + T1' epilogue + copy-out (stores drained)
+  if (lane == 0 && blockIdx.x * 4 + wave < CHAIN_MAXW) {
+#pragma unroll
+    for (int k = 0; k < CHAIN_NSEG; ++k) g_chain_stamps[(blockIdx.x * 4 + wave) * CHAIN_NSEG + k] = ch_sum[k];
+  }
+#endif
 }
 
 // Patch mode (phase A from an LDS patch of the input rows) applies to stride 1, an input row of whole 1-KB
@@ -789,3 +827,11 @@ AI4E_API int ai4e_conv_chain_fwd(const void* x, const void* w2, const void* b2, 
                 : launch_chain<128, 128, 0, false, 4, false>(p, stream);
   return next ? launch_chain<128, 128, 128>(p, stream, patch) : launch_chain<128, 128, 0>(p, stream, patch);
 }
+
+#if AI4E_CHAIN_STAMPS
+// Diagnostic build only: per-wave phase cycle sums of the last chain launch (65536 waves x 4).
+AI4E_API int ai4e_chain_stamps_read(void* host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_chain_stamps), sizeof(g_chain_stamps)) == hipSuccess ? AI4E_OK
+                                                                                                      : AI4E_ELAUNCH;
+}
+#endif
