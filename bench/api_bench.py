@@ -74,8 +74,8 @@ def main():
     extra, dtype = {}, "bf16"
     if a.model.startswith("landcover"):
         kwargs = {"height": size, "width": size, "tile": a.tile, "stride": a.stride, "tile_batch": 16}
-        graphs = False
     if a.model == "landcover_spatial":
+        graphs = False  # P2P inside the servable: the U-Net runs per tile batch, eagerly
         group = a.group
         extra["parallelism"] = f"spatial{group}"
     if a.model.startswith("ensemble"):
