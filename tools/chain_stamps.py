@@ -34,7 +34,7 @@ def read(nwaves):
 
 
 def main():
-    assert "chainst" in str(_ext.library_path()), "run with AI4E_KERNEL_LIB=<the chain stamps build>"
+    assert hasattr(_ext.lib(), "ai4e_chain_stamps_read"), "run with AI4E_KERNEL_LIB=<a chain stamps build>"
     m = FusedResNet(resnet50(seed=0), device="cuda")
     img = torch.randint(0, 256, (250, 224, 224, 3), dtype=torch.uint8, device="cuda")
     out = {}

@@ -27,7 +27,7 @@ NAMES = ["footprint wait + barrier", "MFMA loop (8 K steps)", "barrier + next fo
 
 
 def main():
-    assert "stamps" in str(_ext.library_path()), "run with AI4E_KERNEL_LIB=<the stamps build>"
+    assert hasattr(_ext.lib(), "ai4e_stem_stamps_read"), "run with AI4E_KERNEL_LIB=<a stamps build>"
     m = FusedResNet(resnet50(seed=0), device="cuda")
     img = torch.randint(0, 256, (250, 224, 224, 3), dtype=torch.uint8, device="cuda")
     x = preprocess_s2d_u8(img)
