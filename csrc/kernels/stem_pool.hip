@@ -213,17 +213,7 @@ constexpr int D_W = 0, D_FP = 64 * 512, D_TILE = D_FP + FP_DMA * 4 * 1024, D_LDS
 #ifndef AI4E_STEM_STAMPS
 #define AI4E_STEM_STAMPS 0
 #endif
-// One barrier after the MFMA loop instead of two: the epilogue barrier also releases the footprint for the
-// next tile's DMA (stamps: the post-MFMA barrier + DMA issue held 9 % of the loop).
-#ifndef AI4E_STEM_ONE_BARRIER
-#define AI4E_STEM_ONE_BARRIER 0
-#endif
-// Epilogue tile writes as ds_write_b128 after a permlane16 quad exchange (stamps: the b64 epilogue writes +
-// barrier held 24 % of the loop; b64 LDS stores need ~4 waves per SIMD for full rate, b128 run at full rate
-// with one).
-#ifndef AI4E_STEM_EPI128
-#define AI4E_STEM_EPI128 0
-#endif
+
 constexpr int STEM_NSEG = 8;
 #if AI4E_STEM_STAMPS
 __device__ unsigned long long g_stem_stamps[2048 * 4 * STEM_NSEG];
@@ -378,12 +368,10 @@ void stem_pool_direct_kernel(const StemParams p, int ntiles) {
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[j], fx[i], acc[i][j], 0, 0, 0);
     }
     STEM_STAMP(1);  // MFMA loop
-#if !AI4E_STEM_ONE_BARRIER
     if constexpr (!U8) {
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // every wave finished reading the footprint
       if (t + static_cast<int>(gridDim.x) < ntiles) issue_fp(t + gridDim.x);
     }
-#endif
     STEM_STAMP(2);  // barrier + next footprint DMA issue
     // epilogue: bf16 relu(acc + b) -> tile [256 px][64 ch] (ptile layout)
 #pragma unroll
@@ -391,32 +379,6 @@ void stem_pool_direct_kernel(const StemParams p, int ntiles) {
       const int m = rmi[i];
       const int r = m / SP_RC, cc = m - r * SP_RC;
       const bool live = m < SP_RR * SP_RC && oh0 + r >= 0 && oh0 + r < p.H && ow0 + cc >= 0 && ow0 + cc < p.W;
-#if AI4E_STEM_EPI128
-      // 16-B stores: lanes 16 apart (channel quads 4g and 4g + 4 of the same pixel) trade one quad of a j pair
-      // (v_permlane16_swap), so even-row lanes hold 8 contiguous channels of j0 and odd-row lanes of j1: 8
-      // ds_write_b128 per lane instead of 16 ds_write_b64 (wide LDS stores run at full rate at two waves per SIMD)
-      const int g = lane >> 4;
-#pragma unroll
-      for (int jp = 0; jp < 2; ++jp) {
-        uint2 v[2];
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int j = 2 * jp + h;
-          const float4 b = bias[j];
-          v[h] = make_uint2(0u, 0u);
-          if (live)
-            v[h] = make_uint2(pack_bf16x2(fmaxf(acc[i][j][0] + b.x, 0.f), fmaxf(acc[i][j][1] + b.y, 0.f)),
-                              pack_bf16x2(fmaxf(acc[i][j][2] + b.z, 0.f), fmaxf(acc[i][j][3] + b.w, 0.f)));
-        }
-        const auto sx = __builtin_amdgcn_permlane16_swap(v[0].x, v[1].x, false, false);
-        const auto sy = __builtin_amdgcn_permlane16_swap(v[0].y, v[1].y, false, false);
-        const uint2 lo = make_uint2(sx[0], sy[0]), hi = make_uint2(sx[1], sy[1]);  // channels +0..3, +4..7
-        const int k = 2 * (2 * jp + (g & 1)) + (g >> 1);                           // the 16-B chunk
-        const bool sw = (m >> 3) & 1;                                               // halves stored swapped
-        *reinterpret_cast<uint4*>(tile + ptile(m, k)) =
-            sw ? make_uint4(hi.x, hi.y, lo.x, lo.y) : make_uint4(lo.x, lo.y, hi.x, hi.y);
-      }
-#else
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int n = 16 * j + 4 * (lane >> 4);
@@ -427,16 +389,8 @@ void stem_pool_direct_kernel(const StemParams p, int ntiles) {
                          pack_bf16x2(fmaxf(acc[i][j][2] + b.z, 0.f), fmaxf(acc[i][j][3] + b.w, 0.f)));
         *reinterpret_cast<uint2*>(tile + ptile(m, n >> 3) + ((((n >> 2) ^ (m >> 3)) & 1) << 3)) = v;
       }
-#endif
     }
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-#if AI4E_STEM_ONE_BARRIER
-    // this barrier also means every wave has finished reading the footprint: the next tile's DMA goes now
-    // (still ahead of the c1 operand loads, so the loop-top vmcnt bookkeeping is unchanged)
-    if constexpr (!U8) {
-      if (t + static_cast<int>(gridDim.x) < ntiles) issue_fp(t + gridDim.x);
-    }
-#endif
     STEM_STAMP(3);  // epilogue tile writes + barrier
     // fused c1 operands, issued now so the L2 latency hides under the pooling: W1 fragments (output-channel
     // rows 16j + lane&15, k-chunk lane>>4 of k-step ks; 8 KB, L2-resident) and the bias
