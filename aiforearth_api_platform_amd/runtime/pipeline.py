@@ -234,10 +234,18 @@ class _GraphRunner:
             with torch.cuda.graph(graph, stream=s):
                 static_out = self.fn(static_in)
             torch.cuda.synchronize(self.device)
-            g = self.graphs[key] = (graph, static_in, static_out)
-        graph, static_in, static_out = g
+            g = self.graphs[key] = [graph, static_in, static_out, None]
+        graph, static_in, static_out, done = g
+        if done is not None:
+            # the previous replay of THIS graph must have finished before it is launched again: two back-to-back
+            # launches of one graph faulted the GPU twice in bench/stage_rates.py (never with a host sync between
+            # them); the serving loops sync on every batch anyway, so this costs them nothing
+            done.synchronize()
         static_in.copy_(x)
         graph.replay()
+        ev = torch.cuda.Event()
+        ev.record()
+        g[3] = ev
         return static_out
 
 

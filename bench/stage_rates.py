@@ -22,15 +22,17 @@ sys.path.insert(0, ROOT)
 
 
 def _timed(fn, iters: int) -> float:
+    """Per-call time with a device sync after every call (as in serving: each stage output is consumed on the
+    host before the next batch)."""
     import torch
 
     for _ in range(3):
         fn()
-    torch.cuda.synchronize()
+        torch.cuda.synchronize()
     t = time.perf_counter()
     for _ in range(iters):
         fn()
-    torch.cuda.synchronize()
+        torch.cuda.synchronize()
     return (time.perf_counter() - t) / iters
 
 
