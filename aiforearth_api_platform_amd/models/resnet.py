@@ -152,9 +152,15 @@ class FusedResNet:
                     down = _fold(blk.downsample[0], blk.downsample[1]).to(self.device)
                 self.blocks.append((_fold(blk.conv1, blk.bn1).to(self.device), _fold(blk.conv2, blk.bn2).to(self.device),
                                     _fold(blk.conv3, blk.bn3).to(self.device), down))
-        fcw = model.fc.weight.data.float().reshape(model.fc.out_features, -1, 1, 1)
-        self.fc = pack_conv(fcw, model.fc.bias.data.float()).to(self.device)
+        # the classifier FC runs on K1, whose output rows are whole 8-channel vectors: classes padded to a multiple
+        # of 8 with zero rows, the logits sliced back to num_classes
         self.num_classes = model.fc.out_features
+        ncp = -(-self.num_classes // 8) * 8
+        fcw = torch.zeros(ncp, model.fc.in_features, 1, 1)
+        fcw[:self.num_classes] = model.fc.weight.data.float().reshape(self.num_classes, -1, 1, 1)
+        fcb = torch.zeros(ncp)
+        fcb[:self.num_classes] = model.fc.bias.data.float()
+        self.fc = pack_conv(fcw, fcb).to(self.device)
         self.chunk = chunk if chunk is not None else _env_chunk()
         self.chain = _env_chain()
         if dtype == torch.float16:  # the K1 path is the one built for both element types
@@ -435,8 +441,10 @@ class FusedResNet:
                 k = self.fc.cin_pad
                 self._fc_lin = (self.fc.w_packed[:self.fc.cout, :k].contiguous(),
                                 self.fc.bias[:self.fc.cout].to(self.dtype))
-            return F.linear(f.reshape(f.shape[0], -1), *self._fc_lin)
-        return conv2d_nhwc(f, self.fc).reshape(f.shape[0], -1)
+            y = F.linear(f.reshape(f.shape[0], -1), *self._fc_lin)
+        else:
+            y = conv2d_nhwc(f, self.fc).reshape(f.shape[0], -1)
+        return y if y.shape[1] == self.num_classes else y[:, :self.num_classes].contiguous()
 
     def forward(self, x: torch.Tensor, preprocess=None) -> torch.Tensor:
         return self.logits(x, preprocess).float()
