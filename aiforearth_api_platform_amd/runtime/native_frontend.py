@@ -111,7 +111,8 @@ def spawn_native_frontends(n: int, pools: Dict[str, object], routes: List[dict],
         with os.fdopen(fd, "w") as f:
             f.write("\n".join(lines) + "\n")
         os.chmod(cfg_path, 0o600)  # (subscription keys)
-        p = subprocess.Popen([str(_build.INGESTD), cfg_path], pass_fds=fds, close_fds=True)
+        binary = os.environ.get("AI4E_INGESTD") or str(_build.INGESTD)  # (a sanitizer build in the race tests)
+        p = subprocess.Popen([binary, cfg_path], pass_fds=fds, close_fds=True)
         for c in child_ends:
             c.close()
         procs.append(NativeFrontend(p, cfg_path))

@@ -198,7 +198,11 @@ struct Shard {
   // -1: timed out (the tasks may still be created), else tasks created
   int64_t wait_ack(uint64_t tok, double timeout_s) {
     std::unique_lock<std::mutex> lk(ack_mu);
-    bool ok = ack_cv.wait_for(lk, std::chrono::duration<double>(timeout_s), [&] { return acks[tok].done; });
+    // system_clock deadline (pthread_cond_timedwait), as SlotRing: libtsan does not intercept the steady-clock
+    // pthread_cond_clockwait that wait_for compiles to, and would report the waiter's re-lock as a double lock
+    const auto deadline = std::chrono::system_clock::now() + std::chrono::duration_cast<std::chrono::system_clock::duration>(
+                                                                  std::chrono::duration<double>(timeout_s));
+    bool ok = ack_cv.wait_until(lk, deadline, [&] { return acks[tok].done; });
     int64_t n = ok ? acks[tok].n : -1;
     acks.erase(tok);
     return n;
