@@ -278,7 +278,7 @@ def landcover_spatial(device="cuda", group=None, role: str = "leader", height: i
     # broadcast per dtype (survey C1) instead of every GPU loading its own copy
     broadcast_tensors(f.tensors(), src=0, group=group)
     seg = SpatialSegmenter(f.forward_u8, TileGrid(height, width, tile, stride), f.n_classes, torch.device(device),
-                           tile_batch=tile_batch, group=group)
+                           tile_batch=tile_batch, group=group, tile_graphs=True)
     if role == "leader":
         return _SpatialSegmenterServable(seg, height, width, f.n_classes)
     return _Follower(seg.serve_follower)

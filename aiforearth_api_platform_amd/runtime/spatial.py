@@ -51,10 +51,18 @@ def owned_rows(grid: TileGrid, ranges: List[Tuple[int, int]], r: int) -> Tuple[i
 
 class SpatialSegmenter:
     def __init__(self, model_fn: Callable[[torch.Tensor], torch.Tensor], grid: TileGrid, n_out: int,
-                 device: torch.device, tile_batch: int = 16, group=None, local: bool = False):
+                 device: torch.device, tile_batch: int = 16, group=None, local: bool = False,
+                 tile_graphs: bool = False):
         """model_fn: uint8 tiles [b, ts, ts, C_in] -> logits NHWC [b, ts, ts, n_out].
-        ``local``: one-GPU segmentation even inside an initialized process group (a pool worker)."""
+        ``local``: one-GPU segmentation even inside an initialized process group (a pool worker).
+        ``tile_graphs``: run each tile batch through a HIP graph captured per batch shape (the group form, whose
+        P2P exchanges keep the whole servable out of the worker's graph; the one-GPU form is captured whole)."""
         self.model_fn = model_fn
+        if tile_graphs and torch.device(device).type == "cuda":
+            from .pipeline import _GraphRunner
+
+            self.model_fn = _GraphRunner(model_fn, torch.device(device))
+        self._graphed = self.model_fn is not model_fn
         self.grid = grid
         self.n_out = n_out
         self.device = device
@@ -110,6 +118,9 @@ class SpatialSegmenter:
     def _infer(self, tiles: torch.Tensor) -> torch.Tensor:
         """tiles [n, ts, ts, c] uint8 -> logits [n, ts, ts, n_out]."""
         flat = tiles.contiguous()
+        if self._graphed:  # a graph's output buffer is reused by its next replay: copy each batch out first
+            return torch.cat([self.model_fn(flat[i:i + self.tile_batch])[..., : self.n_out].clone()
+                              for i in range(0, flat.shape[0], self.tile_batch)])
         outs = [self.model_fn(flat[i:i + self.tile_batch]) for i in range(0, flat.shape[0], self.tile_batch)]
         return torch.cat(outs)[..., : self.n_out].contiguous()
 
