@@ -758,11 +758,21 @@ bool ingest(Conn& c, const Request& r, Route& route, Shard& s, bool batch) {
   return respond(c, created < 0 ? 202 : 200, "text/plain; charset=utf-8", "TaskId: " + ids[0], ka, b3);
 }
 
+std::atomic<int> g_conns{0};
+constexpr int kMaxConns = 4096;  // one thread each; beyond this new connections are answered 503 and closed
+
 void serve_conn(int fd) {
+  struct Count {
+    Count() { g_conns.fetch_add(1); }
+    ~Count() { g_conns.fetch_sub(1); }
+  } count;
   int one = 1;
   setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
   int rcv = 4 << 20;
   setsockopt(fd, SOL_SOCKET, SO_RCVBUF, &rcv, sizeof(rcv));
+  struct timeval idle {300, 0};  // an idle keep-alive connection (or a stalled body) releases its thread
+  setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &idle, sizeof(idle));
+  setsockopt(fd, SOL_SOCKET, SO_SNDTIMEO, &idle, sizeof(idle));
   Conn c(fd);
   while (true) {
     Request r;
@@ -838,6 +848,14 @@ int main(int argc, char** argv) {
     int fd = ::accept(lfd, nullptr, nullptr);
     if (fd < 0) {
       if (errno == EINTR) continue;
+      continue;
+    }
+    if (g_conns.load() >= kMaxConns) {
+      static const char busy[] =
+          "HTTP/1.1 503 Service Unavailable\r\nContent-Type: application/json\r\nContent-Length: 51\r\n"
+          "Connection: close\r\n\r\n{\"message\":\"Service is busy, please try again later.\"}";
+      write_all(fd, busy, sizeof(busy) - 1);
+      ::close(fd);
       continue;
     }
     std::thread(serve_conn, fd).detach();
