@@ -852,7 +852,7 @@ int main(int argc, char** argv) {
     }
     if (g_conns.load() >= kMaxConns) {
       static const char busy[] =
-          "HTTP/1.1 503 Service Unavailable\r\nContent-Type: application/json\r\nContent-Length: 51\r\n"
+          "HTTP/1.1 503 Service Unavailable\r\nContent-Type: application/json\r\nContent-Length: 54\r\n"
           "Connection: close\r\n\r\n{\"message\":\"Service is busy, please try again later.\"}";
       write_all(fd, busy, sizeof(busy) - 1);
       ::close(fd);
