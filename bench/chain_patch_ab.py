@@ -1,4 +1,5 @@
-"""A/B of the K1c chain's phase A: LDS-DMA ring (tile 1 / 0) vs the LDS input patch (tile 3), ResNet-50 shapes
+"""A/B of K1c chain tile configs (CHAIN_CFGS, default: LDS-DMA ring (tile 1 / 0) vs the LDS input patch (tile 3);
++8 = residual prefetched into registers), ResNet-50 shapes
 at batch 250. Each shape is timed alone and as two launches on two streams at once (the serving worker's two
 compute streams share the chip)."""
 import json
@@ -41,9 +42,10 @@ def main():
         t1 = [torch.randn(B, hw, hw, mid, device=dev).relu().bfloat16() for _ in range(2)]
         res = [torch.randn(B, hw, hw, 4 * mid, device=dev).bfloat16() for _ in range(2)]
         r = {"case": name, "B": B}
-        ref = 1 if mid == 64 else 0
+        cfgs = [int(c) for c in os.environ.get("CHAIN_CFGS", "").split(",") if c] or [1 if mid == 64 else 0, 3]
+        ref = cfgs[0]
         outs = {}
-        for cfg in (ref, 3):
+        for cfg in cfgs:
             r[f"tile{cfg}_us"] = round(timed(lambda: conv_chain(t1[0], c2, c3, res[0], c1n=c1n, tile_cfg=cfg)), 1)
 
             def pair():
@@ -60,9 +62,10 @@ def main():
             y, t = conv_chain(t1[0], c2, c3, res[0], c1n=c1n, tile_cfg=cfg)
             outs[cfg] = (y.float(), None if t is None else t.float())
         torch.cuda.synchronize()
-        r["max_abs_diff_y"] = (outs[ref][0] - outs[3][0]).abs().max().item()
-        if outs[ref][1] is not None:
-            r["max_abs_diff_t1n"] = (outs[ref][1] - outs[3][1]).abs().max().item()
+        for cfg in cfgs[1:]:
+            r[f"max_abs_diff_y_{cfg}"] = (outs[ref][0] - outs[cfg][0]).abs().max().item()
+            if outs[ref][1] is not None:
+                r[f"max_abs_diff_t1n_{cfg}"] = (outs[ref][1] - outs[cfg][1]).abs().max().item()
         print(json.dumps(r), flush=True)
 
 

@@ -1,0 +1,23 @@
+#!/bin/bash
+# Round-3 session B: build, focused chain tests, chain tile A/B (CHAIN_CFGS), bench, kernel-trace profile.
+# Each GPU step has its own time limit; any failure stops the session.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+python -c "import __graft_entry__ as g; g.build()" > gpurun_out/build.log 2>&1 || { tail gpurun_out/build.log; exit 3; }
+run() {  # name timeout cmd...
+  local name=$1 t=$2; shift 2
+  echo "=== $name"
+  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  tail -n 12 "gpurun_out/$name.log"
+  echo "=== $name rc=$rc"
+  if [ $rc -ne 0 ]; then echo "STOP after $name"; exit $rc; fi
+}
+[ -n "${TESTS:-}" ] && run focus 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -p no:cacheprovider $TESTS
+[ -n "${CHAIN_CFGS:-}" ] && run chain_ab 300 python -u bench/chain_patch_ab.py
+[ -n "${BENCH:-}" ] && run bench 300 python bench.py --steps 20 --warmup 5 --json-out gpurun_out/bench.json
+[ -n "${BENCH2:-}" ] && run bench2 300 env $BENCH2 python bench.py --steps 20 --warmup 5 --json-out gpurun_out/bench2.json
+[ -n "${PROF:-}" ] && run prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --steps 5 --warmup 2
+echo "=== done"
