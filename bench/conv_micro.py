@@ -1,4 +1,6 @@
 """K1 conv micro-benchmark on arbitrary shapes: TFLOP/s per tile config (+ hipBLASLt GEMM of equal size).
+CFGS=9,10 picks the tile configs; TWO=1 also times two copies on two streams at once (the serving worker's
+two compute streams), reported as TFLOP/s of both together.
 
     python bench/conv_micro.py N H W C K ksize stride [N H W C K ksize stride ...]
 """
@@ -36,12 +38,29 @@ def main():
         M, K = n * oh * ow, ks * ks * pc.cin_pad
         flops = 2.0 * M * k * K
         out = {"shape": f"n{n} {h}x{w} {c}->{k} k{ks} s{s}", "M": M, "N": k, "K": K}
-        for cfg in (1, 2, 3, 4, 5, 6):
+        cfgs = [int(c) for c in os.environ.get("CFGS", "1,2,3,4,5,6").split(",")]
+        x2 = x.clone()
+        s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+        for cfg in cfgs:
             try:
                 t = timed(lambda: conv2d_nhwc(x, pc, relu=True, tile_cfg=cfg))
             except RuntimeError:
                 continue
             out[f"cfg{cfg}"] = round(flops / t / 1e6, 1)
+            out[f"cfg{cfg}_us"] = round(t, 1)
+            if os.environ.get("TWO"):
+                def two():
+                    cur = torch.cuda.current_stream()
+                    s1.wait_stream(cur)
+                    s2.wait_stream(cur)
+                    with torch.cuda.stream(s1):
+                        conv2d_nhwc(x, pc, relu=True, tile_cfg=cfg)
+                    with torch.cuda.stream(s2):
+                        conv2d_nhwc(x2, pc, relu=True, tile_cfg=cfg)
+                    cur.wait_stream(s1)
+                    cur.wait_stream(s2)
+                t2 = timed(two)
+                out[f"cfg{cfg}_2s"] = round(2 * flops / t2 / 1e6, 1)
         A = torch.randn(M, K, device=dev).bfloat16()
         B = torch.randn(K, k, device=dev).bfloat16()
         out["gemm"] = round(flops / timed(lambda: A @ B) / 1e6, 1)

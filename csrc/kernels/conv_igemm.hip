@@ -501,10 +501,20 @@ constexpr int U_ROWS = 128, U_BYTES = U_ROWS * 128;
 // {wr*96 + 0..63} (still 128 unit rows), u3 only {wr*96 + 64..95} (64 rows: one DMA per lane, two
 // fragments, 8-MFMA phases 3 and 4). A 14x14 layer of 250 images (M = 49000) is then 256 tiles —
 // one per CU — instead of 192 256-row tiles that leave a quarter of the chip idle.
-template <int GATHER, int BM, bool F16 = false>
+//
+// PH3 (BM 192 only, tile config 10): three 16-MFMA phases per K tile instead of 16/16/8/8 — quadrants (1,1) and
+// (1,0) of the 64-row XQ1 half share one phase — so 6 barriers instead of 8 per K tile. Staging (phase g = 3t+p):
+// p = 0 stages u2 of tile t+1, p = 1 u3 of tile t+1, p = 2 u0 and u1 of tile t+2. Last reads within tile t:
+// u0/u1 at p = 0, u2 at p = 1, u3 at p = 2, so every slot is again overwritten >= 2 phases after its last read
+// and read >= 4 phases after it was staged, and the per-phase wait is the same rule (own DMAs of phases <= g-3).
+// PH3 == 2 (tile config 11): the 3-phase schedule with a static s_setprio 1 for the trailing wave group (waves
+// 4-7, the arbitration loser on every shared SIMD) instead of the per-segment priority flips around the MFMAs
+// (MI355X_MICROARCH.md "Two waves per SIMD", item 4).
+template <int GATHER, int BM, bool F16 = false, int PH3 = 0>
 __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) {
   static_assert(GATHER == GATHER_TAP || GATHER == GATHER_POINTWISE, "256 tile needs C % 64 == 0");
   static_assert(BM == 256 || BM == 192, "wave groups of 128 or 96 pixels");
+  static_assert(PH3 == 0 || BM == 192, "the 3-phase schedule is the 192-pixel tile's");
   constexpr int WROWS = BM / 2;    // pixels per wave group
   constexpr int X1 = WROWS - 64;   // u3 rows per wave group
   constexpr int L3 = X1 / 32;      // DMAs per lane for u3
@@ -645,13 +655,13 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
   }
 #define K256_MFMA(MQ, NQ, WR)                                                                      \
   {                                                                                                \
-    __builtin_amdgcn_s_setprio(1);                                                                 \
+    if constexpr (PH3 < 2) __builtin_amdgcn_s_setprio(1);                                          \
     _Pragma("unroll") for (int s = 0; s < 2; ++s)                                                  \
       _Pragma("unroll") for (int i = 0; i < ((MQ) ? MF1 : 4); ++i)                                 \
         _Pragma("unroll") for (int j = 0; j < 2; ++j)                                              \
           acc[4 * (MQ) + i][2 * (NQ) + j] =                                                        \
               mfma_16x16x32<F16>(WR[j][s], xr[i][s], acc[4 * (MQ) + i][2 * (NQ) + j]);             \
-    __builtin_amdgcn_s_setprio(0);                                                                 \
+    if constexpr (PH3 < 2) __builtin_amdgcn_s_setprio(0);                                          \
   }
 // CHECKED = 0: steady state (kt + 2 < nk): every phase stages a unit, 3 phases of DMAs in flight
 // (NS = this wave's DMAs of those 3 phases: 6 at phase 1, 4 + L3 at phases 2-4, which stage u3 or follow it)
@@ -690,17 +700,79 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
     __builtin_amdgcn_s_barrier();                                                                  \
   }
 
-  // ---- prologue: tile 0 (virtual phases -5..-2) and tile 1's u0, u1 (phases -1, 0)
-#pragma unroll
-  for (int g = -5; g <= 0; ++g) stage_phase(g);
-  if (loads_of(-1) + loads_of(0) == 4) wait_vmcnt<4>();
-  else wait_vmcnt<0>();
-  __builtin_amdgcn_s_barrier();
-  if (wr == 1) __builtin_amdgcn_s_barrier();  // the stagger: group 1 trails by one barrier
+  // 3-phase schedule (PH3): phase g = 3t + p, g >= -6 (the prologue is g = -4 .. -1)
+  auto ph3_tile = [&](int g) { return (g + 6) / 3 - 2; };
+  auto stage3 = [&](int g) {
+    const int t = ph3_tile(g), q = g - 3 * t;
+    if (q == 0) {
+      if (t + 1 < nk) stage(t + 1, 2);
+    } else if (q == 1) {
+      if (t + 1 < nk) stage(t + 1, 3);
+    } else if (t + 2 < nk) {
+      stage(t + 2, 0);
+      stage(t + 2, 1);
+    }
+  };
+  auto loads3 = [&](int g) {
+    const int t = ph3_tile(g), q = g - 3 * t;
+    return q == 0 ? (t + 1 < nk ? 2 : 0) : q == 1 ? (t + 1 < nk ? L3 : 0) : (t + 2 < nk ? 4 : 0);
+  };
+#define K256_SYNC3(G, CHECKED, STAGE_UNCHECKED)                                                       \
+  if (CHECKED) {                                                                                   \
+    stage3(G);                                                                                     \
+    wait_vmcnt_n(loads3((G) - 2) + loads3((G) - 1) + loads3(G));                                   \
+  } else {                                                                                         \
+    STAGE_UNCHECKED;                                                                               \
+    wait_vmcnt<6 + L3>();                                                                          \
+  }                                                                                                \
+  __builtin_amdgcn_s_barrier();                                                                    \
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#define K256_TILE3(KT, CHECKED)                                                                    \
+  {                                                                                                \
+    const int g = 3 * (KT);                                                                        \
+    K256_READ_W(w0r, 0, KT)                                                                        \
+    K256_READ_X(0, KT)                                                                             \
+    K256_SYNC3(g, CHECKED, stage((KT) + 1, 2))                                                     \
+    K256_MFMA(0, 0, w0r)                                                                           \
+    __builtin_amdgcn_s_barrier();                                                                  \
+    K256_READ_W(w1r, 1, KT)                                                                        \
+    K256_SYNC3(g + 1, CHECKED, stage((KT) + 1, 3))                                                 \
+    K256_MFMA(0, 1, w1r)                                                                           \
+    __builtin_amdgcn_s_barrier();                                                                  \
+    K256_READ_X(1, KT)                                                                             \
+    K256_SYNC3(g + 2, CHECKED, (stage((KT) + 2, 0), stage((KT) + 2, 1)))                           \
+    K256_MFMA(1, 1, w1r)                                                                           \
+    K256_MFMA(1, 0, w0r)                                                                           \
+    __builtin_amdgcn_s_barrier();                                                                  \
+  }
 
   int kt = 0;
-  for (; kt + 2 < nk; ++kt) K256_TILE(kt, 0)
-  for (; kt < nk; ++kt) K256_TILE(kt, 1)
+  if constexpr (PH3 > 0) {
+    // ---- prologue: tile 0 (phases -4 .. -2) and tile 1's u0, u1 (phase -1); tile 0's u0/u1 must have landed
+#pragma unroll
+    for (int g = -4; g <= -1; ++g) stage3(g);
+    wait_vmcnt_n(loads3(-3) + loads3(-2) + loads3(-1));
+    __builtin_amdgcn_s_barrier();
+    if (wr == 1) __builtin_amdgcn_s_barrier();  // the stagger: group 1 trails by one barrier
+    if constexpr (PH3 == 2) {
+      if (wr == 1) __builtin_amdgcn_s_setprio(1);
+    }
+    for (; kt + 2 < nk; ++kt) K256_TILE3(kt, 0)
+    for (; kt < nk; ++kt) K256_TILE3(kt, 1)
+    if constexpr (PH3 == 2) __builtin_amdgcn_s_setprio(0);
+  } else {
+    // ---- prologue: tile 0 (virtual phases -5..-2) and tile 1's u0, u1 (phases -1, 0)
+#pragma unroll
+    for (int g = -5; g <= 0; ++g) stage_phase(g);
+    if (loads_of(-1) + loads_of(0) == 4) wait_vmcnt<4>();
+    else wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    if (wr == 1) __builtin_amdgcn_s_barrier();  // the stagger: group 1 trails by one barrier
+    for (; kt + 2 < nk; ++kt) K256_TILE(kt, 0)
+    for (; kt < nk; ++kt) K256_TILE(kt, 1)
+  }
+#undef K256_TILE3
+#undef K256_SYNC3
 #undef K256_TILE
 #undef K256_SYNC_LOADS
 #undef K256_MFMA
@@ -795,7 +867,7 @@ int launch(const ConvParams& p0, hipStream_t s) {
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
 }
 
-template <int BM, bool F16 = false>
+template <int BM, bool F16 = false, int PH3 = 0>
 int launch256(const ConvParams& p0, hipStream_t s) {
   ConvParams p = p0;
   // 256 tile: C % 64 (one tap per 64-wide K tile), 16-B output/residual rows, Kout % 8
@@ -807,9 +879,9 @@ int launch256(const ConvParams& p0, hipStream_t s) {
   p.zero = zero_chunk_ptr();
   if (!p.zero) return AI4E_ELAUNCH;
   if (p.KH == 1 && p.KW == 1 && p.pad == 0)
-    hipLaunchKernelGGL((conv_igemm256_kernel<GATHER_POINTWISE, BM, F16>), dim3(nb), dim3(512), 0, s, p);
+    hipLaunchKernelGGL((conv_igemm256_kernel<GATHER_POINTWISE, BM, F16, PH3>), dim3(nb), dim3(512), 0, s, p);
   else
-    hipLaunchKernelGGL((conv_igemm256_kernel<GATHER_TAP, BM, F16>), dim3(nb), dim3(512), 0, s, p);
+    hipLaunchKernelGGL((conv_igemm256_kernel<GATHER_TAP, BM, F16, PH3>), dim3(nb), dim3(512), 0, s, p);
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
 }
 
@@ -820,7 +892,8 @@ int launch256(const ConvParams& p0, hipStream_t s) {
 // workgroups per CU), 5 = 256x64 with 5 stages (100 KB: one workgroup per CU), 6 = 256x256, 8 waves,
 // ping-pong phases (needs C % 64 == 0, Kout % 8 == 0); 7/8 = the 128x128 / 256x64 tiles with a 3-stage
 // ring (48 KB, two-pass LDS epilogue) built for three workgroups per CU; 9 = the 256x256 schedule with
-// 192-pixel tiles (one tile per CU for 250-image 14x14 layers).
+// 192-pixel tiles (one tile per CU for 250-image 14x14 layers); 10 = config 9 with three 16-MFMA phases per K tile,
+// 11 = 10 with a static priority for the trailing wave group.
 // relu: bit 0 = ReLU; bit 1 = `res` is on the half-resolution grid [N, OH/2, OW/2, ldres] (nearest 2x
 // upsample of the residual, OH and OW even).
 namespace {
@@ -849,7 +922,7 @@ int conv2d_impl(const void* x, const void* w, const void* bias, const void* res,
     // channel tile, tiles that never straddle images, full 16-B output rows
     const bool tall = tile_cfg == 2 || tile_cfg == 5 || tile_cfg == 8;
     const int bm = tall ? 256 : 128, bn = tall ? 64 : 128;
-    if (tile_cfg == 3 || tile_cfg == 6 || tile_cfg == 9 || gn_groups <= 0 || Kout % gn_groups || (OH * OW) % bm || Kout % 8 ||
+    if (tile_cfg == 3 || tile_cfg == 6 || tile_cfg == 9 || tile_cfg == 10 || tile_cfg == 11 || gn_groups <= 0 || Kout % gn_groups || (OH * OW) % bm || Kout % 8 ||
         ldy % 8 || ycoff % 8 || (res && ldres % 8) || bn % (Kout / gn_groups))
       return AI4E_EINVAL;
     p.gnp = gnp;
@@ -865,6 +938,8 @@ int conv2d_impl(const void* x, const void* w, const void* bias, const void* res,
     case 7: return launch<2, 2, 3, 3, F16>(p, stream);
     case 8: return launch<4, 1, 3, 3, F16>(p, stream);
     case 9: return launch256<192, F16>(p, stream);
+    case 10: return launch256<192, F16, 1>(p, stream);
+    case 11: return launch256<192, F16, 2>(p, stream);
     default: return AI4E_EINVAL;
   }
 }

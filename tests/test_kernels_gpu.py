@@ -62,7 +62,7 @@ def test_conv_igemm(case, epi):
     assert err <= 0.02 * ref.abs().max().item() + 0.02, err
 
 
-@pytest.mark.parametrize("tile", [1, 2, 3, 4, 5, 6, 7, 8, 9])
+@pytest.mark.parametrize("tile", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11])
 def test_conv_tile_configs(tile):
     torch.manual_seed(1)
     wt = torch.randn(256, 64, 3, 3) / 24
@@ -100,10 +100,12 @@ CASES_256 = [
     (2, 28, 28, 128, 128, 3, 2, 1),     # Cout < 256: half the channel tile masked
     (2, 7, 7, 512, 2048, 1, 1, 0),      # M = 98 < 256
     (1, 33, 17, 64, 264, 3, 1, 1),      # ragged M, Cout = 256 + 8
+    (2, 14, 14, 128, 256, 1, 1, 0),     # nk = 2: only the checked tail
+    (2, 14, 14, 192, 256, 1, 1, 0),     # nk = 3: one unchecked tile, then the tail
 ]
 
 
-@pytest.mark.parametrize("tile", [6, 9])  # 9: the same schedule with 192-pixel tiles
+@pytest.mark.parametrize("tile", [6, 9, 10, 11])  # 9: the same schedule with 192-pixel tiles; 10/11: its 3-phase forms
 @pytest.mark.parametrize("case", CASES_256)
 @pytest.mark.parametrize("epi", ["plain", "res_relu"])
 def test_conv_tile256(case, epi, tile):

@@ -17,10 +17,19 @@ run() {  # name timeout cmd...
 }
 [ -n "${TESTS:-}" ] && run focus 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -p no:cacheprovider $TESTS
 [ -n "${CHAIN_CFGS:-}" ] && run chain_ab 300 python -u bench/chain_patch_ab.py
+[ -n "${MICRO:-}" ] && run micro 300 env CFGS=${MICRO_CFGS:-9,10} TWO=1 python -u bench/conv_micro.py $MICRO
 [ -n "${CUSPLIT:-}" ] && run cusplit 400 python -u bench/cu_split_probe.py $CUSPLIT
 [ -n "${BENCH:-}" ] && run bench 300 python bench.py --steps 20 --warmup 5 --json-out gpurun_out/bench.json
 [ -n "${BENCH2:-}" ] && run bench2 300 env $BENCH2 python bench.py --steps 20 --warmup 5 --json-out gpurun_out/bench2.json
 [ -n "${PROF:-}" ] && run prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --steps 5 --warmup 2
 [ -n "${HBM:-}" ] && run hbm 200 python -u bench/hbm_probe.py
 [ -n "${PROF2:-}" ] && run prof2 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/prof2 -o run -- python bench.py --steps 120 --warmup 10 --http 0
+# AB="label:ENV=v ...|--bench-args;..." -> bench runs in that order (either part may be empty)
+if [ -n "${AB:-}" ]; then
+  IFS=';' read -ra CASES <<< "$AB"
+  for c in "${CASES[@]}"; do
+    lab=${c%%:*}; a=${c#*:}; envs=${a%%|*}; bargs=${a#*|}; [ "$bargs" = "$a" ] && bargs=""
+    run "ab_$lab" 300 env $envs python bench.py --steps 20 --warmup 5 $bargs --json-out "gpurun_out/ab_$lab.json"
+  done
+fi
 echo "=== done"
