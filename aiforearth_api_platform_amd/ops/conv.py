@@ -125,6 +125,8 @@ def tuned_tile(pc: PackedConv, n: int, h: int, w: int, residual: bool) -> int:
     cfg = _TILES.get(tile_key(pc, n, h, w, residual))
     if cfg is None and 224 <= n <= 288:  # batch sizes near the tuned 256 share its tile choices
         cfg = _TILES.get(tile_key(pc, 256, h, w, residual))
+    if cfg is None and n > 250 and n % 250 == 0:  # whole multiples of the serving batch: its grids, more rounds
+        cfg = _TILES.get(tile_key(pc, 250, h, w, residual))
     return int(cfg or 0)
 
 

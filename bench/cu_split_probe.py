@@ -110,9 +110,10 @@ def main():
                 graphs[k % nbuf].replay()
         return run
     p({"front_alone_full_ms": round(pipeline_rate(serial(full, gf), 20), 4),
-       "back_alone_full_ms": round(pipeline_rate(serial(full, gb), 20), 4)})
+       "back_alone_full_ms": round(pipeline_rate(serial(full, gb), 20), 4),
+       "whole_forward_one_stream_ms": round(pipeline_rate(serial(full, gfull), 20), 4), "batch": B})
 
-    fs = [int(a) for a in sys.argv[1:]] or [96, 112, 128, 144, 160]
+    fs = [int(a) for a in sys.argv[1:]] or ([] if os.environ.get("NO_SPLIT") else [96, 112, 128, 144, 160])
     for F in fs:
         for layout in (("balanced", "contiguous") if F == 128 else ("balanced",)):
             fcus = cup.balanced(F, xcc) if layout == "balanced" else list(range(F))

@@ -19,6 +19,7 @@ run() {  # name timeout cmd...
 [ -n "${CHAIN_CFGS:-}" ] && run chain_ab 300 python -u bench/chain_patch_ab.py
 [ -n "${MICRO:-}" ] && run micro 300 env CFGS=${MICRO_CFGS:-9,10} TWO=1 python -u bench/conv_micro.py $MICRO
 [ -n "${CUSPLIT:-}" ] && run cusplit 400 python -u bench/cu_split_probe.py $CUSPLIT
+[ -n "${BIGB:-}" ] && for bb in $BIGB; do run "bigb_$bb" 400 env B=$bb NO_SPLIT=1 NB=30 python -u bench/cu_split_probe.py; done
 [ -n "${BENCH:-}" ] && run bench 300 python bench.py --steps 20 --warmup 5 --json-out gpurun_out/bench.json
 [ -n "${BENCH2:-}" ] && run bench2 300 env $BENCH2 python bench.py --steps 20 --warmup 5 --json-out gpurun_out/bench2.json
 [ -n "${PROF:-}" ] && run prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --steps 5 --warmup 2
