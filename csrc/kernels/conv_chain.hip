@@ -190,7 +190,10 @@ __device__ __forceinline__ uint32_t tile_off(int r, int n) {
 // pixel per lane, 8 B) right after pass pp's epilogue, so it has a whole C segment, copy-out and B segment to
 // land, instead of an LDS-DMA into the Y buffer at the start of its own pass that only the B segment covers
 // (and the barrier that publishes it). +16 VGPRs; the loads count in the wave's vmcnt bookkeeping (`ops`).
-template <int MID, int BM_, int MIDN, bool DOWN, int ST, bool BL, bool PATCH, bool RREG = false>
+// PWN (patch mode): waves along the output channels in phase A (4 = every wave all BM pixels x MID/4 channels;
+// 2 = a 2 x 2 split: half the pixels x half the channels, half the LDS pixel reads per MFMA for twice the weight
+// fragments from L2).
+template <int MID, int BM_, int MIDN, bool DOWN, int ST, bool BL, bool PATCH, bool RREG = false, int PWN_ = 4>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ChainCfg<MID, BM_, MIDN, DOWN, ST, BL>::MINW,
                                                                      ChainCfg<MID, BM_, MIDN, DOWN, ST, BL>::MINW)))
 void conv_chain_kernel(const ChainParams p) {
@@ -247,7 +250,7 @@ void conv_chain_kernel(const ChainParams p) {
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   // patch mode: the 4 waves split the channels (each all BM pixels = PFI fragments x MID/4 channels = CF
   // fragments), so every weight element is loaded by exactly one wave
-  constexpr int PWN = 4, PWM = 1;
+  constexpr int PWN = PWN_, PWM = 4 / PWN_;
   constexpr int PFI = PATCH ? BM_ / 16 / PWM : 1, CF = PATCH ? MID / 16 / PWN : 1;
   const int pwm = wave % PWM, pwn = wave / PWM;
   f32x4_t pacc[PFI][CF];
@@ -762,7 +765,7 @@ bool patch_fits(const ChainParams& p, int lds_bytes) {
   return static_cast<long>(rows) * (p.W + 2) * MID * 2 <= lds_bytes;
 }
 
-template <int MID, int BM, int MIDN, bool DOWN = false, int ST = 4, bool BL = true, bool RREG = false>
+template <int MID, int BM, int MIDN, bool DOWN = false, int ST = 4, bool BL = true, bool RREG = false, int PWN = 4>
 int launch_chain(const ChainParams& p, hipStream_t s, bool patch = false) {
   using Cfg = ChainCfg<MID, BM, MIDN, DOWN, ST, BL>;
   static bool attr = false;
@@ -771,7 +774,7 @@ int launch_chain(const ChainParams& p, hipStream_t s, bool patch = false) {
                             hipFuncAttributeMaxDynamicSharedMemorySize, Cfg::LDS_ALL) != hipSuccess)
       return AI4E_ELAUNCH;
     if constexpr (BM == 128) {
-      if (hipFuncSetAttribute(reinterpret_cast<const void*>(conv_chain_kernel<MID, BM, MIDN, DOWN, ST, BL, true, RREG>),
+      if (hipFuncSetAttribute(reinterpret_cast<const void*>(conv_chain_kernel<MID, BM, MIDN, DOWN, ST, BL, true, RREG, PWN>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, Cfg::LDS_ALL) != hipSuccess)
         return AI4E_ELAUNCH;
     }
@@ -780,7 +783,7 @@ int launch_chain(const ChainParams& p, hipStream_t s, bool patch = false) {
   const int nb = ai4e_cdiv(p.M, Cfg::BM);
   if constexpr (BM == 128) {
     if (patch && patch_fits<MID, BM>(p, Cfg::LDS)) {
-      hipLaunchKernelGGL((conv_chain_kernel<MID, BM, MIDN, DOWN, ST, BL, true, RREG>), dim3(nb), dim3(256), Cfg::LDS_ALL,
+      hipLaunchKernelGGL((conv_chain_kernel<MID, BM, MIDN, DOWN, ST, BL, true, RREG, PWN>), dim3(nb), dim3(256), Cfg::LDS_ALL,
                          s, p);
       return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
     }
@@ -847,8 +850,15 @@ AI4E_API int ai4e_conv_chain_fwd(const void* x, const void* w2, const void* b2, 
   // 3 = the 128-pixel tiles with phase A in patch mode where the shape allows it (else the ring, as 1);
   // + 8 (9, 11): the same 128-pixel tiles with the residual prefetched into registers a pass ahead (RREG)
   const bool rreg = (tile_cfg & 8) != 0 && !down && (tile_cfg & 7) != 0 && (tile_cfg & 7) != 2;
+  const bool pw2 = (tile_cfg & 16) != 0 && (tile_cfg & 7) == 3 && mid == 64;  // + 16 (19): 2 x 2 phase-A split
   tile_cfg &= 7;
   const bool patch = tile_cfg == 3;
+  if (pw2) {
+    if (down) return launch_chain<64, 128, 64, true, 4, true, false, 2>(p, stream, true);
+    if (next && midn == 128) return launch_chain<64, 128, 128, false, 4, true, false, 2>(p, stream, true);
+    return next ? launch_chain<64, 128, 64, false, 4, true, false, 2>(p, stream, true)
+                : launch_chain<64, 128, 0, false, 4, true, false, 2>(p, stream, true);
+  }
   if (down) return tile_cfg == 2 ? launch_chain<64, 128, 64, true, 4, false>(p, stream)
                                  : launch_chain<64, 128, 64, true>(p, stream, patch);
   if (rreg) {

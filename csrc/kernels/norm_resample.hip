@@ -1,7 +1,8 @@
 // K2 GroupNorm (+ReLU) and K3 bilinear 2x upsample — NHWC bf16, memory-bound, 16-B vectors per lane.
 //
 // GroupNorm is two launches: (1) per-(image, pixel-chunk) partial sums per group, reduced in-register
-// then across the workgroup in LDS and written as fp32 partials (no global atomics); (2) a finalize
+// then across the workgroup in LDS in a fixed order and written as fp32 partials (no atomics: bitwise
+// reproducible); (2) a finalize
 // workgroup per image combines the partials (fp64) into mean / rstd, then the normalize pass applies
 // (x - mean) * rstd * gamma + beta (+ReLU) and writes bf16 — optionally into a channel slice of a
 // wider buffer (U-Net concat).
@@ -33,14 +34,10 @@ __global__ __launch_bounds__(256) void gn_stats_kernel(const uint16_t* __restric
   float s[8] = {0, 0, 0, 0, 0, 0, 0, 0}, q[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   const int pbeg = chunk * GN_PIX_PER_BLOCK, pend = min(HW, pbeg + GN_PIX_PER_BLOCK);
   // the chunk's shift per group: its first pixel's value of the group's first channel
-  __shared__ float gs[64], gq[64], gk[64];
+  __shared__ float gk[64];
   if (static_cast<int>(threadIdx.x) < G) {
     const uint16_t v = x[static_cast<long>(n) * HW * ldx + xcoff + static_cast<long>(pbeg) * ldx + threadIdx.x * cg];
     gk[threadIdx.x] = __uint_as_float(static_cast<uint32_t>(v) << 16);
-  }
-  if (threadIdx.x < 64) {
-    gs[threadIdx.x] = 0.f;
-    gq[threadIdx.x] = 0.f;
   }
   __syncthreads();
   float k[8];
@@ -70,19 +67,27 @@ __global__ __launch_bounds__(256) void gn_stats_kernel(const uint16_t* __restric
     }
     for (; p < pend; p += pix_per_iter) acc(*reinterpret_cast<const uint4*>(xb + static_cast<long>(p) * ldx));
   }
-  // reduce each lane's 8 channels into its group(s), then across lanes holding the same group
-  if (p0 < pix_per_iter) {
+  // every lane's 8 channel sums go to LDS; one thread per group then adds its group's (pixel row, channel)
+  // terms in a fixed order, so the partials (and everything normalized by them) are bitwise reproducible
+  // run to run (LDS float atomics would add in arrival order)
+  __shared__ float rs[256 * 8], rq[256 * 8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int g = (8 * c8 + j) / cg;
-      atomicAdd(&gs[g], s[j]);
-      atomicAdd(&gq[g], q[j]);
-    }
+  for (int j = 0; j < 8; ++j) {
+    rs[threadIdx.x * 8 + j] = s[j];
+    rq[threadIdx.x * 8 + j] = q[j];
   }
   __syncthreads();
   if (static_cast<int>(threadIdx.x) < G) {
-    float* o = partials + ((static_cast<long>(n) * nchunks + chunk) * G + threadIdx.x) * GN_PARTIAL;
-    *reinterpret_cast<float4*>(o) = make_float4(gs[threadIdx.x], gq[threadIdx.x], gk[threadIdx.x], 0.f);
+    const int g = threadIdx.x;
+    float S = 0.f, Q = 0.f;
+    for (int pp = 0; pp < pix_per_iter; ++pp)
+      for (int ch = g * cg; ch < (g + 1) * cg; ++ch) {
+        const int t = pp * lanes_per_pix + (ch >> 3);
+        S += rs[t * 8 + (ch & 7)];
+        Q += rq[t * 8 + (ch & 7)];
+      }
+    float* o = partials + ((static_cast<long>(n) * nchunks + chunk) * G + g) * GN_PARTIAL;
+    *reinterpret_cast<float4*>(o) = make_float4(S, Q, gk[g], 0.f);
   }
 }
 

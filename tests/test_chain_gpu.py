@@ -47,7 +47,7 @@ CASES = [
 
 
 @pytest.mark.parametrize("case", CASES)
-@pytest.mark.parametrize("tile", [0, 1, 3, 9, 11])
+@pytest.mark.parametrize("tile", [0, 1, 3, 9, 11, 19])
 def test_conv_chain(case, tile):
     """tile 3 = phase A from the LDS input patch (stride 1 and a patch that fits; other shapes fall back to the
     ring, which the same comparison then covers)."""
@@ -55,6 +55,8 @@ def test_conv_chain(case, tile):
     midn = 0 if not nxt else (mid if nxt is True else nxt)
     if tile in (1, 9) and (mid != 64 or midn == 128):
         pytest.skip("tile config 1 is the MID-64, same-width variant")
+    if tile == 19 and mid != 64:
+        pytest.skip("tile config 19 (2 x 2 phase-A split) is the MID-64 variant")
     assert chain_kernel_builds(mid, midn)
     torch.manual_seed(7)
     c2 = pack_conv(torch.randn(mid, mid, 3, 3) / (9 * mid) ** 0.5, torch.randn(mid) * 0.1, stride=s, pad=1).to(DEV)
@@ -133,7 +135,7 @@ def test_softmax_topk(shape):
 
 
 @pytest.mark.parametrize("shape", [(2, 56, 56), (1, 15, 13), (3, 12, 8)])
-@pytest.mark.parametrize("tile", [-1, 3])
+@pytest.mark.parametrize("tile", [-1, 3, 19])
 def test_conv_chain_down(shape, tile):
     """K1c DOWN mode: the residual is the 1x1 projection of the block input, folded into c3's K."""
     n, h, w = shape
