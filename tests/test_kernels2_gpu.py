@@ -38,6 +38,17 @@ def test_groupnorm(shape, groups, relu):
     assert (y.float() - ref).abs().max().item() < 0.05
 
 
+@pytest.mark.parametrize("shape,groups", [((2, 64, 64, 64), 32), ((1, 40, 40, 512), 32), ((3, 9, 9, 32), 8)])
+def test_groupnorm_bitwise_reproducible(shape, groups):
+    """The statistics reduction has a fixed order (no float atomics): repeated runs give identical bits."""
+    torch.manual_seed(5)
+    x = (torch.randn(*shape) * 3 + 1.0).to(DEV).bfloat16()
+    g, b = torch.rand(shape[-1]) + 0.5, torch.randn(shape[-1])
+    first = group_norm_nhwc(x, g, b, groups, relu=True)
+    for _ in range(5):
+        assert torch.equal(group_norm_nhwc(x, g, b, groups, relu=True), first)
+
+
 @pytest.mark.parametrize("dc,std", [(50.0, 0.5), (300.0, 2.0)])
 def test_groupnorm_large_dc_offset(dc, std):
     """A group whose mean is far from 0 relative to its spread: the shifted chunk sums keep E[x^2] - mean^2
