@@ -193,7 +193,12 @@ __device__ __forceinline__ uint32_t tile_off(int r, int n) {
 // PWN (patch mode): waves along the output channels in phase A (4 = every wave all BM pixels x MID/4 channels;
 // 2 = a 2 x 2 split: half the pixels x half the channels, half the LDS pixel reads per MFMA for twice the weight
 // fragments from L2).
-template <int MID, int BM_, int MIDN, bool DOWN, int ST, bool BL, bool PATCH, bool RREG = false, int PWN_ = 4>
+// PAD (patch mode, tile config + 32): pixel slots padded to RB + 32 bytes and NOT swizzled: the padding gives the
+// same bank-conflict profile as the XOR swizzle (2-way on about half the fragment reads, bench model), and a
+// fragment's address becomes slot * RBS + 16 * lg per tap with the K step as the ds_read immediate, instead of a
+// per-step XOR + shift + add per fragment (the chain kernels issue ~4-8 VALU per MFMA; PMC, profiles/r3_pad/).
+template <int MID, int BM_, int MIDN, bool DOWN, int ST, bool BL, bool PATCH, bool RREG = false, int PWN_ = 4,
+          bool PAD = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ChainCfg<MID, BM_, MIDN, DOWN, ST, BL>::MINW,
                                                                      ChainCfg<MID, BM_, MIDN, DOWN, ST, BL>::MINW)))
 void conv_chain_kernel(const ChainParams p) {
@@ -261,29 +266,49 @@ void conv_chain_kernel(const ChainParams p) {
   if constexpr (PATCH) {
     constexpr int RB = MID * 2;    // bytes per pixel slot
     constexpr int CPS = RB / 16;   // 16-B chunks per slot
+    constexpr int RBS = PAD ? RB + 32 : RB;  // slot stride
     const int W = p.W, W2 = p.W + 2;
     const int r_lo = m0 / W;                          // flattened (image, row) index of the first pixel
     const int r_hi = (min(m0 + BM, p.M) - 1) / W;
     const int prows = r_hi - r_lo + 3;                // + one halo row above and below
     const int nrows = p.M / W;                        // N * H
     const int ipr = W * RB / 1024;                    // 1-KB DMA pieces per patch row (host: W * RB % 1024 == 0)
-    // the patch: row j = flattened row r_lo - 1 + j, data in slots 1..W (one contiguous 1-KB piece per wave DMA)
-    for (int I = wave; I < prows * ipr; I += 4) {
-      const int j = I / ipr, piece = I - j * ipr;
-      const int R = r_lo - 1 + j;
-      const int o = piece * 1024 + 16 * lane;
-      const int s1 = o / RB;                          // data slot in the row (0-based)
-      const int slot = j * W2 + 1 + s1;
-      const int q = ((o % RB) >> 4) ^ psw<MID>(slot);  // logical chunk that belongs at this physical chunk
-      const bool ok = R >= 0 && R < nrows;
-      glds16(ok ? static_cast<const void*>(p.x + (static_cast<long>(R) * W + s1) * p.ldx + 8 * q) : zero,
-             sb + (j * W2 + 1) * RB + piece * 1024);
-    }
-    // zero pad slots (left / right of every row; slot 0 doubles as the zero source of masked taps)
-    for (int g = tid; g < prows * 2 * CPS; g += 256) {
-      const int j = g / (2 * CPS), e = g - j * 2 * CPS;
-      const int slot = j * W2 + (e >= CPS ? W + 1 : 0);
-      *reinterpret_cast<uint4*>(smem + slot * RB + (e % CPS) * 16) = make_uint4(0u, 0u, 0u, 0u);
+    if constexpr (PAD) {
+      // padded rows: slot k of patch row j at (j * W2 + k) * RBS, slots 0 and W + 1 and the pad bytes from the zero
+      // chunk; one 1-KB DMA piece per wave instruction, the lanes past the row's end masked off
+      const int rowb = W2 * RBS;
+      const int ipr2 = (rowb + 1023) / 1024;
+      for (int I = wave; I < prows * ipr2; I += 4) {
+        const int j = I / ipr2, piece = I - j * ipr2;
+        const int R = r_lo - 1 + j;
+        const int o = piece * 1024 + 16 * lane;
+        if (o < rowb) {
+          const int k = o / RBS;                      // slot in the row (compile-time divisor)
+          const int pos = (o - k * RBS) >> 4;         // 16-B chunk in the slot (>= CPS: pad)
+          const bool ok = R >= 0 && R < nrows && k >= 1 && k <= W && pos < CPS;
+          glds16(ok ? static_cast<const void*>(p.x + (static_cast<long>(R) * W + k - 1) * p.ldx + 8 * pos) : zero,
+                 sb + j * rowb + piece * 1024);
+        }
+      }
+    } else {
+      // the patch: row j = flattened row r_lo - 1 + j, data in slots 1..W (one contiguous 1-KB piece per wave DMA)
+      for (int I = wave; I < prows * ipr; I += 4) {
+        const int j = I / ipr, piece = I - j * ipr;
+        const int R = r_lo - 1 + j;
+        const int o = piece * 1024 + 16 * lane;
+        const int s1 = o / RB;                          // data slot in the row (0-based)
+        const int slot = j * W2 + 1 + s1;
+        const int q = ((o % RB) >> 4) ^ psw<MID>(slot);  // logical chunk that belongs at this physical chunk
+        const bool ok = R >= 0 && R < nrows;
+        glds16(ok ? static_cast<const void*>(p.x + (static_cast<long>(R) * W + s1) * p.ldx + 8 * q) : zero,
+               sb + (j * W2 + 1) * RB + piece * 1024);
+      }
+      // zero pad slots (left / right of every row; slot 0 doubles as the zero source of masked taps)
+      for (int g = tid; g < prows * 2 * CPS; g += 256) {
+        const int j = g / (2 * CPS), e = g - j * 2 * CPS;
+        const int slot = j * W2 + (e >= CPS ? W + 1 : 0);
+        *reinterpret_cast<uint4*>(smem + slot * RB + (e % CPS) * 16) = make_uint4(0u, 0u, 0u, 0u);
+      }
     }
     // per pixel fragment: slot of tap (0, 0) and the row-validity bits of kh = 0, 1, 2
     int sbase[PFI], vmask[PFI];
@@ -318,14 +343,24 @@ void conv_chain_kernel(const ChainParams p) {
 #pragma unroll
       for (int i = 0; i < PFI; ++i) {
         const int slot = (vmask[i] >> kh) & 1 ? sbase[i] + kh * W2 + kw : 0;
-        soff[i] = slot * RB;
-        sws[i] = psw<MID>(slot);
+        if constexpr (PAD) {
+          soff[i] = slot * RBS + 16 * lg;
+        } else {
+          soff[i] = slot * RB;
+          sws[i] = psw<MID>(slot);
+        }
       }
     };
     auto read_px = [&](int s, bf16x8_t (&f)[PFI]) __attribute__((always_inline)) {
       const int q = (s % SPT) * 4 + lg;
 #pragma unroll
-      for (int i = 0; i < PFI; ++i) f[i] = *reinterpret_cast<const bf16x8_t*>(smem + soff[i] + ((q ^ sws[i]) << 4));
+      for (int i = 0; i < PFI; ++i) {
+        if constexpr (PAD) {
+          f[i] = *reinterpret_cast<const bf16x8_t*>(smem + soff[i] + (s % SPT) * 64);
+        } else {
+          f[i] = *reinterpret_cast<const bf16x8_t*>(smem + soff[i] + ((q ^ sws[i]) << 4));
+        }
+      }
     };
     tap_slots(0);
     read_px(0, fx[0]);
@@ -758,14 +793,15 @@ void conv_chain_kernel(const ChainParams p) {
 
 // Patch mode (phase A from an LDS patch of the input rows) applies to stride 1, an input row of whole 1-KB
 // DMA pieces, a dense [N, H, W, MID] input, 128-pixel tiles and a patch that fits the config's LDS.
-template <int MID, int BM>
+template <int MID, int BM, bool PAD = false>
 bool patch_fits(const ChainParams& p, int lds_bytes) {
-  if (BM != 128 || p.stride != 1 || p.ldx != MID || (p.W * MID * 2) % 1024) return false;
+  if (BM != 128 || p.stride != 1 || p.ldx != MID || (!PAD && (p.W * MID * 2) % 1024)) return false;
   const int rows = (BM - 1 + p.W - 1) / p.W + 1 + 2;  // most rows BM consecutive pixels touch, + 2 halo rows
-  return static_cast<long>(rows) * (p.W + 2) * MID * 2 <= lds_bytes;
+  return static_cast<long>(rows) * (p.W + 2) * (MID * 2 + (PAD ? 32 : 0)) <= lds_bytes;
 }
 
-template <int MID, int BM, int MIDN, bool DOWN = false, int ST = 4, bool BL = true, bool RREG = false, int PWN = 4>
+template <int MID, int BM, int MIDN, bool DOWN = false, int ST = 4, bool BL = true, bool RREG = false, int PWN = 4,
+          bool PAD = false>
 int launch_chain(const ChainParams& p, hipStream_t s, bool patch = false) {
   using Cfg = ChainCfg<MID, BM, MIDN, DOWN, ST, BL>;
   static bool attr = false;
@@ -774,7 +810,7 @@ int launch_chain(const ChainParams& p, hipStream_t s, bool patch = false) {
                             hipFuncAttributeMaxDynamicSharedMemorySize, Cfg::LDS_ALL) != hipSuccess)
       return AI4E_ELAUNCH;
     if constexpr (BM == 128) {
-      if (hipFuncSetAttribute(reinterpret_cast<const void*>(conv_chain_kernel<MID, BM, MIDN, DOWN, ST, BL, true, RREG, PWN>),
+      if (hipFuncSetAttribute(reinterpret_cast<const void*>(conv_chain_kernel<MID, BM, MIDN, DOWN, ST, BL, true, RREG, PWN, PAD>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, Cfg::LDS_ALL) != hipSuccess)
         return AI4E_ELAUNCH;
     }
@@ -782,8 +818,8 @@ int launch_chain(const ChainParams& p, hipStream_t s, bool patch = false) {
   }
   const int nb = ai4e_cdiv(p.M, Cfg::BM);
   if constexpr (BM == 128) {
-    if (patch && patch_fits<MID, BM>(p, Cfg::LDS)) {
-      hipLaunchKernelGGL((conv_chain_kernel<MID, BM, MIDN, DOWN, ST, BL, true, RREG, PWN>), dim3(nb), dim3(256), Cfg::LDS_ALL,
+    if (patch && patch_fits<MID, BM, PAD>(p, Cfg::LDS)) {
+      hipLaunchKernelGGL((conv_chain_kernel<MID, BM, MIDN, DOWN, ST, BL, true, RREG, PWN, PAD>), dim3(nb), dim3(256), Cfg::LDS_ALL,
                          s, p);
       return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
     }
@@ -851,8 +887,12 @@ AI4E_API int ai4e_conv_chain_fwd(const void* x, const void* w2, const void* b2, 
   // + 8 (9, 11): the same 128-pixel tiles with the residual prefetched into registers a pass ahead (RREG)
   const bool rreg = (tile_cfg & 8) != 0 && !down && (tile_cfg & 7) != 0 && (tile_cfg & 7) != 2;
   const bool pw2 = (tile_cfg & 16) != 0 && (tile_cfg & 7) == 3 && mid == 64;  // + 16 (19): 2 x 2 phase-A split
+  const bool pad = (tile_cfg & 32) != 0 && (tile_cfg & 7) == 3 && mid == 128 && !down;  // + 32 (35): padded patch
   tile_cfg &= 7;
   const bool patch = tile_cfg == 3;
+  if (pad)
+    return next ? launch_chain<128, 128, 128, false, 4, true, false, 4, true>(p, stream, true)
+                : launch_chain<128, 128, 0, false, 4, true, false, 4, true>(p, stream, true);
   if (pw2) {
     if (down) return launch_chain<64, 128, 64, true, 4, true, false, 2>(p, stream, true);
     if (next && midn == 128) return launch_chain<64, 128, 128, false, 4, true, false, 2>(p, stream, true);

@@ -47,7 +47,7 @@ CASES = [
 
 
 @pytest.mark.parametrize("case", CASES)
-@pytest.mark.parametrize("tile", [0, 1, 3, 9, 11, 19])
+@pytest.mark.parametrize("tile", [0, 1, 3, 9, 11, 19, 35])
 def test_conv_chain(case, tile):
     """tile 3 = phase A from the LDS input patch (stride 1 and a patch that fits; other shapes fall back to the
     ring, which the same comparison then covers)."""
