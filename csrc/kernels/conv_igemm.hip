@@ -47,6 +47,31 @@ using ai4e_conv::wait_vmcnt_n;
 // Source of the zero 16-B chunks the DMA gather reads for padding / out-of-range taps.
 __device__ __attribute__((aligned(64))) uint16_t g_zero_chunk[32];
 
+// Diagnostic build (AI4E_K256_STAMPS=1): s_memtime stamps in the 256-wide kernel's 4-phase loop, per wave, summed per
+// segment: 0 = LDS fragment reads + DMA issue, 1 = counted vmcnt wait, 2 = the two barriers of a phase (+ the
+// lgkmcnt drain), 3 = MFMAs, 4 = prologue, 5 = epilogue. Written to g_k256_stamps (read SHARES: a stamp drains the
+// wave's LDS reads, moving their latency into segment 0).
+#ifndef AI4E_K256_STAMPS
+#define AI4E_K256_STAMPS 0
+#endif
+constexpr int K256_NSEG = 6, K256_MAXW = 32768;
+#if AI4E_K256_STAMPS
+__device__ unsigned long long g_k256_stamps[K256_MAXW * K256_NSEG];
+#define K256_STAMP(k)                                                              \
+  do {                                                                             \
+    __builtin_amdgcn_sched_barrier(0);                                             \
+    unsigned long long _t;                                                         \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");     \
+    __builtin_amdgcn_sched_barrier(0);                                             \
+    k_sum[k] += _t - k_last;                                                       \
+    k_last = _t;                                                                   \
+  } while (0)
+#else
+#define K256_STAMP(k) \
+  do {                \
+  } while (0)
+#endif
+
 struct ConvParams {
   const uint16_t* x;
   const uint16_t* w;
@@ -521,6 +546,10 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
   constexpr int MF1 = X1 / 16;     // u3 fragments per wave
   constexpr int MFR = 4 + MF1;     // accumulator rows
   __shared__ __attribute__((aligned(1024))) uint8_t smem[2 * 4 * U_BYTES];  // the only LDS object
+#if AI4E_K256_STAMPS
+  unsigned long long k_sum[K256_NSEG] = {0, 0, 0, 0, 0, 0}, k_last;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(k_last)::"memory");
+#endif
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -668,13 +697,17 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
 #define K256_SYNC_LOADS(G, CHECKED, NS)                                                            \
   if (CHECKED) {                                                                                   \
     stage_phase(G);                                                                                \
+    K256_STAMP(0);                                                                                 \
     wait_phase(G);                                                                                 \
   } else {                                                                                         \
     stage(phase_tile(G), phase_unit(G));                                                           \
+    K256_STAMP(0);                                                                                 \
     wait_vmcnt<NS>();                                                                              \
   }                                                                                                \
+  K256_STAMP(1);                                                                                   \
   __builtin_amdgcn_s_barrier();                                                                    \
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                               \
+  K256_STAMP(2);
 #define K256_TILE(KT, CHECKED)                                                                     \
   {                                                                                                \
     const int g = 4 * (KT);                                                                        \
@@ -683,21 +716,29 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
     K256_READ_X(0, KT)                                                                             \
     K256_SYNC_LOADS(g + 1, CHECKED, 6)                                                                \
     K256_MFMA(0, 0, w0r)                                                                           \
+    K256_STAMP(3);                                                                                 \
     __builtin_amdgcn_s_barrier();                                                                  \
+    K256_STAMP(2);                                                                                 \
     /* phase 2: quadrant (0,1) */                                                                  \
     K256_READ_W(w1r, 1, KT)                                                                        \
     K256_SYNC_LOADS(g + 2, CHECKED, 4 + L3)                                                                \
     K256_MFMA(0, 1, w1r)                                                                           \
+    K256_STAMP(3);                                                                                 \
     __builtin_amdgcn_s_barrier();                                                                  \
+    K256_STAMP(2);                                                                                 \
     /* phase 3: quadrant (1,1) */                                                                  \
     K256_READ_X(1, KT)                                                                             \
     K256_SYNC_LOADS(g + 3, CHECKED, 4 + L3)                                                                \
     K256_MFMA(1, 1, w1r)                                                                           \
+    K256_STAMP(3);                                                                                 \
     __builtin_amdgcn_s_barrier();                                                                  \
+    K256_STAMP(2);                                                                                 \
     /* phase 4: quadrant (1,0), fragments already in registers */                                  \
     K256_SYNC_LOADS(g + 4, CHECKED, 4 + L3)                                                                \
     K256_MFMA(1, 0, w0r)                                                                           \
+    K256_STAMP(3);                                                                                 \
     __builtin_amdgcn_s_barrier();                                                                  \
+    K256_STAMP(2);                                                                                 \
   }
 
   // 3-phase schedule (PH3): phase g = 3t + p, g >= -6 (the prologue is g = -4 .. -1)
@@ -768,6 +809,7 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
     else wait_vmcnt<0>();
     __builtin_amdgcn_s_barrier();
     if (wr == 1) __builtin_amdgcn_s_barrier();  // the stagger: group 1 trails by one barrier
+    K256_STAMP(4);
     for (; kt + 2 < nk; ++kt) K256_TILE(kt, 0)
     for (; kt < nk; ++kt) K256_TILE(kt, 1)
   }
@@ -826,6 +868,14 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
     }
     __syncthreads();
   }
+#if AI4E_K256_STAMPS
+  wait_vmcnt<0>();
+  K256_STAMP(5);
+  if (lane == 0 && blockIdx.x * 8 + wave < K256_MAXW) {
+#pragma unroll
+    for (int k = 0; k < K256_NSEG; ++k) g_k256_stamps[(blockIdx.x * 8 + wave) * K256_NSEG + k] = k_sum[k];
+  }
+#endif
 }
 
 }  // namespace
@@ -975,6 +1025,14 @@ AI4E_API int ai4e_conv2d_gn_fwd(const void* x, const void* w, const void* bias, 
   return conv2d_impl<false>(x, w, bias, res, y, N, H, W, C, ldx, xcoff, KH, KW, stride, pad, OH, OW, Kout, Kpad, ldy,
                             ycoff, ldres, relu, tile_cfg, static_cast<float*>(gn_partials), gn_groups, stream);
 }
+
+#if AI4E_K256_STAMPS
+// Diagnostic build only: per-wave segment cycle sums of the last 256-wide K1 launch (32768 waves x 6).
+AI4E_API int ai4e_k256_stamps_read(void* host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_k256_stamps), sizeof(g_k256_stamps)) == hipSuccess ? AI4E_OK
+                                                                                                    : AI4E_ELAUNCH;
+}
+#endif
 
 // Weight rows must be padded to this multiple (tile height in the channel dimension).
 AI4E_API int ai4e_conv2d_weight_row_align() { return 256; }

@@ -16,8 +16,11 @@ run() {  # name timeout cmd...
   if [ $rc -ne 0 ]; then echo "STOP after $name"; exit $rc; fi
 }
 [ -n "${TESTS:-}" ] && run focus 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -p no:cacheprovider $TESTS
+[ -n "${FULL:-}" ] && run pytest_gpu 900 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread -p no:cacheprovider
+[ -n "${SMOKE:-}" ] && run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 [ -n "${CHAIN_CFGS:-}" ] && run chain_ab 300 python -u bench/chain_patch_ab.py
 [ -n "${MICRO:-}" ] && run micro 300 env CFGS=${MICRO_CFGS:-9,10} TWO=1 python -u bench/conv_micro.py $MICRO
+[ -n "${K256ST:-}" ] && run k256st 300 python -u tools/k256_stamps.py
 [ -n "${CUSPLIT:-}" ] && run cusplit 400 python -u bench/cu_split_probe.py $CUSPLIT
 [ -n "${BIGB:-}" ] && for bb in $BIGB; do run "bigb_$bb" 400 env B=$bb NO_SPLIT=1 NB=30 python -u bench/cu_split_probe.py; done
 [ -n "${BENCH:-}" ] && run bench 300 python bench.py --steps 20 --warmup 5 --json-out gpurun_out/bench.json
@@ -32,5 +35,9 @@ if [ -n "${AB:-}" ]; then
     lab=${c%%:*}; a=${c#*:}; envs=${a%%|*}; bargs=${a#*|}; [ "$bargs" = "$a" ] && bargs=""
     run "ab_$lab" 300 env $envs python bench.py --steps 20 --warmup 5 $bargs --json-out "gpurun_out/ab_$lab.json"
   done
+fi
+if [ -n "${PMC:-}" ]; then
+  run pmc 700 bash tools/pmc_resnet.sh
+  python tools/pmc_summary.py gpurun_out/pmc > gpurun_out/pmc_summary.txt 2>&1; tail -3 gpurun_out/pmc_summary.txt
 fi
 echo "=== done"
