@@ -535,7 +535,13 @@ constexpr int U_ROWS = 128, U_BYTES = U_ROWS * 128;
 // PH3 == 2 (tile config 11): the 3-phase schedule with a static s_setprio 1 for the trailing wave group (waves
 // 4-7, the arbitration loser on every shared SIMD) instead of the per-segment priority flips around the MFMAs
 // (MI355X_MICROARCH.md "Two waves per SIMD", item 4).
-template <int GATHER, int BM, bool F16 = false, int PH3 = 0>
+// DMAI (4-phase schedule, tile configs 12 / 13 = 9 / 6): a phase's staging DMAs are issued inside the wave's own
+// MFMA segment (between its two halves) instead of before the phase's first barrier, so the load segment the
+// partner's MFMAs must cover holds only the fragment reads and the wait (the stamps of config 9: reads + DMA issue
+// 31 % of a wave's life against 24 % MFMA, profiles/r3_k256/). Staging then lands one barrier later, which every
+// rule above tolerates: the slot's last read is further back, and the wait at phase g counts only the DMAs of
+// phases g-2 and g-1 (phase g's are not issued yet).
+template <int GATHER, int BM, bool F16 = false, int PH3 = 0, bool DMAI = false>
 __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) {
   static_assert(GATHER == GATHER_TAP || GATHER == GATHER_POINTWISE, "256 tile needs C % 64 == 0");
   static_assert(BM == 256 || BM == 192, "wave groups of 128 or 96 pixels");
@@ -692,10 +698,27 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
               mfma_16x16x32<F16>(WR[j][s], xr[i][s], acc[4 * (MQ) + i][2 * (NQ) + j]);             \
     if constexpr (PH3 < 2) __builtin_amdgcn_s_setprio(0);                                          \
   }
+#define K256_MFMA_ST(MQ, NQ, WR, STAGE_STMT)                                                       \
+  {                                                                                                \
+    if constexpr (PH3 < 2) __builtin_amdgcn_s_setprio(1);                                          \
+    _Pragma("unroll") for (int i = 0; i < ((MQ) ? MF1 : 4); ++i)                                   \
+      _Pragma("unroll") for (int j = 0; j < 2; ++j)                                                \
+        acc[4 * (MQ) + i][2 * (NQ) + j] =                                                          \
+            mfma_16x16x32<F16>(WR[j][0], xr[i][0], acc[4 * (MQ) + i][2 * (NQ) + j]);               \
+    STAGE_STMT;                                                                                    \
+    _Pragma("unroll") for (int i = 0; i < ((MQ) ? MF1 : 4); ++i)                                   \
+      _Pragma("unroll") for (int j = 0; j < 2; ++j)                                                \
+        acc[4 * (MQ) + i][2 * (NQ) + j] =                                                          \
+            mfma_16x16x32<F16>(WR[j][1], xr[i][1], acc[4 * (MQ) + i][2 * (NQ) + j]);               \
+    if constexpr (PH3 < 2) __builtin_amdgcn_s_setprio(0);                                          \
+  }
 // CHECKED = 0: steady state (kt + 2 < nk): every phase stages a unit, 3 phases of DMAs in flight
 // (NS = this wave's DMAs of those 3 phases: 6 at phase 1, 4 + L3 at phases 2-4, which stage u3 or follow it)
 #define K256_SYNC_LOADS(G, CHECKED, NS)                                                            \
-  if (CHECKED) {                                                                                   \
+  if constexpr (DMAI) {                                                                            \
+    K256_STAMP(0);                                                                                 \
+    wait_vmcnt_n(loads_of((G) - 2) + loads_of((G) - 1));                                           \
+  } else if (CHECKED) {                                                                            \
     stage_phase(G);                                                                                \
     K256_STAMP(0);                                                                                 \
     wait_phase(G);                                                                                 \
@@ -715,27 +738,43 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
     K256_READ_W(w0r, 0, KT)                                                                        \
     K256_READ_X(0, KT)                                                                             \
     K256_SYNC_LOADS(g + 1, CHECKED, 6)                                                                \
-    K256_MFMA(0, 0, w0r)                                                                           \
+    if constexpr (DMAI) {                                                                          \
+      K256_MFMA_ST(0, 0, w0r, if (CHECKED) stage_phase(g + 1); else stage(phase_tile(g + 1), phase_unit(g + 1))) \
+    } else {                                                                                       \
+      K256_MFMA(0, 0, w0r)                                                                         \
+    }                                                                                              \
     K256_STAMP(3);                                                                                 \
     __builtin_amdgcn_s_barrier();                                                                  \
     K256_STAMP(2);                                                                                 \
     /* phase 2: quadrant (0,1) */                                                                  \
     K256_READ_W(w1r, 1, KT)                                                                        \
     K256_SYNC_LOADS(g + 2, CHECKED, 4 + L3)                                                                \
-    K256_MFMA(0, 1, w1r)                                                                           \
+    if constexpr (DMAI) {                                                                          \
+      K256_MFMA_ST(0, 1, w1r, if (CHECKED) stage_phase(g + 2); else stage(phase_tile(g + 2), phase_unit(g + 2))) \
+    } else {                                                                                       \
+      K256_MFMA(0, 1, w1r)                                                                         \
+    }                                                                                              \
     K256_STAMP(3);                                                                                 \
     __builtin_amdgcn_s_barrier();                                                                  \
     K256_STAMP(2);                                                                                 \
     /* phase 3: quadrant (1,1) */                                                                  \
     K256_READ_X(1, KT)                                                                             \
     K256_SYNC_LOADS(g + 3, CHECKED, 4 + L3)                                                                \
-    K256_MFMA(1, 1, w1r)                                                                           \
+    if constexpr (DMAI) {                                                                          \
+      K256_MFMA_ST(1, 1, w1r, if (CHECKED) stage_phase(g + 3); else stage(phase_tile(g + 3), phase_unit(g + 3))) \
+    } else {                                                                                       \
+      K256_MFMA(1, 1, w1r)                                                                         \
+    }                                                                                              \
     K256_STAMP(3);                                                                                 \
     __builtin_amdgcn_s_barrier();                                                                  \
     K256_STAMP(2);                                                                                 \
     /* phase 4: quadrant (1,0), fragments already in registers */                                  \
     K256_SYNC_LOADS(g + 4, CHECKED, 4 + L3)                                                                \
-    K256_MFMA(1, 0, w0r)                                                                           \
+    if constexpr (DMAI) {                                                                          \
+      K256_MFMA_ST(1, 0, w0r, if (CHECKED) stage_phase(g + 4); else stage(phase_tile(g + 4), phase_unit(g + 4))) \
+    } else {                                                                                       \
+      K256_MFMA(1, 0, w0r)                                                                         \
+    }                                                                                              \
     K256_STAMP(3);                                                                                 \
     __builtin_amdgcn_s_barrier();                                                                  \
     K256_STAMP(2);                                                                                 \
@@ -818,6 +857,7 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
 #undef K256_TILE
 #undef K256_SYNC_LOADS
 #undef K256_MFMA
+#undef K256_MFMA_ST
 #undef K256_READ_W
 #undef K256_READ_X
   if (wr == 0) __builtin_amdgcn_s_barrier();  // re-align the two groups
@@ -917,7 +957,7 @@ int launch(const ConvParams& p0, hipStream_t s) {
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
 }
 
-template <int BM, bool F16 = false, int PH3 = 0>
+template <int BM, bool F16 = false, int PH3 = 0, bool DMAI = false>
 int launch256(const ConvParams& p0, hipStream_t s) {
   ConvParams p = p0;
   // 256 tile: C % 64 (one tap per 64-wide K tile), 16-B output/residual rows, Kout % 8
@@ -929,9 +969,9 @@ int launch256(const ConvParams& p0, hipStream_t s) {
   p.zero = zero_chunk_ptr();
   if (!p.zero) return AI4E_ELAUNCH;
   if (p.KH == 1 && p.KW == 1 && p.pad == 0)
-    hipLaunchKernelGGL((conv_igemm256_kernel<GATHER_POINTWISE, BM, F16, PH3>), dim3(nb), dim3(512), 0, s, p);
+    hipLaunchKernelGGL((conv_igemm256_kernel<GATHER_POINTWISE, BM, F16, PH3, DMAI>), dim3(nb), dim3(512), 0, s, p);
   else
-    hipLaunchKernelGGL((conv_igemm256_kernel<GATHER_TAP, BM, F16, PH3>), dim3(nb), dim3(512), 0, s, p);
+    hipLaunchKernelGGL((conv_igemm256_kernel<GATHER_TAP, BM, F16, PH3, DMAI>), dim3(nb), dim3(512), 0, s, p);
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
 }
 
@@ -943,7 +983,8 @@ int launch256(const ConvParams& p0, hipStream_t s) {
 // ping-pong phases (needs C % 64 == 0, Kout % 8 == 0); 7/8 = the 128x128 / 256x64 tiles with a 3-stage
 // ring (48 KB, two-pass LDS epilogue) built for three workgroups per CU; 9 = the 256x256 schedule with
 // 192-pixel tiles (one tile per CU for 250-image 14x14 layers); 10 = config 9 with three 16-MFMA phases per K tile,
-// 11 = 10 with a static priority for the trailing wave group.
+// 11 = 10 with a static priority for the trailing wave group; 12 / 13 = 9 / 6 with the staging DMAs issued inside
+// the MFMA segments.
 // relu: bit 0 = ReLU; bit 1 = `res` is on the half-resolution grid [N, OH/2, OW/2, ldres] (nearest 2x
 // upsample of the residual, OH and OW even).
 namespace {
@@ -972,7 +1013,7 @@ int conv2d_impl(const void* x, const void* w, const void* bias, const void* res,
     // channel tile, tiles that never straddle images, full 16-B output rows
     const bool tall = tile_cfg == 2 || tile_cfg == 5 || tile_cfg == 8;
     const int bm = tall ? 256 : 128, bn = tall ? 64 : 128;
-    if (tile_cfg == 3 || tile_cfg == 6 || tile_cfg == 9 || tile_cfg == 10 || tile_cfg == 11 || gn_groups <= 0 || Kout % gn_groups || (OH * OW) % bm || Kout % 8 ||
+    if (tile_cfg == 3 || tile_cfg == 6 || tile_cfg == 9 || tile_cfg >= 10 || gn_groups <= 0 || Kout % gn_groups || (OH * OW) % bm || Kout % 8 ||
         ldy % 8 || ycoff % 8 || (res && ldres % 8) || bn % (Kout / gn_groups))
       return AI4E_EINVAL;
     p.gnp = gnp;
@@ -990,6 +1031,8 @@ int conv2d_impl(const void* x, const void* w, const void* bias, const void* res,
     case 9: return launch256<192, F16>(p, stream);
     case 10: return launch256<192, F16, 1>(p, stream);
     case 11: return launch256<192, F16, 2>(p, stream);
+    case 12: return launch256<192, F16, 0, true>(p, stream);
+    case 13: return launch256<256, F16, 0, true>(p, stream);
     default: return AI4E_EINVAL;
   }
 }
