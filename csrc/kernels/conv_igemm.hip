@@ -545,7 +545,13 @@ template <int GATHER, int BM, bool F16 = false, int PH3 = 0, bool DMAI = false>
 __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) {
   static_assert(GATHER == GATHER_TAP || GATHER == GATHER_POINTWISE, "256 tile needs C % 64 == 0");
   static_assert(BM == 256 || BM == 192, "wave groups of 128 or 96 pixels");
-  static_assert(PH3 == 0 || BM == 192, "the 3-phase schedule is the 192-pixel tile's");
+  static_assert(PH3 == 0 || PH3 == 3 || BM == 192, "the 3-phase schedule is the 192-pixel tile's");
+  // PH3 == 3 (tile configs 14 / 15 = 9 / 6 on v_mfma_f32_32x32x16): the same 4-phase schedule and staging, with
+  // 32x32 output blocks (a phase = one 32-channel block x the quadrant's 32-pixel blocks x 4 K16 steps): half the
+  // MFMA instructions for the same pipe cycles, so an MFMA wave blocks its SIMD partner's issue 8 of every 32
+  // cycles instead of 8 of 16 (the stamps: the partner's load segment outlasts the MFMA segment)
+  constexpr bool M32 = PH3 == 3;
+  static_assert(!(M32 && DMAI), "one variant at a time");
   constexpr int WROWS = BM / 2;    // pixels per wave group
   constexpr int X1 = WROWS - 64;   // u3 rows per wave group
   constexpr int L3 = X1 / 32;      // DMAs per lane for u3
@@ -659,11 +665,25 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
   // wait until this wave's DMAs of phases <= g-3 have landed
   auto wait_phase = [&](int g) { wait_vmcnt_n(loads_of(g - 2) + loads_of(g - 1) + loads_of(g)); };
 
-  f32x4_t acc[MFR][4];
+  f32x4_t acc[M32 ? 1 : MFR][4];
 #pragma unroll
-  for (int i = 0; i < MFR; ++i)
+  for (int i = 0; i < (M32 ? 1 : MFR); ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  constexpr int PB = WROWS / 32;  // M32: 32-pixel blocks per wave (2 in XQ0, X1 / 32 in XQ1)
+  f32x16_t acc32[M32 ? PB : 1][2];
+#pragma unroll
+  for (int i = 0; i < (M32 ? PB : 1); ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc32[i][j][e] = 0.f;
+  // M32 operand reads: row (lane & 31) of a 32-row block, logical chunk 2 kk + (lane >> 5) of K16 step kk; the unit
+  // swizzle (row >> 1) & 7 of rows r = 32 b + (lane & 31) is ((lane & 15) >> 1) for every block
+  uint32_t off32[4];
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk) off32[kk] = (lane & 31) * 128 + ((((2 * kk) + (lane >> 5)) ^ ((lane & 15) >> 1)) << 4);
+  bf16x8_t xr32[2][4], w0r32[4], w1r32[4];
 
   // fragment read offsets: row (lane&15) of a 16-row block, logical chunk 4s + (lane>>4)
   const int frow = lane & 15;
@@ -673,6 +693,12 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
   bf16x8_t xr[4][2], w0r[2][2], w1r[2][2];
 
 #define K256_READ_X(XQ, KT)                                                                        \
+  if constexpr (M32) {                                                                             \
+    const uint8_t* b_ = smem + (((KT) & 1) * 4 + ((XQ) ? 3 : 0)) * U_BYTES + (wr * ((XQ) ? X1 : 64)) * 128; \
+    _Pragma("unroll") for (int b = 0; b < ((XQ) ? X1 / 32 : 2); ++b)                               \
+      _Pragma("unroll") for (int kk = 0; kk < 4; ++kk)                                             \
+        xr32[b][kk] = *reinterpret_cast<const bf16x8_t*>(b_ + b * 32 * 128 + off32[kk]);           \
+  } else                                                                                           \
   {                                                                                                \
     const uint8_t* b_ = smem + (((KT) & 1) * 4 + ((XQ) ? 3 : 0)) * U_BYTES + (wr * ((XQ) ? X1 : 64)) * 128; \
     _Pragma("unroll") for (int i = 0; i < ((XQ) ? MF1 : 4); ++i) {                                 \
@@ -681,6 +707,11 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
     }                                                                                              \
   }
 #define K256_READ_W(WR, NQ, KT)                                                                    \
+  if constexpr (M32) {                                                                             \
+    const uint8_t* b_ = smem + (((KT) & 1) * 4 + 1 + (NQ)) * U_BYTES + (wc * 32) * 128;            \
+    _Pragma("unroll") for (int kk = 0; kk < 4; ++kk)                                               \
+      WR##32[kk] = *reinterpret_cast<const bf16x8_t*>(b_ + off32[kk]);                             \
+  } else                                                                                           \
   {                                                                                                \
     const uint8_t* b_ = smem + (((KT) & 1) * 4 + 1 + (NQ)) * U_BYTES + (wc * 32) * 128;            \
     _Pragma("unroll") for (int j = 0; j < 2; ++j) {                                                \
@@ -689,14 +720,21 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
     }                                                                                              \
   }
 #define K256_MFMA(MQ, NQ, WR)                                                                      \
+  if constexpr (M32) {                                                                             \
+    __builtin_amdgcn_s_setprio(1);                                                                 \
+    _Pragma("unroll") for (int b = 0; b < ((MQ) ? X1 / 32 : 2); ++b)                               \
+      _Pragma("unroll") for (int kk = 0; kk < 4; ++kk)                                             \
+        acc32[2 * (MQ) + b][NQ] = mfma_32x32x16<F16>(WR##32[kk], xr32[b][kk], acc32[2 * (MQ) + b][NQ]); \
+    __builtin_amdgcn_s_setprio(0);                                                                 \
+  } else                                                                                           \
   {                                                                                                \
-    if constexpr (PH3 < 2) __builtin_amdgcn_s_setprio(1);                                          \
+    if constexpr (PH3 != 2) __builtin_amdgcn_s_setprio(1);                                         \
     _Pragma("unroll") for (int s = 0; s < 2; ++s)                                                  \
       _Pragma("unroll") for (int i = 0; i < ((MQ) ? MF1 : 4); ++i)                                 \
         _Pragma("unroll") for (int j = 0; j < 2; ++j)                                              \
           acc[4 * (MQ) + i][2 * (NQ) + j] =                                                        \
               mfma_16x16x32<F16>(WR[j][s], xr[i][s], acc[4 * (MQ) + i][2 * (NQ) + j]);             \
-    if constexpr (PH3 < 2) __builtin_amdgcn_s_setprio(0);                                          \
+    if constexpr (PH3 != 2) __builtin_amdgcn_s_setprio(0);                                         \
   }
 #define K256_MFMA_ST(MQ, NQ, WR, STAGE_STMT)                                                       \
   {                                                                                                \
@@ -827,7 +865,7 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
   }
 
   int kt = 0;
-  if constexpr (PH3 > 0) {
+  if constexpr (PH3 == 1 || PH3 == 2) {
     // ---- prologue: tile 0 (phases -4 .. -2) and tile 1's u0, u1 (phase -1); tile 0's u0/u1 must have landed
 #pragma unroll
     for (int g = -4; g <= -1; ++g) stage3(g);
@@ -870,13 +908,30 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
 #pragma unroll
   for (int pass = 0; pass < 2; ++pass) {
     if (wr == pass) {
+      if constexpr (M32) {
+        // 32x32 block (b, nq): lane holds pixel 32 b + (lane & 31), channels 8 g + 4 (lane >> 5) + 0..3 (g = 0..3)
 #pragma unroll
-      for (int i = 0; i < MFR; ++i) {
-        const int r = 16 * i + (lane & 15);
+        for (int b = 0; b < PB; ++b) {
+          const int r = 32 * b + (lane & 31);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int c4 = (wc * 64 + 16 * j) / 4 + (lane >> 4);
-          *reinterpret_cast<f32x4_t*>(tile + r * 256 + 4 * (c4 ^ (r & 7))) = acc[i][j];
+          for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+              const int c4 = wc * 16 + nq * 8 + 2 * g + (lane >> 5);
+              const f32x4_t v = {acc32[b][nq][4 * g], acc32[b][nq][4 * g + 1], acc32[b][nq][4 * g + 2],
+                                 acc32[b][nq][4 * g + 3]};
+              *reinterpret_cast<f32x4_t*>(tile + r * 256 + 4 * (c4 ^ (r & 7))) = v;
+            }
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < MFR; ++i) {
+          const int r = 16 * i + (lane & 15);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int c4 = (wc * 64 + 16 * j) / 4 + (lane >> 4);
+            *reinterpret_cast<f32x4_t*>(tile + r * 256 + 4 * (c4 ^ (r & 7))) = acc[i][j];
+          }
         }
       }
     }
@@ -984,7 +1039,7 @@ int launch256(const ConvParams& p0, hipStream_t s) {
 // ring (48 KB, two-pass LDS epilogue) built for three workgroups per CU; 9 = the 256x256 schedule with
 // 192-pixel tiles (one tile per CU for 250-image 14x14 layers); 10 = config 9 with three 16-MFMA phases per K tile,
 // 11 = 10 with a static priority for the trailing wave group; 12 / 13 = 9 / 6 with the staging DMAs issued inside
-// the MFMA segments.
+// the MFMA segments; 14 / 15 = 9 / 6 on v_mfma_f32_32x32x16 (32x32 output blocks).
 // relu: bit 0 = ReLU; bit 1 = `res` is on the half-resolution grid [N, OH/2, OW/2, ldres] (nearest 2x
 // upsample of the residual, OH and OW even).
 namespace {
@@ -1033,6 +1088,8 @@ int conv2d_impl(const void* x, const void* w, const void* bias, const void* res,
     case 11: return launch256<192, F16, 2>(p, stream);
     case 12: return launch256<192, F16, 0, true>(p, stream);
     case 13: return launch256<256, F16, 0, true>(p, stream);
+    case 14: return launch256<192, F16, 3>(p, stream);
+    case 15: return launch256<256, F16, 3>(p, stream);
     default: return AI4E_EINVAL;
   }
 }
