@@ -153,8 +153,9 @@ class InferenceEngine:
         self._front_done: Optional[torch.cuda.Event] = None
         # CU-partitioned pipeline (AI4E_ENGINE_CU_SPLIT=F, needs output_fn.split): the front graph of every batch
         # replays on a stream masked to F CUs (the same share of every XCD), the back graph on a stream masked to
-        # the other CUs, so batch k+1's HBM-bound front and batch k's MFMA-bound back run side by side on disjoint
-        # CUs instead of taking turns on all of them (runtime/cu_partition.py, profiles/r3_cusplit/)
+        # the other CUs, so batch k+1's front and batch k's back run side by side on disjoint CUs instead of taking
+        # turns on all of them. Off by default: for ResNet-50 both halves scale with their CU count, so every
+        # split measured below two full-chip streams (runtime/cu_partition.py, profiles/r3_cusplit/)
         self.cu_split = int(os.environ.get("AI4E_ENGINE_CU_SPLIT", "0")) if sp is not None else 0
         self.front_stream = self.back_stream = None
         if self.cu_split > 0:
