@@ -545,7 +545,9 @@ template <int GATHER, int BM, bool F16 = false, int PH3 = 0, bool DMAI = false>
 __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) {
   static_assert(GATHER == GATHER_TAP || GATHER == GATHER_POINTWISE, "256 tile needs C % 64 == 0");
   static_assert(BM == 256 || BM == 192, "wave groups of 128 or 96 pixels");
-  static_assert(PH3 == 0 || PH3 == 3 || BM == 192, "the 3-phase schedule is the 192-pixel tile's");
+  static_assert(PH3 == 0 || PH3 >= 3 || BM == 192, "the 3-phase schedule is the 192-pixel tile's");
+  // PH3 == 4 (tile configs 16 / 17 = 9 / 6): priority 1 for the LOAD segment (fragment reads + staging DMA issue)
+  // instead of the MFMA segment, since the stamps show the load segment is the longer one
   // PH3 == 3 (tile configs 14 / 15 = 9 / 6 on v_mfma_f32_32x32x16): the same 4-phase schedule and staging, with
   // 32x32 output blocks (a phase = one 32-channel block x the quadrant's 32-pixel blocks x 4 K16 steps): half the
   // MFMA instructions for the same pipe cycles, so an MFMA wave blocks its SIMD partner's issue 8 of every 32
@@ -728,13 +730,13 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
     __builtin_amdgcn_s_setprio(0);                                                                 \
   } else                                                                                           \
   {                                                                                                \
-    if constexpr (PH3 != 2) __builtin_amdgcn_s_setprio(1);                                         \
+    if constexpr (PH3 != 2 && PH3 != 4) __builtin_amdgcn_s_setprio(1);                             \
     _Pragma("unroll") for (int s = 0; s < 2; ++s)                                                  \
       _Pragma("unroll") for (int i = 0; i < ((MQ) ? MF1 : 4); ++i)                                 \
         _Pragma("unroll") for (int j = 0; j < 2; ++j)                                              \
           acc[4 * (MQ) + i][2 * (NQ) + j] =                                                        \
               mfma_16x16x32<F16>(WR[j][s], xr[i][s], acc[4 * (MQ) + i][2 * (NQ) + j]);             \
-    if constexpr (PH3 != 2) __builtin_amdgcn_s_setprio(0);                                         \
+    if constexpr (PH3 != 2 && PH3 != 4) __builtin_amdgcn_s_setprio(0);                             \
   }
 #define K256_MFMA_ST(MQ, NQ, WR, STAGE_STMT)                                                       \
   {                                                                                                \
@@ -765,6 +767,7 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
     K256_STAMP(0);                                                                                 \
     wait_vmcnt<NS>();                                                                              \
   }                                                                                                \
+  if constexpr (PH3 == 4) __builtin_amdgcn_s_setprio(0);                                           \
   K256_STAMP(1);                                                                                   \
   __builtin_amdgcn_s_barrier();                                                                    \
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                               \
@@ -773,6 +776,7 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
   {                                                                                                \
     const int g = 4 * (KT);                                                                        \
     /* phase 1: quadrant (0,0) */                                                                  \
+    if constexpr (PH3 == 4) __builtin_amdgcn_s_setprio(1);                                         \
     K256_READ_W(w0r, 0, KT)                                                                        \
     K256_READ_X(0, KT)                                                                             \
     K256_SYNC_LOADS(g + 1, CHECKED, 6)                                                                \
@@ -785,6 +789,7 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
     __builtin_amdgcn_s_barrier();                                                                  \
     K256_STAMP(2);                                                                                 \
     /* phase 2: quadrant (0,1) */                                                                  \
+    if constexpr (PH3 == 4) __builtin_amdgcn_s_setprio(1);                                         \
     K256_READ_W(w1r, 1, KT)                                                                        \
     K256_SYNC_LOADS(g + 2, CHECKED, 4 + L3)                                                                \
     if constexpr (DMAI) {                                                                          \
@@ -796,6 +801,7 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
     __builtin_amdgcn_s_barrier();                                                                  \
     K256_STAMP(2);                                                                                 \
     /* phase 3: quadrant (1,1) */                                                                  \
+    if constexpr (PH3 == 4) __builtin_amdgcn_s_setprio(1);                                         \
     K256_READ_X(1, KT)                                                                             \
     K256_SYNC_LOADS(g + 3, CHECKED, 4 + L3)                                                                \
     if constexpr (DMAI) {                                                                          \
@@ -807,6 +813,7 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
     __builtin_amdgcn_s_barrier();                                                                  \
     K256_STAMP(2);                                                                                 \
     /* phase 4: quadrant (1,0), fragments already in registers */                                  \
+    if constexpr (PH3 == 4) __builtin_amdgcn_s_setprio(1);                                         \
     K256_SYNC_LOADS(g + 4, CHECKED, 4 + L3)                                                                \
     if constexpr (DMAI) {                                                                          \
       K256_MFMA_ST(1, 0, w0r, if (CHECKED) stage_phase(g + 4); else stage(phase_tile(g + 4), phase_unit(g + 4))) \
@@ -1039,7 +1046,8 @@ int launch256(const ConvParams& p0, hipStream_t s) {
 // ring (48 KB, two-pass LDS epilogue) built for three workgroups per CU; 9 = the 256x256 schedule with
 // 192-pixel tiles (one tile per CU for 250-image 14x14 layers); 10 = config 9 with three 16-MFMA phases per K tile,
 // 11 = 10 with a static priority for the trailing wave group; 12 / 13 = 9 / 6 with the staging DMAs issued inside
-// the MFMA segments; 14 / 15 = 9 / 6 on v_mfma_f32_32x32x16 (32x32 output blocks).
+// the MFMA segments; 14 / 15 = 9 / 6 on v_mfma_f32_32x32x16 (32x32 output blocks); 16 / 17 = 9 / 6 with priority
+// on the load segment instead of the MFMA segment.
 // relu: bit 0 = ReLU; bit 1 = `res` is on the half-resolution grid [N, OH/2, OW/2, ldres] (nearest 2x
 // upsample of the residual, OH and OW even).
 namespace {
@@ -1090,6 +1098,8 @@ int conv2d_impl(const void* x, const void* w, const void* bias, const void* res,
     case 13: return launch256<256, F16, 0, true>(p, stream);
     case 14: return launch256<192, F16, 3>(p, stream);
     case 15: return launch256<256, F16, 3>(p, stream);
+    case 16: return launch256<192, F16, 4>(p, stream);
+    case 17: return launch256<256, F16, 4>(p, stream);
     default: return AI4E_EINVAL;
   }
 }

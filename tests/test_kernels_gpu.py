@@ -105,7 +105,7 @@ CASES_256 = [
 ]
 
 
-@pytest.mark.parametrize("tile", [6, 9, 10, 11, 12, 13, 14, 15])  # 9: 192-pixel tiles; 10/11: 3-phase; 12/13: DMAs in the MFMA segment; 14/15: 32x32x16
+@pytest.mark.parametrize("tile", [6, 9, 10, 11, 12, 13, 14, 15, 16, 17])  # 9: 192-pixel tiles; 10/11: 3-phase; 12/13: DMAs in the MFMA segment; 14/15: 32x32x16; 16/17: loader priority
 @pytest.mark.parametrize("case", CASES_256)
 @pytest.mark.parametrize("epi", ["plain", "res_relu"])
 def test_conv_tile256(case, epi, tile):
