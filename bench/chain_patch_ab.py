@@ -1,5 +1,5 @@
 """A/B of K1c chain tile configs (CHAIN_CFGS, default: LDS-DMA ring (tile 1 / 0) vs the LDS input patch (tile 3);
-+8 = residual prefetched into registers), ResNet-50 shapes
++16 = 2 x 2 phase-A split, +32 = padded MID-128 patch), ResNet-50 shapes
 at batch 250. Each shape is timed alone and as two launches on two streams at once (the serving worker's two
 compute streams share the chip)."""
 import json

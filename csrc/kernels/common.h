@@ -111,15 +111,6 @@ __device__ __forceinline__ f32x4_t mfma_16x16x32(const bf16x8_t& a, const bf16x8
 }
 
 template <bool F16>
-__device__ __forceinline__ f32x16_t mfma_32x32x16(const bf16x8_t& a, const bf16x8_t& b, const f32x16_t& c) {
-  if constexpr (F16)
-    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8_t, a), __builtin_bit_cast(f16x8_t, b), c, 0,
-                                                  0, 0);
-  else
-    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
-}
-
-template <bool F16>
 __device__ __forceinline__ uint32_t pack2(float lo, float hi) {
   if constexpr (F16) {
     const f32x2_t v = {lo, hi};

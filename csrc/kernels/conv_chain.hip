@@ -186,10 +186,8 @@ __device__ __forceinline__ uint32_t tile_off(int r, int n) {
   return kb * BM * 64 + r * 64 + ((((e >> 3) ^ swz(r)) << 4) | (((e >> 2) & 1) << 3));
 }
 
-// RREG: the residual chunk of pass pp+1 is loaded into registers (the B accumulator layout: 4 channels of one
-// pixel per lane, 8 B) right after pass pp's epilogue, so it has a whole C segment, copy-out and B segment to
-// land, instead of an LDS-DMA into the Y buffer at the start of its own pass that only the B segment covers
-// (and the barrier that publishes it). +16 VGPRs; the loads count in the wave's vmcnt bookkeeping (`ops`).
+// Measured and removed (profiles/r3_rreg/; code in the git history up to commit bc1ff0a): the residual chunk
+// prefetched into registers a pass ahead (tile configs 9 / 11), bit-identical but -2 % end to end.
 // PWN (patch mode): waves along the output channels in phase A (4 = every wave all BM pixels x MID/4 channels;
 // 2 = a 2 x 2 split: half the pixels x half the channels, half the LDS pixel reads per MFMA for twice the weight
 // fragments from L2).
@@ -197,13 +195,12 @@ __device__ __forceinline__ uint32_t tile_off(int r, int n) {
 // same bank-conflict profile as the XOR swizzle (2-way on about half the fragment reads, bench model), and a
 // fragment's address becomes slot * RBS + 16 * lg per tap with the K step as the ds_read immediate, instead of a
 // per-step XOR + shift + add per fragment (the chain kernels issue ~4-8 VALU per MFMA; PMC, profiles/r3_pad/).
-template <int MID, int BM_, int MIDN, bool DOWN, int ST, bool BL, bool PATCH, bool RREG = false, int PWN_ = 4,
+template <int MID, int BM_, int MIDN, bool DOWN, int ST, bool BL, bool PATCH, int PWN_ = 4,
           bool PAD = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ChainCfg<MID, BM_, MIDN, DOWN, ST, BL>::MINW,
                                                                      ChainCfg<MID, BM_, MIDN, DOWN, ST, BL>::MINW)))
 void conv_chain_kernel(const ChainParams p) {
   using Cfg = ChainCfg<MID, BM_, MIDN, DOWN, ST, BL>;
-  static_assert(!(RREG && DOWN), "DOWN mode has no residual tensor");
   static_assert(!PATCH || BM_ == 128, "patch mode: 128-pixel tiles (2 x 2 waves of 64 pixels)");
   constexpr bool NEXT = Cfg::NEXT;
   constexpr int FIC = Cfg::FIC, WPXC = Cfg::WPXC, CBC = Cfg::CBC;
@@ -643,33 +640,6 @@ void conv_chain_kernel(const ChainParams p) {
   uint16_t* ybase[Cfg::NS];
   row_bases(W64{}, p.y, C4, ybase);
 
-  // RREG: residual rows of this wave's B pixels (rows past M re-read row M-1, never stored)
-  uint2 rres[Cfg::BFI][4];
-  const uint16_t* rrow[Cfg::BFI];
-#pragma unroll
-  for (int i = 0; i < Cfg::BFI; ++i)
-    rrow[i] = p.res + static_cast<long>(min(m0 + wave * Cfg::BPW + 16 * i + (lane & 15), p.M - 1)) * C4 + 4 * lg;
-  // The loads are inline asm, outside hipcc's own vmcnt tracking (which would otherwise wait for every LDS-DMA
-  // issued after them before the first use: it cannot count the asm DMAs); the epilogue waits with a counted
-  // vmcnt and then ties the registers (an asm that "rewrites" them), so no use is scheduled before that wait.
-  int r_issued = 0;  // `ops` right after the last residual load
-  auto load_res = [&](int pp) __attribute__((always_inline)) {
-#pragma unroll
-    for (int i = 0; i < Cfg::BFI; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        asm volatile("global_load_dwordx2 %0, %1, off" : "=&v"(rres[i][j]) : "v"(rrow[i] + pp * 64 + 16 * j) : "memory");
-    ops += Cfg::BFI * 4;
-    r_issued = ops;
-  };
-  auto wait_res = [&]() __attribute__((always_inline)) {
-    wait_vmcnt_n(ops - r_issued);
-#pragma unroll
-    for (int i = 0; i < Cfg::BFI; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) asm volatile("" : "+v"(rres[i][j]));
-  };
-  if constexpr (RREG) load_res(0);
 
   auto pass = [&](auto ppc) __attribute__((always_inline)) {
     constexpr int pp = decltype(ppc)::value;
@@ -678,14 +648,14 @@ void conv_chain_kernel(const ChainParams p) {
     // residual chunk R_pp -> ybuf (K-blocked swizzled [BM x 64], 16-B DMA rows; rows past M re-read
     // row M-1, never stored); none in DOWN mode (the projection is part of the B GEMM)
 #pragma unroll
-    for (int s = 0; s < (DOWN || RREG ? 0 : Cfg::NR); ++s) {
+    for (int s = 0; s < (DOWN ? 0 : Cfg::NR); ++s) {
       const int q = wave + 4 * s;
       const int kb = q / (BM / 16), rb = q % (BM / 16);
       const int row = rb * 16 + rin;
       ai4e_conv::glds16_stream(p.res + static_cast<long>(min(m0 + row, p.M - 1)) * C4 + pp * 64 + kb * BK + 8 * c,
              sb + Cfg::T2_BYTES + kb * BM * 64 + rb * 16 * 64);
     }
-    ops += DOWN || RREG ? 0 : Cfg::NR;
+    ops += DOWN ? 0 : Cfg::NR;
     const int r_end = ops;
 
     f32x4_t accb[BFI][4];
@@ -698,11 +668,10 @@ void conv_chain_kernel(const ChainParams p) {
     }
     seg_b(accb, pp * SPW);
 
-    if constexpr (!DOWN && !RREG) {
+    if constexpr (!DOWN) {
       wait_vmcnt_n(ops - r_end);
       lds_barrier();  // residual chunk visible
     }
-    if constexpr (RREG) wait_res();
 #pragma unroll
     for (int i = 0; i < BFI; ++i) {
       const int r = wave * Cfg::BPW + 16 * i + (lane & 15);
@@ -717,14 +686,14 @@ void conv_chain_kernel(const ChainParams p) {
           continue;
         }
         if constexpr (BSEED) {  // residual added straight from its packed bf16 (dot2), ReLU on packed bf16
-          const uint2 rv = RREG ? rres[i][j] : *yp;
+          const uint2 rv = *yp;
           *yp = make_uint2(pack_relu_bf16x2(add_bf16_lo(rv.x, accb[i][j][0]), add_bf16_hi(rv.x, accb[i][j][1])),
                            pack_relu_bf16x2(add_bf16_lo(rv.y, accb[i][j][2]), add_bf16_hi(rv.y, accb[i][j][3])));
           continue;
         }
         float r0 = 0.f, r1 = 0.f, r2 = 0.f, r3 = 0.f;
         if constexpr (!DOWN) {
-          const uint2 rv = RREG ? rres[i][j] : *yp;
+          const uint2 rv = *yp;
           unpack_bf16x2(rv.x, r0, r1);
           unpack_bf16x2(rv.y, r2, r3);
         }
@@ -734,7 +703,6 @@ void conv_chain_kernel(const ChainParams p) {
         }
       }
     }
-    if constexpr (RREG && pp + 1 < Cfg::NP) load_res(pp + 1);  // the registers are free again
     if constexpr (NEXT) {
       seg_c(pp * SPW + NB);  // its first barrier publishes the Y chunk
     } else {
@@ -800,17 +768,17 @@ bool patch_fits(const ChainParams& p, int lds_bytes) {
   return static_cast<long>(rows) * (p.W + 2) * (MID * 2 + (PAD ? 32 : 0)) <= lds_bytes;
 }
 
-template <int MID, int BM, int MIDN, bool DOWN = false, int ST = 4, bool BL = true, bool RREG = false, int PWN = 4,
+template <int MID, int BM, int MIDN, bool DOWN = false, int ST = 4, bool BL = true, int PWN = 4,
           bool PAD = false>
 int launch_chain(const ChainParams& p, hipStream_t s, bool patch = false) {
   using Cfg = ChainCfg<MID, BM, MIDN, DOWN, ST, BL>;
   static bool attr = false;
   if (!attr) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(conv_chain_kernel<MID, BM, MIDN, DOWN, ST, BL, false, RREG>),
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(conv_chain_kernel<MID, BM, MIDN, DOWN, ST, BL, false>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, Cfg::LDS_ALL) != hipSuccess)
       return AI4E_ELAUNCH;
     if constexpr (BM == 128) {
-      if (hipFuncSetAttribute(reinterpret_cast<const void*>(conv_chain_kernel<MID, BM, MIDN, DOWN, ST, BL, true, RREG, PWN, PAD>),
+      if (hipFuncSetAttribute(reinterpret_cast<const void*>(conv_chain_kernel<MID, BM, MIDN, DOWN, ST, BL, true, PWN, PAD>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, Cfg::LDS_ALL) != hipSuccess)
         return AI4E_ELAUNCH;
     }
@@ -819,12 +787,12 @@ int launch_chain(const ChainParams& p, hipStream_t s, bool patch = false) {
   const int nb = ai4e_cdiv(p.M, Cfg::BM);
   if constexpr (BM == 128) {
     if (patch && patch_fits<MID, BM, PAD>(p, Cfg::LDS)) {
-      hipLaunchKernelGGL((conv_chain_kernel<MID, BM, MIDN, DOWN, ST, BL, true, RREG, PWN, PAD>), dim3(nb), dim3(256), Cfg::LDS_ALL,
+      hipLaunchKernelGGL((conv_chain_kernel<MID, BM, MIDN, DOWN, ST, BL, true, PWN, PAD>), dim3(nb), dim3(256), Cfg::LDS_ALL,
                          s, p);
       return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
     }
   }
-  hipLaunchKernelGGL((conv_chain_kernel<MID, BM, MIDN, DOWN, ST, BL, false, RREG>), dim3(nb), dim3(256), Cfg::LDS_ALL, s,
+  hipLaunchKernelGGL((conv_chain_kernel<MID, BM, MIDN, DOWN, ST, BL, false>), dim3(nb), dim3(256), Cfg::LDS_ALL, s,
                      p);
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
 }
@@ -884,32 +852,21 @@ AI4E_API int ai4e_conv_chain_fwd(const void* x, const void* w2, const void* b2, 
   // tile_cfg: 0 = default (MID 64: 256 pixels, MID 128: 128), 1 = 128-pixel MID-64 tile (48 KB LDS, 3 per CU),
   // 2 = the 128-pixel tiles with the SGPR lane-select biases (A/B reference for the LDS / ring-borne biases),
   // 3 = the 128-pixel tiles with phase A in patch mode where the shape allows it (else the ring, as 1);
-  // + 8 (9, 11): the same 128-pixel tiles with the residual prefetched into registers a pass ahead (RREG)
-  const bool rreg = (tile_cfg & 8) != 0 && !down && (tile_cfg & 7) != 0 && (tile_cfg & 7) != 2;
   const bool pw2 = (tile_cfg & 16) != 0 && (tile_cfg & 7) == 3 && mid == 64;  // + 16 (19): 2 x 2 phase-A split
   const bool pad = (tile_cfg & 32) != 0 && (tile_cfg & 7) == 3 && mid == 128 && !down;  // + 32 (35): padded patch
   tile_cfg &= 7;
   const bool patch = tile_cfg == 3;
   if (pad)
-    return next ? launch_chain<128, 128, 128, false, 4, true, false, 4, true>(p, stream, true)
-                : launch_chain<128, 128, 0, false, 4, true, false, 4, true>(p, stream, true);
+    return next ? launch_chain<128, 128, 128, false, 4, true, 4, true>(p, stream, true)
+                : launch_chain<128, 128, 0, false, 4, true, 4, true>(p, stream, true);
   if (pw2) {
-    if (down) return launch_chain<64, 128, 64, true, 4, true, false, 2>(p, stream, true);
-    if (next && midn == 128) return launch_chain<64, 128, 128, false, 4, true, false, 2>(p, stream, true);
-    return next ? launch_chain<64, 128, 64, false, 4, true, false, 2>(p, stream, true)
-                : launch_chain<64, 128, 0, false, 4, true, false, 2>(p, stream, true);
+    if (down) return launch_chain<64, 128, 64, true, 4, true, 2>(p, stream, true);
+    if (next && midn == 128) return launch_chain<64, 128, 128, false, 4, true, 2>(p, stream, true);
+    return next ? launch_chain<64, 128, 64, false, 4, true, 2>(p, stream, true)
+                : launch_chain<64, 128, 0, false, 4, true, 2>(p, stream, true);
   }
   if (down) return tile_cfg == 2 ? launch_chain<64, 128, 64, true, 4, false>(p, stream)
                                  : launch_chain<64, 128, 64, true>(p, stream, patch);
-  if (rreg) {
-    if (mid == 64) {
-      if (next && midn == 128) return launch_chain<64, 128, 128, false, 4, true, true>(p, stream, patch);
-      return next ? launch_chain<64, 128, 64, false, 4, true, true>(p, stream, patch)
-                  : launch_chain<64, 128, 0, false, 4, true, true>(p, stream, patch);
-    }
-    return next ? launch_chain<128, 128, 128, false, 4, true, true>(p, stream, patch)
-                : launch_chain<128, 128, 0, false, 4, true, true>(p, stream, patch);
-  }
   if (mid == 64) {
     if (tile_cfg == 2) {  // A/B reference: the 128-pixel tile with the SGPR-select biases (no LDS staging)
       if (next && midn == 128) return launch_chain<64, 128, 128, false, 4, false>(p, stream);

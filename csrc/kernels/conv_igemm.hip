@@ -532,28 +532,14 @@ constexpr int U_ROWS = 128, U_BYTES = U_ROWS * 128;
 // p = 0 stages u2 of tile t+1, p = 1 u3 of tile t+1, p = 2 u0 and u1 of tile t+2. Last reads within tile t:
 // u0/u1 at p = 0, u2 at p = 1, u3 at p = 2, so every slot is again overwritten >= 2 phases after its last read
 // and read >= 4 phases after it was staged, and the per-phase wait is the same rule (own DMAs of phases <= g-3).
-// PH3 == 2 (tile config 11): the 3-phase schedule with a static s_setprio 1 for the trailing wave group (waves
-// 4-7, the arbitration loser on every shared SIMD) instead of the per-segment priority flips around the MFMAs
-// (MI355X_MICROARCH.md "Two waves per SIMD", item 4).
-// DMAI (4-phase schedule, tile configs 12 / 13 = 9 / 6): a phase's staging DMAs are issued inside the wave's own
-// MFMA segment (between its two halves) instead of before the phase's first barrier, so the load segment the
-// partner's MFMAs must cover holds only the fragment reads and the wait (the stamps of config 9: reads + DMA issue
-// 31 % of a wave's life against 24 % MFMA, profiles/r3_k256/). Staging then lands one barrier later, which every
-// rule above tolerates: the slot's last read is further back, and the wait at phase g counts only the DMAs of
-// phases g-2 and g-1 (phase g's are not issued yet).
-template <int GATHER, int BM, bool F16 = false, int PH3 = 0, bool DMAI = false>
+// Measured and removed (profiles/r3_ph3/, profiles/r3_k256/; the code is in the git history up to commit bc1ff0a):
+// a static priority for the trailing wave group (config 11), the staging DMAs inside the MFMA segment (12 / 13),
+// 32x32x16 MFMAs (14 / 15) and priority on the load segment instead of the MFMAs (16 / 17) — all slower.
+template <int GATHER, int BM, bool F16 = false, bool PH3 = false>
 __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) {
   static_assert(GATHER == GATHER_TAP || GATHER == GATHER_POINTWISE, "256 tile needs C % 64 == 0");
   static_assert(BM == 256 || BM == 192, "wave groups of 128 or 96 pixels");
-  static_assert(PH3 == 0 || PH3 >= 3 || BM == 192, "the 3-phase schedule is the 192-pixel tile's");
-  // PH3 == 4 (tile configs 16 / 17 = 9 / 6): priority 1 for the LOAD segment (fragment reads + staging DMA issue)
-  // instead of the MFMA segment, since the stamps show the load segment is the longer one
-  // PH3 == 3 (tile configs 14 / 15 = 9 / 6 on v_mfma_f32_32x32x16): the same 4-phase schedule and staging, with
-  // 32x32 output blocks (a phase = one 32-channel block x the quadrant's 32-pixel blocks x 4 K16 steps): half the
-  // MFMA instructions for the same pipe cycles, so an MFMA wave blocks its SIMD partner's issue 8 of every 32
-  // cycles instead of 8 of 16 (the stamps: the partner's load segment outlasts the MFMA segment)
-  constexpr bool M32 = PH3 == 3;
-  static_assert(!(M32 && DMAI), "one variant at a time");
+  static_assert(!PH3 || BM == 192, "the 3-phase schedule is the 192-pixel tile's");
   constexpr int WROWS = BM / 2;    // pixels per wave group
   constexpr int X1 = WROWS - 64;   // u3 rows per wave group
   constexpr int L3 = X1 / 32;      // DMAs per lane for u3
@@ -667,25 +653,11 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
   // wait until this wave's DMAs of phases <= g-3 have landed
   auto wait_phase = [&](int g) { wait_vmcnt_n(loads_of(g - 2) + loads_of(g - 1) + loads_of(g)); };
 
-  f32x4_t acc[M32 ? 1 : MFR][4];
+  f32x4_t acc[MFR][4];
 #pragma unroll
-  for (int i = 0; i < (M32 ? 1 : MFR); ++i)
+  for (int i = 0; i < MFR; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  constexpr int PB = WROWS / 32;  // M32: 32-pixel blocks per wave (2 in XQ0, X1 / 32 in XQ1)
-  f32x16_t acc32[M32 ? PB : 1][2];
-#pragma unroll
-  for (int i = 0; i < (M32 ? PB : 1); ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc32[i][j][e] = 0.f;
-  // M32 operand reads: row (lane & 31) of a 32-row block, logical chunk 2 kk + (lane >> 5) of K16 step kk; the unit
-  // swizzle (row >> 1) & 7 of rows r = 32 b + (lane & 31) is ((lane & 15) >> 1) for every block
-  uint32_t off32[4];
-#pragma unroll
-  for (int kk = 0; kk < 4; ++kk) off32[kk] = (lane & 31) * 128 + ((((2 * kk) + (lane >> 5)) ^ ((lane & 15) >> 1)) << 4);
-  bf16x8_t xr32[2][4], w0r32[4], w1r32[4];
 
   // fragment read offsets: row (lane&15) of a 16-row block, logical chunk 4s + (lane>>4)
   const int frow = lane & 15;
@@ -695,12 +667,6 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
   bf16x8_t xr[4][2], w0r[2][2], w1r[2][2];
 
 #define K256_READ_X(XQ, KT)                                                                        \
-  if constexpr (M32) {                                                                             \
-    const uint8_t* b_ = smem + (((KT) & 1) * 4 + ((XQ) ? 3 : 0)) * U_BYTES + (wr * ((XQ) ? X1 : 64)) * 128; \
-    _Pragma("unroll") for (int b = 0; b < ((XQ) ? X1 / 32 : 2); ++b)                               \
-      _Pragma("unroll") for (int kk = 0; kk < 4; ++kk)                                             \
-        xr32[b][kk] = *reinterpret_cast<const bf16x8_t*>(b_ + b * 32 * 128 + off32[kk]);           \
-  } else                                                                                           \
   {                                                                                                \
     const uint8_t* b_ = smem + (((KT) & 1) * 4 + ((XQ) ? 3 : 0)) * U_BYTES + (wr * ((XQ) ? X1 : 64)) * 128; \
     _Pragma("unroll") for (int i = 0; i < ((XQ) ? MF1 : 4); ++i) {                                 \
@@ -709,11 +675,6 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
     }                                                                                              \
   }
 #define K256_READ_W(WR, NQ, KT)                                                                    \
-  if constexpr (M32) {                                                                             \
-    const uint8_t* b_ = smem + (((KT) & 1) * 4 + 1 + (NQ)) * U_BYTES + (wc * 32) * 128;            \
-    _Pragma("unroll") for (int kk = 0; kk < 4; ++kk)                                               \
-      WR##32[kk] = *reinterpret_cast<const bf16x8_t*>(b_ + off32[kk]);                             \
-  } else                                                                                           \
   {                                                                                                \
     const uint8_t* b_ = smem + (((KT) & 1) * 4 + 1 + (NQ)) * U_BYTES + (wc * 32) * 128;            \
     _Pragma("unroll") for (int j = 0; j < 2; ++j) {                                                \
@@ -722,43 +683,19 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
     }                                                                                              \
   }
 #define K256_MFMA(MQ, NQ, WR)                                                                      \
-  if constexpr (M32) {                                                                             \
-    __builtin_amdgcn_s_setprio(1);                                                                 \
-    _Pragma("unroll") for (int b = 0; b < ((MQ) ? X1 / 32 : 2); ++b)                               \
-      _Pragma("unroll") for (int kk = 0; kk < 4; ++kk)                                             \
-        acc32[2 * (MQ) + b][NQ] = mfma_32x32x16<F16>(WR##32[kk], xr32[b][kk], acc32[2 * (MQ) + b][NQ]); \
-    __builtin_amdgcn_s_setprio(0);                                                                 \
-  } else                                                                                           \
   {                                                                                                \
-    if constexpr (PH3 != 2 && PH3 != 4) __builtin_amdgcn_s_setprio(1);                             \
+    __builtin_amdgcn_s_setprio(1);                                                                 \
     _Pragma("unroll") for (int s = 0; s < 2; ++s)                                                  \
       _Pragma("unroll") for (int i = 0; i < ((MQ) ? MF1 : 4); ++i)                                 \
         _Pragma("unroll") for (int j = 0; j < 2; ++j)                                              \
           acc[4 * (MQ) + i][2 * (NQ) + j] =                                                        \
               mfma_16x16x32<F16>(WR[j][s], xr[i][s], acc[4 * (MQ) + i][2 * (NQ) + j]);             \
-    if constexpr (PH3 != 2 && PH3 != 4) __builtin_amdgcn_s_setprio(0);                             \
-  }
-#define K256_MFMA_ST(MQ, NQ, WR, STAGE_STMT)                                                       \
-  {                                                                                                \
-    if constexpr (PH3 < 2) __builtin_amdgcn_s_setprio(1);                                          \
-    _Pragma("unroll") for (int i = 0; i < ((MQ) ? MF1 : 4); ++i)                                   \
-      _Pragma("unroll") for (int j = 0; j < 2; ++j)                                                \
-        acc[4 * (MQ) + i][2 * (NQ) + j] =                                                          \
-            mfma_16x16x32<F16>(WR[j][0], xr[i][0], acc[4 * (MQ) + i][2 * (NQ) + j]);               \
-    STAGE_STMT;                                                                                    \
-    _Pragma("unroll") for (int i = 0; i < ((MQ) ? MF1 : 4); ++i)                                   \
-      _Pragma("unroll") for (int j = 0; j < 2; ++j)                                                \
-        acc[4 * (MQ) + i][2 * (NQ) + j] =                                                          \
-            mfma_16x16x32<F16>(WR[j][1], xr[i][1], acc[4 * (MQ) + i][2 * (NQ) + j]);               \
-    if constexpr (PH3 < 2) __builtin_amdgcn_s_setprio(0);                                          \
+    __builtin_amdgcn_s_setprio(0);                                                                 \
   }
 // CHECKED = 0: steady state (kt + 2 < nk): every phase stages a unit, 3 phases of DMAs in flight
 // (NS = this wave's DMAs of those 3 phases: 6 at phase 1, 4 + L3 at phases 2-4, which stage u3 or follow it)
 #define K256_SYNC_LOADS(G, CHECKED, NS)                                                            \
-  if constexpr (DMAI) {                                                                            \
-    K256_STAMP(0);                                                                                 \
-    wait_vmcnt_n(loads_of((G) - 2) + loads_of((G) - 1));                                           \
-  } else if (CHECKED) {                                                                            \
+  if (CHECKED) {                                                                                   \
     stage_phase(G);                                                                                \
     K256_STAMP(0);                                                                                 \
     wait_phase(G);                                                                                 \
@@ -767,7 +704,6 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
     K256_STAMP(0);                                                                                 \
     wait_vmcnt<NS>();                                                                              \
   }                                                                                                \
-  if constexpr (PH3 == 4) __builtin_amdgcn_s_setprio(0);                                           \
   K256_STAMP(1);                                                                                   \
   __builtin_amdgcn_s_barrier();                                                                    \
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                               \
@@ -776,50 +712,30 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
   {                                                                                                \
     const int g = 4 * (KT);                                                                        \
     /* phase 1: quadrant (0,0) */                                                                  \
-    if constexpr (PH3 == 4) __builtin_amdgcn_s_setprio(1);                                         \
     K256_READ_W(w0r, 0, KT)                                                                        \
     K256_READ_X(0, KT)                                                                             \
     K256_SYNC_LOADS(g + 1, CHECKED, 6)                                                                \
-    if constexpr (DMAI) {                                                                          \
-      K256_MFMA_ST(0, 0, w0r, if (CHECKED) stage_phase(g + 1); else stage(phase_tile(g + 1), phase_unit(g + 1))) \
-    } else {                                                                                       \
-      K256_MFMA(0, 0, w0r)                                                                         \
-    }                                                                                              \
+    K256_MFMA(0, 0, w0r)                                                                           \
     K256_STAMP(3);                                                                                 \
     __builtin_amdgcn_s_barrier();                                                                  \
     K256_STAMP(2);                                                                                 \
     /* phase 2: quadrant (0,1) */                                                                  \
-    if constexpr (PH3 == 4) __builtin_amdgcn_s_setprio(1);                                         \
     K256_READ_W(w1r, 1, KT)                                                                        \
     K256_SYNC_LOADS(g + 2, CHECKED, 4 + L3)                                                                \
-    if constexpr (DMAI) {                                                                          \
-      K256_MFMA_ST(0, 1, w1r, if (CHECKED) stage_phase(g + 2); else stage(phase_tile(g + 2), phase_unit(g + 2))) \
-    } else {                                                                                       \
-      K256_MFMA(0, 1, w1r)                                                                         \
-    }                                                                                              \
+    K256_MFMA(0, 1, w1r)                                                                           \
     K256_STAMP(3);                                                                                 \
     __builtin_amdgcn_s_barrier();                                                                  \
     K256_STAMP(2);                                                                                 \
     /* phase 3: quadrant (1,1) */                                                                  \
-    if constexpr (PH3 == 4) __builtin_amdgcn_s_setprio(1);                                         \
     K256_READ_X(1, KT)                                                                             \
     K256_SYNC_LOADS(g + 3, CHECKED, 4 + L3)                                                                \
-    if constexpr (DMAI) {                                                                          \
-      K256_MFMA_ST(1, 1, w1r, if (CHECKED) stage_phase(g + 3); else stage(phase_tile(g + 3), phase_unit(g + 3))) \
-    } else {                                                                                       \
-      K256_MFMA(1, 1, w1r)                                                                         \
-    }                                                                                              \
+    K256_MFMA(1, 1, w1r)                                                                           \
     K256_STAMP(3);                                                                                 \
     __builtin_amdgcn_s_barrier();                                                                  \
     K256_STAMP(2);                                                                                 \
     /* phase 4: quadrant (1,0), fragments already in registers */                                  \
-    if constexpr (PH3 == 4) __builtin_amdgcn_s_setprio(1);                                         \
     K256_SYNC_LOADS(g + 4, CHECKED, 4 + L3)                                                                \
-    if constexpr (DMAI) {                                                                          \
-      K256_MFMA_ST(1, 0, w0r, if (CHECKED) stage_phase(g + 4); else stage(phase_tile(g + 4), phase_unit(g + 4))) \
-    } else {                                                                                       \
-      K256_MFMA(1, 0, w0r)                                                                         \
-    }                                                                                              \
+    K256_MFMA(1, 0, w0r)                                                                           \
     K256_STAMP(3);                                                                                 \
     __builtin_amdgcn_s_barrier();                                                                  \
     K256_STAMP(2);                                                                                 \
@@ -872,19 +788,15 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
   }
 
   int kt = 0;
-  if constexpr (PH3 == 1 || PH3 == 2) {
+  if constexpr (PH3) {
     // ---- prologue: tile 0 (phases -4 .. -2) and tile 1's u0, u1 (phase -1); tile 0's u0/u1 must have landed
 #pragma unroll
     for (int g = -4; g <= -1; ++g) stage3(g);
     wait_vmcnt_n(loads3(-3) + loads3(-2) + loads3(-1));
     __builtin_amdgcn_s_barrier();
     if (wr == 1) __builtin_amdgcn_s_barrier();  // the stagger: group 1 trails by one barrier
-    if constexpr (PH3 == 2) {
-      if (wr == 1) __builtin_amdgcn_s_setprio(1);
-    }
     for (; kt + 2 < nk; ++kt) K256_TILE3(kt, 0)
     for (; kt < nk; ++kt) K256_TILE3(kt, 1)
-    if constexpr (PH3 == 2) __builtin_amdgcn_s_setprio(0);
   } else {
     // ---- prologue: tile 0 (virtual phases -5..-2) and tile 1's u0, u1 (phases -1, 0)
 #pragma unroll
@@ -902,7 +814,6 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
 #undef K256_TILE
 #undef K256_SYNC_LOADS
 #undef K256_MFMA
-#undef K256_MFMA_ST
 #undef K256_READ_W
 #undef K256_READ_X
   if (wr == 0) __builtin_amdgcn_s_barrier();  // re-align the two groups
@@ -915,30 +826,13 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
 #pragma unroll
   for (int pass = 0; pass < 2; ++pass) {
     if (wr == pass) {
-      if constexpr (M32) {
-        // 32x32 block (b, nq): lane holds pixel 32 b + (lane & 31), channels 8 g + 4 (lane >> 5) + 0..3 (g = 0..3)
 #pragma unroll
-        for (int b = 0; b < PB; ++b) {
-          const int r = 32 * b + (lane & 31);
+      for (int i = 0; i < MFR; ++i) {
+        const int r = 16 * i + (lane & 15);
 #pragma unroll
-          for (int nq = 0; nq < 2; ++nq)
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-              const int c4 = wc * 16 + nq * 8 + 2 * g + (lane >> 5);
-              const f32x4_t v = {acc32[b][nq][4 * g], acc32[b][nq][4 * g + 1], acc32[b][nq][4 * g + 2],
-                                 acc32[b][nq][4 * g + 3]};
-              *reinterpret_cast<f32x4_t*>(tile + r * 256 + 4 * (c4 ^ (r & 7))) = v;
-            }
-        }
-      } else {
-#pragma unroll
-        for (int i = 0; i < MFR; ++i) {
-          const int r = 16 * i + (lane & 15);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int c4 = (wc * 64 + 16 * j) / 4 + (lane >> 4);
-            *reinterpret_cast<f32x4_t*>(tile + r * 256 + 4 * (c4 ^ (r & 7))) = acc[i][j];
-          }
+        for (int j = 0; j < 4; ++j) {
+          const int c4 = (wc * 64 + 16 * j) / 4 + (lane >> 4);
+          *reinterpret_cast<f32x4_t*>(tile + r * 256 + 4 * (c4 ^ (r & 7))) = acc[i][j];
         }
       }
     }
@@ -1019,7 +913,7 @@ int launch(const ConvParams& p0, hipStream_t s) {
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
 }
 
-template <int BM, bool F16 = false, int PH3 = 0, bool DMAI = false>
+template <int BM, bool F16 = false, bool PH3 = false>
 int launch256(const ConvParams& p0, hipStream_t s) {
   ConvParams p = p0;
   // 256 tile: C % 64 (one tap per 64-wide K tile), 16-B output/residual rows, Kout % 8
@@ -1031,9 +925,9 @@ int launch256(const ConvParams& p0, hipStream_t s) {
   p.zero = zero_chunk_ptr();
   if (!p.zero) return AI4E_ELAUNCH;
   if (p.KH == 1 && p.KW == 1 && p.pad == 0)
-    hipLaunchKernelGGL((conv_igemm256_kernel<GATHER_POINTWISE, BM, F16, PH3, DMAI>), dim3(nb), dim3(512), 0, s, p);
+    hipLaunchKernelGGL((conv_igemm256_kernel<GATHER_POINTWISE, BM, F16, PH3>), dim3(nb), dim3(512), 0, s, p);
   else
-    hipLaunchKernelGGL((conv_igemm256_kernel<GATHER_TAP, BM, F16, PH3, DMAI>), dim3(nb), dim3(512), 0, s, p);
+    hipLaunchKernelGGL((conv_igemm256_kernel<GATHER_TAP, BM, F16, PH3>), dim3(nb), dim3(512), 0, s, p);
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
 }
 
@@ -1044,10 +938,7 @@ int launch256(const ConvParams& p0, hipStream_t s) {
 // workgroups per CU), 5 = 256x64 with 5 stages (100 KB: one workgroup per CU), 6 = 256x256, 8 waves,
 // ping-pong phases (needs C % 64 == 0, Kout % 8 == 0); 7/8 = the 128x128 / 256x64 tiles with a 3-stage
 // ring (48 KB, two-pass LDS epilogue) built for three workgroups per CU; 9 = the 256x256 schedule with
-// 192-pixel tiles (one tile per CU for 250-image 14x14 layers); 10 = config 9 with three 16-MFMA phases per K tile,
-// 11 = 10 with a static priority for the trailing wave group; 12 / 13 = 9 / 6 with the staging DMAs issued inside
-// the MFMA segments; 14 / 15 = 9 / 6 on v_mfma_f32_32x32x16 (32x32 output blocks); 16 / 17 = 9 / 6 with priority
-// on the load segment instead of the MFMA segment.
+// 192-pixel tiles (one tile per CU for 250-image 14x14 layers); 10 = config 9 with three 16-MFMA phases per K tile.
 // relu: bit 0 = ReLU; bit 1 = `res` is on the half-resolution grid [N, OH/2, OW/2, ldres] (nearest 2x
 // upsample of the residual, OH and OW even).
 namespace {
@@ -1076,7 +967,7 @@ int conv2d_impl(const void* x, const void* w, const void* bias, const void* res,
     // channel tile, tiles that never straddle images, full 16-B output rows
     const bool tall = tile_cfg == 2 || tile_cfg == 5 || tile_cfg == 8;
     const int bm = tall ? 256 : 128, bn = tall ? 64 : 128;
-    if (tile_cfg == 3 || tile_cfg == 6 || tile_cfg == 9 || tile_cfg >= 10 || gn_groups <= 0 || Kout % gn_groups || (OH * OW) % bm || Kout % 8 ||
+    if (tile_cfg == 3 || tile_cfg == 6 || tile_cfg == 9 || tile_cfg == 10 || gn_groups <= 0 || Kout % gn_groups || (OH * OW) % bm || Kout % 8 ||
         ldy % 8 || ycoff % 8 || (res && ldres % 8) || bn % (Kout / gn_groups))
       return AI4E_EINVAL;
     p.gnp = gnp;
@@ -1092,14 +983,7 @@ int conv2d_impl(const void* x, const void* w, const void* bias, const void* res,
     case 7: return launch<2, 2, 3, 3, F16>(p, stream);
     case 8: return launch<4, 1, 3, 3, F16>(p, stream);
     case 9: return launch256<192, F16>(p, stream);
-    case 10: return launch256<192, F16, 1>(p, stream);
-    case 11: return launch256<192, F16, 2>(p, stream);
-    case 12: return launch256<192, F16, 0, true>(p, stream);
-    case 13: return launch256<256, F16, 0, true>(p, stream);
-    case 14: return launch256<192, F16, 3>(p, stream);
-    case 15: return launch256<256, F16, 3>(p, stream);
-    case 16: return launch256<192, F16, 4>(p, stream);
-    case 17: return launch256<256, F16, 4>(p, stream);
+    case 10: return launch256<192, F16, true>(p, stream);
     default: return AI4E_EINVAL;
   }
 }

@@ -47,13 +47,13 @@ CASES = [
 
 
 @pytest.mark.parametrize("case", CASES)
-@pytest.mark.parametrize("tile", [0, 1, 3, 9, 11, 19, 35])
+@pytest.mark.parametrize("tile", [0, 1, 3, 19, 35])
 def test_conv_chain(case, tile):
     """tile 3 = phase A from the LDS input patch (stride 1 and a patch that fits; other shapes fall back to the
     ring, which the same comparison then covers)."""
     n, h, w, mid, s, nxt = case
     midn = 0 if not nxt else (mid if nxt is True else nxt)
-    if tile in (1, 9) and (mid != 64 or midn == 128):
+    if tile == 1 and (mid != 64 or midn == 128):
         pytest.skip("tile config 1 is the MID-64, same-width variant")
     if tile == 19 and mid != 64:
         pytest.skip("tile config 19 (2 x 2 phase-A split) is the MID-64 variant")

@@ -62,7 +62,7 @@ def test_conv_igemm(case, epi):
     assert err <= 0.02 * ref.abs().max().item() + 0.02, err
 
 
-@pytest.mark.parametrize("tile", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15])
+@pytest.mark.parametrize("tile", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10])
 def test_conv_tile_configs(tile):
     torch.manual_seed(1)
     wt = torch.randn(256, 64, 3, 3) / 24
@@ -105,7 +105,7 @@ CASES_256 = [
 ]
 
 
-@pytest.mark.parametrize("tile", [6, 9, 10, 11, 12, 13, 14, 15, 16, 17])  # 9: 192-pixel tiles; 10/11: 3-phase; 12/13: DMAs in the MFMA segment; 14/15: 32x32x16; 16/17: loader priority
+@pytest.mark.parametrize("tile", [6, 9, 10])  # 9: the same schedule with 192-pixel tiles; 10: its 3-phase form
 @pytest.mark.parametrize("case", CASES_256)
 @pytest.mark.parametrize("epi", ["plain", "res_relu"])
 def test_conv_tile256(case, epi, tile):
