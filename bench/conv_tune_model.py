@@ -64,7 +64,7 @@ def time_cfg(pc, n, h, w, res, cfg, dev):
 PAIR = os.environ.get("TUNE_PAIR", "0") == "1"
 
 
-def time_pair(x, pc, r, cfg, reps=6):
+def time_pair(x, pc, r, cfg, reps=int(os.environ.get("TUNE_REPS", "6"))):
     cur = torch.cuda.current_stream()
     streams = [torch.cuda.Stream(), torch.cuda.Stream()]
     xs = [x, x.clone()]
@@ -109,20 +109,21 @@ def main():
         raise SystemExit(f"unknown model {which}")
     table = {}
     for key, (pc, n, h, w, res) in shapes.items():
-        times = {c: t for c in (1, 2, 3, 4, 5, 6, 7, 8, 9) if (t := time_cfg(pc, n, h, w, res, c, dev)) is not None}
+        times = {c: t for c in (1, 2, 3, 4, 5, 6, 7, 8, 9, 10) if (t := time_cfg(pc, n, h, w, res, c, dev)) is not None}
         best = min(times, key=times.get)
         table[key] = best
         print(json.dumps({"key": key, "us": {k: round(v, 1) for k, v in times.items()}, "best": best}), flush=True)
-    if "--write" in sys.argv:
+    out_path = os.environ.get("TUNE_OUT")  # write the merged table here instead of the repo table (A/B runs)
+    if "--write" in sys.argv or out_path:
         try:
             with open(TILES) as f:
                 merged = json.load(f)
         except (OSError, ValueError):
             merged = {}
         merged.update(table)
-        with open(TILES, "w") as f:
+        with open(out_path or TILES, "w") as f:
             json.dump(merged, f, indent=1, sort_keys=True)
-        print("merged", len(table), "entries into", TILES, flush=True)
+        print("merged", len(table), "entries into", out_path or TILES, flush=True)
 
 
 if __name__ == "__main__":
