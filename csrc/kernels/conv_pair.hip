@@ -66,6 +66,31 @@ __device__ __forceinline__ f32x4_t pbias4(const float* blk, int g) {
 
 __device__ __forceinline__ void pbarrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+// Diagnostic build (AI4E_PAIR_STAMPS=1): s_memtime stamps per wave, summed per segment: 0 = prologue (T2 tile,
+// first operands, barrier), 1 = C-weight load issue + B phase (incl. the wait for its weights), 2 = residual wait +
+// Y epilogue + barrier, 3 = next-pass load issue + Y copy-out, 4 = C phase (incl. the wait for its weights),
+// 5 = T1' epilogue + stores (drained). Shares only: a stamp drains the wave's LDS reads.
+#ifndef AI4E_PAIR_STAMPS
+#define AI4E_PAIR_STAMPS 0
+#endif
+constexpr int PAIR_NSEG = 6, PAIR_MAXW = 32768;
+#if AI4E_PAIR_STAMPS
+__device__ unsigned long long g_pair_stamps[PAIR_MAXW * PAIR_NSEG];
+#define PAIR_STAMP(k)                                                              \
+  do {                                                                             \
+    __builtin_amdgcn_sched_barrier(0);                                             \
+    unsigned long long _t;                                                         \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");     \
+    __builtin_amdgcn_sched_barrier(0);                                             \
+    ps_sum[k] += _t - ps_last;                                                     \
+    ps_last = _t;                                                                  \
+  } while (0)
+#else
+#define PAIR_STAMP(k) \
+  do {                \
+  } while (0)
+#endif
+
 struct PairParams {
   const uint16_t* t2;   // [M, MID]
   const uint16_t* w3p;  // packed [C4/16][MID/32][64][8]
@@ -78,7 +103,11 @@ struct PairParams {
   int M;
 };
 
-template <int MID, int C4, int MIDN, int BM, bool KF = true>
+// SP (bm_cfg 98, the default for the layer3 pair): the residual loads of the next pass and this pass's Y copy-out are spread over the C-phase steps
+// (one store chunk and FI / NKC residual loads after each step's MFMAs) instead of a burst between the Y barrier and
+// the C phase: the stamps (profiles/r3_pair/) put 33 % of a wave's life in that burst (vector-memory issue backs up).
+// (Spreading the next pass's B weight fragments over the C steps as well was measured slower: profiles/r3_pair/.)
+template <int MID, int C4, int MIDN, int BM, bool KF = true, bool SP = false>
 __global__ __launch_bounds__(512) void conv_pair_kernel(const PairParams p) {
   constexpr int FI = BM / 16;            // pixel fragments
   constexpr int NKB = MID / 32;          // B K steps
@@ -93,6 +122,10 @@ __global__ __launch_bounds__(512) void conv_pair_kernel(const PairParams p) {
   static_assert(T2_BYTES + 2 * Y_BYTES >= MIDN / 32 * KBS, "T1' staging fits the T2 + Y regions");
   extern __shared__ __attribute__((aligned(1024))) uint8_t smem[];
   uint8_t* const t2s = smem;
+#if AI4E_PAIR_STAMPS
+  unsigned long long ps_sum[PAIR_NSEG] = {0, 0, 0, 0, 0, 0}, ps_last;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(ps_last)::"memory");
+#endif
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -155,6 +188,7 @@ __global__ __launch_bounds__(512) void conv_pair_kernel(const PairParams p) {
   for (int i = 0; i < FI; ++i) rr[i] = *reinterpret_cast<const uint2*>(resl[i]);
 
   pbarrier();  // T2 tile visible
+  PAIR_STAMP(0);
 
   constexpr int NS = BM * PR_CH / 8 / 512;  // Y copy-out: thread g -> (row g / 16, 16-B chunk g % 16)
 
@@ -189,6 +223,7 @@ __global__ __launch_bounds__(512) void conv_pair_kernel(const PairParams p) {
       if constexpr (KF) __builtin_amdgcn_sched_barrier(0);
     }
 
+    PAIR_STAMP(1);
     // ---- epilogue: + residual (registers), ReLU, bf16 -> Y chunk (LDS)
 #pragma unroll
     for (int i = 0; i < FI; ++i) {
@@ -198,6 +233,7 @@ __global__ __launch_bounds__(512) void conv_pair_kernel(const PairParams p) {
                      pack_relu_bf16x2(add_bf16_lo(rv.y, accb[i][2]), add_bf16_hi(rv.y, accb[i][3])));
     }
     pbarrier();  // Y chunk visible (and every wave is past the chunk buffer's previous readers)
+    PAIR_STAMP(2);
 
     // next pass's bias and B fragments (waited for at the next B phase) and residual (waited for at the next
     // epilogue), issued in that order and ahead of this pass's Y stores: every wait is then a count of younger
@@ -206,19 +242,22 @@ __global__ __launch_bounds__(512) void conv_pair_kernel(const PairParams p) {
     b3v = *reinterpret_cast<const f32x4_t*>(p.b3 + pn * PR_CH + 16 * w + 4 * lg);
 #pragma unroll
     for (int k = 0; k < NKB; ++k) wb[k] = w3frag(pn, k);
-#pragma unroll
-    for (int i = 0; i < FI; ++i) rr[i] = *reinterpret_cast<const uint2*>(resl[i] + pn * PR_CH);
-    __builtin_amdgcn_sched_barrier(0);
-    // ---- Y chunk -> HBM (16-B row stores)
-#pragma unroll
-    for (int e = 0; e < NS; ++e) {
+    auto copy_out = [&](int e) __attribute__((always_inline)) {  // ---- Y chunk -> HBM (16-B row stores)
       const int g = tid + 512 * e;
       const int r = g >> 4, cq = g & 15;
       const uint4 v = *reinterpret_cast<const uint4*>(ybuf + (cq >> 2) * KBS + r * 64 + (((cq & 3) ^ pswz(r)) << 4));
       if (m0 + r < p.M) ai4e_conv::st16_stream(p.y + static_cast<long>(m0 + r) * C4 + pass * PR_CH + 8 * cq, v);
+    };
+    if constexpr (!SP) {
+#pragma unroll
+      for (int i = 0; i < FI; ++i) rr[i] = *reinterpret_cast<const uint2*>(resl[i] + pn * PR_CH);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int e = 0; e < NS; ++e) copy_out(e);
+      __builtin_amdgcn_sched_barrier(0);
     }
-    __builtin_amdgcn_sched_barrier(0);
 
+    PAIR_STAMP(3);
     // ---- C: accn += Y chunk . W1'[:, chunk]^T (pixel fragments one K step ahead, as in B)
     bf16x8_t fy[2][FI];
 #pragma unroll
@@ -236,8 +275,17 @@ __global__ __launch_bounds__(512) void conv_pair_kernel(const PairParams p) {
 #pragma unroll
         for (int j = 0; j < JC; ++j)
           accn[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wc[k][j], fy[k & 1][i], accn[i][j], 0, 0, 0);
+      if constexpr (SP) {
+        constexpr int RPS = (FI + NKC - 1) / NKC;  // residual loads per C step
+        if (k < NS) copy_out(k);
+#pragma unroll
+        for (int i = k * RPS; i < (k + 1) * RPS && i < FI; ++i)
+          rr[i] = *reinterpret_cast<const uint2*>(resl[i] + pn * PR_CH);
+        static_assert(NS <= NKC, "one Y store chunk per C step");
+      }
       if constexpr (KF) __builtin_amdgcn_sched_barrier(0);
     }
+    PAIR_STAMP(4);
   }
 
   // ---- T1' epilogue through the T2 region (every wave finished its last B phase before the last barrier);
@@ -258,19 +306,27 @@ __global__ __launch_bounds__(512) void conv_pair_kernel(const PairParams p) {
     const uint4 v = *reinterpret_cast<const uint4*>(t2s + (cq >> 2) * KBS + r * 64 + (((cq & 3) ^ pswz(r)) << 4));
     if (m0 + r < p.M) ai4e_conv::st16_stream(p.t1n + static_cast<long>(m0 + r) * MIDN + 8 * cq, v);
   }
+#if AI4E_PAIR_STAMPS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  PAIR_STAMP(5);
+  if (lane == 0 && blockIdx.x * PR_WAVES + w < PAIR_MAXW) {
+#pragma unroll
+    for (int k = 0; k < PAIR_NSEG; ++k) g_pair_stamps[(blockIdx.x * PR_WAVES + w) * PAIR_NSEG + k] = ps_sum[k];
+  }
+#endif
 }
 
-template <int MID, int C4, int MIDN, int BM, bool KF = true>
+template <int MID, int C4, int MIDN, int BM, bool KF = true, bool SP = false>
 int launch_pair(const PairParams& p, hipStream_t s) {
   constexpr int LDS = (MID / 32 + 2 * PR_CH / 32 > MIDN / 32 ? MID / 32 + 2 * PR_CH / 32 : MIDN / 32) * kbs<BM>();
   static bool attr = false;
   if (!attr) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(conv_pair_kernel<MID, C4, MIDN, BM, KF>),
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(conv_pair_kernel<MID, C4, MIDN, BM, KF, SP>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, LDS) != hipSuccess)
       return AI4E_ELAUNCH;
     attr = true;
   }
-  hipLaunchKernelGGL((conv_pair_kernel<MID, C4, MIDN, BM, KF>), dim3(ai4e_cdiv(p.M, BM)), dim3(512), LDS, s, p);
+  hipLaunchKernelGGL((conv_pair_kernel<MID, C4, MIDN, BM, KF, SP>), dim3(ai4e_cdiv(p.M, BM)), dim3(512), LDS, s, p);
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
 }
 
@@ -281,6 +337,14 @@ int launch_pair(const PairParams& p, hipStream_t s) {
 // (mid, c4, midn) = (256, 1024, 256) (layer3), (128, 512, 256) (layer2 -> layer3), (256, 1024, 512) (layer3 -> layer4)
 // or (512, 2048, 512) (layer4). bm_cfg: 0 = default tile,
 // else the tile height in pixels (64 or 96 for layer3, 32 for layer4; taller tiles spill at 256 VGPRs).
+#if AI4E_PAIR_STAMPS
+// Diagnostic build only: per-wave segment cycle sums of the last K1p launch (32768 waves x 6).
+AI4E_API int ai4e_pair_stamps_read(void* host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_pair_stamps), sizeof(g_pair_stamps)) == hipSuccess ? AI4E_OK
+                                                                                                  : AI4E_ELAUNCH;
+}
+#endif
+
 AI4E_API int ai4e_conv_pair_fwd(const void* t2, const void* w3p, const void* b3, const void* res, void* y,
                                 const void* w1p, const void* b1n, void* t1n, int M, int mid, int c4, int midn,
                                 int bm_cfg, hipStream_t stream) {
@@ -298,8 +362,9 @@ AI4E_API int ai4e_conv_pair_fwd(const void* t2, const void* w3p, const void* b3,
   if (M == 0) return AI4E_OK;
   if (mid == 256 && c4 == 1024 && midn == 256) {
     switch (bm_cfg) {
-      case 0:
-      case 96: return launch_pair<256, 1024, 256, 96>(p, stream);
+      case 0:   // default: loads + stores spread over the C phase (profiles/r3_pair/)
+      case 98: return launch_pair<256, 1024, 256, 96, true, true>(p, stream);
+      case 96: return launch_pair<256, 1024, 256, 96>(p, stream);  // A/B reference: the burst after the Y barrier
       case 64: return launch_pair<256, 1024, 256, 64>(p, stream);
       case 97: return launch_pair<256, 1024, 256, 96, false>(p, stream);  // A/B: scheduler-placed fragment reads
       default: return AI4E_EINVAL;

@@ -33,6 +33,8 @@ CASES = [
     (2, 14, 14, 256, 64),
     (1, 5, 7, 256, 0),        # M = 35 < one tile
     (8, 14, 14, 256, 96),     # M = 1568: 17 tiles
+    (8, 14, 14, 256, 98),     # loads + stores spread over the C phase
+    (1, 5, 7, 256, 98),       # ... with a partial tile
     (2, 7, 7, 512, 0),        # layer4 shape
     (1, 3, 5, 512, 32),
 ]

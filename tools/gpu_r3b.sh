@@ -21,6 +21,8 @@ run() {  # name timeout cmd...
 [ -n "${CHAIN_CFGS:-}" ] && run chain_ab 300 python -u bench/chain_patch_ab.py
 [ -n "${MICRO:-}" ] && run micro 300 env CFGS=${MICRO_CFGS:-9,10} TWO=1 python -u bench/conv_micro.py $MICRO
 [ -n "${RETUNE:-}" ] && run retune 900 env B=250 TUNE_PAIR=1 TUNE_REPS=${TUNE_REPS:-12} TUNE_OUT=gpurun_out/conv_tiles_retuned.json python -u bench/conv_tune_model.py resnet
+[ -n "${PAIRMICRO:-}" ] && run pairmicro 300 env PAIR_TILES=$PAIRMICRO python -u bench/pair_micro.py
+[ -n "${PAIRST:-}" ] && run pairst 300 python -u tools/pair_stamps.py
 [ -n "${K256ST:-}" ] && run k256st 300 python -u tools/k256_stamps.py
 [ -n "${CUSPLIT:-}" ] && run cusplit 400 python -u bench/cu_split_probe.py $CUSPLIT
 [ -n "${BIGB:-}" ] && for bb in $BIGB; do run "bigb_$bb" 400 env B=$bb NO_SPLIT=1 NB=30 python -u bench/cu_split_probe.py; done
