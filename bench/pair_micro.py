@@ -39,7 +39,7 @@ def main():
     dev = "cuda"
     out = {}
     for mid, hw, tiles, midn in ((256, 14, tuple(int(t) for t in os.environ.get("PAIR_TILES", "96,64").split(",")), 256),
-                                 (128, 28, (96, 64), 256), (256, 14, (64,), 512), (512, 7, (32,), 512)):
+                                 (128, 28, (96, 98), 256), (256, 14, (64, 98), 512), (512, 7, (32, 98), 512)):
         c4 = 4 * mid
         torch.manual_seed(0)
         c3 = pack_conv(torch.randn(c4, mid, 1, 1) / mid ** 0.5, torch.randn(c4) * 0.1).to(dev)

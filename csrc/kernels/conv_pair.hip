@@ -372,16 +372,18 @@ AI4E_API int ai4e_conv_pair_fwd(const void* t2, const void* w3p, const void* b3,
   }
   if (mid == 128 && c4 == 512 && midn == 256) {  // last layer2 block -> layer3's first c1
     switch (bm_cfg) {
-      case 0:
       case 96: return launch_pair<128, 512, 256, 96>(p, stream);
+      case 0:
+      case 98: return launch_pair<128, 512, 256, 96, true, true>(p, stream);  // spread loads/stores (A/B)
       case 64: return launch_pair<128, 512, 256, 64>(p, stream);
       default: return AI4E_EINVAL;
     }
   }
   if (mid == 256 && c4 == 1024 && midn == 512) {  // last layer3 block -> layer4's first c1 (BM 64: 241 VGPRs at 96)
     switch (bm_cfg) {
-      case 0:
       case 64: return launch_pair<256, 1024, 512, 64>(p, stream);
+      case 0:
+      case 98: return launch_pair<256, 1024, 512, 64, true, true>(p, stream);  // spread loads/stores (A/B)
       default: return AI4E_EINVAL;
     }
   }
@@ -389,6 +391,7 @@ AI4E_API int ai4e_conv_pair_fwd(const void* t2, const void* w3p, const void* b3,
     switch (bm_cfg) {
       case 0:
       case 32: return launch_pair<512, 2048, 512, 32>(p, stream);
+      case 98: return launch_pair<512, 2048, 512, 32, true, true>(p, stream);  // spread loads/stores (A/B)
       default: return AI4E_EINVAL;
     }
   }

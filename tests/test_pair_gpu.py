@@ -37,6 +37,12 @@ CASES = [
     (1, 5, 7, 256, 98),       # ... with a partial tile
     (2, 7, 7, 512, 0),        # layer4 shape
     (1, 3, 5, 512, 32),
+    (2, 14, 14, 256, 98, 512),  # spread variant of the other shapes
+    (1, 5, 7, 256, 98, 512),
+    (2, 28, 28, 128, 98, 256),
+    (1, 5, 9, 128, 98, 256),
+    (2, 7, 7, 512, 98),
+    (1, 3, 5, 512, 98),
 ]
 
 
