@@ -119,7 +119,9 @@ def build_tools(verbose: bool = False, force: bool = False) -> None:
     headers = sorted((CSRC / "core").glob("*.h"))
     for src, out in ((CSRC / "ingest" / "ingestd.cpp", INGESTD), (CSRC / "ingest" / "http_load.cpp", HTTP_LOAD)):
         if force or _stale(out, [src, *headers]):
-            _run([cxx, "-O2", "-std=c++17", "-Wall", "-pthread", str(src), "-o", str(out), "-lrt"], verbose)
+            # OpenSSL (TLS termination in ai4e_ingestd, HTTPS load generation in ai4e_http_load)
+            _run([cxx, "-O2", "-std=c++17", "-Wall", "-pthread", str(src), "-o", str(out), "-lrt", "-lssl", "-lcrypto"],
+                 verbose)
 
 
 def build_all(verbose: bool = False, force: bool = False) -> None:

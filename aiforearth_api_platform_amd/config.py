@@ -104,6 +104,10 @@ class Config:
     # Ocp-Apim-Subscription-Key header or the subscription-key query parameter; routes may add keys of their own
     # (`keys:` in the route table). Empty and no route keys = open access.
     subscription_keys: str = field(default="", metadata={"env": "AI4E_SUBSCRIPTION_KEYS"})
+    # keys of the control routes (cache upsert/get, requests upsert/get, backend webhook, metrics/stats; the
+    # reference's Function keys): besides the global keys. Once ANY key is configured (global, per route or here)
+    # the control routes refuse unkeyed requests, so per-route keys alone never leave them open.
+    control_keys: str = field(default="", metadata={"env": "AI4E_CONTROL_KEYS"})
     # --- autoscaler (HPA analogue, autoscaler.yaml: min/max replicas, target CURRENT_REQUESTS per replica) ---
     autoscale: bool = field(default=False, metadata={"env": "AI4E_AUTOSCALE"})
     autoscale_min_workers: int = field(default=1, metadata={"env": "AI4E_AUTOSCALE_MIN"})

@@ -59,10 +59,12 @@ class KeyAuth:
             ok |= hmac.compare_digest(key.encode(), a.encode())
         return ok
 
-    def check(self, headers, query=None, route_keys: Optional[Iterable[str]] = None) -> Optional[Tuple[int, dict]]:
-        """None when the request may pass, else (401, APIM-style body)."""
+    def check(self, headers, query=None, route_keys: Optional[Iterable[str]] = None,
+              locked: bool = False) -> Optional[Tuple[int, dict]]:
+        """None when the request may pass, else (401, APIM-style body). ``locked``: the route is protected even
+        when no key opens it (a request then always gets 401)."""
         allowed = list(self.global_keys) + parse_keys(route_keys or [])
-        if not allowed:
+        if not allowed and not locked:
             return None
         key = self.presented(headers, query)
         if not key:

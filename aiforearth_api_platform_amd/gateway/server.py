@@ -138,14 +138,35 @@ class Gateway:
 
     # ------------------------------------------------------------------ security
     OPEN_PATHS = ("/", "/openapi.json")
+    TASK_PREFIX = "/v1/taskmanagement/"
+    CONTROL_PATHS = ("/v1/cache/upsert", "/v1/cache/get", "/v1/requests/upsert", "/v1/requests/get",
+                     "/v1/backend/webhook", "/metrics", "/v1/platform/stats")
+
+    def _route_keys(self) -> List[str]:
+        keys: List[str] = []
+        for r in self.routes.routes:
+            keys += list(r.keys or [])
+        return keys
 
     @web.middleware
     async def _key_middleware(self, request, handler):
-        """Subscription-key check ahead of every handler: API routes accept the global keys and their own; the
-        task-management and control routes the global keys; health and the OpenAPI document are open."""
-        if request.path not in self.OPEN_PATHS:
-            route = self.routes.match(request.path)
-            rej = self.auth.check(request.headers, request.query, route.keys if route is not None else None)
+        """Subscription-key check ahead of every handler. API routes accept the global keys and their own. Once
+        any key is configured anywhere, the task-management routes accept the global keys, the control keys and
+        any route's keys (every subscriber polls its tasks), and the control routes only the global and control
+        keys (no key at all opens them then: they are the reference's key-protected Function endpoints). Health
+        and the OpenAPI document are open."""
+        path = request.path
+        if path not in self.OPEN_PATHS:
+            control_keys = parse_keys(getattr(self.cp.cfg, "control_keys", ""))
+            route_keys = self._route_keys()
+            protected = bool(self.auth.global_keys or control_keys or route_keys)
+            if path in self.CONTROL_PATHS:
+                rej = self.auth.check(request.headers, request.query, control_keys, locked=protected)
+            elif path.startswith(self.TASK_PREFIX):
+                rej = self.auth.check(request.headers, request.query, control_keys + route_keys, locked=protected)
+            else:
+                route = self.routes.match(path)
+                rej = self.auth.check(request.headers, request.query, route.keys if route is not None else None)
             if rej is not None:
                 return web.json_response(rej[1], status=rej[0])
         return await handler(request)

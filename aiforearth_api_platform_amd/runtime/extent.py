@@ -134,18 +134,23 @@ def encode_request(body: bytes, mosaics: Sequence[MosaicSpec], op: int, max_hw: 
         xs, ys = (float(e["xmin"]), float(e["xmax"])), (float(e["ymin"]), float(e["ymax"]))
     except PayloadError:
         raise
-    except (ValueError, KeyError, TypeError) as err:
+    except (ValueError, KeyError, TypeError, AttributeError, IndexError) as err:  # (non-object bodies too)
         raise PayloadError(f"extent request must be JSON {{mosaic, extent: {{xmin, ymin, xmax, ymax}}, crs}}: {err}")
+    if not all(math.isfinite(v) for v in xs + ys):  # json.loads accepts NaN / Infinity
+        raise PayloadError("extent coordinates must be finite numbers")
     crs = str(d.get("crs", "pixel")).lower()
-    if crs == "geo":
-        corners = [m.geotransform.to_pixel(x, y) for x in xs for y in ys]
-        c0, c1 = min(c for c, _ in corners), max(c for c, _ in corners)
-        r0, r1 = min(r for _, r in corners), max(r for _, r in corners)
-        x0, x1, y0, y1 = math.floor(c0), math.ceil(c1), math.floor(r0), math.ceil(r1)
-    elif crs == "pixel":
-        x0, x1, y0, y1 = int(xs[0]), int(xs[1]), int(ys[0]), int(ys[1])
-    else:
-        raise PayloadError(f"crs must be 'pixel' or 'geo', got {crs!r}")
+    try:
+        if crs == "geo":
+            corners = [m.geotransform.to_pixel(x, y) for x in xs for y in ys]
+            c0, c1 = min(c for c, _ in corners), max(c for c, _ in corners)
+            r0, r1 = min(r for _, r in corners), max(r for _, r in corners)
+            x0, x1, y0, y1 = math.floor(c0), math.ceil(c1), math.floor(r0), math.ceil(r1)
+        elif crs == "pixel":
+            x0, x1, y0, y1 = int(xs[0]), int(xs[1]), int(ys[0]), int(ys[1])
+        else:
+            raise PayloadError(f"crs must be 'pixel' or 'geo', got {crs!r}")
+    except (OverflowError, ValueError) as err:  # (a finite extent far outside any raster in geo units)
+        raise PayloadError(f"extent out of range: {err}")
     x0, y0 = max(0, x0), max(0, y0)
     x1, y1 = min(m.width, x1), min(m.height, y1)
     if x1 <= x0 or y1 <= y0:
@@ -194,6 +199,10 @@ class ExtentSegmenter:
         self.grids = [TileGrid(m.height, m.width, ts, stride) for m in self.specs]
         self.mosaics = [m.load(self.device) for m in self.specs]  # resident in HBM for the worker's lifetime
 
+    def valid(self, rec: Sequence[int]) -> bool:
+        _, mi, x0, y0, x1, y1 = (int(v) for v in rec[:6])
+        return 0 <= mi < len(self.grids) and 0 <= x0 < x1 <= self.grids[mi].width and 0 <= y0 < y1 <= self.grids[mi].height
+
     def __call__(self, rec: Sequence[int]) -> Tuple[torch.Tensor, Tuple[int, int, int, int]]:
         """Class map of the record's window (the ingest already resolved the op to a window)."""
         from ..ops.stitch import TileGrid, tile_stitch
@@ -240,13 +249,24 @@ class ExtentServable(Servable):
         for i in range(b):
             if int(recs[i, 0]) != _MAGIC:  # (padding rows of a partial batch bucket)
                 continue
-            if int(recs[i, 4]) - int(recs[i, 2]) > self.max_hw[1] or int(recs[i, 5]) - int(recs[i, 3]) > self.max_hw[0]:
-                raise ValueError("extent window larger than the endpoint's class-map canvas")
+            # a record that did not come through encode_request (e.g. raw bytes) fails on its own: window x = -1
+            # marks it invalid (invalid_rows), the other requests of the batch are served
+            if (int(recs[i, 4]) - int(recs[i, 2]) > self.max_hw[1] or int(recs[i, 5]) - int(recs[i, 3]) > self.max_hw[0]
+                    or not self.seg.valid(recs[i])):
+                win[i, 0] = -1
+                continue
             cls, (x, y, w, h) = self.seg(recs[i])
             canvas[i, :h, :w] = cls
             win[i] = torch.tensor([x, y, w, h], dtype=torch.int32)
             hist[i] = torch.bincount(cls.reshape(-1).long(), minlength=self.n_classes)[: self.n_classes]
         return canvas, win.to(records_u8.device), hist
+
+    @staticmethod
+    def invalid_rows(outputs) -> np.ndarray:
+        """Rows whose record was refused (worker: status IT_INVALID for those items only)."""
+        win = outputs[1]
+        win = win.numpy() if isinstance(win, torch.Tensor) else np.asarray(win)
+        return win[:, 0] < 0
 
     @staticmethod
     def format(fields):

@@ -161,7 +161,8 @@ def frontend_main(index: int, host: str, port: int, internal_url: str, endpoints
 
     async def handle(request):
         r = match(request.path)
-        if request.path not in ("/", "/openapi.json"):
+        # route-less paths (task management, control routes) are proxied: the serving process's key policy decides
+        if request.path not in ("/", "/openapi.json") and r is not None:
             rej = auth.check(request.headers, request.query, r.get("keys") if r is not None else None)
             if rej is not None:
                 return web.json_response(rej[1], status=rej[0])

@@ -313,9 +313,22 @@ class GpuWorker:
         h2d_ms, comp_ms = p.res.gpu_ms()
         self.busy_ms += h2d_ms + comp_ms
         rows = self._rows(p.n, p.valid, p.res.outputs)
+        self._mark_invalid(p.status, p.valid, p.res.outputs)
         if getattr(self.servable, "stages", 0):  # ensemble hop (AddPipelineTask) for this batch's tasks
             self.conn.stage(p.bid, 0)
         self.conn.done(p.bid, p.status, rows, self.row_bytes, (p.t_recv, p.res.t_launch, t_done, h2d_ms, comp_ms))
+
+    def _mark_invalid(self, status: np.ndarray, valid: np.ndarray, outputs) -> None:
+        """Servables that refuse single rows (``invalid_rows(outputs)`` -> bool per valid row, e.g. an extent record
+        that did not come through the request decoder) fail those items alone as invalid payloads."""
+        fn = getattr(self.servable, "invalid_rows", None)
+        if fn is None:
+            return
+        bad = np.asarray(fn(outputs), bool)
+        idx = np.nonzero(valid)[0]
+        bad = bad[: idx.shape[0]]
+        if bad.any():
+            status[idx[bad]] = P.IT_INVALID
 
     def _isolate(self, bid: int, slots: np.ndarray, valid: np.ndarray, status: np.ndarray, t_recv: float) -> None:
         """Batch launch failed (pipeline already drained): run each valid item alone."""
@@ -333,6 +346,9 @@ class GpuWorker:
                     raise RuntimeError("injected item failure")
                 outs = self.engine.run_sync(self.buf[int(slots[i]): int(slots[i]) + 1])
                 rows[i] = np.frombuffer(encode_rows([o.numpy() for o in outs], 1), np.uint8)
+                one = np.zeros(1, np.uint8)
+                self._mark_invalid(one, np.ones(1, bool), outs)
+                status[i] = max(status[i], one[0])
             except Exception as e:  # this item fails on its own
                 import sys
                 print(f"[ai4e worker {self.rank}] item (slot {int(slots[i])}) failed alone: {e!r}", file=sys.stderr,

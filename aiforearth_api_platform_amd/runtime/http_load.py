@@ -101,7 +101,8 @@ def run_native_clients(url: str, seconds: float, conc: int, body: bytes, content
     start_at = time.time() + 1.0
     ps = []
     for i in range(procs):
-        cmd = [str(_build.HTTP_LOAD), u.hostname, str(u.port), u.path + (("?" + u.query) if u.query else ""),
+        host = ("tls:" if u.scheme == "https" else "") + u.hostname  # (https: TLS sessions, no cert verification)
+        cmd = [str(_build.HTTP_LOAD), host, str(u.port), u.path + (("?" + u.query) if u.query else ""),
                content_type, body_path, str(conc), str(seconds), f"{start_at:.6f}", os.path.join(tmp, f"ids{i}.txt"),
                *headers]
         ps.append(subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))

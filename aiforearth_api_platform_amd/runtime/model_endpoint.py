@@ -156,6 +156,8 @@ class ModelEndpoint:
 
     def submit_raw_batch(self, body: bytes, trace: str = "") -> List[str]:
         """Binary batch ingest: ``n * prod(item_shape)`` raw uint8 bytes -> n tasks (one copy per run)."""
+        if self.custom_decode:
+            raise PayloadError("binary batch ingest is not accepted by this endpoint (its requests are decoded)", 415)
         item = int(np.prod(self.item_shape))
         if len(body) == 0 or len(body) % item:
             raise PayloadError(f"batch payload must be a multiple of {item} bytes (uint8 {self.item_shape})")
@@ -165,6 +167,8 @@ class ModelEndpoint:
     def begin_stream_batch(self, nbytes: int, trace: str = "") -> "StreamedBatch":
         """Binary batch ingest without buffering the body: ``nbytes`` (a multiple of the item size) are
         fed chunk by chunk straight into ring slots allocated up front, then enqueued (``finish``)."""
+        if self.custom_decode:
+            raise PayloadError("binary batch ingest is not accepted by this endpoint (its requests are decoded)", 415)
         item = int(np.prod(self.item_shape))
         if nbytes <= 0 or nbytes % item:
             raise PayloadError(f"batch payload must be a multiple of {item} bytes (uint8 {self.item_shape})")

@@ -6,7 +6,8 @@ ring, SUBMIT_IDS / SUBMITTED / FREE with the node scheduler over its own ingest 
 C++: a binary batch or a raw single payload is ``recv()``'d straight into ring slots (one kernel->ring copy,
 no interpreter on the path), one thread per client connection. Requests it does not ingest itself (encoded
 images, task API, sync routes, upstream ``taskId`` requests, chunked bodies) are proxied to the serving
-process. TLS is not terminated there: with a certificate configured the platform starts the Python front-ends.
+process. With a certificate configured (``security["tls_cert"]`` / ``["tls_key"]``) every client connection is a
+TLS session terminated in the native process (OpenSSL); the body is decrypted straight into the ring slots.
 
 The scheduler connection is the socket end of a ``multiprocessing.Pipe`` (a socketpair) inherited by the
 child; the config is a small line-oriented file (``ingestd.cpp`` ``parse_config``).
@@ -76,8 +77,8 @@ def spawn_native_frontends(n: int, pools: Dict[str, object], routes: List[dict],
     if not n or not pools:
         return []
     sec = security or {}
-    if sec.get("tls_cert"):
-        raise ValueError("the native front-end does not terminate TLS; use the Python front-ends")
+    if bool(sec.get("tls_cert")) != bool(sec.get("tls_key")):
+        raise ValueError("TLS needs both a certificate (AI4E_TLS_CERT) and a private key (AI4E_TLS_KEY)")
     _build.build_tools()
     ihost, iport = internal_url.split("://", 1)[1].rsplit(":", 1)
     names = list(pools)
@@ -86,6 +87,8 @@ def spawn_native_frontends(n: int, pools: Dict[str, object], routes: List[dict],
         lines = [f"listen {_token(host)} {int(port)}", f"internal {_token(ihost)} {int(iport)}",
                  f"ack_timeout {float(ack_timeout_s)}"]
         lines += [f"key {_token(k)}" for k in sec.get("keys") or []]
+        if sec.get("tls_cert"):
+            lines.append(f"tls {_token(os.path.abspath(sec['tls_cert']))} {_token(os.path.abspath(sec['tls_key']))}")
         child_ends, fds = [], []
         for si, name in enumerate(names):
             ep = pools[name]

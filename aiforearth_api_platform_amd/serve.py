@@ -69,7 +69,7 @@ def start_frontends(cfg: Config, doc: Dict[str, Any], endpoints: Dict[str, Any],
                        "max_content_length": r.get("max_content_length"), "max_concurrent": r.get("max_concurrent"),
                        "keys": parse_keys(r.get("keys"))})
     security = {"keys": parse_keys(cfg.subscription_keys), "tls_cert": cfg.tls_cert, "tls_key": cfg.tls_key}
-    if cfg.frontend_impl == "native" and not cfg.tls_cert:
+    if cfg.frontend_impl == "native":  # (TLS terminated in the native front-ends too)
         from .runtime.native_frontend import spawn_native_frontends
 
         return spawn_native_frontends(frontend_count(cfg), pools, routes, cfg.host, port,

@@ -7,6 +7,9 @@
 //
 //   ai4e_http_load HOST PORT PATH CONTENT_TYPE BODY_FILE CONNS SECONDS START_AT_EPOCH IDS_OUT [HEADER...]
 //
+// HOST = "tls:ADDR" speaks HTTPS (TLS 1.2+, OpenSSL, no certificate verification: a load generator against the
+// platform's own front door); each request is then one SSL_write of the prebuilt head + body.
+//
 // Prints one JSON line: requests, ok, errors, t0, t1 (epoch s), bytes_sent, cpu_user_s, cpu_sys_s.
 // IDS_OUT receives one task id per line (TaskId / TaskIds of every 2xx answer).
 #include <arpa/inet.h>
@@ -30,7 +33,33 @@
 #include <thread>
 #include <vector>
 
+#include <openssl/err.h>
+#include <openssl/ssl.h>
+
 namespace {
+
+SSL_CTX* g_tls = nullptr;
+
+// one client connection: plain TCP or a TLS session over it
+struct Link {
+  int fd = -1;
+  SSL* ssl = nullptr;
+  void close() {
+    if (ssl) {
+      SSL_free(ssl);
+      ssl = nullptr;
+    }
+    if (fd >= 0) ::close(fd);
+    fd = -1;
+  }
+  ssize_t recv_some(char* p, size_t n) {
+    if (ssl) {
+      const int k = SSL_read(ssl, p, static_cast<int>(n));
+      return k > 0 ? k : 0;
+    }
+    return ::recv(fd, p, n, 0);
+  }
+};
 
 double now() {
   return std::chrono::duration<double>(std::chrono::system_clock::now().time_since_epoch()).count();
@@ -62,11 +91,11 @@ bool send_all(int fd, const struct iovec* iov0, int cnt) {
 }
 
 // Reads one response; returns the status (0 on a broken connection) and its body.
-int read_response(int fd, std::string& buf, std::string& body) {
+int read_response(Link& l, std::string& buf, std::string& body) {
   size_t hend;
   while ((hend = buf.find("\r\n\r\n")) == std::string::npos) {
     char tmp[65536];
-    ssize_t k = ::recv(fd, tmp, sizeof(tmp), 0);
+    ssize_t k = l.recv_some(tmp, sizeof(tmp));
     if (k <= 0) return 0;
     buf.append(tmp, static_cast<size_t>(k));
   }
@@ -78,7 +107,7 @@ int read_response(int fd, std::string& buf, std::string& body) {
   if (p != std::string::npos) clen = std::strtoull(head.c_str() + p + 15, nullptr, 10);
   while (buf.size() < hend + 4 + clen) {
     char tmp[65536];
-    ssize_t k = ::recv(fd, tmp, sizeof(tmp), 0);
+    ssize_t k = l.recv_some(tmp, sizeof(tmp));
     if (k <= 0) return 0;
     buf.append(tmp, static_cast<size_t>(k));
   }
@@ -110,7 +139,7 @@ void extract_ids(const std::string& body, std::vector<std::string>& out) {
   }
 }
 
-int dial(const char* host, int port) {
+int dial_tcp(const char* host, int port) {
   int fd = ::socket(AF_INET, SOCK_STREAM, 0);
   sockaddr_in a{};
   a.sin_family = AF_INET;
@@ -129,6 +158,30 @@ int dial(const char* host, int port) {
   return fd;
 }
 
+Link dial(const char* host, int port) {
+  Link l;
+  l.fd = dial_tcp(host, port);
+  if (l.fd >= 0 && g_tls) {
+    l.ssl = SSL_new(g_tls);
+    if (!l.ssl || SSL_set_fd(l.ssl, l.fd) != 1 || SSL_connect(l.ssl) != 1) {
+      ERR_clear_error();
+      l.close();
+    }
+  }
+  return l;
+}
+
+bool send_req(Link& l, const struct iovec* iov, const std::string& whole) {
+  if (!l.ssl) return send_all(l.fd, iov, 2);
+  size_t off = 0;
+  while (off < whole.size()) {
+    const int k = SSL_write(l.ssl, whole.data() + off, static_cast<int>(std::min<size_t>(whole.size() - off, 1u << 30)));
+    if (k <= 0) return false;
+    off += static_cast<size_t>(k);
+  }
+  return true;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -139,6 +192,13 @@ int main(int argc, char** argv) {
     return 2;
   }
   const char* host = argv[1];
+  if (std::strncmp(host, "tls:", 4) == 0) {
+    host += 4;
+    g_tls = SSL_CTX_new(TLS_client_method());
+    SSL_CTX_set_min_proto_version(g_tls, TLS1_2_VERSION);
+    SSL_CTX_set_verify(g_tls, SSL_VERIFY_NONE, nullptr);
+    SSL_CTX_set_mode(g_tls, SSL_MODE_AUTO_RETRY);
+  }
   const int port = std::atoi(argv[2]);
   const std::string path = argv[3], ctype = argv[4];
   std::ifstream bf(argv[5], std::ios::binary);
@@ -150,6 +210,7 @@ int main(int argc, char** argv) {
                      "\r\nContent-Type: " + ctype + "\r\nContent-Length: " + std::to_string(body.size()) + "\r\n";
   for (int i = 10; i < argc; ++i) head += std::string(argv[i]) + "\r\n";
   head += "\r\n";
+  const std::string whole = g_tls ? head + body : std::string();  // (TLS: one SSL_write per request)
 
   std::vector<Result> res(static_cast<size_t>(conns));
   while (now() < start_at) std::this_thread::sleep_for(std::chrono::microseconds(200));
@@ -158,24 +219,24 @@ int main(int argc, char** argv) {
   for (int c = 0; c < conns; ++c) {
     th.emplace_back([&, c] {
       Result& r = res[static_cast<size_t>(c)];
-      int fd = dial(host, port);
+      Link l = dial(host, port);
       std::string buf, rbody;
       struct iovec iov[2] = {{const_cast<char*>(head.data()), head.size()},
                              {const_cast<char*>(body.data()), body.size()}};
-      while (fd >= 0 && now() < t_end) {
-        if (!send_all(fd, iov, 2)) {
-          ::close(fd);
-          fd = dial(host, port);
+      while (l.fd >= 0 && now() < t_end) {
+        if (!send_req(l, iov, whole)) {
+          l.close();
+          l = dial(host, port);
           ++r.errors;
           continue;
         }
         ++r.requests;
         r.bytes += static_cast<double>(head.size() + body.size());
-        int st = read_response(fd, buf, rbody);
+        int st = read_response(l, buf, rbody);
         if (st == 0) {
-          ::close(fd);
+          l.close();
           buf.clear();
-          fd = dial(host, port);
+          l = dial(host, port);
           ++r.errors;
           continue;
         }
@@ -186,7 +247,7 @@ int main(int argc, char** argv) {
           ++r.errors;
         }
       }
-      if (fd >= 0) ::close(fd);
+      l.close();
     });
   }
   for (auto& t : th) t.join();

@@ -13,8 +13,14 @@
 //     upstream taskId, chunked bodies) is proxied to the serving process's internal listener.
 //
 // Admission matches the gateway (gateway/server.py, gateway/security.py): subscription keys (401), the
-// route's max_concurrent (429), draining after SIGTERM (503), content type (401), length (413). TLS is not
-// terminated here: with a certificate configured the platform runs the Python front-ends instead.
+// route's max_concurrent (429), draining after SIGTERM (503), content type (401), length (413; proxied bodies too,
+// with a global 1 GiB cap as aiohttp's client_max_size, chunked bodies counted as they arrive).
+//
+// TLS (the reference's Istio gateway on :443 with a mounted certificate, Cluster/networking/secure_routing_base.yml):
+// with "tls CERT KEY" in the config every client connection is a TLS 1.2+ session (OpenSSL; kernel TLS offload
+// where the kernel has it), and the ingest path SSL_read()s the request body straight into the ring slots — the
+// decryption is the one copy. The connection to the serving process's internal listener stays plain TCP on
+// loopback.
 //
 // Threads: one acceptor, one thread per client connection (blocking I/O, keep-alive), one reader per
 // scheduler connection. The process exits when a scheduler connection closes (the serving process is gone)
@@ -50,6 +56,9 @@
 #include <unordered_map>
 #include <vector>
 
+#include <openssl/err.h>
+#include <openssl/ssl.h>
+
 #include "../core/common.h"
 #include "../core/slot_ring.h"
 
@@ -66,6 +75,9 @@ const char* kInvalidKey =
     "Access denied due to invalid subscription key. Make sure to provide a valid key for an active subscription.";
 
 std::atomic<bool> g_draining{false};
+SSL_CTX* g_tls = nullptr;                     // non-null: client connections are TLS sessions
+constexpr int64_t kMaxBody = int64_t{1} << 30;  // global request-body cap (aiohttp client_max_size of the gateway)
+constexpr int64_t kMaxUpstreamBody = int64_t{1} << 34;  // responses of the (trusted) serving process
 
 // ------------------------------------------------------------------ socket helpers
 bool write_all(int fd, const void* p, size_t n) {
@@ -274,7 +286,7 @@ struct Config {
 
 Config g_cfg;
 
-// "listen H P" | "internal H P" | "key K" | "ack_timeout S" | "alloc_timeout S"
+// "listen H P" | "internal H P" | "key K" | "tls CERT KEY" | "ack_timeout S" | "alloc_timeout S"
 // "shard IDX FD SHM NSLOTS ITEM BASE LEN ENDPOINT SHAPE" | "route PREFIX MODE SHARD MCL MC TYPES|- KEYS|-"
 void parse_config(const char* path) {
   std::ifstream in(path);
@@ -295,6 +307,21 @@ void parse_config(const char* path) {
       std::string k;
       ls >> k;
       g_cfg.keys.push_back(k);
+    } else if (kw == "tls") {
+      std::string cert, key;
+      ls >> cert >> key;
+      g_tls = SSL_CTX_new(TLS_server_method());
+      if (!g_tls || SSL_CTX_set_min_proto_version(g_tls, TLS1_2_VERSION) != 1 ||
+          SSL_CTX_use_certificate_chain_file(g_tls, cert.c_str()) != 1 ||
+          SSL_CTX_use_PrivateKey_file(g_tls, key.c_str(), SSL_FILETYPE_PEM) != 1 || SSL_CTX_check_private_key(g_tls) != 1) {
+        std::fprintf(stderr, "ai4e_ingestd: cannot load TLS certificate %s / key %s\n", cert.c_str(), key.c_str());
+        ERR_print_errors_fp(stderr);
+        std::exit(2);
+      }
+      SSL_CTX_set_mode(g_tls, SSL_MODE_AUTO_RETRY);
+#ifdef SSL_OP_ENABLE_KTLS
+      SSL_CTX_set_options(g_tls, SSL_OP_ENABLE_KTLS);  // kernel TLS offload where available (no-op otherwise)
+#endif
     } else if (kw == "ack_timeout") {
       ls >> g_cfg.ack_timeout;
     } else if (kw == "alloc_timeout") {
@@ -350,6 +377,7 @@ struct Request {
 
 struct Conn {
   int fd;
+  SSL* ssl = nullptr;     // TLS session of a client connection (g_tls), else plain recv/send
   std::vector<char> buf;  // bytes received past the current parse point
   size_t pos = 0, end = 0;
   int upstream = -1;      // keep-alive connection to the internal listener
@@ -358,6 +386,41 @@ struct Conn {
   explicit Conn(int f) : fd(f), buf(1 << 16) {}
   ~Conn() {
     if (upstream >= 0) ::close(upstream);
+    if (ssl) SSL_free(ssl);
+  }
+  // one read of up to n bytes (> 0), 0 = closed / error
+  ssize_t recv_some(void* dst, size_t n) {
+    if (ssl) {
+      const int k = SSL_read(ssl, dst, static_cast<int>(std::min<size_t>(n, 1u << 30)));
+      return k > 0 ? k : 0;
+    }
+    ssize_t k;
+    do {
+      k = ::recv(fd, dst, n, 0);
+    } while (k < 0 && errno == EINTR);
+    return k > 0 ? k : 0;
+  }
+  bool read_exact(void* p, size_t n) {
+    if (!ssl) return ::read_exact(fd, p, n);
+    char* d = static_cast<char*>(p);
+    while (n) {
+      const ssize_t k = recv_some(d, n);
+      if (k <= 0) return false;
+      d += k;
+      n -= static_cast<size_t>(k);
+    }
+    return true;
+  }
+  bool send_all(const void* p, size_t n) {
+    if (!ssl) return write_all(fd, p, n);
+    const char* d = static_cast<const char*>(p);
+    while (n) {
+      const int k = SSL_write(ssl, d, static_cast<int>(std::min<size_t>(n, 1u << 30)));
+      if (k <= 0) return false;
+      d += k;
+      n -= static_cast<size_t>(k);
+    }
+    return true;
   }
   size_t avail() const { return end - pos; }
   bool fill() {
@@ -371,10 +434,7 @@ struct Conn {
         buf.resize(buf.size() * 2);
       }
     }
-    ssize_t k;
-    do {
-      k = ::recv(fd, buf.data() + end, buf.size() - end, 0);
-    } while (k < 0 && errno == EINTR);
+    const ssize_t k = recv_some(buf.data() + end, buf.size() - end);
     if (k <= 0) return false;
     end += static_cast<size_t>(k);
     return true;
@@ -388,7 +448,7 @@ struct Conn {
       dst += take;
       n -= take;
     }
-    return n == 0 || read_exact(fd, dst, n);
+    return n == 0 || read_exact(dst, n);
   }
   bool discard(size_t n) {
     std::vector<char> tmp(1 << 16);
@@ -397,7 +457,7 @@ struct Conn {
     n -= take;
     while (n) {
       size_t k = std::min(n, tmp.size());
-      if (!read_exact(fd, tmp.data(), k)) return false;
+      if (!read_exact(tmp.data(), k)) return false;
       n -= k;
     }
     return true;
@@ -422,7 +482,7 @@ bool read_head(Conn& c, Request& r) {
   while (true) {
     const char* b = c.buf.data() + c.pos;
     size_t n = c.avail();
-    for (size_t i = scanned ? scanned - 3 : 0; i + 3 < n; ++i) {
+    for (size_t i = scanned >= 3 ? scanned - 3 : 0; i + 3 < n; ++i) {
       if (b[i] == '\r' && b[i + 1] == '\n' && b[i + 2] == '\r' && b[i + 3] == '\n') {
         std::string head(b, i);
         c.pos += i + 4;
@@ -482,6 +542,7 @@ bool respond(Conn& c, int code, const std::string& ctype, const std::string& bod
   std::string h = "HTTP/1.1 " + std::to_string(code) + " " + reason(code) + "\r\nContent-Type: " + ctype +
                   "\r\nContent-Length: " + std::to_string(body.size()) + "\r\n" + extra_headers +
                   (keep_alive ? "" : "Connection: close\r\n") + "Server: ai4e-ingestd\r\n\r\n";
+  if (c.ssl) return c.send_all((h + body).data(), h.size() + body.size());  // one TLS record run
   struct iovec iov[2] = {{const_cast<char*>(h.data()), h.size()}, {const_cast<char*>(body.data()), body.size()}};
   size_t total = h.size() + body.size(), sent = 0;
   int idx = 0;
@@ -511,10 +572,30 @@ std::string message_json(const std::string& m) {
   return out + "}";
 }
 
+// application/x-www-form-urlencoded decoding of a query component (%XX, '+' = space), as aiohttp's request.query
+std::string url_decode(const std::string& v) {
+  std::string out;
+  out.reserve(v.size());
+  auto hex = [](char ch) {
+    return ch >= '0' && ch <= '9' ? ch - '0' : ch >= 'a' && ch <= 'f' ? ch - 'a' + 10 : ch >= 'A' && ch <= 'F' ? ch - 'A' + 10 : -1;
+  };
+  for (size_t i = 0; i < v.size(); ++i) {
+    if (v[i] == '+') {
+      out.push_back(' ');
+    } else if (v[i] == '%' && i + 2 < v.size() && hex(v[i + 1]) >= 0 && hex(v[i + 2]) >= 0) {
+      out.push_back(static_cast<char>(hex(v[i + 1]) * 16 + hex(v[i + 2])));
+      i += 2;
+    } else {
+      out.push_back(v[i]);
+    }
+  }
+  return out;
+}
+
 std::string query_param(const std::string& q, const std::string& name) {
   for (auto& kv : split(q, '&')) {
     auto eq = kv.find('=');
-    if (eq != std::string::npos && kv.substr(0, eq) == name) return kv.substr(eq + 1);
+    if (eq != std::string::npos && url_decode(kv.substr(0, eq)) == name) return url_decode(kv.substr(eq + 1));
   }
   return "";
 }
@@ -526,8 +607,10 @@ bool ct_equal(const std::string& a, const std::string& b) {  // constant time pe
   return d == 0;
 }
 
-// nullptr = allowed, else the APIM-style 401 message
+// nullptr = allowed, else the APIM-style 401 message. Only the API routes are checked here: route-less paths
+// (task management, control routes) are proxied and the serving process's key policy decides (gateway/server.py).
 const char* check_key(const Request& r, const Route* route) {
+  if (!route) return nullptr;
   std::vector<const std::string*> allowed;
   for (auto& k : g_cfg.keys) allowed.push_back(&k);
   if (route)
@@ -567,29 +650,37 @@ int connect_internal() {
   return fd;
 }
 
-bool read_body(Conn& c, const Request& r, std::string& body) {
+// 0 = body read, -1 = connection error, 413 = the body (declared length, or chunks so far) exceeds `limit`
+// bytes: nothing beyond the limit is allocated or read.
+int read_body(Conn& c, const Request& r, std::string& body, int64_t limit) {
   if (r.chunked) {
     while (true) {
       std::string l;
-      if (!c.line(l)) return false;
-      size_t n = std::strtoull(l.c_str(), nullptr, 16);
+      if (!c.line(l)) return -1;
+      if (l.size() > 32) return 413;  // a chunk-size line this long is not a size we would accept
+      errno = 0;
+      const unsigned long long n = std::strtoull(l.c_str(), nullptr, 16);
+      if (errno == ERANGE || n > static_cast<unsigned long long>(limit) ||
+          body.size() + n > static_cast<unsigned long long>(limit))
+        return 413;
       if (n == 0) {
         do {
-          if (!c.line(l)) return false;
+          if (!c.line(l)) return -1;
         } while (!l.empty());
-        return true;
+        return 0;
       }
       size_t off = body.size();
-      body.resize(off + n);
-      if (!c.body_into(reinterpret_cast<uint8_t*>(&body[off]), n)) return false;
-      if (!c.line(l)) return false;
+      body.resize(off + static_cast<size_t>(n));
+      if (!c.body_into(reinterpret_cast<uint8_t*>(&body[off]), static_cast<size_t>(n))) return -1;
+      if (!c.line(l)) return -1;
     }
   }
+  if (r.content_length > limit) return 413;
   if (r.content_length > 0) {
     body.resize(static_cast<size_t>(r.content_length));
-    return c.body_into(reinterpret_cast<uint8_t*>(&body[0]), body.size());
+    return c.body_into(reinterpret_cast<uint8_t*>(&body[0]), body.size()) ? 0 : -1;
   }
-  return true;
+  return 0;
 }
 
 bool is_hop(const std::string& k) {
@@ -601,9 +692,18 @@ bool is_hop(const std::string& k) {
   return false;
 }
 
-bool proxy(Conn& c, const Request& r) {
+bool too_large(Conn& c, int64_t limit) {  // answered before the body is read: the connection closes after
+  respond(c, 413, "application/json",
+          message_json("Request content too large. Must be smaller than: " + std::to_string(limit)), false);
+  return false;
+}
+
+bool proxy(Conn& c, const Request& r, const Route* route) {
+  const int64_t limit = route && route->max_content_length > 0 ? std::min(route->max_content_length, kMaxBody) : kMaxBody;
   std::string body;
-  if (!read_body(c, r, body)) return false;
+  const int rb = read_body(c, r, body, limit);
+  if (rb == 413) return too_large(c, limit);
+  if (rb != 0) return false;
   std::string req = r.method + " " + r.target + " HTTP/1.1\r\n";
   for (auto& kv : r.headers)
     if (!is_hop(kv.first)) req += kv.first + ": " + kv.second + "\r\n";
@@ -631,7 +731,7 @@ bool proxy(Conn& c, const Request& r) {
     if (status < 200 || status == 204 || status == 304 || r.method == "HEAD") {
       ok = true;  // no body by definition
     } else if (resp.chunked || resp.content_length >= 0) {
-      ok = read_body(up, resp, rbody);
+      ok = read_body(up, resp, rbody, kMaxUpstreamBody) == 0;
     } else {  // no length: until the upstream closes
       rbody.assign(up.buf.data() + up.pos, up.avail());
       up.pos = up.end;
@@ -705,6 +805,7 @@ bool ingest(Conn& c, const Request& r, Route& route, Shard& s, bool batch) {
   if (!route.content_types.empty() &&
       std::find(route.content_types.begin(), route.content_types.end(), ctype) == route.content_types.end())
     return reject(401, "Content-type must be " + py_list(route.content_types));
+  if (nbytes > kMaxBody) return reject(413, "Request content too large (" + std::to_string(nbytes) + ")");
   if (route.max_content_length > 0 && nbytes > route.max_content_length)
     return reject(413, "Request content too large (" + std::to_string(nbytes) +
                            "). Must be smaller than: " + std::to_string(route.max_content_length));
@@ -715,7 +816,7 @@ bool ingest(Conn& c, const Request& r, Route& route, Shard& s, bool batch) {
   if (n > s.len)
     return reject(413, "batch of " + std::to_string(n) + " items exceeds the ingest partition (" +
                            std::to_string(s.len) + " slots)");
-  if (lower(r.get("expect")) == "100-continue" && !write_all(c.fd, "HTTP/1.1 100 Continue\r\n\r\n", 25)) return false;
+  if (lower(r.get("expect")) == "100-continue" && !c.send_all("HTTP/1.1 100 Continue\r\n\r\n", 25)) return false;
   std::vector<int64_t> sl = s.slots->alloc(n, g_cfg.alloc_timeout);
   if (sl.empty()) {  // no ring slot in time: nothing was created
     if (!c.discard(static_cast<size_t>(nbytes))) return false;
@@ -758,6 +859,7 @@ bool ingest(Conn& c, const Request& r, Route& route, Shard& s, bool batch) {
   return respond(c, created < 0 ? 202 : 200, "text/plain; charset=utf-8", "TaskId: " + ids[0], ka, b3);
 }
 
+void serve_requests(Conn& c);
 std::atomic<int> g_conns{0};
 constexpr int kMaxConns = 4096;  // one thread each; beyond this new connections are answered 503 and closed
 
@@ -774,6 +876,24 @@ void serve_conn(int fd) {
   setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &idle, sizeof(idle));
   setsockopt(fd, SOL_SOCKET, SO_SNDTIMEO, &idle, sizeof(idle));
   Conn c(fd);
+  if (g_tls) {
+    c.ssl = SSL_new(g_tls);
+    if (!c.ssl || SSL_set_fd(c.ssl, fd) != 1 || SSL_accept(c.ssl) != 1) {
+      ERR_clear_error();
+      ::close(fd);
+      return;
+    }
+  }
+  try {
+    serve_requests(c);
+  } catch (const std::exception& e) {  // (bad_alloc, length_error, ...): this connection ends, the process stays
+    std::fprintf(stderr, "ai4e_ingestd: connection dropped: %s\n", e.what());
+  }
+  if (c.ssl) SSL_shutdown(c.ssl);
+  ::close(fd);
+}
+
+void serve_requests(Conn& c) {
   while (true) {
     Request r;
     if (!read_head(c, r)) break;
@@ -783,7 +903,8 @@ void serve_conn(int fd) {
         std::string body = "{\"statusCode\":401,\"message\":";
         ai4e::json_escape_into(body, msg);
         body += "}";
-        bool drained = r.chunked ? false : c.discard(static_cast<size_t>(std::max<int64_t>(0, r.content_length)));
+        bool drained = !r.chunked && r.content_length <= (1 << 20) &&
+                       c.discard(static_cast<size_t>(std::max<int64_t>(0, r.content_length)));
         if (!respond(c, 401, "application/json", body, r.keep_alive && drained) || !r.keep_alive || !drained) break;
         continue;
       }
@@ -798,11 +919,10 @@ void serve_conn(int fd) {
     } else if (ingestible && ctype == kRawType && r.content_length == s->item) {
       ok = ingest(c, r, *route, *s, false);
     } else {
-      ok = proxy(c, r);  // encoded images, task API, sync routes, ... -> the serving process
+      ok = proxy(c, r, route);  // encoded images, task API, sync routes, ... -> the serving process
     }
     if (!ok || !r.keep_alive) break;
   }
-  ::close(fd);
 }
 
 int listen_on(const std::string& host, int port) {
@@ -851,6 +971,10 @@ int main(int argc, char** argv) {
       continue;
     }
     if (g_conns.load() >= kMaxConns) {
+      if (g_tls) {  // (no handshake for a connection we are not going to serve)
+        ::close(fd);
+        continue;
+      }
       static const char busy[] =
           "HTTP/1.1 503 Service Unavailable\r\nContent-Type: application/json\r\nContent-Length: 54\r\n"
           "Connection: close\r\n\r\n{\"message\":\"Service is busy, please try again later.\"}";

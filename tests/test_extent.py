@@ -121,6 +121,17 @@ def test_extent_routes_through_pool_and_gateway(full_map):
             r = await c.post("/v2/landcover/classifybyextent", data=b"\x00" * 64,
                              headers={"Content-Type": "image/png"})
             out["badtype"] = r.status
+            # NaN / Infinity (json.loads accepts them), a non-object body, a geo extent past float range: 400
+            hj = {"Content-Type": "application/json"}
+            out["odd"] = [(await c.post("/v2/landcover/classifybyextent", data=b, headers=hj)).status for b in (
+                b'{"extent": {"xmin": NaN, "ymin": 0, "xmax": 5, "ymax": 5}}',
+                b'{"extent": {"xmin": 0, "ymin": -Infinity, "xmax": 5, "ymax": 5}}',
+                b'[1, 2, 3]', b'"text"',
+                b'{"crs": "geo", "extent": {"xmin": 1e308, "ymin": 0, "xmax": 1.7e308, "ymax": 5}}')]
+            # raw 64-byte records must not reach the workers: binary batch ingest is refused
+            r = await c.post("/v2/landcover/classifybyextent-async", data=b"\x00" * 128,
+                             headers={"Content-Type": "application/x-ai4e-batch"})
+            out["batch"] = r.status
             return out
         finally:
             await c.close()
@@ -142,3 +153,24 @@ def test_extent_routes_through_pool_and_gateway(full_map):
     assert np.array_equal(_png(out["tile"]["class_map"]),
                           full_map[tw["y0"]:tw["y0"] + tw["height"], tw["x0"]:tw["x0"] + tw["width"]])
     assert out["bad"] == 400 and out["badtype"] == 415
+    assert out["odd"] == [400] * 5, out["odd"]
+    assert out["batch"] == 415
+
+
+def test_extent_servable_refuses_bad_records_per_item():
+    """A record that did not come through encode_request (bad window / mosaic index) is marked invalid on its own
+    (invalid_rows -> IT_INVALID in the worker); the other requests of the batch are served."""
+    from aiforearth_api_platform_amd.models.unet import FusedUNet, unet_landcover
+    from aiforearth_api_platform_amd.runtime.extent import _MAGIC, ExtentServable
+
+    f = FusedUNet(unet_landcover(n_classes=NC, seed=0, width=32), device="cpu")
+    seg = ExtentSegmenter(f.forward_u8, MosaicSpec.parse(MOSAICS), TS, ST, f.n_classes, "cpu", tile_batch=8)
+    sv = ExtentServable(seg, (64, 64), NC)
+    good = _rec({"extent": {"xmin": 10, "ymin": 20, "xmax": 40, "ymax": 41}}, max_hw=(64, 64))
+    recs = np.stack([good, good.copy(), good.copy(), np.zeros(16, np.int32)])
+    recs[1, 4] = W + 500                     # window past the mosaic
+    recs[2, 1] = 7                           # no such mosaic
+    canvas, win, hist = sv(torch.from_numpy(recs.view(np.uint8)))
+    bad = ExtentServable.invalid_rows([canvas, win, hist])
+    assert bad.tolist() == [False, True, True, False]  # (row 3: padding without the magic)
+    assert int(recs[0, 0]) == _MAGIC and tuple(win[0].tolist()) == (10, 20, 30, 21)

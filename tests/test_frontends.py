@@ -264,3 +264,123 @@ def test_ingest_throughput_scales_with_native_frontends(tmp_path):
     r2 = _ingest_rate(cfgp, 2)
     print(f"ingest req/s: gateway only {r0:.0f}, + 2 native front-ends {r2:.0f}")
     assert r2 >= 1.5 * r0, (r0, r2)
+
+
+def _raw(port, payload: bytes, tls: bool, want_server: bool = True, tries: int = 40) -> bytes:
+    """One request on a fresh (TLS) connection; retried until the native front-end answered (SO_REUSEPORT spreads
+    connections over the listeners). Returns the raw response head + body."""
+    import socket
+    import ssl
+
+    ctx = ssl.create_default_context()
+    ctx.check_hostname, ctx.verify_mode = False, ssl.CERT_NONE
+    last = b""
+    for _ in range(tries):
+        s = socket.create_connection(("127.0.0.1", port), timeout=20)
+        if tls:
+            s = ctx.wrap_socket(s)
+        s.settimeout(3.0)  # (the serving process's aiohttp waits for a chunk it will never get: try the next one)
+        try:
+            s.sendall(payload)
+            out = b""
+            while b"\r\n\r\n" not in out:
+                chunk = s.recv(65536)
+                if not chunk:
+                    break
+                out += chunk
+            head = out.split(b"\r\n\r\n", 1)[0].lower()
+            clen = [int(line.split(b":", 1)[1]) for line in head.split(b"\r\n") if line.startswith(b"content-length:")]
+            while clen and len(out) < len(head) + 4 + clen[0]:
+                chunk = s.recv(65536)
+                if not chunk:
+                    break
+                out += chunk
+        except (TimeoutError, OSError):
+            out = b""
+        finally:
+            s.close()
+        last = out
+        if (b"server: ai4e-ingestd" in out.lower()) == want_server:
+            return out
+    return last
+
+
+def test_native_frontend_tls_and_body_limits(tmp_path):
+    """The native front-end terminates TLS (the reference's Istio gateway on :443): HTTPS requests are served by
+    ai4e_ingestd itself (raw and batch ingest into the ring, proxied task API), a percent-encoded subscription key
+    in the query string is decoded, and oversized bodies — a huge Content-Length on a proxied route, a huge chunk
+    size — get 413 without the process allocating them; the front-end keeps serving afterwards. HTTPS batch ingest
+    through the C++ load generator's TLS mode completes every task."""
+    from aiforearth_api_platform_amd.gateway.security import KEY_HEADER
+    from aiforearth_api_platform_amd.runtime.http_load import run_native_clients
+
+    cert = os.path.join(ROOT, "tests", "fixtures", "tls_test_cert.pem")
+    key = os.path.join(ROOT, "tests", "fixtures", "tls_test_key.pem")
+    doc = yaml.safe_load(open(os.path.join(ROOT, "examples", "platform_cpu.yaml")))
+    doc["endpoints"]["tiny"]["max_batch"] = 64
+    doc["routes"] = [{"prefix": "/v1/tiny/async", "mode": "async", "backend": "inproc:tiny",
+                      "max_content_length": 1 << 20}]
+    cfgp = tmp_path / "platform.yaml"
+    cfgp.write_text(yaml.safe_dump(doc))
+    port = _port()
+    env = dict(os.environ, PYTHONPATH=ROOT, AI4E_FRONTEND_PROCESSES="1", AI4E_FRONTEND_IMPL="native",
+               AI4E_TLS_CERT=cert, AI4E_TLS_KEY=key, AI4E_SUBSCRIPTION_KEYS="g+k")
+    proc = subprocess.Popen([sys.executable, "-m", "aiforearth_api_platform_amd.serve", "--config", str(cfgp),
+                             "--port", str(port)], cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+    base = f"https://127.0.0.1:{port}"
+    s = requests.Session()
+    s.verify, s.trust_env = cert, False
+    try:
+        for _ in range(600):
+            try:
+                if s.get(base + "/", timeout=1).status_code == 200:
+                    break
+            except requests.exceptions.ConnectionError:
+                time.sleep(0.1)
+        else:
+            raise AssertionError("server did not come up")
+        time.sleep(2.0)
+        img = np.zeros((4, 4, 3), np.uint8)
+        img[..., 1] = 70
+        hdr = f"Host: x\r\nContent-Type: application/octet-stream\r\n{KEY_HEADER}: g+k\r\nConnection: close\r\n"
+        r = _raw(port, (f"POST /v1/tiny/async HTTP/1.1\r\n{hdr}Content-Length: 48\r\n\r\n").encode() + img.tobytes(),
+                 tls=True)
+        assert r.startswith(b"HTTP/1.1 200") and b"server: ai4e-ingestd" in r.lower(), r[:300]
+        tid = json.loads(r.split(b"\r\n\r\n", 1)[1])["TaskId"]
+        # the key in the query string, percent-encoded ('+' must arrive as %2B)
+        r = _raw(port, b"POST /v1/tiny/async?subscription-key=g%2Bk HTTP/1.1\r\nHost: x\r\nContent-Type: "
+                 b"application/octet-stream\r\nConnection: close\r\nContent-Length: 48\r\n\r\n" + img.tobytes(), tls=True)
+        assert r.startswith(b"HTTP/1.1 200"), r[:300]
+        # a proxied route (JSON body) declaring 1 TB, and a chunked body with an absurd chunk size: 413, no body read
+        big = (f"POST /v1/tiny/async HTTP/1.1\r\nHost: x\r\nContent-Type: application/json\r\n{KEY_HEADER}: g+k\r\n"
+               f"Content-Length: 999999999999\r\n\r\n").encode()
+        r = _raw(port, big, tls=True)
+        assert r.startswith(b"HTTP/1.1 413") and b"server: ai4e-ingestd" in r.lower(), r[:300]
+        chunked = (f"POST /v1/tiny/async HTTP/1.1\r\nHost: x\r\nContent-Type: application/json\r\n{KEY_HEADER}: g+k\r\n"
+                   f"Transfer-Encoding: chunked\r\n\r\nfffffffffffffff\r\nxx").encode()
+        r = _raw(port, chunked, tls=True)
+        assert r.startswith(b"HTTP/1.1 413") and b"server: ai4e-ingestd" in r.lower(), r[:300]
+        # still serving (the same process: it would have been restarted by nobody)
+        r = _raw(port, (f"GET /v1/taskmanagement/task/{tid} HTTP/1.1\r\n{hdr}\r\n").encode(), tls=True)
+        assert r.startswith(b"HTTP/1.1 200") and b"server: ai4e-ingestd" in r.lower(), r[:300]
+        # HTTPS batch ingest from the C++ generator (4 connections, 16-image batches)
+        res = run_native_clients(f"{base}/v1/tiny/async", 1.5, 4, np.repeat(img[None], 16, 0).tobytes(),
+                                 "application/x-ai4e-batch", procs=1, headers=(f"{KEY_HEADER}: g+k",))
+        assert res["errors"] == 0 and len(res["ids"]) >= 16 and len(set(res["ids"])) == len(res["ids"])
+        deadline = time.time() + 60
+        pending = set(res["ids"][-64:])
+        while pending and time.time() < deadline:
+            for t in list(pending):
+                if s.get(f"{base}/v1/taskmanagement/task/{t}", headers={KEY_HEADER: "g+k"}).json()["BackendStatus"] \
+                        == "completed":
+                    pending.discard(t)
+            time.sleep(0.05)
+        assert not pending
+        out = _drain(proc)
+        assert "ai4e_ingestd pid" in out
+    finally:
+        proc.terminate()
+        try:
+            proc.wait(20)
+        except subprocess.TimeoutExpired:
+            proc.kill()

@@ -34,8 +34,8 @@ def _echo(task_id, body, headers):
     return 200, {"echo": json.loads(body or b"null")}
 
 
-def _gateway(global_keys):
-    cp = ControlPlane(Config.load(env={}, subscription_keys=global_keys))
+def _gateway(global_keys, control_keys=""):
+    cp = ControlPlane(Config.load(env={}, subscription_keys=global_keys, control_keys=control_keys))
     t = RouteTable()
     t.add(Route("/v1/echo", "sync", _echo, content_types=["application/json"], keys=["route-key"]))
     t.add(Route("/v1/open", "sync", _echo))
@@ -93,6 +93,8 @@ def test_gateway_keys_global_and_per_route():
 
 
 def test_route_keys_without_global_keys():
+    """Per-route keys only: unkeyed routes stay open, but the task-management routes want a key (any route's) and
+    the control routes (the reference's key-protected Function endpoints) open to no route key."""
     cp, gw = _gateway("")
 
     async def go():
@@ -101,9 +103,41 @@ def test_route_keys_without_global_keys():
         try:
             body, hdr = json.dumps({"b": 2}), {"Content-Type": "application/json"}
             assert (await c.post("/v1/open", data=body, headers=hdr)).status == 200
-            assert (await c.get("/v1/taskmanagement/task/abc")).status == 204
+            assert (await c.get("/v1/taskmanagement/task/abc")).status == 401
+            assert (await c.get("/v1/taskmanagement/task/abc", headers={KEY_HEADER: "route-key"})).status == 204
             assert (await c.post("/v1/echo", data=body, headers=hdr)).status == 401
             assert (await c.post("/v1/echo", data=body, headers=dict(hdr, **{KEY_HEADER: "route-key"}))).status == 200
+            upsert = json.dumps({"TaskId": "", "Status": "created", "BackendStatus": "created",
+                                 "Endpoint": "http://h/v1/x", "Body": "", "PublishToGrid": False})
+            for h in ({}, {KEY_HEADER: "route-key"}):
+                assert (await c.post("/v1/cache/upsert", data=upsert, headers=h)).status == 401
+                assert (await c.get("/v1/cache/get", params={"taskId": "abc"}, headers=h)).status == 401
+                assert (await c.post("/v1/backend/webhook", data="[]", headers=h)).status == 401
+                assert (await c.post("/v1/requests/upsert", data="{}", headers=h)).status == 401
+        finally:
+            await c.close()
+
+    run(go())
+    cp.close()
+
+
+def test_control_keys_open_control_routes():
+    cp, gw = _gateway("", control_keys="ck")
+
+    async def go():
+        c = TestClient(TestServer(gw.app))
+        await c.start_server()
+        try:
+            upsert = json.dumps({"TaskId": "", "Status": "created", "BackendStatus": "created",
+                                 "Endpoint": "http://h/v1/x", "Body": "", "PublishToGrid": False})
+            assert (await c.post("/v1/cache/upsert", data=upsert)).status == 401
+            assert (await c.post("/v1/cache/upsert", data=upsert, headers={KEY_HEADER: "route-key"})).status == 401
+            r = await c.post("/v1/cache/upsert", data=upsert, headers={KEY_HEADER: "ck"})
+            assert r.status == 200
+            tid = (await r.json())["TaskId"]
+            assert (await c.get(f"/v1/taskmanagement/task/{tid}", headers={KEY_HEADER: "ck"})).status == 200
+            assert (await c.get("/metrics", headers={KEY_HEADER: "ck"})).status == 200
+            assert (await c.get("/metrics")).status == 401
         finally:
             await c.close()
 
