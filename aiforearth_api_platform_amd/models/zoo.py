@@ -141,52 +141,14 @@ def camera_trap_ensemble(device="cuda", seed: int = 0, max_crops: int = 4, score
 
 
 # ------------------------------------------------------------------ worker-group (multi-GPU) forms
-class _PairEnsembleServable(EnsembleServable):
-    """Leader of a detector -> classifier GPU pair: detection + crops here, classification on the
-    follower GPU, crops and results over RCCL P2P (xGMI) — BASELINE config #5 as an API."""
-
-    stages = 1
-
-    def __init__(self, pipeline, max_crops: int):
-        super().__init__(pipeline, max_crops)
-
-    def __call__(self, images_u8):
-        from ..runtime.servable import pack_ensemble
-
-        _, sel, cls = self.pipeline.run_batches([images_u8])[0]
-        return pack_ensemble(images_u8.shape[0], sel, cls, self.max_crops)
-
-    def xgmi_bytes(self) -> dict:
-        return {"sent": self.pipeline.bytes_sent, "received": self.pipeline.bytes_received}
-
-    def close(self) -> None:
-        self.pipeline.stop()
-
-
 class _Follower:
     def __init__(self, serve):
         self.serve_follower = serve
 
 
-def camera_trap_ensemble_pair(device="cuda", group=None, role: str = "leader", seed: int = 0, max_crops: int = 4,
-                              score_thresh: float = 0.5, class_id: Optional[int] = 1, num_species: int = 200,
-                              wire_dtype: str = "uint8", **det_cfg):
-    """Worker group of 2 (``ModelSpec.group_size=2``, ``hip_graphs: false``): leader = detector GPU,
-    follower = species-classifier GPU."""
-    from ..runtime.pipeline import DetectClassifyPipeline, PipelineConfig
-
-    cfg = PipelineConfig(score_thresh=score_thresh, class_id=class_id, max_crops_per_image=max_crops,
-                         wire_dtype=wire_dtype)
-    dev = torch.device(device)
-    if role == "leader":
-        from .faster_rcnn import DetectorConfig, FasterRCNN
-
-        det = FasterRCNN(DetectorConfig(**det_cfg), seed=seed, device=device)
-        return _PairEnsembleServable(DetectClassifyPipeline(det, None, dev, cfg, group=group), max_crops)
-    from .resnet import FusedResNet, resnet50
-
-    cls = FusedResNet(resnet50(num_classes=num_species, seed=seed + 1), device=device)
-    return _Follower(DetectClassifyPipeline(None, cls.forward_u8, dev, cfg, group=group).serve_classifier)
+def camera_trap_ensemble_pair(device="cuda", group=None, role: str = "leader", **kw):
+    """The detector -> classifier GPU pair (``ModelSpec.group_size=2``): the 1:1 stage graph."""
+    return camera_trap_ensemble_group(device, group, role, group_rank=0, n_leaders=1, **kw)
 
 
 class _StageGraphEnsembleServable(EnsembleServable):

@@ -182,6 +182,12 @@ def run_node_bench(args, spec, path: str, metric: str, unit: str = "images/s", c
     from .worker_pool import WorkerPool
 
     endpoint = "http://127.0.0.1" + path
+    hang_s = float(os.environ.get("AI4E_HANG_DUMP_S", "0"))  # diagnostic: every thread's stack after this long
+    if hang_s > 0:
+        import faulthandler
+        import sys
+
+        faulthandler.dump_traceback_later(hang_s, repeat=False, file=sys.stderr)
     _, world, _ = env_ranks()
     if world > 1 and args.gpus != world:
         raise SystemExit(f"--gpus {args.gpus} != WORLD_SIZE {world}")
@@ -218,7 +224,9 @@ def run_node_bench(args, spec, path: str, metric: str, unit: str = "images/s", c
             from multiprocessing.connection import Listener
 
             key = secrets.token_bytes(16)
-            listener = Listener(("127.0.0.1", 0), authkey=key)
+            # backlog = every remote rank: with the default of 1, ranks that connect at once overflow the accept queue,
+            # their SYNs are dropped and retried after 1, 2, 4, ... s (a 40-90 s stall, 2 in 6 world-8 runs)
+            listener = Listener(("127.0.0.1", 0), authkey=key, backlog=max(1, world))
             info = {"shm": pool.ring.name, "nslots": pool.ring.nslots, "addr": listener.address, "key": key.hex()}
         objs = [info]
         if world > 1:

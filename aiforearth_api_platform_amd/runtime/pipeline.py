@@ -3,23 +3,21 @@
 The reference chains APIs by re-publishing the same TaskId to the next endpoint
 (``APIs/1.0/Common/task_management/distributed_api_task.py:67-100``,
 ``CacheConnectorUpsert.cs:144-176``): every hop is queue -> HTTP -> JSON. Here the stages are
-GPU ranks of one node and the hand-off is a tensor over xGMI:
+GPU ranks of one node and the hand-off is a tensor over xGMI (:class:`StageGraphPipeline`, N detector GPUs : M
+classifier GPUs of one group; 1:1 is the pair form):
 
 * detector ranks run Faster-RCNN on a batch, pick the confident animal boxes, crop + bilinear-resize
   them on the GPU to uint8 ``[N, 224, 224, 3]`` (``crop_resize_u8``, K5/K7: 147 KiB per crop, the
   classifier's own input format, half the bytes of fp16 and a sixth of a bf16x8 stem tensor) and
-  ``send`` a count header then the crops to their paired classifier rank over RCCL;
-* classifier ranks ``recv`` the count, the crops, run the crop classifier (fused ResNet-50 on K1,
-  the headline model's uint8 entry point) and send back ``[N, 2]`` (class, probability);
-* the detector side keeps one batch in flight: it sends batch i, starts detecting batch i+1, then
-  collects batch i's classifications — compute and transfer overlap; message order is fixed
-  (header, payload, results) so the pairing can never deadlock;
+  ``send`` a count header then the crops to their classifier rank over RCCL;
+* classifier ranks ``recv`` the count, the crops, run the crop classifier (fused ResNet-50, bf16 or fp16)
+  and send back ``[N, 2]`` (class, probability);
+* a detector keeps one batch in flight: it sends batch i, starts detecting batch i+1, then collects batch
+  i's classifications — compute and transfer overlap; message order per pair is fixed (header, payload,
+  results) so the pairing can never deadlock;
 * the task record keeps one TaskId across both stages (``stage_transition`` /
   ``TaskStore.retarget_many``): created@detector -> running -> created@classifier
   ("AddPipelineTask") -> running -> completed.
-
-Pairing: with ``world`` ranks, rank 2i (detector) talks to rank 2i+1 (classifier). ``world == 1``
-runs both stages on one GPU with a local hand-off (no RCCL), same code path otherwise.
 """
 from __future__ import annotations
 
@@ -35,6 +33,7 @@ from ..ops.detection import crop_resize_u8
 from ..store import STATE_COMPLETED, STATE_CREATED, STATE_RUNNING
 
 STOP = -1
+_REPLAY_SYNC = os.environ.get("AI4E_GRAPH_REPLAY_SYNC", "1") not in ("0", "off", "")
 
 
 @dataclass
@@ -48,150 +47,11 @@ class PipelineConfig:
     wire_dtype: str = "uint8"
 
 
-def select_crops(dets, cfg: PipelineConfig) -> torch.Tensor:
-    """Padded detections -> [N, 6] (img, x1, y1, x2, y2, score) of confident target-class boxes,
-    grouped by image in score order."""
-    boxes, scores, labels, n = dets
-    B, D = scores.shape
-    rank = torch.arange(D, device=scores.device)[None].expand(B, D)
-    ok = (rank < n[:, None].long()) & (scores > cfg.score_thresh)
-    if cfg.class_id is not None:
-        ok &= labels == cfg.class_id
-    # cap per image (detections are score-sorted)
-    ok &= torch.cumsum(ok.int(), 1) <= cfg.max_crops_per_image
-    img = torch.arange(B, device=scores.device, dtype=torch.float32)[:, None].expand(B, D)
-    sel = torch.cat([img[..., None], boxes.float(), scores.float()[..., None]], -1)[ok]
-    return sel
-
-
 def stage_transition(store, task_ids: Sequence[str], next_endpoint: str, status: str = "running - classifying"):
     """AddPipelineTask analogue: same TaskIds re-targeted at the next stage's endpoint."""
     for t in task_ids:
         store.upsert(t, STATE_CREATED, STATE_CREATED, next_endpoint, None, False)
     store.transition_many(list(task_ids), STATE_RUNNING, status)
-
-
-class DetectClassifyPipeline:
-    def __init__(self, detector: Callable, classifier: Callable[[torch.Tensor], torch.Tensor], device: torch.device,
-                 cfg: Optional[PipelineConfig] = None, group=None):
-        self.detector = detector        # uint8 NHWC images -> padded detections tuple
-        self.classifier = classifier    # uint8 crops [N, h, w, 3] -> logits [N, K]
-        self.device = device
-        self.cfg = cfg or PipelineConfig()
-        self.group = group
-        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
-        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
-        self.is_detector = self.world == 1 or self.rank % 2 == 0
-        self.peer = self.rank + 1 if self.rank % 2 == 0 else self.rank - 1
-        if self.world > 1 and self.peer >= self.world:
-            raise ValueError("pipeline needs an even number of ranks (detector/classifier pairs)")
-        self.wire_dtype = getattr(torch, self.cfg.wire_dtype)
-        self.bytes_sent = 0       # xGMI payload bytes (crops + headers), for the metrics registry
-        self.bytes_received = 0
-        # fault injection (survey §5.3): AI4E_FAULT_INJECTION=xgmi_fail_batch=<k> makes the k-th hand-off of
-        # this detector fail before anything is on the wire (a lost / refused P2P transfer)
-        self._handoffs = 0
-        self._fail_at = 0
-        for item in filter(None, os.environ.get("AI4E_FAULT_INJECTION", "").split(",")):
-            k, _, v = item.partition("=")
-            if k.strip() == "xgmi_fail_batch":
-                self._fail_at = int(v.split("@")[0])
-
-    # ------------------------------------------------------------ classifier stage
-    def classify(self, crops: torch.Tensor) -> torch.Tensor:
-        if crops.shape[0] == 0:
-            return torch.zeros(0, 2, device=self.device)
-        p = torch.softmax(self.classifier(crops).float(), 1)
-        prob, cls = p.max(1)
-        return torch.stack([cls.float(), prob], 1)
-
-    def serve_classifier(self) -> int:
-        """Classifier-rank loop: until the detector sends STOP. Returns #crops classified."""
-        total = 0
-        h, w = self.cfg.crop_hw
-        hdr = torch.zeros(1, dtype=torch.int64, device=self.device)
-        while True:
-            dist.recv(hdr, group_src=self.peer, group=self.group)
-            n = int(hdr.item())
-            if n == STOP:
-                return total
-            crops = torch.empty(n, h, w, 3, dtype=self.wire_dtype, device=self.device)
-            if n:
-                dist.recv(crops, group_src=self.peer, group=self.group)
-                self.bytes_received += crops.numel() * crops.element_size()
-            res = self.classify(self._from_wire(crops))
-            if n:
-                dist.send(res.contiguous(), group_dst=self.peer, group=self.group)
-                self.bytes_sent += res.numel() * res.element_size()
-            total += n
-
-    # ------------------------------------------------------------ detector stage
-    def _to_wire(self, crops_u8: torch.Tensor) -> torch.Tensor:
-        return crops_u8 if self.wire_dtype == torch.uint8 else crops_u8.to(self.wire_dtype)
-
-    def _from_wire(self, crops: torch.Tensor) -> torch.Tensor:
-        return crops if crops.dtype == torch.uint8 else crops.round().clamp(0, 255).to(torch.uint8)
-
-    def _detect_and_crop(self, images: torch.Tensor):
-        dets = self.detector(images)
-        boxes = select_crops(dets, self.cfg)
-        crops = crop_resize_u8(images[..., :3].contiguous() if images.shape[-1] != 3 else images, boxes[:, :5],
-                               self.cfg.crop_hw)
-        return dets, boxes, crops
-
-    def _send(self, crops: torch.Tensor) -> list:
-        """Non-blocking: the detector must be free to post the recv of the previous batch's results
-        while these bytes move, or both sides block in send (rendezvous) and deadlock."""
-        self._handoffs += 1
-        if self._fail_at and self._handoffs == self._fail_at:
-            raise RuntimeError(f"injected xGMI hand-off failure (batch {self._handoffs})")
-        n = torch.tensor([crops.shape[0]], dtype=torch.int64, device=self.device)
-        works = [(dist.isend(n, group_dst=self.peer, group=self.group), n)]
-        self.bytes_sent += 8
-        if crops.shape[0]:
-            c = crops.contiguous()
-            works.append((dist.isend(c, group_dst=self.peer, group=self.group), c))
-            self.bytes_sent += c.numel() * c.element_size()
-        return works
-
-    def _recv_results(self, n: int) -> torch.Tensor:
-        res = torch.empty(n, 2, device=self.device)
-        if n:
-            dist.recv(res, group_src=self.peer, group=self.group)
-            self.bytes_received += res.numel() * res.element_size()
-        return res
-
-    def run_batches(self, batches: Sequence[torch.Tensor]) -> List[Tuple]:
-        """Detector rank: process image batches with one batch in flight. Returns per batch
-        (dets, crop boxes [N,5], classifications [N,2])."""
-        out = []
-        if self.world == 1:
-            for imgs in batches:
-                dets, boxes, crops = self._detect_and_crop(imgs)
-                out.append((dets, boxes, self.classify(crops)))
-            return out
-        pending = None
-        inflight: list = []
-        for imgs in batches:
-            dets, boxes, crops = self._detect_and_crop(imgs)
-            works = self._send(self._to_wire(crops))  # hand batch i to the classifier ...
-            if pending is not None:                 # ... then collect batch i-1 while it works
-                pd, pb = pending
-                out.append((pd, pb, self._recv_results(pb.shape[0])))
-            for w, _ in inflight:                   # batch i-1's sends are done by now
-                w.wait()
-            inflight = works
-            pending = (dets, boxes)
-        if pending is not None:
-            pd, pb = pending
-            out.append((pd, pb, self._recv_results(pb.shape[0])))
-        for w, _ in inflight:
-            w.wait()
-        return out
-
-    def stop(self) -> None:
-        if self.world > 1 and self.is_detector:
-            dist.send(torch.tensor([STOP], dtype=torch.int64, device=self.device), group_dst=self.peer, group=self.group)
 
 
 # ----------------------------------------------------------------------------------------------------------
@@ -206,6 +66,50 @@ def stage_assignment(n_leaders: int, world: int) -> List[List[int]]:
     if n_leaders < 1 or m < 1:
         raise ValueError(f"stage graph needs >= 1 detector and >= 1 classifier rank, got {n_leaders}:{m}")
     return [[d for d in range(n_leaders) if d % m == c] for c in range(m)]
+
+
+def _fault_at() -> int:
+    """AI4E_FAULT_INJECTION=xgmi_fail_batch=<k>: the k-th hand-off of a detector fails before anything is on the
+    wire (a lost / refused P2P transfer; survey §5.3)."""
+    for item in filter(None, os.environ.get("AI4E_FAULT_INJECTION", "").split(",")):
+        k, _, v = item.partition("=")
+        if k.strip() == "xgmi_fail_batch":
+            return int(v.split("@")[0])
+    return 0
+
+
+class _Completion:
+    """Host-visible completion of a posted receive, one test for every backend: RCCL's ``is_completed`` is an event
+    query that advances on its own; gloo completes a receive only inside ``wait`` (which blocks), so there a waiter
+    thread does the wait and sets a flag. The classifier's header loop polls ``done()`` either way."""
+
+    def __init__(self, work, blocking_wait: bool):
+        self.work = work
+        self._ev = None
+        if blocking_wait:
+            import threading
+
+            self._ev = threading.Event()
+            self._err: list = []
+
+            def waiter():
+                try:
+                    work.wait()
+                except Exception as e:  # (surfaced by wait() on the serving thread)
+                    self._err.append(e)
+                self._ev.set()
+            threading.Thread(target=waiter, daemon=True).start()
+
+    def done(self) -> bool:
+        return self._ev.is_set() if self._ev is not None else self.work.is_completed()
+
+    def wait(self) -> None:
+        if self._ev is not None:
+            self._ev.wait()
+            if self._err:
+                raise self._err[0]
+        else:
+            self.work.wait()
 
 
 class _GraphRunner:
@@ -236,10 +140,9 @@ class _GraphRunner:
             torch.cuda.synchronize(self.device)
             g = self.graphs[key] = [graph, static_in, static_out, None]
         graph, static_in, static_out, done = g
-        if done is not None:
-            # the previous replay of THIS graph must have finished before it is launched again: two back-to-back
-            # launches of one graph faulted the GPU twice in bench/stage_rates.py (never with a host sync between
-            # them); the serving loops sync on every batch anyway, so this costs them nothing
+        if done is not None and _REPLAY_SYNC:
+            # round-3 workaround under investigation (bench/replay_repro.py, tests/test_graph_replay_gpu.py): the
+            # previous replay of this graph finished before it is launched again
             done.synchronize()
         static_in.copy_(x)
         graph.replay()
@@ -280,6 +183,7 @@ class StageGraphPipeline:
             self.serves = self.assign[self.rank - n_leaders] if not self.is_detector else []
         self.wire_dtype = getattr(torch, cfg.wire_dtype)
         self.bytes_sent = self.bytes_received = 0
+        self._handoffs, self._fail_at = 0, _fault_at()
         self._det_graph = _GraphRunner(self._detect_crop_compact, device) if self.is_detector else None
         self._cls_graph = _GraphRunner(self._classify_static, device) if classifier is not None else None
 
@@ -302,11 +206,17 @@ class StageGraphPipeline:
         return dets, boxes, scores, valid, packed[: b * m].to(self.wire_dtype), count
 
     def _send(self, crops: torch.Tensor, n: int) -> list:
+        """Non-blocking: the detector must be free to post the receive of the previous batch's results while these
+        bytes move, or both sides block in send (rendezvous) and deadlock. The crops are copied out of the detector
+        graph's static output first (the next batch's replay rewrites it while this send may still be reading)."""
+        self._handoffs += 1
+        if self._fail_at and self._handoffs == self._fail_at:
+            raise RuntimeError(f"injected xGMI hand-off failure (batch {self._handoffs})")
         hdr = torch.tensor([n], dtype=torch.int64, device=self.device)
         works = [(dist.isend(hdr, group_dst=self.peer, group=self.group), hdr)]
         self.bytes_sent += 8
         if n:
-            c = crops[:n].contiguous()
+            c = crops[:n].clone()
             works.append((dist.isend(c, group_dst=self.peer, group=self.group), c))
             self.bytes_sent += c.numel() * c.element_size()
         return works
@@ -366,26 +276,18 @@ class StageGraphPipeline:
         return self._cls_graph(crops)[:n].clone()
 
     def _headers(self):
-        """Yield (detector, n) as headers arrive from the detectors this rank serves. RCCL: one posted ``irecv``
-        per detector, polled with ``is_completed`` (an event query), so an idle detector never blocks a busy
-        one. gloo (CPU tests) only marks a receive complete inside ``wait``, so there one any-source receive
-        is posted instead — the sender's FIFO order keeps the next unmatched message of every peer a header."""
-        alive = set(self.serves)
-        if dist.get_backend(self.group) == "gloo":
-            hdr = torch.zeros(1, dtype=torch.int64, device=self.device)
-            while alive:
-                wk = dist.irecv(hdr, group=self.group)
-                wk.wait()
-                d = wk._source_rank()
-                n = int(hdr.item())
-                if n == STOP:
-                    alive.discard(d)
-                yield d, n
-            return
-        hdrs = {d: torch.zeros(1, dtype=torch.int64, device=self.device) for d in alive}
-        posted = {d: dist.irecv(hdrs[d], group_src=d, group=self.group) for d in alive}
+        """Yield (detector, n) as headers arrive from the detectors this rank serves: one posted ``irecv`` per
+        detector, polled (``_Completion``: an event query on RCCL, a waiter thread on gloo — the same loop on both),
+        so an idle detector never blocks a busy one. A detector's next header is posted only after its crops were
+        received, so every posted receive matches a header."""
+        blocking = dist.get_backend(self.group) == "gloo"
+        hdrs = {d: torch.zeros(1, dtype=torch.int64, device=self.device) for d in self.serves}
+
+        def post(d):
+            return _Completion(dist.irecv(hdrs[d], group_src=d, group=self.group), blocking)
+        posted = {d: post(d) for d in self.serves}
         while posted:
-            ready = [d for d, wk in posted.items() if wk.is_completed()]
+            ready = [d for d, c in posted.items() if c.done()]
             if not ready:
                 time.sleep(0.0002)
                 continue
@@ -394,7 +296,7 @@ class StageGraphPipeline:
                 n = int(hdrs[d].item())
                 yield d, n  # (the crops are received before this detector's next header is posted)
                 if n != STOP:
-                    posted[d] = dist.irecv(hdrs[d], group_src=d, group=self.group)
+                    posted[d] = post(d)
 
     def serve(self) -> int:
         """Classifier rank loop; returns the number of crops classified."""

@@ -14,8 +14,8 @@ Servables for the platform's model families:
   (ResNet-50, the camera-trap crop classifier);
 * :class:`DetectorServable` — Faster-RCNN padded detections -> ``detections`` (boxes, scores, labels);
 * :class:`SegmenterServable` — land-cover U-Net over a tiled mosaic -> class map (+ histogram);
-* :class:`EnsembleServable` — detector -> crop classifier on one GPU (the two-GPU RCCL form is
-  :mod:`runtime.ensemble`).
+* :class:`EnsembleServable` — detector -> crop classifier (one GPU: ``models.zoo.StaticEnsemble``; N:M GPUs over
+  RCCL: :class:`runtime.pipeline.StageGraphPipeline`).
 """
 from __future__ import annotations
 
@@ -189,7 +189,7 @@ class EnsembleServable(Servable):
     kind = "ensemble"
 
     def __init__(self, pipeline, max_crops: int):
-        self.pipeline = pipeline  # runtime.pipeline.DetectClassifyPipeline (world 1)
+        self.pipeline = pipeline  # (subclasses: a StaticEnsemble or a StageGraphPipeline leader)
         self.max_crops = int(max_crops)
         m = self.max_crops
         self.outputs = [OutputField("boxes", "float32", (m, 4)), OutputField("det_scores", "float32", (m,)),
@@ -197,8 +197,7 @@ class EnsembleServable(Servable):
                         OutputField("count", "int32", (1,))]
 
     def __call__(self, images_u8):
-        dets, sel, cls = self.pipeline.run_batches([images_u8])[0]
-        return pack_ensemble(images_u8.shape[0], sel, cls, self.max_crops)
+        raise NotImplementedError  # (boxes, det_scores, species, species_prob, count) per image
 
     @staticmethod
     def format(fields):
@@ -208,32 +207,6 @@ class EnsembleServable(Servable):
                              "species": int(fields["species"][i]),
                              "species_probability": round(float(fields["species_prob"][i]), 4)}
                             for i in range(k)]}
-
-
-def pack_ensemble(b: int, sel: torch.Tensor, cls: torch.Tensor, max_crops: int):
-    """Per-image padded arrays from the pipeline's flat crop list (sel [N,6] img,x1,y1,x2,y2,score;
-    cls [N,2] class,prob); crops are grouped by image in detection-score order."""
-    dev = sel.device
-    boxes = torch.zeros(b, max_crops, 4, device=dev)
-    scores = torch.zeros(b, max_crops, device=dev)
-    species = torch.full((b, max_crops), -1, dtype=torch.int32, device=dev)
-    prob = torch.zeros(b, max_crops, device=dev)
-    count = torch.zeros(b, 1, dtype=torch.int32, device=dev)
-    if sel.shape[0]:
-        img = sel[:, 0].long()
-        # rank of each crop within its image (crops are grouped by image, score-sorted)
-        first = torch.zeros(b + 1, dtype=torch.long, device=dev)
-        first.index_add_(0, img + 1, torch.ones_like(img))
-        start = torch.cumsum(first, 0)[:-1]
-        r = torch.arange(sel.shape[0], device=dev) - start[img]
-        keep = r < max_crops
-        img, r = img[keep], r[keep]
-        boxes[img, r] = sel[keep, 1:5].float()
-        species[img, r] = cls[keep, 0].to(torch.int32)
-        prob[img, r] = cls[keep, 1].float()
-        scores[img, r] = sel[keep, 5].float()
-        count[:, 0] = torch.bincount(img, minlength=b)[:b].to(torch.int32)
-    return boxes, scores, species, prob, count
 
 
 class ResizingServable(Servable):

@@ -40,6 +40,12 @@ class Dist:
             self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
         return [float(v) for v in t.cpu()]
 
+    def sum(self, *vals):
+        t = torch.tensor(vals, dtype=torch.float64, device=self.device if self.dist else "cpu")
+        if self.dist is not None:
+            self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
+        return [float(v) for v in t.cpu()]
+
     def emit(self, record, path=""):
         if self.rank == 0:
             line = json.dumps(record)

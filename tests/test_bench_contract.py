@@ -52,7 +52,7 @@ def test_bench_single_process_cpu():
     _check(lines[0], 1)
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_bench_torchrun_ranks_gloo(world):
     """The driver's multi-GPU launch shape (torchrun, one rank per device; rank 0 = node scheduler, the other
     ranks attach as workers + ingest shards) with gloo on CPU ranks."""

@@ -83,14 +83,15 @@ def test_pipeline_and_spatial_single_gpu():
     from aiforearth_api_platform_amd.models.resnet import FusedResNet, resnet50
     from aiforearth_api_platform_amd.models.unet import FusedUNet, unet_landcover
     from aiforearth_api_platform_amd.ops.stitch import TileGrid
-    from aiforearth_api_platform_amd.runtime.pipeline import DetectClassifyPipeline, PipelineConfig
+    from aiforearth_api_platform_amd.runtime.pipeline import PipelineConfig, StageGraphPipeline
     from aiforearth_api_platform_amd.runtime.spatial import SpatialSegmenter
     det = FasterRCNN(DetectorConfig(box_score_thresh=0.0), seed=0, device=DEV)
     cls = FusedResNet(resnet50(num_classes=20, seed=1), device=DEV)
-    p = DetectClassifyPipeline(det, cls.forward_u8, DEV, PipelineConfig(score_thresh=0.0, class_id=None))
+    p = StageGraphPipeline(det.forward_u8, cls.forward_u8, torch.device(DEV),
+                           PipelineConfig(score_thresh=0.0, class_id=None))
     out = p.run_batches([torch.randint(0, 256, (2, 256, 256, 3), dtype=torch.uint8, device=DEV)])
-    dets, boxes, res = out[0]
-    assert boxes.shape[0] == res.shape[0] > 0 and torch.all((res[:, 0] >= 0) & (res[:, 0] < 20))
+    boxes, scores, valid, res = out[0]
+    assert int(valid.sum()) == res.shape[0] > 0 and torch.all((res[:, 0] >= 0) & (res[:, 0] < 20))
     f = FusedUNet(unet_landcover(seed=0), device=DEV)
     seg = SpatialSegmenter(f.forward_u8, TileGrid(700, 600, 256, 224), 7, DEV, tile_batch=8)
     cls_map = seg.run(torch.randint(0, 256, (700, 600, 4), dtype=torch.uint8))

@@ -1,12 +1,15 @@
-"""Detector -> classifier pipeline over gloo (2 CPU ranks) == local single-process pipeline."""
+"""Detector -> classifier stage graph over gloo (CPU ranks; gloo stands in for RCCL) == the same stages in one
+process: 1:1 (2 ranks) and 3:1 (4 ranks) with several batches per detector (one batch's crops on the wire while
+the next is detected), plus the AddPipelineTask-style task retargeting."""
 import os
 import socket
 
+import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from aiforearth_api_platform_amd.runtime.pipeline import DetectClassifyPipeline, PipelineConfig, select_crops, stage_transition
+from aiforearth_api_platform_amd.runtime.pipeline import PipelineConfig, StageGraphPipeline, stage_transition
 
 CFG = PipelineConfig(crop_hw=(32, 32), score_thresh=0.0, class_id=None, max_crops_per_image=3)
 
@@ -25,53 +28,52 @@ def _stages():
     det = FasterRCNN(DetectorConfig(pre_nms_top_n=100, post_nms_top_n=50, detections_per_img=10,
                                     box_score_thresh=0.0), seed=0)
     cls = FusedResNet(resnet50(num_classes=10, seed=1))
-    return det, cls.forward_u8
+    return det.forward_u8, cls.forward_u8
 
 
-def _batches():
-    g = torch.Generator().manual_seed(0)
+def _batches(rank):
+    g = torch.Generator().manual_seed(100 + rank)
     return [torch.randint(0, 256, (2, 128, 128, 3), dtype=torch.uint8, generator=g) for _ in range(3)]
 
 
-def _worker(rank, port, q):
+def _worker(rank, world, leaders, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=2)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
     det, cls = _stages()
-    p = DetectClassifyPipeline(det, cls, torch.device("cpu"), CFG)
+    p = StageGraphPipeline(det if rank < leaders else None, cls if rank >= leaders else None, torch.device("cpu"), CFG,
+                           n_leaders=leaders)
     if p.is_detector:
-        out = p.run_batches(_batches())
+        out = p.run_batches(_batches(rank))
         p.stop()
-        q.put([(b, r) for _, b, r in out])
+        q.put((rank, [(v, r) for _, _, v, r in out]))
     else:
-        q.put(("classified", p.serve_classifier()))
+        q.put((rank, p.serve()))
     dist.destroy_process_group()
 
 
-def test_pipeline_gloo_matches_local():
+@pytest.mark.parametrize("world,leaders", [(2, 1), (4, 3)])
+def test_stage_graph_gloo_matches_local(world, leaders):
     det, cls = _stages()
-    local = DetectClassifyPipeline(det, cls, torch.device("cpu"), CFG).run_batches(_batches())
+    local = StageGraphPipeline(det, cls, torch.device("cpu"), CFG)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_worker, args=(r, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, leaders, port, q)) for r in range(world)]
     [p.start() for p in procs]
-    got = [q.get(timeout=300) for _ in range(2)]
+    got = dict(q.get(timeout=600) for _ in range(world))
     [p.join(60) for p in procs]
     assert all(p.exitcode == 0 for p in procs)
-    dist_out = next(g for g in got if isinstance(g, list))
-    ncls = next(g for g in got if isinstance(g, tuple))[1]
-    assert ncls == sum(b.shape[0] for b, _ in dist_out) > 0
-    for (lb, lr), (_, b, r) in zip(dist_out, local):
-        assert torch.equal(lb, b)
-        assert torch.allclose(lr, r, atol=1e-4)
+    total = 0
+    for r in range(leaders):
+        ref = local.run_batches(_batches(r))
+        for (v, res), (_, _, lv, lres) in zip(got[r], ref):
+            assert torch.equal(v, lv)
+            assert torch.allclose(res, lres, atol=1e-4)
+            total += res.shape[0]
+    assert sum(got[r] for r in range(leaders, world)) == total > 0
 
 
-def test_select_crops_and_stage_transition():
-    boxes = torch.tensor([[[0, 0, 10, 10.], [5, 5, 20, 20], [1, 1, 2, 2]]])
-    scores = torch.tensor([[0.9, 0.8, 0.7]])
-    labels = torch.tensor([[1, 2, 1]])
-    sel = select_crops((boxes, scores, labels, torch.tensor([2])), PipelineConfig(score_thresh=0.5))
-    assert [round(v, 4) for v in sel[0].tolist()] == [0, 0, 0, 10, 10, 0.9] and sel.shape == (1, 6)
+def test_stage_transition():
     from aiforearth_api_platform_amd.store import make_store
     s = make_store()
     ids = s.create_many("http://h/v1/ct/detect", 2)

@@ -93,24 +93,25 @@ def test_ensemble_pair_recovers_from_failed_xgmi_handoff(monkeypatch):
     assert all(g is not None and "animals" in g for g in got)
 
 
-@pytest.mark.parametrize("leaders", [3, 2])
-def test_stage_graph_3_to_1_matches_single_process(leaders):
-    """Config 5 as an N:M stage graph: 3 detector leaders (each its own scheduler connection and batches) feed
-    1 classifier process over P2P — and 2:2, each classifier serving its own detector; every task equals the
-    single-process ensemble."""
+@pytest.mark.parametrize("world,leaders", [(4, 3), (4, 2), (8, 7), (8, 6)])
+def test_stage_graph_matches_single_process(world, leaders):
+    """Config 5 as an N:M stage graph through the pool: 3:1 and 7:1 (detector leaders, each its own scheduler
+    connection and batches, feeding one classifier process over P2P), 2:2 and 6:2 (detectors d % 2 per
+    classifier); every task equals the single-process ensemble."""
     from aiforearth_api_platform_amd.models import zoo
     from aiforearth_api_platform_amd.runtime.servable import decode_row, encode_rows
 
-    imgs = np.random.default_rng(11).integers(0, 256, (9, 128, 128, 3), dtype=np.uint8)
+    n = 9 if world == 4 else 14
+    imgs = np.random.default_rng(11).integers(0, 256, (n, 128, 128, 3), dtype=np.uint8)
     spec = ModelSpec("aiforearth_api_platform_amd.models.zoo:camera_trap_ensemble_group", (128, 128, 3), 2, 5, ENS,
-                     False, (), ("http://127.0.0.1/v1/group/classify",), 4, leaders)
-    got, stats = _serve(spec, ["cpu"] * 4, imgs, "/v1/group/classify")
-    assert len(stats["workers"]) == leaders and sum(w["images"] for w in stats["workers"]) == 9
+                     False, (), ("http://127.0.0.1/v1/group/classify",), world, leaders)
+    got, stats = _serve(spec, ["cpu"] * world, imgs, "/v1/group/classify")
+    assert len(stats["workers"]) == leaders and sum(w["images"] for w in stats["workers"]) == n
     local = zoo.camera_trap_ensemble("cpu", **ENS)
     outs = [o.numpy() for o in local(torch.from_numpy(imgs))]
     rb = sum(f.nbytes for f in local.outputs)
-    rows = encode_rows(outs, 9)
-    for i in range(9):
+    rows = encode_rows(outs, n)
+    for i in range(n):
         ref = local.format(decode_row(rows[i * rb:(i + 1) * rb], local.outputs))
         assert [a["species"] for a in got[i]["animals"]] == [a["species"] for a in ref["animals"]]
         assert [a["bbox"] for a in got[i]["animals"]] == [a["bbox"] for a in ref["animals"]]
