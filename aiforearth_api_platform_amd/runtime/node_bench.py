@@ -1,13 +1,23 @@
 """Node serving benchmark harness (library): drives an endpoint through the production path.
 
 Used by ``bench.py`` (the headline ResNet-50 API) and ``bench/api_bench.py`` (detector, land-cover,
-ensemble): ONE node scheduler (native task store + dispatch queue + NodeScheduler) and ONE GPU
-worker process per GPU. N = 1: the calling process is the scheduler and spawns the worker for
-cuda:0. N > 1 (torchrun, one rank per GPU): rank 0 is the scheduler (+ spawns the worker for its
-GPU); ranks 1..N-1 connect to it over TCP and are the GPU workers of their devices. Every rank is
-also an ingest shard owning a partition of the shared payload ring: its clients write their
-payloads into the ring inside the timed region and enqueue them (weak scaling: --batch items per
-step per GPU). torch.distributed (RCCL) brackets the timed region and takes the MAX of the timings.
+ensemble): a node scheduler (native task store + dispatch queue + NodeScheduler) and ONE GPU worker
+process per GPU. N = 1: the calling process is the scheduler and spawns the worker for cuda:0.
+
+N > 1 (torchrun, one rank per GPU), two control-plane layouts:
+
+* ``sharded`` (default; AI4E_BENCH_CP=sharded): every rank is the node scheduler of its own GPU — its own task
+  store shard, dispatch queue, payload ring and spawned worker process, its own clients — the reference's replica
+  DP (HPA replicas behind Istio's ROUND_ROBIN, ``APIs/Charts/templates/async-gpu/autoscaler.yaml``) with the
+  control plane scaling with the GPUs instead of serializing through one process (the reference's single
+  dispatch point, ``ProcessManager/BackendQueueProcessor/host.json:3-11``). The window is the UNION of the
+  ranks' steady-state windows (earliest start to latest end on the host's monotonic clock), so the whole-node
+  rate is a lower bound;
+* ``central`` (AI4E_BENCH_CP=central): rank 0 is the one scheduler (+ spawns the worker for its GPU); ranks
+  1..N-1 connect to it over TCP as the GPU workers of their devices and ingest shards of a shared ring.
+
+Clients write their payloads into the ring inside the timed region and enqueue them (weak scaling: --batch items
+per step per GPU). torch.distributed (RCCL) brackets the timed region and reduces the timings.
 """
 from __future__ import annotations
 
@@ -199,15 +209,18 @@ def run_node_bench(args, spec, path: str, metric: str, unit: str = "images/s", c
     # rank 0 builds the in-tree HIP/C++ libraries, then everyone joins (RCCL on GPU, gloo on CPU)
     denv = init_from_env(args.device, build=_build.build_all)
     rank, device = denv.rank, denv.device
+    sharded = world > 1 and group == 1 and os.environ.get("AI4E_BENCH_CP", "sharded") != "central"
     B = args.batch
     part = B * (args.inflight + 1)  # ring slots per ingest shard
     hb = 0.5
-    total_images = (args.warmup + args.steps) * B * world
+    # completions this rank's scheduler counts: the whole node's (central) or its own shard's (sharded)
+    counted_world = 1 if sharded else world
+    total_images = (args.warmup + args.steps) * B * counted_world
 
-    if rank == 0:
+    if rank == 0 or sharded:
         cfg = Config.load(env={}, max_batch=B, max_batch_delay_ms=0.0)
         cp = ControlPlane(cfg)
-        remote = [(part * r, part, r) for r in range(1, world)]
+        remote = [] if sharded else [(part * r, part, r) for r in range(1, world)]
         if group > 1:
             devices = [f"cuda:{i}" for i in range(group)] if args.device == "cuda" else ["cpu"] * group
         else:
@@ -219,7 +232,7 @@ def run_node_bench(args, spec, path: str, metric: str, unit: str = "images/s", c
                           frontend_slots=3 * B)  # (REST phase only: keep the pinned ring small)
         info = None
         listener = None
-        if world > 1:
+        if world > 1 and not sharded:
             import secrets
             from multiprocessing.connection import Listener
 
@@ -229,7 +242,7 @@ def run_node_bench(args, spec, path: str, metric: str, unit: str = "images/s", c
             listener = Listener(("127.0.0.1", 0), authkey=key, backlog=max(1, world))
             info = {"shm": pool.ring.name, "nslots": pool.ring.nslots, "addr": listener.address, "key": key.hex()}
         objs = [info]
-        if world > 1:
+        if world > 1 and not sharded:
             import torch.distributed as dist
 
             dist.broadcast_object_list(objs, src=0)
@@ -243,7 +256,7 @@ def run_node_bench(args, spec, path: str, metric: str, unit: str = "images/s", c
             acc = threading.Thread(target=accept, daemon=True)
             acc.start()
         pool.start(wait_ready_s=900)
-        if world > 1:
+        if world > 1 and not sharded:
             acc.join(900)
             pool.wait_ready(900)
         client = Client(pool.ring.buf, lambda n: pool.ring.alloc(n, timeout=600), pool.submit_slots, B, rank)
@@ -291,7 +304,7 @@ def run_node_bench(args, spec, path: str, metric: str, unit: str = "images/s", c
     # The tail keeps the pipeline full up to t1 (its images are served, not counted). The barrier +
     # device drain bracket the whole run on every rank.
     tail = max(1, args.inflight + 1)
-    warm_n = args.warmup * B * world
+    warm_n = args.warmup * B * counted_world
     sync(denv)
     tune_gc()
     tel = None
@@ -305,7 +318,7 @@ def run_node_bench(args, spec, path: str, metric: str, unit: str = "images/s", c
     cth.start()
     dt, ramp_s, drain_s = 0.0, 0.0, 0.0
     tm0 = tm1 = time.monotonic()
-    if rank == 0:
+    if rank == 0 or sharded:
         if warm_n:  # (no warmup: the window starts at the first submission, fill included)
             wait_images(warm_n)
             t0, tm0 = time.perf_counter(), time.monotonic()
@@ -314,20 +327,36 @@ def run_node_bench(args, spec, path: str, metric: str, unit: str = "images/s", c
         wait_images(total_images)
         t1, tm1 = time.perf_counter(), time.monotonic()
         dt, ramp_s = t1 - t0, t0 - t_start
-        wait_images(total_images + tail * B * world)
+        wait_images(total_images + tail * B * counted_world)
         drain_s = time.perf_counter() - t1
     cth.join()
     sync(denv)
     telemetry = tel.stop() if tel is not None else {}
     p50 = p99 = 0.0
     stats = {}
-    if rank == 0:
+    lat = []
+    if rank == 0 or sharded:
         from ..store.pystore import absolute_path
 
         lat = sorted(x for pth in [path] + [absolute_path(e) for e in spec.stage_endpoints]
                      for x in cp.store.latencies_window(pth, tm0, tm1))  # ensembles finish at the last stage
         p50, p99 = percentile(lat, 50) * 1e3, percentile(lat, 99) * 1e3
         stats = pool.stats()
+    if sharded:
+        # the union of the ranks' windows (monotonic clock, one host): every counted image completed inside it
+        from ..parallel.dist import gather_objects
+
+        per = gather_objects({"tm0": tm0, "tm1": tm1, "lat": lat, "ramp": ramp_s, "drain": drain_s,
+                              "stats": stats}, denv)
+        dt = max(r["tm1"] for r in per) - min(r["tm0"] for r in per)
+        ramp_s, drain_s = max(r["ramp"] for r in per), max(r["drain"] for r in per)
+        lat = sorted(x for r in per for x in r["lat"])
+        p50, p99 = percentile(lat, 50) * 1e3, percentile(lat, 99) * 1e3
+        if rank == 0:
+            stats = dict(per[0]["stats"])
+            stats["workers"] = [dict(w, rank=i) for i, r in enumerate(per) for w in r["stats"].get("workers", [])]
+            hists = [r["stats"].get("batch_histogram") or [] for r in per]
+            stats["batch_histogram"] = [sum(h[i] for h in hists if i < len(h)) for i in range(max(map(len, hists)))]
     dt, p50, p99 = all_reduce_max([dt, p50, p99], denv)  # slowest rank defines the step time
     images = args.steps * B * world
     value = images / dt
@@ -358,7 +387,9 @@ def run_node_bench(args, spec, path: str, metric: str, unit: str = "images/s", c
                        "tail_steps_uncounted": tail},
             "config": dict(config or {}, global_batch=B * world, per_gpu_batch=B,
                            parallelism=(config or {}).get("parallelism", f"dp{world}"),
-                           serving_path="node scheduler (native) + 1 GPU worker process per GPU",
+                           serving_path=("one node scheduler (native) + GPU worker process per GPU, sharded by GPU"
+                                         if sharded else "node scheduler (native) + 1 GPU worker process per GPU"),
+                           control_plane="sharded" if sharded else "central",
                            ingest_shards=world, ring_slots_per_shard=part, hip_graphs=spec.use_graphs),
             "workers": workers, "batch_histogram": stats.get("batch_histogram"), "http": http,
         }
@@ -372,7 +403,7 @@ def run_node_bench(args, spec, path: str, metric: str, unit: str = "images/s", c
             with open(args.json_out, "w") as f:
                 f.write(line + "\n")
     sync(denv)
-    if rank == 0:
+    if rank == 0 or sharded:
         pool.stop()
         cp.close()
     else:

@@ -47,14 +47,90 @@ def fake_worker(conn, rank: int, row_bytes: int):
             return
 
 
+def fake_rank(conn, rank: int, row_bytes: int, batch: int, base: int, part: int, stop_at: float):
+    """A torchrun rank of the multi-GPU bench without the GPU: its ingest partition [base, base + part) submitted
+    over its own scheduler connection (SUBMIT frames of `batch` slots), BATCHes answered with DONE at once, FREE
+    frames returned to the partition — the per-task traffic rank 0's scheduler sees from 7 remote GPUs."""
+    import numpy as np
+
+    from aiforearth_api_platform_amd.runtime import protocol as P
+    from aiforearth_api_platform_amd.store import native
+
+    fc = P.FrameConn(conn)
+    ring = native.SlotRing(part, base)
+    fc.ready(rank, False, {"kind": "classifier", "outputs": [["classes", "int32", [5]], ["probabilities", "float32",
+                                                                                         [5]]]})
+    zeros = bytes(row_bytes * 1024)
+
+    def submitter():
+        while time.time() < stop_at:
+            s = ring.alloc(batch, 0.5)
+            if s:
+                fc.submit(s)
+
+    th = threading.Thread(target=submitter, daemon=True)
+    th.start()
+    while True:
+        try:
+            buf = fc.recv()
+        except (EOFError, OSError):
+            return
+        t = P.frame_type(buf)
+        if t == P.F_BATCH:
+            bid, slots = P.parse_batch(buf)
+            n = slots.shape[0]
+            now = time.monotonic()
+            fc.done(bid, np.zeros(n, np.uint8), zeros[: n * row_bytes], row_bytes, (now, now, now, 0.0, 0.0))
+        elif t == P.F_FREE:
+            ring.free(P.parse_slots(buf).tolist())
+        elif t == P.F_STOP:
+            return
+
+
+def _shard(args, barrier, out_q):
+    """One control-plane shard (the sharded multi-GPU bench: one node scheduler per GPU) in its own process."""
+    import argparse as _a
+
+    a = _a.Namespace(**args)
+    barrier.wait()
+    out_q.put(run(a))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--workers", type=int, default=8)
     ap.add_argument("--batch", type=int, default=250)
     ap.add_argument("--seconds", type=float, default=5.0)
     ap.add_argument("--ingest-threads", type=int, default=4)
+    ap.add_argument("--remote", action="store_true",
+                    help="every worker is a separate rank process that also submits its own tasks (torchrun topology)")
+    ap.add_argument("--shards", type=int, default=0,
+                    help="K independent scheduler processes (one per GPU, the sharded bench layout), "
+                         "--workers fake workers each; the value is their sum")
     ap.add_argument("--json-out", default="")
     a = ap.parse_args()
+    if a.shards:
+        ctx = mp.get_context("spawn")
+        bar, q = ctx.Barrier(a.shards), ctx.Queue()
+        kw = dict(vars(a), shards=0, json_out="")
+        ps = [ctx.Process(target=_shard, args=(kw, bar, q)) for _ in range(a.shards)]
+        [p.start() for p in ps]
+        res = [q.get(timeout=600) for _ in ps]
+        [p.join(60) for p in ps]
+        out = {"metric": res[0]["metric"], "value": sum(r["value"] for r in res), "unit": "tasks/s",
+               "shards": a.shards, "per_shard": [r["value"] for r in res], "workers_per_shard": a.workers,
+               "batch": a.batch, "ingest": res[0]["ingest"], "seconds": a.seconds,
+               "p50_task_latency_ms": max(r["p50_task_latency_ms"] or 0 for r in res), "cpu_count": os.cpu_count()}
+    else:
+        out = run(a)
+    line = json.dumps(out)
+    print(line)
+    if a.json_out:
+        with open(a.json_out, "w") as f:
+            f.write(line + "\n")
+
+
+def run(a) -> dict:
     from aiforearth_api_platform_amd.config import Config
     from aiforearth_api_platform_amd.gateway.control import ControlPlane
     from aiforearth_api_platform_amd.store import native
@@ -68,19 +144,35 @@ def main():
     nslots = per_thread * a.ingest_threads
     sched = native.NodeScheduler(cp.store, q, "http://127.0.0.1" + path, nslots, max_batch=B, linger_s=0.0005,
                                  depth=2, hb_timeout_s=60.0, poll_s=0.005)
-    rings = [native.SlotRing(per_thread, i * per_thread) for i in range(a.ingest_threads)]
-    for r in rings:
-        sched.add_local_ring(r)
     ctx = mp.get_context("spawn")
     procs = []
-    for r in range(a.workers):
-        parent, child = ctx.Pipe()
-        p = ctx.Process(target=fake_worker, args=(child, r, 40), daemon=True)
-        p.start()
-        child.close()
-        sched.attach(r, os.dup(parent.fileno()), True)
-        parent.close()
-        procs.append(p)
+    rings = []
+    if a.remote:
+        part = B * int(os.environ.get("CP_PART_BATCHES", "16"))
+        sched = native.NodeScheduler(cp.store, q, "http://127.0.0.1" + path, part * a.workers, max_batch=B,
+                                     linger_s=0.0005, depth=2, hb_timeout_s=60.0, poll_s=0.005)
+        stop_at = time.time() + 1.0 + a.seconds + 30.0
+        for r in range(a.workers):
+            sched.add_remote_partition(r * part, part, r)
+            parent, child = ctx.Pipe()
+            p = ctx.Process(target=fake_rank, args=(child, r, 40, B, r * part, part, stop_at), daemon=True)
+            p.start()
+            child.close()
+            sched.attach(r, os.dup(parent.fileno()), True)
+            parent.close()
+            procs.append(p)
+    else:
+        rings = [native.SlotRing(per_thread, i * per_thread) for i in range(a.ingest_threads)]
+        for r in rings:
+            sched.add_local_ring(r)
+        for r in range(a.workers):
+            parent, child = ctx.Pipe()
+            p = ctx.Process(target=fake_worker, args=(child, r, 40), daemon=True)
+            p.start()
+            child.close()
+            sched.attach(r, os.dup(parent.fileno()), True)
+            parent.close()
+            procs.append(p)
     while sum(1 for w in sched.worker_stats() if w["ready"]) < a.workers:
         time.sleep(0.01)
     stop = threading.Event()
@@ -113,19 +205,18 @@ def main():
     evict_stop.set()
     rate = (n1 - n0) / (t1 - t0)
     out = {"metric": "control-plane tasks/s (create + dispatch + complete + result attach), no model",
-           "value": round(rate), "unit": "tasks/s", "workers": a.workers, "batch": B, "ingest_threads": a.ingest_threads,
+           "value": round(rate), "unit": "tasks/s", "workers": a.workers, "batch": B,
+           "ingest": "remote ranks (SUBMIT frames)" if a.remote else f"{a.ingest_threads} local Python threads",
            "seconds": a.seconds, "p50_task_latency_ms": round(percentile(lat, 50) * 1e3, 3) if lat else None,
            "store_size_end": cp.store.size(), "cpu_count": os.cpu_count(),
            "batch_histogram": sched.batch_histogram()}
     sched.stop()
     for p in procs:
         p.join(5)
+        if p.is_alive():
+            p.terminate()
     cp.close()
-    line = json.dumps(out)
-    print(line)
-    if a.json_out:
-        with open(a.json_out, "w") as f:
-            f.write(line + "\n")
+    return out
 
 
 if __name__ == "__main__":
