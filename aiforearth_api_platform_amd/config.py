@@ -47,6 +47,9 @@ class Config:
     service_container_version: str = field(default="", metadata={"env": "SERVICE_CONTAINER_VERSION"})
     next_api_name_in_pipeline: str = field(default="", metadata={"env": "NEXT_API_NAME_IN_PIPELINE"})
     debug: bool = field(default=False, metadata={"env": "DEBUG"})
+    # adaptive telemetry sampling of the structured logs (App Insights samplingSettings.maxTelemetryItemsPerSecond = 50,
+    # ProcessManager/CacheManager/host.json:3-9): the emitted rate is held near this many items/s; 0 = keep everything
+    telemetry_max_per_s: float = field(default=50.0, metadata={"env": "AI4E_TELEMETRY_MAX_PER_S"})
     # --- transport / dispatcher (setup_env.sh:65-74, BackendQueueProcessor/host.json) ---
     transport: str = field(default="inproc", metadata={"env": "AI4E_TRANSPORT"})  # inproc|queue|eventgrid
     queue_retry_delay_ms: int = field(default=60000, metadata={"env": "QUEUE_RETRY_DELAY_MS"})

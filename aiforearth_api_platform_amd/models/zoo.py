@@ -235,9 +235,10 @@ def landcover_spatial(device="cuda", group=None, role: str = "leader", height: i
 
     from ..parallel.dist import broadcast_tensors
 
-    f = FusedUNet(unet_landcover(n_classes=n_classes, seed=seed), device=device)
-    # weights are the leader's: loaded once there, replicated over the group's links in one bucketed
-    # broadcast per dtype (survey C1) instead of every GPU loading its own copy
+    # weights are the leader's: loaded (here: seeded) once there, replicated over the group's links in one bucketed
+    # broadcast per dtype (survey C1). Followers start from DIFFERENT weights, so the group's outputs equal the
+    # single-GPU model only because of that broadcast (tests/test_worker_groups.py checks the equality)
+    f = FusedUNet(unet_landcover(n_classes=n_classes, seed=seed if role == "leader" else seed + 7919), device=device)
     broadcast_tensors(f.tensors(), src=0, group=group)
     seg = SpatialSegmenter(f.forward_u8, TileGrid(height, width, tile, stride), f.n_classes, torch.device(device),
                            tile_batch=tile_batch, group=group, tile_graphs=True)

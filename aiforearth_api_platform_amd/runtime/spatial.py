@@ -118,11 +118,15 @@ class SpatialSegmenter:
     def _infer(self, tiles: torch.Tensor) -> torch.Tensor:
         """tiles [n, ts, ts, c] uint8 -> logits [n, ts, ts, n_out]."""
         flat = tiles.contiguous()
-        if self._graphed:  # a graph's output buffer is reused by its next replay: copy each batch out first
-            return torch.cat([self.model_fn(flat[i:i + self.tile_batch])[..., : self.n_out].clone()
-                              for i in range(0, flat.shape[0], self.tile_batch)])
-        outs = [self.model_fn(flat[i:i + self.tile_batch]) for i in range(0, flat.shape[0], self.tile_batch)]
-        return torch.cat(outs)[..., : self.n_out].contiguous()
+        out = None
+        for i in range(0, flat.shape[0], self.tile_batch):
+            # each batch's logits go straight into one preallocated buffer (a graph's output buffer is reused by
+            # its next replay; one copy per batch instead of a clone plus a concatenation)
+            y = self.model_fn(flat[i:i + self.tile_batch])[..., : self.n_out]
+            if out is None:
+                out = torch.empty(flat.shape[0], *y.shape[1:], dtype=y.dtype, device=y.device)
+            out[i:i + y.shape[0]].copy_(y)
+        return out
 
     def run(self, mosaic: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
         """mosaic [H, W, C] uint8 on rank 0 (ignored elsewhere). Returns the class map on rank 0."""

@@ -10,12 +10,74 @@ from __future__ import annotations
 import json
 import logging
 import sys
+import threading
 import time
 import traceback
+import zlib
 from typing import Any, Optional
 
 from ..config import get_config
 from .tracing import Tracer, get_tracer
+
+
+class TelemetrySampler:
+    """Adaptive sampling of telemetry items, as Application Insights does for the reference's Function apps
+    (``samplingSettings: {isEnabled, maxTelemetryItemsPerSecond: 50}``, ``ProcessManager/CacheManager/host.json:3-9``)
+    and its Istio adapter (adaptive sampling limit, ``application-insights-istio-mixer-adapter-deployment.yaml:36``):
+
+    * the sampling ratio is re-estimated every ``interval_s`` from the offered rate of the previous interval,
+      ``ratio = min(1, max_per_s / offered_per_s)``, so the emitted rate tracks ``max_per_s`` at any load;
+    * items of one task are kept or dropped together (the decision hashes the task id against the ratio, App
+      Insights' per-operation sampling), so a kept task's log lines stay complete; items without a task id are
+      sampled by a deterministic counter;
+    * within an interval at most twice the interval's budget is kept (a sudden burst is cut before the next
+      re-estimate; the one place a task can lose some of its lines);
+    * ERROR items are always kept (rare, and the ones an operator needs; a deviation from App Insights, which would
+      sample exceptions too) but count toward the offered rate;
+    * every emitted item carries ``sample_rate`` = 1 / ratio (App Insights' itemCount) so counts can be re-weighted.
+    """
+
+    def __init__(self, max_per_s: float = 50.0, interval_s: float = 1.0, clock=time.monotonic):
+        self.max_per_s, self.interval_s, self.clock = float(max_per_s), float(interval_s), clock
+        self.ratio = 1.0
+        self.seen = self.kept = 0
+        self._t0 = clock()
+        self._n = 0          # items offered in the current interval
+        self._k = 0          # items kept in the current interval
+        self._untagged = 0.0
+        self._mu = threading.Lock()
+
+    def _roll(self, now: float) -> None:
+        dt = now - self._t0
+        if dt < self.interval_s:
+            return
+        offered = self._n / dt
+        self.ratio = 1.0 if offered <= self.max_per_s else self.max_per_s / offered
+        self._t0, self._n, self._k = now, 0, 0
+
+    def keep(self, task_id: str = "", always: bool = False) -> bool:
+        if self.max_per_s <= 0:
+            return True
+        with self._mu:
+            self._roll(self.clock())
+            self._n += 1
+            self.seen += 1
+            if always:
+                ok = True
+            elif self._k >= 2.0 * self.max_per_s * self.interval_s:
+                ok = False
+            elif self.ratio >= 1.0:
+                ok = True
+            elif task_id:
+                ok = (zlib.crc32(task_id.encode()) & 0xFFFFFFFF) < self.ratio * 4294967296.0
+            else:
+                self._untagged += self.ratio
+                ok = self._untagged >= 1.0
+                if ok:
+                    self._untagged -= 1.0
+            self.kept += ok
+            self._k += ok
+            return ok
 
 
 class AI4ELogger:
@@ -36,10 +98,15 @@ class AI4ELogger:
         self.tracer = tracer if tracer is not None else get_tracer()
         self.records = []  # last N records kept for /v1/platform/logs and tests
         self._keep = 1000
+        self.sampler = TelemetrySampler(getattr(cfg, "telemetry_max_per_s", 50.0))
 
     def _emit(self, level: str, msg: str, uri: str = "", task_id: str = "", **extra: Any) -> None:
+        if not self.sampler.keep(task_id, always=level in ("ERROR", "CRITICAL")):
+            return
         rec = {"ts": time.time(), "level": level, "message": msg, **self.fields, "uri": uri,
                "task_id": task_id, **extra}
+        if self.sampler.ratio < 1.0:
+            rec["sample_rate"] = round(1.0 / self.sampler.ratio, 3)
         self.records.append(rec)
         if len(self.records) > self._keep:
             del self.records[: len(self.records) - self._keep]

@@ -142,3 +142,33 @@ def test_webhook_validation_and_retry(backend):
     assert json.loads(cp.get(t2["TaskId"])[1])["BackendStatus"] == "failed"
     code, _ = wh2.handle_event({"Id": "x", "Subject": "http://h/v1/push", "Data": {"a": 1}, "EventType": "task"})
     assert code == 503
+
+
+def test_telemetry_sampler_holds_the_rate_and_keeps_tasks_whole():
+    """App Insights-style adaptive sampling (maxTelemetryItemsPerSecond = 50, the reference's host.json): at 2000
+    offered items/s the emitted rate settles near 50/s, a task's items are kept or dropped together, errors always
+    pass, and emitted records carry the re-weighting factor."""
+    import io
+
+    from aiforearth_api_platform_amd.utils.logging import AI4ELogger, TelemetrySampler
+
+    now = [0.0]
+    s = TelemetrySampler(50.0, clock=lambda: now[0])
+    kept_by_task = {}
+    for i in range(20000):  # 10 s at 2000 items/s, 4 items per task
+        now[0] = i / 2000.0
+        t = f"task-{i // 4}"
+        kept_by_task.setdefault(t, set()).add(s.keep(t))
+    assert all(len(v) == 1 for v in kept_by_task.values())  # whole tasks
+    late = sum(1 for t, v in kept_by_task.items() if int(t.split("-")[1]) >= 1000 and True in v) * 4
+    assert 30 * 7.5 < late < 70 * 7.5, late  # last 7.5 s: ~50 items/s
+    assert s.keep("", always=True) and 0.02 < s.ratio < 0.04
+    log = AI4ELogger(stream=io.StringIO())
+    log.sampler = TelemetrySampler(5.0, clock=lambda: now[0])
+    for i in range(4000):
+        now[0] = 100 + i / 1000.0
+        log.log_info("x", task_id=f"t{i}")
+    log.log_error("boom", task_id="t-err")
+    assert 10 < len(log.records) < 40 and log.records[-1]["message"] == "boom"
+    assert any(r.get("sample_rate", 1) > 100 for r in log.records)
+    assert TelemetrySampler(0).keep("any")
