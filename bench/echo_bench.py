@@ -7,7 +7,14 @@
 Each server runs in its own process (its own GIL, like a deployed service); the asyncio HTTP client
 drives it at fixed concurrency from this process and reports req/s and p50/p99 latency.
 
-    python bench/echo_bench.py [--requests 5000 --concurrency 64]
+The client is the measuring instrument, so its own host stalls must stay out of the numbers: it opens all
+``--concurrency`` connections with an untimed warm-up wave first, and runs with its garbage collector frozen
+(as the servers do, runtime/hostperf.py). Round 3's p99 of 160 ms (5000 requests) was one generation-2 GC pause of
+the client (25-35 ms here, longer on the GPU box) stalling all 64 in-flight requests at once — 64 of 5000 requests
+is more than the top 1 % — plus the connection-opening first wave; at 8000 requests (round 2) the same stall fell
+just outside p99 (16 ms).
+
+    python bench/echo_bench.py [--requests 20000 --concurrency 64]
 """
 import argparse
 import asyncio
@@ -63,7 +70,9 @@ def start_reference(port):
     app.run("127.0.0.1", port, threaded=True)
 
 
-async def drive(url, n, conc):
+async def drive(url, n, conc, warm: int = 0):
+    import gc
+
     import aiohttp
 
     lat = []
@@ -78,24 +87,34 @@ async def drive(url, n, conc):
                 await asyncio.sleep(0.05)
         sem = asyncio.Semaphore(conc)
 
-        async def one():
+        async def one(timed=True):
             async with sem:
                 t = time.perf_counter()
                 async with s.post(url, data=payload, headers={"Content-Type": "application/json"}) as r:
                     assert r.status == 200, r.status
                     await r.read()
-                lat.append(time.perf_counter() - t)
+                if timed:
+                    lat.append(time.perf_counter() - t)
 
-        t0 = time.perf_counter()
-        await asyncio.gather(*[one() for _ in range(n)])
-        dt = time.perf_counter() - t0
+        # untimed warm-up: every connection of the pool opened, both sides' first-use paths taken
+        await asyncio.gather(*[one(False) for _ in range(warm or 4 * conc)])
+        gc.collect()
+        gc.freeze()  # the client's own generation-2 pauses would stall every in-flight request at once
+        gc.disable()
+        try:
+            t0 = time.perf_counter()
+            await asyncio.gather(*[one() for _ in range(n)])
+            dt = time.perf_counter() - t0
+        finally:
+            gc.enable()
+            gc.unfreeze()
     lat.sort()
     return n / dt, lat[len(lat) // 2] * 1e3, lat[int(len(lat) * 0.99)] * 1e3
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--requests", type=int, default=5000)
+    ap.add_argument("--requests", type=int, default=20000)
     ap.add_argument("--concurrency", type=int, default=64)
     ap.add_argument("--json-out", default="")
     a = ap.parse_args()
