@@ -112,6 +112,25 @@ class _Completion:
             self.work.wait()
 
 
+def plan_ensemble(gpus: int, det_images_per_s: float, cls_crops_per_s: float, crops_per_image: float,
+                  colocated_images_per_s: Optional[float] = None) -> dict:
+    """Placement of config 5 on ``gpus`` GPUs from measured stage rates (bench/stage_rates.py): every N:M stage
+    graph (N detector GPUs, M = gpus - N classifier GPUs; node rate = min(N x detector rate, M x classifier rate /
+    crops per image)) against the colocated form (both stages on every GPU, DP; per GPU 1 / (1/det + c/cls), or
+    the measured colocated rate). Returns the fastest as {"form": "stage" | "colocated", "leaders", "classifiers",
+    "images_per_s"} plus every candidate's estimate."""
+    c = max(float(crops_per_image), 1e-9)
+    cands = []
+    for n in range(1, gpus):
+        m = gpus - n
+        cands.append({"form": "stage", "leaders": n, "classifiers": m,
+                      "images_per_s": min(n * det_images_per_s, m * cls_crops_per_s / c)})
+    per_gpu = colocated_images_per_s or 1.0 / (1.0 / det_images_per_s + c / cls_crops_per_s)
+    cands.append({"form": "colocated", "leaders": gpus, "classifiers": 0, "images_per_s": gpus * per_gpu})
+    best = max(cands, key=lambda x: x["images_per_s"])
+    return dict(best, candidates=cands)
+
+
 class _GraphRunner:
     """One static-shape callable captured per input size in HIP graphs (CUDA graphs on ROCm); eager on CPU."""
 

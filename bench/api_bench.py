@@ -58,7 +58,11 @@ def main():
     ap.add_argument("--http-seconds", type=float, default=6.0)
     ap.add_argument("--json-out", default="")
     ap.add_argument("--group", type=int, default=2, help="GPUs per worker group (ensemble_group, landcover_spatial)")
-    ap.add_argument("--classifiers", type=int, default=1, help="classifier GPUs of an ensemble_group")
+    ap.add_argument("--classifiers", type=int, default=1,
+                    help="classifier GPUs of an ensemble_group; 0 = the split runtime/pipeline.py plan_ensemble picks "
+                         "from the measured stage rates (--stage-rates) at --crops-per-image")
+    ap.add_argument("--stage-rates", default=os.path.join(ROOT, "profiles", "r4_stage_rates", "stage_rates.json"))
+    ap.add_argument("--crops-per-image", type=float, default=4.0)
     ap.add_argument("--classifier-dtype", default="fp16", choices=["bf16", "fp16"])
     ap.add_argument("--wire", default="uint8", choices=["uint8", "float16"])
     ap.add_argument("--tile", type=int, default=512)
@@ -82,6 +86,21 @@ def main():
         kwargs = {"max_crops": 4, "score_thresh": 0.0, "class_id": None}  # random weights: keep crops flowing
         stages = ("http://127.0.0.1" + path.replace("/detect", "/classify"),)
     if a.model == "ensemble_group":
+        if a.classifiers == 0:  # placement from the measured stage rates
+            import json
+
+            from aiforearth_api_platform_amd.runtime.pipeline import plan_ensemble
+
+            with open(a.stage_rates) as f:
+                r = json.load(f)
+            plan = plan_ensemble(a.group, r["detector_stage"]["images_per_s"],
+                                 r[f"classifier_stage_{a.classifier_dtype}"]["crops_per_s"], a.crops_per_image)
+            stage = max((c for c in plan["candidates"] if c["form"] == "stage"), key=lambda c: c["images_per_s"])
+            a.classifiers = stage["classifiers"]
+            extra["placement"] = {"best": {k: v for k, v in plan.items() if k != "candidates"},
+                                  "stage_graph": stage, "crops_per_image": a.crops_per_image}
+            print(f"[api_bench] placement: {plan['form']} is fastest ({plan['images_per_s']:.0f} images/s est.); "
+                  f"stage graph {stage['leaders']}:{stage['classifiers']} ({stage['images_per_s']:.0f})", flush=True)
         if not 1 <= a.classifiers < a.group:
             raise SystemExit("--classifiers must leave at least one detector GPU in --group")
         group, leaders = a.group, a.group - a.classifiers

@@ -79,3 +79,20 @@ def test_stage_transition():
     ids = s.create_many("http://h/v1/ct/detect", 2)
     stage_transition(s, ids, "http://h/v1/ct/classify")
     assert s.zcard("/v1/ct/classify_running") == 2 and s.zcard("/v1/ct/detect_created") == 0
+
+
+def test_plan_ensemble_from_stage_rates():
+    from aiforearth_api_platform_amd.runtime.pipeline import plan_ensemble
+
+    # round 3's measured rates: detector 3.3k images/s, fp16 classifier 44.7k crops/s, 4 crops per image
+    p = plan_ensemble(8, 3299.0, 44662.0, 4.0)
+    stage = max((c for c in p["candidates"] if c["form"] == "stage"), key=lambda c: c["images_per_s"])
+    assert (stage["leaders"], stage["classifiers"]) == (6, 2)       # 7:1 is classifier-bound at 4 crops/image
+    assert p["form"] == "colocated"                                  # the detector is the heavy stage
+    p1 = plan_ensemble(8, 3299.0, 56452.0, 1.0)
+    assert max((c for c in p1["candidates"] if c["form"] == "stage"),
+               key=lambda c: c["images_per_s"])["classifiers"] == 1  # few crops: 7:1
+    # ideal colocation is never slower than a split (harmonic mean); a measured colocated rate below that
+    # (e.g. two models' working sets thrashing one GPU) makes the stage graph the choice
+    p2 = plan_ensemble(8, 20000.0, 8000.0, 4.0, colocated_images_per_s=1000.0)
+    assert p2["form"] == "stage" and (p2["leaders"], p2["classifiers"]) == (1, 7)
