@@ -135,8 +135,8 @@ class FusedResNet:
 
     def __init__(self, model: ResNet, device="cpu", in_ch: Optional[int] = None,
                  chunk: Optional[Tuple[int, int]] = None, dtype: torch.dtype = torch.bfloat16):
-        """``dtype``: bf16 (the fused serving graph: K1s stem, K1c chains, K1p pairs) or fp16 (every conv one K1
-        launch on f16 MFMA, weights re-rounded from fp32 — the ensemble's crop classifier)."""
+        """``dtype``: bf16 or fp16 (the ensemble's crop classifier, weights re-rounded from fp32): the same fused
+        serving graph (K1s stem with the fused c1, K1c chains, K1p pairs, K1 elsewhere) on bf16 or f16 MFMA."""
         model = model.eval()
         self.device = torch.device(device)
         self.dtype = dtype
@@ -163,11 +163,11 @@ class FusedResNet:
         self.fc = pack_conv(fcw, fcb).to(self.device)
         self.chunk = chunk if chunk is not None else _env_chunk()
         self.chain = _env_chain()
-        if dtype == torch.float16:  # the K1 path is the one built for both element types
+        if dtype == torch.float16:  # K1 / K1s / K1c / K1p all have f16-MFMA instantiations
             self.stem = self.stem.cast(dtype)
             self.blocks = [tuple(c.cast(dtype) if c is not None else None for c in blk) for blk in self.blocks]
             self.fc = self.fc.cast(dtype)
-            self.chain, self.chunk = False, None
+            self.chunk = None
         elif dtype != torch.bfloat16:
             raise ValueError(f"FusedResNet dtype must be bf16 or fp16, got {dtype}")
         self.fold_down = os.environ.get("AI4E_RESNET_FOLD_DOWN", "1") not in ("0", "off", "")
@@ -236,7 +236,7 @@ class FusedResNet:
         return space_to_depth_shifted(x[..., : self.in_ch])
 
     def _stem(self, x: torch.Tensor) -> torch.Tensor:
-        if self.dtype == torch.float16:  # K1 s2d conv + the max-pool kernel (K1s is bf16-only)
+        if self.dtype == torch.float16:  # K1 s2d conv + the max-pool kernel (the stem-only K1s is bf16-only)
             return maxpool2d_nhwc(conv2d_nhwc(self.stem_input(x), self.stem, relu=True))
         return stem_pool(self.stem_input(x), self.stem)  # K1s: conv + bias + ReLU + 3x3/2 max-pool
 

@@ -304,8 +304,12 @@ def conv_chain(t1: torch.Tensor, c2: PackedConv, c3: PackedConv, residual: Optio
             return conv_pair(y2, c3, residual, c1n, out=out, t1n_out=t1n_out)  # K1p: c3 + residual + next c1
         conv2d_nhwc(y2, c3, residual=residual, relu=True, out=out)
         return out, (conv2d_nhwc(out, c1n, relu=True, out=t1n_out) if c1n is not None else None)
-    if t1.dtype != torch.bfloat16 or not t1.is_contiguous() or not out.is_contiguous():
-        raise ValueError("conv_chain: contiguous bf16 NHWC tensors required")
+    f16 = t1.dtype == torch.float16  # (the f16-MFMA instantiation: the ensemble's fp16 crop classifier)
+    if t1.dtype not in (torch.bfloat16, torch.float16) or not t1.is_contiguous() or not out.is_contiguous():
+        raise ValueError("conv_chain: contiguous bf16 or fp16 NHWC tensors required")
+    if any(c is not None and c.w_packed.dtype != t1.dtype for c in (c2, c3, c1n, down)) or \
+            (residual is not None and residual.dtype != t1.dtype) or out.dtype != t1.dtype:
+        raise TypeError("conv_chain: activations, weights (PackedConv.cast) and residual in one dtype")
     if residual is not None and (residual.shape != (n, oh, ow, 4 * mid) or not residual.is_contiguous()):
         raise ValueError("conv_chain: residual must be contiguous [N,OH,OW,4*mid]")
     w3, b3, kpad3 = c3.w_packed, c3.bias, c3.kpad
@@ -317,7 +321,8 @@ def conv_chain(t1: torch.Tensor, c2: PackedConv, c3: PackedConv, residual: Optio
         t1n = torch.empty(n, oh, ow, midn, device=t1.device, dtype=t1.dtype) if t1n_out is None else t1n_out
         if t1n.shape != (n, oh, ow, midn) or not t1n.is_contiguous():
             raise ValueError("conv_chain: bad t1n_out buffer")
-    _ext.call("ai4e_conv_chain_fwd", t1.data_ptr(), c2.w_packed.data_ptr(), c2.bias.data_ptr(),
+    _ext.call("ai4e_conv_chain_f16_fwd" if f16 else "ai4e_conv_chain_fwd", t1.data_ptr(), c2.w_packed.data_ptr(),
+              c2.bias.data_ptr(),
               w3.data_ptr(), b3.data_ptr(), _ext.ptr(residual), out.data_ptr(),
               _ext.ptr(c1n.w_packed if c1n is not None else None), _ext.ptr(c1n.bias if c1n is not None else None),
               _ext.ptr(t1n), n, h, w, mid, mid, midn, c2.stride, c2.kpad, kpad3, c1n.kpad if c1n is not None else 0,
@@ -336,8 +341,10 @@ def pack_mfma_frags(w: torch.Tensor) -> torch.Tensor:
     return w.reshape(r // 16, 16, k // 32, 4, 8).permute(0, 2, 3, 1, 4).contiguous().reshape(r // 16, k // 32, 64, 8)
 
 
-def pair_supported(mid: int, c4: int, midn: int) -> bool:
-    """Shapes the fused 1x1 pair kernel K1p (csrc/kernels/conv_pair.hip) is built for."""
+def pair_supported(mid: int, c4: int, midn: int, dtype: torch.dtype = torch.bfloat16) -> bool:
+    """Shapes the fused 1x1 pair kernel K1p (csrc/kernels/conv_pair.hip) is built for (fp16: the layer3 pair)."""
+    if dtype == torch.float16:
+        return (mid, c4, midn) == (256, 1024, 256)
     return (mid, c4, midn) in ((256, 1024, 256), (128, 512, 256), (256, 1024, 512), (512, 2048, 512))
 
 
@@ -372,16 +379,18 @@ def conv_pair(t2: torch.Tensor, c3: PackedConv, residual: torch.Tensor, c1n: Pac
     if out is None:
         out = torch.empty(n, h, w, c4, device=t2.device, dtype=t2.dtype)
     t1n = torch.empty(n, h, w, midn, device=t2.device, dtype=t2.dtype) if t1n_out is None else t1n_out
-    ok = (_ext.backend_for(t2) == "hip" and pair_supported(mid, c4, midn) and c3.kh == 1 and c3.stride == 1
+    ok = (_ext.backend_for(t2) == "hip" and pair_supported(mid, c4, midn, t2.dtype) and c3.kh == 1 and c3.stride == 1
           and c1n.kh == 1 and c1n.stride == 1 and c3.cin_pad == mid and c1n.cin_pad == c4 and t2.is_contiguous()
           and residual.is_contiguous() and residual.shape == (n, h, w, c4) and out.is_contiguous()
-          and t1n.is_contiguous() and t1n.shape == (n, h, w, midn) and t2.dtype == torch.bfloat16)
+          and t1n.is_contiguous() and t1n.shape == (n, h, w, midn) and t2.dtype in (torch.bfloat16, torch.float16)
+          and c3.w_packed.dtype == t2.dtype and c1n.w_packed.dtype == t2.dtype and residual.dtype == t2.dtype)
     if not ok:
         conv2d_nhwc(t2, c3, residual=residual, relu=True, out=out)
         conv2d_nhwc(out, c1n, relu=True, out=t1n)
         return out, t1n
     w3p, w1p = _pair_pack(c3, c1n)
-    _ext.call("ai4e_conv_pair_fwd", t2.data_ptr(), w3p.data_ptr(), c3.bias.data_ptr(), residual.data_ptr(),
+    _ext.call("ai4e_conv_pair_f16_fwd" if t2.dtype == torch.float16 else "ai4e_conv_pair_fwd", t2.data_ptr(),
+              w3p.data_ptr(), c3.bias.data_ptr(), residual.data_ptr(),
               out.data_ptr(), w1p.data_ptr(), c1n.bias.data_ptr(), t1n.data_ptr(), n * h * w, mid, c4, midn,
               (PAIR_TILE if (mid, midn) == (256, 256) else 0) if tile_cfg < 0 else tile_cfg, _ext.stream_ptr(t2.device))
     return out, t1n
@@ -431,15 +440,22 @@ def stem_pool_c1(x: torch.Tensor, pc: PackedConv, c1: PackedConv):
     while it is still in LDS: returns ``(y, relu(c1(y)))`` from ONE launch (no re-read of y). Other backends /
     shapes: ``stem_pool`` then a K1 conv."""
     n, h, w, c = x.shape
+    f16 = x.dtype == torch.float16
     if (_ext.backend_for(x) != "hip" or pc.cout != 64 or c != 16 or (pc.kh, pc.kw, pc.pad, pc.pad_hi) != (4, 4, 1, 2)
             or (c1.kh, c1.kw, c1.stride, c1.pad, c1.cin_pad, c1.cout) != (1, 1, 1, 0, 64, 64) or STEM_VARIANT != 0
-            or x.dtype != torch.bfloat16 or not x.is_contiguous()):
-        y = stem_pool(x, pc)
+            or x.dtype not in (torch.bfloat16, torch.float16) or pc.w_packed.dtype != x.dtype
+            or c1.w_packed.dtype != x.dtype or not x.is_contiguous()):
+        if f16:  # (K1s is built for bf16 and fp16; other shapes: K1 conv + the max-pool kernel)
+            from .pool import maxpool2d_nhwc
+            y = maxpool2d_nhwc(conv2d_nhwc(x, pc, relu=True), 3, 2, 1)
+        else:
+            y = stem_pool(x, pc)
         return y, conv2d_nhwc(y, c1, relu=True)
     ph, pw = (h - 1) // 2 + 1, (w - 1) // 2 + 1
     y = torch.empty(n, ph, pw, 64, device=x.device, dtype=x.dtype)
     t1 = torch.empty(n, ph, pw, 64, device=x.device, dtype=x.dtype)
-    _ext.call("ai4e_stem_pool_c1_fwd", x.data_ptr(), pc.w_packed.data_ptr(), pc.bias.data_ptr(), y.data_ptr(),
+    _ext.call("ai4e_stem_pool_c1_f16_fwd" if f16 else "ai4e_stem_pool_c1_fwd", x.data_ptr(), pc.w_packed.data_ptr(),
+              pc.bias.data_ptr(), y.data_ptr(),
               c1.w_packed.data_ptr(), c1.bias.data_ptr(), t1.data_ptr(), c1.kpad, n, h, w, pc.kpad,
               _ext.stream_ptr(x.device))
     return y, t1

@@ -144,6 +144,27 @@ __device__ __forceinline__ uint32_t f16_sel_hi() {
   return v;
 }
 
+// (a + r.lo / r.hi) of packed bf16 / fp16 r (dot2 against a (1, 0) / (0, 1) selector)
+template <bool F16>
+__device__ __forceinline__ float add_lo(uint32_t r, float a) {
+  if constexpr (F16)
+    return __builtin_amdgcn_fdot2(__builtin_bit_cast(f16x2_t, r), __builtin_bit_cast(f16x2_t, f16_sel_lo()), a, false);
+  else
+    return add_bf16_lo(r, a);
+}
+template <bool F16>
+__device__ __forceinline__ float add_hi(uint32_t r, float a) {
+  if constexpr (F16)
+    return __builtin_amdgcn_fdot2(__builtin_bit_cast(f16x2_t, r), __builtin_bit_cast(f16x2_t, f16_sel_hi()), a, false);
+  else
+    return add_bf16_hi(r, a);
+}
+// relu(lo, hi) packed to bf16 / fp16 (sign-bit ReLU on the packed halves, valid for both formats)
+template <bool F16>
+__device__ __forceinline__ uint32_t pack_relu2(float lo, float hi) {
+  return relu_bf16x2(pack2<F16>(lo, hi));
+}
+
 template <bool F16>
 __device__ __forceinline__ uint4 epilogue8(const float (&f)[8], bool has_res, const uint4& r, bool relu) {
   if constexpr (!F16) {

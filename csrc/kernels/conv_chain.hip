@@ -46,6 +46,45 @@ __device__ __attribute__((aligned(64))) uint16_t g_chain_sink[512 + 64];
 // clobber so hipcc moves no LDS access across it (the raw builtin is not a compiler memory barrier).
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+// Conflict-free chain layout (round 4; profiles/r4_chain_cf/: neutral in time against the round-3 layout, which was
+// 2-way conflicted on every epilogue write and on the patch reads of fragments that wrap an image row):
+// * the T2 / Y / T1' tiles use the 16-B chunk swizzle swt(r) = gray((r >> 1) & 3), chosen (exhaustive search over
+//   per-row chunk rotations of a 64-B row) so that BOTH the MFMA fragment reads (ds_read_b128, 4 x 16 lane groups,
+//   rows 0-3 / 12-15 at chunk c and rows 4-11 at c ^ 1) AND the epilogue's 16-B row writes (ds_write_b128, 8 x 8
+//   contiguous lanes = 8 consecutive rows, banks mod 32) hit every bank once. The epilogues first regroup two 16-channel
+//   accumulator blocks with v_permlane16_swap so each lane writes 8 consecutive channels (one ds_write_b128 instead of
+//   two 2-way-conflicted ds_write_b64; the same for the residual read);
+// * patch rows are padded to W + 8 slots (row stride = W mod 8), so 16 consecutive pixels read 16 consecutive slots mod 8
+//   even where a fragment wraps to the next image row, and a masked tap reads a zero slot of the same residue mod 8
+//   instead of slot 0 (both were 2-way conflicts on the patch reads of phase A).
+#ifndef AI4E_CHAIN_PD
+#define AI4E_CHAIN_PD 4
+#endif
+__device__ __forceinline__ int swt(int r) {
+  const int x = (r >> 1) & 3;
+  return x ^ (x >> 1);
+}
+
+// Regroup two accumulator blocks of one 32-channel K block: a = this lane's 4 values of channels 4*lg.. of block j,
+// b = the same of block j + 1 (j even). After the row swaps (lanes 16-31 of a <-> lanes 0-15 of b, and 48-63 <-> 32-47)
+// the lane holds 8 consecutive channels [a | b] of 16-B chunk swap_chunk(lg) of that K block. With a, b = one block of
+// two fragments 16 rows apart instead, the lane holds row + 16 * (lg & 1), chunk of the block + (lg >> 1).
+__device__ __forceinline__ void swap16(f32x4_t& a, f32x4_t& b) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(a[q]), __float_as_uint(b[q]), false, false);
+    a[q] = __uint_as_float(r[0]);
+    b[q] = __uint_as_float(r[1]);
+  }
+}
+__device__ __forceinline__ int swap_chunk(int lg) { return ((lg & 1) << 1) | (lg >> 1); }
+// 8 values -> 8 x bf16 / fp16 with ReLU (the sign-bit ReLU of relu_bf16x2 holds for fp16 bits too)
+template <bool F16>
+__device__ __forceinline__ uint4 relu8(const f32x4_t& a, const f32x4_t& b) {
+  return make_uint4(relu_bf16x2(pack2<F16>(a[0], a[1])), relu_bf16x2(pack2<F16>(a[2], a[3])),
+                    relu_bf16x2(pack2<F16>(b[0], b[1])), relu_bf16x2(pack2<F16>(b[2], b[3])));
+}
+
 // Diagnostic build (AI4E_CHAIN_STAMPS=1): s_memtime stamps at the phase boundaries (phase A, B/C setup + T2
 // epilogue, the passes, the T1' epilogue + copy-out), per wave, written to g_chain_stamps (read SHARES only).
 #ifndef AI4E_CHAIN_STAMPS
@@ -108,6 +147,7 @@ struct ChainParams {
   uint16_t* sink;
   const uint16_t* x0;   // DOWN: the block input [M, ldx0] (64 channels) whose 1x1 projection is the residual
   int ldx0;
+  int pw2;              // patch mode: slots per patch row (W + 8 where it fits, else W + 2)
 };
 
 // Phase A "patch" mode (PATCH, stride 1): instead of gathering every 3x3 tap of every pixel through the
@@ -179,11 +219,10 @@ struct ChainCfg {
   static_assert(FI >= 1 && FI <= 4 && BFI >= 1 && FIC >= 1 && FIC <= 4, "tile");
 };
 
-// byte offset of the 8-byte group holding channels n..n+3 of row r in a K-blocked swizzled tile of BM rows
+// byte offset of 16-B chunk c (channels 8c .. 8c + 7) of row r in the same tile
 template <int BM>
-__device__ __forceinline__ uint32_t tile_off(int r, int n) {
-  const int kb = n >> 5, e = n & 31;
-  return kb * BM * 64 + r * 64 + ((((e >> 3) ^ swz(r)) << 4) | (((e >> 2) & 1) << 3));
+__device__ __forceinline__ uint32_t tile_off16(int r, int c) {
+  return (c >> 2) * BM * 64 + r * 64 + (((c & 3) ^ swt(r)) << 4);
 }
 
 // Measured and removed (profiles/r3_rreg/; code in the git history up to commit bc1ff0a): the residual chunk
@@ -196,7 +235,7 @@ __device__ __forceinline__ uint32_t tile_off(int r, int n) {
 // fragment's address becomes slot * RBS + 16 * lg per tap with the K step as the ds_read immediate, instead of a
 // per-step XOR + shift + add per fragment (the chain kernels issue ~4-8 VALU per MFMA; PMC, profiles/r3_pad/).
 template <int MID, int BM_, int MIDN, bool DOWN, int ST, bool BL, bool PATCH, int PWN_ = 4,
-          bool PAD = false>
+          bool PAD = false, bool F16 = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ChainCfg<MID, BM_, MIDN, DOWN, ST, BL>::MINW,
                                                                      ChainCfg<MID, BM_, MIDN, DOWN, ST, BL>::MINW)))
 void conv_chain_kernel(const ChainParams p) {
@@ -232,6 +271,8 @@ void conv_chain_kernel(const ChainParams p) {
   const int c = (lane & 3) ^ swz(rin);
   const int frow = lane & 15;
   const uint32_t fofs = frow * 64 + ((((lane >> 4) ^ swz(frow)) << 4));  // fragment byte offset in a 16-row block
+  const uint32_t tofs = frow * 64 + ((((lane >> 4) ^ swt(frow)) << 4));  // the same in the T2 / Y / T1' tiles
+  const int ct = (lane & 3) ^ swt(rin);  // logical chunk of a tile DMA lane (rows rin, physical chunk lane & 3)
 
   // bias values this thread stages into LDS once phase A has drained (loaded now, ahead of the DMA asm)
   float bstage[2] = {0.f, 0.f};
@@ -264,7 +305,8 @@ void conv_chain_kernel(const ChainParams p) {
     constexpr int RB = MID * 2;    // bytes per pixel slot
     constexpr int CPS = RB / 16;   // 16-B chunks per slot
     constexpr int RBS = PAD ? RB + 32 : RB;  // slot stride
-    const int W = p.W, W2 = p.W + 2;
+    const int W = p.W, W2 = PAD ? p.W + 2 : p.pw2;
+    const int NZ = W2 - W;   // zero slots per patch row: slot 0 and W + 1 .. W2 - 1
     const int r_lo = m0 / W;                          // flattened (image, row) index of the first pixel
     const int r_hi = (min(m0 + BM, p.M) - 1) / W;
     const int prows = r_hi - r_lo + 3;                // + one halo row above and below
@@ -300,11 +342,13 @@ void conv_chain_kernel(const ChainParams p) {
         glds16(ok ? static_cast<const void*>(p.x + (static_cast<long>(R) * W + s1) * p.ldx + 8 * q) : zero,
                sb + (j * W2 + 1) * RB + piece * 1024);
       }
-      // zero pad slots (left / right of every row; slot 0 doubles as the zero source of masked taps)
-      for (int g = tid; g < prows * 2 * CPS; g += 256) {
-        const int j = g / (2 * CPS), e = g - j * 2 * CPS;
-        const int slot = j * W2 + (e >= CPS ? W + 1 : 0);
-        *reinterpret_cast<uint4*>(smem + slot * RB + (e % CPS) * 16) = make_uint4(0u, 0u, 0u, 0u);
+      // zero pad slots (left / right of every row; with NZ = 8 the slots W + 1 .. W + 8 (= slot 0 of the next row)
+      // hold one zero slot per residue mod 8, the source of masked taps; else slot 0)
+      for (int g = tid; g < prows * NZ * CPS; g += 256) {
+        const int j = g / (NZ * CPS), e = g - j * NZ * CPS;
+        const int z = e / CPS;
+        const int slot = j * W2 + (z == 0 ? 0 : W + z);
+        *reinterpret_cast<uint4*>(smem + slot * RB + (e - z * CPS) * 16) = make_uint4(0u, 0u, 0u, 0u);
       }
     }
     // per pixel fragment: slot of tap (0, 0) and the row-validity bits of kh = 0, 1, 2
@@ -324,7 +368,7 @@ void conv_chain_kernel(const ChainParams p) {
     }
     constexpr int SPT = MID / 32;   // K steps per tap
     constexpr int NKA = 9 * SPT;
-    constexpr int PD = 4;           // weight K steps prefetched into registers
+    constexpr int PD = AI4E_CHAIN_PD;  // weight K steps prefetched into registers
     const uint16_t* const wp = p.w2 + static_cast<long>(pwn * (MID / PWN) + (lane & 15)) * p.kpad2 + 8 * lg;
     bf16x8_t wr[PD][CF];
 #pragma unroll
@@ -339,7 +383,8 @@ void conv_chain_kernel(const ChainParams p) {
       const int kh = t / 3, kw = t - 3 * (t / 3);
 #pragma unroll
       for (int i = 0; i < PFI; ++i) {
-        const int slot = (vmask[i] >> kh) & 1 ? sbase[i] + kh * W2 + kw : 0;
+        const int s0 = sbase[i] + kh * W2 + kw;
+        const int slot = (vmask[i] >> kh) & 1 ? s0 : (!PAD && NZ == 8 ? W + 1 + ((s0 - W - 1) & 7) : 0);
         if constexpr (PAD) {
           soff[i] = slot * RBS + 16 * lg;
         } else {
@@ -371,7 +416,7 @@ void conv_chain_kernel(const ChainParams p) {
       for (int i = 0; i < PFI; ++i)
 #pragma unroll
         for (int j = 0; j < CF; ++j)
-          pacc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wr[s % PD][j], fx[s & 1][i], pacc[i][j], 0, 0, 0);
+          pacc[i][j] = mfma_16x16x32<F16>(wr[s % PD][j], fx[s & 1][i], pacc[i][j]);
       if (s + PD < NKA) {
 #pragma unroll
         for (int j = 0; j < CF; ++j)
@@ -441,7 +486,7 @@ void conv_chain_kernel(const ChainParams p) {
     KC_READ(FWN, FXN, kt_ + 1)                                                                          \
     _Pragma("unroll") for (int i = 0; i < FI; ++i)                                                      \
       _Pragma("unroll") for (int j = 0; j < 4; ++j)                                                     \
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(FWC[j], FXC[i], acc[i][j], 0, 0, 0);        \
+        acc[i][j] = mfma_16x16x32<F16>(FWC[j], FXC[i], acc[i][j]);        \
     issue_a(kt_ + STAGES - 1);                                                                          \
   }
 #pragma unroll
@@ -501,7 +546,7 @@ void conv_chain_kernel(const ChainParams p) {
       const int q = wave + 4 * s;
       const int kb = q / (BM / 16), rb = q % (BM / 16);
       const int row = rb * 16 + rin;
-      glds16(p.x0 + static_cast<long>(min(m0 + row, p.M - 1)) * p.ldx0 + kb * BK + 8 * c,
+      glds16(p.x0 + static_cast<long>(min(m0 + row, p.M - 1)) * p.ldx0 + kb * BK + 8 * ct,
              sb + (MID / 32 + kb) * BM * 64 + rb * 16 * 64);
     }
     ops += BM / 32;
@@ -509,22 +554,38 @@ void conv_chain_kernel(const ChainParams p) {
 #pragma unroll
   for (int t = 0; t < STAGES - 1; ++t) issue_w(t);
 
-  const float lo = 0.f;
   // T2 epilogue: + b2, ReLU, bf16 -> t2buf (phase A wave layout); the lane-group bias select once per j
   // (readfirstlane is convergent: hipcc does not CSE it across the i loop)
-  if constexpr (PATCH) {
+  if constexpr (PATCH && CF % 2 == 0) {
+    // pairs of 16-channel blocks (j, j + 1) of one K block -> one 16-B write per lane and fragment
 #pragma unroll
-    for (int j = 0; j < CF; ++j) {
-      const f32x4_t b = bias4(p.b2 + pwn * (MID / PWN) + 16 * j, lg);
+    for (int jp = 0; jp < CF / 2; ++jp) {
+      const int nb = pwn * (MID / PWN) + 32 * jp;
+      const f32x4_t b0 = bias4(p.b2 + nb, lg), b1 = bias4(p.b2 + nb + 16, lg);
 #pragma unroll
       for (int i = 0; i < PFI; ++i) {
         const int r = pwm * (BM / PWM) + 16 * i + (lane & 15);
-        const int n = pwn * (MID / PWN) + 16 * j + 4 * lg;
-        *reinterpret_cast<uint2*>(t2buf + tile_off<BM>(r, n)) =
-            make_uint2(pack_relu_bf16x2(pacc[i][j][0] + b[0], pacc[i][j][1] + b[1]),
-                       pack_relu_bf16x2(pacc[i][j][2] + b[2], pacc[i][j][3] + b[3]));
+        f32x4_t a = pacc[i][2 * jp] + b0, b = pacc[i][2 * jp + 1] + b1;
+        swap16(a, b);
+        *reinterpret_cast<uint4*>(t2buf + tile_off16<BM>(r, nb / 8 + swap_chunk(lg))) = relu8<F16>(a, b);
       }
     }
+  } else if constexpr (PATCH && PFI % 2 == 0) {
+    // one 16-channel block per wave (MID 64): pairs of fragments 16 rows apart -> one 16-B write per lane
+#pragma unroll
+    for (int j = 0; j < CF; ++j) {
+      const int nb = pwn * (MID / PWN) + 16 * j;
+      const f32x4_t bj = bias4(p.b2 + nb, lg);
+#pragma unroll
+      for (int ip = 0; ip < PFI / 2; ++ip) {
+        const int r = pwm * (BM / PWM) + 32 * ip + (lane & 15) + 16 * (lg & 1);
+        f32x4_t a = pacc[2 * ip][j] + bj, b = pacc[2 * ip + 1][j] + bj;
+        swap16(a, b);
+        *reinterpret_cast<uint4*>(t2buf + tile_off16<BM>(r, nb / 8 + (lg >> 1))) = relu8<F16>(a, b);
+      }
+    }
+  } else if constexpr (PATCH) {
+    static_assert(!PATCH, "patch-mode T2 epilogue: CF or PFI even");
   }
   f32x4_t b2v[4];
 #pragma unroll
@@ -533,12 +594,10 @@ void conv_chain_kernel(const ChainParams p) {
   for (int i = 0; i < (PATCH ? 0 : FI); ++i) {
     const int r = wm * WPX + 16 * i + (lane & 15);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int n = wn * 64 + 16 * j + 4 * lg;
-      const f32x4_t b = b2v[j];
-      *reinterpret_cast<uint2*>(t2buf + tile_off<BM>(r, n)) =
-          make_uint2(pack_relu_bf16x2(acc[i][j][0] + b[0], acc[i][j][1] + b[1]),
-                     pack_relu_bf16x2(acc[i][j][2] + b[2], acc[i][j][3] + b[3]));
+    for (int jp = 0; jp < 2; ++jp) {
+      f32x4_t a = acc[i][2 * jp] + b2v[2 * jp], b = acc[i][2 * jp + 1] + b2v[2 * jp + 1];
+      swap16(a, b);
+      *reinterpret_cast<uint4*>(t2buf + tile_off16<BM>(r, (wn * 64 + 32 * jp) / 8 + swap_chunk(lg))) = relu8<F16>(a, b);
     }
   }
 
@@ -564,7 +623,7 @@ void conv_chain_kernel(const ChainParams p) {
       step_wait(t);
       bf16x8_t fw[4], fx[BFI];
       const uint8_t* w_ = smem + Cfg::RING + (t % STAGES) * Cfg::SLOT * 64 + fofs;
-      const uint8_t* x_ = t2buf + kk * BM * 64 + (wave * Cfg::BPW) * 64 + fofs;
+      const uint8_t* x_ = t2buf + kk * BM * 64 + (wave * Cfg::BPW) * 64 + tofs;
 #pragma unroll
       for (int j = 0; j < 4; ++j) fw[j] = *reinterpret_cast<const bf16x8_t*>(w_ + j * 1024);
 #pragma unroll
@@ -577,13 +636,13 @@ void conv_chain_kernel(const ChainParams p) {
 #pragma unroll
         for (int i = 0; i < BFI; ++i)
 #pragma unroll
-          for (int j = 0; j < 4; ++j) a[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[j], fx[i], bj[j], 0, 0, 0);
+          for (int j = 0; j < 4; ++j) a[i][j] = mfma_16x16x32<F16>(fw[j], fx[i], bj[j]);
       } else {
 #pragma unroll
         for (int i = 0; i < BFI; ++i)
 #pragma unroll
           for (int j = 0; j < 4; ++j)
-            a[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[j], fx[i], a[i][j], 0, 0, 0);
+            a[i][j] = mfma_16x16x32<F16>(fw[j], fx[i], a[i][j]);
       }
       issue_w(t + STAGES - 1);
     }
@@ -596,7 +655,7 @@ void conv_chain_kernel(const ChainParams p) {
       step_wait(t);
       bf16x8_t fw[4], fx[FIC];
       const uint8_t* w_ = smem + Cfg::RING + (t % STAGES) * Cfg::SLOT * 64 + (wnc * 64) * 64 + fofs;
-      const uint8_t* x_ = ybuf + kk * BM * 64 + (wmc * WPXC) * 64 + fofs;
+      const uint8_t* x_ = ybuf + kk * BM * 64 + (wmc * WPXC) * 64 + tofs;
 #pragma unroll
       for (int j = 0; j < 4; ++j) fw[j] = *reinterpret_cast<const bf16x8_t*>(w_ + j * 1024);
 #pragma unroll
@@ -605,7 +664,7 @@ void conv_chain_kernel(const ChainParams p) {
       for (int i = 0; i < FIC; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          accn[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[j], fx[i], accn[i][j], 0, 0, 0);
+          accn[i][j] = mfma_16x16x32<F16>(fw[j], fx[i], accn[i][j]);
       issue_w(t + STAGES - 1);
     }
   };
@@ -630,7 +689,7 @@ void conv_chain_kernel(const ChainParams p) {
     for (int e = 0; e < N; ++e) {
       const int g = tid + 256 * e;
       const int r = g / CPR, cq = g % CPR;
-      const uint4 v = *reinterpret_cast<const uint4*>(tile + (cq >> 2) * BM * 64 + r * 64 + (((cq & 3) ^ swz(r)) << 4));
+      const uint4 v = *reinterpret_cast<const uint4*>(tile + (cq >> 2) * BM * 64 + r * 64 + (((cq & 3) ^ swt(r)) << 4));
       ai4e_conv::st16_stream(base[e] + coff, v);
     }
     ops += N;
@@ -652,7 +711,7 @@ void conv_chain_kernel(const ChainParams p) {
       const int q = wave + 4 * s;
       const int kb = q / (BM / 16), rb = q % (BM / 16);
       const int row = rb * 16 + rin;
-      ai4e_conv::glds16_stream(p.res + static_cast<long>(min(m0 + row, p.M - 1)) * C4 + pp * 64 + kb * BK + 8 * c,
+      ai4e_conv::glds16_stream(p.res + static_cast<long>(min(m0 + row, p.M - 1)) * C4 + pp * 64 + kb * BK + 8 * ct,
              sb + Cfg::T2_BYTES + kb * BM * 64 + rb * 16 * 64);
     }
     ops += DOWN ? 0 : Cfg::NR;
@@ -675,32 +734,18 @@ void conv_chain_kernel(const ChainParams p) {
 #pragma unroll
     for (int i = 0; i < BFI; ++i) {
       const int r = wave * Cfg::BPW + 16 * i + (lane & 15);
+      constexpr bool BSEED = Cfg::BIAS_LDS || Cfg::BIAS_RING;  // bias already in the accumulators
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int n = 16 * j + 4 * lg;
-        constexpr bool BSEED = Cfg::BIAS_LDS || Cfg::BIAS_RING;  // bias already in the accumulators
-        const f32x4_t b = BSEED ? f32x4_t{0.f, 0.f, 0.f, 0.f} : bias4(p.b3 + pp * 64 + 16 * j, lg);
-        uint2* yp = reinterpret_cast<uint2*>(ybuf + tile_off<BM>(r, n));
-        if constexpr (BSEED && DOWN) {
-          *yp = make_uint2(pack_relu_bf16x2(accb[i][j][0], accb[i][j][1]), pack_relu_bf16x2(accb[i][j][2], accb[i][j][3]));
-          continue;
+      for (int jp = 0; jp < 2; ++jp) {
+        f32x4_t a = accb[i][2 * jp], b = accb[i][2 * jp + 1];
+        if constexpr (!BSEED) {
+          a += bias4(p.b3 + pp * 64 + 32 * jp, lg);
+          b += bias4(p.b3 + pp * 64 + 32 * jp + 16, lg);
         }
-        if constexpr (BSEED) {  // residual added straight from its packed bf16 (dot2), ReLU on packed bf16
-          const uint2 rv = *yp;
-          *yp = make_uint2(pack_relu_bf16x2(add_bf16_lo(rv.x, accb[i][j][0]), add_bf16_hi(rv.x, accb[i][j][1])),
-                           pack_relu_bf16x2(add_bf16_lo(rv.y, accb[i][j][2]), add_bf16_hi(rv.y, accb[i][j][3])));
-          continue;
-        }
-        float r0 = 0.f, r1 = 0.f, r2 = 0.f, r3 = 0.f;
-        if constexpr (!DOWN) {
-          const uint2 rv = *yp;
-          unpack_bf16x2(rv.x, r0, r1);
-          unpack_bf16x2(rv.y, r2, r3);
-        }
-        {
-          *yp = make_uint2(pack_bf16x2(fmaxf(accb[i][j][0] + b[0] + r0, lo), fmaxf(accb[i][j][1] + b[1] + r1, lo)),
-                           pack_bf16x2(fmaxf(accb[i][j][2] + b[2] + r2, lo), fmaxf(accb[i][j][3] + b[3] + r3, lo)));
-        }
+        swap16(a, b);
+        uint4* yp = reinterpret_cast<uint4*>(ybuf + tile_off16<BM>(r, 4 * jp + swap_chunk(lg)));
+        const float f[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+        *yp = epilogue8<F16>(f, !DOWN, DOWN ? make_uint4(0u, 0u, 0u, 0u) : *yp, true);
       }
     }
     if constexpr (NEXT) {
@@ -736,12 +781,10 @@ void conv_chain_kernel(const ChainParams p) {
     for (int i = 0; i < FIC; ++i) {
       const int r = wmc * WPXC + 16 * i + (lane & 15);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int n = wnc * 64 + 16 * j + 4 * lg;
-        const f32x4_t b = b1v[j];
-        *reinterpret_cast<uint2*>(t2buf + tile_off<BM>(r, n)) =
-            make_uint2(pack_relu_bf16x2(accn[i][j][0] + b[0], accn[i][j][1] + b[1]),
-                       pack_relu_bf16x2(accn[i][j][2] + b[2], accn[i][j][3] + b[3]));
+      for (int jp = 0; jp < 2; ++jp) {
+        f32x4_t a = accn[i][2 * jp] + b1v[2 * jp], b = accn[i][2 * jp + 1] + b1v[2 * jp + 1];
+        swap16(a, b);
+        *reinterpret_cast<uint4*>(t2buf + tile_off16<BM>(r, (wnc * 64 + 32 * jp) / 8 + swap_chunk(lg))) = relu8<F16>(a, b);
       }
     }
     lds_barrier();
@@ -761,24 +804,27 @@ void conv_chain_kernel(const ChainParams p) {
 
 // Patch mode (phase A from an LDS patch of the input rows) applies to stride 1, an input row of whole 1-KB
 // DMA pieces, a dense [N, H, W, MID] input, 128-pixel tiles and a patch that fits the config's LDS.
+// Returns the patch row stride in slots (W + 8 where that fits, else W + 2), 0 = no patch mode.
 template <int MID, int BM, bool PAD = false>
-bool patch_fits(const ChainParams& p, int lds_bytes) {
-  if (BM != 128 || p.stride != 1 || p.ldx != MID || (!PAD && (p.W * MID * 2) % 1024)) return false;
-  const int rows = (BM - 1 + p.W - 1) / p.W + 1 + 2;  // most rows BM consecutive pixels touch, + 2 halo rows
-  return static_cast<long>(rows) * (p.W + 2) * (MID * 2 + (PAD ? 32 : 0)) <= lds_bytes;
+int patch_fits(const ChainParams& p, int lds_bytes) {
+  if (BM != 128 || p.stride != 1 || p.ldx != MID || (!PAD && (p.W * MID * 2) % 1024)) return 0;
+  const long rows = (BM - 1 + p.W - 1) / p.W + 1 + 2;  // most rows BM consecutive pixels touch, + 2 halo rows
+  const long rb = MID * 2 + (PAD ? 32 : 0);
+  if (!PAD && rows * (p.W + 8) * rb <= lds_bytes) return p.W + 8;
+  return rows * (p.W + 2) * rb <= lds_bytes ? p.W + 2 : 0;
 }
 
 template <int MID, int BM, int MIDN, bool DOWN = false, int ST = 4, bool BL = true, int PWN = 4,
-          bool PAD = false>
-int launch_chain(const ChainParams& p, hipStream_t s, bool patch = false) {
+          bool PAD = false, bool F16 = false>
+int launch_chain(ChainParams p, hipStream_t s, bool patch = false) {
   using Cfg = ChainCfg<MID, BM, MIDN, DOWN, ST, BL>;
   static bool attr = false;
   if (!attr) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(conv_chain_kernel<MID, BM, MIDN, DOWN, ST, BL, false>),
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(conv_chain_kernel<MID, BM, MIDN, DOWN, ST, BL, false, 4, false, F16>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, Cfg::LDS_ALL) != hipSuccess)
       return AI4E_ELAUNCH;
     if constexpr (BM == 128) {
-      if (hipFuncSetAttribute(reinterpret_cast<const void*>(conv_chain_kernel<MID, BM, MIDN, DOWN, ST, BL, true, PWN, PAD>),
+      if (hipFuncSetAttribute(reinterpret_cast<const void*>(conv_chain_kernel<MID, BM, MIDN, DOWN, ST, BL, true, PWN, PAD, F16>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, Cfg::LDS_ALL) != hipSuccess)
         return AI4E_ELAUNCH;
     }
@@ -786,14 +832,14 @@ int launch_chain(const ChainParams& p, hipStream_t s, bool patch = false) {
   }
   const int nb = ai4e_cdiv(p.M, Cfg::BM);
   if constexpr (BM == 128) {
-    if (patch && patch_fits<MID, BM, PAD>(p, Cfg::LDS)) {
-      hipLaunchKernelGGL((conv_chain_kernel<MID, BM, MIDN, DOWN, ST, BL, true, PWN, PAD>), dim3(nb), dim3(256), Cfg::LDS_ALL,
+    if (patch && (p.pw2 = patch_fits<MID, BM, PAD>(p, Cfg::LDS)) > 0) {
+      hipLaunchKernelGGL((conv_chain_kernel<MID, BM, MIDN, DOWN, ST, BL, true, PWN, PAD, F16>), dim3(nb), dim3(256), Cfg::LDS_ALL,
                          s, p);
       return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
     }
   }
-  hipLaunchKernelGGL((conv_chain_kernel<MID, BM, MIDN, DOWN, ST, BL, false>), dim3(nb), dim3(256), Cfg::LDS_ALL, s,
-                     p);
+  hipLaunchKernelGGL((conv_chain_kernel<MID, BM, MIDN, DOWN, ST, BL, false, 4, false, F16>), dim3(nb), dim3(256),
+                     Cfg::LDS_ALL, s, p);
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
 }
 
@@ -805,14 +851,24 @@ T* symbol_ptr(const void* sym) {
 
 }  // namespace
 
-// Fused bottleneck chain (see header). x: T1 NHWC [N,H,W,ldx] bf16 (MID channels at offset 0);
-// w2 [>=MID rows, kpad2 >= 9*MID] (k = (kh, kw, c)); w3 [>=4*MID rows, kpad3 >= MID];
-// w1n [>=MIDN rows, kpad1n >= 4*MID] (nullptr: no next block, t1n unused); res, y [M, 4*MID];
-// t1n [M, MIDN]. 3x3, pad 1, stride 1 or 2. (MID, MIDN) in {(64, 64), (64, 128), (128, 128)}; midn 0 = mid.
-AI4E_API int ai4e_conv_chain_fwd(const void* x, const void* w2, const void* b2, const void* w3, const void* b3,
-                                 const void* res, void* y, const void* w1n, const void* b1n, void* t1n, int N, int H,
-                                 int W, int ldx, int mid, int midn, int stride, int kpad2, int kpad3, int kpad1n,
-                                 int tile_cfg, const void* x0, int ldx0, hipStream_t stream) {
+namespace {
+// fp16 (the ensemble's crop classifier, v_mfma_f32_16x16x32_f16): the default 128-pixel tiles with phase A from the
+// LDS patch where the shape allows it, else the LDS-DMA ring; no A/B reference configs
+int chain_f16(const ChainParams& p, bool down, bool next, int mid, int midn, hipStream_t stream) {
+  if (down) return launch_chain<64, 128, 64, true, 4, true, 4, false, true>(p, stream, true);
+  if (mid == 64) {
+    if (next && midn == 128) return launch_chain<64, 128, 128, false, 4, true, 4, false, true>(p, stream, true);
+    return next ? launch_chain<64, 128, 64, false, 4, true, 4, false, true>(p, stream, true)
+                : launch_chain<64, 128, 0, false, 4, true, 4, false, true>(p, stream, true);
+  }
+  return next ? launch_chain<128, 128, 128, false, 4, true, 4, false, true>(p, stream, true)
+              : launch_chain<128, 128, 0, false, 4, true, 4, false, true>(p, stream, true);
+}
+
+int chain_fwd(bool f16, const void* x, const void* w2, const void* b2, const void* w3, const void* b3,
+              const void* res, void* y, const void* w1n, const void* b1n, void* t1n, int N, int H,
+              int W, int ldx, int mid, int midn, int stride, int kpad2, int kpad3, int kpad1n,
+              int tile_cfg, const void* x0, int ldx0, hipStream_t stream) {
   if (midn == 0) midn = mid;
   // DOWN mode (x0 given, res null): the residual is the 1x1 projection of x0 [M, ldx0] (64 channels), folded
   // into w3 = [W3 | Wd] (kpad3 >= mid + 64) and b3 = b3 + bd; MID 64, same-width chained c1', stride 1.
@@ -849,6 +905,7 @@ AI4E_API int ai4e_conv_chain_fwd(const void* x, const void* w2, const void* b2, 
   p.ldx0 = ldx0;
   if (p.M <= 0) return AI4E_OK;
   const bool next = w1n != nullptr;
+  if (f16) return chain_f16(p, down, next, mid, midn, stream);
   // tile_cfg: 0 = default (MID 64: 256 pixels, MID 128: 128), 1 = 128-pixel MID-64 tile (48 KB LDS, 3 per CU),
   // 2 = the 128-pixel tiles with the SGPR lane-select biases (A/B reference for the LDS / ring-borne biases),
   // 3 = the 128-pixel tiles with phase A in patch mode where the shape allows it (else the ring, as 1);
@@ -881,6 +938,28 @@ AI4E_API int ai4e_conv_chain_fwd(const void* x, const void* w2, const void* b2, 
     return next ? launch_chain<128, 128, 128, false, 4, false>(p, stream)
                 : launch_chain<128, 128, 0, false, 4, false>(p, stream);
   return next ? launch_chain<128, 128, 128>(p, stream, patch) : launch_chain<128, 128, 0>(p, stream, patch);
+}
+}  // namespace
+
+// Fused bottleneck chain (see header). x: T1 NHWC [N,H,W,ldx] bf16 (MID channels at offset 0);
+// w2 [>=MID rows, kpad2 >= 9*MID] (k = (kh, kw, c)); w3 [>=4*MID rows, kpad3 >= MID];
+// w1n [>=MIDN rows, kpad1n >= 4*MID] (nullptr: no next block, t1n unused); res, y [M, 4*MID];
+// t1n [M, MIDN]. 3x3, pad 1, stride 1 or 2. (MID, MIDN) in {(64, 64), (64, 128), (128, 128)}; midn 0 = mid.
+AI4E_API int ai4e_conv_chain_fwd(const void* x, const void* w2, const void* b2, const void* w3, const void* b3,
+                                 const void* res, void* y, const void* w1n, const void* b1n, void* t1n, int N, int H,
+                                 int W, int ldx, int mid, int midn, int stride, int kpad2, int kpad3, int kpad1n,
+                                 int tile_cfg, const void* x0, int ldx0, hipStream_t stream) {
+  return chain_fwd(false, x, w2, b2, w3, b3, res, y, w1n, b1n, t1n, N, H, W, ldx, mid, midn, stride, kpad2, kpad3,
+                   kpad1n, tile_cfg, x0, ldx0, stream);
+}
+
+// The same chain on fp16 activations and weights (f16 MFMA, fp32 accumulation; tile_cfg ignored).
+AI4E_API int ai4e_conv_chain_f16_fwd(const void* x, const void* w2, const void* b2, const void* w3, const void* b3,
+                                     const void* res, void* y, const void* w1n, const void* b1n, void* t1n, int N, int H,
+                                     int W, int ldx, int mid, int midn, int stride, int kpad2, int kpad3, int kpad1n,
+                                     int tile_cfg, const void* x0, int ldx0, hipStream_t stream) {
+  return chain_fwd(true, x, w2, b2, w3, b3, res, y, w1n, b1n, t1n, N, H, W, ldx, mid, midn, stride, kpad2, kpad3,
+                   kpad1n, tile_cfg, x0, ldx0, stream);
 }
 
 #if AI4E_CHAIN_STAMPS

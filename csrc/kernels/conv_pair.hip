@@ -107,7 +107,7 @@ struct PairParams {
 // (one store chunk and FI / NKC residual loads after each step's MFMAs) instead of a burst between the Y barrier and
 // the C phase: the stamps (profiles/r3_pair/) put 33 % of a wave's life in that burst (vector-memory issue backs up).
 // (Spreading the next pass's B weight fragments over the C steps as well was measured slower: profiles/r3_pair/.)
-template <int MID, int C4, int MIDN, int BM, bool KF = true, bool SP = false>
+template <int MID, int C4, int MIDN, int BM, bool KF = true, bool SP = false, bool F16 = false>
 __global__ __launch_bounds__(512) void conv_pair_kernel(const PairParams p) {
   constexpr int FI = BM / 16;            // pixel fragments
   constexpr int NKB = MID / 32;          // B K steps
@@ -219,7 +219,7 @@ __global__ __launch_bounds__(512) void conv_pair_kernel(const PairParams p) {
       }
       if constexpr (KF) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int i = 0; i < FI; ++i) accb[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[k], fx[k & 1][i], accb[i], 0, 0, 0);
+      for (int i = 0; i < FI; ++i) accb[i] = mfma_16x16x32<F16>(wb[k], fx[k & 1][i], accb[i]);
       if constexpr (KF) __builtin_amdgcn_sched_barrier(0);
     }
 
@@ -229,8 +229,8 @@ __global__ __launch_bounds__(512) void conv_pair_kernel(const PairParams p) {
     for (int i = 0; i < FI; ++i) {
       const uint2 rv = rr[i];
       *reinterpret_cast<uint2*>(ybuf + poff<BM>(16 * i + frow, 16 * w + 4 * lg)) =
-          make_uint2(pack_relu_bf16x2(add_bf16_lo(rv.x, accb[i][0]), add_bf16_hi(rv.x, accb[i][1])),
-                     pack_relu_bf16x2(add_bf16_lo(rv.y, accb[i][2]), add_bf16_hi(rv.y, accb[i][3])));
+          make_uint2(pack_relu2<F16>(add_lo<F16>(rv.x, accb[i][0]), add_hi<F16>(rv.x, accb[i][1])),
+                     pack_relu2<F16>(add_lo<F16>(rv.y, accb[i][2]), add_hi<F16>(rv.y, accb[i][3])));
     }
     pbarrier();  // Y chunk visible (and every wave is past the chunk buffer's previous readers)
     PAIR_STAMP(2);
@@ -274,7 +274,7 @@ __global__ __launch_bounds__(512) void conv_pair_kernel(const PairParams p) {
       for (int i = 0; i < FI; ++i)
 #pragma unroll
         for (int j = 0; j < JC; ++j)
-          accn[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wc[k][j], fy[k & 1][i], accn[i][j], 0, 0, 0);
+          accn[i][j] = mfma_16x16x32<F16>(wc[k][j], fy[k & 1][i], accn[i][j]);
       if constexpr (SP) {
         constexpr int RPS = (FI + NKC - 1) / NKC;  // residual loads per C step
         if (k < NS) copy_out(k);
@@ -296,7 +296,7 @@ __global__ __launch_bounds__(512) void conv_pair_kernel(const PairParams p) {
 #pragma unroll
     for (int j = 0; j < JC; ++j)
       *reinterpret_cast<uint2*>(t2s + poff<BM>(16 * i + frow, (w * JC + j) * 16 + 4 * lg)) =
-          make_uint2(pack_relu_bf16x2(accn[i][j][0], accn[i][j][1]), pack_relu_bf16x2(accn[i][j][2], accn[i][j][3]));
+          make_uint2(pack_relu2<F16>(accn[i][j][0], accn[i][j][1]), pack_relu2<F16>(accn[i][j][2], accn[i][j][3]));
   pbarrier();
   constexpr int NT = BM * MIDN / 8 / 512;
 #pragma unroll
@@ -316,17 +316,17 @@ __global__ __launch_bounds__(512) void conv_pair_kernel(const PairParams p) {
 #endif
 }
 
-template <int MID, int C4, int MIDN, int BM, bool KF = true, bool SP = false>
+template <int MID, int C4, int MIDN, int BM, bool KF = true, bool SP = false, bool F16 = false>
 int launch_pair(const PairParams& p, hipStream_t s) {
   constexpr int LDS = (MID / 32 + 2 * PR_CH / 32 > MIDN / 32 ? MID / 32 + 2 * PR_CH / 32 : MIDN / 32) * kbs<BM>();
   static bool attr = false;
   if (!attr) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(conv_pair_kernel<MID, C4, MIDN, BM, KF, SP>),
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(conv_pair_kernel<MID, C4, MIDN, BM, KF, SP, F16>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, LDS) != hipSuccess)
       return AI4E_ELAUNCH;
     attr = true;
   }
-  hipLaunchKernelGGL((conv_pair_kernel<MID, C4, MIDN, BM, KF, SP>), dim3(ai4e_cdiv(p.M, BM)), dim3(512), LDS, s, p);
+  hipLaunchKernelGGL((conv_pair_kernel<MID, C4, MIDN, BM, KF, SP, F16>), dim3(ai4e_cdiv(p.M, BM)), dim3(512), LDS, s, p);
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
 }
 
@@ -344,6 +344,33 @@ AI4E_API int ai4e_pair_stamps_read(void* host) {
                                                                                                   : AI4E_ELAUNCH;
 }
 #endif
+
+namespace {
+PairParams pair_params(const void* t2, const void* w3p, const void* b3, const void* res, void* y, const void* w1p,
+                       const void* b1n, void* t1n, int M) {
+  PairParams p{};
+  p.t2 = static_cast<const uint16_t*>(t2);
+  p.w3p = static_cast<const uint16_t*>(w3p);
+  p.b3 = static_cast<const float*>(b3);
+  p.res = static_cast<const uint16_t*>(res);
+  p.y = static_cast<uint16_t*>(y);
+  p.w1p = static_cast<const uint16_t*>(w1p);
+  p.b1n = static_cast<const float*>(b1n);
+  p.t1n = static_cast<uint16_t*>(t1n);
+  p.M = M;
+  return p;
+}
+}  // namespace
+
+// fp16 form (the ensemble's crop classifier: f16 MFMA, fp32 accumulation): the default layer3 pair only.
+AI4E_API int ai4e_conv_pair_f16_fwd(const void* t2, const void* w3p, const void* b3, const void* res, void* y,
+                                    const void* w1p, const void* b1n, void* t1n, int M, int mid, int c4, int midn,
+                                    int bm_cfg, hipStream_t stream) {
+  if (!t2 || !w3p || !b3 || !res || !y || !w1p || !b1n || !t1n || M < 0) return AI4E_EINVAL;
+  if (mid != 256 || c4 != 1024 || midn != 256 || (bm_cfg != 0 && bm_cfg != 98)) return AI4E_EINVAL;
+  if (M == 0) return AI4E_OK;
+  return launch_pair<256, 1024, 256, 96, true, true, true>(pair_params(t2, w3p, b3, res, y, w1p, b1n, t1n, M), stream);
+}
 
 AI4E_API int ai4e_conv_pair_fwd(const void* t2, const void* w3p, const void* b3, const void* res, void* y,
                                 const void* w1p, const void* b1n, void* t1n, int M, int mid, int c4, int midn,

@@ -232,7 +232,7 @@ __device__ unsigned long long g_stem_stamps[2048 * 4 * STEM_NSEG];
   } while (0)
 #endif
 
-template <bool U8, bool C1 = false>
+template <bool U8, bool C1 = false, bool F16 = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void stem_pool_direct_kernel(const StemParams p, int ntiles) {
 #if AI4E_STEM_STAMPS
@@ -326,9 +326,9 @@ void stem_pool_direct_kernel(const StemParams p, int ntiles) {
         }
         uint4* d0 = reinterpret_cast<uint4*>(dsm + D_FP + pix * 16);
         uint4* d1 = reinterpret_cast<uint4*>(dsm + D_FP + (FP_STRIDE + pix) * 16);
-        *d0 = make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]), pack_bf16x2(v[6], v[7]));
-        *d1 = make_uint4(pack_bf16x2(v[8], v[9]), pack_bf16x2(v[10], v[11]), pack_bf16x2(v[12], v[13]),
-                         pack_bf16x2(v[14], v[15]));
+        *d0 = make_uint4(pack2<F16>(v[0], v[1]), pack2<F16>(v[2], v[3]), pack2<F16>(v[4], v[5]), pack2<F16>(v[6], v[7]));
+        *d1 = make_uint4(pack2<F16>(v[8], v[9]), pack2<F16>(v[10], v[11]), pack2<F16>(v[12], v[13]),
+                         pack2<F16>(v[14], v[15]));
       }
     }
     // this tile's footprint landed. From the second tile on (C1) the DMA is already complete: the previous
@@ -365,7 +365,7 @@ void stem_pool_direct_kernel(const StemParams p, int ntiles) {
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[j], fx[i], acc[i][j], 0, 0, 0);
+          acc[i][j] = mfma_16x16x32<F16>(fw[j], fx[i], acc[i][j]);
     }
     STEM_STAMP(1);  // MFMA loop
     if constexpr (!U8) {
@@ -385,8 +385,8 @@ void stem_pool_direct_kernel(const StemParams p, int ntiles) {
         const float4 b = bias[j];
         uint2 v = make_uint2(0u, 0u);
         if (live)
-          v = make_uint2(pack_bf16x2(fmaxf(acc[i][j][0] + b.x, 0.f), fmaxf(acc[i][j][1] + b.y, 0.f)),
-                         pack_bf16x2(fmaxf(acc[i][j][2] + b.z, 0.f), fmaxf(acc[i][j][3] + b.w, 0.f)));
+          v = make_uint2(pack2<F16>(fmaxf(acc[i][j][0] + b.x, 0.f), fmaxf(acc[i][j][1] + b.y, 0.f)),
+                         pack2<F16>(fmaxf(acc[i][j][2] + b.z, 0.f), fmaxf(acc[i][j][3] + b.w, 0.f)));
         *reinterpret_cast<uint2*>(tile + ptile(m, n >> 3) + ((((n >> 2) ^ (m >> 3)) & 1) << 3)) = v;
       }
     }
@@ -463,7 +463,7 @@ void stem_pool_direct_kernel(const StemParams p, int ntiles) {
         const bf16x8_t fx = *reinterpret_cast<const bf16x8_t*>(tile + ks * 64 * 64 + r * 64 +
                                                                (((lane >> 4) ^ swz(r)) << 4));
 #pragma unroll
-        for (int j = 0; j < 4; ++j) a1[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1f[j][ks], fx, a1[j], 0, 0, 0);
+        for (int j = 0; j < 4; ++j) a1[j] = mfma_16x16x32<F16>(w1f[j][ks], fx, a1[j]);
       }
       const int py = r / SP_TC, px = r - py * SP_TC;
       const int ph = ph0 + py, pw = pw0 + px;
@@ -472,7 +472,7 @@ void stem_pool_direct_kernel(const StemParams p, int ntiles) {
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           *reinterpret_cast<uint2*>(dst + 16 * j) =
-              make_uint2(pack_relu_bf16x2(a1[j][0], a1[j][1]), pack_relu_bf16x2(a1[j][2], a1[j][3]));
+              make_uint2(pack_relu2<F16>(a1[j][0], a1[j][1]), pack_relu2<F16>(a1[j][2], a1[j][3]));
       }
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // pooled rows read before the next epilogue
     }
@@ -487,11 +487,11 @@ void stem_pool_direct_kernel(const StemParams p, int ntiles) {
 #endif
 }
 
-template <bool U8, bool C1 = false>
+template <bool U8, bool C1 = false, bool F16 = false>
 int launch_direct(const StemParams& p, long nb, hipStream_t stream) {
   static bool attr = false;
   if (!attr) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(stem_pool_direct_kernel<U8, C1>),
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(stem_pool_direct_kernel<U8, C1, F16>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, D_LDS) != hipSuccess)
       return AI4E_ELAUNCH;
     attr = true;
@@ -507,7 +507,7 @@ int launch_direct(const StemParams& p, long nb, hipStream_t stream) {
     return v < 1 ? 1L : v;
   }();
   const long grid = nb < wpc * cus ? nb : wpc * cus;
-  hipLaunchKernelGGL((stem_pool_direct_kernel<U8, C1>), dim3(static_cast<unsigned>(grid)), dim3(256), D_LDS, stream, p,
+  hipLaunchKernelGGL((stem_pool_direct_kernel<U8, C1, F16>), dim3(static_cast<unsigned>(grid)), dim3(256), D_LDS, stream, p,
                      static_cast<int>(nb));
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
 }
@@ -558,9 +558,9 @@ AI4E_API int ai4e_stem_pool_u8_fwd(const void* img, const void* w, const void* b
 // Stem + pool + the first bottleneck's 1x1 c1 (64 -> 64, bias, ReLU) in one launch: y as ai4e_stem_pool_fwd,
 // plus t1 [N, PH, PW, 64] = relu(y . W1^T + b1) (w1 [>= 64 rows, kpad1 >= 64] bf16, b1 [>= 64] fp32), computed
 // from the pooled tile while it is still in LDS (no re-read of y, no separate launch).
-AI4E_API int ai4e_stem_pool_c1_fwd(const void* x, const void* w, const void* bias, void* y, const void* w1,
-                                   const void* b1, void* t1, int kpad1, int N, int H, int W, int kpad,
-                                   hipStream_t stream) {
+namespace {
+int stem_c1(bool f16, const void* x, const void* w, const void* bias, void* y, const void* w1, const void* b1, void* t1,
+            int kpad1, int N, int H, int W, int kpad, hipStream_t stream) {
   if (!x || !w || !bias || !y || !w1 || !b1 || !t1 || kpad < 256 || kpad % 8 || kpad1 < 64 || kpad1 % 8 || H <= 0 ||
       W <= 0)
     return AI4E_EINVAL;
@@ -583,7 +583,22 @@ AI4E_API int ai4e_stem_pool_c1_fwd(const void* x, const void* w, const void* bia
   p.tiles_c = ai4e_cdiv(p.PW, SP_TC);
   const long nb = static_cast<long>(N) * p.tiles_r * p.tiles_c;
   if (nb <= 0) return AI4E_OK;
-  return launch_direct<false, true>(p, nb, stream);
+  return f16 ? launch_direct<false, true, true>(p, nb, stream) : launch_direct<false, true>(p, nb, stream);
+}
+}  // namespace
+
+AI4E_API int ai4e_stem_pool_c1_fwd(const void* x, const void* w, const void* bias, void* y, const void* w1,
+                                   const void* b1, void* t1, int kpad1, int N, int H, int W, int kpad,
+                                   hipStream_t stream) {
+  return stem_c1(false, x, w, bias, y, w1, b1, t1, kpad1, N, H, W, kpad, stream);
+}
+
+// The same on fp16 input / weights / outputs (f16 MFMA, fp32 accumulation; the max-pool's unsigned 16-bit max
+// orders non-negative fp16 exactly as it does bf16).
+AI4E_API int ai4e_stem_pool_c1_f16_fwd(const void* x, const void* w, const void* bias, void* y, const void* w1,
+                                       const void* b1, void* t1, int kpad1, int N, int H, int W, int kpad,
+                                       hipStream_t stream) {
+  return stem_c1(true, x, w, bias, y, w1, b1, t1, kpad1, N, H, W, kpad, stream);
 }
 
 // x: s2d stem input [N, H, W, 16] bf16; w: packed 4x4x16 stem weights [>= 64 rows, kpad >= 256] (pad 1/2,
