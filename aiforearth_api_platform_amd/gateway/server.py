@@ -53,6 +53,7 @@ def valid_task_id(tid: str) -> bool:
     ASCII characters (the wire carries ids as fixed-length byte strings, runtime/protocol.py)."""
     return 0 < len(tid) <= 128 and tid.isascii() and tid.isprintable()
 BATCH_CONTENT_TYPE = "application/x-ai4e-batch"
+MAX_BODY = 1 << 30  # request-body cap (aiohttp client_max_size; the native front-end applies the same one)
 
 
 @dataclass
@@ -119,7 +120,7 @@ class Gateway:
         self.on_drain: List[Callable[[], None]] = []
         self._stopped = threading.Event()
         self._session: Optional[ClientSession] = None
-        self.app = web.Application(client_max_size=1 << 30, middlewares=[self._key_middleware])
+        self.app = web.Application(client_max_size=MAX_BODY, middlewares=[self._key_middleware])
         self.app.router.add_get("/", self.health)
         self.app.router.add_get("/openapi.json", self.openapi)
         self.app.router.add_get("/metrics", self.metrics)
@@ -295,9 +296,10 @@ class Gateway:
             return web.json_response({"message": "Service is busy, please try again later."}, status=429)
         if route.content_types and request.content_type not in route.content_types:
             return web.json_response({"message": f"Content-type must be {route.content_types}"}, status=401)
-        if route.max_content_length and (request.content_length or 0) > route.max_content_length:
+        limit = min(route.max_content_length or MAX_BODY, MAX_BODY)
+        if (request.content_length or 0) > limit:  # declared length: answered before any of the body is read
             return web.json_response({"message": f"Request content too large ({request.content_length}). Must be "
-                                                 f"smaller than: {route.max_content_length}"}, status=413)
+                                                 f"smaller than: {limit}"}, status=413)
         return None
 
     async def dispatch(self, request):

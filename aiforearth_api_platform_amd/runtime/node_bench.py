@@ -58,13 +58,15 @@ class Client:
             self.step()
 
 
-def http_phase(cp, pool, seconds: float, batch: int, item_shape, path: str, frontends: int = 0) -> dict:
+def http_phase(cp, pool, seconds: float, batch: int, item_shape, path: str, frontends: int = 0,
+               tls: bool = False) -> dict:
     """REST ingest on this node: aiohttp gateway (this process) + binary batch route (streamed into the
     payload ring), then single-image requests. ``frontends``: ingest front-end processes sharing the port
     (native C++ ``ai4e_ingestd`` by default, AI4E_FRONTEND_IMPL=python for runtime/frontend.py; the pool needs
     as many partitions). Load: the C++ generator (runtime/http_load.py ``run_native_clients``) in separate
     processes; the record carries the client and server CPU seconds, so a reader can see which side was
-    the ceiling."""
+    the ceiling. ``tls``: the front-ends terminate TLS (OpenSSL in ``ai4e_ingestd``, the test certificate under
+    tests/fixtures) and every client connection is an HTTPS session."""
     import asyncio
 
     from aiohttp import web
@@ -109,11 +111,18 @@ def http_phase(cp, pool, seconds: float, batch: int, item_shape, path: str, fron
     spawn = spawn_frontends
     if impl == "native":
         from .native_frontend import spawn_native_frontends as spawn
+    sec = None
+    if tls:
+        if not frontends or impl != "native":
+            raise ValueError("the HTTPS phase needs native front-ends (they terminate TLS)")
+        fx = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))), "tests",
+                          "fixtures")
+        sec = {"tls_cert": os.path.join(fx, "tls_test_cert.pem"), "tls_key": os.path.join(fx, "tls_test_key.pem")}
     fe = spawn(frontends, {"bench": ep}, [{"prefix": "/v1/bench/async", "mode": "async", "endpoint": "bench"}],
-               "127.0.0.1", port, f"http://127.0.0.1:{socks[1].getsockname()[1]}") if frontends else []
+               "127.0.0.1", port, f"http://127.0.0.1:{socks[1].getsockname()[1]}", security=sec) if frontends else []
     if fe:
         time.sleep(5.0 if impl != "native" else 1.0)  # they start and bind the shared port
-    url = f"http://127.0.0.1:{port}/v1/bench/async"
+    url = f"{'https' if tls else 'http'}://127.0.0.1:{port}/v1/bench/async"
     rng = np.random.default_rng(7)
     img = rng.integers(0, 256, tuple(item_shape), dtype=np.uint8)
     batch_body = np.broadcast_to(img, (batch, *img.shape)).tobytes()
@@ -159,6 +168,7 @@ def http_phase(cp, pool, seconds: float, batch: int, item_shape, path: str, fron
         out[name] = {"images": len(ids), "images_per_s": round(len(ids) / dt, 1), "connections": procs * conc,
                      "client_processes": procs, "client": "c++ ai4e_http_load" if native else "python aiohttp",
                      "ingest_frontends": len(fe), "frontend_impl": impl if fe else None, "errors": errors,
+                     "scheme": "https" if tls else "http",
                      "p50_task_latency_ms": round(percentile(lat, 50) * 1e3, 3),
                      "p99_task_latency_ms": round(percentile(lat, 99) * 1e3, 3),
                      "server_cpu_s": round(server_cpu() - c0, 3), "window_s": round(dt, 3)}
@@ -371,6 +381,13 @@ def run_node_bench(args, spec, path: str, metric: str, unit: str = "images/s", c
                     http["with_frontends"] = http_phase(cp, pool, args.http_seconds, B, spec.item_shape, path, nfe)
             except Exception as e:  # the headline number stands on its own
                 http = {"error": repr(e)}
+            nfe = getattr(args, "http_frontends", 0)
+            if getattr(args, "http_tls", 0) and nfe and isinstance(http, dict) and "error" not in http:
+                try:
+                    http["with_frontends_tls"] = http_phase(cp, pool, args.http_seconds, B, spec.item_shape, path,
+                                                            nfe, tls=True)
+                except Exception as e:
+                    http["with_frontends_tls"] = {"error": repr(e)}
         workers = [{k: w.get(k) for k in ("rank", "images", "batches", "pinned", "hbm_used", "gpu_busy_ms", "gfx_mhz",
                                           "power_w")}
                    for w in stats.get("workers", [])]

@@ -384,3 +384,30 @@ def test_native_frontend_tls_and_body_limits(tmp_path):
             proc.wait(20)
         except subprocess.TimeoutExpired:
             proc.kill()
+
+
+def test_bench_http_phase_over_tls():
+    """bench.py's REST phase over HTTPS: native front-ends terminate TLS with the fixture certificate and the C++
+    load generator drives HTTPS sessions into both the batch and the single-image route (CPU worker)."""
+    from aiforearth_api_platform_amd.config import Config
+    from aiforearth_api_platform_amd.gateway.control import ControlPlane
+    from aiforearth_api_platform_amd.runtime import native_frontend
+    from aiforearth_api_platform_amd.runtime.node_bench import http_phase
+    from aiforearth_api_platform_amd.runtime.worker_pool import ModelSpec, WorkerPool
+
+    if not native_frontend.available():
+        pytest.skip("ai4e_ingestd not built")
+    shape = (4, 4, 3)
+    spec = ModelSpec("aiforearth_api_platform_amd.models.toy:tiny_classifier", shape, max_batch=8, topk=2,
+                     use_graphs=False)
+    cp = ControlPlane(Config.load(env={}))
+    ep = "http://127.0.0.1/v1/bench/async"
+    pool = WorkerPool(cp, ep, spec, ["cpu"], max_delay_s=0.001, frontends=2, frontend_slots=64).start(120)
+    try:
+        out = http_phase(cp, pool, 2.0, 4, shape, ep, frontends=2, tls=True)
+    finally:
+        pool.stop()
+        cp.close()
+    for name in ("batch_route", "single_image_route"):
+        r = out[name]
+        assert r["scheme"] == "https" and r["errors"] == 0 and r["images"] > 0, r

@@ -254,3 +254,28 @@ def test_https_platform_with_frontend_parity(tmp_path):
             proc.wait(20)
         except subprocess.TimeoutExpired:
             proc.kill()
+
+
+def test_gateway_refuses_oversized_declared_length():
+    """A declared Content-Length above the route's max_content_length — or, with none set, above the global 1 GiB
+    body cap — is answered 413 from the headers, before any of the body is read (the native front-end's rule)."""
+    cp, gw = _gateway("")
+
+    async def go():
+        c = TestClient(TestServer(gw.app))
+        await c.start_server()
+        try:
+            r, w = await asyncio.open_connection("127.0.0.1", c.server.port)
+            w.write(b"POST /v1/open HTTP/1.1\r\nHost: x\r\nContent-Type: application/json\r\n"
+                    b"Content-Length: 999999999999\r\n\r\n")
+            await w.drain()
+            head = await asyncio.wait_for(r.readline(), 10)
+            w.close()
+            assert b" 413 " in head
+            ok = await c.post("/v1/open", data=json.dumps({"a": 1}), headers={"Content-Type": "application/json"})
+            assert ok.status == 200
+        finally:
+            await c.close()
+
+    run(go())
+    cp.close()

@@ -20,11 +20,12 @@ def test_native_core_is_tsan_clean(tmp_path):
 
 @pytest.mark.slow
 @pytest.mark.skipif(shutil.which("g++") is None, reason="needs g++ with -fsanitize=thread")
-@pytest.mark.parametrize("san", ["thread", "address"])
-def test_native_ingest_frontend_sanitizers(tmp_path, san):
+@pytest.mark.parametrize("san,tls", [("thread", False), ("address", False), ("thread", True), ("address", True)])
+def test_native_ingest_frontend_sanitizers(tmp_path, san, tls):
     """ai4e_ingestd built with -fsanitize=thread / address behind the CPU platform: concurrent keep-alive
-    batch + single-image ingest from the C++ load generator, proxied task queries and fresh-connection admission
-    errors; the sanitizer must report nothing."""
+    batch + single-image ingest from the C++ load generator, proxied task queries, fresh-connection admission
+    errors and an oversized Content-Length (413); plain HTTP and TLS (OpenSSL sessions in the connection threads);
+    the sanitizer must report nothing."""
     import sys
     import time
 
@@ -36,7 +37,7 @@ def test_native_ingest_frontend_sanitizers(tmp_path, san):
 
     binary = str(tmp_path / f"ingestd_{san}")
     r = subprocess.run(["g++", "-O1", "-g", f"-fsanitize={san}", "-std=c++17", "-pthread",
-                        os.path.join(ROOT, "csrc", "ingest", "ingestd.cpp"), "-o", binary, "-lrt"],
+                        os.path.join(ROOT, "csrc", "ingest", "ingestd.cpp"), "-o", binary, "-lrt", "-lssl", "-lcrypto"],
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]
     doc = yaml.safe_load(open(os.path.join(ROOT, "examples", "platform_cpu.yaml")))
@@ -51,13 +52,30 @@ def test_native_ingest_frontend_sanitizers(tmp_path, san):
     log = tmp_path / "serve.log"
     env = dict(os.environ, PYTHONPATH=ROOT, AI4E_FRONTEND_PROCESSES="2", AI4E_FRONTEND_IMPL="native",
                AI4E_INGESTD=binary, TSAN_OPTIONS="report_signal_unsafe=0", ASAN_OPTIONS="detect_leaks=0")
+    if tls:
+        fx = os.path.join(ROOT, "tests", "fixtures")
+        env.update(AI4E_TLS_CERT=os.path.join(fx, "tls_test_cert.pem"), AI4E_TLS_KEY=os.path.join(fx, "tls_test_key.pem"))
     proc = subprocess.Popen([sys.executable, "-m", "aiforearth_api_platform_amd.serve", "--config", str(cfgp),
                              "--port", str(port)], cwd=ROOT, env=env, stdout=open(log, "w"), stderr=subprocess.STDOUT)
-    base = f"http://127.0.0.1:{port}"
+    base = f"{'https' if tls else 'http'}://127.0.0.1:{port}"
+    import ssl
+    import urllib3
+
+    urllib3.disable_warnings()
+    ctx = ssl.create_default_context()
+    ctx.check_hostname, ctx.verify_mode = False, ssl.CERT_NONE
+
+    def oversized() -> bytes:
+        raw = socket.create_connection(("127.0.0.1", port), timeout=10)
+        c = ctx.wrap_socket(raw) if tls else raw
+        with c:
+            c.sendall(b"POST /v1/tiny/async HTTP/1.1\r\nHost: x\r\nContent-Type: application/octet-stream\r\n"
+                      b"Content-Length: 999999999999\r\n\r\n")
+            return c.recv(256)
     try:
         for _ in range(600):
             try:
-                if requests.get(base + "/", timeout=1).status_code == 200:
+                if requests.get(base + "/", timeout=1, verify=False).status_code == 200:
                     break
             except requests.ConnectionError:
                 time.sleep(0.1)
@@ -68,10 +86,12 @@ def test_native_ingest_frontend_sanitizers(tmp_path, san):
         b = run_native_clients(url, 1.5, 8, img.tobytes(), "application/octet-stream", procs=2)
         assert a["errors"] == 0 and b["errors"] == 0 and a["ids"] and b["ids"]
         for _ in range(20):  # fresh connections: proxied queries and admission errors through any listener
-            assert requests.get(f"{base}/v1/taskmanagement/task/{b['ids'][0]}",
+            assert requests.get(f"{base}/v1/taskmanagement/task/{b['ids'][0]}", verify=False,
                                 headers={"Connection": "close"}).status_code == 200
-            assert requests.post(url, data=b"\x00" * 50, headers={"Content-Type": "application/x-ai4e-batch",
-                                                                  "Connection": "close"}).status_code == 400
+            assert requests.post(url, data=b"\x00" * 50, verify=False,
+                                 headers={"Content-Type": "application/x-ai4e-batch",
+                                          "Connection": "close"}).status_code == 400
+            assert b" 413 " in oversized()
     finally:
         proc.terminate()
         try:
