@@ -1,6 +1,10 @@
 """Per-dispatch PMC summary of one eager ResNet-50 forward (tools/pmc_resnet.sh output).
 
     python tools/pmc_summary.py gpurun_out/pmc [> profiles/.../pmc_summary.txt]
+    python tools/pmc_summary.py gpurun_out/pmc_detector --start spin_kernel --by-kernel
+
+``--start NAME``: the forward begins after the last dispatch whose name contains NAME (default: at the last
+``preprocess`` launch); ``--by-kernel``: one line per kernel name (summed over its dispatches, sorted by time).
 
 Joins the counter passes by dispatch order (the profiled program is deterministic), keeps the last
 forward (from the last preprocess launch on), and prints per dispatch: duration, MFMA busy fraction
@@ -32,7 +36,14 @@ def short(n):
 
 
 def main():
-    d = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
+    import argparse
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("dir", nargs="?", default="gpurun_out/pmc")
+    ap.add_argument("--start", default="")
+    ap.add_argument("--by-kernel", action="store_true")
+    a = ap.parse_args()
+    d = a.dir
     passes = [load(p) for p in sorted(glob.glob(os.path.join(d, "pass*_counter_collection.csv")))]
     n = min(len(p) for p in passes)
     rows = []
@@ -42,8 +53,20 @@ def main():
             r.update({k: v for k, v in p[i].items() if k not in r or k not in ("t",)})
         r["t"] = min(p[i]["t"] for p in passes)
         rows.append(r)
-    starts = [i for i, r in enumerate(rows) if "preprocess" in r["name"]]
-    seg = rows[starts[-1]:]
+    if a.start:
+        seg = rows[[i for i, r in enumerate(rows) if a.start in r["name"]][-1] + 1:]
+    else:
+        seg = rows[[i for i, r in enumerate(rows) if "preprocess" in r["name"]][-1]:]
+    if a.by_kernel:
+        agg = collections.OrderedDict()
+        for r in seg:
+            k = short(r["name"])
+            g = agg.setdefault(k, {"name": r["name"], "grid": r["grid"], "t": 0.0, "n": 0})
+            g["n"] += 1
+            for key, v in r.items():
+                if key not in ("name", "grid"):
+                    g[key] = g.get(key, 0.0) + v if key != "n" else g[key]
+        seg = sorted(agg.values(), key=lambda g: -g["t"])
     print(f"{'us':>7} {'mfma%':>6} {'HBM MB':>8} {'TB/s':>5} {'L2hit%':>6} {'ldsconf%':>8} {'wait%':>6}  kernel")
     tot_t = tot_b = 0.0
     for r in seg:
@@ -60,7 +83,8 @@ def main():
         tot_t += t
         tot_b += b
         print(f"{t:7.1f} {mfma:6.1f} {b / 1e6:8.1f} {b / t / 1e6 if t else 0:5.2f} "
-              f"{100 * hit / (hit + miss) if hit + miss else 0:6.1f} {conf:8.1f} {wait:6.1f}  {short(r['name'])} g{r['grid']}")
+              f"{100 * hit / (hit + miss) if hit + miss else 0:6.1f} {conf:8.1f} {wait:6.1f}  {short(r['name'])} "
+              + (f"x{r['n']}" if a.by_kernel else f"g{r['grid']}"))
     print(f"total {tot_t:.1f} us, {tot_b / 1e9:.2f} GB HBM-side")
 
 
