@@ -69,12 +69,16 @@ __global__ __launch_bounds__(256) void gn_stats_kernel(const uint16_t* __restric
   }
   // every lane's 8 channel sums go to LDS; one thread per group then adds its group's (pixel row, channel)
   // terms in a fixed order, so the partials (and everything normalized by them) are bitwise reproducible
-  // run to run (LDS float atomics would add in arrival order)
-  __shared__ float rs[256 * 8], rq[256 * 8];
+  // run to run (LDS float atomics would add in arrival order). Layout [channel-in-vector j][thread], rows padded
+  // to 257 floats: the stores are lane-contiguous (conflict-free; [thread][j] put 8 lanes on each bank, 73 % of the
+  // kernel's LDS cycles were bank conflicts, profiles/r4_unet/pmc_by_kernel.txt) and a group's reads fall <= 2 lanes
+  // per bank for every C this kernel takes. Same addition order as before: bitwise-identical partials.
+  constexpr int RS = 257;
+  __shared__ float rs[8 * RS], rq[8 * RS];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    rs[threadIdx.x * 8 + j] = s[j];
-    rq[threadIdx.x * 8 + j] = q[j];
+    rs[j * RS + threadIdx.x] = s[j];
+    rq[j * RS + threadIdx.x] = q[j];
   }
   __syncthreads();
   if (static_cast<int>(threadIdx.x) < G) {
@@ -83,8 +87,8 @@ __global__ __launch_bounds__(256) void gn_stats_kernel(const uint16_t* __restric
     for (int pp = 0; pp < pix_per_iter; ++pp)
       for (int ch = g * cg; ch < (g + 1) * cg; ++ch) {
         const int t = pp * lanes_per_pix + (ch >> 3);
-        S += rs[t * 8 + (ch & 7)];
-        Q += rq[t * 8 + (ch & 7)];
+        S += rs[(ch & 7) * RS + t];
+        Q += rq[(ch & 7) * RS + t];
       }
     float* o = partials + ((static_cast<long>(n) * nchunks + chunk) * G + g) * GN_PARTIAL;
     *reinterpret_cast<float4*>(o) = make_float4(S, Q, gk[g], 0.f);
