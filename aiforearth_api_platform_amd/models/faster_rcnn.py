@@ -23,7 +23,9 @@ import torch
 import torch.nn as nn
 
 from ..ops.conv import PackedConv, conv2d_nhwc, linear_nhwc, pack_conv
-from ..ops.detection import det_decode, nms_batched_sorted, roi_align_fpn, rpn_decode_into
+from ..ops.debug import crumb
+from ..ops.detection import (argsort_desc_rows, det_decode, nms_batched_sorted, roi_align_fpn, rpn_decode_into,
+                              rpn_topk)
 from ..ops.pool import maxpool2d_nhwc, preprocess_s2d_u8, preprocess_u8
 from .resnet import FusedResNet, resnet50
 
@@ -146,17 +148,19 @@ class FasterRCNN:
         for li, (p, k) in enumerate(zip(P, ks)):
             t = conv2d_nhwc(p, self.rpn_conv, relu=True)
             head = conv2d_nhwc(t, self.rpn_head)                   # [B, h, w, 16]: A logits, 4A deltas
-            _, idx = head[..., :A].reshape(B, -1).topk(k, dim=1)  # per-level pre-NMS top-k
+            idx = rpn_topk(head, A, k)                            # per-level pre-NMS top-k
             # decode + clip + sigmoid + min-size mask straight into the all-level buffers (one HIP launch)
+            crumb(f"rpn.topk{li}", idx)
             rpn_decode_into(head, idx, anchors[li], A, boxes, scores, lvl, off, li, img_hw, cfg.rpn_min_size)
             off += k
         # batched NMS across levels via coordinate offsets; invalid (small) boxes sort last
-        order = scores.argsort(dim=1, descending=True)
+        order = argsort_desc_rows(scores)
         boxes_s = torch.gather(boxes, 1, order[..., None].expand_as(boxes))
         scores_s = torch.gather(scores, 1, order)
         off = torch.gather(lvl, 1, order)[..., None] * (max(img_hw) + 1.0)
         valid = (scores_s >= 0).sum(1).to(torch.int32)
         keep, count = nms_batched_sorted(boxes_s + off, cfg.rpn_nms_thresh, cfg.post_nms_top_n, valid)
+        crumb("rpn.nms", keep)
         keep_l = keep.clamp(min=0).long()
         props = torch.gather(boxes_s, 1, keep_l[..., None].expand(B, keep.shape[1], 4))
         pad = (keep < 0)[..., None]
@@ -170,6 +174,7 @@ class FasterRCNN:
         rois = torch.cat([bidx, props], -1).reshape(B * R, 5)
         strides = [img_hw[0] // p.shape[1] for p in P[:4]]
         feats = roi_align_fpn(P[:4], [1.0 / s for s in strides], rois, (7, 7), 2)  # [B*R, 7, 7, C]
+        crumb("box.roi_align", feats)
         x = feats.reshape(B * R, 1, 1, -1)
         fc = linear_nhwc if self.fc_blas else conv2d_nhwc  # FCs as library GEMMs (AI4E_DET_FC_BLAS=0: K1)
         x = fc(x, self.fc6, relu=True)
@@ -190,6 +195,7 @@ class FasterRCNN:
         valid = (s_s >= 0).sum(1).to(torch.int32)
         off = l_s[..., None].float() * (max(img_hw) + 1.0)
         keep, ndet = nms_batched_sorted(b_s + off, cfg.box_nms_thresh, cfg.detections_per_img, valid)
+        crumb("post.nms", keep)
         k = keep.clamp(min=0).long()
         det_boxes = torch.gather(b_s, 1, k[..., None].expand(B, k.shape[1], 4))
         det_scores = torch.gather(s_s, 1, k)
@@ -201,9 +207,14 @@ class FasterRCNN:
         """x normalized NHWC [B, H, W, 8] (H, W multiples of 64). Returns padded detections:
         boxes [B, D, 4], scores [B, D], labels [B, D], counts [B]."""
         img_hw = (x.shape[1], x.shape[2]) if x.shape[-1] != 16 else (2 * x.shape[1], 2 * x.shape[2])
-        P = self.fpn(self.backbone_stages(x))
+        feats = self.backbone_stages(x)
+        crumb("backbone", feats[-1])
+        P = self.fpn(feats)
+        crumb("fpn", P[-1])
         props, count = self.proposals(P, img_hw)
-        return self.postprocess(props, count, self.box_head(P, props, img_hw), img_hw)
+        pred = self.box_head(P, props, img_hw)
+        crumb("box.head", pred)
+        return self.postprocess(props, count, pred, img_hw)
 
     def forward_u8(self, img_u8: torch.Tensor):
         return self.forward(preprocess_s2d_u8(img_u8))

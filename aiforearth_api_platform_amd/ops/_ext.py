@@ -58,6 +58,8 @@ _SIGS = {
     "ai4e_nms_mask": [_vp, _c_int, _c_int, _c_float, _vp, _vp],
     "ai4e_nms_reduce": [_vp, _vp, _c_int, _c_int, _c_int, _vp, _vp, _vp],
     "ai4e_rpn_decode": [_vp] * 6 + [_c_int] * 7 + [_c_float] * 5 + [_vp],
+    "ai4e_row_sort_desc": [_vp, _c_int, _c_int, _vp, _vp],
+    "ai4e_rpn_topk": [_vp] + [_c_int] * 5 + [_vp, _vp],
     "ai4e_det_decode": [_vp] * 6 + [_c_int] * 4 + [_vp] + [_c_float] * 4 + [_vp],
     "ai4e_roi_align_nhwc": [_vp, _vp, _vp] + [_c_int] * 7 + [_c_float, _c_int, _c_int, _vp],
     "ai4e_roi_align_fpn_nhwc": [_vp] * 8 + [_c_int] * 6 + [_vp],
@@ -67,6 +69,8 @@ _SIGS = {
     "ai4e_stream_destroy": [_vp],
     "ai4e_stream_get_cu_mask": [_vp, _vp, _c_int],
     "ai4e_cu_census": [_vp, _c_int, _c_int, _vp],
+    "ai4e_crumbs_alloc": [_c_int, _vp, _vp],
+    "ai4e_crumb": [_vp, _c_int, _vp],
 }
 
 

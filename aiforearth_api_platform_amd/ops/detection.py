@@ -75,6 +75,36 @@ def rpn_decode_into(head: torch.Tensor, idx: torch.Tensor, anchors: torch.Tensor
     lvl[:, off:off + k] = float(level)
 
 
+def argsort_desc_rows(scores: torch.Tensor) -> torch.Tensor:
+    """``scores.argsort(1, descending=True)`` for fp32 [B, N] rows; HIP (N <= 8192): one workgroup per row, a bitonic
+    network in LDS, ties in index order (deterministic), no library temporaries (graph-safe, profiles/r4_replay/)."""
+    B, N = scores.shape
+    if _ext.backend_for(scores) == "hip" and scores.dtype == torch.float32 and N <= 8192:
+        s = scores.contiguous()
+        order = torch.empty(B, N, dtype=torch.long, device=scores.device)
+        _ext.call("ai4e_row_sort_desc", s.data_ptr(), B, N, order.data_ptr(), _ext.stream_ptr(scores.device))
+        return order
+    return scores.argsort(dim=1, descending=True, stable=True)
+
+
+def rpn_topk(head: torch.Tensor, num_anchors: int, k: int) -> torch.Tensor:
+    """Flat indices ``pos * A + a`` [B, k] (int64) of the k largest objectness logits of one FPN level, read straight
+    from the RPN head bf16 [B, h, w, >= A] (channels 0..A-1). HIP: one workgroup per image, radix select, a fixed
+    deterministic output order (the proposals are re-sorted by score across levels afterwards) and graph-safe (no
+    library temporaries: torch.topk's multi-block path faulted replaying in a graph, profiles/r4_replay/).
+    Elsewhere: torch.topk (value order)."""
+    B = head.shape[0]
+    hw = head.shape[1] * head.shape[2]
+    if k > hw * num_anchors:
+        raise ValueError(f"rpn_topk: k={k} > {hw * num_anchors} candidates")
+    if _ext.backend_for(head) == "hip" and head.dtype == torch.bfloat16 and head.is_contiguous():
+        idx = torch.empty(B, k, dtype=torch.long, device=head.device)
+        _ext.call("ai4e_rpn_topk", head.data_ptr(), B, hw, head.shape[-1], num_anchors, k, idx.data_ptr(),
+                  _ext.stream_ptr(head.device))
+        return idx
+    return head[..., :num_anchors].reshape(B, -1).topk(k, dim=1)[1]
+
+
 def det_decode(pred: torch.Tensor, props: torch.Tensor, count: torch.Tensor, num_classes: int,
                weights: Sequence[float], img_hw: Tuple[int, int], score_thresh: float,
                clip: float = math.log(1000.0 / 16)) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:

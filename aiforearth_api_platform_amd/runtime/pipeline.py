@@ -29,11 +29,11 @@ from typing import Callable, List, Optional, Sequence, Tuple
 import torch
 import torch.distributed as dist
 
+from ..ops.debug import crumb
 from ..ops.detection import crop_resize_u8
 from ..store import STATE_COMPLETED, STATE_CREATED, STATE_RUNNING
 
 STOP = -1
-_REPLAY_SYNC = os.environ.get("AI4E_GRAPH_REPLAY_SYNC", "1") not in ("0", "off", "")
 
 
 @dataclass
@@ -157,17 +157,12 @@ class _GraphRunner:
             with torch.cuda.graph(graph, stream=s):
                 static_out = self.fn(static_in)
             torch.cuda.synchronize(self.device)
-            g = self.graphs[key] = [graph, static_in, static_out, None]
-        graph, static_in, static_out, done = g
-        if done is not None and _REPLAY_SYNC:
-            # round-3 workaround under investigation (bench/replay_repro.py, tests/test_graph_replay_gpu.py): the
-            # previous replay of this graph finished before it is launched again
-            done.synchronize()
+            g = self.graphs[key] = (graph, static_in, static_out)
+        graph, static_in, static_out = g
+        # stream-ordered: back-to-back replays need no host sync (the round-3/4 replay fault was the library's
+        # multi-block top-k inside the detector graph, now rpn_topk; profiles/r4_replay/, tests/test_graph_replay_gpu.py)
         static_in.copy_(x)
         graph.replay()
-        ev = torch.cuda.Event()
-        ev.record()
-        g[3] = ev
         return static_out
 
 
@@ -212,16 +207,23 @@ class StageGraphPipeline:
 
         b, m = images.shape[0], self.cfg.max_crops_per_image
         dets = self.detector(images)
+        crumb("pipe.detected", dets[0])
         boxes, scores, valid = select_crops_padded(dets, m, self.cfg.score_thresh, self.cfg.class_id)
+        crumb("pipe.selected", boxes)
         img = torch.arange(b, device=boxes.device, dtype=torch.float32)[:, None, None].expand(b, m, 1)
         crops = crop_resize_u8(images[..., :3].contiguous() if images.shape[-1] != 3 else images,
                                torch.cat([img, boxes], -1).reshape(b * m, 5), self.cfg.crop_hw)
+        crumb("pipe.cropped", crops)
         flat = valid.reshape(-1)
-        dst = torch.where(flat, torch.cumsum(flat.int(), 0) - 1, torch.full_like(flat, b * m, dtype=torch.int32))
+        # (a 2-D innermost-dim cumsum: the library's own scan kernel; a 1-D cumsum goes to a device-wide library scan
+        # with temporaries, kept out of captured graphs, profiles/r4_replay/)
+        pos = torch.cumsum(flat.int().reshape(1, -1), 1).reshape(-1) - 1
+        dst = torch.where(flat, pos, torch.full_like(flat, b * m, dtype=torch.int32))
         h, w = self.cfg.crop_hw
         packed = torch.zeros(b * m + 1, h, w, 3, dtype=torch.uint8, device=crops.device)
         packed.index_copy_(0, dst.long(), crops)           # valid crops first, in (image, score) order
         count = flat.sum().reshape(1).to(torch.int64)
+        crumb("pipe.compacted", count)
         return dets, boxes, scores, valid, packed[: b * m].to(self.wire_dtype), count
 
     def _send(self, crops: torch.Tensor, n: int) -> list:

@@ -141,6 +141,130 @@ __global__ __launch_bounds__(256) void rpn_decode_kernel(const uint16_t* __restr
   lvl[o] = level;
 }
 
+// RPN top-k of one FPN level (replaces the logits copy + torch.topk, whose multi-block path is not safe to replay in a
+// HIP graph once other allocations have come and gone between replays: bench/replay_repro.py, profiles/r4_replay/).
+// One 1024-thread workgroup per image reads the A objectness logits per pixel straight from the RPN head (bf16
+// [B, HW, ldh]) and selects the k largest by a two-pass 8-bit radix select on order-preserving 16-bit keys (LDS
+// histograms; NaN above +inf, as torch.topk). Output: the k flat indices pos * A + a (int64, [B, k]) of every key above
+// the k-th largest plus as many of the k-th key's ties as fill k, in a fixed (thread, step) order: deterministic,
+// no global atomics, every write inside [0, k) by construction (the host guarantees k <= HW * A).
+constexpr int TOPK_THREADS = 1024;
+
+__device__ __forceinline__ uint32_t bf16_order_key(uint16_t v) {
+  return (v & 0x8000u) ? (~static_cast<uint32_t>(v) & 0xffffu) : (static_cast<uint32_t>(v) | 0x8000u);
+}
+
+__global__ __launch_bounds__(TOPK_THREADS) void rpn_topk_kernel(const uint16_t* __restrict__ head, int HW, int ldh,
+                                                                int A, int k, long* __restrict__ idx) {
+  const int b = blockIdx.x;
+  const int t = threadIdx.x;
+  const int n = HW * A;
+  const uint16_t* const hb = head + static_cast<long>(b) * HW * ldh;
+  __shared__ int hist[256];
+  __shared__ int sel[3];  // high byte of the k-th key, its low byte, keys above it
+  __shared__ int sg[TOPK_THREADS], se[TOPK_THREADS];
+  auto key_at = [&](int e) __attribute__((always_inline)) {
+    const int pos = e / A;
+    return bf16_order_key(hb[static_cast<long>(pos) * ldh + (e - pos * A)]);
+  };
+  // pass 1: histogram of the high byte
+  if (t < 256) hist[t] = 0;
+  __syncthreads();
+  for (int e = t; e < n; e += TOPK_THREADS) atomicAdd(&hist[key_at(e) >> 8], 1);
+  __syncthreads();
+  if (t == 0) {
+    int cum = 0, d = 255;
+    for (; d > 0 && cum + hist[d] < k; --d) cum += hist[d];
+    sel[0] = d;
+    sel[2] = cum;
+  }
+  __syncthreads();
+  const uint32_t hi = static_cast<uint32_t>(sel[0]);
+  // pass 2: histogram of the low byte among the keys with that high byte
+  if (t < 256) hist[t] = 0;
+  __syncthreads();
+  for (int e = t; e < n; e += TOPK_THREADS) {
+    const uint32_t kk = key_at(e);
+    if ((kk >> 8) == hi) atomicAdd(&hist[kk & 255u], 1);
+  }
+  __syncthreads();
+  if (t == 0) {
+    int cum = sel[2], d = 255;
+    for (; d > 0 && cum + hist[d] < k; --d) cum += hist[d];
+    sel[1] = d;
+    sel[2] = cum;
+  }
+  __syncthreads();
+  const uint32_t T = (hi << 8) | static_cast<uint32_t>(sel[1]);
+  const int gt = sel[2], need = k - gt;  // keys above T; ties of T to take
+  // pass 3: per-thread counts, exclusive scans, then the writes
+  int cg = 0, ce = 0;
+  for (int e = t; e < n; e += TOPK_THREADS) {
+    const uint32_t kk = key_at(e);
+    cg += kk > T;
+    ce += kk == T;
+  }
+  sg[t] = cg;
+  se[t] = ce;
+  __syncthreads();
+  for (int off = 1; off < TOPK_THREADS; off <<= 1) {
+    const int a = t >= off ? sg[t - off] : 0, c = t >= off ? se[t - off] : 0;
+    __syncthreads();
+    sg[t] += a;
+    se[t] += c;
+    __syncthreads();
+  }
+  int og = sg[t] - cg, oe = se[t] - ce;
+  long* const out = idx + static_cast<long>(b) * k;
+  for (int e = t; e < n; e += TOPK_THREADS) {
+    const uint32_t kk = key_at(e);
+    if (kk > T) {
+      out[og++] = e;
+    } else if (kk == T && oe < need) {
+      out[gt + oe++] = e;
+    }
+  }
+}
+
+// Descending sort of every row of fp32 scores [B, N] (N <= 8192) -> order [B, N] int64, ties by lower index first: one
+// 1024-thread workgroup per row runs a bitonic network over next_pow2(N) 64-bit keys (order(score) << 32 | ~index) in LDS.
+// Replaces torch.argsort for the RPN's all-level proposal sort (N = 4300 at 640^2, above the library's in-place small
+// sort, so it went to a multi-kernel library sort with temporaries; kept out of captured graphs, profiles/r4_replay/).
+constexpr int ROWSORT_THREADS = 1024, ROWSORT_MAX = 8192;
+
+__device__ __forceinline__ uint32_t f32_order_key(float f) {
+  const uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+__global__ __launch_bounds__(ROWSORT_THREADS) void row_sort_desc_kernel(const float* __restrict__ scores, int N, int P,
+                                                                       long* __restrict__ order) {
+  __shared__ unsigned long long key[ROWSORT_MAX];
+  const int t = threadIdx.x;
+  const float* const sr = scores + static_cast<long>(blockIdx.x) * N;
+  for (int i = t; i < P; i += ROWSORT_THREADS)  // padding keys are 0: below every real key (whose low word is ~i > 0)
+    key[i] = i < N ? (static_cast<unsigned long long>(f32_order_key(sr[i])) << 32) | (0xffffffffu - static_cast<uint32_t>(i))
+                   : 0ull;
+  __syncthreads();
+  for (int k = 2; k <= P; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = t; i < P; i += ROWSORT_THREADS) {
+        const int l = i ^ j;
+        if (l > i) {
+          const unsigned long long a = key[i], c = key[l];
+          if (((i & k) == 0) ? (a < c) : (a > c)) {  // descending runs where bit k of i is clear
+            key[i] = c;
+            key[l] = a;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  long* const o = order + static_cast<long>(blockIdx.x) * N;
+  for (int i = t; i < N; i += ROWSORT_THREADS) o[i] = static_cast<long>(0xffffffffu - static_cast<uint32_t>(key[i]));
+}
+
 // Box-head postprocess (one thread per (image, RoI, foreground class)): softmax over the RoI's nc logits,
 // the class's box decoded from its proposal with the regression weights, clipped; score -1 unless the RoI
 // is real (r < count[b]), the score clears thresh and the box is at least 1e-2 wide and high.
@@ -497,6 +621,24 @@ AI4E_API int ai4e_rpn_decode(const void* head, const void* idx, const void* anch
                      static_cast<const long*>(idx), static_cast<const float4*>(anchors), static_cast<float4*>(boxes),
                      static_cast<float*>(scores), static_cast<float*>(lvl), B, HW, ldh, A, k, KT, off, level, img_h,
                      img_w, min_size, clip);
+  return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
+}
+
+AI4E_API int ai4e_row_sort_desc(const void* scores, int B, int N, void* order, hipStream_t s) {
+  if (B <= 0 || N <= 0) return AI4E_OK;
+  if (!scores || !order || N > ROWSORT_MAX) return AI4E_EINVAL;
+  int P = 1;
+  while (P < N) P <<= 1;
+  hipLaunchKernelGGL(row_sort_desc_kernel, dim3(B), dim3(ROWSORT_THREADS), 0, s, static_cast<const float*>(scores), N, P,
+                     static_cast<long*>(order));
+  return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
+}
+
+AI4E_API int ai4e_rpn_topk(const void* head, int B, int HW, int ldh, int A, int k, void* idx, hipStream_t s) {
+  if (B <= 0 || k <= 0) return AI4E_OK;
+  if (!head || !idx || A < 1 || ldh < A || k > HW * A || static_cast<long>(HW) * A >= (1L << 31)) return AI4E_EINVAL;
+  hipLaunchKernelGGL(rpn_topk_kernel, dim3(B), dim3(TOPK_THREADS), 0, s, static_cast<const uint16_t*>(head), HW, ldh, A,
+                     k, static_cast<long*>(idx));
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
 }
 

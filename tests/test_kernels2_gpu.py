@@ -208,6 +208,57 @@ def test_rpn_decode_matches_reference(B, h, w, k):
     assert (b1[:, :off] == 7.0).all() and (b1[:, off + k:] == 7.0).all()
 
 
+@pytest.mark.parametrize("B,h,w,k,ties", [(2, 160, 160, 1000, False), (3, 40, 40, 1000, True), (1, 5, 7, 105, False),
+                                           (2, 20, 20, 1, True)])
+def test_rpn_topk_selects_the_k_largest(B, h, w, k, ties):
+    """Graph-safe RPN top-k (radix select, one workgroup per image) vs torch.topk on the fp32 CPU copy: the same
+    multiset of selected values (exact; unique even with ties), distinct in-range indices, every unselected value
+    <= every selected one; and a deterministic output (two calls bitwise equal)."""
+    from aiforearth_api_platform_amd.ops.detection import rpn_topk
+
+    A = 3
+    torch.manual_seed(11)
+    head = torch.randn(B, h, w, 16) * 3
+    if ties:
+        head = head.round()  # a handful of distinct values: many ties at the k-th
+    head[0, 0, 0, 0] = float("-inf")
+    head = head.to(torch.bfloat16)
+    idx = rpn_topk(head.to(DEV), A, k)
+    assert torch.equal(idx, rpn_topk(head.to(DEV), A, k))
+    idx = idx.cpu()
+    logits = head[..., :A].float().reshape(B, -1)
+    ref = logits.topk(k, dim=1)[0]
+    assert idx.shape == (B, k) and int(idx.min()) >= 0 and int(idx.max()) < h * w * A
+    for b in range(B):
+        assert idx[b].unique().numel() == k
+        got = logits[b, idx[b]]
+        assert torch.equal(got.sort(descending=True)[0], ref[b])
+        rest = torch.ones(h * w * A, dtype=torch.bool)
+        rest[idx[b]] = False
+        if rest.any():
+            assert logits[b, rest].max() <= got.min()
+
+
+@pytest.mark.parametrize("B,N", [(32, 4300), (2, 8192), (3, 1), (4, 3000)])
+def test_argsort_desc_rows_matches_sort(B, N):
+    """Graph-safe row sort (bitonic in LDS) vs torch.sort on the CPU: the gathered scores equal the descending sorted
+    values exactly, the order is a permutation, and ties (-1 padding scores, repeated values) come in index order."""
+    from aiforearth_api_platform_amd.ops.detection import argsort_desc_rows
+
+    torch.manual_seed(5)
+    sc = torch.rand(B, N)
+    sc[:, ::7] = -1.0                       # invalid proposals
+    sc[:, 1::11] = 0.5                      # ties
+    order = argsort_desc_rows(sc.to(DEV)).cpu()
+    assert order.shape == (B, N) and order.dtype == torch.long
+    for b in range(B):
+        assert torch.equal(order[b].sort()[0], torch.arange(N))
+        got = sc[b, order[b]]
+        assert torch.equal(got, sc[b].sort(descending=True)[0])
+        same = got[1:] == got[:-1]
+        assert bool((order[b, 1:][same] > order[b, :-1][same]).all())
+
+
 @pytest.mark.parametrize("B,R,nc", [(2, 1000, 4), (3, 37, 7)])
 def test_det_decode_matches_reference(B, R, nc):
     """Fused box-head postprocess (softmax + per-class decode + clip + validity mask) vs its PyTorch form."""
