@@ -7,8 +7,9 @@ one GPU worker process per GPU, per-submission payload writes, torchrun for N > 
   (mosaics/s + p50; the spatial-parallel single-mosaic form is bench/landcover_bench.py);
 * ``--model ensemble``  — config 5 as an API: detector -> species classifier under one TaskId (the
   AddPipelineTask hop), both stages in one HIP graph per GPU; images/s + p50.
-* ``--model ensemble_group --group 8 --classifiers 1`` — config 5 as an N:M stage graph over RCCL: N = group -
-  classifiers detector GPUs take batches from the scheduler, the classifier GPU(s) classify their crops
+* ``--model ensemble_group --group 8 [--classifiers M]`` — config 5 as an N:M stage graph over RCCL: N = group -
+  M detector GPUs take batches from the scheduler, the classifier GPU(s) classify their crops (M defaults to the
+  split ``plan_ensemble`` picks from the measured stage rates: 6:2 at 4 crops per image)
   (``--classifier-dtype fp16`` by default, ``--wire uint8``); ``parallelism: pipeline{N}:{M}``.
 * ``--model landcover_spatial --group k`` — config 4 in its spatial form: each 4096^2 mosaic segmented by k GPUs
   together (tiles split evenly, bands scattered, halo logits over P2P); ``parallelism: spatial{k}``.
@@ -58,7 +59,7 @@ def main():
     ap.add_argument("--http-seconds", type=float, default=6.0)
     ap.add_argument("--json-out", default="")
     ap.add_argument("--group", type=int, default=2, help="GPUs per worker group (ensemble_group, landcover_spatial)")
-    ap.add_argument("--classifiers", type=int, default=1,
+    ap.add_argument("--classifiers", type=int, default=0,
                     help="classifier GPUs of an ensemble_group; 0 = the split runtime/pipeline.py plan_ensemble picks "
                          "from the measured stage rates (--stage-rates) at --crops-per-image")
     ap.add_argument("--stage-rates", default=os.path.join(ROOT, "profiles", "r4_stage_rates", "stage_rates.json"))
