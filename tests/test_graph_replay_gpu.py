@@ -45,3 +45,29 @@ def test_detector_stage_graph_back_to_back_replays_match_eager():
             assert torch.equal(a, c), name
     assert int(last[-1]) == int(last[6].sum()) > 0
     assert all(int(k[0]) == i for i, k in enumerate(keep))     # and the graph wrote nothing into eager memory
+
+
+def test_breadcrumbs_count_graph_replays():
+    """The fault-locating breadcrumbs (ops/debug.py): counters bumped by kernels inside a captured graph read back
+    from host-mapped memory without a copy — one per eager call and one per replay, in stream order."""
+    from aiforearth_api_platform_amd.ops.debug import Breadcrumbs
+
+    c = Breadcrumbs(8)
+    dev = torch.device(DEV)
+    x = torch.ones(1024, device=dev)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        c.mark("a", dev)
+        y = x * 2
+        c.mark("b", dev)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        c.mark("a", dev)
+        y = x * 2
+        c.mark("b", dev)
+    for _ in range(5):
+        g.replay()
+    torch.cuda.synchronize()
+    assert c.read() == {"a": 6, "b": 6} and float(y[0]) == 2.0
