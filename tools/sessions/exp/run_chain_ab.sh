@@ -1,4 +1,4 @@
-# chain_tune timings (B=250) with the default kernel library and experiment libraries (tools/exp/*.so)
+# chain_tune timings (B=250) with the default kernel library and experiment libraries (tools/sessions/exp/*.so)
 set -o pipefail
 mkdir -p gpurun_out/exp
 export TMPDIR=/tmp
