@@ -24,8 +24,8 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ..ops.conv import PackedConv, conv2d_gn_nhwc, conv2d_nhwc, pack_conv
-from ..ops.norm import group_norm_nhwc, upsample2x_nhwc
+from ..ops.conv import PackedConv, conv2d_gn_nhwc, conv2d_nhwc, conv3x3_tile64, pack_conv, tile64_supported
+from ..ops.norm import group_norm_affine, group_norm_nhwc, upsample2x_nhwc
 from ..ops.pool import maxpool2d_nhwc, preprocess_u8
 
 # per-band normalisation for uint8 RGB+NIR imagery (NAIP-style); NIR uses the same scale
@@ -101,6 +101,14 @@ class _FusedDouble:
                  pool_out: Optional[torch.Tensor] = None) -> torch.Tensor:
         # GroupNorm statistics come out of the conv epilogues (conv2d_gn_nhwc) where the tile allows
         y, st = conv2d_gn_nhwc(x, self.c1, self.g1[2])
+        if st is not None and tile64_supported(y, self.c2) and 64 % self.g2[2] == 0 and 64 // self.g2[2] <= 4:
+            # 64 -> 64 at full resolution (K1t): c1's GroupNorm + ReLU is applied while c2 loads its input patch, so
+            # the normalized c1 output is never written (csrc/kernels/conv_tile3x3.hip)
+            n, h, w, c = y.shape
+            ss = group_norm_affine(st, *self.g1[:2], n=n, hw=h * w, c=c, groups=self.g1[2])
+            z, st = conv3x3_tile64(y, self.c2, pro=ss, pro_relu=True, gn_groups=self.g2[2])
+            return group_norm_nhwc(z, *self.g2[:2], groups=self.g2[2], relu=True, out=out if out is not None else z,
+                                   stats=st, pool_out=pool_out)
         y = group_norm_nhwc(y, *self.g1[:2], groups=self.g1[2], relu=True, out=y, stats=st)
         z, st = conv2d_gn_nhwc(y, self.c2, self.g2[2])
         return group_norm_nhwc(z, *self.g2[:2], groups=self.g2[2], relu=True, out=out if out is not None else z,

@@ -24,6 +24,20 @@ def _base_ptr(t: torch.Tensor) -> int:
     return t.untyped_storage().data_ptr() + t.element_size() * (t.storage_offset() - coff)
 
 
+def group_norm_affine(stats, gamma: torch.Tensor, beta: torch.Tensor, n: int, hw: int, c: int, groups: int = 32,
+                      eps: float = 1e-5) -> torch.Tensor:
+    """The per-(image, channel) affine (a, b) of a GroupNorm whose statistics a conv epilogue produced (``stats`` =
+    ``(partials, nchunks)``), without applying it: float32 [N, C, 2] (a view into the partials buffer) for a consumer
+    that normalizes while loading (``conv.conv3x3_tile64`` ``pro``)."""
+    partials, nchunks = stats
+    g32 = gamma.to(partials.device, torch.float32).contiguous()
+    b32 = beta.to(partials.device, torch.float32).contiguous()
+    _ext.call("ai4e_groupnorm_finalize", partials.data_ptr(), g32.data_ptr(), b32.data_ptr(), n, hw, c, groups, eps,
+              nchunks, _ext.stream_ptr(partials.device))
+    off = n * nchunks * groups * 4
+    return partials[off:off + n * c * 2].view(n, c, 2)
+
+
 def group_norm_nhwc(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, groups: int = 32, eps: float = 1e-5,
                     relu: bool = False, out: Optional[torch.Tensor] = None, stats=None,
                     pool_out: Optional[torch.Tensor] = None) -> torch.Tensor:

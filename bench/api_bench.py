@@ -68,6 +68,7 @@ def main():
     ap.add_argument("--wire", default="uint8", choices=["uint8", "float16"])
     ap.add_argument("--tile", type=int, default=512)
     ap.add_argument("--stride", type=int, default=448)
+    ap.add_argument("--tile-batch", type=int, default=16, help="land-cover tiles per U-Net batch (81 tiles per mosaic)")
     a = ap.parse_args()
     from aiforearth_api_platform_amd.runtime.node_bench import run_node_bench
     from aiforearth_api_platform_amd.runtime.worker_pool import ModelSpec
@@ -78,7 +79,7 @@ def main():
     kwargs, graphs, stages, group, leaders = {}, not a.no_graphs, (), 1, 1
     extra, dtype = {}, "bf16"
     if a.model.startswith("landcover"):
-        kwargs = {"height": size, "width": size, "tile": a.tile, "stride": a.stride, "tile_batch": 16}
+        kwargs = {"height": size, "width": size, "tile": a.tile, "stride": a.stride, "tile_batch": a.tile_batch}
     if a.model == "landcover_spatial":
         graphs = False  # P2P inside the servable: the U-Net runs per tile batch, eagerly
         group = a.group

@@ -1,0 +1,285 @@
+// K1t: 3x3 / stride 1 / pad 1 convolution, 64 -> 64 channels, NHWC bf16, for wide feature maps: the U-Net's
+// full-resolution level (512^2 tiles), where the K1 implicit GEMM gathers every tap of every pixel through the
+// LDS-DMA ring (nine 16-B gathers per pixel and 32-channel step) and ran at 23 % MFMA / 1.3 TB/s
+// (profiles/r4_unet/pmc_by_kernel.txt) against an HBM floor of ~half its time.
+//
+// One workgroup (4 waves) per 8 x 32 output tile:
+// * the 10 x 34 x 64 input patch (halo 1, zero outside the image) is loaded ONCE into LDS (43.5 KB, 16-B chunks of a
+//   pixel slot XOR-swizzled by the slot index so the 16 pixels of a fragment read conflict-free), optionally through
+//   a prologue: x * a[c] + b[c] (+ ReLU) per (image, channel) — the previous layer's GroupNorm apply, so that the
+//   normalized tensor is never written (its statistics came from the previous conv's epilogue);
+// * the nine taps then run as LDS-read + MFMA steps (v_mfma_f32_16x16x32_bf16; weights as the A operand, 4 channel
+//   fragments, pixels as B, 4 pixel fragments per wave: 64 px x 64 ch per wave), the next tap's weights (8 KB) loaded
+//   from L2 during the current tap into the other half of a two-tap LDS buffer;
+// * epilogue: + bias, bf16 store, and the GroupNorm statistics of the stored values per (image, tile, group) in the
+//   K1 conv-epilogue format (shifted sums S, Q and the shift K: norm_resample.hip gn_finalize_kernel).
+// Every global address is inside its tensor by construction (host: H % 8 == 0, W % 32 == 0, exact grid).
+#include "common.h"
+
+namespace {
+
+constexpr int T_H = 8, T_W = 32;                 // output tile
+constexpr int P_W = T_W + 2, P_SLOTS = (T_H + 2) * P_W;  // input patch with halo
+constexpr int CH = 64;                           // input and output channels
+constexpr int L_PATCH = P_SLOTS * CH * 2;        // 43,520 B
+constexpr int L_AFF = CH * 8;                    // prologue affine of this image: 64 x (a, b)
+constexpr int L_W = CH * CH * 2;                 // one tap's weights, 8 KB
+constexpr int L_TOTAL = L_PATCH + L_AFF + 2 * L_W;  // 60,416 B: two workgroups per CU
+constexpr int P_CHUNKS = P_SLOTS * 8;            // 16-B chunks of the patch
+constexpr int P_ITERS = (P_CHUNKS + 255) / 256;  // 11
+
+struct TileParams {
+  const uint16_t* x;
+  int ldx, xcoff;          // input [N, H, W, ldx], channels [xcoff, xcoff + 64)
+  const uint16_t* w;
+  int kpad;                // packed weights [64 rows, kpad >= 576], K = (kh, kw, c)
+  const float* bias;       // [64]
+  const float2* pro;       // prologue (a, b) per (image, channel) [N, 64]; null = none
+  int pro_relu;
+  uint16_t* y;
+  int ldy, ycoff;          // output [N, H, W, ldy], channels [ycoff, ycoff + 64)
+  float* gnp;              // GroupNorm partials [N, tiles per image, G, 4]; null = off
+  int gn_groups;
+  int H, W, tiles_w, tiles_per_img;
+};
+
+__device__ __forceinline__ uint32_t swz(int row, int c) { return static_cast<uint32_t>((c ^ (row & 7)) << 4); }
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv3x3_tile_kernel(
+    const TileParams p) {
+  extern __shared__ __attribute__((aligned(1024))) uint8_t sm[];
+  uint8_t* const patch = sm;
+  float2* const aff = reinterpret_cast<float2*>(sm + L_PATCH);
+  uint8_t* const wbuf = sm + L_PATCH + L_AFF;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int t = blockIdx.x;
+  const int img = t / p.tiles_per_img;
+  const int tin = t - img * p.tiles_per_img;
+  const int tr = tin / p.tiles_w, tc = tin - tr * p.tiles_w;
+  const int h0 = tr * T_H, w0 = tc * T_W;
+
+  // ---- loads: tap 0's weights, the prologue affine, the patch; then the LDS stores
+  uint4 wv[2];
+  auto load_w = [&](int tap) __attribute__((always_inline)) {
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int idx = tid + 256 * e, n = idx >> 3, c = idx & 7;
+      wv[e] = *reinterpret_cast<const uint4*>(p.w + static_cast<long>(n) * p.kpad + tap * CH + 8 * c);
+    }
+  };
+  auto store_w = [&](int buf) __attribute__((always_inline)) {
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int idx = tid + 256 * e, n = idx >> 3, c = idx & 7;
+      *reinterpret_cast<uint4*>(wbuf + buf * L_W + n * 128 + swz(n, c)) = wv[e];
+    }
+  };
+  load_w(0);
+  if (p.pro != nullptr && tid < CH) aff[tid] = p.pro[img * CH + tid];
+  uint4 pv[P_ITERS];
+  bool pin[P_ITERS];
+  const uint16_t* const xi = p.x + static_cast<long>(img) * p.H * p.W * p.ldx + p.xcoff;
+#pragma unroll
+  for (int k = 0; k < P_ITERS; ++k) {
+    const int e = tid + 256 * k;
+    const int slot = e >> 3, c = e & 7;
+    const int pr = slot / P_W, pc = slot - pr * P_W;
+    const int ih = h0 - 1 + pr, iw = w0 - 1 + pc;
+    pin[k] = e < P_CHUNKS && static_cast<unsigned>(ih) < static_cast<unsigned>(p.H) &&
+             static_cast<unsigned>(iw) < static_cast<unsigned>(p.W);
+    pv[k] = pin[k] ? *reinterpret_cast<const uint4*>(xi + (static_cast<long>(ih) * p.W + iw) * p.ldx + 8 * c)
+                   : make_uint4(0u, 0u, 0u, 0u);
+  }
+  store_w(0);
+  if (p.pro != nullptr) __syncthreads();  // the affine is in LDS
+#pragma unroll
+  for (int k = 0; k < P_ITERS; ++k) {
+    const int e = tid + 256 * k;
+    if (e >= P_CHUNKS) continue;
+    const int slot = e >> 3, c = e & 7;
+    uint4 v = pv[k];
+    if (p.pro != nullptr && pin[k]) {  // padding stays zero: the conv pads the normalized tensor
+      uint32_t wds[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float lo, hi;
+        unpack_bf16x2(wds[q], lo, hi);
+        const float2 a0 = aff[8 * c + 2 * q], a1 = aff[8 * c + 2 * q + 1];
+        lo = lo * a0.x + a0.y;
+        hi = hi * a1.x + a1.y;
+        if (p.pro_relu) {
+          lo = fmaxf(lo, 0.f);
+          hi = fmaxf(hi, 0.f);
+        }
+        wds[q] = pack_bf16x2(lo, hi);
+      }
+      v = make_uint4(wds[0], wds[1], wds[2], wds[3]);
+    }
+    *reinterpret_cast<uint4*>(patch + slot * 128 + swz(slot, c)) = v;
+  }
+  __syncthreads();
+
+  // ---- nine taps x two 32-channel steps
+  const int g4 = lane >> 4;
+  int sbase[4];  // slot of tap (0, 0) for this lane's pixel in fragment f: tile row 2 wave + f / 2, column 16 (f & 1) + lane % 16
+#pragma unroll
+  for (int f = 0; f < 4; ++f) sbase[f] = (2 * wave + (f >> 1)) * P_W + 16 * (f & 1) + (lane & 15);
+  f32x4_t acc[4][4];
+#pragma unroll
+  for (int f = 0; f < 4; ++f)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[f][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  for (int tap = 0; tap < 9; ++tap) {
+    if (tap + 1 < 9) load_w(tap + 1);  // in flight under this tap's MFMAs
+    const int kh = tap / 3, kw = tap - 3 * kh;
+    const uint8_t* const wb = wbuf + (tap & 1) * L_W;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int chunk = 4 * s + g4;
+      bf16x8_t fx[4], fw[4];
+#pragma unroll
+      for (int f = 0; f < 4; ++f) {
+        const int slot = sbase[f] + kh * P_W + kw;
+        fx[f] = *reinterpret_cast<const bf16x8_t*>(patch + slot * 128 + swz(slot, chunk));
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = 16 * j + (lane & 15);
+        fw[j] = *reinterpret_cast<const bf16x8_t*>(wb + n * 128 + swz(n, chunk));
+      }
+#pragma unroll
+      for (int f = 0; f < 4; ++f)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[f][j] = mfma_16x16x32<false>(fw[j], fx[f], acc[f][j]);
+    }
+    if (tap + 1 < 9) store_w((tap + 1) & 1);  // that half was last read at tap - 1 (before the previous barrier)
+    __syncthreads();
+  }
+
+  // ---- epilogue: lane holds channels 16 j + 4 g4 + v of pixel (lane % 16) of each fragment
+  float bv[4][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) bv[j][v] = p.bias[16 * j + 4 * g4 + v];
+  float* const kshift = reinterpret_cast<float*>(wbuf);        // [64] the tile's first pixel, as stored
+  float* const red = reinterpret_cast<float*>(wbuf) + CH;      // [4 waves][64 channels][2]
+  uint2 ov[4][4];
+#pragma unroll
+  for (int f = 0; f < 4; ++f) {
+    const int oh = h0 + 2 * wave + (f >> 1), ow = w0 + 16 * (f & 1) + (lane & 15);
+    uint16_t* const dst = p.y + ((static_cast<long>(img) * p.H + oh) * p.W + ow) * p.ldy + p.ycoff;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      ov[f][j] = make_uint2(pack_bf16x2(acc[f][j][0] + bv[j][0], acc[f][j][1] + bv[j][1]),
+                            pack_bf16x2(acc[f][j][2] + bv[j][2], acc[f][j][3] + bv[j][3]));
+      *reinterpret_cast<uint2*>(dst + 16 * j + 4 * g4) = ov[f][j];
+    }
+  }
+  if (p.gnp == nullptr) return;
+  // GroupNorm statistics of the stored values (cg = 64 / G channels per group, cg in {1, 2, 4}: a lane's 4 channels
+  // of one j hold whole groups), shifted by the tile's first pixel at each group's first channel
+  if (wave == 0 && (lane & 15) == 0) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float a, b, c, d;
+      unpack_bf16x2(ov[0][j].x, a, b);
+      unpack_bf16x2(ov[0][j].y, c, d);
+      kshift[16 * j + 4 * g4] = a;
+      kshift[16 * j + 4 * g4 + 1] = b;
+      kshift[16 * j + 4 * g4 + 2] = c;
+      kshift[16 * j + 4 * g4 + 3] = d;
+    }
+  }
+  __syncthreads();
+  const int cg = CH / p.gn_groups;
+  float gs[4][4], gq[4][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int ch = 16 * j + 4 * g4 + v;
+      const float K = kshift[ch - ch % cg];
+      float s = 0.f, q = 0.f;
+#pragma unroll
+      for (int f = 0; f < 4; ++f) {
+        float a, b;
+        unpack_bf16x2(v < 2 ? ov[f][j].x : ov[f][j].y, a, b);
+        const float d = ((v & 1) ? b : a) - K;
+        s += d;
+        q += d * d;
+      }
+      gs[j][v] = s;
+      gq[j][v] = q;
+    }
+#pragma unroll
+  for (int off = 1; off < 16; off <<= 1)  // over the 16 pixels of a fragment row (lanes sharing g4)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        gs[j][v] += __shfl_xor(gs[j][v], off);
+        gq[j][v] += __shfl_xor(gq[j][v], off);
+      }
+  if ((lane & 15) == 0) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int ch = 16 * j + 4 * g4 + v;
+        red[(wave * CH + ch) * 2] = gs[j][v];
+        red[(wave * CH + ch) * 2 + 1] = gq[j][v];
+      }
+  }
+  __syncthreads();
+  if (tid < p.gn_groups) {
+    float S = 0.f, Q = 0.f;
+    for (int w = 0; w < 4; ++w)
+      for (int c = 0; c < cg; ++c) {
+        S += red[(w * CH + tid * cg + c) * 2];
+        Q += red[(w * CH + tid * cg + c) * 2 + 1];
+      }
+    float* const o = p.gnp + ((static_cast<long>(img) * p.tiles_per_img + tin) * p.gn_groups + tid) * 4;
+    *reinterpret_cast<float4*>(o) = make_float4(S, Q, kshift[tid * cg], 0.f);
+  }
+}
+
+}  // namespace
+
+// y = conv3x3(pro(x)) + bias (64 -> 64 channels, stride 1, pad 1) with GroupNorm partials of y (gn_groups > 0):
+// [N, (H / 8) * (W / 32), G, 4]. pro: null or float2 [N, 64] (x * a + b, then ReLU if pro_relu).
+AI4E_API int ai4e_conv3x3_tile64_fwd(const void* x, const void* w, const void* bias, const void* pro, int pro_relu,
+                                      void* y, int N, int H, int W, int ldx, int xcoff, int kpad, int ldy, int ycoff,
+                                      void* gn_partials, int gn_groups, hipStream_t stream) {
+  if (!x || !w || !bias || !y || N <= 0 || H % T_H || W % T_W || kpad < 9 * CH || ldx % 8 || xcoff % 8 ||
+      xcoff + CH > ldx || ldy % 8 || ycoff % 8 || ycoff + CH > ldy)
+    return AI4E_EINVAL;
+  if (gn_partials && (gn_groups <= 0 || CH % gn_groups || CH / gn_groups > 4)) return AI4E_EINVAL;
+  if (static_cast<long>(N) * H * W * (ldx > ldy ? ldx : ldy) >= (1L << 40)) return AI4E_EINVAL;
+  TileParams p;
+  p.x = static_cast<const uint16_t*>(x);
+  p.ldx = ldx;
+  p.xcoff = xcoff;
+  p.w = static_cast<const uint16_t*>(w);
+  p.kpad = kpad;
+  p.bias = static_cast<const float*>(bias);
+  p.pro = static_cast<const float2*>(pro);
+  p.pro_relu = pro_relu;
+  p.y = static_cast<uint16_t*>(y);
+  p.ldy = ldy;
+  p.ycoff = ycoff;
+  p.gnp = static_cast<float*>(gn_partials);
+  p.gn_groups = gn_partials ? gn_groups : 1;
+  p.H = H;
+  p.W = W;
+  p.tiles_w = W / T_W;
+  p.tiles_per_img = (H / T_H) * p.tiles_w;
+  static bool attr = [] {
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(conv3x3_tile_kernel),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, L_TOTAL) == hipSuccess;
+  }();
+  if (!attr) return AI4E_ELAUNCH;
+  hipLaunchKernelGGL(conv3x3_tile_kernel, dim3(static_cast<unsigned>(N * p.tiles_per_img)), dim3(256), L_TOTAL, stream, p);
+  return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
+}

@@ -366,6 +366,21 @@ AI4E_API int ai4e_groupnorm_apply_nhwc(const void* x, void* y, const void* gamma
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
 }
 
+// GroupNorm statistics -> per-(image, channel) affine only (no apply pass): partials [N, nchunks, G, 4] from a conv
+// epilogue, the affine (a, b) written after them as float2 [N, C] (y = x * a + b). For a consumer that applies the norm
+// itself while loading its input (conv_tile3x3.hip's prologue).
+AI4E_API int ai4e_groupnorm_finalize(void* partials, const void* gamma, const void* beta, int N, int HW, int C, int G,
+                                     float eps, int nchunks, hipStream_t s) {
+  if (!partials || !gamma || !beta || N <= 0 || G <= 0 || G > 64 || C % G || nchunks <= 0 || HW % nchunks)
+    return AI4E_EINVAL;
+  float2* ss =
+      reinterpret_cast<float2*>(static_cast<float*>(partials) + static_cast<long>(N) * nchunks * G * GN_PARTIAL);
+  hipLaunchKernelGGL(gn_finalize_kernel, gn_finalize_grid(N, G), dim3(GN_FIN_THREADS), 0, s, static_cast<const float*>(partials),
+                     static_cast<const float*>(gamma), static_cast<const float*>(beta), ss, HW, C, G, eps, nchunks,
+                     HW / nchunks);
+  return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
+}
+
 // GN (precomputed statistics, as ai4e_groupnorm_apply_nhwc) that also writes the 2x2/2 max-pool of its output
 // into pooled [N, H/2, W/2, C] (contiguous); H and W even.
 AI4E_API int ai4e_groupnorm_apply_pool_nhwc(const void* x, void* y, const void* gamma, const void* beta, void* partials,

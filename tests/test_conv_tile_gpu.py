@@ -1,0 +1,98 @@
+"""K1t (csrc/kernels/conv_tile3x3.hip): the 64 -> 64 3x3 conv from an LDS input patch, against fp32 PyTorch
+references of the same op — plain, with the fused GroupNorm + ReLU input prologue, on a channel-sliced input — its
+GroupNorm statistics against the statistics of the stored output, and the U-Net forward with and without it."""
+import os
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _conv_ref(xin: torch.Tensor, w: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    y = F.conv2d(xin.permute(0, 3, 1, 2).float(), w.float(), b.float(), padding=1)
+    return y.permute(0, 2, 3, 1)
+
+
+def _case(n, h, w, seed):
+    from aiforearth_api_platform_amd.ops.conv import pack_conv
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn(n, h, w, 64, generator=g).to(torch.bfloat16)
+    wt = (torch.randn(64, 64, 3, 3, generator=g) * 0.05).to(torch.bfloat16).float()
+    b = torch.randn(64, generator=g) * 0.1
+    return x, wt, b, pack_conv(wt, b, pad=1).to(DEV)
+
+
+@pytest.mark.parametrize("n,h,w", [(2, 16, 64), (1, 64, 32), (3, 8, 96)])
+def test_conv3x3_tile64_matches_fp32(n, h, w):
+    from aiforearth_api_platform_amd.ops.conv import conv3x3_tile64
+    x, wt, b, pc = _case(n, h, w, n * 100 + h)
+    y, st = conv3x3_tile64(x.to(DEV), pc)
+    assert st is None
+    ref = _conv_ref(x, wt, b)
+    rel = ((y.float().cpu() - ref).norm() / ref.norm()).item()
+    assert rel < 6e-3, rel
+
+
+def test_conv3x3_tile64_prologue_and_sliced_input():
+    from aiforearth_api_platform_amd.ops.conv import conv3x3_tile64
+    n, h, w = 2, 16, 64
+    x, wt, b, pc = _case(n, h, w, 7)
+    g = torch.Generator().manual_seed(8)
+    aff = torch.stack([0.5 + torch.rand(n, 64, generator=g), torch.randn(n, 64, generator=g) * 0.5], -1)
+    wide = torch.zeros(n, h, w, 128, dtype=torch.bfloat16)
+    wide[..., 64:] = x
+    y, _ = conv3x3_tile64(wide.to(DEV)[..., 64:], pc, pro=aff.to(DEV).contiguous(), pro_relu=True)
+    xin = torch.relu(x.float() * aff[:, None, None, :, 0] + aff[:, None, None, :, 1]).to(torch.bfloat16)
+    ref = _conv_ref(xin, wt, b)
+    rel = ((y.float().cpu() - ref).norm() / ref.norm()).item()
+    assert rel < 6e-3, rel
+
+
+@pytest.mark.parametrize("groups", [32, 16])
+def test_conv3x3_tile64_groupnorm_statistics(groups):
+    """The epilogue's shifted per-tile sums, finalized (ops.norm.group_norm_affine), equal the GroupNorm affine of
+    the stored output computed directly in fp64."""
+    from aiforearth_api_platform_amd.ops.conv import conv3x3_tile64
+    from aiforearth_api_platform_amd.ops.norm import group_norm_affine
+    n, h, w = 2, 32, 64
+    x, wt, b, pc = _case(n, h, w, 21)
+    y, st = conv3x3_tile64(x.to(DEV), pc, gn_groups=groups)
+    gamma = torch.linspace(0.5, 1.5, 64)
+    beta = torch.linspace(-0.2, 0.2, 64)
+    ss = group_norm_affine(st, gamma, beta, n=n, hw=h * w, c=64, groups=groups).cpu()
+    yd = y.double().cpu().reshape(n, h * w, groups, 64 // groups)
+    mean = yd.mean(dim=(1, 3))
+    var = yd.var(dim=(1, 3), unbiased=False)
+    rstd = (var + 1e-5).rsqrt()
+    a = (gamma.double().reshape(groups, -1)[None] * rstd[..., None]).reshape(n, 64)
+    bb = beta.double()[None] - (mean[..., None] * a.reshape(n, groups, -1)).reshape(n, 64)
+    assert torch.allclose(ss[..., 0].double(), a, rtol=1e-4, atol=1e-5)
+    assert torch.allclose(ss[..., 1].double(), bb, rtol=1e-4, atol=1e-4)
+
+
+def test_unet_forward_with_and_without_k1t():
+    """The land-cover U-Net (its full-resolution DoubleConvs take K1t with the fused GroupNorm prologue) equals the
+    K1 path (AI4E_CONV_TILE64=0) and stays within the fp32 reference's tolerance."""
+    from aiforearth_api_platform_amd.models.unet import FusedUNet, unet_landcover
+    m = unet_landcover(seed=3)
+    f = FusedUNet(m, device=DEV)
+    img = torch.randint(0, 256, (2, 256, 256, 4), dtype=torch.uint8, generator=torch.Generator().manual_seed(3))
+    y_tile = f.forward_u8(img.to(DEV)).float()
+    old = os.environ.get("AI4E_CONV_TILE64")
+    os.environ["AI4E_CONV_TILE64"] = "0"
+    try:
+        y_k1 = f.forward_u8(img.to(DEV)).float()
+    finally:
+        if old is None:
+            del os.environ["AI4E_CONV_TILE64"]
+        else:
+            os.environ["AI4E_CONV_TILE64"] = old
+    k = f.n_classes
+    rel = ((y_tile[..., :k] - y_k1[..., :k]).norm() / y_k1[..., :k].norm()).item()
+    assert rel < 2e-2, rel
+    agree = (y_tile[..., :k].argmax(-1) == y_k1[..., :k].argmax(-1)).float().mean().item()
+    assert agree > 0.97, agree
