@@ -97,11 +97,18 @@ class _FusedDouble:
         self.g1 = (dc.n1.weight.data.float().to(device), dc.n1.bias.data.float().to(device), dc.n1.num_groups)
         self.g2 = (dc.n2.weight.data.float().to(device), dc.n2.bias.data.float().to(device), dc.n2.num_groups)
 
+    @staticmethod
+    def _k1t_groups(g: int) -> bool:  # K1t's epilogue sums whole groups within a lane's 4 channels
+        return 64 % g == 0 and 64 // g <= 4
+
     def __call__(self, x: torch.Tensor, out: Optional[torch.Tensor] = None,
                  pool_out: Optional[torch.Tensor] = None) -> torch.Tensor:
-        # GroupNorm statistics come out of the conv epilogues (conv2d_gn_nhwc) where the tile allows
-        y, st = conv2d_gn_nhwc(x, self.c1, self.g1[2])
-        if st is not None and tile64_supported(y, self.c2) and 64 % self.g2[2] == 0 and 64 // self.g2[2] <= 4:
+        # GroupNorm statistics come out of the conv epilogues (conv2d_gn_nhwc, K1t) where the tile allows
+        if tile64_supported(x, self.c1) and self._k1t_groups(self.g1[2]):
+            y, st = conv3x3_tile64(x, self.c1, gn_groups=self.g1[2])  # e.g. the last decoder's 128 -> 64 c1
+        else:
+            y, st = conv2d_gn_nhwc(x, self.c1, self.g1[2])
+        if st is not None and tile64_supported(y, self.c2) and self._k1t_groups(self.g2[2]):
             # 64 -> 64 at full resolution (K1t): c1's GroupNorm + ReLU is applied while c2 loads its input patch, so
             # the normalized c1 output is never written (csrc/kernels/conv_tile3x3.hip)
             n, h, w, c = y.shape

@@ -233,39 +233,45 @@ def conv2d_gn_nhwc(x: torch.Tensor, pc: PackedConv, groups: int, out: Optional[t
     return out, (partials, nchunks)
 
 
+def _tile_rows(cin: int) -> int:
+    return 8 if cin == 64 else 4
+
+
 def tile64_supported(x: torch.Tensor, pc: PackedConv) -> bool:
-    """Shapes K1t (``conv3x3_tile64``, csrc/kernels/conv_tile3x3.hip) takes: 3x3 / stride 1 / pad 1, 64 -> 64 channels,
-    bf16, H % 8 == 0 and W % 32 == 0 (8 x 32 output tiles); AI4E_CONV_TILE64=0 turns it off (A/B)."""
+    """Shapes K1t (``conv3x3_tile64``, csrc/kernels/conv_tile3x3.hip) takes: 3x3 / stride 1 / pad 1, 64 or 128 -> 64
+    channels, bf16, W % 32 == 0 and H % 8 (64 channels) or % 4 (128): 8 x 32 / 4 x 32 output tiles;
+    AI4E_CONV_TILE64=0 turns it off (A/B)."""
     n, h, w, c = x.shape
     return (os.environ.get("AI4E_CONV_TILE64", "1") != "0" and _ext.backend_for(x) == "hip"
             and x.dtype == torch.bfloat16 and pc.w_packed.dtype == torch.bfloat16 and (pc.kh, pc.kw) == (3, 3)
-            and pc.stride == 1 and pc.pad == 1 and (pc.pad if pc.pad_hi is None else pc.pad_hi) == 1 and pc.cin_pad == 64 and c == 64 and pc.cout == 64
-            and h % 8 == 0 and w % 32 == 0 and x.stride(3) == 1 and x.stride(2) % 8 == 0
+            and pc.stride == 1 and pc.pad == 1 and (pc.pad if pc.pad_hi is None else pc.pad_hi) == 1
+            and pc.cin_pad in (64, 128) and c == pc.cin_pad and pc.cout == 64
+            and h % _tile_rows(c) == 0 and w % 32 == 0 and x.stride(3) == 1 and x.stride(2) % 8 == 0
             and x.stride(2) * w == x.stride(1) and x.stride(1) * h == x.stride(0))
 
 
 def conv3x3_tile64(x: torch.Tensor, pc: PackedConv, pro: Optional[torch.Tensor] = None, pro_relu: bool = True,
                    gn_groups: int = 0) -> Tuple[torch.Tensor, Optional[tuple]]:
-    """K1t: ``conv3x3(pro(x)) + bias`` for 64 -> 64 channels (see ``tile64_supported``), one 8 x 32 output tile per
-    workgroup from an LDS input patch. ``pro``: float32 [N, 64, 2] per-(image, channel) affine applied to the input as
-    it is loaded (``x * a + b``, then ReLU with ``pro_relu``): the previous GroupNorm, which then needs no apply pass
-    (``norm.group_norm_affine``). Returns ``(y, stats)`` with ``stats`` = ``(partials, nchunks)`` GroupNorm
-    statistics of y (as ``conv2d_gn_nhwc``) when ``gn_groups``, else None."""
+    """K1t: ``conv3x3(pro(x)) + bias`` for 64 or 128 -> 64 channels (see ``tile64_supported``), one 8 x 32 (4 x 32)
+    output tile per workgroup from an LDS input patch. ``pro``: float32 [N, C, 2] per-(image, channel) affine applied
+    to the input as it is loaded (``x * a + b``, then ReLU with ``pro_relu``): the previous GroupNorm, which then
+    needs no apply pass (``norm.group_norm_affine``). Returns ``(y, stats)`` with ``stats`` = ``(partials,
+    nchunks)`` GroupNorm statistics of y (as ``conv2d_gn_nhwc``) when ``gn_groups``, else None."""
     n, h, w, c = x.shape
     if not tile64_supported(x, pc):
         raise ValueError("conv3x3_tile64: unsupported shape / dtype / layout")
-    if pro is not None and (pro.dtype != torch.float32 or not pro.is_contiguous() or tuple(pro.shape) != (n, 64, 2)):
-        raise ValueError("conv3x3_tile64: pro must be contiguous float32 [N, 64, 2]")
+    if pro is not None and (pro.dtype != torch.float32 or not pro.is_contiguous() or tuple(pro.shape) != (n, c, 2)):
+        raise ValueError(f"conv3x3_tile64: pro must be contiguous float32 [N, {c}, 2]")
     ldx = x.stride(2)
     xoff = x.storage_offset()
     base = x.untyped_storage().data_ptr() + 2 * (xoff - xoff % ldx)
     out = torch.empty(n, h, w, 64, device=x.device, dtype=x.dtype)
-    nchunks = (h // 8) * (w // 32)
+    nchunks = (h // _tile_rows(c)) * (w // 32)
     partials = None
     if gn_groups:
         partials = torch.empty(n * nchunks * gn_groups * 4 + n * 64 * 2, device=x.device, dtype=torch.float32)
     _ext.call("ai4e_conv3x3_tile64_fwd", base, pc.w_packed.data_ptr(), pc.bias.data_ptr(), _ext.ptr(pro),
-              int(pro_relu), out.data_ptr(), n, h, w, ldx, xoff % ldx, pc.kpad, 64, 0, _ext.ptr(partials),
+              int(pro_relu), out.data_ptr(), n, h, w, c, ldx, xoff % ldx, pc.kpad, 64, 0, _ext.ptr(partials),
               gn_groups, _ext.stream_ptr(x.device))
     return out, ((partials, nchunks) if gn_groups else None)
 

@@ -18,15 +18,30 @@
 
 namespace {
 
-constexpr int T_H = 8, T_W = 32;                 // output tile
-constexpr int P_W = T_W + 2, P_SLOTS = (T_H + 2) * P_W;  // input patch with halo
-constexpr int CH = 64;                           // input and output channels
-constexpr int L_PATCH = P_SLOTS * CH * 2;        // 43,520 B
-constexpr int L_AFF = CH * 8;                    // prologue affine of this image: 64 x (a, b)
-constexpr int L_W = CH * CH * 2;                 // one tap's weights, 8 KB
-constexpr int L_TOTAL = L_PATCH + L_AFF + 2 * L_W;  // 60,416 B: two workgroups per CU
-constexpr int P_CHUNKS = P_SLOTS * 8;            // 16-B chunks of the patch
-constexpr int P_ITERS = (P_CHUNKS + 255) / 256;  // 11
+constexpr int T_W = 32, P_W = T_W + 2;           // output tile width; patch width with halo
+constexpr int CH = 64;                           // output channels (and the channels of one weight stage)
+constexpr int L_W = CH * CH * 2;                 // one weight stage: 64 output x 64 input channels of one tap, 8 KB
+
+// CIN = 64: 8 x 32 tiles (patch 10 x 34 x 128 B = 43.5 KB); CIN = 128 (the U-Net's last decoder c1, reading the
+// [skip | upsampled] concat): 4 x 32 tiles (patch 6 x 34 x 256 B = 52 KB), each tap's weights in two 64-channel
+// stages. Both keep two workgroups per CU.
+template <int CIN>
+struct TileCfg {
+  static constexpr int TH = CIN == 64 ? 8 : 4;          // output tile rows
+  static constexpr int P_SLOTS = (TH + 2) * P_W;
+  static constexpr int NCH = CIN / 8;                   // 16-B chunks per pixel slot
+  static constexpr int SLOT_B = CIN * 2;
+  static constexpr int L_PATCH = P_SLOTS * SLOT_B;
+  static constexpr int L_AFF = CIN * 8;                 // prologue affine of this image: CIN x (a, b)
+  static constexpr int L_TOTAL = L_PATCH + L_AFF + 2 * L_W;
+  static constexpr int P_CHUNKS = P_SLOTS * NCH;
+  static constexpr int P_ITERS = (P_CHUNKS + 255) / 256;
+  static constexpr int HALVES = CIN / 64;               // weight stages per tap
+  static constexpr int NST = 9 * HALVES;
+  static constexpr int FPW = TH / 2;                    // pixel fragments per wave (TH / 4 rows x 2 half-rows)
+  static_assert(CIN == 64 || CIN == 128, "K1t: 64 or 128 input channels");
+  static_assert(L_TOTAL <= 80 * 1024, "two workgroups per CU");
+};
 
 struct TileParams {
   const uint16_t* x;
@@ -43,47 +58,54 @@ struct TileParams {
   int H, W, tiles_w, tiles_per_img;
 };
 
-__device__ __forceinline__ uint32_t swz(int row, int c) { return static_cast<uint32_t>((c ^ (row & 7)) << 4); }
+// 16-B chunk c of row `row` (M chunks per row, a power of two) at physical chunk c ^ (row % M)
+template <int M>
+__device__ __forceinline__ uint32_t swz(int row, int c) { return static_cast<uint32_t>((c ^ (row & (M - 1))) << 4); }
 
+template <int CIN>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv3x3_tile_kernel(
     const TileParams p) {
+  using Cfg = TileCfg<CIN>;
+  constexpr int TH = Cfg::TH, P_CHUNKS = Cfg::P_CHUNKS, P_ITERS = Cfg::P_ITERS, NCH = Cfg::NCH, SLOT_B = Cfg::SLOT_B;
+  constexpr int HALVES = Cfg::HALVES, NST = Cfg::NST, FPW = Cfg::FPW;
   extern __shared__ __attribute__((aligned(1024))) uint8_t sm[];
   uint8_t* const patch = sm;
-  float2* const aff = reinterpret_cast<float2*>(sm + L_PATCH);
-  uint8_t* const wbuf = sm + L_PATCH + L_AFF;
+  float2* const aff = reinterpret_cast<float2*>(sm + Cfg::L_PATCH);
+  uint8_t* const wbuf = sm + Cfg::L_PATCH + Cfg::L_AFF;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int t = blockIdx.x;
   const int img = t / p.tiles_per_img;
   const int tin = t - img * p.tiles_per_img;
   const int tr = tin / p.tiles_w, tc = tin - tr * p.tiles_w;
-  const int h0 = tr * T_H, w0 = tc * T_W;
+  const int h0 = tr * TH, w0 = tc * T_W;
 
   // ---- loads: tap 0's weights, the prologue affine, the patch; then the LDS stores
   uint4 wv[2];
-  auto load_w = [&](int tap) __attribute__((always_inline)) {
+  auto load_w = [&](int st) __attribute__((always_inline)) {  // stage st = (tap, 64-channel half)
+    const int tap = st / HALVES, half = st - tap * HALVES;
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
       const int idx = tid + 256 * e, n = idx >> 3, c = idx & 7;
-      wv[e] = *reinterpret_cast<const uint4*>(p.w + static_cast<long>(n) * p.kpad + tap * CH + 8 * c);
+      wv[e] = *reinterpret_cast<const uint4*>(p.w + static_cast<long>(n) * p.kpad + tap * CIN + half * 64 + 8 * c);
     }
   };
   auto store_w = [&](int buf) __attribute__((always_inline)) {
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
       const int idx = tid + 256 * e, n = idx >> 3, c = idx & 7;
-      *reinterpret_cast<uint4*>(wbuf + buf * L_W + n * 128 + swz(n, c)) = wv[e];
+      *reinterpret_cast<uint4*>(wbuf + buf * L_W + n * 128 + swz<8>(n, c)) = wv[e];
     }
   };
   load_w(0);
-  if (p.pro != nullptr && tid < CH) aff[tid] = p.pro[img * CH + tid];
+  if (p.pro != nullptr && tid < CIN) aff[tid] = p.pro[img * CIN + tid];
   uint4 pv[P_ITERS];
   bool pin[P_ITERS];
   const uint16_t* const xi = p.x + static_cast<long>(img) * p.H * p.W * p.ldx + p.xcoff;
 #pragma unroll
   for (int k = 0; k < P_ITERS; ++k) {
     const int e = tid + 256 * k;
-    const int slot = e >> 3, c = e & 7;
+    const int slot = e / NCH, c = e - slot * NCH;
     const int pr = slot / P_W, pc = slot - pr * P_W;
     const int ih = h0 - 1 + pr, iw = w0 - 1 + pc;
     pin[k] = e < P_CHUNKS && static_cast<unsigned>(ih) < static_cast<unsigned>(p.H) &&
@@ -97,7 +119,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   for (int k = 0; k < P_ITERS; ++k) {
     const int e = tid + 256 * k;
     if (e >= P_CHUNKS) continue;
-    const int slot = e >> 3, c = e & 7;
+    const int slot = e / NCH, c = e - slot * NCH;
     uint4 v = pv[k];
     if (p.pro != nullptr && pin[k]) {  // padding stays zero: the conv pads the normalized tensor
       uint32_t wds[4] = {v.x, v.y, v.z, v.w};
@@ -116,44 +138,46 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       }
       v = make_uint4(wds[0], wds[1], wds[2], wds[3]);
     }
-    *reinterpret_cast<uint4*>(patch + slot * 128 + swz(slot, c)) = v;
+    *reinterpret_cast<uint4*>(patch + slot * SLOT_B + swz<NCH>(slot, c)) = v;
   }
   __syncthreads();
 
-  // ---- nine taps x two 32-channel steps
+  // ---- weight stages (9 taps x CIN / 64 halves) x two 32-channel steps
   const int g4 = lane >> 4;
-  int sbase[4];  // slot of tap (0, 0) for this lane's pixel in fragment f: tile row 2 wave + f / 2, column 16 (f & 1) + lane % 16
+  // slot of tap (0, 0) for this lane's pixel in fragment f: tile row (TH / 4) wave + f / 2, column 16 (f & 1) + lane % 16
+  int sbase[FPW];
 #pragma unroll
-  for (int f = 0; f < 4; ++f) sbase[f] = (2 * wave + (f >> 1)) * P_W + 16 * (f & 1) + (lane & 15);
-  f32x4_t acc[4][4];
+  for (int f = 0; f < FPW; ++f) sbase[f] = ((TH / 4) * wave + (f >> 1)) * P_W + 16 * (f & 1) + (lane & 15);
+  f32x4_t acc[FPW][4];
 #pragma unroll
-  for (int f = 0; f < 4; ++f)
+  for (int f = 0; f < FPW; ++f)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[f][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  for (int tap = 0; tap < 9; ++tap) {
-    if (tap + 1 < 9) load_w(tap + 1);  // in flight under this tap's MFMAs
+  for (int st = 0; st < NST; ++st) {
+    if (st + 1 < NST) load_w(st + 1);  // in flight under this stage's MFMAs
+    const int tap = st / HALVES, half = st - tap * HALVES;
     const int kh = tap / 3, kw = tap - 3 * kh;
-    const uint8_t* const wb = wbuf + (tap & 1) * L_W;
+    const uint8_t* const wb = wbuf + (st & 1) * L_W;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      const int chunk = 4 * s + g4;
-      bf16x8_t fx[4], fw[4];
+      const int wc = 4 * s + g4;  // chunk within the stage's 64 channels
+      bf16x8_t fx[FPW], fw[4];
 #pragma unroll
-      for (int f = 0; f < 4; ++f) {
+      for (int f = 0; f < FPW; ++f) {
         const int slot = sbase[f] + kh * P_W + kw;
-        fx[f] = *reinterpret_cast<const bf16x8_t*>(patch + slot * 128 + swz(slot, chunk));
+        fx[f] = *reinterpret_cast<const bf16x8_t*>(patch + slot * SLOT_B + swz<NCH>(slot, 8 * half + wc));
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int n = 16 * j + (lane & 15);
-        fw[j] = *reinterpret_cast<const bf16x8_t*>(wb + n * 128 + swz(n, chunk));
+        fw[j] = *reinterpret_cast<const bf16x8_t*>(wb + n * 128 + swz<8>(n, wc));
       }
 #pragma unroll
-      for (int f = 0; f < 4; ++f)
+      for (int f = 0; f < FPW; ++f)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[f][j] = mfma_16x16x32<false>(fw[j], fx[f], acc[f][j]);
     }
-    if (tap + 1 < 9) store_w((tap + 1) & 1);  // that half was last read at tap - 1 (before the previous barrier)
+    if (st + 1 < NST) store_w((st + 1) & 1);  // that buffer was last read at stage st - 1 (before the previous barrier)
     __syncthreads();
   }
 
@@ -165,10 +189,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     for (int v = 0; v < 4; ++v) bv[j][v] = p.bias[16 * j + 4 * g4 + v];
   float* const kshift = reinterpret_cast<float*>(wbuf);        // [64] the tile's first pixel, as stored
   float* const red = reinterpret_cast<float*>(wbuf) + CH;      // [4 waves][64 channels][2]
-  uint2 ov[4][4];
+  uint2 ov[FPW][4];
 #pragma unroll
-  for (int f = 0; f < 4; ++f) {
-    const int oh = h0 + 2 * wave + (f >> 1), ow = w0 + 16 * (f & 1) + (lane & 15);
+  for (int f = 0; f < FPW; ++f) {
+    const int oh = h0 + (TH / 4) * wave + (f >> 1), ow = w0 + 16 * (f & 1) + (lane & 15);
     uint16_t* const dst = p.y + ((static_cast<long>(img) * p.H + oh) * p.W + ow) * p.ldy + p.ycoff;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -203,7 +227,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       const float K = kshift[ch - ch % cg];
       float s = 0.f, q = 0.f;
 #pragma unroll
-      for (int f = 0; f < 4; ++f) {
+      for (int f = 0; f < FPW; ++f) {
         float a, b;
         unpack_bf16x2(v < 2 ? ov[f][j].x : ov[f][j].y, a, b);
         const float d = ((v & 1) ? b : a) - K;
@@ -247,13 +271,32 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 
 }  // namespace
 
-// y = conv3x3(pro(x)) + bias (64 -> 64 channels, stride 1, pad 1) with GroupNorm partials of y (gn_groups > 0):
-// [N, (H / 8) * (W / 32), G, 4]. pro: null or float2 [N, 64] (x * a + b, then ReLU if pro_relu).
+namespace {
+
+template <int CIN>
+int launch_tile(const TileParams& p, int N, hipStream_t stream) {
+  constexpr int L = TileCfg<CIN>::L_TOTAL;
+  static bool attr = [] {
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(conv3x3_tile_kernel<CIN>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, L) == hipSuccess;
+  }();
+  if (!attr) return AI4E_ELAUNCH;
+  hipLaunchKernelGGL(conv3x3_tile_kernel<CIN>, dim3(static_cast<unsigned>(N * p.tiles_per_img)), dim3(256), L, stream,
+                     p);
+  return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
+}
+
+}  // namespace
+
+// y = conv3x3(pro(x)) + bias (cin = 64 or 128 -> 64 channels, stride 1, pad 1) with GroupNorm partials of y
+// (gn_groups > 0): [N, (H / TH) * (W / 32), G, 4] (TH = 8 for cin 64, 4 for 128). pro: null or float2 [N, cin]
+// (x * a + b, then ReLU if pro_relu).
 AI4E_API int ai4e_conv3x3_tile64_fwd(const void* x, const void* w, const void* bias, const void* pro, int pro_relu,
-                                      void* y, int N, int H, int W, int ldx, int xcoff, int kpad, int ldy, int ycoff,
-                                      void* gn_partials, int gn_groups, hipStream_t stream) {
-  if (!x || !w || !bias || !y || N <= 0 || H % T_H || W % T_W || kpad < 9 * CH || ldx % 8 || xcoff % 8 ||
-      xcoff + CH > ldx || ldy % 8 || ycoff % 8 || ycoff + CH > ldy)
+                                      void* y, int N, int H, int W, int cin, int ldx, int xcoff, int kpad, int ldy,
+                                      int ycoff, void* gn_partials, int gn_groups, hipStream_t stream) {
+  const int th = cin == 64 ? TileCfg<64>::TH : TileCfg<128>::TH;
+  if (!x || !w || !bias || !y || N <= 0 || (cin != 64 && cin != 128) || H % th || W % T_W || kpad < 9 * cin ||
+      ldx % 8 || xcoff % 8 || xcoff + cin > ldx || ldy % 8 || ycoff % 8 || ycoff + CH > ldy)
     return AI4E_EINVAL;
   if (gn_partials && (gn_groups <= 0 || CH % gn_groups || CH / gn_groups > 4)) return AI4E_EINVAL;
   if (static_cast<long>(N) * H * W * (ldx > ldy ? ldx : ldy) >= (1L << 40)) return AI4E_EINVAL;
@@ -274,12 +317,6 @@ AI4E_API int ai4e_conv3x3_tile64_fwd(const void* x, const void* w, const void* b
   p.H = H;
   p.W = W;
   p.tiles_w = W / T_W;
-  p.tiles_per_img = (H / T_H) * p.tiles_w;
-  static bool attr = [] {
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(conv3x3_tile_kernel),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, L_TOTAL) == hipSuccess;
-  }();
-  if (!attr) return AI4E_ELAUNCH;
-  hipLaunchKernelGGL(conv3x3_tile_kernel, dim3(static_cast<unsigned>(N * p.tiles_per_img)), dim3(256), L_TOTAL, stream, p);
-  return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
+  p.tiles_per_img = (H / th) * p.tiles_w;
+  return cin == 64 ? launch_tile<64>(p, N, stream) : launch_tile<128>(p, N, stream);
 }

@@ -17,19 +17,20 @@ def _conv_ref(xin: torch.Tensor, w: torch.Tensor, b: torch.Tensor) -> torch.Tens
     return y.permute(0, 2, 3, 1)
 
 
-def _case(n, h, w, seed):
+def _case(n, h, w, seed, cin=64):
     from aiforearth_api_platform_amd.ops.conv import pack_conv
     g = torch.Generator().manual_seed(seed)
-    x = torch.randn(n, h, w, 64, generator=g).to(torch.bfloat16)
-    wt = (torch.randn(64, 64, 3, 3, generator=g) * 0.05).to(torch.bfloat16).float()
+    x = torch.randn(n, h, w, cin, generator=g).to(torch.bfloat16)
+    wt = (torch.randn(64, cin, 3, 3, generator=g) * 0.05).to(torch.bfloat16).float()
     b = torch.randn(64, generator=g) * 0.1
     return x, wt, b, pack_conv(wt, b, pad=1).to(DEV)
 
 
-@pytest.mark.parametrize("n,h,w", [(2, 16, 64), (1, 64, 32), (3, 8, 96)])
-def test_conv3x3_tile64_matches_fp32(n, h, w):
+@pytest.mark.parametrize("n,h,w,cin", [(2, 16, 64, 64), (1, 64, 32, 64), (3, 8, 96, 64), (2, 12, 64, 128),
+                                       (1, 4, 32, 128)])
+def test_conv3x3_tile64_matches_fp32(n, h, w, cin):
     from aiforearth_api_platform_amd.ops.conv import conv3x3_tile64
-    x, wt, b, pc = _case(n, h, w, n * 100 + h)
+    x, wt, b, pc = _case(n, h, w, n * 100 + h, cin)
     y, st = conv3x3_tile64(x.to(DEV), pc)
     assert st is None
     ref = _conv_ref(x, wt, b)
@@ -37,13 +38,14 @@ def test_conv3x3_tile64_matches_fp32(n, h, w):
     assert rel < 6e-3, rel
 
 
-def test_conv3x3_tile64_prologue_and_sliced_input():
+@pytest.mark.parametrize("cin", [64, 128])
+def test_conv3x3_tile64_prologue_and_sliced_input(cin):
     from aiforearth_api_platform_amd.ops.conv import conv3x3_tile64
     n, h, w = 2, 16, 64
-    x, wt, b, pc = _case(n, h, w, 7)
+    x, wt, b, pc = _case(n, h, w, 7, cin)
     g = torch.Generator().manual_seed(8)
-    aff = torch.stack([0.5 + torch.rand(n, 64, generator=g), torch.randn(n, 64, generator=g) * 0.5], -1)
-    wide = torch.zeros(n, h, w, 128, dtype=torch.bfloat16)
+    aff = torch.stack([0.5 + torch.rand(n, cin, generator=g), torch.randn(n, cin, generator=g) * 0.5], -1)
+    wide = torch.zeros(n, h, w, cin + 64, dtype=torch.bfloat16)
     wide[..., 64:] = x
     y, _ = conv3x3_tile64(wide.to(DEV)[..., 64:], pc, pro=aff.to(DEV).contiguous(), pro_relu=True)
     xin = torch.relu(x.float() * aff[:, None, None, :, 0] + aff[:, None, None, :, 1]).to(torch.bfloat16)
@@ -52,14 +54,14 @@ def test_conv3x3_tile64_prologue_and_sliced_input():
     assert rel < 6e-3, rel
 
 
-@pytest.mark.parametrize("groups", [32, 16])
-def test_conv3x3_tile64_groupnorm_statistics(groups):
+@pytest.mark.parametrize("groups,cin", [(32, 64), (16, 64), (32, 128)])
+def test_conv3x3_tile64_groupnorm_statistics(groups, cin):
     """The epilogue's shifted per-tile sums, finalized (ops.norm.group_norm_affine), equal the GroupNorm affine of
     the stored output computed directly in fp64."""
     from aiforearth_api_platform_amd.ops.conv import conv3x3_tile64
     from aiforearth_api_platform_amd.ops.norm import group_norm_affine
     n, h, w = 2, 32, 64
-    x, wt, b, pc = _case(n, h, w, 21)
+    x, wt, b, pc = _case(n, h, w, 21, cin)
     y, st = conv3x3_tile64(x.to(DEV), pc, gn_groups=groups)
     gamma = torch.linspace(0.5, 1.5, 64)
     beta = torch.linspace(-0.2, 0.2, 64)
