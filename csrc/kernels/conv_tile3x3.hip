@@ -1,4 +1,4 @@
-// K1t: 3x3 / stride 1 / pad 1 convolution, 64 -> 64 channels, NHWC bf16, for wide feature maps: the U-Net's
+// K1t: 3x3 / stride 1 / pad 1 convolution, 64 (or 128) -> 64 channels, NHWC bf16, for wide feature maps: the U-Net's
 // full-resolution level (512^2 tiles), where the K1 implicit GEMM gathers every tap of every pixel through the
 // LDS-DMA ring (nine 16-B gathers per pixel and 32-channel step) and ran at 23 % MFMA / 1.3 TB/s
 // (profiles/r4_unet/pmc_by_kernel.txt) against an HBM floor of ~half its time.
@@ -13,7 +13,8 @@
 //   from L2 during the current tap into the other half of a two-tap LDS buffer;
 // * epilogue: + bias, bf16 store, and the GroupNorm statistics of the stored values per (image, tile, group) in the
 //   K1 conv-epilogue format (shifted sums S, Q and the shift K: norm_resample.hip gn_finalize_kernel).
-// Every global address is inside its tensor by construction (host: H % 8 == 0, W % 32 == 0, exact grid).
+// 128 input channels (TileCfg): 4 x 32 tiles, each tap's weights in two 64-channel stages.
+// Every global address is inside its tensor by construction (host: H % TH == 0, W % 32 == 0, exact grid).
 #include "common.h"
 
 namespace {
@@ -45,11 +46,11 @@ struct TileCfg {
 
 struct TileParams {
   const uint16_t* x;
-  int ldx, xcoff;          // input [N, H, W, ldx], channels [xcoff, xcoff + 64)
+  int ldx, xcoff;          // input [N, H, W, ldx], channels [xcoff, xcoff + CIN)
   const uint16_t* w;
-  int kpad;                // packed weights [64 rows, kpad >= 576], K = (kh, kw, c)
+  int kpad;                // packed weights [64 rows, kpad >= 9 CIN], K = (kh, kw, c)
   const float* bias;       // [64]
-  const float2* pro;       // prologue (a, b) per (image, channel) [N, 64]; null = none
+  const float2* pro;       // prologue (a, b) per (image, channel) [N, CIN]; null = none
   int pro_relu;
   uint16_t* y;
   int ldy, ycoff;          // output [N, H, W, ldy], channels [ycoff, ycoff + 64)
