@@ -240,9 +240,9 @@ def _tile_rows(cin: int) -> int:
 def tile64_supported(x: torch.Tensor, pc: PackedConv) -> bool:
     """Shapes K1t (``conv3x3_tile64``, csrc/kernels/conv_tile3x3.hip) takes: 3x3 / stride 1 / pad 1, 64 or 128 -> 64
     channels, bf16, W % 32 == 0 and H % 8 (64 channels) or % 4 (128): 8 x 32 / 4 x 32 output tiles;
-    AI4E_CONV_TILE64=0 turns it off (A/B)."""
+    opt-in (AI4E_CONV_TILE64=1) until measured against K1 on the GPU."""
     n, h, w, c = x.shape
-    return (os.environ.get("AI4E_CONV_TILE64", "1") != "0" and _ext.backend_for(x) == "hip"
+    return (os.environ.get("AI4E_CONV_TILE64", "0") != "0" and _ext.backend_for(x) == "hip"
             and x.dtype == torch.bfloat16 and pc.w_packed.dtype == torch.bfloat16 and (pc.kh, pc.kw) == (3, 3)
             and pc.stride == 1 and pc.pad == 1 and (pc.pad if pc.pad_hi is None else pc.pad_hi) == 1
             and pc.cin_pad in (64, 128) and c == pc.cin_pad and pc.cout == 64

@@ -12,6 +12,11 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
+@pytest.fixture(autouse=True)
+def _k1t_on(monkeypatch):
+    monkeypatch.setenv("AI4E_CONV_TILE64", "1")
+
+
 def _conv_ref(xin: torch.Tensor, w: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     y = F.conv2d(xin.permute(0, 3, 1, 2).float(), w.float(), b.float(), padding=1)
     return y.permute(0, 2, 3, 1)
@@ -84,15 +89,8 @@ def test_unet_forward_with_and_without_k1t():
     f = FusedUNet(m, device=DEV)
     img = torch.randint(0, 256, (2, 256, 256, 4), dtype=torch.uint8, generator=torch.Generator().manual_seed(3))
     y_tile = f.forward_u8(img.to(DEV)).float()
-    old = os.environ.get("AI4E_CONV_TILE64")
-    os.environ["AI4E_CONV_TILE64"] = "0"
-    try:
-        y_k1 = f.forward_u8(img.to(DEV)).float()
-    finally:
-        if old is None:
-            del os.environ["AI4E_CONV_TILE64"]
-        else:
-            os.environ["AI4E_CONV_TILE64"] = old
+    os.environ["AI4E_CONV_TILE64"] = "0"  # (the fixture restores it)
+    y_k1 = f.forward_u8(img.to(DEV)).float()
     k = f.n_classes
     rel = ((y_tile[..., :k] - y_k1[..., :k]).norm() / y_k1[..., :k].norm()).item()
     assert rel < 2e-2, rel
