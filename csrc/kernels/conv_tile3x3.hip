@@ -59,9 +59,15 @@ struct TileParams {
   int H, W, tiles_w, tiles_per_img;
 };
 
-// 16-B chunk c of row `row` (M chunks per row, a power of two) at physical chunk c ^ (row % M)
+// Byte offset within its row of 16-B chunk c of row `row` (M = 8 or 16 chunks per row): ds_read_b128 serves 16 lanes
+// per pass, and a fragment's 16 lanes read one logical chunk of 16 consecutive rows, so the physical chunks must tile
+// all 64 banks: 128-B rows (M = 8) pair up in a 256-B bank line, so the XOR key is the row PAIR index
+// ((row >> 1) & 7); 256-B rows (M = 16) each span the line, key row & 15 (tests/test_tile_layout.py).
 template <int M>
-__device__ __forceinline__ uint32_t swz(int row, int c) { return static_cast<uint32_t>((c ^ (row & (M - 1))) << 4); }
+__device__ __forceinline__ uint32_t swz(int row, int c) {
+  static_assert(M == 8 || M == 16, "8 or 16 chunks per row");
+  return static_cast<uint32_t>((c ^ (M == 8 ? ((row >> 1) & 7) : (row & 15))) << 4);
+}
 
 template <int CIN>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv3x3_tile_kernel(
