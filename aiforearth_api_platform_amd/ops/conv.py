@@ -242,7 +242,8 @@ def tile64_supported(x: torch.Tensor, pc: PackedConv) -> bool:
     channels, bf16, W % 32 == 0 and H % 8 (64 channels) or % 4 (128): 8 x 32 / 4 x 32 output tiles;
     opt-in (AI4E_CONV_TILE64=1) until measured against K1 on the GPU."""
     n, h, w, c = x.shape
-    return (os.environ.get("AI4E_CONV_TILE64", "0") != "0" and _ext.backend_for(x) == "hip"
+    mode = os.environ.get("AI4E_CONV_TILE64", "0")  # "1": both instances, "64": only 64 input channels
+    return (mode != "0" and (mode != "64" or c == 64) and _ext.backend_for(x) == "hip"
             and x.dtype == torch.bfloat16 and pc.w_packed.dtype == torch.bfloat16 and (pc.kh, pc.kw) == (3, 3)
             and pc.stride == 1 and pc.pad == 1 and (pc.pad if pc.pad_hi is None else pc.pad_hi) == 1
             and pc.cin_pad in (64, 128) and c == pc.cin_pad and pc.cout == 64
