@@ -14,7 +14,13 @@
 // * epilogue: + bias, bf16 store, and the GroupNorm statistics of the stored values per (image, tile, group) in the
 //   K1 conv-epilogue format (shifted sums S, Q and the shift K: norm_resample.hip gn_finalize_kernel).
 // 128 input channels (TileCfg): 4 x 32 tiles, each tap's weights in two 64-channel stages.
-// Every global address is inside its tensor by construction (host: H % TH == 0, W % 32 == 0, exact grid).
+// Persistent: min(tiles, 2 x CUs) workgroups walk the tiles with stride gridDim.x; the next tile's patch (11 x 16 B
+// per thread) is loaded into registers while the current tile's taps run, and its first weight stage while the
+// epilogue runs, then stored into LDS (through the prologue) behind one barrier — the per-tile load latency that
+// the one-tile-per-workgroup version exposed (1.54 TB/s, profiles/r4_k1t) hides under the MFMAs.
+// Every global address is inside its tensor by construction (host: H % TH == 0, W % 32 == 0; tile t < ntiles).
+#include <cstdlib>
+
 #include "common.h"
 
 namespace {
@@ -69,210 +75,254 @@ __device__ __forceinline__ uint32_t swz(int row, int c) {
   return static_cast<uint32_t>((c ^ (M == 8 ? ((row >> 1) & 7) : (row & 15))) << 4);
 }
 
+#ifndef AI4E_K1T_PF
+#define AI4E_K1T_PF 32
+#endif
+
 template <int CIN>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv3x3_tile_kernel(
-    const TileParams p) {
+    const TileParams p, int ntiles) {
   using Cfg = TileCfg<CIN>;
   constexpr int TH = Cfg::TH, P_CHUNKS = Cfg::P_CHUNKS, P_ITERS = Cfg::P_ITERS, NCH = Cfg::NCH, SLOT_B = Cfg::SLOT_B;
   constexpr int HALVES = Cfg::HALVES, NST = Cfg::NST, FPW = Cfg::FPW;
+  static_assert(P_ITERS <= 32, "in-image mask bits");
+  constexpr int PF = AI4E_K1T_PF < P_ITERS ? AI4E_K1T_PF : P_ITERS;  // patch chunks prefetched under the MFMAs
   extern __shared__ __attribute__((aligned(1024))) uint8_t sm[];
   uint8_t* const patch = sm;
   float2* const aff = reinterpret_cast<float2*>(sm + Cfg::L_PATCH);
   uint8_t* const wbuf = sm + Cfg::L_PATCH + Cfg::L_AFF;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int t = blockIdx.x;
-  const int img = t / p.tiles_per_img;
-  const int tin = t - img * p.tiles_per_img;
-  const int tr = tin / p.tiles_w, tc = tin - tr * p.tiles_w;
-  const int h0 = tr * TH, w0 = tc * T_W;
+  const int g4 = lane >> 4;
 
-  // ---- loads: tap 0's weights, the prologue affine, the patch; then the LDS stores
-  uint4 wv[2];
+  uint4 wv0, wv1;  // one weight stage in flight: rows n = tid / 8 and 32 + tid / 8, 16-B chunk tid % 8
   auto load_w = [&](int st) __attribute__((always_inline)) {  // stage st = (tap, 64-channel half)
     const int tap = st / HALVES, half = st - tap * HALVES;
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const int idx = tid + 256 * e, n = idx >> 3, c = idx & 7;
-      wv[e] = *reinterpret_cast<const uint4*>(p.w + static_cast<long>(n) * p.kpad + tap * CIN + half * 64 + 8 * c);
-    }
+    const uint16_t* const src = p.w + static_cast<long>(tid >> 3) * p.kpad + tap * CIN + half * 64 + 8 * (tid & 7);
+    wv0 = *reinterpret_cast<const uint4*>(src);
+    wv1 = *reinterpret_cast<const uint4*>(src + 32L * p.kpad);
   };
   auto store_w = [&](int buf) __attribute__((always_inline)) {
+    const int n = tid >> 3, c = tid & 7;
+    *reinterpret_cast<uint4*>(wbuf + buf * L_W + n * 128 + swz<8>(n, c)) = wv0;
+    *reinterpret_cast<uint4*>(wbuf + buf * L_W + (n + 32) * 128 + swz<8>(n + 32, c)) = wv1;
+  };
+  // the patch of one tile: global -> registers (pv, in-image chunks in pmask), later registers -> LDS
+  uint4 pv[P_ITERS];
+  uint32_t pmask = 0;
+  auto load_patch = [&](int img, int h0, int w0, int k0, int k1) __attribute__((always_inline)) {
+    const uint16_t* const xi = p.x + static_cast<long>(img) * p.H * p.W * p.ldx + p.xcoff;
+    int tq = tid;
+    asm volatile("" : "+v"(tq));  // recompute the chunk address math per tile (hoisted, it spills)
 #pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const int idx = tid + 256 * e, n = idx >> 3, c = idx & 7;
-      *reinterpret_cast<uint4*>(wbuf + buf * L_W + n * 128 + swz<8>(n, c)) = wv[e];
+    for (int k = k0; k < k1; ++k) {
+      const int e = tq + 256 * k;
+      const int slot = e / NCH, c = e - slot * NCH;
+      const int pr = slot / P_W, pc = slot - pr * P_W;
+      const int ih = h0 - 1 + pr, iw = w0 - 1 + pc;
+      const bool in = e < P_CHUNKS && static_cast<unsigned>(ih) < static_cast<unsigned>(p.H) &&
+                      static_cast<unsigned>(iw) < static_cast<unsigned>(p.W);
+      pmask |= in ? (1u << k) : 0u;
+      pv[k] = in ? *reinterpret_cast<const uint4*>(xi + (static_cast<long>(ih) * p.W + iw) * p.ldx + 8 * c)
+                 : make_uint4(0u, 0u, 0u, 0u);
     }
   };
+  auto store_patch = [&]() __attribute__((always_inline)) {
+    int tq = tid;
+    asm volatile("" : "+v"(tq));
+#pragma unroll
+    for (int k = 0; k < P_ITERS; ++k) {
+      const int e = tq + 256 * k;
+      if (e >= P_CHUNKS) continue;
+      const int slot = e / NCH, c = e - slot * NCH;
+      uint4 v = pv[k];
+      if (p.pro != nullptr && ((pmask >> k) & 1u)) {  // padding stays zero: the conv pads the normalized tensor
+        uint32_t wds[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          float lo, hi;
+          unpack_bf16x2(wds[q], lo, hi);
+          const float2 a0 = aff[8 * c + 2 * q], a1 = aff[8 * c + 2 * q + 1];
+          lo = lo * a0.x + a0.y;
+          hi = hi * a1.x + a1.y;
+          if (p.pro_relu) {
+            lo = fmaxf(lo, 0.f);
+            hi = fmaxf(hi, 0.f);
+          }
+          wds[q] = pack_bf16x2(lo, hi);
+        }
+        v = make_uint4(wds[0], wds[1], wds[2], wds[3]);
+      }
+      *reinterpret_cast<uint4*>(patch + slot * SLOT_B + swz<NCH>(slot, c)) = v;
+    }
+  };
+  auto coords = [&](int t, int& img, int& tin, int& h0, int& w0) __attribute__((always_inline)) {
+    img = t / p.tiles_per_img;
+    tin = t - img * p.tiles_per_img;
+    const int tr = tin / p.tiles_w, tc = tin - tr * p.tiles_w;
+    h0 = tr * TH;
+    w0 = tc * T_W;
+  };
+
+  // persistent: tiles blockIdx.x, + gridDim.x, ... (host: gridDim.x <= ntiles). The next tile's patch is loaded into
+  // registers under the current tile's weight stages and stored into the patch buffer after its epilogue.
+  int t = blockIdx.x, img, tin, h0, w0;
+  coords(t, img, tin, h0, w0);
   load_w(0);
   if (p.pro != nullptr && tid < CIN) aff[tid] = p.pro[img * CIN + tid];
-  uint4 pv[P_ITERS];
-  bool pin[P_ITERS];
-  const uint16_t* const xi = p.x + static_cast<long>(img) * p.H * p.W * p.ldx + p.xcoff;
-#pragma unroll
-  for (int k = 0; k < P_ITERS; ++k) {
-    const int e = tid + 256 * k;
-    const int slot = e / NCH, c = e - slot * NCH;
-    const int pr = slot / P_W, pc = slot - pr * P_W;
-    const int ih = h0 - 1 + pr, iw = w0 - 1 + pc;
-    pin[k] = e < P_CHUNKS && static_cast<unsigned>(ih) < static_cast<unsigned>(p.H) &&
-             static_cast<unsigned>(iw) < static_cast<unsigned>(p.W);
-    pv[k] = pin[k] ? *reinterpret_cast<const uint4*>(xi + (static_cast<long>(ih) * p.W + iw) * p.ldx + 8 * c)
-                   : make_uint4(0u, 0u, 0u, 0u);
-  }
+  pmask = 0;
+  load_patch(img, h0, w0, 0, P_ITERS);
   store_w(0);
-  if (p.pro != nullptr) __syncthreads();  // the affine is in LDS
-#pragma unroll
-  for (int k = 0; k < P_ITERS; ++k) {
-    const int e = tid + 256 * k;
-    if (e >= P_CHUNKS) continue;
-    const int slot = e / NCH, c = e - slot * NCH;
-    uint4 v = pv[k];
-    if (p.pro != nullptr && pin[k]) {  // padding stays zero: the conv pads the normalized tensor
-      uint32_t wds[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        float lo, hi;
-        unpack_bf16x2(wds[q], lo, hi);
-        const float2 a0 = aff[8 * c + 2 * q], a1 = aff[8 * c + 2 * q + 1];
-        lo = lo * a0.x + a0.y;
-        hi = hi * a1.x + a1.y;
-        if (p.pro_relu) {
-          lo = fmaxf(lo, 0.f);
-          hi = fmaxf(hi, 0.f);
-        }
-        wds[q] = pack_bf16x2(lo, hi);
-      }
-      v = make_uint4(wds[0], wds[1], wds[2], wds[3]);
-    }
-    *reinterpret_cast<uint4*>(patch + slot * SLOT_B + swz<NCH>(slot, c)) = v;
-  }
+  __syncthreads();  // the affine is in LDS
+  store_patch();
   __syncthreads();
 
-  // ---- weight stages (9 taps x CIN / 64 halves) x two 32-channel steps
-  const int g4 = lane >> 4;
-  // slot of tap (0, 0) for this lane's pixel in fragment f: tile row (TH / 4) wave + f / 2, column 16 (f & 1) + lane % 16
-  int sbase[FPW];
-#pragma unroll
-  for (int f = 0; f < FPW; ++f) sbase[f] = ((TH / 4) * wave + (f >> 1)) * P_W + 16 * (f & 1) + (lane & 15);
-  f32x4_t acc[FPW][4];
-#pragma unroll
-  for (int f = 0; f < FPW; ++f)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[f][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  for (int st = 0; st < NST; ++st) {
-    if (st + 1 < NST) load_w(st + 1);  // in flight under this stage's MFMAs
-    const int tap = st / HALVES, half = st - tap * HALVES;
-    const int kh = tap / 3, kw = tap - 3 * kh;
-    const uint8_t* const wb = wbuf + (st & 1) * L_W;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int wc = 4 * s + g4;  // chunk within the stage's 64 channels
-      bf16x8_t fx[FPW], fw[4];
-#pragma unroll
-      for (int f = 0; f < FPW; ++f) {
-        const int slot = sbase[f] + kh * P_W + kw;
-        fx[f] = *reinterpret_cast<const bf16x8_t*>(patch + slot * SLOT_B + swz<NCH>(slot, 8 * half + wc));
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int n = 16 * j + (lane & 15);
-        fw[j] = *reinterpret_cast<const bf16x8_t*>(wb + n * 128 + swz<8>(n, wc));
-      }
-#pragma unroll
-      for (int f = 0; f < FPW; ++f)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[f][j] = mfma_16x16x32<false>(fw[j], fx[f], acc[f][j]);
-    }
-    if (st + 1 < NST) store_w((st + 1) & 1);  // that buffer was last read at stage st - 1 (before the previous barrier)
-    __syncthreads();
-  }
-
-  // ---- epilogue: lane holds channels 16 j + 4 g4 + v of pixel (lane % 16) of each fragment
-  float bv[4][4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int v = 0; v < 4; ++v) bv[j][v] = p.bias[16 * j + 4 * g4 + v];
   float* const kshift = reinterpret_cast<float*>(wbuf);        // [64] the tile's first pixel, as stored
   float* const red = reinterpret_cast<float*>(wbuf) + CH;      // [4 waves][64 channels][2]
-  uint2 ov[FPW][4];
-#pragma unroll
-  for (int f = 0; f < FPW; ++f) {
-    const int oh = h0 + (TH / 4) * wave + (f >> 1), ow = w0 + 16 * (f & 1) + (lane & 15);
-    uint16_t* const dst = p.y + ((static_cast<long>(img) * p.H + oh) * p.W + ow) * p.ldy + p.ycoff;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      ov[f][j] = make_uint2(pack_bf16x2(acc[f][j][0] + bv[j][0], acc[f][j][1] + bv[j][1]),
-                            pack_bf16x2(acc[f][j][2] + bv[j][2], acc[f][j][3] + bv[j][3]));
-      *reinterpret_cast<uint2*>(dst + 16 * j + 4 * g4) = ov[f][j];
+
+  for (;;) {
+    const int tn = t + static_cast<int>(gridDim.x);
+    const bool has_next = tn < ntiles;  // workgroup-uniform
+    int imgn = 0, tinn = 0, h0n = 0, w0n = 0;
+    if (has_next) {
+      coords(tn, imgn, tinn, h0n, w0n);
+      pmask = 0;
+      load_patch(imgn, h0n, w0n, 0, PF);  // in flight under this tile's MFMAs (the rest under the epilogue)
     }
-  }
-  if (p.gnp == nullptr) return;
-  // GroupNorm statistics of the stored values (cg = 64 / G channels per group, cg in {1, 2, 4}: a lane's 4 channels
-  // of one j hold whole groups), shifted by the tile's first pixel at each group's first channel
-  if (wave == 0 && (lane & 15) == 0) {
+    // ---- weight stages (9 taps x CIN / 64 halves) x two 32-channel steps
+    int l16 = lane & 15;
+    asm volatile("" : "+v"(l16));  // per-tile fragment offsets (hoisted out of the tile loop, they spill)
+    // slot of tap (0, 0) for this lane's pixel in fragment f: tile row (TH / 4) wave + f / 2, column 16 (f & 1) + l16
+    int sbase[FPW];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      float a, b, c, d;
-      unpack_bf16x2(ov[0][j].x, a, b);
-      unpack_bf16x2(ov[0][j].y, c, d);
-      kshift[16 * j + 4 * g4] = a;
-      kshift[16 * j + 4 * g4 + 1] = b;
-      kshift[16 * j + 4 * g4 + 2] = c;
-      kshift[16 * j + 4 * g4 + 3] = d;
+    for (int f = 0; f < FPW; ++f) sbase[f] = ((TH / 4) * wave + (f >> 1)) * P_W + 16 * (f & 1) + l16;
+    f32x4_t acc[FPW][4];
+#pragma unroll
+    for (int f = 0; f < FPW; ++f)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[f][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    for (int st = 0; st < NST; ++st) {
+      if (st + 1 < NST) load_w(st + 1);  // in flight under this stage's MFMAs
+      const int tap = st / HALVES, half = st - tap * HALVES;
+      const int kh = tap / 3, kw = tap - 3 * kh;
+      const uint8_t* const wb = wbuf + (st & 1) * L_W;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int wc = 4 * s + g4;  // chunk within the stage's 64 channels
+        bf16x8_t fx[FPW], fw[4];
+#pragma unroll
+        for (int f = 0; f < FPW; ++f) {
+          const int slot = sbase[f] + kh * P_W + kw;
+          fx[f] = *reinterpret_cast<const bf16x8_t*>(patch + slot * SLOT_B + swz<NCH>(slot, 8 * half + wc));
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int n = 16 * j + l16;
+          fw[j] = *reinterpret_cast<const bf16x8_t*>(wb + n * 128 + swz<8>(n, wc));
+        }
+#pragma unroll
+        for (int f = 0; f < FPW; ++f)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[f][j] = mfma_16x16x32<false>(fw[j], fx[f], acc[f][j]);
+      }
+      if (st + 1 < NST) store_w((st + 1) & 1);  // that buffer was last read at stage st - 1 (before the previous barrier)
+      __syncthreads();
     }
-  }
-  __syncthreads();
-  const int cg = CH / p.gn_groups;
-  float gs[4][4], gq[4][4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      const int ch = 16 * j + 4 * g4 + v;
-      const float K = kshift[ch - ch % cg];
-      float s = 0.f, q = 0.f;
-#pragma unroll
-      for (int f = 0; f < FPW; ++f) {
-        float a, b;
-        unpack_bf16x2(v < 2 ? ov[f][j].x : ov[f][j].y, a, b);
-        const float d = ((v & 1) ? b : a) - K;
-        s += d;
-        q += d * d;
-      }
-      gs[j][v] = s;
-      gq[j][v] = q;
+    if (has_next) {  // the next tile's first weight stage and the rest of its patch, in flight under the epilogue
+      load_w(0);
+      load_patch(imgn, h0n, w0n, PF, P_ITERS);
     }
+
+    // ---- epilogue: lane holds channels 16 j + 4 g4 + v of pixel (lane % 16) of each fragment
+    uint2 ov[FPW][4];
 #pragma unroll
-  for (int off = 1; off < 16; off <<= 1)  // over the 16 pixels of a fragment row (lanes sharing g4)
+    for (int f = 0; f < FPW; ++f) {
+      const int oh = h0 + (TH / 4) * wave + (f >> 1), ow = w0 + 16 * (f & 1) + (lane & 15);
+      uint16_t* const dst = p.y + ((static_cast<long>(img) * p.H + oh) * p.W + ow) * p.ldy + p.ycoff;
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        gs[j][v] += __shfl_xor(gs[j][v], off);
-        gq[j][v] += __shfl_xor(gq[j][v], off);
+      for (int j = 0; j < 4; ++j) {
+        const float4 bv = *reinterpret_cast<const float4*>(p.bias + 16 * j + 4 * g4);  // (re-read: frees 16 VGPRs)
+        ov[f][j] = make_uint2(pack_bf16x2(acc[f][j][0] + bv.x, acc[f][j][1] + bv.y),
+                              pack_bf16x2(acc[f][j][2] + bv.z, acc[f][j][3] + bv.w));
+        *reinterpret_cast<uint2*>(dst + 16 * j + 4 * g4) = ov[f][j];
       }
-  if ((lane & 15) == 0) {
+    }
+    if (p.gnp != nullptr) {
+      // GroupNorm statistics of the stored values (cg = 64 / G channels per group, cg in {1, 2, 4}: a lane's 4
+      // channels of one j hold whole groups), shifted by the tile's first pixel at each group's first channel
+      if (wave == 0 && (lane & 15) == 0) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < 4; ++j) {
+          float a, b, c, d;
+          unpack_bf16x2(ov[0][j].x, a, b);
+          unpack_bf16x2(ov[0][j].y, c, d);
+          kshift[16 * j + 4 * g4] = a;
+          kshift[16 * j + 4 * g4 + 1] = b;
+          kshift[16 * j + 4 * g4 + 2] = c;
+          kshift[16 * j + 4 * g4 + 3] = d;
+        }
+      }
+      __syncthreads();
+      const int cg = CH / p.gn_groups;
 #pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const int ch = 16 * j + 4 * g4 + v;
-        red[(wave * CH + ch) * 2] = gs[j][v];
-        red[(wave * CH + ch) * 2 + 1] = gq[j][v];
+      for (int j = 0; j < 4; ++j) {  // one 16-channel block at a time (register pressure)
+        float gs[4], gq[4];
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const int ch = 16 * j + 4 * g4 + v;
+          const float K = kshift[ch - ch % cg];
+          float s = 0.f, q = 0.f;
+#pragma unroll
+          for (int f = 0; f < FPW; ++f) {
+            float a, b;
+            unpack_bf16x2(v < 2 ? ov[f][j].x : ov[f][j].y, a, b);
+            const float d = ((v & 1) ? b : a) - K;
+            s += d;
+            q += d * d;
+          }
+          gs[v] = s;
+          gq[v] = q;
+        }
+#pragma unroll
+        for (int off = 1; off < 16; off <<= 1)  // over the 16 pixels of a fragment row (lanes sharing g4)
+#pragma unroll
+          for (int v = 0; v < 4; ++v) {
+            gs[v] += __shfl_xor(gs[v], off);
+            gq[v] += __shfl_xor(gq[v], off);
+          }
+        if ((lane & 15) == 0) {
+#pragma unroll
+          for (int v = 0; v < 4; ++v) {
+            const int ch = 16 * j + 4 * g4 + v;
+            red[(wave * CH + ch) * 2] = gs[v];
+            red[(wave * CH + ch) * 2 + 1] = gq[v];
+          }
+        }
       }
-  }
-  __syncthreads();
-  if (tid < p.gn_groups) {
-    float S = 0.f, Q = 0.f;
-    for (int w = 0; w < 4; ++w)
-      for (int c = 0; c < cg; ++c) {
-        S += red[(w * CH + tid * cg + c) * 2];
-        Q += red[(w * CH + tid * cg + c) * 2 + 1];
+      __syncthreads();
+      if (tid < p.gn_groups) {
+        float S = 0.f, Q = 0.f;
+        for (int w = 0; w < 4; ++w)
+          for (int c = 0; c < cg; ++c) {
+            S += red[(w * CH + tid * cg + c) * 2];
+            Q += red[(w * CH + tid * cg + c) * 2 + 1];
+          }
+        float* const o = p.gnp + ((static_cast<long>(img) * p.tiles_per_img + tin) * p.gn_groups + tid) * 4;
+        *reinterpret_cast<float4*>(o) = make_float4(S, Q, kshift[tid * cg], 0.f);
       }
-    float* const o = p.gnp + ((static_cast<long>(img) * p.tiles_per_img + tin) * p.gn_groups + tid) * 4;
-    *reinterpret_cast<float4*>(o) = make_float4(S, Q, kshift[tid * cg], 0.f);
+    }
+    if (!has_next) break;
+    __syncthreads();  // this tile's patch, weight stages and statistics scratch are read
+    if (p.pro != nullptr && tid < CIN) aff[tid] = p.pro[imgn * CIN + tid];
+    store_w(0);
+    __syncthreads();  // the next tile's affine is in LDS
+    store_patch();
+    __syncthreads();
+    t = tn;
+    img = imgn;
+    tin = tinn;
+    h0 = h0n;
+    w0 = w0n;
   }
 }
 
@@ -288,8 +338,19 @@ int launch_tile(const TileParams& p, int N, hipStream_t stream) {
                                hipFuncAttributeMaxDynamicSharedMemorySize, L) == hipSuccess;
   }();
   if (!attr) return AI4E_ELAUNCH;
-  hipLaunchKernelGGL(conv3x3_tile_kernel<CIN>, dim3(static_cast<unsigned>(N * p.tiles_per_img)), dim3(256), L, stream,
-                     p);
+  // persistent grid: two workgroups per CU (LDS), never more workgroups than tiles; AI4E_K1T_PERSIST=0 launches one
+  // workgroup per tile (no next tile, so no prefetch: the A/B reference)
+  static const bool persist = [] {
+    const char* e = std::getenv("AI4E_K1T_PERSIST");
+    return !(e && e[0] == '0');
+  }();
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+    return AI4E_ELAUNCH;
+  const int ntiles = N * p.tiles_per_img;
+  const int grid = persist && ntiles > 2 * cus ? 2 * cus : ntiles;
+  hipLaunchKernelGGL(conv3x3_tile_kernel<CIN>, dim3(static_cast<unsigned>(grid)), dim3(256), L, stream, p, ntiles);
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
 }
 
@@ -305,6 +366,7 @@ AI4E_API int ai4e_conv3x3_tile64_fwd(const void* x, const void* w, const void* b
   if (!x || !w || !bias || !y || N <= 0 || (cin != 64 && cin != 128) || H % th || W % T_W || kpad < 9 * cin ||
       ldx % 8 || xcoff % 8 || xcoff + cin > ldx || ldy % 8 || ycoff % 8 || ycoff + CH > ldy)
     return AI4E_EINVAL;
+  if (reinterpret_cast<uintptr_t>(bias) % 16) return AI4E_EINVAL;  // float4 reads in the epilogue
   if (gn_partials && (gn_groups <= 0 || CH % gn_groups || CH / gn_groups > 4)) return AI4E_EINVAL;
   if (static_cast<long>(N) * H * W * (ldx > ldy ? ldx : ldy) >= (1L << 40)) return AI4E_EINVAL;
   TileParams p;

@@ -31,8 +31,9 @@ def _case(n, h, w, seed, cin=64):
     return x, wt, b, pack_conv(wt, b, pad=1).to(DEV)
 
 
+# the last two: 768 tiles > the persistent grid (2 x 256 CUs), so workgroups walk several tiles (next-tile prefetch)
 @pytest.mark.parametrize("n,h,w,cin", [(2, 16, 64, 64), (1, 64, 32, 64), (3, 8, 96, 64), (2, 12, 64, 128),
-                                       (1, 4, 32, 128)])
+                                       (1, 4, 32, 128), (3, 128, 512, 64), (3, 64, 512, 128)])
 def test_conv3x3_tile64_matches_fp32(n, h, w, cin):
     from aiforearth_api_platform_amd.ops.conv import conv3x3_tile64
     x, wt, b, pc = _case(n, h, w, n * 100 + h, cin)
@@ -45,8 +46,9 @@ def test_conv3x3_tile64_matches_fp32(n, h, w, cin):
 
 @pytest.mark.parametrize("cin", [64, 128])
 def test_conv3x3_tile64_prologue_and_sliced_input(cin):
+    """The prologue affine is per image: 3 images of 256 (512) tiles, so persistent workgroups cross images."""
     from aiforearth_api_platform_amd.ops.conv import conv3x3_tile64
-    n, h, w = 2, 16, 64
+    n, h, w = 3, 128 if cin == 64 else 64, 512
     x, wt, b, pc = _case(n, h, w, 7, cin)
     g = torch.Generator().manual_seed(8)
     aff = torch.stack([0.5 + torch.rand(n, cin, generator=g), torch.randn(n, cin, generator=g) * 0.5], -1)
@@ -59,13 +61,13 @@ def test_conv3x3_tile64_prologue_and_sliced_input(cin):
     assert rel < 6e-3, rel
 
 
-@pytest.mark.parametrize("groups,cin", [(32, 64), (16, 64), (32, 128)])
-def test_conv3x3_tile64_groupnorm_statistics(groups, cin):
+@pytest.mark.parametrize("groups,cin,n,h,w", [(32, 64, 2, 32, 64), (16, 64, 2, 32, 64), (32, 128, 2, 32, 64),
+                                              (32, 64, 3, 128, 512)])
+def test_conv3x3_tile64_groupnorm_statistics(groups, cin, n, h, w):
     """The epilogue's shifted per-tile sums, finalized (ops.norm.group_norm_affine), equal the GroupNorm affine of
-    the stored output computed directly in fp64."""
+    the stored output computed directly in fp64 (the last case: several tiles per persistent workgroup)."""
     from aiforearth_api_platform_amd.ops.conv import conv3x3_tile64
     from aiforearth_api_platform_amd.ops.norm import group_norm_affine
-    n, h, w = 2, 32, 64
     x, wt, b, pc = _case(n, h, w, 21, cin)
     y, st = conv3x3_tile64(x.to(DEV), pc, gn_groups=groups)
     gamma = torch.linspace(0.5, 1.5, 64)
