@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Per-kernel VGPR / spill / occupancy table of one HIP source (hipcc -Rpass-analysis=kernel-resource-usage).
+"""Per-kernel VGPR / spill / scratch / occupancy table of one HIP source (hipcc -Rpass-analysis=kernel-resource-usage).
 
     python tools/kernel_resources.py csrc/kernels/conv_chain.hip [name-filter]
 """
@@ -26,5 +26,7 @@ for line in out.splitlines():
         cur[k] = v
 for r in rows:
     if flt in r["name"]:
+        # scratch also counts private arrays the compiler did not promote to registers (not reported as spills)
         print(f"{r.get('VGPRs','?'):>4} vgpr {r.get('AGPRs','?'):>3} agpr spill {r.get('VGPRs Spill','?'):>3} "
+              f"scratch {r.get('ScratchSize [bytes/lane]','?'):>4} "
               f"occ {r.get('Occupancy [waves/SIMD]','?'):>2}  {r['name'][:150]}")
