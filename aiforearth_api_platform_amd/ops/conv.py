@@ -234,12 +234,12 @@ def conv2d_gn_nhwc(x: torch.Tensor, pc: PackedConv, groups: int, out: Optional[t
 
 
 def _tile_rows(cin: int) -> int:
-    return 8 if cin == 64 else 4
+    return 8  # both instances: 8 x 32 tiles (128 input channels as two 64-channel k-slices)
 
 
 def tile64_supported(x: torch.Tensor, pc: PackedConv) -> bool:
     """Shapes K1t (``conv3x3_tile64``, csrc/kernels/conv_tile3x3.hip) takes: 3x3 / stride 1 / pad 1, 64 or 128 -> 64
-    channels, bf16, W % 32 == 0 and H % 8 (64 channels) or % 4 (128): 8 x 32 / 4 x 32 output tiles
+    channels, bf16, W % 32 == 0 and H % 8 == 0: 8 x 32 output tiles
     (AI4E_CONV_TILE64: "64" default, "1" both instances, "0" off)."""
     n, h, w, c = x.shape
     # default "64": the 64 -> 64 instance only (with its fused GroupNorm prologue the U-Net's full-resolution DoubleConv
@@ -256,7 +256,7 @@ def tile64_supported(x: torch.Tensor, pc: PackedConv) -> bool:
 def conv3x3_tile64(x: torch.Tensor, pc: PackedConv, pro: Optional[torch.Tensor] = None, pro_relu: bool = True,
                    gn_groups: int = 0) -> Tuple[torch.Tensor, Optional[tuple]]:
     """K1t: ``conv3x3(pro(x)) + bias`` for 64 or 128 -> 64 channels (see ``tile64_supported``), one 8 x 32 (4 x 32)
-    output tile per workgroup from an LDS input patch. ``pro``: float32 [N, C, 2] per-(image, channel) affine applied
+    output tile at a time per persistent workgroup from an LDS input patch. ``pro``: float32 [N, C, 2] per-(image, channel) affine applied
     to the input as it is loaded (``x * a + b``, then ReLU with ``pro_relu``): the previous GroupNorm, which then
     needs no apply pass (``norm.group_norm_affine``). Returns ``(y, stats)`` with ``stats`` = ``(partials,
     nchunks)`` GroupNorm statistics of y (as ``conv2d_gn_nhwc``) when ``gn_groups``, else None."""

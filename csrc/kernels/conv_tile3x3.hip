@@ -3,7 +3,7 @@
 // LDS-DMA ring (nine 16-B gathers per pixel and 32-channel step) and ran at 23 % MFMA / 1.3 TB/s
 // (profiles/r4_unet/pmc_by_kernel.txt) against an HBM floor of ~half its time.
 //
-// One workgroup (4 waves) per 8 x 32 output tile:
+// Each 8 x 32 output tile is computed by one workgroup (4 waves):
 // * the 10 x 34 x 64 input patch (halo 1, zero outside the image) is loaded ONCE into LDS (43.5 KB, 16-B chunks of a
 //   pixel slot XOR-swizzled by the slot index so the 16 pixels of a fragment read conflict-free), optionally through
 //   a prologue: x * a[c] + b[c] (+ ReLU) per (image, channel) — the previous layer's GroupNorm apply, so that the
@@ -13,7 +13,7 @@
 //   from L2 during the current tap into the other half of a two-tap LDS buffer;
 // * epilogue: + bias, bf16 store, and the GroupNorm statistics of the stored values per (image, tile, group) in the
 //   K1 conv-epilogue format (shifted sums S, Q and the shift K: norm_resample.hip gn_finalize_kernel).
-// 128 input channels (TileCfg): 4 x 32 tiles, each tap's weights in two 64-channel stages.
+// 128 input channels (TileCfg): the same 8 x 32 tiles, run as two 64-channel k-slices (accumulators carried over).
 // Persistent: min(tiles, 2 x CUs) workgroups walk the tiles with stride gridDim.x; the next tile's patch (11 x 16 B
 // per thread) is loaded into registers while the current tile's taps run, and its first weight stage while the
 // epilogue runs, then stored into LDS (through the prologue) behind one barrier — the per-tile load latency that
@@ -29,22 +29,23 @@ constexpr int T_W = 32, P_W = T_W + 2;           // output tile width; patch wid
 constexpr int CH = 64;                           // output channels (and the channels of one weight stage)
 constexpr int L_W = CH * CH * 2;                 // one weight stage: 64 output x 64 input channels of one tap, 8 KB
 
-// CIN = 64: 8 x 32 tiles (patch 10 x 34 x 128 B = 43.5 KB); CIN = 128 (the U-Net's last decoder c1, reading the
-// [skip | upsampled] concat): 4 x 32 tiles (patch 6 x 34 x 256 B = 52 KB), each tap's weights in two 64-channel
-// stages. Both keep two workgroups per CU.
+// 8 x 32 output tiles from a 10 x 34 x 64-channel input patch (43.5 KB). CIN = 128 (the U-Net's last decoder c1,
+// reading the [skip | upsampled] concat) runs each tile as two 64-channel k-slices through the same patch buffer:
+// the accumulators carry over, the epilogue runs once, and the second slice's patch is prefetched under the first
+// slice's taps like the next tile's. LDS: patch + CIN x 8 B affine + two 8 KB weight stages; two workgroups per CU.
 template <int CIN>
 struct TileCfg {
-  static constexpr int TH = CIN == 64 ? 8 : 4;          // output tile rows
+  static constexpr int TH = 8;                          // output tile rows
   static constexpr int P_SLOTS = (TH + 2) * P_W;
-  static constexpr int NCH = CIN / 8;                   // 16-B chunks per pixel slot
-  static constexpr int SLOT_B = CIN * 2;
+  static constexpr int NCH = 8;                         // 16-B chunks per 64-channel pixel slot
+  static constexpr int SLOT_B = 128;
   static constexpr int L_PATCH = P_SLOTS * SLOT_B;
   static constexpr int L_AFF = CIN * 8;                 // prologue affine of this image: CIN x (a, b)
   static constexpr int L_TOTAL = L_PATCH + L_AFF + 2 * L_W;
   static constexpr int P_CHUNKS = P_SLOTS * NCH;
   static constexpr int P_ITERS = (P_CHUNKS + 255) / 256;
-  static constexpr int HALVES = CIN / 64;               // weight stages per tap
-  static constexpr int NST = 9 * HALVES;
+  static constexpr int KS = CIN / 64;                   // 64-channel k-slices per tile
+  static constexpr int NST = 9;                         // weight stages (taps) per k-slice
   static constexpr int FPW = TH / 2;                    // pixel fragments per wave (TH / 4 rows x 2 half-rows)
   static_assert(CIN == 64 || CIN == 128, "K1t: 64 or 128 input channels");
   static_assert(L_TOTAL <= 80 * 1024, "two workgroups per CU");
@@ -65,14 +66,14 @@ struct TileParams {
   int H, W, tiles_w, tiles_per_img;
 };
 
-// Byte offset within its row of 16-B chunk c of row `row` (M = 8 or 16 chunks per row): ds_read_b128 serves 16 lanes
-// per pass, and a fragment's 16 lanes read one logical chunk of 16 consecutive rows, so the physical chunks must tile
-// all 64 banks: 128-B rows (M = 8) pair up in a 256-B bank line, so the XOR key is the row PAIR index
-// ((row >> 1) & 7); 256-B rows (M = 16) each span the line, key row & 15 (tests/test_tile_layout.py).
+// Byte offset within its row of 16-B chunk c of row `row` (M = 8 chunks per row): ds_read_b128 serves 16 lanes per
+// pass, and a fragment's 16 lanes read one logical chunk of 16 consecutive rows, so the physical chunks must tile all
+// 64 banks: 128-B rows pair up in a 256-B bank line, so the XOR key is the row PAIR index ((row >> 1) & 7)
+// (tests/test_tile_layout.py).
 template <int M>
 __device__ __forceinline__ uint32_t swz(int row, int c) {
-  static_assert(M == 8 || M == 16, "8 or 16 chunks per row");
-  return static_cast<uint32_t>((c ^ (M == 8 ? ((row >> 1) & 7) : (row & 15))) << 4);
+  static_assert(M == 8, "8 chunks per row");
+  return static_cast<uint32_t>((c ^ ((row >> 1) & 7)) << 4);
 }
 
 #ifndef AI4E_K1T_PF
@@ -84,7 +85,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     const TileParams p, int ntiles) {
   using Cfg = TileCfg<CIN>;
   constexpr int TH = Cfg::TH, P_CHUNKS = Cfg::P_CHUNKS, P_ITERS = Cfg::P_ITERS, NCH = Cfg::NCH, SLOT_B = Cfg::SLOT_B;
-  constexpr int HALVES = Cfg::HALVES, NST = Cfg::NST, FPW = Cfg::FPW;
+  constexpr int KS = Cfg::KS, NST = Cfg::NST, FPW = Cfg::FPW;
   static_assert(P_ITERS <= 32, "in-image mask bits");
   constexpr int PF = AI4E_K1T_PF < P_ITERS ? AI4E_K1T_PF : P_ITERS;  // patch chunks prefetched under the MFMAs
   extern __shared__ __attribute__((aligned(1024))) uint8_t sm[];
@@ -96,9 +97,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const int g4 = lane >> 4;
 
   uint4 wv0, wv1;  // one weight stage in flight: rows n = tid / 8 and 32 + tid / 8, 16-B chunk tid % 8
-  auto load_w = [&](int st) __attribute__((always_inline)) {  // stage st = (tap, 64-channel half)
-    const int tap = st / HALVES, half = st - tap * HALVES;
-    const uint16_t* const src = p.w + static_cast<long>(tid >> 3) * p.kpad + tap * CIN + half * 64 + 8 * (tid & 7);
+  auto load_w = [&](int tap, int ks) __attribute__((always_inline)) {  // stage = (tap, 64-channel k-slice)
+    const uint16_t* const src = p.w + static_cast<long>(tid >> 3) * p.kpad + tap * CIN + ks * 64 + 8 * (tid & 7);
     wv0 = *reinterpret_cast<const uint4*>(src);
     wv1 = *reinterpret_cast<const uint4*>(src + 32L * p.kpad);
   };
@@ -110,8 +110,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   // the patch of one tile: global -> registers (pv, in-image chunks in pmask), later registers -> LDS
   uint4 pv[P_ITERS];
   uint32_t pmask = 0;
-  auto load_patch = [&](int img, int h0, int w0, int k0, int k1) __attribute__((always_inline)) {
-    const uint16_t* const xi = p.x + static_cast<long>(img) * p.H * p.W * p.ldx + p.xcoff;
+  auto load_patch = [&](int img, int h0, int w0, int ks, int k0, int k1) __attribute__((always_inline)) {
+    const uint16_t* const xi = p.x + static_cast<long>(img) * p.H * p.W * p.ldx + p.xcoff + 64 * ks;
     int tq = tid;
     asm volatile("" : "+v"(tq));  // recompute the chunk address math per tile (hoisted, it spills)
 #pragma unroll
@@ -127,7 +127,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
                  : make_uint4(0u, 0u, 0u, 0u);
     }
   };
-  auto store_patch = [&]() __attribute__((always_inline)) {
+  auto store_patch = [&](int ks) __attribute__((always_inline)) {
     int tq = tid;
     asm volatile("" : "+v"(tq));
 #pragma unroll
@@ -142,7 +142,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         for (int q = 0; q < 4; ++q) {
           float lo, hi;
           unpack_bf16x2(wds[q], lo, hi);
-          const float2 a0 = aff[8 * c + 2 * q], a1 = aff[8 * c + 2 * q + 1];
+          const float2 a0 = aff[64 * ks + 8 * c + 2 * q], a1 = aff[64 * ks + 8 * c + 2 * q + 1];
           lo = lo * a0.x + a0.y;
           hi = hi * a1.x + a1.y;
           if (p.pro_relu) {
@@ -164,30 +164,42 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     w0 = tc * T_W;
   };
 
-  // persistent: tiles blockIdx.x, + gridDim.x, ... (host: gridDim.x <= ntiles). The next tile's patch is loaded into
-  // registers under the current tile's weight stages and stored into the patch buffer after its epilogue.
-  int t = blockIdx.x, img, tin, h0, w0;
+  // persistent: tiles blockIdx.x, + gridDim.x, ... (host: gridDim.x <= ntiles), each as KS k-slices. The next
+  // (tile, slice)'s patch is loaded into registers under the current slice's taps and stored into the patch buffer
+  // after it (and after the tile's epilogue).
+  int t = blockIdx.x, ks = 0, img, tin, h0, w0;
   coords(t, img, tin, h0, w0);
-  load_w(0);
+  load_w(0, 0);
   if (p.pro != nullptr && tid < CIN) aff[tid] = p.pro[img * CIN + tid];
   pmask = 0;
-  load_patch(img, h0, w0, 0, P_ITERS);
+  load_patch(img, h0, w0, 0, 0, P_ITERS);
   store_w(0);
   __syncthreads();  // the affine is in LDS
-  store_patch();
+  store_patch(0);
   __syncthreads();
 
   float* const kshift = reinterpret_cast<float*>(wbuf);        // [64] the tile's first pixel, as stored
   float* const red = reinterpret_cast<float*>(wbuf) + CH;      // [4 waves][64 channels][2]
 
+  f32x4_t acc[FPW][4];  // carried over the k-slices of a tile; zeroed here and after each tile's epilogue
+  auto zero_acc = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int f = 0; f < FPW; ++f)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[f][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  };
+  zero_acc();
   for (;;) {
-    const int tn = t + static_cast<int>(gridDim.x);
-    const bool has_next = tn < ntiles;  // workgroup-uniform
-    int imgn = 0, tinn = 0, h0n = 0, w0n = 0;
+    // the next (tile, slice): workgroup-uniform
+    const bool last_slice = ks == KS - 1;
+    const int tn = last_slice ? t + static_cast<int>(gridDim.x) : t;
+    const int ksn = last_slice ? 0 : ks + 1;
+    const bool has_next = tn < ntiles;
+    int imgn = img, tinn = tin, h0n = h0, w0n = w0;
     if (has_next) {
-      coords(tn, imgn, tinn, h0n, w0n);
+      if (last_slice) coords(tn, imgn, tinn, h0n, w0n);
       pmask = 0;
-      load_patch(imgn, h0n, w0n, 0, PF);  // in flight under this tile's MFMAs (the rest under the epilogue)
+      load_patch(imgn, h0n, w0n, ksn, 0, PF);  // in flight under this slice's MFMAs (the rest under the epilogue)
     }
     // ---- weight stages (9 taps x CIN / 64 halves) x two 32-channel steps
     int l16 = lane & 15;
@@ -196,15 +208,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     int sbase[FPW];
 #pragma unroll
     for (int f = 0; f < FPW; ++f) sbase[f] = ((TH / 4) * wave + (f >> 1)) * P_W + 16 * (f & 1) + l16;
-    f32x4_t acc[FPW][4];
-#pragma unroll
-    for (int f = 0; f < FPW; ++f)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[f][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-    for (int st = 0; st < NST; ++st) {
-      if (st + 1 < NST) load_w(st + 1);  // in flight under this stage's MFMAs
-      const int tap = st / HALVES, half = st - tap * HALVES;
-      const int kh = tap / 3, kw = tap - 3 * kh;
+    for (int st = 0; st < NST; ++st) {  // stage = tap
+      if (st + 1 < NST) load_w(st + 1, ks);  // in flight under this stage's MFMAs
+      const int kh = st / 3, kw = st - 3 * kh;
       const uint8_t* const wb = wbuf + (st & 1) * L_W;
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
@@ -213,7 +219,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
         for (int f = 0; f < FPW; ++f) {
           const int slot = sbase[f] + kh * P_W + kw;
-          fx[f] = *reinterpret_cast<const bf16x8_t*>(patch + slot * SLOT_B + swz<NCH>(slot, 8 * half + wc));
+          fx[f] = *reinterpret_cast<const bf16x8_t*>(patch + slot * SLOT_B + swz<NCH>(slot, wc));
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -228,97 +234,102 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       if (st + 1 < NST) store_w((st + 1) & 1);  // that buffer was last read at stage st - 1 (before the previous barrier)
       __syncthreads();
     }
-    if (has_next) {  // the next tile's first weight stage and the rest of its patch, in flight under the epilogue
-      load_w(0);
-      load_patch(imgn, h0n, w0n, PF, P_ITERS);
+    if (has_next) {  // the next slice's first weight stage and the rest of its patch, in flight under the epilogue
+      load_w(0, ksn);
+      load_patch(imgn, h0n, w0n, ksn, PF, P_ITERS);
     }
 
-    // ---- epilogue: lane holds channels 16 j + 4 g4 + v of pixel (lane % 16) of each fragment
-    uint2 ov[FPW][4];
-#pragma unroll
-    for (int f = 0; f < FPW; ++f) {
-      const int oh = h0 + (TH / 4) * wave + (f >> 1), ow = w0 + 16 * (f & 1) + (lane & 15);
-      uint16_t* const dst = p.y + ((static_cast<long>(img) * p.H + oh) * p.W + ow) * p.ldy + p.ycoff;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float4 bv = *reinterpret_cast<const float4*>(p.bias + 16 * j + 4 * g4);  // (re-read: frees 16 VGPRs)
-        ov[f][j] = make_uint2(pack_bf16x2(acc[f][j][0] + bv.x, acc[f][j][1] + bv.y),
-                              pack_bf16x2(acc[f][j][2] + bv.z, acc[f][j][3] + bv.w));
-        *reinterpret_cast<uint2*>(dst + 16 * j + 4 * g4) = ov[f][j];
-      }
-    }
-    if (p.gnp != nullptr) {
-      // GroupNorm statistics of the stored values (cg = 64 / G channels per group, cg in {1, 2, 4}: a lane's 4
-      // channels of one j hold whole groups), shifted by the tile's first pixel at each group's first channel
-      if (wave == 0 && (lane & 15) == 0) {
-#pragma unroll
+    // ---- epilogue (after the tile's last slice): lane holds channels 16 j + 4 g4 + v of pixel (lane % 16) of
+    // each fragment
+    if (last_slice) {
+      uint2 ov[FPW][4];
+  #pragma unroll
+      for (int f = 0; f < FPW; ++f) {
+        const int oh = h0 + (TH / 4) * wave + (f >> 1), ow = w0 + 16 * (f & 1) + (lane & 15);
+        uint16_t* const dst = p.y + ((static_cast<long>(img) * p.H + oh) * p.W + ow) * p.ldy + p.ycoff;
+  #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          float a, b, c, d;
-          unpack_bf16x2(ov[0][j].x, a, b);
-          unpack_bf16x2(ov[0][j].y, c, d);
-          kshift[16 * j + 4 * g4] = a;
-          kshift[16 * j + 4 * g4 + 1] = b;
-          kshift[16 * j + 4 * g4 + 2] = c;
-          kshift[16 * j + 4 * g4 + 3] = d;
+          const float4 bv = *reinterpret_cast<const float4*>(p.bias + 16 * j + 4 * g4);  // (re-read: frees 16 VGPRs)
+          ov[f][j] = make_uint2(pack_bf16x2(acc[f][j][0] + bv.x, acc[f][j][1] + bv.y),
+                                pack_bf16x2(acc[f][j][2] + bv.z, acc[f][j][3] + bv.w));
+          *reinterpret_cast<uint2*>(dst + 16 * j + 4 * g4) = ov[f][j];
         }
       }
-      __syncthreads();
-      const int cg = CH / p.gn_groups;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {  // one 16-channel block at a time (register pressure)
-        float gs[4], gq[4];
-#pragma unroll
-        for (int v = 0; v < 4; ++v) {
-          const int ch = 16 * j + 4 * g4 + v;
-          const float K = kshift[ch - ch % cg];
-          float s = 0.f, q = 0.f;
-#pragma unroll
-          for (int f = 0; f < FPW; ++f) {
-            float a, b;
-            unpack_bf16x2(v < 2 ? ov[f][j].x : ov[f][j].y, a, b);
-            const float d = ((v & 1) ? b : a) - K;
-            s += d;
-            q += d * d;
+      if (p.gnp != nullptr) {
+        // GroupNorm statistics of the stored values (cg = 64 / G channels per group, cg in {1, 2, 4}: a lane's 4
+        // channels of one j hold whole groups), shifted by the tile's first pixel at each group's first channel
+        if (wave == 0 && (lane & 15) == 0) {
+  #pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            float a, b, c, d;
+            unpack_bf16x2(ov[0][j].x, a, b);
+            unpack_bf16x2(ov[0][j].y, c, d);
+            kshift[16 * j + 4 * g4] = a;
+            kshift[16 * j + 4 * g4 + 1] = b;
+            kshift[16 * j + 4 * g4 + 2] = c;
+            kshift[16 * j + 4 * g4 + 3] = d;
           }
-          gs[v] = s;
-          gq[v] = q;
         }
-#pragma unroll
-        for (int off = 1; off < 16; off <<= 1)  // over the 16 pixels of a fragment row (lanes sharing g4)
-#pragma unroll
-          for (int v = 0; v < 4; ++v) {
-            gs[v] += __shfl_xor(gs[v], off);
-            gq[v] += __shfl_xor(gq[v], off);
-          }
-        if ((lane & 15) == 0) {
-#pragma unroll
+        __syncthreads();
+        const int cg = CH / p.gn_groups;
+  #pragma unroll
+        for (int j = 0; j < 4; ++j) {  // one 16-channel block at a time (register pressure)
+          float gs[4], gq[4];
+  #pragma unroll
           for (int v = 0; v < 4; ++v) {
             const int ch = 16 * j + 4 * g4 + v;
-            red[(wave * CH + ch) * 2] = gs[v];
-            red[(wave * CH + ch) * 2 + 1] = gq[v];
+            const float K = kshift[ch - ch % cg];
+            float s = 0.f, q = 0.f;
+  #pragma unroll
+            for (int f = 0; f < FPW; ++f) {
+              float a, b;
+              unpack_bf16x2(v < 2 ? ov[f][j].x : ov[f][j].y, a, b);
+              const float d = ((v & 1) ? b : a) - K;
+              s += d;
+              q += d * d;
+            }
+            gs[v] = s;
+            gq[v] = q;
+          }
+  #pragma unroll
+          for (int off = 1; off < 16; off <<= 1)  // over the 16 pixels of a fragment row (lanes sharing g4)
+  #pragma unroll
+            for (int v = 0; v < 4; ++v) {
+              gs[v] += __shfl_xor(gs[v], off);
+              gq[v] += __shfl_xor(gq[v], off);
+            }
+          if ((lane & 15) == 0) {
+  #pragma unroll
+            for (int v = 0; v < 4; ++v) {
+              const int ch = 16 * j + 4 * g4 + v;
+              red[(wave * CH + ch) * 2] = gs[v];
+              red[(wave * CH + ch) * 2 + 1] = gq[v];
+            }
           }
         }
+        __syncthreads();
+        if (tid < p.gn_groups) {
+          float S = 0.f, Q = 0.f;
+          for (int w = 0; w < 4; ++w)
+            for (int c = 0; c < cg; ++c) {
+              S += red[(w * CH + tid * cg + c) * 2];
+              Q += red[(w * CH + tid * cg + c) * 2 + 1];
+            }
+          float* const o = p.gnp + ((static_cast<long>(img) * p.tiles_per_img + tin) * p.gn_groups + tid) * 4;
+          *reinterpret_cast<float4*>(o) = make_float4(S, Q, kshift[tid * cg], 0.f);
+        }
       }
-      __syncthreads();
-      if (tid < p.gn_groups) {
-        float S = 0.f, Q = 0.f;
-        for (int w = 0; w < 4; ++w)
-          for (int c = 0; c < cg; ++c) {
-            S += red[(w * CH + tid * cg + c) * 2];
-            Q += red[(w * CH + tid * cg + c) * 2 + 1];
-          }
-        float* const o = p.gnp + ((static_cast<long>(img) * p.tiles_per_img + tin) * p.gn_groups + tid) * 4;
-        *reinterpret_cast<float4*>(o) = make_float4(S, Q, kshift[tid * cg], 0.f);
-      }
-    }
+      zero_acc();  // (not at the next slice's start: that keeps the old values live through the epilogue)
+    }  // last_slice
     if (!has_next) break;
-    __syncthreads();  // this tile's patch, weight stages and statistics scratch are read
-    if (p.pro != nullptr && tid < CIN) aff[tid] = p.pro[imgn * CIN + tid];
+    __syncthreads();  // this slice's patch, weight stages and statistics scratch are read
+    if (last_slice && p.pro != nullptr && tid < CIN) aff[tid] = p.pro[imgn * CIN + tid];
     store_w(0);
     __syncthreads();  // the next tile's affine is in LDS
-    store_patch();
+    store_patch(ksn);
     __syncthreads();
     t = tn;
+    ks = ksn;
     img = imgn;
     tin = tinn;
     h0 = h0n;
@@ -357,12 +368,13 @@ int launch_tile(const TileParams& p, int N, hipStream_t stream) {
 }  // namespace
 
 // y = conv3x3(pro(x)) + bias (cin = 64 or 128 -> 64 channels, stride 1, pad 1) with GroupNorm partials of y
-// (gn_groups > 0): [N, (H / TH) * (W / 32), G, 4] (TH = 8 for cin 64, 4 for 128). pro: null or float2 [N, cin]
+// (gn_groups > 0): [N, (H / 8) * (W / 32), G, 4]. pro: null or float2 [N, cin]
 // (x * a + b, then ReLU if pro_relu).
 AI4E_API int ai4e_conv3x3_tile64_fwd(const void* x, const void* w, const void* bias, const void* pro, int pro_relu,
                                       void* y, int N, int H, int W, int cin, int ldx, int xcoff, int kpad, int ldy,
                                       int ycoff, void* gn_partials, int gn_groups, hipStream_t stream) {
-  const int th = cin == 64 ? TileCfg<64>::TH : TileCfg<128>::TH;
+  const int th = TileCfg<64>::TH;
+  static_assert(TileCfg<64>::TH == TileCfg<128>::TH, "one tile geometry");
   if (!x || !w || !bias || !y || N <= 0 || (cin != 64 && cin != 128) || H % th || W % T_W || kpad < 9 * cin ||
       ldx % 8 || xcoff % 8 || xcoff + cin > ldx || ldy % 8 || ycoff % 8 || ycoff + CH > ldy)
     return AI4E_EINVAL;
