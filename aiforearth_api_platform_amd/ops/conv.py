@@ -240,11 +240,11 @@ def _tile_rows(cin: int) -> int:
 def tile64_supported(x: torch.Tensor, pc: PackedConv) -> bool:
     """Shapes K1t (``conv3x3_tile64``, csrc/kernels/conv_tile3x3.hip) takes: 3x3 / stride 1 / pad 1, 64 or 128 -> 64
     channels, bf16, W % 32 == 0 and H % 8 == 0: 8 x 32 output tiles
-    (AI4E_CONV_TILE64: "64" default, "1" both instances, "0" off)."""
+    (AI4E_CONV_TILE64: "1" default, both instances; "64" the 64 -> 64 instance only; "0" off)."""
     n, h, w, c = x.shape
-    # default "64": the 64 -> 64 instance only (with its fused GroupNorm prologue the U-Net's full-resolution DoubleConv
-    # beats K1 + the apply pass; the 128 -> 64 instance is 55 % slower than K1: profiles/r4_k1t/); "1": both; "0": off
-    mode = os.environ.get("AI4E_CONV_TILE64", "64")
+    # both instances beat K1 (profiles/r4_k1t/: 600 vs 665 us and 871 vs 1000 us per conv over 16 tiles of 512^2;
+    # U-Net 24.0 vs 22.5 mosaics/s with K1)
+    mode = os.environ.get("AI4E_CONV_TILE64", "1")
     return (mode != "0" and (mode != "64" or c == 64) and _ext.backend_for(x) == "hip"
             and x.dtype == torch.bfloat16 and pc.w_packed.dtype == torch.bfloat16 and (pc.kh, pc.kw) == (3, 3)
             and pc.stride == 1 and pc.pad == 1 and (pc.pad if pc.pad_hi is None else pc.pad_hi) == 1
