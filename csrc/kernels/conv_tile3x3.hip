@@ -41,7 +41,7 @@ struct TileCfg {
   static constexpr int SLOT_B = 128;
   static constexpr int L_PATCH = P_SLOTS * SLOT_B;
   static constexpr int L_AFF = CIN * 8;                 // prologue affine of this image: CIN x (a, b)
-  static constexpr int L_TOTAL = L_PATCH + L_AFF + 2 * L_W;
+  static constexpr int L_TOTAL = L_PATCH + L_AFF + 2 * L_W + CH * 4;  // + the bias (64 floats)
   static constexpr int P_CHUNKS = P_SLOTS * NCH;
   static constexpr int P_ITERS = (P_CHUNKS + 255) / 256;
   static constexpr int KS = CIN / 64;                   // 64-channel k-slices per tile
@@ -73,15 +73,17 @@ struct TileParams {
 // 8 (row & 1) + (c ^ key(row)), so for every window of 16 rows the keys of each row parity, with the middle pixels'
 // extra ^ 1, must be distinct: key = row & 6 is (tests/test_tile_layout.py searches and checks this). The earlier key
 // (row >> 1) & 7 was conflict-free only for contiguous 16-lane groups, and measured 16-18 % bank conflicts.
+// LDS handoff between the waves: wait for this wave's LDS operations, then the barrier. Not __syncthreads(): its
+// workgroup release fence makes the compiler drain vmcnt (which on gfx9 counts loads and stores together) before
+// every barrier, so the weight and next-patch loads in flight would be waited for at each of the 9 stages. Nothing
+// in this kernel passes data between waves through global memory.
+__device__ __forceinline__ void tile_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 template <int M>
 __device__ __forceinline__ uint32_t swz(int row, int c) {
   static_assert(M == 8, "8 chunks per row");
   return static_cast<uint32_t>((c ^ (row & 6)) << 4);
 }
-
-#ifndef AI4E_K1T_PF
-#define AI4E_K1T_PF 32
-#endif
 
 template <int CIN>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv3x3_tile_kernel(
@@ -90,11 +92,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   constexpr int TH = Cfg::TH, P_CHUNKS = Cfg::P_CHUNKS, P_ITERS = Cfg::P_ITERS, NCH = Cfg::NCH, SLOT_B = Cfg::SLOT_B;
   constexpr int KS = Cfg::KS, NST = Cfg::NST, FPW = Cfg::FPW;
   static_assert(P_ITERS <= 32, "in-image mask bits");
-  constexpr int PF = AI4E_K1T_PF < P_ITERS ? AI4E_K1T_PF : P_ITERS;  // patch chunks prefetched under the MFMAs
+  constexpr int PPS = (P_ITERS + NST - 2) / (NST - 1);  // next-patch chunk loads per stage (stages 0 .. NST - 2)
   extern __shared__ __attribute__((aligned(1024))) uint8_t sm[];
   uint8_t* const patch = sm;
   float2* const aff = reinterpret_cast<float2*>(sm + Cfg::L_PATCH);
   uint8_t* const wbuf = sm + Cfg::L_PATCH + Cfg::L_AFF;
+  float* const sbias = reinterpret_cast<float*>(wbuf + 2 * L_W);  // [64]: epilogue reads stay off the vmcnt queue
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g4 = lane >> 4;
@@ -126,8 +129,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       const bool in = e < P_CHUNKS && static_cast<unsigned>(ih) < static_cast<unsigned>(p.H) &&
                       static_cast<unsigned>(iw) < static_cast<unsigned>(p.W);
       pmask |= in ? (1u << k) : 0u;
-      pv[k] = in ? *reinterpret_cast<const uint4*>(xi + (static_cast<long>(ih) * p.W + iw) * p.ldx + 8 * c)
-                 : make_uint4(0u, 0u, 0u, 0u);
+      // unconditional load from the nearest in-image pixel (no branch around it, so the vmcnt waits stay exact);
+      // store_patch zeroes the chunks outside the image
+      const int ihc = min(max(ih, 0), p.H - 1), iwc = min(max(iw, 0), p.W - 1);
+      pv[k] = *reinterpret_cast<const uint4*>(xi + (static_cast<long>(ihc) * p.W + iwc) * p.ldx + 8 * (c & 7));
     }
   };
   auto store_patch = [&](int ks) __attribute__((always_inline)) {
@@ -138,8 +143,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       const int e = tq + 256 * k;
       if (e >= P_CHUNKS) continue;
       const int slot = e / NCH, c = e - slot * NCH;
-      uint4 v = pv[k];
-      if (p.pro != nullptr && ((pmask >> k) & 1u)) {  // padding stays zero: the conv pads the normalized tensor
+      const bool in = (pmask >> k) & 1u;
+      uint4 v = in ? pv[k] : make_uint4(0u, 0u, 0u, 0u);
+      if (p.pro != nullptr && in) {  // padding stays zero: the conv pads the normalized tensor
         uint32_t wds[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -174,12 +180,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   coords(t, img, tin, h0, w0);
   load_w(0, 0);
   if (p.pro != nullptr && tid < CIN) aff[tid] = p.pro[img * CIN + tid];
+  if (tid < CH) sbias[tid] = p.bias[tid];
   pmask = 0;
   load_patch(img, h0, w0, 0, 0, P_ITERS);
   store_w(0);
-  __syncthreads();  // the affine is in LDS
+  tile_barrier();  // the affine is in LDS
   store_patch(0);
-  __syncthreads();
+  tile_barrier();
 
   float* const kshift = reinterpret_cast<float*>(wbuf);        // [64] the tile's first pixel, as stored
   float* const red = reinterpret_cast<float*>(wbuf) + CH;      // [4 waves][64 channels][2]
@@ -198,12 +205,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     const int tn = last_slice ? t + static_cast<int>(gridDim.x) : t;
     const int ksn = last_slice ? 0 : ks + 1;
     const bool has_next = tn < ntiles;
+    // without a next item the "next" coordinates stay the current ones: the loads below are then issued anyway (to
+    // valid addresses, their data unused) — a branch around them would make every later vmcnt wait a full drain
     int imgn = img, tinn = tin, h0n = h0, w0n = w0;
-    if (has_next) {
-      if (last_slice) coords(tn, imgn, tinn, h0n, w0n);
-      pmask = 0;
-      load_patch(imgn, h0n, w0n, ksn, 0, PF);  // in flight under this slice's MFMAs (the rest under the epilogue)
-    }
+    if (has_next && last_slice) coords(tn, imgn, tinn, h0n, w0n);
+    pmask = 0;
     // ---- weight stages (9 taps x CIN / 64 halves) x two 32-channel steps
     int l16 = lane & 15;
     asm volatile("" : "+v"(l16));  // per-tile fragment offsets (hoisted out of the tile loop, they spill)
@@ -211,8 +217,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     int sbase[FPW];
 #pragma unroll
     for (int f = 0; f < FPW; ++f) sbase[f] = ((TH / 4) * wave + (f >> 1)) * P_W + 16 * (f & 1) + l16;
+#pragma unroll
     for (int st = 0; st < NST; ++st) {  // stage = tap
-      if (st + 1 < NST) load_w(st + 1, ks);  // in flight under this stage's MFMAs
+      // issue order is the wait order (vmcnt retires in order): this stage's weight chunks first, then PPS chunks
+      // of the next (tile, slice)'s patch, which the waits of later stages cover; pinned against the scheduler,
+      // which otherwise sinks the weight loads to their use at the end of the stage
+      if (st + 1 < NST) load_w(st + 1, ks);
+      load_patch(imgn, h0n, w0n, ksn, st * PPS < P_ITERS ? st * PPS : P_ITERS,
+                 (st + 1) * PPS < P_ITERS ? (st + 1) * PPS : P_ITERS);
+      __builtin_amdgcn_sched_barrier(0);
       const int kh = st / 3, kw = st - 3 * kh;
       const uint8_t* const wb = wbuf + (st & 1) * L_W;
 #pragma unroll
@@ -235,12 +248,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
           for (int j = 0; j < 4; ++j) acc[f][j] = mfma_16x16x32<false>(fw[j], fx[f], acc[f][j]);
       }
       if (st + 1 < NST) store_w((st + 1) & 1);  // that buffer was last read at stage st - 1 (before the previous barrier)
-      __syncthreads();
+      tile_barrier();
     }
-    if (has_next) {  // the next slice's first weight stage and the rest of its patch, in flight under the epilogue
-      load_w(0, ksn);
-      load_patch(imgn, h0n, w0n, ksn, PF, P_ITERS);
-    }
+    load_w(0, ksn);  // the next slice's first weight stage, in flight under the epilogue (unused after the last)
 
     // ---- epilogue (after the tile's last slice): lane holds channels 16 j + 4 g4 + v of pixel (lane % 16) of
     // each fragment
@@ -252,7 +262,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         uint16_t* const dst = p.y + ((static_cast<long>(img) * p.H + oh) * p.W + ow) * p.ldy + p.ycoff;
   #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const float4 bv = *reinterpret_cast<const float4*>(p.bias + 16 * j + 4 * g4);  // (re-read: frees 16 VGPRs)
+          const float4 bv = *reinterpret_cast<const float4*>(sbias + 16 * j + 4 * g4);  // LDS: frees 16 VGPRs
           ov[f][j] = make_uint2(pack_bf16x2(acc[f][j][0] + bv.x, acc[f][j][1] + bv.y),
                                 pack_bf16x2(acc[f][j][2] + bv.z, acc[f][j][3] + bv.w));
           *reinterpret_cast<uint2*>(dst + 16 * j + 4 * g4) = ov[f][j];
@@ -273,7 +283,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
             kshift[16 * j + 4 * g4 + 3] = d;
           }
         }
-        __syncthreads();
+        tile_barrier();
         const int cg = CH / p.gn_groups;
   #pragma unroll
         for (int j = 0; j < 4; ++j) {  // one 16-channel block at a time (register pressure)
@@ -310,7 +320,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
             }
           }
         }
-        __syncthreads();
+        tile_barrier();
         if (tid < p.gn_groups) {
           float S = 0.f, Q = 0.f;
           for (int w = 0; w < 4; ++w)
@@ -325,12 +335,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       zero_acc();  // (not at the next slice's start: that keeps the old values live through the epilogue)
     }  // last_slice
     if (!has_next) break;
-    __syncthreads();  // this slice's patch, weight stages and statistics scratch are read
+    tile_barrier();  // this slice's patch, weight stages and statistics scratch are read
     if (last_slice && p.pro != nullptr && tid < CIN) aff[tid] = p.pro[imgn * CIN + tid];
     store_w(0);
-    __syncthreads();  // the next tile's affine is in LDS
+    tile_barrier();  // the next tile's affine is in LDS
     store_patch(ksn);
-    __syncthreads();
+    tile_barrier();
     t = tn;
     ks = ksn;
     img = imgn;
