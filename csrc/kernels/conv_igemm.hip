@@ -113,6 +113,21 @@ enum { GATHER_GENERAL = 0,  // any C % 8: a 32-wide K chunk may span taps -> per
 // OCC = workgroups per CU the config is built for (waves per SIMD): 2 for the 4-stage ring (64 KB of
 // LDS), 3 for the 3-stage ring (48 KB) — the register budget (<= 512/OCC VGPRs) must let that many
 // resident, which is what lets a 766-tile layer3 grid run as ONE balanced round on 256 CUs.
+// Epilogue LDS handoffs between the waves (the staged fp32 tile, the GroupNorm reduction): wait for this wave's LDS
+// operations, then the barrier. Not __syncthreads(): its workgroup release fence makes the compiler drain vmcnt (on
+// gfx9 it counts loads and stores together) at every handoff, so each pass waited for the previous pass's output
+// stores and its residual loads, and the last pass for all its stores before the workgroup could retire. The ring's
+// LDS-DMA loads are drained explicitly (wait_vmcnt<0>) before the epilogue. AI4E_EPI_FENCE=1 builds the old form
+// (A/B library variant).
+#ifndef AI4E_EPI_FENCE
+#define AI4E_EPI_FENCE 0
+#endif
+#if AI4E_EPI_FENCE
+#define EPI_BARRIER() __syncthreads()
+#else
+#define EPI_BARRIER() asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory")
+#endif
+
 template <int WAVES_M, int WAVES_N, int STAGES, int GATHER, bool EPI_LDS, int OCC = 2, bool F16 = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC > 2 ? OCC : 1, OCC))) void conv_igemm_kernel(const ConvParams p) {
   static_assert(WAVES_M * WAVES_N == 4, "4 waves per workgroup");
@@ -345,7 +360,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC > 2 ? O
     __builtin_amdgcn_s_barrier();  // all waves finished reading the last stage
 #pragma unroll
     for (int pass = 0; pass < EPI_PASSES; ++pass) {
-    if (pass) __syncthreads();  // the first half is stored before the second overwrites it
+    if (pass) EPI_BARRIER();  // the first half is stored before the second overwrites it
     constexpr int PC = EPI_CHUNKS / EPI_PASSES;
     uint4 rlate[PC];
     if constexpr (!EARLY_RES) {
@@ -369,7 +384,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC > 2 ? O
         }
       }
     }
-    __syncthreads();
+    EPI_BARRIER();
     if (p.gnp && pass == 0) {
       // GN shift per channel slot: the tile's first pixel (row 0, unswizzled) at the group's first channel
       const int cg = p.Kout / p.gn_groups;
@@ -445,7 +460,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC > 2 ? O
         case 4: reduce(std::integral_constant<int, 4>{}); break;
         default: reduce(std::integral_constant<int, 8>{}); break;
       }
-      __syncthreads();
+      EPI_BARRIER();
       float* red = tile;  // [4 waves][BN channel slots][2]; slot c holds channels c .. c + cgm - 1
       if (lane < CPR) {
 #pragma unroll
@@ -456,7 +471,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC > 2 ? O
           }
         }
       }
-      __syncthreads();
+      EPI_BARRIER();
       const int ng = min(BN, p.Kout - n0) / cg;  // host: BN % cg == 0, Kout % cg == 0
       if (tid < ng) {
         float S = 0.f, Q = 0.f;
@@ -836,7 +851,7 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
         }
       }
     }
-    __syncthreads();
+    EPI_BARRIER();
     constexpr int EP = WROWS / 16;  // 16-B output chunks per thread and pass
     uint4 rv[EP];
     if (p.res) {
@@ -862,7 +877,7 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
       const uint4 o = epilogue8<F16>(f, p.res != nullptr, rv[e], (p.relu & 1) != 0);
       if (m < p.M && n < p.Kout) ai4e_conv::st16_stream(p.y + static_cast<long>(m) * p.ldy + p.ycoff + n, o);
     }
-    __syncthreads();
+    EPI_BARRIER();
   }
 #if AI4E_K256_STAMPS
   wait_vmcnt<0>();
