@@ -25,7 +25,8 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops.conv import PackedConv, conv2d_gn_nhwc, conv2d_nhwc, conv3x3_tile64, pack_conv, tile64_supported
-from ..ops.norm import group_norm_affine, group_norm_nhwc, upsample2x_nhwc
+from ..ops.norm import (gn_relu_head8, gn_relu_head8_supported, group_norm_affine, group_norm_nhwc,
+                        upsample2x_nhwc)
 from ..ops.pool import maxpool2d_nhwc, preprocess_u8
 
 # per-band normalisation for uint8 RGB+NIR imagery (NAIP-style); NIR uses the same scale
@@ -102,7 +103,10 @@ class _FusedDouble:
         return 64 % g == 0 and 64 // g <= 4
 
     def __call__(self, x: torch.Tensor, out: Optional[torch.Tensor] = None,
-                 pool_out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                 pool_out: Optional[torch.Tensor] = None, head=None):
+        """``head``: a 1x1 PackedConv to apply after the final GroupNorm + ReLU; then returns ``(y, headed)`` where
+        ``headed`` says whether ``y`` is already the head's output (fused: csrc/kernels/norm_resample.hip
+        gn_relu_head8_kernel) or still the block output."""
         # GroupNorm statistics come out of the conv epilogues (conv2d_gn_nhwc, K1t) where the tile allows
         if tile64_supported(x, self.c1) and self._k1t_groups(self.g1[2]):
             y, st = conv3x3_tile64(x, self.c1, gn_groups=self.g1[2])  # e.g. the last decoder's 128 -> 64 c1
@@ -114,12 +118,19 @@ class _FusedDouble:
             n, h, w, c = y.shape
             ss = group_norm_affine(st, *self.g1[:2], n=n, hw=h * w, c=c, groups=self.g1[2])
             z, st = conv3x3_tile64(y, self.c2, pro=ss, pro_relu=True, gn_groups=self.g2[2])
-            return group_norm_nhwc(z, *self.g2[:2], groups=self.g2[2], relu=True, out=out if out is not None else z,
-                                   stats=st, pool_out=pool_out)
+            if head is not None and pool_out is None and gn_relu_head8_supported(z, head):
+                # the last decoder: GroupNorm + ReLU + the 1x1 head in one pass over z (the normalized tensor is
+                # never written, and the head conv does not read it back)
+                ss2 = group_norm_affine(st, *self.g2[:2], n=n, hw=h * w, c=c, groups=self.g2[2])
+                return gn_relu_head8(z, ss2, head), True
+            r = group_norm_nhwc(z, *self.g2[:2], groups=self.g2[2], relu=True, out=out if out is not None else z,
+                                stats=st, pool_out=pool_out)
+            return (r, False) if head is not None else r
         y = group_norm_nhwc(y, *self.g1[:2], groups=self.g1[2], relu=True, out=y, stats=st)
         z, st = conv2d_gn_nhwc(y, self.c2, self.g2[2])
-        return group_norm_nhwc(z, *self.g2[:2], groups=self.g2[2], relu=True, out=out if out is not None else z,
-                               stats=st, pool_out=pool_out)
+        r = group_norm_nhwc(z, *self.g2[:2], groups=self.g2[2], relu=True, out=out if out is not None else z,
+                            stats=st, pool_out=pool_out)
+        return (r, False) if head is not None else r
 
 
 class FusedUNet:
@@ -139,6 +150,8 @@ class FusedUNet:
         self.outc = pack_conv(w, b).to(d)
         self.out_channels = kout
         self.fused_pool = os.environ.get("AI4E_UNET_FUSED_POOL", "1") != "0"
+        # the last decoder's GroupNorm + ReLU and the 1x1 head in one pass (AI4E_UNET_FUSED_HEAD=0: apply, then conv)
+        self.fused_head = os.environ.get("AI4E_UNET_FUSED_HEAD", "1") != "0"
 
     def tensors(self) -> List[torch.Tensor]:
         """Every weight tensor (packed convs + GroupNorm affine), for ``parallel.dist.broadcast_tensors``."""
@@ -174,7 +187,12 @@ class FusedUNet:
         for i, lvl in enumerate((3, 2, 1, 0)):
             buf = cat[lvl]
             upsample2x_nhwc(y, out=buf, out_coff=enc_c[lvl])
-            y = self.up[i](buf)
+            if i == 3 and self.fused_head:
+                y, headed = self.up[i](buf, head=self.outc)
+                if headed:
+                    return y
+            else:
+                y = self.up[i](buf)
         return conv2d_nhwc(y, self.outc)
 
     def _forward_unfused(self, x, cat, enc_c):

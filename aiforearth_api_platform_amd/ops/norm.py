@@ -38,6 +38,30 @@ def group_norm_affine(stats, gamma: torch.Tensor, beta: torch.Tensor, n: int, hw
     return partials[off:off + n * c * 2].view(n, c, 2)
 
 
+def gn_relu_head8_supported(z: torch.Tensor, pc) -> bool:
+    """Shapes ``gn_relu_head8`` takes: bf16 NHWC z with 64 channels (may be a channel slice), H * W % 32 == 0, and a
+    1x1 / stride-1 conv of 64 -> 8 output channels (the U-Net head with its classes padded to 8)."""
+    n, h, w, c = z.shape
+    return (_ext.backend_for(z) == "hip" and z.dtype == torch.bfloat16 and c == 64 and (h * w) % 32 == 0
+            and (pc.kh, pc.kw) == (1, 1) and pc.stride == 1 and pc.pad == 0 and pc.cin_pad == 64 and pc.cout == 8
+            and pc.w_packed.dtype == torch.bfloat16 and z.stride(3) == 1 and z.stride(2) % 8 == 0
+            and z.stride(1) == w * z.stride(2) and z.stride(0) == h * z.stride(1))
+
+
+def gn_relu_head8(z: torch.Tensor, ss: torch.Tensor, pc) -> torch.Tensor:
+    """``conv1x1(relu(z * a + b)) + bias`` for 64 -> 8 channels in one pass over ``z`` (csrc/kernels/norm_resample.hip
+    gn_relu_head8_kernel): ``ss`` float32 [N, 64, 2] is the GroupNorm affine from ``group_norm_affine``; the normalized
+    tensor is never written. Returns [N, H, W, 8] bf16."""
+    n, h, w, c = z.shape
+    if not gn_relu_head8_supported(z, pc):
+        raise ValueError("gn_relu_head8: unsupported shape / layout (see gn_relu_head8_supported)")
+    ldz, zoff = _nhwc_ld(z)
+    y = torch.empty(n, h, w, 8, device=z.device, dtype=torch.bfloat16)
+    _ext.call("ai4e_gn_relu_head8", _base_ptr(z), ldz, zoff, ss.data_ptr(), pc.w_packed.data_ptr(), pc.kpad,
+              pc.bias.data_ptr(), y.data_ptr(), n, h * w, _ext.stream_ptr(z.device))
+    return y
+
+
 def group_norm_nhwc(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, groups: int = 32, eps: float = 1e-5,
                     relu: bool = False, out: Optional[torch.Tensor] = None, stats=None,
                     pool_out: Optional[torch.Tensor] = None) -> torch.Tensor:

@@ -213,6 +213,73 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const uint16_t* __restric
   }
 }
 
+// U-Net head: logits = conv1x1(relu(GroupNorm(z))) + bias, 64 -> 8 channels, in ONE pass over z (instead of an apply
+// pass that writes the normalized tensor and a 1x1 conv that reads it back: ~2x the HBM traffic of the full-resolution
+// 64-channel tensor). The norm arrives as the per-(image, channel) affine of ai4e_groupnorm_finalize. 8 lanes per
+// pixel: lane = 8-channel column (one coalesced 16-B load; a wave covers 8 whole pixels), the normalized values are
+// rounded to bf16 and ReLU'd exactly as the apply pass stores them, each lane forms the 8 outputs' partial dot
+// products over its 8 channels, and a transpose-reduce over the 8 lanes (xor 4, 2, 1: 4 + 2 + 1 shuffles) leaves lane
+// c8 with output channel c8, so a wave stores 8 pixels x 8 bf16 = 128 contiguous bytes. Host: HW % 32 == 0, so every
+// block iteration covers 32 whole pixels and all lanes run the same trip count (full shuffle groups).
+__global__ __launch_bounds__(256) void gn_relu_head8_kernel(const uint16_t* __restrict__ z, int ldz,
+                                                            const float2* __restrict__ ss,
+                                                            const uint16_t* __restrict__ w, int kpad,
+                                                            const float* __restrict__ bias, uint16_t* __restrict__ y,
+                                                            int HW) {
+  const int n = blockIdx.y;
+  const int c8 = threadIdx.x & 7;
+  float a[8], b[8], wt[8][8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float2 v = ss[n * 64 + 8 * c8 + j];
+    a[j] = v.x;
+    b[j] = v.y;
+  }
+#pragma unroll
+  for (int o = 0; o < 8; ++o)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) wt[o][j] = bf16_to_f32(w[o * kpad + 8 * c8 + j]);
+  const float bo = bias[c8];
+  const bool h4 = (c8 & 4) != 0, h2 = (c8 & 2) != 0, h1 = (c8 & 1) != 0;
+  const uint16_t* const zn = z + static_cast<long>(n) * HW * ldz + 8 * c8;
+  uint16_t* const yn = y + static_cast<long>(n) * HW * 8;
+  const int S = gridDim.x * 32;  // pixels per grid stride
+  for (int p0 = blockIdx.x * 32; p0 < HW; p0 += 4 * S) {  // block-uniform bounds (HW % 32 == 0)
+    uint4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)  // the lane's loads first, then the math
+      if (p0 + u * S < HW) v[u] = *reinterpret_cast<const uint4*>(zn + static_cast<long>(p0 + u * S + (threadIdx.x >> 3)) * ldz);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (p0 + u * S >= HW) break;
+      const uint32_t q[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+      float f[8];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        float lo, hi;
+        unpack_bf16x2(q[k], lo, hi);
+        unpack_bf16x2(relu_bf16x2(cvt_bf16x2(fmaf(lo, a[2 * k], b[2 * k]), fmaf(hi, a[2 * k + 1], b[2 * k + 1]))),
+                      f[2 * k], f[2 * k + 1]);
+      }
+      float s8[8];
+#pragma unroll
+      for (int o = 0; o < 8; ++o) {
+        float acc = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc = fmaf(wt[o][j], f[j], acc);
+        s8[o] = acc;
+      }
+      float t[4], r2[2];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) t[k] = (h4 ? s8[k + 4] : s8[k]) + __shfl_xor(h4 ? s8[k] : s8[k + 4], 4);
+#pragma unroll
+      for (int k = 0; k < 2; ++k) r2[k] = (h2 ? t[k + 2] : t[k]) + __shfl_xor(h2 ? t[k] : t[k + 2], 2);
+      const float r = (h1 ? r2[1] : r2[0]) + __shfl_xor(h1 ? r2[0] : r2[1], 1);  // output channel 4 h4 + 2 h2 + h1
+      yn[static_cast<long>(p0 + u * S + (threadIdx.x >> 3)) * 8 + c8] = f32_to_bf16(r + bo);
+    }
+  }
+}
+
 // GN apply (+ReLU) that also emits the 2x2/2 max-pool of its output (the U-Net encoder's skip tensor and the
 // next level's input from one pass: the pool never re-reads the skip). One lane = one 8-channel column of a
 // 2x2 pixel quad; H, W even; pooled [N, H/2, W/2, C] contiguous.
@@ -417,5 +484,22 @@ AI4E_API int ai4e_upsample2x_bilinear(const void* x, void* y, int N, int H, int 
   else
     hipLaunchKernelGGL(upsample2x_kernel<long>, dim3(grid_for(total)), dim3(256), 0, s, static_cast<const uint16_t*>(x),
                        static_cast<uint16_t*>(y), N, H, W, C, ldy, ycoff);
+  return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
+}
+
+// logits [N, HW, 8] = conv1x1(relu(z * a + b)) + bias: z [N, HW, ldz] bf16, channels [zoff, zoff + 64); ss float2
+// [N, 64] (ai4e_groupnorm_finalize); w bf16 [>= 8 rows, kpad >= 64] (row o = output channel o, K = input channel);
+// bias fp32 [>= 8]. HW % 32 == 0.
+AI4E_API int ai4e_gn_relu_head8(const void* z, int ldz, int zoff, const void* ss, const void* w, int kpad,
+                                const void* bias, void* y, int N, int HW, hipStream_t s) {
+  if (!z || !ss || !w || !bias || !y || N <= 0 || HW <= 0 || HW % 32 || ldz % 8 || zoff % 8 || zoff + 64 > ldz ||
+      kpad < 64 || N > 65535)
+    return AI4E_EINVAL;
+  if (static_cast<long>(HW) * ldz >= (1L << 40)) return AI4E_EINVAL;
+  const int blocks = HW / 32;
+  const int gx = blocks < 4 * 1024 ? (blocks + 3) / 4 : 1024;  // ~4 pixels per lane
+  hipLaunchKernelGGL(gn_relu_head8_kernel, dim3(gx, N), dim3(256), 0, s, static_cast<const uint16_t*>(z) + zoff, ldz,
+                     static_cast<const float2*>(ss), static_cast<const uint16_t*>(w), kpad,
+                     static_cast<const float*>(bias), static_cast<uint16_t*>(y), HW);
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
 }

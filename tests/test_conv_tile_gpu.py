@@ -99,3 +99,44 @@ def test_unet_forward_with_and_without_k1t():
     assert rel < 2e-2, rel
     agree = (y_tile[..., :k].argmax(-1) == y_k1[..., :k].argmax(-1)).float().mean().item()
     assert agree > 0.97, agree
+
+
+@pytest.mark.parametrize("n,h,w,slice_", [(2, 32, 64, False), (3, 64, 96, True)])
+def test_gn_relu_head8_matches_fp32(n, h, w, slice_):
+    """The fused U-Net head (csrc/kernels/norm_resample.hip gn_relu_head8_kernel): conv1x1(relu(z * a + b)) + bias,
+    64 -> 8, against fp32 PyTorch of the same op (normalized values rounded to bf16 as the apply pass stores them)."""
+    from aiforearth_api_platform_amd.ops.conv import pack_conv
+    from aiforearth_api_platform_amd.ops.norm import gn_relu_head8
+    g = torch.Generator().manual_seed(n * 7 + h)
+    z = torch.randn(n, h, w, 64, generator=g).to(torch.bfloat16)
+    ss = torch.stack([0.5 + torch.rand(n, 64, generator=g), torch.randn(n, 64, generator=g) * 0.3], -1)
+    wt = (torch.randn(8, 64, 1, 1, generator=g) * 0.1).to(torch.bfloat16).float()
+    b = torch.randn(8, generator=g) * 0.1
+    pc = pack_conv(wt, b).to(DEV)
+    zin = z
+    if slice_:  # a channel slice of a wider buffer
+        wide = torch.zeros(n, h, w, 128, dtype=torch.bfloat16)
+        wide[..., 64:] = z
+        zin = wide.to(DEV)[..., 64:]
+    y = gn_relu_head8(zin.to(DEV), ss.to(DEV).contiguous(), pc).float().cpu()
+    xn = torch.relu((z.float() * ss[:, None, None, :, 0] + ss[:, None, None, :, 1]).to(torch.bfloat16).float())
+    ref = xn @ wt.reshape(8, 64).t() + b
+    rel = ((y - ref).norm() / ref.norm()).item()
+    assert rel < 6e-3, rel
+
+
+def test_unet_fused_head_equals_apply_then_conv():
+    """The U-Net forward with the fused head equals AI4E_UNET_FUSED_HEAD=0 (GroupNorm apply, then the 1x1 head)."""
+    from aiforearth_api_platform_amd.models.unet import FusedUNet, unet_landcover
+    m = unet_landcover(seed=5)
+    img = torch.randint(0, 256, (2, 256, 256, 4), dtype=torch.uint8, generator=torch.Generator().manual_seed(5))
+    y_f = FusedUNet(m, device=DEV).forward_u8(img.to(DEV)).float()
+    os.environ["AI4E_UNET_FUSED_HEAD"] = "0"
+    try:
+        y_u = FusedUNet(m, device=DEV).forward_u8(img.to(DEV)).float()
+    finally:
+        del os.environ["AI4E_UNET_FUSED_HEAD"]
+    k = m.n_classes
+    rel = ((y_f[..., :k] - y_u[..., :k]).norm() / y_u[..., :k].norm()).item()
+    assert rel < 1e-2, rel
+    assert (y_f[..., :k].argmax(-1) == y_u[..., :k].argmax(-1)).float().mean().item() > 0.99
