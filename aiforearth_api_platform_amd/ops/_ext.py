@@ -70,6 +70,7 @@ _SIGS = {
     "ai4e_stream_get_cu_mask": [_vp, _vp, _c_int],
     "ai4e_cu_census": [_vp, _c_int, _c_int, _vp],
     "ai4e_groupnorm_finalize": [_vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_float, _c_int, _vp],
+    "ai4e_gn_chunk_px": [],
     "ai4e_gn_relu_head8": [_vp, _c_int, _c_int, _vp, _vp, _c_int, _vp, _vp, _c_int, _c_int, _vp],
     "ai4e_conv3x3_tile64_fwd": [_vp, _vp, _vp, _vp, _c_int, _vp] + [_c_int] * 9 + [_vp, _c_int, _vp],
     "ai4e_crumbs_alloc": [_c_int, _vp, _vp],
@@ -109,6 +110,18 @@ def call(name: str, *args) -> None:
     rc = getattr(lib(), name)(*args)
     if rc != 0:
         raise KernelError(f"{name} failed with status {rc}")
+
+
+def call_int(name: str, *args) -> int:
+    """A library function that returns a value rather than a status (e.g. ``ai4e_gn_chunk_px``)."""
+    if name not in _SIGS:
+        raise KernelError(f"{name}: no argument signature registered in ops/_ext.py _SIGS")
+    return int(getattr(lib(), name)(*args))
+
+
+def has(name: str) -> bool:
+    """Whether the loaded kernel library exports ``name`` (an A/B build of an older tree may not)."""
+    return getattr(lib(), name, None) is not None
 
 
 def stream_ptr(device: Optional[torch.device] = None) -> int:

@@ -8,7 +8,16 @@ import torch.nn.functional as F
 
 from . import _ext
 
-GN_PIX_PER_BLOCK = 1024
+_GN_CHUNK = []
+
+
+def _gn_chunk_px() -> int:
+    """Pixels per GroupNorm statistics chunk, from the kernel library (csrc/kernels/norm_resample.hip
+    GN_PIX_PER_BLOCK): the workspace of ``ai4e_groupnorm_nhwc`` is sized from it."""
+    if not _GN_CHUNK:
+        # a library from before the export used 1024-pixel chunks
+        _GN_CHUNK.append(_ext.call_int("ai4e_gn_chunk_px") if _ext.has("ai4e_gn_chunk_px") else 1024)
+    return _GN_CHUNK[0]
 
 
 def _nhwc_ld(t: torch.Tensor):
@@ -98,7 +107,8 @@ def group_norm_nhwc(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, gr
                       partials.data_ptr(), n, h * w, c, groups, eps, int(relu), ldx | (ldy << 16),
                       xcoff | (ycoff << 16), nchunks, _ext.stream_ptr(x.device))
             return out
-        nchunks = (h * w + GN_PIX_PER_BLOCK - 1) // GN_PIX_PER_BLOCK
+        chunk = _gn_chunk_px()
+        nchunks = (h * w + chunk - 1) // chunk
         # chunk partials, then the per-channel affine (scale, shift) the finalize launch writes
         partials = torch.empty(n * nchunks * groups * 4 + n * c * 2, device=x.device, dtype=torch.float32)
         g32 = gamma.to(x.device, torch.float32).contiguous()

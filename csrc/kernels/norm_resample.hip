@@ -16,7 +16,13 @@
 
 namespace {
 
-constexpr int GN_PIX_PER_BLOCK = 1024;
+// pixels per statistics chunk (one workgroup each). 256, not 1024: the U-Net's deep levels (64^2 and 32^2 maps of
+// 512-1024 channels, 16 tiles) then still launch 256 / 64 workgroups instead of 64 / 16, which ran the statistics
+// pass at 1.06 TB/s (profiles/r4h_unet/pmc_by_kernel.txt). ops/norm.py sizes the workspace from ai4e_gn_chunk_px().
+#ifndef AI4E_GN_CHUNK
+#define AI4E_GN_CHUNK 256
+#endif
+constexpr int GN_PIX_PER_BLOCK = AI4E_GN_CHUNK;
 constexpr int GN_PARTIAL = 4;  // floats per (chunk, group) partial: S, Q, K, pad
 
 // x: [N, HW, C] (row stride ldx, channel offset xcoff); partials: [N, nchunks, G, 2]
@@ -382,7 +388,7 @@ inline int grid_for(long work) {
 
 }  // namespace
 
-// partials (workspace) must hold N * ceil(HW / 1024) * G * 4 + N * C * 2 floats (chunk partials, then the
+// partials (workspace) must hold N * ceil(HW / GN_PIX_PER_BLOCK (256)) * G * 4 + N * C * 2 floats (chunk partials, then the
 // per-channel affine). HW * C / 8 < 2^31.
 AI4E_API int ai4e_groupnorm_nhwc(const void* x, void* y, const void* gamma, const void* beta, void* partials, int N,
                                  int HW, int C, int G, float eps, int relu, int ldx_ldy_pack, int coff_pack,
@@ -503,3 +509,6 @@ AI4E_API int ai4e_gn_relu_head8(const void* z, int ldz, int zoff, const void* ss
                      static_cast<const float*>(bias), static_cast<uint16_t*>(y), HW);
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
 }
+
+// pixels per GroupNorm statistics chunk (the workspace of ai4e_groupnorm_nhwc is sized from it)
+AI4E_API int ai4e_gn_chunk_px() { return GN_PIX_PER_BLOCK; }

@@ -1,4 +1,5 @@
 """The ctypes signatures in ops/_ext.py must match the C ABI of csrc/kernels/*.hip (CPU check)."""
+import pytest
 import re
 from pathlib import Path
 
@@ -40,3 +41,12 @@ def test_every_launcher_signature_matches():
         py = [pykind[t] for t in _ext._SIGS[name]]
         c = [_kind(a) for a in c_args]
         assert py == c, f"{name}: python {py} != C {c}"
+
+
+def test_gn_chunk_px_exported():
+    """ops/norm.py sizes the GroupNorm workspace from the library's statistics chunk (ai4e_gn_chunk_px)."""
+    from aiforearth_api_platform_amd.ops import _ext, norm
+    if not _ext.available():
+        pytest.skip("kernel library not built")
+    assert _ext.has("ai4e_gn_chunk_px")
+    assert norm._gn_chunk_px() == _ext.call_int("ai4e_gn_chunk_px") > 0
