@@ -19,6 +19,9 @@ namespace {
 // pixels per statistics chunk (one workgroup each). 256, not 1024: the U-Net's deep levels (64^2 and 32^2 maps of
 // 512-1024 channels, 16 tiles) then still launch 256 / 64 workgroups instead of 64 / 16, which ran the statistics
 // pass at 1.06 TB/s (profiles/r4h_unet/pmc_by_kernel.txt). ops/norm.py sizes the workspace from ai4e_gn_chunk_px().
+#ifndef AI4E_UPSAMPLE_QUAD
+#define AI4E_UPSAMPLE_QUAD 1  // 0: the per-output-vector upsample kernel (A/B library variant)
+#endif
 #ifndef AI4E_GN_CHUNK
 #define AI4E_GN_CHUNK 256
 #endif
@@ -381,6 +384,94 @@ __global__ __launch_bounds__(256) void upsample2x_kernel(const uint16_t* __restr
   }
 }
 
+// The same upsample, one thread per INPUT pixel and 8-channel column: its 2x2 output quad (2i .. 2i + 1, 2j .. 2j + 1)
+// reads only the 3x3 neighbourhood (rows i - 1 .. i + 1, columns j - 1 .. j + 1, clamped), loaded once: 9 gathers for
+// 4 outputs instead of 16, and the index math (divisions by C8, W, H) once per quad. With align_corners=False the
+// even output row uses rows (i - 1, i) at ly = 0.75 (at i = 0: rows (0, min(1, H - 1)) at ly = 0), the odd one rows
+// (i, min(i + 1, H - 1)) at ly = 0.25; columns alike. Rows and columns are chosen by register selects (a runtime-
+// indexed register array would live in scratch); the weights and the sum are formed exactly as upsample2x_kernel's.
+template <typename IDX>
+__global__ __launch_bounds__(256) void upsample2x_quad_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
+                                                              int N, int H, int W, int C, int ldy, int ycoff) {
+  const int C8 = C >> 3;
+  const IDX total = static_cast<IDX>(N) * H * W * C8;
+  for (IDX t = static_cast<IDX>(blockIdx.x) * 256 + threadIdx.x; t < total; t += static_cast<IDX>(gridDim.x) * 256) {
+    const IDX pix = t / C8;
+    const int c8 = static_cast<int>(t - pix * C8);
+    const IDX row = pix / W;
+    const int j = static_cast<int>(pix - row * W);
+    const int n = static_cast<int>(row / H);
+    const int i = static_cast<int>(row - static_cast<IDX>(n) * H);
+    const int r0 = i > 0 ? i - 1 : 0, r2 = i + 1 < H ? i + 1 : H - 1;
+    const int q0 = j > 0 ? j - 1 : 0, q2 = j + 1 < W ? j + 1 : W - 1;
+    const uint4* base = reinterpret_cast<const uint4*>(x) + static_cast<long>(n) * H * W * C8 + c8;
+    const int rr[3] = {r0, i, r2}, qq[3] = {q0, j, q2};
+    uint4 v[3][3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+#pragma unroll
+      for (int b = 0; b < 3; ++b) v[a][b] = base[(static_cast<long>(rr[a]) * W + qq[b]) * C8];
+    const bool top = i > 0, left = j > 0;
+#pragma unroll
+    for (int dy = 0; dy < 2; ++dy) {
+      const int oy = 2 * i + dy;
+      const float sy = fmaxf((oy + 0.5f) * 0.5f - 0.5f, 0.f);
+      const float ly = sy - static_cast<int>(sy);
+#pragma unroll
+      for (int dx = 0; dx < 2; ++dx) {
+        const int ox = 2 * j + dx;
+        const float sx = fmaxf((ox + 0.5f) * 0.5f - 0.5f, 0.f);
+        const float lx = sx - static_cast<int>(sx);
+        const float w00 = (1 - ly) * (1 - lx), w01 = (1 - ly) * lx, w10 = ly * (1 - lx), w11 = ly * lx;
+        // (y0, y1) window rows: even row (0, 1) when i > 0 else (1, 2); odd row (1, 2). Columns alike.
+        uint4 a, b, c, d;
+        auto pick = [&](const uint4& p0, const uint4& p1, bool s1) __attribute__((always_inline)) {
+          return s1 ? p0 : p1;
+        };
+        if (dy == 0) {
+          if (dx == 0) {
+            a = pick(pick(v[0][0], v[0][1], left), pick(v[1][0], v[1][1], left), top);
+            b = pick(pick(v[0][1], v[0][2], left), pick(v[1][1], v[1][2], left), top);
+            c = pick(pick(v[1][0], v[1][1], left), pick(v[2][0], v[2][1], left), top);
+            d = pick(pick(v[1][1], v[1][2], left), pick(v[2][1], v[2][2], left), top);
+          } else {
+            a = pick(v[0][1], v[1][1], top);
+            b = pick(v[0][2], v[1][2], top);
+            c = pick(v[1][1], v[2][1], top);
+            d = pick(v[1][2], v[2][2], top);
+          }
+        } else {
+          if (dx == 0) {
+            a = pick(v[1][0], v[1][1], left);
+            b = pick(v[1][1], v[1][2], left);
+            c = pick(v[2][0], v[2][1], left);
+            d = pick(v[2][1], v[2][2], left);
+          } else {
+            a = v[1][1];
+            b = v[1][2];
+            c = v[2][1];
+            d = v[2][2];
+          }
+        }
+        uint32_t out[4];
+        const uint32_t pa[4] = {a.x, a.y, a.z, a.w}, pb[4] = {b.x, b.y, b.z, b.w};
+        const uint32_t pc[4] = {c.x, c.y, c.z, c.w}, pd[4] = {d.x, d.y, d.z, d.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          float a0, a1, b0, b1, c0, c1, d0, d1;
+          unpack_bf16x2(pa[k], a0, a1);
+          unpack_bf16x2(pb[k], b0, b1);
+          unpack_bf16x2(pc[k], c0, c1);
+          unpack_bf16x2(pd[k], d0, d1);
+          out[k] = pack_bf16x2(w00 * a0 + w01 * b0 + w10 * c0 + w11 * d0, w00 * a1 + w01 * b1 + w10 * c1 + w11 * d1);
+        }
+        *reinterpret_cast<uint4*>(y + ((static_cast<long>(n) * 2 * H + oy) * 2 * W + ox) * ldy + ycoff + 8 * c8) =
+            make_uint4(out[0], out[1], out[2], out[3]);
+      }
+    }
+  }
+}
+
 inline int grid_for(long work) {
   long g = (work + 255) / 256;
   return static_cast<int>(g < 1 ? 1 : (g > 8192 ? 8192 : g));
@@ -484,6 +575,16 @@ AI4E_API int ai4e_upsample2x_bilinear(const void* x, void* y, int N, int H, int 
   (void)unused;
   if (C % 8 || ldy % 8 || ycoff % 8) return AI4E_EINVAL;
   const long total = static_cast<long>(N) * 4 * H * W * (C / 8);
+#if AI4E_UPSAMPLE_QUAD
+  const long quads = total / 4;
+  if (quads < (1L << 31) - 4 * 8192L * 256)
+    hipLaunchKernelGGL(upsample2x_quad_kernel<int>, dim3(grid_for(quads)), dim3(256), 0, s,
+                       static_cast<const uint16_t*>(x), static_cast<uint16_t*>(y), N, H, W, C, ldy, ycoff);
+  else
+    hipLaunchKernelGGL(upsample2x_quad_kernel<long>, dim3(grid_for(quads)), dim3(256), 0, s,
+                       static_cast<const uint16_t*>(x), static_cast<uint16_t*>(y), N, H, W, C, ldy, ycoff);
+  return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
+#endif
   if (total < (1L << 31) - 4 * 8192L * 256)
     hipLaunchKernelGGL(upsample2x_kernel<int>, dim3(grid_for(total)), dim3(256), 0, s, static_cast<const uint16_t*>(x),
                        static_cast<uint16_t*>(y), N, H, W, C, ldy, ycoff);

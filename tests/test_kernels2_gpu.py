@@ -90,7 +90,7 @@ def test_groupnorm_concat_slices():
     assert (out[..., 64:].float() - ref).abs().max().item() < 0.05
 
 
-@pytest.mark.parametrize("shape", [(2, 16, 16, 64), (1, 7, 9, 32), (1, 64, 64, 128)])
+@pytest.mark.parametrize("shape", [(2, 16, 16, 64), (1, 7, 9, 32), (1, 64, 64, 128), (1, 1, 1, 8), (2, 1, 5, 16), (1, 3, 1, 8)])
 def test_upsample_into_concat(shape):
     x = torch.randn(*shape, device=DEV).bfloat16()
     n, h, w, c = shape
