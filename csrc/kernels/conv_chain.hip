@@ -57,8 +57,13 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 // * patch rows are padded to W + 8 slots (row stride = W mod 8), so 16 consecutive pixels read 16 consecutive slots mod 8
 //   even where a fragment wraps to the next image row, and a masked tap reads a zero slot of the same residue mod 8
 //   instead of slot 0 (both were 2-way conflicts on the patch reads of phase A).
+// phase-A weight K steps prefetched into registers (patch mode), MID 128 / MID 64 (the MID-64 chains stay at 144
+// VGPRs and 3 workgroups per CU up to 8; deeper MID-128 prefetch spills)
 #ifndef AI4E_CHAIN_PD
 #define AI4E_CHAIN_PD 4
+#endif
+#ifndef AI4E_CHAIN_PD64
+#define AI4E_CHAIN_PD64 4
 #endif
 __device__ __forceinline__ int swt(int r) {
   const int x = (r >> 1) & 3;
@@ -368,7 +373,7 @@ void conv_chain_kernel(const ChainParams p) {
     }
     constexpr int SPT = MID / 32;   // K steps per tap
     constexpr int NKA = 9 * SPT;
-    constexpr int PD = AI4E_CHAIN_PD;  // weight K steps prefetched into registers
+    constexpr int PD = MID == 64 ? AI4E_CHAIN_PD64 : AI4E_CHAIN_PD;  // weight K steps prefetched into registers
     const uint16_t* const wp = p.w2 + static_cast<long>(pwn * (MID / PWN) + (lane & 15)) * p.kpad2 + 8 * lg;
     bf16x8_t wr[PD][CF];
 #pragma unroll
