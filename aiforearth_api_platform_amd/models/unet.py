@@ -99,8 +99,8 @@ class _FusedDouble:
         self.g2 = (dc.n2.weight.data.float().to(device), dc.n2.bias.data.float().to(device), dc.n2.num_groups)
 
     @staticmethod
-    def _k1t_groups(g: int) -> bool:  # K1t's epilogue sums whole groups within a lane's 4 channels
-        return 64 % g == 0 and 64 // g <= 4
+    def _k1t_groups(g: int, cout: int = 64) -> bool:  # K1t's epilogue sums whole groups within a lane's 4 channels
+        return cout % g == 0 and cout // g <= 4 and g <= 64
 
     def __call__(self, x: torch.Tensor, out: Optional[torch.Tensor] = None,
                  pool_out: Optional[torch.Tensor] = None, head=None):
@@ -108,11 +108,11 @@ class _FusedDouble:
         ``headed`` says whether ``y`` is already the head's output (fused: csrc/kernels/norm_resample.hip
         gn_relu_head8_kernel) or still the block output."""
         # GroupNorm statistics come out of the conv epilogues (conv2d_gn_nhwc, K1t) where the tile allows
-        if tile64_supported(x, self.c1) and self._k1t_groups(self.g1[2]):
+        if tile64_supported(x, self.c1) and self._k1t_groups(self.g1[2], self.c1.cout):
             y, st = conv3x3_tile64(x, self.c1, gn_groups=self.g1[2])  # e.g. the last decoder's 128 -> 64 c1
         else:
             y, st = conv2d_gn_nhwc(x, self.c1, self.g1[2])
-        if st is not None and tile64_supported(y, self.c2) and self._k1t_groups(self.g2[2]):
+        if st is not None and tile64_supported(y, self.c2) and self._k1t_groups(self.g2[2], self.c2.cout):
             # 64 -> 64 at full resolution (K1t): c1's GroupNorm + ReLU is applied while c2 loads its input patch, so
             # the normalized c1 output is never written (csrc/kernels/conv_tile3x3.hip)
             n, h, w, c = y.shape

@@ -233,48 +233,53 @@ def conv2d_gn_nhwc(x: torch.Tensor, pc: PackedConv, groups: int, out: Optional[t
     return out, (partials, nchunks)
 
 
-def _tile_rows(cin: int) -> int:
-    return 8  # both instances: 8 x 32 tiles (128 input channels as two 64-channel k-slices)
+def _tile_rows(cout: int) -> int:
+    return 8 if cout == 64 else 4  # output tile rows (x 32 columns); the input channels run as 64-channel k-slices
 
 
 def tile64_supported(x: torch.Tensor, pc: PackedConv) -> bool:
-    """Shapes K1t (``conv3x3_tile64``, csrc/kernels/conv_tile3x3.hip) takes: 3x3 / stride 1 / pad 1, 64 or 128 -> 64
-    channels, bf16, W % 32 == 0 and H % 8 == 0: 8 x 32 output tiles
-    (AI4E_CONV_TILE64: "1" default, both instances; "64" the 64 -> 64 instance only; "0" off)."""
+    """Shapes K1t (``conv3x3_tile64``, csrc/kernels/conv_tile3x3.hip) takes: 3x3 / stride 1 / pad 1, bf16, 64 or 128
+    -> 64 channels (8 x 32 output tiles, H % 8 == 0) or 64 / 128 / 256 -> 128 channels (4 x 32 tiles, H % 4 == 0),
+    W % 32 == 0. AI4E_CONV_TILE64: "1" default, every instance; "64" the 64 -> 64 instance only; "0" off.
+    AI4E_K1T_COUT128=0 turns off the 128-output-channel instances alone."""
     n, h, w, c = x.shape
-    # both instances beat K1 (profiles/r4_k1t/: 600 vs 665 us and 871 vs 1000 us per conv over 16 tiles of 512^2;
-    # U-Net 24.0 vs 22.5 mosaics/s with K1)
+    # the 64-channel instances beat K1 (profiles/r4_k1t/: 558 vs 670 us and 829 vs 1022 us per conv over 16 tiles of
+    # 512^2; U-Net 24.4 vs 22.5 mosaics/s with K1)
     mode = os.environ.get("AI4E_CONV_TILE64", "1")
-    return (mode != "0" and (mode != "64" or c == 64) and _ext.backend_for(x) == "hip"
+    if pc.cout == 128 and os.environ.get("AI4E_K1T_COUT128", "1") == "0":
+        return False
+    ok_c = (pc.cout == 64 and pc.cin_pad in (64, 128)) or (pc.cout == 128 and pc.cin_pad in (64, 128, 256))
+    return (mode != "0" and (mode != "64" or (c == 64 and pc.cout == 64)) and _ext.backend_for(x) == "hip"
             and x.dtype == torch.bfloat16 and pc.w_packed.dtype == torch.bfloat16 and (pc.kh, pc.kw) == (3, 3)
             and pc.stride == 1 and pc.pad == 1 and (pc.pad if pc.pad_hi is None else pc.pad_hi) == 1
-            and pc.cin_pad in (64, 128) and c == pc.cin_pad and pc.cout == 64
-            and h % _tile_rows(c) == 0 and w % 32 == 0 and x.stride(3) == 1 and x.stride(2) % 8 == 0
+            and ok_c and c == pc.cin_pad and pc.w_packed.shape[0] >= pc.cout
+            and h % _tile_rows(pc.cout) == 0 and w % 32 == 0 and x.stride(3) == 1 and x.stride(2) % 8 == 0
             and x.stride(2) * w == x.stride(1) and x.stride(1) * h == x.stride(0))
 
 
 def conv3x3_tile64(x: torch.Tensor, pc: PackedConv, pro: Optional[torch.Tensor] = None, pro_relu: bool = True,
                    gn_groups: int = 0) -> Tuple[torch.Tensor, Optional[tuple]]:
-    """K1t: ``conv3x3(pro(x)) + bias`` for 64 or 128 -> 64 channels (see ``tile64_supported``), one 8 x 32 (4 x 32)
-    output tile at a time per persistent workgroup from an LDS input patch. ``pro``: float32 [N, C, 2] per-(image, channel) affine applied
-    to the input as it is loaded (``x * a + b``, then ReLU with ``pro_relu``): the previous GroupNorm, which then
-    needs no apply pass (``norm.group_norm_affine``). Returns ``(y, stats)`` with ``stats`` = ``(partials,
-    nchunks)`` GroupNorm statistics of y (as ``conv2d_gn_nhwc``) when ``gn_groups``, else None."""
+    """K1t: ``conv3x3(pro(x)) + bias`` (see ``tile64_supported``), one 8 x 32 (cout 64) or 4 x 32 (cout 128) output
+    tile at a time per persistent workgroup from an LDS input patch. ``pro``: float32 [N, C, 2] per-(image, channel)
+    affine applied to the input as it is loaded (``x * a + b``, then ReLU with ``pro_relu``): the previous GroupNorm,
+    which then needs no apply pass (``norm.group_norm_affine``). Returns ``(y, stats)`` with ``stats`` =
+    ``(partials, nchunks)`` GroupNorm statistics of y (as ``conv2d_gn_nhwc``) when ``gn_groups``, else None."""
     n, h, w, c = x.shape
     if not tile64_supported(x, pc):
         raise ValueError("conv3x3_tile64: unsupported shape / dtype / layout")
     if pro is not None and (pro.dtype != torch.float32 or not pro.is_contiguous() or tuple(pro.shape) != (n, c, 2)):
         raise ValueError(f"conv3x3_tile64: pro must be contiguous float32 [N, {c}, 2]")
+    cout = pc.cout
     ldx = x.stride(2)
     xoff = x.storage_offset()
     base = x.untyped_storage().data_ptr() + 2 * (xoff - xoff % ldx)
-    out = torch.empty(n, h, w, 64, device=x.device, dtype=x.dtype)
-    nchunks = (h // _tile_rows(c)) * (w // 32)
+    out = torch.empty(n, h, w, cout, device=x.device, dtype=x.dtype)
+    nchunks = (h // _tile_rows(cout)) * (w // 32)
     partials = None
     if gn_groups:
-        partials = torch.empty(n * nchunks * gn_groups * 4 + n * 64 * 2, device=x.device, dtype=torch.float32)
-    _ext.call("ai4e_conv3x3_tile64_fwd", base, pc.w_packed.data_ptr(), pc.bias.data_ptr(), _ext.ptr(pro),
-              int(pro_relu), out.data_ptr(), n, h, w, c, ldx, xoff % ldx, pc.kpad, 64, 0, _ext.ptr(partials),
+        partials = torch.empty(n * nchunks * gn_groups * 4 + n * cout * 2, device=x.device, dtype=torch.float32)
+    _ext.call("ai4e_conv3x3_tile_fwd", base, pc.w_packed.data_ptr(), pc.bias.data_ptr(), _ext.ptr(pro),
+              int(pro_relu), out.data_ptr(), n, h, w, c, cout, ldx, xoff % ldx, pc.kpad, cout, 0, _ext.ptr(partials),
               gn_groups, _ext.stream_ptr(x.device))
     return out, ((partials, nchunks) if gn_groups else None)
 

@@ -26,41 +26,46 @@
 namespace {
 
 constexpr int T_W = 32, P_W = T_W + 2;           // output tile width; patch width with halo
-constexpr int CH = 64;                           // output channels (and the channels of one weight stage)
-constexpr int L_W = CH * CH * 2;                 // one weight stage: 64 output x 64 input channels of one tap, 8 KB
 
-// 8 x 32 output tiles from a 10 x 34 x 64-channel input patch (43.5 KB). CIN = 128 (the U-Net's last decoder c1,
-// reading the [skip | upsampled] concat) runs each tile as two 64-channel k-slices through the same patch buffer:
-// the accumulators carry over, the epilogue runs once, and the second slice's patch is prefetched under the first
-// slice's taps like the next tile's. LDS: patch + CIN x 8 B affine + two 8 KB weight stages; two workgroups per CU.
-template <int CIN>
+// COUT = 64: 8 x 32 output tiles from a 10 x 34 x 64-channel input patch (43.5 KB); COUT = 128 (the U-Net's level-1
+// convs): 4 x 32 tiles (a 6 x 34 patch, 26 KB), each wave 32 pixels x 128 channels, so a wave issues the same 32
+// MFMAs per stage from the same 64 accumulators. CIN = 128 / 256 (decoder c1s reading a [skip | upsampled] concat)
+// runs each tile as CIN / 64 k-slices through the same patch buffer: the accumulators carry over, the epilogue runs
+// once, and the next slice's patch is prefetched under the current slice's taps like the next tile's.
+// LDS: patch + CIN x 8 B affine + two COUT x 128 B weight stages + the bias; two workgroups per CU.
+template <int CIN, int COUT>
 struct TileCfg {
-  static constexpr int TH = 8;                          // output tile rows
+  static constexpr int TH = COUT == 64 ? 8 : 4;         // output tile rows
   static constexpr int P_SLOTS = (TH + 2) * P_W;
   static constexpr int NCH = 8;                         // 16-B chunks per 64-channel pixel slot
   static constexpr int SLOT_B = 128;
   static constexpr int L_PATCH = P_SLOTS * SLOT_B;
   static constexpr int L_AFF = CIN * 8;                 // prologue affine of this image: CIN x (a, b)
-  static constexpr int L_TOTAL = L_PATCH + L_AFF + 2 * L_W + CH * 4;  // + the bias (64 floats)
+  static constexpr int L_W = COUT * 128;                // one weight stage: COUT rows x 64 input channels of one tap
+  static constexpr int L_TOTAL = L_PATCH + L_AFF + 2 * L_W + COUT * 4;  // + the bias
   static constexpr int P_CHUNKS = P_SLOTS * NCH;
   static constexpr int P_ITERS = (P_CHUNKS + 255) / 256;
   static constexpr int KS = CIN / 64;                   // 64-channel k-slices per tile
   static constexpr int NST = 9;                         // weight stages (taps) per k-slice
   static constexpr int FPW = TH / 2;                    // pixel fragments per wave (TH / 4 rows x 2 half-rows)
-  static_assert(CIN == 64 || CIN == 128, "K1t: 64 or 128 input channels");
+  static constexpr int NJ = COUT / 16;                  // 16-channel output blocks per wave
+  static constexpr int NWV = COUT / 32;                 // 16-B weight chunks per thread per stage
+  static_assert(CIN == 64 || CIN == 128 || CIN == 256, "K1t: 64, 128 or 256 input channels");
+  static_assert(COUT == 64 || COUT == 128, "K1t: 64 or 128 output channels");
   static_assert(L_TOTAL <= 80 * 1024, "two workgroups per CU");
+  static_assert((COUT + 4 * COUT * 2) * 4 <= L_W, "GroupNorm scratch (shift + 4-wave sums) fits a weight stage");
 };
 
 struct TileParams {
   const uint16_t* x;
   int ldx, xcoff;          // input [N, H, W, ldx], channels [xcoff, xcoff + CIN)
   const uint16_t* w;
-  int kpad;                // packed weights [64 rows, kpad >= 9 CIN], K = (kh, kw, c)
-  const float* bias;       // [64]
+  int kpad;                // packed weights [COUT rows, kpad >= 9 CIN], K = (kh, kw, c)
+  const float* bias;       // [COUT]
   const float2* pro;       // prologue (a, b) per (image, channel) [N, CIN]; null = none
   int pro_relu;
   uint16_t* y;
-  int ldy, ycoff;          // output [N, H, W, ldy], channels [ycoff, ycoff + 64)
+  int ldy, ycoff;          // output [N, H, W, ldy], channels [ycoff, ycoff + COUT)
   float* gnp;              // GroupNorm partials [N, tiles per image, G, 4]; null = off
   int gn_groups;
   int H, W, tiles_w, tiles_per_img;
@@ -85,10 +90,11 @@ __device__ __forceinline__ uint32_t swz(int row, int c) {
   return static_cast<uint32_t>((c ^ (row & 6)) << 4);
 }
 
-template <int CIN>
+template <int CIN, int COUT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv3x3_tile_kernel(
     const TileParams p, int ntiles) {
-  using Cfg = TileCfg<CIN>;
+  using Cfg = TileCfg<CIN, COUT>;
+  constexpr int NJ = Cfg::NJ, L_W = Cfg::L_W;
   constexpr int TH = Cfg::TH, P_CHUNKS = Cfg::P_CHUNKS, P_ITERS = Cfg::P_ITERS, NCH = Cfg::NCH, SLOT_B = Cfg::SLOT_B;
   constexpr int KS = Cfg::KS, NST = Cfg::NST, FPW = Cfg::FPW;
   static_assert(P_ITERS <= 32, "in-image mask bits");
@@ -97,21 +103,35 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   uint8_t* const patch = sm;
   float2* const aff = reinterpret_cast<float2*>(sm + Cfg::L_PATCH);
   uint8_t* const wbuf = sm + Cfg::L_PATCH + Cfg::L_AFF;
-  float* const sbias = reinterpret_cast<float*>(wbuf + 2 * L_W);  // [64]: epilogue reads stay off the vmcnt queue
+  float* const sbias = reinterpret_cast<float*>(wbuf + 2 * L_W);  // [COUT]: epilogue reads stay off the vmcnt queue
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g4 = lane >> 4;
 
-  uint4 wv0, wv1;  // one weight stage in flight: rows n = tid / 8 and 32 + tid / 8, 16-B chunk tid % 8
+  // one weight stage in flight: rows n = tid / 8 + 32 e (e < NWV), 16-B chunk tid % 8 (named registers: an array
+  // indexed inside these lambdas was kept in scratch)
+  uint4 wv0, wv1, wv2, wv3;
   auto load_w = [&](int tap, int ks) __attribute__((always_inline)) {  // stage = (tap, 64-channel k-slice)
-    const uint16_t* const src = p.w + static_cast<long>(tid >> 3) * p.kpad + tap * CIN + ks * 64 + 8 * (tid & 7);
+    int tq = tid;
+    asm volatile("" : "+v"(tq));  // per-call address math: with one k-slice every stage's address is loop-invariant,
+                                  // and hoisting all 9 out of the tile loop spills (64 -> 128 instance)
+    const uint16_t* const src = p.w + static_cast<long>(tq >> 3) * p.kpad + tap * CIN + ks * 64 + 8 * (tq & 7);
     wv0 = *reinterpret_cast<const uint4*>(src);
     wv1 = *reinterpret_cast<const uint4*>(src + 32L * p.kpad);
+    if constexpr (Cfg::NWV == 4) {
+      wv2 = *reinterpret_cast<const uint4*>(src + 64L * p.kpad);
+      wv3 = *reinterpret_cast<const uint4*>(src + 96L * p.kpad);
+    }
   };
   auto store_w = [&](int buf) __attribute__((always_inline)) {
     const int n = tid >> 3, c = tid & 7;
-    *reinterpret_cast<uint4*>(wbuf + buf * L_W + n * 128 + swz<8>(n, c)) = wv0;
-    *reinterpret_cast<uint4*>(wbuf + buf * L_W + (n + 32) * 128 + swz<8>(n + 32, c)) = wv1;
+    uint8_t* const b = wbuf + buf * L_W;
+    *reinterpret_cast<uint4*>(b + n * 128 + swz<8>(n, c)) = wv0;
+    *reinterpret_cast<uint4*>(b + (n + 32) * 128 + swz<8>(n + 32, c)) = wv1;
+    if constexpr (Cfg::NWV == 4) {
+      *reinterpret_cast<uint4*>(b + (n + 64) * 128 + swz<8>(n + 64, c)) = wv2;
+      *reinterpret_cast<uint4*>(b + (n + 96) * 128 + swz<8>(n + 96, c)) = wv3;
+    }
   };
   // the patch of one tile: global -> registers (pv, in-image chunks in pmask), later registers -> LDS
   uint4 pv[P_ITERS];
@@ -180,7 +200,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   coords(t, img, tin, h0, w0);
   load_w(0, 0);
   if (p.pro != nullptr && tid < CIN) aff[tid] = p.pro[img * CIN + tid];
-  if (tid < CH) sbias[tid] = p.bias[tid];
+  if (tid < COUT) sbias[tid] = p.bias[tid];
   pmask = 0;
   load_patch(img, h0, w0, 0, 0, P_ITERS);
   store_w(0);
@@ -188,15 +208,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   store_patch(0);
   tile_barrier();
 
-  float* const kshift = reinterpret_cast<float*>(wbuf);        // [64] the tile's first pixel, as stored
-  float* const red = reinterpret_cast<float*>(wbuf) + CH;      // [4 waves][64 channels][2]
+  float* const kshift = reinterpret_cast<float*>(wbuf);        // [COUT] the tile's first pixel, as stored
+  float* const red = reinterpret_cast<float*>(wbuf) + COUT;    // [4 waves][COUT channels][2]
 
-  f32x4_t acc[FPW][4];  // carried over the k-slices of a tile; zeroed here and after each tile's epilogue
+  f32x4_t acc[FPW][NJ];  // carried over the k-slices of a tile; zeroed here and after each tile's epilogue
   auto zero_acc = [&]() __attribute__((always_inline)) {
 #pragma unroll
     for (int f = 0; f < FPW; ++f)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[f][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < NJ; ++j) acc[f][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   };
   zero_acc();
   for (;;) {
@@ -231,21 +251,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         const int wc = 4 * s + g4;  // chunk within the stage's 64 channels
-        bf16x8_t fx[FPW], fw[4];
+        bf16x8_t fx[FPW], fw[NJ];
 #pragma unroll
         for (int f = 0; f < FPW; ++f) {
           const int slot = sbase[f] + kh * P_W + kw;
           fx[f] = *reinterpret_cast<const bf16x8_t*>(patch + slot * SLOT_B + swz<NCH>(slot, wc));
         }
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < NJ; ++j) {
           const int n = 16 * j + l16;
           fw[j] = *reinterpret_cast<const bf16x8_t*>(wb + n * 128 + swz<8>(n, wc));
         }
 #pragma unroll
         for (int f = 0; f < FPW; ++f)
 #pragma unroll
-          for (int j = 0; j < 4; ++j) acc[f][j] = mfma_16x16x32<false>(fw[j], fx[f], acc[f][j]);
+          for (int j = 0; j < NJ; ++j) acc[f][j] = mfma_16x16x32<false>(fw[j], fx[f], acc[f][j]);
       }
       if (st + 1 < NST) store_w((st + 1) & 1);  // that buffer was last read at stage st - 1 (before the previous barrier)
       tile_barrier();
@@ -255,13 +275,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     // ---- epilogue (after the tile's last slice): lane holds channels 16 j + 4 g4 + v of pixel (lane % 16) of
     // each fragment
     if (last_slice) {
-      uint2 ov[FPW][4];
+      uint2 ov[FPW][NJ];
   #pragma unroll
       for (int f = 0; f < FPW; ++f) {
         const int oh = h0 + (TH / 4) * wave + (f >> 1), ow = w0 + 16 * (f & 1) + (lane & 15);
         uint16_t* const dst = p.y + ((static_cast<long>(img) * p.H + oh) * p.W + ow) * p.ldy + p.ycoff;
   #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < NJ; ++j) {
           const float4 bv = *reinterpret_cast<const float4*>(sbias + 16 * j + 4 * g4);  // LDS: frees 16 VGPRs
           ov[f][j] = make_uint2(pack_bf16x2(acc[f][j][0] + bv.x, acc[f][j][1] + bv.y),
                                 pack_bf16x2(acc[f][j][2] + bv.z, acc[f][j][3] + bv.w));
@@ -269,11 +289,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         }
       }
       if (p.gnp != nullptr) {
-        // GroupNorm statistics of the stored values (cg = 64 / G channels per group, cg in {1, 2, 4}: a lane's 4
+        // GroupNorm statistics of the stored values (cg = COUT / G channels per group, cg in {1, 2, 4}: a lane's 4
         // channels of one j hold whole groups), shifted by the tile's first pixel at each group's first channel
         if (wave == 0 && (lane & 15) == 0) {
   #pragma unroll
-          for (int j = 0; j < 4; ++j) {
+          for (int j = 0; j < NJ; ++j) {
             float a, b, c, d;
             unpack_bf16x2(ov[0][j].x, a, b);
             unpack_bf16x2(ov[0][j].y, c, d);
@@ -284,9 +304,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
           }
         }
         tile_barrier();
-        const int cg = CH / p.gn_groups;
+        const int cg = COUT / p.gn_groups;
   #pragma unroll
-        for (int j = 0; j < 4; ++j) {  // one 16-channel block at a time (register pressure)
+        for (int j = 0; j < NJ; ++j) {  // one 16-channel block at a time (register pressure)
           float gs[4], gq[4];
   #pragma unroll
           for (int v = 0; v < 4; ++v) {
@@ -315,8 +335,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   #pragma unroll
             for (int v = 0; v < 4; ++v) {
               const int ch = 16 * j + 4 * g4 + v;
-              red[(wave * CH + ch) * 2] = gs[v];
-              red[(wave * CH + ch) * 2 + 1] = gq[v];
+              red[(wave * COUT + ch) * 2] = gs[v];
+              red[(wave * COUT + ch) * 2 + 1] = gq[v];
             }
           }
         }
@@ -325,8 +345,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
           float S = 0.f, Q = 0.f;
           for (int w = 0; w < 4; ++w)
             for (int c = 0; c < cg; ++c) {
-              S += red[(w * CH + tid * cg + c) * 2];
-              Q += red[(w * CH + tid * cg + c) * 2 + 1];
+              S += red[(w * COUT + tid * cg + c) * 2];
+              Q += red[(w * COUT + tid * cg + c) * 2 + 1];
             }
           float* const o = p.gnp + ((static_cast<long>(img) * p.tiles_per_img + tin) * p.gn_groups + tid) * 4;
           *reinterpret_cast<float4*>(o) = make_float4(S, Q, kshift[tid * cg], 0.f);
@@ -354,11 +374,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 
 namespace {
 
-template <int CIN>
+template <int CIN, int COUT>
 int launch_tile(const TileParams& p, int N, hipStream_t stream) {
-  constexpr int L = TileCfg<CIN>::L_TOTAL;
+  constexpr int L = TileCfg<CIN, COUT>::L_TOTAL;
   static bool attr = [] {
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(conv3x3_tile_kernel<CIN>),
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(conv3x3_tile_kernel<CIN, COUT>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, L) == hipSuccess;
   }();
   if (!attr) return AI4E_ELAUNCH;
@@ -374,25 +394,26 @@ int launch_tile(const TileParams& p, int N, hipStream_t stream) {
     return AI4E_ELAUNCH;
   const int ntiles = N * p.tiles_per_img;
   const int grid = persist && ntiles > 2 * cus ? 2 * cus : ntiles;
-  hipLaunchKernelGGL(conv3x3_tile_kernel<CIN>, dim3(static_cast<unsigned>(grid)), dim3(256), L, stream, p, ntiles);
+  hipLaunchKernelGGL((conv3x3_tile_kernel<CIN, COUT>), dim3(static_cast<unsigned>(grid)), dim3(256), L, stream, p, ntiles);
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
 }
 
 }  // namespace
 
-// y = conv3x3(pro(x)) + bias (cin = 64 or 128 -> 64 channels, stride 1, pad 1) with GroupNorm partials of y
-// (gn_groups > 0): [N, (H / 8) * (W / 32), G, 4]. pro: null or float2 [N, cin]
-// (x * a + b, then ReLU if pro_relu).
-AI4E_API int ai4e_conv3x3_tile64_fwd(const void* x, const void* w, const void* bias, const void* pro, int pro_relu,
-                                      void* y, int N, int H, int W, int cin, int ldx, int xcoff, int kpad, int ldy,
-                                      int ycoff, void* gn_partials, int gn_groups, hipStream_t stream) {
-  const int th = TileCfg<64>::TH;
-  static_assert(TileCfg<64>::TH == TileCfg<128>::TH, "one tile geometry");
-  if (!x || !w || !bias || !y || N <= 0 || (cin != 64 && cin != 128) || H % th || W % T_W || kpad < 9 * cin ||
-      ldx % 8 || xcoff % 8 || xcoff + cin > ldx || ldy % 8 || ycoff % 8 || ycoff + CH > ldy)
+// y = conv3x3(pro(x)) + bias (cin 64 / 128 -> 64 channels, or cin 64 / 128 / 256 -> 128 channels; stride 1, pad 1)
+// with GroupNorm partials of y (gn_groups > 0): [N, (H / TH) * (W / 32), G, 4], TH = 8 (cout 64) or 4 (cout 128).
+// pro: null or float2 [N, cin] (x * a + b, then ReLU if pro_relu).
+AI4E_API int ai4e_conv3x3_tile_fwd(const void* x, const void* w, const void* bias, const void* pro, int pro_relu,
+                                   void* y, int N, int H, int W, int cin, int cout, int ldx, int xcoff, int kpad,
+                                   int ldy, int ycoff, void* gn_partials, int gn_groups, hipStream_t stream) {
+  const bool ok_c = (cout == 64 && (cin == 64 || cin == 128)) || (cout == 128 && (cin == 64 || cin == 128 || cin == 256));
+  const int th = cout == 64 ? TileCfg<64, 64>::TH : TileCfg<64, 128>::TH;
+  if (!x || !w || !bias || !y || N <= 0 || !ok_c || H % th || W % T_W || kpad < 9 * cin || ldx % 8 || xcoff % 8 ||
+      xcoff + cin > ldx || ldy % 8 || ycoff % 8 || ycoff + cout > ldy)
     return AI4E_EINVAL;
   if (reinterpret_cast<uintptr_t>(bias) % 16) return AI4E_EINVAL;  // float4 reads in the epilogue
-  if (gn_partials && (gn_groups <= 0 || CH % gn_groups || CH / gn_groups > 4)) return AI4E_EINVAL;
+  if (gn_partials && (gn_groups <= 0 || gn_groups > 64 || cout % gn_groups || cout / gn_groups > 4))
+    return AI4E_EINVAL;
   if (static_cast<long>(N) * H * W * (ldx > ldy ? ldx : ldy) >= (1L << 40)) return AI4E_EINVAL;
   TileParams p;
   p.x = static_cast<const uint16_t*>(x);
@@ -412,5 +433,7 @@ AI4E_API int ai4e_conv3x3_tile64_fwd(const void* x, const void* w, const void* b
   p.W = W;
   p.tiles_w = W / T_W;
   p.tiles_per_img = (H / th) * p.tiles_w;
-  return cin == 64 ? launch_tile<64>(p, N, stream) : launch_tile<128>(p, N, stream);
+  if (cout == 64) return cin == 64 ? launch_tile<64, 64>(p, N, stream) : launch_tile<128, 64>(p, N, stream);
+  if (cin == 64) return launch_tile<64, 128>(p, N, stream);
+  return cin == 128 ? launch_tile<128, 128>(p, N, stream) : launch_tile<256, 128>(p, N, stream);
 }

@@ -22,21 +22,24 @@ def _conv_ref(xin: torch.Tensor, w: torch.Tensor, b: torch.Tensor) -> torch.Tens
     return y.permute(0, 2, 3, 1)
 
 
-def _case(n, h, w, seed, cin=64):
+def _case(n, h, w, seed, cin=64, cout=64):
     from aiforearth_api_platform_amd.ops.conv import pack_conv
     g = torch.Generator().manual_seed(seed)
     x = torch.randn(n, h, w, cin, generator=g).to(torch.bfloat16)
-    wt = (torch.randn(64, cin, 3, 3, generator=g) * 0.05).to(torch.bfloat16).float()
-    b = torch.randn(64, generator=g) * 0.1
+    wt = (torch.randn(cout, cin, 3, 3, generator=g) * 0.05).to(torch.bfloat16).float()
+    b = torch.randn(cout, generator=g) * 0.1
     return x, wt, b, pack_conv(wt, b, pad=1).to(DEV)
 
 
 # the last two: 768 tiles > the persistent grid (2 x 256 CUs), so workgroups walk several tiles (next-tile prefetch)
-@pytest.mark.parametrize("n,h,w,cin", [(2, 16, 64, 64), (1, 64, 32, 64), (3, 8, 96, 64), (2, 16, 64, 128),
-                                       (1, 8, 32, 128), (3, 128, 512, 64), (3, 128, 512, 128)])
-def test_conv3x3_tile64_matches_fp32(n, h, w, cin):
+@pytest.mark.parametrize("n,h,w,cin,cout", [(2, 16, 64, 64, 64), (1, 64, 32, 64, 64), (3, 8, 96, 64, 64),
+                                            (2, 16, 64, 128, 64), (1, 8, 32, 128, 64), (3, 128, 512, 64, 64),
+                                            (3, 128, 512, 128, 64),
+                                            (2, 8, 64, 64, 128), (1, 4, 32, 128, 128), (2, 12, 96, 256, 128),
+                                            (3, 64, 512, 64, 128), (3, 64, 512, 256, 128)])
+def test_conv3x3_tile64_matches_fp32(n, h, w, cin, cout):
     from aiforearth_api_platform_amd.ops.conv import conv3x3_tile64
-    x, wt, b, pc = _case(n, h, w, n * 100 + h, cin)
+    x, wt, b, pc = _case(n, h, w, n * 100 + h, cin, cout)
     y, st = conv3x3_tile64(x.to(DEV), pc)
     assert st is None
     ref = _conv_ref(x, wt, b)
@@ -44,13 +47,13 @@ def test_conv3x3_tile64_matches_fp32(n, h, w, cin):
     assert rel < 6e-3, rel
 
 
-@pytest.mark.parametrize("cin", [64, 128])
-def test_conv3x3_tile64_prologue_and_sliced_input(cin):
-    """The prologue affine is per image (and per k-slice for 128 channels): 3 images of 256 tiles, so persistent
-    workgroups cross images."""
+@pytest.mark.parametrize("cin,cout", [(64, 64), (128, 64), (128, 128), (256, 128)])
+def test_conv3x3_tile64_prologue_and_sliced_input(cin, cout):
+    """The prologue affine is per image (and per k-slice for 128 / 256 channels): 3 images of 256 / 512 tiles, so
+    persistent workgroups cross images."""
     from aiforearth_api_platform_amd.ops.conv import conv3x3_tile64
     n, h, w = 3, 128, 512
-    x, wt, b, pc = _case(n, h, w, 7, cin)
+    x, wt, b, pc = _case(n, h, w, 7, cin, cout)
     g = torch.Generator().manual_seed(8)
     aff = torch.stack([0.5 + torch.rand(n, cin, generator=g), torch.randn(n, cin, generator=g) * 0.5], -1)
     wide = torch.zeros(n, h, w, cin + 64, dtype=torch.bfloat16)
@@ -62,24 +65,26 @@ def test_conv3x3_tile64_prologue_and_sliced_input(cin):
     assert rel < 6e-3, rel
 
 
-@pytest.mark.parametrize("groups,cin,n,h,w", [(32, 64, 2, 32, 64), (16, 64, 2, 32, 64), (32, 128, 2, 32, 64),
-                                              (32, 64, 3, 128, 512), (32, 128, 3, 128, 512)])
-def test_conv3x3_tile64_groupnorm_statistics(groups, cin, n, h, w):
+@pytest.mark.parametrize("groups,cin,n,h,w,cout", [(32, 64, 2, 32, 64, 64), (16, 64, 2, 32, 64, 64),
+                                                   (32, 128, 2, 32, 64, 64), (32, 64, 3, 128, 512, 64),
+                                                   (32, 128, 3, 128, 512, 64), (32, 128, 2, 32, 64, 128),
+                                                   (32, 256, 3, 64, 512, 128), (64, 64, 2, 16, 64, 128)])
+def test_conv3x3_tile64_groupnorm_statistics(groups, cin, n, h, w, cout):
     """The epilogue's shifted per-tile sums, finalized (ops.norm.group_norm_affine), equal the GroupNorm affine of
     the stored output computed directly in fp64 (the last case: several tiles per persistent workgroup)."""
     from aiforearth_api_platform_amd.ops.conv import conv3x3_tile64
     from aiforearth_api_platform_amd.ops.norm import group_norm_affine
-    x, wt, b, pc = _case(n, h, w, 21, cin)
+    x, wt, b, pc = _case(n, h, w, 21, cin, cout)
     y, st = conv3x3_tile64(x.to(DEV), pc, gn_groups=groups)
-    gamma = torch.linspace(0.5, 1.5, 64)
-    beta = torch.linspace(-0.2, 0.2, 64)
-    ss = group_norm_affine(st, gamma, beta, n=n, hw=h * w, c=64, groups=groups).cpu()
-    yd = y.double().cpu().reshape(n, h * w, groups, 64 // groups)
+    gamma = torch.linspace(0.5, 1.5, cout)
+    beta = torch.linspace(-0.2, 0.2, cout)
+    ss = group_norm_affine(st, gamma, beta, n=n, hw=h * w, c=cout, groups=groups).cpu()
+    yd = y.double().cpu().reshape(n, h * w, groups, cout // groups)
     mean = yd.mean(dim=(1, 3))
     var = yd.var(dim=(1, 3), unbiased=False)
     rstd = (var + 1e-5).rsqrt()
-    a = (gamma.double().reshape(groups, -1)[None] * rstd[..., None]).reshape(n, 64)
-    bb = beta.double()[None] - (mean[..., None] * a.reshape(n, groups, -1)).reshape(n, 64)
+    a = (gamma.double().reshape(groups, -1)[None] * rstd[..., None]).reshape(n, cout)
+    bb = beta.double()[None] - (mean[..., None] * a.reshape(n, groups, -1)).reshape(n, cout)
     assert torch.allclose(ss[..., 0].double(), a, rtol=1e-4, atol=1e-5)
     assert torch.allclose(ss[..., 1].double(), bb, rtol=1e-4, atol=1e-4)
 

@@ -7,7 +7,8 @@ import numpy as np
 import pytest
 
 P_W = 34
-TH, NCH, SLOT_B = 8, 8, 128        # TileCfg: 8 x 32 tiles, 64-channel pixel slots
+NCH, SLOT_B = 8, 128               # 64-channel pixel slots (16-B chunks)
+TH = 8                             # TileCfg<*, 64>: 8 x 32 tiles; TileCfg<*, 128>: 4 x 32 (tests below take th)
 P_SLOTS = (TH + 2) * P_W
 
 
@@ -20,8 +21,10 @@ B128_GROUPS = [[*range(0, 4), *range(12, 16), *range(20, 28)], [*range(4, 12), *
 B128_GROUPS += [[lane + 32 for lane in g] for g in B128_GROUPS]
 
 
-@pytest.mark.parametrize("cin", [64, 128])
-def test_patch_writes_and_fragment_reads_agree(cin):
+@pytest.mark.parametrize("cin,cout", [(64, 64), (128, 64), (64, 128), (128, 128), (256, 128)])
+def test_patch_writes_and_fragment_reads_agree(cin, cout):
+    TH = 8 if cout == 64 else 4
+    P_SLOTS = (TH + 2) * P_W
     fpw, ks_n = TH // 2, cin // 64
     for ks in range(ks_n):  # each k-slice refills the same patch buffer from input channels 64 ks .. 64 ks + 63
         lds = np.full(P_SLOTS * SLOT_B // 16, -1, dtype=np.int64)  # per 16-B chunk: the (slot, c) it holds
@@ -52,23 +55,23 @@ def test_patch_writes_and_fragment_reads_agree(cin):
                             assert 64 * ks + 8 * got_c == 64 * ks + 32 * s + 8 * g4
 
 
-@pytest.mark.parametrize("cin", [64, 128])
-def test_weight_stage_writes_and_reads_agree(cin):
+@pytest.mark.parametrize("cin,cout", [(64, 64), (128, 64), (64, 128), (128, 128), (256, 128)])
+def test_weight_stage_writes_and_reads_agree(cin, cout):
     kpad = 9 * cin
     for tap in range(9):
         for ks in range(cin // 64):
-            lds = np.full(64 * 128 // 16, -1, dtype=np.int64)  # per 16-B chunk: the packed-weight element it holds
-            for tid in range(256):  # load_w(tap, ks) + store_w: rows tid / 8 and 32 + tid / 8, chunk tid % 8
+            lds = np.full(cout * 128 // 16, -1, dtype=np.int64)  # per 16-B chunk: the packed-weight element it holds
+            for tid in range(256):  # load_w(tap, ks) + store_w: rows tid / 8 + 32 e (e < cout / 32), chunk tid % 8
                 n, c = tid >> 3, tid & 7
                 col = tap * cin + ks * 64 + 8 * c
                 assert col + 8 <= kpad
-                for row in (n, n + 32):
+                for row in range(n, cout, 32):
                     off = row * 128 + swz(row, c)
                     assert lds[off // 16] == -1
                     lds[off // 16] = row * kpad + col
             assert (lds >= 0).all()
             for lane in range(64):
-                for j in range(4):
+                for j in range(cout // 16):
                     for s in range(2):
                         n = 16 * j + (lane & 15)
                         wc = 4 * s + (lane >> 4)
@@ -77,7 +80,8 @@ def test_weight_stage_writes_and_reads_agree(cin):
                         assert got == n * kpad + tap * cin + 64 * ks + 8 * wc
 
 
-def test_fragment_reads_are_bank_conflict_free():
+@pytest.mark.parametrize("TH", [8, 4])
+def test_fragment_reads_are_bank_conflict_free(TH):
     """Every ds_read_b128 lane group of a fragment read (lane l: pixel l % 16 at chunk 4 s + l / 16) hits 16 distinct
     16-B bank groups ((a / 4) % 64 over 4 banks each), for every tap offset of the window."""
     for wave in range(4):
@@ -95,7 +99,7 @@ def test_fragment_reads_are_bank_conflict_free():
 
 
 def test_weight_reads_are_bank_conflict_free():
-    for j in range(4):
+    for j in range(8):
         for s in range(2):
             for g in B128_GROUPS:
                 banks = set()
@@ -121,6 +125,6 @@ def test_old_key_conflicts_with_the_real_lane_groups():
 
 def test_patch_and_weight_stores_are_bank_conflict_free():
     """ds_write_b128: 8 groups of 8 contiguous lanes, bank (a / 4) % 32; 8 lanes write one row's 8 chunks."""
-    for row0 in range(0, 64, 1):
+    for row0 in range(0, 128, 1):
         offs = [(row0 * 128 + swz(row0, c)) // 16 % 8 for c in range(8)]
         assert sorted(offs) == list(range(8))
