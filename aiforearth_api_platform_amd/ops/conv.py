@@ -240,13 +240,14 @@ def _tile_rows(cout: int) -> int:
 def tile64_supported(x: torch.Tensor, pc: PackedConv) -> bool:
     """Shapes K1t (``conv3x3_tile64``, csrc/kernels/conv_tile3x3.hip) takes: 3x3 / stride 1 / pad 1, bf16, 64 or 128
     -> 64 channels (8 x 32 output tiles, H % 8 == 0) or 64 / 128 / 256 -> 128 channels (4 x 32 tiles, H % 4 == 0),
-    W % 32 == 0. AI4E_CONV_TILE64: "1" default, every instance; "64" the 64 -> 64 instance only; "0" off.
-    AI4E_K1T_COUT128=0 turns off the 128-output-channel instances alone."""
+    W % 32 == 0. AI4E_CONV_TILE64: "1" default, the 64-output-channel instances; "64" the 64 -> 64 instance only;
+    "0" off. The 128-output-channel instances are opt-in (AI4E_K1T_COUT128=1): correct, but the U-Net is 1.4 % slower
+    with them than with K1 at level 1 (profiles/r4_k1t/cout128/)."""
     n, h, w, c = x.shape
     # the 64-channel instances beat K1 (profiles/r4_k1t/: 558 vs 670 us and 829 vs 1022 us per conv over 16 tiles of
     # 512^2; U-Net 24.4 vs 22.5 mosaics/s with K1)
     mode = os.environ.get("AI4E_CONV_TILE64", "1")
-    if pc.cout == 128 and os.environ.get("AI4E_K1T_COUT128", "1") == "0":
+    if pc.cout == 128 and os.environ.get("AI4E_K1T_COUT128", "0") != "1":
         return False
     ok_c = (pc.cout == 64 and pc.cin_pad in (64, 128)) or (pc.cout == 128 and pc.cin_pad in (64, 128, 256))
     return (mode != "0" and (mode != "64" or (c == 64 and pc.cout == 64)) and _ext.backend_for(x) == "hip"

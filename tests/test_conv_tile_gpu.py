@@ -15,6 +15,7 @@ DEV = "cuda"
 @pytest.fixture(autouse=True)
 def _k1t_on(monkeypatch):
     monkeypatch.setenv("AI4E_CONV_TILE64", "1")
+    monkeypatch.setenv("AI4E_K1T_COUT128", "1")
 
 
 def _conv_ref(xin: torch.Tensor, w: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
