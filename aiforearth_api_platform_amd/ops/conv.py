@@ -259,18 +259,24 @@ def tile64_supported(x: torch.Tensor, pc: PackedConv) -> bool:
 
 
 def conv3x3_tile64(x: torch.Tensor, pc: PackedConv, pro: Optional[torch.Tensor] = None, pro_relu: bool = True,
-                   gn_groups: int = 0) -> Tuple[torch.Tensor, Optional[tuple]]:
+                   gn_groups: int = 0, up: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, Optional[tuple]]:
     """K1t: ``conv3x3(pro(x)) + bias`` (see ``tile64_supported``), one 8 x 32 (cout 64) or 4 x 32 (cout 128) output
     tile at a time per persistent workgroup from an LDS input patch. ``pro``: float32 [N, C, 2] per-(image, channel)
     affine applied to the input as it is loaded (``x * a + b``, then ReLU with ``pro_relu``): the previous GroupNorm,
     which then needs no apply pass (``norm.group_norm_affine``). Returns ``(y, stats)`` with ``stats`` =
-    ``(partials, nchunks)`` GroupNorm statistics of y (as ``conv2d_gn_nhwc``) when ``gn_groups``, else None."""
+    ``(partials, nchunks)`` GroupNorm statistics of y (as ``conv2d_gn_nhwc``) when ``gn_groups``, else None.
+    ``up`` (128 -> 64 only, no ``pro``): a contiguous [N, H/2, W/2, 64] tensor whose bilinear 2x upsample
+    (align_corners=False) replaces input channels 64-127, formed per tile in LDS: x's channels 64-127 are not read,
+    so the upsampled half of a [skip | upsampled] concat need not be written."""
     n, h, w, c = x.shape
     if not tile64_supported(x, pc):
         raise ValueError("conv3x3_tile64: unsupported shape / dtype / layout")
     if pro is not None and (pro.dtype != torch.float32 or not pro.is_contiguous() or tuple(pro.shape) != (n, c, 2)):
         raise ValueError(f"conv3x3_tile64: pro must be contiguous float32 [N, {c}, 2]")
     cout = pc.cout
+    if up is not None and (c != 128 or cout != 64 or pro is not None or up.dtype != torch.bfloat16
+                           or not up.is_contiguous() or tuple(up.shape) != (n, h // 2, w // 2, 64) or h % 2 or w % 2):
+        raise ValueError("conv3x3_tile64: up needs the 128 -> 64 conv, no prologue, a contiguous bf16 [N, H/2, W/2, 64]")
     ldx = x.stride(2)
     xoff = x.storage_offset()
     base = x.untyped_storage().data_ptr() + 2 * (xoff - xoff % ldx)
@@ -281,7 +287,7 @@ def conv3x3_tile64(x: torch.Tensor, pc: PackedConv, pro: Optional[torch.Tensor] 
         partials = torch.empty(n * nchunks * gn_groups * 4 + n * cout * 2, device=x.device, dtype=torch.float32)
     _ext.call("ai4e_conv3x3_tile_fwd", base, pc.w_packed.data_ptr(), pc.bias.data_ptr(), _ext.ptr(pro),
               int(pro_relu), out.data_ptr(), n, h, w, c, cout, ldx, xoff % ldx, pc.kpad, cout, 0, _ext.ptr(partials),
-              gn_groups, _ext.stream_ptr(x.device))
+              gn_groups, _ext.ptr(up), _ext.stream_ptr(x.device))
     return out, ((partials, nchunks) if gn_groups else None)
 
 

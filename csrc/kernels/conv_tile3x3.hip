@@ -20,6 +20,7 @@
 // the one-tile-per-workgroup version exposed (1.54 TB/s, profiles/r4_k1t) hides under the MFMAs.
 // Every global address is inside its tensor by construction (host: H % TH == 0, W % 32 == 0; tile t < ntiles).
 #include <cstdlib>
+#include <type_traits>
 
 #include "common.h"
 
@@ -33,7 +34,11 @@ constexpr int T_W = 32, P_W = T_W + 2;           // output tile width; patch wid
 // runs each tile as CIN / 64 k-slices through the same patch buffer: the accumulators carry over, the epilogue runs
 // once, and the next slice's patch is prefetched under the current slice's taps like the next tile's.
 // LDS: patch + CIN x 8 B affine + two COUT x 128 B weight stages + the bias; two workgroups per CU.
-template <int CIN, int COUT>
+// UPS (CIN 128 -> COUT 64 only): the second k-slice (input channels 64-127) is the bilinear 2x upsample (PyTorch
+// align_corners=False) of a coarse 64-channel tensor [N, H/2, W/2, 64], formed in LDS from its CR x CC coarse block
+// instead of read from a materialized [skip | upsampled] concat: the U-Net's level-0 decoder c1 then never needs the
+// upsampled half written (537 MB per 16 tiles of 512^2) nor reads it back.
+template <int CIN, int COUT, bool UPS = false>
 struct TileCfg {
   static constexpr int TH = COUT == 64 ? 8 : 4;         // output tile rows
   static constexpr int P_SLOTS = (TH + 2) * P_W;
@@ -50,6 +55,13 @@ struct TileCfg {
   static constexpr int FPW = TH / 2;                    // pixel fragments per wave (TH / 4 rows x 2 half-rows)
   static constexpr int NJ = COUT / 16;                  // 16-channel output blocks per wave
   static constexpr int NWV = COUT / 32;                 // 16-B weight chunks per thread per stage
+  static constexpr int CR = TH / 2 + 2, CC = T_W / 2 + 3;  // UPS coarse block: rows h0/2 - 1 .., cols w0/2 - 1 ..
+  static constexpr int C_CHUNKS = CR * CC * 8;
+  static constexpr int C_ITERS = (C_CHUNKS + 255) / 256;
+  static constexpr int L_CO = UPS ? CR * CC * 128 : 0;
+  static constexpr int L_ALL = L_TOTAL + L_CO;
+  static_assert(!UPS || (CIN == 128 && COUT == 64), "UPS: the 128 -> 64 instance");
+  static_assert(L_ALL <= 80 * 1024, "two workgroups per CU (with the coarse block)");
   static_assert(CIN == 64 || CIN == 128 || CIN == 256, "K1t: 64, 128 or 256 input channels");
   static_assert(COUT == 64 || COUT == 128, "K1t: 64 or 128 output channels");
   static_assert(L_TOTAL <= 80 * 1024, "two workgroups per CU");
@@ -69,6 +81,7 @@ struct TileParams {
   float* gnp;              // GroupNorm partials [N, tiles per image, G, 4]; null = off
   int gn_groups;
   int H, W, tiles_w, tiles_per_img;
+  const uint16_t* xu;      // UPS: coarse [N, H / 2, W / 2, 64] (input channels 64-127 = its 2x upsample)
 };
 
 // Byte offset within its row of 16-B chunk c of row `row` (M = 8 chunks per row). ds_read_b128 is serviced in four
@@ -90,10 +103,10 @@ __device__ __forceinline__ uint32_t swz(int row, int c) {
   return static_cast<uint32_t>((c ^ (row & 6)) << 4);
 }
 
-template <int CIN, int COUT>
+template <int CIN, int COUT, bool UPS = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv3x3_tile_kernel(
     const TileParams p, int ntiles) {
-  using Cfg = TileCfg<CIN, COUT>;
+  using Cfg = TileCfg<CIN, COUT, UPS>;
   constexpr int NJ = Cfg::NJ, L_W = Cfg::L_W;
   constexpr int TH = Cfg::TH, P_CHUNKS = Cfg::P_CHUNKS, P_ITERS = Cfg::P_ITERS, NCH = Cfg::NCH, SLOT_B = Cfg::SLOT_B;
   constexpr int KS = Cfg::KS, NST = Cfg::NST, FPW = Cfg::FPW;
@@ -104,6 +117,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   float2* const aff = reinterpret_cast<float2*>(sm + Cfg::L_PATCH);
   uint8_t* const wbuf = sm + Cfg::L_PATCH + Cfg::L_AFF;
   float* const sbias = reinterpret_cast<float*>(wbuf + 2 * L_W);  // [COUT]: epilogue reads stay off the vmcnt queue
+  uint8_t* const coarse = wbuf + 2 * L_W + COUT * 4;                // UPS: [CR x CC slots][128 B]
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g4 = lane >> 4;
@@ -137,7 +151,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   // the patch of one tile: global -> registers (pv, in-image chunks in pmask), later registers -> LDS
   uint4 pv[P_ITERS];
   uint32_t pmask = 0;
-  auto load_patch = [&](int img, int h0, int w0, int ks, int k0, int k1) __attribute__((always_inline)) {
+  auto load_patch = [&](int img, int h0, int w0, int ks, int k0, int k1, bool coarse_mode = false)
+                        __attribute__((always_inline)) {
     const uint16_t* const xi = p.x + static_cast<long>(img) * p.H * p.W * p.ldx + p.xcoff + 64 * ks;
     int tq = tid;
     asm volatile("" : "+v"(tq));  // recompute the chunk address math per tile (hoisted, it spills)
@@ -153,7 +168,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       // unconditional load from the nearest in-image pixel (no branch around it, so the vmcnt waits stay exact);
       // store_patch zeroes the chunks outside the image
       const int ihc = min(max(ih, 0), p.H - 1), iwc = min(max(iw, 0), p.W - 1);
-      pv[k] = *reinterpret_cast<const uint4*>(xi + (static_cast<long>(ihc) * p.W + iwc) * p.ldx + 8 * (c & 7));
+      const uint16_t* src = xi + (static_cast<long>(ihc) * p.W + iwc) * p.ldx + 8 * (c & 7);
+      if constexpr (UPS) {  // coarse-block chunk k (k < C_ITERS; beyond, a repeat of chunk 0), clamped in-tensor
+        const int ek = k < Cfg::C_ITERS ? e : tq;
+        const int cs = ek >> 3, cc8 = ek & 7;
+        const int cr = cs / Cfg::CC, ccol = cs - cr * Cfg::CC;
+        const int cy = min(max((h0 >> 1) - 1 + cr, 0), (p.H >> 1) - 1);
+        const int cx = min(max((w0 >> 1) - 1 + ccol, 0), (p.W >> 1) - 1);
+        const uint16_t* csrc = p.xu + ((static_cast<long>(img) * (p.H >> 1) + cy) * (p.W >> 1) + cx) * 64 + 8 * cc8;
+        src = coarse_mode ? csrc : src;
+      }
+      pv[k] = *reinterpret_cast<const uint4*>(src);
     }
   };
   auto store_patch = [&](int ks) __attribute__((always_inline)) {
@@ -182,6 +207,62 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
           wds[q] = pack_bf16x2(lo, hi);
         }
         v = make_uint4(wds[0], wds[1], wds[2], wds[3]);
+      }
+      *reinterpret_cast<uint4*>(patch + slot * SLOT_B + swz<NCH>(slot, c)) = v;
+    }
+  };
+  // UPS: the coarse block of a tile (global -> the prefetch registers pv via load_patch, clamped in-tensor addresses;
+  // later -> LDS), then the fine
+  // 64-channel patch from it with upsample2x_kernel's exact arithmetic (norm_resample.hip)
+  constexpr int C_ITERS = Cfg::C_ITERS, CR = Cfg::CR, CC = Cfg::CC;
+  static_assert(!UPS || C_ITERS <= P_ITERS, "the coarse block reuses the patch prefetch registers");
+  const int Hc = p.H >> 1, Wc = p.W >> 1;
+  auto store_coarse = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int k = 0; k < C_ITERS; ++k) {
+      const int e = tid + 256 * k;
+      if (e >= Cfg::C_CHUNKS) continue;
+      const int slot = e >> 3, c = e & 7;
+      *reinterpret_cast<uint4*>(coarse + slot * 128 + swz<8>(slot, c)) = pv[k];
+    }
+  };
+  auto fine_from_coarse = [&](int h0, int w0) __attribute__((always_inline)) {
+    int tq = tid;
+    asm volatile("" : "+v"(tq));
+    const int cy0 = (h0 >> 1) - 1, cx0 = (w0 >> 1) - 1;
+#pragma unroll
+    for (int k = 0; k < P_ITERS; ++k) {
+      const int e = tq + 256 * k;
+      if (e >= P_CHUNKS) continue;
+      const int slot = e / NCH, c = e - slot * NCH;
+      const int pr = slot / P_W, pc = slot - pr * P_W;
+      const int ih = h0 - 1 + pr, iw = w0 - 1 + pc;
+      uint4 v = make_uint4(0u, 0u, 0u, 0u);  // the conv's zero padding outside the image
+      if (static_cast<unsigned>(ih) < static_cast<unsigned>(p.H) && static_cast<unsigned>(iw) < static_cast<unsigned>(p.W)) {
+        const float sy = fmaxf((ih + 0.5f) * 0.5f - 0.5f, 0.f), sx = fmaxf((iw + 0.5f) * 0.5f - 0.5f, 0.f);
+        const int y0 = static_cast<int>(sy), x0 = static_cast<int>(sx);
+        const int y1 = min(y0 + 1, Hc - 1), x1 = min(x0 + 1, Wc - 1);
+        const float ly = sy - y0, lx = sx - x0;
+        const float w00 = (1 - ly) * (1 - lx), w01 = (1 - ly) * lx, w10 = ly * (1 - lx), w11 = ly * lx;
+        const int s00 = (y0 - cy0) * CC + (x0 - cx0), s01 = (y0 - cy0) * CC + (x1 - cx0);
+        const int s10 = (y1 - cy0) * CC + (x0 - cx0), s11 = (y1 - cy0) * CC + (x1 - cx0);
+        const uint4 a = *reinterpret_cast<const uint4*>(coarse + s00 * 128 + swz<8>(s00, c));
+        const uint4 b = *reinterpret_cast<const uint4*>(coarse + s01 * 128 + swz<8>(s01, c));
+        const uint4 cq = *reinterpret_cast<const uint4*>(coarse + s10 * 128 + swz<8>(s10, c));
+        const uint4 d = *reinterpret_cast<const uint4*>(coarse + s11 * 128 + swz<8>(s11, c));
+        const uint32_t pa[4] = {a.x, a.y, a.z, a.w}, pb[4] = {b.x, b.y, b.z, b.w};
+        const uint32_t pcq[4] = {cq.x, cq.y, cq.z, cq.w}, pd[4] = {d.x, d.y, d.z, d.w};
+        uint32_t o[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          float a0, a1, b0, b1, c0, c1, d0, d1;
+          unpack_bf16x2(pa[q], a0, a1);
+          unpack_bf16x2(pb[q], b0, b1);
+          unpack_bf16x2(pcq[q], c0, c1);
+          unpack_bf16x2(pd[q], d0, d1);
+          o[q] = pack_bf16x2(w00 * a0 + w01 * b0 + w10 * c0 + w11 * d0, w00 * a1 + w01 * b1 + w10 * c1 + w11 * d1);
+        }
+        v = make_uint4(o[0], o[1], o[2], o[3]);
       }
       *reinterpret_cast<uint4*>(patch + slot * SLOT_B + swz<NCH>(slot, c)) = v;
     }
@@ -238,6 +319,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     int sbase[FPW];
 #pragma unroll
     for (int f = 0; f < FPW; ++f) sbase[f] = ((TH / 4) * wave + (f >> 1)) * P_W + 16 * (f & 1) + l16;
+    // UPS: the next item is the coarse block when it is this tile's second slice; the loads stay on one code path
+    // (address chosen by select: a runtime branch around the loads would make the waits inexact)
+    const bool coarse_next = UPS && ksn == 1;
 #pragma unroll
     for (int st = 0; st < NST; ++st) {  // stage = tap
       // issue order is the wait order (vmcnt retires in order): this stage's weight chunks first, then PPS chunks
@@ -245,7 +329,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       // which otherwise sinks the weight loads to their use at the end of the stage
       if (st + 1 < NST) load_w(st + 1, ks);
       load_patch(imgn, h0n, w0n, ksn, st * PPS < P_ITERS ? st * PPS : P_ITERS,
-                 (st + 1) * PPS < P_ITERS ? (st + 1) * PPS : P_ITERS);
+                 (st + 1) * PPS < P_ITERS ? (st + 1) * PPS : P_ITERS, coarse_next);
       __builtin_amdgcn_sched_barrier(0);
       const int kh = st / 3, kw = st - 3 * kh;
       const uint8_t* const wb = wbuf + (st & 1) * L_W;
@@ -359,8 +443,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     tile_barrier();  // this slice's patch, weight stages and statistics scratch are read
     if (last_slice && p.pro != nullptr && tid < CIN) aff[tid] = p.pro[imgn * CIN + tid];
     store_w(0);
-    tile_barrier();  // the next tile's affine is in LDS
-    store_patch(ksn);
+    if (UPS && ksn == 1) {
+      store_coarse();
+      tile_barrier();  // the coarse block is in LDS
+      fine_from_coarse(h0n, w0n);
+    } else {
+      tile_barrier();  // the next tile's affine is in LDS
+      store_patch(ksn);
+    }
     tile_barrier();
     t = tn;
     ks = ksn;
@@ -375,11 +465,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 
 namespace {
 
-template <int CIN, int COUT>
+template <int CIN, int COUT, bool UPS = false>
 int launch_tile(const TileParams& p, int N, hipStream_t stream) {
-  constexpr int L = TileCfg<CIN, COUT>::L_TOTAL;
+  constexpr int L = TileCfg<CIN, COUT, UPS>::L_ALL;
   static bool attr = [] {
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(conv3x3_tile_kernel<CIN, COUT>),
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(conv3x3_tile_kernel<CIN, COUT, UPS>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, L) == hipSuccess;
   }();
   if (!attr) return AI4E_ELAUNCH;
@@ -395,7 +485,7 @@ int launch_tile(const TileParams& p, int N, hipStream_t stream) {
     return AI4E_ELAUNCH;
   const int ntiles = N * p.tiles_per_img;
   const int grid = persist && ntiles > 2 * cus ? 2 * cus : ntiles;
-  hipLaunchKernelGGL((conv3x3_tile_kernel<CIN, COUT>), dim3(static_cast<unsigned>(grid)), dim3(256), L, stream, p, ntiles);
+  hipLaunchKernelGGL((conv3x3_tile_kernel<CIN, COUT, UPS>), dim3(static_cast<unsigned>(grid)), dim3(256), L, stream, p, ntiles);
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
 }
 
@@ -404,15 +494,20 @@ int launch_tile(const TileParams& p, int N, hipStream_t stream) {
 // y = conv3x3(pro(x)) + bias (cin 64 / 128 -> 64 channels, or cin 64 / 128 / 256 -> 128 channels; stride 1, pad 1)
 // with GroupNorm partials of y (gn_groups > 0): [N, (H / TH) * (W / 32), G, 4], TH = 8 (cout 64) or 4 (cout 128).
 // pro: null or float2 [N, cin] (x * a + b, then ReLU if pro_relu).
+// xu (UPS): null, or a contiguous coarse [N, H / 2, W / 2, 64] tensor whose bilinear 2x upsample (align_corners=False)
+// replaces input channels 64-127 (cin 128 -> cout 64, no prologue): x then supplies channels 0-63 only.
 AI4E_API int ai4e_conv3x3_tile_fwd(const void* x, const void* w, const void* bias, const void* pro, int pro_relu,
                                    void* y, int N, int H, int W, int cin, int cout, int ldx, int xcoff, int kpad,
-                                   int ldy, int ycoff, void* gn_partials, int gn_groups, hipStream_t stream) {
+                                   int ldy, int ycoff, void* gn_partials, int gn_groups, const void* xu,
+                                   hipStream_t stream) {
   const bool ok_c = (cout == 64 && (cin == 64 || cin == 128)) || (cout == 128 && (cin == 64 || cin == 128 || cin == 256));
   const int th = cout == 64 ? TileCfg<64, 64>::TH : TileCfg<64, 128>::TH;
   if (!x || !w || !bias || !y || N <= 0 || !ok_c || H % th || W % T_W || kpad < 9 * cin || ldx % 8 || xcoff % 8 ||
       xcoff + cin > ldx || ldy % 8 || ycoff % 8 || ycoff + cout > ldy)
     return AI4E_EINVAL;
   if (reinterpret_cast<uintptr_t>(bias) % 16) return AI4E_EINVAL;  // float4 reads in the epilogue
+  if (xu && (cin != 128 || cout != 64 || pro || H % 2 || W % 2 || reinterpret_cast<uintptr_t>(xu) % 16))
+    return AI4E_EINVAL;
   if (gn_partials && (gn_groups <= 0 || gn_groups > 64 || cout % gn_groups || cout / gn_groups > 4))
     return AI4E_EINVAL;
   if (static_cast<long>(N) * H * W * (ldx > ldy ? ldx : ldy) >= (1L << 40)) return AI4E_EINVAL;
@@ -434,6 +529,8 @@ AI4E_API int ai4e_conv3x3_tile_fwd(const void* x, const void* w, const void* bia
   p.W = W;
   p.tiles_w = W / T_W;
   p.tiles_per_img = (H / th) * p.tiles_w;
+  p.xu = static_cast<const uint16_t*>(xu);
+  if (xu) return launch_tile<128, 64, true>(p, N, stream);
   if (cout == 64) return cin == 64 ? launch_tile<64, 64>(p, N, stream) : launch_tile<128, 64>(p, N, stream);
   if (cin == 64) return launch_tile<64, 128>(p, N, stream);
   return cin == 128 ? launch_tile<128, 128>(p, N, stream) : launch_tile<256, 128>(p, N, stream);

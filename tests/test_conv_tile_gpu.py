@@ -146,3 +146,38 @@ def test_unet_fused_head_equals_apply_then_conv():
     rel = ((y_f[..., :k] - y_u[..., :k]).norm() / y_u[..., :k].norm()).item()
     assert rel < 1e-2, rel
     assert (y_f[..., :k].argmax(-1) == y_u[..., :k].argmax(-1)).float().mean().item() > 0.99
+
+
+@pytest.mark.parametrize("n,h,w", [(1, 8, 32), (2, 16, 64), (3, 128, 512)])
+def test_conv3x3_tile64_ups_equals_explicit_upsample(n, h, w):
+    """K1t UPS: the 128 -> 64 conv whose input channels 64-127 are the bilinear 2x upsample of a coarse tensor, formed
+    in LDS, equals the same conv over a concat with the upsample written by upsample2x_nhwc — bitwise (the patch
+    values use the upsample kernel's exact arithmetic), GroupNorm statistics included. The concat's upsampled half is
+    garbage in the UPS call: it must not be read."""
+    from aiforearth_api_platform_amd.ops.conv import conv3x3_tile64
+    from aiforearth_api_platform_amd.ops.norm import upsample2x_nhwc
+    x, wt, b, pc = _case(n, h, w, 31, 128, 64)
+    g = torch.Generator().manual_seed(32)
+    coarse = torch.randn(n, h // 2, w // 2, 64, generator=g).to(torch.bfloat16).to(DEV)
+    cat = x.to(DEV).clone()
+    upsample2x_nhwc(coarse, out=cat, out_coff=64)
+    y_ref, st_ref = conv3x3_tile64(cat, pc, gn_groups=32)
+    junk = cat.clone()
+    junk[..., 64:] = float("nan")
+    y_ups, st_ups = conv3x3_tile64(junk, pc, gn_groups=32, up=coarse)
+    assert torch.equal(y_ups, y_ref)
+    assert torch.equal(st_ups[0], st_ref[0])
+
+
+def test_unet_fused_upsample_equals_unfused():
+    """The U-Net with the level-0 upsample fused into the decoder c1 (AI4E_UNET_FUSED_UP=1) equals the default."""
+    from aiforearth_api_platform_amd.models.unet import FusedUNet, unet_landcover
+    m = unet_landcover(seed=9)
+    img = torch.randint(0, 256, (2, 256, 256, 4), dtype=torch.uint8, generator=torch.Generator().manual_seed(9))
+    y_ref = FusedUNet(m, device=DEV).forward_u8(img.to(DEV))
+    os.environ["AI4E_UNET_FUSED_UP"] = "1"
+    try:
+        y_f = FusedUNet(m, device=DEV).forward_u8(img.to(DEV))
+    finally:
+        del os.environ["AI4E_UNET_FUSED_UP"]
+    assert torch.equal(y_f, y_ref)

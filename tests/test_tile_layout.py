@@ -128,3 +128,32 @@ def test_patch_and_weight_stores_are_bank_conflict_free():
     for row0 in range(0, 128, 1):
         offs = [(row0 * 128 + swz(row0, c)) // 16 % 8 for c in range(8)]
         assert sorted(offs) == list(range(8))
+
+
+@pytest.mark.parametrize("H,W", [(8, 32), (16, 64), (64, 96), (512, 512)])
+def test_ups_coarse_block_covers_every_fine_pixel(H, W):
+    """K1t UPS (the 128 -> 64 instance's second k-slice = bilinear 2x upsample of a coarse [H/2, W/2] tensor): the
+    coarse block of a tile (CR x CC slots from (h0/2 - 1, w0/2 - 1), loads clamped into the tensor) holds every
+    source pixel of the upsample formula (upsample2x_kernel) for every in-image fine pixel of the tile's patch."""
+    th, tw, pw = 8, 32, 34
+    cr_n, cc_n = th // 2 + 2, tw // 2 + 3
+    hc, wc = H // 2, W // 2
+    for h0 in range(0, H, th):
+        for w0 in range(0, W, tw):
+            cy0, cx0 = h0 // 2 - 1, w0 // 2 - 1
+            # what each coarse slot holds (the kernel's clamped load)
+            held = {(r, c): (min(max(cy0 + r, 0), hc - 1), min(max(cx0 + c, 0), wc - 1))
+                    for r in range(cr_n) for c in range(cc_n)}
+            for pr in range(th + 2):
+                for pc in range(pw):
+                    ih, iw = h0 - 1 + pr, w0 - 1 + pc
+                    if not (0 <= ih < H and 0 <= iw < W):
+                        continue
+                    sy, sx = max((ih + 0.5) * 0.5 - 0.5, 0.0), max((iw + 0.5) * 0.5 - 0.5, 0.0)
+                    y0, x0 = int(sy), int(sx)
+                    y1, x1 = min(y0 + 1, hc - 1), min(x0 + 1, wc - 1)
+                    for yy in (y0, y1):
+                        for xx in (x0, x1):
+                            r, c = yy - cy0, xx - cx0
+                            assert 0 <= r < cr_n and 0 <= c < cc_n, (h0, w0, ih, iw, r, c)
+                            assert held[(r, c)] == (yy, xx)
