@@ -166,7 +166,8 @@ def test_conv3x3_tile64_ups_equals_explicit_upsample(n, h, w):
     junk[..., 64:] = float("nan")
     y_ups, st_ups = conv3x3_tile64(junk, pc, gn_groups=32, up=coarse)
     assert torch.equal(y_ups, y_ref)
-    assert torch.equal(st_ups[0], st_ref[0])
+    k = n * st_ref[1] * 32 * 4  # the partials (the buffer's tail is the finalize's workspace, uninitialized here)
+    assert torch.equal(st_ups[0][:k], st_ref[0][:k])
 
 
 def test_unet_fused_upsample_equals_unfused():
