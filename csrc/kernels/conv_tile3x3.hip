@@ -1,24 +1,25 @@
-// K1t: 3x3 / stride 1 / pad 1 convolution, 64 (or 128) -> 64 channels, NHWC bf16, for wide feature maps: the U-Net's
-// full-resolution level (512^2 tiles), where the K1 implicit GEMM gathers every tap of every pixel through the
-// LDS-DMA ring (nine 16-B gathers per pixel and 32-channel step) and ran at 23 % MFMA / 1.3 TB/s
-// (profiles/r4_unet/pmc_by_kernel.txt) against an HBM floor of ~half its time.
+// K1t: 3x3 / stride 1 / pad 1 convolution, NHWC bf16, for wide feature maps: 64 / 128 -> 64 channels (the U-Net's
+// full-resolution level, 512^2 tiles; default) and 64 / 128 / 256 -> 128 channels (level 1; opt-in, slower than K1
+// there). At level 0 the K1 implicit GEMM gathers every tap of every pixel through the LDS-DMA ring (nine 16-B
+// gathers per pixel and 32-channel step) and ran at 23 % MFMA / 1.3 TB/s (profiles/r4_unet/pmc_by_kernel.txt).
 //
-// Each 8 x 32 output tile is computed by one workgroup (4 waves):
-// * the 10 x 34 x 64 input patch (halo 1, zero outside the image) is loaded ONCE into LDS (43.5 KB, 16-B chunks of a
-//   pixel slot XOR-swizzled by the slot index so the 16 pixels of a fragment read conflict-free), optionally through
-//   a prologue: x * a[c] + b[c] (+ ReLU) per (image, channel) — the previous layer's GroupNorm apply, so that the
-//   normalized tensor is never written (its statistics came from the previous conv's epilogue);
-// * the nine taps then run as LDS-read + MFMA steps (v_mfma_f32_16x16x32_bf16; weights as the A operand, 4 channel
-//   fragments, pixels as B, 4 pixel fragments per wave: 64 px x 64 ch per wave), the next tap's weights (8 KB) loaded
-//   from L2 during the current tap into the other half of a two-tap LDS buffer;
+// Each output tile (8 x 32 for COUT 64, 4 x 32 for COUT 128) is computed by one workgroup (4 waves):
+// * the (TH + 2) x 34 x 64 input patch (halo 1, zero outside the image) is loaded ONCE into LDS (16-B chunks of a
+//   pixel slot XOR-swizzled for the real ds_read_b128 lane groups), optionally through a prologue: x * a[c] + b[c]
+//   (+ ReLU) per (image, channel) — the previous layer's GroupNorm apply, so that the normalized tensor is never
+//   written (its statistics came from the previous conv's epilogue);
+// * the nine taps then run as LDS-read + MFMA steps (v_mfma_f32_16x16x32_bf16; weights as the A operand, pixels as
+//   B; per wave 64 px x 64 ch or 32 px x 128 ch: 32 MFMAs per stage), the next tap's weights loaded from L2 during
+//   the current tap into the other half of a two-tap LDS buffer;
 // * epilogue: + bias, bf16 store, and the GroupNorm statistics of the stored values per (image, tile, group) in the
 //   K1 conv-epilogue format (shifted sums S, Q and the shift K: norm_resample.hip gn_finalize_kernel).
-// 128 input channels (TileCfg): the same 8 x 32 tiles, run as two 64-channel k-slices (accumulators carried over).
-// Persistent: min(tiles, 2 x CUs) workgroups walk the tiles with stride gridDim.x; the next tile's patch (11 x 16 B
-// per thread) is loaded into registers while the current tile's taps run, and its first weight stage while the
-// epilogue runs, then stored into LDS (through the prologue) behind one barrier — the per-tile load latency that
-// the one-tile-per-workgroup version exposed (1.54 TB/s, profiles/r4_k1t) hides under the MFMAs.
-// Every global address is inside its tensor by construction (host: H % TH == 0, W % 32 == 0; tile t < ntiles).
+// CIN > 64: the same tiles, run as CIN / 64 k-slices through one 64-channel patch buffer (accumulators carried over).
+// UPS (128 -> 64, opt-in): the second k-slice is the bilinear 2x upsample of a coarse tensor, formed in LDS.
+// Persistent: min(tiles, 2 x CUs) workgroups walk the tiles with stride gridDim.x. The next (tile, slice)'s patch is
+// loaded into registers while the current taps run (spread over the stages, so every vmcnt wait stays exact), and its
+// first weight stage while the epilogue runs, then stored into LDS (through the prologue) behind one barrier.
+// Every global address is inside its tensor by construction (host: H % TH == 0, W % 32 == 0; tile t < ntiles; patch
+// and coarse loads clamped to in-tensor pixels, out-of-image chunks zeroed in LDS).
 #include <cstdlib>
 #include <type_traits>
 
@@ -91,17 +92,17 @@ struct TileParams {
 // 8 (row & 1) + (c ^ key(row)), so for every window of 16 rows the keys of each row parity, with the middle pixels'
 // extra ^ 1, must be distinct: key = row & 6 is (tests/test_tile_layout.py searches and checks this). The earlier key
 // (row >> 1) & 7 was conflict-free only for contiguous 16-lane groups, and measured 16-18 % bank conflicts.
-// LDS handoff between the waves: wait for this wave's LDS operations, then the barrier. Not __syncthreads(): its
-// workgroup release fence makes the compiler drain vmcnt (which on gfx9 counts loads and stores together) before
-// every barrier, so the weight and next-patch loads in flight would be waited for at each of the 9 stages. Nothing
-// in this kernel passes data between waves through global memory.
-__device__ __forceinline__ void tile_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-
 template <int M>
 __device__ __forceinline__ uint32_t swz(int row, int c) {
   static_assert(M == 8, "8 chunks per row");
   return static_cast<uint32_t>((c ^ (row & 6)) << 4);
 }
+
+// LDS handoff between the waves: wait for this wave's LDS operations, then the barrier. Not __syncthreads(): its
+// workgroup release fence makes the compiler drain vmcnt (which on gfx9 counts loads and stores together) before
+// every barrier, so the weight and next-patch loads in flight would be waited for at each of the 9 stages. Nothing
+// in this kernel passes data between waves through global memory.
+__device__ __forceinline__ void tile_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 template <int CIN, int COUT, bool UPS = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv3x3_tile_kernel(
