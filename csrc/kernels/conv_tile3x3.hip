@@ -24,6 +24,14 @@
 #include <type_traits>
 
 #include "common.h"
+#include "conv_common.h"
+
+// Weight stages by LDS-DMA (global_load_lds_dwordx4) into THREE stage buffers, issued two stages ahead: no registers
+// hold weights in flight and each stage's weights get two stages of latency hiding; explicit counted vmcnt waits
+// (the instance with the UPS coarse block keeps the register path: a third buffer would not fit 80 KB).
+#ifndef AI4E_K1T_WDMA
+#define AI4E_K1T_WDMA 1
+#endif
 
 namespace {
 
@@ -48,7 +56,9 @@ struct TileCfg {
   static constexpr int L_PATCH = P_SLOTS * SLOT_B;
   static constexpr int L_AFF = CIN * 8;                 // prologue affine of this image: CIN x (a, b)
   static constexpr int L_W = COUT * 128;                // one weight stage: COUT rows x 64 input channels of one tap
-  static constexpr int L_TOTAL = L_PATCH + L_AFF + 2 * L_W + COUT * 4;  // + the bias
+  static constexpr bool WDMA = AI4E_K1T_WDMA && !UPS;
+  static constexpr int NWB = WDMA ? 3 : 2;              // weight stage buffers
+  static constexpr int L_TOTAL = L_PATCH + L_AFF + NWB * L_W + COUT * 4;  // + the bias
   static constexpr int P_CHUNKS = P_SLOTS * NCH;
   static constexpr int P_ITERS = (P_CHUNKS + 255) / 256;
   static constexpr int KS = CIN / 64;                   // 64-channel k-slices per tile
@@ -67,6 +77,7 @@ struct TileCfg {
   static_assert(COUT == 64 || COUT == 128, "K1t: 64 or 128 output channels");
   static_assert(L_TOTAL <= 80 * 1024, "two workgroups per CU");
   static_assert((COUT + 4 * COUT * 2) * 4 <= L_W, "GroupNorm scratch (shift + 4-wave sums) fits a weight stage");
+  static_assert((COUT + 4 * COUT * 2) * 4 <= L_PATCH, "... and the patch buffer (its home with WDMA)");
 };
 
 struct TileParams {
@@ -117,8 +128,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   uint8_t* const patch = sm;
   float2* const aff = reinterpret_cast<float2*>(sm + Cfg::L_PATCH);
   uint8_t* const wbuf = sm + Cfg::L_PATCH + Cfg::L_AFF;
-  float* const sbias = reinterpret_cast<float*>(wbuf + 2 * L_W);  // [COUT]: epilogue reads stay off the vmcnt queue
-  uint8_t* const coarse = wbuf + 2 * L_W + COUT * 4;                // UPS: [CR x CC slots][128 B]
+  constexpr bool WDMA = Cfg::WDMA;
+  constexpr int NWB = Cfg::NWB;
+  float* const sbias = reinterpret_cast<float*>(wbuf + NWB * L_W);  // [COUT]: epilogue reads stay off the vmcnt queue
+  uint8_t* const coarse = wbuf + NWB * L_W + COUT * 4;              // UPS: [CR x CC slots][128 B]
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g4 = lane >> 4;
@@ -147,6 +160,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     if constexpr (Cfg::NWV == 4) {
       *reinterpret_cast<uint4*>(b + (n + 64) * 128 + swz<8>(n + 64, c)) = wv2;
       *reinterpret_cast<uint4*>(b + (n + 96) * 128 + swz<8>(n + 96, c)) = wv3;
+    }
+  };
+  // WDMA: the weight stage (tap, ks) straight into LDS buffer `buf`: wave w's instruction i fills rows
+  // (NWV w + i) * 8 .. + 7 (1 KB, base + 16 lane); the XOR swizzle is applied to the per-lane SOURCE chunk
+  // (physical chunk lane % 8 of row r holds logical chunk (lane % 8) ^ (r & 6), as swz<8>)
+  const uint32_t wlds = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(wbuf));
+  auto dma_w = [&](int tap, int ks, int buf) __attribute__((always_inline)) {
+    int lq = lane;
+    asm volatile("" : "+v"(lq));  // per-call address math (with one k-slice all 9 stages' addresses would be hoisted)
+#pragma unroll
+    for (int i = 0; i < Cfg::NWV; ++i) {
+      const int r = (Cfg::NWV * wave + i) * 8 + (lq >> 3);
+      const int c = (lq & 7) ^ (r & 6);
+      ai4e_conv::glds16(p.w + static_cast<long>(r) * p.kpad + tap * CIN + ks * 64 + 8 * c,
+                        wlds + buf * L_W + (Cfg::NWV * wave + i) * 1024);
     }
   };
   // the patch of one tile: global -> registers (pv, in-image chunks in pmask), later registers -> LDS
@@ -281,18 +309,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   // after it (and after the tile's epilogue).
   int t = blockIdx.x, ks = 0, img, tin, h0, w0;
   coords(t, img, tin, h0, w0);
-  load_w(0, 0);
+  if constexpr (WDMA) {
+    dma_w(0, 0, 0);
+    dma_w(1, 0, 1);
+  } else {
+    load_w(0, 0);
+  }
   if (p.pro != nullptr && tid < CIN) aff[tid] = p.pro[img * CIN + tid];
   if (tid < COUT) sbias[tid] = p.bias[tid];
   pmask = 0;
   load_patch(img, h0, w0, 0, 0, P_ITERS);
-  store_w(0);
+  if constexpr (WDMA) ai4e_conv::wait_vmcnt<0>();  // the first two weight stages landed
+  else store_w(0);
   tile_barrier();  // the affine is in LDS
   store_patch(0);
   tile_barrier();
 
-  float* const kshift = reinterpret_cast<float*>(wbuf);        // [COUT] the tile's first pixel, as stored
-  float* const red = reinterpret_cast<float*>(wbuf) + COUT;    // [4 waves][COUT channels][2]
+  // GroupNorm scratch: the weight buffer 0, or (WDMA: the next item's weights are landing there during the epilogue)
+  // the patch buffer, dead between the last stage and the next item's patch store
+  float* const kshift = reinterpret_cast<float*>(WDMA ? patch : wbuf);  // [COUT] the tile's first pixel, as stored
+  float* const red = kshift + COUT;                                    // [4 waves][COUT channels][2]
 
   f32x4_t acc[FPW][NJ];  // carried over the k-slices of a tile; zeroed here and after each tile's epilogue
   auto zero_acc = [&]() __attribute__((always_inline)) {
@@ -328,12 +364,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       // issue order is the wait order (vmcnt retires in order): this stage's weight chunks first, then PPS chunks
       // of the next (tile, slice)'s patch, which the waits of later stages cover; pinned against the scheduler,
       // which otherwise sinks the weight loads to their use at the end of the stage
-      if (st + 1 < NST) load_w(st + 1, ks);
+      if constexpr (WDMA) {  // two stages ahead: this item's stage st + 2, or the next item's stage st - 7
+        if (st + 2 < NST) dma_w(st + 2, ks, (st + 2) % 3);
+        else dma_w(st + 2 - NST, ksn, (st + 2) % 3);
+      } else if (st + 1 < NST) {
+        load_w(st + 1, ks);
+      }
       load_patch(imgn, h0n, w0n, ksn, st * PPS < P_ITERS ? st * PPS : P_ITERS,
                  (st + 1) * PPS < P_ITERS ? (st + 1) * PPS : P_ITERS, coarse_next);
       __builtin_amdgcn_sched_barrier(0);
       const int kh = st / 3, kw = st - 3 * kh;
-      const uint8_t* const wb = wbuf + (st & 1) * L_W;
+      const uint8_t* const wb = wbuf + (WDMA ? st % 3 : (st & 1)) * L_W;
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         const int wc = 4 * s + g4;  // chunk within the stage's 64 channels
@@ -353,10 +394,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
           for (int j = 0; j < NJ; ++j) acc[f][j] = mfma_16x16x32<false>(fw[j], fx[f], acc[f][j]);
       }
-      if (st + 1 < NST) store_w((st + 1) & 1);  // that buffer was last read at stage st - 1 (before the previous barrier)
+      if constexpr (WDMA) {
+        // the next stage's weights (issued at stage st - 1, or before the loop / at the previous item's last stage
+        // for st = 0: then counted as if nothing older were pending, a stricter wait) are in LDS: at most the
+        // operations issued after them may be outstanding
+        constexpr int ND = Cfg::NWV;
+        auto pl = [](int q) { return q < 0 ? 0 : (q * PPS < P_ITERS ? ((q + 1) * PPS < P_ITERS ? PPS : P_ITERS - q * PPS) : 0); };
+        ai4e_conv::wait_vmcnt_n(st == 0 ? ND + pl(0) : pl(st - 1) + ND + pl(st));
+      } else if (st + 1 < NST) {
+        store_w((st + 1) & 1);  // that buffer was last read at stage st - 1 (before the previous barrier)
+      }
       tile_barrier();
     }
-    load_w(0, ksn);  // the next slice's first weight stage, in flight under the epilogue (unused after the last)
+    if constexpr (!WDMA) load_w(0, ksn);  // the next slice's first weight stage, in flight under the epilogue
 
     // ---- epilogue (after the tile's last slice): lane holds channels 16 j + 4 g4 + v of pixel (lane % 16) of
     // each fragment
@@ -443,7 +493,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     if (!has_next) break;
     tile_barrier();  // this slice's patch, weight stages and statistics scratch are read
     if (last_slice && p.pro != nullptr && tid < CIN) aff[tid] = p.pro[imgn * CIN + tid];
-    store_w(0);
+    if constexpr (!WDMA) store_w(0);
     if (UPS && ksn == 1) {
       store_coarse();
       tile_barrier();  // the coarse block is in LDS

@@ -157,3 +157,32 @@ def test_ups_coarse_block_covers_every_fine_pixel(H, W):
                             r, c = yy - cy0, xx - cx0
                             assert 0 <= r < cr_n and 0 <= c < cc_n, (h0, w0, ih, iw, r, c)
                             assert held[(r, c)] == (yy, xx)
+
+
+@pytest.mark.parametrize("cin,cout", [(64, 64), (128, 64), (64, 128), (256, 128)])
+def test_weight_stage_lds_dma_matches_the_reads(cin, cout):
+    """WDMA (weights by global_load_lds_dwordx4, 16 B per lane at base + 16 lane): wave w's instruction i fills rows
+    (NWV w + i) * 8 .. + 7 with the per-lane SOURCE chunk (lane % 8) ^ (row & 6). Every LDS chunk is written once and
+    holds what the MFMA fragment read of swz<8> expects."""
+    nwv, kpad = cout // 32, 9 * cin
+    for tap in (0, 4, 8):
+        for ks in range(cin // 64):
+            lds = {}
+            for wave in range(4):
+                for i in range(nwv):
+                    base = (nwv * wave + i) * 1024
+                    for lane in range(64):
+                        r = (nwv * wave + i) * 8 + (lane >> 3)
+                        c = (lane & 7) ^ (r & 6)
+                        col = tap * cin + ks * 64 + 8 * c
+                        assert r < cout and col + 8 <= kpad
+                        off = base + 16 * lane
+                        assert off not in lds
+                        lds[off] = r * kpad + col
+            assert len(lds) == cout * 8
+            for lane in range(64):
+                for j in range(cout // 16):
+                    for s in range(2):
+                        n = 16 * j + (lane & 15)
+                        wc = 4 * s + (lane >> 4)
+                        assert lds[n * 128 + swz(n, wc)] == n * kpad + tap * cin + 64 * ks + 8 * wc
