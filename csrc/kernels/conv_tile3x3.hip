@@ -26,11 +26,11 @@
 #include "common.h"
 #include "conv_common.h"
 
-// Weight stages by LDS-DMA (global_load_lds_dwordx4) into THREE stage buffers, issued two stages ahead: no registers
-// hold weights in flight and each stage's weights get two stages of latency hiding; explicit counted vmcnt waits
-// (the instance with the UPS coarse block keeps the register path: a third buffer would not fit 80 KB).
+// Build switch: weight stages by LDS-DMA (global_load_lds_dwordx4) into THREE stage buffers, issued two stages ahead
+// (no registers hold weights in flight; explicit counted vmcnt waits; the UPS instance keeps the register path: a
+// third buffer would not fit 80 KB). Off: 2 % slower end to end than the register path (profiles/r4_k1t/wdma/).
 #ifndef AI4E_K1T_WDMA
-#define AI4E_K1T_WDMA 1
+#define AI4E_K1T_WDMA 0  // measured 2 % slower end to end (profiles/r4_k1t/wdma/): opt-in build switch
 #endif
 
 namespace {
