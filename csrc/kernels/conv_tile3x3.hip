@@ -221,19 +221,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       const bool in = (pmask >> k) & 1u;
       uint4 v = in ? pv[k] : make_uint4(0u, 0u, 0u, 0u);
       if (p.pro != nullptr && in) {  // padding stays zero: the conv pads the normalized tensor
+        // packed math per channel pair: one v_pk_fma_f32, one v_cvt_pk_bf16_f32 and (ReLU) one v_pk_max_i16 on the
+        // packed bf16 (relu(round(x)) == round(relu(x))), instead of two FMAs, two max and a pack
         uint32_t wds[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           float lo, hi;
           unpack_bf16x2(wds[q], lo, hi);
-          const float2 a0 = aff[64 * ks + 8 * c + 2 * q], a1 = aff[64 * ks + 8 * c + 2 * q + 1];
-          lo = lo * a0.x + a0.y;
-          hi = hi * a1.x + a1.y;
-          if (p.pro_relu) {
-            lo = fmaxf(lo, 0.f);
-            hi = fmaxf(hi, 0.f);
-          }
-          wds[q] = pack_bf16x2(lo, hi);
+          const float4 ab = *reinterpret_cast<const float4*>(aff + 64 * ks + 8 * c + 2 * q);  // (a0, b0, a1, b1)
+          const f32x2_t x2 = {lo, hi}, a2 = {ab.x, ab.z}, b2 = {ab.y, ab.w};
+          const f32x2_t y2 = __builtin_elementwise_fma(x2, a2, b2);
+          const uint32_t packed = __builtin_bit_cast(uint32_t, __builtin_convertvector(y2, bf16x2_t));
+          wds[q] = p.pro_relu ? relu_bf16x2(packed) : packed;
         }
         v = make_uint4(wds[0], wds[1], wds[2], wds[3]);
       }
