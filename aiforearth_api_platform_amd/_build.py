@@ -10,11 +10,15 @@ the GPU box (see README "Build"):
 * ``_lib/ai4e_ingestd`` / ``_lib/ai4e_http_load`` — the native ingest front-end and the REST load
   generator (``csrc/ingest/*.cpp``), g++ -O2.
 
-Rebuilds are incremental on source mtime.  ``python -m aiforearth_api_platform_amd._build``.
+Rebuilds are decided by CONTENT: every artefact has a ``<artefact>.sha`` manifest next to it holding the sha256 of
+its sources, headers, compiler and flags; an artefact whose manifest does not match what the tree would build now is
+rebuilt, whatever the file times say (a snapshot pushed to a GPU box never runs a stale library, and a fresh checkout
+with a matching manifest never rebuilds).  ``python -m aiforearth_api_platform_amd._build``.
 """
 from __future__ import annotations
 
 import concurrent.futures as cf
+import hashlib
 import os
 import shutil
 import subprocess
@@ -40,11 +44,30 @@ def _hipcc() -> str:
     raise RuntimeError("hipcc not found (ROCm toolchain required to build the gfx950 kernels)")
 
 
-def _stale(out: Path, deps) -> bool:
+def _digest(deps, cmd) -> str:
+    h = hashlib.sha256()
+    for part in cmd:
+        h.update(str(part).encode() + b"\0")
+    for d in sorted(map(str, deps)):
+        h.update(d.rsplit("/", 1)[-1].encode() + b"\0")
+        h.update(Path(d).read_bytes())
+    return h.hexdigest()
+
+
+def _manifest(out: Path) -> Path:
+    return out.with_name(out.name + ".sha")
+
+
+def _stale(out: Path, deps, cmd=()) -> bool:
+    """True unless ``out`` exists and its manifest holds the digest of ``deps`` + ``cmd`` (content, not mtime)."""
     if not out.exists():
         return True
-    t = out.stat().st_mtime
-    return any(Path(d).stat().st_mtime > t for d in deps)
+    m = _manifest(out)
+    return not m.exists() or m.read_text().strip() != _digest(deps, cmd)
+
+
+def _stamp(out: Path, deps, cmd=()) -> None:
+    _manifest(out).write_text(_digest(deps, cmd) + "\n")
 
 
 def _run(cmd, verbose):
@@ -59,18 +82,20 @@ def _run(cmd, verbose):
 def build_core(verbose: bool = False, force: bool = False) -> Path:
     src = sorted((CSRC / "core").glob("*.cpp"))
     headers = sorted((CSRC / "core").glob("*.h"))
-    if not force and not _stale(CORE_SO, [*src, *headers]):
+    cxx = os.environ.get("CXX", "g++")
+    extra = os.environ.get("AI4E_CORE_CXXFLAGS", "")  # e.g. "-fsanitize=thread -g" for the TSAN build
+    key = [cxx, "-O3", "-std=c++17", extra]
+    if not force and not _stale(CORE_SO, [*src, *headers], key):
         return CORE_SO
     import pybind11
 
-    cxx = os.environ.get("CXX", "g++")
     cmd = [cxx, "-O3", "-std=c++17", "-shared", "-fPIC", "-fvisibility=hidden", "-Wall",
            f"-I{sysconfig.get_paths()['include']}", f"-I{pybind11.get_include()}",
            *map(str, src), "-o", str(CORE_SO), "-lpthread"]
-    extra = os.environ.get("AI4E_CORE_CXXFLAGS")  # e.g. "-fsanitize=thread -g" for the TSAN build
     if extra:
         cmd[1:1] = extra.split()
     _run(cmd, verbose)
+    _stamp(CORE_SO, [*src, *headers], key)
     return CORE_SO
 
 
@@ -94,17 +119,21 @@ def build_kernels(verbose: bool = False, force: bool = False, jobs: int = 8, def
              "-mllvm", "-amdgpu-mfma-vgpr-form=1", "-Wno-unused-result", f"-I{CSRC / 'kernels'}",
              *[f"-D{d}" for d in defines]]
 
+    key = [hipcc, *flags]
+    if not force and not _stale(out_so, [*srcs, *headers], key):
+        return out_so  # the library matches the tree: no object is needed
+
     def one(src: Path) -> Path:
         obj = objdir / (src.stem + ".o")
-        if force or _stale(obj, [src, *headers]):
+        if force or _stale(obj, [src, *headers], key):
             _run([hipcc, *flags, "-c", str(src), "-o", str(obj)], verbose)
+            _stamp(obj, [src, *headers], key)
         return obj
 
     with cf.ThreadPoolExecutor(max_workers=max(1, min(jobs, len(srcs) or 1))) as ex:
         objs = list(ex.map(one, srcs))
-    if force or _stale(out_so, objs):
-        _run([hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs), "-o", str(out_so)],
-             verbose)
+    _run([hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs), "-o", str(out_so)], verbose)
+    _stamp(out_so, [*srcs, *headers], key)
     return out_so
 
 
@@ -118,10 +147,12 @@ def build_tools(verbose: bool = False, force: bool = False) -> None:
     cxx = os.environ.get("CXX", "g++")
     headers = sorted((CSRC / "core").glob("*.h"))
     for src, out in ((CSRC / "ingest" / "ingestd.cpp", INGESTD), (CSRC / "ingest" / "http_load.cpp", HTTP_LOAD)):
-        if force or _stale(out, [src, *headers]):
+        key = [cxx, "-O2"]
+        if force or _stale(out, [src, *headers], key):
             # OpenSSL (TLS termination in ai4e_ingestd, HTTPS load generation in ai4e_http_load)
             _run([cxx, "-O2", "-std=c++17", "-Wall", "-pthread", str(src), "-o", str(out), "-lrt", "-lssl", "-lcrypto"],
                  verbose)
+            _stamp(out, [src, *headers], key)
 
 
 def build_all(verbose: bool = False, force: bool = False) -> None:

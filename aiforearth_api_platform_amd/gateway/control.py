@@ -44,12 +44,16 @@ class ControlPlane:
         self._replayers: Dict[str, Callable[[str, Optional[str]], bool]] = {}
 
     # ------------------------------------------------------------------ queues
-    def queue_for(self, endpoint: str):
+    def queue_for(self, endpoint: str, shard: Optional[int] = None):
         """Queue per endpoint, named like the reference's Service Bus queue (CacheConnectorUpsert.cs:269-271).
 
         Queues are keyed by the endpoint *path* so ``http://host/v1/x`` and ``/v1/x`` share one queue.
+        ``shard``: the queue of one control-plane shard of a GPU-sharded endpoint (``<name>-s<k>``,
+        runtime/worker_pool.py ShardedWorkerPool).
         """
         key = queue_name_for_endpoint(APITask(Endpoint=endpoint).EndpointPath)
+        if shard is not None:
+            key = f"{key}-s{int(shard)}"
         with self._qmu:
             q = self._queues.get(key)
             if q is None:

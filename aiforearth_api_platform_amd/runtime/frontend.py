@@ -59,7 +59,18 @@ def frontend_main(index: int, host: str, port: int, internal_url: str, endpoints
     # the serving process owns the store and the rings: when its connection closes, this process has nothing
     # left to serve (and must not outlive it as an orphan holding the port)
     shards = {name: IngestShard(conns[name], e["endpoint"], e["shm"], e["nslots"], e["item_shape"], e["base"],
-                                e["len"], on_close=lambda: os._exit(0)) for name, e in endpoints.items()}
+                                e["len"], on_close=lambda: os._exit(0), digits=e.get("digits"))
+              for name, e in endpoints.items()}
+    # endpoint name -> its control-plane shards ("name", "name#1", ...: one per scheduler shard of a sharded pool)
+    groups: Dict[str, List[IngestShard]] = {}
+    for name in endpoints:
+        groups.setdefault(name.split("#", 1)[0], []).append(shards[name])
+    rr = [0]
+
+    def pick(group: List[IngestShard]) -> IngestShard:  # least-loaded partition, ties round-robin
+        rr[0] += 1
+        k = len(group)
+        return min((group[(rr[0] + i) % k] for i in range(k)), key=lambda sh: sh.slots.used() / max(1, sh.part_len))
     table = sorted(routes, key=lambda r: -len(r["prefix"]))
     state: Dict[str, object] = {"session": None, "draining": False}
     sec = security or {}
@@ -166,9 +177,9 @@ def frontend_main(index: int, host: str, port: int, internal_url: str, endpoints
             rej = auth.check(request.headers, request.query, r.get("keys") if r is not None else None)
             if rej is not None:
                 return web.json_response(rej[1], status=rej[0])
-        if (r is not None and r["mode"] == "async" and r.get("endpoint") in shards and request.method in ("POST", "PUT")
+        if (r is not None and r["mode"] == "async" and r.get("endpoint") in groups and request.method in ("POST", "PUT")
                 and not request.headers.get("taskId")):
-            return await ingest(request, r, shards[r["endpoint"]])
+            return await ingest(request, r, pick(groups[r["endpoint"]]))
         return await proxy(request)
 
     app = web.Application(client_max_size=1 << 30)
@@ -221,12 +232,15 @@ def spawn_frontends(n: int, pools: Dict[str, object], routes: List[dict], host: 
     for i in range(n):
         eps, conns = {}, {}
         for name, ep in pools.items():
-            base, length, rank = ep.worker.frontend_partitions[i]
-            parent, child = ctx.Pipe(duplex=True)
-            ep.worker.attach_ingest(rank, parent)
-            conns[name] = child
-            eps[name] = {"endpoint": ep.endpoint, "shm": ep.ring.name, "nslots": ep.ring.nslots,
-                         "item_shape": list(ep.item_shape), "base": base, "len": length}
+            for k, pool in enumerate(getattr(ep.worker, "control_shards", [ep.worker])):
+                base, length, rank = pool.frontend_partitions[i]
+                parent, child = ctx.Pipe(duplex=True)
+                pool.attach_ingest(rank, parent)
+                key = name if k == 0 else f"{name}#{k}"
+                conns[key] = child
+                eps[key] = {"endpoint": ep.endpoint, "shm": ep.ring.name, "nslots": ep.ring.nslots,
+                            "item_shape": list(ep.item_shape), "base": base, "len": length,
+                            "digits": pool.mint_digits() if hasattr(pool, "mint_digits") else None}
         p = ctx.Process(target=frontend_main, args=(i, host, port, internal_url, eps, routes, conns),
                         kwargs={"security": security}, daemon=True, name=f"ai4e-frontend-{i}")
         p.start()

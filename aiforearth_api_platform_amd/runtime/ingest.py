@@ -87,7 +87,7 @@ class IngestShard:
     :class:`StreamedBatch` expects of an endpoint."""
 
     def __init__(self, conn, endpoint: str, shm_name: str, nslots: int, item_shape: Sequence[int], base: int,
-                 length: int, on_close=None):
+                 length: int, on_close=None, digits: Optional[str] = None):
         from multiprocessing import shared_memory
 
         from ..store import native
@@ -107,6 +107,7 @@ class IngestShard:
         self._acks: Dict[int, object] = {}
         self._amu = threading.Lock()
         self._shard = itertools.count()
+        self._digits = digits or "01234567"  # the task-store lock domains of this scheduler shard
         self._on_close = on_close  # called once the scheduler connection is gone (the serving process exited)
         self._closing = False
         self.ring = self  # StreamedBatch's view of an endpoint
@@ -129,7 +130,7 @@ class IngestShard:
     # ---------------------------------------------------------------- tasks
     def mint_ids(self, n: int) -> List[str]:
         """uuid4 task ids whose last hex digit picks one store shard for the whole call (csrc task_store.h)."""
-        d = "%x" % (next(self._shard) % 8)
+        d = self._digits[next(self._shard) % len(self._digits)]
         return [str(uuid.uuid4())[:-1] + d for _ in range(n)]
 
     def submit_ids(self, slots: Sequence[int], ids: Sequence[str], trace: str = ""):

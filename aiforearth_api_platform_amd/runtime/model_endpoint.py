@@ -74,6 +74,10 @@ class ModelEndpoint:
         return tuple(self.ring.item_shape)
 
     # ------------------------------------------------------------- ingest
+    def _queue(self, slot: int):
+        """The dispatch queue that serves a payload in ``slot`` (a GPU-sharded pool: the owning shard's)."""
+        return self.worker.queue_for_slot(slot) if self.is_pool else self.queue
+
     def _enqueue(self, slots: List[int], trace: str = "") -> List[str]:
         if self.is_pool:
             return self.worker.submit_slots(slots, trace)
@@ -118,7 +122,7 @@ class ModelEndpoint:
                 self.cp.store.set_trace(tid, trace)
             if on_done is not None:
                 self._add_waiter(tid, on_done)
-            if not self.queue.send(tid, slot, ""):
+            if not self._queue(slot).send(tid, slot, ""):
                 self.ring.free([slot])
                 serialized, _ = self.cp.store.upsert(tid, PUBLISH_FAILED, STATE_FAILED, self.endpoint, None, True)
                 self._fire(tid)
@@ -196,7 +200,7 @@ class ModelEndpoint:
         slot = self.ring.alloc(1, timeout=30)[0]
         self._write([slot], arr[None])
         self.cp.store.upsert(task_id, "created - requeued after restart", STATE_CREATED, self.endpoint, None, True)
-        if not self.queue.send(task_id, slot, ""):
+        if not self._queue(slot).send(task_id, slot, ""):
             self.ring.free([slot])
             self.cp.store.upsert(task_id, PUBLISH_FAILED, STATE_FAILED, self.endpoint, None, True)
             return False

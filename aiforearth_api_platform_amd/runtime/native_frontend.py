@@ -70,8 +70,13 @@ def _token(v) -> str:
 
 def spawn_native_frontends(n: int, pools: Dict[str, object], routes: List[dict], host: str, port: int,
                            internal_url: str, security: Optional[dict] = None,
-                           ack_timeout_s: float = 30.0) -> List[NativeFrontend]:
-    """Start ``n`` native front-ends; arguments as :func:`runtime.frontend.spawn_frontends`."""
+                           ack_timeout_s: float = 30.0, max_queue_ms: float = 0.0) -> List[NativeFrontend]:
+    """Start ``n`` native front-ends; arguments as :func:`runtime.frontend.spawn_frontends`.
+
+    Each front-end attaches to every control-plane shard of every pool endpoint (one ``shard`` line per shard: its
+    ring partition, scheduler connection and the task-store digits its ids end in); a route lists its endpoint's
+    shards and the front-end picks the least-loaded one per request. ``max_queue_ms`` > 0: latency-budgeted
+    admission (429 + Retry-After once a request's projected queue wait exceeds the budget)."""
     import multiprocessing as mp
 
     if not n or not pools:
@@ -86,25 +91,32 @@ def spawn_native_frontends(n: int, pools: Dict[str, object], routes: List[dict],
     for i in range(n):
         lines = [f"listen {_token(host)} {int(port)}", f"internal {_token(ihost)} {int(iport)}",
                  f"ack_timeout {float(ack_timeout_s)}"]
+        if max_queue_ms and max_queue_ms > 0:
+            lines.append(f"max_queue_ms {float(max_queue_ms)}")
         lines += [f"key {_token(k)}" for k in sec.get("keys") or []]
         if sec.get("tls_cert"):
             lines.append(f"tls {_token(os.path.abspath(sec['tls_cert']))} {_token(os.path.abspath(sec['tls_key']))}")
         child_ends, fds = [], []
-        for si, name in enumerate(names):
+        shard_lines: Dict[str, List[int]] = {}  # endpoint name -> its shard line indices
+        for name in names:
             ep = pools[name]
-            base, length, rank = ep.worker.frontend_partitions[i]
-            parent, child = mp.Pipe(duplex=True)
-            ep.worker.attach_ingest(rank, parent)
-            child_ends.append(child)
-            fds.append(child.fileno())
-            item = 1
-            for v in ep.item_shape:
-                item *= int(v)
-            shape = "(" + ",".join(str(int(v)) for v in ep.item_shape) + ")"
-            lines.append(f"shard {si} {child.fileno()} {_token(ep.ring.name)} {int(ep.ring.nslots)} {item} "
-                         f"{int(base)} {int(length)} {_token(ep.endpoint)} {shape}")
+            for pool in getattr(ep.worker, "control_shards", [ep.worker]):
+                base, length, rank = pool.frontend_partitions[i]
+                parent, child = mp.Pipe(duplex=True)
+                pool.attach_ingest(rank, parent)
+                child_ends.append(child)
+                fds.append(child.fileno())
+                item = 1
+                for v in ep.item_shape:
+                    item *= int(v)
+                shape = "(" + ",".join(str(int(v)) for v in ep.item_shape) + ")"
+                si = sum(len(v) for v in shard_lines.values())
+                shard_lines.setdefault(name, []).append(si)
+                digits = pool.mint_digits() if hasattr(pool, "mint_digits") else "-"
+                lines.append(f"shard {si} {child.fileno()} {_token(ep.ring.name)} {int(ep.ring.nslots)} {item} "
+                             f"{int(base)} {int(length)} {_token(ep.endpoint)} {shape} {_token(digits)}")
         for r in routes:
-            si = names.index(r["endpoint"]) if r.get("endpoint") in pools else -1
+            si = ",".join(map(str, shard_lines[r["endpoint"]])) if r.get("endpoint") in pools else "-1"
             types = ",".join(_token(t) for t in r.get("content_types") or []) or "-"
             keys = ",".join(_token(k) for k in r.get("keys") or []) or "-"
             mc = r.get("max_concurrent")

@@ -90,6 +90,31 @@ class SharedPayloadRing:
             pass
 
 
+class RingPartition:
+    """One control-plane shard's view of a node ring shared by several shards: the same shared memory
+    (``name`` / ``nslots`` / ``buf``: workers address every slot by its global index) with its own native slot
+    allocator over ``[base, base + length)``."""
+
+    def __init__(self, ring: SharedPayloadRing, base: int, length: int):
+        self.parent = ring
+        self.nslots = ring.nslots
+        self.item_shape = ring.item_shape
+        self.buf = ring.buf
+        self.base, self.length = int(base), int(length)
+        self.slots = native.SlotRing(self.length, self.base)
+
+    @property
+    def name(self) -> str:
+        return self.parent.name
+
+    alloc = SharedPayloadRing.alloc
+    free = SharedPayloadRing.free
+    write = SharedPayloadRing.write
+
+    def close(self) -> None:  # (the owner of the shared memory closes it)
+        self.slots.close()
+
+
 class _WorkerHandle:
     def __init__(self, rank: int, device: str):
         self.rank = rank
@@ -125,12 +150,16 @@ class WorkerPool:
                  max_delay_s: float = 0.0005, heartbeat_interval_s: float = 0.5, heartbeat_timeout_s: float = 10.0,
                  max_restarts: int = 2, pipeline_depth: int = 3, retry_delay_s: float = 1.0,
                  remote_partitions: Sequence[Tuple[int, int, int]] = (), completion_feed: bool = False,
-                 poll_s: float = 0.02, frontends: int = 0, frontend_slots: int = 0):
+                 poll_s: float = 0.02, frontends: int = 0, frontend_slots: int = 0,
+                 shard: Optional["ShardLayout"] = None):
+        """``shard``: this pool is one control-plane shard of a :class:`ShardedWorkerPool` (its own dispatch queue
+        and scheduler, a partition of the shared ring, ids minted in its own task-store lock domains)."""
         if native is None:
             raise RuntimeError("the worker pool needs the native core (_ai4e_core)")
         self.cp = control_plane
         self.endpoint = endpoint
-        self.queue = control_plane.queue_for(endpoint)
+        self.shard = shard
+        self.queue = control_plane.queue_for(endpoint, shard=None if shard is None else shard.index)
         self.store = control_plane.store
         if not isinstance(self.store, native.TaskStore) or not isinstance(self.queue, native.DispatchQueue):
             raise RuntimeError("the worker pool needs the native store/queue backend (AI4E_STORE_BACKEND=native)")
@@ -142,21 +171,29 @@ class WorkerPool:
         # 3 batches in flight per worker: two overlap on the GPU's two compute streams while the third is
         # already copied in, so a finishing batch never leaves the GPU waiting for the next H2D
         # (ResNet-50 @250: 67.4-69.5k -> 75.7-77.7k images/s, p50 10.6 -> 9.1-9.4 ms; profiles/r2_pool/)
-        local = ring_slots or spec.max_batch * (pipeline_depth + 2) * max(1, len(self.devices))
         self.remote_partitions = [tuple(int(v) for v in p) for p in remote_partitions]  # (base, len, rank)
-        # ingest front-end processes (runtime/frontend.py): one ring partition each, after everything else
-        end = max([local] + [b + n for b, n, _ in self.remote_partitions])
-        fs = frontend_slots or spec.max_batch * 4
-        self.frontend_partitions = [(end + i * fs, fs, FRONTEND_RANK0 + i) for i in range(int(frontends))]
-        self.remote_partitions += self.frontend_partitions
-        total = max([local] + [b + n for b, n, _ in self.remote_partitions])
-        self.ring = SharedPayloadRing(total, spec.item_shape, local_slots=local)
+        if shard is not None:
+            self.frontend_partitions = list(shard.frontend_parts)
+            self.remote_partitions += self.frontend_partitions
+            self.ring = RingPartition(shard.ring, shard.local[0], shard.local[1])
+            total = shard.ring.nslots
+        else:
+            local = ring_slots or spec.max_batch * (pipeline_depth + 2) * max(1, len(self.devices))
+            # ingest front-end processes (runtime/frontend.py): one ring partition each, after everything else
+            end = max([local] + [b + n for b, n, _ in self.remote_partitions])
+            fs = frontend_slots or spec.max_batch * 4
+            self.frontend_partitions = [(end + i * fs, fs, FRONTEND_RANK0 + i) for i in range(int(frontends))]
+            self.remote_partitions += self.frontend_partitions
+            total = max([local] + [b + n for b, n, _ in self.remote_partitions])
+            self.ring = SharedPayloadRing(total, spec.item_shape, local_slots=local)
         self.hb_interval = heartbeat_interval_s
         self.max_restarts = max_restarts
         self.sched = native.NodeScheduler(self.store, self.queue, endpoint, total, max_batch=spec.max_batch,
                                           linger_s=max_delay_s, depth=pipeline_depth, retry_delay_s=retry_delay_s,
                                           hb_timeout_s=heartbeat_timeout_s, poll_s=poll_s)
         self.sched.add_local_ring(self.ring.slots)
+        if shard is not None:
+            self.sched.set_store_shards(list(shard.store_shards))
         if spec.stage_endpoints:
             self.sched.set_stage_endpoints(list(spec.stage_endpoints),
                                            ["running - stage %d" % (i + 2) for i in range(len(spec.stage_endpoints))])
@@ -363,6 +400,21 @@ class WorkerPool:
     def submit_slots(self, slots: Sequence[int], trace: str = "") -> List[str]:
         return self.sched.submit(list(slots), trace)
 
+    @property
+    def control_shards(self) -> List["WorkerPool"]:
+        """The scheduler shards behind this endpoint (ingest front-ends attach to each): just this pool."""
+        return [self]
+
+    def queue_for_slot(self, slot: int):
+        return self.queue
+
+    def mint_digits(self) -> str:
+        """Last hex digits the ids of this shard's tasks may end in: its task-store lock domains."""
+        if self.shard is None:
+            return "".join("%x" % d for d in range(min(16, max(1, self.store.nshards))))
+        n = self.store.nshards
+        return "".join("%x" % d for d in range(16) if d % n in set(self.shard.store_shards))
+
     def submit_many(self, images_u8: np.ndarray) -> List[str]:
         slots = self.ring.alloc(images_u8.shape[0], timeout=60)
         self.ring.write(slots, images_u8)
@@ -426,3 +478,248 @@ class WorkerPool:
         return {"workers": [dict(w.stats, device=w.device, restarts=w.restarts) for w in self.workers],
                 "batch_histogram": self.sched.batch_histogram(), "images": self.images,
                 "ring": {"slots": self.ring.nslots, "local_used": self.ring.slots.used()}}
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# Control plane sharded by GPU
+class ShardLayout:
+    """Where one control-plane shard lives: shard ``index``, its partition ``local`` = (base, length) of the node ring
+    ``ring`` (ingest from this process), the ring partitions of the ingest front-ends attached to it
+    (base, length, scheduler rank) and the task-store lock domains it mints ids in."""
+
+    def __init__(self, index: int, ring: SharedPayloadRing, local: Tuple[int, int],
+                 frontend_parts: Sequence[Tuple[int, int, int]], store_shards: Sequence[int]):
+        self.index, self.ring, self.local = int(index), ring, (int(local[0]), int(local[1]))
+        self.frontend_parts = [tuple(int(v) for v in p) for p in frontend_parts]
+        self.store_shards = [int(v) for v in store_shards]
+
+
+class _ShardedRing:
+    """The endpoint's view of the node ring across shards (what :class:`ModelEndpoint` and the decode pool use):
+    ``alloc`` picks the least-loaded shard with a live worker and returns global slot indices; ``free`` / ``write``
+    route by slot range; ``name`` / ``nslots`` / ``buf`` are the one shared memory segment."""
+
+    def __init__(self, ring: SharedPayloadRing, pools: Sequence["WorkerPool"]):
+        self.parent, self.pools = ring, list(pools)
+        self.nslots, self.item_shape, self.buf = ring.nslots, ring.item_shape, ring.buf
+        self._rr = 0
+        self._mu = threading.Lock()
+
+    @property
+    def name(self) -> str:
+        return self.parent.name
+
+    def pick(self) -> "WorkerPool":
+        with self._mu:
+            self._rr += 1
+            start = self._rr
+        k = len(self.pools)
+        order = [self.pools[(start + i) % k] for i in range(k)]
+        live = [p for p in order if p.active()] or order
+        return min(live, key=lambda p: p.ring.slots.used() / max(1, p.ring.length))
+
+    def owner(self, slot: int) -> "WorkerPool":
+        for p in self.pools:
+            if p.ring.base <= slot < p.ring.base + p.ring.length:
+                return p
+        raise ValueError(f"slot {slot} is not in any control-plane shard's local partition")
+
+    def alloc(self, n: int, timeout: Optional[float] = None) -> List[int]:
+        return self.pick().ring.alloc(n, timeout)
+
+    def free(self, slots: Sequence[int]) -> None:
+        for p, part in self._by_owner(slots):
+            p.ring.free(part)
+
+    def write(self, slots: Sequence[int], images_u8: np.ndarray) -> None:
+        self.parent.write(slots, images_u8)
+
+    def _by_owner(self, slots: Sequence[int]):
+        groups: Dict[int, Tuple["WorkerPool", List[int]]] = {}
+        for s in slots:
+            p = self.owner(int(s))
+            groups.setdefault(id(p), (p, []))[1].append(int(s))
+        return list(groups.values())
+
+
+class _QueueStats:
+    """Aggregated dispatch-queue statistics of the shards (the autoscaler's queue-depth input)."""
+
+    def __init__(self, pools: Sequence["WorkerPool"]):
+        self.pools = list(pools)
+
+    def stats(self) -> dict:
+        out: Dict[str, float] = {}
+        for p in self.pools:
+            for k, v in p.queue.stats().items():
+                if isinstance(v, (int, float)) and not isinstance(v, bool):
+                    out[k] = out.get(k, 0) + v
+        return out
+
+    def depth(self) -> int:
+        return sum(p.queue.depth() for p in self.pools)
+
+
+class ShardedWorkerPool:
+    """A pool-backed endpoint whose control plane scales with its GPUs: one scheduler shard per GPU (or worker
+    group), each with its own dispatch queue, node scheduler threads, partition of the node's payload ring and
+    task-store lock domains, behind the one gateway and the native front-ends.
+
+    The reference scales an API as HPA replicas (``APIs/Charts/templates/async-gpu/autoscaler.yaml:11-21``) behind
+    Istio's ROUND_ROBIN (``APIs/Charts/templates/routing.yml:26-28``); its single serial dispatch point
+    (``ProcessManager/BackendQueueProcessor/host.json:3-11``) is what this layout avoids: every task of an N-GPU
+    endpoint passes through the scheduler of ONE shard, and shards share nothing on the per-task path.
+
+    * ingest picks a shard per request: least-loaded by the shard's ring partition (the native front-ends
+      the same per front-end partition, ``csrc/ingest/ingestd.cpp`` ``pick_shard``);
+    * a task id's last hex digit names its task-store lock domain and so its shard, so status / result / trace
+      lookups go straight to one domain (no broadcast);
+    * queue-length and ``CURRENT_REQUESTS`` metrics aggregate over shards (the store's merged indexes,
+      :class:`_QueueStats`).
+    """
+
+    def __init__(self, control_plane, endpoint: str, spec: ModelSpec, devices: Sequence[str], shards: int = 0,
+                 ring_slots: int = 0, frontends: int = 0, frontend_slots: int = 0, pipeline_depth: int = 3,
+                 **kw):
+        self.cp, self.endpoint, self.spec = control_plane, endpoint, spec
+        self.devices = list(devices)
+        k = max(1, spec.group_size)
+        if len(self.devices) % k:
+            raise ValueError(f"{len(self.devices)} devices cannot form worker groups of {k}")
+        groups = [self.devices[i * k:(i + 1) * k] for i in range(len(self.devices) // k)]
+        K = max(1, min(int(shards or len(groups)), len(groups)))
+        nstore = control_plane.store.nshards
+        if K > 16:
+            raise ValueError("at most 16 control-plane shards (a task id's last hex digit names its shard)")
+        if K > nstore:
+            raise ValueError(f"{K} control-plane shards need a task store of >= {K} lock domains (has {nstore})")
+        shard_devs = [[d for g in groups[i::K] for d in g] for i in range(K)]
+        fs = frontend_slots or spec.max_batch * 4
+        layout, base = [], 0
+        for i in range(K):
+            n_local = ring_slots or spec.max_batch * (pipeline_depth + 2) * max(1, len(shard_devs[i]))
+            layout.append([(base, n_local)])
+            base += n_local
+        for i in range(K):
+            parts = []
+            for f in range(int(frontends)):
+                parts.append((base, fs, FRONTEND_RANK0 + f))
+                base += fs
+            layout[i].append(parts)
+        self._ring = SharedPayloadRing(base, spec.item_shape, local_slots=1)
+        self.pools: List[WorkerPool] = []
+        for i in range(K):
+            lay = ShardLayout(i, self._ring, layout[i][0], layout[i][1], [s for s in range(nstore) if s % K == i])
+            self.pools.append(WorkerPool(control_plane, endpoint, spec, shard_devs[i], pipeline_depth=pipeline_depth,
+                                         frontends=frontends, frontend_slots=fs, shard=lay, **kw))
+        self.ring = _ShardedRing(self._ring, self.pools)
+        self.queue = _QueueStats(self.pools)
+
+    # ------------------------------------------------------------ lifecycle
+    def start(self, wait_ready_s: float = 600.0) -> "ShardedWorkerPool":
+        for p in self.pools:  # spawn every shard's workers first, then wait for all of them together
+            p.start(wait_ready_s=0.0)
+        self.wait_ready(wait_ready_s)
+        return self
+
+    def wait_ready(self, timeout_s: float = 600.0, n: Optional[int] = None) -> bool:
+        deadline = time.time() + timeout_s
+        ok = True
+        for p in self.pools:
+            ok = p.wait_ready(max(0.0, deadline - time.time())) and ok
+        return ok
+
+    def stop(self) -> None:
+        for p in self.pools:
+            p.stop()
+        self._ring.close()
+
+    def active(self) -> int:
+        return sum(p.active() for p in self.pools)
+
+    def resize(self, n: int, devices: Optional[Sequence[str]] = None) -> None:
+        """Elastic: n workers spread over the shards, never below one per shard (a shard's queued tasks need one)."""
+        K = len(self.pools)
+        n = max(K, int(n))
+        for i, p in enumerate(self.pools):
+            p.resize(n // K + (1 if i < n % K else 0))
+
+    @property
+    def workers(self) -> list:
+        return [w for p in self.pools for w in p.workers]
+
+    @property
+    def events(self) -> list:
+        return sorted(e for p in self.pools for e in p.events)
+
+    @property
+    def control_shards(self) -> List[WorkerPool]:
+        return list(self.pools)
+
+    # ------------------------------------------------------------ ingest
+    def submit_slots(self, slots: Sequence[int], trace: str = "") -> List[str]:
+        ids: List[str] = []
+        for p, part in self.ring._by_owner(slots):
+            ids += p.submit_slots(part, trace)
+        return ids
+
+    def submit_many(self, images_u8: np.ndarray) -> List[str]:
+        p = self.ring.pick()
+        slots = p.ring.alloc(images_u8.shape[0], timeout=60)
+        p.ring.write(slots, images_u8)
+        return p.submit_slots(slots)
+
+    def queue_for_slot(self, slot: int):
+        return self.ring.owner(int(slot)).queue
+
+    def attach_ingest(self, rank: int, conn) -> None:
+        raise TypeError("attach ingest front-ends per control-plane shard (ShardedWorkerPool.control_shards)")
+
+    # ------------------------------------------------------------ completion feed / results / stats
+    def enable_completion_feed(self) -> None:
+        for p in self.pools:
+            p.enable_completion_feed()
+
+    def _owner_of(self, task_id: str) -> WorkerPool:
+        return self.pools[self.cp.store.shard_index(task_id) % len(self.pools)]
+
+    def add_waiter(self, task_id: str, cb: Callable[[str], None]) -> None:
+        self._owner_of(task_id).add_waiter(task_id, cb)
+
+    def pop_waiter(self, task_id: str) -> Optional[Callable[[str], None]]:
+        cb = self._owner_of(task_id).pop_waiter(task_id)
+        if cb is None:  # (a task created outside its shard's lock domains: the explicit-TaskId upsert path)
+            for p in self.pools:
+                cb = p.pop_waiter(task_id)
+                if cb is not None:
+                    break
+        return cb
+
+    def refresh(self) -> None:
+        for p in self.pools:
+            p.refresh()
+
+    @property
+    def describe(self) -> dict:
+        for p in self.pools:
+            if not p.describe:
+                p.refresh()
+            if p.describe:
+                return p.describe
+        return {}
+
+    def result(self, task_id: str) -> Optional[dict]:
+        return self._owner_of(task_id).result(task_id) if self.describe else None
+
+    @property
+    def images(self) -> int:
+        return sum(p.images for p in self.pools)
+
+    def stats(self) -> dict:
+        per = [p.stats() for p in self.pools]
+        hists = [s.get("batch_histogram") or [] for s in per]
+        return {"workers": [dict(w, shard=i) for i, s in enumerate(per) for w in s["workers"]],
+                "batch_histogram": [sum(h[i] for h in hists if i < len(h)) for i in range(max(map(len, hists)))],
+                "images": self.images, "control_plane_shards": len(self.pools),
+                "ring": {"slots": self._ring.nslots, "local_used": sum(s["ring"]["local_used"] for s in per)}}
+

@@ -73,7 +73,8 @@ def start_frontends(cfg: Config, doc: Dict[str, Any], endpoints: Dict[str, Any],
         from .runtime.native_frontend import spawn_native_frontends
 
         return spawn_native_frontends(frontend_count(cfg), pools, routes, cfg.host, port,
-                                      f"http://127.0.0.1:{internal_port}", security=security)
+                                      f"http://127.0.0.1:{internal_port}", security=security,
+                                      max_queue_ms=cfg.max_queue_ms)
     return spawn_frontends(frontend_count(cfg), pools, routes, cfg.host, port, f"http://127.0.0.1:{internal_port}",
                            security=security)
 
@@ -91,13 +92,23 @@ def _request_decoder(e: Dict[str, Any]):
                            int(kw.get("stride", 448)))
 
 
+def control_plane_shards(cfg: Config, e: Dict[str, Any], spec, devs) -> int:
+    """Scheduler shards of a pool endpoint: the YAML's ``control_plane_shards``, else the config's, where 0 means
+    one per GPU (worker group); stage-graph pools (several leaders per group) keep one scheduler."""
+    groups = max(1, len(devs) // max(1, spec.group_size))
+    if spec.group_leaders > 1 or spec.stage_endpoints:
+        return 1
+    n = int(e.get("control_plane_shards", cfg.control_plane_shards))
+    return max(1, min(groups, n if n > 0 else groups, 8))
+
+
 def build_platform(doc: Dict[str, Any], cfg: Config):
     """Build (control_plane, gateway, endpoints, dispatchers) from a platform YAML document."""
     from .runtime.engine import InferenceEngine, PayloadRing
     from .runtime.model_endpoint import ModelEndpoint
     from .runtime.servable import as_servable
     from .runtime.serving import GpuBatchWorker
-    from .runtime.worker_pool import ModelSpec, WorkerPool
+    from .runtime.worker_pool import ModelSpec, ShardedWorkerPool, WorkerPool
 
     cp = ControlPlane(cfg, AI4ELogger(level=logging.DEBUG if cfg.debug else logging.INFO))
     set_control_plane(cp)
@@ -113,11 +124,14 @@ def build_platform(doc: Dict[str, Any], cfg: Config):
             spec = ModelSpec(e["factory"], shape, mb, int(e.get("topk", 5)), dict(e.get("kwargs") or {}), graphs,
                              tuple(buckets), tuple(base_url + p for p in e.get("stage_paths", [])),
                              int(e.get("group_size", 1)), int(e.get("group_leaders", 1)))
-            pool = WorkerPool(cp, base_url + e["path"], spec, devs, max_delay_s=cfg.max_batch_delay_ms / 1e3,
-                              heartbeat_interval_s=cfg.heartbeat_interval_s,
-                              heartbeat_timeout_s=cfg.heartbeat_timeout_s,
-                              ring_slots=int(e.get("ring_slots", 0)), frontends=frontend_count(cfg),
-                              frontend_slots=int(e.get("frontend_ring_slots", cfg.frontend_ring_slots)))
+            kw = dict(max_delay_s=cfg.max_batch_delay_ms / 1e3, heartbeat_interval_s=cfg.heartbeat_interval_s,
+                      heartbeat_timeout_s=cfg.heartbeat_timeout_s, ring_slots=int(e.get("ring_slots", 0)),
+                      frontends=frontend_count(cfg),
+                      frontend_slots=int(e.get("frontend_ring_slots", cfg.frontend_ring_slots)))
+            nshards = control_plane_shards(cfg, e, spec, devs)
+            # the control plane scales with the GPUs: one scheduler shard per GPU (worker group) by default
+            pool = (ShardedWorkerPool(cp, base_url + e["path"], spec, devs, shards=nshards, **kw) if nshards > 1
+                    else WorkerPool(cp, base_url + e["path"], spec, devs, **kw))
             decode = _request_decoder(e)
             ep = ModelEndpoint(cp, e["path"], worker=pool, base_url=base_url, decode=decode,
                                decode_processes=0 if decode else int(e.get("decode_processes", cfg.decode_processes)))

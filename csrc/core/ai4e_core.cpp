@@ -71,6 +71,9 @@ PYBIND11_MODULE(_ai4e_core, m) {
            py::call_guard<py::gil_scoped_release>())
       .def("create_many", &TaskStore::create_many, py::arg("endpoint"), py::arg("n"), py::arg("status") = "created",
            py::arg("trace") = "", py::call_guard<py::gil_scoped_release>())
+      .def("create_many_in", &TaskStore::create_many_in, py::arg("shard"), py::arg("endpoint"), py::arg("n"),
+           py::arg("status") = "created", py::arg("trace") = "", py::call_guard<py::gil_scoped_release>())
+      .def("shard_index", &TaskStore::shard_index)
       .def("create_ids", &TaskStore::create_ids, py::arg("endpoint"), py::arg("ids"), py::arg("status") = "created",
            py::arg("trace") = "", py::call_guard<py::gil_scoped_release>())
       .def("transition_many", &TaskStore::transition_many, py::arg("ids"), py::arg("backend_status"),
@@ -271,6 +274,7 @@ PYBIND11_MODULE(_ai4e_core, m) {
       .def("add_local_ring", &NodeScheduler::add_local_ring)
       .def("add_remote_partition", &NodeScheduler::add_remote_partition)
       .def("set_stage_endpoints", &NodeScheduler::set_stage_endpoints)
+      .def("set_store_shards", &NodeScheduler::set_store_shards)
       .def("enable_completion_feed", &NodeScheduler::enable_completion_feed)
       .def("attach", &NodeScheduler::attach, py::arg("rank"), py::arg("fd"), py::arg("dispatch") = true,
            py::call_guard<py::gil_scoped_release>())

@@ -125,6 +125,12 @@ class NodeScheduler {
     std::lock_guard<std::mutex> g(feed_mu_);
     feed_on_ = on;
   }
+  // Control-plane shard: tasks this scheduler creates are minted in these task-store lock domains only
+  // (round-robin per batch). Empty (the default): any domain, the store's own round-robin.
+  void set_store_shards(std::vector<int> shards) {
+    std::lock_guard<std::mutex> g(mu_);
+    store_shards_ = std::move(shards);
+  }
 
   // Takes ownership of `fd` (a connected stream socket). dispatch=false: ingest-only connection.
   void attach(int rank, int fd, bool dispatch) {
@@ -390,7 +396,13 @@ class NodeScheduler {
   }
 
   std::vector<std::string> enqueue(const std::vector<int64_t>& slots, const std::string& trace) {
-    auto ids = store_->create_many(endpoint_, slots.size(), "created", trace);
+    int shard = -1;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      if (!store_shards_.empty()) shard = store_shards_[store_rr_++ % store_shards_.size()];
+    }
+    auto ids = shard < 0 ? store_->create_many(endpoint_, slots.size(), "created", trace)
+                         : store_->create_many_in(static_cast<size_t>(shard), endpoint_, slots.size(), "created", trace);
     const size_t sent = queue_->send_many(ids, slots);
     if (sent < ids.size()) {  // backpressure / closed: CacheConnectorUpsert.cs:181-199
       std::vector<std::string> rest(ids.begin() + static_cast<long>(sent), ids.end());
@@ -800,6 +812,8 @@ class NodeScheduler {
   std::vector<std::shared_ptr<SlotRing>> local_rings_;
   std::vector<RemotePart> remote_parts_;
   std::vector<std::string> stage_eps_, stage_status_;
+  std::vector<int> store_shards_;
+  size_t store_rr_ = 0;
   std::atomic<uint64_t> next_bid_{1};
   std::atomic<uint64_t> images_done_{0};
   std::mutex fail_mu_;

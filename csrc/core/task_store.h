@@ -642,6 +642,13 @@ class TaskStore {
                                        const std::string& trace = std::string()) {
     return next_shard().create_many(endpoint, n, status, trace);
   }
+  // The same in lock domain `shard` (mod nshards): a control-plane shard (one NodeScheduler per GPU) mints every id
+  // in the store shards it owns, so shards never contend on each other's locks and an id names its owner.
+  std::vector<std::string> create_many_in(size_t shard, const std::string& endpoint, size_t n, const std::string& status,
+                                          const std::string& trace = std::string()) {
+    return shards_[shard % nshards_]->create_many(endpoint, n, status, trace);
+  }
+  size_t shard_index(const std::string& id) const { return shard_of(id, nshards_); }
 
   std::vector<uint8_t> create_ids(const std::string& endpoint, const std::vector<std::string>& ids,
                                   const std::string& status, const std::string& trace = std::string()) {

@@ -41,6 +41,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cerrno>
+#include <cmath>
 #include <condition_variable>
 #include <cstdint>
 #include <cstdio>
@@ -163,6 +164,32 @@ struct Shard {
   std::atomic<uint64_t> token{1}, shard_ctr{0};
   std::mutex id_mu;
   ai4e::Uuid4 uuid;
+  // last hex digits the ids of this scheduler shard may end in (= the task-store lock domains it owns;
+  // default 0-7: any domain of the 8-way store)
+  std::string digits = "01234567";
+  // service rate of this partition (slots coming back FREE per second, EWMA over ~50 ms samples): the
+  // latency-budget admission projects a new request's queue wait as (slots in use + n) / rate
+  std::atomic<int64_t> freed{0};
+  std::mutex rate_mu;
+  double rate = 0.0, rate_t = 0.0;
+  int64_t rate_n = 0;
+
+  double service_rate() {
+    std::lock_guard<std::mutex> g(rate_mu);
+    const double t = ai4e::mono_now();
+    const int64_t n = freed.load();
+    if (rate_t == 0.0) {
+      rate_t = t;
+      rate_n = n;
+    } else if (t - rate_t >= 0.05) {
+      const double r = static_cast<double>(n - rate_n) / (t - rate_t);
+      // an idle partition (nothing in use) keeps its last rate: no traffic is not a slow GPU
+      if (n > rate_n || slots->used() > 0) rate = rate == 0.0 ? r : 0.7 * rate + 0.3 * r;
+      rate_t = t;
+      rate_n = n;
+    }
+    return rate;
+  }
 
   bool send_frame(const std::string& payload) {
     uint32_t be = htonl(static_cast<uint32_t>(payload.size()));
@@ -172,7 +199,8 @@ struct Shard {
 
   std::vector<std::string> mint(size_t n) {
     static const char* hx = "0123456789abcdef";
-    const char d = hx[shard_ctr.fetch_add(1) % 8];
+    (void)hx;
+    const char d = digits[shard_ctr.fetch_add(1) % digits.size()];
     std::vector<std::string> ids(n);
     std::lock_guard<std::mutex> g(id_mu);
     for (auto& s : ids) {
@@ -244,6 +272,7 @@ struct Shard {
         if (12 + 8ull * cnt <= len) {
           std::memcpy(s.data(), buf.data() + 12, 8ull * cnt);
           slots->free(s);
+          freed.fetch_add(cnt);
         }
       } else if (type == F_SUBMITTED && len >= 20) {  // u32 type, u64 token, u32 n, u32 pad
         uint64_t tok;
@@ -267,7 +296,8 @@ struct Shard {
 
 struct Route {
   std::string prefix, mode;
-  int shard = -1;
+  std::vector<int> shards;  // the endpoint's control-plane shards (one scheduler per GPU); empty: proxied
+  std::atomic<uint64_t> rr{0};
   int64_t max_content_length = 0, max_concurrent = -1;
   std::vector<std::string> content_types, keys;
   std::atomic<int64_t> inflight{0};
@@ -279,6 +309,7 @@ struct Config {
   std::string internal_host = "127.0.0.1";
   int internal_port = 0;
   double ack_timeout = 30.0, alloc_timeout = 60.0;
+  double max_queue_s = 0.0;  // latency budget of an ingested request's queue wait (0: no budget, wait for slots)
   std::vector<std::string> keys;
   std::vector<std::unique_ptr<Shard>> shards;
   std::vector<std::unique_ptr<Route>> routes;  // longest prefix first
@@ -326,10 +357,16 @@ void parse_config(const char* path) {
       ls >> g_cfg.ack_timeout;
     } else if (kw == "alloc_timeout") {
       ls >> g_cfg.alloc_timeout;
+    } else if (kw == "max_queue_ms") {
+      double ms = 0;
+      ls >> ms;
+      g_cfg.max_queue_s = ms / 1e3;
     } else if (kw == "shard") {
       auto s = std::make_unique<Shard>();
       std::string shm;
       ls >> s->idx >> s->fd >> shm >> s->nslots >> s->item >> s->base >> s->len >> s->endpoint >> s->shape_str;
+      std::string dg;
+      if (ls >> dg && !dg.empty() && dg != "-") s->digits = dg;
       s->endpoint_path = ai4e::absolute_path(s->endpoint);
       int mfd = shm_open(("/" + shm).c_str(), O_RDWR, 0);
       if (mfd < 0) {
@@ -347,8 +384,10 @@ void parse_config(const char* path) {
       g_cfg.shards.push_back(std::move(s));
     } else if (kw == "route") {
       auto r = std::make_unique<Route>();
-      std::string types, keys;
-      ls >> r->prefix >> r->mode >> r->shard >> r->max_content_length >> r->max_concurrent >> types >> keys;
+      std::string types, keys, shards;
+      ls >> r->prefix >> r->mode >> shards >> r->max_content_length >> r->max_concurrent >> types >> keys;
+      for (auto& v : split(shards, ','))
+        if (!v.empty() && std::atoi(v.c_str()) >= 0) r->shards.push_back(std::atoi(v.c_str()));
       if (types != "-")
         for (auto& t : split(types, ',')) r->content_types.push_back(t);
       if (keys != "-")
@@ -816,6 +855,22 @@ bool ingest(Conn& c, const Request& r, Route& route, Shard& s, bool batch) {
   if (n > s.len)
     return reject(413, "batch of " + std::to_string(n) + " items exceeds the ingest partition (" +
                            std::to_string(s.len) + " slots)");
+  if (g_cfg.max_queue_s > 0.0) {
+    // latency-budgeted admission (the reference's busy path: BackendQueueProcessor.cs:54-64 answers 429 and the
+    // message is retried later; ai4e_service.py:122-125): a request whose projected queue wait exceeds the budget is
+    // refused with 429 + Retry-After instead of queueing behind a deep ring
+    const double rate = s.service_rate();
+    const double wait = rate > 0.0 ? static_cast<double>(s.slots->used() + n) / rate : 0.0;
+    if (wait > g_cfg.max_queue_s) {
+      const double retry_s = std::max(0.001, wait - g_cfg.max_queue_s);
+      const std::string h = "Retry-After: " + std::to_string(static_cast<int>(std::ceil(retry_s))) +
+                            "\r\nx-ai4e-retry-after-ms: " + std::to_string(static_cast<int>(std::ceil(retry_s * 1e3))) +
+                            "\r\n";
+      if (lower(r.get("expect")) != "100-continue" && !c.discard(static_cast<size_t>(nbytes))) return false;
+      return respond(c, 429, "application/json", message_json("Service is busy, please try again later."),
+                     ka && lower(r.get("expect")) != "100-continue", h);
+    }
+  }
   if (lower(r.get("expect")) == "100-continue" && !c.send_all("HTTP/1.1 100 Continue\r\n\r\n", 25)) return false;
   std::vector<int64_t> sl = s.slots->alloc(n, g_cfg.alloc_timeout);
   if (sl.empty()) {  // no ring slot in time: nothing was created
@@ -857,6 +912,26 @@ bool ingest(Conn& c, const Request& r, Route& route, Shard& s, bool batch) {
       accept.find("*/*") != std::string::npos)
     return respond(c, created < 0 ? 202 : 200, "application/json", task_json(ids[0], s), ka, b3);
   return respond(c, created < 0 ? 202 : 200, "text/plain; charset=utf-8", "TaskId: " + ids[0], ka, b3);
+}
+
+// The control-plane shard of an endpoint that takes the next request: the one whose partition of this front-end has
+// the smallest share of its slots in use (least loaded), ties round-robin.
+Shard* pick_shard(Route& route) {
+  const size_t k = route.shards.size();
+  if (k == 0) return nullptr;
+  if (k == 1) return g_cfg.shards[static_cast<size_t>(route.shards[0])].get();
+  const size_t start = static_cast<size_t>(route.rr.fetch_add(1) % k);
+  Shard* best = nullptr;
+  double best_load = 2.0;
+  for (size_t i = 0; i < k; ++i) {
+    Shard* s = g_cfg.shards[static_cast<size_t>(route.shards[(start + i) % k])].get();
+    const double load = static_cast<double>(s->slots->used()) / static_cast<double>(std::max<int64_t>(1, s->len));
+    if (load < best_load) {
+      best_load = load;
+      best = s;
+    }
+  }
+  return best;
 }
 
 void serve_requests(Conn& c);
@@ -911,7 +986,7 @@ void serve_requests(Conn& c) {
     }
     bool ok;
     std::string ctype = lower(trim(split(r.get("content-type"), ';')[0]));
-    Shard* s = route && route->shard >= 0 ? g_cfg.shards[static_cast<size_t>(route->shard)].get() : nullptr;
+    Shard* s = route ? pick_shard(*route) : nullptr;
     const bool ingestible = s && route->mode == "async" && (r.method == "POST" || r.method == "PUT") &&
                             r.get("taskid").empty() && !r.chunked && r.content_length >= 0;
     if (ingestible && ctype == kBatchType && r.content_length > 0) {
