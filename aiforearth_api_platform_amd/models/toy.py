@@ -7,11 +7,16 @@ import torch
 class ChannelMeanClassifier:
     """logits[b] = [mean(channel 0..C-1), 0, 0, 0]: deterministic, cheap, device-agnostic."""
 
-    def __init__(self, device="cpu", extra_classes: int = 3):
+    def __init__(self, device="cpu", extra_classes: int = 3, delay_ms: float = 0.0):
         self.device = torch.device(device)
         self.extra = extra_classes
+        self.delay_s = float(delay_ms) / 1e3  # a slow "GPU" per batch (admission / overload tests)
 
     def __call__(self, x_u8: torch.Tensor) -> torch.Tensor:
+        if self.delay_s:
+            import time
+
+            time.sleep(self.delay_s)
         m = x_u8.float().mean(dim=(1, 2))
         return torch.cat([m, torch.zeros(m.shape[0], self.extra, device=m.device)], dim=1)
 

@@ -82,7 +82,7 @@ def run_clients(url: str, seconds: float, conc: int, body: bytes, content_type: 
 
 def run_native_clients(url: str, seconds: float, conc: int, body: bytes, content_type: str, procs: int = 2,
                        headers=()) -> dict:
-    """``procs`` C++ load processes x ``conc`` connections each. Returns {ids, t0, t1, errors, requests,
+    """``procs`` C++ load processes x ``conc`` connections each. Returns {ids, t0, t1, errors, busy, requests,
     bytes_sent, client_cpu_s (user + system, all client processes), client_processes, connections}."""
     import json
     import os
@@ -106,7 +106,7 @@ def run_native_clients(url: str, seconds: float, conc: int, body: bytes, content
                content_type, body_path, str(conc), str(seconds), f"{start_at:.6f}", os.path.join(tmp, f"ids{i}.txt"),
                *headers]
         ps.append(subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
-    out = {"ids": [], "t0": float("inf"), "t1": 0.0, "errors": 0, "requests": 0, "bytes_sent": 0.0,
+    out = {"ids": [], "t0": float("inf"), "t1": 0.0, "errors": 0, "busy": 0, "requests": 0, "bytes_sent": 0.0,
            "client_cpu_s": 0.0, "client_processes": procs, "connections": procs * conc}
     for i, p in enumerate(ps):
         try:
@@ -120,6 +120,7 @@ def run_native_clients(url: str, seconds: float, conc: int, body: bytes, content
         st = json.loads(so.strip().splitlines()[-1])
         out["t0"], out["t1"] = min(out["t0"], st["t0"]), max(out["t1"], st["t1"])
         out["errors"] += st["errors"]
+        out["busy"] += st.get("busy", 0)  # 429 answers of the latency-budgeted admission (retried by the client)
         out["requests"] += st["requests"]
         out["bytes_sent"] += st["bytes_sent"]
         out["client_cpu_s"] += st["cpu_user_s"] + st["cpu_sys_s"]

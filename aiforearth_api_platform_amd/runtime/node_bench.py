@@ -59,14 +59,15 @@ class Client:
 
 
 def http_phase(cp, pool, seconds: float, batch: int, item_shape, path: str, frontends: int = 0,
-               tls: bool = False) -> dict:
+               tls: bool = False, max_queue_ms: float = 0.0) -> dict:
     """REST ingest on this node: aiohttp gateway (this process) + binary batch route (streamed into the
     payload ring), then single-image requests. ``frontends``: ingest front-end processes sharing the port
     (native C++ ``ai4e_ingestd`` by default, AI4E_FRONTEND_IMPL=python for runtime/frontend.py; the pool needs
     as many partitions). Load: the C++ generator (runtime/http_load.py ``run_native_clients``) in separate
     processes; the record carries the client and server CPU seconds, so a reader can see which side was
     the ceiling. ``tls``: the front-ends terminate TLS (OpenSSL in ``ai4e_ingestd``, the test certificate under
-    tests/fixtures) and every client connection is an HTTPS session."""
+    tests/fixtures) and every client connection is an HTTPS session. ``max_queue_ms`` > 0: the front-ends' latency-
+    budgeted admission (429 + Retry-After past the budget; the load generator backs off and retries)."""
     import asyncio
 
     from aiohttp import web
@@ -118,8 +119,10 @@ def http_phase(cp, pool, seconds: float, batch: int, item_shape, path: str, fron
         fx = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))), "tests",
                           "fixtures")
         sec = {"tls_cert": os.path.join(fx, "tls_test_cert.pem"), "tls_key": os.path.join(fx, "tls_test_key.pem")}
+    kw = {"max_queue_ms": max_queue_ms} if impl == "native" and max_queue_ms > 0 else {}
     fe = spawn(frontends, {"bench": ep}, [{"prefix": "/v1/bench/async", "mode": "async", "endpoint": "bench"}],
-               "127.0.0.1", port, f"http://127.0.0.1:{socks[1].getsockname()[1]}", security=sec) if frontends else []
+               "127.0.0.1", port, f"http://127.0.0.1:{socks[1].getsockname()[1]}", security=sec, **kw) \
+        if frontends else []
     if fe:
         time.sleep(5.0 if impl != "native" else 1.0)  # they start and bind the shared port
     url = f"{'https' if tls else 'http'}://127.0.0.1:{port}/v1/bench/async"
@@ -168,7 +171,8 @@ def http_phase(cp, pool, seconds: float, batch: int, item_shape, path: str, fron
         out[name] = {"images": len(ids), "images_per_s": round(len(ids) / dt, 1), "connections": procs * conc,
                      "client_processes": procs, "client": "c++ ai4e_http_load" if native else "python aiohttp",
                      "ingest_frontends": len(fe), "frontend_impl": impl if fe else None, "errors": errors,
-                     "scheme": "https" if tls else "http",
+                     "scheme": "https" if tls else "http", "max_queue_ms": max_queue_ms if fe else None,
+                     "busy_429": res.get("busy") if res else None,
                      "p50_task_latency_ms": round(percentile(lat, 50) * 1e3, 3),
                      "p99_task_latency_ms": round(percentile(lat, 99) * 1e3, 3),
                      "server_cpu_s": round(server_cpu() - c0, 3), "window_s": round(dt, 3)}
@@ -378,14 +382,15 @@ def run_node_bench(args, spec, path: str, metric: str, unit: str = "images/s", c
                 http = http_phase(cp, pool, args.http_seconds, B, spec.item_shape, path)
                 nfe = getattr(args, "http_frontends", 0)
                 if nfe:
-                    http["with_frontends"] = http_phase(cp, pool, args.http_seconds, B, spec.item_shape, path, nfe)
+                    http["with_frontends"] = http_phase(cp, pool, args.http_seconds, B, spec.item_shape, path, nfe,
+                                                        max_queue_ms=getattr(args, "max_queue_ms", 0.0))
             except Exception as e:  # the headline number stands on its own
                 http = {"error": repr(e)}
             nfe = getattr(args, "http_frontends", 0)
             if getattr(args, "http_tls", 0) and nfe and isinstance(http, dict) and "error" not in http:
                 try:
                     http["with_frontends_tls"] = http_phase(cp, pool, args.http_seconds, B, spec.item_shape, path,
-                                                            nfe, tls=True)
+                                                            nfe, tls=True, max_queue_ms=getattr(args, "max_queue_ms", 0.0))
                 except Exception as e:
                     http["with_frontends_tls"] = {"error": repr(e)}
         workers = [{k: w.get(k) for k in ("rank", "images", "batches", "pinned", "hbm_used", "gpu_busy_ms", "gfx_mhz",

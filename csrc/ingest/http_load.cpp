@@ -10,7 +10,8 @@
 // HOST = "tls:ADDR" speaks HTTPS (TLS 1.2+, OpenSSL, no certificate verification: a load generator against the
 // platform's own front door); each request is then one SSL_write of the prebuilt head + body.
 //
-// Prints one JSON line: requests, ok, errors, t0, t1 (epoch s), bytes_sent, cpu_user_s, cpu_sys_s.
+// Prints one JSON line: requests, ok, errors, busy (429s, retried after the server's Retry-After), t0, t1 (epoch s),
+// bytes_sent, cpu_user_s, cpu_sys_s.
 // IDS_OUT receives one task id per line (TaskId / TaskIds of every 2xx answer).
 #include <arpa/inet.h>
 #include <netinet/in.h>
@@ -20,6 +21,7 @@
 #include <sys/uio.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <atomic>
 #include <cerrno>
 #include <chrono>
@@ -66,7 +68,7 @@ double now() {
 }
 
 struct Result {
-  long requests = 0, ok = 0, errors = 0;
+  long requests = 0, ok = 0, errors = 0, busy = 0;
   double bytes = 0;
   std::vector<std::string> ids;
 };
@@ -91,7 +93,7 @@ bool send_all(int fd, const struct iovec* iov0, int cnt) {
 }
 
 // Reads one response; returns the status (0 on a broken connection) and its body.
-int read_response(Link& l, std::string& buf, std::string& body) {
+int read_response(Link& l, std::string& buf, std::string& body, double* retry_ms = nullptr) {
   size_t hend;
   while ((hend = buf.find("\r\n\r\n")) == std::string::npos) {
     char tmp[65536];
@@ -105,6 +107,15 @@ int read_response(Link& l, std::string& buf, std::string& body) {
   for (auto& ch : head) ch = static_cast<char>(std::tolower(static_cast<unsigned char>(ch)));
   auto p = head.find("content-length:");
   if (p != std::string::npos) clen = std::strtoull(head.c_str() + p + 15, nullptr, 10);
+  if (retry_ms) {  // 429: the server's projected wait (x-ai4e-retry-after-ms, else Retry-After seconds)
+    *retry_ms = 0;
+    auto q = head.find("x-ai4e-retry-after-ms:");
+    if (q != std::string::npos) {
+      *retry_ms = std::atof(head.c_str() + q + 22);
+    } else if ((q = head.find("retry-after:")) != std::string::npos) {
+      *retry_ms = 1e3 * std::atof(head.c_str() + q + 12);
+    }
+  }
   while (buf.size() < hend + 4 + clen) {
     char tmp[65536];
     ssize_t k = l.recv_some(tmp, sizeof(tmp));
@@ -232,7 +243,8 @@ int main(int argc, char** argv) {
         }
         ++r.requests;
         r.bytes += static_cast<double>(head.size() + body.size());
-        int st = read_response(l, buf, rbody);
+        double retry_ms = 0;
+        int st = read_response(l, buf, rbody, &retry_ms);
         if (st == 0) {
           l.close();
           buf.clear();
@@ -243,6 +255,10 @@ int main(int argc, char** argv) {
         if (st >= 200 && st < 300) {
           ++r.ok;
           extract_ids(rbody, r.ids);
+        } else if (st == 429) {  // admission refused: back off for the server's projected wait, then retry
+          ++r.busy;
+          const double ms = std::min(1000.0, std::max(0.5, retry_ms));
+          std::this_thread::sleep_for(std::chrono::microseconds(static_cast<long>(ms * 1e3)));
         } else {
           ++r.errors;
         }
@@ -258,6 +274,7 @@ int main(int argc, char** argv) {
     tot.requests += r.requests;
     tot.ok += r.ok;
     tot.errors += r.errors;
+    tot.busy += r.busy;
     tot.bytes += r.bytes;
     if (f)
       for (auto& id : r.ids) std::fprintf(f, "%s\n", id.c_str());
@@ -266,9 +283,9 @@ int main(int argc, char** argv) {
   struct rusage ru {};
   getrusage(RUSAGE_SELF, &ru);
   std::printf(
-      "{\"requests\": %ld, \"ok\": %ld, \"errors\": %ld, \"t0\": %.6f, \"t1\": %.6f, \"bytes_sent\": %.0f, "
+      "{\"requests\": %ld, \"ok\": %ld, \"errors\": %ld, \"busy\": %ld, \"t0\": %.6f, \"t1\": %.6f, \"bytes_sent\": %.0f, "
       "\"cpu_user_s\": %.3f, \"cpu_sys_s\": %.3f, \"connections\": %d}\n",
-      tot.requests, tot.ok, tot.errors, t0, t1, tot.bytes, ru.ru_utime.tv_sec + ru.ru_utime.tv_usec * 1e-6,
+      tot.requests, tot.ok, tot.errors, tot.busy, t0, t1, tot.bytes, ru.ru_utime.tv_sec + ru.ru_utime.tv_usec * 1e-6,
       ru.ru_stime.tv_sec + ru.ru_stime.tv_usec * 1e-6, conns);
   return 0;
 }

@@ -95,7 +95,7 @@ __device__ __forceinline__ uint4 relu8(const f32x4_t& a, const f32x4_t& b) {
 #ifndef AI4E_CHAIN_STAMPS
 #define AI4E_CHAIN_STAMPS 0
 #endif
-constexpr int CHAIN_NSEG = 4, CHAIN_MAXW = 65536;
+constexpr int CHAIN_NSEG = 5, CHAIN_MAXW = 65536;
 #if AI4E_CHAIN_STAMPS
 __device__ unsigned long long g_chain_stamps[CHAIN_MAXW * CHAIN_NSEG];
 #define CHAIN_STAMP(k)                                                             \
@@ -258,7 +258,7 @@ void conv_chain_kernel(const ChainParams p) {
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
 #if AI4E_CHAIN_STAMPS
-  unsigned long long ch_sum[CHAIN_NSEG] = {0, 0, 0, 0}, ch_last;
+  unsigned long long ch_sum[CHAIN_NSEG] = {0, 0, 0, 0, 0}, ch_last;
   asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(ch_last)::"memory");
 #endif
   const int wm = wave % WM;
@@ -382,6 +382,7 @@ void conv_chain_kernel(const ChainParams p) {
       for (int j = 0; j < CF; ++j) wr[s][j] = *reinterpret_cast<const bf16x8_t*>(wp + j * 16L * p.kpad2 + s * 32);
     wait_vmcnt<0>();  // the patch landed (the weight loads above retire with it)
     lds_barrier();
+    CHAIN_STAMP(4);  // patch DMA issue + wait (patch mode; its time is also inside segment 0 of ring mode)
     bf16x8_t fx[2][PFI];
     int soff[PFI], sws[PFI];
     auto tap_slots = [&](int t) __attribute__((always_inline)) {

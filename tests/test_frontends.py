@@ -4,6 +4,7 @@ land on the serving process or on a front-end (SO_REUSEPORT), every task complet
 task API (proxied to the serving process), batch ingest and sync routes work through any listener; admission
 (keys, content type, length) answers the same whichever process accepts the connection."""
 import json
+import socket
 import os
 import subprocess
 import sys
@@ -411,3 +412,83 @@ def test_bench_http_phase_over_tls():
     for name in ("batch_route", "single_image_route"):
         r = out[name]
         assert r["scheme"] == "https" and r["errors"] == 0 and r["images"] > 0, r
+
+
+def test_latency_budget_admission_429_no_lost_tasks():
+    """Overload a slow worker (20 ms per batch of <= 8) through one native front-end with a 40 ms queue budget:
+    requests past the budget are answered 429 + Retry-After (the reference's busy path, BackendQueueProcessor.cs:54-64)
+    instead of queueing behind the ring, the load generator backs off and retries, every accepted task completes, and
+    the accepted tasks' queue-to-done latency stays near the budget rather than at the depth of the ring partition."""
+    from aiforearth_api_platform_amd.config import Config
+    from aiforearth_api_platform_amd.gateway.control import ControlPlane
+    from aiforearth_api_platform_amd.gateway.server import Gateway, RouteTable
+    from aiforearth_api_platform_amd.runtime import native_frontend
+    from aiforearth_api_platform_amd.runtime.frontend import open_listeners
+    from aiforearth_api_platform_amd.runtime.http_load import run_native_clients
+    from aiforearth_api_platform_amd.runtime.model_endpoint import ModelEndpoint
+    from aiforearth_api_platform_amd.runtime.worker_pool import ModelSpec, WorkerPool
+    from aiforearth_api_platform_amd.utils.metrics import percentile
+
+    if not native_frontend.available():
+        pytest.skip("ai4e_ingestd not buildable here")
+    import asyncio
+    import threading
+
+    from aiohttp import web
+
+    shape = (4, 4, 3)
+    spec = ModelSpec("aiforearth_api_platform_amd.models.toy:tiny_classifier", shape, max_batch=8, topk=2,
+                     kwargs={"delay_ms": 20.0}, use_graphs=False)
+    cp = ControlPlane(Config.load(env={}))
+    path = "/v1/adm/classify"
+    pool = WorkerPool(cp, "http://127.0.0.1" + path, spec, ["cpu"], max_delay_s=0.001, frontends=1,
+                      frontend_slots=128).start(120)
+    ep = ModelEndpoint(cp, path, worker=pool)
+    gw = Gateway(cp, RouteTable())
+    s0 = socket.socket()
+    s0.bind(("127.0.0.1", 0))
+    port = s0.getsockname()[1]
+    s0.close()
+    socks = open_listeners("127.0.0.1", port, shared=True)
+    box = {}
+
+    def serve():
+        loop = asyncio.new_event_loop()
+        asyncio.set_event_loop(loop)
+        runner = web.AppRunner(gw.app, access_log=None)
+        loop.run_until_complete(runner.setup())
+        loop.run_until_complete(web.SockSite(runner, socks[1]).start())  # (the internal listener only)
+        box["loop"] = loop
+        loop.run_forever()
+
+    th = threading.Thread(target=serve, daemon=True)
+    th.start()
+    socks[0].close()  # only the front-end answers on the public port
+    fe = native_frontend.spawn_native_frontends(
+        1, {"adm": ep}, [{"prefix": "/v1/adm/async", "mode": "async", "endpoint": "adm"}], "127.0.0.1", port,
+        f"http://127.0.0.1:{socks[1].getsockname()[1]}", max_queue_ms=40.0)
+    try:
+        time.sleep(1.0)
+        img = np.zeros(shape, np.uint8).tobytes()
+        res = run_native_clients(f"http://127.0.0.1:{port}/v1/adm/async", 3.0, 16, img, "application/octet-stream",
+                                 procs=1)
+        assert res["busy"] > 0, res  # overload was refused, not queued
+        assert res["errors"] == 0, res
+        ids = res["ids"]
+        assert len(ids) > 50
+        deadline = time.time() + 60
+        while time.time() < deadline and len(cp.store.latencies(ids)) < len(ids):
+            time.sleep(0.05)
+        lat = cp.store.latencies(ids)
+        assert len(lat) == len(ids)  # no accepted task was lost
+        # the 128-slot partition would hold ~16 batches = 320 ms of queue at 20 ms per batch of 8
+        assert percentile(sorted(lat), 50) < 0.15, percentile(sorted(lat), 50)
+    finally:
+        for p in fe:
+            p.terminate()
+        for p in fe:
+            p.join(10)
+        if "loop" in box:
+            box["loop"].call_soon_threadsafe(box["loop"].stop)
+        pool.stop()
+        cp.close()

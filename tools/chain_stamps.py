@@ -21,16 +21,17 @@ from aiforearth_api_platform_amd.ops import _ext  # noqa: E402
 from aiforearth_api_platform_amd.ops.pool import preprocess_s2d_u8  # noqa: E402
 
 NAMES = ["phase A (3x3 main loop)", "B/C weight prologue + T2 epilogue", "passes (B, residual + Y epilogue, C)",
-         "T1' epilogue + copy-out (stores drained)"]
+         "T1' epilogue + copy-out (stores drained)", "phase A patch DMA + wait (patch mode)"]
 
 
 def read(nwaves):
-    buf = np.zeros(65536 * 4, np.uint64)
+    buf = np.zeros(65536 * 5, np.uint64)
     _ext.call("ai4e_chain_stamps_read", buf.ctypes.data_as(ctypes.c_void_p))
-    w = buf.reshape(-1, 4)[:nwaves].astype(np.float64)
+    w = buf.reshape(-1, 5)[:nwaves].astype(np.float64)
     tot = w.sum(0)
     return {"waves": int(nwaves), "cycles_per_wave_mean": round(float(w.sum(1).mean()), 1),
-            "shares": {n: round(float(v / tot.sum()), 4) for n, v in zip(NAMES, tot)}}
+            "shares": {n: round(float(v / tot.sum()), 4) for n, v in zip(NAMES, tot)},
+            "cycles_per_wave": {n: round(float(v / max(1, nwaves)), 1) for n, v in zip(NAMES, tot)}}
 
 
 def main():
