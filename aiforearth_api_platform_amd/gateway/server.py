@@ -78,10 +78,12 @@ class Route:
 class RouteTable:
     def __init__(self, routes: Optional[List[Route]] = None):
         self.routes: List[Route] = list(routes or [])
+        self.version = 0  # bumped on every change (the gateway's precomputed key sets follow it)
 
     def add(self, route: Route) -> Route:
         self.routes.append(route)
         self.routes.sort(key=lambda r: -len(r.prefix))  # longest prefix wins
+        self.version += 1
         return route
 
     def match(self, path: str) -> Optional[Route]:
@@ -143,11 +145,18 @@ class Gateway:
     CONTROL_PATHS = ("/v1/cache/upsert", "/v1/cache/get", "/v1/requests/upsert", "/v1/requests/get",
                      "/v1/backend/webhook", "/metrics", "/v1/platform/stats")
 
-    def _route_keys(self) -> List[str]:
-        keys: List[str] = []
-        for r in self.routes.routes:
-            keys += list(r.keys or [])
-        return keys
+    def _key_sets(self):
+        """(control keys, control + every route's keys, protected?) — computed once per route-table version and
+        control-key setting instead of on every request."""
+        control = getattr(self.cp.cfg, "control_keys", "")
+        tag = (self.routes.version, len(self.routes.routes), control, tuple(self.auth.global_keys))
+        if getattr(self, "_keys_tag", None) != tag:
+            control_keys = parse_keys(control)
+            route_keys = [k for r in self.routes.routes for k in (r.keys or [])]
+            self._keys = (control_keys, control_keys + route_keys,
+                          bool(self.auth.global_keys or control_keys or route_keys))
+            self._keys_tag = tag
+        return self._keys
 
     @web.middleware
     async def _key_middleware(self, request, handler):
@@ -155,16 +164,19 @@ class Gateway:
         any key is configured anywhere, the task-management routes accept the global keys, the control keys and
         any route's keys (every subscriber polls its tasks), and the control routes only the global and control
         keys (no key at all opens them then: they are the reference's key-protected Function endpoints). Health
-        and the OpenAPI document are open."""
+        and the OpenAPI document are open.
+
+        Task scope is intentionally the APIM product's, not the route's: the reference publishes its TaskManagement
+        API beside the model APIs for every subscriber (InfrastructureDeployment/deploy_api_management.sh:58-100, APIManagement/task_management_api_body.json),
+        so a subscriber with any route's key may poll a task by id, and the id (uuid4, 122 random bits, never listed)
+        is the capability. Route-scoped task reads would need the creating route's key set recorded on the task."""
         path = request.path
         if path not in self.OPEN_PATHS:
-            control_keys = parse_keys(getattr(self.cp.cfg, "control_keys", ""))
-            route_keys = self._route_keys()
-            protected = bool(self.auth.global_keys or control_keys or route_keys)
+            control_keys, task_keys, protected = self._key_sets()
             if path in self.CONTROL_PATHS:
                 rej = self.auth.check(request.headers, request.query, control_keys, locked=protected)
             elif path.startswith(self.TASK_PREFIX):
-                rej = self.auth.check(request.headers, request.query, control_keys + route_keys, locked=protected)
+                rej = self.auth.check(request.headers, request.query, task_keys, locked=protected)
             else:
                 route = self.routes.match(path)
                 rej = self.auth.check(request.headers, request.query, route.keys if route is not None else None)

@@ -24,8 +24,8 @@ import torch.nn as nn
 
 from ..ops.conv import PackedConv, conv2d_nhwc, linear_nhwc, pack_conv
 from ..ops.debug import crumb
-from ..ops.detection import (argsort_desc_rows, det_decode, nms_batched_sorted, roi_align_fpn, rpn_decode_into,
-                              rpn_topk)
+from ..ops.detection import (det_decode, gather_keep, nms_batched_sorted, roi_align_fpn, rpn_decode_into, rpn_topk,
+                              sort_select)
 from ..ops.pool import maxpool2d_nhwc, preprocess_s2d_u8, preprocess_u8
 from .resnet import FusedResNet, resnet50
 
@@ -94,6 +94,18 @@ class FasterRCNN:
         # box-head FCs on K1 (the 256x256 tile, tuned per batch in conv_tiles.json); AI4E_DET_FC_BLAS=1: hipBLASLt
         self.fc_blas = os.environ.get("AI4E_DET_FC_BLAS", "0") not in ("0", "off", "")
 
+    def sort_rows(self, img_hw: Tuple[int, int]) -> Dict[str, int]:
+        """Row lengths of the two NMS-stage sorts at an input size: the all-level proposal sort (sum of the per-level
+        pre-NMS top-k) and the detections' sort (post-NMS proposals x foreground classes). Both must fit the HIP row
+        sort (ops.detection.ROW_SORT_MAX) for a graph-captured forward (tests/test_detector_cpu.py pins the defaults)."""
+        cfg = self.cfg
+        A = len(cfg.aspect_ratios)
+        h, w = img_hw
+        rpn = 0
+        for s in (4, 8, 16, 32, 64):  # P2..P6
+            rpn += min(cfg.pre_nms_top_n, -(-h // s) * -(-w // s) * A)
+        return {"rpn": rpn, "detections": cfg.post_nms_top_n * (cfg.num_classes - 1)}
+
     # ------------------------------------------------------------------ backbone + FPN
     def backbone_stages(self, x: torch.Tensor) -> List[torch.Tensor]:
         """C2..C5 of the ResNet-50 backbone: fused stem + max-pool (K1s) and the bottleneck chains (K1c)."""
@@ -153,18 +165,12 @@ class FasterRCNN:
             crumb(f"rpn.topk{li}", idx)
             rpn_decode_into(head, idx, anchors[li], A, boxes, scores, lvl, off, li, img_hw, cfg.rpn_min_size)
             off += k
-        # batched NMS across levels via coordinate offsets; invalid (small) boxes sort last
-        order = argsort_desc_rows(scores)
-        boxes_s = torch.gather(boxes, 1, order[..., None].expand_as(boxes))
-        scores_s = torch.gather(scores, 1, order)
-        off = torch.gather(lvl, 1, order)[..., None] * (max(img_hw) + 1.0)
-        valid = (scores_s >= 0).sum(1).to(torch.int32)
-        keep, count = nms_batched_sorted(boxes_s + off, cfg.rpn_nms_thresh, cfg.post_nms_top_n, valid)
+        # batched NMS across levels via coordinate offsets; invalid (small) boxes sort last. Sort, gathers, level
+        # offsets and the valid count in one launch (sort_select), the kept rows in another (gather_keep)
+        _, boxes_s, boxes_off, _, valid = sort_select(scores, boxes, max(img_hw) + 1.0, groups=lvl)
+        keep, count = nms_batched_sorted(boxes_off, cfg.rpn_nms_thresh, cfg.post_nms_top_n, valid)
         crumb("rpn.nms", keep)
-        keep_l = keep.clamp(min=0).long()
-        props = torch.gather(boxes_s, 1, keep_l[..., None].expand(B, keep.shape[1], 4))
-        pad = (keep < 0)[..., None]
-        props = props.masked_fill(pad, 0.0)
+        props, _, _ = gather_keep(keep, boxes=boxes_s)
         return props, count
 
     # ------------------------------------------------------------------ box head + postprocess
@@ -184,22 +190,15 @@ class FasterRCNN:
 
     def postprocess(self, props, count, pred, img_hw):
         cfg = self.cfg
-        B = props.shape[0]
         # softmax (background dropped) + per-class decode + clip + validity mask: one HIP launch
-        boxes, scores, labels = det_decode(pred, props, count, cfg.num_classes, cfg.box_reg_weights, img_hw,
-                                           cfg.box_score_thresh)
-        order = scores.argsort(1, descending=True)
-        s_s = torch.gather(scores, 1, order)
-        b_s = torch.gather(boxes, 1, order[..., None].expand_as(boxes))
-        l_s = torch.gather(labels, 1, order)
-        valid = (s_s >= 0).sum(1).to(torch.int32)
-        off = l_s[..., None].float() * (max(img_hw) + 1.0)
-        keep, ndet = nms_batched_sorted(b_s + off, cfg.box_nms_thresh, cfg.detections_per_img, valid)
+        boxes, scores, _ = det_decode(pred, props, count, cfg.num_classes, cfg.box_reg_weights, img_hw,
+                                      cfg.box_score_thresh)
+        # class label of entry j of the [R, nc - 1] layout = j % (nc - 1) + 1: per-class NMS by label offsets
+        s_s, b_s, b_off, l_s, valid = sort_select(scores, boxes, max(img_hw) + 1.0, group_mod=cfg.num_classes - 1,
+                                                  want_labels=True)
+        keep, ndet = nms_batched_sorted(b_off, cfg.box_nms_thresh, cfg.detections_per_img, valid)
         crumb("post.nms", keep)
-        k = keep.clamp(min=0).long()
-        det_boxes = torch.gather(b_s, 1, k[..., None].expand(B, k.shape[1], 4))
-        det_scores = torch.gather(s_s, 1, k)
-        det_labels = torch.gather(l_s, 1, k)
+        det_boxes, det_scores, det_labels = gather_keep(keep, boxes=b_s, scores=s_s, labels=l_s)
         return det_boxes, det_scores, det_labels, ndet
 
     # ------------------------------------------------------------------ forward

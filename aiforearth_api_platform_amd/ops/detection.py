@@ -75,24 +75,102 @@ def rpn_decode_into(head: torch.Tensor, idx: torch.Tensor, anchors: torch.Tensor
     lvl[:, off:off + k] = float(level)
 
 
+ROW_SORT_MAX = 8192  # longest row the HIP sorts take (one workgroup's LDS bitonic network, csrc detection.hip)
+
+
+def _graph_safe_fallback(what: str, t: torch.Tensor) -> None:
+    """A library fallback (multi-kernel sort with temporaries) must never be captured into a HIP graph: replaying it
+    after other allocations came and went faulted the GPU (profiles/r4_replay/). Refuse loudly instead."""
+    if t.is_cuda and torch.cuda.is_current_stream_capturing():
+        raise RuntimeError(f"{what}: shape {tuple(t.shape)} exceeds the HIP kernel's limit (rows <= {ROW_SORT_MAX}); "
+                           "its library fallback is not graph-safe — run this configuration without HIP graphs")
+
+
 def argsort_desc_rows(scores: torch.Tensor) -> torch.Tensor:
     """``scores.argsort(1, descending=True)`` for fp32 [B, N] rows; HIP (N <= 8192): one workgroup per row, a bitonic
     network in LDS, ties in index order (deterministic), no library temporaries (graph-safe, profiles/r4_replay/)."""
     B, N = scores.shape
-    if _ext.backend_for(scores) == "hip" and scores.dtype == torch.float32 and N <= 8192:
+    if _ext.backend_for(scores) == "hip" and scores.dtype == torch.float32 and N <= ROW_SORT_MAX:
         s = scores.contiguous()
         order = torch.empty(B, N, dtype=torch.long, device=scores.device)
         _ext.call("ai4e_row_sort_desc", s.data_ptr(), B, N, order.data_ptr(), _ext.stream_ptr(scores.device))
         return order
+    _graph_safe_fallback("argsort_desc_rows", scores)
     return scores.argsort(dim=1, descending=True, stable=True)
+
+
+def sort_select(scores: torch.Tensor, boxes: torch.Tensor, scale: float, groups: Optional[torch.Tensor] = None,
+                group_mod: int = 0, want_labels: bool = False):
+    """One NMS stage's sort + select: rows of fp32 ``scores`` [B, N] sorted descending (ties: lower index first) with
+    their ``boxes`` [B, N, 4]; each box also offset by ``group * scale`` (batched NMS of several groups at once by
+    coordinate offsets), the group being ``groups`` [B, N] (fp32, e.g. the FPN level) or, without it, the index's
+    ``index % group_mod + 1`` (the class label of det_decode's [R, nc - 1] layout).
+
+    Returns (scores_s [B, N], boxes_s [B, N, 4], boxes_off [B, N, 4], groups_s [B, N] fp32 or labels [B, N] int64 with
+    ``want_labels``, valid [B] int32 = entries with score >= 0). HIP (N <= 8192): one launch (sort_select_kernel)."""
+    B, N = scores.shape
+    dev = scores.device
+    if _ext.backend_for(scores) == "hip" and N <= ROW_SORT_MAX:
+        sc = scores.float().contiguous()
+        bx = boxes.float().contiguous()
+        g = None if groups is None else groups.float().contiguous()
+        s_s = torch.empty(B, N, dtype=torch.float32, device=dev)
+        b_s = torch.empty(B, N, 4, dtype=torch.float32, device=dev)
+        b_o = torch.empty(B, N, 4, dtype=torch.float32, device=dev)
+        g_s = None if want_labels else torch.empty(B, N, dtype=torch.float32, device=dev)
+        lab = torch.empty(B, N, dtype=torch.int64, device=dev) if want_labels else None
+        valid = torch.empty(B, dtype=torch.int32, device=dev)
+        _ext.call("ai4e_sort_select", sc.data_ptr(), bx.data_ptr(), _ext.ptr(g), int(group_mod), float(scale), B, N,
+                  s_s.data_ptr(), b_s.data_ptr(), b_o.data_ptr(), _ext.ptr(g_s), _ext.ptr(lab), valid.data_ptr(),
+                  _ext.stream_ptr(dev))
+        return s_s, b_s, b_o, (lab if want_labels else g_s), valid
+    _graph_safe_fallback("sort_select", scores)
+    order = scores.float().argsort(dim=1, descending=True, stable=True)
+    s_s = torch.gather(scores.float(), 1, order)
+    b_s = torch.gather(boxes.float(), 1, order[..., None].expand(B, N, 4))
+    if groups is not None:
+        g_s = torch.gather(groups.float(), 1, order)
+    else:
+        g_s = (order % int(group_mod) + 1).float()
+    b_o = b_s + (g_s * float(scale))[..., None]
+    valid = (s_s >= 0).sum(1).to(torch.int32)
+    return s_s, b_s, b_o, (g_s.long() if want_labels else g_s), valid
+
+
+def gather_keep(keep: torch.Tensor, boxes: Optional[torch.Tensor] = None, scores: Optional[torch.Tensor] = None,
+                labels: Optional[torch.Tensor] = None):
+    """Rows kept by NMS (``keep`` [B, K] int32, -1 = padding): (boxes [B, K, 4], scores [B, K], labels [B, K]) gathered
+    from [B, N, ...] sources (None where the source is None), zero at padding. HIP: one launch (gather_keep_kernel)."""
+    B, K = keep.shape
+    src = next(t for t in (boxes, scores, labels) if t is not None)
+    N = src.shape[1]
+    dev = keep.device
+    if _ext.backend_for(keep) == "hip":
+        kp = keep.to(torch.int32).contiguous()
+        bs = None if boxes is None else boxes.float().contiguous()
+        ss = None if scores is None else scores.float().contiguous()
+        ls = None if labels is None else labels.long().contiguous()
+        bo = None if bs is None else torch.empty(B, K, 4, dtype=torch.float32, device=dev)
+        so = None if ss is None else torch.empty(B, K, dtype=torch.float32, device=dev)
+        lo = None if ls is None else torch.empty(B, K, dtype=torch.int64, device=dev)
+        _ext.call("ai4e_gather_keep", kp.data_ptr(), B, K, N, _ext.ptr(bs), _ext.ptr(ss), _ext.ptr(ls), _ext.ptr(bo),
+                  _ext.ptr(so), _ext.ptr(lo), _ext.stream_ptr(dev))
+        return bo, so, lo
+    k = keep.clamp(min=0).long()
+    pad = keep < 0
+    bo = None if boxes is None else torch.gather(boxes.float(), 1, k[..., None].expand(B, K, 4)).masked_fill(
+        pad[..., None], 0.0)
+    so = None if scores is None else torch.gather(scores.float(), 1, k).masked_fill(pad, 0.0)
+    lo = None if labels is None else torch.gather(labels.long(), 1, k).masked_fill(pad, 0)
+    return bo, so, lo
 
 
 def rpn_topk(head: torch.Tensor, num_anchors: int, k: int) -> torch.Tensor:
     """Flat indices ``pos * A + a`` [B, k] (int64) of the k largest objectness logits of one FPN level, read straight
     from the RPN head bf16 [B, h, w, >= A] (channels 0..A-1). HIP: one workgroup per image, radix select, a fixed
     deterministic output order (the proposals are re-sorted by score across levels afterwards) and graph-safe (no
-    library temporaries: torch.topk's multi-block path faulted replaying in a graph, profiles/r4_replay/).
-    Elsewhere: torch.topk (value order)."""
+    library temporaries: torch.topk's multi-block path faulted replaying in a graph, profiles/r4_replay/). Ties of
+    the k-th value are taken lowest index first on every backend (elsewhere: a stable descending sort's first k)."""
     B = head.shape[0]
     hw = head.shape[1] * head.shape[2]
     if k > hw * num_anchors:
@@ -102,7 +180,8 @@ def rpn_topk(head: torch.Tensor, num_anchors: int, k: int) -> torch.Tensor:
         _ext.call("ai4e_rpn_topk", head.data_ptr(), B, hw, head.shape[-1], num_anchors, k, idx.data_ptr(),
                   _ext.stream_ptr(head.device))
         return idx
-    return head[..., :num_anchors].reshape(B, -1).topk(k, dim=1)[1]
+    # the k largest by (value desc, index asc): the same SET as the HIP kernel's (ties by lowest flat index)
+    return head[..., :num_anchors].reshape(B, -1).float().argsort(dim=1, descending=True, stable=True)[:, :k]
 
 
 def det_decode(pred: torch.Tensor, props: torch.Tensor, count: torch.Tensor, num_classes: int,

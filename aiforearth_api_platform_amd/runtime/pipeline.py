@@ -160,7 +160,10 @@ class _GraphRunner:
             g = self.graphs[key] = (graph, static_in, static_out)
         graph, static_in, static_out = g
         # stream-ordered: back-to-back replays need no host sync (the round-3/4 replay fault was the library's
-        # multi-block top-k inside the detector graph, now rpn_topk; profiles/r4_replay/, tests/test_graph_replay_gpu.py)
+        # multi-block top-k inside the detector graph, now rpn_topk; profiles/r4_replay/, tests/test_graph_replay_gpu.py).
+        # Every sort in the captured forward is a HIP row sort (rpn_topk, sort_select); a shape past their limit makes
+        # the capture itself raise (ops.detection._graph_safe_fallback) instead of capturing a library sort, so no
+        # graph reaching this replay holds library temporaries (tests/test_detector_cpu.py pins the default shapes)
         static_in.copy_(x)
         graph.replay()
         return static_out

@@ -30,10 +30,14 @@ class TelemetrySampler:
     * items of one task are kept or dropped together (the decision hashes the task id against the ratio, App
       Insights' per-operation sampling), so a kept task's log lines stay complete; items without a task id are
       sampled by a deterministic counter;
-    * within an interval at most twice the interval's budget is kept (a sudden burst is cut before the next
-      re-estimate; the one place a task can lose some of its lines);
+    * within an interval at most twice the interval's budget of SAMPLED items is kept (a sudden burst is cut before
+      the next re-estimate; the one place a task can lose some of its lines);
     * ERROR items are always kept (rare, and the ones an operator needs; a deviation from App Insights, which would
-      sample exceptions too) but count toward the offered rate;
+      sample exceptions too): they count toward the offered rate but not toward the burst cap, so an error burst does
+      not starve the INFO / WARN lines of the same tasks;
+    * sampling applies to the EXPORTED stream only (the telemetry sink, here the JSON lines on the stream); the
+      service's own recent-records ring (``AI4ELogger.records``, /v1/platform/logs) stays complete, as App Insights
+      sampling never touches the application's local view;
     * every emitted item carries ``sample_rate`` = 1 / ratio (App Insights' itemCount) so counts can be re-weighted.
     """
 
@@ -63,8 +67,9 @@ class TelemetrySampler:
             self._n += 1
             self.seen += 1
             if always:
-                ok = True
-            elif self._k >= 2.0 * self.max_per_s * self.interval_s:
+                self.kept += 1
+                return True
+            if self._k >= 2.0 * self.max_per_s * self.interval_s:
                 ok = False
             elif self.ratio >= 1.0:
                 ok = True
@@ -101,17 +106,18 @@ class AI4ELogger:
         self.sampler = TelemetrySampler(getattr(cfg, "telemetry_max_per_s", 50.0))
 
     def _emit(self, level: str, msg: str, uri: str = "", task_id: str = "", **extra: Any) -> None:
-        if not self.sampler.keep(task_id, always=level in ("ERROR", "CRITICAL")):
-            return
         rec = {"ts": time.time(), "level": level, "message": msg, **self.fields, "uri": uri,
                "task_id": task_id, **extra}
-        if self.sampler.ratio < 1.0:
-            rec["sample_rate"] = round(1.0 / self.sampler.ratio, 3)
-        self.records.append(rec)
+        self.records.append(rec)  # the local view is complete: sampling is an export decision
         if len(self.records) > self._keep:
             del self.records[: len(self.records) - self._keep]
-        if logging.getLevelName(level) >= self.level and self.stream is not None:
-            self.stream.write(json.dumps(rec, default=str) + "\n")
+        if logging.getLevelName(level) < self.level or self.stream is None:
+            return
+        if not self.sampler.keep(task_id, always=level in ("ERROR", "CRITICAL")):
+            return
+        if self.sampler.ratio < 1.0:
+            rec = dict(rec, sample_rate=round(1.0 / self.sampler.ratio, 3))
+        self.stream.write(json.dumps(rec, default=str) + "\n")
 
     def log_debug(self, msg: str, uri: str = "", task_id: str = "", **kw) -> None:
         self._emit("DEBUG", msg, uri, task_id, **kw)

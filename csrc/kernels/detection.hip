@@ -151,9 +151,14 @@ __global__ __launch_bounds__(256) void rpn_decode_kernel(const uint16_t* __restr
 // HIP graph once other allocations have come and gone between replays: bench/replay_repro.py, profiles/r4_replay/).
 // One 1024-thread workgroup per image reads the A objectness logits per pixel straight from the RPN head (bf16
 // [B, HW, ldh]) and selects the k largest by a two-pass 8-bit radix select on order-preserving 16-bit keys (LDS
-// histograms; NaN above +inf, as torch.topk). Output: the k flat indices pos * A + a (int64, [B, k]) of every key above
-// the k-th largest plus as many of the k-th key's ties as fill k, in a fixed (thread, step) order: deterministic,
-// no global atomics, every write inside [0, k) by construction (the host guarantees k <= HW * A).
+// histograms; NaN above +inf, as torch.topk). Ties of the k-th largest key are taken lowest flat index first, so the
+// selected SET is the k largest by (value desc, index asc), the same set as a stable descending sort's first k
+// (ops/detection.py's CPU path). Output: the k flat indices pos * A + a (int64, [B, k]): every key above the k-th in
+// index order, then the taken ties in index order — deterministic, no global atomics, every write inside [0, k) by
+// construction (the host guarantees k <= HW * A).
+// Histogram updates are run-length coalesced per thread (a thread adds its count for a bin once per run of equal bins
+// instead of once per element): the RPN logits of a level crowd into a few high-byte bins, and one LDS atomic per
+// element serialized those lanes (68.8 % bank conflicts, profiles/r4h_det/pmc_by_kernel.txt).
 constexpr int TOPK_THREADS = 1024;
 
 __device__ __forceinline__ uint32_t bf16_order_key(uint16_t v) {
@@ -176,7 +181,19 @@ __global__ __launch_bounds__(TOPK_THREADS) void rpn_topk_kernel(const uint16_t* 
   // pass 1: histogram of the high byte
   if (t < 256) hist[t] = 0;
   __syncthreads();
-  for (int e = t; e < n; e += TOPK_THREADS) atomicAdd(&hist[key_at(e) >> 8], 1);
+  {
+    int cur = -1, cnt = 0;
+    for (int e = t; e < n; e += TOPK_THREADS) {
+      const int bin = static_cast<int>(key_at(e) >> 8);
+      if (bin != cur) {
+        if (cnt) atomicAdd(&hist[cur], cnt);
+        cur = bin;
+        cnt = 0;
+      }
+      ++cnt;
+    }
+    if (cnt) atomicAdd(&hist[cur], cnt);
+  }
   __syncthreads();
   if (t == 0) {
     int cum = 0, d = 255;
@@ -189,9 +206,20 @@ __global__ __launch_bounds__(TOPK_THREADS) void rpn_topk_kernel(const uint16_t* 
   // pass 2: histogram of the low byte among the keys with that high byte
   if (t < 256) hist[t] = 0;
   __syncthreads();
-  for (int e = t; e < n; e += TOPK_THREADS) {
-    const uint32_t kk = key_at(e);
-    if ((kk >> 8) == hi) atomicAdd(&hist[kk & 255u], 1);
+  {
+    int cur = -1, cnt = 0;
+    for (int e = t; e < n; e += TOPK_THREADS) {
+      const uint32_t kk = key_at(e);
+      if ((kk >> 8) != hi) continue;
+      const int bin = static_cast<int>(kk & 255u);
+      if (bin != cur) {
+        if (cnt) atomicAdd(&hist[cur], cnt);
+        cur = bin;
+        cnt = 0;
+      }
+      ++cnt;
+    }
+    if (cnt) atomicAdd(&hist[cur], cnt);
   }
   __syncthreads();
   if (t == 0) {
@@ -203,9 +231,12 @@ __global__ __launch_bounds__(TOPK_THREADS) void rpn_topk_kernel(const uint16_t* 
   __syncthreads();
   const uint32_t T = (hi << 8) | static_cast<uint32_t>(sel[1]);
   const int gt = sel[2], need = k - gt;  // keys above T; ties of T to take
-  // pass 3: per-thread counts, exclusive scans, then the writes
+  // pass 3: thread t owns the contiguous index range [e0, e1) (index order across threads), per-thread counts,
+  // exclusive scans, then the writes
+  const int chunk = (n + TOPK_THREADS - 1) / TOPK_THREADS;
+  const int e0 = min(n, t * chunk), e1 = min(n, e0 + chunk);
   int cg = 0, ce = 0;
-  for (int e = t; e < n; e += TOPK_THREADS) {
+  for (int e = e0; e < e1; ++e) {
     const uint32_t kk = key_at(e);
     cg += kk > T;
     ce += kk == T;
@@ -222,7 +253,7 @@ __global__ __launch_bounds__(TOPK_THREADS) void rpn_topk_kernel(const uint16_t* 
   }
   int og = sg[t] - cg, oe = se[t] - ce;
   long* const out = idx + static_cast<long>(b) * k;
-  for (int e = t; e < n; e += TOPK_THREADS) {
+  for (int e = e0; e < e1; ++e) {
     const uint32_t kk = key_at(e);
     if (kk > T) {
       out[og++] = e;
@@ -269,6 +300,79 @@ __global__ __launch_bounds__(ROWSORT_THREADS) void row_sort_desc_kernel(const fl
   }
   long* const o = order + static_cast<long>(blockIdx.x) * N;
   for (int i = t; i < N; i += ROWSORT_THREADS) o[i] = static_cast<long>(0xffffffffu - static_cast<uint32_t>(key[i]));
+}
+
+// Sort + select of one NMS stage (the proposals' all-level sort, the detections' per-class sort), one 1024-thread
+// workgroup per row: the row's scores are sorted descending in LDS (the bitonic network of row_sort_desc_kernel, ties by
+// lower index), then the same workgroup gathers the sorted scores and boxes, the boxes offset by their group
+// (group * scale: batched NMS across FPN levels / classes by coordinate offsets), the sorted group values and the
+// number of valid entries (score >= 0; invalid ones carry -1 and sort last). Groups come from `grp` (fp32, e.g. the
+// FPN level) or, with grp null, from the index: group = index % grp_mod + 1 (the detections' class label, as laid out
+// by det_decode_kernel). Replaces argsort (a library radix sort over 4 K+ keys, not graph-safe) + four gathers + a
+// sum-reduction + the offset arithmetic: ~10 library launches per NMS stage.
+__global__ __launch_bounds__(ROWSORT_THREADS) void sort_select_kernel(
+    const float* __restrict__ scores, const float4* __restrict__ boxes, const float* __restrict__ grp, int grp_mod,
+    float scale, int N, int P, float* __restrict__ s_out, float4* __restrict__ b_out, float4* __restrict__ boff_out,
+    float* __restrict__ g_out, long* __restrict__ lab_out, int* __restrict__ valid) {
+  __shared__ unsigned long long key[ROWSORT_MAX];
+  __shared__ int nvalid;
+  const int t = threadIdx.x;
+  const long row = blockIdx.x;
+  const float* const sr = scores + row * N;
+  if (t == 0) nvalid = 0;
+  for (int i = t; i < P; i += ROWSORT_THREADS)
+    key[i] = i < N ? (static_cast<unsigned long long>(f32_order_key(sr[i])) << 32) | (0xffffffffu - static_cast<uint32_t>(i))
+                   : 0ull;
+  __syncthreads();
+  for (int k = 2; k <= P; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = t; i < P; i += ROWSORT_THREADS) {
+        const int l = i ^ j;
+        if (l > i) {
+          const unsigned long long a = key[i], c = key[l];
+          if (((i & k) == 0) ? (a < c) : (a > c)) {
+            key[i] = c;
+            key[l] = a;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  int mine = 0;
+  for (int i = t; i < N; i += ROWSORT_THREADS) {
+    const int src = static_cast<int>(0xffffffffu - static_cast<uint32_t>(key[i]));
+    const float sc = sr[src];
+    const float4 bx = boxes[row * N + src];
+    const float g = grp ? grp[row * N + src] : static_cast<float>(src % grp_mod + 1);
+    const float o = g * scale;
+    s_out[row * N + i] = sc;
+    b_out[row * N + i] = bx;
+    boff_out[row * N + i] = make_float4(bx.x + o, bx.y + o, bx.z + o, bx.w + o);
+    if (g_out) g_out[row * N + i] = g;
+    if (lab_out) lab_out[row * N + i] = static_cast<long>(g);
+    mine += sc >= 0.f;
+  }
+  if (mine) atomicAdd(&nvalid, mine);
+  __syncthreads();
+  if (t == 0) valid[row] = nvalid;
+}
+
+// Rows kept by NMS: out[b, j] = src[b, keep[b, j]] for boxes (float4), scores and labels (each optional), zero where
+// keep is -1 (padding past the image's count). Replaces clamp + three gathers + masked_fill.
+__global__ __launch_bounds__(256) void gather_keep_kernel(const int* __restrict__ keep, int K, int N,
+                                                          const float4* __restrict__ bsrc, const float* __restrict__ ssrc,
+                                                          const long* __restrict__ lsrc, float4* __restrict__ bout,
+                                                          float* __restrict__ sout, long* __restrict__ lout, int total) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const long b = i / K;
+  const int k = keep[i];
+  const bool ok = k >= 0 && k < N;
+  const long src = b * N + (ok ? k : 0);
+  if (bout) bout[i] = ok ? bsrc[src] : make_float4(0.f, 0.f, 0.f, 0.f);
+  if (sout) sout[i] = ok ? ssrc[src] : 0.f;
+  if (lout) lout[i] = ok ? lsrc[src] : 0;
 }
 
 // Box-head postprocess (one thread per (image, RoI, foreground class)): softmax over the RoI's nc logits,
@@ -637,6 +741,32 @@ AI4E_API int ai4e_row_sort_desc(const void* scores, int B, int N, void* order, h
   while (P < N) P <<= 1;
   hipLaunchKernelGGL(row_sort_desc_kernel, dim3(B), dim3(ROWSORT_THREADS), 0, s, static_cast<const float*>(scores), N, P,
                      static_cast<long*>(order));
+  return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
+}
+
+AI4E_API int ai4e_sort_select(const void* scores, const void* boxes, const void* grp, int grp_mod, float scale, int B,
+                              int N, void* s_out, void* b_out, void* boff_out, void* g_out, void* lab_out, void* valid,
+                              hipStream_t s) {
+  if (B <= 0 || N <= 0) return AI4E_OK;
+  if (!scores || !boxes || !s_out || !b_out || !boff_out || !valid || N > ROWSORT_MAX || (!grp && grp_mod < 1))
+    return AI4E_EINVAL;
+  int P = 1;
+  while (P < N) P <<= 1;
+  hipLaunchKernelGGL(sort_select_kernel, dim3(B), dim3(ROWSORT_THREADS), 0, s, static_cast<const float*>(scores),
+                     static_cast<const float4*>(boxes), static_cast<const float*>(grp), grp_mod, scale, N, P,
+                     static_cast<float*>(s_out), static_cast<float4*>(b_out), static_cast<float4*>(boff_out),
+                     static_cast<float*>(g_out), static_cast<long*>(lab_out), static_cast<int*>(valid));
+  return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
+}
+
+AI4E_API int ai4e_gather_keep(const void* keep, int B, int K, int N, const void* bsrc, const void* ssrc, const void* lsrc,
+                              void* bout, void* sout, void* lout, hipStream_t s) {
+  if (B <= 0 || K <= 0) return AI4E_OK;
+  if (!keep || N <= 0 || (bout && !bsrc) || (sout && !ssrc) || (lout && !lsrc)) return AI4E_EINVAL;
+  const int total = B * K;
+  hipLaunchKernelGGL(gather_keep_kernel, dim3((total + 255) / 256), dim3(256), 0, s, static_cast<const int*>(keep), K, N,
+                     static_cast<const float4*>(bsrc), static_cast<const float*>(ssrc), static_cast<const long*>(lsrc),
+                     static_cast<float4*>(bout), static_cast<float*>(sout), static_cast<long*>(lout), total);
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
 }
 

@@ -163,12 +163,23 @@ def test_telemetry_sampler_holds_the_rate_and_keeps_tasks_whole():
     late = sum(1 for t, v in kept_by_task.items() if int(t.split("-")[1]) >= 1000 and True in v) * 4
     assert 30 * 7.5 < late < 70 * 7.5, late  # last 7.5 s: ~50 items/s
     assert s.keep("", always=True) and 0.02 < s.ratio < 0.04
-    log = AI4ELogger(stream=io.StringIO())
+    import json
+
+    out = io.StringIO()
+    log = AI4ELogger(stream=out)
     log.sampler = TelemetrySampler(5.0, clock=lambda: now[0])
     for i in range(4000):
         now[0] = 100 + i / 1000.0
         log.log_info("x", task_id=f"t{i}")
     log.log_error("boom", task_id="t-err")
-    assert 10 < len(log.records) < 40 and log.records[-1]["message"] == "boom"
-    assert any(r.get("sample_rate", 1) > 100 for r in log.records)
+    exported = [json.loads(l) for l in out.getvalue().splitlines()]
+    assert 10 < len(exported) < 40 and exported[-1]["message"] == "boom"
+    assert any(r.get("sample_rate", 1) > 100 for r in exported)
+    # the local ring (/v1/platform/logs) is not sampled: its last 1000 records are all there
+    assert len(log.records) == 1000 and log.records[-1]["message"] == "boom"
+    assert "sample_rate" not in log.records[-2]
+    # an error burst does not use up the burst cap of the sampled lines
+    s2 = TelemetrySampler(5.0, clock=lambda: 0.5)
+    assert all(s2.keep("", always=True) for _ in range(100))
+    assert s2.keep("t")
     assert TelemetrySampler(0).keep("any")

@@ -49,3 +49,39 @@ def test_nms_reference_hand_computed():
     assert nms_reference(boxes, scores, 0.5).tolist() == [2, 1, 3]
     # thr 0.9: nothing overlaps that much
     assert nms_reference(boxes, scores, 0.9).tolist() == [2, 0, 1, 3]
+
+
+def test_nms_sort_rows_fit_the_graph_safe_hip_sort():
+    """Both NMS-stage sorts of the default detector fit the HIP row sort at the served sizes, so no multi-kernel
+    library sort (not graph-safe) can enter a captured forward; a configuration that does not fit must refuse to run
+    its fallback under capture (num_classes >= 10 pushes the detections' sort past 8192)."""
+    from aiforearth_api_platform_amd.models.faster_rcnn import DetectorConfig, FasterRCNN
+    from aiforearth_api_platform_amd.ops.detection import ROW_SORT_MAX
+
+    det = FasterRCNN.__new__(FasterRCNN)
+    det.cfg = DetectorConfig()
+    for hw in ((640, 640), (1024, 1024), (1536, 2048)):
+        rows = det.sort_rows(hw)
+        assert rows["rpn"] <= ROW_SORT_MAX and rows["detections"] <= ROW_SORT_MAX, (hw, rows)
+    det.cfg = DetectorConfig(num_classes=10)
+    assert det.sort_rows((640, 640))["detections"] > ROW_SORT_MAX
+
+
+def test_sort_select_and_gather_keep_cpu_reference():
+    import torch
+
+    from aiforearth_api_platform_amd.ops.detection import gather_keep, sort_select
+
+    sc = torch.tensor([[0.2, -1.0, 0.9, 0.2, 0.5, -1.0]])
+    bx = torch.arange(24, dtype=torch.float32).reshape(1, 6, 4)
+    s_s, b_s, b_o, lab, valid = sort_select(sc, bx, 100.0, group_mod=2, want_labels=True)
+    assert torch.equal(s_s, torch.tensor([[0.9, 0.5, 0.2, 0.2, -1.0, -1.0]]))
+    order = [2, 4, 0, 3, 1, 5]  # ties (0.2 at 0 and 3, -1 at 1 and 5) by lower index
+    assert torch.equal(b_s[0], bx[0, order])
+    assert lab.tolist() == [[i % 2 + 1 for i in order]]
+    assert torch.equal(b_o[0], bx[0, order] + (lab[0].float() * 100.0)[:, None])
+    assert valid.tolist() == [4]
+    keep = torch.tensor([[1, 0, -1]], dtype=torch.int32)
+    kb, ks, kl = gather_keep(keep, b_s, s_s, lab)
+    assert torch.equal(kb[0, :2], b_s[0, [1, 0]]) and (kb[0, 2] == 0).all()
+    assert torch.equal(ks, torch.tensor([[0.5, 0.9, 0.0]])) and kl[0, 2] == 0

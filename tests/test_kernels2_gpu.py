@@ -239,6 +239,65 @@ def test_rpn_topk_selects_the_k_largest(B, h, w, k, ties):
             assert logits[b, rest].max() <= got.min()
 
 
+@pytest.mark.parametrize("B,h,w,k", [(2, 40, 40, 1000), (1, 20, 20, 7)])
+def test_rpn_topk_tied_logits_same_set_as_cpu(B, h, w, k):
+    """Deliberately tied logits (a few distinct values): the HIP selection is the SET of the k largest by
+    (value desc, index asc) — the CPU path's stable-sort set — so proposals (and NMS winners among equal scores)
+    do not depend on the backend."""
+    from aiforearth_api_platform_amd.ops.detection import rpn_topk
+
+    A = 3
+    torch.manual_seed(3)
+    head = (torch.randn(B, h, w, 16) * 1.5).round().to(torch.bfloat16)
+    got = rpn_topk(head.to(DEV), A, k).cpu()
+    ref = rpn_topk(head, A, k)  # CPU: stable descending sort, first k
+    for b in range(B):
+        assert set(got[b].tolist()) == set(ref[b].tolist())
+        # output order: the keys above the k-th value, then the taken ties, each in index order
+        vals = head[b, ..., :A].float().reshape(-1)[got[b]]
+        kth = vals.min()
+        above, tie = got[b][vals > kth], got[b][vals == kth]
+        assert torch.equal(above, above.sort()[0]) and torch.equal(tie, tie.sort()[0])
+
+
+@pytest.mark.parametrize("B,N,groups", [(32, 4300, "lvl"), (2, 3000, "label"), (3, 1, "lvl"), (2, 8192, "label")])
+def test_sort_select_matches_reference(B, N, groups):
+    """One-launch NMS-stage sort + select (sort_select_kernel) vs the PyTorch form: sorted scores exact (ties in index
+    order), gathered boxes / offset boxes / groups / labels exact, valid counts exact."""
+    from aiforearth_api_platform_amd.ops.detection import sort_select
+
+    torch.manual_seed(9)
+    sc = torch.rand(B, N)
+    sc[:, ::7] = -1.0
+    sc[:, 1::11] = 0.25
+    bx = torch.rand(B, N, 4) * 600
+    scale = 641.0
+    if groups == "lvl":
+        lvl = torch.randint(0, 5, (B, N)).float()
+        got = sort_select(sc.to(DEV), bx.to(DEV), scale, groups=lvl.to(DEV))
+        ref = sort_select(sc, bx, scale, groups=lvl)
+    else:
+        got = sort_select(sc.to(DEV), bx.to(DEV), scale, group_mod=3, want_labels=True)
+        ref = sort_select(sc, bx, scale, group_mod=3, want_labels=True)
+    for g, r in zip(got, ref):
+        assert torch.equal(g.cpu(), r), (g.cpu(), r)
+
+
+def test_gather_keep_matches_reference():
+    from aiforearth_api_platform_amd.ops.detection import gather_keep
+
+    torch.manual_seed(2)
+    B, N, K = 3, 500, 100
+    bx, sc, lb = torch.rand(B, N, 4), torch.rand(B, N), torch.randint(1, 4, (B, N))
+    keep = torch.randint(0, N, (B, K), dtype=torch.int32)
+    keep[:, 60:] = -1
+    got = gather_keep(keep.to(DEV), bx.to(DEV), sc.to(DEV), lb.to(DEV))
+    ref = gather_keep(keep, bx, sc, lb)
+    for g, r in zip(got, ref):
+        assert torch.equal(g.cpu(), r)
+    assert (got[0][:, 60:] == 0).all()
+
+
 @pytest.mark.parametrize("B,N", [(32, 4300), (2, 8192), (3, 1), (4, 3000)])
 def test_argsort_desc_rows_matches_sort(B, N):
     """Graph-safe row sort (bitonic in LDS) vs torch.sort on the CPU: the gathered scores equal the descending sorted
