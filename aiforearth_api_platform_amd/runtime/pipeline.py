@@ -231,8 +231,10 @@ class StageGraphPipeline:
 
     def _send(self, crops: torch.Tensor, n: int) -> list:
         """Non-blocking: the detector must be free to post the receive of the previous batch's results while these
-        bytes move, or both sides block in send (rendezvous) and deadlock. The crops are copied out of the detector
-        graph's static output first (the next batch's replay rewrites it while this send may still be reading)."""
+        bytes move, or both sides block in send (rendezvous) and deadlock. The crops leave through a pair of
+        preallocated wire buffers used alternately (batch i in buffer i % 2): the detector graph's static output is
+        rewritten by the next replay while this send may still read, and ``run_batches`` waits for batch i's send
+        before batch i + 2 reuses its buffer — one device copy into a resident buffer per batch, no allocation."""
         self._handoffs += 1
         if self._fail_at and self._handoffs == self._fail_at:
             raise RuntimeError(f"injected xGMI hand-off failure (batch {self._handoffs})")
@@ -240,10 +242,20 @@ class StageGraphPipeline:
         works = [(dist.isend(hdr, group_dst=self.peer, group=self.group), hdr)]
         self.bytes_sent += 8
         if n:
-            c = crops[:n].clone()
+            wire = self._wire_buffer(crops)
+            c = wire[:n]
+            c.copy_(crops[:n])
             works.append((dist.isend(c, group_dst=self.peer, group=self.group), c))
             self.bytes_sent += c.numel() * c.element_size()
         return works
+
+    def _wire_buffer(self, crops: torch.Tensor) -> torch.Tensor:
+        """The ping-pong wire buffer of this hand-off (grown to the largest crop batch seen)."""
+        if not hasattr(self, "_wire") or self._wire[0].shape[0] < crops.shape[0] or \
+                self._wire[0].shape[1:] != crops.shape[1:] or self._wire[0].dtype != crops.dtype:
+            # (an in-flight send of the previous pair keeps its buffer alive through its works entry)
+            self._wire = [torch.empty_like(crops), torch.empty_like(crops)]
+        return self._wire[self._handoffs % 2]
 
     def _recv_results(self, n: int) -> torch.Tensor:
         res = torch.empty(n, 2, device=self.device)

@@ -10,12 +10,15 @@ context parallelism (survey §5.7):
    U-Net on its own tiles only (no redundant compute);
 2. rank 0 owns the request and sends each rank only the mosaic rows its tiles cover (one P2P
    message per rank over its own xGMI link, instead of broadcasting the whole 64 MiB mosaic);
-3. **halo exchange**: stitching is by tile rows (a rank blends the mosaic rows from its first tile
-   row's origin to the next rank's), so a rank needs the logits of its tile rows plus the row above;
-   the tiles of those rows computed elsewhere come over in one ``batch_isend_irecv`` — contiguous
-   slices, mostly from the two neighbouring ranks;
+3. **halo exchange, overlapped with compute**: stitching is by tile rows (a rank blends the mosaic rows
+   from its first tile row's origin to the next rank's), so a rank needs the logits of its tile rows plus
+   the row above; the tiles of those rows computed elsewhere come over in one ``batch_isend_irecv`` —
+   contiguous slices, mostly from the two neighbouring ranks. Each rank infers its BOUNDARY tiles (the
+   ones other ranks stitch over) first and posts the whole exchange right after them, so the halo moves
+   over xGMI while the interior tiles run (survey §7.5.5/§7.5.6);
 4. each rank blends + argmaxes its own mosaic rows with the gather-form stitch kernel (K6);
-5. the per-rank class bands are sent to rank 0 (P2P) and concatenated.
+5. the per-rank class bands go to rank 0 in one batched P2P exchange (every band's receive posted at
+   once) and are concatenated.
 
 Works with any ``torch.distributed`` backend (``nccl`` = RCCL on the GPU node; ``gloo`` in the CPU
 tests) and degenerates to a single-process path when world size is 1.
@@ -73,6 +76,7 @@ class SpatialSegmenter:
         self.world = dist.get_world_size(group) if dist_on else 1
         self.bytes_sent = 0      # P2P / broadcast payload bytes over the group (xGMI on the GPU node)
         self.bytes_received = 0
+        self.events: List[tuple] = []  # ("tiles", lo, hi) per inferred batch, ("halo_posted", ...) (tests)
         if grid.ts >= 2 * grid.stride:
             raise ValueError("tile overlap must be < 50% (a halo of one tile row per boundary)")
         if grid.nty < self.world:
@@ -115,18 +119,50 @@ class SpatialSegmenter:
             out.append(row[t0:t1])
         return torch.cat(out)
 
-    def _infer(self, tiles: torch.Tensor) -> torch.Tensor:
-        """tiles [n, ts, ts, c] uint8 -> logits [n, ts, ts, n_out]."""
+    def _infer(self, tiles: torch.Tensor, order: Optional[List[Tuple[int, int]]] = None,
+               after: Optional[Tuple[int, Callable[[torch.Tensor], None]]] = None) -> torch.Tensor:
+        """tiles [n, ts, ts, c] uint8 -> logits [n, ts, ts, n_out]. ``order``: the tile ranges [lo, hi) to run, in
+        that order (default: all, in index order); ``after`` = (k, fn): fn(logits) once the first k ranges are done
+        (the halo exchange is posted there, before the remaining tiles run)."""
         flat = tiles.contiguous()
         out = None
-        for i in range(0, flat.shape[0], self.tile_batch):
-            # each batch's logits go straight into one preallocated buffer (a graph's output buffer is reused by
-            # its next replay; one copy per batch instead of a clone plus a concatenation)
-            y = self.model_fn(flat[i:i + self.tile_batch])[..., : self.n_out]
-            if out is None:
-                out = torch.empty(flat.shape[0], *y.shape[1:], dtype=y.dtype, device=y.device)
-            out[i:i + y.shape[0]].copy_(y)
+        ranges = order if order is not None else [(0, flat.shape[0])]
+        pending = after is not None
+        for j, (lo, hi) in enumerate(ranges):
+            for i in range(lo, hi, self.tile_batch):
+                if pending and j >= after[0] and out is not None:  # (the first moment the logits buffer exists)
+                    after[1](out)
+                    pending = False
+                # each batch's logits go straight into one preallocated buffer (a graph's output buffer is reused by
+                # its next replay; one copy per batch instead of a clone plus a concatenation)
+                y = self.model_fn(flat[i:min(hi, i + self.tile_batch)])[..., : self.n_out]
+                if out is None:
+                    out = torch.empty(flat.shape[0], *y.shape[1:], dtype=y.dtype, device=y.device)
+                out[i:i + y.shape[0]].copy_(y)
+                self.events.append(("tiles", i, i + y.shape[0]))
+        if pending and out is not None:
+            after[1](out)
         return out
+
+    @staticmethod
+    def _boundary_first(a: int, b: int, sends: List[Tuple[int, int]]) -> Tuple[List[Tuple[int, int]], int]:
+        """Tile ranges of [a, b) (local indices) with every range another rank needs first; returns (ranges, number
+        of leading boundary ranges)."""
+        cover = sorted((lo - a, hi - a) for lo, hi in sends if hi > lo)
+        merged: List[Tuple[int, int]] = []
+        for lo, hi in cover:
+            if merged and lo <= merged[-1][1]:
+                merged[-1] = (merged[-1][0], max(merged[-1][1], hi))
+            else:
+                merged.append((lo, hi))
+        rest, t = [], 0
+        for lo, hi in merged:
+            if lo > t:
+                rest.append((t, lo))
+            t = hi
+        if t < b - a:
+            rest.append((t, b - a))
+        return merged + rest, len(merged)
 
     def run(self, mosaic: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
         """mosaic [H, W, C] uint8 on rank 0 (ignored elsewhere). Returns the class map on rank 0."""
@@ -169,31 +205,40 @@ class SpatialSegmenter:
         r, world = self.rank, self.world
         comp, own, need, _ = self._plan()
         a, b = comp[r]
-        logits = self._infer(self._tiles_range(band, y0, a, b))       # [b - a, ts, ts, n_out]
         na, nb = need[r]
+        tiles = self._tiles_range(band, y0, a, b)
         if world == 1:
-            full = logits
+            full = self._infer(tiles)                                      # [b - a, ts, ts, n_out]
         else:
             # halo exchange: each rank sends every other rank the slice of its computed tiles that rank stitches
-            # over (contiguous flat ranges: typically the neighbours' boundary tiles), all in one batch
-            full = torch.empty(nb - na, *logits.shape[1:], dtype=logits.dtype, device=self.device)
-            ops = []
-            for s in range(world):
-                if s == r:
-                    continue
-                lo, hi = max(a, need[s][0]), min(b, need[s][1])
-                if hi > lo:
-                    t = logits[lo - a:hi - a]
-                    ops.append(dist.P2POp(dist.isend, t, group=self.group, group_peer=s))
-                    self.bytes_sent += t.numel() * t.element_size()
-                lo, hi = max(comp[s][0], na), min(comp[s][1], nb)
-                if hi > lo:
-                    ops.append(dist.P2POp(dist.irecv, full[lo - na:hi - na], group=self.group, group_peer=s))
-                    self.bytes_received += (hi - lo) * logits[0].numel() * logits.element_size()
+            # over (contiguous flat ranges: typically the neighbours' boundary tiles), all in one batch. Those
+            # boundary tiles run first; the exchange is posted as soon as they are done and completes over xGMI
+            # while the interior tiles run (the receives land in `full`, which only the stitch reads)
+            sends = [(s, max(a, need[s][0]), min(b, need[s][1])) for s in range(world) if s != r]
+            order, nfirst = self._boundary_first(a, b, [(lo, hi) for _, lo, hi in sends])
+            box = {}
+
+            def post(logits: torch.Tensor) -> None:
+                full = torch.empty(nb - na, *logits.shape[1:], dtype=logits.dtype, device=self.device)
+                ops = []
+                for s, lo, hi in sends:
+                    if hi > lo:
+                        t = logits[lo - a:hi - a]
+                        ops.append(dist.P2POp(dist.isend, t, group=self.group, group_peer=s))
+                        self.bytes_sent += t.numel() * t.element_size()
+                    lo, hi = max(comp[s][0], na), min(comp[s][1], nb)
+                    if hi > lo:
+                        ops.append(dist.P2POp(dist.irecv, full[lo - na:hi - na], group=self.group, group_peer=s))
+                        self.bytes_received += (hi - lo) * logits[0].numel() * logits.element_size()
+                box["full"], box["works"] = full, (dist.batch_isend_irecv(ops) if ops else [])
+                self.events.append(("halo_posted", len(ops)))
+
+            logits = self._infer(tiles, order=order, after=(nfirst, post))
+            full = box["full"]
             lo, hi = max(a, na), min(b, nb)
             if hi > lo:
                 full[lo - na:hi - na] = logits[lo - a:hi - a]
-            for wk in dist.batch_isend_irecv(ops) if ops else []:
+            for wk in box["works"]:
                 wk.wait()
         ty0, ty1 = own[r]
         row0, row1 = owned_rows(g, own, r)
@@ -202,17 +247,25 @@ class SpatialSegmenter:
         if world == 1:
             return cls
         if r != 0:
-            dist.send(cls.contiguous(), group_dst=0, group=self.group)
+            for wk in dist.batch_isend_irecv([dist.P2POp(dist.isend, cls.contiguous(), group=self.group,
+                                                         group_peer=0)]):
+                wk.wait()
             self.bytes_sent += cls.numel()
             return None
-        bands = [cls]
+        # the class bands: every rank's receive posted at once straight into its rows of the output (no sequential
+        # blocking receives, no concatenation copy)
+        out = torch.empty(g.height, g.width, dtype=torch.uint8, device=self.device)
+        r0, r1 = owned_rows(g, own, 0)
+        out[r0:r1] = cls
+        ops = []
         for src in range(1, world):
             lo, hi = owned_rows(g, own, src)
-            buf = torch.empty(hi - lo, g.width, dtype=torch.uint8, device=self.device)
-            dist.recv(buf, group_src=src, group=self.group)
-            self.bytes_received += buf.numel()
-            bands.append(buf)
-        return torch.cat(bands)
+            if hi > lo:
+                ops.append(dist.P2POp(dist.irecv, out[lo:hi], group=self.group, group_peer=src))
+                self.bytes_received += (hi - lo) * g.width
+        for wk in dist.batch_isend_irecv(ops) if ops else []:
+            wk.wait()
+        return out
 
     # ------------------------------------------------------------ API worker group (leader + followers)
     def serve_follower(self) -> int:

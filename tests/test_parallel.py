@@ -31,7 +31,7 @@ def _bcast_worker(rank, world, port, q):
     m = FusedResNet(resnet50(seed=rank))  # different weights per rank until the broadcast
     broadcast_tensors(m.tensors(), src=0, bucket_bytes=8 << 20)  # small buckets: several collectives
     img = torch.randint(0, 256, (2, 64, 64, 3), dtype=torch.uint8, generator=torch.Generator().manual_seed(9))
-    q.put((rank, m.forward_u8(img)))
+    q.put((rank, m.forward_u8(img).numpy().copy()))  # (by value: see tests/test_pipeline_dist.py)
     dist.barrier()
     dist.destroy_process_group()
 
@@ -53,7 +53,7 @@ def test_broadcast_tensors_replicates_rank0_weights():
     procs = [ctx.Process(target=_bcast_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    outs = dict(q.get(timeout=300) for _ in range(2))
+    outs = {r: torch.from_numpy(o) for r, o in (q.get(timeout=300) for _ in range(2))}
     for p in procs:
         p.join(timeout=60)
     img = torch.randint(0, 256, (2, 64, 64, 3), dtype=torch.uint8, generator=torch.Generator().manual_seed(9))

@@ -45,7 +45,9 @@ def _worker(rank, world, leaders, port, q):
     if p.is_detector:
         out = p.run_batches(_batches(rank))
         p.stop()
-        q.put((rank, [(v, r) for _, _, v, r in out]))
+        # numpy copies travel by value: a torch tensor would go through a shared-memory fd that the parent may only
+        # open after this process has exited (FileNotFoundError in the resource sharer, a flaky failure)
+        q.put((rank, [(v.numpy().copy(), r.numpy().copy()) for _, _, v, r in out]))
     else:
         q.put((rank, p.serve()))
     dist.destroy_process_group()
@@ -67,6 +69,7 @@ def test_stage_graph_gloo_matches_local(world, leaders):
     for r in range(leaders):
         ref = local.run_batches(_batches(r))
         for (v, res), (_, _, lv, lres) in zip(got[r], ref):
+            v, res = torch.from_numpy(v), torch.from_numpy(res)
             assert torch.equal(v, lv)
             assert torch.allclose(res, lres, atol=1e-4)
             total += res.shape[0]

@@ -36,7 +36,7 @@ def _worker(rank, world, port, mosaic, q, grid=GRID):
     torch.manual_seed(0)
     seg = SpatialSegmenter(_model(), grid, 5, torch.device("cpu"), tile_batch=8)
     out = seg.run(mosaic if rank == 0 else None)
-    q.put((rank, out, seg.bytes_received))
+    q.put((rank, None if out is None else out.numpy().copy(), seg.bytes_received))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -76,7 +76,7 @@ def test_spatial_matches_single_process(world):
     res = {}
     for _ in range(world):
         r, out, nbytes = q.get(timeout=240)
-        res[r] = (out, nbytes)
+        res[r] = (None if out is None else torch.from_numpy(out), nbytes)
     [p.join(60) for p in procs]
     assert all(p.exitcode == 0 for p in procs)
     assert torch.equal(res[0][0], single)
@@ -89,3 +89,51 @@ def test_spatial_matches_single_process(world):
         for r in range(1, world):
             band_bytes = res[r][1] - (res[r][1] // ts_bytes) * ts_bytes
             assert band_bytes < mosaic_bytes // 2, (r, band_bytes, mosaic_bytes)
+
+
+def _delayed_worker(rank, world, port, mosaic, q, grid, delay_rank):
+    """A rank whose tiles run slowly (the delayed peer); every rank records its event order."""
+    import time as _t
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(0)
+    base = _model()
+
+    def slow(t):
+        if rank == delay_rank:
+            _t.sleep(0.15)
+        return base(t)
+
+    seg = SpatialSegmenter(slow, grid, 5, torch.device("cpu"), tile_batch=2)
+    out = seg.run(mosaic if rank == 0 else None)
+    q.put((rank, None if out is None else out.numpy().copy(), list(seg.events)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_halo_posted_before_interior_tiles_finish():
+    """Boundary tiles run first and the halo exchange is posted right after them: on every rank the post precedes the
+    last interior tile batch (with a delayed peer the exchange is in flight while the interior tiles still run), and
+    the result still equals the single-process class map."""
+    grid = GRID9
+    torch.manual_seed(0)
+    mosaic = torch.randint(0, 256, (grid.height, grid.width, 4), dtype=torch.uint8)
+    single = SpatialSegmenter(_model(), grid, 5, torch.device("cpu"), tile_batch=8).run(mosaic)
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_delayed_worker, args=(r, world, port, mosaic, q, grid, 1)) for r in range(world)]
+    [p.start() for p in procs]
+    res = {}
+    for _ in range(world):
+        r, out, ev = q.get(timeout=240)
+        res[r] = (None if out is None else torch.from_numpy(out), ev)
+    [p.join(60) for p in procs]
+    assert torch.equal(res[0][0], single)
+    for r, (_, ev) in res.items():
+        kinds = [e[0] for e in ev]
+        assert kinds.count("halo_posted") == 1, ev
+        post = kinds.index("halo_posted")
+        assert 0 < post < len(ev) - 1, (r, ev)  # boundary tiles before it, interior tiles after it
