@@ -22,7 +22,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import torch
 import torch.nn as nn
 
-from ..ops.conv import PackedConv, conv2d_nhwc, linear_nhwc, pack_conv
+from ..ops.conv import PackedConv, conv2d_nhwc, pack_conv
 from ..ops.debug import crumb
 from ..ops.detection import (det_decode, gather_keep, nms_batched_sorted, roi_align_fpn, rpn_decode_into, rpn_topk,
                               sort_select)
@@ -91,8 +91,6 @@ class FasterRCNN:
         wp[nc: nc + 4 * nc] = torch.randn(4 * nc, rep, 1, 1, generator=g) * 0.001
         self.predictor = pack_conv(wp, torch.zeros(pred_out)).to(d)
         self._anchor_cache: Dict[Tuple, List[torch.Tensor]] = {}
-        # box-head FCs on K1 (the 256x256 tile, tuned per batch in conv_tiles.json); AI4E_DET_FC_BLAS=1: hipBLASLt
-        self.fc_blas = os.environ.get("AI4E_DET_FC_BLAS", "0") not in ("0", "off", "")
 
     def sort_rows(self, img_hw: Tuple[int, int]) -> Dict[str, int]:
         """Row lengths of the two NMS-stage sorts at an input size: the all-level proposal sort (sum of the per-level
@@ -182,9 +180,9 @@ class FasterRCNN:
         feats = roi_align_fpn(P[:4], [1.0 / s for s in strides], rois, (7, 7), 2)  # [B*R, 7, 7, C]
         crumb("box.roi_align", feats)
         x = feats.reshape(B * R, 1, 1, -1)
-        fc = linear_nhwc if self.fc_blas else conv2d_nhwc  # FCs as library GEMMs (AI4E_DET_FC_BLAS=0: K1)
-        x = fc(x, self.fc6, relu=True)
-        x = fc(x, self.fc7, relu=True)
+        # box-head FCs on K1 (the 256x256 tile, tuned per batch in conv_tiles.json)
+        x = conv2d_nhwc(x, self.fc6, relu=True)
+        x = conv2d_nhwc(x, self.fc7, relu=True)
         # [B, R, >= 5 nc]: nc class logits, then 4 nc box deltas
         return conv2d_nhwc(x, self.predictor).reshape(B, R, -1)
 

@@ -176,11 +176,8 @@ class FusedResNet:
         self.stem_u8 = os.environ.get("AI4E_STEM_U8", "0") not in ("0", "off", "")
         # the first bottleneck's 1x1 c1 fused into the stem kernel (computed from the pooled tile in LDS)
         self.stem_c1 = os.environ.get("AI4E_STEM_C1", "1") not in ("0", "off", "")
-        # classifier FC through hipBLASLt (AI4E_FC_BLAS=0: the K1 conv kernel)
         # classifier FC on K1 (1x1 conv over the pooled features) by default: parity-or-better with hipBLASLt in
         # the captured forward (80.7/80.7k vs 81.3/80.9k images/s same-box A/B) and no library kernel left
-        self.fc_blas = os.environ.get("AI4E_FC_BLAS", "0") not in ("0", "off", "")
-        self._fc_lin = None
         # chained micro-batching (AI4E_RESNET_CHAIN_MB=mb:nstages): stem + the first nstages run mb images at a time
         cmb = os.environ.get("AI4E_RESNET_CHAIN_MB", "")
         self.chain_mb: Optional[Tuple[int, int]] = tuple(int(v) for v in cmb.split(":")) if ":" in cmb else None
@@ -416,34 +413,9 @@ class FusedResNet:
         """Logits [N, classes] in the model dtype (bf16 / fp16)."""
         return self._head_logits(self.forward_features(x, preprocess))
 
-    # Two-part serving forward (runtime/engine.py ``split``): stem .. layer2 | layer3 .. top-k. The serving engine
-    # captures each part as its own graph and starts batch k+1's front part only once batch k's has finished, so
-    # the two compute streams run an HBM-heavy front (stem, layer1/2 chains) beside a back (layer3/4, head).
-    SPLIT_STAGE = 2
-
-    def can_split(self) -> bool:
-        return self.chain and not self.chain_mb and not self.chunk and len(self.stages) > self.SPLIT_STAGE
-
-    def front_u8(self, img_u8: torch.Tensor) -> Tuple[torch.Tensor, ...]:
-        y, t1 = self._stem_t1(preprocess_s2d_u8(img_u8))
-        y, t1 = self._stages_chained(y, t1=t1, s1=self.SPLIT_STAGE)
-        return (y,) if t1 is None else (y, t1)
-
-    def back_topk(self, y: torch.Tensor, t1: Optional[torch.Tensor] = None, k: int = 5):
-        return softmax_topk(self._head_logits(self._stages_chained(y, t1=t1, s0=self.SPLIT_STAGE)), k)
-
     def _head_logits(self, feats: torch.Tensor) -> torch.Tensor:
         f = global_avgpool_nhwc(feats)
-        if self.fc_blas and f.is_cuda:
-            # [N, 2048] x [2048, classes]: a plain library GEMM (hipBLASLt picks split-K); the K1 tile grid
-            # has only 16 workgroups at N = 256
-            if self._fc_lin is None:
-                k = self.fc.cin_pad
-                self._fc_lin = (self.fc.w_packed[:self.fc.cout, :k].contiguous(),
-                                self.fc.bias[:self.fc.cout].to(self.dtype))
-            y = F.linear(f.reshape(f.shape[0], -1), *self._fc_lin)
-        else:
-            y = conv2d_nhwc(f, self.fc).reshape(f.shape[0], -1)
+        y = conv2d_nhwc(f, self.fc).reshape(f.shape[0], -1)
         return y if y.shape[1] == self.num_classes else y[:, :self.num_classes].contiguous()
 
     def forward(self, x: torch.Tensor, preprocess=None) -> torch.Tensor:

@@ -103,24 +103,12 @@ class _FusedDouble:
         return cout % g == 0 and cout // g <= 4 and g <= 64
 
     def __call__(self, x: torch.Tensor, out: Optional[torch.Tensor] = None,
-                 pool_out: Optional[torch.Tensor] = None, head=None, up: Optional[torch.Tensor] = None,
-                 up_coff: int = 0):
+                 pool_out: Optional[torch.Tensor] = None, head=None):
         """``head``: a 1x1 PackedConv to apply after the final GroupNorm + ReLU; then returns ``(y, headed)`` where
         ``headed`` says whether ``y`` is already the head's output (fused: csrc/kernels/norm_resample.hip
-        gn_relu_head8_kernel) or still the block output. ``up``: the coarse tensor whose 2x upsample belongs in
-        ``x[..., up_coff:]`` (the decoder concat): fused into c1 when K1t takes it (csrc/kernels/conv_tile3x3.hip UPS),
-        else upsampled into ``x`` first."""
-        fused_up = False
-        if up is not None:
-            fused_up = (tile64_supported(x, self.c1) and self._k1t_groups(self.g1[2], self.c1.cout)
-                        and self.c1.cin_pad == 128 and self.c1.cout == 64 and up_coff == 64 and up.is_contiguous()
-                        and tuple(up.shape) == (x.shape[0], x.shape[1] // 2, x.shape[2] // 2, 64))
-            if not fused_up:
-                upsample2x_nhwc(up, out=x, out_coff=up_coff)
+        gn_relu_head8_kernel) or still the block output."""
         # GroupNorm statistics come out of the conv epilogues (conv2d_gn_nhwc, K1t) where the tile allows
-        if fused_up:
-            y, st = conv3x3_tile64(x, self.c1, gn_groups=self.g1[2], up=up)
-        elif tile64_supported(x, self.c1) and self._k1t_groups(self.g1[2], self.c1.cout):
+        if tile64_supported(x, self.c1) and self._k1t_groups(self.g1[2], self.c1.cout):
             y, st = conv3x3_tile64(x, self.c1, gn_groups=self.g1[2])  # e.g. the last decoder's 128 -> 64 c1
         else:
             y, st = conv2d_gn_nhwc(x, self.c1, self.g1[2])
@@ -164,8 +152,6 @@ class FusedUNet:
         self.fused_pool = os.environ.get("AI4E_UNET_FUSED_POOL", "1") != "0"
         # the last decoder's GroupNorm + ReLU and the 1x1 head in one pass (AI4E_UNET_FUSED_HEAD=0: apply, then conv)
         self.fused_head = os.environ.get("AI4E_UNET_FUSED_HEAD", "1") != "0"
-        # the level-0 decoder's bilinear upsample formed inside its c1 (K1t UPS) instead of written into the concat
-        self.fused_up = os.environ.get("AI4E_UNET_FUSED_UP", "0") == "1"
 
     def tensors(self) -> List[torch.Tensor]:
         """Every weight tensor (packed convs + GroupNorm affine), for ``parallel.dist.broadcast_tensors``."""
@@ -200,12 +186,6 @@ class FusedUNet:
                 y = self.down[3](pooled)
         for i, lvl in enumerate((3, 2, 1, 0)):
             buf = cat[lvl]
-            if i == 3 and self.fused_up:  # no upsample pass: c1 forms it from y (or upsamples into buf itself)
-                r = self.up[i](buf, head=self.outc if self.fused_head else None, up=y, up_coff=enc_c[lvl])
-                if not self.fused_head:
-                    return conv2d_nhwc(r, self.outc)
-                y, headed = r
-                return y if headed else conv2d_nhwc(y, self.outc)
             upsample2x_nhwc(y, out=buf, out_coff=enc_c[lvl])
             if i == 3 and self.fused_head:
                 y, headed = self.up[i](buf, head=self.outc)

@@ -67,14 +67,10 @@ _SIGS = {
     "ai4e_roi_align_fpn_nhwc": [_vp] * 8 + [_c_int] * 6 + [_vp],
     "ai4e_crop_resize_nhwc": [_vp, _vp, _vp, _vp] + [_c_int] * 7 + [_vp],
     "ai4e_tile_stitch": [_vp, _vp, _vp] + [_c_int] * 10 + [_vp],
-    "ai4e_stream_create_cu_mask": [_vp, _c_int, _vp],
-    "ai4e_stream_destroy": [_vp],
-    "ai4e_stream_get_cu_mask": [_vp, _vp, _c_int],
-    "ai4e_cu_census": [_vp, _c_int, _c_int, _vp],
     "ai4e_groupnorm_finalize": [_vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_float, _c_int, _vp],
     "ai4e_gn_chunk_px": [],
     "ai4e_gn_relu_head8": [_vp, _c_int, _c_int, _vp, _vp, _c_int, _vp, _vp, _c_int, _c_int, _vp],
-    "ai4e_conv3x3_tile_fwd": [_vp, _vp, _vp, _vp, _c_int, _vp] + [_c_int] * 10 + [_vp, _c_int, _vp, _vp],
+    "ai4e_conv3x3_tile_fwd": [_vp, _vp, _vp, _vp, _c_int, _vp] + [_c_int] * 10 + [_vp, _c_int, _vp],
     "ai4e_crumbs_alloc": [_c_int, _vp, _vp],
     "ai4e_crumb": [_vp, _c_int, _vp],
 }

@@ -141,10 +141,6 @@ def conv2d_nhwc(x: torch.Tensor, pc: PackedConv, residual: Optional[torch.Tensor
     if c != pc.cin_pad:
         raise ValueError(f"conv expects C={pc.cin_pad} (padded), got {c}")
     oh, ow = pc.out_hw(h, w)
-    if (out is None and residual is None and BLAS_1X1 and pc.kh == 1 and pc.kw == 1 and pc.stride == 1 and pc.pad == 0
-            and pc.cin_pad >= 512 and pc.cout >= 256 and x.is_contiguous() and tile_cfg <= 0
-            and _ext.backend_for(x) == "hip" and x.dtype == torch.bfloat16):
-        return _pointwise_blas(x, pc, relu)
     if out is None:
         out = torch.empty(n, oh, ow, pc.cout, device=x.device, dtype=x.dtype)
         out_coff = 0
@@ -158,22 +154,8 @@ def conv2d_nhwc(x: torch.Tensor, pc: PackedConv, residual: Optional[torch.Tensor
     return out
 
 
-# Wide-K pointwise convs without a residual (ResNet layer3/4 c1: 512/1024/2048 -> 256/512) as hipBLASLt GEMMs with
-# the bias + ReLU epilogue (AI4E_BLAS_1X1=1). In isolation they are 7-14 us faster per launch than K1 at batch
-# 256 (bench/blas_vs_k1.py), but inside the captured ResNet forward the A/B is flat (3.797 vs 3.797 ms), so K1
-# stays the default; the residual convs never route (K1's fused residual epilogue beats addmm + ReLU).
-BLAS_1X1 = os.environ.get("AI4E_BLAS_1X1", "0") not in ("0", "off", "")
-
-
-def _pointwise_blas(x, pc, relu):
-    n, h, w, c = x.shape
-    lin = getattr(pc, "_linear", None)
-    if lin is None:
-        lin = (pc.w_packed[:pc.cout, :pc.cin_pad].contiguous(), pc.bias[:pc.cout].to(torch.bfloat16))
-        pc._linear = lin
-    x2 = x.reshape(-1, c)
-    y = torch._addmm_activation(lin[1], x2, lin[0].t()) if relu else torch.addmm(lin[1], x2, lin[0].t())
-    return y.reshape(n, h, w, pc.cout)
+# (measured and removed in round 5: hipBLASLt routes for the wide-K 1x1 convs, the classifier FC and the detector's
+# box-head FCs — flat or slower inside the captured forwards than K1; patch in profiles/r5_pruned/)
 
 
 def _conv_hip(x, pc, residual, relu, out, out_coff, tile_cfg, residual_up2=False, gn=None):
@@ -234,22 +216,19 @@ def conv2d_gn_nhwc(x: torch.Tensor, pc: PackedConv, groups: int, out: Optional[t
 
 
 def _tile_rows(cout: int) -> int:
-    return 8 if cout == 64 else 4  # output tile rows (x 32 columns); the input channels run as 64-channel k-slices
+    return 8  # output tile rows (x 32 columns); the input channels run as 64-channel k-slices
 
 
 def tile64_supported(x: torch.Tensor, pc: PackedConv) -> bool:
     """Shapes K1t (``conv3x3_tile64``, csrc/kernels/conv_tile3x3.hip) takes: 3x3 / stride 1 / pad 1, bf16, 64 or 128
-    -> 64 channels (8 x 32 output tiles, H % 8 == 0) or 64 / 128 / 256 -> 128 channels (4 x 32 tiles, H % 4 == 0),
-    W % 32 == 0. AI4E_CONV_TILE64: "1" default, the 64-output-channel instances; "64" the 64 -> 64 instance only;
-    "0" off. The 128-output-channel instances are opt-in (AI4E_K1T_COUT128=1): correct, but the U-Net is 1.4 % slower
-    with them than with K1 at level 1 (profiles/r4_k1t/cout128/)."""
+    -> 64 channels (8 x 32 output tiles, H % 8 == 0, W % 32 == 0). AI4E_CONV_TILE64: "1" default; "64" the 64 -> 64
+    instance only; "0" off (K1 everywhere: the A/B reference). 128-output-channel instances were measured 1.4 % slower
+    than K1 at level 1 and removed (profiles/r4_k1t/cout128/, patch in profiles/r5_pruned/)."""
     n, h, w, c = x.shape
     # the 64-channel instances beat K1 (profiles/r4_k1t/: 558 vs 670 us and 829 vs 1022 us per conv over 16 tiles of
     # 512^2; U-Net 24.4 vs 22.5 mosaics/s with K1)
     mode = os.environ.get("AI4E_CONV_TILE64", "1")
-    if pc.cout == 128 and os.environ.get("AI4E_K1T_COUT128", "0") != "1":
-        return False
-    ok_c = (pc.cout == 64 and pc.cin_pad in (64, 128)) or (pc.cout == 128 and pc.cin_pad in (64, 128, 256))
+    ok_c = pc.cout == 64 and pc.cin_pad in (64, 128)
     return (mode != "0" and (mode != "64" or (c == 64 and pc.cout == 64)) and _ext.backend_for(x) == "hip"
             and x.dtype == torch.bfloat16 and pc.w_packed.dtype == torch.bfloat16 and (pc.kh, pc.kw) == (3, 3)
             and pc.stride == 1 and pc.pad == 1 and (pc.pad if pc.pad_hi is None else pc.pad_hi) == 1
@@ -259,24 +238,18 @@ def tile64_supported(x: torch.Tensor, pc: PackedConv) -> bool:
 
 
 def conv3x3_tile64(x: torch.Tensor, pc: PackedConv, pro: Optional[torch.Tensor] = None, pro_relu: bool = True,
-                   gn_groups: int = 0, up: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, Optional[tuple]]:
-    """K1t: ``conv3x3(pro(x)) + bias`` (see ``tile64_supported``), one 8 x 32 (cout 64) or 4 x 32 (cout 128) output
-    tile at a time per persistent workgroup from an LDS input patch. ``pro``: float32 [N, C, 2] per-(image, channel)
-    affine applied to the input as it is loaded (``x * a + b``, then ReLU with ``pro_relu``): the previous GroupNorm,
-    which then needs no apply pass (``norm.group_norm_affine``). Returns ``(y, stats)`` with ``stats`` =
-    ``(partials, nchunks)`` GroupNorm statistics of y (as ``conv2d_gn_nhwc``) when ``gn_groups``, else None.
-    ``up`` (128 -> 64 only, no ``pro``): a contiguous [N, H/2, W/2, 64] tensor whose bilinear 2x upsample
-    (align_corners=False) replaces input channels 64-127, formed per tile in LDS: x's channels 64-127 are not read,
-    so the upsampled half of a [skip | upsampled] concat need not be written."""
+                   gn_groups: int = 0) -> Tuple[torch.Tensor, Optional[tuple]]:
+    """K1t: ``conv3x3(pro(x)) + bias`` (see ``tile64_supported``), one 8 x 32 output tile at a time per persistent
+    workgroup from an LDS input patch. ``pro``: float32 [N, C, 2] per-(image, channel) affine applied to the input as
+    it is loaded (``x * a + b``, then ReLU with ``pro_relu``): the previous GroupNorm, which then needs no apply pass
+    (``norm.group_norm_affine``). Returns ``(y, stats)`` with ``stats`` = ``(partials, nchunks)`` GroupNorm
+    statistics of y (as ``conv2d_gn_nhwc``) when ``gn_groups``, else None."""
     n, h, w, c = x.shape
     if not tile64_supported(x, pc):
         raise ValueError("conv3x3_tile64: unsupported shape / dtype / layout")
     if pro is not None and (pro.dtype != torch.float32 or not pro.is_contiguous() or tuple(pro.shape) != (n, c, 2)):
         raise ValueError(f"conv3x3_tile64: pro must be contiguous float32 [N, {c}, 2]")
     cout = pc.cout
-    if up is not None and (c != 128 or cout != 64 or pro is not None or up.dtype != torch.bfloat16
-                           or not up.is_contiguous() or tuple(up.shape) != (n, h // 2, w // 2, 64) or h % 2 or w % 2):
-        raise ValueError("conv3x3_tile64: up needs the 128 -> 64 conv, no prologue, a contiguous bf16 [N, H/2, W/2, 64]")
     ldx = x.stride(2)
     xoff = x.storage_offset()
     base = x.untyped_storage().data_ptr() + 2 * (xoff - xoff % ldx)
@@ -287,18 +260,8 @@ def conv3x3_tile64(x: torch.Tensor, pc: PackedConv, pro: Optional[torch.Tensor] 
         partials = torch.empty(n * nchunks * gn_groups * 4 + n * cout * 2, device=x.device, dtype=torch.float32)
     _ext.call("ai4e_conv3x3_tile_fwd", base, pc.w_packed.data_ptr(), pc.bias.data_ptr(), _ext.ptr(pro),
               int(pro_relu), out.data_ptr(), n, h, w, c, cout, ldx, xoff % ldx, pc.kpad, cout, 0, _ext.ptr(partials),
-              gn_groups, _ext.ptr(up), _ext.stream_ptr(x.device))
+              gn_groups, _ext.stream_ptr(x.device))
     return out, ((partials, nchunks) if gn_groups else None)
-
-
-def linear_nhwc(x: torch.Tensor, pc: PackedConv, relu: bool = False) -> torch.Tensor:
-    """A 1x1 conv on [M, 1, 1, C] rows (a fully connected layer) as a plain library GEMM (hipBLASLt via
-    ``F.linear``) on the GPU: large-K FCs (the detector's box head, K = 12544) where the library's split-K /
-    stream-K tilings beat K1's fixed tile grid. Returns [M, 1, 1, Cout] bf16; other backends use K1."""
-    if not (x.is_cuda and _ext.backend_for(x) == "hip" and x.dtype == torch.bfloat16 and pc.kh == 1 and pc.kw == 1
-            and x.shape[1] == 1 and x.shape[2] == 1 and x.shape[-1] == pc.cin_pad):
-        return conv2d_nhwc(x, pc, relu=relu)
-    return _pointwise_blas(x.contiguous(), pc, relu)
 
 
 def chain_kernel_builds(mid: int, midn: int = 0) -> bool:
@@ -411,7 +374,7 @@ def pair_route(mid: int, c4: int, midn: int) -> bool:
     if not PAIR or not pair_supported(mid, c4, midn):
         return False
     if mid == 128:
-        return PAIR_B
+        return False  # the last layer2 block stays a K1c chain (K1 3x3 + K1p measured slower, removed in round 5)
     if mid == 512:
         return PAIR_L4
     return midn == mid or PAIR_X
@@ -463,15 +426,12 @@ PAIR_L4 = os.environ.get("AI4E_PAIR_L4", "0") not in ("0", "off", "")
 # the last layer3 block's c3 + residual with layer4's first (512-wide) c1, opt-in (AI4E_PAIR_X=1): 110 vs 124 us in
 # isolation, but -1 to -7 % images/s in the serving worker (profiles/r2_pair/README.md)
 PAIR_X = os.environ.get("AI4E_PAIR_X", "0") not in ("0", "off", "")
-# the last layer2 block as a K1 3x3 + K1p (c3 + residual + layer3's first c1) instead of the K1c chain + a K1 c1
-# (AI4E_PAIR_B=1)
-PAIR_B = os.environ.get("AI4E_PAIR_B", "0") not in ("0", "off", "")
 
 
 # K1c tile config per bottleneck width: 3 = 128-pixel tiles with phase A from the LDS input patch wherever the
 # shape allows it (stride 1, patch fits), else the LDS-DMA ring (bench/chain_patch_ab.py: layer1 chains 14-17 %,
-# layer2 6 % faster at batch 250); AI4E_CHAIN_TILE64 / AI4E_CHAIN_TILE128 = 1 / 0 for the ring everywhere
-CHAIN_TILE = {64: int(os.environ.get("AI4E_CHAIN_TILE64", "3")), 128: int(os.environ.get("AI4E_CHAIN_TILE128", "3"))}
+# layer2 6 % faster at batch 250); conv_chain(tile_cfg=0) runs the ring everywhere (the A/B reference and its tests)
+CHAIN_TILE = {64: 3, 128: 3}
 
 # K1s variant: 0 = direct conv from the LDS input footprint (default), 1 = DMA-gather implicit GEMM
 STEM_VARIANT = int(os.environ.get("AI4E_STEM_VARIANT", "0"))

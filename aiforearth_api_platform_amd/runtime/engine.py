@@ -144,30 +144,8 @@ class InferenceEngine:
         self._graph_out: Dict[Tuple[int, int], Tuple[torch.Tensor, ...]] = {}
         self.compute_done: List[Optional[torch.cuda.Event]] = [None] * self.nbuf
         self._k = 0
-        # phase-offset split (AI4E_ENGINE_SPLIT=1, output_fn.split = (front, back)): two graphs per (buffer, bucket);
-        # batch k+1's front waits for batch k's front, so the compute streams pair a front with a back
-        sp = getattr(output_fn, "split", None) if cuda and len(self.compute_streams) > 1 else None
-        self.split = sp if sp is not None and os.environ.get("AI4E_ENGINE_SPLIT", "0") not in ("0", "off", "") else None
-        self.graphs2: Dict[Tuple[int, int], torch.cuda.CUDAGraph] = {}
-        self._mid: Dict[Tuple[int, int], Tuple[torch.Tensor, ...]] = {}
-        self._front_done: Optional[torch.cuda.Event] = None
-        # CU-partitioned pipeline (AI4E_ENGINE_CU_SPLIT=F, needs output_fn.split): the front graph of every batch
-        # replays on a stream masked to F CUs (the same share of every XCD), the back graph on a stream masked to
-        # the other CUs, so batch k+1's front and batch k's back run side by side on disjoint CUs instead of taking
-        # turns on all of them. Off by default: for ResNet-50 both halves scale with their CU count, so every
-        # split measured below two full-chip streams (runtime/cu_partition.py, profiles/r3_cusplit/)
-        self.cu_split = int(os.environ.get("AI4E_ENGINE_CU_SPLIT", "0")) if sp is not None else 0
-        self.front_stream = self.back_stream = None
-        if self.cu_split > 0:
-            from . import cu_partition as cup
-            total = cup.cu_count(self.device)
-            if not 0 < self.cu_split < total:
-                raise ValueError(f"AI4E_ENGINE_CU_SPLIT={self.cu_split}: need 0 < F < {total}")
-            fcus = cup.balanced(self.cu_split, cup.xcc_of_cus(self.device))
-            fset = set(fcus)
-            self.front_stream = cup.masked_stream(fcus, self.device)
-            self.back_stream = cup.masked_stream([c for c in range(total) if c not in fset], self.device)
-            self.split = sp
+        # (measured and removed in round 5: the phase-offset front/back split and the CU-partitioned pipeline,
+        # both slower than two full-chip streams; profiles/r3_cusplit/, patches in profiles/r5_pruned/)
 
     # -------------------------------------------------------------- forward
     def _forward_into(self, buf: int, b: int) -> Tuple[torch.Tensor, ...]:
@@ -209,18 +187,8 @@ class InferenceEngine:
         for buf in range(self.nbuf):
             for b in self.buckets:
                 g = torch.cuda.CUDAGraph()
-                if self.split is not None:
-                    front, back = self.split
-                    with torch.cuda.graph(g, stream=self.compute_stream):
-                        mid = tuple(front(self.inputs[buf][:b]))
-                    g2 = torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(g2, stream=self.compute_stream):
-                        outs = tuple(back(*mid))
-                    self._mid[(buf, b)] = mid  # keeps the front graph's outputs alive for the back graph
-                    self.graphs2[(buf, b)] = g2
-                else:
-                    with torch.cuda.graph(g, stream=self.compute_stream):
-                        outs = self._forward_into(buf, b)
+                with torch.cuda.graph(g, stream=self.compute_stream):
+                    outs = self._forward_into(buf, b)
                 self.graphs[(buf, b)] = g
                 self._graph_out[(buf, b)] = outs
         torch.cuda.synchronize(self.device)
@@ -255,38 +223,10 @@ class InferenceEngine:
         ev.record(cs)
         if self.timing:
             ev1 = ev
-        if self.front_stream is not None and self.use_graphs and (buf, b) in self.graphs2:
-            # CU-partitioned pipeline: front on its CUs, back on the rest; the copy into `buf` already waited for
-            # this buffer's previous back (compute_done), which also frees the front graph's outputs (mid)
-            sf, st = self.front_stream, self.back_stream
-            sf.wait_event(ev)
-            with torch.cuda.stream(sf):
-                self.graphs[(buf, b)].replay()
-            fe = torch.cuda.Event()
-            fe.record(sf)
-            st.wait_event(fe)
-            with torch.cuda.stream(st):
-                self.graphs2[(buf, b)].replay()
-                outs = self._graph_out[(buf, b)]
-                host = self.host_out[buf]
-                for h, o in zip(host, outs):
-                    h[:n].copy_(o[:n], non_blocking=True)
-                done = torch.cuda.Event(enable_timing=self.timing)
-                done.record(st)
-            self.compute_done[buf] = done
-            return BatchResult([h[:n] for h in self.host_out[buf]], done, n, t_launch, ev0, ev1)
         st = self.compute_streams[buf % len(self.compute_streams)]
         st.wait_event(ev)
         with torch.cuda.stream(st):
-            if self.use_graphs and (buf, b) in self.graphs2:
-                if self._front_done is not None:
-                    st.wait_event(self._front_done)
-                self.graphs[(buf, b)].replay()
-                self._front_done = torch.cuda.Event()
-                self._front_done.record(st)
-                self.graphs2[(buf, b)].replay()
-                outs = self._graph_out[(buf, b)]
-            elif self.use_graphs and (buf, b) in self.graphs:
+            if self.use_graphs and (buf, b) in self.graphs:
                 self.graphs[(buf, b)].replay()
                 outs = self._graph_out[(buf, b)]
             else:

@@ -99,14 +99,6 @@ class ClassifierServable(Servable):
         self.outputs = [OutputField("classes", "int32", (self.topk,)), OutputField("probabilities", "float32",
                                                                                    (self.topk,))]
 
-    @property
-    def split(self):
-        """(front, back) parts for the engine's phase-offset graphs, when the model has them."""
-        m = self.model
-        if self.head is None or not hasattr(m, "front_u8") or not m.can_split():
-            return None
-        return m.front_u8, lambda *mid: m.back_topk(*mid, k=self.topk)
-
     def __call__(self, images_u8: torch.Tensor):
         if self.head is not None:
             i, p = self.head(images_u8, self.topk)

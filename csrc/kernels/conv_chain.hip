@@ -57,14 +57,9 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 // * patch rows are padded to W + 8 slots (row stride = W mod 8), so 16 consecutive pixels read 16 consecutive slots mod 8
 //   even where a fragment wraps to the next image row, and a masked tap reads a zero slot of the same residue mod 8
 //   instead of slot 0 (both were 2-way conflicts on the patch reads of phase A).
-// phase-A weight K steps prefetched into registers (patch mode), MID 128 / MID 64 (the MID-64 chains stay at 144
-// VGPRs and 3 workgroups per CU up to 8; deeper MID-128 prefetch spills)
-#ifndef AI4E_CHAIN_PD
-#define AI4E_CHAIN_PD 4
-#endif
-#ifndef AI4E_CHAIN_PD64
-#define AI4E_CHAIN_PD64 4
-#endif
+// phase-A weight K steps prefetched into registers (patch mode): 4 (6 / 8 were neutral on the MID-64 chains,
+// profiles/r4_chain_pd/; deeper MID-128 prefetch spills)
+constexpr int CHAIN_PD = 4;
 __device__ __forceinline__ int swt(int r) {
   const int x = (r >> 1) & 3;
   return x ^ (x >> 1);
@@ -94,6 +89,11 @@ __device__ __forceinline__ uint4 relu8(const f32x4_t& a, const f32x4_t& b) {
 // epilogue, the passes, the T1' epilogue + copy-out), per wave, written to g_chain_stamps (read SHARES only).
 #ifndef AI4E_CHAIN_STAMPS
 #define AI4E_CHAIN_STAMPS 0
+#endif
+// Diagnostic what-if builds (wrong numerics, timing only; tools/chain_stamps.py): 1 = phase A without its per-step
+// weight loads (the K-loop reuses the first PD prefetched steps), 2 = no patch DMA (phase A reads whatever is in LDS)
+#ifndef AI4E_CHAIN_WHATIF
+#define AI4E_CHAIN_WHATIF 0
 #endif
 constexpr int CHAIN_NSEG = 5, CHAIN_MAXW = 65536;
 #if AI4E_CHAIN_STAMPS
@@ -232,20 +232,16 @@ __device__ __forceinline__ uint32_t tile_off16(int r, int c) {
 
 // Measured and removed (profiles/r3_rreg/; code in the git history up to commit bc1ff0a): the residual chunk
 // prefetched into registers a pass ahead (tile configs 9 / 11), bit-identical but -2 % end to end.
-// PWN (patch mode): waves along the output channels in phase A (4 = every wave all BM pixels x MID/4 channels;
-// 2 = a 2 x 2 split: half the pixels x half the channels, half the LDS pixel reads per MFMA for twice the weight
-// fragments from L2).
-// PAD (patch mode, tile config + 32): pixel slots padded to RB + 32 bytes and NOT swizzled: the padding gives the
-// same bank-conflict profile as the XOR swizzle (2-way on about half the fragment reads, bench model), and a
-// fragment's address becomes slot * RBS + 16 * lg per tap with the K step as the ds_read immediate, instead of a
-// per-step XOR + shift + add per fragment (the chain kernels issue ~4-8 VALU per MFMA; PMC, profiles/r3_pad/).
-template <int MID, int BM_, int MIDN, bool DOWN, int ST, bool BL, bool PATCH, int PWN_ = 4,
-          bool PAD = false, bool F16 = false>
+// Phase A in patch mode: every wave computes all BM pixels x MID/4 output channels (PWN = 4 waves along the channels).
+// Measured and removed in round 5 (patches in profiles/r5_pruned/): a 2 x 2 phase-A split (PWN 2, neutral,
+// profiles/r3_pw2/), padded unswizzled patch slots (neutral, profiles/r3_pad/), the SGPR lane-select biases of the
+// round-2 kernel (the A/B reference of the LDS / ring-borne biases) and 256-pixel MID-64 ring tiles.
+template <int MID, int BM_, int MIDN, bool DOWN, int ST, bool BL, bool PATCH, bool F16 = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ChainCfg<MID, BM_, MIDN, DOWN, ST, BL>::MINW,
                                                                      ChainCfg<MID, BM_, MIDN, DOWN, ST, BL>::MINW)))
 void conv_chain_kernel(const ChainParams p) {
   using Cfg = ChainCfg<MID, BM_, MIDN, DOWN, ST, BL>;
-  static_assert(!PATCH || BM_ == 128, "patch mode: 128-pixel tiles (2 x 2 waves of 64 pixels)");
+  static_assert(BM_ == 128, "128-pixel tiles (patch mode: 4 waves x all pixels; ring: 2 x 2 waves of 64 pixels)");
   constexpr bool NEXT = Cfg::NEXT;
   constexpr int FIC = Cfg::FIC, WPXC = Cfg::WPXC, CBC = Cfg::CBC;
   constexpr int WM = Cfg::WM, BM = Cfg::BM, STAGES = Cfg::STAGES, CA = Cfg::CA, CB = Cfg::CB;
@@ -298,7 +294,7 @@ void conv_chain_kernel(const ChainParams p) {
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   // patch mode: the 4 waves split the channels (each all BM pixels = PFI fragments x MID/4 channels = CF
   // fragments), so every weight element is loaded by exactly one wave
-  constexpr int PWN = PWN_, PWM = 4 / PWN_;
+  constexpr int PWN = 4, PWM = 1;
   constexpr int PFI = PATCH ? BM_ / 16 / PWM : 1, CF = PATCH ? MID / 16 / PWN : 1;
   const int pwm = wave % PWM, pwn = wave / PWM;
   f32x4_t pacc[PFI][CF];
@@ -309,32 +305,14 @@ void conv_chain_kernel(const ChainParams p) {
   if constexpr (PATCH) {
     constexpr int RB = MID * 2;    // bytes per pixel slot
     constexpr int CPS = RB / 16;   // 16-B chunks per slot
-    constexpr int RBS = PAD ? RB + 32 : RB;  // slot stride
-    const int W = p.W, W2 = PAD ? p.W + 2 : p.pw2;
+    const int W = p.W, W2 = p.pw2;
     const int NZ = W2 - W;   // zero slots per patch row: slot 0 and W + 1 .. W2 - 1
     const int r_lo = m0 / W;                          // flattened (image, row) index of the first pixel
     const int r_hi = (min(m0 + BM, p.M) - 1) / W;
     const int prows = r_hi - r_lo + 3;                // + one halo row above and below
     const int nrows = p.M / W;                        // N * H
     const int ipr = W * RB / 1024;                    // 1-KB DMA pieces per patch row (host: W * RB % 1024 == 0)
-    if constexpr (PAD) {
-      // padded rows: slot k of patch row j at (j * W2 + k) * RBS, slots 0 and W + 1 and the pad bytes from the zero
-      // chunk; one 1-KB DMA piece per wave instruction, the lanes past the row's end masked off
-      const int rowb = W2 * RBS;
-      const int ipr2 = (rowb + 1023) / 1024;
-      for (int I = wave; I < prows * ipr2; I += 4) {
-        const int j = I / ipr2, piece = I - j * ipr2;
-        const int R = r_lo - 1 + j;
-        const int o = piece * 1024 + 16 * lane;
-        if (o < rowb) {
-          const int k = o / RBS;                      // slot in the row (compile-time divisor)
-          const int pos = (o - k * RBS) >> 4;         // 16-B chunk in the slot (>= CPS: pad)
-          const bool ok = R >= 0 && R < nrows && k >= 1 && k <= W && pos < CPS;
-          glds16(ok ? static_cast<const void*>(p.x + (static_cast<long>(R) * W + k - 1) * p.ldx + 8 * pos) : zero,
-                 sb + j * rowb + piece * 1024);
-        }
-      }
-    } else {
+    {
       // the patch: row j = flattened row r_lo - 1 + j, data in slots 1..W (one contiguous 1-KB piece per wave DMA)
       for (int I = wave; I < prows * ipr; I += 4) {
         const int j = I / ipr, piece = I - j * ipr;
@@ -344,8 +322,9 @@ void conv_chain_kernel(const ChainParams p) {
         const int slot = j * W2 + 1 + s1;
         const int q = ((o % RB) >> 4) ^ psw<MID>(slot);  // logical chunk that belongs at this physical chunk
         const bool ok = R >= 0 && R < nrows;
-        glds16(ok ? static_cast<const void*>(p.x + (static_cast<long>(R) * W + s1) * p.ldx + 8 * q) : zero,
-               sb + (j * W2 + 1) * RB + piece * 1024);
+        if (AI4E_CHAIN_WHATIF != 2)
+          glds16(ok ? static_cast<const void*>(p.x + (static_cast<long>(R) * W + s1) * p.ldx + 8 * q) : zero,
+                 sb + (j * W2 + 1) * RB + piece * 1024);
       }
       // zero pad slots (left / right of every row; with NZ = 8 the slots W + 1 .. W + 8 (= slot 0 of the next row)
       // hold one zero slot per residue mod 8, the source of masked taps; else slot 0)
@@ -373,7 +352,7 @@ void conv_chain_kernel(const ChainParams p) {
     }
     constexpr int SPT = MID / 32;   // K steps per tap
     constexpr int NKA = 9 * SPT;
-    constexpr int PD = MID == 64 ? AI4E_CHAIN_PD64 : AI4E_CHAIN_PD;  // weight K steps prefetched into registers
+    constexpr int PD = CHAIN_PD;  // weight K steps prefetched into registers
     const uint16_t* const wp = p.w2 + static_cast<long>(pwn * (MID / PWN) + (lane & 15)) * p.kpad2 + 8 * lg;
     bf16x8_t wr[PD][CF];
 #pragma unroll
@@ -390,24 +369,16 @@ void conv_chain_kernel(const ChainParams p) {
 #pragma unroll
       for (int i = 0; i < PFI; ++i) {
         const int s0 = sbase[i] + kh * W2 + kw;
-        const int slot = (vmask[i] >> kh) & 1 ? s0 : (!PAD && NZ == 8 ? W + 1 + ((s0 - W - 1) & 7) : 0);
-        if constexpr (PAD) {
-          soff[i] = slot * RBS + 16 * lg;
-        } else {
-          soff[i] = slot * RB;
-          sws[i] = psw<MID>(slot);
-        }
+        const int slot = (vmask[i] >> kh) & 1 ? s0 : (NZ == 8 ? W + 1 + ((s0 - W - 1) & 7) : 0);
+        soff[i] = slot * RB;
+        sws[i] = psw<MID>(slot);
       }
     };
     auto read_px = [&](int s, bf16x8_t (&f)[PFI]) __attribute__((always_inline)) {
       const int q = (s % SPT) * 4 + lg;
 #pragma unroll
       for (int i = 0; i < PFI; ++i) {
-        if constexpr (PAD) {
-          f[i] = *reinterpret_cast<const bf16x8_t*>(smem + soff[i] + (s % SPT) * 64);
-        } else {
-          f[i] = *reinterpret_cast<const bf16x8_t*>(smem + soff[i] + ((q ^ sws[i]) << 4));
-        }
+        f[i] = *reinterpret_cast<const bf16x8_t*>(smem + soff[i] + ((q ^ sws[i]) << 4));
       }
     };
     tap_slots(0);
@@ -423,11 +394,13 @@ void conv_chain_kernel(const ChainParams p) {
 #pragma unroll
         for (int j = 0; j < CF; ++j)
           pacc[i][j] = mfma_16x16x32<F16>(wr[s % PD][j], fx[s & 1][i], pacc[i][j]);
+#if AI4E_CHAIN_WHATIF != 1  // what-if 1 (diagnostic, wrong numerics): no phase-A weight loads inside the K-loop
       if (s + PD < NKA) {
 #pragma unroll
         for (int j = 0; j < CF; ++j)
           wr[s % PD][j] = *reinterpret_cast<const bf16x8_t*>(wp + j * 16L * p.kpad2 + (s + PD) * 32);
       }
+#endif
     }
     lds_barrier();  // every wave finished reading the patch before phases B/C reuse the LDS
   } else {
@@ -811,40 +784,37 @@ void conv_chain_kernel(const ChainParams p) {
 // Patch mode (phase A from an LDS patch of the input rows) applies to stride 1, an input row of whole 1-KB
 // DMA pieces, a dense [N, H, W, MID] input, 128-pixel tiles and a patch that fits the config's LDS.
 // Returns the patch row stride in slots (W + 8 where that fits, else W + 2), 0 = no patch mode.
-template <int MID, int BM, bool PAD = false>
+template <int MID, int BM>
 int patch_fits(const ChainParams& p, int lds_bytes) {
-  if (BM != 128 || p.stride != 1 || p.ldx != MID || (!PAD && (p.W * MID * 2) % 1024)) return 0;
+  if (BM != 128 || p.stride != 1 || p.ldx != MID || (p.W * MID * 2) % 1024) return 0;
   const long rows = (BM - 1 + p.W - 1) / p.W + 1 + 2;  // most rows BM consecutive pixels touch, + 2 halo rows
-  const long rb = MID * 2 + (PAD ? 32 : 0);
-  if (!PAD && rows * (p.W + 8) * rb <= lds_bytes) return p.W + 8;
+  const long rb = MID * 2;
+  if (rows * (p.W + 8) * rb <= lds_bytes) return p.W + 8;
   return rows * (p.W + 2) * rb <= lds_bytes ? p.W + 2 : 0;
 }
 
-template <int MID, int BM, int MIDN, bool DOWN = false, int ST = 4, bool BL = true, int PWN = 4,
-          bool PAD = false, bool F16 = false>
+template <int MID, int MIDN, bool DOWN = false, bool F16 = false>
 int launch_chain(ChainParams p, hipStream_t s, bool patch = false) {
+  constexpr int BM = 128, ST = 4;
+  constexpr bool BL = true;
   using Cfg = ChainCfg<MID, BM, MIDN, DOWN, ST, BL>;
   static bool attr = false;
   if (!attr) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(conv_chain_kernel<MID, BM, MIDN, DOWN, ST, BL, false, 4, false, F16>),
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(conv_chain_kernel<MID, BM, MIDN, DOWN, ST, BL, false, F16>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, Cfg::LDS_ALL) != hipSuccess)
       return AI4E_ELAUNCH;
-    if constexpr (BM == 128) {
-      if (hipFuncSetAttribute(reinterpret_cast<const void*>(conv_chain_kernel<MID, BM, MIDN, DOWN, ST, BL, true, PWN, PAD, F16>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, Cfg::LDS_ALL) != hipSuccess)
-        return AI4E_ELAUNCH;
-    }
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(conv_chain_kernel<MID, BM, MIDN, DOWN, ST, BL, true, F16>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, Cfg::LDS_ALL) != hipSuccess)
+      return AI4E_ELAUNCH;
     attr = true;
   }
   const int nb = ai4e_cdiv(p.M, Cfg::BM);
-  if constexpr (BM == 128) {
-    if (patch && (p.pw2 = patch_fits<MID, BM, PAD>(p, Cfg::LDS)) > 0) {
-      hipLaunchKernelGGL((conv_chain_kernel<MID, BM, MIDN, DOWN, ST, BL, true, PWN, PAD, F16>), dim3(nb), dim3(256), Cfg::LDS_ALL,
-                         s, p);
-      return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
-    }
+  if (patch && (p.pw2 = patch_fits<MID, BM>(p, Cfg::LDS)) > 0) {
+    hipLaunchKernelGGL((conv_chain_kernel<MID, BM, MIDN, DOWN, ST, BL, true, F16>), dim3(nb), dim3(256), Cfg::LDS_ALL,
+                       s, p);
+    return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
   }
-  hipLaunchKernelGGL((conv_chain_kernel<MID, BM, MIDN, DOWN, ST, BL, false, 4, false, F16>), dim3(nb), dim3(256),
+  hipLaunchKernelGGL((conv_chain_kernel<MID, BM, MIDN, DOWN, ST, BL, false, F16>), dim3(nb), dim3(256),
                      Cfg::LDS_ALL, s, p);
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
 }
@@ -861,14 +831,12 @@ namespace {
 // fp16 (the ensemble's crop classifier, v_mfma_f32_16x16x32_f16): the default 128-pixel tiles with phase A from the
 // LDS patch where the shape allows it, else the LDS-DMA ring; no A/B reference configs
 int chain_f16(const ChainParams& p, bool down, bool next, int mid, int midn, hipStream_t stream) {
-  if (down) return launch_chain<64, 128, 64, true, 4, true, 4, false, true>(p, stream, true);
+  if (down) return launch_chain<64, 64, true, true>(p, stream, true);
   if (mid == 64) {
-    if (next && midn == 128) return launch_chain<64, 128, 128, false, 4, true, 4, false, true>(p, stream, true);
-    return next ? launch_chain<64, 128, 64, false, 4, true, 4, false, true>(p, stream, true)
-                : launch_chain<64, 128, 0, false, 4, true, 4, false, true>(p, stream, true);
+    if (next && midn == 128) return launch_chain<64, 128, false, true>(p, stream, true);
+    return next ? launch_chain<64, 64, false, true>(p, stream, true) : launch_chain<64, 0, false, true>(p, stream, true);
   }
-  return next ? launch_chain<128, 128, 128, false, 4, true, 4, false, true>(p, stream, true)
-              : launch_chain<128, 128, 0, false, 4, true, 4, false, true>(p, stream, true);
+  return next ? launch_chain<128, 128, false, true>(p, stream, true) : launch_chain<128, 0, false, true>(p, stream, true);
 }
 
 int chain_fwd(bool f16, const void* x, const void* w2, const void* b2, const void* w3, const void* b3,
@@ -912,38 +880,15 @@ int chain_fwd(bool f16, const void* x, const void* w2, const void* b2, const voi
   if (p.M <= 0) return AI4E_OK;
   const bool next = w1n != nullptr;
   if (f16) return chain_f16(p, down, next, mid, midn, stream);
-  // tile_cfg: 0 = default (MID 64: 256 pixels, MID 128: 128), 1 = 128-pixel MID-64 tile (48 KB LDS, 3 per CU),
-  // 2 = the 128-pixel tiles with the SGPR lane-select biases (A/B reference for the LDS / ring-borne biases),
-  // 3 = the 128-pixel tiles with phase A in patch mode where the shape allows it (else the ring, as 1);
-  const bool pw2 = (tile_cfg & 16) != 0 && (tile_cfg & 7) == 3 && mid == 64;  // + 16 (19): 2 x 2 phase-A split
-  const bool pad = (tile_cfg & 32) != 0 && (tile_cfg & 7) == 3 && mid == 128 && !down;  // + 32 (35): padded patch
-  tile_cfg &= 7;
-  const bool patch = tile_cfg == 3;
-  if (pad)
-    return next ? launch_chain<128, 128, 128, false, 4, true, 4, true>(p, stream, true)
-                : launch_chain<128, 128, 0, false, 4, true, 4, true>(p, stream, true);
-  if (pw2) {
-    if (down) return launch_chain<64, 128, 64, true, 4, true, 2>(p, stream, true);
-    if (next && midn == 128) return launch_chain<64, 128, 128, false, 4, true, 2>(p, stream, true);
-    return next ? launch_chain<64, 128, 64, false, 4, true, 2>(p, stream, true)
-                : launch_chain<64, 128, 0, false, 4, true, 2>(p, stream, true);
-  }
-  if (down) return tile_cfg == 2 ? launch_chain<64, 128, 64, true, 4, false>(p, stream)
-                                 : launch_chain<64, 128, 64, true>(p, stream, patch);
+  // tile_cfg: 3 = phase A from the LDS input patch where the shape allows it (stride 1, patch fits; the default),
+  // else (and for any other value) the LDS-DMA ring; 128-pixel tiles either way
+  const bool patch = (tile_cfg & 7) == 3;
+  if (down) return launch_chain<64, 64, true>(p, stream, patch);
   if (mid == 64) {
-    if (tile_cfg == 2) {  // A/B reference: the 128-pixel tile with the SGPR-select biases (no LDS staging)
-      if (next && midn == 128) return launch_chain<64, 128, 128, false, 4, false>(p, stream);
-      return next ? launch_chain<64, 128, 64, false, 4, false>(p, stream) : launch_chain<64, 128, 0, false, 4, false>(p, stream);
-    }
-    if (next && midn == 128) return launch_chain<64, 128, 128>(p, stream, patch);
-    if (tile_cfg == 1 || patch)
-      return next ? launch_chain<64, 128, 64>(p, stream, patch) : launch_chain<64, 128, 0>(p, stream, patch);
-    return next ? launch_chain<64, 256, 64>(p, stream) : launch_chain<64, 256, 0>(p, stream);
+    if (next && midn == 128) return launch_chain<64, 128>(p, stream, patch);
+    return next ? launch_chain<64, 64>(p, stream, patch) : launch_chain<64, 0>(p, stream, patch);
   }
-  if (tile_cfg == 2)  // A/B reference: SGPR-select biases
-    return next ? launch_chain<128, 128, 128, false, 4, false>(p, stream)
-                : launch_chain<128, 128, 0, false, 4, false>(p, stream);
-  return next ? launch_chain<128, 128, 128>(p, stream, patch) : launch_chain<128, 128, 0>(p, stream, patch);
+  return next ? launch_chain<128, 128>(p, stream, patch) : launch_chain<128, 0>(p, stream, patch);
 }
 }  // namespace
 

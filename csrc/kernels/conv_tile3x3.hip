@@ -1,63 +1,50 @@
 // K1t: 3x3 / stride 1 / pad 1 convolution, NHWC bf16, for wide feature maps: 64 / 128 -> 64 channels (the U-Net's
-// full-resolution level, 512^2 tiles; default) and 64 / 128 / 256 -> 128 channels (level 1; opt-in, slower than K1
-// there). At level 0 the K1 implicit GEMM gathers every tap of every pixel through the LDS-DMA ring (nine 16-B
-// gathers per pixel and 32-channel step) and ran at 23 % MFMA / 1.3 TB/s (profiles/r4_unet/pmc_by_kernel.txt).
+// full-resolution level, 512^2 tiles). At level 0 the K1 implicit GEMM gathers every tap of every pixel through the
+// LDS-DMA ring (nine 16-B gathers per pixel and 32-channel step) and ran at 23 % MFMA / 1.3 TB/s
+// (profiles/r4_unet/pmc_by_kernel.txt).
 //
-// Each output tile (8 x 32 for COUT 64, 4 x 32 for COUT 128) is computed by one workgroup (4 waves):
+// Each 8 x 32 output tile is computed by one workgroup (4 waves):
 // * the (TH + 2) x 34 x 64 input patch (halo 1, zero outside the image) is loaded ONCE into LDS (16-B chunks of a
 //   pixel slot XOR-swizzled for the real ds_read_b128 lane groups), optionally through a prologue: x * a[c] + b[c]
 //   (+ ReLU) per (image, channel) — the previous layer's GroupNorm apply, so that the normalized tensor is never
 //   written (its statistics came from the previous conv's epilogue);
 // * the nine taps then run as LDS-read + MFMA steps (v_mfma_f32_16x16x32_bf16; weights as the A operand, pixels as
-//   B; per wave 64 px x 64 ch or 32 px x 128 ch: 32 MFMAs per stage), the next tap's weights loaded from L2 during
+//   B; per wave 64 px x 64 ch: 32 MFMAs per stage), the next tap's weights loaded from L2 during
 //   the current tap into the other half of a two-tap LDS buffer;
 // * epilogue: + bias, bf16 store, and the GroupNorm statistics of the stored values per (image, tile, group) in the
 //   K1 conv-epilogue format (shifted sums S, Q and the shift K: norm_resample.hip gn_finalize_kernel).
 // CIN > 64: the same tiles, run as CIN / 64 k-slices through one 64-channel patch buffer (accumulators carried over).
-// UPS (128 -> 64, opt-in): the second k-slice is the bilinear 2x upsample of a coarse tensor, formed in LDS.
+// Measured and removed in round 5 (patches in profiles/r5_pruned/): 128-output-channel instances (-1.4 % on the
+// U-Net, profiles/r4_k1t/cout128/), weight stages by LDS-DMA (-2 %, profiles/r4_k1t/wdma/) and the 2x upsample formed
+// in LDS for the decoder c1 (neutral, profiles/r4_k1t/ups/).
 // Persistent: min(tiles, 2 x CUs) workgroups walk the tiles with stride gridDim.x. The next (tile, slice)'s patch is
 // loaded into registers while the current taps run (spread over the stages, so every vmcnt wait stays exact), and its
 // first weight stage while the epilogue runs, then stored into LDS (through the prologue) behind one barrier.
 // Every global address is inside its tensor by construction (host: H % TH == 0, W % 32 == 0; tile t < ntiles; patch
-// and coarse loads clamped to in-tensor pixels, out-of-image chunks zeroed in LDS).
-#include <cstdlib>
+// loads clamped to in-tensor pixels, out-of-image chunks zeroed in LDS).
 #include <type_traits>
 
 #include "common.h"
 #include "conv_common.h"
 
-// Build switch: weight stages by LDS-DMA (global_load_lds_dwordx4) into THREE stage buffers, issued two stages ahead
-// (no registers hold weights in flight; explicit counted vmcnt waits; the UPS instance keeps the register path: a
-// third buffer would not fit 80 KB). Off: 2 % slower end to end than the register path (profiles/r4_k1t/wdma/).
-#ifndef AI4E_K1T_WDMA
-#define AI4E_K1T_WDMA 0  // measured 2 % slower end to end (profiles/r4_k1t/wdma/): opt-in build switch
-#endif
-
 namespace {
 
 constexpr int T_W = 32, P_W = T_W + 2;           // output tile width; patch width with halo
 
-// COUT = 64: 8 x 32 output tiles from a 10 x 34 x 64-channel input patch (43.5 KB); COUT = 128 (the U-Net's level-1
-// convs): 4 x 32 tiles (a 6 x 34 patch, 26 KB), each wave 32 pixels x 128 channels, so a wave issues the same 32
-// MFMAs per stage from the same 64 accumulators. CIN = 128 / 256 (decoder c1s reading a [skip | upsampled] concat)
-// runs each tile as CIN / 64 k-slices through the same patch buffer: the accumulators carry over, the epilogue runs
-// once, and the next slice's patch is prefetched under the current slice's taps like the next tile's.
-// LDS: patch + CIN x 8 B affine + two COUT x 128 B weight stages + the bias; two workgroups per CU.
-// UPS (CIN 128 -> COUT 64 only): the second k-slice (input channels 64-127) is the bilinear 2x upsample (PyTorch
-// align_corners=False) of a coarse 64-channel tensor [N, H/2, W/2, 64], formed in LDS from its CR x CC coarse block
-// instead of read from a materialized [skip | upsampled] concat: the U-Net's level-0 decoder c1 then never needs the
-// upsampled half written (537 MB per 16 tiles of 512^2) nor reads it back.
-template <int CIN, int COUT, bool UPS = false>
+// 8 x 32 output tiles from a 10 x 34 x 64-channel input patch (43.5 KB). CIN = 128 (decoder c1s reading a
+// [skip | upsampled] concat) runs each tile as 2 k-slices through the same patch buffer: the accumulators carry over,
+// the epilogue runs once, and the next slice's patch is prefetched under the current slice's taps like the next tile's.
+// LDS: patch + CIN x 8 B affine + two 64 x 128 B weight stages + the bias; two workgroups per CU.
+template <int CIN, int COUT = 64>
 struct TileCfg {
-  static constexpr int TH = COUT == 64 ? 8 : 4;         // output tile rows
+  static constexpr int TH = 8;                          // output tile rows
   static constexpr int P_SLOTS = (TH + 2) * P_W;
   static constexpr int NCH = 8;                         // 16-B chunks per 64-channel pixel slot
   static constexpr int SLOT_B = 128;
   static constexpr int L_PATCH = P_SLOTS * SLOT_B;
   static constexpr int L_AFF = CIN * 8;                 // prologue affine of this image: CIN x (a, b)
   static constexpr int L_W = COUT * 128;                // one weight stage: COUT rows x 64 input channels of one tap
-  static constexpr bool WDMA = AI4E_K1T_WDMA && !UPS;
-  static constexpr int NWB = WDMA ? 3 : 2;              // weight stage buffers
+  static constexpr int NWB = 2;                         // weight stage buffers
   static constexpr int L_TOTAL = L_PATCH + L_AFF + NWB * L_W + COUT * 4;  // + the bias
   static constexpr int P_CHUNKS = P_SLOTS * NCH;
   static constexpr int P_ITERS = (P_CHUNKS + 255) / 256;
@@ -66,18 +53,11 @@ struct TileCfg {
   static constexpr int FPW = TH / 2;                    // pixel fragments per wave (TH / 4 rows x 2 half-rows)
   static constexpr int NJ = COUT / 16;                  // 16-channel output blocks per wave
   static constexpr int NWV = COUT / 32;                 // 16-B weight chunks per thread per stage
-  static constexpr int CR = TH / 2 + 2, CC = T_W / 2 + 3;  // UPS coarse block: rows h0/2 - 1 .., cols w0/2 - 1 ..
-  static constexpr int C_CHUNKS = CR * CC * 8;
-  static constexpr int C_ITERS = (C_CHUNKS + 255) / 256;
-  static constexpr int L_CO = UPS ? CR * CC * 128 : 0;
-  static constexpr int L_ALL = L_TOTAL + L_CO;
-  static_assert(!UPS || (CIN == 128 && COUT == 64), "UPS: the 128 -> 64 instance");
-  static_assert(L_ALL <= 80 * 1024, "two workgroups per CU (with the coarse block)");
-  static_assert(CIN == 64 || CIN == 128 || CIN == 256, "K1t: 64, 128 or 256 input channels");
-  static_assert(COUT == 64 || COUT == 128, "K1t: 64 or 128 output channels");
+  static constexpr int L_ALL = L_TOTAL;
+  static_assert(CIN == 64 || CIN == 128, "K1t: 64 or 128 input channels");
+  static_assert(COUT == 64, "K1t: 64 output channels");
   static_assert(L_TOTAL <= 80 * 1024, "two workgroups per CU");
   static_assert((COUT + 4 * COUT * 2) * 4 <= L_W, "GroupNorm scratch (shift + 4-wave sums) fits a weight stage");
-  static_assert((COUT + 4 * COUT * 2) * 4 <= L_PATCH, "... and the patch buffer (its home with WDMA)");
 };
 
 struct TileParams {
@@ -93,7 +73,6 @@ struct TileParams {
   float* gnp;              // GroupNorm partials [N, tiles per image, G, 4]; null = off
   int gn_groups;
   int H, W, tiles_w, tiles_per_img;
-  const uint16_t* xu;      // UPS: coarse [N, H / 2, W / 2, 64] (input channels 64-127 = its 2x upsample)
 };
 
 // Byte offset within its row of 16-B chunk c of row `row` (M = 8 chunks per row). ds_read_b128 is serviced in four
@@ -115,10 +94,10 @@ __device__ __forceinline__ uint32_t swz(int row, int c) {
 // in this kernel passes data between waves through global memory.
 __device__ __forceinline__ void tile_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-template <int CIN, int COUT, bool UPS = false>
+template <int CIN, int COUT = 64>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv3x3_tile_kernel(
     const TileParams p, int ntiles) {
-  using Cfg = TileCfg<CIN, COUT, UPS>;
+  using Cfg = TileCfg<CIN, COUT>;
   constexpr int NJ = Cfg::NJ, L_W = Cfg::L_W;
   constexpr int TH = Cfg::TH, P_CHUNKS = Cfg::P_CHUNKS, P_ITERS = Cfg::P_ITERS, NCH = Cfg::NCH, SLOT_B = Cfg::SLOT_B;
   constexpr int KS = Cfg::KS, NST = Cfg::NST, FPW = Cfg::FPW;
@@ -128,60 +107,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   uint8_t* const patch = sm;
   float2* const aff = reinterpret_cast<float2*>(sm + Cfg::L_PATCH);
   uint8_t* const wbuf = sm + Cfg::L_PATCH + Cfg::L_AFF;
-  constexpr bool WDMA = Cfg::WDMA;
   constexpr int NWB = Cfg::NWB;
   float* const sbias = reinterpret_cast<float*>(wbuf + NWB * L_W);  // [COUT]: epilogue reads stay off the vmcnt queue
-  uint8_t* const coarse = wbuf + NWB * L_W + COUT * 4;              // UPS: [CR x CC slots][128 B]
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g4 = lane >> 4;
 
   // one weight stage in flight: rows n = tid / 8 + 32 e (e < NWV), 16-B chunk tid % 8 (named registers: an array
   // indexed inside these lambdas was kept in scratch)
-  uint4 wv0, wv1, wv2, wv3;
+  uint4 wv0, wv1;
   auto load_w = [&](int tap, int ks) __attribute__((always_inline)) {  // stage = (tap, 64-channel k-slice)
-    int tq = tid;
-    // COUT 128: per-call address math (with one k-slice every stage's address is loop-invariant, and hoisting all 9
-    // out of the tile loop spills the 64 -> 128 instance); COUT 64 keeps the hoisted addresses (3-4 % faster)
-    if constexpr (COUT == 128) asm volatile("" : "+v"(tq));
+    const int tq = tid;  // (the hoisted per-stage addresses: 3-4 % faster than per-call address math)
     const uint16_t* const src = p.w + static_cast<long>(tq >> 3) * p.kpad + tap * CIN + ks * 64 + 8 * (tq & 7);
     wv0 = *reinterpret_cast<const uint4*>(src);
     wv1 = *reinterpret_cast<const uint4*>(src + 32L * p.kpad);
-    if constexpr (Cfg::NWV == 4) {
-      wv2 = *reinterpret_cast<const uint4*>(src + 64L * p.kpad);
-      wv3 = *reinterpret_cast<const uint4*>(src + 96L * p.kpad);
-    }
   };
   auto store_w = [&](int buf) __attribute__((always_inline)) {
     const int n = tid >> 3, c = tid & 7;
     uint8_t* const b = wbuf + buf * L_W;
     *reinterpret_cast<uint4*>(b + n * 128 + swz<8>(n, c)) = wv0;
     *reinterpret_cast<uint4*>(b + (n + 32) * 128 + swz<8>(n + 32, c)) = wv1;
-    if constexpr (Cfg::NWV == 4) {
-      *reinterpret_cast<uint4*>(b + (n + 64) * 128 + swz<8>(n + 64, c)) = wv2;
-      *reinterpret_cast<uint4*>(b + (n + 96) * 128 + swz<8>(n + 96, c)) = wv3;
-    }
-  };
-  // WDMA: the weight stage (tap, ks) straight into LDS buffer `buf`: wave w's instruction i fills rows
-  // (NWV w + i) * 8 .. + 7 (1 KB, base + 16 lane); the XOR swizzle is applied to the per-lane SOURCE chunk
-  // (physical chunk lane % 8 of row r holds logical chunk (lane % 8) ^ (r & 6), as swz<8>)
-  const uint32_t wlds = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(wbuf));
-  auto dma_w = [&](int tap, int ks, int buf) __attribute__((always_inline)) {
-    int lq = lane;
-    asm volatile("" : "+v"(lq));  // per-call address math (with one k-slice all 9 stages' addresses would be hoisted)
-#pragma unroll
-    for (int i = 0; i < Cfg::NWV; ++i) {
-      const int r = (Cfg::NWV * wave + i) * 8 + (lq >> 3);
-      const int c = (lq & 7) ^ (r & 6);
-      ai4e_conv::glds16(p.w + static_cast<long>(r) * p.kpad + tap * CIN + ks * 64 + 8 * c,
-                        wlds + buf * L_W + (Cfg::NWV * wave + i) * 1024);
-    }
   };
   // the patch of one tile: global -> registers (pv, in-image chunks in pmask), later registers -> LDS
   uint4 pv[P_ITERS];
   uint32_t pmask = 0;
-  auto load_patch = [&](int img, int h0, int w0, int ks, int k0, int k1, bool coarse_mode = false)
-                        __attribute__((always_inline)) {
+  auto load_patch = [&](int img, int h0, int w0, int ks, int k0, int k1) __attribute__((always_inline)) {
     const uint16_t* const xi = p.x + static_cast<long>(img) * p.H * p.W * p.ldx + p.xcoff + 64 * ks;
     int tq = tid;
     asm volatile("" : "+v"(tq));  // recompute the chunk address math per tile (hoisted, it spills)
@@ -198,15 +148,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       // store_patch zeroes the chunks outside the image
       const int ihc = min(max(ih, 0), p.H - 1), iwc = min(max(iw, 0), p.W - 1);
       const uint16_t* src = xi + (static_cast<long>(ihc) * p.W + iwc) * p.ldx + 8 * (c & 7);
-      if constexpr (UPS) {  // coarse-block chunk k (k < C_ITERS; beyond, a repeat of chunk 0), clamped in-tensor
-        const int ek = k < Cfg::C_ITERS ? e : tq;
-        const int cs = ek >> 3, cc8 = ek & 7;
-        const int cr = cs / Cfg::CC, ccol = cs - cr * Cfg::CC;
-        const int cy = min(max((h0 >> 1) - 1 + cr, 0), (p.H >> 1) - 1);
-        const int cx = min(max((w0 >> 1) - 1 + ccol, 0), (p.W >> 1) - 1);
-        const uint16_t* csrc = p.xu + ((static_cast<long>(img) * (p.H >> 1) + cy) * (p.W >> 1) + cx) * 64 + 8 * cc8;
-        src = coarse_mode ? csrc : src;
-      }
       pv[k] = *reinterpret_cast<const uint4*>(src);
     }
   };
@@ -239,62 +180,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       *reinterpret_cast<uint4*>(patch + slot * SLOT_B + swz<NCH>(slot, c)) = v;
     }
   };
-  // UPS: the coarse block of a tile (global -> the prefetch registers pv via load_patch, clamped in-tensor addresses;
-  // later -> LDS), then the fine
-  // 64-channel patch from it with upsample2x_kernel's exact arithmetic (norm_resample.hip)
-  constexpr int C_ITERS = Cfg::C_ITERS, CR = Cfg::CR, CC = Cfg::CC;
-  static_assert(!UPS || C_ITERS <= P_ITERS, "the coarse block reuses the patch prefetch registers");
-  const int Hc = p.H >> 1, Wc = p.W >> 1;
-  auto store_coarse = [&]() __attribute__((always_inline)) {
-#pragma unroll
-    for (int k = 0; k < C_ITERS; ++k) {
-      const int e = tid + 256 * k;
-      if (e >= Cfg::C_CHUNKS) continue;
-      const int slot = e >> 3, c = e & 7;
-      *reinterpret_cast<uint4*>(coarse + slot * 128 + swz<8>(slot, c)) = pv[k];
-    }
-  };
-  auto fine_from_coarse = [&](int h0, int w0) __attribute__((always_inline)) {
-    int tq = tid;
-    asm volatile("" : "+v"(tq));
-    const int cy0 = (h0 >> 1) - 1, cx0 = (w0 >> 1) - 1;
-#pragma unroll
-    for (int k = 0; k < P_ITERS; ++k) {
-      const int e = tq + 256 * k;
-      if (e >= P_CHUNKS) continue;
-      const int slot = e / NCH, c = e - slot * NCH;
-      const int pr = slot / P_W, pc = slot - pr * P_W;
-      const int ih = h0 - 1 + pr, iw = w0 - 1 + pc;
-      uint4 v = make_uint4(0u, 0u, 0u, 0u);  // the conv's zero padding outside the image
-      if (static_cast<unsigned>(ih) < static_cast<unsigned>(p.H) && static_cast<unsigned>(iw) < static_cast<unsigned>(p.W)) {
-        const float sy = fmaxf((ih + 0.5f) * 0.5f - 0.5f, 0.f), sx = fmaxf((iw + 0.5f) * 0.5f - 0.5f, 0.f);
-        const int y0 = static_cast<int>(sy), x0 = static_cast<int>(sx);
-        const int y1 = min(y0 + 1, Hc - 1), x1 = min(x0 + 1, Wc - 1);
-        const float ly = sy - y0, lx = sx - x0;
-        const float w00 = (1 - ly) * (1 - lx), w01 = (1 - ly) * lx, w10 = ly * (1 - lx), w11 = ly * lx;
-        const int s00 = (y0 - cy0) * CC + (x0 - cx0), s01 = (y0 - cy0) * CC + (x1 - cx0);
-        const int s10 = (y1 - cy0) * CC + (x0 - cx0), s11 = (y1 - cy0) * CC + (x1 - cx0);
-        const uint4 a = *reinterpret_cast<const uint4*>(coarse + s00 * 128 + swz<8>(s00, c));
-        const uint4 b = *reinterpret_cast<const uint4*>(coarse + s01 * 128 + swz<8>(s01, c));
-        const uint4 cq = *reinterpret_cast<const uint4*>(coarse + s10 * 128 + swz<8>(s10, c));
-        const uint4 d = *reinterpret_cast<const uint4*>(coarse + s11 * 128 + swz<8>(s11, c));
-        const uint32_t pa[4] = {a.x, a.y, a.z, a.w}, pb[4] = {b.x, b.y, b.z, b.w};
-        const uint32_t pcq[4] = {cq.x, cq.y, cq.z, cq.w}, pd[4] = {d.x, d.y, d.z, d.w};
-        uint32_t o[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          float a0, a1, b0, b1, c0, c1, d0, d1;
-          unpack_bf16x2(pa[q], a0, a1);
-          unpack_bf16x2(pb[q], b0, b1);
-          unpack_bf16x2(pcq[q], c0, c1);
-          unpack_bf16x2(pd[q], d0, d1);
-          o[q] = pack_bf16x2(w00 * a0 + w01 * b0 + w10 * c0 + w11 * d0, w00 * a1 + w01 * b1 + w10 * c1 + w11 * d1);
-        }
-        v = make_uint4(o[0], o[1], o[2], o[3]);
-      }
-      *reinterpret_cast<uint4*>(patch + slot * SLOT_B + swz<NCH>(slot, c)) = v;
-    }
-  };
   auto coords = [&](int t, int& img, int& tin, int& h0, int& w0) __attribute__((always_inline)) {
     img = t / p.tiles_per_img;
     tin = t - img * p.tiles_per_img;
@@ -308,25 +193,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   // after it (and after the tile's epilogue).
   int t = blockIdx.x, ks = 0, img, tin, h0, w0;
   coords(t, img, tin, h0, w0);
-  if constexpr (WDMA) {
-    dma_w(0, 0, 0);
-    dma_w(1, 0, 1);
-  } else {
-    load_w(0, 0);
-  }
+  load_w(0, 0);
   if (p.pro != nullptr && tid < CIN) aff[tid] = p.pro[img * CIN + tid];
   if (tid < COUT) sbias[tid] = p.bias[tid];
   pmask = 0;
   load_patch(img, h0, w0, 0, 0, P_ITERS);
-  if constexpr (WDMA) ai4e_conv::wait_vmcnt<0>();  // the first two weight stages landed
-  else store_w(0);
+  store_w(0);
   tile_barrier();  // the affine is in LDS
   store_patch(0);
   tile_barrier();
 
-  // GroupNorm scratch: the weight buffer 0, or (WDMA: the next item's weights are landing there during the epilogue)
-  // the patch buffer, dead between the last stage and the next item's patch store
-  float* const kshift = reinterpret_cast<float*>(WDMA ? patch : wbuf);  // [COUT] the tile's first pixel, as stored
+  // GroupNorm scratch: the weight buffer 0 (its next stage is stored behind the next barrier)
+  float* const kshift = reinterpret_cast<float*>(wbuf);  // [COUT] the tile's first pixel, as stored
   float* const red = kshift + COUT;                                    // [4 waves][COUT channels][2]
 
   f32x4_t acc[FPW][NJ];  // carried over the k-slices of a tile; zeroed here and after each tile's epilogue
@@ -355,25 +233,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     int sbase[FPW];
 #pragma unroll
     for (int f = 0; f < FPW; ++f) sbase[f] = ((TH / 4) * wave + (f >> 1)) * P_W + 16 * (f & 1) + l16;
-    // UPS: the next item is the coarse block when it is this tile's second slice; the loads stay on one code path
-    // (address chosen by select: a runtime branch around the loads would make the waits inexact)
-    const bool coarse_next = UPS && ksn == 1;
 #pragma unroll
     for (int st = 0; st < NST; ++st) {  // stage = tap
       // issue order is the wait order (vmcnt retires in order): this stage's weight chunks first, then PPS chunks
       // of the next (tile, slice)'s patch, which the waits of later stages cover; pinned against the scheduler,
       // which otherwise sinks the weight loads to their use at the end of the stage
-      if constexpr (WDMA) {  // two stages ahead: this item's stage st + 2, or the next item's stage st - 7
-        if (st + 2 < NST) dma_w(st + 2, ks, (st + 2) % 3);
-        else dma_w(st + 2 - NST, ksn, (st + 2) % 3);
-      } else if (st + 1 < NST) {
-        load_w(st + 1, ks);
-      }
+      if (st + 1 < NST) load_w(st + 1, ks);
       load_patch(imgn, h0n, w0n, ksn, st * PPS < P_ITERS ? st * PPS : P_ITERS,
-                 (st + 1) * PPS < P_ITERS ? (st + 1) * PPS : P_ITERS, coarse_next);
+                 (st + 1) * PPS < P_ITERS ? (st + 1) * PPS : P_ITERS);
       __builtin_amdgcn_sched_barrier(0);
       const int kh = st / 3, kw = st - 3 * kh;
-      const uint8_t* const wb = wbuf + (WDMA ? st % 3 : (st & 1)) * L_W;
+      const uint8_t* const wb = wbuf + (st & 1) * L_W;
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         const int wc = 4 * s + g4;  // chunk within the stage's 64 channels
@@ -393,19 +263,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
           for (int j = 0; j < NJ; ++j) acc[f][j] = mfma_16x16x32<false>(fw[j], fx[f], acc[f][j]);
       }
-      if constexpr (WDMA) {
-        // the next stage's weights (issued at stage st - 1, or before the loop / at the previous item's last stage
-        // for st = 0: then counted as if nothing older were pending, a stricter wait) are in LDS: at most the
-        // operations issued after them may be outstanding
-        constexpr int ND = Cfg::NWV;
-        auto pl = [](int q) { return q < 0 ? 0 : (q * PPS < P_ITERS ? ((q + 1) * PPS < P_ITERS ? PPS : P_ITERS - q * PPS) : 0); };
-        ai4e_conv::wait_vmcnt_n(st == 0 ? ND + pl(0) : pl(st - 1) + ND + pl(st));
-      } else if (st + 1 < NST) {
-        store_w((st + 1) & 1);  // that buffer was last read at stage st - 1 (before the previous barrier)
-      }
+      if (st + 1 < NST) store_w((st + 1) & 1);  // that buffer was last read at stage st - 1 (before the previous barrier)
       tile_barrier();
     }
-    if constexpr (!WDMA) load_w(0, ksn);  // the next slice's first weight stage, in flight under the epilogue
+    load_w(0, ksn);  // the next slice's first weight stage, in flight under the epilogue
 
     // ---- epilogue (after the tile's last slice): lane holds channels 16 j + 4 g4 + v of pixel (lane % 16) of
     // each fragment
@@ -492,15 +353,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     if (!has_next) break;
     tile_barrier();  // this slice's patch, weight stages and statistics scratch are read
     if (last_slice && p.pro != nullptr && tid < CIN) aff[tid] = p.pro[imgn * CIN + tid];
-    if constexpr (!WDMA) store_w(0);
-    if (UPS && ksn == 1) {
-      store_coarse();
-      tile_barrier();  // the coarse block is in LDS
-      fine_from_coarse(h0n, w0n);
-    } else {
-      tile_barrier();  // the next tile's affine is in LDS
-      store_patch(ksn);
-    }
+    store_w(0);
+    tile_barrier();  // the next tile's affine is in LDS
+    store_patch(ksn);
     tile_barrier();
     t = tn;
     ks = ksn;
@@ -515,49 +370,38 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 
 namespace {
 
-template <int CIN, int COUT, bool UPS = false>
+template <int CIN>
 int launch_tile(const TileParams& p, int N, hipStream_t stream) {
-  constexpr int L = TileCfg<CIN, COUT, UPS>::L_ALL;
+  constexpr int L = TileCfg<CIN>::L_ALL;
   static bool attr = [] {
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(conv3x3_tile_kernel<CIN, COUT, UPS>),
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(conv3x3_tile_kernel<CIN>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, L) == hipSuccess;
   }();
   if (!attr) return AI4E_ELAUNCH;
-  // persistent grid: two workgroups per CU (LDS), never more workgroups than tiles; AI4E_K1T_PERSIST=0 launches one
-  // workgroup per tile (no next tile, so no prefetch: the A/B reference)
-  static const bool persist = [] {
-    const char* e = std::getenv("AI4E_K1T_PERSIST");
-    return !(e && e[0] == '0');
-  }();
+  // persistent grid: two workgroups per CU (LDS), never more workgroups than tiles
   int dev = 0, cus = 0;
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
     return AI4E_ELAUNCH;
   const int ntiles = N * p.tiles_per_img;
-  const int grid = persist && ntiles > 2 * cus ? 2 * cus : ntiles;
-  hipLaunchKernelGGL((conv3x3_tile_kernel<CIN, COUT, UPS>), dim3(static_cast<unsigned>(grid)), dim3(256), L, stream, p, ntiles);
+  const int grid = ntiles > 2 * cus ? 2 * cus : ntiles;
+  hipLaunchKernelGGL((conv3x3_tile_kernel<CIN>), dim3(static_cast<unsigned>(grid)), dim3(256), L, stream, p, ntiles);
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
 }
 
 }  // namespace
 
-// y = conv3x3(pro(x)) + bias (cin 64 / 128 -> 64 channels, or cin 64 / 128 / 256 -> 128 channels; stride 1, pad 1)
-// with GroupNorm partials of y (gn_groups > 0): [N, (H / TH) * (W / 32), G, 4], TH = 8 (cout 64) or 4 (cout 128).
-// pro: null or float2 [N, cin] (x * a + b, then ReLU if pro_relu).
-// xu (UPS): null, or a contiguous coarse [N, H / 2, W / 2, 64] tensor whose bilinear 2x upsample (align_corners=False)
-// replaces input channels 64-127 (cin 128 -> cout 64, no prologue): x then supplies channels 0-63 only.
+// y = conv3x3(pro(x)) + bias (cin 64 / 128 -> 64 channels; stride 1, pad 1) with GroupNorm partials of y
+// (gn_groups > 0): [N, (H / 8) * (W / 32), G, 4]. pro: null or float2 [N, cin] (x * a + b, then ReLU if pro_relu).
 AI4E_API int ai4e_conv3x3_tile_fwd(const void* x, const void* w, const void* bias, const void* pro, int pro_relu,
                                    void* y, int N, int H, int W, int cin, int cout, int ldx, int xcoff, int kpad,
-                                   int ldy, int ycoff, void* gn_partials, int gn_groups, const void* xu,
-                                   hipStream_t stream) {
-  const bool ok_c = (cout == 64 && (cin == 64 || cin == 128)) || (cout == 128 && (cin == 64 || cin == 128 || cin == 256));
-  const int th = cout == 64 ? TileCfg<64, 64>::TH : TileCfg<64, 128>::TH;
+                                   int ldy, int ycoff, void* gn_partials, int gn_groups, hipStream_t stream) {
+  const bool ok_c = cout == 64 && (cin == 64 || cin == 128);
+  const int th = TileCfg<64>::TH;
   if (!x || !w || !bias || !y || N <= 0 || !ok_c || H % th || W % T_W || kpad < 9 * cin || ldx % 8 || xcoff % 8 ||
       xcoff + cin > ldx || ldy % 8 || ycoff % 8 || ycoff + cout > ldy)
     return AI4E_EINVAL;
   if (reinterpret_cast<uintptr_t>(bias) % 16) return AI4E_EINVAL;  // float4 reads in the epilogue
-  if (xu && (cin != 128 || cout != 64 || pro || H % 2 || W % 2 || reinterpret_cast<uintptr_t>(xu) % 16))
-    return AI4E_EINVAL;
   if (gn_partials && (gn_groups <= 0 || gn_groups > 64 || cout % gn_groups || cout / gn_groups > 4))
     return AI4E_EINVAL;
   if (static_cast<long>(N) * H * W * (ldx > ldy ? ldx : ldy) >= (1L << 40)) return AI4E_EINVAL;
@@ -579,9 +423,5 @@ AI4E_API int ai4e_conv3x3_tile_fwd(const void* x, const void* w, const void* bia
   p.W = W;
   p.tiles_w = W / T_W;
   p.tiles_per_img = (H / th) * p.tiles_w;
-  p.xu = static_cast<const uint16_t*>(xu);
-  if (xu) return launch_tile<128, 64, true>(p, N, stream);
-  if (cout == 64) return cin == 64 ? launch_tile<64, 64>(p, N, stream) : launch_tile<128, 64>(p, N, stream);
-  if (cin == 64) return launch_tile<64, 128>(p, N, stream);
-  return cin == 128 ? launch_tile<128, 128>(p, N, stream) : launch_tile<256, 128>(p, N, stream);
+  return cin == 64 ? launch_tile<64>(p, N, stream) : launch_tile<128>(p, N, stream);
 }

@@ -47,16 +47,12 @@ CASES = [
 
 
 @pytest.mark.parametrize("case", CASES)
-@pytest.mark.parametrize("tile", [0, 1, 3, 19, 35])
+@pytest.mark.parametrize("tile", [0, 3])
 def test_conv_chain(case, tile):
     """tile 3 = phase A from the LDS input patch (stride 1 and a patch that fits; other shapes fall back to the
-    ring, which the same comparison then covers)."""
+    ring, which the same comparison then covers); tile 0 = the LDS-DMA ring everywhere."""
     n, h, w, mid, s, nxt = case
     midn = 0 if not nxt else (mid if nxt is True else nxt)
-    if tile == 1 and (mid != 64 or midn == 128):
-        pytest.skip("tile config 1 is the MID-64, same-width variant")
-    if tile == 19 and mid != 64:
-        pytest.skip("tile config 19 (2 x 2 phase-A split) is the MID-64 variant")
     assert chain_kernel_builds(mid, midn)
     torch.manual_seed(7)
     c2 = pack_conv(torch.randn(mid, mid, 3, 3) / (9 * mid) ** 0.5, torch.randn(mid) * 0.1, stride=s, pad=1).to(DEV)

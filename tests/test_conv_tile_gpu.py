@@ -15,7 +15,6 @@ DEV = "cuda"
 @pytest.fixture(autouse=True)
 def _k1t_on(monkeypatch):
     monkeypatch.setenv("AI4E_CONV_TILE64", "1")
-    monkeypatch.setenv("AI4E_K1T_COUT128", "1")
 
 
 def _conv_ref(xin: torch.Tensor, w: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
@@ -35,9 +34,7 @@ def _case(n, h, w, seed, cin=64, cout=64):
 # the last two: 768 tiles > the persistent grid (2 x 256 CUs), so workgroups walk several tiles (next-tile prefetch)
 @pytest.mark.parametrize("n,h,w,cin,cout", [(2, 16, 64, 64, 64), (1, 64, 32, 64, 64), (3, 8, 96, 64, 64),
                                             (2, 16, 64, 128, 64), (1, 8, 32, 128, 64), (3, 128, 512, 64, 64),
-                                            (3, 128, 512, 128, 64),
-                                            (2, 8, 64, 64, 128), (1, 4, 32, 128, 128), (2, 12, 96, 256, 128),
-                                            (3, 64, 512, 64, 128), (3, 64, 512, 256, 128)])
+                                            (3, 128, 512, 128, 64)])
 def test_conv3x3_tile64_matches_fp32(n, h, w, cin, cout):
     from aiforearth_api_platform_amd.ops.conv import conv3x3_tile64
     x, wt, b, pc = _case(n, h, w, n * 100 + h, cin, cout)
@@ -48,7 +45,7 @@ def test_conv3x3_tile64_matches_fp32(n, h, w, cin, cout):
     assert rel < 6e-3, rel
 
 
-@pytest.mark.parametrize("cin,cout", [(64, 64), (128, 64), (128, 128), (256, 128)])
+@pytest.mark.parametrize("cin,cout", [(64, 64), (128, 64)])
 def test_conv3x3_tile64_prologue_and_sliced_input(cin, cout):
     """The prologue affine is per image (and per k-slice for 128 / 256 channels): 3 images of 256 / 512 tiles, so
     persistent workgroups cross images."""
@@ -68,8 +65,7 @@ def test_conv3x3_tile64_prologue_and_sliced_input(cin, cout):
 
 @pytest.mark.parametrize("groups,cin,n,h,w,cout", [(32, 64, 2, 32, 64, 64), (16, 64, 2, 32, 64, 64),
                                                    (32, 128, 2, 32, 64, 64), (32, 64, 3, 128, 512, 64),
-                                                   (32, 128, 3, 128, 512, 64), (32, 128, 2, 32, 64, 128),
-                                                   (32, 256, 3, 64, 512, 128), (64, 64, 2, 16, 64, 128)])
+                                                   (32, 128, 3, 128, 512, 64)])
 def test_conv3x3_tile64_groupnorm_statistics(groups, cin, n, h, w, cout):
     """The epilogue's shifted per-tile sums, finalized (ops.norm.group_norm_affine), equal the GroupNorm affine of
     the stored output computed directly in fp64 (the last case: several tiles per persistent workgroup)."""
@@ -146,39 +142,3 @@ def test_unet_fused_head_equals_apply_then_conv():
     rel = ((y_f[..., :k] - y_u[..., :k]).norm() / y_u[..., :k].norm()).item()
     assert rel < 1e-2, rel
     assert (y_f[..., :k].argmax(-1) == y_u[..., :k].argmax(-1)).float().mean().item() > 0.99
-
-
-@pytest.mark.parametrize("n,h,w", [(1, 8, 32), (2, 16, 64), (3, 128, 512)])
-def test_conv3x3_tile64_ups_equals_explicit_upsample(n, h, w):
-    """K1t UPS: the 128 -> 64 conv whose input channels 64-127 are the bilinear 2x upsample of a coarse tensor, formed
-    in LDS, equals the same conv over a concat with the upsample written by upsample2x_nhwc — bitwise (the patch
-    values use the upsample kernel's exact arithmetic), GroupNorm statistics included. The concat's upsampled half is
-    garbage in the UPS call: it must not be read."""
-    from aiforearth_api_platform_amd.ops.conv import conv3x3_tile64
-    from aiforearth_api_platform_amd.ops.norm import upsample2x_nhwc
-    x, wt, b, pc = _case(n, h, w, 31, 128, 64)
-    g = torch.Generator().manual_seed(32)
-    coarse = torch.randn(n, h // 2, w // 2, 64, generator=g).to(torch.bfloat16).to(DEV)
-    cat = x.to(DEV).clone()
-    upsample2x_nhwc(coarse, out=cat, out_coff=64)
-    y_ref, st_ref = conv3x3_tile64(cat, pc, gn_groups=32)
-    junk = cat.clone()
-    junk[..., 64:] = float("nan")
-    y_ups, st_ups = conv3x3_tile64(junk, pc, gn_groups=32, up=coarse)
-    assert torch.equal(y_ups, y_ref)
-    k = n * st_ref[1] * 32 * 4  # the partials (the buffer's tail is the finalize's workspace, uninitialized here)
-    assert torch.equal(st_ups[0][:k], st_ref[0][:k])
-
-
-def test_unet_fused_upsample_equals_unfused():
-    """The U-Net with the level-0 upsample fused into the decoder c1 (AI4E_UNET_FUSED_UP=1) equals the default."""
-    from aiforearth_api_platform_amd.models.unet import FusedUNet, unet_landcover
-    m = unet_landcover(seed=9)
-    img = torch.randint(0, 256, (2, 256, 256, 4), dtype=torch.uint8, generator=torch.Generator().manual_seed(9))
-    y_ref = FusedUNet(m, device=DEV).forward_u8(img.to(DEV))
-    os.environ["AI4E_UNET_FUSED_UP"] = "1"
-    try:
-        y_f = FusedUNet(m, device=DEV).forward_u8(img.to(DEV))
-    finally:
-        del os.environ["AI4E_UNET_FUSED_UP"]
-    assert torch.equal(y_f, y_ref)

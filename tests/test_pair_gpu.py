@@ -107,28 +107,3 @@ def test_side_stream_downsample_matches_serial():
     assert torch.equal(out, ref)
 
 
-def test_engine_phase_offset_split_matches_single_graph(monkeypatch):
-    """AI4E_ENGINE_SPLIT=1: the ResNet forward as two captured graphs (stem..layer2 | layer3..top-k) with batch k+1's
-    front ordered after batch k's front gives the single-graph results."""
-    from aiforearth_api_platform_amd.models.resnet import FusedResNet, resnet50
-    from aiforearth_api_platform_amd.runtime.engine import InferenceEngine
-    from aiforearth_api_platform_amd.runtime.servable import ClassifierServable
-
-    torch.manual_seed(0)
-    m = FusedResNet(resnet50(), device=DEV)
-    s = ClassifierServable(m, 5, head=m.topk_u8)
-    monkeypatch.setenv("AI4E_ENGINE_SPLIT", "1")
-    eng = InferenceEngine(None, (224, 224, 3), 16, device=torch.device(DEV), output_fn=s, buckets=[8, 16])
-    assert eng.split is not None
-    eng.warmup()
-    assert eng.graphs2
-    host = torch.randint(0, 256, (16, 224, 224, 3), dtype=torch.uint8).pin_memory()
-    res = [eng.submit(host, list(range(16))), eng.submit(host, list(range(8))), eng.submit(host, list(range(16)))]
-    for r in res:
-        r.done.synchronize()
-    with torch.no_grad():
-        ref_i, ref_p = m.topk_u8(host.to(DEV), 5)
-    for r in res:
-        n = r.outputs[0].shape[0]
-        assert torch.equal(r.outputs[0], ref_i[:n].cpu())
-        assert torch.allclose(r.outputs[1], ref_p[:n].cpu(), atol=1e-3)

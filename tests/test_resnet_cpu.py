@@ -87,29 +87,11 @@ def test_chained_microbatch_matches_full_batch():
         assert (out - ref).abs().max().item() < 1e-4, cfg
 
 
-def test_split_front_back_matches_topk_cpu():
-    """The two-part serving forward (engine phase-offset split) composes to the fused top-k (CPU reference path)."""
-    import torch
-
-    from aiforearth_api_platform_amd.models.resnet import FusedResNet, resnet50
-    from aiforearth_api_platform_amd.runtime.servable import ClassifierServable
-
-    torch.manual_seed(0)
-    m = FusedResNet(resnet50())
-    x = torch.randint(0, 256, (2, 64, 64, 3), dtype=torch.uint8)
-    s = ClassifierServable(m, 5, head=m.topk_u8)
-    assert s.split is not None
-    front, back = s.split
-    i, p = back(*front(x))
-    ri, rp = m.topk_u8(x, 5)
-    assert torch.equal(i, ri) and torch.allclose(p, rp)
-
-
 def test_pair_route_defaults():
     from aiforearth_api_platform_amd.ops import conv as convmod
 
     assert convmod.pair_route(256, 1024, 256)          # layer3 pairs: K1p by default
-    assert not convmod.pair_route(128, 512, 256)       # layer2 -> layer3: opt-in (AI4E_PAIR_B)
+    assert not convmod.pair_route(128, 512, 256)       # layer2 -> layer3: the K1c chain
     assert not convmod.pair_route(256, 1024, 512)      # layer3 -> layer4: opt-in (AI4E_PAIR_X)
     assert not convmod.pair_route(512, 2048, 512)      # layer4: opt-in (AI4E_PAIR_L4)
     assert not convmod.pair_route(64, 256, 64)         # not a K1p shape

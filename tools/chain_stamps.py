@@ -49,6 +49,17 @@ def main():
             m._stages_chained(y1, t1=t11, s0=1, s1=2)
         torch.cuda.synchronize()
         out["layer2_last_chain"] = read(4 * ((250 * 28 * 28 + 127) // 128))
+        # wall time of the whole layer1 / layer2 stages (stamped build: compare variants, not against the release build)
+        for name, fn in (("layer1_ms", lambda: m._stages_chained(y, t1=t1, s0=0, s1=1)),
+                         ("layer2_ms", lambda: m._stages_chained(y1, t1=t11, s0=1, s1=2))):
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+            fn()
+            ev[0].record()
+            for _ in range(10):
+                fn()
+            ev[1].record()
+            torch.cuda.synchronize()
+            out[name] = round(ev[0].elapsed_time(ev[1]) / 10, 4)
     print(json.dumps(out, indent=1))
 
 
