@@ -199,9 +199,13 @@ def conv2d_gn_nhwc(x: torch.Tensor, pc: PackedConv, groups: int, out: Optional[t
     n, h, w, c = x.shape
     oh, ow = pc.out_hw(h, w)
     cfg = tuned_tile(pc, n, h, w, False) or (2 if pc.cout <= 64 else 1)
-    bm, bn = (256, 64) if cfg in (2, 5, 8) else (128, 128)
-    ok = (_ext.backend_for(x) == "hip" and cfg in (1, 2, 4, 5, 7, 8) and groups > 0 and pc.cout % groups == 0
-          and (oh * ow) % bm == 0 and pc.cout % 8 == 0 and bn % (pc.cout // groups) == 0 and out_coff % 8 == 0
+    # statistics tile (pixels, channels) of each config: the 256-wide ping-pong configs (6: 256 x 256, 9 / 10:
+    # 192 x 256) emit them from their epilogue too (round 5: the U-Net's deep-level convs lost their stats pass)
+    bm, bn = {2: (256, 64), 5: (256, 64), 8: (256, 64), 6: (256, 256), 9: (192, 256), 10: (192, 256)}.get(cfg, (128, 128))
+    cg = pc.cout // groups if groups > 0 else 0
+    ok = (_ext.backend_for(x) == "hip" and cfg in (1, 2, 4, 5, 6, 7, 8, 9, 10) and groups > 0 and pc.cout % groups == 0
+          and (oh * ow) % bm == 0 and pc.cout % 8 == 0 and bn % cg == 0 and out_coff % 8 == 0
+          and (cfg not in (6, 9, 10) or cg & (cg - 1) == 0)
           and (out is None or out.stride(2) % 8 == 0) and x.dtype == torch.bfloat16 and c == pc.cin_pad)
     if not ok:
         return conv2d_nhwc(x, pc, out=out, out_coff=out_coff), None

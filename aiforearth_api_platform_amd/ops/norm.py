@@ -126,9 +126,12 @@ def group_norm_nhwc(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, gr
     return out
 
 
-def upsample2x_nhwc(x: torch.Tensor, out: Optional[torch.Tensor] = None, out_coff: int = 0) -> torch.Tensor:
+def upsample2x_nhwc(x: torch.Tensor, out: Optional[torch.Tensor] = None, out_coff: int = 0,
+                    pro: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Bilinear x2 (align_corners=False). ``out`` may be a wider concat buffer; writes channels
-    [out_coff, out_coff + C)."""
+    [out_coff, out_coff + C). ``pro``: float32 [N, C, 2] GroupNorm affine (``group_norm_affine``) of ``x``: the input
+    is ``relu(x * a + b)`` rounded to bf16 as the apply pass would store it, so the normalized tensor is never written
+    (csrc/kernels/norm_resample.hip ``ai4e_upsample2x_gn_relu``)."""
     n, h, w, c = x.shape
     if out is None:
         out = torch.empty(n, 2 * h, 2 * w, c, device=x.device, dtype=x.dtype)
@@ -137,9 +140,18 @@ def upsample2x_nhwc(x: torch.Tensor, out: Optional[torch.Tensor] = None, out_cof
         x = x.contiguous()
         if out.stride(3) != 1:
             raise ValueError("bad output buffer")
+        if pro is not None:
+            if tuple(pro.shape) != (n, c, 2) or pro.dtype != torch.float32 or not pro.is_contiguous():
+                raise ValueError("pro must be float32 [N, C, 2] contiguous")
+            _ext.call("ai4e_upsample2x_gn_relu", x.data_ptr(), out.data_ptr(), pro.data_ptr(), n, h, w, c,
+                      out.stride(2), out_coff, _ext.stream_ptr(x.device))
+            return out
         _ext.call("ai4e_upsample2x_bilinear", x.data_ptr(), out.data_ptr(), n, h, w, c, out.stride(2), out_coff, 0,
                   _ext.stream_ptr(x.device))
         return out
+    if pro is not None:
+        p = pro.to(x.device, torch.float32)
+        x = torch.relu((x.float() * p[..., 0].reshape(n, 1, 1, c) + p[..., 1].reshape(n, 1, 1, c)).to(x.dtype))
     y = F.interpolate(x.permute(0, 3, 1, 2).float(), scale_factor=2, mode="bilinear", align_corners=False)
     out[..., out_coff:out_coff + c] = y.permute(0, 2, 3, 1).to(out.dtype)
     return out

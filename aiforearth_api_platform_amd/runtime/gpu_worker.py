@@ -377,12 +377,20 @@ def join_group(device: str, group_rank: int, group_size: int, port: int, n_leade
     return kw
 
 
+def _share_cpu(dev: torch.device, spec: ModelSpec) -> None:
+    """CPU worker groups (tests, CPU-only deployments): the group's processes share the host's cores instead of
+    each running an intra-op pool as wide as the machine (8 processes x 8 threads on 8 cores thrash)."""
+    if dev.type == "cpu" and spec.group_size > 1 and "OMP_NUM_THREADS" not in os.environ:
+        torch.set_num_threads(max(1, (os.cpu_count() or 1) // spec.group_size))
+
+
 def follower_main(device: str, spec: ModelSpec, group_rank: int, group_size: int, port: int) -> None:
     """A non-leader process of a worker group: builds its part of the model and serves the leader
     (``servable.serve_follower()`` returns when the leader releases the group)."""
     dev = torch.device(device)
     if dev.type == "cuda":
         torch.cuda.set_device(dev)
+    _share_cpu(dev, spec)
     gk = join_group(device, group_rank, group_size, port, spec.group_leaders)
     part = load_factory(spec.factory)(device=device, **spec.kwargs, **gk)
     try:
@@ -403,6 +411,7 @@ def worker_main(conn, rank: int, device: str, spec: ModelSpec, shm_name: str, ns
     dev = torch.device(device)
     if dev.type == "cuda":
         torch.cuda.set_device(dev)
+    _share_cpu(dev, spec)
     group_kwargs = (join_group(device, group_rank, spec.group_size, group_port, spec.group_leaders)
                     if spec.group_size > 1 else None)
     shm, buf = attach_ring(shm_name, nslots, spec.item_shape, untrack=untrack)

@@ -4,9 +4,14 @@ Used by ``bench.py`` (the headline ResNet-50 API) and ``bench/api_bench.py`` (de
 ensemble): a node scheduler (native task store + dispatch queue + NodeScheduler) and ONE GPU worker
 process per GPU. N = 1: the calling process is the scheduler and spawns the worker for cuda:0.
 
-N > 1 (torchrun, one rank per GPU), two control-plane layouts:
+N > 1 (torchrun, one rank per GPU), three control-plane layouts:
 
-* ``sharded`` (default; AI4E_BENCH_CP=sharded): every rank is the node scheduler of its own GPU — its own task
+* ``serve`` (default; AI4E_BENCH_CP=serve): the shipped server's topology (serve.py -> ShardedWorkerPool): rank 0 hosts
+  the whole control plane — one task store, and one control-plane SHARD per GPU (node scheduler threads, dispatch
+  queue, ring partition, ids minted in the shard's own store lock domains) — and spawns the worker for its GPU; rank r
+  attaches to shard r over TCP as that shard's GPU worker and ingests its clients' payloads into its own partition of
+  the one shared ring. Nothing per task crosses shards, and no task passes through another GPU's scheduler;
+* ``sharded`` (AI4E_BENCH_CP=sharded): every rank is the node scheduler of its own GPU — its own task
   store shard, dispatch queue, payload ring and spawned worker process, its own clients — the reference's replica
   DP (HPA replicas behind Istio's ROUND_ROBIN, ``APIs/Charts/templates/async-gpu/autoscaler.yaml``) with the
   control plane scaling with the GPUs instead of serializing through one process (the reference's single
@@ -223,7 +228,11 @@ def run_node_bench(args, spec, path: str, metric: str, unit: str = "images/s", c
     # rank 0 builds the in-tree HIP/C++ libraries, then everyone joins (RCCL on GPU, gloo on CPU)
     denv = init_from_env(args.device, build=_build.build_all)
     rank, device = denv.rank, denv.device
-    sharded = world > 1 and group == 1 and os.environ.get("AI4E_BENCH_CP", "sharded") != "central"
+    cp_mode = os.environ.get("AI4E_BENCH_CP", "serve") if world > 1 and group == 1 else "central"
+    if cp_mode not in ("serve", "sharded", "central"):
+        raise SystemExit(f"AI4E_BENCH_CP={cp_mode}: serve, sharded or central")
+    sharded = cp_mode == "sharded"
+    served = cp_mode == "serve"
     B = args.batch
     part = B * (args.inflight + 1)  # ring slots per ingest shard
     hb = 0.5
@@ -239,11 +248,20 @@ def run_node_bench(args, spec, path: str, metric: str, unit: str = "images/s", c
             devices = [f"cuda:{i}" for i in range(group)] if args.device == "cuda" else ["cpu"] * group
         else:
             devices = [f"{args.device}:{denv.local_rank}" if args.device == "cuda" else "cpu"]
-        pool = WorkerPool(cp, endpoint, spec, devices,
-                          ring_slots=part, max_delay_s=0.0005, heartbeat_interval_s=hb, heartbeat_timeout_s=120.0,
-                          remote_partitions=remote, pipeline_depth=int(os.environ.get("AI4E_PIPELINE_DEPTH", "3")),
-                          poll_s=0.005, frontends=getattr(args, "http_frontends", 0) if args.http else 0,
-                          frontend_slots=3 * B)  # (REST phase only: keep the pinned ring small)
+        pkw = dict(ring_slots=part, max_delay_s=0.0005, heartbeat_interval_s=hb, heartbeat_timeout_s=120.0,
+                   pipeline_depth=int(os.environ.get("AI4E_PIPELINE_DEPTH", "3")), poll_s=0.005,
+                   frontends=getattr(args, "http_frontends", 0) if args.http else 0,
+                   frontend_slots=3 * B)  # (REST phase only: keep the pinned ring small)
+        if served:
+            from .worker_pool import ShardedWorkerPool
+
+            # shard r serves GPU r; shards 1..N-1 are served by the torchrun ranks that attach below
+            pool = ShardedWorkerPool(cp, endpoint, spec, [f"{args.device}:{r}" if args.device == "cuda" else "cpu"
+                                                          for r in range(world)],
+                                     shards=world, remote=range(1, world), remote_slots=part, **pkw)
+            remote = [pool.remote_partition(r) for r in range(1, world)]
+        else:
+            pool = WorkerPool(cp, endpoint, spec, devices, remote_partitions=remote, **pkw)
         info = None
         listener = None
         if world > 1 and not sharded:
@@ -254,7 +272,8 @@ def run_node_bench(args, spec, path: str, metric: str, unit: str = "images/s", c
             # backlog = every remote rank: with the default of 1, ranks that connect at once overflow the accept queue,
             # their SYNs are dropped and retried after 1, 2, 4, ... s (a 40-90 s stall, 2 in 6 world-8 runs)
             listener = Listener(("127.0.0.1", 0), authkey=key, backlog=max(1, world))
-            info = {"shm": pool.ring.name, "nslots": pool.ring.nslots, "addr": listener.address, "key": key.hex()}
+            info = {"shm": pool.ring.name, "nslots": pool.ring.nslots, "addr": listener.address, "key": key.hex(),
+                    "parts": {int(rk): int(b) for b, _, rk in remote}}  # rank -> its ingest partition base
         objs = [info]
         if world > 1 and not sharded:
             import torch.distributed as dist
@@ -265,7 +284,7 @@ def run_node_bench(args, spec, path: str, metric: str, unit: str = "images/s", c
                 for _ in range(world - 1):
                     c = listener.accept()
                     r = int(c.recv_bytes().decode())
-                    pool.attach_remote(r, c, device=f"cuda:{r}")
+                    (pool.control_shards[r] if served else pool).attach_remote(r, c, device=f"cuda:{r}")
 
             acc = threading.Thread(target=accept, daemon=True)
             acc.start()
@@ -273,7 +292,9 @@ def run_node_bench(args, spec, path: str, metric: str, unit: str = "images/s", c
         if world > 1 and not sharded:
             acc.join(900)
             pool.wait_ready(900)
-        client = Client(pool.ring.buf, lambda n: pool.ring.alloc(n, timeout=600), pool.submit_slots, B, rank)
+        # (serve: rank 0's clients feed shard 0 only, like every other rank feeds its own shard)
+        own = pool.control_shards[0] if served else pool
+        client = Client(pool.ring.buf, lambda n: own.ring.alloc(n, timeout=600), own.submit_slots, B, rank)
     else:
         import torch.distributed as dist
         from multiprocessing.connection import Client as MPClient
@@ -287,7 +308,7 @@ def run_node_bench(args, spec, path: str, metric: str, unit: str = "images/s", c
         conn = MPClient(tuple(info["addr"]), authkey=bytes.fromhex(info["key"]))
         conn.send_bytes(str(rank).encode())
         fc = P.FrameConn(conn)
-        local_ring = native.SlotRing(part, part * rank)
+        local_ring = native.SlotRing(part, int(info.get("parts", {}).get(rank, part * rank)))
         shm, ring_buf = attach_ring(info["shm"], info["nslots"], spec.item_shape, untrack=True)
 
         def alloc(n):
@@ -409,9 +430,11 @@ def run_node_bench(args, spec, path: str, metric: str, unit: str = "images/s", c
                        "tail_steps_uncounted": tail},
             "config": dict(config or {}, global_batch=B * world, per_gpu_batch=B,
                            parallelism=(config or {}).get("parallelism", f"dp{world}"),
-                           serving_path=("one node scheduler (native) + GPU worker process per GPU, sharded by GPU"
+                           serving_path=("the serve topology: one control plane process, a scheduler shard per GPU "
+                                         "(ShardedWorkerPool) + 1 GPU worker per GPU" if served else
+                                         "one node scheduler (native) + GPU worker process per GPU, sharded by GPU"
                                          if sharded else "node scheduler (native) + 1 GPU worker process per GPU"),
-                           control_plane="sharded" if sharded else "central",
+                           control_plane=cp_mode,
                            ingest_shards=world, ring_slots_per_shard=part, hip_graphs=spec.use_graphs),
             "workers": workers, "batch_histogram": stats.get("batch_histogram"), "http": http,
         }

@@ -174,7 +174,7 @@ class WorkerPool:
         self.remote_partitions = [tuple(int(v) for v in p) for p in remote_partitions]  # (base, len, rank)
         if shard is not None:
             self.frontend_partitions = list(shard.frontend_parts)
-            self.remote_partitions += self.frontend_partitions
+            self.remote_partitions += list(shard.remote_parts) + self.frontend_partitions
             self.ring = RingPartition(shard.ring, shard.local[0], shard.local[1])
             total = shard.ring.nslots
         else:
@@ -488,10 +488,14 @@ class ShardLayout:
     (base, length, scheduler rank) and the task-store lock domains it mints ids in."""
 
     def __init__(self, index: int, ring: SharedPayloadRing, local: Tuple[int, int],
-                 frontend_parts: Sequence[Tuple[int, int, int]], store_shards: Sequence[int]):
+                 frontend_parts: Sequence[Tuple[int, int, int]], store_shards: Sequence[int],
+                 remote_parts: Sequence[Tuple[int, int, int]] = ()):
         self.index, self.ring, self.local = int(index), ring, (int(local[0]), int(local[1]))
         self.frontend_parts = [tuple(int(v) for v in p) for p in frontend_parts]
         self.store_shards = [int(v) for v in store_shards]
+        # ingest partitions of remote worker processes (a torchrun rank that serves this shard and submits its own
+        # clients' payloads over its scheduler connection): (base, length, rank)
+        self.remote_parts = [tuple(int(v) for v in p) for p in remote_parts]
 
 
 class _ShardedRing:
@@ -580,7 +584,10 @@ class ShardedWorkerPool:
 
     def __init__(self, control_plane, endpoint: str, spec: ModelSpec, devices: Sequence[str], shards: int = 0,
                  ring_slots: int = 0, frontends: int = 0, frontend_slots: int = 0, pipeline_depth: int = 3,
-                 **kw):
+                 remote: Sequence[int] = (), remote_slots: int = 0, **kw):
+        """``remote``: shards whose worker is a process started elsewhere (a torchrun rank of the multi-GPU bench) that
+        attaches with ``control_shards[i].attach_remote(i, conn)`` and ingests into its own ``remote_slots`` partition
+        (``remote_partition(i)``); nothing is spawned for those shards."""
         self.cp, self.endpoint, self.spec = control_plane, endpoint, spec
         self.devices = list(devices)
         k = max(1, spec.group_size)
@@ -594,12 +601,21 @@ class ShardedWorkerPool:
         if K > nstore:
             raise ValueError(f"{K} control-plane shards need a task store of >= {K} lock domains (has {nstore})")
         shard_devs = [[d for g in groups[i::K] for d in g] for i in range(K)]
+        self.remote = sorted(set(int(i) for i in remote))
+        if any(not 0 <= i < K for i in self.remote):
+            raise ValueError(f"remote shards {self.remote} outside 0..{K - 1}")
+        for i in self.remote:
+            shard_devs[i] = []  # (its worker attaches from elsewhere)
         fs = frontend_slots or spec.max_batch * 4
         layout, base = [], 0
         for i in range(K):
             n_local = ring_slots or spec.max_batch * (pipeline_depth + 2) * max(1, len(shard_devs[i]))
             layout.append([(base, n_local)])
             base += n_local
+        self._remote_parts: Dict[int, Tuple[int, int, int]] = {}
+        for i in self.remote:
+            self._remote_parts[i] = (base, int(remote_slots or spec.max_batch * 4), i)
+            base += self._remote_parts[i][1]
         for i in range(K):
             parts = []
             for f in range(int(frontends)):
@@ -609,7 +625,8 @@ class ShardedWorkerPool:
         self._ring = SharedPayloadRing(base, spec.item_shape, local_slots=1)
         self.pools: List[WorkerPool] = []
         for i in range(K):
-            lay = ShardLayout(i, self._ring, layout[i][0], layout[i][1], [s for s in range(nstore) if s % K == i])
+            lay = ShardLayout(i, self._ring, layout[i][0], layout[i][1], [s for s in range(nstore) if s % K == i],
+                              [self._remote_parts[i]] if i in self._remote_parts else [])
             self.pools.append(WorkerPool(control_plane, endpoint, spec, shard_devs[i], pipeline_depth=pipeline_depth,
                                          frontends=frontends, frontend_slots=fs, shard=lay, **kw))
         self.ring = _ShardedRing(self._ring, self.pools)
@@ -655,6 +672,10 @@ class ShardedWorkerPool:
     @property
     def control_shards(self) -> List[WorkerPool]:
         return list(self.pools)
+
+    def remote_partition(self, shard: int) -> Tuple[int, int, int]:
+        """(base, length, rank) of a remote shard's ingest partition of the shared ring."""
+        return self._remote_parts[int(shard)]
 
     # ------------------------------------------------------------ ingest
     def submit_slots(self, slots: Sequence[int], trace: str = "") -> List[str]:

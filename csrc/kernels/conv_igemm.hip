@@ -837,7 +837,13 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
 
   // ---- epilogue, one pixel group at a time: fp32 [WROWS][256] tile in LDS (16-B chunk index
   //      XOR (row & 7)), then every thread handles 16-B output chunks: + bias (+ residual), ReLU.
+  //      With p.gnp: the GroupNorm statistics of the stored values as well (the K1 epilogue's shifted partial sums,
+  //      one [BM-pixel chunk, group] record each), so a GroupNorm after a 256-wide conv needs no statistics pass. A
+  //      thread always owns the same 8 channels (c8 = tid % 32) of every row it stores.
   float* tile = reinterpret_cast<float*>(smem);
+  float gs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, gq[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float gk[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, kout = 0.f;  // GN shifts: the tile's first pixel, per group
+  const float lo_gn = (p.relu & 1) ? 0.f : -INFINITY;
 #pragma unroll
   for (int pass = 0; pass < 2; ++pass) {
     if (wr == pass) {
@@ -852,6 +858,17 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
       }
     }
     EPI_BARRIER();
+    if (p.gnp && pass == 0) {
+      // shift per channel slot: row 0 (unswizzled) + bias at the group's first channel (host: power-of-two groups)
+      const int cg = p.Kout / p.gn_groups;
+      const int c8 = 8 * (tid & 31);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int c = (c8 + k) & -cg;
+        gk[k] = fmaxf(tile[c] + p.bias[min(n0 + c, p.Kout - 1)], lo_gn);
+      }
+      if (tid < 256 / cg) kout = fmaxf(tile[tid * cg] + p.bias[min(n0 + tid * cg, p.Kout - 1)], lo_gn);
+    }
     constexpr int EP = WROWS / 16;  // 16-B output chunks per thread and pass
     uint4 rv[EP];
     if (p.res) {
@@ -876,8 +893,72 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
                           v1.x + b1.x, v1.y + b1.y, v1.z + b1.z, v1.w + b1.w};
       const uint4 o = epilogue8<F16>(f, p.res != nullptr, rv[e], (p.relu & 1) != 0);
       if (m < p.M && n < p.Kout) ai4e_conv::st16_stream(p.y + static_cast<long>(m) * p.ldy + p.ycoff + n, o);
+      if (p.gnp && m < p.M && n < p.Kout) {  // statistics of the values as stored (bf16)
+        const uint32_t ow[4] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          float a, b;
+          unpack2<F16>(ow[q], a, b);
+          a -= gk[2 * q];
+          b -= gk[2 * q + 1];
+          gs[2 * q] += a; gq[2 * q] += a * a;
+          gs[2 * q + 1] += b; gq[2 * q + 1] += b * b;
+        }
+      }
     }
     EPI_BARRIER();
+  }
+  if (p.gnp) {
+    // (1) in-thread: this thread's 8 channels into their groups (cgm = min(channels per group, 8) adjacent channels
+    // per slot); (2) the two lanes of a wave that own the same channels (lane, lane ^ 32) by one xor shuffle; (3) the
+    // 8 waves and each group's slots meet in LDS (the staged tile is dead after the last pass's barrier)
+    const int cg = p.Kout / p.gn_groups;
+    const int cgm = cg < 8 ? cg : 8;
+    auto reduce = [&](auto cgc) __attribute__((always_inline)) {
+      constexpr int CG = decltype(cgc)::value;
+#pragma unroll
+      for (int w = 1; w < CG; w <<= 1)
+#pragma unroll
+        for (int k = 0; k < 8; k += 2 * w) {
+          gs[k] += gs[k + w];
+          gq[k] += gq[k + w];
+        }
+#pragma unroll
+      for (int k = 0; k < 8; k += CG) {
+        gs[k] += __shfl_xor(gs[k], 32);
+        gq[k] += __shfl_xor(gq[k], 32);
+      }
+    };
+    switch (cgm) {
+      case 1: reduce(std::integral_constant<int, 1>{}); break;
+      case 2: reduce(std::integral_constant<int, 2>{}); break;
+      case 4: reduce(std::integral_constant<int, 4>{}); break;
+      default: reduce(std::integral_constant<int, 8>{}); break;
+    }
+    float* red = tile;  // [8 waves][256 channel slots][2]; slot c holds channels c .. c + cgm - 1
+    if (lane < 32) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        if (k % cgm == 0) {
+          red[(wave * 256 + lane * 8 + k) * 2] = gs[k];
+          red[(wave * 256 + lane * 8 + k) * 2 + 1] = gq[k];
+        }
+      }
+    }
+    EPI_BARRIER();
+    const int ng = min(256, p.Kout - n0) / cg;  // host: 256 % cg == 0, Kout % cg == 0
+    if (tid < ng) {
+      float S = 0.f, Q = 0.f;
+      for (int w = 0; w < 8; ++w)
+        for (int c = 0; c < cg; c += cgm) {
+          S += red[(w * 256 + tid * cg + c) * 2];
+          Q += red[(w * 256 + tid * cg + c) * 2 + 1];
+        }
+      const int ohw = p.OH * p.OW;  // host: ohw % BM == 0, so a tile never straddles images
+      const int img = m0 / ohw, chunk = (m0 - img * ohw) / BM;
+      float* o = p.gnp + ((static_cast<long>(img) * (ohw / BM) + chunk) * p.gn_groups + n0 / 256 * (256 / cg) + tid) * 4;
+      *reinterpret_cast<float4*>(o) = make_float4(S, Q, kout, 0.f);  // shifted sums, shift
+    }
   }
 #if AI4E_K256_STAMPS
   wait_vmcnt<0>();
@@ -978,12 +1059,15 @@ int conv2d_impl(const void* x, const void* w, const void* bias, const void* res,
   if (p.M <= 0) return AI4E_OK;
   if (tile_cfg == 0) tile_cfg = Kout <= 64 ? 2 : 1;
   if (gnp) {
-    // fused GroupNorm statistics: 128-wide LDS-epilogue tiles only (configs 1, 2, 4, 5), whole groups per
-    // channel tile, tiles that never straddle images, full 16-B output rows
+    // fused GroupNorm statistics: the LDS-epilogue tiles (configs 1, 2, 4, 5, 7, 8) and the 256-wide ones (6, 9,
+    // 10), whole groups per channel tile, power-of-two group widths, tiles that never straddle images, full 16-B
+    // output rows
     const bool tall = tile_cfg == 2 || tile_cfg == 5 || tile_cfg == 8;
-    const int bm = tall ? 256 : 128, bn = tall ? 64 : 128;
-    if (tile_cfg == 3 || tile_cfg == 6 || tile_cfg == 9 || tile_cfg == 10 || gn_groups <= 0 || Kout % gn_groups || (OH * OW) % bm || Kout % 8 ||
-        ldy % 8 || ycoff % 8 || (res && ldres % 8) || bn % (Kout / gn_groups))
+    const bool wide = tile_cfg == 6 || tile_cfg == 9 || tile_cfg == 10;
+    const int bm = tall ? 256 : wide ? (tile_cfg == 6 ? 256 : 192) : 128, bn = tall ? 64 : wide ? 256 : 128;
+    const int cgw = gn_groups > 0 ? Kout / gn_groups : 0;
+    if (tile_cfg == 3 || gn_groups <= 0 || Kout % gn_groups || (OH * OW) % bm || Kout % 8 || ldy % 8 || ycoff % 8 ||
+        (res && ldres % 8) || bn % cgw || (wide && (cgw & (cgw - 1))))
       return AI4E_EINVAL;
     p.gnp = gnp;
     p.gn_groups = gn_groups;
@@ -1024,8 +1108,8 @@ AI4E_API int ai4e_conv2d_f16_fwd(const void* x, const void* w, const void* bias,
 
 // Same conv, plus the GroupNorm statistics of its output (gn_groups groups over Kout channels) written as
 // per-(image, tile-row chunk, group) shifted partial sums (sum(x - K), sum((x - K)^2), K, pad) into gn_partials
-// [N, OH*OW / BM, gn_groups, 4] fp32 (BM = 256 for tile configs 2, 5 and 8, else 128). Configs 3, 6 and 9 and
-// shapes whose tiles would straddle images are refused (EINVAL) before anything is launched.
+// [N, OH*OW / BM, gn_groups, 4] fp32 (BM = 256 for tile configs 2, 5, 6 and 8, 192 for 9 and 10, else 128). Config 3
+// and shapes whose tiles would straddle images are refused (EINVAL) before anything is launched.
 AI4E_API int ai4e_conv2d_gn_fwd(const void* x, const void* w, const void* bias, const void* res, void* y, int N,
                                 int H, int W, int C, int ldx, int xcoff, int KH, int KW, int stride, int pad, int OH,
                                 int OW, int Kout, int Kpad, int ldy, int ycoff, int ldres, int relu, int tile_cfg,

@@ -481,8 +481,10 @@ def test_latency_budget_admission_429_no_lost_tasks():
             time.sleep(0.05)
         lat = cp.store.latencies(ids)
         assert len(lat) == len(ids)  # no accepted task was lost
-        # the 128-slot partition would hold ~16 batches = 320 ms of queue at 20 ms per batch of 8
-        assert percentile(sorted(lat), 50) < 0.15, percentile(sorted(lat), 50)
+        # without the budget the 128-slot partition fills: a queue of 128 / rate seconds (~320 ms at 20 ms per batch
+        # of 8); with it the median wait stays well under that at whatever rate this (shared) CPU delivers
+        rate = len(ids) / 3.0
+        assert percentile(sorted(lat), 50) < 0.5 * 128 / rate, (percentile(sorted(lat), 50), rate)
     finally:
         for p in fe:
             p.terminate()

@@ -102,6 +102,40 @@ def test_upsample_into_concat(shape):
     assert buf[..., :16].abs().max() == 0
 
 
+@pytest.mark.parametrize("shape", [(2, 16, 16, 64), (1, 7, 9, 32), (3, 32, 32, 1024), (1, 1, 1, 8)])
+def test_upsample_gn_relu_equals_apply_then_upsample(shape):
+    """The decoder's upsample with the producing block's GroupNorm + ReLU folded in (``pro`` affine) == the apply pass
+    (bf16 store) then the plain upsample, bit for bit, and == an fp32 PyTorch reference within bf16."""
+    n, h, w, c = shape
+    torch.manual_seed(3)
+    x = (torch.randn(*shape, device=DEV) * 3 + 1).bfloat16()
+    ab = torch.stack([torch.rand(n, c, device=DEV) + 0.5, torch.randn(n, c, device=DEV)], -1).contiguous()
+    buf = torch.zeros(n, 2 * h, 2 * w, c + 16, device=DEV, dtype=torch.bfloat16)
+    upsample2x_nhwc(x, out=buf, out_coff=16, pro=ab)
+    applied = torch.relu((x.float() * ab[:, None, None, :, 0] + ab[:, None, None, :, 1]).bfloat16())
+    two = upsample2x_nhwc(applied)
+    ref = F.interpolate(applied.float().permute(0, 3, 1, 2), scale_factor=2, mode="bilinear",
+                        align_corners=False).permute(0, 2, 3, 1)
+    torch.cuda.synchronize()
+    assert torch.equal(buf[..., 16:], two)
+    assert (buf[..., 16:].float() - ref).abs().max().item() <= 0.02 * max(1.0, ref.abs().max().item())
+    assert buf[..., :16].abs().max() == 0
+
+
+def test_unet_fused_up_gn_matches_apply_pass(monkeypatch):
+    """FusedUNet with the decoder GroupNorm + ReLU inside the upsample == with the apply pass (AI4E_UNET_FUSED_UP_GN=0),
+    bit for bit."""
+    from aiforearth_api_platform_amd.models.unet import FusedUNet, unet_landcover
+
+    m = unet_landcover(seed=0)
+    img = torch.randint(0, 256, (2, 256, 256, 4), dtype=torch.uint8, device=DEV)
+    a = FusedUNet(m, device=DEV)(img)
+    monkeypatch.setenv("AI4E_UNET_FUSED_UP_GN", "0")
+    b = FusedUNet(m, device=DEV)(img)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("N,thr", [(100, 0.5), (2000, 0.7), (777, 0.3)])
 def test_nms_matches_reference(N, thr):
     """Parity unpinned against torchvision.ops.nms (not installed in this image): the kernel is compared with the
@@ -362,6 +396,40 @@ def test_conv_fused_groupnorm_stats(cfg, shape, monkeypatch):
     b = group_norm_nhwc(y, gamma, beta, groups=g, relu=True)
     torch.cuda.synchronize()
     assert (a.float() - b.float()).abs().max().item() <= 0.02
+
+
+@pytest.mark.parametrize("cfg", [6, 9])
+@pytest.mark.parametrize("shape", [(2, 24, 32, 64, 256, 32), (1, 48, 16, 128, 512, 32), (3, 16, 48, 256, 256, 64),
+                                   (2, 24, 32, 64, 384, 48)])
+def test_conv256_fused_groupnorm_stats(cfg, shape, monkeypatch):
+    """The 256-wide ping-pong configs (6: 256-pixel, 9: 192-pixel tiles) emit the GroupNorm statistics from their
+    epilogue too: normalizing with them == the norm's own statistics pass over the stored output, and both == an fp32
+    PyTorch GroupNorm of it; the last shape has a 128-channel tail tile (Kout 384)."""
+    from aiforearth_api_platform_amd.ops import conv as convmod
+    from aiforearth_api_platform_amd.ops.conv import conv2d_gn_nhwc, pack_conv
+
+    n, h, w, cin, cout, g = shape
+    monkeypatch.setattr(convmod, "tuned_tile", lambda *a: cfg)
+    torch.manual_seed(6)
+    pc = pack_conv(torch.randn(cout, cin, 3, 3) / (9 * cin) ** 0.5, torch.randn(cout) * 0.3 + 2.0, pad=1).to(DEV)
+    x = torch.randn(n, h, w, cin, device=DEV).to(torch.bfloat16)
+    gamma, beta = torch.rand(cout, device=DEV) + 0.5, torch.randn(cout, device=DEV) * 0.1
+    y, st = conv2d_gn_nhwc(x, pc, g)
+    assert st is not None
+    # the finalized affine (a, b) from the epilogue statistics == the fp32 GroupNorm of the stored output (any C)
+    from aiforearth_api_platform_amd.ops.norm import group_norm_affine
+
+    ab = group_norm_affine(st, gamma, beta, n, h * w, cout, g).clone()
+    ref = F.group_norm(y.float().permute(0, 3, 1, 2), g, gamma, beta).permute(0, 2, 3, 1)
+    got = y.float() * ab[:, None, None, :, 0] + ab[:, None, None, :, 1]
+    torch.cuda.synchronize()
+    assert (got - ref).abs().max().item() <= 0.03
+    if (cout // 8) <= 256 and 256 % (cout // 8) == 0:  # (the apply kernel's channel limit)
+        a = group_norm_nhwc(y, gamma, beta, groups=g, relu=True, stats=st)
+        b = group_norm_nhwc(y, gamma, beta, groups=g, relu=True)
+        torch.cuda.synchronize()
+        assert (a.float() - b.float()).abs().max().item() <= 0.02
+        assert (a.float() - F.relu(ref)).abs().max().item() <= 0.03
 
 
 @pytest.mark.parametrize("shape", [(2, 32, 32, 64, 64, 32), (1, 16, 24, 128, 256, 16)])

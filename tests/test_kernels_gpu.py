@@ -224,14 +224,12 @@ def test_resnet_chunked_prefix_matches_full_batch_gpu():
         assert (out - ref).abs().max().item() < 2e-2, chunk
 
 
-@pytest.mark.parametrize("tile", [1, 2, 4, 6])
-@pytest.mark.parametrize("shape", [(2, 40, 40, 256, 256), (3, 10, 14, 512, 256), (1, 6, 2, 64, 68)])
+@pytest.mark.parametrize("shape,tile", [(s, t) for s in [(2, 40, 40, 256, 256), (3, 10, 14, 512, 256), (1, 6, 2, 64, 68)]
+                                        for t in (1, 2, 4, 6) if t != 6 or s[4] % 8 == 0])  # (tile 6: Cout % 8 == 0)
 def test_conv_residual_upsampled2x(tile, shape):
     """FPN top-down merge fused into the lateral 1x1: the epilogue reads the residual from the half-resolution
     map at (oh/2, ow/2) (nearest 2x upsample) == conv + explicitly upsampled residual."""
     n, h, w, cin, cout = shape
-    if tile == 6 and cout % 8:
-        pytest.skip("256 tile needs Cout % 8 == 0")
     torch.manual_seed(2)
     pc = pack_conv(torch.randn(cout, cin, 1, 1) / cin ** 0.5, torch.randn(cout) * 0.1).to(DEV)
     x = torch.randn(n, h, w, cin, device=DEV).to(torch.bfloat16)

@@ -5,6 +5,7 @@
 * config 4: spatial-parallel land-cover over a 3-process group (tile rows split, halo rows over P2P,
   bands gathered on the leader) == the single-process segmentation.
 """
+import os
 import time
 
 import pytest
@@ -76,7 +77,14 @@ def test_spatial_landcover_group_matches_single_process():
                      (), (), 3)
     got, stats = _serve(spec, ["cpu", "cpu", "cpu"], mosaic, "/v1/group/in")
     cls = np.asarray(Image.open(io.BytesIO(base64.b64decode(got[0]["class_map"]))))
-    ref = zoo.landcover("cpu", **kw)(torch.from_numpy(mosaic))[0][0].numpy()
+    # the group's CPU processes run os.cpu_count() // 3 intra-op threads each (gpu_worker._share_cpu): the reference
+    # uses the same count, so the fp32 reductions (and the argmax) are the same
+    nt = torch.get_num_threads()
+    torch.set_num_threads(max(1, (os.cpu_count() or 1) // 3))
+    try:
+        ref = zoo.landcover("cpu", **kw)(torch.from_numpy(mosaic))[0][0].numpy()
+    finally:
+        torch.set_num_threads(nt)
     assert np.array_equal(cls, ref)
     assert stats["workers"][0]["xgmi_rx_bytes"] > 0
 

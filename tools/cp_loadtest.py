@@ -8,6 +8,7 @@ DONE parse + result attach + completed transition + queue complete + slot releas
 ~70k images/s = 560k tasks/s.
 
     python tools/cp_loadtest.py [--workers 8 --batch 250 --seconds 5 --ingest-threads 4]
+    python tools/cp_loadtest.py --serve --workers 8 --frontends 4   (the shipped serve topology, over HTTP)
 """
 from __future__ import annotations
 
@@ -87,6 +88,110 @@ def fake_rank(conn, rank: int, row_bytes: int, batch: int, base: int, part: int,
             return
 
 
+def run_serve(a) -> dict:
+    """The SHIPPED server's topology (serve.py): one serving process whose pool endpoint is a ShardedWorkerPool —
+    one node scheduler + dispatch queue + ring partition per GPU, ``--workers`` of them, each with one fake worker
+    process (DONE at once) — behind ``--frontends`` native ingest front-ends (ai4e_ingestd) on the public port, driven
+    over HTTP by the C++ load generator with binary batches of ``--batch`` tiny (4x4x3) items. Counts completed tasks
+    per second in the middle of the load window."""
+    import asyncio
+    import socket
+
+    from aiohttp import web
+
+    from aiforearth_api_platform_amd.config import Config
+    from aiforearth_api_platform_amd.gateway.control import ControlPlane
+    from aiforearth_api_platform_amd.gateway.server import BATCH_CONTENT_TYPE, Gateway, Route, RouteTable
+    from aiforearth_api_platform_amd.runtime.frontend import open_listeners
+    from aiforearth_api_platform_amd.runtime.http_load import run_native_clients
+    from aiforearth_api_platform_amd.runtime.model_endpoint import ModelEndpoint
+    from aiforearth_api_platform_amd.runtime.native_frontend import spawn_native_frontends
+    from aiforearth_api_platform_amd.runtime.worker_pool import ModelSpec, ShardedWorkerPool
+
+    cp = ControlPlane(Config.load(env={}))
+    path = "/v1/ai4e/lt/classify"
+    shape = (4, 4, 3)
+    B = a.batch
+    spec = ModelSpec("aiforearth_api_platform_amd.models.toy:tiny_classifier", shape, B, 5, {}, False)
+    pool = ShardedWorkerPool(cp, "http://127.0.0.1" + path, spec, ["cpu"] * a.workers, frontends=a.frontends,
+                             frontend_slots=B * 16, ring_slots=B * 4, max_delay_s=0.0005, poll_s=0.005,
+                             heartbeat_timeout_s=60.0)
+    ctx = mp.get_context("spawn")
+    procs = []
+    for i, shard in enumerate(pool.control_shards):  # one fake worker per control-plane shard
+        parent, child = ctx.Pipe()
+        p = ctx.Process(target=fake_worker, args=(child, i, 40), daemon=True)
+        p.start()
+        child.close()
+        shard.attach_remote(i, parent, device="fake")
+        procs.append(p)
+    while sum(1 for w in pool.workers if w.stats.get("ready")) < a.workers:
+        pool.refresh()
+        time.sleep(0.01)
+    ep = ModelEndpoint(cp, path, worker=pool)
+    table = RouteTable()
+    table.add(Route("/v1/lt/async", "async", ep))
+    gw = Gateway(cp, table)
+    with socket.socket() as s0:
+        s0.bind(("127.0.0.1", 0))
+        port = s0.getsockname()[1]
+    socks = open_listeners("127.0.0.1", port, shared=True)
+    box = {}
+
+    def serve():
+        loop = asyncio.new_event_loop()
+        asyncio.set_event_loop(loop)
+        runner = web.AppRunner(gw.app, access_log=None)
+        loop.run_until_complete(runner.setup())
+        loop.run_until_complete(web.SockSite(runner, socks[1]).start())
+        box["loop"] = loop
+        loop.run_forever()
+
+    threading.Thread(target=serve, daemon=True).start()
+    socks[0].close()  # only the front-ends answer on the public port
+    fe = spawn_native_frontends(a.frontends, {"lt": ep}, [{"prefix": "/v1/lt/async", "mode": "async", "endpoint": "lt"}],
+                                "127.0.0.1", port, f"http://127.0.0.1:{socks[1].getsockname()[1]}")
+    time.sleep(1.0)
+    body = bytes(B * 48)
+    samples = {}
+
+    def sampler():
+        time.sleep(1.0 + a.seconds * 0.25)  # (load generators start 1 s after the call)
+        samples["n0"], samples["t0"] = pool.images, time.perf_counter()
+        time.sleep(a.seconds * 0.5)
+        samples["n1"], samples["t1"] = pool.images, time.perf_counter()
+
+    th = threading.Thread(target=sampler)
+    th.start()
+    res = run_native_clients(f"http://127.0.0.1:{port}/v1/lt/async", a.seconds, a.conc, body, BATCH_CONTENT_TYPE,
+                             procs=a.client_procs)
+    th.join()
+    rate = (samples["n1"] - samples["n0"]) / (samples["t1"] - samples["t0"])
+    ids = res["ids"]
+    lat = sorted(cp.store.latencies(ids[-20000:]))
+    from aiforearth_api_platform_amd.utils.metrics import percentile
+
+    out = {"metric": "control-plane tasks/s through the shipped serve topology (native front-ends -> sharded schedulers "
+                     "-> fake workers), no model",
+           "value": round(rate), "unit": "tasks/s", "control_plane_shards": len(pool.control_shards),
+           "fake_workers": a.workers, "ingest_frontends": a.frontends, "batch": B, "http_requests": res["requests"],
+           "http_errors": res["errors"], "busy_429": res.get("busy"), "accepted_tasks": len(ids),
+           "client_cpu_s": round(res["client_cpu_s"], 2), "seconds": a.seconds, "cpu_count": os.cpu_count(),
+           "p50_task_latency_ms": round(percentile(lat, 50) * 1e3, 3) if lat else None}
+    for p in fe:
+        p.terminate()
+    for p in fe:
+        p.join(10)
+    box["loop"].call_soon_threadsafe(box["loop"].stop)
+    pool.stop()
+    for p in procs:
+        p.join(5)
+        if p.is_alive():
+            p.terminate()
+    cp.close()
+    return out
+
+
 def _shard(args, barrier, out_q):
     """One control-plane shard (the sharded multi-GPU bench: one node scheduler per GPU) in its own process."""
     import argparse as _a
@@ -107,9 +212,16 @@ def main():
     ap.add_argument("--shards", type=int, default=0,
                     help="K independent scheduler processes (one per GPU, the sharded bench layout), "
                          "--workers fake workers each; the value is their sum")
+    ap.add_argument("--serve", action="store_true",
+                    help="the shipped server's topology: ShardedWorkerPool (one scheduler per worker) + native front-ends")
+    ap.add_argument("--frontends", type=int, default=4)
+    ap.add_argument("--conc", type=int, default=16, help="(--serve) HTTP connections per load process")
+    ap.add_argument("--client-procs", type=int, default=2)
     ap.add_argument("--json-out", default="")
     a = ap.parse_args()
-    if a.shards:
+    if a.serve:
+        out = run_serve(a)
+    elif a.shards:
         ctx = mp.get_context("spawn")
         bar, q = ctx.Barrier(a.shards), ctx.Queue()
         kw = dict(vars(a), shards=0, json_out="")
