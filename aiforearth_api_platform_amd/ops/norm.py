@@ -47,6 +47,32 @@ def group_norm_affine(stats, gamma: torch.Tensor, beta: torch.Tensor, n: int, hw
     return partials[off:off + n * c * 2].view(n, c, 2)
 
 
+def group_norm_pool_only_supported(x: torch.Tensor, pool_out: torch.Tensor) -> bool:
+    n, h, w, c = x.shape
+    return (_ext.backend_for(x) == "hip" and h % 2 == 0 and w % 2 == 0 and c % 8 == 0 and c // 8 <= 256
+            and 256 % (c // 8) == 0 and pool_out.is_contiguous() and tuple(pool_out.shape) == (n, h // 2, w // 2, c))
+
+
+def group_norm_pool_only(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, groups: int, stats,
+                         pool_out: torch.Tensor, eps: float = 1e-5) -> torch.Tensor:
+    """The 2x2/2 max-pool of ``relu(GroupNorm(x))`` into ``pool_out`` WITHOUT storing the normalized ``x`` (it stays
+    raw for a consumer that normalizes while loading). ``stats`` from the producing conv's epilogue. Returns the
+    GroupNorm affine float32 [N, C, 2] (a view into the stats buffer, written by the same launch) for that consumer
+    (``conv.conv3x3_tile64(pro=...)``)."""
+    n, h, w, c = x.shape
+    if stats is None or not group_norm_pool_only_supported(x, pool_out):
+        raise ValueError("group_norm_pool_only: unsupported shape (see group_norm_pool_only_supported)")
+    partials, nchunks = stats
+    ldx, xcoff = _nhwc_ld(x)
+    g32 = gamma.to(x.device, torch.float32).contiguous()
+    b32 = beta.to(x.device, torch.float32).contiguous()
+    _ext.call("ai4e_groupnorm_apply_pool_nhwc", _base_ptr(x), None, g32.data_ptr(), b32.data_ptr(),
+              partials.data_ptr(), pool_out.data_ptr(), n, h, w, c, groups, eps, 1, ldx, xcoff,
+              nchunks, _ext.stream_ptr(x.device))
+    off = n * nchunks * groups * 4
+    return partials[off:off + n * c * 2].view(n, c, 2)
+
+
 def gn_relu_head8_supported(z: torch.Tensor, pc) -> bool:
     """Shapes ``gn_relu_head8`` takes: bf16 NHWC z with 64 channels (may be a channel slice), H * W % 32 == 0, and a
     1x1 / stride-1 conv of 64 -> 8 output channels (the U-Net head with its classes padded to 8)."""

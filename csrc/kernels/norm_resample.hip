@@ -309,7 +309,9 @@ __global__ __launch_bounds__(256) void gn_apply_pool_kernel(const uint16_t* __re
   }
   const int PW = W >> 1, PH = H >> 1;
   const uint16_t* xn = x + static_cast<long>(n) * H * W * ldx + xcoff + 8 * c8;
-  uint16_t* yn = y + static_cast<long>(n) * H * W * ldy + ycoff + 8 * c8;
+  // y == null: only the pooled tensor is written (the U-Net's level-1 skip stays raw in the concat buffer and its
+  // consumer applies the norm while loading, conv_tile3x3.hip's prologue)
+  uint16_t* yn = y ? y + static_cast<long>(n) * H * W * ldy + ycoff + 8 * c8 : nullptr;
   uint16_t* pn = pooled + static_cast<long>(n) * PH * PW * C + 8 * c8;
   const int total = PH * PW * C8;
   for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
@@ -333,8 +335,9 @@ __global__ __launch_bounds__(256) void gn_apply_pool_kernel(const uint16_t* __re
         if (relu) f[j] = fmaxf(f[j], 0.f);
         m[j] = d == 0 ? f[j] : fmaxf(m[j], f[j]);
       }
-      *reinterpret_cast<uint4*>(yn + static_cast<long>((2 * qh + (d >> 1)) * W + 2 * qw + (d & 1)) * ldy) =
-          make_uint4(cvt_bf16x2(f[0], f[1]), cvt_bf16x2(f[2], f[3]), cvt_bf16x2(f[4], f[5]), cvt_bf16x2(f[6], f[7]));
+      if (yn)
+        *reinterpret_cast<uint4*>(yn + static_cast<long>((2 * qh + (d >> 1)) * W + 2 * qw + (d & 1)) * ldy) =
+            make_uint4(cvt_bf16x2(f[0], f[1]), cvt_bf16x2(f[2], f[3]), cvt_bf16x2(f[4], f[5]), cvt_bf16x2(f[6], f[7]));
     }
     // max of the rounded values == rounded max (rounding is monotonic)
     *reinterpret_cast<uint4*>(pn + static_cast<long>(q) * C) =

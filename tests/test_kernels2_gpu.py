@@ -122,18 +122,46 @@ def test_upsample_gn_relu_equals_apply_then_upsample(shape):
     assert buf[..., :16].abs().max() == 0
 
 
-def test_unet_fused_up_gn_matches_apply_pass(monkeypatch):
-    """FusedUNet with the decoder GroupNorm + ReLU inside the upsample == with the apply pass (AI4E_UNET_FUSED_UP_GN=0),
-    bit for bit."""
+@pytest.mark.parametrize("knob", ["AI4E_UNET_FUSED_UP_GN", "AI4E_UNET_RAW_SKIP"])
+def test_unet_deferred_norms_match_apply_passes(knob, monkeypatch):
+    """FusedUNet with the decoder GroupNorm + ReLU inside the upsample, and with the level-1 skip stored raw and
+    normalized by the last decoder's K1t on load == with the apply passes (knob = 0), bit for bit."""
     from aiforearth_api_platform_amd.models.unet import FusedUNet, unet_landcover
 
     m = unet_landcover(seed=0)
     img = torch.randint(0, 256, (2, 256, 256, 4), dtype=torch.uint8, device=DEV)
     a = FusedUNet(m, device=DEV)(img)
-    monkeypatch.setenv("AI4E_UNET_FUSED_UP_GN", "0")
+    monkeypatch.setenv(knob, "0")
     b = FusedUNet(m, device=DEV)(img)
     torch.cuda.synchronize()
     assert torch.equal(a, b)
+
+
+def test_groupnorm_pool_only_and_k1t_slice_output():
+    """K1t writing into a channel slice of a concat buffer == its contiguous output; the pool-only GroupNorm writes
+    the same pooled tensor as apply + pool, leaves the raw slice untouched and returns the same affine."""
+    from aiforearth_api_platform_amd.ops.conv import conv3x3_tile64, pack_conv
+    from aiforearth_api_platform_amd.ops.norm import group_norm_affine, group_norm_pool_only
+
+    torch.manual_seed(9)
+    n, h, w, g = 2, 32, 64, 32
+    pc = pack_conv(torch.randn(64, 64, 3, 3) / 24.0, torch.randn(64) * 0.2, pad=1).to(DEV)
+    x = torch.randn(n, h, w, 64, device=DEV).bfloat16()
+    gamma, beta = torch.rand(64, device=DEV) + 0.5, torch.randn(64, device=DEV) * 0.1
+    ref, st_ref = conv3x3_tile64(x, pc, gn_groups=g)
+    cat = torch.full((n, h, w, 128), 3.0, device=DEV, dtype=torch.bfloat16)
+    z, st = conv3x3_tile64(x, pc, gn_groups=g, out=cat[..., :64])
+    pooled = torch.empty(n, h // 2, w // 2, 64, device=DEV, dtype=torch.bfloat16)
+    aff = group_norm_pool_only(z, gamma, beta, g, st, pooled).clone()
+    pooled_ref = torch.empty_like(pooled)
+    applied = group_norm_nhwc(ref, gamma, beta, groups=g, relu=True, stats=st_ref, out=torch.empty_like(ref),
+                              pool_out=pooled_ref)
+    aff_ref = group_norm_affine(st_ref, gamma, beta, n, h * w, 64, g)
+    torch.cuda.synchronize()
+    assert torch.equal(cat[..., :64], ref) and (cat[..., 64:] == 3.0).all()
+    assert torch.equal(pooled, pooled_ref)
+    assert torch.equal(aff, aff_ref)
+    assert applied.shape == ref.shape
 
 
 @pytest.mark.parametrize("N,thr", [(100, 0.5), (2000, 0.7), (777, 0.3)])
@@ -152,6 +180,27 @@ def test_nms_matches_reference(N, thr):
     for b in range(B):
         n = int(valid[b])
         ref = nms_reference(boxes[b, :n], torch.arange(n, 0, -1).float(), thr)[:1000]
+        assert keep[b, :cnt[b]].long().tolist() == ref.tolist()
+
+
+@pytest.mark.parametrize("N,thr,max_out,dense", [(4352, 0.7, 1000, False), (8192, 0.5, 300, False),
+                                                  (130, 0.9, 1000, False), (3000, 0.3, 1000, True)])
+def test_nms_multiwave_scan_matches_reference(N, thr, max_out, dense):
+    """The RPN-sized scans (4352 proposals, max_out truncation, the 8192 limit, a dense cluster where most boxes are
+    suppressed) through the default multi-wave reduce (csrc/kernels/detection.hip nms_reduce_mw_kernel) == the greedy
+    reference."""
+    g = torch.Generator().manual_seed(N + int(dense))
+    B = 2
+    xy = torch.rand(B, N, 2, generator=g) * (60 if dense else 600)
+    wh = torch.rand(B, N, 2, generator=g) * 120 + 2
+    boxes = torch.cat([xy, xy + wh], -1)
+    valid = torch.tensor([N, N - 37], dtype=torch.int32)
+    keep, cnt = nms_batched_sorted(boxes.to(DEV), thr, max_out, valid.to(DEV))
+    keep, cnt = keep.cpu(), cnt.cpu()
+    for b in range(B):
+        n = int(valid[b])
+        ref = nms_reference(boxes[b, :n], torch.arange(n, 0, -1).float(), thr)[:max_out]
+        assert int(cnt[b]) == len(ref)
         assert keep[b, :cnt[b]].long().tolist() == ref.tolist()
 
 

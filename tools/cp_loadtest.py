@@ -115,10 +115,12 @@ def run_serve(a) -> dict:
     spec = ModelSpec("aiforearth_api_platform_amd.models.toy:tiny_classifier", shape, B, 5, {}, False)
     pool = ShardedWorkerPool(cp, "http://127.0.0.1" + path, spec, ["cpu"] * a.workers, frontends=a.frontends,
                              frontend_slots=B * 16, ring_slots=B * 4, max_delay_s=0.0005, poll_s=0.005,
-                             heartbeat_timeout_s=60.0)
+                             heartbeat_timeout_s=60.0, shards=a.shards)
     ctx = mp.get_context("spawn")
     procs = []
-    for i, shard in enumerate(pool.control_shards):  # one fake worker per control-plane shard
+    shards = pool.control_shards
+    for i in range(a.workers):  # fake workers dealt round-robin over the control-plane shards
+        shard = shards[i % len(shards)]
         parent, child = ctx.Pipe()
         p = ctx.Process(target=fake_worker, args=(child, i, 40), daemon=True)
         p.start()
