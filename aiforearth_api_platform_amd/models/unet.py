@@ -24,10 +24,8 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ..ops import _ext
 from ..ops.conv import PackedConv, conv2d_gn_nhwc, conv2d_nhwc, conv3x3_tile64, pack_conv, tile64_supported
 from ..ops.norm import (gn_relu_head8, gn_relu_head8_supported, group_norm_affine, group_norm_nhwc,
-                        group_norm_pool_only, group_norm_pool_only_supported,
                         upsample2x_nhwc)
 from ..ops.pool import maxpool2d_nhwc, preprocess_u8
 
@@ -105,40 +103,21 @@ class _FusedDouble:
         return cout % g == 0 and cout // g <= 4 and g <= 64
 
     def __call__(self, x: torch.Tensor, out: Optional[torch.Tensor] = None,
-                 pool_out: Optional[torch.Tensor] = None, head=None, defer: bool = False,
-                 pro_in: Optional[torch.Tensor] = None, raw_skip: bool = False):
+                 pool_out: Optional[torch.Tensor] = None, head=None):
         """``head``: a 1x1 PackedConv to apply after the final GroupNorm + ReLU; then returns ``(y, headed)`` where
         ``headed`` says whether ``y`` is already the head's output (fused: csrc/kernels/norm_resample.hip
-        gn_relu_head8_kernel) or still the block output. ``defer``: returns ``(z, ss)`` — the second conv's raw output
-        and its GroupNorm affine float32 [N, C, 2] for a consumer that applies norm + ReLU while reading it (the
-        decoder's upsample, ``upsample2x_nhwc(pro=ss)``) — or ``(y, None)`` when the statistics were not fused.
-        ``pro_in``: float32 [N, Cin, 2] affine (+ ReLU) the first conv applies to ``x`` while loading it (K1t only).
-        ``raw_skip`` (with ``out`` and ``pool_out``): the second conv's raw output goes to ``out`` and only the pooled
-        normalized tensor is written; returns the GroupNorm affine for the skip's consumer, or None when the block
-        took the normal path (``out`` then holds the normalized output)."""
+        gn_relu_head8_kernel) or still the block output."""
         # GroupNorm statistics come out of the conv epilogues (conv2d_gn_nhwc, K1t) where the tile allows
         if tile64_supported(x, self.c1) and self._k1t_groups(self.g1[2], self.c1.cout):
-            # e.g. the last decoder's 128 -> 64 c1 (pro_in: the level-1 skip's GroupNorm, applied on load)
-            y, st = conv3x3_tile64(x, self.c1, pro=pro_in, pro_relu=True, gn_groups=self.g1[2])
+            y, st = conv3x3_tile64(x, self.c1, gn_groups=self.g1[2])  # e.g. the last decoder's 128 -> 64 c1
         else:
-            if pro_in is not None:
-                raise ValueError("pro_in needs the K1t first conv (tile64_supported)")
             y, st = conv2d_gn_nhwc(x, self.c1, self.g1[2])
         if st is not None and tile64_supported(y, self.c2) and self._k1t_groups(self.g2[2], self.c2.cout):
             # 64 -> 64 at full resolution (K1t): c1's GroupNorm + ReLU is applied while c2 loads its input patch, so
             # the normalized c1 output is never written (csrc/kernels/conv_tile3x3.hip)
             n, h, w, c = y.shape
             ss = group_norm_affine(st, *self.g1[:2], n=n, hw=h * w, c=c, groups=self.g1[2])
-            if (raw_skip and out is not None and pool_out is not None and st is not None
-                    and group_norm_pool_only_supported(out, pool_out)):
-                z, st = conv3x3_tile64(y, self.c2, pro=ss, pro_relu=True, gn_groups=self.g2[2], out=out)
-                if st is not None:
-                    return group_norm_pool_only(z, *self.g2[:2], groups=self.g2[2], stats=st, pool_out=pool_out)
-                group_norm_nhwc(z, *self.g2[:2], groups=self.g2[2], relu=True, out=out, pool_out=pool_out)
-                return None
             z, st = conv3x3_tile64(y, self.c2, pro=ss, pro_relu=True, gn_groups=self.g2[2])
-            if defer and st is not None:
-                return z, group_norm_affine(st, *self.g2[:2], n=n, hw=h * w, c=c, groups=self.g2[2])
             if head is not None and pool_out is None and gn_relu_head8_supported(z, head):
                 # the last decoder: GroupNorm + ReLU + the 1x1 head in one pass over z (the normalized tensor is
                 # never written, and the head conv does not read it back)
@@ -146,19 +125,12 @@ class _FusedDouble:
                 return gn_relu_head8(z, ss2, head), True
             r = group_norm_nhwc(z, *self.g2[:2], groups=self.g2[2], relu=True, out=out if out is not None else z,
                                 stats=st, pool_out=pool_out)
-            if raw_skip:
-                return None
-            return (r, None) if defer else (r, False) if head is not None else r
+            return (r, False) if head is not None else r
         y = group_norm_nhwc(y, *self.g1[:2], groups=self.g1[2], relu=True, out=y, stats=st)
         z, st = conv2d_gn_nhwc(y, self.c2, self.g2[2])
-        if defer and st is not None:
-            n, h, w, c = z.shape
-            return z, group_norm_affine(st, *self.g2[:2], n=n, hw=h * w, c=c, groups=self.g2[2])
         r = group_norm_nhwc(z, *self.g2[:2], groups=self.g2[2], relu=True, out=out if out is not None else z,
                             stats=st, pool_out=pool_out)
-        if raw_skip:
-            return None
-        return (r, None) if defer else (r, False) if head is not None else r
+        return (r, False) if head is not None else r
 
 
 class FusedUNet:
@@ -180,10 +152,6 @@ class FusedUNet:
         self.fused_pool = os.environ.get("AI4E_UNET_FUSED_POOL", "1") != "0"
         # the last decoder's GroupNorm + ReLU and the 1x1 head in one pass (AI4E_UNET_FUSED_HEAD=0: apply, then conv)
         self.fused_head = os.environ.get("AI4E_UNET_FUSED_HEAD", "1") != "0"
-        # GroupNorm + ReLU of the blocks feeding an upsample inside it (AI4E_UNET_FUSED_UP_GN=0: apply pass, then up)
-        self.fused_up_gn = os.environ.get("AI4E_UNET_FUSED_UP_GN", "1") != "0"
-        # the level-1 skip stored raw, normalized by its consumer (AI4E_UNET_RAW_SKIP=0: normalized skip stored)
-        self.raw_skip = os.environ.get("AI4E_UNET_RAW_SKIP", "1") != "0"
 
     def tensors(self) -> List[torch.Tensor]:
         """Every weight tensor (packed convs + GroupNorm affine), for ``parallel.dist.broadcast_tensors``."""
@@ -206,19 +174,8 @@ class FusedUNet:
         # each encoder level's GN apply also writes the 2x2 max-pool the next level reads (no pool pass)
         if not self.fused_pool:
             return self._forward_unfused(x, cat, enc_c)
-        # the decoder blocks' last GroupNorm + ReLU is applied by the upsample that reads them (no apply pass)
-        defer = self.fused_up_gn and _ext.backend_for(x) == "hip"
-        # the level-1 skip stays raw in the concat buffer; the last decoder's K1t c1 normalizes it while loading
-        raw = (self.raw_skip and _ext.backend_for(x) == "hip" and self.fused_head
-               and tile64_supported(cat[0], self.up[3].c1) and self.up[3]._k1t_groups(self.up[3].g1[2]))
         pooled = torch.empty(n, h // 2, w // 2, enc_c[0], device=x.device, dtype=x.dtype)
-        skip_aff = self.inc(x, out=cat[0][..., : enc_c[0]], pool_out=pooled, raw_skip=raw)
-        pro0 = None
-        if raw and skip_aff is not None:
-            # [skip affine ; identity for the upsampled channels] (those are ReLU outputs: relu(1 * v + 0) == v)
-            ident = torch.zeros(n, up_c[3], 2, device=x.device, dtype=torch.float32)
-            ident[..., 0] = 1.0
-            pro0 = torch.cat([skip_aff, ident], 1)
+        self.inc(x, out=cat[0][..., : enc_c[0]], pool_out=pooled)
         for lvl in range(1, 5):
             if lvl < 4:
                 s = 2 ** (lvl + 1)
@@ -226,18 +183,16 @@ class FusedUNet:
                 self.down[lvl - 1](pooled, out=cat[lvl][..., : enc_c[lvl]], pool_out=nxt)
                 pooled = nxt
             else:
-                y, pro = self.down[3](pooled, defer=True) if defer else (self.down[3](pooled), None)
+                y = self.down[3](pooled)
         for i, lvl in enumerate((3, 2, 1, 0)):
             buf = cat[lvl]
-            upsample2x_nhwc(y, out=buf, out_coff=enc_c[lvl], pro=pro)
+            upsample2x_nhwc(y, out=buf, out_coff=enc_c[lvl])
             if i == 3 and self.fused_head:
-                y, headed = self.up[i](buf, head=self.outc, pro_in=pro0)
+                y, headed = self.up[i](buf, head=self.outc)
                 if headed:
                     return y
-            elif defer and i < 3:
-                y, pro = self.up[i](buf, defer=True)
             else:
-                y, pro = self.up[i](buf), None
+                y = self.up[i](buf)
         return conv2d_nhwc(y, self.outc)
 
     def _forward_unfused(self, x, cat, enc_c):

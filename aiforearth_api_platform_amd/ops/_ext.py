@@ -55,7 +55,6 @@ _SIGS = {
                                   _c_int, _c_int, _vp],
     "ai4e_groupnorm_apply_pool_nhwc": [_vp] * 6 + [_c_int] * 5 + [_c_float] + [_c_int] * 4 + [_vp],
     "ai4e_upsample2x_bilinear": [_vp, _vp] + [_c_int] * 7 + [_vp],
-    "ai4e_upsample2x_gn_relu": [_vp, _vp, _vp] + [_c_int] * 6 + [_vp],
     "ai4e_nms_mask": [_vp, _c_int, _c_int, _c_float, _vp, _vp],
     "ai4e_nms_reduce": [_vp, _vp, _c_int, _c_int, _c_int, _vp, _vp, _vp],
     "ai4e_rpn_decode": [_vp] * 6 + [_c_int] * 7 + [_c_float] * 5 + [_vp],

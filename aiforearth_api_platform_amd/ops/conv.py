@@ -242,13 +242,12 @@ def tile64_supported(x: torch.Tensor, pc: PackedConv) -> bool:
 
 
 def conv3x3_tile64(x: torch.Tensor, pc: PackedConv, pro: Optional[torch.Tensor] = None, pro_relu: bool = True,
-                   gn_groups: int = 0, out: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, Optional[tuple]]:
+                   gn_groups: int = 0) -> Tuple[torch.Tensor, Optional[tuple]]:
     """K1t: ``conv3x3(pro(x)) + bias`` (see ``tile64_supported``), one 8 x 32 output tile at a time per persistent
     workgroup from an LDS input patch. ``pro``: float32 [N, C, 2] per-(image, channel) affine applied to the input as
     it is loaded (``x * a + b``, then ReLU with ``pro_relu``): the previous GroupNorm, which then needs no apply pass
     (``norm.group_norm_affine``). Returns ``(y, stats)`` with ``stats`` = ``(partials, nchunks)`` GroupNorm
-    statistics of y (as ``conv2d_gn_nhwc``) when ``gn_groups``, else None. ``out``: an NHWC [N, H, W, Cout] view
-    (may be a channel slice of a wider concat buffer) that receives y."""
+    statistics of y (as ``conv2d_gn_nhwc``) when ``gn_groups``, else None."""
     n, h, w, c = x.shape
     if not tile64_supported(x, pc):
         raise ValueError("conv3x3_tile64: unsupported shape / dtype / layout")
@@ -258,21 +257,13 @@ def conv3x3_tile64(x: torch.Tensor, pc: PackedConv, pro: Optional[torch.Tensor] 
     ldx = x.stride(2)
     xoff = x.storage_offset()
     base = x.untyped_storage().data_ptr() + 2 * (xoff - xoff % ldx)
-    if out is None:
-        out = torch.empty(n, h, w, cout, device=x.device, dtype=x.dtype)
-    if (tuple(out.shape) != (n, h, w, cout) or out.dtype != x.dtype or out.stride(3) != 1 or out.stride(2) % 8
-            or out.stride(1) != w * out.stride(2) or out.stride(0) != h * out.stride(1)
-            or (out.storage_offset() % out.stride(2)) % 8):
-        raise ValueError("conv3x3_tile64: out must be an NHWC [N, H, W, Cout] bf16 view with 8-aligned channels")
-    ldy = out.stride(2)
-    ycoff = out.storage_offset() % ldy
-    ybase = out.untyped_storage().data_ptr() + 2 * (out.storage_offset() - ycoff)
+    out = torch.empty(n, h, w, cout, device=x.device, dtype=x.dtype)
     nchunks = (h // _tile_rows(cout)) * (w // 32)
     partials = None
     if gn_groups:
         partials = torch.empty(n * nchunks * gn_groups * 4 + n * cout * 2, device=x.device, dtype=torch.float32)
     _ext.call("ai4e_conv3x3_tile_fwd", base, pc.w_packed.data_ptr(), pc.bias.data_ptr(), _ext.ptr(pro),
-              int(pro_relu), ybase, n, h, w, c, cout, ldx, xoff % ldx, pc.kpad, ldy, ycoff, _ext.ptr(partials),
+              int(pro_relu), out.data_ptr(), n, h, w, c, cout, ldx, xoff % ldx, pc.kpad, cout, 0, _ext.ptr(partials),
               gn_groups, _ext.stream_ptr(x.device))
     return out, ((partials, nchunks) if gn_groups else None)
 

@@ -47,32 +47,6 @@ def group_norm_affine(stats, gamma: torch.Tensor, beta: torch.Tensor, n: int, hw
     return partials[off:off + n * c * 2].view(n, c, 2)
 
 
-def group_norm_pool_only_supported(x: torch.Tensor, pool_out: torch.Tensor) -> bool:
-    n, h, w, c = x.shape
-    return (_ext.backend_for(x) == "hip" and h % 2 == 0 and w % 2 == 0 and c % 8 == 0 and c // 8 <= 256
-            and 256 % (c // 8) == 0 and pool_out.is_contiguous() and tuple(pool_out.shape) == (n, h // 2, w // 2, c))
-
-
-def group_norm_pool_only(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, groups: int, stats,
-                         pool_out: torch.Tensor, eps: float = 1e-5) -> torch.Tensor:
-    """The 2x2/2 max-pool of ``relu(GroupNorm(x))`` into ``pool_out`` WITHOUT storing the normalized ``x`` (it stays
-    raw for a consumer that normalizes while loading). ``stats`` from the producing conv's epilogue. Returns the
-    GroupNorm affine float32 [N, C, 2] (a view into the stats buffer, written by the same launch) for that consumer
-    (``conv.conv3x3_tile64(pro=...)``)."""
-    n, h, w, c = x.shape
-    if stats is None or not group_norm_pool_only_supported(x, pool_out):
-        raise ValueError("group_norm_pool_only: unsupported shape (see group_norm_pool_only_supported)")
-    partials, nchunks = stats
-    ldx, xcoff = _nhwc_ld(x)
-    g32 = gamma.to(x.device, torch.float32).contiguous()
-    b32 = beta.to(x.device, torch.float32).contiguous()
-    _ext.call("ai4e_groupnorm_apply_pool_nhwc", _base_ptr(x), None, g32.data_ptr(), b32.data_ptr(),
-              partials.data_ptr(), pool_out.data_ptr(), n, h, w, c, groups, eps, 1, ldx, xcoff,
-              nchunks, _ext.stream_ptr(x.device))
-    off = n * nchunks * groups * 4
-    return partials[off:off + n * c * 2].view(n, c, 2)
-
-
 def gn_relu_head8_supported(z: torch.Tensor, pc) -> bool:
     """Shapes ``gn_relu_head8`` takes: bf16 NHWC z with 64 channels (may be a channel slice), H * W % 32 == 0, and a
     1x1 / stride-1 conv of 64 -> 8 output channels (the U-Net head with its classes padded to 8)."""
@@ -152,12 +126,9 @@ def group_norm_nhwc(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, gr
     return out
 
 
-def upsample2x_nhwc(x: torch.Tensor, out: Optional[torch.Tensor] = None, out_coff: int = 0,
-                    pro: Optional[torch.Tensor] = None) -> torch.Tensor:
+def upsample2x_nhwc(x: torch.Tensor, out: Optional[torch.Tensor] = None, out_coff: int = 0) -> torch.Tensor:
     """Bilinear x2 (align_corners=False). ``out`` may be a wider concat buffer; writes channels
-    [out_coff, out_coff + C). ``pro``: float32 [N, C, 2] GroupNorm affine (``group_norm_affine``) of ``x``: the input
-    is ``relu(x * a + b)`` rounded to bf16 as the apply pass would store it, so the normalized tensor is never written
-    (csrc/kernels/norm_resample.hip ``ai4e_upsample2x_gn_relu``)."""
+    [out_coff, out_coff + C)."""
     n, h, w, c = x.shape
     if out is None:
         out = torch.empty(n, 2 * h, 2 * w, c, device=x.device, dtype=x.dtype)
@@ -166,18 +137,9 @@ def upsample2x_nhwc(x: torch.Tensor, out: Optional[torch.Tensor] = None, out_cof
         x = x.contiguous()
         if out.stride(3) != 1:
             raise ValueError("bad output buffer")
-        if pro is not None:
-            if tuple(pro.shape) != (n, c, 2) or pro.dtype != torch.float32 or not pro.is_contiguous():
-                raise ValueError("pro must be float32 [N, C, 2] contiguous")
-            _ext.call("ai4e_upsample2x_gn_relu", x.data_ptr(), out.data_ptr(), pro.data_ptr(), n, h, w, c,
-                      out.stride(2), out_coff, _ext.stream_ptr(x.device))
-            return out
         _ext.call("ai4e_upsample2x_bilinear", x.data_ptr(), out.data_ptr(), n, h, w, c, out.stride(2), out_coff, 0,
                   _ext.stream_ptr(x.device))
         return out
-    if pro is not None:
-        p = pro.to(x.device, torch.float32)
-        x = torch.relu((x.float() * p[..., 0].reshape(n, 1, 1, c) + p[..., 1].reshape(n, 1, 1, c)).to(x.dtype))
     y = F.interpolate(x.permute(0, 3, 1, 2).float(), scale_factor=2, mode="bilinear", align_corners=False)
     out[..., out_coff:out_coff + c] = y.permute(0, 2, 3, 1).to(out.dtype)
     return out

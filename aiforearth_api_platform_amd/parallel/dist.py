@@ -57,9 +57,13 @@ def init_from_env(device_type: str = "cuda", build: Optional[Callable[[], None]]
     import datetime
 
     rank, world, local = env_ranks()
+    # AI4E_REHEARSE_ONE_GPU=1: every rank on cuda:0 with gloo collectives — rehearses the multi-rank GPU path (the
+    # serve topology's remote workers, HIP graphs in worker threads) on a one-GPU box; RCCL refuses two ranks per GPU
+    rehearse = device_type == "cuda" and os.environ.get("AI4E_REHEARSE_ONE_GPU") == "1"
     if device_type == "cuda":
-        torch.cuda.set_device(local)
-        device = torch.device(f"cuda:{local}")
+        dev_index = 0 if rehearse else local
+        torch.cuda.set_device(dev_index)
+        device = torch.device(f"cuda:{dev_index}")
     else:
         device = torch.device("cpu")
     if rank == 0 and build is not None:
@@ -67,7 +71,7 @@ def init_from_env(device_type: str = "cuda", build: Optional[Callable[[], None]]
     if world == 1:
         return DistEnv(rank, 1, local, device, None)
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    backend = "nccl" if device_type == "cuda" else "gloo"
+    backend = "nccl" if device_type == "cuda" and not rehearse else "gloo"
     kw = {"device_id": device} if backend == "nccl" else {}
     dist.init_process_group(backend, rank=rank, world_size=world,
                             timeout=datetime.timedelta(seconds=timeout_s), **kw)

@@ -1,8 +1,8 @@
 """In-process A/B of the U-Net forward (16 tiles of 512^2, the config-4 tile batch) with HIP-graph replays, variants
 interleaved over rounds in ONE process (cdna guide §5.4 rule 24). Variant "base" is the shipped code; "no256stats"
 takes the 256-wide K1 configs' fused GroupNorm statistics away again (the round-4 behaviour: those GroupNorms run
-their own statistics pass); "apply_up" puts the decoder GroupNorm apply pass back in front of each upsample
-(AI4E_UNET_FUSED_UP_GN=0); "stored_skip" stores the level-1 skip normalized again (AI4E_UNET_RAW_SKIP=0).
+their own statistics pass). (Round 5 also measured the decoder
+GroupNorm folded into the upsample and a raw level-1 skip with this script: neutral, see profiles/r5_pruned/.)
 
     python bench/unet_forward_ab.py [rounds 6] [replays 10]
 """
@@ -22,12 +22,6 @@ reps = int(sys.argv[2]) if len(sys.argv) > 2 else 10
 dev = torch.device("cuda:0")
 model = unet_landcover(seed=0)
 net = FusedUNet(model, device=dev)
-os.environ["AI4E_UNET_FUSED_UP_GN"] = "0"
-net_apply = FusedUNet(model, device=dev)
-os.environ.pop("AI4E_UNET_FUSED_UP_GN")
-os.environ["AI4E_UNET_RAW_SKIP"] = "0"
-net_stored = FusedUNet(model, device=dev)
-os.environ.pop("AI4E_UNET_RAW_SKIP")
 x = torch.randint(0, 256, (16, 512, 512, 4), dtype=torch.uint8, device=dev)
 orig = convmod.conv2d_gn_nhwc
 
@@ -41,8 +35,7 @@ def no256(xx, pc, groups, out=None, out_coff=0):
 
 import aiforearth_api_platform_amd.models.unet as unetmod  # noqa: E402
 
-variants = {"base": (orig, net), "no256stats": (no256, net), "apply_up": (orig, net_apply),
-            "stored_skip": (orig, net_stored)}
+variants = {"base": (orig, net), "no256stats": (no256, net)}
 graphs = {}
 for name, (fn, nn_) in variants.items():
     unetmod.conv2d_gn_nhwc = fn
@@ -64,7 +57,7 @@ graphs["base"][0].replay()  # (capture runs nothing: replay before reading an ou
 torch.cuda.synchronize()
 ref = graphs["base"][1].clone()
 err = {}
-for k in ("no256stats", "apply_up", "stored_skip"):
+for k in ("no256stats",):
     graphs[k][0].replay()
     torch.cuda.synchronize()
     err[k] = (graphs[k][1].float() - ref.float()).abs().max().item()

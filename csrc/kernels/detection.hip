@@ -447,16 +447,30 @@ __global__ __launch_bounds__(ROWSORT_THREADS) void sort_select_kernel(
     key[i] = i < N ? (static_cast<unsigned long long>(f32_order_key(sr[i])) << 32) | (0xffffffffu - static_cast<uint32_t>(i))
                    : 0ull;
   __syncthreads();
+  // bitonic network over pairs: pair p = (i, i | j) with i = p with a zero bit inserted at log2(j), so every lane
+  // has a compare-exchange in every step (the per-element form left half the lanes idle), and a lane's <= 4 pairs
+  // are all loaded before the first compare (one LDS latency per step instead of one per pair)
+  constexpr int PAIRS = ROWSORT_MAX / 2 / ROWSORT_THREADS;
+  const int half = P >> 1;
   for (int k = 2; k <= P; k <<= 1) {
     for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int i = t; i < P; i += ROWSORT_THREADS) {
-        const int l = i ^ j;
-        if (l > i) {
-          const unsigned long long a = key[i], c = key[l];
-          if (((i & k) == 0) ? (a < c) : (a > c)) {
-            key[i] = c;
-            key[l] = a;
-          }
+      unsigned long long a[PAIRS], c[PAIRS];
+      int ii[PAIRS];
+#pragma unroll
+      for (int u = 0; u < PAIRS; ++u) {
+        const int p = t + u * ROWSORT_THREADS;
+        ii[u] = ((p & ~(j - 1)) << 1) | (p & (j - 1));
+        if (p < half) {
+          a[u] = key[ii[u]];
+          c[u] = key[ii[u] | j];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < PAIRS; ++u) {
+        const int p = t + u * ROWSORT_THREADS;
+        if (p < half && (((ii[u] & k) == 0) ? (a[u] < c[u]) : (a[u] > c[u]))) {
+          key[ii[u]] = c[u];
+          key[ii[u] | j] = a[u];
         }
       }
       __syncthreads();

@@ -309,9 +309,7 @@ __global__ __launch_bounds__(256) void gn_apply_pool_kernel(const uint16_t* __re
   }
   const int PW = W >> 1, PH = H >> 1;
   const uint16_t* xn = x + static_cast<long>(n) * H * W * ldx + xcoff + 8 * c8;
-  // y == null: only the pooled tensor is written (the U-Net's level-1 skip stays raw in the concat buffer and its
-  // consumer applies the norm while loading, conv_tile3x3.hip's prologue)
-  uint16_t* yn = y ? y + static_cast<long>(n) * H * W * ldy + ycoff + 8 * c8 : nullptr;
+  uint16_t* yn = y + static_cast<long>(n) * H * W * ldy + ycoff + 8 * c8;
   uint16_t* pn = pooled + static_cast<long>(n) * PH * PW * C + 8 * c8;
   const int total = PH * PW * C8;
   for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
@@ -335,9 +333,8 @@ __global__ __launch_bounds__(256) void gn_apply_pool_kernel(const uint16_t* __re
         if (relu) f[j] = fmaxf(f[j], 0.f);
         m[j] = d == 0 ? f[j] : fmaxf(m[j], f[j]);
       }
-      if (yn)
-        *reinterpret_cast<uint4*>(yn + static_cast<long>((2 * qh + (d >> 1)) * W + 2 * qw + (d & 1)) * ldy) =
-            make_uint4(cvt_bf16x2(f[0], f[1]), cvt_bf16x2(f[2], f[3]), cvt_bf16x2(f[4], f[5]), cvt_bf16x2(f[6], f[7]));
+      *reinterpret_cast<uint4*>(yn + static_cast<long>((2 * qh + (d >> 1)) * W + 2 * qw + (d & 1)) * ldy) =
+          make_uint4(cvt_bf16x2(f[0], f[1]), cvt_bf16x2(f[2], f[3]), cvt_bf16x2(f[4], f[5]), cvt_bf16x2(f[6], f[7]));
     }
     // max of the rounded values == rounded max (rounding is monotonic)
     *reinterpret_cast<uint4*>(pn + static_cast<long>(q) * C) =
@@ -393,14 +390,9 @@ __global__ __launch_bounds__(256) void upsample2x_kernel(const uint16_t* __restr
 // even output row uses rows (i - 1, i) at ly = 0.75 (at i = 0: rows (0, min(1, H - 1)) at ly = 0), the odd one rows
 // (i, min(i + 1, H - 1)) at ly = 0.25; columns alike. Rows and columns are chosen by register selects (a runtime-
 // indexed register array would live in scratch); the weights and the sum are formed exactly as upsample2x_kernel's.
-//
-// PRO: x is a conv output whose GroupNorm (+ ReLU) was never applied; ss float2 [N, C] is its affine
-// (ai4e_groupnorm_finalize). Each of the 9 source vectors is normalized, rounded to bf16 and ReLU'd exactly as
-// gn_apply_kernel would have stored it, so the result is bit-identical to apply-then-upsample without the apply pass.
-template <typename IDX, bool PRO>
+template <typename IDX>
 __global__ __launch_bounds__(256) void upsample2x_quad_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
-                                                              int N, int H, int W, int C, int ldy, int ycoff,
-                                                              const float2* __restrict__ ss) {
+                                                              int N, int H, int W, int C, int ldy, int ycoff) {
   const int C8 = C >> 3;
   const IDX total = static_cast<IDX>(N) * H * W * C8;
   for (IDX t = static_cast<IDX>(blockIdx.x) * 256 + threadIdx.x; t < total; t += static_cast<IDX>(gridDim.x) * 256) {
@@ -419,29 +411,6 @@ __global__ __launch_bounds__(256) void upsample2x_quad_kernel(const uint16_t* __
     for (int a = 0; a < 3; ++a)
 #pragma unroll
       for (int b = 0; b < 3; ++b) v[a][b] = base[(static_cast<long>(rr[a]) * W + qq[b]) * C8];
-    if constexpr (PRO) {
-      float ga[8], gb[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const float2 ab = ss[static_cast<long>(n) * C + 8 * c8 + k];
-        ga[k] = ab.x;
-        gb[k] = ab.y;
-      }
-#pragma unroll
-      for (int a = 0; a < 3; ++a)
-#pragma unroll
-        for (int b = 0; b < 3; ++b) {
-          float f[8];
-          unpack_bf16x2(v[a][b].x, f[0], f[1]);
-          unpack_bf16x2(v[a][b].y, f[2], f[3]);
-          unpack_bf16x2(v[a][b].z, f[4], f[5]);
-          unpack_bf16x2(v[a][b].w, f[6], f[7]);
-#pragma unroll
-          for (int k = 0; k < 8; ++k) f[k] = fmaf(f[k], ga[k], gb[k]);
-          v[a][b] = make_uint4(relu_bf16x2(cvt_bf16x2(f[0], f[1])), relu_bf16x2(cvt_bf16x2(f[2], f[3])),
-                               relu_bf16x2(cvt_bf16x2(f[4], f[5])), relu_bf16x2(cvt_bf16x2(f[6], f[7])));
-        }
-    }
     const bool top = i > 0, left = j > 0;
 #pragma unroll
     for (int dy = 0; dy < 2; ++dy) {
@@ -609,11 +578,11 @@ AI4E_API int ai4e_upsample2x_bilinear(const void* x, void* y, int N, int H, int 
 #if AI4E_UPSAMPLE_QUAD
   const long quads = total / 4;
   if (quads < (1L << 31) - 4 * 8192L * 256)
-    hipLaunchKernelGGL((upsample2x_quad_kernel<int, false>), dim3(grid_for(quads)), dim3(256), 0, s,
-                       static_cast<const uint16_t*>(x), static_cast<uint16_t*>(y), N, H, W, C, ldy, ycoff, nullptr);
+    hipLaunchKernelGGL(upsample2x_quad_kernel<int>, dim3(grid_for(quads)), dim3(256), 0, s,
+                       static_cast<const uint16_t*>(x), static_cast<uint16_t*>(y), N, H, W, C, ldy, ycoff);
   else
-    hipLaunchKernelGGL((upsample2x_quad_kernel<long, false>), dim3(grid_for(quads)), dim3(256), 0, s,
-                       static_cast<const uint16_t*>(x), static_cast<uint16_t*>(y), N, H, W, C, ldy, ycoff, nullptr);
+    hipLaunchKernelGGL(upsample2x_quad_kernel<long>, dim3(grid_for(quads)), dim3(256), 0, s,
+                       static_cast<const uint16_t*>(x), static_cast<uint16_t*>(y), N, H, W, C, ldy, ycoff);
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
 #endif
   if (total < (1L << 31) - 4 * 8192L * 256)
@@ -622,24 +591,6 @@ AI4E_API int ai4e_upsample2x_bilinear(const void* x, void* y, int N, int H, int 
   else
     hipLaunchKernelGGL(upsample2x_kernel<long>, dim3(grid_for(total)), dim3(256), 0, s, static_cast<const uint16_t*>(x),
                        static_cast<uint16_t*>(y), N, H, W, C, ldy, ycoff);
-  return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
-}
-
-// Bilinear x2 of relu(GroupNorm(x)) without the normalized tensor: ss float2 [N, C] is the GroupNorm affine
-// (ai4e_groupnorm_finalize of the producing conv's epilogue statistics). Writes y channels [ycoff, ycoff + C).
-AI4E_API int ai4e_upsample2x_gn_relu(const void* x, void* y, const void* ss, int N, int H, int W, int C, int ldy,
-                                     int ycoff, hipStream_t s) {
-  if (!x || !y || !ss || N <= 0 || H <= 0 || W <= 0 || C % 8 || ldy % 8 || ycoff % 8 || ycoff + C > ldy)
-    return AI4E_EINVAL;
-  const long quads = static_cast<long>(N) * H * W * (C / 8);
-  if (quads < (1L << 31) - 4 * 8192L * 256)
-    hipLaunchKernelGGL((upsample2x_quad_kernel<int, true>), dim3(grid_for(quads)), dim3(256), 0, s,
-                       static_cast<const uint16_t*>(x), static_cast<uint16_t*>(y), N, H, W, C, ldy, ycoff,
-                       static_cast<const float2*>(ss));
-  else
-    hipLaunchKernelGGL((upsample2x_quad_kernel<long, true>), dim3(grid_for(quads)), dim3(256), 0, s,
-                       static_cast<const uint16_t*>(x), static_cast<uint16_t*>(y), N, H, W, C, ldy, ycoff,
-                       static_cast<const float2*>(ss));
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
 }
 

@@ -102,68 +102,6 @@ def test_upsample_into_concat(shape):
     assert buf[..., :16].abs().max() == 0
 
 
-@pytest.mark.parametrize("shape", [(2, 16, 16, 64), (1, 7, 9, 32), (3, 32, 32, 1024), (1, 1, 1, 8)])
-def test_upsample_gn_relu_equals_apply_then_upsample(shape):
-    """The decoder's upsample with the producing block's GroupNorm + ReLU folded in (``pro`` affine) == the apply pass
-    (bf16 store) then the plain upsample, bit for bit, and == an fp32 PyTorch reference within bf16."""
-    n, h, w, c = shape
-    torch.manual_seed(3)
-    x = (torch.randn(*shape, device=DEV) * 3 + 1).bfloat16()
-    ab = torch.stack([torch.rand(n, c, device=DEV) + 0.5, torch.randn(n, c, device=DEV)], -1).contiguous()
-    buf = torch.zeros(n, 2 * h, 2 * w, c + 16, device=DEV, dtype=torch.bfloat16)
-    upsample2x_nhwc(x, out=buf, out_coff=16, pro=ab)
-    applied = torch.relu((x.float() * ab[:, None, None, :, 0] + ab[:, None, None, :, 1]).bfloat16())
-    two = upsample2x_nhwc(applied)
-    ref = F.interpolate(applied.float().permute(0, 3, 1, 2), scale_factor=2, mode="bilinear",
-                        align_corners=False).permute(0, 2, 3, 1)
-    torch.cuda.synchronize()
-    assert torch.equal(buf[..., 16:], two)
-    assert (buf[..., 16:].float() - ref).abs().max().item() <= 0.02 * max(1.0, ref.abs().max().item())
-    assert buf[..., :16].abs().max() == 0
-
-
-@pytest.mark.parametrize("knob", ["AI4E_UNET_FUSED_UP_GN", "AI4E_UNET_RAW_SKIP"])
-def test_unet_deferred_norms_match_apply_passes(knob, monkeypatch):
-    """FusedUNet with the decoder GroupNorm + ReLU inside the upsample, and with the level-1 skip stored raw and
-    normalized by the last decoder's K1t on load == with the apply passes (knob = 0), bit for bit."""
-    from aiforearth_api_platform_amd.models.unet import FusedUNet, unet_landcover
-
-    m = unet_landcover(seed=0)
-    img = torch.randint(0, 256, (2, 256, 256, 4), dtype=torch.uint8, device=DEV)
-    a = FusedUNet(m, device=DEV)(img)
-    monkeypatch.setenv(knob, "0")
-    b = FusedUNet(m, device=DEV)(img)
-    torch.cuda.synchronize()
-    assert torch.equal(a, b)
-
-
-def test_groupnorm_pool_only_and_k1t_slice_output():
-    """K1t writing into a channel slice of a concat buffer == its contiguous output; the pool-only GroupNorm writes
-    the same pooled tensor as apply + pool, leaves the raw slice untouched and returns the same affine."""
-    from aiforearth_api_platform_amd.ops.conv import conv3x3_tile64, pack_conv
-    from aiforearth_api_platform_amd.ops.norm import group_norm_affine, group_norm_pool_only
-
-    torch.manual_seed(9)
-    n, h, w, g = 2, 32, 64, 32
-    pc = pack_conv(torch.randn(64, 64, 3, 3) / 24.0, torch.randn(64) * 0.2, pad=1).to(DEV)
-    x = torch.randn(n, h, w, 64, device=DEV).bfloat16()
-    gamma, beta = torch.rand(64, device=DEV) + 0.5, torch.randn(64, device=DEV) * 0.1
-    ref, st_ref = conv3x3_tile64(x, pc, gn_groups=g)
-    cat = torch.full((n, h, w, 128), 3.0, device=DEV, dtype=torch.bfloat16)
-    z, st = conv3x3_tile64(x, pc, gn_groups=g, out=cat[..., :64])
-    pooled = torch.empty(n, h // 2, w // 2, 64, device=DEV, dtype=torch.bfloat16)
-    aff = group_norm_pool_only(z, gamma, beta, g, st, pooled).clone()
-    pooled_ref = torch.empty_like(pooled)
-    applied = group_norm_nhwc(ref, gamma, beta, groups=g, relu=True, stats=st_ref, out=torch.empty_like(ref),
-                              pool_out=pooled_ref)
-    aff_ref = group_norm_affine(st_ref, gamma, beta, n, h * w, 64, g)
-    torch.cuda.synchronize()
-    assert torch.equal(cat[..., :64], ref) and (cat[..., 64:] == 3.0).all()
-    assert torch.equal(pooled, pooled_ref)
-    assert torch.equal(aff, aff_ref)
-    assert applied.shape == ref.shape
-
-
 @pytest.mark.parametrize("N,thr", [(100, 0.5), (2000, 0.7), (777, 0.3)])
 def test_nms_matches_reference(N, thr):
     """Parity unpinned against torchvision.ops.nms (not installed in this image): the kernel is compared with the
