@@ -61,7 +61,7 @@ def parse():
     p.add_argument("--http-seconds", type=float, default=6.0)
     p.add_argument("--http-frontends", type=int, default=4,
                    help="also measure the REST ingest with this many ingest front-end processes (0 = skip)")
-    p.add_argument("--max-queue-ms", type=float, default=12.0,
+    p.add_argument("--max-queue-ms", type=float, default=15.0,
                    help="front-end latency budget of the REST phase (429 + Retry-After past it; 0 = queue for slots)")
     p.add_argument("--http-tls", type=int, default=1,
                    help="also measure the front-end REST ingest over HTTPS (TLS terminated in the native front-ends)")

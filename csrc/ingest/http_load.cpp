@@ -13,6 +13,9 @@
 // Prints one JSON line: requests, ok, errors, busy (429s, retried after the server's Retry-After), t0, t1 (epoch s),
 // bytes_sent, cpu_user_s, cpu_sys_s.
 // IDS_OUT receives one task id per line (TaskId / TaskIds of every 2xx answer).
+// Bodies of 1 MiB or more are sent as real clients (curl) send them: headers with `Expect: 100-continue` first, the
+// body only after `100 Continue`, so a request the server's admission refuses (429) costs a header round trip, not
+// the upload of the body. The server closes such a connection after the refusal; the client dials again.
 #include <arpa/inet.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
@@ -182,6 +185,20 @@ Link dial(const char* host, int port) {
   return l;
 }
 
+bool send_bytes(Link& l, const char* p, size_t n) {
+  if (!l.ssl) {
+    struct iovec one = {const_cast<char*>(p), n};
+    return send_all(l.fd, &one, 1);
+  }
+  size_t off = 0;
+  while (off < n) {
+    const int k = SSL_write(l.ssl, p + off, static_cast<int>(std::min<size_t>(n - off, 1u << 30)));
+    if (k <= 0) return false;
+    off += static_cast<size_t>(k);
+  }
+  return true;
+}
+
 bool send_req(Link& l, const struct iovec* iov, const std::string& whole) {
   if (!l.ssl) return send_all(l.fd, iov, 2);
   size_t off = 0;
@@ -220,6 +237,8 @@ int main(int argc, char** argv) {
   std::string head = "POST " + path + " HTTP/1.1\r\nHost: " + std::string(host) + ":" + std::to_string(port) +
                      "\r\nContent-Type: " + ctype + "\r\nContent-Length: " + std::to_string(body.size()) + "\r\n";
   for (int i = 10; i < argc; ++i) head += std::string(argv[i]) + "\r\n";
+  const bool expect = body.size() >= (1u << 20);
+  if (expect) head += "Expect: 100-continue\r\n";
   head += "\r\n";
   const std::string whole = g_tls ? head + body : std::string();  // (TLS: one SSL_write per request)
 
@@ -235,6 +254,35 @@ int main(int argc, char** argv) {
       struct iovec iov[2] = {{const_cast<char*>(head.data()), head.size()},
                              {const_cast<char*>(body.data()), body.size()}};
       while (l.fd >= 0 && now() < t_end) {
+        if (expect) {
+          // headers, then the body only once the server's admission let the request in
+          double retry_ms = 0;
+          int st = send_bytes(l, head.data(), head.size()) ? read_response(l, buf, rbody, &retry_ms) : 0;
+          if (st == 100) {
+            ++r.requests;
+            r.bytes += static_cast<double>(head.size() + body.size());
+            st = send_bytes(l, body.data(), body.size()) ? read_response(l, buf, rbody, &retry_ms) : 0;
+          } else if (st != 0) {
+            ++r.requests;
+            r.bytes += static_cast<double>(head.size());
+          }
+          if (st >= 200 && st < 300) {
+            ++r.ok;
+            extract_ids(rbody, r.ids);
+            continue;
+          }
+          l.close();  // a refusal before the body: the server closes the connection
+          buf.clear();
+          if (st == 429) {
+            ++r.busy;
+            const double ms = std::min(1000.0, std::max(0.5, retry_ms));
+            std::this_thread::sleep_for(std::chrono::microseconds(static_cast<long>(ms * 1e3)));
+          } else {
+            ++r.errors;
+          }
+          l = dial(host, port);
+          continue;
+        }
         if (!send_req(l, iov, whole)) {
           l.close();
           l = dial(host, port);

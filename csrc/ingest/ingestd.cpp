@@ -171,7 +171,7 @@ struct Shard {
   // latency-budget admission projects a new request's queue wait as (slots in use + n) / rate
   std::atomic<int64_t> freed{0};
   std::mutex rate_mu;
-  double rate = 0.0, rate_t = 0.0;
+  double rate = 0.0, rate_t = 0.0, peak = 0.0;
   int64_t rate_n = 0;
 
   double service_rate() {
@@ -185,10 +185,14 @@ struct Shard {
       const double r = static_cast<double>(n - rate_n) / (t - rate_t);
       // an idle partition (nothing in use) keeps its last rate: no traffic is not a slow GPU
       if (n > rate_n || slots->used() > 0) rate = rate == 0.0 ? r : 0.7 * rate + 0.3 * r;
+      // the capacity estimate holds the smoothed rate's recent peak and decays ~10 % per second: a dip in demand
+      // (clients backing off after 429s) must not read as a slower GPU, or admission would throttle further and
+      // feed on itself
+      peak = std::max(rate, peak * std::pow(0.9, t - rate_t));
       rate_t = t;
       rate_n = n;
     }
-    return rate;
+    return peak;
   }
 
   bool send_frame(const std::string& payload) {

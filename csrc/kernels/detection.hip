@@ -208,13 +208,15 @@ __global__ __launch_bounds__(64 * NMS_MW_WAVES) void nms_reduce_mw_kernel(const 
   const int w0 = lane, w1 = lane + 64;
   for (int wb = 0; wb < nblk; ++wb) {
     if (lane == (wb & 63)) s_part[wave] = wb < 64 ? rem0 : rem1;  // blocks <= wb-2 (wb-1 is wave 0's carry)
+    __syncthreads();  // B1
+    __syncthreads();  // B2
+    // block wb-1's rows (loads issued after the previous B2): OR-ed only now, so their latency overlaps this
+    // block's diagonal instead of delaying B1
 #pragma unroll
     for (int u = 0; u < NMS_MW_ROWS; ++u) {
       rem0 |= p0[u];
       rem1 |= p1[u];
     }
-    __syncthreads();  // B1
-    __syncthreads();  // B2
     unsigned long long kbits = s_keep;
     const int kept = s_kept;
     // this wave's share of the block's kept rows: the k-th kept box (bit order) goes to wave 1 + k % (waves - 1)
@@ -669,13 +671,6 @@ __global__ __launch_bounds__(256) void roi_align_fpn_kernel(FpnLevels lv, const 
 // Same op, one workgroup per RoI (PW * C/8 <= 256 lanes, one (pw, 8-channel chunk) each) walking the output
 // rows in order: the sample rows of bin row ph and ph+1 share feature rows, and with the whole RoI on one CU
 // those re-reads hit its L1 instead of going to L2 from 7 different CUs (the per-row grid's pattern).
-//
-// ROWS (sampling 2): the 2 * PH sample rows are walked in order with the two feature rows of the current sample held
-// in registers (4 columns each: the lane's 2 sample columns x 2 corners); a feature row shared by consecutive samples
-// (sample spacing bh / 2 < 1 px for the 7-14 px windows the level assignment produces) is loaded once instead of once
-// per sample, about halving the loads (~60 instead of 112 per lane per RoI). The row indices are workgroup-uniform,
-// so the reuse tests are uniform branches. Same weights and summation order as the per-row form: bit-identical.
-template <bool ROWS>
 __global__ __launch_bounds__(256) void roi_align_fpn_roi_kernel(FpnLevels lv, const float* __restrict__ rois,
                                                                 uint16_t* __restrict__ out, int C, int R, int PH,
                                                                 int PW, int sampling, int aligned) {
@@ -722,61 +717,6 @@ __global__ __launch_bounds__(256) void roi_align_fpn_roi_kernel(FpnLevels lv, co
       xo[ix][1] = x1i * C + 8 * c8;
       xw[ix][0] = 1.f - lx;
       xw[ix][1] = lx;
-    }
-    if constexpr (ROWS) {
-      uint4 ra[4], rb[4];  // feature rows ya / yb at the lane's 4 columns (ix * 2 + cx)
-      int ya = -1, yb = -1;
-      float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-      for (int s2 = 0; s2 < 2 * PH; ++s2) {
-        const int ph = s2 >> 1, iy = s2 & 1;
-        float y = y1 + ph * bh + (iy + 0.5f) * bh * 0.5f;
-        const bool yok = !(y < -1.f || y > H);
-        y = fmaxf(y, 0.f);
-        int y0 = static_cast<int>(y), y1i;
-        if (y0 >= H - 1) { y1i = y0 = H - 1; y = static_cast<float>(y0); } else { y1i = y0 + 1; }
-        const float ly = y - y0;
-        const float yw0 = yok ? (1.f - ly) * inv : 0.f, yw1 = yok ? ly * inv : 0.f;
-        // rows needed (y0 <= y1i) never decrease with s2: shift or load
-        if (y0 == yb) {
-#pragma unroll
-          for (int k = 0; k < 4; ++k) ra[k] = rb[k];
-          ya = yb;
-        } else if (y0 != ya) {
-          const uint16_t* fr = f + static_cast<long>(y0) * W * C;
-#pragma unroll
-          for (int k = 0; k < 4; ++k) ra[k] = *reinterpret_cast<const uint4*>(fr + xo[k >> 1][k & 1]);
-          ya = y0;
-        }
-        if (y1i == ya) {
-#pragma unroll
-          for (int k = 0; k < 4; ++k) rb[k] = ra[k];
-          yb = ya;
-        } else if (y1i != yb) {
-          const uint16_t* fr = f + static_cast<long>(y1i) * W * C;
-#pragma unroll
-          for (int k = 0; k < 4; ++k) rb[k] = *reinterpret_cast<const uint4*>(fr + xo[k >> 1][k & 1]);
-          yb = y1i;
-        }
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {  // q = (ix * 2 + cy) * 2 + cx, the per-row form's order within one iy
-          const int ix = q >> 2, cy = (q >> 1) & 1, cx = q & 1;
-          const float w = xok[ix] ? (cy ? yw1 : yw0) * xw[ix][cx] : 0.f;
-          const uint4 v = cy ? rb[ix * 2 + cx] : ra[ix * 2 + cx];
-          float a, b;
-          unpack_bf16x2(v.x, a, b); acc[0] += w * a; acc[1] += w * b;
-          unpack_bf16x2(v.y, a, b); acc[2] += w * a; acc[3] += w * b;
-          unpack_bf16x2(v.z, a, b); acc[4] += w * a; acc[5] += w * b;
-          unpack_bf16x2(v.w, a, b); acc[6] += w * a; acc[7] += w * b;
-        }
-        if (iy) {
-          *reinterpret_cast<uint4*>(o + static_cast<long>(ph) * PW * C) =
-              make_uint4(pack_bf16x2(acc[0], acc[1]), pack_bf16x2(acc[2], acc[3]), pack_bf16x2(acc[4], acc[5]),
-                         pack_bf16x2(acc[6], acc[7]));
-#pragma unroll
-          for (int k = 0; k < 8; ++k) acc[k] = 0.f;
-        }
-      }
-      return;
     }
     for (int ph = 0; ph < PH; ++ph) {
       long ro[2][2];
@@ -1029,15 +969,8 @@ AI4E_API int ai4e_roi_align_fpn_nhwc(const void* f0, const void* f1, const void*
     const char* e = getenv("AI4E_ROI_PER_ROI");  // A/B switch: 0 = one workgroup per (RoI, output row)
     return e ? atoi(e) : 1;
   }();
-  static const int rows = [] {
-    const char* e = getenv("AI4E_ROI_ROWS");  // A/B switch: 0 = every sample loads its 4 corner rows
-    return e ? atoi(e) : 1;
-  }();
-  if (per_roi && PW * (C / 8) <= 256 && rows)
-    hipLaunchKernelGGL(roi_align_fpn_roi_kernel<true>, dim3(static_cast<unsigned>(R)), dim3(256), 0, s, lv,
-                       static_cast<const float*>(rois), static_cast<uint16_t*>(out), C, R, PH, PW, sampling, aligned);
-  else if (per_roi && PW * (C / 8) <= 256)
-    hipLaunchKernelGGL(roi_align_fpn_roi_kernel<false>, dim3(static_cast<unsigned>(R)), dim3(256), 0, s, lv,
+  if (per_roi && PW * (C / 8) <= 256)
+    hipLaunchKernelGGL(roi_align_fpn_roi_kernel, dim3(static_cast<unsigned>(R)), dim3(256), 0, s, lv,
                        static_cast<const float*>(rois), static_cast<uint16_t*>(out), C, R, PH, PW, sampling, aligned);
   else
     hipLaunchKernelGGL(roi_align_fpn_kernel, dim3(static_cast<unsigned>(R * PH)), dim3(256), 0, s,
