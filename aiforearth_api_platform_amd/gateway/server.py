@@ -471,11 +471,13 @@ class Gateway:
             except ValueError:
                 pass
 
-    def run(self, host: str = "127.0.0.1", port: int = 8080, socks=None, ssl_context=None) -> None:
+    def run(self, host: str = "127.0.0.1", port: int = 8080, socks=None, ssl_context=None,
+            internal_only: bool = False) -> None:
         """Serve on (host, port), or on the given listening sockets (public SO_REUSEPORT socket shared with
         the ingest front-ends + the internal socket they proxy to: serve.open_listeners), until the drain
         (install_signal_handlers) has finished. ``ssl_context`` (default: from the config's TLS cert/key) makes the
-        public listener HTTPS; the front-ends' internal loopback listener (the second socket) stays plain HTTP."""
+        public listener HTTPS; the front-ends' internal loopback listener (the second socket) stays plain HTTP.
+        ``internal_only``: ``socks`` is just that internal listener (native front-ends own the public port)."""
         if ssl_context is None:
             ssl_context = server_ssl_context(self.cp.cfg.tls_cert, self.cp.cfg.tls_key)
 
@@ -485,7 +487,7 @@ class Gateway:
             runner = web.AppRunner(self.app, handle_signals=False, access_log=None, shutdown_timeout=2.0)
             await runner.setup()
             if socks:
-                sites = [web.SockSite(runner, sk, ssl_context=ssl_context if i == 0 else None)
+                sites = [web.SockSite(runner, sk, ssl_context=ssl_context if i == 0 and not internal_only else None)
                          for i, sk in enumerate(socks)]
             else:
                 sites = [web.TCPSite(runner, host, port, ssl_context=ssl_context)]

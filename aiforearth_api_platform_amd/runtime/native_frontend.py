@@ -17,6 +17,7 @@ from __future__ import annotations
 import os
 import subprocess
 import tempfile
+import time
 from typing import Dict, List, Optional
 
 from .. import _build
@@ -70,13 +71,16 @@ def _token(v) -> str:
 
 def spawn_native_frontends(n: int, pools: Dict[str, object], routes: List[dict], host: str, port: int,
                            internal_url: str, security: Optional[dict] = None,
-                           ack_timeout_s: float = 30.0, max_queue_ms: float = 0.0) -> List[NativeFrontend]:
+                           ack_timeout_s: float = 30.0, max_queue_ms: float = 0.0,
+                           wait_ready_s: float = 30.0) -> List[NativeFrontend]:
     """Start ``n`` native front-ends; arguments as :func:`runtime.frontend.spawn_frontends`.
 
     Each front-end attaches to every control-plane shard of every pool endpoint (one ``shard`` line per shard: its
     ring partition, scheduler connection and the task-store digits its ids end in); a route lists its endpoint's
     shards and the front-end picks the least-loaded one per request. ``max_queue_ms`` > 0: latency-budgeted
-    admission (429 + Retry-After once a request's projected queue wait exceeds the budget)."""
+    admission (429 + Retry-After once a request's projected queue wait exceeds the budget). Returns once every
+    front-end listens on the public port (each writes one byte to a ready pipe after ``listen``), so the caller
+    can hand the port over (:func:`handover_public_port`)."""
     import multiprocessing as mp
 
     if not n or not pools:
@@ -87,7 +91,7 @@ def spawn_native_frontends(n: int, pools: Dict[str, object], routes: List[dict],
     _build.build_tools()
     ihost, iport = internal_url.split("://", 1)[1].rsplit(":", 1)
     names = list(pools)
-    procs = []
+    procs, readies = [], []
     for i in range(n):
         lines = [f"listen {_token(host)} {int(port)}", f"internal {_token(ihost)} {int(iport)}",
                  f"ack_timeout {float(ack_timeout_s)}"]
@@ -96,7 +100,9 @@ def spawn_native_frontends(n: int, pools: Dict[str, object], routes: List[dict],
         lines += [f"key {_token(k)}" for k in sec.get("keys") or []]
         if sec.get("tls_cert"):
             lines.append(f"tls {_token(os.path.abspath(sec['tls_cert']))} {_token(os.path.abspath(sec['tls_key']))}")
-        child_ends, fds = [], []
+        ready_r, ready_w = os.pipe()
+        lines.append(f"ready {ready_w}")
+        child_ends, fds = [], [ready_w]
         shard_lines: Dict[str, List[int]] = {}  # endpoint name -> its shard line indices
         for name in names:
             ep = pools[name]
@@ -130,5 +136,27 @@ def spawn_native_frontends(n: int, pools: Dict[str, object], routes: List[dict],
         p = subprocess.Popen([binary, cfg_path], pass_fds=fds, close_fds=True)
         for c in child_ends:
             c.close()
+        os.close(ready_w)
         procs.append(NativeFrontend(p, cfg_path))
+        readies.append(ready_r)
+    import select
+
+    deadline = time.time() + wait_ready_s
+    for fd in readies:
+        try:
+            r, _, _ = select.select([fd], [], [], max(0.0, deadline - time.time()))
+            if not r or not os.read(fd, 1):
+                raise RuntimeError("a native ingest front-end did not start listening")
+        finally:
+            os.close(fd)
     return procs
+
+
+def handover_public_port(socks: list, frontends: list) -> list:
+    """With native front-ends listening (they run the latency-budgeted admission), the serving process stops
+    accepting on the shared public port: a connection a 429 closed reconnects to a front-end, never drifting onto a
+    path without admission. Returns the sockets the gateway keeps serving (the internal one)."""
+    if frontends and len(socks) > 1 and all(isinstance(p, NativeFrontend) for p in frontends):
+        socks[0].close()
+        return socks[1:]
+    return socks

@@ -97,13 +97,17 @@ def http_phase(cp, pool, seconds: float, batch: int, item_shape, path: str, fron
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     socks = open_listeners("127.0.0.1", port, shared=frontends > 0)
+    impl = os.environ.get("AI4E_FRONTEND_IMPL", "native")
+    # native front-ends take the public port over (serve.py's handover_public_port): the gateway serves only its
+    # internal listener, the one the front-ends proxy to
+    served = socks[1:] if frontends and impl == "native" else socks
 
     def serve():
         loop = asyncio.new_event_loop()
         asyncio.set_event_loop(loop)
         runner = web.AppRunner(gw.app, access_log=None)
         loop.run_until_complete(runner.setup())
-        for sk in socks:
+        for sk in served:
             loop.run_until_complete(web.SockSite(runner, sk).start())
         box["loop"], box["runner"] = loop, runner
         ready.set()
@@ -113,7 +117,6 @@ def http_phase(cp, pool, seconds: float, batch: int, item_shape, path: str, fron
     th = threading.Thread(target=serve, daemon=True)
     th.start()
     ready.wait(30)
-    impl = os.environ.get("AI4E_FRONTEND_IMPL", "native")
     spawn = spawn_frontends
     if impl == "native":
         from .native_frontend import spawn_native_frontends as spawn
@@ -129,7 +132,12 @@ def http_phase(cp, pool, seconds: float, batch: int, item_shape, path: str, fron
                "127.0.0.1", port, f"http://127.0.0.1:{socks[1].getsockname()[1]}", security=sec, **kw) \
         if frontends else []
     if fe:
-        time.sleep(5.0 if impl != "native" else 1.0)  # they start and bind the shared port
+        if impl == "native":  # (they listen already: the serving process leaves the public port to them)
+            from .native_frontend import handover_public_port
+
+            handover_public_port(socks, fe)
+        else:
+            time.sleep(5.0)  # they start and bind the shared port
     url = f"{'https' if tls else 'http'}://127.0.0.1:{port}/v1/bench/async"
     rng = np.random.default_rng(7)
     img = rng.integers(0, 256, tuple(item_shape), dtype=np.uint8)
@@ -340,14 +348,15 @@ def run_node_bench(args, spec, path: str, metric: str, unit: str = "images/s", c
     # device drain bracket the whole run on every rank.
     tail = max(1, args.inflight + 1)
     warm_n = args.warmup * B * counted_world
-    sync(denv)
-    tune_gc()
     tel = None
     if rank == 0 and args.device == "cuda":
         from ..utils.gpu_telemetry import GpuTelemetry
 
+        # (started before the barrier: its init must not hold rank 0 back while the other ranks' clients already run)
         tel = GpuTelemetry(denv.local_rank)  # clocks / power / hotspot sampled every 200 ms (fail-soft)
         tel.start()
+    tune_gc()
+    sync(denv)
     t_start = time.perf_counter()
     cth = threading.Thread(target=client.run, args=(args.warmup + args.steps + tail,), daemon=True)
     cth.start()

@@ -207,12 +207,17 @@ def main(argv=None) -> int:
     nfe = frontend_count(cfg)
     socks = open_listeners(cfg.host, cfg.port, shared=nfe > 0)
     frontends = start_frontends(cfg, doc, endpoints, cfg.port, socks[1].getsockname()[1]) if nfe else []
+    # native front-ends own the public port once they listen (admission on every public connection)
+    from .runtime.native_frontend import handover_public_port
+
+    n_socks = len(socks)
+    socks = handover_public_port(socks, frontends)
     # SIGTERM drain: the front-ends stop first (their own graceful shutdown), so no new tasks arrive meanwhile
     gw.on_drain.append(lambda: [p.terminate() for p in frontends])
     print(f"ai4e-mi355x gateway on {'https' if cfg.tls_cert else 'http'}://{cfg.host}:{cfg.port} endpoints={list(endpoints)} "
           f"ingest_frontends={len(frontends)}", file=sys.stderr, flush=True)
     try:
-        gw.run(cfg.host, cfg.port, socks=socks)
+        gw.run(cfg.host, cfg.port, socks=socks, internal_only=len(socks) < n_socks)
     finally:
         for p in frontends:
             p.terminate()

@@ -275,7 +275,7 @@ int main(int argc, char** argv) {
           buf.clear();
           if (st == 429) {
             ++r.busy;
-            const double ms = std::min(1000.0, std::max(0.5, retry_ms));
+            const double ms = std::min(100.0, std::max(0.5, retry_ms));
             std::this_thread::sleep_for(std::chrono::microseconds(static_cast<long>(ms * 1e3)));
           } else {
             ++r.errors;
@@ -305,7 +305,7 @@ int main(int argc, char** argv) {
           extract_ids(rbody, r.ids);
         } else if (st == 429) {  // admission refused: back off for the server's projected wait, then retry
           ++r.busy;
-          const double ms = std::min(1000.0, std::max(0.5, retry_ms));
+          const double ms = std::min(100.0, std::max(0.5, retry_ms));
           std::this_thread::sleep_for(std::chrono::microseconds(static_cast<long>(ms * 1e3)));
         } else {
           ++r.errors;

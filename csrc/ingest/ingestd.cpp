@@ -183,8 +183,9 @@ struct Shard {
       rate_n = n;
     } else if (t - rate_t >= 0.05) {
       const double r = static_cast<double>(n - rate_n) / (t - rate_t);
-      // an idle partition (nothing in use) keeps its last rate: no traffic is not a slow GPU
-      if (n > rate_n || slots->used() > 0) rate = rate == 0.0 ? r : 0.7 * rate + 0.3 * r;
+      // only samples with completions update the rate: an idle partition (no traffic) or a pipeline still
+      // filling (slots in use, none freed yet) is not a slow GPU
+      if (n > rate_n) rate = rate == 0.0 ? r : 0.7 * rate + 0.3 * r;
       // the capacity estimate holds the smoothed rate's recent peak and decays ~10 % per second: a dip in demand
       // (clients backing off after 429s) must not read as a slower GPU, or admission would throttle further and
       // feed on itself
@@ -314,6 +315,7 @@ struct Config {
   int internal_port = 0;
   double ack_timeout = 30.0, alloc_timeout = 60.0;
   double max_queue_s = 0.0;  // latency budget of an ingested request's queue wait (0: no budget, wait for slots)
+  int ready_fd = -1;  // "ready FD": one byte written once the public socket listens (the parent hands the port over)
   std::vector<std::string> keys;
   std::vector<std::unique_ptr<Shard>> shards;
   std::vector<std::unique_ptr<Route>> routes;  // longest prefix first
@@ -321,7 +323,7 @@ struct Config {
 
 Config g_cfg;
 
-// "listen H P" | "internal H P" | "key K" | "tls CERT KEY" | "ack_timeout S" | "alloc_timeout S"
+// "listen H P" | "internal H P" | "key K" | "tls CERT KEY" | "ack_timeout S" | "alloc_timeout S" | "ready FD"
 // "shard IDX FD SHM NSLOTS ITEM BASE LEN ENDPOINT SHAPE" | "route PREFIX MODE SHARD MCL MC TYPES|- KEYS|-"
 void parse_config(const char* path) {
   std::ifstream in(path);
@@ -361,6 +363,8 @@ void parse_config(const char* path) {
       ls >> g_cfg.ack_timeout;
     } else if (kw == "alloc_timeout") {
       ls >> g_cfg.alloc_timeout;
+    } else if (kw == "ready") {
+      ls >> g_cfg.ready_fd;
     } else if (kw == "max_queue_ms") {
       double ms = 0;
       ls >> ms;
@@ -866,7 +870,9 @@ bool ingest(Conn& c, const Request& r, Route& route, Shard& s, bool batch) {
     const double rate = s.service_rate();
     const double wait = rate > 0.0 ? static_cast<double>(s.slots->used() + n) / rate : 0.0;
     if (wait > g_cfg.max_queue_s) {
-      const double retry_s = std::max(0.001, wait - g_cfg.max_queue_s);
+      // the hint is capped at twice the budget: a request refused on a stale estimate comes back soon and is judged
+      // again, instead of idling its client for the whole projected wait
+      const double retry_s = std::min(2.0 * g_cfg.max_queue_s, std::max(0.001, wait - g_cfg.max_queue_s));
       const std::string h = "Retry-After: " + std::to_string(static_cast<int>(std::ceil(retry_s))) +
                             "\r\nx-ai4e-retry-after-ms: " + std::to_string(static_cast<int>(std::ceil(retry_s * 1e3))) +
                             "\r\n";
@@ -1041,6 +1047,11 @@ int main(int argc, char** argv) {
   sigaction(SIGALRM, &al, nullptr);
   for (auto& s : g_cfg.shards) std::thread([p = s.get()] { p->reader(); }).detach();
   int lfd = listen_on(g_cfg.host, g_cfg.port);
+  if (g_cfg.ready_fd >= 0) {
+    const char one = 'R';
+    (void)!::write(g_cfg.ready_fd, &one, 1);
+    ::close(g_cfg.ready_fd);
+  }
   std::fprintf(stderr, "ai4e_ingestd pid %d on %s:%d (%zu endpoints, %zu routes)\n", getpid(), g_cfg.host.c_str(),
                g_cfg.port, g_cfg.shards.size(), g_cfg.routes.size());
   while (true) {

@@ -77,10 +77,12 @@ def test_frontend_processes_end_to_end(impl):
             proc.kill()
 
 
-def test_native_frontend_admission_parity(tmp_path):
-    """Subscription keys (global + per route), content type, length and payload-size errors through a native
-    front-end and the serving process: every request class gets the same status on both paths, the ids it
-    mints are real tasks, and encoded / odd-sized payloads fall through to the serving process."""
+@pytest.mark.parametrize("nfe", [2, 0])
+def test_native_frontend_admission_parity(tmp_path, nfe):
+    """Subscription keys (global + per route), content type, length and payload-size errors through native
+    front-ends (nfe=2: they own the public port and proxy what they do not ingest) and through the serving process
+    alone (nfe=0): every request class gets the same status on both paths, the ids it mints are real tasks, and
+    encoded / odd-sized payloads fall through to the serving process."""
     from aiforearth_api_platform_amd.gateway.security import KEY_HEADER
 
     doc = yaml.safe_load(open(os.path.join(ROOT, "examples", "platform_cpu.yaml")))
@@ -93,7 +95,7 @@ def test_native_frontend_admission_parity(tmp_path):
     cfgp = tmp_path / "platform.yaml"
     cfgp.write_text(yaml.safe_dump(doc))
     port = _port()
-    env = dict(os.environ, PYTHONPATH=ROOT, AI4E_FRONTEND_PROCESSES="2", AI4E_FRONTEND_IMPL="native",
+    env = dict(os.environ, PYTHONPATH=ROOT, AI4E_FRONTEND_PROCESSES=str(nfe), AI4E_FRONTEND_IMPL="native",
                AI4E_SUBSCRIPTION_KEYS="gk")
     proc = subprocess.Popen([sys.executable, "-m", "aiforearth_api_platform_amd.serve", "--config", str(cfgp),
                              "--port", str(port)], cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
@@ -137,7 +139,9 @@ def test_native_frontend_admission_parity(tmp_path):
                     js = r.json()
                     ids += js["TaskIds"] if "TaskIds" in js else [js["TaskId"]]
                     assert r.headers.get("x-b3-traceid")
-        assert servers == {True, False}  # both the native front-ends and the serving process answered
+        # with front-ends every public connection is theirs (ingest answered natively, the rest proxied to the
+        # serving process); without, the serving process answers all
+        assert servers == ({True} if nfe else {False})
         # keep-alive: several requests on one connection, batch + proxied task queries interleaved
         ka = requests.Session()
         ka.trust_env = False
@@ -160,7 +164,7 @@ def test_native_frontend_admission_parity(tmp_path):
         assert r.json()["Result"]["classes"][0] == 2
         assert s.get(f"{base}/v1/taskmanagement/task/nope", headers={KEY_HEADER: "gk"}).status_code == 204
         assert json.loads(s.get(base + "/openapi.json").text)["openapi"].startswith("3.")
-        assert "ai4e_ingestd pid" in _drain(proc)
+        assert ("ai4e_ingestd pid" in _drain(proc)) == (nfe > 0)
     finally:
         proc.terminate()
         try:
@@ -192,6 +196,7 @@ def test_submit_ids_protocol_in_process():
     from aiforearth_api_platform_amd.runtime.ingest import IngestShard
     from aiforearth_api_platform_amd.runtime.worker_pool import ModelSpec, WorkerPool
 
+    shape = (4, 4, 3)
     spec = ModelSpec("aiforearth_api_platform_amd.models.toy:tiny_classifier", shape, max_batch=8, topk=2,
                      use_graphs=False)
     cp = ControlPlane(Config.load(env={}))
@@ -437,7 +442,6 @@ def test_latency_budget_admission_429_no_lost_tasks(shape):
 
     from aiohttp import web
 
-    shape = (4, 4, 3)
     spec = ModelSpec("aiforearth_api_platform_amd.models.toy:tiny_classifier", shape, max_batch=8, topk=2,
                      kwargs={"delay_ms": 20.0}, use_graphs=False)
     cp = ControlPlane(Config.load(env={}))

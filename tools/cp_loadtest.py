@@ -20,11 +20,13 @@ import sys
 import threading
 import time
 
+import numpy as np
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def fake_worker(conn, rank: int, row_bytes: int):
+def fake_worker(conn, rank: int, row_bytes: int, batch_ms: float = 0.0):
     import numpy as np
 
     from aiforearth_api_platform_amd.runtime import protocol as P
@@ -42,6 +44,8 @@ def fake_worker(conn, rank: int, row_bytes: int):
         if t == P.F_BATCH:
             bid, slots = P.parse_batch(buf)
             n = slots.shape[0]
+            if batch_ms > 0:  # a GPU that takes batch_ms per batch (REST admission experiments)
+                time.sleep(batch_ms / 1e3)
             now = time.monotonic()
             fc.done(bid, np.zeros(n, np.uint8), zeros[: n * row_bytes], row_bytes, (now, now, now, 0.0, 0.0))
         elif t == P.F_STOP:
@@ -110,7 +114,7 @@ def run_serve(a) -> dict:
 
     cp = ControlPlane(Config.load(env={}))
     path = "/v1/ai4e/lt/classify"
-    shape = (4, 4, 3)
+    shape = tuple(int(v) for v in a.item_shape.split("x"))
     B = a.batch
     spec = ModelSpec("aiforearth_api_platform_amd.models.toy:tiny_classifier", shape, B, 5, {}, False)
     pool = ShardedWorkerPool(cp, "http://127.0.0.1" + path, spec, ["cpu"] * a.workers, frontends=a.frontends,
@@ -122,7 +126,7 @@ def run_serve(a) -> dict:
     for i in range(a.workers):  # fake workers dealt round-robin over the control-plane shards
         shard = shards[i % len(shards)]
         parent, child = ctx.Pipe()
-        p = ctx.Process(target=fake_worker, args=(child, i, 40), daemon=True)
+        p = ctx.Process(target=fake_worker, args=(child, i, 40, a.batch_ms), daemon=True)
         p.start()
         child.close()
         shard.attach_remote(i, parent, device="fake")
@@ -152,9 +156,10 @@ def run_serve(a) -> dict:
     threading.Thread(target=serve, daemon=True).start()
     socks[0].close()  # only the front-ends answer on the public port
     fe = spawn_native_frontends(a.frontends, {"lt": ep}, [{"prefix": "/v1/lt/async", "mode": "async", "endpoint": "lt"}],
-                                "127.0.0.1", port, f"http://127.0.0.1:{socks[1].getsockname()[1]}")
+                                "127.0.0.1", port, f"http://127.0.0.1:{socks[1].getsockname()[1]}",
+                                max_queue_ms=a.max_queue_ms)
     time.sleep(1.0)
-    body = bytes(B * 48)
+    body = bytes(B * int(np.prod(shape)))
     samples = {}
 
     def sampler():
@@ -179,7 +184,8 @@ def run_serve(a) -> dict:
            "fake_workers": a.workers, "ingest_frontends": a.frontends, "batch": B, "http_requests": res["requests"],
            "http_errors": res["errors"], "busy_429": res.get("busy"), "accepted_tasks": len(ids),
            "client_cpu_s": round(res["client_cpu_s"], 2), "seconds": a.seconds, "cpu_count": os.cpu_count(),
-           "p50_task_latency_ms": round(percentile(lat, 50) * 1e3, 3) if lat else None}
+           "p50_task_latency_ms": round(percentile(lat, 50) * 1e3, 3) if lat else None,
+           "item_shape": list(shape), "batch_ms": a.batch_ms, "max_queue_ms": a.max_queue_ms}
     for p in fe:
         p.terminate()
     for p in fe:
@@ -219,6 +225,9 @@ def main():
     ap.add_argument("--frontends", type=int, default=4)
     ap.add_argument("--conc", type=int, default=16, help="(--serve) HTTP connections per load process")
     ap.add_argument("--client-procs", type=int, default=2)
+    ap.add_argument("--item-shape", default="4x4x3", help="(--serve) uint8 item shape HxWxC")
+    ap.add_argument("--batch-ms", type=float, default=0.0, help="(--serve) fake GPU time per batch")
+    ap.add_argument("--max-queue-ms", type=float, default=0.0, help="(--serve) front-end latency budget")
     ap.add_argument("--json-out", default="")
     a = ap.parse_args()
     if a.serve:
