@@ -192,6 +192,11 @@ class WorkerPool:
                                           linger_s=max_delay_s, depth=pipeline_depth, retry_delay_s=retry_delay_s,
                                           hb_timeout_s=heartbeat_timeout_s, poll_s=poll_s)
         self.sched.add_local_ring(self.ring.slots)
+        # shard load (tasks queued / finished) in shm for the native front-ends' admission (unlinked with the scheduler)
+        self.stat_name = ""
+        if int(frontends) > 0 and hasattr(self.sched, "open_stat"):
+            name = f"ai4e_stat_{os.getpid()}_{id(self):x}"
+            self.stat_name = name if self.sched.open_stat(name) else ""
         if shard is not None:
             self.sched.set_store_shards(list(shard.store_shards))
         if spec.stage_endpoints:

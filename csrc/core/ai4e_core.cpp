@@ -320,5 +320,6 @@ PYBIND11_MODULE(_ai4e_core, m) {
            })
       .def("batch_histogram", &NodeScheduler::batch_histogram)
       .def("images_done", &NodeScheduler::images_done)
+      .def("open_stat", &NodeScheduler::open_stat)
       .def("stop", &NodeScheduler::stop, py::call_guard<py::gil_scoped_release>());
 }

@@ -35,6 +35,8 @@
 #pragma once
 
 #include <arpa/inet.h>
+#include <fcntl.h>
+#include <sys/mman.h>
 #include <sys/socket.h>
 #include <unistd.h>
 
@@ -46,6 +48,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <new>
 #include <string>
 #include <thread>
 #include <unordered_map>
@@ -103,7 +106,40 @@ class NodeScheduler {
                 int64_t ring_slots, SchedConfig cfg)
       : store_(std::move(store)), queue_(std::move(queue)), endpoint_(std::move(endpoint)), ring_slots_(ring_slots),
         cfg_(cfg), hist_(12, 0) {}
-  ~NodeScheduler() { stop(); }
+  ~NodeScheduler() {
+    stop();
+    if (stat_) {
+      munmap(stat_, sizeof(ShardStat));
+      shm_unlink(("/" + stat_name_).c_str());
+    }
+  }
+
+  // Shard load published in a small POSIX shm block (the native ingest front-ends map it read-only): tasks queued
+  // into this scheduler and tasks finished, so a front-end's latency-budget admission projects the shard's whole
+  // backlog over its whole completion rate instead of its own partition's share (which, with several front-ends
+  // and 250-image requests, is mostly bodies still uploading and batch-quantization noise).
+  struct ShardStat {
+    std::atomic<uint64_t> enq;
+    std::atomic<uint64_t> done;
+    std::atomic<uint64_t> pending;  // written by the front-ends: admitted request bodies still uploading
+    uint64_t pad[5];
+  };
+  bool open_stat(const std::string& name) {
+    if (stat_ || name.empty() || name.find('/') != std::string::npos) return false;
+    const int fd = shm_open(("/" + name).c_str(), O_CREAT | O_RDWR, 0600);
+    if (fd < 0) return false;
+    void* p = MAP_FAILED;
+    if (ftruncate(fd, sizeof(ShardStat)) == 0)
+      p = mmap(nullptr, sizeof(ShardStat), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    ::close(fd);
+    if (p == MAP_FAILED) {
+      shm_unlink(("/" + name).c_str());
+      return false;
+    }
+    stat_ = new (p) ShardStat{};
+    stat_name_ = name;
+    return true;
+  }
 
   // Partition of the payload ring freed in this process (the ingest ring of the gateway).
   void add_local_ring(std::shared_ptr<SlotRing> ring) {
@@ -404,6 +440,7 @@ class NodeScheduler {
     auto ids = shard < 0 ? store_->create_many(endpoint_, slots.size(), "created", trace)
                          : store_->create_many_in(static_cast<size_t>(shard), endpoint_, slots.size(), "created", trace);
     const size_t sent = queue_->send_many(ids, slots);
+    if (stat_) stat_->enq.fetch_add(sent);
     if (sent < ids.size()) {  // backpressure / closed: CacheConnectorUpsert.cs:181-199
       std::vector<std::string> rest(ids.begin() + static_cast<long>(sent), ids.end());
       std::vector<int64_t> rs(slots.begin() + static_cast<long>(sent), slots.end());
@@ -435,6 +472,7 @@ class NodeScheduler {
     slots.resize(k);
     free_slots(drop);
     const size_t sent = queue_->send_many(ids, slots);
+    if (stat_) stat_->enq.fetch_add(sent);
     if (sent < ids.size()) {
       std::vector<std::string> rest(ids.begin() + static_cast<long>(sent), ids.end());
       std::vector<int64_t> rs(slots.begin() + static_cast<long>(sent), slots.end());
@@ -793,6 +831,7 @@ class NodeScheduler {
         w.retried_items += retry.size();
       }
       images_done_.fetch_add(n - retry.size());
+      if (stat_) stat_->done.fetch_add(n - retry.size());
       std::vector<std::string> fed;
       fed.reserve(n);
       for (uint32_t i = 0; i < n; ++i)
@@ -816,6 +855,8 @@ class NodeScheduler {
   size_t store_rr_ = 0;
   std::atomic<uint64_t> next_bid_{1};
   std::atomic<uint64_t> images_done_{0};
+  ShardStat* stat_ = nullptr;
+  std::string stat_name_;
   std::mutex fail_mu_;
   std::condition_variable fail_cv_;
   std::vector<int> failed_;

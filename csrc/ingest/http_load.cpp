@@ -96,7 +96,7 @@ bool send_all(int fd, const struct iovec* iov0, int cnt) {
 }
 
 // Reads one response; returns the status (0 on a broken connection) and its body.
-int read_response(Link& l, std::string& buf, std::string& body, double* retry_ms = nullptr) {
+int read_response(Link& l, std::string& buf, std::string& body, double* retry_ms = nullptr, bool* closes = nullptr) {
   size_t hend;
   while ((hend = buf.find("\r\n\r\n")) == std::string::npos) {
     char tmp[65536];
@@ -110,6 +110,7 @@ int read_response(Link& l, std::string& buf, std::string& body, double* retry_ms
   for (auto& ch : head) ch = static_cast<char>(std::tolower(static_cast<unsigned char>(ch)));
   auto p = head.find("content-length:");
   if (p != std::string::npos) clen = std::strtoull(head.c_str() + p + 15, nullptr, 10);
+  if (closes) *closes = head.find("connection: close") != std::string::npos;
   if (retry_ms) {  // 429: the server's projected wait (x-ai4e-retry-after-ms, else Retry-After seconds)
     *retry_ms = 0;
     auto q = head.find("x-ai4e-retry-after-ms:");
@@ -257,7 +258,8 @@ int main(int argc, char** argv) {
         if (expect) {
           // headers, then the body only once the server's admission let the request in
           double retry_ms = 0;
-          int st = send_bytes(l, head.data(), head.size()) ? read_response(l, buf, rbody, &retry_ms) : 0;
+          bool closes = false;
+          int st = send_bytes(l, head.data(), head.size()) ? read_response(l, buf, rbody, &retry_ms, &closes) : 0;
           if (st == 100) {
             ++r.requests;
             r.bytes += static_cast<double>(head.size() + body.size());
@@ -271,8 +273,6 @@ int main(int argc, char** argv) {
             extract_ids(rbody, r.ids);
             continue;
           }
-          l.close();  // a refusal before the body: the server closes the connection
-          buf.clear();
           if (st == 429) {
             ++r.busy;
             const double ms = std::min(100.0, std::max(0.5, retry_ms));
@@ -280,7 +280,11 @@ int main(int argc, char** argv) {
           } else {
             ++r.errors;
           }
-          l = dial(host, port);
+          if (st == 0 || closes) {  // (a refusal the server closed: dial again; a keep-alive one is reused)
+            l.close();
+            buf.clear();
+            l = dial(host, port);
+          }
           continue;
         }
         if (!send_req(l, iov, whole)) {

@@ -174,10 +174,15 @@ struct Shard {
   double rate = 0.0, rate_t = 0.0, peak = 0.0;
   int64_t rate_n = 0;
 
+  // the scheduler shard's load counters (NodeScheduler::open_stat, "stat NAME" on the shard line): tasks queued /
+  // finished across every ingest path of the shard; null = estimate from this partition alone
+  // [0] queued, [1] finished (the scheduler's), [2] admitted bodies still uploading (every front-end's)
+  std::atomic<uint64_t>* st = nullptr;
+
   double service_rate() {
     std::lock_guard<std::mutex> g(rate_mu);
     const double t = ai4e::mono_now();
-    const int64_t n = freed.load();
+    const int64_t n = st ? static_cast<int64_t>(st[1].load(std::memory_order_relaxed)) : freed.load();
     if (rate_t == 0.0) {
       rate_t = t;
       rate_n = n;
@@ -194,6 +199,37 @@ struct Shard {
       rate_n = n;
     }
     return peak;
+  }
+
+  // request-body upload rate of this front-end (bytes/s, EWMA over completed bodies): a request's tasks only join
+  // the queue once its body has arrived, by when the shard has worked off nbytes / upload_bw of its backlog
+  std::mutex up_mu;
+  double upload_bw = 0.0;
+  void note_upload(double bytes, double secs) {
+    if (secs <= 0.0 || bytes < 65536.0) return;
+    std::lock_guard<std::mutex> g(up_mu);
+    const double bw = bytes / secs;
+    upload_bw = upload_bw == 0.0 ? bw : 0.8 * upload_bw + 0.2 * bw;
+  }
+
+  // projected queue wait of n more items (nbytes of body) once they are queued: the shard's backlog (queued, not yet
+  // finished, plus every front-end's admitted bodies still arriving) over its completion rate, minus what drains
+  // while this body uploads; or this partition's slots in use over its FREE rate when the shard publishes no counters
+  double projected_wait(int64_t n, double nbytes) {
+    const double rate = service_rate();
+    if (rate <= 0.0) return 0.0;
+    if (st) {
+      const uint64_t e = st[0].load(std::memory_order_relaxed), d = st[1].load(std::memory_order_relaxed);
+      const double backlog = (e > d ? static_cast<double>(e - d) : 0.0) +
+                             static_cast<double>(st[2].load(std::memory_order_relaxed));
+      double up = 0.0;
+      {
+        std::lock_guard<std::mutex> g(up_mu);
+        if (upload_bw > 0.0) up = nbytes / upload_bw;
+      }
+      return std::max(0.0, (backlog + static_cast<double>(n)) / rate - up);
+    }
+    return static_cast<double>(slots->used() + n) / rate;
   }
 
   bool send_frame(const std::string& payload) {
@@ -373,8 +409,14 @@ void parse_config(const char* path) {
       auto s = std::make_unique<Shard>();
       std::string shm;
       ls >> s->idx >> s->fd >> shm >> s->nslots >> s->item >> s->base >> s->len >> s->endpoint >> s->shape_str;
-      std::string dg;
+      std::string dg, stat;
       if (ls >> dg && !dg.empty() && dg != "-") s->digits = dg;
+      if (ls >> stat && !stat.empty() && stat != "-") {
+        const int sfd = shm_open(("/" + stat).c_str(), O_RDWR, 0);
+        void* sp = sfd >= 0 ? mmap(nullptr, 64, PROT_READ | PROT_WRITE, MAP_SHARED, sfd, 0) : MAP_FAILED;
+        if (sfd >= 0) ::close(sfd);
+        if (sp != MAP_FAILED) s->st = static_cast<std::atomic<uint64_t>*>(sp);  // (else: partition estimate)
+      }
       s->endpoint_path = ai4e::absolute_path(s->endpoint);
       int mfd = shm_open(("/" + shm).c_str(), O_RDWR, 0);
       if (mfd < 0) {
@@ -867,8 +909,7 @@ bool ingest(Conn& c, const Request& r, Route& route, Shard& s, bool batch) {
     // latency-budgeted admission (the reference's busy path: BackendQueueProcessor.cs:54-64 answers 429 and the
     // message is retried later; ai4e_service.py:122-125): a request whose projected queue wait exceeds the budget is
     // refused with 429 + Retry-After instead of queueing behind a deep ring
-    const double rate = s.service_rate();
-    const double wait = rate > 0.0 ? static_cast<double>(s.slots->used() + n) / rate : 0.0;
+    const double wait = s.projected_wait(n, static_cast<double>(nbytes));
     if (wait > g_cfg.max_queue_s) {
       // the hint is capped at twice the budget: a request refused on a stale estimate comes back soon and is judged
       // again, instead of idling its client for the whole projected wait
@@ -876,11 +917,21 @@ bool ingest(Conn& c, const Request& r, Route& route, Shard& s, bool batch) {
       const std::string h = "Retry-After: " + std::to_string(static_cast<int>(std::ceil(retry_s))) +
                             "\r\nx-ai4e-retry-after-ms: " + std::to_string(static_cast<int>(std::ceil(retry_s * 1e3))) +
                             "\r\n";
+      // (an Expect: 100-continue client sends no body after a final answer, so its connection stays usable: a
+      // refusal costs a header round trip, not a reconnect and, over HTTPS, a new TLS handshake)
       if (lower(r.get("expect")) != "100-continue" && !c.discard(static_cast<size_t>(nbytes))) return false;
-      return respond(c, 429, "application/json", message_json("Service is busy, please try again later."),
-                     ka && lower(r.get("expect")) != "100-continue", h);
+      return respond(c, 429, "application/json", message_json("Service is busy, please try again later."), ka, h);
     }
   }
+  // admitted: until its tasks exist the body counts as the shard's backlog for every front-end's admission
+  struct Pending {
+    std::atomic<uint64_t>* p;
+    uint64_t n;
+    ~Pending() {
+      if (p) p->fetch_sub(n);
+    }
+  } pending{g_cfg.max_queue_s > 0.0 && s.st ? &s.st[2] : nullptr, static_cast<uint64_t>(n)};
+  if (pending.p) pending.p->fetch_add(pending.n);
   if (lower(r.get("expect")) == "100-continue" && !c.send_all("HTTP/1.1 100 Continue\r\n\r\n", 25)) return false;
   std::vector<int64_t> sl = s.slots->alloc(n, g_cfg.alloc_timeout);
   if (sl.empty()) {  // no ring slot in time: nothing was created
@@ -888,6 +939,7 @@ bool ingest(Conn& c, const Request& r, Route& route, Shard& s, bool batch) {
     return respond(c, 429, "application/json", message_json("Service is busy, please try again later."), ka);
   }
   // body -> ring: one recv per contiguous slot run
+  const double t_up = ai4e::mono_now();
   for (size_t i = 0; i < sl.size();) {
     size_t j = i + 1;
     while (j < sl.size() && sl[j] == sl[j - 1] + 1) ++j;
@@ -897,6 +949,7 @@ bool ingest(Conn& c, const Request& r, Route& route, Shard& s, bool batch) {
     }
     i = j;
   }
+  s.note_upload(static_cast<double>(nbytes), ai4e::mono_now() - t_up);
   // B3: a child span of the caller's (utils/tracing.py b3_from_headers / b3_pack)
   std::string trace_id = r.get("x-b3-traceid"), parent = r.get("x-b3-spanid"), sampled = r.get("x-b3-sampled");
   if (trace_id.empty()) trace_id = hexid(c.rng, 128);
