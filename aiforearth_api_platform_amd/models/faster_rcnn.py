@@ -142,7 +142,8 @@ class FasterRCNN:
         return self._anchor_cache[key]
 
     # ------------------------------------------------------------------ RPN + proposals
-    def proposals(self, P: List[torch.Tensor], img_hw: Tuple[int, int]) -> Tuple[torch.Tensor, torch.Tensor]:
+    def proposals(self, P: List[torch.Tensor], img_hw: Tuple[int, int]
+                  ) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
         cfg = self.cfg
         A = self.num_anchors
         B = P[0].shape[0]
@@ -168,14 +169,17 @@ class FasterRCNN:
         _, boxes_s, boxes_off, _, valid = sort_select(scores, boxes, max(img_hw) + 1.0, groups=lvl)
         keep, count = nms_batched_sorted(boxes_off, cfg.rpn_nms_thresh, cfg.post_nms_top_n, valid)
         crumb("rpn.nms", keep)
-        props, _, _ = gather_keep(keep, boxes=boxes_s)
-        return props, count
+        # the proposals [B, R, 4] and the same boxes as RoIAlign rows [B * R, 5] (image, box), one launch
+        props, _, _, rois = gather_keep(keep, boxes=boxes_s, rois=True)
+        return props, count, rois
 
     # ------------------------------------------------------------------ box head + postprocess
-    def box_head(self, P: List[torch.Tensor], props: torch.Tensor, img_hw):
+    def box_head(self, P: List[torch.Tensor], props: torch.Tensor, img_hw, rois: Optional[torch.Tensor] = None):
+        """``rois``: the proposals as RoIAlign rows [B * R, 5] (from ``proposals``), else formed here."""
         B, R, _ = props.shape
-        bidx = torch.arange(B, device=props.device, dtype=torch.float32)[:, None, None].expand(B, R, 1)
-        rois = torch.cat([bidx, props], -1).reshape(B * R, 5)
+        if rois is None:
+            bidx = torch.arange(B, device=props.device, dtype=torch.float32)[:, None, None].expand(B, R, 1)
+            rois = torch.cat([bidx, props], -1).reshape(B * R, 5)
         strides = [img_hw[0] // p.shape[1] for p in P[:4]]
         feats = roi_align_fpn(P[:4], [1.0 / s for s in strides], rois, (7, 7), 2)  # [B*R, 7, 7, C]
         crumb("box.roi_align", feats)
@@ -208,8 +212,8 @@ class FasterRCNN:
         crumb("backbone", feats[-1])
         P = self.fpn(feats)
         crumb("fpn", P[-1])
-        props, count = self.proposals(P, img_hw)
-        pred = self.box_head(P, props, img_hw)
+        props, count, rois = self.proposals(P, img_hw)
+        pred = self.box_head(P, props, img_hw, rois)
         crumb("box.head", pred)
         return self.postprocess(props, count, pred, img_hw)
 

@@ -60,9 +60,9 @@ _SIGS = {
     "ai4e_rpn_decode": [_vp] * 6 + [_c_int] * 7 + [_c_float] * 5 + [_vp],
     "ai4e_row_sort_desc": [_vp, _c_int, _c_int, _vp, _vp],
     "ai4e_sort_select": [_vp, _vp, _vp, _c_int, _c_float, _c_int, _c_int] + [_vp] * 7,
-    "ai4e_gather_keep": [_vp, _c_int, _c_int, _c_int] + [_vp] * 7,
+    "ai4e_gather_keep": [_vp, _c_int, _c_int, _c_int] + [_vp] * 8,
     "ai4e_rpn_topk": [_vp] + [_c_int] * 5 + [_vp, _vp],
-    "ai4e_det_decode": [_vp] * 6 + [_c_int] * 4 + [_vp] + [_c_float] * 4 + [_vp],
+    "ai4e_det_decode": [_vp] * 6 + [_c_int] * 4 + [_vp] + [_c_float] * 4 + [_c_int, _vp],
     "ai4e_roi_align_nhwc": [_vp, _vp, _vp] + [_c_int] * 7 + [_c_float, _c_int, _c_int, _vp],
     "ai4e_roi_align_fpn_nhwc": [_vp] * 8 + [_c_int] * 6 + [_vp],
     "ai4e_crop_resize_nhwc": [_vp, _vp, _vp, _vp] + [_c_int] * 7 + [_vp],

@@ -138,9 +138,10 @@ def sort_select(scores: torch.Tensor, boxes: torch.Tensor, scale: float, groups:
 
 
 def gather_keep(keep: torch.Tensor, boxes: Optional[torch.Tensor] = None, scores: Optional[torch.Tensor] = None,
-                labels: Optional[torch.Tensor] = None):
+                labels: Optional[torch.Tensor] = None, rois: bool = False):
     """Rows kept by NMS (``keep`` [B, K] int32, -1 = padding): (boxes [B, K, 4], scores [B, K], labels [B, K]) gathered
-    from [B, N, ...] sources (None where the source is None), zero at padding. HIP: one launch (gather_keep_kernel)."""
+    from [B, N, ...] sources (None where the source is None), zero at padding. HIP: one launch (gather_keep_kernel).
+    ``rois``: a fourth result, the boxes as RoIAlign rows [B * K, 5] = (image, x1, y1, x2, y2), from the same launch."""
     B, K = keep.shape
     src = next(t for t in (boxes, scores, labels) if t is not None)
     N = src.shape[1]
@@ -153,15 +154,21 @@ def gather_keep(keep: torch.Tensor, boxes: Optional[torch.Tensor] = None, scores
         bo = None if bs is None else torch.empty(B, K, 4, dtype=torch.float32, device=dev)
         so = None if ss is None else torch.empty(B, K, dtype=torch.float32, device=dev)
         lo = None if ls is None else torch.empty(B, K, dtype=torch.int64, device=dev)
+        ro = torch.empty(B * K, 5, dtype=torch.float32, device=dev) if rois else None
+        if rois and bs is None:
+            raise ValueError("gather_keep(rois=True) needs boxes")
         _ext.call("ai4e_gather_keep", kp.data_ptr(), B, K, N, _ext.ptr(bs), _ext.ptr(ss), _ext.ptr(ls), _ext.ptr(bo),
-                  _ext.ptr(so), _ext.ptr(lo), _ext.stream_ptr(dev))
-        return bo, so, lo
+                  _ext.ptr(so), _ext.ptr(lo), _ext.ptr(ro), _ext.stream_ptr(dev))
+        return (bo, so, lo, ro) if rois else (bo, so, lo)
     k = keep.clamp(min=0).long()
     pad = keep < 0
     bo = None if boxes is None else torch.gather(boxes.float(), 1, k[..., None].expand(B, K, 4)).masked_fill(
         pad[..., None], 0.0)
     so = None if scores is None else torch.gather(scores.float(), 1, k).masked_fill(pad, 0.0)
     lo = None if labels is None else torch.gather(labels.long(), 1, k).masked_fill(pad, 0)
+    if rois:
+        bidx = torch.arange(B, device=dev, dtype=torch.float32)[:, None, None].expand(B, K, 1)
+        return bo, so, lo, torch.cat([bidx, bo], -1).reshape(B * K, 5)
     return bo, so, lo
 
 
@@ -195,7 +202,8 @@ def det_decode(pred: torch.Tensor, props: torch.Tensor, count: torch.Tensor, num
     B, R, ldp = pred.shape
     nc = num_classes
     if _ext.backend_for(pred) == "hip":
-        pred = pred.float().contiguous()
+        bf16 = pred.dtype == torch.bfloat16  # (read as bf16 in the kernel: no conversion launch)
+        pred = pred.contiguous() if bf16 else pred.float().contiguous()
         boxes = torch.empty(B, R * (nc - 1), 4, device=pred.device, dtype=torch.float32)
         scores = torch.empty(B, R * (nc - 1), device=pred.device, dtype=torch.float32)
         labels = torch.empty(B, R * (nc - 1), device=pred.device, dtype=torch.int64)
@@ -203,7 +211,7 @@ def det_decode(pred: torch.Tensor, props: torch.Tensor, count: torch.Tensor, num
         _ext.call("ai4e_det_decode", pred.data_ptr(), props.float().contiguous().data_ptr(),
                   count.to(torch.int32).contiguous().data_ptr(), boxes.data_ptr(), scores.data_ptr(), labels.data_ptr(),
                   B, R, ldp, nc, ctypes.addressof(w4), float(img_hw[0]), float(img_hw[1]), float(score_thresh),
-                  float(clip), _ext.stream_ptr(pred.device))
+                  float(clip), int(bf16), _ext.stream_ptr(pred.device))
         return boxes, scores, labels
     pred = pred.float()
     logits, deltas = pred[..., :nc], pred[..., nc: 5 * nc].reshape(B, R, nc, 4)
@@ -246,7 +254,7 @@ def nms_batched_sorted(boxes: torch.Tensor, thr: float, max_out: int, valid: Opt
         boxes = boxes.float().contiguous()
         words = (N + 63) // 64
         mask = torch.empty(B, N, words, dtype=torch.int64, device=boxes.device)
-        keep = torch.full((B, max_out), -1, dtype=torch.int32, device=boxes.device)
+        keep = torch.empty(B, max_out, dtype=torch.int32, device=boxes.device)  # (the reduce pads with -1)
         count = torch.empty(B, dtype=torch.int32, device=boxes.device)
         vptr = None if valid is None else valid.to(torch.int32).contiguous()
         st = _ext.stream_ptr(boxes.device)

@@ -114,6 +114,7 @@ __global__ __launch_bounds__(64) void nms_reduce_kernel(const unsigned long long
     }
   }
   if (lane == 0) count[b] = min(kept, max_out);
+  for (int i = min(kept, max_out) + lane; i < max_out; i += 64) keep[static_cast<long>(b) * max_out + i] = -1;
 }
 
 // Multi-wave form of nms_reduce_kernel (one workgroup of NMS_MW_WAVES waves per image). The per-image greedy scan
@@ -198,6 +199,8 @@ __global__ __launch_bounds__(64 * NMS_MW_WAVES) void nms_reduce_mw_kernel(const 
       if (kept >= max_out) break;
     }
     if (lane == 0) count[b] = min(kept, max_out);
+    // the rows past the count are padding (-1): the caller needs no fill launch
+    for (int i = min(kept, max_out) + lane; i < max_out; i += 64) keep[static_cast<long>(b) * max_out + i] = -1;
     return;
   }
   // row waves: partial bitmap words lane and lane + 64
@@ -502,14 +505,24 @@ __global__ __launch_bounds__(ROWSORT_THREADS) void sort_select_kernel(
 __global__ __launch_bounds__(256) void gather_keep_kernel(const int* __restrict__ keep, int K, int N,
                                                           const float4* __restrict__ bsrc, const float* __restrict__ ssrc,
                                                           const long* __restrict__ lsrc, float4* __restrict__ bout,
-                                                          float* __restrict__ sout, long* __restrict__ lout, int total) {
+                                                          float* __restrict__ sout, long* __restrict__ lout,
+                                                          float* __restrict__ rout, int total) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= total) return;
   const long b = i / K;
   const int k = keep[i];
   const bool ok = k >= 0 && k < N;
   const long src = b * N + (ok ? k : 0);
-  if (bout) bout[i] = ok ? bsrc[src] : make_float4(0.f, 0.f, 0.f, 0.f);
+  const float4 bx = ok && bsrc ? bsrc[src] : make_float4(0.f, 0.f, 0.f, 0.f);
+  if (bout) bout[i] = bx;
+  if (rout) {  // RoIAlign rows (image, x1, y1, x2, y2): no arange + cat launches
+    float* r = rout + 5L * i;
+    r[0] = static_cast<float>(b);
+    r[1] = bx.x;
+    r[2] = bx.y;
+    r[3] = bx.z;
+    r[4] = bx.w;
+  }
   if (sout) sout[i] = ok ? ssrc[src] : 0.f;
   if (lout) lout[i] = ok ? lsrc[src] : 0;
 }
@@ -518,7 +531,14 @@ __global__ __launch_bounds__(256) void gather_keep_kernel(const int* __restrict_
 // the class's box decoded from its proposal with the regression weights, clipped; score -1 unless the RoI
 // is real (r < count[b]), the score clears thresh and the box is at least 1e-2 wide and high.
 // pred: fp32 [B, R, ldp] (nc logits, then 4 nc deltas); props fp32 [B, R, 4]; outputs [B, R * (nc - 1)].
-__global__ __launch_bounds__(256) void det_decode_kernel(const float* __restrict__ pred, const float4* __restrict__ props,
+// pred element as fp32 (T = float, or uint16_t = the predictor's bf16 output read without a conversion launch)
+__device__ __forceinline__ float pred_at(const float* p, int i) { return p[i]; }
+__device__ __forceinline__ float pred_at(const uint16_t* p, int i) {
+  return __uint_as_float(static_cast<uint32_t>(p[i]) << 16);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void det_decode_kernel(const T* __restrict__ pred, const float4* __restrict__ props,
                                                          const int* __restrict__ count, float4* __restrict__ boxes,
                                                          float* __restrict__ scores, long* __restrict__ labels, int B,
                                                          int R, int ldp, int nc, float4 wts, float img_h, float img_w,
@@ -529,18 +549,18 @@ __global__ __launch_bounds__(256) void det_decode_kernel(const float* __restrict
   const int b = t / (R * ncf);
   const int rc = t - b * R * ncf;
   const int r = rc / ncf, c = rc - r * ncf + 1;
-  const float* lp = pred + (static_cast<long>(b) * R + r) * ldp;
-  float mx = lp[0];
-  for (int q = 1; q < nc; ++q) mx = fmaxf(mx, lp[q]);
+  const T* lp = pred + (static_cast<long>(b) * R + r) * ldp;
+  float mx = pred_at(lp, 0);
+  for (int q = 1; q < nc; ++q) mx = fmaxf(mx, pred_at(lp, q));
   float den = 0.f;
-  for (int q = 0; q < nc; ++q) den += expf(lp[q] - mx);
-  const float sc = expf(lp[c] - mx) / den;
+  for (int q = 0; q < nc; ++q) den += expf(pred_at(lp, q) - mx);
+  const float sc = expf(pred_at(lp, c) - mx) / den;
   const float4 pr = props[static_cast<long>(b) * R + r];
-  const float* dp = lp + nc + 4 * c;
+  const T* dp = lp + nc + 4 * c;
   const float w = pr.z - pr.x, h = pr.w - pr.y;
   const float cx = pr.x + 0.5f * w, cy = pr.y + 0.5f * h;
-  const float dx = dp[0] / wts.x, dy = dp[1] / wts.y;
-  const float dw = fminf(dp[2] / wts.z, clip), dh = fminf(dp[3] / wts.w, clip);
+  const float dx = pred_at(dp, 0) / wts.x, dy = pred_at(dp, 1) / wts.y;
+  const float dw = fminf(pred_at(dp, 2) / wts.z, clip), dh = fminf(pred_at(dp, 3) / wts.w, clip);
   const float pcx = dx * w + cx, pcy = dy * h + cy, pw = expf(dw) * w, ph = expf(dh) * h;
   const float x1 = fminf(fmaxf(pcx - 0.5f * pw, 0.f), img_w), y1 = fminf(fmaxf(pcy - 0.5f * ph, 0.f), img_h);
   const float x2 = fminf(fmaxf(pcx + 0.5f * pw, 0.f), img_w), y2 = fminf(fmaxf(pcy + 0.5f * ph, 0.f), img_h);
@@ -908,13 +928,14 @@ AI4E_API int ai4e_sort_select(const void* scores, const void* boxes, const void*
 }
 
 AI4E_API int ai4e_gather_keep(const void* keep, int B, int K, int N, const void* bsrc, const void* ssrc, const void* lsrc,
-                              void* bout, void* sout, void* lout, hipStream_t s) {
+                              void* bout, void* sout, void* lout, void* rout, hipStream_t s) {
   if (B <= 0 || K <= 0) return AI4E_OK;
-  if (!keep || N <= 0 || (bout && !bsrc) || (sout && !ssrc) || (lout && !lsrc)) return AI4E_EINVAL;
+  if (!keep || N <= 0 || (bout && !bsrc) || (sout && !ssrc) || (lout && !lsrc) || (rout && !bsrc)) return AI4E_EINVAL;
   const int total = B * K;
   hipLaunchKernelGGL(gather_keep_kernel, dim3((total + 255) / 256), dim3(256), 0, s, static_cast<const int*>(keep), K, N,
                      static_cast<const float4*>(bsrc), static_cast<const float*>(ssrc), static_cast<const long*>(lsrc),
-                     static_cast<float4*>(bout), static_cast<float*>(sout), static_cast<long*>(lout), total);
+                     static_cast<float4*>(bout), static_cast<float*>(sout), static_cast<long*>(lout),
+                     static_cast<float*>(rout), total);
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
 }
 
@@ -928,14 +949,22 @@ AI4E_API int ai4e_rpn_topk(const void* head, int B, int HW, int ldh, int A, int 
 
 AI4E_API int ai4e_det_decode(const void* pred, const void* props, const void* count, void* boxes, void* scores,
                              void* labels, int B, int R, int ldp, int nc, const float* wts4, float img_h, float img_w,
-                             float thresh, float clip, hipStream_t s) {
+                             float thresh, float clip, int pred_bf16, hipStream_t s) {
   if (B <= 0 || R <= 0) return AI4E_OK;
   if (!pred || !props || !count || !boxes || !scores || !labels || !wts4 || nc < 2 || ldp < 5 * nc) return AI4E_EINVAL;
   const long n = static_cast<long>(B) * R * (nc - 1);
-  hipLaunchKernelGGL(det_decode_kernel, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, s,
-                     static_cast<const float*>(pred), static_cast<const float4*>(props), static_cast<const int*>(count),
-                     static_cast<float4*>(boxes), static_cast<float*>(scores), static_cast<long*>(labels), B, R, ldp, nc,
-                     make_float4(wts4[0], wts4[1], wts4[2], wts4[3]), img_h, img_w, thresh, clip);
+  const dim3 g(static_cast<unsigned>((n + 255) / 256));
+  const float4 w = make_float4(wts4[0], wts4[1], wts4[2], wts4[3]);
+  if (pred_bf16)
+    hipLaunchKernelGGL(det_decode_kernel<uint16_t>, g, dim3(256), 0, s, static_cast<const uint16_t*>(pred),
+                       static_cast<const float4*>(props), static_cast<const int*>(count), static_cast<float4*>(boxes),
+                       static_cast<float*>(scores), static_cast<long*>(labels), B, R, ldp, nc, w, img_h, img_w, thresh,
+                       clip);
+  else
+    hipLaunchKernelGGL(det_decode_kernel<float>, g, dim3(256), 0, s, static_cast<const float*>(pred),
+                       static_cast<const float4*>(props), static_cast<const int*>(count), static_cast<float4*>(boxes),
+                       static_cast<float*>(scores), static_cast<long*>(labels), B, R, ldp, nc, w, img_h, img_w, thresh,
+                       clip);
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
 }
 

@@ -140,6 +140,7 @@ def test_nms_multiwave_scan_matches_reference(N, thr, max_out, dense):
         ref = nms_reference(boxes[b, :n], torch.arange(n, 0, -1).float(), thr)[:max_out]
         assert int(cnt[b]) == len(ref)
         assert keep[b, :cnt[b]].long().tolist() == ref.tolist()
+        assert (keep[b, cnt[b]:] == -1).all()  # padded by the scan itself (no fill launch)
 
 
 @pytest.mark.parametrize("aligned", [False, True])
@@ -312,11 +313,13 @@ def test_gather_keep_matches_reference():
     bx, sc, lb = torch.rand(B, N, 4), torch.rand(B, N), torch.randint(1, 4, (B, N))
     keep = torch.randint(0, N, (B, K), dtype=torch.int32)
     keep[:, 60:] = -1
-    got = gather_keep(keep.to(DEV), bx.to(DEV), sc.to(DEV), lb.to(DEV))
-    ref = gather_keep(keep, bx, sc, lb)
+    got = gather_keep(keep.to(DEV), bx.to(DEV), sc.to(DEV), lb.to(DEV), rois=True)
+    ref = gather_keep(keep, bx, sc, lb, rois=True)
     for g, r in zip(got, ref):
         assert torch.equal(g.cpu(), r)
     assert (got[0][:, 60:] == 0).all()
+    # the RoIAlign rows: (image, box) per kept row, from the same launch
+    assert got[3].shape == (B * K, 5) and torch.equal(got[3][:, 0].cpu(), torch.arange(B).repeat_interleave(K).float())
 
 
 @pytest.mark.parametrize("B,N", [(32, 4300), (2, 8192), (3, 1), (4, 3000)])
