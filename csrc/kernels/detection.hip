@@ -293,6 +293,84 @@ __device__ __forceinline__ uint32_t bf16_order_key(uint16_t v) {
   return (v & 0x8000u) ? (~static_cast<uint32_t>(v) & 0xffffu) : (static_cast<uint32_t>(v) | 0x8000u);
 }
 
+// Wave-aggregated LDS histogram update: the lanes of a wave that hold the same bin add their count with ONE atomic
+// (a loop over the distinct bins present, usually 2-5 for the RPN logits' high bytes) instead of 64 atomics that
+// serialize on the same bank. Called from wave-uniform control flow.
+__device__ __forceinline__ void wave_hist_add(int* hist, int bin, bool valid) {
+  const int lane = threadIdx.x & 63;
+  unsigned long long active = __ballot(valid);
+  while (active) {
+    const int leader = __ffsll(static_cast<long long>(active)) - 1;
+    const int lb = __shfl(bin, leader, 64);
+    const unsigned long long same = __ballot(valid && bin == lb);
+    if (lane == leader) atomicAdd(&hist[lb], static_cast<int>(__popcll(same)));
+    active &= ~same;
+    valid = valid && bin != lb;
+  }
+}
+
+// The radix-select bin step, in parallel: the bin d holding the k-th largest key (counting down from 255; keys above
+// it: cum0 + the bins above d) is the one whose exclusive suffix sum is < k and inclusive one >= k (bin 0 when fewer
+// than k keys). Threads 0..255 (4 waves): wave-level inclusive scan + the waves' totals. Was one thread walking up to
+// 256 bins with an LDS round trip each: ~11 us per pass, the fixed cost that made a 300-key level take 26 us.
+__device__ __forceinline__ void topk_select_bin(const int* hist, int k, int cum0, int* sel_bin, int* sel_cum,
+                                                int* wsum) {
+  const int t = threadIdx.x;
+  const int lane = t & 63, w = t >> 6;
+  int h = 0, v = 0;
+  if (t < 256) {
+    h = hist[255 - t];  // t-th bin from the top
+    v = h;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int y = __shfl_up(v, off, 64);
+      if (lane >= off) v += y;
+    }
+    if (lane == 63) wsum[w] = v;
+  }
+  __syncthreads();
+  if (t < 256) {
+    int base = cum0;
+    for (int q = 0; q < w; ++q) base += wsum[q];
+    const int incl = base + v, above = incl - h, d = 255 - t;
+    if (above < k && (incl >= k || d == 0)) {
+      *sel_bin = d;
+      *sel_cum = above;
+    }
+  }
+  __syncthreads();
+}
+
+// Exclusive scans of two per-thread counts over the 1024 threads: wave shuffles, then the 16 wave totals.
+__device__ __forceinline__ void topk_scan2(int a, int c, int& ea, int& ec, int* wa, int* wc) {
+  const int t = threadIdx.x;
+  const int lane = t & 63, w = t >> 6;
+  int va = a, vc = c;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int ya = __shfl_up(va, off, 64), yc = __shfl_up(vc, off, 64);
+    if (lane >= off) {
+      va += ya;
+      vc += yc;
+    }
+  }
+  if (lane == 63) {
+    wa[w] = va;
+    wc[w] = vc;
+  }
+  __syncthreads();
+  int ba = 0, bc = 0;
+  for (int q = 0; q < w; ++q) {
+    ba += wa[q];
+    bc += wc[q];
+  }
+  ea = ba + va - a;
+  ec = bc + vc - c;
+}
+
+constexpr int TOPK_UNROLL = 8;       // keys a thread has in flight per histogram step
+constexpr int TOPK_MASK_WORDS = 4;   // pass 3 keeps a chunk's > / == flags in registers for chunks <= 128 keys
+
 __global__ __launch_bounds__(TOPK_THREADS) void rpn_topk_kernel(const uint16_t* __restrict__ head, int HW, int ldh,
                                                                 int A, int k, long* __restrict__ idx) {
   const int b = blockIdx.x;
@@ -301,86 +379,136 @@ __global__ __launch_bounds__(TOPK_THREADS) void rpn_topk_kernel(const uint16_t* 
   const uint16_t* const hb = head + static_cast<long>(b) * HW * ldh;
   __shared__ int hist[256];
   __shared__ int sel[3];  // high byte of the k-th key, its low byte, keys above it
-  __shared__ int sg[TOPK_THREADS], se[TOPK_THREADS];
+  __shared__ int wa[TOPK_THREADS / 64], wc[TOPK_THREADS / 64];
   auto key_at = [&](int e) __attribute__((always_inline)) {
     const int pos = e / A;
     return bf16_order_key(hb[static_cast<long>(pos) * ldh + (e - pos * A)]);
   };
-  // pass 1: histogram of the high byte
-  if (t < 256) hist[t] = 0;
-  __syncthreads();
-  {
-    int cur = -1, cnt = 0;
-    for (int e = t; e < n; e += TOPK_THREADS) {
-      const int bin = static_cast<int>(key_at(e) >> 8);
-      if (bin != cur) {
-        if (cnt) atomicAdd(&hist[cur], cnt);
-        cur = bin;
-        cnt = 0;
+  // passes 1 / 2: the histogram of the high byte, then of the low byte among keys with the selected high byte. Every
+  // thread keeps TOPK_UNROLL keys in flight (the loop is latency-bound: one workgroup per image), and the updates
+  // are wave-aggregated (the logits crowd into a few bins)
+  // a pixel's A <= 4 logits as one 8-byte load (the head rows are 8-byte aligned: ldh % 4 == 0) instead of A loads
+  const bool vec = A <= 4 && (ldh & 3) == 0 && (reinterpret_cast<uintptr_t>(head) & 7) == 0;
+  auto pix4 = [&](int pos) __attribute__((always_inline)) {
+    return *reinterpret_cast<const uint2*>(hb + static_cast<long>(pos) * ldh);
+  };
+  auto lane16 = [](const uint2& v, int a) __attribute__((always_inline)) {
+    const uint32_t w = a < 2 ? v.x : v.y;
+    return static_cast<uint16_t>((a & 1) ? (w >> 16) : (w & 0xffffu));
+  };
+  auto histogram = [&](int pass, uint32_t hi) __attribute__((always_inline)) {
+    if (t < 256) hist[t] = 0;
+    __syncthreads();
+    if (vec) {
+      for (int p0 = 0; p0 < HW; p0 += TOPK_THREADS * TOPK_UNROLL) {
+        uint2 pv[TOPK_UNROLL];
+#pragma unroll
+        for (int u = 0; u < TOPK_UNROLL; ++u) {
+          const int pos = p0 + u * TOPK_THREADS + t;
+          pv[u] = pos < HW ? pix4(pos) : make_uint2(0u, 0u);
+        }
+#pragma unroll
+        for (int u = 0; u < TOPK_UNROLL; ++u) {
+          const bool inp = p0 + u * TOPK_THREADS + t < HW;
+          for (int a = 0; a < A; ++a) {  // (A is workgroup-uniform: the wave-aggregated update stays uniform)
+            const uint32_t kk = bf16_order_key(lane16(pv[u], a));
+            if (pass == 0) {
+              wave_hist_add(hist, static_cast<int>(kk >> 8), inp);
+            } else if (inp && (kk >> 8) == hi) {
+              atomicAdd(&hist[kk & 255u], 1);
+            }
+          }
+        }
       }
-      ++cnt;
+      __syncthreads();
+      return;
     }
-    if (cnt) atomicAdd(&hist[cur], cnt);
-  }
-  __syncthreads();
-  if (t == 0) {
-    int cum = 0, d = 255;
-    for (; d > 0 && cum + hist[d] < k; --d) cum += hist[d];
-    sel[0] = d;
-    sel[2] = cum;
-  }
-  __syncthreads();
+    for (int e0 = 0; e0 < n; e0 += TOPK_THREADS * TOPK_UNROLL) {
+      uint32_t kk[TOPK_UNROLL];
+#pragma unroll
+      for (int u = 0; u < TOPK_UNROLL; ++u) {
+        const int e = e0 + u * TOPK_THREADS + t;
+        kk[u] = e < n ? key_at(e) : 0xffffffffu;
+      }
+#pragma unroll
+      for (int u = 0; u < TOPK_UNROLL; ++u) {
+        if (pass == 0) {  // high bytes: a few hot bins, one atomic per distinct bin per wave
+          wave_hist_add(hist, static_cast<int>(kk[u] >> 8), kk[u] != 0xffffffffu);
+        } else if (kk[u] != 0xffffffffu && (kk[u] >> 8) == hi) {  // low bytes of one high bin: spread, few keys
+          atomicAdd(&hist[kk[u] & 255u], 1);
+        }
+      }
+    }
+    __syncthreads();
+  };
+  histogram(0, 0u);
+  topk_select_bin(hist, k, 0, &sel[0], &sel[2], wa);
   const uint32_t hi = static_cast<uint32_t>(sel[0]);
-  // pass 2: histogram of the low byte among the keys with that high byte
-  if (t < 256) hist[t] = 0;
-  __syncthreads();
-  {
-    int cur = -1, cnt = 0;
-    for (int e = t; e < n; e += TOPK_THREADS) {
-      const uint32_t kk = key_at(e);
-      if ((kk >> 8) != hi) continue;
-      const int bin = static_cast<int>(kk & 255u);
-      if (bin != cur) {
-        if (cnt) atomicAdd(&hist[cur], cnt);
-        cur = bin;
-        cnt = 0;
-      }
-      ++cnt;
-    }
-    if (cnt) atomicAdd(&hist[cur], cnt);
-  }
-  __syncthreads();
-  if (t == 0) {
-    int cum = sel[2], d = 255;
-    for (; d > 0 && cum + hist[d] < k; --d) cum += hist[d];
-    sel[1] = d;
-    sel[2] = cum;
-  }
-  __syncthreads();
+  const int cum_hi = sel[2];
+  histogram(1, hi);
+  topk_select_bin(hist, k, cum_hi, &sel[1], &sel[2], wa);
   const uint32_t T = (hi << 8) | static_cast<uint32_t>(sel[1]);
   const int gt = sel[2], need = k - gt;  // keys above T; ties of T to take
   // pass 3: thread t owns the contiguous index range [e0, e1) (index order across threads), per-thread counts,
-  // exclusive scans, then the writes
+  // exclusive scans, then the writes; the counting loop remembers each key's > / == flags in registers so the write
+  // loop does not read the keys again (chunks of <= 32 * TOPK_MASK_WORDS keys; longer ones re-read)
   const int chunk = (n + TOPK_THREADS - 1) / TOPK_THREADS;
   const int e0 = min(n, t * chunk), e1 = min(n, e0 + chunk);
+  const bool masked = chunk <= 32 * TOPK_MASK_WORDS;
+  uint32_t mg[TOPK_MASK_WORDS] = {0u, 0u, 0u, 0u}, me[TOPK_MASK_WORDS] = {0u, 0u, 0u, 0u};
   int cg = 0, ce = 0;
-  for (int e = e0; e < e1; ++e) {
-    const uint32_t kk = key_at(e);
-    cg += kk > T;
-    ce += kk == T;
+  int cur_pos = -1;
+  uint2 cur_v = make_uint2(0u, 0u);
+  auto key_seq = [&](int e) __attribute__((always_inline)) {  // keys in index order: one load per pixel
+    if (!vec) return key_at(e);
+    const int pos = e / A;
+    if (pos != cur_pos) {
+      cur_pos = pos;
+      cur_v = pix4(pos);
+    }
+    return bf16_order_key(lane16(cur_v, e - pos * A));
+  };
+  for (int e = e0; e < e1; e += TOPK_UNROLL) {
+    uint32_t kk[TOPK_UNROLL];
+#pragma unroll
+    for (int u = 0; u < TOPK_UNROLL; ++u) kk[u] = e + u < e1 ? key_seq(e + u) : 0u;
+#pragma unroll
+    for (int u = 0; u < TOPK_UNROLL; ++u) {
+      if (e + u >= e1) break;
+      const bool g = kk[u] > T, q = kk[u] == T;
+      cg += g;
+      ce += q;
+      const int j = e + u - e0;
+      if (masked) {
+#pragma unroll
+        for (int w = 0; w < TOPK_MASK_WORDS; ++w)  // (register-select: no runtime-indexed array)
+          if ((j >> 5) == w) {
+            mg[w] |= static_cast<uint32_t>(g) << (j & 31);
+            me[w] |= static_cast<uint32_t>(q) << (j & 31);
+          }
+      }
+    }
   }
-  sg[t] = cg;
-  se[t] = ce;
-  __syncthreads();
-  for (int off = 1; off < TOPK_THREADS; off <<= 1) {
-    const int a = t >= off ? sg[t - off] : 0, c = t >= off ? se[t - off] : 0;
-    __syncthreads();
-    sg[t] += a;
-    se[t] += c;
-    __syncthreads();
-  }
-  int og = sg[t] - cg, oe = se[t] - ce;
+  int og, oe;
+  topk_scan2(cg, ce, og, oe, wa, wc);
   long* const out = idx + static_cast<long>(b) * k;
+  if (masked) {
+#pragma unroll
+    for (int w = 0; w < TOPK_MASK_WORDS; ++w) {
+      uint32_t m = mg[w] | me[w];
+      while (m) {
+        const int bit = __builtin_ctz(m);
+        m &= m - 1;
+        const int e = e0 + 32 * w + bit;
+        if ((mg[w] >> bit) & 1u) {
+          out[og++] = e;
+        } else if (oe < need) {
+          out[gt + oe++] = e;
+        }
+      }
+    }
+    return;
+  }
   for (int e = e0; e < e1; ++e) {
     const uint32_t kk = key_at(e);
     if (kk > T) {
