@@ -121,16 +121,26 @@ __global__ __launch_bounds__(64) void nms_reduce_kernel(const unsigned long long
 // is serial in the 64-box blocks; what the one-wave form spends most of its time on is the memory latency of OR-ing
 // each block's kept rows into the bitmap (one round trip per 8 kept boxes) and of the next block's diagonal words,
 // both on the critical path. Here:
-//  * wave 0 resolves the blocks' diagonals; it prefetches block wb+1's diagonal word AND the word after it (column
-//    wb+2) one block ahead, so the contribution of a block's kept boxes to the NEXT block's diagonal is an OR over
-//    lanes of registers already loaded (no load on the critical path);
-//  * waves 1..N-1 OR the kept rows' remaining words (> wb+1) into their partial bitmaps; their loads are issued
-//    after a block is resolved and consumed one block later (a whole block period to land);
+//  * wave 0 resolves the blocks' diagonals; it prefetches each block's diagonal word AND the two words after it, two
+//    blocks ahead, so the contribution of a block's kept boxes to the next two blocks' diagonals is an OR over lanes
+//    of registers already loaded (no load on the critical path);
+//  * waves 1..N-1 OR the kept rows' remaining words (> wb+2) into their partial bitmaps; their loads are issued
+//    after a block is resolved and consumed two blocks later (with one block to land, the block period stretched
+//    to the load latency: ~2.9 us per 64-box block);
 //  * per block, two workgroup barriers: the row waves publish their partial word of the block, wave 0 publishes the
 //    block's kept bits.
 // Same greedy result as nms_reduce_kernel (same kept set, same order).
 constexpr int NMS_MW_WAVES = 9;
 constexpr int NMS_MW_ROWS = (64 + NMS_MW_WAVES - 2) / (NMS_MW_WAVES - 1);  // kept rows per row wave per block
+static_assert(NMS_MW_ROWS * (NMS_MW_WAVES - 1) == 64, "row waves split a block's 64 bit positions evenly");
+
+// a wave-uniform value read from LDS lands in VGPRs; moving it to SGPRs keeps the scalar loops scalar (a ctz of a
+// VGPR value gives a VGPR lane index, and v_readlane with a VGPR index becomes a waterfall loop)
+__device__ __forceinline__ unsigned long long uniform_u64(unsigned long long v) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v));
+  const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v >> 32));
+  return (static_cast<unsigned long long>(hi) << 32) | lo;
+}
 
 __device__ __forceinline__ unsigned long long wave_or_u64(unsigned long long v) {
   uint32_t lo = static_cast<uint32_t>(v), hi = static_cast<uint32_t>(v >> 32);
@@ -157,90 +167,113 @@ __global__ __launch_bounds__(64 * NMS_MW_WAVES) void nms_reduce_mw_kernel(const 
   const int nblk = (n + 63) / 64;
   if (wave == 0) {
     int kept = 0;
-    unsigned long long carry = 0;  // kept boxes of the previous block, at this block's diagonal word
-    auto diag_words = [&](int wb, unsigned long long& d, unsigned long long& nx) __attribute__((always_inline)) {
-      const int i_l = 64 * wb + lane;
-      d = (wb < nblk && i_l < n) ? mb[static_cast<long>(i_l) * W + wb] : 0ull;
-      nx = (wb < nblk && i_l < n && wb + 1 < W) ? mb[static_cast<long>(i_l) * W + wb + 1] : 0ull;
+    // words of block k's rows: the diagonal (col k) and the next two (cols k+1, k+2); prefetched two blocks ahead
+    struct Diag {
+      unsigned long long d, n1, n2;
     };
-    unsigned long long mine, nextc;
-    diag_words(0, mine, nextc);
-    for (int wb = 0; wb < nblk; ++wb) {
-      unsigned long long mine_n, nextc_n;
-      diag_words(wb + 1, mine_n, nextc_n);  // prefetch: consumed one block later
+    auto diag_words = [&](int wb) __attribute__((always_inline)) {
+      const int i_l = 64 * wb + lane;
+      const bool in = wb < nblk && i_l < n;
+      const long row = static_cast<long>(i_l) * W;
+      Diag g;
+      g.d = in ? mb[row + wb] : 0ull;
+      g.n1 = in && wb + 1 < W ? mb[row + wb + 1] : 0ull;
+      g.n2 = in && wb + 2 < W ? mb[row + wb + 2] : 0ull;
+      return g;
+    };
+    // three register sets used round robin with STATIC roles (the loop body is unrolled by 3): rotating them with
+    // copies made the compiler wait for every outstanding load (vmcnt(0)) at the first use, i.e. for the prefetch
+    // issued two blocks ahead
+    Diag dA = diag_words(0), dB = diag_words(1), dC;
+    // kept boxes' contributions to a later block's diagonal word that the row waves have not OR-ed yet:
+    // c1 = block wb-1 at word wb, c2a = block wb-2 at word wb, c2b = block wb-1 at word wb+1
+    unsigned long long c1 = 0, c2a = 0, c2b = 0;
+    // one block: prefetch block wb+2 into `into`, resolve block wb from `cur`; false when the scan is over
+    auto step = [&](int wb, const Diag& cur, Diag& into) __attribute__((always_inline)) {
+      into = diag_words(wb + 2);  // consumed two blocks later
       if (lane == 0) s_part[0] = 0ull;
-      __syncthreads();  // B1: the row waves' partial words of block wb are published
-      unsigned long long remw = carry;
+      __syncthreads();  // B1: the row waves' partial words of block wb are published (blocks <= wb-3)
+      unsigned long long remw = c1 | c2a;
 #pragma unroll
       for (int w = 1; w < NMS_MW_WAVES; ++w) remw |= s_part[w];
+      remw = uniform_u64(remw);
       const int inblk = min(64, n - 64 * wb);
       unsigned long long alive = ~remw & (inblk == 64 ? ~0ull : ((1ull << inblk) - 1));
-      unsigned long long keepbits = 0;
+      unsigned long long keepbits = 0, k1 = 0, k2 = 0;
       int kb = 0;
       while (alive && kept + kb < max_out) {
         const int i = __builtin_ctzll(alive);
         keepbits |= 1ull << i;
         ++kb;
         alive &= ~(1ull << i);
-        alive &= ~readlane_u64(mine, i);
+        alive &= ~readlane_u64(cur.d, i);
+        // the kept box's words of the next two blocks, read in the same scalar loop (a 64-lane OR reduction by
+        // shuffles cost ~12 dependent LDS round trips per word)
+        k1 |= readlane_u64(cur.n1, i);
+        k2 |= readlane_u64(cur.n2, i);
       }
       if ((keepbits >> lane) & 1ull)
         keep[static_cast<long>(b) * max_out + kept + __builtin_popcountll(keepbits & ((1ull << lane) - 1))] =
             64 * wb + lane;
       kept += kb;
-      carry = wave_or_u64(((keepbits >> lane) & 1ull) ? nextc : 0ull);
+      c1 = k1;   // block wb at word wb+1
+      c2a = c2b; // block wb-1 at word wb+1
+      c2b = k2;  // block wb at word wb+2
       if (lane == 0) {
         s_keep = keepbits;
         s_kept = kept;
       }
       __syncthreads();  // B2: block wb resolved
-      mine = mine_n;
-      nextc = nextc_n;
-      if (kept >= max_out) break;
+      return wb + 1 < nblk && kept < max_out;
+    };
+    for (int wb = 0; wb < nblk; wb += 3) {
+      if (!step(wb, dA, dC)) break;
+      if (!step(wb + 1, dB, dA)) break;
+      if (!step(wb + 2, dC, dB)) break;
     }
     if (lane == 0) count[b] = min(kept, max_out);
     // the rows past the count are padding (-1): the caller needs no fill launch
     for (int i = min(kept, max_out) + lane; i < max_out; i += 64) keep[static_cast<long>(b) * max_out + i] = -1;
     return;
   }
-  // row waves: partial bitmap words lane and lane + 64
+  // row waves: partial bitmap words lane and lane + 64. A block's kept rows are loaded after its B2 and OR-ed two
+  // blocks later (pA), so two block periods hide the load latency; words wb+1 and wb+2 come from wave 0's carries
   unsigned long long rem0 = 0, rem1 = 0;
-  unsigned long long p0[NMS_MW_ROWS], p1[NMS_MW_ROWS];  // the previous block's loaded rows, OR-ed one block later
+  // two row buffers with static roles (the loop body is unrolled by 2; see wave 0's note on register rotation):
+  // at block wb the buffer of parity wb holds block wb-2's rows, is OR-ed, then refilled with block wb's rows
+  unsigned long long pa0[NMS_MW_ROWS], pa1[NMS_MW_ROWS], pb0[NMS_MW_ROWS], pb1[NMS_MW_ROWS];
 #pragma unroll
-  for (int u = 0; u < NMS_MW_ROWS; ++u) p0[u] = p1[u] = 0ull;
+  for (int u = 0; u < NMS_MW_ROWS; ++u) pa0[u] = pa1[u] = pb0[u] = pb1[u] = 0ull;
   const int w0 = lane, w1 = lane + 64;
-  for (int wb = 0; wb < nblk; ++wb) {
-    if (lane == (wb & 63)) s_part[wave] = wb < 64 ? rem0 : rem1;  // blocks <= wb-2 (wb-1 is wave 0's carry)
+  auto rstep = [&](int wb, unsigned long long (&q0)[NMS_MW_ROWS], unsigned long long (&q1)[NMS_MW_ROWS])
+      __attribute__((always_inline)) {
+    if (lane == (wb & 63)) s_part[wave] = wb < 64 ? rem0 : rem1;  // blocks <= wb-3
     __syncthreads();  // B1
     __syncthreads();  // B2
-    // block wb-1's rows (loads issued after the previous B2): OR-ed only now, so their latency overlaps this
-    // block's diagonal instead of delaying B1
 #pragma unroll
-    for (int u = 0; u < NMS_MW_ROWS; ++u) {
-      rem0 |= p0[u];
-      rem1 |= p1[u];
+    for (int u = 0; u < NMS_MW_ROWS; ++u) {  // block wb-2's rows
+      rem0 |= q0[u];
+      rem1 |= q1[u];
     }
-    unsigned long long kbits = s_keep;
-    const int kept = s_kept;
-    // this wave's share of the block's kept rows: the k-th kept box (bit order) goes to wave 1 + k % (waves - 1)
-    int k = 0;
-    const bool ok0 = w0 > wb + 1 && w0 < W, ok1 = w1 > wb + 1 && w1 < W;
-    int u = 0;
+    unsigned long long kbits = uniform_u64(s_keep);
+    const int kept = __builtin_amdgcn_readfirstlane(s_kept);
+    // this wave's share of the block's kept rows: the kept boxes at bit positions [8 (wave-1), 8 wave)
+    const bool ok0 = w0 > wb + 2 && w0 < W, ok1 = w1 > wb + 2 && w1 < W;
+    const int base_bit = NMS_MW_ROWS * (wave - 1);
     long rows[NMS_MW_ROWS];
 #pragma unroll
-    for (int q = 0; q < NMS_MW_ROWS; ++q) rows[q] = -1;
-    while (kbits && u < NMS_MW_ROWS) {
-      const int i = __builtin_ctzll(kbits);
-      kbits &= kbits - 1;
-      if (k % (NMS_MW_WAVES - 1) == wave - 1) rows[u++] = static_cast<long>(64 * wb + i) * W;
-      ++k;
-    }
+    for (int q = 0; q < NMS_MW_ROWS; ++q)  // (static indices: a compacted runtime-indexed array went to scratch)
+      rows[q] = ((kbits >> (base_bit + q)) & 1ull) ? static_cast<long>(64 * wb + base_bit + q) * W : -1;
 #pragma unroll
     for (int q = 0; q < NMS_MW_ROWS; ++q) {
-      p0[q] = rows[q] >= 0 && ok0 ? mb[rows[q] + w0] : 0ull;
-      p1[q] = rows[q] >= 0 && ok1 ? mb[rows[q] + w1] : 0ull;
+      q0[q] = rows[q] >= 0 && ok0 ? mb[rows[q] + w0] : 0ull;
+      q1[q] = rows[q] >= 0 && ok1 ? mb[rows[q] + w1] : 0ull;
     }
-    if (kept >= max_out) break;
+    return wb + 1 < nblk && kept < max_out;
+  };
+  for (int wb = 0; wb < nblk; wb += 2) {
+    if (!rstep(wb, pa0, pa1)) break;
+    if (!rstep(wb + 1, pb0, pb1)) break;
   }
 }
 
