@@ -471,6 +471,17 @@ class Gateway:
             except ValueError:
                 pass
 
+    def add_public_socket(self, sock) -> bool:
+        """Start serving one more listening socket (HTTPS when the gateway has a certificate) while ``run`` is
+        running: the public port taken back from native front-ends that all exited (``serve.py``)."""
+        serving = getattr(self, "_serving", None)
+        if serving is None:
+            return False
+        loop, runner, ssl_context = serving
+        fut = asyncio.run_coroutine_threadsafe(web.SockSite(runner, sock, ssl_context=ssl_context).start(), loop)
+        fut.result(10)
+        return True
+
     def run(self, host: str = "127.0.0.1", port: int = 8080, socks=None, ssl_context=None,
             internal_only: bool = False) -> None:
         """Serve on (host, port), or on the given listening sockets (public SO_REUSEPORT socket shared with
@@ -486,6 +497,7 @@ class Gateway:
             # (e.g. the front-ends' proxy sessions) for aiohttp's default 60 s
             runner = web.AppRunner(self.app, handle_signals=False, access_log=None, shutdown_timeout=2.0)
             await runner.setup()
+            self._serving = (asyncio.get_running_loop(), runner, ssl_context)  # (add_public_socket)
             if socks:
                 sites = [web.SockSite(runner, sk, ssl_context=ssl_context if i == 0 and not internal_only else None)
                          for i, sk in enumerate(socks)]

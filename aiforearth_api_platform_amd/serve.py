@@ -18,6 +18,8 @@ import importlib
 import logging
 import os
 import sys
+import threading
+import time
 from typing import Any, Dict
 
 import torch
@@ -77,6 +79,25 @@ def start_frontends(cfg: Config, doc: Dict[str, Any], endpoints: Dict[str, Any],
                                       max_queue_ms=cfg.max_queue_ms)
     return spawn_frontends(frontend_count(cfg), pools, routes, cfg.host, port, f"http://127.0.0.1:{internal_port}",
                            security=security)
+
+
+def _public_port_watchdog(gw, frontends, host: str, port: int, period_s: float = 1.0) -> None:
+    """Native front-ends own the public port (``handover_public_port``). If every one of them exits while the
+    gateway is not draining, the serving process binds the port again and serves it itself (the gateway path: the
+    same routes and admission rules, without the native ingest), so the service stays reachable."""
+    while not gw.is_terminating:
+        time.sleep(period_s)
+        if gw.is_terminating or any(p.is_alive() for p in frontends):
+            continue
+        pub, internal = open_listeners(host, port, shared=True)
+        internal.close()
+        sock = pub
+        if gw.add_public_socket(sock):
+            print(f"ai4e-mi355x: every ingest front-end exited; the gateway serves {host}:{port} itself",
+                  file=sys.stderr, flush=True)
+        else:
+            sock.close()
+        return
 
 
 def _request_decoder(e: Dict[str, Any]):
@@ -212,6 +233,8 @@ def main(argv=None) -> int:
 
     n_socks = len(socks)
     socks = handover_public_port(socks, frontends)
+    if len(socks) < n_socks:  # the front-ends own the public port: take it back if every one of them exits
+        threading.Thread(target=_public_port_watchdog, args=(gw, frontends, cfg.host, cfg.port), daemon=True).start()
     # SIGTERM drain: the front-ends stop first (their own graceful shutdown), so no new tasks arrive meanwhile
     gw.on_drain.append(lambda: [p.terminate() for p in frontends])
     print(f"ai4e-mi355x gateway on {'https' if cfg.tls_cert else 'http'}://{cfg.host}:{cfg.port} endpoints={list(endpoints)} "

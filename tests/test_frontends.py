@@ -77,6 +77,57 @@ def test_frontend_processes_end_to_end(impl):
             proc.kill()
 
 
+def test_public_port_taken_back_when_frontends_exit():
+    """Native front-ends own the public port; when every one of them exits (killed here) the serving process binds
+    the port again and answers itself within a few seconds (serve.py _public_port_watchdog)."""
+    import re
+    import signal
+
+    port = _port()
+    env = dict(os.environ, PYTHONPATH=ROOT, AI4E_FRONTEND_PROCESSES="1", AI4E_FRONTEND_IMPL="native")
+    proc = subprocess.Popen([sys.executable, "-m", "aiforearth_api_platform_amd.serve", "--config",
+                             os.path.join(ROOT, "examples", "platform_cpu.yaml"), "--port", str(port)],
+                            cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+    base = f"http://127.0.0.1:{port}"
+    s = requests.Session()
+    s.trust_env = False
+    try:
+        for _ in range(600):
+            try:
+                if s.get(base + "/", timeout=1).status_code == 200:
+                    break
+            except requests.ConnectionError:
+                time.sleep(0.1)
+        else:
+            raise AssertionError("server did not come up")
+        out = _drain(proc)
+        m = re.search(r"ai4e_ingestd pid (\d+)", out)
+        assert m, out[-2000:]
+        r = s.get(base + "/", headers={"Connection": "close"})
+        assert r.headers.get("Server", "").startswith("ai4e-ingestd")
+        os.kill(int(m.group(1)), signal.SIGKILL)
+        ok = False
+        for _ in range(100):
+            time.sleep(0.1)
+            try:
+                r = s.get(base + "/", timeout=1, headers={"Connection": "close"})
+                ok = r.status_code == 200 and not r.headers.get("Server", "").startswith("ai4e-ingestd")
+                if ok:
+                    break
+            except requests.ConnectionError:
+                pass
+        assert ok, "the serving process did not take the public port back"
+        img = np.zeros((4, 4, 3), np.uint8)
+        r = s.post(base + "/v1/tiny/async", data=img.tobytes(), headers={"Content-Type": "application/octet-stream"})
+        assert r.status_code == 200 and r.json()["BackendStatus"] == "created"
+    finally:
+        proc.terminate()
+        try:
+            proc.wait(20)
+        except subprocess.TimeoutExpired:
+            proc.kill()
+
+
 @pytest.mark.parametrize("nfe", [2, 0])
 def test_native_frontend_admission_parity(tmp_path, nfe):
     """Subscription keys (global + per route), content type, length and payload-size errors through native
