@@ -599,6 +599,26 @@ __global__ __launch_bounds__(ROWSORT_THREADS) void row_sort_desc_kernel(const fl
 // FPN level) or, with grp null, from the index: group = index % grp_mod + 1 (the detections' class label, as laid out
 // by det_decode_kernel). Replaces argsort (a library radix sort over 4 K+ keys, not graph-safe) + four gathers + a
 // sum-reduction + the offset arithmetic: ~10 library launches per NMS stage.
+// Register-resident bitonic network: thread t holds keys t * KPT .. t * KPT + KPT - 1 in registers. Steps with
+// partner distance j < KPT are compare-exchanges inside a thread, KPT <= j < 64 KPT cross lanes of one wave by
+// shuffles (no barrier), and only j >= 64 KPT (the last log2(total / 64 KPT) steps of each merge: 10 of the 91 steps
+// at 8192 keys) go through LDS with barriers. The LDS steps use a transposed layout (key (t, r) at r * 1024 + t) so a
+// wave's reads are consecutive. Same network, same comparisons: the same order as the all-LDS form.
+template <int KPT, int J>
+__device__ __forceinline__ void bitonic_regs(unsigned long long (&v)[KPT], int base, int k) {
+#pragma unroll
+  for (int r = 0; r < KPT; ++r) {
+    if ((r & J) == 0) {
+      const bool desc = ((base + r) & k) == 0;
+      const unsigned long long a = v[r], c = v[r + J];
+      const unsigned long long hi = a > c ? a : c, lo = a > c ? c : a;
+      v[r] = desc ? hi : lo;
+      v[r + J] = desc ? lo : hi;
+    }
+  }
+}
+
+template <int KPT>
 __global__ __launch_bounds__(ROWSORT_THREADS) void sort_select_kernel(
     const float* __restrict__ scores, const float4* __restrict__ boxes, const float* __restrict__ grp, int grp_mod,
     float scale, int N, int P, float* __restrict__ s_out, float4* __restrict__ b_out, float4* __restrict__ boff_out,
@@ -609,39 +629,54 @@ __global__ __launch_bounds__(ROWSORT_THREADS) void sort_select_kernel(
   const long row = blockIdx.x;
   const float* const sr = scores + row * N;
   if (t == 0) nvalid = 0;
-  for (int i = t; i < P; i += ROWSORT_THREADS)
-    key[i] = i < N ? (static_cast<unsigned long long>(f32_order_key(sr[i])) << 32) | (0xffffffffu - static_cast<uint32_t>(i))
-                   : 0ull;
-  __syncthreads();
-  // bitonic network over pairs: pair p = (i, i | j) with i = p with a zero bit inserted at log2(j), so every lane
-  // has a compare-exchange in every step (the per-element form left half the lanes idle), and a lane's <= 4 pairs
-  // are all loaded before the first compare (one LDS latency per step instead of one per pair)
-  constexpr int PAIRS = ROWSORT_MAX / 2 / ROWSORT_THREADS;
-  const int half = P >> 1;
-  for (int k = 2; k <= P; k <<= 1) {
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      unsigned long long a[PAIRS], c[PAIRS];
-      int ii[PAIRS];
+  constexpr int total = KPT * ROWSORT_THREADS;  // >= P (padding keys 0 sort last)
+  const int base = t * KPT;
+  unsigned long long v[KPT];
 #pragma unroll
-      for (int u = 0; u < PAIRS; ++u) {
-        const int p = t + u * ROWSORT_THREADS;
-        ii[u] = ((p & ~(j - 1)) << 1) | (p & (j - 1));
-        if (p < half) {
-          a[u] = key[ii[u]];
-          c[u] = key[ii[u] | j];
+  for (int r = 0; r < KPT; ++r) {
+    const int i = base + r;
+    v[r] = i < N ? (static_cast<unsigned long long>(f32_order_key(sr[i])) << 32) | (0xffffffffu - static_cast<uint32_t>(i))
+                 : 0ull;
+  }
+  (void)P;
+  for (int k = 2; k <= total; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      if (j < KPT) {
+        if constexpr (KPT > 4) { if (j == 4) bitonic_regs<KPT, 4>(v, base, k); }
+        if constexpr (KPT > 2) { if (j == 2) bitonic_regs<KPT, 2>(v, base, k); }
+        if constexpr (KPT > 1) { if (j == 1) bitonic_regs<KPT, 1>(v, base, k); }
+        continue;
+      }
+      const int m = j / KPT;  // partner thread t ^ m, same register r
+      if (m < 64) {
+#pragma unroll
+        for (int r = 0; r < KPT; ++r) {
+          const unsigned long long x = v[r];
+          const uint32_t ylo = static_cast<uint32_t>(__shfl_xor(static_cast<int>(static_cast<uint32_t>(x)), m, 64));
+          const uint32_t yhi = static_cast<uint32_t>(__shfl_xor(static_cast<int>(static_cast<uint32_t>(x >> 32)), m, 64));
+          const unsigned long long y = (static_cast<unsigned long long>(yhi) << 32) | ylo;
+          const int i = base + r;
+          const bool keep_hi = ((i & j) == 0) == ((i & k) == 0);
+          v[r] = keep_hi ? (x > y ? x : y) : (x > y ? y : x);
         }
+        continue;
       }
 #pragma unroll
-      for (int u = 0; u < PAIRS; ++u) {
-        const int p = t + u * ROWSORT_THREADS;
-        if (p < half && (((ii[u] & k) == 0) ? (a[u] < c[u]) : (a[u] > c[u]))) {
-          key[ii[u]] = c[u];
-          key[ii[u] | j] = a[u];
-        }
+      for (int r = 0; r < KPT; ++r) key[r * ROWSORT_THREADS + t] = v[r];
+      __syncthreads();
+#pragma unroll
+      for (int r = 0; r < KPT; ++r) {
+        const unsigned long long x = v[r], y = key[r * ROWSORT_THREADS + (t ^ m)];
+        const int i = base + r;
+        const bool keep_hi = ((i & j) == 0) == ((i & k) == 0);
+        v[r] = keep_hi ? (x > y ? x : y) : (x > y ? y : x);
       }
       __syncthreads();
     }
   }
+#pragma unroll
+  for (int r = 0; r < KPT; ++r) key[base + r] = v[r];  // natural order for the gathers below
+  __syncthreads();
   int mine = 0;
   for (int i = t; i < N; i += ROWSORT_THREADS) {
     const int src = static_cast<int>(0xffffffffu - static_cast<uint32_t>(key[i]));
@@ -1081,10 +1116,21 @@ AI4E_API int ai4e_sort_select(const void* scores, const void* boxes, const void*
     return AI4E_EINVAL;
   int P = 1;
   while (P < N) P <<= 1;
-  hipLaunchKernelGGL(sort_select_kernel, dim3(B), dim3(ROWSORT_THREADS), 0, s, static_cast<const float*>(scores),
-                     static_cast<const float4*>(boxes), static_cast<const float*>(grp), grp_mod, scale, N, P,
-                     static_cast<float*>(s_out), static_cast<float4*>(b_out), static_cast<float4*>(boff_out),
-                     static_cast<float*>(g_out), static_cast<long*>(lab_out), static_cast<int*>(valid));
+#define AI4E_SORT_SELECT(KPT)                                                                                      \
+  hipLaunchKernelGGL((sort_select_kernel<KPT>), dim3(B), dim3(ROWSORT_THREADS), 0, s,                                \
+                     static_cast<const float*>(scores), static_cast<const float4*>(boxes),                           \
+                     static_cast<const float*>(grp), grp_mod, scale, N, P, static_cast<float*>(s_out),              \
+                     static_cast<float4*>(b_out), static_cast<float4*>(boff_out), static_cast<float*>(g_out),      \
+                     static_cast<long*>(lab_out), static_cast<int*>(valid))
+  if (P > 4 * ROWSORT_THREADS)
+    AI4E_SORT_SELECT(8);
+  else if (P > 2 * ROWSORT_THREADS)
+    AI4E_SORT_SELECT(4);
+  else if (P > ROWSORT_THREADS)
+    AI4E_SORT_SELECT(2);
+  else
+    AI4E_SORT_SELECT(1);
+#undef AI4E_SORT_SELECT
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
 }
 
