@@ -20,7 +20,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops.conv import (PackedConv, chain_supported, conv2d_nhwc, conv_chain, fold_bn, pack_conv, pack_stem_s2d,
-                        pair_route, pair_supported, stem_pool, stem_pool_c1, stem_pool_u8)
+                        pair_route, pair_supported, stem_pool, stem_pool_c1)
 from ..ops.head import softmax_topk
 from ..ops.pool import (global_avgpool_nhwc, maxpool2d_nhwc, preprocess_s2d_u8, preprocess_u8,
                         space_to_depth_shifted)
@@ -171,16 +171,10 @@ class FusedResNet:
         elif dtype != torch.bfloat16:
             raise ValueError(f"FusedResNet dtype must be bf16 or fp16, got {dtype}")
         self.fold_down = os.environ.get("AI4E_RESNET_FOLD_DOWN", "1") not in ("0", "off", "")
-        # uint8 preprocess fused into the stem kernel (AI4E_STEM_U8=1); off by default: measured 0.1 ms slower
-        # per batch of 256 than the separate K7 preprocess + K1s (byte gathers serialize with the conv)
-        self.stem_u8 = os.environ.get("AI4E_STEM_U8", "0") not in ("0", "off", "")
         # the first bottleneck's 1x1 c1 fused into the stem kernel (computed from the pooled tile in LDS)
         self.stem_c1 = os.environ.get("AI4E_STEM_C1", "1") not in ("0", "off", "")
         # classifier FC on K1 (1x1 conv over the pooled features) by default: parity-or-better with hipBLASLt in
         # the captured forward (80.7/80.7k vs 81.3/80.9k images/s same-box A/B) and no library kernel left
-        # chained micro-batching (AI4E_RESNET_CHAIN_MB=mb:nstages): stem + the first nstages run mb images at a time
-        cmb = os.environ.get("AI4E_RESNET_CHAIN_MB", "")
-        self.chain_mb: Optional[Tuple[int, int]] = tuple(int(v) for v in cmb.split(":")) if ":" in cmb else None
         # stage entry: the downsample projection on a side stream, concurrent with the stage's first c1 (both read
         # the previous stage's output, both are latency-bound short-K GEMMs); forked and joined inside the caller's
         # stream, so a captured HIP graph holds the two as parallel branches. Opt-in (AI4E_PAR_DOWN=1): -27 us on a
@@ -252,15 +246,14 @@ class FusedResNet:
         return conv2d_nhwc(y, c3, residual=idt, relu=True, out=out)
 
     def _stages_chained(self, y: torch.Tensor, collect: bool = False, t1: Optional[torch.Tensor] = None,
-                        s0: int = 0, s1: Optional[int] = None, y_out: Optional[torch.Tensor] = None,
-                        t1_out: Optional[torch.Tensor] = None):
+                        s0: int = 0, s1: Optional[int] = None):
         """Stages ``s0 .. s1-1`` with the K1c chains: the first block's downsample runs as a K1 conv, then every
         block is ONE kernel (c2 -> c3 + residual -> the next block's c1, across stage boundaries too: the
         last block of a stage computes the next stage's first c1). Shapes K1c does not build fall back to
         separate K1 convs inside ``conv_chain``. ``collect`` returns every stage's output (FPN backbones).
         ``t1`` is stage ``s0``'s first c1 output when a previous call already computed it; with ``s1`` short
-        of the last stage the call returns ``(y, t1)`` for the next call, written into ``y_out`` / ``t1_out``
-        when given (micro-batch slices of the full-batch buffers)."""
+        of the last stage the call returns ``(y, t1)`` for the next call (``tools/chain_stamps.py`` times
+        the stages one at a time that way)."""
         s1 = len(self.stages) if s1 is None else s1
         outs = []
         for si in range(s0, s1):
@@ -287,9 +280,7 @@ class FusedResNet:
                 if (nxt is not None and i + 1 == len(blocks) and not chain_supported(c2.cout, nxt.cout)
                         and not pair_supported(c2.cout, c3.cout, nxt.cout) and self._side_ok(t1)):
                     nxt = None  # the next stage's c1 runs at its entry, beside its downsample
-                last = si + 1 == s1 and i + 1 == len(blocks)
-                idt, t1 = conv_chain(t1, c2, c3, idt, c1n=nxt, down=dn, x0=x0, out=y_out if last else None,
-                                     t1n_out=t1_out if last and nxt is not None else None)
+                idt, t1 = conv_chain(t1, c2, c3, idt, c1n=nxt, down=dn, x0=x0)
                 x0 = dn = None
             y = idt
             outs.append(y)
@@ -317,33 +308,6 @@ class FusedResNet:
         main.wait_stream(side)
         idt.record_stream(main)
         return t1, idt
-
-    def _chained_microbatched(self, x: torch.Tensor, pre, mb: int, nstages: int) -> torch.Tensor:
-        if not 0 < nstages < len(self.stages):
-            raise ValueError(f"chained micro-batching: nstages must be in 1..{len(self.stages) - 1}")
-        """Cache-resident micro-batching over the K1c chains: the stem and the first ``nstages`` stages run
-        ``mb`` images at a time (a layer1 activation of 32 images is 51 MB, so each chain's input comes
-        back from the 256 MB Infinity Cache instead of HBM), writing the stage output and the next stage's
-        first c1 straight into full-batch buffers; the later stages run on the whole batch."""
-        n = x.shape[0]
-        y_full = t1_full = None
-        for n0 in range(0, n, mb):
-            xs = x[n0:n0 + mb]
-            y = stem_pool_u8(xs, self.stem) if pre is preprocess_s2d_u8 and self.stem_u8 else self._stem(
-                pre(xs) if pre is not None else xs)
-            if y_full is None:
-                h, w = y.shape[1], y.shape[2]
-                for si in range(nstages):
-                    h, w = self.stages[si][0][1].out_hw(h, w)
-                c2, c3 = self.stages[nstages - 1][-1][1:3]
-                y_full = torch.empty(n, h, w, c3.cout, device=y.device, dtype=y.dtype)
-                nxt = self.stages[nstages][0][0]
-                if not (not chain_supported(c2.cout, nxt.cout) and chain_supported(c2.cout)):
-                    t1_full = torch.empty(n, h, w, nxt.cout, device=y.device, dtype=y.dtype)
-            m = y.shape[0]
-            self._stages_chained(y, s1=nstages, y_out=y_full[n0:n0 + m],
-                                 t1_out=None if t1_full is None else t1_full[n0:n0 + m])
-        return self._stages_chained(y_full, t1=t1_full, s0=nstages)
 
     def stage_features(self, x_s2d: torch.Tensor):
         """Space-to-depth input -> the four stage outputs (C2..C5) through K1s + the K1c chains; the
@@ -384,8 +348,6 @@ class FusedResNet:
         """
         n = x.shape[0]
         mb, nblocks = self.chunk if self.chunk else (n, 0)
-        if self.chain and self.chain_mb and self.chain_mb[0] < n:
-            return self._chained_microbatched(x, preprocess, *self.chain_mb)
         pre = preprocess or (lambda t: t)
         if mb < n and nblocks > 0:
             s2d = preprocess is None and x.shape[-1] == 16
@@ -396,8 +358,6 @@ class FusedResNet:
                 for i in range(nblocks):
                     y = self._block(y, self.blocks[i], out=feats[n0:n0 + mb] if i == nblocks - 1 else None)
             y = feats
-        elif preprocess is preprocess_s2d_u8 and self.stem_u8:
-            y, nblocks = stem_pool_u8(x, self.stem), 0  # K7 preprocess fused into the stem kernel
         elif self.chain:
             y, t1 = self._stem_t1(pre(x))
             return self._stages_chained(y, t1=t1)

@@ -40,7 +40,6 @@ _SIGS = {
     "ai4e_chain_stamps_read": [_vp],
     "ai4e_k256_stamps_read": [_vp],  # (AI4E_K256_STAMPS diagnostic builds only)
     "ai4e_pair_stamps_read": [_vp],  # (AI4E_PAIR_STAMPS diagnostic builds only)
-    "ai4e_stem_pool_u8_fwd": [_vp] * 4 + [_c_int] * 5 + [_vp, _vp, _c_float, _vp],
     "ai4e_softmax_topk": [_vp, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp],
     "ai4e_preprocess_u8": [_vp, _vp, _c_long, _c_int, _vp, _vp, _c_float, _vp],
     "ai4e_preprocess_s2d_u8": [_vp, _vp, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _c_float, _vp],

@@ -483,28 +483,6 @@ def stem_pool_c1(x: torch.Tensor, pc: PackedConv, c1: PackedConv):
     return y, t1
 
 
-def stem_pool_u8(img: torch.Tensor, pc: PackedConv, mean=None, std=None, scale: float = 1.0 / 255.0) -> torch.Tensor:
-    """uint8 NHWC images -> pooled stem output: the s2d preprocess (K7) fused into K1s, so the normalized
-    space-to-depth image (103 MB at batch 256) is never written. Same math as
-    ``stem_pool(preprocess_s2d_u8(img), pc)``, which is also the non-HIP path."""
-    import ctypes
-
-    from .pool import IMAGENET_MEAN, IMAGENET_STD, ctypes_floats, preprocess_s2d_u8
-
-    mean = IMAGENET_MEAN if mean is None else mean
-    std = IMAGENET_STD if std is None else std
-    n, h, w, cin = img.shape
-    if (_ext.backend_for(img) != "hip" or img.dtype != torch.uint8 or cin > 4 or h % 2 or w % 2
-            or not img.is_contiguous() or pc.cout != 64 or (pc.kh, pc.kw, pc.pad, pc.pad_hi) != (4, 4, 1, 2)):
-        return stem_pool(preprocess_s2d_u8(img, mean, std, scale), pc)
-    m4 = ctypes_floats(list(mean) + [0.0] * (4 - len(mean)))
-    s4 = ctypes_floats(list(std) + [1.0] * (4 - len(std)))
-    y = torch.empty(n, (h // 2 - 1) // 2 + 1, (w // 2 - 1) // 2 + 1, 64, device=img.device, dtype=torch.bfloat16)
-    _ext.call("ai4e_stem_pool_u8_fwd", img.data_ptr(), pc.w_packed.data_ptr(), pc.bias.data_ptr(), y.data_ptr(),
-              n, h, w, cin, pc.kpad, ctypes.addressof(m4), ctypes.addressof(s4), scale, _ext.stream_ptr(img.device))
-    return y
-
-
 def _conv_torch(x, pc, residual, relu):
     cdt = torch.float32 if not x.is_cuda else x.dtype
     xin = x[..., :pc.cin].permute(0, 3, 1, 2).to(cdt)

@@ -57,70 +57,10 @@ __device__ __forceinline__ unsigned long long readlane_u64(unsigned long long v,
   return (static_cast<unsigned long long>(hi) << 32) | lo;
 }
 
-__global__ __launch_bounds__(64) void nms_reduce_kernel(const unsigned long long* __restrict__ mask,
-                                                        const int* __restrict__ valid, int N, int max_out,
-                                                        int* __restrict__ keep, int* __restrict__ count) {
-  const int b = blockIdx.x;
-  const int W = (N + 63) / 64;
-  const int lane = threadIdx.x;
-  const int n = valid ? min(valid[b], N) : N;
-  const unsigned long long* const mb = mask + static_cast<long>(b) * N * W;
-  unsigned long long rem0 = 0, rem1 = 0;  // removed bits of words lane, lane + 64
-  int kept = 0;
-  const int nblk = (n + 63) / 64;
-  for (int wb = 0; wb < nblk && kept < max_out; ++wb) {
-    const unsigned long long remw = wb < 64 ? readlane_u64(rem0, wb) : readlane_u64(rem1, wb - 64);
-    const int inblk = min(64, n - 64 * wb);
-    unsigned long long alive = ~remw & (inblk == 64 ? ~0ull : ((1ull << inblk) - 1));
-    const int i_l = 64 * wb + lane;
-    const unsigned long long mine = i_l < n ? mb[static_cast<long>(i_l) * W + wb] : 0ull;
-    unsigned long long keepbits = 0;
-    int kb = 0;
-    while (alive && kept + kb < max_out) {
-      const int i = __builtin_ctzll(alive);
-      keepbits |= 1ull << i;
-      ++kb;
-      alive &= ~(1ull << i);
-      alive &= ~readlane_u64(mine, i);  // box i suppresses the later boxes of this block
-    }
-    if ((keepbits >> lane) & 1ull)
-      keep[static_cast<long>(b) * max_out + kept + __builtin_popcountll(keepbits & ((1ull << lane) - 1))] = i_l;
-    kept += kb;
-    // OR the kept rows' later words into the bitmap, 8 rows per batch
-    const int w0 = lane, w1 = lane + 64;
-    const bool ok0 = w0 > wb && w0 < W, ok1 = w1 > wb && w1 < W;
-    while (keepbits && wb + 1 < W) {
-      long rows[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        if (keepbits) {
-          rows[u] = static_cast<long>(64 * wb + __builtin_ctzll(keepbits)) * W;
-          keepbits &= keepbits - 1;
-        } else {
-          rows[u] = -1;
-        }
-      }
-      unsigned long long r0[8], r1[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        r0[u] = rows[u] >= 0 && ok0 ? mb[rows[u] + w0] : 0ull;
-        r1[u] = rows[u] >= 0 && ok1 ? mb[rows[u] + w1] : 0ull;
-      }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        rem0 |= r0[u];
-        rem1 |= r1[u];
-      }
-    }
-  }
-  if (lane == 0) count[b] = min(kept, max_out);
-  for (int i = min(kept, max_out) + lane; i < max_out; i += 64) keep[static_cast<long>(b) * max_out + i] = -1;
-}
-
-// Multi-wave form of nms_reduce_kernel (one workgroup of NMS_MW_WAVES waves per image). The per-image greedy scan
-// is serial in the 64-box blocks; what the one-wave form spends most of its time on is the memory latency of OR-ing
-// each block's kept rows into the bitmap (one round trip per 8 kept boxes) and of the next block's diagonal words,
-// both on the critical path. Here:
+// Greedy scan, one workgroup of NMS_MW_WAVES waves per image (round 5; the one-wave form it replaced, 210 vs
+// 121 µs for the RPN call at batch 32, is in profiles/r5_pruned/). The scan is serial in the 64-box blocks; the
+// one-wave form spent most of its time on the memory latency of OR-ing each block's kept rows into the bitmap (one
+// round trip per 8 kept boxes) and of the next block's diagonal words, both on the critical path. Here:
 //  * wave 0 resolves the blocks' diagonals; it prefetches each block's diagonal word AND the two words after it, two
 //    blocks ahead, so the contribution of a block's kept boxes to the next two blocks' diagonals is an OR over lanes
 //    of registers already loaded (no load on the critical path);
@@ -129,7 +69,7 @@ __global__ __launch_bounds__(64) void nms_reduce_kernel(const unsigned long long
 //    to the load latency: ~2.9 us per 64-box block);
 //  * per block, two workgroup barriers: the row waves publish their partial word of the block, wave 0 publishes the
 //    block's kept bits.
-// Same greedy result as nms_reduce_kernel (same kept set, same order).
+// Same greedy result as the sequential algorithm (same kept set, same order).
 constexpr int NMS_MW_WAVES = 9;
 constexpr int NMS_MW_ROWS = (64 + NMS_MW_WAVES - 2) / (NMS_MW_WAVES - 1);  // kept rows per row wave per block
 static_assert(NMS_MW_ROWS * (NMS_MW_WAVES - 1) == 64, "row waves split a block's 64 bit positions evenly");
@@ -1072,17 +1012,9 @@ AI4E_API int ai4e_nms_mask(const void* boxes, int B, int N, float thr, void* mas
 AI4E_API int ai4e_nms_reduce(const void* mask, const void* valid, int B, int N, int max_out, void* keep, void* count,
                              hipStream_t s) {
   if (N > 8192) return AI4E_EINVAL;
-  static const int mw = [] {
-    const char* e = getenv("AI4E_NMS_MW");  // A/B switch: 0 = the one-wave scan
-    return e ? atoi(e) : 1;
-  }();
-  if (mw)
-    hipLaunchKernelGGL(nms_reduce_mw_kernel, dim3(B), dim3(64 * NMS_MW_WAVES), 0, s,
-                       static_cast<const unsigned long long*>(mask), static_cast<const int*>(valid), N, max_out,
-                       static_cast<int*>(keep), static_cast<int*>(count));
-  else
-    hipLaunchKernelGGL(nms_reduce_kernel, dim3(B), dim3(64), 0, s, static_cast<const unsigned long long*>(mask),
-                       static_cast<const int*>(valid), N, max_out, static_cast<int*>(keep), static_cast<int*>(count));
+  hipLaunchKernelGGL(nms_reduce_mw_kernel, dim3(B), dim3(64 * NMS_MW_WAVES), 0, s,
+                     static_cast<const unsigned long long*>(mask), static_cast<const int*>(valid), N, max_out,
+                     static_cast<int*>(keep), static_cast<int*>(count));
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
 }
 
@@ -1201,11 +1133,8 @@ AI4E_API int ai4e_roi_align_fpn_nhwc(const void* f0, const void* f1, const void*
     lv.scale[i] = scales[i];
   }
   if (static_cast<long>(R) * PH >= (1L << 31)) return AI4E_EINVAL;
-  static const int per_roi = [] {
-    const char* e = getenv("AI4E_ROI_PER_ROI");  // A/B switch: 0 = one workgroup per (RoI, output row)
-    return e ? atoi(e) : 1;
-  }();
-  if (per_roi && PW * (C / 8) <= 256)
+  // one workgroup per RoI; per (RoI, output row) only when a row's (column, 8-channel chunk) lanes exceed 256
+  if (PW * (C / 8) <= 256)
     hipLaunchKernelGGL(roi_align_fpn_roi_kernel, dim3(static_cast<unsigned>(R)), dim3(256), 0, s, lv,
                        static_cast<const float*>(rois), static_cast<uint16_t*>(out), C, R, PH, PW, sampling, aligned);
   else

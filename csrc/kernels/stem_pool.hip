@@ -37,11 +37,6 @@ struct StemParams {
   uint16_t* y;         // [N, PH, PW, 64]
   const uint16_t* zero;
   int H, W, PH, PW, kpad, tiles_r, tiles_c;
-  // fused preprocess (stem_pool_direct_kernel<true>): raw uint8 NHWC images [N, 2H, 2W, cin], normalized
-  // as (u8 * scale - mean[c]) * istd[c] while the s2d footprint is built (same math as preprocess_s2d)
-  const uint8_t* img;
-  int cin;
-  float mean[4], istd[4], scale;
   // fused next 1x1 (the first bottleneck's c1, 64 -> 64, + bias, ReLU) on the pooled tile (null = off):
   // t1 [N, PH, PW, 64] = relu(y . W1^T + b1), W1 [>= 64 rows, kpad1 >= 64]
   const uint16_t* w1;
@@ -232,7 +227,7 @@ __device__ unsigned long long g_stem_stamps[2048 * 4 * STEM_NSEG];
   } while (0)
 #endif
 
-template <bool U8, bool C1 = false, bool F16 = false>
+template <bool C1 = false, bool F16 = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void stem_pool_direct_kernel(const StemParams p, int ntiles) {
 #if AI4E_STEM_STAMPS
@@ -290,9 +285,7 @@ void stem_pool_direct_kernel(const StemParams p, int ntiles) {
              sb + D_FP + (wave + 4 * q) * 1024);
     }
   };
-  if constexpr (!U8) {
-    if (static_cast<int>(blockIdx.x) < ntiles) issue_fp(blockIdx.x);
-  }
+  if (static_cast<int>(blockIdx.x) < ntiles) issue_fp(blockIdx.x);
 
   for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
     const int img = t / per_img;
@@ -300,42 +293,11 @@ void stem_pool_direct_kernel(const StemParams p, int ntiles) {
     const int tc = t - img * per_img - tr * p.tiles_c;
     const int ph0 = tr * SP_TR, pw0 = tc * SP_TC;
     const int oh0 = 2 * ph0 - 1, ow0 = 2 * pw0 - 1;
-    if constexpr (U8) {
-      // fused preprocess: one thread per footprint pixel builds its 16 s2d channels
-      // ((dy*2+dx)*cin + c = norm(img[2ih+dy-1, 2iw+dx-1, c]), zero outside the image) and writes both planes
-      const int Hi = 2 * p.H, Wi = 2 * p.W;
-      const uint8_t* const ii = p.img + static_cast<long>(img) * Hi * Wi * p.cin;
-      for (int pix = tid; pix < FP_PIX; pix += 256) {
-        const int a = pix / FP_C, b = pix - a * FP_C;
-        const int ih = oh0 - 1 + a, iw = ow0 - 1 + b;
-        float v[16];
-#pragma unroll
-        for (int k = 0; k < 16; ++k) v[k] = 0.f;
-        if (static_cast<unsigned>(ih) < static_cast<unsigned>(p.H) && static_cast<unsigned>(iw) < static_cast<unsigned>(p.W)) {
-#pragma unroll
-          for (int dy = 0; dy < 2; ++dy)
-#pragma unroll
-            for (int dx = 0; dx < 2; ++dx) {
-              const int yy = 2 * ih + dy - 1, xx = 2 * iw + dx - 1;
-              if (yy < 0 || yy >= Hi || xx < 0 || xx >= Wi) continue;
-              const uint8_t* src = ii + (static_cast<long>(yy) * Wi + xx) * p.cin;
-#pragma unroll
-              for (int c = 0; c < 4; ++c)
-                if (c < p.cin) v[(dy * 2 + dx) * p.cin + c] = (src[c] * p.scale - p.mean[c]) * p.istd[c];
-            }
-        }
-        uint4* d0 = reinterpret_cast<uint4*>(dsm + D_FP + pix * 16);
-        uint4* d1 = reinterpret_cast<uint4*>(dsm + D_FP + (FP_STRIDE + pix) * 16);
-        *d0 = make_uint4(pack2<F16>(v[0], v[1]), pack2<F16>(v[2], v[3]), pack2<F16>(v[4], v[5]), pack2<F16>(v[6], v[7]));
-        *d1 = make_uint4(pack2<F16>(v[8], v[9]), pack2<F16>(v[10], v[11]), pack2<F16>(v[12], v[13]),
-                         pack2<F16>(v[14], v[15]));
-      }
-    }
     // this tile's footprint landed. From the second tile on (C1) the DMA is already complete: the previous
     // iteration waited for its c1 weight loads, issued after the DMA (vmcnt retires in issue order), so only the
     // previous tile's stores can be outstanding (<= 2 pooled-row + 4 t1 stores per wave): they may stay in flight
-    STEM_STAMP(7);  // (U8 preprocess / loop overhead)
-    if (C1 && !U8 && t != static_cast<int>(blockIdx.x)) {
+    STEM_STAMP(7);  // loop overhead
+    if (C1 && t != static_cast<int>(blockIdx.x)) {
       wait_vmcnt<6>();
     } else {
       wait_vmcnt<0>();
@@ -368,10 +330,8 @@ void stem_pool_direct_kernel(const StemParams p, int ntiles) {
           acc[i][j] = mfma_16x16x32<F16>(fw[j], fx[i], acc[i][j]);
     }
     STEM_STAMP(1);  // MFMA loop
-    if constexpr (!U8) {
-      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // every wave finished reading the footprint
-      if (t + static_cast<int>(gridDim.x) < ntiles) issue_fp(t + gridDim.x);
-    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // every wave finished reading the footprint
+    if (t + static_cast<int>(gridDim.x) < ntiles) issue_fp(t + gridDim.x);
     STEM_STAMP(2);  // barrier + next footprint DMA issue
     // epilogue: bf16 relu(acc + b) -> tile [256 px][64 ch] (ptile layout)
 #pragma unroll
@@ -487,11 +447,11 @@ void stem_pool_direct_kernel(const StemParams p, int ntiles) {
 #endif
 }
 
-template <bool U8, bool C1 = false, bool F16 = false>
+template <bool C1 = false, bool F16 = false>
 int launch_direct(const StemParams& p, long nb, hipStream_t stream) {
   static bool attr = false;
   if (!attr) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(stem_pool_direct_kernel<U8, C1, F16>),
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(stem_pool_direct_kernel<C1, F16>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, D_LDS) != hipSuccess)
       return AI4E_ELAUNCH;
     attr = true;
@@ -507,7 +467,7 @@ int launch_direct(const StemParams& p, long nb, hipStream_t stream) {
     return v < 1 ? 1L : v;
   }();
   const long grid = nb < wpc * cus ? nb : wpc * cus;
-  hipLaunchKernelGGL((stem_pool_direct_kernel<U8, C1, F16>), dim3(static_cast<unsigned>(grid)), dim3(256), D_LDS, stream, p,
+  hipLaunchKernelGGL((stem_pool_direct_kernel<C1, F16>), dim3(static_cast<unsigned>(grid)), dim3(256), D_LDS, stream, p,
                      static_cast<int>(nb));
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
 }
@@ -522,38 +482,6 @@ const uint16_t* stem_zero_ptr() {
 }
 
 }  // namespace
-
-// Fused preprocess + stem + max-pool: uint8 NHWC images [N, Hi, Wi, cin<=4] (Hi, Wi even) ->
-// [N, ceil(Hi/4), ceil(Wi/4), 64] bf16. mean4/std4 per channel (host arrays), value = (u8 * scale - mean) / std.
-AI4E_API int ai4e_stem_pool_u8_fwd(const void* img, const void* w, const void* bias, void* y, int N, int Hi, int Wi,
-                                   int cin, int kpad, const float* mean4, const float* std4, float scale,
-                                   hipStream_t stream) {
-  if (!img || !w || !bias || !y || !mean4 || !std4 || kpad < 256 || kpad % 8 || Hi <= 0 || Wi <= 0 || (Hi & 1) ||
-      (Wi & 1) || cin < 1 || cin > 4)
-    return AI4E_EINVAL;
-  StemParams p{};
-  p.w = static_cast<const uint16_t*>(w);
-  p.bias = static_cast<const float*>(bias);
-  p.y = static_cast<uint16_t*>(y);
-  p.zero = stem_zero_ptr();
-  if (!p.zero) return AI4E_ELAUNCH;
-  p.img = static_cast<const uint8_t*>(img);
-  p.cin = cin;
-  for (int c = 0; c < 4; ++c) {
-    p.mean[c] = c < cin ? mean4[c] : 0.f;
-    p.istd[c] = c < cin ? 1.f / std4[c] : 0.f;
-  }
-  p.scale = scale;
-  p.H = Hi / 2; p.W = Wi / 2;
-  p.PH = (p.H - 1) / 2 + 1;
-  p.PW = (p.W - 1) / 2 + 1;
-  p.kpad = kpad;
-  p.tiles_r = ai4e_cdiv(p.PH, SP_TR);
-  p.tiles_c = ai4e_cdiv(p.PW, SP_TC);
-  const long nb = static_cast<long>(N) * p.tiles_r * p.tiles_c;
-  if (nb <= 0) return AI4E_OK;
-  return launch_direct<true>(p, nb, stream);
-}
 
 // Stem + pool + the first bottleneck's 1x1 c1 (64 -> 64, bias, ReLU) in one launch: y as ai4e_stem_pool_fwd,
 // plus t1 [N, PH, PW, 64] = relu(y . W1^T + b1) (w1 [>= 64 rows, kpad1 >= 64] bf16, b1 [>= 64] fp32), computed
@@ -583,7 +511,7 @@ int stem_c1(bool f16, const void* x, const void* w, const void* bias, void* y, c
   p.tiles_c = ai4e_cdiv(p.PW, SP_TC);
   const long nb = static_cast<long>(N) * p.tiles_r * p.tiles_c;
   if (nb <= 0) return AI4E_OK;
-  return f16 ? launch_direct<false, true, true>(p, nb, stream) : launch_direct<false, true>(p, nb, stream);
+  return f16 ? launch_direct<true, true>(p, nb, stream) : launch_direct<true>(p, nb, stream);
 }
 }  // namespace
 
@@ -627,7 +555,7 @@ AI4E_API int ai4e_stem_pool_fwd(const void* x, const void* w, const void* bias, 
   p.tiles_c = ai4e_cdiv(p.PW, SP_TC);
   const long nb = static_cast<long>(N) * p.tiles_r * p.tiles_c;
   if (nb <= 0) return AI4E_OK;
-  if (variant == 0) return launch_direct<false>(p, nb, stream);
+  if (variant == 0) return launch_direct<>(p, nb, stream);
   hipLaunchKernelGGL(stem_pool_kernel, dim3(static_cast<unsigned>(nb)), dim3(256), 0, stream, p);
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
 }

@@ -155,24 +155,6 @@ def test_conv_chain_down(shape, tile):
     assert err <= 0.02 * tr.abs().max().item() + 0.03, err
 
 
-@pytest.mark.parametrize("shape", [(3, 224, 224, 3), (2, 62, 50, 4), (1, 34, 18, 3)])
-def test_stem_pool_u8_fused_preprocess(shape):
-    """Preprocess fused into the stem kernel == preprocess kernel + stem kernel (same bf16 math)."""
-    from aiforearth_api_platform_amd.ops.conv import pack_stem_s2d, stem_pool, stem_pool_u8
-    from aiforearth_api_platform_amd.ops.pool import preprocess_s2d_u8
-
-    n, h, w, c = shape
-    torch.manual_seed(6)
-    pc = pack_stem_s2d(torch.randn(64, c, 7, 7) / 12, torch.randn(64) * 0.1).to(DEV)
-    img = torch.randint(0, 256, (n, h, w, c), dtype=torch.uint8, device=DEV)
-    mean, std = [0.4, 0.5, 0.3, 0.2][:c], [0.2, 0.25, 0.3, 0.5][:c]
-    a = stem_pool_u8(img, pc, mean, std)
-    b = stem_pool(preprocess_s2d_u8(img, mean, std), pc)
-    torch.cuda.synchronize()
-    assert a.shape == b.shape
-    assert (a.float() - b.float()).abs().max().item() <= 1e-2 * b.float().abs().max().item() + 1e-3
-
-
 @pytest.mark.parametrize("shape", [(3, 112, 112), (2, 31, 25), (1, 17, 9)])
 def test_stem_pool_fused_c1(shape):
     """K1s with the first bottleneck's 1x1 fused (t1 from the pooled tile in LDS) == K1s + a K1 conv."""

@@ -74,19 +74,6 @@ def test_chunked_prefix_matches_full_batch():
         assert (out - ref).abs().max().item() < 1e-2, chunk
 
 
-def test_chained_microbatch_matches_full_batch():
-    """Chained micro-batching (stem + the first stages mb images at a time, outputs written into
-    full-batch buffers, the next stage's first c1 carried across) does not change the result."""
-    m = resnet50(seed=5)
-    img = torch.randint(0, 256, (6, 64, 64, 3), dtype=torch.uint8)
-    fused = FusedResNet(m)
-    ref = fused.forward_u8(img)
-    for cfg in [(2, 1), (4, 2), (4, 3), (5, 1)]:
-        fused.chain_mb = cfg
-        out = fused.forward_u8(img)
-        assert (out - ref).abs().max().item() < 1e-4, cfg
-
-
 def test_pair_route_defaults():
     from aiforearth_api_platform_amd.ops import conv as convmod
 
