@@ -22,7 +22,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import torch
 import torch.nn as nn
 
-from ..ops.conv import PackedConv, conv2d_nhwc, pack_conv
+from ..ops.conv import PackedConv, conv2d_head_nhwc, conv2d_nhwc, pack_conv
 from ..ops.debug import crumb
 from ..ops.detection import (det_decode, gather_keep, nms_batched_sorted, roi_align_fpn, rpn_decode_into, rpn_topk,
                               sort_select)
@@ -157,8 +157,8 @@ class FasterRCNN:
         lvl = torch.empty(B, KT, device=P[0].device, dtype=torch.float32)
         off = 0
         for li, (p, k) in enumerate(zip(P, ks)):
-            t = conv2d_nhwc(p, self.rpn_conv, relu=True)
-            head = conv2d_nhwc(t, self.rpn_head)                   # [B, h, w, 16]: A logits, 4A deltas
+            # [B, h, w, 16]: A logits, 4A deltas; on the 256-wide tiles the head runs in the RPN conv's epilogue
+            head = conv2d_head_nhwc(p, self.rpn_conv, self.rpn_head)
             idx = rpn_topk(head, A, k)                            # per-level pre-NMS top-k
             # decode + clip + sigmoid + min-size mask straight into the all-level buffers (one HIP launch)
             crumb(f"rpn.topk{li}", idx)

@@ -189,6 +189,30 @@ def _conv_hip(x, pc, residual, relu, out, out_coff, tile_cfg, residual_up2=False
         _ext.call("ai4e_conv2d_gn_fwd", *args, gn[0].data_ptr(), gn[1], _ext.stream_ptr(x.device))
 
 
+def conv2d_head_nhwc(x: torch.Tensor, pc: PackedConv, head: PackedConv, relu: bool = True,
+                     tile_cfg: int = -1) -> torch.Tensor:
+    """``conv2d_nhwc(conv2d_nhwc(x, pc, relu=relu), head)`` for a 256-channel conv followed by a 1x1 conv to 16
+    channels whose input is used nowhere else (the FPN RPN conv and its objectness / box-delta head). On a 256-wide
+    tile config the head runs inside the conv's epilogue on the staged output tile (``ai4e_conv2d_head_fwd``): the
+    256-channel intermediate is never written and the head's separate pass over it disappears. Other shapes run the
+    two convs. Returns [N, OH, OW, 16]. ``tile_cfg`` overrides the tuned tile of the first conv (tests)."""
+    n, h, w, c = x.shape
+    oh, ow = pc.out_hw(h, w)
+    cfg = tuned_tile(pc, n, h, w, False) if tile_cfg < 0 else tile_cfg
+    fused = (_ext.backend_for(x) == "hip" and cfg in (6, 9, 10) and pc.cout == 256 and head.cout == 16
+             and (head.kh, head.kw, head.stride, head.pad) == (1, 1, 1, 0) and head.cin_pad == 256
+             and head.kpad >= 256 and x.dtype == torch.bfloat16 and pc.w_packed.dtype == torch.bfloat16
+             and head.w_packed.dtype == torch.bfloat16 and c == pc.cin_pad and x.is_contiguous()
+             and _ext.has("ai4e_conv2d_head_fwd"))
+    if not fused:
+        return conv2d_nhwc(conv2d_nhwc(x, pc, relu=relu, tile_cfg=tile_cfg), head)
+    y = torch.empty(n, oh, ow, 16, device=x.device, dtype=x.dtype)
+    _ext.call("ai4e_conv2d_head_fwd", x.data_ptr(), pc.w_packed.data_ptr(), pc.bias.data_ptr(), None, None, n, h, w,
+              c, c, 0, pc.kh, pc.kw, pc.stride, pc.pad, oh, ow, pc.cout, pc.kpad, pc.cout, 0, 0, int(relu), cfg,
+              head.w_packed.data_ptr(), head.kpad, head.bias.data_ptr(), y.data_ptr(), _ext.stream_ptr(x.device))
+    return y
+
+
 def conv2d_gn_nhwc(x: torch.Tensor, pc: PackedConv, groups: int, out: Optional[torch.Tensor] = None,
                    out_coff: int = 0):
     """``conv2d_nhwc(x, pc)`` that also produces the GroupNorm statistics of its output from the same epilogue

@@ -92,6 +92,12 @@ struct ConvParams {
   // gnp[((img * (OH*OW/BM) + chunk) * gn_groups + g) * 4 + {0, 1, 2}]
   float* gnp;
   int gn_groups;
+  // a 1x1 conv to 16 channels fused after this one (256-wide configs, Kout == 256; null = off): hy [M, 16] =
+  // (the stored bf16 output) . hw^T + hb, hw [16 rows, ld hw_ld >= 256]; y may then be null (output not stored)
+  const uint16_t* hw;
+  const float* hb;
+  uint16_t* hy;
+  int hw_ld;
 };
 
 // Row of the residual tensor for output pixel m: m itself, or (relu flag bit 1) the pixel (oh/2, ow/2) of a
@@ -560,7 +566,10 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
   constexpr int L3 = X1 / 32;      // DMAs per lane for u3
   constexpr int MF1 = X1 / 16;     // u3 fragments per wave
   constexpr int MFR = 4 + MF1;     // accumulator rows
-  __shared__ __attribute__((aligned(1024))) uint8_t smem[2 * 4 * U_BYTES];  // the only LDS object
+  __shared__ __attribute__((aligned(1024))) uint8_t smem[2 * 4 * U_BYTES];  // the ring, then the epilogue tile
+  // fused head only (p.hy): its 16 x 256 weights, 8 KB of dynamic LDS past the ring (still one workgroup per CU),
+  // row r's 16-B chunk c at chunk c ^ r (the head's 16 lanes of a K chunk read 16 different chunks)
+  extern __shared__ __attribute__((aligned(16))) uint8_t hsm[];
 #if AI4E_K256_STAMPS
   unsigned long long k_sum[K256_NSEG] = {0, 0, 0, 0, 0, 0}, k_last;
   asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(k_last)::"memory");
@@ -578,6 +587,11 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
   const int n0 = nt * 256;
   const int nk = p.Kpad / 64;
   const uint32_t sbase = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(smem));
+  if (p.hy) {
+    // the oldest DMA of the launch, so every counted ring wait below also covers it; thread tid fills slot tid
+    const int hr = tid >> 5, hc = (tid & 31) ^ hr;
+    glds16(p.hw + hr * p.hw_ld + 8 * hc, static_cast<uint32_t>(reinterpret_cast<uintptr_t>(hsm)) + wave * 1024);
+  }
 
   // ---- DMA sources. Lane writes unit row R_i = 16*wave + 8*i + (lane>>3) (u3 of BM 192: 8*wave +
   //      (lane>>3)), physical 16-B chunk lane&7, holding logical chunk q_i = (lane&7) ^ ((R_i >> 1) & 7).
@@ -869,8 +883,45 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
       }
       if (tid < 256 / cg) kout = fmaxf(tile[tid * cg] + p.bias[min(n0 + tid * cg, p.Kout - 1)], lo_gn);
     }
+    if (p.hy) {
+      // the fused 16-channel 1x1 (the FPN RPN head after its 3x3 conv): each wave takes 16-pixel blocks of this pass;
+      // the B operand is the epilogue's bf16 output (bias, ReLU, same rounding as the stored tensor) built from the
+      // staged fp32 tile, the A operand the head weights (row = lane & 15) from the 8 KB of dynamic LDS they were
+      // DMA'd into at kernel start
+      const uint4 nores = make_uint4(0u, 0u, 0u, 0u);
+      for (int blk = wave; blk < WROWS / 16; blk += 8) {
+        const int r = 16 * blk + (lane & 15);
+        f32x4_t hacc = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+          const int c8 = 4 * s + (lane >> 4);  // 8-channel chunk of K
+          const float4 v0 = *reinterpret_cast<const float4*>(tile + r * 256 + 4 * ((2 * c8) ^ (r & 7)));
+          const float4 v1 = *reinterpret_cast<const float4*>(tile + r * 256 + 4 * ((2 * c8 + 1) ^ (r & 7)));
+          const float4 b0 = *reinterpret_cast<const float4*>(p.bias + 8 * c8);
+          const float4 b1 = *reinterpret_cast<const float4*>(p.bias + 8 * c8 + 4);
+          const float f[8] = {v0.x + b0.x, v0.y + b0.y, v0.z + b0.z, v0.w + b0.w,
+                              v1.x + b1.x, v1.y + b1.y, v1.z + b1.z, v1.w + b1.w};
+          const uint4 o = epilogue8<F16>(f, false, nores, (p.relu & 1) != 0);
+          const int hr = lane & 15;
+          const bf16x8_t wb = *reinterpret_cast<const bf16x8_t*>(hsm + hr * 512 + ((c8 ^ hr) << 4));
+          hacc = mfma_16x16x32<F16>(wb, __builtin_bit_cast(bf16x8_t, o), hacc);
+        }
+        // lane: pixel r, head channels 4 * (lane >> 4) + 0..3
+        const int m = m0 + WROWS * pass + r;
+        if (m < p.M) {
+          const int hc = 4 * (lane >> 4);
+          const float4 hb = *reinterpret_cast<const float4*>(p.hb + hc);
+          const uint2 ho = make_uint2(pack2<F16>(hacc[0] + hb.x, hacc[1] + hb.y), pack2<F16>(hacc[2] + hb.z, hacc[3] + hb.w));
+          *reinterpret_cast<uint2*>(p.hy + static_cast<long>(m) * 16 + hc) = ho;
+        }
+      }
+    }
     constexpr int EP = WROWS / 16;  // 16-B output chunks per thread and pass
     uint4 rv[EP];
+    if (!p.y) {  // head only: the conv's own output is not stored
+      EPI_BARRIER();
+      continue;
+    }
     if (p.res) {
 #pragma unroll
       for (int e = 0; e < EP; ++e) {
@@ -892,7 +943,7 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
       const float f[8] = {v0.x + b0.x, v0.y + b0.y, v0.z + b0.z, v0.w + b0.w,
                           v1.x + b1.x, v1.y + b1.y, v1.z + b1.z, v1.w + b1.w};
       const uint4 o = epilogue8<F16>(f, p.res != nullptr, rv[e], (p.relu & 1) != 0);
-      if (m < p.M && n < p.Kout) ai4e_conv::st16_stream(p.y + static_cast<long>(m) * p.ldy + p.ycoff + n, o);
+      if (m < p.M && n < p.Kout && p.y) ai4e_conv::st16_stream(p.y + static_cast<long>(m) * p.ldy + p.ycoff + n, o);
       if (p.gnp && m < p.M && n < p.Kout) {  // statistics of the values as stored (bf16)
         const uint32_t ow[4] = {o.x, o.y, o.z, o.w};
 #pragma unroll
@@ -1020,10 +1071,11 @@ int launch256(const ConvParams& p0, hipStream_t s) {
   const int nb = mt * p.ntiles_n;
   p.zero = zero_chunk_ptr();
   if (!p.zero) return AI4E_ELAUNCH;
+  const unsigned dyn = p.hy ? 16u * 512u : 0u;  // the fused head's weights
   if (p.KH == 1 && p.KW == 1 && p.pad == 0)
-    hipLaunchKernelGGL((conv_igemm256_kernel<GATHER_POINTWISE, BM, F16, PH3>), dim3(nb), dim3(512), 0, s, p);
+    hipLaunchKernelGGL((conv_igemm256_kernel<GATHER_POINTWISE, BM, F16, PH3>), dim3(nb), dim3(512), dyn, s, p);
   else
-    hipLaunchKernelGGL((conv_igemm256_kernel<GATHER_TAP, BM, F16, PH3>), dim3(nb), dim3(512), 0, s, p);
+    hipLaunchKernelGGL((conv_igemm256_kernel<GATHER_TAP, BM, F16, PH3>), dim3(nb), dim3(512), dyn, s, p);
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
 }
 
@@ -1041,7 +1093,8 @@ namespace {
 template <bool F16>
 int conv2d_impl(const void* x, const void* w, const void* bias, const void* res, void* y, int N, int H, int W, int C,
                 int ldx, int xcoff, int KH, int KW, int stride, int pad, int OH, int OW, int Kout, int Kpad, int ldy,
-                int ycoff, int ldres, int relu, int tile_cfg, float* gnp, int gn_groups, hipStream_t stream) {
+                int ycoff, int ldres, int relu, int tile_cfg, float* gnp, int gn_groups, hipStream_t stream,
+                const void* hw = nullptr, int hw_ld = 0, const void* hb = nullptr, void* hy = nullptr) {
   if (C % 8 || ldx % 8 || xcoff % 8 || Kpad % (2 * BK) || Kout % 4 || ldy % 4 || ycoff % 4 || (res && ldres % 4) ||
       Kpad < KH * KW * C)
     return AI4E_EINVAL;
@@ -1056,6 +1109,18 @@ int conv2d_impl(const void* x, const void* w, const void* bias, const void* res,
   p.Kout = Kout; p.Kpad = Kpad; p.ldy = ldy; p.ycoff = ycoff; p.ldres = ldres; p.relu = relu;
   p.M = N * OH * OW;
   if ((relu & 2) && (!res || (OH & 1) || (OW & 1))) return AI4E_EINVAL;  // half-resolution residual grid
+  if (hy) {
+    // fused 16-channel head: the 256-wide configs with the whole Kout = 256 in one channel tile
+    if (!hw || !hb || hw_ld < 256 || hw_ld % 8 || Kout != 256 || gnp || (relu & 2) ||
+        !(tile_cfg == 6 || tile_cfg == 9 || tile_cfg == 10))
+      return AI4E_EINVAL;
+    p.hw = static_cast<const uint16_t*>(hw);
+    p.hw_ld = hw_ld;
+    p.hb = static_cast<const float*>(hb);
+    p.hy = static_cast<uint16_t*>(hy);
+  } else if (!y) {
+    return AI4E_EINVAL;
+  }
   if (p.M <= 0) return AI4E_OK;
   if (tile_cfg == 0) tile_cfg = Kout <= 64 ? 2 : 1;
   if (gnp) {
@@ -1117,6 +1182,19 @@ AI4E_API int ai4e_conv2d_gn_fwd(const void* x, const void* w, const void* bias, 
   if (!gn_partials) return AI4E_EINVAL;
   return conv2d_impl<false>(x, w, bias, res, y, N, H, W, C, ldx, xcoff, KH, KW, stride, pad, OH, OW, Kout, Kpad, ldy,
                             ycoff, ldres, relu, tile_cfg, static_cast<float*>(gn_partials), gn_groups, stream);
+}
+
+// Same conv (a 256-wide tile config: 6, 9 or 10; Kout == 256, no residual upsample, no GroupNorm) with a 1x1 conv
+// to 16 channels fused into its epilogue: head [N*OH*OW, 16] = (the conv's stored bf16 output) . hw^T + hb, hw
+// [16 rows, ld hw_ld] bf16, hb [16] fp32. y may be null: the conv's output is then never written (the FPN RPN conv,
+// whose only consumer is its 16-channel head).
+AI4E_API int ai4e_conv2d_head_fwd(const void* x, const void* w, const void* bias, const void* res, void* y, int N,
+                                  int H, int W, int C, int ldx, int xcoff, int KH, int KW, int stride, int pad, int OH,
+                                  int OW, int Kout, int Kpad, int ldy, int ycoff, int ldres, int relu, int tile_cfg,
+                                  const void* hw, int hw_ld, const void* hb, void* head, hipStream_t stream) {
+  if (!head) return AI4E_EINVAL;
+  return conv2d_impl<false>(x, w, bias, res, y, N, H, W, C, ldx, xcoff, KH, KW, stride, pad, OH, OW, Kout, Kpad, ldy,
+                            ycoff, ldres, relu, tile_cfg, nullptr, 0, stream, hw, hw_ld, hb, head);
 }
 
 #if AI4E_K256_STAMPS

@@ -32,25 +32,32 @@ __global__ __launch_bounds__(NMS_BLOCK) void nms_mask_kernel(const float4* __res
   const float ai = (bi.z - bi.x) * (bi.w - bi.y);
   unsigned long long bits = 0;
   const int jn = min(NMS_BLOCK, N - jb * NMS_BLOCK);
-  for (int k = (ib == jb ? t + 1 : 0); k < jn; ++k) {
+  auto pair = [&](int k) __attribute__((always_inline)) {
     const float4 bj = sb[k];
     const float iw = fmaxf(fminf(bi.z, bj.z) - fmaxf(bi.x, bj.x), 0.f);
     const float ih = fmaxf(fminf(bi.w, bj.w) - fmaxf(bi.y, bj.y), 0.f);
     const float inter = iw * ih;
     const float ua = ai + sarea[k] - inter;
-    if (ua > 0.f && inter > thr * ua) bits |= 1ull << k;
+    return ua > 0.f && inter > thr * ua;
+  };
+  if (jn == NMS_BLOCK) {
+    // full column block: a uniform, fully unrolled walk (constant LDS offsets and bit positions); the diagonal
+    // block's j <= i pairs are masked off afterwards instead of starting each lane's loop at its own t + 1
+    uint32_t lo = 0, hi = 0;
+#pragma unroll
+    for (int k = 0; k < 32; ++k) lo |= pair(k) ? (1u << k) : 0u;
+#pragma unroll
+    for (int k = 0; k < 32; ++k) hi |= pair(k + 32) ? (1u << k) : 0u;
+    bits = (static_cast<unsigned long long>(hi) << 32) | lo;
+    if (ib == jb) bits &= t == 63 ? 0ull : ~0ull << (t + 1);
+  } else {
+    for (int k = (ib == jb ? t + 1 : 0); k < jn; ++k)
+      if (pair(k)) bits |= 1ull << k;
   }
   mask[(static_cast<long>(b) * N + i) * W + jb] = bits;
 }
 
-// One wave per image: greedy scan in score order over the bitmask, 64 candidates (one mask word) at a
-// time. valid[b] = number of real boxes (the rest are padding). keep[b][0..count) = kept indices
-// (<= max_out), count[b].
-//  * the "removed" bitmap lives in registers: lane l owns words l and l + 64 (N <= 8192);
-//  * inside a 64-box block the greedy order is resolved on the block's own mask words (lane i holds box i's
-//    word for this block, one coalesced load; a scalar loop over the alive bits with lane reads);
-//  * the full rows of the block's kept boxes are OR-ed into the bitmap 8 rows per batch, so their loads are
-//    in flight together (one memory latency per 8 kept boxes instead of one per box).
+// 64-bit lane read (two v_readlane_b32) for the greedy scan below.
 __device__ __forceinline__ unsigned long long readlane_u64(unsigned long long v, int l) {
   const uint32_t lo = __builtin_amdgcn_readlane(static_cast<uint32_t>(v), l);
   const uint32_t hi = __builtin_amdgcn_readlane(static_cast<uint32_t>(v >> 32), l);

@@ -474,3 +474,35 @@ def test_resizing_servable_scales_boxes_to_frame_coordinates():
     assert torch.equal(count, c2)
     k = int(count[0, 0])
     assert torch.allclose(boxes[0, :k], b2[0, :k] * torch.tensor([2.5, 1.875, 2.5, 1.875], device=DEV), atol=1e-3)
+
+
+@pytest.mark.parametrize("cfg,shape", [(6, (2, 32, 32)), (9, (3, 24, 16)), (10, (1, 40, 20)), (6, (1, 10, 10))])
+def test_conv_fused_rpn_head_matches_two_convs(cfg, shape):
+    """The 16-channel 1x1 head run in the 256-wide conv's epilogue (``conv2d_head_nhwc``, the RPN conv + head) against
+    the two separate convs (same bf16 intermediate; only the head's fp32 summation order differs) and against fp32
+    PyTorch of the same bf16 weights. The last shape has a partial pixel tile (M % BM != 0)."""
+    from aiforearth_api_platform_amd.ops.conv import conv2d_head_nhwc, conv2d_nhwc, pack_conv
+
+    n, h, w = shape
+    g = torch.Generator().manual_seed(11)
+    pc = pack_conv(torch.randn(256, 256, 3, 3, generator=g) * 0.02, torch.randn(256, generator=g) * 0.1, pad=1).to(DEV)
+    hw = torch.zeros(16, 256, 1, 1)
+    hw[:15] = torch.randn(15, 256, 1, 1, generator=g) * 0.05
+    hb = torch.zeros(16)
+    hb[:15] = torch.randn(15, generator=g) * 0.1
+    head = pack_conv(hw, hb).to(DEV)
+    x = (torch.randn(n, h, w, 256, generator=g)).to(DEV, torch.bfloat16)
+    fused = conv2d_head_nhwc(x, pc, head, tile_cfg=cfg)
+    t = conv2d_nhwc(x, pc, relu=True, tile_cfg=cfg)
+    two = conv2d_nhwc(t, head)
+    torch.cuda.synchronize()
+    assert fused.shape == (n, h, w, 16)
+    err = (fused.float() - two.float()).abs().max().item()
+    assert err <= 1e-2 * two.float().abs().max().item() + 1e-3, err
+    # fp32 reference of the same (bf16-rounded) weights
+    w1 = pc.w_packed[:256, :2304].float().reshape(256, 3, 3, 256).permute(0, 3, 1, 2)
+    ref_t = F.relu(F.conv2d(x.float().permute(0, 3, 1, 2), w1, pc.bias[:256], padding=1))
+    ref = F.conv2d(ref_t, head.w_packed[:16, :256].float()[:, :, None, None], head.bias[:16])
+    ref = ref.permute(0, 2, 3, 1)
+    err = (fused.float() - ref).abs().max().item()
+    assert err <= 2e-2 * ref.abs().max().item() + 1e-2, err
