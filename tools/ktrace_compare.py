@@ -1,3 +1,8 @@
+"""Per-kernel comparison of two rocprofv3 --kernel-trace CSVs of ``bench/profile_model.py``: sums each kernel's
+dispatches from the last stem launch on (the second, timed forward).
+
+    python tools/ktrace_compare.py before/run_kernel_trace.csv after/run_kernel_trace.csv
+"""
 import csv,sys,collections
 def load(path):
     rows=list(csv.DictReader(open(path)))
