@@ -65,7 +65,6 @@ _SIGS = {
     "ai4e_det_decode": [_vp] * 6 + [_c_int] * 4 + [_vp] + [_c_float] * 4 + [_c_int, _vp],
     "ai4e_roi_align_nhwc": [_vp, _vp, _vp] + [_c_int] * 7 + [_c_float, _c_int, _c_int, _vp],
     "ai4e_roi_align_fpn_nhwc": [_vp] * 8 + [_c_int] * 6 + [_vp],
-    "ai4e_roi_align_fpn_ordered_nhwc": [_vp] * 8 + [_c_int] * 6 + [_vp, _c_int, _vp],
     "ai4e_crop_resize_nhwc": [_vp, _vp, _vp, _vp] + [_c_int] * 7 + [_vp],
     "ai4e_tile_stitch": [_vp, _vp, _vp] + [_c_int] * 10 + [_vp],
     "ai4e_groupnorm_finalize": [_vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_float, _c_int, _vp],

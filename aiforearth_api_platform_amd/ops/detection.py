@@ -368,11 +368,8 @@ def multiscale_roi_align(feats: Sequence[torch.Tensor], scales: Sequence[float],
 
 
 def roi_align_fpn(feats: Sequence[torch.Tensor], scales: Sequence[float], rois: torch.Tensor, out_hw=(7, 7),
-                  sampling: int = 2, aligned: bool = False, order: Optional[torch.Tensor] = None,
-                  xcd: bool = False) -> torch.Tensor:
-    """Multi-level RoIAlign over P2..P5 with in-kernel level assignment (static shapes, graph-safe). ``order``
-    (int32 [R], a permutation): the workgroups take the RoIs in that order (outputs stay in RoI order); ``xcd``: each
-    XCD takes a contiguous range of that order instead of every 8th workgroup."""
+                  sampling: int = 2, aligned: bool = False) -> torch.Tensor:
+    """Multi-level RoIAlign over P2..P5 with in-kernel level assignment (static shapes, graph-safe)."""
     if len(feats) != 4:
         raise ValueError("roi_align_fpn expects 4 levels (P2..P5)")
     if _ext.backend_for(feats[0]) == "hip":
@@ -383,13 +380,9 @@ def roi_align_fpn(feats: Sequence[torch.Tensor], scales: Sequence[float], rois: 
         sc = (ctypes.c_float * 4)(*[float(s) for s in scales])
         rois = rois.float().contiguous()
         out = torch.empty(R, out_hw[0], out_hw[1], C, device=feats[0].device, dtype=feats[0].dtype)
-        if order is not None:
-            order = order.to(torch.int32).contiguous()
-            if order.shape != (R,):
-                raise ValueError("order must be a permutation of the RoI rows")
-        _ext.call("ai4e_roi_align_fpn_ordered_nhwc", *[f.data_ptr() for f in feats], ctypes.addressof(hw),
-                  ctypes.addressof(sc), rois.data_ptr(), out.data_ptr(), C, R, out_hw[0], out_hw[1], sampling,
-                  int(aligned), None if order is None else order.data_ptr(), int(xcd), _ext.stream_ptr(feats[0].device))
+        _ext.call("ai4e_roi_align_fpn_nhwc", *[f.data_ptr() for f in feats], ctypes.addressof(hw), ctypes.addressof(sc),
+                  rois.data_ptr(), out.data_ptr(), C, R, out_hw[0], out_hw[1], sampling, int(aligned),
+                  _ext.stream_ptr(feats[0].device))
         return out
     return multiscale_roi_align(feats, scales, rois, out_hw, sampling)
 
