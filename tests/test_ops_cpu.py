@@ -142,3 +142,18 @@ def test_gpu_telemetry_fail_soft_and_summary():
     out = summarize([{"gfx_mhz": 2000.0, "power_w": 900.0}, {"gfx_mhz": 2400.0}])
     assert out["gfx_mhz"] == {"min": 2000.0, "mean": 2200.0, "max": 2400.0, "n": 2}
     assert out["power_w"]["n"] == 1
+
+
+def test_conv_head_cpu_fallback_matches_two_convs():
+    """``conv2d_head_nhwc`` (the RPN conv with its 16-channel head fused on the GPU's 256-wide tiles) falls back to the
+    two convs off the HIP backend; the result is the head of the ReLU'd conv, [N, H, W, 16]."""
+    from aiforearth_api_platform_amd.ops.conv import conv2d_head_nhwc, conv2d_nhwc, pack_conv
+
+    g = torch.Generator().manual_seed(3)
+    pc = pack_conv(torch.randn(256, 256, 3, 3, generator=g) * 0.02, torch.randn(256, generator=g) * 0.1, pad=1)
+    head = pack_conv(torch.randn(16, 256, 1, 1, generator=g) * 0.05, torch.randn(16, generator=g) * 0.1)
+    x = torch.randn(1, 6, 5, 256, generator=g)
+    y = conv2d_head_nhwc(x, pc, head, tile_cfg=6)
+    ref = conv2d_nhwc(conv2d_nhwc(x, pc, relu=True), head)
+    assert y.shape == (1, 6, 5, 16)
+    assert torch.equal(y, ref)
