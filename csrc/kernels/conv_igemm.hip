@@ -1060,148 +1060,6 @@ int launch(const ConvParams& p0, hipStream_t s) {
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
 }
 
-}  // namespace
-
-namespace {
-
-// ============================================================================================
-// K1w (tile config 11, round 5): 1x1 convs with a short K (C = 128 or 256: the FPN P2 lateral, the stride-2
-// downsamples into layer2), which the staged K1 schedules run at 2.6-3.3 TB/s — their K loop is 4-8 steps, too short
-// to hide a 2-tile staging prologue and the LDS epilogue of a one-workgroup-per-CU tile. Here the workgroup keeps a
-// 128-output-channel slice of the weights resident in LDS (C x 256 B: 32 / 64 KB, two workgroups per CU) and walks
-// 128-pixel tiles persistently; each wave loads its 32 pixels' activations straight into MFMA B-operand registers
-// (16 B per lane per K step, no LDS), each step of the next tile right after this tile's MFMAs of that step, and
-// stores its outputs from the
-// accumulators (bias, residual — also the nearest-2x half-resolution one — ReLU), so loads, MFMAs and stores of
-// consecutive tiles overlap inside each wave.
-// Weights in LDS: row n (C x 2 B), 16-B chunk c stored at chunk c ^ (n & 15): the 16 rows one MFMA A-operand read
-// takes at a fixed chunk land on 16 different 4-bank groups.
-template <int KS>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv1x1_wres_kernel(
-    const ConvParams p, int mtiles, int nslices) {
-  constexpr int ROWB = 64 * KS;  // bytes per weight row (K = 32 KS)
-  __shared__ __attribute__((aligned(16))) uint8_t wsm[128 * ROWB];
-  // per wave: one 16-pixel x 128-channel bf16 output block, turned from the accumulator layout (8 B per lane, 32-B
-  // pieces of 16 rows) into whole 256-B rows for the stores; 16-B chunk c of row r at chunk c ^ r
-  __shared__ __attribute__((aligned(16))) uint8_t ost[4][16 * 256];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  // the nslices workgroups of one pixel tile sit on the same XCD (block ids 8 apart), so the activations they each
-  // read meet in that XCD's L2; host: gridDim.x = step * nslices with step % 8 == 0
-  const int xcd = static_cast<int>(blockIdx.x) & 7, q = static_cast<int>(blockIdx.x) >> 3;
-  const int slice = q % nslices;
-  const int n0 = slice * 128;
-  const int step = static_cast<int>(gridDim.x) / nslices;
-  for (int e = tid; e < 128 * 4 * KS; e += 256) {
-    const int r = e / (4 * KS), c = e - r * (4 * KS);
-    *reinterpret_cast<uint4*>(wsm + r * ROWB + ((c ^ (r & 15)) << 4)) =
-        *reinterpret_cast<const uint4*>(p.w + static_cast<long>(n0 + r) * p.Kpad + 8 * c);
-  }
-  const int OHW = p.OH * p.OW;
-  // this lane's source row (16 B at channel 8 (lane >> 4)) of pixel block pb of tile mt; nullptr past M
-  auto src_of = [&](int mt, int pb) __attribute__((always_inline)) -> const uint16_t* {
-    const int m = mt * 128 + wave * 32 + pb * 16 + (lane & 15);
-    if (m >= p.M) return nullptr;
-    const int img = m / OHW, rem = m - img * OHW;
-    const int oh = rem / p.OW, ow = rem - oh * p.OW;
-    return p.x + (static_cast<long>(img) * p.H * p.W + static_cast<long>(oh * p.stride) * p.W + ow * p.stride) * p.ldx +
-           p.xcoff + 8 * (lane >> 4);
-  };
-  auto ld16 = [](const uint16_t* src, int ks) __attribute__((always_inline)) {
-    return src ? *reinterpret_cast<const uint4*>(src + 32 * ks) : make_uint4(0u, 0u, 0u, 0u);
-  };
-  int mt = (q / nslices) * 8 + xcd;
-  // one register set: K step ks of the next tile is loaded as soon as this tile's MFMAs of step ks are issued, so
-  // each load has the rest of the tile (its later steps and the epilogue) to land
-  uint4 a[2][KS];
-  if (mt < mtiles) {
-    const uint16_t* s0 = src_of(mt, 0);
-    const uint16_t* s1 = src_of(mt, 1);
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      a[0][ks] = ld16(s0, ks);
-      a[1][ks] = ld16(s1, ks);
-    }
-  }
-  __syncthreads();  // the weight slice is in LDS
-  for (; mt < mtiles; mt += step) {
-    const int mn = mt + step;
-    const uint16_t* s0 = mn < mtiles ? src_of(mn, 0) : nullptr;
-    const uint16_t* s1 = mn < mtiles ? src_of(mn, 1) : nullptr;
-    f32x4_t acc[2][8];
-#pragma unroll
-    for (int pb = 0; pb < 2; ++pb)
-#pragma unroll
-      for (int nb = 0; nb < 8; ++nb) acc[pb][nb] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-#pragma unroll
-      for (int nb = 0; nb < 8; ++nb) {
-        const int r = nb * 16 + (lane & 15), c = 4 * ks + (lane >> 4);
-        const bf16x8_t wf = *reinterpret_cast<const bf16x8_t*>(wsm + r * ROWB + ((c ^ (r & 15)) << 4));
-#pragma unroll
-        for (int pb = 0; pb < 2; ++pb)
-          acc[pb][nb] = mfma_16x16x32<false>(wf, __builtin_bit_cast(bf16x8_t, a[pb][ks]), acc[pb][nb]);
-      }
-      if (mn < mtiles) {
-        a[0][ks] = ld16(s0, ks);
-        a[1][ks] = ld16(s1, ks);
-      }
-      // one K step at a time: hoisting every step's weight fragments ahead (8 x 32 VGPRs) spilled
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    // lane: pixel (lane & 15) of each 16-pixel block, output channels n0 + 16 nb + 4 (lane >> 4) + 0..3
-#pragma unroll
-    for (int pb = 0; pb < 2; ++pb) {
-      const int m = min(mt * 128 + wave * 32 + pb * 16 + (lane & 15), p.M - 1);  // rows past M: computed, not stored
-      const long rrow = p.res ? res_row(p, m) * p.ldres : 0;
-#pragma unroll
-      for (int nb = 0; nb < 8; ++nb) {
-        const int n = n0 + 16 * nb + 4 * (lane >> 4);
-        const float4 b = *reinterpret_cast<const float4*>(p.bias + n);
-        float f0 = acc[pb][nb][0] + b.x, f1 = acc[pb][nb][1] + b.y, f2 = acc[pb][nb][2] + b.z, f3 = acc[pb][nb][3] + b.w;
-        if (p.res) {
-          const uint2 rv = *reinterpret_cast<const uint2*>(p.res + rrow + n);
-          f0 = add_bf16_lo(rv.x, f0); f1 = add_bf16_hi(rv.x, f1);
-          f2 = add_bf16_lo(rv.y, f2); f3 = add_bf16_hi(rv.y, f3);
-        }
-        uint2 o = make_uint2(cvt_bf16x2(f0, f1), cvt_bf16x2(f2, f3));
-        if (p.relu & 1) {
-          o.x = relu_bf16x2(o.x);
-          o.y = relu_bf16x2(o.y);
-        }
-        const int pr = lane & 15;
-        *reinterpret_cast<uint2*>(ost[wave] + pr * 256 + (((2 * nb + (lane >> 5)) ^ pr) << 4) + ((lane >> 4) & 1) * 8) = o;
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int pr = 4 * i + (lane >> 4), ch = lane & 15;
-        const uint4 v = *reinterpret_cast<const uint4*>(ost[wave] + pr * 256 + ((ch ^ pr) << 4));
-        const int mo = mt * 128 + wave * 32 + pb * 16 + pr;
-        if (mo < p.M) *reinterpret_cast<uint4*>(p.y + static_cast<long>(mo) * p.ldy + p.ycoff + n0 + 8 * ch) = v;
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    }
-  }
-}
-
-template <int KS>
-int launch_wres(const ConvParams& p, hipStream_t s) {
-  const int mtiles = ai4e_cdiv(p.M, 128);
-  const int nslices = p.Kout / 128;
-  int dev = 0, cus = 256;
-  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-    cus = 256;
-  // about two resident workgroups per CU; per slice a multiple of 8 (whole XCD rounds, see the kernel)
-  long per_slice = (2L * cus) / nslices / 8 * 8;
-  if (per_slice < 8) per_slice = 8;
-  if (per_slice > ai4e_cdiv(mtiles, 8) * 8L) per_slice = ai4e_cdiv(mtiles, 8) * 8L;
-  const long grid = per_slice * nslices;
-  hipLaunchKernelGGL((conv1x1_wres_kernel<KS>), dim3(static_cast<unsigned>(grid)), dim3(256), 0, s, p, mtiles, nslices);
-  return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
-}
-
 template <int BM, bool F16 = false, bool PH3 = false>
 int launch256(const ConvParams& p0, hipStream_t s) {
   ConvParams p = p0;
@@ -1290,13 +1148,6 @@ int conv2d_impl(const void* x, const void* w, const void* bias, const void* res,
     case 8: return launch<4, 1, 3, 3, F16>(p, stream);
     case 9: return launch256<192, F16>(p, stream);
     case 10: return launch256<192, F16, true>(p, stream);
-    case 11:
-      // K1w: bf16 1x1 / pad 0 with C = 128 or 256 channels read from the input row (no channel slice beyond ldx),
-      // output channels in whole 128-channel slices, 8-B output and residual rows
-      if (F16 || p.KH != 1 || p.KW != 1 || p.pad || (p.C != 128 && p.C != 256) || p.Kout % 128 || p.ldy % 4 ||
-          p.ycoff % 8 || p.ldy % 8 || (p.res && p.ldres % 4) || p.gnp || p.hy)
-        return AI4E_EINVAL;
-      return p.C == 256 ? launch_wres<8>(p, stream) : launch_wres<4>(p, stream);
     default: return AI4E_EINVAL;
   }
 }

@@ -507,34 +507,3 @@ def test_conv_fused_rpn_head_matches_two_convs(cfg, shape):
     err = (fused.float() - ref).abs().max().item()
     assert err <= 2e-2 * ref.abs().max().item() + 1e-2, err
 
-
-@pytest.mark.parametrize("n,h,w,c,k,stride,res", [(2, 20, 20, 256, 256, 1, "up2"), (3, 14, 14, 256, 512, 2, None),
-                                                  (1, 9, 7, 128, 128, 1, "full"), (2, 16, 16, 256, 384, 1, None)])
-def test_conv1x1_weights_resident_matches_reference(n, h, w, c, k, stride, res):
-    """K1w (tile config 11: short-K 1x1 with the weight slice resident in LDS, activations straight into MFMA
-    registers) against K1 config 1 and fp32 PyTorch; the third shape's M is not a multiple of the 128-pixel tile."""
-    from aiforearth_api_platform_amd.ops.conv import conv2d_nhwc, pack_conv
-
-    g = torch.Generator().manual_seed(c + k + h)
-    pc = pack_conv(torch.randn(k, c, 1, 1, generator=g) / c ** 0.5, torch.randn(k, generator=g) * 0.1,
-                   stride=stride).to(DEV)
-    x = torch.randn(n, h, w, c, generator=g).to(DEV, torch.bfloat16)
-    oh, ow = pc.out_hw(h, w)
-    r = None
-    if res == "up2":
-        r = torch.randn(n, oh // 2, ow // 2, k, generator=g).to(DEV, torch.bfloat16)
-    elif res == "full":
-        r = torch.randn(n, oh, ow, k, generator=g).to(DEV, torch.bfloat16)
-    y = conv2d_nhwc(x, pc, residual=r, relu=True, tile_cfg=11, residual_up2=res == "up2")
-    y1 = conv2d_nhwc(x, pc, residual=r, relu=True, tile_cfg=1, residual_up2=res == "up2")
-    torch.cuda.synchronize()
-    wq = pc.w_packed[:k, :c].float()
-    ref = F.conv2d(x.float().permute(0, 3, 1, 2), wq[:, :, None, None], pc.bias[:k], stride=stride)
-    if r is not None:
-        rr = r.float().permute(0, 3, 1, 2)
-        if res == "up2":
-            rr = rr.repeat_interleave(2, dim=2).repeat_interleave(2, dim=3)
-        ref = ref + rr
-    ref = F.relu(ref).permute(0, 2, 3, 1)
-    assert (y.float() - y1.float()).abs().max().item() <= 1e-2 * ref.abs().max().item() + 1e-2
-    assert (y.float() - ref).abs().max().item() <= 1e-2 * ref.abs().max().item() + 1e-2
