@@ -22,11 +22,11 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import torch
 import torch.nn as nn
 
-from ..ops.conv import PackedConv, conv2d_head_nhwc, conv2d_nhwc, pack_conv
+from ..ops.conv import conv2d_head_nhwc, conv2d_nhwc, pack_conv
 from ..ops.debug import crumb
 from ..ops.detection import (det_decode, gather_keep, nms_batched_sorted, roi_align_fpn, rpn_decode_into, rpn_topk,
                               sort_select)
-from ..ops.pool import maxpool2d_nhwc, preprocess_s2d_u8, preprocess_u8
+from ..ops.pool import maxpool2d_nhwc, preprocess_s2d_u8
 from .resnet import FusedResNet, resnet50
 
 MEGADETECTOR_CLASSES = ("background", "animal", "person", "vehicle")

@@ -22,8 +22,7 @@ import torch.nn.functional as F
 from ..ops.conv import (PackedConv, chain_supported, conv2d_nhwc, conv_chain, fold_bn, pack_conv, pack_stem_s2d,
                         pair_route, pair_supported, stem_pool, stem_pool_c1)
 from ..ops.head import softmax_topk
-from ..ops.pool import (global_avgpool_nhwc, maxpool2d_nhwc, preprocess_s2d_u8, preprocess_u8,
-                        space_to_depth_shifted)
+from ..ops.pool import global_avgpool_nhwc, maxpool2d_nhwc, preprocess_s2d_u8, space_to_depth_shifted
 
 
 class Bottleneck(nn.Module):

@@ -18,13 +18,13 @@ from __future__ import annotations
 
 import os
 
-from typing import List, Optional, Tuple
+from typing import List, Optional
 
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ..ops.conv import PackedConv, conv2d_gn_nhwc, conv2d_nhwc, conv3x3_tile64, pack_conv, tile64_supported
+from ..ops.conv import conv2d_gn_nhwc, conv2d_nhwc, conv3x3_tile64, pack_conv, tile64_supported
 from ..ops.norm import (gn_relu_head8, gn_relu_head8_supported, group_norm_affine, group_norm_nhwc,
                         upsample2x_nhwc)
 from ..ops.pool import maxpool2d_nhwc, preprocess_u8

@@ -9,7 +9,6 @@ permission, the summary is simply empty.
 from __future__ import annotations
 
 import threading
-import time
 from typing import Dict, List, Optional
 
 

@@ -22,7 +22,6 @@ import json
 import os
 import socket
 import sys
-import threading
 import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))

@@ -1,7 +1,6 @@
 """APIService decorator API on a Flask app: sync/async semantics, admission control, drain, tasks."""
 import json
 import threading
-import time
 
 import pytest
 from flask import Flask

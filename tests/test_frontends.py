@@ -119,7 +119,8 @@ def test_public_port_taken_back_when_frontends_exit():
         assert ok, "the serving process did not take the public port back"
         img = np.zeros((4, 4, 3), np.uint8)
         r = s.post(base + "/v1/tiny/async", data=img.tobytes(), headers={"Content-Type": "application/octet-stream"})
-        assert r.status_code == 200 and r.json()["BackendStatus"] == "created"
+        # the task record comes back as soon as it is queued; a fast worker may already have it running
+        assert r.status_code == 200 and r.json()["BackendStatus"] in ("created", "running", "completed")
     finally:
         proc.terminate()
         try:

@@ -2,7 +2,6 @@
 import asyncio
 import io
 import json
-import time
 
 import numpy as np
 import pytest

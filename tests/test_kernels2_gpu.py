@@ -1,5 +1,4 @@
 """HIP kernels K2-K6 vs the PyTorch references (GPU box only)."""
-import os
 
 import pytest
 import torch

@@ -1,7 +1,6 @@
 """Restart recovery from the journal, and the legacy Containers/ task-manager surface."""
 import json
 
-import pytest
 from flask import Flask
 
 from aiforearth_api_platform_amd.api import InProcTaskClient, TaskManager

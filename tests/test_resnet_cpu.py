@@ -2,7 +2,7 @@
 import torch
 import torch.nn.functional as F
 
-from aiforearth_api_platform_amd.models.resnet import FusedResNet, ResNet, randomize_bn_, resnet50
+from aiforearth_api_platform_amd.models.resnet import FusedResNet, resnet50
 from aiforearth_api_platform_amd.ops.conv import conv2d_nhwc, pack_conv
 from aiforearth_api_platform_amd.ops.pool import preprocess_u8
 

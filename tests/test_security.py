@@ -5,7 +5,6 @@ process accepts the connection)."""
 import asyncio
 import json
 import os
-import ssl
 import subprocess
 import sys
 import time

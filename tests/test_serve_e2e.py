@@ -1,5 +1,4 @@
 """End-to-end: launch the platform CLI (CPU config) as a process, drive it over real HTTP."""
-import json
 import os
 import socket
 import subprocess

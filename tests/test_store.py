@@ -2,7 +2,6 @@
 import json
 import time
 
-import pytest
 
 from aiforearth_api_platform_amd.store import make_queue, make_store, pystore
 
