@@ -78,9 +78,10 @@ class Config:
     # "native": the C++ front-end (csrc/ingest/ingestd.cpp: bodies recv()'d straight into ring slots);
     # "python": runtime/frontend.py (aiohttp). TLS listeners always use the Python front-ends.
     frontend_impl: str = field(default="native", metadata={"env": "AI4E_FRONTEND_IMPL"})
-    # latency budget of an ingested request's queue wait at the front-ends: a request whose projected wait
-    # (slots in use + its own / the partition's service rate) exceeds it is answered 429 + Retry-After (0 = off)
-    max_queue_ms: float = field(default=0.0, metadata={"env": "AI4E_MAX_QUEUE_MS"})
+    # latency budget of an ingested request's queue wait at the native front-ends: a request whose projected wait
+    # (the shard's unfinished tasks + bodies uploading + its own, over the shard's measured capacity) exceeds it is
+    # answered 429 + Retry-After (0 = off: requests queue until the ring partition is full)
+    max_queue_ms: float = field(default=15.0, metadata={"env": "AI4E_MAX_QUEUE_MS"})
     # control-plane shards per pool endpoint (one node scheduler + dispatch queue + ring partition each);
     # 0 = one per GPU (worker group), 1 = one scheduler for all of the endpoint's GPUs
     control_plane_shards: int = field(default=0, metadata={"env": "AI4E_CONTROL_PLANE_SHARDS"})

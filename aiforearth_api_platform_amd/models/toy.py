@@ -28,3 +28,19 @@ def tiny_classifier(device="cpu", **kw):
 def echo(task_id: str, body: bytes, headers=None):
     """Sync echo backend (BASELINE config #1: plumbing, no GPU)."""
     return 200, body
+
+
+class NullClassifier:
+    """logits = zeros (never reads the pixels): a worker that costs nothing, so an ingest benchmark on CPU measures
+    the front door alone (runtime/node_bench.py ingest probes)."""
+
+    def __init__(self, device="cpu", classes: int = 4):
+        self.device = torch.device(device)
+        self.classes = classes
+
+    def __call__(self, x_u8: torch.Tensor) -> torch.Tensor:
+        return torch.zeros(x_u8.shape[0], self.classes, device=x_u8.device)
+
+
+def null_classifier(device="cpu", **kw):
+    return NullClassifier(device, **kw)

@@ -77,7 +77,13 @@ def attach_ring(shm_name: str, nslots: int, item_shape: Sequence[int], untrack: 
     share the owner's tracker and must not."""
     from multiprocessing import resource_tracker, shared_memory
 
-    shm = shared_memory.SharedMemory(name=shm_name)
+    if shm_name.startswith("ai4ej_"):  # a durable ring outlives a crash: never tracked (runtime/durable_ring.py)
+        from .durable_ring import open_untracked
+
+        shm = open_untracked(shm_name)
+        untrack = False
+    else:
+        shm = shared_memory.SharedMemory(name=shm_name)
     if untrack:
         try:
             resource_tracker.unregister(shm._name, "shared_memory")  # type: ignore[attr-defined]

@@ -78,6 +78,12 @@ class ModelEndpoint:
         """The dispatch queue that serves a payload in ``slot`` (a GPU-sharded pool: the owning shard's)."""
         return self.worker.queue_for_slot(slot) if self.is_pool else self.queue
 
+    def _send_existing(self, tid: str, slot: int) -> bool:
+        """Queue an existing task record (through the pool's scheduler, so the shard's load counters see it)."""
+        if self.is_pool and hasattr(self.worker, "send_existing"):
+            return self.worker.send_existing(tid, slot)
+        return self._queue(slot).send(tid, slot, "")
+
     def _enqueue(self, slots: List[int], trace: str = "") -> List[str]:
         if self.is_pool:
             return self.worker.submit_slots(slots, trace)
@@ -122,7 +128,7 @@ class ModelEndpoint:
                 self.cp.store.set_trace(tid, trace)
             if on_done is not None:
                 self._add_waiter(tid, on_done)
-            if not self._queue(slot).send(tid, slot, ""):
+            if not self._send_existing(tid, slot):
                 self.ring.free([slot])
                 serialized, _ = self.cp.store.upsert(tid, PUBLISH_FAILED, STATE_FAILED, self.endpoint, None, True)
                 self._fire(tid)
@@ -177,8 +183,9 @@ class ModelEndpoint:
         if nbytes <= 0 or nbytes % item:
             raise PayloadError(f"batch payload must be a multiple of {item} bytes (uint8 {self.item_shape})")
         n = nbytes // item
-        if n > self.ring.nslots:
-            raise PayloadError(f"batch of {n} items exceeds the payload ring ({self.ring.nslots} slots)", 413)
+        cap = int(getattr(self.ring, "max_alloc", self.ring.nslots))  # (one allocation: one shard's partition)
+        if n > cap:
+            raise PayloadError(f"batch of {n} items exceeds the payload ring partition ({cap} slots)", 413)
         return StreamedBatch(self, n, item, trace)
 
     def _orig(self, body: bytes, content_type: str) -> Optional[str]:
@@ -187,20 +194,27 @@ class ModelEndpoint:
         return _ORIG_PREFIX + (content_type or "") + ";" + base64.b64encode(body).decode()
 
     def replay(self, task_id: str, orig: Optional[str]) -> bool:
-        """Restart recovery of one unfinished task: re-ingest its journaled payload, or fail it."""
+        """Restart recovery of one unfinished task: re-ingest its journaled payload (the ``_ORIG`` body of the
+        gateway path, or the slot of the previous crash-surviving ring the native ingest path wrote it to), or fail
+        it with a reason."""
         if not orig or not orig.startswith(_ORIG_PREFIX):
-            self.cp.store.upsert(task_id, PAYLOAD_LOST, STATE_FAILED, self.endpoint, None, True)
-            return False
-        ct, b64 = orig[len(_ORIG_PREFIX):].split(";", 1)
-        try:
-            arr = self.decode(base64.b64decode(b64), ct)
-        except PayloadError:
-            self.cp.store.upsert(task_id, "Task failed - invalid payload", STATE_FAILED, self.endpoint, None, True)
-            return False
+            durable = getattr(self.worker, "durable", None) if self.is_pool else None
+            arr = durable.payload(task_id) if durable is not None else None
+            if arr is None:
+                self.cp.store.upsert(task_id, PAYLOAD_LOST, STATE_FAILED, self.endpoint, None, True)
+                return False
+        else:
+            ct, b64 = orig[len(_ORIG_PREFIX):].split(";", 1)
+            try:
+                arr = self.decode(base64.b64decode(b64), ct)
+            except PayloadError:
+                self.cp.store.upsert(task_id, "Task failed - invalid payload", STATE_FAILED, self.endpoint, None,
+                                     True)
+                return False
         slot = self.ring.alloc(1, timeout=30)[0]
         self._write([slot], arr[None])
         self.cp.store.upsert(task_id, "created - requeued after restart", STATE_CREATED, self.endpoint, None, True)
-        if not self._queue(slot).send(task_id, slot, ""):
+        if not self._send_existing(task_id, slot):
             self.ring.free([slot])
             self.cp.store.upsert(task_id, PUBLISH_FAILED, STATE_FAILED, self.endpoint, None, True)
             return False
@@ -238,6 +252,13 @@ class ModelEndpoint:
     def start(self) -> "ModelEndpoint":
         self.worker.start()
         return self
+
+    def finish_recovery(self) -> None:
+        """Restart recovery (``ControlPlane.recover``) has re-ingested what it could: drop the previous generation of
+        the crash-surviving ring."""
+        durable = getattr(self.worker, "durable", None) if self.is_pool else None
+        if durable is not None:
+            durable.release_previous()
 
     def stop(self) -> None:
         if self.decode_pool is not None:

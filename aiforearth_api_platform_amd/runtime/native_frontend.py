@@ -94,7 +94,7 @@ def spawn_native_frontends(n: int, pools: Dict[str, object], routes: List[dict],
     procs, readies = [], []
     for i in range(n):
         lines = [f"listen {_token(host)} {int(port)}", f"internal {_token(ihost)} {int(iport)}",
-                 f"ack_timeout {float(ack_timeout_s)}"]
+                 f"ack_timeout {float(ack_timeout_s)}", f"frontend_index {i}"]
         if max_queue_ms and max_queue_ms > 0:
             lines.append(f"max_queue_ms {float(max_queue_ms)}")
         lines += [f"key {_token(k)}" for k in sec.get("keys") or []]

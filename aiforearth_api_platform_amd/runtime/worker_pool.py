@@ -14,6 +14,11 @@ Failure handling (survey §5.3): a worker that exits, or whose heartbeat stops f
 bounded by the queue's max delivery count -> task failed with a reason) and is restarted up to
 ``max_restarts`` times. ``resize(n)`` grows or shrinks the active GPU set without losing queued
 tasks; :class:`runtime.autoscale.QueueDepthAutoscaler` drives it from queue depth (the HPA analogue).
+In a :class:`ShardedWorkerPool` the shards' schedulers are competing consumers of each other's queues
+(``NodeScheduler.set_peers``): a shard left without a live worker (restarts exhausted, or resized to zero) has its
+queue drained by the others, and an idle shard helps a peer holding more than a full batch — any live GPU
+finishes any queued task, as every replica of the reference consumes the one Service Bus queue
+(``ProcessManager/BackendQueueProcessor/BackendQueueProcessor.cs:54-64``, ``host.json:3-11``).
 Fault injection: ``AI4E_FAULT_INJECTION`` (see :mod:`runtime.gpu_worker`).
 """
 from __future__ import annotations
@@ -48,17 +53,29 @@ class SharedPayloadRing:
     """The node's payload ring in POSIX shared memory + the native slot allocator of this process's
     ingest partition ``[0, local_slots)``; slots beyond belong to remote ingest shards."""
 
-    def __init__(self, nslots: int, item_shape: Sequence[int], local_slots: Optional[int] = None):
+    def __init__(self, nslots: int, item_shape: Sequence[int], local_slots: Optional[int] = None, durable=None):
+        """``durable``: a :class:`runtime.durable_ring.DurableRing` (a task journal is configured): the ring is a
+        crash-surviving segment with a per-slot task-id tag segment (``tags_name``) the schedulers write."""
         self.nslots = int(nslots)
         self.item_shape = tuple(int(x) for x in item_shape)
         nbytes = self.nslots * int(np.prod(self.item_shape))
-        self.shm = shared_memory.SharedMemory(create=True, size=max(nbytes, 1))
+        self.durable = durable
+        self.tags_name = ""
+        if durable is not None:
+            self.shm, self.tags_name = durable.create(self.nslots, self.item_shape)
+        else:
+            self.shm = shared_memory.SharedMemory(create=True, size=max(nbytes, 1))
         self.buf = torch.frombuffer(self.shm.buf, dtype=torch.uint8, count=nbytes).view(self.nslots, *self.item_shape)
         self.slots = native.SlotRing(int(local_slots or self.nslots), 0)
 
     @property
     def name(self) -> str:
         return self.shm.name
+
+    @property
+    def max_alloc(self) -> int:
+        """The largest batch one allocation can hold (this process's ingest partition)."""
+        return int(self.slots.capacity)
 
     def alloc(self, n: int, timeout: Optional[float] = None) -> List[int]:
         s = self.slots.alloc(int(n), -1.0 if timeout is None else float(timeout))
@@ -83,8 +100,11 @@ class SharedPayloadRing:
     def close(self) -> None:
         self.slots.close()
         del self.buf
+        self.shm.close()
+        if self.durable is not None:  # (its segments are unknown to the resource tracker)
+            self.durable.close()
+            return
         try:
-            self.shm.close()
             self.shm.unlink()
         except FileNotFoundError:
             pass
@@ -109,6 +129,7 @@ class RingPartition:
 
     alloc = SharedPayloadRing.alloc
     free = SharedPayloadRing.free
+    max_alloc = SharedPayloadRing.max_alloc
     write = SharedPayloadRing.write
 
     def close(self) -> None:  # (the owner of the shared memory closes it)
@@ -145,13 +166,34 @@ class _WorkerHandle:
 FRONTEND_RANK0 = 1 << 20  # scheduler connection ids of ingest front-ends (GPU worker ranks stay below)
 
 
+def _sweep_stale_stats() -> None:
+    """Unlink shard-counter segments (``ai4e_stat_<pid>_*``) left behind by serving processes that were killed."""
+    try:
+        names = os.listdir("/dev/shm")
+    except OSError:
+        return
+    for n in names:
+        if not n.startswith("ai4e_stat_"):
+            continue
+        try:
+            pid = int(n.split("_")[2])
+            os.kill(pid, 0)
+        except ProcessLookupError:
+            try:
+                os.unlink(os.path.join("/dev/shm", n))
+            except OSError:
+                pass
+        except (ValueError, IndexError, PermissionError):
+            pass
+
+
 class WorkerPool:
     def __init__(self, control_plane, endpoint: str, spec: ModelSpec, devices: Sequence[str], ring_slots: int = 0,
                  max_delay_s: float = 0.0005, heartbeat_interval_s: float = 0.5, heartbeat_timeout_s: float = 10.0,
                  max_restarts: int = 2, pipeline_depth: int = 3, retry_delay_s: float = 1.0,
                  remote_partitions: Sequence[Tuple[int, int, int]] = (), completion_feed: bool = False,
                  poll_s: float = 0.02, frontends: int = 0, frontend_slots: int = 0,
-                 shard: Optional["ShardLayout"] = None):
+                 shard: Optional["ShardLayout"] = None, durable=None):
         """``shard``: this pool is one control-plane shard of a :class:`ShardedWorkerPool` (its own dispatch queue
         and scheduler, a partition of the shared ring, ids minted in its own task-store lock domains)."""
         if native is None:
@@ -185,16 +227,20 @@ class WorkerPool:
             self.frontend_partitions = [(end + i * fs, fs, FRONTEND_RANK0 + i) for i in range(int(frontends))]
             self.remote_partitions += self.frontend_partitions
             total = max([local] + [b + n for b, n, _ in self.remote_partitions])
-            self.ring = SharedPayloadRing(total, spec.item_shape, local_slots=local)
+            self.ring = SharedPayloadRing(total, spec.item_shape, local_slots=local, durable=durable)
         self.hb_interval = heartbeat_interval_s
         self.max_restarts = max_restarts
         self.sched = native.NodeScheduler(self.store, self.queue, endpoint, total, max_batch=spec.max_batch,
                                           linger_s=max_delay_s, depth=pipeline_depth, retry_delay_s=retry_delay_s,
                                           hb_timeout_s=heartbeat_timeout_s, poll_s=poll_s)
         self.sched.add_local_ring(self.ring.slots)
+        tags = getattr(getattr(self.ring, "parent", self.ring), "tags_name", "")
+        if tags and not self.sched.set_slot_tags(tags):
+            raise RuntimeError(f"cannot map the payload ring's tag segment {tags}")
         # shard load (tasks queued / finished) in shm for the native front-ends' admission (unlinked with the scheduler)
         self.stat_name = ""
         if int(frontends) > 0 and hasattr(self.sched, "open_stat"):
+            _sweep_stale_stats()
             name = f"ai4e_stat_{os.getpid()}_{id(self):x}"
             self.stat_name = name if self.sched.open_stat(name) else ""
         if shard is not None:
@@ -389,6 +435,8 @@ class WorkerPool:
             if not w.stop.is_set():
                 w.stop.set()
         self.sched.stop()
+        if self.stat_name:
+            self.sched.unlink_stat()
         for w in self.workers:
             if w.proc is not None:
                 w.proc.join(30)
@@ -405,10 +453,19 @@ class WorkerPool:
     def submit_slots(self, slots: Sequence[int], trace: str = "") -> List[str]:
         return self.sched.submit(list(slots), trace)
 
+    def send_existing(self, task_id: str, slot: int) -> bool:
+        """Queue a task whose record already exists (explicit TaskId, journal replay) for the payload in ``slot``."""
+        return self.sched.send_existing([task_id], [int(slot)]) == 1
+
     @property
     def control_shards(self) -> List["WorkerPool"]:
         """The scheduler shards behind this endpoint (ingest front-ends attach to each): just this pool."""
         return [self]
+
+    @property
+    def durable(self):
+        """The crash-surviving ring (:class:`runtime.durable_ring.DurableRing`) when a journal is configured."""
+        return getattr(getattr(self.ring, "parent", self.ring), "durable", None)
 
     def queue_for_slot(self, slot: int):
         return self.queue
@@ -527,6 +584,10 @@ class _ShardedRing:
         live = [p for p in order if p.active()] or order
         return min(live, key=lambda p: p.ring.slots.used() / max(1, p.ring.length))
 
+    @property
+    def max_alloc(self) -> int:
+        return max(p.ring.length for p in self.pools)
+
     def owner(self, slot: int) -> "WorkerPool":
         for p in self.pools:
             if p.ring.base <= slot < p.ring.base + p.ring.length:
@@ -589,7 +650,7 @@ class ShardedWorkerPool:
 
     def __init__(self, control_plane, endpoint: str, spec: ModelSpec, devices: Sequence[str], shards: int = 0,
                  ring_slots: int = 0, frontends: int = 0, frontend_slots: int = 0, pipeline_depth: int = 3,
-                 remote: Sequence[int] = (), remote_slots: int = 0, **kw):
+                 remote: Sequence[int] = (), remote_slots: int = 0, durable=None, **kw):
         """``remote``: shards whose worker is a process started elsewhere (a torchrun rank of the multi-GPU bench) that
         attaches with ``control_shards[i].attach_remote(i, conn)`` and ingests into its own ``remote_slots`` partition
         (``remote_partition(i)``); nothing is spawned for those shards."""
@@ -627,7 +688,7 @@ class ShardedWorkerPool:
                 parts.append((base, fs, FRONTEND_RANK0 + f))
                 base += fs
             layout[i].append(parts)
-        self._ring = SharedPayloadRing(base, spec.item_shape, local_slots=1)
+        self._ring = SharedPayloadRing(base, spec.item_shape, local_slots=1, durable=durable)
         self.pools: List[WorkerPool] = []
         for i in range(K):
             lay = ShardLayout(i, self._ring, layout[i][0], layout[i][1], [s for s in range(nstore) if s % K == i],
@@ -636,6 +697,15 @@ class ShardedWorkerPool:
                                          frontends=frontends, frontend_slots=fs, shard=lay, **kw))
         self.ring = _ShardedRing(self._ring, self.pools)
         self.queue = _QueueStats(self.pools)
+        # one waiter table for every shard: a task's completion may come from any shard's scheduler (a stolen batch,
+        # or a task created outside its shard's lock domains), and each shard's feed loop drains into the same table
+        self._waiters: Dict[str, Callable[[str], None]] = {}
+        self._wmu = threading.Lock()
+        for p in self.pools:
+            p._waiters, p._wmu = self._waiters, self._wmu
+        scheds = [p.sched for p in self.pools]
+        for p in self.pools:
+            p.sched.set_peers(scheds)
 
     # ------------------------------------------------------------ lifecycle
     def start(self, wait_ready_s: float = 600.0) -> "ShardedWorkerPool":
@@ -660,11 +730,16 @@ class ShardedWorkerPool:
         return sum(p.active() for p in self.pools)
 
     def resize(self, n: int, devices: Optional[Sequence[str]] = None) -> None:
-        """Elastic: n workers spread over the shards, never below one per shard (a shard's queued tasks need one)."""
-        K = len(self.pools)
-        n = max(K, int(n))
-        for i, p in enumerate(self.pools):
-            p.resize(n // K + (1 if i < n % K else 0))
+        """Elastic: n local workers spread over the shards that have local devices (a remote shard's worker is a
+        torchrun rank, not ours to spawn or retire). A shard resized to zero keeps its queue and ring partition; the
+        live shards drain it (competing consumers) and new ingest skips it."""
+        local = [p for i, p in enumerate(self.pools) if i not in self.remote and p.devices]
+        if not local:
+            return
+        n = max(0, int(n))
+        k = len(local)
+        for i, p in enumerate(local):
+            p.resize(n // k + (1 if i < n % k else 0))
 
     @property
     def workers(self) -> list:
@@ -677,6 +752,10 @@ class ShardedWorkerPool:
     @property
     def control_shards(self) -> List[WorkerPool]:
         return list(self.pools)
+
+    @property
+    def durable(self):
+        return self._ring.durable
 
     def remote_partition(self, shard: int) -> Tuple[int, int, int]:
         """(base, length, rank) of a remote shard's ingest partition of the shared ring."""
@@ -710,16 +789,15 @@ class ShardedWorkerPool:
         return self.pools[self.cp.store.shard_index(task_id) % len(self.pools)]
 
     def add_waiter(self, task_id: str, cb: Callable[[str], None]) -> None:
-        self._owner_of(task_id).add_waiter(task_id, cb)
+        with self._wmu:
+            self._waiters[task_id] = cb
 
     def pop_waiter(self, task_id: str) -> Optional[Callable[[str], None]]:
-        cb = self._owner_of(task_id).pop_waiter(task_id)
-        if cb is None:  # (a task created outside its shard's lock domains: the explicit-TaskId upsert path)
-            for p in self.pools:
-                cb = p.pop_waiter(task_id)
-                if cb is not None:
-                    break
-        return cb
+        with self._wmu:
+            return self._waiters.pop(task_id, None)
+
+    def send_existing(self, task_id: str, slot: int) -> bool:
+        return self.ring.owner(int(slot)).send_existing(task_id, slot)
 
     def refresh(self) -> None:
         for p in self.pools:
@@ -747,5 +825,7 @@ class ShardedWorkerPool:
         return {"workers": [dict(w, shard=i) for i, s in enumerate(per) for w in s["workers"]],
                 "batch_histogram": [sum(h[i] for h in hists if i < len(h)) for i in range(max(map(len, hists)))],
                 "images": self.images, "control_plane_shards": len(self.pools),
+                "live_workers_per_shard": [p.sched.live_workers() for p in self.pools],
+                "stolen_items": sum(p.sched.stolen_items() for p in self.pools),
                 "ring": {"slots": self._ring.nslots, "local_used": sum(s["ring"]["local_used"] for s in per)}}
 

@@ -49,9 +49,9 @@ from .runtime.frontend import open_listeners  # noqa: E402  (re-exported for the
 
 
 def frontend_count(cfg: Config) -> int:
-    """Ingest front-end processes to run (none while payloads are journaled: the journal is written by the
-    serving process's store, so those endpoints must ingest there)."""
-    return 0 if cfg.journal_path else max(0, int(cfg.frontend_processes))
+    """Ingest front-end processes to run. With a task journal, the payloads they ingest stay durable in the
+    crash-surviving ring of each pool endpoint (runtime/durable_ring.py)."""
+    return max(0, int(cfg.frontend_processes))
 
 
 def start_frontends(cfg: Config, doc: Dict[str, Any], endpoints: Dict[str, Any], port: int, internal_port: int):
@@ -150,6 +150,10 @@ def build_platform(doc: Dict[str, Any], cfg: Config):
                       frontends=frontend_count(cfg),
                       frontend_slots=int(e.get("frontend_ring_slots", cfg.frontend_ring_slots)))
             nshards = control_plane_shards(cfg, e, spec, devs)
+            if cfg.journal_path:  # payloads survive a crash in the ring itself (any ingest path)
+                from .runtime.durable_ring import DurableRing
+
+                kw["durable"] = DurableRing(cfg.journal_path, e["path"])
             # the control plane scales with the GPUs: one scheduler shard per GPU (worker group) by default
             pool = (ShardedWorkerPool(cp, base_url + e["path"], spec, devs, shards=nshards, **kw) if nshards > 1
                     else WorkerPool(cp, base_url + e["path"], spec, devs, **kw))
@@ -208,10 +212,13 @@ def main(argv=None) -> int:
                       transport=args.transport)
     set_config(cfg)
     cp, gw, endpoints, dispatchers = build_platform(doc, cfg)
+    for ep in endpoints.values():  # (workers first: a recovery larger than the ring drains while it re-ingests)
+        ep.start()
     if cfg.journal_path and os.path.exists(cfg.journal_path):
         print(f"recovered from journal: {cp.recover(cfg.journal_path)}", file=sys.stderr, flush=True)
     for ep in endpoints.values():
-        ep.start()
+        if hasattr(ep, "finish_recovery"):
+            ep.finish_recovery()
     for d in dispatchers:
         d.start()
     cp.start_metric_timers()

@@ -161,6 +161,7 @@ PYBIND11_MODULE(_ai4e_core, m) {
            py::arg("max_finished") = static_cast<size_t>(SIZE_MAX), py::call_guard<py::gil_scoped_release>())
       .def("size", &TaskStore::size)
       .def("flush", &TaskStore::flush)
+      .def("journaled", &TaskStore::journaled)
       .def("replay", [](TaskStore& s, const std::string& path) {
         py::module_ json = py::module_::import("json");
         return s.replay(path, [&](const std::string& line, TaskStore::JournalLine& jl) {
@@ -321,5 +322,14 @@ PYBIND11_MODULE(_ai4e_core, m) {
       .def("batch_histogram", &NodeScheduler::batch_histogram)
       .def("images_done", &NodeScheduler::images_done)
       .def("open_stat", &NodeScheduler::open_stat)
+      .def("stat_counters", &NodeScheduler::stat_counters)
+      .def("unlink_stat", &NodeScheduler::unlink_stat)
+      .def("set_slot_tags", &NodeScheduler::set_slot_tags, py::arg("name"))
+      .def("send_existing", &NodeScheduler::send_existing, py::arg("ids"), py::arg("slots"),
+           py::call_guard<py::gil_scoped_release>())
+      .def("set_peers", &NodeScheduler::set_peers, py::arg("peers"))
+      .def("set_steal", &NodeScheduler::set_steal, py::arg("orphans") = true, py::arg("idle") = true)
+      .def("live_workers", &NodeScheduler::live_workers)
+      .def("stolen_items", &NodeScheduler::stolen_items)
       .def("stop", &NodeScheduler::stop, py::call_guard<py::gil_scoped_release>());
 }

@@ -110,20 +110,48 @@ class NodeScheduler {
     stop();
     if (stat_) {
       munmap(stat_, sizeof(ShardStat));
-      shm_unlink(("/" + stat_name_).c_str());
+      if (!stat_name_.empty()) shm_unlink(("/" + stat_name_).c_str());
     }
+    if (tags_) munmap(tags_, static_cast<size_t>(ring_slots_) * kTagBytes);
   }
 
-  // Shard load published in a small POSIX shm block (the native ingest front-ends map it read-only): tasks queued
-  // into this scheduler and tasks finished, so a front-end's latency-budget admission projects the shard's whole
-  // backlog over its whole completion rate instead of its own partition's share (which, with several front-ends
-  // and 250-image requests, is mostly bodies still uploading and batch-quantization noise).
+  // Durable payloads (a task journal is configured): the payload ring itself outlives a crash of the serving tree
+  // (POSIX shm that nothing unlinks on a crash), and this tag array — kTagBytes per ring slot, the id of the task
+  // whose payload the slot holds — lets a restarted node find each unfinished task's payload there
+  // (runtime/durable_ring.py). Tags are written before a task is acknowledged (the journal record is flushed to
+  // the kernel first too), so every acknowledged task has its record and its payload on a crash; the reference's
+  // equivalent is the Redis "{TaskId}_ORIG" body of CacheConnectorUpsert.cs:125-176.
+  static constexpr size_t kTagBytes = 48;
+  bool set_slot_tags(const std::string& name) {
+    if (tags_ || name.empty() || name.find('/') != std::string::npos) return false;
+    const int fd = shm_open(("/" + name).c_str(), O_RDWR, 0);
+    if (fd < 0) return false;
+    void* p = mmap(nullptr, static_cast<size_t>(ring_slots_) * kTagBytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    ::close(fd);
+    if (p == MAP_FAILED) return false;
+    tags_ = static_cast<char*>(p);
+    return true;
+  }
+
+  // Shard load published in a small POSIX shm block (the native ingest front-ends map it read-write): tasks queued
+  // into this scheduler, tasks that reached a terminal state (completed, failed, dead-lettered), items out at the GPU
+  // workers and the live dispatch workers, so a front-end's latency-budget admission projects the shard's whole
+  // backlog over its service rate instead of its own partition's share (which, with several front-ends and 250-image
+  // requests, is mostly bodies still uploading and batch-quantization noise), and routes around a shard with no live
+  // worker. Every front-end owns one `fe_pending` word (admitted bodies still uploading); the scheduler zeroes it
+  // when that front-end's connection closes, so a front-end killed mid-upload never leaves phantom backlog behind.
+  static constexpr int kStatFrontends = 56;
   struct ShardStat {
-    std::atomic<uint64_t> enq;
-    std::atomic<uint64_t> done;
-    std::atomic<uint64_t> pending;  // written by the front-ends: admitted request bodies still uploading
-    uint64_t pad[5];
+    std::atomic<uint64_t> enq;       // [0]
+    std::atomic<uint64_t> done;      // [1] terminal outcomes
+    std::atomic<uint64_t> pending;   // [2] bodies uploading at front-ends without a word of their own
+    std::atomic<uint64_t> live;      // [3] dispatch workers that are ready
+    std::atomic<uint64_t> inflight;  // [4] items handed to GPU workers, not yet finished or requeued
+    uint64_t pad[3];
+    std::atomic<uint64_t> fe_pending[kStatFrontends];  // [8 + i] front-end i (scheduler rank kFrontendRank0 + i)
   };
+  static_assert(sizeof(ShardStat) == 512, "ShardStat is mapped as 512 bytes by csrc/ingest/ingestd.cpp");
+  static constexpr int kFrontendRank0 = 1 << 20;  // runtime/worker_pool.py FRONTEND_RANK0
   bool open_stat(const std::string& name) {
     if (stat_ || name.empty() || name.find('/') != std::string::npos) return false;
     const int fd = shm_open(("/" + name).c_str(), O_CREAT | O_RDWR, 0600);
@@ -137,9 +165,50 @@ class NodeScheduler {
       return false;
     }
     stat_ = new (p) ShardStat{};
+    stat_->live.store(static_cast<uint64_t>(live_.load()));
     stat_name_ = name;
     return true;
   }
+  // Unlink the counters' name (the mapping stays valid for everyone who has it): on a clean stop.
+  void unlink_stat() {
+    if (!stat_name_.empty()) shm_unlink(("/" + stat_name_).c_str());
+    stat_name_.clear();
+  }
+  // (tests / stats) the published counters: enq, done, pending (all front-ends), live, inflight
+  std::vector<uint64_t> stat_counters() {
+    std::vector<uint64_t> out(5, 0);
+    if (!stat_) {
+      out[3] = static_cast<uint64_t>(live_.load());
+      return out;
+    }
+    out[0] = stat_->enq.load();
+    out[1] = stat_->done.load();
+    out[2] = stat_->pending.load();
+    for (int i = 0; i < kStatFrontends; ++i) out[2] += stat_->fe_pending[i].load();
+    out[3] = stat_->live.load();
+    out[4] = stat_->inflight.load();
+    return out;
+  }
+
+  // Competing consumers across control-plane shards (the reference's replicas all consume ONE Service Bus queue:
+  // BackendQueueProcessor.cs:54-64, host.json:3-11 — an abandoned or orphaned message goes to whichever consumer is
+  // alive). A shard's dispatchers take batches from a peer's queue (a) first, whenever that peer has no live
+  // dispatch worker (its workers died past max_restarts, or it was resized to zero), and (b) when their own queue
+  // stayed empty for a whole poll while the peer holds at least a full batch. A stolen batch stays the peer's: its
+  // messages complete / abandon on the peer's queue, its slots go back to the peer's ring partitions and its
+  // terminal counts to the peer's ShardStat.
+  void set_peers(const std::vector<std::shared_ptr<NodeScheduler>>& peers) {
+    std::lock_guard<std::mutex> g(mu_);
+    peers_.clear();
+    for (auto& p : peers)
+      if (p.get() != this) peers_.push_back(p);
+  }
+  void set_steal(bool orphans, bool idle) {
+    steal_orphans_.store(orphans);
+    steal_idle_.store(idle);
+  }
+  int live_workers() const { return live_.load(); }
+  uint64_t stolen_items() const { return stolen_.load(); }
 
   // Partition of the payload ring freed in this process (the ingest ring of the gateway).
   void add_local_ring(std::shared_ptr<SlotRing> ring) {
@@ -212,6 +281,7 @@ class NodeScheduler {
     {
       std::unique_lock<std::mutex> lk(w->mu);
       w->draining = true;
+      set_live(*w, false);
       w->cv.notify_all();
       cv_wait_s(w->cv, lk, timeout_s, [&] { return w->out.empty() || !w->alive; });
     }
@@ -239,6 +309,16 @@ class NodeScheduler {
   // In-process ingest (gateway): create tasks for payloads already written to `slots`.
   std::vector<std::string> submit(const std::vector<int64_t>& slots, const std::string& trace) {
     return enqueue(slots, trace);
+  }
+
+  // Tasks whose records already exist (explicit-TaskId upsert, journal replay) queued on this shard; returns how many
+  // were queued (the rest hit backpressure).
+  size_t send_existing(const std::vector<std::string>& ids, const std::vector<int64_t>& slots) {
+    tag_slots(ids, slots);
+    if (store_->journaled()) store_->flush();
+    const size_t sent = queue_->send_many(ids, slots);
+    if (stat_) stat_->enq.fetch_add(sent);
+    return sent;
   }
 
   std::vector<std::string> wait_completed(double timeout_s) {
@@ -288,6 +368,7 @@ class NodeScheduler {
   uint64_t images_done() const { return images_done_.load(); }
 
   void stop() {
+    halted_.store(true);
     {
       std::lock_guard<std::mutex> g(fail_mu_);
       stopped_ = true;
@@ -316,6 +397,7 @@ class NodeScheduler {
     std::vector<std::string> ids;
     std::vector<uint64_t> seqs;
     std::vector<int64_t> slots;
+    std::shared_ptr<NodeScheduler> src;  // the peer shard whose queue the batch came from (null: this one)
   };
   struct Worker {
     int rank = -1;
@@ -327,6 +409,7 @@ class NodeScheduler {
     std::condition_variable cv;
     std::atomic<bool> alive{false};
     bool ready = false, draining = false, pinned = false;
+    bool live_counted = false;  // counted in live_ (a ready dispatch worker)
     double last_hb = 0;
     std::unordered_map<uint64_t, Outstanding> out;
     uint64_t batches = 0, images = 0, failed_items = 0, retried_items = 0;
@@ -439,6 +522,8 @@ class NodeScheduler {
     }
     auto ids = shard < 0 ? store_->create_many(endpoint_, slots.size(), "created", trace)
                          : store_->create_many_in(static_cast<size_t>(shard), endpoint_, slots.size(), "created", trace);
+    tag_slots(ids, slots);
+    if (store_->journaled()) store_->flush();  // (the caller acknowledges these ids once this returns)
     const size_t sent = queue_->send_many(ids, slots);
     if (stat_) stat_->enq.fetch_add(sent);
     if (sent < ids.size()) {  // backpressure / closed: CacheConnectorUpsert.cs:181-199
@@ -471,6 +556,8 @@ class NodeScheduler {
     ids.resize(k);
     slots.resize(k);
     free_slots(drop);
+    tag_slots(ids, slots);
+    if (store_->journaled()) store_->flush();  // (the front-end acknowledges these ids on SUBMITTED)
     const size_t sent = queue_->send_many(ids, slots);
     if (stat_) stat_->enq.fetch_add(sent);
     if (sent < ids.size()) {
@@ -481,6 +568,17 @@ class NodeScheduler {
       feed(rest);
     }
     return ids.size();
+  }
+
+  void tag_slots(const std::vector<std::string>& ids, const std::vector<int64_t>& slots) {
+    if (!tags_) return;
+    for (size_t i = 0; i < ids.size() && i < slots.size(); ++i) {
+      if (slots[i] < 0 || slots[i] >= ring_slots_) continue;
+      char* t = tags_ + static_cast<size_t>(slots[i]) * kTagBytes;
+      const size_t n = std::min(ids[i].size(), kTagBytes - 1);
+      std::memcpy(t, ids[i].data(), n);
+      std::memset(t + n, 0, kTagBytes - n);
+    }
   }
 
   // A connection with a declared ring partition (torchrun rank, ingest front-end) may only submit slots of
@@ -520,10 +618,24 @@ class NodeScheduler {
     }
     queue_->take_deadletters();  // drained here: the scheduler fails them itself
     if (!dead.empty()) {
+      if (stat_) stat_->done.fetch_add(dead.size());
       store_->transition_many(dead, "failed", kFailMaxRetries);
       free_slots(dead_slots);
       feed(dead);
     }
+  }
+
+  void set_live(Worker& w, bool on) {  // (w.mu held)
+    if (w.live_counted == on) return;
+    w.live_counted = on;
+    const int v = live_.fetch_add(on ? 1 : -1) + (on ? 1 : -1);
+    if (stat_) stat_->live.store(static_cast<uint64_t>(std::max(0, v)));
+  }
+  NodeScheduler& owner(const Outstanding& o) { return o.src ? *o.src : *this; }
+  void add_inflight(NodeScheduler& own, size_t n, bool add) {
+    if (!own.stat_ || !n) return;
+    if (add) own.stat_->inflight.fetch_add(n);
+    else own.stat_->inflight.fetch_sub(n);
   }
 
   void mark_dead(Worker& w, const char* why, bool report) {
@@ -532,9 +644,14 @@ class NodeScheduler {
     {
       std::lock_guard<std::mutex> g(w.mu);
       out.swap(w.out);
+      set_live(w, false);
       w.cv.notify_all();
     }
-    for (auto& kv : out) requeue(kv.second.ids, kv.second.seqs, kv.second.slots, 0.0, kRequeued);
+    for (auto& kv : out) {
+      NodeScheduler& own = owner(kv.second);
+      add_inflight(own, kv.second.ids.size(), false);
+      own.requeue(kv.second.ids, kv.second.seqs, kv.second.slots, 0.0, kRequeued);
+    }
     {
       std::lock_guard<std::mutex> g(w.send_mu);
       if (w.fd >= 0) ::shutdown(w.fd, SHUT_RDWR);
@@ -578,9 +695,16 @@ class NodeScheduler {
         std::this_thread::sleep_for(std::chrono::milliseconds(20));
         continue;
       }
-      auto msgs = queue_->receive(cfg_.max_batch, cfg_.poll_s, cfg_.linger_s);
+      std::shared_ptr<NodeScheduler> src;
+      auto msgs = take_orphaned(src);
+      if (msgs.empty()) {
+        msgs = queue_->receive(cfg_.max_batch, cfg_.poll_s, cfg_.linger_s);
+        if (msgs.empty()) msgs = take_idle(src);
+      }
       if (msgs.empty()) continue;
+      NodeScheduler& own = src ? *src : *this;
       Outstanding o;
+      o.src = src;
       std::vector<std::string> bad;
       std::vector<uint64_t> bad_seqs;
       o.ids.reserve(msgs.size());
@@ -589,7 +713,7 @@ class NodeScheduler {
       for (auto& m : msgs) {
         // poison guard: a message without a valid payload slot (e.g. recovered after a restart
         // with its ring slot gone) fails on its own instead of poisoning the batch
-        if (m.ref < 0 || m.ref >= ring_slots_) {
+        if (m.ref < 0 || m.ref >= own.ring_slots_) {
           bad.push_back(m.task_id);
           bad_seqs.push_back(m.seq);
           continue;
@@ -600,7 +724,8 @@ class NodeScheduler {
       }
       if (!bad.empty()) {
         store_->transition_many(bad, "failed", kFailInvalid);
-        queue_->complete(bad_seqs);
+        own.queue_->complete(bad_seqs);
+        if (own.stat_) own.stat_->done.fetch_add(bad.size());
         feed(bad);
       }
       if (o.ids.empty()) continue;
@@ -613,14 +738,18 @@ class NodeScheduler {
       }
       const uint64_t bid = next_bid_.fetch_add(1);
       std::vector<int64_t> slots = o.slots;
+      const size_t nitems = o.ids.size();
       bool died = false;
       {
         std::lock_guard<std::mutex> g(w.mu);
         died = !w.alive;
-        if (!died) w.out.emplace(bid, std::move(o));
+        if (!died) {
+          add_inflight(own, nitems, true);
+          w.out.emplace(bid, std::move(o));
+        }
       }
       if (died) {  // died while we were receiving: hand the batch straight back
-        requeue(o.ids, o.seqs, o.slots, 0.0, kRequeued);
+        own.requeue(o.ids, o.seqs, o.slots, 0.0, kRequeued);
         break;
       }
       if (!send_slots(w, F_BATCH, bid, slots, true)) {
@@ -630,10 +759,64 @@ class NodeScheduler {
     }
   }
 
+  std::vector<std::shared_ptr<NodeScheduler>> live_peers() {
+    std::vector<std::shared_ptr<NodeScheduler>> ps;
+    std::lock_guard<std::mutex> g(mu_);
+    ps.reserve(peers_.size());
+    for (auto& wp : peers_)
+      if (auto p = wp.lock())
+        if (!p->halted_.load()) ps.push_back(std::move(p));
+    return ps;
+  }
+  // (a) a peer shard without a live dispatch worker: its queued work is ours to finish, before our own
+  std::vector<Message> take_orphaned(std::shared_ptr<NodeScheduler>& src) {
+    if (!steal_orphans_.load() || peers_empty_()) return {};
+    auto ps = live_peers();
+    const size_t k = ps.size(), start = k ? steal_rr_.fetch_add(1) % k : 0;
+    for (size_t i = 0; i < k; ++i) {
+      auto& p = ps[(start + i) % k];
+      if (p->live_.load() > 0 || p->queue_->depth() == 0) continue;
+      auto m = p->queue_->receive(cfg_.max_batch, 0.0, 0.0);
+      if (!m.empty()) {
+        stolen_.fetch_add(m.size());
+        src = p;
+        return m;
+      }
+    }
+    return {};
+  }
+  // (b) our queue stayed empty for a whole poll: help the peer with the deepest backlog of at least a full batch
+  std::vector<Message> take_idle(std::shared_ptr<NodeScheduler>& src) {
+    if (!steal_idle_.load() || peers_empty_()) return {};
+    std::shared_ptr<NodeScheduler> best;
+    size_t best_depth = 0;
+    for (auto& p : live_peers()) {
+      const size_t d = p->queue_->depth();
+      if (d >= cfg_.max_batch && d > best_depth) {
+        best_depth = d;
+        best = p;
+      }
+    }
+    if (!best) return {};
+    auto m = best->queue_->receive(cfg_.max_batch, 0.0, 0.0);
+    if (!m.empty()) {
+      stolen_.fetch_add(m.size());
+      src = best;
+    }
+    return m;
+  }
+  bool peers_empty_() {
+    std::lock_guard<std::mutex> g(mu_);
+    return peers_.empty();
+  }
+
   void reader_loop(Worker& w) {
     std::string f;
     while (true) {
       if (!read_frame(w.fd, f)) {
+        // an ingest front-end that went away (killed mid-upload) leaves no admitted-body backlog behind
+        if (!w.dispatch && stat_ && w.rank >= kFrontendRank0 && w.rank - kFrontendRank0 < kStatFrontends)
+          stat_->fe_pending[w.rank - kFrontendRank0].store(0);
         if (w.alive) mark_dead(w, "connection lost", true);
         return;
       }
@@ -652,6 +835,7 @@ class NodeScheduler {
           }
           w.ready = true;
           w.last_hb = mono_now();
+          if (w.dispatch && !w.draining && w.alive) set_live(w, true);
           w.cv.notify_all();
           break;
         }
@@ -771,11 +955,14 @@ class NodeScheduler {
       o = std::move(it->second);
       w.out.erase(it);
     }
+    NodeScheduler& own = owner(o);
+    add_inflight(own, o.ids.size(), false);
     if (len < need || n != o.ids.size()) {  // malformed: treat the batch as a model error
       std::vector<uint8_t> none(o.ids.size(), 0);
       store_->finish_many(o.ids, nullptr, none, "completed", kFailError);
-      queue_->complete(o.seqs);
-      free_slots(o.slots);
+      own.queue_->complete(o.seqs);
+      own.free_slots(o.slots);
+      if (own.stat_) own.stat_->done.fetch_add(o.ids.size());
       feed(o.ids);
     } else {
       res->data.assign(status + spad, static_cast<size_t>(n) * row_bytes);
@@ -816,10 +1003,10 @@ class NodeScheduler {
         store_->finish_many(fin, sub, fok, "completed", kFailError);
       }
       if (!invalid.empty()) store_->transition_many(invalid, "failed", kFailInvalid);
-      queue_->complete(done_seqs);
-      free_slots(free_s);
-      if (!retry.empty()) requeue(retry, retry_seqs, retry_slots, cfg_.retry_delay_s,
-                                  "Awaiting service availability. Batch failed; retrying.");
+      own.queue_->complete(done_seqs);
+      own.free_slots(free_s);
+      if (!retry.empty()) own.requeue(retry, retry_seqs, retry_slots, cfg_.retry_delay_s,
+                                      "Awaiting service availability. Batch failed; retrying.");
       size_t nfail = 0;
       for (uint32_t i = 0; i < n; ++i) nfail += status[i] == IT_INVALID || status[i] == IT_ERROR;
       (void)any_err;
@@ -831,7 +1018,7 @@ class NodeScheduler {
         w.retried_items += retry.size();
       }
       images_done_.fetch_add(n - retry.size());
-      if (stat_) stat_->done.fetch_add(n - retry.size());
+      if (own.stat_) own.stat_->done.fetch_add(n - retry.size());
       std::vector<std::string> fed;
       fed.reserve(n);
       for (uint32_t i = 0; i < n; ++i)
@@ -853,10 +1040,16 @@ class NodeScheduler {
   std::vector<std::string> stage_eps_, stage_status_;
   std::vector<int> store_shards_;
   size_t store_rr_ = 0;
+  std::vector<std::weak_ptr<NodeScheduler>> peers_;
+  std::atomic<bool> steal_orphans_{true}, steal_idle_{true}, halted_{false};
+  std::atomic<size_t> steal_rr_{0};
+  std::atomic<uint64_t> stolen_{0};
+  std::atomic<int> live_{0};
   std::atomic<uint64_t> next_bid_{1};
   std::atomic<uint64_t> images_done_{0};
   ShardStat* stat_ = nullptr;
   std::string stat_name_;
+  char* tags_ = nullptr;
   std::mutex fail_mu_;
   std::condition_variable fail_cv_;
   std::vector<int> failed_;

@@ -771,6 +771,7 @@ class TaskStore {
     std::lock_guard<std::mutex> g(journal_.mu);
     if (journal_.f) std::fflush(journal_.f);
   }
+  bool journaled() const { return journal_.f != nullptr; }
 
   template <class Parse>
   size_t replay(const std::string& path, Parse parse) {

@@ -13,9 +13,9 @@
 // Prints one JSON line: requests, ok, errors, busy (429s, retried after the server's Retry-After), t0, t1 (epoch s),
 // bytes_sent, cpu_user_s, cpu_sys_s.
 // IDS_OUT receives one task id per line (TaskId / TaskIds of every 2xx answer).
-// Bodies of 1 MiB or more are sent as real clients (curl) send them: headers with `Expect: 100-continue` first, the
+// Bodies of 64 KiB or more are sent as careful clients (curl: past 1 MiB) send them: `Expect: 100-continue` first, the
 // body only after `100 Continue`, so a request the server's admission refuses (429) costs a header round trip, not
-// the upload of the body. The server closes such a connection after the refusal; the client dials again.
+// the upload of the body, and the connection stays open (a refusal the server closes: the client dials again).
 #include <arpa/inet.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
@@ -238,7 +238,8 @@ int main(int argc, char** argv) {
   std::string head = "POST " + path + " HTTP/1.1\r\nHost: " + std::string(host) + ":" + std::to_string(port) +
                      "\r\nContent-Type: " + ctype + "\r\nContent-Length: " + std::to_string(body.size()) + "\r\n";
   for (int i = 10; i < argc; ++i) head += std::string(argv[i]) + "\r\n";
-  const bool expect = body.size() >= (1u << 20);
+  // (curl sends Expect for bodies past 1 MiB; 64 KiB here, so a refused camera frame costs its headers, not its body)
+  const bool expect = body.size() >= (64u << 10);
   if (expect) head += "Expect: 100-continue\r\n";
   head += "\r\n";
   const std::string whole = g_tls ? head + body : std::string();  // (TLS: one SSL_write per request)
@@ -287,16 +288,23 @@ int main(int argc, char** argv) {
           }
           continue;
         }
-        if (!send_req(l, iov, whole)) {
-          l.close();
-          l = dial(host, port);
-          ++r.errors;
-          continue;
-        }
+        const bool sent = send_req(l, iov, whole);
         ++r.requests;
         r.bytes += static_cast<double>(head.size() + body.size());
         double retry_ms = 0;
-        int st = read_response(l, buf, rbody, &retry_ms);
+        bool closes = false;
+        // (a send cut short may still have its answer waiting: the server refuses an unread body with 429 and closes)
+        int st = read_response(l, buf, rbody, &retry_ms, &closes);
+        if (!sent && st != 429) st = 0;
+        if (st == 429 && (closes || !sent)) {  // refused unread: back off, then dial again
+          ++r.busy;
+          const double ms = std::min(100.0, std::max(0.5, retry_ms));
+          std::this_thread::sleep_for(std::chrono::microseconds(static_cast<long>(ms * 1e3)));
+          l.close();
+          buf.clear();
+          l = dial(host, port);
+          continue;
+        }
         if (st == 0) {
           l.close();
           buf.clear();

@@ -171,34 +171,69 @@ struct Shard {
   // latency-budget admission projects a new request's queue wait as (slots in use + n) / rate
   std::atomic<int64_t> freed{0};
   std::mutex rate_mu;
-  double rate = 0.0, rate_t = 0.0, peak = 0.0;
+  double rate = 0.0, rate_t = 0.0;
   int64_t rate_n = 0;
+  bool rate_sat = false;
 
-  // the scheduler shard's load counters (NodeScheduler::open_stat, "stat NAME" on the shard line): tasks queued /
-  // finished across every ingest path of the shard; null = estimate from this partition alone
-  // [0] queued, [1] finished (the scheduler's), [2] admitted bodies still uploading (every front-end's)
+  // the scheduler shard's load counters (NodeScheduler::ShardStat, "stat NAME" on the shard line), 64 words:
+  // [0] queued, [1] finished (terminal), [2] bodies uploading (front-ends without a word of their own), [3] live
+  // dispatch workers, [4] items out at the GPU workers, [8 + i] bodies uploading at front-end i; null = estimate
+  // from this partition alone
   std::atomic<uint64_t>* st = nullptr;
+  static constexpr int kStatWords = 64, kStatFe0 = 8, kStatFrontends = 56;
 
+  bool live() const { return !st || st[3].load(std::memory_order_relaxed) > 0; }
+  // tasks of the shard not yet finished, plus every front-end's admitted bodies still uploading
+  double backlog() const {
+    const uint64_t e = st[0].load(std::memory_order_relaxed), d = st[1].load(std::memory_order_relaxed);
+    uint64_t up = st[2].load(std::memory_order_relaxed);
+    for (int i = 0; i < kStatFrontends; ++i) up += st[kStatFe0 + i].load(std::memory_order_relaxed);
+    return (e > d ? static_cast<double>(e - d) : 0.0) + static_cast<double>(up);
+  }
+  // items queued behind the GPU workers' pipelines (not yet handed to a worker)
+  bool queued() const {
+    const uint64_t e = st[0].load(std::memory_order_relaxed), d = st[1].load(std::memory_order_relaxed),
+                   f = st[4].load(std::memory_order_relaxed);
+    return e > d + f;
+  }
+  // ... or admitted bodies still uploading: work that will have to wait for the pipelines too
+  bool waiting() const {
+    if (queued()) return true;
+    uint64_t up = st[2].load(std::memory_order_relaxed);
+    for (int i = 0; i < kStatFrontends; ++i) up += st[kStatFe0 + i].load(std::memory_order_relaxed);
+    return up > 0;
+  }
+
+  // The shard's capacity in items per second at the batches it actually forms. A completion-rate sample taken while
+  // tasks waited in the queue at both ends (the workers never starved) measures that capacity and is averaged in;
+  // a sample from a shard that ran out of work only measures the demand, a lower bound: it can raise the estimate,
+  // never lower it. (Round 5 held the smoothed rate's peak and let it decay 10 %/s, so a route whose clients were
+  // slower than the GPU — single images — read as a slow GPU and throttled itself to 0.59x.)
   double service_rate() {
     std::lock_guard<std::mutex> g(rate_mu);
     const double t = ai4e::mono_now();
     const int64_t n = st ? static_cast<int64_t>(st[1].load(std::memory_order_relaxed)) : freed.load();
+    const bool sat = st ? queued() : false;
     if (rate_t == 0.0) {
       rate_t = t;
       rate_n = n;
+      rate_sat = sat;
     } else if (t - rate_t >= 0.05) {
       const double r = static_cast<double>(n - rate_n) / (t - rate_t);
-      // only samples with completions update the rate: an idle partition (no traffic) or a pipeline still
-      // filling (slots in use, none freed yet) is not a slow GPU
-      if (n > rate_n) rate = rate == 0.0 ? r : 0.7 * rate + 0.3 * r;
-      // the capacity estimate holds the smoothed rate's recent peak and decays ~10 % per second: a dip in demand
-      // (clients backing off after 429s) must not read as a slower GPU, or admission would throttle further and
-      // feed on itself
-      peak = std::max(rate, peak * std::pow(0.9, t - rate_t));
+      if (n > rate_n) {
+        if (!st) {
+          rate = rate == 0.0 ? r : 0.7 * rate + 0.3 * r;
+        } else if (rate_sat && sat) {
+          rate = rate == 0.0 ? r : 0.7 * rate + 0.3 * r;
+        } else if (r > rate) {
+          rate = r;
+        }
+      }
       rate_t = t;
       rate_n = n;
+      rate_sat = sat;
     }
-    return peak;
+    return rate;
   }
 
   // request-body upload rate of this front-end (bytes/s, EWMA over completed bodies): a request's tasks only join
@@ -212,24 +247,28 @@ struct Shard {
     upload_bw = upload_bw == 0.0 ? bw : 0.8 * upload_bw + 0.2 * bw;
   }
 
-  // projected queue wait of n more items (nbytes of body) once they are queued: the shard's backlog (queued, not yet
-  // finished, plus every front-end's admitted bodies still arriving) over its completion rate, minus what drains
-  // while this body uploads; or this partition's slots in use over its FREE rate when the shard publishes no counters
+  // projected queue wait of n more items (nbytes of body) once they are queued: the shard's backlog over its
+  // capacity, minus what drains while this body uploads; or this partition's slots in use over its FREE rate when
+  // the shard publishes no counters. Nothing waiting behind the GPU workers' pipelines means no queue wait at all,
+  // whatever the estimate (a shard whose demand never reached its capacity has only a lower bound of it).
   double projected_wait(int64_t n, double nbytes) {
     const double rate = service_rate();
     if (rate <= 0.0) return 0.0;
     if (st) {
-      const uint64_t e = st[0].load(std::memory_order_relaxed), d = st[1].load(std::memory_order_relaxed);
-      const double backlog = (e > d ? static_cast<double>(e - d) : 0.0) +
-                             static_cast<double>(st[2].load(std::memory_order_relaxed));
+      if (!waiting()) return 0.0;
       double up = 0.0;
       {
         std::lock_guard<std::mutex> g(up_mu);
         if (upload_bw > 0.0) up = nbytes / upload_bw;
       }
-      return std::max(0.0, (backlog + static_cast<double>(n)) / rate - up);
+      return std::max(0.0, (backlog() + static_cast<double>(n)) / rate - up);
     }
     return static_cast<double>(slots->used() + n) / rate;
+  }
+  // this front-end's admitted-bodies word in the shard's counters
+  std::atomic<uint64_t>* pending_word(int fe) {
+    if (!st) return nullptr;
+    return fe >= 0 && fe < kStatFrontends ? &st[kStatFe0 + fe] : &st[2];
   }
 
   bool send_frame(const std::string& payload) {
@@ -352,6 +391,7 @@ struct Config {
   double ack_timeout = 30.0, alloc_timeout = 60.0;
   double max_queue_s = 0.0;  // latency budget of an ingested request's queue wait (0: no budget, wait for slots)
   int ready_fd = -1;  // "ready FD": one byte written once the public socket listens (the parent hands the port over)
+  int frontend_index = -1;  // "frontend_index I": this process's word in every shard's counters
   std::vector<std::string> keys;
   std::vector<std::unique_ptr<Shard>> shards;
   std::vector<std::unique_ptr<Route>> routes;  // longest prefix first
@@ -401,6 +441,8 @@ void parse_config(const char* path) {
       ls >> g_cfg.alloc_timeout;
     } else if (kw == "ready") {
       ls >> g_cfg.ready_fd;
+    } else if (kw == "frontend_index") {
+      ls >> g_cfg.frontend_index;
     } else if (kw == "max_queue_ms") {
       double ms = 0;
       ls >> ms;
@@ -413,7 +455,8 @@ void parse_config(const char* path) {
       if (ls >> dg && !dg.empty() && dg != "-") s->digits = dg;
       if (ls >> stat && !stat.empty() && stat != "-") {
         const int sfd = shm_open(("/" + stat).c_str(), O_RDWR, 0);
-        void* sp = sfd >= 0 ? mmap(nullptr, 64, PROT_READ | PROT_WRITE, MAP_SHARED, sfd, 0) : MAP_FAILED;
+        void* sp = sfd >= 0 ? mmap(nullptr, Shard::kStatWords * 8, PROT_READ | PROT_WRITE, MAP_SHARED, sfd, 0)
+                            : MAP_FAILED;
         if (sfd >= 0) ::close(sfd);
         if (sp != MAP_FAILED) s->st = static_cast<std::atomic<uint64_t>*>(sp);  // (else: partition estimate)
       }
@@ -875,6 +918,8 @@ std::string py_list(const std::vector<std::string>& v) {  // Python's repr of a 
   return out + "]";
 }
 
+constexpr int64_t kDrainMax = 1 << 20;  // refused bodies read and dropped to keep a non-Expect connection
+
 bool ingest(Conn& c, const Request& r, Route& route, Shard& s, bool batch) {
   const int64_t nbytes = r.content_length;
   const bool ka = r.keep_alive;
@@ -911,15 +956,25 @@ bool ingest(Conn& c, const Request& r, Route& route, Shard& s, bool batch) {
     // refused with 429 + Retry-After instead of queueing behind a deep ring
     const double wait = s.projected_wait(n, static_cast<double>(nbytes));
     if (wait > g_cfg.max_queue_s) {
-      // the hint is capped at twice the budget: a request refused on a stale estimate comes back soon and is judged
-      // again, instead of idling its client for the whole projected wait
-      const double retry_s = std::min(2.0 * g_cfg.max_queue_s, std::max(0.001, wait - g_cfg.max_queue_s));
+      // the hint: the time for the backlog above the budget to drain, at least one budget (every refused client comes
+      // back competing with the others: sub-millisecond hints made the single-image route answer more 429s than it
+      // admitted) and at most two (a request refused on a stale estimate is judged again soon)
+      const double retry_s = std::min(2.0 * g_cfg.max_queue_s, std::max(g_cfg.max_queue_s, wait - g_cfg.max_queue_s));
       const std::string h = "Retry-After: " + std::to_string(static_cast<int>(std::ceil(retry_s))) +
                             "\r\nx-ai4e-retry-after-ms: " + std::to_string(static_cast<int>(std::ceil(retry_s * 1e3))) +
                             "\r\n";
-      // (an Expect: 100-continue client sends no body after a final answer, so its connection stays usable: a
-      // refusal costs a header round trip, not a reconnect and, over HTTPS, a new TLS handshake)
-      if (lower(r.get("expect")) != "100-continue" && !c.discard(static_cast<size_t>(nbytes))) return false;
+      // An Expect: 100-continue client (the load generator sends it for bodies of 64 KiB or more) sends no body after
+      // a final answer, so its connection stays usable: a refusal costs a header round trip. Any other client's body
+      // is on its way: one under kDrainMax is read and dropped (measured: closing instead made every refusal a
+      // reconnect + a new connection thread, and the single-image route fell from 48k to 23k images/s); a larger
+      // one is refused unread and the connection closed.
+      if (lower(r.get("expect")) != "100-continue") {
+        if (nbytes <= kDrainMax && c.discard(static_cast<size_t>(nbytes)))
+          return respond(c, 429, "application/json", message_json("Service is busy, please try again later."), ka, h);
+        respond(c, 429, "application/json", message_json("Service is busy, please try again later."), false, h);
+        ::shutdown(c.fd, SHUT_WR);
+        return false;
+      }
       return respond(c, 429, "application/json", message_json("Service is busy, please try again later."), ka, h);
     }
   }
@@ -930,7 +985,7 @@ bool ingest(Conn& c, const Request& r, Route& route, Shard& s, bool batch) {
     ~Pending() {
       if (p) p->fetch_sub(n);
     }
-  } pending{g_cfg.max_queue_s > 0.0 && s.st ? &s.st[2] : nullptr, static_cast<uint64_t>(n)};
+  } pending{g_cfg.max_queue_s > 0.0 ? s.pending_word(g_cfg.frontend_index) : nullptr, static_cast<uint64_t>(n)};
   if (pending.p) pending.p->fetch_add(pending.n);
   if (lower(r.get("expect")) == "100-continue" && !c.send_all("HTTP/1.1 100 Continue\r\n\r\n", 25)) return false;
   std::vector<int64_t> sl = s.slots->alloc(n, g_cfg.alloc_timeout);
@@ -977,21 +1032,27 @@ bool ingest(Conn& c, const Request& r, Route& route, Shard& s, bool batch) {
   return respond(c, created < 0 ? 202 : 200, "text/plain; charset=utf-8", "TaskId: " + ids[0], ka, b3);
 }
 
-// The control-plane shard of an endpoint that takes the next request: the one whose partition of this front-end has
-// the smallest share of its slots in use (least loaded), ties round-robin.
+// The control-plane shard of an endpoint that takes the next request: among the shards with a live GPU worker, the
+// one with the smallest backlog (the scheduler's published counters: tasks not finished + bodies uploading), else the
+// smallest share of this front-end's partition in use; ties round-robin. A shard without a live worker is only
+// picked when no shard has one (its peers drain its queue: NodeScheduler competing consumers).
 Shard* pick_shard(Route& route) {
   const size_t k = route.shards.size();
   if (k == 0) return nullptr;
   if (k == 1) return g_cfg.shards[static_cast<size_t>(route.shards[0])].get();
   const size_t start = static_cast<size_t>(route.rr.fetch_add(1) % k);
   Shard* best = nullptr;
-  double best_load = 2.0;
+  double best_load = 0.0;
+  bool best_live = false;
   for (size_t i = 0; i < k; ++i) {
     Shard* s = g_cfg.shards[static_cast<size_t>(route.shards[(start + i) % k])].get();
-    const double load = static_cast<double>(s->slots->used()) / static_cast<double>(std::max<int64_t>(1, s->len));
-    if (load < best_load) {
-      best_load = load;
+    const bool live = s->live();
+    const double load = s->st ? s->backlog() + static_cast<double>(s->slots->used())
+                              : static_cast<double>(s->slots->used()) / static_cast<double>(std::max<int64_t>(1, s->len));
+    if (!best || (live && !best_live) || (live == best_live && load < best_load)) {
       best = s;
+      best_load = load;
+      best_live = live;
     }
   }
   return best;
