@@ -158,16 +158,15 @@ class _StageGraphEnsembleServable(EnsembleServable):
     stages = 1
 
     def __call__(self, images_u8):
-        boxes, scores, valid, res = self.pipeline.run_batches([images_u8])[0]
+        # no host synchronization: the answer rows come back padded to the crop capacity, valid crops first
+        boxes, scores, valid, res, _ = self.pipeline.run_batches([images_u8], padded=True)[0]
         b, m = valid.shape
         flat = valid.reshape(-1)
-        species = torch.full((b * m,), -1, dtype=torch.int32, device=valid.device)
-        prob = torch.zeros(b * m, device=valid.device)
-        n = res.shape[0]
-        if n:
-            pos = torch.nonzero(flat).reshape(-1)[:n]  # the valid slots, in the order the crops were packed
-            species[pos] = res[:, 0].to(torch.int32)
-            prob[pos] = res[:, 1].float()
+        # valid slot s was packed at position (number of valid slots before it): its answer row
+        pos = (torch.cumsum(flat.int().reshape(1, -1), 1).reshape(-1) - 1).clamp(min=0).long()
+        rows = res.index_select(0, pos)
+        species = torch.where(flat, rows[:, 0].to(torch.int32), torch.full_like(pos, -1, dtype=torch.int32))
+        prob = torch.where(flat, rows[:, 1].float(), torch.zeros_like(rows[:, 1]))
         count = valid.sum(1, keepdim=True).to(torch.int32)
         return (boxes.float().contiguous(), (scores * valid).float().contiguous(), species.reshape(b, m),
                 prob.reshape(b, m), count)

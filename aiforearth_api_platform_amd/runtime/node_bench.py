@@ -157,22 +157,22 @@ def http_phase(cp, pool, seconds: float, batch: int, item_shape, path: str, fron
 
     server_procs = [psutil.Process(os.getpid())] + [psutil.Process(p.pid) for p in fe]
 
-    def server_cpu() -> float:
-        tot = 0.0
+    def server_cpu(split: bool = False):
+        per = []
         for p in server_procs:
             try:
                 c = p.cpu_times()
-                tot += c.user + c.system
+                per.append(c.user + c.system)
             except psutil.Error:
-                pass
-        return tot
+                per.append(0.0)
+        return (per[0], sum(per[1:])) if split else sum(per)
 
     native = os.environ.get("AI4E_HTTP_CLIENT", "native") == "native"
     out = {}
     for name, body, ctype, is_batch, procs, conc in (
             ("batch_route", batch_body, BATCH_CONTENT_TYPE, True, 4, 4),
             ("single_image_route", img.tobytes(), "application/octet-stream", False, 4, 32)):
-        c0 = server_cpu()
+        c0, s0 = server_cpu(), server_cpu(True)
         if native:
             res = run_native_clients(url, seconds / 2, conc, body, ctype, procs=procs)
             ids, t0, errors = res["ids"], res["t0"], res["errors"]
@@ -189,6 +189,9 @@ def http_phase(cp, pool, seconds: float, batch: int, item_shape, path: str, fron
                      "p50_task_latency_ms": round(percentile(lat, 50) * 1e3, 3),
                      "p99_task_latency_ms": round(percentile(lat, 99) * 1e3, 3),
                      "server_cpu_s": round(server_cpu() - c0, 3), "window_s": round(dt, 3)}
+        s1 = server_cpu(True)  # where the server's CPU went: the serving process (scheduler, gateway) / front-ends
+        out[name]["server_cpu_split_s"] = {"serving_process": round(s1[0] - s0[0], 3),
+                                           "frontends": round(s1[1] - s0[1], 3)}
         if res:
             out[name]["client_cpu_s"] = round(res["client_cpu_s"], 3)
             out[name]["request_gbytes_per_s"] = round(res["bytes_sent"] / max(1e-9, res["t1"] - res["t0"]) / 1e9, 3)

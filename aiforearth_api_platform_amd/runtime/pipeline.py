@@ -9,9 +9,12 @@ classifier GPUs of one group; 1:1 is the pair form):
 * detector ranks run Faster-RCNN on a batch, pick the confident animal boxes, crop + bilinear-resize
   them on the GPU to uint8 ``[N, 224, 224, 3]`` (``crop_resize_u8``, K5/K7: 147 KiB per crop, the
   classifier's own input format, half the bytes of fp16 and a sixth of a bf16x8 stem tensor) and
-  ``send`` a count header then the crops to their classifier rank over RCCL;
-* classifier ranks ``recv`` the count, the crops, run the crop classifier (fused ResNet-50, bf16 or fp16)
-  and send back ``[N, 2]`` (class, probability);
+  send a fixed-size message to their classifier rank over RCCL: a device-side header (crop count, capacity)
+  and the capacity-sized crop buffer, valid crops first. The detector never reads the count on the host: its
+  hand-off is stream-ordered behind its graph replay, so consecutive replays never drain to the host;
+* classifier ranks ``recv`` the header, the crops, run the crop classifier (fused ResNet-50, bf16 or fp16) on
+  the valid prefix and send back ``[capacity, 2]`` (class, probability), whose receive the detector posted
+  with its send;
 * a detector keeps one batch in flight: it sends batch i, starts detecting batch i+1, then collects batch
   i's classifications — compute and transfer overlap; message order per pair is fixed (header, payload,
   results) so the pairing can never deadlock;
@@ -22,7 +25,6 @@ classifier GPUs of one group; 1:1 is the pair form):
 from __future__ import annotations
 
 import os
-import time
 from dataclasses import dataclass
 from typing import Callable, List, Optional, Sequence, Tuple
 
@@ -78,38 +80,49 @@ def _fault_at() -> int:
     return 0
 
 
-class _Completion:
-    """Host-visible completion of a posted receive, one test for every backend: RCCL's ``is_completed`` is an event
-    query that advances on its own; gloo completes a receive only inside ``wait`` (which blocks), so there a waiter
-    thread does the wait and sets a flag. The classifier's header loop polls ``done()`` either way."""
+class _Arrivals:
+    """Event-driven completion of posted receives, one form for every backend: ``post(d, work)`` hands the receive
+    of detector ``d`` to a waiter thread and ``next()`` blocks until any posted receive has landed. On gloo the waiter
+    blocks in ``work.wait()`` (gloo completes a receive only there); on RCCL the work is made a dependency of a
+    per-detector side stream and the waiter sleeps in a blocking-sync HIP event recorded behind it (no NCCL call off
+    the serving thread, no polling)."""
 
-    def __init__(self, work, blocking_wait: bool):
-        self.work = work
-        self._ev = None
-        if blocking_wait:
-            import threading
+    def __init__(self, device: torch.device, blocking_wait: bool):
+        import queue
+        import threading
 
-            self._ev = threading.Event()
-            self._err: list = []
+        self.device, self.blocking = device, blocking_wait
+        self.ready: "queue.Queue" = queue.Queue()
+        self._threading = threading
+        self._streams: dict = {}
 
-            def waiter():
-                try:
-                    work.wait()
-                except Exception as e:  # (surfaced by wait() on the serving thread)
-                    self._err.append(e)
-                self._ev.set()
-            threading.Thread(target=waiter, daemon=True).start()
-
-    def done(self) -> bool:
-        return self._ev.is_set() if self._ev is not None else self.work.is_completed()
-
-    def wait(self) -> None:
-        if self._ev is not None:
-            self._ev.wait()
-            if self._err:
-                raise self._err[0]
+    def post(self, d: int, work) -> None:
+        if self.blocking or self.device.type != "cuda":
+            target = work.wait
         else:
-            self.work.wait()
+            s = self._streams.get(d)
+            if s is None:
+                s = self._streams[d] = torch.cuda.Stream(device=self.device)
+            with torch.cuda.stream(s):
+                work.wait()  # (RCCL: the side stream waits for the receive)
+            ev = torch.cuda.Event(blocking=True)
+            ev.record(s)
+            target = ev.synchronize
+
+        def waiter():
+            err = None
+            try:
+                target()
+            except Exception as e:  # (surfaced by next() on the serving thread)
+                err = e
+            self.ready.put((d, err))
+        self._threading.Thread(target=waiter, daemon=True).start()
+
+    def next(self) -> int:
+        d, err = self.ready.get()
+        if err is not None:
+            raise err
+        return d
 
 
 def plan_ensemble(gpus: int, det_images_per_s: float, cls_crops_per_s: float, crops_per_image: float,
@@ -229,67 +242,87 @@ class StageGraphPipeline:
         crumb("pipe.compacted", count)
         return dets, boxes, scores, valid, packed[: b * m].to(self.wire_dtype), count
 
-    def _send(self, crops: torch.Tensor, n: int) -> list:
-        """Non-blocking: the detector must be free to post the receive of the previous batch's results while these
-        bytes move, or both sides block in send (rendezvous) and deadlock. The crops leave through a pair of
-        preallocated wire buffers used alternately (batch i in buffer i % 2): the detector graph's static output is
-        rewritten by the next replay while this send may still read, and ``run_batches`` waits for batch i's send
-        before batch i + 2 reuses its buffer — one device copy into a resident buffer per batch, no allocation."""
+    def _send(self, crops: torch.Tensor, count: torch.Tensor):
+        """Non-blocking, and without the crop count on the host: a device-side header [count, capacity] and the
+        whole capacity-sized crop buffer (valid crops first) go to the classifier, and the receive of its
+        [capacity, 2] answer is posted right behind. The crops leave through a pair of preallocated wire buffers used
+        alternately (batch i in buffer i % 2): the detector graph's static output is rewritten by the next replay
+        while this send may still read, and batch i + 2 waits (stream-side on RCCL) for batch i's send before it
+        reuses the buffer — one device copy into a resident buffer per batch, no allocation. Returns the works to
+        wait for and the answer tensor."""
         self._handoffs += 1
         if self._fail_at and self._handoffs == self._fail_at:
             raise RuntimeError(f"injected xGMI hand-off failure (batch {self._handoffs})")
-        hdr = torch.tensor([n], dtype=torch.int64, device=self.device)
-        works = [(dist.isend(hdr, group_dst=self.peer, group=self.group), hdr)]
-        self.bytes_sent += 8
-        if n:
-            wire = self._wire_buffer(crops)
-            c = wire[:n]
-            c.copy_(crops[:n])
-            works.append((dist.isend(c, group_dst=self.peer, group=self.group), c))
-            self.bytes_sent += c.numel() * c.element_size()
-        return works
+        cap = crops.shape[0]
+        hdr = torch.empty(2, dtype=torch.int64, device=self.device)
+        hdr[:1].copy_(count.reshape(1))
+        hdr[1:].fill_(cap)
+        k = self._handoffs % 2
+        wire = self._wire_buffer(crops)
+        for w in self._buf_works[k]:  # batch i - 2's send out of this buffer has finished reading it
+            w.wait()
+        wire.copy_(crops)
+        sends = [dist.isend(hdr, group_dst=self.peer, group=self.group),
+                 dist.isend(wire, group_dst=self.peer, group=self.group)]
+        self._buf_works[k] = sends
+        self._hdr_keep[k] = hdr  # (alive until its send is done)
+        self.bytes_sent += hdr.numel() * 8 + wire.numel() * wire.element_size()
+        res = torch.empty(cap, 2, device=self.device)
+        rw = dist.irecv(res, group_src=self.peer, group=self.group)
+        return rw, res
 
     def _wire_buffer(self, crops: torch.Tensor) -> torch.Tensor:
-        """The ping-pong wire buffer of this hand-off (grown to the largest crop batch seen)."""
-        if not hasattr(self, "_wire") or self._wire[0].shape[0] < crops.shape[0] or \
-                self._wire[0].shape[1:] != crops.shape[1:] or self._wire[0].dtype != crops.dtype:
-            # (an in-flight send of the previous pair keeps its buffer alive through its works entry)
+        """The ping-pong wire buffer of this hand-off (sized to the detector batch's crop capacity)."""
+        if not hasattr(self, "_wire") or self._wire[0].shape != crops.shape or self._wire[0].dtype != crops.dtype:
+            for ws in getattr(self, "_buf_works", [[], []]):  # (the old buffers' sends finish before they go)
+                for w in ws:
+                    w.wait()
             self._wire = [torch.empty_like(crops), torch.empty_like(crops)]
+            self._buf_works, self._hdr_keep = [[], []], [None, None]
         return self._wire[self._handoffs % 2]
 
-    def _recv_results(self, n: int) -> torch.Tensor:
-        res = torch.empty(n, 2, device=self.device)
-        if n:
-            dist.recv(res, group_src=self.peer, group=self.group)
-            self.bytes_received += res.numel() * res.element_size()
-        return res
-
-    def run_batches(self, batches: Sequence[torch.Tensor]) -> List[Tuple]:
+    def run_batches(self, batches: Sequence[torch.Tensor], padded: bool = False) -> List[Tuple]:
         """Detector rank: per batch (boxes [B, M, 4], det scores [B, M], valid [B, M], classes [n, 2] for the
-        valid crops in (image, score) order), one batch's crops on the wire while the next one is detected."""
-        out, pending, inflight = [], None, []
+        valid crops in (image, score) order), one batch's crops on the wire while the next one is detected.
+        ``padded``: (boxes, scores, valid, classes [B * M, 2] — the valid crops' rows first —, count [1]) with no
+        host synchronization at all (the serving path: every tensor stays stream-ordered on the device)."""
+        out, pending = [], None
+
+        def finish(p):
+            boxes, scores, valid, count, rw, res = p
+            rw.wait()  # (RCCL: stream-ordered; gloo: blocks)
+            self.bytes_received += res.numel() * res.element_size()
+            if padded:
+                return boxes, scores, valid, res, count
+            return boxes, scores, valid, res[: int(count.item())]
+
         for imgs in batches:
             _, boxes, scores, valid, crops, count = self._det_graph(imgs)
             boxes, scores, valid = boxes.clone(), scores.clone(), valid.clone()  # (graph outputs are reused)
-            n = int(count.item())
             if self.world == 1:
-                out.append((boxes, scores, valid, self.classify(crops[:n])))
+                if padded:
+                    res = torch.zeros(crops.shape[0], 2, device=self.device)
+                    n = int(count.item())
+                    res[:n] = self.classify(crops[:n])
+                    out.append((boxes, scores, valid, res, count.clone()))
+                else:
+                    out.append((boxes, scores, valid, self.classify(crops[: int(count.item())])))
                 continue
-            works = self._send(crops, n)
+            rw, res = self._send(crops, count)
             if pending is not None:
-                out.append(pending[:3] + (self._recv_results(pending[3]),))
-            for w, _ in inflight:
-                w.wait()
-            inflight, pending = works, (boxes, scores, valid, n)
+                out.append(finish(pending))
+            pending = (boxes, scores, valid, count.clone(), rw, res)
         if pending is not None:
-            out.append(pending[:3] + (self._recv_results(pending[3]),))
-        for w, _ in inflight:
-            w.wait()
+            out.append(finish(pending))
         return out
 
     def stop(self) -> None:
         if self.world > 1 and self.is_detector:
-            dist.send(torch.tensor([STOP], dtype=torch.int64, device=self.device), group_dst=self.peer, group=self.group)
+            for ws in getattr(self, "_buf_works", []):
+                for w in ws:
+                    w.wait()
+            dist.send(torch.tensor([STOP, 0], dtype=torch.int64, device=self.device), group_dst=self.peer,
+                      group=self.group)
 
     # ------------------------------------------------------------ classifier stage
     def _classify_static(self, crops_u8: torch.Tensor) -> torch.Tensor:
@@ -312,40 +345,41 @@ class StageGraphPipeline:
         return self._cls_graph(crops)[:n].clone()
 
     def _headers(self):
-        """Yield (detector, n) as headers arrive from the detectors this rank serves: one posted ``irecv`` per
-        detector, polled (``_Completion``: an event query on RCCL, a waiter thread on gloo — the same loop on both),
-        so an idle detector never blocks a busy one. A detector's next header is posted only after its crops were
-        received, so every posted receive matches a header."""
-        blocking = dist.get_backend(self.group) == "gloo"
-        hdrs = {d: torch.zeros(1, dtype=torch.int64, device=self.device) for d in self.serves}
+        """Yield (detector, count, capacity) as headers arrive from the detectors this rank serves: one posted
+        ``irecv`` per detector, completed event-driven (``_Arrivals``), so an idle detector never blocks a busy one.
+        A detector's next header is posted only after its crops were received, so every posted receive matches a
+        header."""
+        arrivals = _Arrivals(self.device, dist.get_backend(self.group) == "gloo")
+        hdrs = {d: torch.zeros(2, dtype=torch.int64, device=self.device) for d in self.serves}
 
         def post(d):
-            return _Completion(dist.irecv(hdrs[d], group_src=d, group=self.group), blocking)
-        posted = {d: post(d) for d in self.serves}
-        while posted:
-            ready = [d for d, c in posted.items() if c.done()]
-            if not ready:
-                time.sleep(0.0002)
-                continue
-            for d in ready:
-                posted.pop(d).wait()
-                n = int(hdrs[d].item())
-                yield d, n  # (the crops are received before this detector's next header is posted)
-                if n != STOP:
-                    posted[d] = post(d)
+            arrivals.post(d, dist.irecv(hdrs[d], group_src=d, group=self.group))
+        for d in self.serves:
+            post(d)
+        live = len(self.serves)
+        while live:
+            d = arrivals.next()
+            n, cap = (int(v) for v in hdrs[d].tolist())
+            yield d, n, cap  # (the crops are received before this detector's next header is posted)
+            if n == STOP:
+                live -= 1
+            else:
+                post(d)
 
     def serve(self) -> int:
         """Classifier rank loop; returns the number of crops classified."""
         h, w = self.cfg.crop_hw
         total = 0
-        for d, n in self._headers():
-            if n == STOP or n == 0:
+        for d, n, cap in self._headers():
+            if n == STOP:
                 continue
-            crops = torch.empty(n, h, w, 3, dtype=self.wire_dtype, device=self.device)
+            crops = torch.empty(cap, h, w, 3, dtype=self.wire_dtype, device=self.device)
             dist.recv(crops, group_src=d, group=self.group)
             self.bytes_received += crops.numel() * crops.element_size()
-            res = self.classify(crops)
-            dist.send(res.contiguous(), group_dst=d, group=self.group)
+            res = torch.zeros(cap, 2, device=self.device)
+            if n:
+                res[:n] = self.classify(crops[:n])
+            dist.send(res, group_dst=d, group=self.group)
             self.bytes_sent += res.numel() * res.element_size()
             total += n
         return total

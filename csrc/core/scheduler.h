@@ -38,6 +38,7 @@
 #include <fcntl.h>
 #include <sys/mman.h>
 #include <sys/socket.h>
+#include <sys/uio.h>
 #include <unistd.h>
 
 #include <atomic>
@@ -450,24 +451,86 @@ class NodeScheduler {
     }
     return true;
   }
-  static bool read_frame(int fd, std::string& out) {
-    int32_t be;
-    if (!read_exact(fd, &be, 4)) return false;
-    int64_t len = static_cast<int32_t>(ntohl(static_cast<uint32_t>(be)));
-    if (len == -1) {  // multiprocessing's >2 GiB form: 8-byte big-endian length follows
-      uint64_t be8;
-      if (!read_exact(fd, &be8, 8)) return false;
-      len = static_cast<int64_t>(be64toh(be8));
+  // Buffered frame reader of one connection: one recv() usually brings several small frames (SUBMIT_IDS of many
+  // front-end requests, heartbeats, DONE headers), each then parsed without a syscall of its own.
+  struct FrameReader {
+    int fd;
+    std::vector<char> buf = std::vector<char>(1 << 18);
+    size_t pos = 0, end = 0;
+    bool fill(size_t need) {  // at least `need` unread bytes buffered
+      if (end - pos >= need) return true;
+      if (pos) {
+        std::memmove(buf.data(), buf.data() + pos, end - pos);
+        end -= pos;
+        pos = 0;
+      }
+      if (need > buf.size()) buf.resize(need);
+      while (end < need) {
+        const ssize_t k = ::recv(fd, buf.data() + end, buf.size() - end, 0);
+        if (k == 0) return false;
+        if (k < 0) {
+          if (errno == EINTR) continue;
+          return false;
+        }
+        end += static_cast<size_t>(k);
+      }
+      return true;
     }
-    if (len < 4) return false;
-    out.resize(static_cast<size_t>(len));
-    return read_exact(fd, out.data(), out.size());
-  }
+    bool next(std::string& out) {
+      if (!fill(4)) return false;
+      int32_t be;
+      std::memcpy(&be, buf.data() + pos, 4);
+      int64_t len = static_cast<int32_t>(ntohl(static_cast<uint32_t>(be)));
+      size_t hdr = 4;
+      if (len == -1) {  // multiprocessing's >2 GiB form: 8-byte big-endian length follows
+        if (!fill(12)) return false;
+        uint64_t be8;
+        std::memcpy(&be8, buf.data() + pos + 4, 8);
+        len = static_cast<int64_t>(be64toh(be8));
+        hdr = 12;
+      }
+      if (len < 4) return false;
+      if (static_cast<size_t>(len) > (1u << 20)) {  // a large frame (a DONE of big result rows): straight into `out`
+        out.resize(static_cast<size_t>(len));
+        const size_t have = std::min(end - pos - hdr, out.size());
+        std::memcpy(out.data(), buf.data() + pos + hdr, have);
+        pos = end = 0;
+        return have == out.size() || read_exact(fd, out.data() + have, out.size() - have);
+      }
+      if (!fill(hdr + static_cast<size_t>(len))) return false;
+      out.assign(buf.data() + pos + hdr, static_cast<size_t>(len));
+      pos += hdr + static_cast<size_t>(len);
+      return true;
+    }
+  };
   bool send_frame(Worker& w, const std::string& payload) {
     std::lock_guard<std::mutex> g(w.send_mu);
     if (w.fd < 0) return false;
-    const uint32_t be = htonl(static_cast<uint32_t>(payload.size()));
-    return write_all(w.fd, &be, 4) && write_all(w.fd, payload.data(), payload.size());
+    uint32_t be = htonl(static_cast<uint32_t>(payload.size()));
+    struct iovec iov[2] = {{&be, 4}, {const_cast<char*>(payload.data()), payload.size()}};
+    size_t left = 4 + payload.size();
+    int idx = 0;
+    while (left) {  // one sendmsg for the length prefix and the payload (partial writes resume mid-iovec)
+      msghdr mh{};
+      mh.msg_iov = iov + idx;
+      mh.msg_iovlen = static_cast<size_t>(2 - idx);
+      const ssize_t k = ::sendmsg(w.fd, &mh, MSG_NOSIGNAL);
+      if (k < 0) {
+        if (errno == EINTR) continue;
+        return false;
+      }
+      size_t kk = static_cast<size_t>(k);
+      left -= kk;
+      while (idx < 2 && kk >= iov[idx].iov_len) {
+        kk -= iov[idx].iov_len;
+        ++idx;
+      }
+      if (idx < 2) {
+        iov[idx].iov_base = static_cast<char*>(iov[idx].iov_base) + kk;
+        iov[idx].iov_len -= kk;
+      }
+    }
+    return true;
   }
   bool send_simple(Worker& w, uint32_t type) {
     std::string p(4, '\0');
@@ -812,8 +875,9 @@ class NodeScheduler {
 
   void reader_loop(Worker& w) {
     std::string f;
+    FrameReader rd{w.fd};
     while (true) {
-      if (!read_frame(w.fd, f)) {
+      if (!rd.next(f)) {
         // an ingest front-end that went away (killed mid-upload) leaves no admitted-body backlog behind
         if (!w.dispatch && stat_ && w.rank >= kFrontendRank0 && w.rank - kFrontendRank0 < kStatFrontends)
           stat_->fe_pending[w.rank - kFrontendRank0].store(0);

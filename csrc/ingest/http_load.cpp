@@ -29,7 +29,9 @@
 #include <cerrno>
 #include <chrono>
 #include <cstdio>
+#include <csignal>
 #include <cstdlib>
+#include <random>
 #include <cstring>
 #include <fstream>
 #include <mutex>
@@ -214,6 +216,7 @@ bool send_req(Link& l, const struct iovec* iov, const std::string& whole) {
 }  // namespace
 
 int main(int argc, char** argv) {
+  signal(SIGPIPE, SIG_IGN);  // (a refused body the server closed on: the send fails, the answer is still read)
   if (argc < 10) {
     std::fprintf(stderr,
                  "usage: ai4e_http_load HOST PORT PATH CONTENT_TYPE BODY_FILE CONNS SECONDS START_AT IDS_OUT "
@@ -239,7 +242,8 @@ int main(int argc, char** argv) {
                      "\r\nContent-Type: " + ctype + "\r\nContent-Length: " + std::to_string(body.size()) + "\r\n";
   for (int i = 10; i < argc; ++i) head += std::string(argv[i]) + "\r\n";
   // (curl sends Expect for bodies past 1 MiB; 64 KiB here, so a refused camera frame costs its headers, not its body)
-  const bool expect = body.size() >= (64u << 10);
+  const char* emin = std::getenv("AI4E_HTTP_EXPECT_MIN");  // (bytes; A/B knob)
+  const bool expect = body.size() >= (emin ? std::strtoull(emin, nullptr, 10) : (64u << 10));
   if (expect) head += "Expect: 100-continue\r\n";
   head += "\r\n";
   const std::string whole = g_tls ? head + body : std::string();  // (TLS: one SSL_write per request)
@@ -252,6 +256,20 @@ int main(int argc, char** argv) {
     th.emplace_back([&, c] {
       Result& r = res[static_cast<size_t>(c)];
       Link l = dial(host, port);
+      // a refused request waits the server's hint, doubled for every further refusal in a row (capped at 100 ms),
+      // with +-25 % jitter so refused clients do not all return at once; an admitted request resets it
+      std::mt19937 rng(static_cast<unsigned>(c) * 7919u + 17u);
+      int refusals = 0;
+      const int64_t ok0 = -1;
+      int64_t seen_ok = ok0;
+      auto backoff = [&](double hint_ms) {
+        if (static_cast<int64_t>(r.ok) != seen_ok) refusals = 0;
+        seen_ok = static_cast<int64_t>(r.ok);
+        const double base = std::max(0.5, hint_ms) * static_cast<double>(1u << std::min(refusals, 8));
+        ++refusals;
+        const double ms = std::min(100.0, base) * std::uniform_real_distribution<double>(0.75, 1.25)(rng);
+        std::this_thread::sleep_for(std::chrono::microseconds(static_cast<long>(ms * 1e3)));
+      };
       std::string buf, rbody;
       struct iovec iov[2] = {{const_cast<char*>(head.data()), head.size()},
                              {const_cast<char*>(body.data()), body.size()}};
@@ -276,8 +294,7 @@ int main(int argc, char** argv) {
           }
           if (st == 429) {
             ++r.busy;
-            const double ms = std::min(100.0, std::max(0.5, retry_ms));
-            std::this_thread::sleep_for(std::chrono::microseconds(static_cast<long>(ms * 1e3)));
+            backoff(retry_ms);
           } else {
             ++r.errors;
           }
@@ -298,8 +315,7 @@ int main(int argc, char** argv) {
         if (!sent && st != 429) st = 0;
         if (st == 429 && (closes || !sent)) {  // refused unread: back off, then dial again
           ++r.busy;
-          const double ms = std::min(100.0, std::max(0.5, retry_ms));
-          std::this_thread::sleep_for(std::chrono::microseconds(static_cast<long>(ms * 1e3)));
+          backoff(retry_ms);
           l.close();
           buf.clear();
           l = dial(host, port);
@@ -317,8 +333,7 @@ int main(int argc, char** argv) {
           extract_ids(rbody, r.ids);
         } else if (st == 429) {  // admission refused: back off for the server's projected wait, then retry
           ++r.busy;
-          const double ms = std::min(100.0, std::max(0.5, retry_ms));
-          std::this_thread::sleep_for(std::chrono::microseconds(static_cast<long>(ms * 1e3)));
+          backoff(retry_ms);
         } else {
           ++r.errors;
         }

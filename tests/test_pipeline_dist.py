@@ -43,7 +43,18 @@ def _worker(rank, world, leaders, port, q):
     p = StageGraphPipeline(det if rank < leaders else None, cls if rank >= leaders else None, torch.device("cpu"), CFG,
                            n_leaders=leaders)
     if p.is_detector:
-        out = p.run_batches(_batches(rank))
+        # the serving form (padded=True) never reads a device value on the host: every hand-off is stream-ordered
+        # behind the detector's graph replay (no count.item() between replays)
+        real_item, real_tolist = torch.Tensor.item, torch.Tensor.tolist
+
+        def no_host_read(*a, **k):
+            raise AssertionError("host read of a device value on the detector's hand-off path")
+        torch.Tensor.item, torch.Tensor.tolist = no_host_read, no_host_read
+        try:
+            padded = p.run_batches(_batches(rank), padded=True)
+        finally:
+            torch.Tensor.item, torch.Tensor.tolist = real_item, real_tolist
+        out = [(b, s_, v, r[: int(c.item())]) for b, s_, v, r, c in padded]
         p.stop()
         # numpy copies travel by value: a torch tensor would go through a shared-memory fd that the parent may only
         # open after this process has exited (FileNotFoundError in the resource sharer, a flaky failure)
