@@ -126,6 +126,10 @@ def run_native_clients(url: str, seconds: float, conc: int, body: bytes, content
         out["client_cpu_s"] += st["cpu_user_s"] + st["cpu_sys_s"]
         with open(os.path.join(tmp, f"ids{i}.txt")) as f:
             out["ids"] += [l.strip() for l in f if l.strip()]
+        lp = os.path.join(tmp, f"ids{i}.txt.lat")
+        if os.path.exists(lp):
+            with open(lp) as f:
+                out.setdefault("request_latency_ms", []).extend(float(l) for l in f if l.strip())
     for name in os.listdir(tmp):
         os.unlink(os.path.join(tmp, name))
     os.rmdir(tmp)

@@ -194,6 +194,10 @@ def http_phase(cp, pool, seconds: float, batch: int, item_shape, path: str, fron
                                            "frontends": round(s1[1] - s0[1], 3)}
         if res:
             out[name]["client_cpu_s"] = round(res["client_cpu_s"], 3)
+            rl = sorted(res.get("request_latency_ms") or [])
+            if rl:  # what a client sees: first attempt -> 2xx, including 429 back-offs and retries
+                out[name]["p50_request_latency_ms"] = round(percentile(rl, 50), 3)
+                out[name]["p99_request_latency_ms"] = round(percentile(rl, 99), 3)
             out[name]["request_gbytes_per_s"] = round(res["bytes_sent"] / max(1e-9, res["t1"] - res["t0"]) / 1e9, 3)
         if is_batch:
             out[name]["request_images"] = batch

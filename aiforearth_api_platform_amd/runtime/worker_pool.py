@@ -193,9 +193,12 @@ class WorkerPool:
                  max_restarts: int = 2, pipeline_depth: int = 3, retry_delay_s: float = 1.0,
                  remote_partitions: Sequence[Tuple[int, int, int]] = (), completion_feed: bool = False,
                  poll_s: float = 0.02, frontends: int = 0, frontend_slots: int = 0,
-                 shard: Optional["ShardLayout"] = None, durable=None):
-        """``shard``: this pool is one control-plane shard of a :class:`ShardedWorkerPool` (its own dispatch queue
-        and scheduler, a partition of the shared ring, ids minted in its own task-store lock domains)."""
+                 shard: Optional["ShardLayout"] = None, durable=None, busy_delay_s: float = 0.002):
+        """``max_delay_s``: how long a batch waits to fill when the worker is idle; ``busy_delay_s``: when it already
+        has a batch in flight (its GPU is busy: a fuller batch costs no throughput, and arrivals of single images
+        otherwise leave as many small batches, each in a padded graph bucket). ``shard``: this pool is one
+        control-plane shard of a :class:`ShardedWorkerPool` (its own dispatch queue and scheduler, a partition of the
+        shared ring, ids minted in its own task-store lock domains)."""
         if native is None:
             raise RuntimeError("the worker pool needs the native core (_ai4e_core)")
         self.cp = control_plane
@@ -232,7 +235,8 @@ class WorkerPool:
         self.max_restarts = max_restarts
         self.sched = native.NodeScheduler(self.store, self.queue, endpoint, total, max_batch=spec.max_batch,
                                           linger_s=max_delay_s, depth=pipeline_depth, retry_delay_s=retry_delay_s,
-                                          hb_timeout_s=heartbeat_timeout_s, poll_s=poll_s)
+                                          hb_timeout_s=heartbeat_timeout_s, poll_s=poll_s,
+                                          busy_linger_s=busy_delay_s)
         self.sched.add_local_ring(self.ring.slots)
         tags = getattr(getattr(self.ring, "parent", self.ring), "tags_name", "")
         if tags and not self.sched.set_slot_tags(tags):

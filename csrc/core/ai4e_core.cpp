@@ -258,10 +258,11 @@ PYBIND11_MODULE(_ai4e_core, m) {
   py::class_<NodeScheduler, std::shared_ptr<NodeScheduler>>(m, "NodeScheduler")
       .def(py::init([](std::shared_ptr<TaskStore> store, std::shared_ptr<DispatchQueue> queue, std::string endpoint,
                        int64_t ring_slots, size_t max_batch, double linger_s, int depth, double retry_delay_s,
-                       double hb_timeout_s, double poll_s) {
+                       double hb_timeout_s, double poll_s, double busy_linger_s) {
              SchedConfig c;
              c.max_batch = max_batch;
              c.linger_s = linger_s;
+             c.busy_linger_s = busy_linger_s;
              c.depth = depth;
              c.retry_delay_s = retry_delay_s;
              c.hb_timeout_s = hb_timeout_s;
@@ -271,7 +272,7 @@ PYBIND11_MODULE(_ai4e_core, m) {
            }),
            py::arg("store"), py::arg("queue"), py::arg("endpoint"), py::arg("ring_slots"), py::arg("max_batch") = 250,
            py::arg("linger_s") = 0.0005, py::arg("depth") = 2, py::arg("retry_delay_s") = 1.0,
-           py::arg("hb_timeout_s") = 10.0, py::arg("poll_s") = 0.02)
+           py::arg("hb_timeout_s") = 10.0, py::arg("poll_s") = 0.02, py::arg("busy_linger_s") = 0.0)
       .def("add_local_ring", &NodeScheduler::add_local_ring)
       .def("add_remote_partition", &NodeScheduler::add_remote_partition)
       .def("set_stage_endpoints", &NodeScheduler::set_stage_endpoints)

@@ -24,6 +24,9 @@
 //          char ids[n][id_len], trace   (an ingest front-end process enqueued n payloads under task ids it
 //          minted; flags bit 0: answer with SUBMITTED once the tasks exist, so its HTTP reply never races them)
 //   SUBMITTED (s->w) u64 token, u32 n_created, u32 0
+//   SUBMIT_MULTI (w->s) u32 nreq, u64 token, then per request u32 n, u32 trace_len, u32 id_len, u32 0, i64 slots[n],
+//          char ids[n][id_len], trace   (a front-end's group commit: the requests of several client connections)
+//   SUBMITTED_MULTI (s->w) u64 token, u32 nreq, u32 created[nreq]
 //   STAGE  (w->s) u64 bid, u32 stage, u32 0        (ensemble hop: AddPipelineTask for the batch)
 //
 // Item status in DONE: 0 ok, 1 invalid payload (failed, not retried), 2 model error (failed,
@@ -72,7 +75,7 @@ inline bool cv_wait_s(std::condition_variable& cv, std::unique_lock<std::mutex>&
 
 enum : uint32_t {
   F_READY = 1, F_HB = 2, F_DONE = 3, F_BATCH = 4, F_STOP = 5, F_SUBMIT = 6, F_FREE = 7, F_STAGE = 8, F_SUBMIT_IDS = 9,
-  F_SUBMITTED = 10
+  F_SUBMITTED = 10, F_SUBMIT_MULTI = 11, F_SUBMITTED_MULTI = 12
 };
 enum : uint8_t { IT_OK = 0, IT_INVALID = 1, IT_ERROR = 2, IT_RETRY = 3 };
 
@@ -85,6 +88,9 @@ static const char* kPublishFailed = "Failed - unable to send to backend service.
 struct SchedConfig {
   size_t max_batch = 250;
   double linger_s = 0.0005;
+  // linger while the worker already has a batch in flight: its GPU is busy anyway, so a fuller batch costs no
+  // throughput (single-image arrivals otherwise leave as many small batches, each run in a padded graph bucket)
+  double busy_linger_s = 0.0;
   int depth = 2;               // batches in flight per worker
   double retry_delay_s = 1.0;  // abandon delay for IT_RETRY items
   double hb_timeout_s = 10.0;
@@ -601,6 +607,40 @@ class NodeScheduler {
 
   // SUBMIT_IDS: the front-end already answered its clients with these ids; a payload whose id could not be
   // created (duplicate) or queued is dropped and its slot freed.
+  // SUBMIT_MULTI: every request's records (each with its own trace), then ONE tag pass, journal flush and queue
+  // send for all of them. Returns the tasks created per request.
+  std::vector<uint32_t> enqueue_ids_multi(std::vector<std::vector<int64_t>>& slots, std::vector<std::vector<std::string>>& ids,
+                                          const std::vector<std::string>& traces) {
+    std::vector<uint32_t> created(slots.size(), 0);
+    std::vector<int64_t> all_slots, drop;
+    std::vector<std::string> all_ids;
+    for (size_t r = 0; r < slots.size(); ++r) {
+      auto ok = store_->create_ids(endpoint_, ids[r], "created", traces[r]);
+      for (size_t i = 0; i < ids[r].size(); ++i) {
+        if (!ok[i]) {
+          drop.push_back(slots[r][i]);
+          continue;
+        }
+        all_ids.push_back(std::move(ids[r][i]));
+        all_slots.push_back(slots[r][i]);
+        ++created[r];
+      }
+    }
+    free_slots(drop);
+    tag_slots(all_ids, all_slots);
+    if (store_->journaled()) store_->flush();
+    const size_t sent = queue_->send_many(all_ids, all_slots);
+    if (stat_) stat_->enq.fetch_add(sent);
+    if (sent < all_ids.size()) {
+      std::vector<std::string> rest(all_ids.begin() + static_cast<long>(sent), all_ids.end());
+      std::vector<int64_t> rs(all_slots.begin() + static_cast<long>(sent), all_slots.end());
+      store_->transition_many(rest, "failed", kPublishFailed);
+      free_slots(rs);
+      feed(rest);
+    }
+    return created;
+  }
+
   size_t enqueue_ids(std::vector<int64_t> slots, std::vector<std::string> ids, const std::string& trace) {
     auto ok = store_->create_ids(endpoint_, ids, "created", trace);
     std::vector<int64_t> drop;
@@ -741,6 +781,7 @@ class NodeScheduler {
   // ------------------------------------------------------------------ threads
   void dispatch_loop(Worker& w) {
     while (w.alive) {
+      bool busy = false;
       {
         std::unique_lock<std::mutex> lk(w.mu);
         cv_wait_s(w.cv, lk, 0.05, [&] {
@@ -753,6 +794,7 @@ class NodeScheduler {
           break;
         }
         if (!w.ready || w.draining || w.out.size() >= static_cast<size_t>(cfg_.depth)) continue;
+        busy = !w.out.empty();
       }
       if (queue_->closed()) {
         std::this_thread::sleep_for(std::chrono::milliseconds(20));
@@ -761,7 +803,8 @@ class NodeScheduler {
       std::shared_ptr<NodeScheduler> src;
       auto msgs = take_orphaned(src);
       if (msgs.empty()) {
-        msgs = queue_->receive(cfg_.max_batch, cfg_.poll_s, cfg_.linger_s);
+        msgs = queue_->receive(cfg_.max_batch, cfg_.poll_s,
+                               busy ? std::max(cfg_.linger_s, cfg_.busy_linger_s) : cfg_.linger_s);
         if (msgs.empty()) msgs = take_idle(src);
       }
       if (msgs.empty()) continue;
@@ -962,6 +1005,60 @@ class NodeScheduler {
             std::memcpy(&ack[16], &z, 4);
             send_frame(w, ack);
           }
+          break;
+        }
+        case F_SUBMIT_MULTI: {
+          if (len < 12) break;
+          uint32_t nreq;
+          uint64_t token;
+          std::memcpy(&nreq, p, 4);
+          std::memcpy(&token, p + 4, 8);
+          std::vector<std::vector<int64_t>> slots;
+          std::vector<std::vector<std::string>> ids;
+          std::vector<std::string> traces;
+          slots.reserve(nreq);
+          ids.reserve(nreq);
+          traces.reserve(nreq);
+          size_t off = 12;
+          bool bad = false;
+          for (uint32_t r = 0; r < nreq && !bad; ++r) {
+            if (len < off + 16) {
+              bad = true;
+              break;
+            }
+            uint32_t n, tl, il;
+            std::memcpy(&n, p + off, 4);
+            std::memcpy(&tl, p + off + 4, 4);
+            std::memcpy(&il, p + off + 8, 4);
+            off += 16;
+            if (len < off + n * (8ull + il) + tl) {
+              bad = true;
+              break;
+            }
+            std::vector<int64_t> sl(n);
+            if (n) std::memcpy(sl.data(), p + off, n * 8ull);
+            off += n * 8ull;
+            std::vector<std::string> rid(n);
+            for (uint32_t i = 0; i < n; ++i) rid[i].assign(p + off + i * static_cast<size_t>(il), il);
+            off += n * static_cast<size_t>(il);
+            traces.emplace_back(p + off, tl);
+            off += tl;
+            if (!in_partition(w.rank, sl)) {  // (outside the sender's partition: this request creates nothing)
+              sl.clear();
+              rid.clear();
+            }
+            slots.push_back(std::move(sl));
+            ids.push_back(std::move(rid));
+          }
+          if (bad) break;  // malformed: ignore
+          const auto created = enqueue_ids_multi(slots, ids, traces);
+          std::string ack(16 + 4 * created.size(), '\0');
+          const uint32_t t = F_SUBMITTED_MULTI, nr = static_cast<uint32_t>(created.size());
+          std::memcpy(&ack[0], &t, 4);
+          std::memcpy(&ack[4], &token, 8);
+          std::memcpy(&ack[12], &nr, 4);
+          if (nr) std::memcpy(&ack[16], created.data(), 4ull * nr);
+          send_frame(w, ack);
           break;
         }
         case F_STAGE: {

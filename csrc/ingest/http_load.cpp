@@ -76,6 +76,7 @@ struct Result {
   long requests = 0, ok = 0, errors = 0, busy = 0;
   double bytes = 0;
   std::vector<std::string> ids;
+  std::vector<float> lat_ms;  // per admitted request: first attempt -> 2xx, 429 back-offs and retries included
 };
 
 bool send_all(int fd, const struct iovec* iov0, int cnt) {
@@ -262,6 +263,7 @@ int main(int argc, char** argv) {
       int refusals = 0;
       const int64_t ok0 = -1;
       int64_t seen_ok = ok0;
+      double t_first = -1.0;  // start of the current logical request (kept across its 429 retries)
       auto backoff = [&](double hint_ms) {
         if (static_cast<int64_t>(r.ok) != seen_ok) refusals = 0;
         seen_ok = static_cast<int64_t>(r.ok);
@@ -274,6 +276,7 @@ int main(int argc, char** argv) {
       struct iovec iov[2] = {{const_cast<char*>(head.data()), head.size()},
                              {const_cast<char*>(body.data()), body.size()}};
       while (l.fd >= 0 && now() < t_end) {
+        if (t_first < 0) t_first = now();
         if (expect) {
           // headers, then the body only once the server's admission let the request in
           double retry_ms = 0;
@@ -290,6 +293,8 @@ int main(int argc, char** argv) {
           if (st >= 200 && st < 300) {
             ++r.ok;
             extract_ids(rbody, r.ids);
+            r.lat_ms.push_back(static_cast<float>((now() - t_first) * 1e3));
+            t_first = -1.0;
             continue;
           }
           if (st == 429) {
@@ -331,6 +336,8 @@ int main(int argc, char** argv) {
         if (st >= 200 && st < 300) {
           ++r.ok;
           extract_ids(rbody, r.ids);
+          r.lat_ms.push_back(static_cast<float>((now() - t_first) * 1e3));
+          t_first = -1.0;
         } else if (st == 429) {  // admission refused: back off for the server's projected wait, then retry
           ++r.busy;
           backoff(retry_ms);
@@ -355,6 +362,12 @@ int main(int argc, char** argv) {
       for (auto& id : r.ids) std::fprintf(f, "%s\n", id.c_str());
   }
   if (f) std::fclose(f);
+  FILE* lf = std::fopen((std::string(ids_out) + ".lat").c_str(), "w");  // request latencies, ms, one per line
+  if (lf) {
+    for (auto& r : res)
+      for (float v : r.lat_ms) std::fprintf(lf, "%.3f\n", v);
+    std::fclose(lf);
+  }
   struct rusage ru {};
   getrusage(RUSAGE_SELF, &ru);
   std::printf(

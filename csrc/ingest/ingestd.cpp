@@ -65,7 +65,8 @@
 
 namespace {
 
-constexpr uint32_t F_STOP = 5, F_FREE = 7, F_SUBMIT_IDS = 9, F_SUBMITTED = 10;
+constexpr uint32_t F_STOP = 5, F_FREE = 7, F_SUBMIT_IDS = 9, F_SUBMITTED = 10, F_SUBMIT_MULTI = 11,
+                   F_SUBMITTED_MULTI = 12;
 const char* kBatchType = "application/x-ai4e-batch";
 const char* kRawType = "application/octet-stream";
 const char* kKeyHeader = "ocp-apim-subscription-key";
@@ -150,6 +151,17 @@ std::string hexid(std::mt19937_64& rng, int bits) {
 struct Ack {
   bool done = false;
   uint32_t n = 0;
+  std::vector<uint32_t> per;  // SUBMITTED_MULTI: tasks created per request of the frame
+};
+
+// One request's ingest waiting to be submitted (group commit: the connection threads of a shard queue their
+// requests and one of them — whoever finds no frame in flight — sends every queued request in ONE SUBMIT_MULTI frame
+// and hands each its own created count from the one SUBMITTED_MULTI answer)
+struct PendingSubmit {
+  const std::vector<int64_t>* sl;
+  const std::vector<std::string>* ids;
+  std::string trace;
+  int64_t created = -2;  // -2 pending, -1 ack timed out, else tasks created
 };
 
 struct Shard {
@@ -316,6 +328,86 @@ struct Shard {
     return tok;
   }
 
+  // Group commit (see PendingSubmit): queue this request; the first thread to find no frame in flight sends every
+  // queued request in one frame and waits for its answer, then the next group goes. Under load one scheduler frame and
+  // one answer carry many requests (one scheduler wake-up, one journal flush, one queue notify for all of them)
+  // instead of one frame and one answer each; alone, a request goes out at once as before.
+  std::mutex gc_mu;
+  std::condition_variable gc_cv;
+  std::vector<PendingSubmit*> gc_q;
+  bool gc_busy = false;
+  int64_t submit_wait(const std::vector<int64_t>& sl, const std::vector<std::string>& ids, std::string trace,
+                      double timeout_s) {
+    PendingSubmit me{&sl, &ids, std::move(trace)};
+    std::unique_lock<std::mutex> lk(gc_mu);
+    gc_q.push_back(&me);
+    while (me.created == -2) {
+      if (gc_busy) {
+        gc_cv.wait(lk);
+        continue;
+      }
+      gc_busy = true;
+      std::vector<PendingSubmit*> group;
+      group.swap(gc_q);
+      lk.unlock();
+      std::vector<int64_t> got;
+      if (group.size() == 1) {
+        const PendingSubmit& p = *group[0];
+        got.push_back(wait_ack(submit(*p.sl, *p.ids, p.trace), timeout_s));
+      } else {
+        got = wait_ack_multi(submit_multi(group), group.size(), timeout_s);
+      }
+      lk.lock();
+      for (size_t i = 0; i < group.size(); ++i) group[i]->created = got[i];
+      gc_busy = false;
+      gc_cv.notify_all();
+    }
+    return me.created;
+  }
+
+  // SUBMIT_MULTI: u32 type, u32 nreq, u64 token | per request: u32 n, u32 trace_len, u32 id_len, u32 0,
+  // i64 slots[n], ids, trace
+  uint64_t submit_multi(const std::vector<PendingSubmit*>& group) {
+    const uint64_t tok = token.fetch_add(1);
+    {
+      std::lock_guard<std::mutex> g(ack_mu);
+      acks[tok] = Ack{};
+    }
+    size_t bytes = 20;
+    for (auto* p : group)
+      bytes += 16 + 8 * p->sl->size() + (p->ids->empty() ? 0 : p->ids->size() * (*p->ids)[0].size()) + p->trace.size();
+    std::string f(4, '\0');  // (length prefix, filled by send_frame)
+    f.reserve(bytes);
+    auto put32 = [&](uint32_t v) { f.append(reinterpret_cast<const char*>(&v), 4); };
+    put32(F_SUBMIT_MULTI);
+    put32(static_cast<uint32_t>(group.size()));
+    f.append(reinterpret_cast<const char*>(&tok), 8);
+    for (auto* p : group) {
+      const uint32_t n = static_cast<uint32_t>(p->sl->size());
+      put32(n);
+      put32(static_cast<uint32_t>(p->trace.size()));
+      put32(p->ids->empty() ? 0 : static_cast<uint32_t>((*p->ids)[0].size()));
+      put32(0);
+      f.append(reinterpret_cast<const char*>(p->sl->data()), 8 * p->sl->size());
+      for (auto& id : *p->ids) f += id;
+      f += p->trace;
+    }
+    if (!send_frame(f)) std::_Exit(0);  // the serving process is gone
+    return tok;
+  }
+
+  std::vector<int64_t> wait_ack_multi(uint64_t tok, size_t nreq, double timeout_s) {
+    std::unique_lock<std::mutex> lk(ack_mu);
+    const auto deadline = std::chrono::system_clock::now() + std::chrono::duration_cast<std::chrono::system_clock::duration>(
+                                                                  std::chrono::duration<double>(timeout_s));
+    const bool ok = ack_cv.wait_until(lk, deadline, [&] { return acks[tok].done; });
+    std::vector<int64_t> out(nreq, -1);
+    if (ok)
+      for (size_t i = 0; i < nreq && i < acks[tok].per.size(); ++i) out[i] = acks[tok].per[i];
+    acks.erase(tok);
+    return out;
+  }
+
   // -1: timed out (the tasks may still be created), else tasks created
   int64_t wait_ack(uint64_t tok, double timeout_s) {
     std::unique_lock<std::mutex> lk(ack_mu);
@@ -392,6 +484,21 @@ struct Shard {
           it->second.n = cnt;
         }
         ack_cv.notify_all();
+      } else if (type == F_SUBMITTED_MULTI && len >= 16) {  // u32 type, u64 token, u32 nreq, u32 created[nreq]
+        uint64_t tok;
+        uint32_t nreq;
+        std::memcpy(&tok, buf.data() + 4, 8);
+        std::memcpy(&nreq, buf.data() + 12, 4);
+        if (16 + 4ull * nreq <= len) {
+          std::lock_guard<std::mutex> g(ack_mu);
+          auto it = acks.find(tok);
+          if (it != acks.end()) {
+            it->second.per.resize(nreq);
+            if (nreq) std::memcpy(it->second.per.data(), buf.data() + 16, 4ull * nreq);
+            it->second.done = true;
+          }
+          ack_cv.notify_all();
+        }
       } else if (type == F_STOP) {
         break;
       }
@@ -416,6 +523,7 @@ struct Config {
   int internal_port = 0;
   double ack_timeout = 30.0, alloc_timeout = 60.0;
   double max_queue_s = 0.0;  // latency budget of an ingested request's queue wait (0: no budget, wait for slots)
+  double hold_s = -1.0;      // longest wait at the door before a 429 (< 0: one budget)
   int ready_fd = -1;  // "ready FD": one byte written once the public socket listens (the parent hands the port over)
   int frontend_index = -1;  // "frontend_index I": this process's word in every shard's counters
   std::vector<std::string> keys;
@@ -469,6 +577,10 @@ void parse_config(const char* path) {
       ls >> g_cfg.ready_fd;
     } else if (kw == "frontend_index") {
       ls >> g_cfg.frontend_index;
+    } else if (kw == "hold_ms") {
+      double ms = 0;
+      ls >> ms;
+      g_cfg.hold_s = ms / 1e3;
     } else if (kw == "max_queue_ms") {
       double ms = 0;
       ls >> ms;
@@ -980,8 +1092,27 @@ bool ingest(Conn& c, const Request& r, Route& route, Shard& s, bool batch) {
     // latency-budgeted admission (the reference's busy path: BackendQueueProcessor.cs:54-64 answers 429 and the
     // message is retried later; ai4e_service.py:122-125): a request whose projected queue wait exceeds the budget is
     // refused with 429 + Retry-After instead of queueing behind a deep ring
-    const double wait = s.projected_wait(n, static_cast<double>(nbytes));
+    double wait = s.projected_wait(n, static_cast<double>(nbytes));
+    // A request only a little over the budget waits at the door — before its body is read and before any task
+    // exists — for the backlog to drain, instead of a 429 and a client back-off round trip: at saturation with many
+    // small clients almost every refusal is of this kind (projected wait a few ms past the budget), and the refused
+    // client would be back within those milliseconds anyway. The wait shows in the client's request latency, not in
+    // any task's queue wait.
+    const double hold_max = g_cfg.hold_s >= 0.0 ? g_cfg.hold_s : g_cfg.max_queue_s;
+    double held = 0.0;
+    while (wait > g_cfg.max_queue_s && held + (wait - g_cfg.max_queue_s) <= hold_max) {
+      const double d = std::max(2e-4, wait - g_cfg.max_queue_s);
+      std::this_thread::sleep_for(std::chrono::microseconds(static_cast<long>(d * 1e6)));
+      held += d;
+      wait = s.projected_wait(n, static_cast<double>(nbytes));
+    }
     if (wait > g_cfg.max_queue_s) {
+      static const bool dbg = std::getenv("AI4E_INGESTD_DEBUG") != nullptr;
+      static std::atomic<int> dbg_n{0};
+      if (dbg && s.st && dbg_n.fetch_add(1) % 500 == 0)
+        std::fprintf(stderr, "ingestd 429: wait %.2f ms backlog %.0f rate %.0f enq %llu done %llu inflight %llu\n",
+                     wait * 1e3, s.backlog(), s.rate, static_cast<unsigned long long>(s.st[0].load()),
+                     static_cast<unsigned long long>(s.st[1].load()), static_cast<unsigned long long>(s.st[4].load()));
       // the hint: the time for the backlog above the budget to drain (>= 1 ms), at most twice the budget (a request
       // refused on a stale estimate is judged again soon). A hint of a whole budget starved the batch route (16
       // clients, 250 images each: 78k -> 67k images/s); clients back off exponentially on repeated refusals instead
@@ -1040,8 +1171,7 @@ bool ingest(Conn& c, const Request& r, Route& route, Shard& s, bool batch) {
   std::string b3 = "x-b3-traceid: " + trace_id + "\r\nx-b3-spanid: " + span + "\r\nx-b3-parentspanid: " + parent +
                    "\r\nx-b3-sampled: " + sampled + "\r\n";
   std::vector<std::string> ids = s.mint(static_cast<size_t>(n));
-  const uint64_t tok = s.submit(sl, ids, trace_id + "/" + span + "/" + parent);
-  const int64_t created = s.wait_ack(tok, g_cfg.ack_timeout);
+  const int64_t created = s.submit_wait(sl, ids, trace_id + "/" + span + "/" + parent, g_cfg.ack_timeout);
   if (batch) {
     std::string body = "{\"TaskIds\":[";
     for (size_t i = 0; i < ids.size(); ++i) body += (i ? ",\"" : "\"") + ids[i] + "\"";
