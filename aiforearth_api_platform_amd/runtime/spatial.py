@@ -25,8 +25,6 @@ tests) and degenerates to a single-process path when world size is 1.
 """
 from __future__ import annotations
 
-import os
-
 from typing import Callable, List, Optional, Tuple
 
 import torch
@@ -131,40 +129,19 @@ class SpatialSegmenter:
         ranges = order if order is not None else [(0, flat.shape[0])]
         pending = after is not None
         for j, (lo, hi) in enumerate(ranges):
-            for i, e in self._chunks(lo, hi):
+            for i in range(lo, hi, self.tile_batch):
                 if pending and j >= after[0] and out is not None:  # (the first moment the logits buffer exists)
                     after[1](out)
                     pending = False
                 # each batch's logits go straight into one preallocated buffer (a graph's output buffer is reused by
                 # its next replay; one copy per batch instead of a clone plus a concatenation)
-                y = self.model_fn(flat[i:e])[..., : self.n_out]
+                y = self.model_fn(flat[i:min(hi, i + self.tile_batch)])[..., : self.n_out]
                 if out is None:
                     out = torch.empty(flat.shape[0], *y.shape[1:], dtype=y.dtype, device=y.device)
                 out[i:i + y.shape[0]].copy_(y)
                 self.events.append(("tiles", i, i + y.shape[0]))
         if pending and out is not None:
             after[1](out)
-        return out
-
-    def _chunks(self, lo: int, hi: int) -> List[Tuple[int, int]]:
-        """Tile batches of [lo, hi): balanced, of up to 1.25x ``tile_batch``: a 4096^2 mosaic's 81 tiles run as
-        17 + 4 x 16 instead of 5 x 16 + a forward of ONE tile (~90 kernels of one tile each; the one-GPU servable is
-        captured whole, so the shapes are fixed per mosaic size). Per-batch tile graphs keep the fixed batch."""
-        n, tb = hi - lo, self.tile_batch
-        if n <= 0:
-            return []
-        k = -(-n // tb)
-        if self._graphed or os.environ.get("AI4E_TILE_BALANCE", "1") == "0":  # (per-batch graphs: one shape)
-            return [(i, min(hi, i + tb)) for i in range(lo, hi, tb)]
-        k2 = max(1, round(n / tb))
-        if -(-n // k2) <= tb + tb // 4:
-            k = k2
-        base, extra = divmod(n, k)
-        out, i = [], lo
-        for c in range(k):
-            e = i + base + (1 if c < extra else 0)
-            out.append((i, e))
-            i = e
         return out
 
     @staticmethod

@@ -162,6 +162,8 @@ struct PendingSubmit {
   const std::vector<std::string>* ids;
   std::string trace;
   int64_t created = -2;  // -2 pending, -1 ack timed out, else tasks created
+  bool leader = false;   // this request's thread sends the next group
+  std::condition_variable cv;  // its own wake-up (no herd: one notify per waiter)
 };
 
 struct Shard {
@@ -222,7 +224,8 @@ struct Shard {
   // never lower it. (Round 5 held the smoothed rate's peak and let it decay 10 %/s, so a route whose clients were
   // slower than the GPU — single images — read as a slow GPU and throttled itself to 0.59x.)
   double service_rate() {
-    std::lock_guard<std::mutex> g(rate_mu);
+    std::unique_lock<std::mutex> g(rate_mu, std::try_to_lock);
+    if (!g.owns_lock()) return rate_seen.load(std::memory_order_relaxed);  // (another thread is sampling)
     const double t = ai4e::mono_now();
     const int64_t n = st ? static_cast<int64_t>(st[1].load(std::memory_order_relaxed)) : freed.load();
     const bool sat = st ? queued() : false;
@@ -245,8 +248,10 @@ struct Shard {
       rate_n = n;
       rate_sat = sat;
     }
+    rate_seen.store(rate, std::memory_order_relaxed);
     return rate;
   }
+  std::atomic<double> rate_seen{0.0};
 
   // request-body upload rate of this front-end (bytes/s, EWMA over completed bodies): a request's tasks only join
   // the queue once its body has arrived, by when the shard has worked off nbytes / upload_bw of its backlog
@@ -333,34 +338,41 @@ struct Shard {
   // one answer carry many requests (one scheduler wake-up, one journal flush, one queue notify for all of them)
   // instead of one frame and one answer each; alone, a request goes out at once as before.
   std::mutex gc_mu;
-  std::condition_variable gc_cv;
   std::vector<PendingSubmit*> gc_q;
   bool gc_busy = false;
   int64_t submit_wait(const std::vector<int64_t>& sl, const std::vector<std::string>& ids, std::string trace,
                       double timeout_s) {
-    PendingSubmit me{&sl, &ids, std::move(trace)};
+    PendingSubmit me;
+    me.sl = &sl;
+    me.ids = &ids;
+    me.trace = std::move(trace);
     std::unique_lock<std::mutex> lk(gc_mu);
     gc_q.push_back(&me);
-    while (me.created == -2) {
-      if (gc_busy) {
-        gc_cv.wait(lk);
-        continue;
-      }
+    if (!gc_busy) {
       gc_busy = true;
-      std::vector<PendingSubmit*> group;
-      group.swap(gc_q);
-      lk.unlock();
-      std::vector<int64_t> got;
-      if (group.size() == 1) {
-        const PendingSubmit& p = *group[0];
-        got.push_back(wait_ack(submit(*p.sl, *p.ids, p.trace), timeout_s));
-      } else {
-        got = wait_ack_multi(submit_multi(group), group.size(), timeout_s);
-      }
-      lk.lock();
-      for (size_t i = 0; i < group.size(); ++i) group[i]->created = got[i];
+      me.leader = true;
+    }
+    while (!me.leader && me.created == -2) me.cv.wait(lk);
+    if (me.created != -2) return me.created;  // a leader sent it
+    std::vector<PendingSubmit*> group;  // leader: everything queued so far (this request included)
+    group.swap(gc_q);
+    lk.unlock();
+    std::vector<int64_t> got;
+    if (group.size() == 1) {
+      got.push_back(wait_ack(submit(*me.sl, *me.ids, me.trace), timeout_s));
+    } else {
+      got = wait_ack_multi(submit_multi(group), group.size(), timeout_s);
+    }
+    lk.lock();
+    for (size_t i = 0; i < group.size(); ++i) {
+      group[i]->created = got[i];
+      if (group[i] != &me) group[i]->cv.notify_one();
+    }
+    if (!gc_q.empty()) {  // hand the lead to the oldest request that queued meanwhile
+      gc_q.front()->leader = true;
+      gc_q.front()->cv.notify_one();
+    } else {
       gc_busy = false;
-      gc_cv.notify_all();
     }
     return me.created;
   }

@@ -935,8 +935,14 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
       const int g = tid + 512 * e;
       const int r = g >> 5, c8 = g & 31;
       const int m = m0 + WROWS * pass + r, n = n0 + 8 * c8;
-      const float4 v0 = *reinterpret_cast<const float4*>(tile + r * 256 + 4 * ((2 * c8) ^ (r & 7)));
-      const float4 v1 = *reinterpret_cast<const float4*>(tile + r * 256 + 4 * ((2 * c8 + 1) ^ (r & 7)));
+      // the lane's two fp32 chunks (2 c8, 2 c8 + 1), the odd one first in the upper half of the row (c8 >= 16): a
+      // ds_read_b128 lane group ({0-3, 12-15, 20-27}, {4-11, 16-19, 28-31}: 16 lanes of one row) then covers 16
+      // distinct bank quads; reading both halves even-first put every group's 16 lanes on 8 quads (2-way conflicts
+      // on every epilogue read: profiles/r5_pmc/ ldsconf 9-14 % on the 1x1 configs)
+      const int hi = (c8 >> 4) & 1;
+      const float4 va = *reinterpret_cast<const float4*>(tile + r * 256 + 4 * ((2 * c8 + hi) ^ (r & 7)));
+      const float4 vb = *reinterpret_cast<const float4*>(tile + r * 256 + 4 * ((2 * c8 + 1 - hi) ^ (r & 7)));
+      const float4 v0 = hi ? vb : va, v1 = hi ? va : vb;
       const int nb = min(n, p.Kout - 8);
       const float4 b0 = *reinterpret_cast<const float4*>(p.bias + nb);
       const float4 b1 = *reinterpret_cast<const float4*>(p.bias + nb + 4);
