@@ -107,7 +107,8 @@ def build_kernels(verbose: bool = False, force: bool = False, jobs: int = 8, def
     """``defines`` + ``variant``: an A/B build of the library (``_lib/libai4e_kernels_<variant>.so``, objects in
     their own directory), loaded with AI4E_KERNEL_LIB=<path> (ops/_ext.py)."""
     srcs = _kernel_sources()
-    headers = sorted((CSRC / "kernels").glob("*.h"))
+    # + the layout / span-decoder headers the JPEG kernels share with the CPU preparer
+    headers = sorted((CSRC / "kernels").glob("*.h")) + [CSRC / "core" / "jpeg_layout.h", CSRC / "core" / "jpeg_span.h"]
     objdir = OBJDIR if not variant else OBJDIR.parent / f"obj_{variant}"
     out_so = KERNEL_SO if not variant else LIBDIR / f"libai4e_kernels_{variant}.so"
     LIBDIR.mkdir(parents=True, exist_ok=True)

@@ -71,6 +71,7 @@ _SIGS = {
     "ai4e_gn_chunk_px": [],
     "ai4e_gn_relu_head8": [_vp, _c_int, _c_int, _vp, _vp, _c_int, _vp, _vp, _c_int, _c_int, _vp],
     "ai4e_conv3x3_tile_fwd": [_vp, _vp, _vp, _vp, _c_int, _vp] + [_c_int] * 10 + [_vp, _c_int, _vp],
+    "ai4e_jpeg_decode": [_vp, _c_int, _c_int, _c_int, _c_long, _c_long, _c_int, _vp],
     "ai4e_crumbs_alloc": [_c_int, _vp, _vp],
     "ai4e_crumb": [_vp, _c_int, _vp],
 }

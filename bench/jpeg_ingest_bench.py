@@ -1,4 +1,5 @@
-"""JPEG ingest cost of the image endpoints (CPU): decode + resize of camera frames to the model size.
+"""JPEG ingest cost of the image endpoints: decode + resize of camera frames to the model size, on CPU threads and
+with the on-GPU reconstruction (``--gpu``: runtime/jpeg_gpu.py, csrc/kernels/jpeg.hip).
 
 Real camera-trap clients post JPEG frames (the reference's detection API takes image files). The
 gateway decodes them on CPU threads (`runtime/model_endpoint.decode_image`, Pillow + libjpeg-turbo,
@@ -7,7 +8,11 @@ to 1/2..1/8 scale in the DCT domain ("draft") before the final bilinear resize. 
 for both decode paths at 1 and N threads, and for N decode worker processes writing into a shared ring,
 for the classifier (224x224) and detector (640x640) sizes.
 
-    python bench/jpeg_ingest_bench.py [--frame 1536x2048 --threads 8 --seconds 3]
+    python bench/jpeg_ingest_bench.py [--frame 1536x2048 --threads 8 --seconds 3] [--gpu --batch 64]
+
+``--gpu``: ``--threads`` CPU threads prepare the frames (header parse + unstuffed copy, ~0.2 ms each) and one GPU does
+the rest, batches pipelined (batch i+1 is prepared while the GPU decodes batch i); the output of every frame is
+checked against ``decode_image`` (the CPU path the endpoints use) and the maximum absolute difference reported.
 """
 import argparse
 import io
@@ -55,15 +60,64 @@ def rate(fn, body, shape, threads, seconds):
     return sum(counts) / (time.perf_counter() - t0)
 
 
+def gpu_rate(bodies, shape, threads, batch, seconds):
+    """Frames/s of the on-GPU path over `seconds`, and the max |GPU - decode_image| over the distinct bodies."""
+    import torch
+
+    from aiforearth_api_platform_amd.runtime.jpeg_gpu import JpegGpuDecoder
+
+    dec = JpegGpuDecoder(shape, "cuda", threads=threads)
+    frames = [bodies[i % len(bodies)] for i in range(batch)]
+    out = dec.decode(frames)  # warm-up (allocations, coefficient tables)
+    torch.cuda.synchronize()
+    diff = 0
+    for i, b in enumerate(bodies):
+        ref = decode_image(b, "image/jpeg", shape)
+        diff = max(diff, int(np.abs(out[i].cpu().numpy().astype(np.int16) - ref).max()))
+    outs = [torch.empty((batch,) + tuple(shape), dtype=torch.uint8, device="cuda") for _ in range(2)]
+    n = 0
+    t0 = time.perf_counter()
+    pend = None
+    k = 0
+    while time.perf_counter() - t0 < seconds:
+        p = dec.submit(frames, outs[k & 1])
+        if pend is not None:
+            dec.finish(pend)
+        pend = p
+        n += batch
+        k += 1
+    dec.finish(pend)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    stats = dict(dec.stats)
+    dec.close()
+    return {"frames_per_s": round(n / dt, 1), "batch": batch, "cpu_threads": threads, "max_abs_diff_vs_decode_image":
+            diff, "gpu_frames": stats["gpu_frames"], "cpu_fallback_frames": stats["cpu_frames"]}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--frame", default="1536x2048")
     ap.add_argument("--threads", type=int, default=8)
     ap.add_argument("--seconds", type=float, default=3.0)
     ap.add_argument("--json-out", default="")
+    ap.add_argument("--gpu", action="store_true", help="only the on-GPU reconstruction (one GPU)")
+    ap.add_argument("--batch", type=int, default=64)
     a = ap.parse_args()
     h, w = (int(v) for v in a.frame.split("x"))
     body = frame_jpeg(h, w)
+    if a.gpu:
+        bodies = [frame_jpeg(h, w, quality=q) for q in (90, 85, 80, 75)]
+        out = {"metric": "JPEG frames decoded + resized per second (on-GPU reconstruction, 1 GPU)", "frame": [h, w],
+               "jpeg_bytes": [len(b) for b in bodies], "threads": a.threads, "results": {}}
+        for shape in ((640, 640, 3), (224, 224, 3)):
+            out["results"][f"{shape[0]}x{shape[1]}"] = gpu_rate(bodies, shape, a.threads, a.batch, a.seconds)
+        line = json.dumps(out)
+        print(line)
+        if a.json_out:
+            with open(a.json_out, "w") as f:
+                f.write(line + "\n")
+        return
     out = {"metric": "JPEG frames decoded + resized per second (CPU)", "frame": [h, w], "jpeg_bytes": len(body),
            "threads": a.threads, "cpu_count": os.cpu_count(), "results": {}}
     for shape in ((224, 224, 3), (640, 640, 3)):

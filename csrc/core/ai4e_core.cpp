@@ -16,6 +16,7 @@
 #include <pybind11/stl.h>
 
 #include "dispatch_queue.h"
+#include "jpeg_coef.h"
 #include "scheduler.h"
 #include "slot_ring.h"
 #include "task_store.h"
@@ -254,6 +255,44 @@ PYBIND11_MODULE(_ai4e_core, m) {
       .def("close", &SlotRing::close)
       .def_property_readonly("capacity", &SlotRing::capacity)
       .def_property_readonly("base", &SlotRing::base);
+
+  // Huffman-decode a baseline JPEG into the compact coefficient layout of csrc/core/jpeg_coef.h at address `out`
+  // (capacity `cap` bytes; e.g. a payload-ring slot). Returns (status, bytes used); status 0 ok, 1 unsupported
+  // (progressive / 12-bit / non-interleaved: decode on the CPU instead), 2 corrupt, 3 does not fit.
+  m.def(
+      "jpeg_coef_decode",
+      [](py::bytes data, uintptr_t out, size_t cap) {
+        std::string_view v(data);
+        size_t used = 0;
+        int st;
+        {
+          py::gil_scoped_release rel;
+          JpegCoefDecoder dec;
+          st = dec.decode(reinterpret_cast<const uint8_t*>(v.data()), v.size(), reinterpret_cast<uint8_t*>(out), cap,
+                          &used);
+        }
+        return py::make_tuple(st, used);
+      },
+      py::arg("data"), py::arg("out"), py::arg("cap"));
+  m.attr("JPEG_COEF_HEADER_BYTES") = sizeof(JpegCoefHeader);
+  // Headers, GPU Huffman tables and the unstuffed scan (JpegScanHeader layout) for the on-GPU decoder
+  // (csrc/kernels/jpeg.hip); same status codes (restart intervals: 1, decode on the CPU).
+  m.def(
+      "jpeg_scan_prepare",
+      [](py::bytes data, uintptr_t out, size_t cap) {
+        std::string_view v(data);
+        size_t used = 0;
+        int st;
+        {
+          py::gil_scoped_release rel;
+          JpegCoefDecoder dec;
+          st = dec.prepare(reinterpret_cast<const uint8_t*>(v.data()), v.size(), reinterpret_cast<uint8_t*>(out), cap,
+                           &used);
+        }
+        return py::make_tuple(st, used);
+      },
+      py::arg("data"), py::arg("out"), py::arg("cap"));
+  m.attr("JPEG_SCAN_HEADER_BYTES") = sizeof(JpegScanHeader);
 
   py::class_<NodeScheduler, std::shared_ptr<NodeScheduler>>(m, "NodeScheduler")
       .def(py::init([](std::shared_ptr<TaskStore> store, std::shared_ptr<DispatchQueue> queue, std::string endpoint,
