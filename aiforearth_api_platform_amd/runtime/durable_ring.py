@@ -103,8 +103,11 @@ class DurableRing:
     # ---------------------------------------------------------------- this generation
     def create(self, nslots: int, item_shape: Sequence[int]) -> Tuple[shared_memory.SharedMemory, str]:
         """Create this generation's ring + tag segments and record them in the sidecar. Returns the ring segment."""
+        from .jpeg_gpu import RING_TAIL_BYTES
+
         item = int(np.prod(item_shape))
-        self.ring_shm = _create(self.ring_name, int(nslots) * item)
+        self._nbytes = int(nslots) * item
+        self.ring_shm = _create(self.ring_name, self._nbytes + RING_TAIL_BYTES)
         self.tags_shm = _create(self.tags_name, int(nslots) * TAG_BYTES)
         meta = {"gen": self.gen, "ring": self.ring_name, "tags": self.tags_name, "nslots": int(nslots),
                 "item_shape": [int(v) for v in item_shape]}
@@ -163,8 +166,18 @@ class DurableRing:
             return None
         shape = tuple(int(v) for v in self.prev["item_shape"])
         item = int(np.prod(shape))
-        ring = np.frombuffer(self._prev_ring.buf, dtype=np.uint8, count=int(self.prev["nslots"]) * item)
-        return ring[slot * item:(slot + 1) * item].reshape(shape).copy()
+        nbytes = int(self.prev["nslots"]) * item
+        ring = np.frombuffer(self._prev_ring.buf, dtype=np.uint8, count=nbytes)
+        out = ring[slot * item:(slot + 1) * item].copy()
+        # a JPEG frame prepared into the slot is marked with the previous ring's key: re-key it for this ring's workers
+        from .jpeg_gpu import SLOT_MAGIC, TRAILER_BYTES, ring_key
+
+        old_key = ring_key(self._prev_ring.buf, nbytes)
+        if old_key and item > TRAILER_BYTES:
+            tr = out[item - TRAILER_BYTES:item - TRAILER_BYTES + 16].view(np.uint64)
+            if int(tr[0]) == SLOT_MAGIC and int(tr[1]) == old_key:
+                tr[1] = ring_key(self.ring_shm.buf, self._nbytes) if self.ring_shm is not None else 0
+        return out.reshape(shape)
 
     def release_previous(self) -> None:
         """Recovery is over: unlink the previous generation's segments."""

@@ -90,6 +90,14 @@ class BatchResult:
     t_launch: float = 0.0        # host CLOCK_MONOTONIC at launch
     ev_copy0: Optional["torch.cuda.Event"] = None
     ev_copy1: Optional["torch.cuda.Event"] = None
+    jpeg: Optional[Tuple[List[int], torch.Tensor]] = None  # (batch rows decoded from JPEG, their status, valid after done)
+
+    def jpeg_failed(self) -> List[int]:
+        """Batch rows whose prepared JPEG frame could not be decoded (corrupt data): their outputs are garbage."""
+        if self.jpeg is None:
+            return []
+        idx, st = self.jpeg
+        return [idx[k] for k in range(len(idx)) if int(st[k]) != 0]
 
     @property
     def top_idx(self) -> torch.Tensor:
@@ -144,6 +152,10 @@ class InferenceEngine:
         self._graph_out: Dict[Tuple[int, int], Tuple[torch.Tensor, ...]] = {}
         self.compute_done: List[Optional[torch.cuda.Event]] = [None] * self.nbuf
         self._k = 0
+        # JPEG frames prepared into ring slots (runtime/jpeg_gpu.py): decoded on the copy stream into the input rows
+        self._jpeg = None
+        self._jpeg_scan: List[Optional[torch.Tensor]] = [None] * self.nbuf
+        self._jpeg_host: List[Optional[torch.Tensor]] = [None] * self.nbuf
         # (measured and removed in round 5: the phase-offset front/back split and the CU-partitioned pipeline,
         # both slower than two full-chip streams; profiles/r3_cusplit/, patches in profiles/r5_pruned/)
 
@@ -194,13 +206,30 @@ class InferenceEngine:
         torch.cuda.synchronize(self.device)
 
     # -------------------------------------------------------------- submit
-    def submit(self, host_src: torch.Tensor, slots: Sequence[int]) -> BatchResult:
-        """Copy ``host_src[slots]`` to the next device buffer, run, and return an async result."""
+    def submit(self, host_src: torch.Tensor, slots: Sequence[int], jpeg=None) -> BatchResult:
+        """Copy ``host_src[slots]`` to the next device buffer, run, and return an async result. ``jpeg``: [(batch row,
+        prepared bytes, header, plan)] of the rows whose slot holds a prepared JPEG frame (runtime/jpeg_gpu.py): those
+        are decoded on the copy stream straight into their input rows instead of copied."""
         n = len(slots)
         t_launch = time.monotonic()
         if self.device.type != "cuda":  # CPU path (tests / CPU-only hosts): synchronous
-            outs = self.run_sync(host_src[list(slots)])
-            return BatchResult(list(outs), _DoneEvent(), n, t_launch)
+            x = host_src[list(slots)]
+            st = None
+            if jpeg:
+                from .jpeg_gpu import decode_prepared_cpu
+
+                x = x.clone()
+                st = torch.zeros(len(jpeg), dtype=torch.int32)
+                for k, (j, used, _, _) in enumerate(jpeg):
+                    img = decode_prepared_cpu(host_src[slots[j]].reshape(-1)[:used].numpy(), self.item_shape)
+                    if img is None:
+                        st[k] = 2
+                        x[j].zero_()
+                    else:
+                        x[j].copy_(torch.from_numpy(img))
+            outs = self.run_sync(x)
+            return BatchResult(list(outs), _DoneEvent(), n, t_launch,
+                               jpeg=([j for j, _, _, _ in jpeg], st) if jpeg else None)
         if not self.host_out[0]:
             raise RuntimeError("InferenceEngine.warmup() must run before submit() on a GPU")
         buf = self._k % self.nbuf
@@ -216,9 +245,13 @@ class InferenceEngine:
         if self.timing:
             ev0 = torch.cuda.Event(enable_timing=True)
             ev0.record(cs)
+        jstatus = None
         with torch.cuda.stream(cs):
-            for dst, src, ln in contiguous_runs(list(slots)):
-                dev_in[dst:dst + ln].copy_(host_src[src:src + ln], non_blocking=True)
+            if not jpeg:
+                for dst, src, ln in contiguous_runs(list(slots)):
+                    dev_in[dst:dst + ln].copy_(host_src[src:src + ln], non_blocking=True)
+            else:
+                jstatus = self._submit_jpeg(buf, host_src, slots, jpeg, dev_in, cs)
         ev = torch.cuda.Event(enable_timing=self.timing)
         ev.record(cs)
         if self.timing:
@@ -234,10 +267,49 @@ class InferenceEngine:
             host = self.host_out[buf]
             for h, o in zip(host, outs):
                 h[:n].copy_(o[:n], non_blocking=True)
+            jres = None
+            if jstatus is not None:
+                hs = self._jpeg_host[buf]
+                if hs is None or hs.numel() < jstatus.numel():
+                    hs = self._jpeg_host[buf] = torch.zeros(max(self.max_batch, jstatus.numel()), dtype=torch.int32,
+                                                            pin_memory=True)
+                hs[:jstatus.numel()].copy_(jstatus, non_blocking=True)
+                jstatus.record_stream(st)  # (allocated on the copy stream, read here)
+                jres = ([j for j, _, _, _ in jpeg], hs[:jstatus.numel()])
             done = torch.cuda.Event(enable_timing=self.timing)
             done.record(st)
         self.compute_done[buf] = done
-        return BatchResult([h[:n] for h in self.host_out[buf]], done, n, t_launch, ev0, ev1)
+        return BatchResult([h[:n] for h in self.host_out[buf]], done, n, t_launch, ev0, ev1, jres)
+
+    def _submit_jpeg(self, buf: int, host_src: torch.Tensor, slots: Sequence[int], jpeg, dev_in: torch.Tensor, cs):
+        """(on the copy stream) raw rows by contiguous runs; prepared JPEG rows: their bytes into a device scan area,
+        then the decode kernels write the rows. Returns the per-frame status (device)."""
+        from .jpeg_gpu import JpegLauncher, _align
+
+        if self._jpeg is None:
+            self._jpeg = JpegLauncher(self.device)
+        jrows = {j for j, _, _, _ in jpeg}
+        raw = [(j, s) for j, s in enumerate(slots) if j not in jrows]
+        i = 0
+        while i < len(raw):
+            k = i + 1
+            while k < len(raw) and raw[k][0] == raw[k - 1][0] + 1 and raw[k][1] == raw[k - 1][1] + 1:
+                k += 1
+            d0, s0 = raw[i]
+            dev_in[d0:d0 + (k - i)].copy_(host_src[s0:s0 + (k - i)], non_blocking=True)
+            i = k
+        offs, total = [], 0
+        for _, used, _, _ in jpeg:
+            offs.append(total)
+            total += _align(used)
+        scan = self._jpeg_scan[buf] = self._jpeg.grow(self._jpeg_scan[buf], total)
+        flat = host_src.view(host_src.shape[0], -1)
+        for (j, used, _, _), o in zip(jpeg, offs):
+            scan[o:o + used].copy_(flat[slots[j], :used], non_blocking=True)
+        base = scan.data_ptr()
+        frames = [(hdr, plan, base + o, dev_in[j].data_ptr()) for (j, _, hdr, plan), o in zip(jpeg, offs)]
+        status, _keep = self._jpeg.launch(frames, cs)
+        return status
 
     def run_sync(self, images_u8: torch.Tensor) -> Tuple[torch.Tensor, ...]:
         """Convenience (sync API / tests): images already on host or device."""

@@ -52,6 +52,9 @@ def frontend_main(index: int, host: str, port: int, internal_url: str, endpoints
     from ..store.pystore import absolute_path, dotnet_timestamp
     from ..utils.tracing import b3_from_headers, b3_pack
     from .decode import PayloadError, decode_image
+    import numpy as np
+
+    from .jpeg_gpu import JPEG_TYPES, prepare_into_slot
     from .ingest import IngestShard
 
     import os
@@ -149,9 +152,24 @@ def frontend_main(index: int, host: str, port: int, internal_url: str, endpoints
                                              status=202, headers=b3)
                 return web.json_response({"TaskIds": ids}, headers=b3)
             body = await request.read()
-            arr = await loop.run_in_executor(None, decode_image, body, request.content_type, shard.item_shape)
-            slot = shard.slots.alloc(1, 0.0) or await loop.run_in_executor(None, shard.alloc, 1)
-            shard.write(slot[0], arr)
+            if shard.jpeg_key and request.content_type in JPEG_TYPES:
+                # prepared into the slot for the worker's GPU decode (runtime/jpeg_gpu.py); else decoded here
+                slot = shard.slots.alloc(1, 0.0) or await loop.run_in_executor(None, shard.alloc, 1)
+                try:
+                    addr = shard.buf[slot[0]].ctypes.data
+                    item = int(np.prod(shard.item_shape))
+                    if not await loop.run_in_executor(None, prepare_into_slot, body, addr, item, shard.item_shape,
+                                                      shard.jpeg_key):
+                        arr = await loop.run_in_executor(None, decode_image, body, request.content_type,
+                                                         shard.item_shape)
+                        shard.write(slot[0], arr)
+                except BaseException:
+                    shard.free(slot)
+                    raise
+            else:
+                arr = await loop.run_in_executor(None, decode_image, body, request.content_type, shard.item_shape)
+                slot = shard.slots.alloc(1, 0.0) or await loop.run_in_executor(None, shard.alloc, 1)
+                shard.write(slot[0], arr)
             tid = shard.mint_ids(1)[0]
             try:
                 n = await shard.submit_ids(slot, [tid], trace).wait_async(ack_timeout_s)

@@ -25,7 +25,7 @@ import queue
 import threading
 import time
 from dataclasses import dataclass, field
-from typing import Any, Dict, Optional, Sequence, Tuple
+from typing import Any, Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -94,6 +94,13 @@ def attach_ring(shm_name: str, nslots: int, item_shape: Sequence[int], untrack: 
     return shm, buf
 
 
+def ring_jpeg_key(shm, nslots: int, item_shape: Sequence[int]) -> int:
+    """The key marking slots that hold prepared JPEG frames (runtime/jpeg_gpu.py; 0: the ring has none)."""
+    from .jpeg_gpu import ring_key
+
+    return ring_key(shm.buf, int(nslots) * int(np.prod(item_shape)))
+
+
 def pin_host(buf: torch.Tensor) -> bool:
     """Register the mapped ring as pinned host memory for direct DMA (hipHostRegister)."""
     try:
@@ -114,13 +121,17 @@ class GpuWorker:
     """The loop of one worker process (also usable in a thread for tests)."""
 
     def __init__(self, conn: P.FrameConn, rank: int, device: str, spec: ModelSpec, ring_buf: torch.Tensor,
-                 local_ring=None, hb_interval: float = 0.5, depth: int = 2, group_kwargs: Optional[dict] = None):
+                 local_ring=None, hb_interval: float = 0.5, depth: int = 2, group_kwargs: Optional[dict] = None,
+                 jpeg_key: int = 0):
         self.conn = conn
         self.rank = rank
         self.device = torch.device(device)
         self.spec = spec
         self.buf = ring_buf
         self.nslots = ring_buf.shape[0]
+        self.jpeg_key = int(jpeg_key)  # slots holding prepared JPEG frames are decoded on the device (engine.py)
+        self._ring_u8 = ring_buf.view(self.nslots, -1).numpy() if self.jpeg_key else None
+        self.jpeg_frames = 0
         self.local_ring = local_ring  # native SlotRing of this process's ingest partition (FREE frames)
         self.hb_interval = hb_interval
         self.depth = depth
@@ -281,13 +292,14 @@ class GpuWorker:
         if not vslots:
             self.conn.done(bid, status, bytes(n * self.row_bytes), self.row_bytes, (t_recv, t_recv, t_recv, 0, 0))
             return
+        jpeg = self._jpeg_rows(vslots, status, valid)
         # the engine has 3 buffer sets: never launch a 3rd batch over one not yet retired
         with self._idle:
             self._idle.wait_for(lambda: self._inflight < self.engine.nbuf, timeout=120)
         try:
             if f.get("fail_batch") == self.batches:
                 raise RuntimeError("injected batch launch failure")
-            res = self.engine.submit(self.buf, vslots)
+            res = self.engine.submit(self.buf, vslots, jpeg=jpeg)
         except Exception as e:
             import sys
 
@@ -300,6 +312,29 @@ class GpuWorker:
         with self._idle:
             self._inflight += 1
         self._done_q.put(_Pending(bid, n, valid, res, t_recv, status))
+
+    def _jpeg_rows(self, vslots: List[int], status: np.ndarray, valid: np.ndarray):
+        """[(batch row, prepared bytes, header, plan)] of the valid slots holding prepared JPEG frames; a marked slot
+        whose header does not hold up is failed as an invalid payload (and its row computed from whatever it holds)."""
+        if not self.jpeg_key:
+            return None
+        from .jpeg_gpu import header_sane, parse_header, plan_frame, slot_frames
+
+        frames = slot_frames(self._ring_u8, vslots, self.jpeg_key)
+        if not frames:
+            return None
+        h, w, c = self.spec.item_shape
+        out = []
+        vidx = np.nonzero(valid)[0]
+        for j, used in frames:
+            hdr = parse_header(self._ring_u8[vslots[j], :160].tobytes())
+            plan = plan_frame(hdr, w, h, c) if header_sane(hdr, used) else None
+            if plan is None:
+                status[vidx[j]] = P.IT_INVALID
+                continue
+            out.append((j, used, hdr, plan))
+        self.jpeg_frames += len(out)
+        return out or None
 
     def _rows(self, n: int, valid: np.ndarray, outputs) -> bytes:
         nv = int(valid.sum())
@@ -320,6 +355,9 @@ class GpuWorker:
         self.busy_ms += h2d_ms + comp_ms
         rows = self._rows(p.n, p.valid, p.res.outputs)
         self._mark_invalid(p.status, p.valid, p.res.outputs)
+        bad = p.res.jpeg_failed()
+        if bad:  # corrupt entropy-coded data in a prepared JPEG frame
+            p.status[np.nonzero(p.valid)[0][bad]] = P.IT_INVALID
         if getattr(self.servable, "stages", 0):  # ensemble hop (AddPipelineTask) for this batch's tasks
             self.conn.stage(p.bid, 0)
         self.conn.done(p.bid, p.status, rows, self.row_bytes, (p.t_recv, p.res.t_launch, t_done, h2d_ms, comp_ms))
@@ -350,10 +388,15 @@ class GpuWorker:
             try:
                 if self.fault.get("fail_item") == int(slots[i]):
                     raise RuntimeError("injected item failure")
-                outs = self.engine.run_sync(self.buf[int(slots[i]): int(slots[i]) + 1])
-                rows[i] = np.frombuffer(encode_rows([o.numpy() for o in outs], 1), np.uint8)
                 one = np.zeros(1, np.uint8)
+                jpeg = self._jpeg_rows([int(slots[i])], one, np.ones(1, bool))
+                res = self.engine.submit(self.buf, [int(slots[i])], jpeg=jpeg)
+                res.done.synchronize()
+                outs = [o.clone() for o in res.outputs]
+                rows[i] = np.frombuffer(encode_rows([o.numpy() for o in outs], 1), np.uint8)
                 self._mark_invalid(one, np.ones(1, bool), outs)
+                if res.jpeg_failed():
+                    one[0] = P.IT_INVALID
                 status[i] = max(status[i], one[0])
             except Exception as e:  # this item fails on its own
                 import sys
@@ -427,7 +470,8 @@ def worker_main(conn, rank: int, device: str, spec: ModelSpec, shm_name: str, ns
 
         local_ring = native.SlotRing(partition[1], partition[0])
     fc = conn if isinstance(conn, P.FrameConn) else P.FrameConn(conn)
-    w = GpuWorker(fc, rank, device, spec, buf, local_ring=local_ring, hb_interval=hb_interval, group_kwargs=group_kwargs)
+    w = GpuWorker(fc, rank, device, spec, buf, local_ring=local_ring, hb_interval=hb_interval, group_kwargs=group_kwargs,
+                  jpeg_key=ring_jpeg_key(shm, nslots, spec.item_shape))
     if ready_event is not None:  # graphs are captured: the hosting process may use the device again
         ready_event.set()
     try:

@@ -99,6 +99,9 @@ class IngestShard:
         # spawned by the ring's owner: same resource tracker (no unregister, see worker_pool.SharedPayloadRing)
         self._shm = shared_memory.SharedMemory(name=shm_name)
         self.buf = np.ndarray((self.nslots, *self.item_shape), dtype=np.uint8, buffer=self._shm.buf)
+        from .jpeg_gpu import ring_key
+
+        self.jpeg_key = ring_key(self._shm.buf, self.buf.nbytes)  # (runtime/jpeg_gpu.py prepared JPEG slots)
         self.slots = native.SlotRing(int(length), int(base))
         self.part_len = int(length)
         self.fc = P.FrameConn(conn)

@@ -16,7 +16,9 @@ PIL's ``reducing_gap`` pre-reduction) and frames whose decode reports an error a
 """
 from __future__ import annotations
 
+import functools
 import math
+import struct
 import threading
 from concurrent.futures import ThreadPoolExecutor
 from dataclasses import dataclass
@@ -76,22 +78,32 @@ def component_ssize(hmax: int, vmax: int, h: int, v: int, scale: int) -> Tuple[i
     return ss, (hmax * min_s) // (h * ss), (vmax * min_s) // (v * ss)
 
 
+_HDR = struct.Struct("<40I")
+
+
 def parse_header(buf) -> dict:
     """The fixed part of a prepared frame (JpegScanHeader or JpegCoefHeader)."""
-    u32 = np.frombuffer(buf, np.uint32, 40)
-    magic, W, H, nc, hmax, vmax, nb, nbytes = (int(x) for x in u32[:8])
-    comp = tuple(tuple(int(x) for x in u32[8 + 8 * c: 16 + 8 * c]) for c in range(nc))
+    u32 = _HDR.unpack_from(buf)
+    magic, W, H, nc, hmax, vmax, nb, nbytes = u32[:8]
+    nc = min(nc, 3)
+    comp = tuple(u32[8 + 8 * c: 16 + 8 * c] for c in range(nc))
     d = dict(magic=magic, width=W, height=H, ncomp=nc, hmax=hmax, vmax=vmax, nblocks=nb, data_bytes=nbytes, comp=comp)
     if magic == SCAN_MAGIC:
-        d.update(mcux=int(u32[32]), mcuy=int(u32[33]), bpm=int(u32[34]), total_bits=int(u32[36]))
+        d.update(mcux=u32[32], mcuy=u32[33], bpm=u32[34], total_bits=u32[36])
     return d
 
 
 def plan_frame(hdr: dict, out_w: int, out_h: int, out_c: int = 3) -> Optional[FramePlan]:
     """The GPU plan of a frame for a (out_h, out_w, out_c) model input, or None when the CPU path must decode it."""
+    return _plan(hdr["width"], hdr["height"], hdr["ncomp"], hdr["hmax"], hdr["vmax"],
+                 tuple(tuple(c[:6]) for c in hdr["comp"]), hdr["nblocks"], out_w, out_h, out_c)
+
+
+@functools.lru_cache(maxsize=1024)
+def _plan(W, H, ncomp, hmax, vmax, comps, nblocks, out_w, out_h, out_c) -> Optional[FramePlan]:
+    hdr = dict(width=W, height=H, ncomp=ncomp, hmax=hmax, vmax=vmax, comp=comps, nblocks=nblocks)
     if out_c != 3:
         return None
-    W, H = hdr["width"], hdr["height"]
     s = draft_scale(W, H, out_w, out_h)
     src_w, src_h = -(-W // s), -(-H // s)
     # Image.resize(reducing_gap=2.0) pre-reduces by box averaging when the size is >= 4x the target: CPU path
@@ -241,19 +253,10 @@ def coef_planes(buf) -> Tuple[dict, List[np.ndarray]]:
     return hdr, blocks
 
 
-def reference_decode(body: bytes, shape: Tuple[int, int, int]) -> Optional[np.ndarray]:
-    """The GPU pipeline in numpy over the CPU Huffman decoder's coefficients (tests: bit-exact vs ``decode_image``)."""
-    from aiforearth_api_platform_amd import _ai4e_core as core
-
-    h_out, w_out, c_out = shape
-    buf = np.zeros(max(8 << 20, 8 * len(body)), np.uint8)
-    st, used = core.jpeg_coef_decode(body, buf.ctypes.data, buf.nbytes)
-    if st != ST_OK:
-        return None
-    hdr, blocks = coef_planes(buf[:used].tobytes())
-    plan = plan_frame(hdr, w_out, h_out, c_out)
-    if plan is None:
-        return None
+def reconstruct_reference(blocks: List[np.ndarray], plan: FramePlan) -> np.ndarray:
+    """Dequantised blocks per component ([bh, bw, 8, 8] each) -> uint8 [out_h, out_w, 3]: the kernels' IDCT, colour
+    and resize steps in numpy."""
+    h_out, w_out = plan.out_h, plan.out_w
     planes = []
     for b, s in zip(blocks, plan.ssize):
         bh, bw = b.shape[:2]
@@ -281,6 +284,112 @@ def reference_decode(body: bytes, shape: Tuple[int, int, int]) -> Optional[np.nd
     return out.astype(np.uint8)
 
 
+def reference_decode(body: bytes, shape: Tuple[int, int, int]) -> Optional[np.ndarray]:
+    """The GPU pipeline in numpy over the CPU Huffman decoder's coefficients (tests: bit-exact vs ``decode_image``)."""
+    from aiforearth_api_platform_amd import _ai4e_core as core
+
+    h_out, w_out, c_out = shape
+    buf = np.zeros(max(8 << 20, 8 * len(body)), np.uint8)
+    st, used = core.jpeg_coef_decode(body, buf.ctypes.data, buf.nbytes)
+    if st != ST_OK:
+        return None
+    hdr, blocks = coef_planes(buf[:used].tobytes())
+    plan = plan_frame(hdr, w_out, h_out, c_out)
+    if plan is None:
+        return None
+    return reconstruct_reference(blocks, plan)
+
+
+def decode_prepared_cpu(prepared: np.ndarray, shape: Tuple[int, int, int]) -> Optional[np.ndarray]:
+    """Decode a prepared frame (uint8 array holding a JpegScanHeader + scan) on the CPU: the kernels' span decoder run
+    sequentially (``_ai4e_core.jpeg_scan_coefs``) + the numpy reconstruction. Workers on CPU devices; None if the frame
+    is corrupt or outside the plan."""
+    from aiforearth_api_platform_amd import _ai4e_core as core
+
+    prepared = np.ascontiguousarray(prepared)
+    hdr = parse_header(prepared[:160].tobytes())
+    plan = plan_frame(hdr, shape[1], shape[0], shape[2])
+    if hdr["magic"] != SCAN_MAGIC or plan is None:
+        return None
+    coef = np.zeros((hdr["nblocks"], 64), np.int16)
+    if core.jpeg_scan_coefs(prepared.ctypes.data, prepared.nbytes, coef.ctypes.data) != 0:
+        return None
+    u8 = prepared[:core.JPEG_SCAN_HEADER_BYTES]
+    bc, bdy, bdx = u8[160:176].astype(np.int64), u8[176:192].astype(np.int64), u8[192:208].astype(np.int64)
+    quant = u8[224:736].view(np.uint16).reshape(4, 64).astype(np.int64)
+    q = np.arange(hdr["nblocks"])
+    m, k = q // hdr["bpm"], q % hdr["bpm"]
+    blocks = []
+    for c, comp in enumerate(hdr["comp"]):
+        h, v, bw, bh, _, tq = comp[:6]
+        sel = bc[k] == c
+        row = (m[sel] // hdr["mcux"]) * v + bdy[k[sel]]
+        col = (m[sel] % hdr["mcux"]) * h + bdx[k[sel]]
+        blk = np.zeros((bh, bw, 64), np.int64)
+        blk[row, col] = coef[sel].astype(np.int64) * quant[tq][None]
+        blocks.append(blk.reshape(bh, bw, 8, 8))
+    return reconstruct_reference(blocks, plan)
+
+
+# ------------------------------------------------------------------------------------------------ payload-ring slots
+# A request's JPEG body can be prepared straight into its payload-ring slot (front-ends: model_endpoint.py,
+# csrc/ingest/ingestd.cpp); the slot then ends with a JpegSlotTrailer holding the ring's key, and the worker decodes
+# it on the GPU into the model input (engine.py). csrc/core/jpeg_layout.h.
+SLOT_MAGIC = 0x3153504A45344941  # "AI4EJPS1"
+RING_TAIL_MAGIC = 0x474E495245344941  # "AI4ERING"
+RING_TAIL_BYTES = 64
+TRAILER_BYTES = 32
+JPEG_TYPES = ("image/jpeg", "image/jpg", "image/pjpeg")
+
+
+def init_ring_tail(shm_buf, nbytes: int, enabled: bool) -> int:
+    """Write the ring's tail (after ``nbytes`` of slots): magic + a random key (0 = prepared frames disabled)."""
+    import secrets
+
+    key = (secrets.randbits(63) | 1) if enabled else 0
+    np.frombuffer(shm_buf, np.uint64, 2, nbytes)[:] = (RING_TAIL_MAGIC, key)
+    return key
+
+
+def ring_key(shm_buf, nbytes: int) -> int:
+    """The key of a ring whose shared memory holds a tail, else 0."""
+    if len(shm_buf) < nbytes + RING_TAIL_BYTES:
+        return 0
+    magic, key = (int(x) for x in np.frombuffer(shm_buf, np.uint64, 2, nbytes))
+    return key if magic == RING_TAIL_MAGIC else 0
+
+
+def prepare_into_slot(body: bytes, slot_addr: int, item_bytes: int, shape: Tuple[int, int, int], key: int) -> bool:
+    """Prepare a JPEG body into a slot (address ``slot_addr``) and mark it; False (slot untouched as far as the
+    trailer goes) when the frame must be decoded on the CPU instead."""
+    from aiforearth_api_platform_amd import _ai4e_core as core
+
+    if not key or item_bytes <= core.JPEG_SCAN_HEADER_BYTES + TRAILER_BYTES + 64:
+        return False
+    st, used = core.jpeg_scan_prepare(body, slot_addr, item_bytes - TRAILER_BYTES)
+    if st != ST_OK:
+        return False
+    import ctypes
+
+    hdr = parse_header(ctypes.string_at(slot_addr, 160))
+    if plan_frame(hdr, shape[1], shape[0], shape[2]) is None:
+        return False
+    trailer = np.array([SLOT_MAGIC, key, used], np.uint64)
+    ctypes.memmove(slot_addr + item_bytes - TRAILER_BYTES, trailer.ctypes.data, 24)
+    return True
+
+
+def slot_frames(ring_u8: np.ndarray, slots: Sequence[int], key: int) -> List[Tuple[int, int]]:
+    """[(index in ``slots``, prepared bytes)] of the slots that hold prepared frames (``ring_u8``: [nslots, item])."""
+    if not key or len(slots) == 0:
+        return []
+    tail = ring_u8[np.asarray(slots, np.int64), -TRAILER_BYTES:]
+    words = np.ascontiguousarray(tail).view(np.uint64)
+    hit = np.nonzero((words[:, 0] == np.uint64(SLOT_MAGIC)) & (words[:, 1] == np.uint64(key)))[0]
+    item = ring_u8.shape[1]
+    return [(int(j), int(words[j, 2])) for j in hit if 0 < int(words[j, 2]) <= item - TRAILER_BYTES]
+
+
 # ----------------------------------------------------------------------------------------------------- GPU decoder
 _DESC_FIELDS = ([("scan", "u8"), ("coef", "u8"), ("exit0", "u8"), ("exit1", "u8"), ("chg0", "u8"), ("chg1", "u8"),
                  ("counts", "u8"), ("planes", "u8"), ("rows", "u8"), ("out", "u8"), ("hk", "u8"), ("hb", "u8"),
@@ -294,6 +403,146 @@ assert DESC_DTYPE.itemsize == 200  # sizeof(JpegFrameDesc)
 
 def _align(n: int, a: int = 256) -> int:
     return (n + a - 1) // a * a
+
+
+def header_sane(hdr: dict, used: int) -> bool:
+    """Consistency of a prepared frame's header with its own geometry and size (the worker checks what the front-end
+    wrote before any kernel reads it)."""
+    from aiforearth_api_platform_amd import _ai4e_core as core
+
+    try:
+        W, H, nc, hm, vm = hdr["width"], hdr["height"], hdr["ncomp"], hdr["hmax"], hdr["vmax"]
+        if hdr["magic"] != SCAN_MAGIC or nc not in (1, 3) or not (0 < W <= 65535 and 0 < H <= 65535):
+            return False
+        if core.JPEG_SCAN_HEADER_BYTES + hdr["data_bytes"] + 64 > used or hdr["total_bits"] > 8 * hdr["data_bytes"]:
+            return False
+        if nc == 1:
+            mcux, mcuy, bpm = -(-W // 8), -(-H // 8), 1
+        else:
+            mcux, mcuy = -(-W // (8 * hm)), -(-H // (8 * vm))
+            bpm = sum(c[0] * c[1] for c in hdr["comp"])
+        if (hdr["mcux"], hdr["mcuy"], hdr["bpm"]) != (mcux, mcuy, bpm) or bpm > 10:
+            return False
+        nb = 0
+        for c in hdr["comp"]:
+            h, v, bw, bh, first, tq = c[:6]
+            if nc == 3 and (bw != mcux * h or bh != mcuy * v):
+                return False
+            if first != nb or tq > 3 or c[6] > 1 or c[7] > 1:
+                return False
+            nb += bw * bh
+        return nb == hdr["nblocks"] == mcux * mcuy * bpm
+    except (KeyError, IndexError, TypeError):
+        return False
+
+
+class JpegLauncher:
+    """Device work areas + frame descriptors + one ``ai4e_jpeg_decode`` launch for a batch of prepared frames that are
+    already on the device. Launches on one stream are ordered, so the work areas and the coefficient array (zero
+    between batches: the IDCT clears what it reads) are reused batch after batch."""
+
+    def __init__(self, device, span_bits: int = DEFAULT_SPAN_BITS, sync_passes: int = DEFAULT_SYNC_PASSES):
+        import torch
+
+        from aiforearth_api_platform_amd.ops import _ext
+
+        self.torch, self._ext = torch, _ext
+        _ext.lib()  # loud failure when the kernel library is missing
+        self.device = torch.device(device)
+        self.span_bits = int(span_bits)
+        self.sync_passes = int(sync_passes)
+        self._work = None
+        self._coef = None
+        self._coeff_cache = {}
+        self._templates = {}
+
+    def _resample(self, n_in: int, n_out: int):
+        t = self._coeff_cache.get((n_in, n_out))
+        if t is None:
+            bounds, kk = pil_bilinear_coeffs(n_in, n_out)
+            torch = self.torch
+            t = (torch.from_numpy(bounds).to(self.device), torch.from_numpy(kk).to(self.device), kk.shape[1])
+            self._coeff_cache[(n_in, n_out)] = t
+        return t
+
+    def grow(self, cur, nbytes: int):
+        """A uint8 device area of at least ``nbytes`` (``cur`` when it is large enough)."""
+        return self._buf(cur, nbytes)
+
+    def _buf(self, cur, nbytes: int, zero: bool = False):
+        torch = self.torch
+        if cur is not None and cur.numel() * cur.element_size() >= nbytes:
+            return cur
+        n = _align(max(int(nbytes * 1.25), 1), 1 << 20)
+        if zero:
+            return torch.zeros(n // 2, dtype=torch.int16, device=self.device)
+        return torch.empty(n, dtype=torch.uint8, device=self.device)
+
+    def _template(self, plan: FramePlan):
+        """The plan-dependent part of a descriptor (+ its planes / rows bytes), built once per plan."""
+        t = self._templates.get(plan)
+        if t is None:
+            d = np.zeros(1, DESC_DTYPE)[0]
+            dims = plan.plane_dims
+            poff = 0
+            for c in range(3):
+                if c < plan.ncomp:
+                    d[f"ssize{c}"], d[f"plane_off{c}"], d[f"plane_pitch{c}"] = plan.ssize[c], poff, dims[c][0]
+                    poff += dims[c][0] * dims[c][1]
+                else:
+                    d[f"ssize{c}"], d[f"plane_off{c}"], d[f"plane_pitch{c}"] = 1, 0, dims[0][0]
+            d["span_bits"] = self.span_bits
+            d["src_w"], d["src_h"], d["out_w"], d["out_h"], d["out_c"] = plan.src_w, plan.src_h, plan.out_w, plan.out_h, 3
+            hv = [c[0] * c[1] for c in plan.comp]
+            d["kbase1"] = hv[0]
+            d["kbase2"] = hv[0] + (hv[1] if len(hv) > 1 else 0)
+            hb, hk, hks = self._resample(plan.src_w, plan.out_w)
+            vb, vk, vks = self._resample(plan.src_h, plan.out_h)
+            d["hb"], d["hk"], d["hks"] = hb.data_ptr(), hk.data_ptr(), hks
+            d["vb"], d["vk"], d["vks"] = vb.data_ptr(), vk.data_ptr(), vks
+            t = (d, poff, plan.src_h * plan.out_w * 3)
+            self._templates[plan] = t
+        return t
+
+    def launch(self, frames, stream):
+        """``frames``: [(hdr, plan, device address of the prepared bytes, device address of the uint8 HWC output)].
+        Returns the per-frame status (int32 device tensor: 0 ok, bit 1 corrupt data) and what must stay alive until
+        the launch has run. Descriptors are built column-wise (one template per distinct plan)."""
+        torch = self.torch
+        n = len(frames)
+        with torch.cuda.stream(stream):
+            tmpl = [self._template(p) for _, p, _, _ in frames]
+            descs = np.array([t[0] for t in tmpl], DESC_DTYPE)
+            nthr = np.array([max(1, -(-h["total_bits"] // self.span_bits)) for h, _, _, _ in frames], np.int64)
+            nblk = np.array([h["nblocks"] for h, _, _, _ in frames], np.int64)
+            al = lambda x: (x + 255) // 256 * 256  # noqa: E731
+            e8, c4, c16 = al(8 * nthr), al(4 * nthr), al(16 * nthr)
+            pl = al(np.array([t[1] for t in tmpl], np.int64))
+            rw = al(np.array([t[2] for t in tmpl], np.int64))
+            per = 2 * e8 + 2 * c4 + c16 + pl + rw
+            fbase = np.concatenate([[0], np.cumsum(per)[:-1]])
+            cbytes = nblk * 128
+            cb = np.concatenate([[0], np.cumsum(cbytes)[:-1]])
+            self._work = self._buf(self._work, int(per.sum()))
+            self._coef = self._buf(self._coef, int(cbytes.sum()), zero=True)
+            status = torch.zeros(n, dtype=torch.int32, device=self.device)
+            w = self._work.data_ptr() + fbase
+            descs["exit0"], descs["exit1"] = w, w + e8
+            descs["chg0"], descs["chg1"] = w + 2 * e8, w + 2 * e8 + c4
+            descs["counts"] = w + 2 * e8 + 2 * c4
+            descs["planes"] = w + 2 * e8 + 2 * c4 + c16
+            descs["rows"] = w + 2 * e8 + 2 * c4 + c16 + pl
+            descs["coef"] = self._coef.data_ptr() + cb
+            descs["scan"] = np.array([f[2] for f in frames], np.uint64)
+            descs["out"] = np.array([f[3] for f in frames], np.uint64)
+            descs["status"] = status.data_ptr() + 4 * np.arange(n, dtype=np.uint64)
+            descs["nthreads"] = nthr
+            max_rows = int(max(t[0]["src_h"] for t in tmpl)) * int(max(t[0]["out_w"] for t in tmpl))
+            max_out = int(max(t[0]["out_h"] * t[0]["out_w"] for t in tmpl)) * 3
+            ddesc = torch.from_numpy(descs.view(np.uint8)).pin_memory().to(self.device, non_blocking=True)
+            self._ext.call("ai4e_jpeg_decode", ddesc.data_ptr(), n, int(nthr.max()), int(nblk.max()), max_rows, max_out,
+                           self.sync_passes, stream.cuda_stream)
+        return status, ddesc
 
 
 @dataclass
@@ -311,12 +560,11 @@ class JpegGpuDecoder:
     """Batched on-GPU decode of JPEG bodies to uint8 [B, H, W, 3] on ``device`` (bit-identical to ``decode_image``).
 
     ``submit(bodies)`` prepares the frames on ``threads`` CPU threads (header parse + unstuffed copy into pinned
-    staging, laid out back to back so one copy moves the batch), copies them to the GPU and launches
-    ``ai4e_jpeg_decode`` on the current stream without waiting; ``finish(pending)`` reads the per-frame statuses (one
-    small read per batch) and decodes on the CPU (``decode_image``) the frames the GPU path does not cover or whose
-    decode reported an error. Two batches may be in flight (double-buffered staging), so a caller overlaps preparing
-    batch i+1 with the GPU decoding batch i. ``errors`` holds the message of each frame that could not be decoded at
-    all (its output is left zero).
+    staging, laid out back to back so one copy moves the batch), copies them to the GPU and launches the kernels on the
+    current stream without waiting; ``finish(pending)`` reads the per-frame statuses (one small read per batch) and
+    decodes on the CPU (``decode_image``) the frames the GPU path does not cover or whose data is corrupt. Two batches
+    may be in flight (double-buffered staging), so a caller overlaps preparing batch i+1 with the GPU decoding batch i.
+    ``errors`` holds the message of each frame that could not be decoded at all (its output is left zero).
     """
 
     def __init__(self, shape: Tuple[int, int, int], device="cuda", threads: int = 8, span_bits: int = DEFAULT_SPAN_BITS,
@@ -324,28 +572,22 @@ class JpegGpuDecoder:
         import torch
 
         from aiforearth_api_platform_amd import _ai4e_core as core
-        from aiforearth_api_platform_amd.ops import _ext
 
-        self.torch, self.core, self._ext = torch, core, _ext
-        _ext.lib()  # loud failure when the kernel library is missing
+        self.torch, self.core = torch, core
         self.shape = tuple(shape)
         self.device = torch.device(device)
-        self.span_bits = int(span_bits)
-        self.sync_passes = int(sync_passes)
+        self.launcher = JpegLauncher(self.device, span_bits, sync_passes)
         self.hdr_bytes = int(core.JPEG_SCAN_HEADER_BYTES)
-        self.pool = ThreadPoolExecutor(max(1, threads), thread_name_prefix="jpeg-prep")
+        self.threads = max(1, int(threads))
+        self.pool = ThreadPoolExecutor(self.threads, thread_name_prefix="jpeg-prep")
         self._staging: List = [None, None]  # pinned host staging, double-buffered across batches
         self._staging_evt: List = [None, None]
+        self._scan: List = [None, None]
         self._flip = 0
-        self._coef = torch.zeros(0, dtype=torch.int16, device=self.device)  # zero between batches (the IDCT clears it)
-        self._work = [torch.empty(0, dtype=torch.uint8, device=self.device) for _ in range(2)]
-        self._scan = [torch.empty(0, dtype=torch.uint8, device=self.device) for _ in range(2)]
-        self._coeff_cache = {}
         self._lock = threading.Lock()
         self.errors = {}
         self.stats = dict(frames=0, gpu_frames=0, cpu_frames=0, unsupported=0, failed=0)
 
-    # -- helpers
     def _pinned(self, nbytes: int):
         torch = self.torch
         i = self._flip
@@ -357,26 +599,6 @@ class JpegGpuDecoder:
             self._staging[i] = buf
         return buf
 
-    def _resample(self, n_in: int, n_out: int):
-        key = (n_in, n_out)
-        t = self._coeff_cache.get(key)
-        if t is None:
-            bounds, kk = pil_bilinear_coeffs(n_in, n_out)
-            torch = self.torch
-            t = (torch.from_numpy(bounds).to(self.device), torch.from_numpy(kk).to(self.device), kk.shape[1])
-            self._coeff_cache[key] = t
-        return t
-
-    def _device_buf(self, cur, nbytes: int, zero: bool = False):
-        torch = self.torch
-        if cur.numel() * cur.element_size() >= nbytes:
-            return cur
-        n = _align(int(nbytes * 1.25), 1 << 20)
-        if zero:
-            return torch.zeros(n // 2, dtype=torch.int16, device=self.device)
-        return torch.empty(n, dtype=torch.uint8, device=self.device)
-
-    # -- API
     def decode(self, bodies: Sequence[bytes], out=None):
         """uint8 [len(bodies), H, W, 3] on the device (``out`` if given), all frames decoded."""
         return self.finish(self.submit(bodies, out))
@@ -394,23 +616,39 @@ class JpegGpuDecoder:
         offs = np.concatenate([[0], np.cumsum(caps)]).astype(np.int64)
         staging = self._pinned(int(offs[-1]))
         base = staging.data_ptr()
-        results = list(self.pool.map(lambda i: self.core.jpeg_scan_prepare(bodies[i], base + int(offs[i]), caps[i]),
-                                     range(B)))
+        nt = min(self.threads, B)
+
+        def chunk(k):  # one task per thread (a future per frame costs more than the frame's header parse)
+            return [self.core.jpeg_scan_prepare(bodies[i], base + int(offs[i]), caps[i]) for i in range(k, B, nt)]
+
+        parts = list(self.pool.map(chunk, range(nt)))
+        results = [parts[i % nt][i // nt] for i in range(B)]
         host = staging.numpy()
-        plans: List = []
+        frames, gpu, cpu = [], [], []
         for i, (st, used) in enumerate(results):
-            plan = None
             if st == ST_OK:
                 hdr = parse_header(host[offs[i]:offs[i] + 160])
-                p = plan_frame(hdr, w_out, h_out, c_out)
-                if p is not None:
-                    plan = (p, hdr, used)
-            plans.append(plan)
-        gpu = [i for i, p in enumerate(plans) if p is not None]
-        cpu = [i for i, p in enumerate(plans) if p is None]
+                plan = plan_frame(hdr, w_out, h_out, c_out)
+                if plan is not None:
+                    frames.append((hdr, plan, int(offs[i]), out[i].data_ptr()))
+                    gpu.append(i)
+                    continue
+            cpu.append(i)
         pending = Pending(bodies, out, gpu, cpu)
         if gpu:
-            pending.status, pending.keep = self._launch(gpu, plans, staging, offs, out)
+            k = self._flip
+            stream = torch.cuda.current_stream(self.device)
+            total = int(offs[gpu[-1] + 1])
+            with torch.cuda.stream(stream):
+                self._scan[k] = self.launcher._buf(self._scan[k], total)
+                self._scan[k][:total].copy_(staging[:total], non_blocking=True)  # the whole batch in one copy
+            evt = torch.cuda.Event()
+            evt.record(stream)
+            self._staging_evt[k] = evt
+            sbase = self._scan[k].data_ptr()
+            frames = [(h, p, sbase + o, dst) for h, p, o, dst in frames]
+            pending.status, keep = self.launcher.launch(frames, stream)
+            pending.keep = (keep, self._scan[k])
         self._flip ^= 1
         with self._lock:
             self.stats["frames"] += B
@@ -445,72 +683,6 @@ class JpegGpuDecoder:
             with self._lock:
                 self.stats["cpu_frames"] += len(cpu)
         return p.out
-
-    def _launch(self, gpu: List[int], plans, staging, offs, out):
-        torch = self.torch
-        h_out, w_out, c_out = self.shape
-        k = self._flip
-        total = int(offs[gpu[-1] + 1])
-        dscan = self._scan[k] = self._device_buf(self._scan[k], total)
-        dscan[:total].copy_(staging[:total], non_blocking=True)  # the whole batch in one copy
-        evt = torch.cuda.Event()
-        evt.record(torch.cuda.current_stream(self.device))
-        self._staging_evt[k] = evt
-        descs = np.zeros(len(gpu), DESC_DTYPE)
-        work_off = coef_off = 0
-        layout = []
-        max_threads = max_blocks = max_rows = max_out = 0
-        for j, i in enumerate(gpu):
-            plan, hdr, used = plans[i]
-            nthreads = max(1, -(-hdr["total_bits"] // self.span_bits))
-            dims = plan.plane_dims
-            sizes = dict(exit0=8 * nthreads, exit1=8 * nthreads, chg0=4 * nthreads, chg1=4 * nthreads,
-                         counts=16 * nthreads, planes=sum(pp * r for pp, r in dims), rows=plan.src_h * w_out * c_out)
-            fo = {}
-            for name, v in sizes.items():
-                fo[name] = work_off
-                work_off += _align(v)
-            layout.append((fo, coef_off))
-            coef_off += hdr["nblocks"] * 128
-            max_threads = max(max_threads, nthreads)
-            max_blocks = max(max_blocks, hdr["nblocks"])
-            max_rows = max(max_rows, plan.src_h * w_out)
-            max_out = max(max_out, h_out * w_out * c_out)
-            d = descs[j]
-            d["nthreads"], d["span_bits"] = nthreads, self.span_bits
-            poff = 0
-            for c in range(3):
-                if c < plan.ncomp:
-                    d[f"ssize{c}"], d[f"plane_off{c}"], d[f"plane_pitch{c}"] = plan.ssize[c], poff, dims[c][0]
-                    poff += dims[c][0] * dims[c][1]
-                else:
-                    d[f"ssize{c}"], d[f"plane_off{c}"], d[f"plane_pitch{c}"] = 1, 0, dims[0][0]
-            d["src_w"], d["src_h"], d["out_w"], d["out_h"], d["out_c"] = plan.src_w, plan.src_h, w_out, h_out, c_out
-            hv = [c[0] * c[1] for c in plan.comp]
-            d["kbase1"] = hv[0]
-            d["kbase2"] = hv[0] + (hv[1] if len(hv) > 1 else 0)
-        work = self._work[k] = self._device_buf(self._work[k], work_off)
-        self._coef = self._device_buf(self._coef, coef_off, zero=True)
-        wbase, cbase, sbase = work.data_ptr(), self._coef.data_ptr(), dscan.data_ptr()
-        status = torch.zeros(len(gpu), dtype=torch.int32, device=self.device)
-        for j, i in enumerate(gpu):
-            plan = plans[i][0]
-            fo, coff = layout[j]
-            d = descs[j]
-            d["scan"] = sbase + int(offs[i])
-            d["coef"] = cbase + coff
-            for name in ("exit0", "exit1", "chg0", "chg1", "counts", "planes", "rows"):
-                d[name] = wbase + fo[name]
-            d["status"] = status.data_ptr() + 4 * j
-            d["out"] = out[i].data_ptr()
-            hb, hk, hks = self._resample(plan.src_w, w_out)
-            vb, vk, vks = self._resample(plan.src_h, h_out)
-            d["hb"], d["hk"], d["hks"] = hb.data_ptr(), hk.data_ptr(), hks
-            d["vb"], d["vk"], d["vks"] = vb.data_ptr(), vk.data_ptr(), vks
-        ddesc = torch.from_numpy(descs.view(np.uint8)).pin_memory().to(self.device, non_blocking=True)
-        self._ext.call("ai4e_jpeg_decode", ddesc.data_ptr(), len(gpu), max_threads, max_blocks, max_rows, max_out,
-                       self.sync_passes, self._ext.stream_ptr(self.device))
-        return status, (ddesc, dscan, work)
 
     def close(self):
         self.pool.shutdown(wait=True)

@@ -26,6 +26,7 @@ import torch
 from ..store import STATE_CREATED, STATE_FAILED
 from .decode import PayloadError, decode_image  # noqa: F401  (re-exported: the endpoint's payload API)
 from .ingest import StreamedBatch
+from .jpeg_gpu import JPEG_TYPES, prepare_into_slot
 from .serving import GpuBatchWorker
 
 PAYLOAD_LOST = "Task failed - payload lost on restart"
@@ -108,7 +109,19 @@ class ModelEndpoint:
 
         Raises :class:`PayloadError` (-> HTTP 400/415) before any task exists for undecodable bodies."""
         ct = (content_type or "").split(";")[0].strip().lower()
-        if self.decode_pool is not None and ct not in ("", "application/octet-stream"):
+        key = getattr(self.ring, "jpeg_key", 0) if self.is_pool and not self.custom_decode else 0
+        if key and ct in JPEG_TYPES:
+            # JPEG: prepared straight into the slot (headers + unstuffed scan, ~0.2 ms) for the worker to decode on its
+            # GPU (runtime/jpeg_gpu.py); frames outside the GPU path's envelope are decoded here as before
+            slot = self.ring.alloc(1, timeout=30)[0]
+            try:
+                item = int(np.prod(self.item_shape))
+                if not prepare_into_slot(body, self.ring.buf[slot].data_ptr(), item, self.item_shape, key):
+                    self._write([slot], self.decode(body, content_type)[None])
+            except BaseException:
+                self.ring.free([slot])
+                raise
+        elif self.decode_pool is not None and ct not in ("", "application/octet-stream"):
             slot = self.ring.alloc(1, timeout=30)[0]
             try:
                 self.decode_pool.decode_into(slot, body, content_type)

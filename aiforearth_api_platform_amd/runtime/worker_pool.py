@@ -49,13 +49,28 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
+def _jpeg_slots_default(devices: Sequence[str], flag: Optional[bool]) -> bool:
+    """Prepared JPEG slots are decoded on the GPU; a CPU worker would decode them with the slow numpy reference."""
+    if flag is not None:
+        return bool(flag)
+    env = os.environ.get("AI4E_JPEG_SLOTS", "")
+    if env:
+        return env not in ("0", "false", "no")
+    return any(str(d).startswith("cuda") for d in devices)
+
+
 class SharedPayloadRing:
     """The node's payload ring in POSIX shared memory + the native slot allocator of this process's
     ingest partition ``[0, local_slots)``; slots beyond belong to remote ingest shards."""
 
-    def __init__(self, nslots: int, item_shape: Sequence[int], local_slots: Optional[int] = None, durable=None):
+    def __init__(self, nslots: int, item_shape: Sequence[int], local_slots: Optional[int] = None, durable=None,
+                 jpeg_slots: bool = False):
         """``durable``: a :class:`runtime.durable_ring.DurableRing` (a task journal is configured): the ring is a
-        crash-surviving segment with a per-slot task-id tag segment (``tags_name``) the schedulers write."""
+        crash-surviving segment with a per-slot task-id tag segment (``tags_name``) the schedulers write.
+        ``jpeg_slots``: the ring's workers decode JPEG frames prepared into slots (runtime/jpeg_gpu.py): the segment's
+        tail holds the key front-ends mark such slots with (``jpeg_key``; 0 when off)."""
+        from .jpeg_gpu import RING_TAIL_BYTES, init_ring_tail
+
         self.nslots = int(nslots)
         self.item_shape = tuple(int(x) for x in item_shape)
         nbytes = self.nslots * int(np.prod(self.item_shape))
@@ -64,7 +79,9 @@ class SharedPayloadRing:
         if durable is not None:
             self.shm, self.tags_name = durable.create(self.nslots, self.item_shape)
         else:
-            self.shm = shared_memory.SharedMemory(create=True, size=max(nbytes, 1))
+            self.shm = shared_memory.SharedMemory(create=True, size=nbytes + RING_TAIL_BYTES)
+        image = len(self.item_shape) == 3 and self.item_shape[2] == 3
+        self.jpeg_key = init_ring_tail(self.shm.buf, nbytes, bool(jpeg_slots) and image)
         self.buf = torch.frombuffer(self.shm.buf, dtype=torch.uint8, count=nbytes).view(self.nslots, *self.item_shape)
         self.slots = native.SlotRing(int(local_slots or self.nslots), 0)
 
@@ -122,6 +139,7 @@ class RingPartition:
         self.buf = ring.buf
         self.base, self.length = int(base), int(length)
         self.slots = native.SlotRing(self.length, self.base)
+        self.jpeg_key = ring.jpeg_key
 
     @property
     def name(self) -> str:
@@ -193,12 +211,15 @@ class WorkerPool:
                  max_restarts: int = 2, pipeline_depth: int = 3, retry_delay_s: float = 1.0,
                  remote_partitions: Sequence[Tuple[int, int, int]] = (), completion_feed: bool = False,
                  poll_s: float = 0.02, frontends: int = 0, frontend_slots: int = 0,
-                 shard: Optional["ShardLayout"] = None, durable=None, busy_delay_s: float = 0.002):
+                 shard: Optional["ShardLayout"] = None, durable=None, busy_delay_s: float = 0.002,
+                 jpeg_slots: Optional[bool] = None):
         """``max_delay_s``: how long a batch waits to fill when the worker is idle; ``busy_delay_s``: when it already
         has a batch in flight (its GPU is busy: a fuller batch costs no throughput, and arrivals of single images
         otherwise leave as many small batches, each in a padded graph bucket). ``shard``: this pool is one
         control-plane shard of a :class:`ShardedWorkerPool` (its own dispatch queue and scheduler, a partition of the
-        shared ring, ids minted in its own task-store lock domains)."""
+        shared ring, ids minted in its own task-store lock domains). ``jpeg_slots``: front-ends may prepare JPEG
+        bodies into slots for the workers to decode on the GPU (runtime/jpeg_gpu.py; default: when the devices are
+        GPUs, or AI4E_JPEG_SLOTS=1)."""
         if native is None:
             raise RuntimeError("the worker pool needs the native core (_ai4e_core)")
         self.cp = control_plane
@@ -230,7 +251,8 @@ class WorkerPool:
             self.frontend_partitions = [(end + i * fs, fs, FRONTEND_RANK0 + i) for i in range(int(frontends))]
             self.remote_partitions += self.frontend_partitions
             total = max([local] + [b + n for b, n, _ in self.remote_partitions])
-            self.ring = SharedPayloadRing(total, spec.item_shape, local_slots=local, durable=durable)
+            self.ring = SharedPayloadRing(total, spec.item_shape, local_slots=local, durable=durable,
+                                          jpeg_slots=_jpeg_slots_default(devices, jpeg_slots))
         self.hb_interval = heartbeat_interval_s
         self.max_restarts = max_restarts
         self.sched = native.NodeScheduler(self.store, self.queue, endpoint, total, max_batch=spec.max_batch,
@@ -654,7 +676,8 @@ class ShardedWorkerPool:
 
     def __init__(self, control_plane, endpoint: str, spec: ModelSpec, devices: Sequence[str], shards: int = 0,
                  ring_slots: int = 0, frontends: int = 0, frontend_slots: int = 0, pipeline_depth: int = 3,
-                 remote: Sequence[int] = (), remote_slots: int = 0, durable=None, **kw):
+                 remote: Sequence[int] = (), remote_slots: int = 0, durable=None, jpeg_slots: Optional[bool] = None,
+                 **kw):
         """``remote``: shards whose worker is a process started elsewhere (a torchrun rank of the multi-GPU bench) that
         attaches with ``control_shards[i].attach_remote(i, conn)`` and ingests into its own ``remote_slots`` partition
         (``remote_partition(i)``); nothing is spawned for those shards."""
@@ -692,7 +715,8 @@ class ShardedWorkerPool:
                 parts.append((base, fs, FRONTEND_RANK0 + f))
                 base += fs
             layout[i].append(parts)
-        self._ring = SharedPayloadRing(base, spec.item_shape, local_slots=1, durable=durable)
+        self._ring = SharedPayloadRing(base, spec.item_shape, local_slots=1, durable=durable,
+                                       jpeg_slots=_jpeg_slots_default(self.devices, jpeg_slots))
         self.pools: List[WorkerPool] = []
         for i in range(K):
             lay = ShardLayout(i, self._ring, layout[i][0], layout[i][1], [s for s in range(nstore) if s % K == i],

@@ -17,6 +17,8 @@
 
 #include "dispatch_queue.h"
 #include "jpeg_coef.h"
+#define AI4E_HD
+#include "jpeg_span.h"
 #include "scheduler.h"
 #include "slot_ring.h"
 #include "task_store.h"
@@ -293,6 +295,44 @@ PYBIND11_MODULE(_ai4e_core, m) {
       },
       py::arg("data"), py::arg("out"), py::arg("cap"));
   m.attr("JPEG_SCAN_HEADER_BYTES") = sizeof(JpegScanHeader);
+  // Sequential CPU decode of a prepared frame (address `src`, `size` bytes) into int16 [nblocks][64] at `out` (MCU
+  // order, natural order, DC undifferenced, not dequantised): the GPU kernels' own span decoder run as one span. For
+  // workers on CPU devices and tests. Returns 0 ok, 2 corrupt.
+  m.def(
+      "jpeg_scan_coefs",
+      [](uintptr_t src, size_t size, uintptr_t out) {
+        py::gil_scoped_release rel;
+        const auto* H = reinterpret_cast<const JpegScanHeader*>(src);
+        if (size < sizeof(JpegScanHeader) || H->magic != kJpegScanMagic || H->bpm == 0 || H->bpm > 16 ||
+            sizeof(JpegScanHeader) + H->scan_bytes + kJpegScanPad > size)
+          return 2;
+        static const uint8_t zz[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,
+                                       12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13, 6,  7,  14, 21, 28,
+                                       35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
+                                       58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
+        std::vector<uint32_t> lut(4u << kGpuLook);
+        for (int t = 0; t < 2; ++t) {
+          std::memcpy(&lut[static_cast<size_t>(t) << kGpuLook], H->dc[t].fast, sizeof(H->dc[t].fast));
+          std::memcpy(&lut[static_cast<size_t>(2 + t) << kGpuLook], H->ac[t].fast, sizeof(H->ac[t].fast));
+        }
+        uint8_t nat[80], btab[16] = {};
+        for (int i = 0; i < 80; ++i) nat[i] = i < 64 ? zz[i] : 63;
+        for (uint32_t k = 0; k < H->bpm; ++k) {
+          const int c = H->blk_comp[k] < 3 ? H->blk_comp[k] : 0;
+          btab[k] = static_cast<uint8_t>((H->comp[c][6] & 1) | ((H->comp[c][7] & 1) << 2) | (c << 4));
+        }
+        const auto* words = reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(src) +
+                                                              sizeof(JpegScanHeader));
+        JSpanTables T{lut.data(), H->dc, btab, nat, words,
+                      static_cast<uint32_t>((H->scan_bytes + kJpegScanPad) / 4), static_cast<int>(H->bpm)};
+        auto* coef = reinterpret_cast<int16_t*>(out);
+        std::memset(coef, 0, static_cast<size_t>(H->nblocks) * 128);
+        const int32_t pred[3] = {0, 0, 0};
+        JSpanResult r;
+        jspan_decode<true>(T, 0, 0, 0, H->total_bits, r, coef, 0, pred, static_cast<int32_t>(H->nblocks));
+        return (r.bad || r.nblk < static_cast<int32_t>(H->nblocks)) ? 2 : 0;
+      },
+      py::arg("src"), py::arg("size"), py::arg("out"));
 
   py::class_<NodeScheduler, std::shared_ptr<NodeScheduler>>(m, "NodeScheduler")
       .def(py::init([](std::shared_ptr<TaskStore> store, std::shared_ptr<DispatchQueue> queue, std::string endpoint,

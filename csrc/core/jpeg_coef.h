@@ -51,6 +51,32 @@ static const uint8_t kZigzag[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 
                                     35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
                                     58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
 
+// Whether a prepared frame can be decoded on the GPU for a (out_h, out_w, out_c) model input bit-identically to the CPU
+// path (runtime/decode.py decode_image: PIL's draft scale, libjpeg's per-component IDCT sizes with no upsampling left
+// over, no reducing_gap pre-reduction in the resize). Mirrors runtime/jpeg_gpu.py plan_frame.
+inline bool jpeg_gpu_plan_ok(const JpegScanHeader& H, int out_h, int out_w, int out_c) {
+  if (out_c != 3 || out_h <= 0 || out_w <= 0 || H.magic != kJpegScanMagic) return false;
+  const int W = static_cast<int>(H.width), Ht = static_cast<int>(H.height);
+  int s = 1;
+  if (W >= 2 * out_w || Ht >= 2 * out_h) {
+    const int sc = std::min(W / out_w, Ht / out_h);
+    s = sc >= 8 ? 8 : sc >= 4 ? 4 : sc >= 2 ? 2 : 1;
+  }
+  const int src_w = (W + s - 1) / s, src_h = (Ht + s - 1) / s;
+  if (static_cast<int>(static_cast<double>(src_w) / out_w / 2.0) > 1 ||
+      static_cast<int>(static_cast<double>(src_h) / out_h / 2.0) > 1)
+    return false;
+  const int min_s = 8 / s;
+  for (uint32_t c = 0; c < H.ncomp; ++c) {
+    const int h = static_cast<int>(H.comp[c][0]), v = static_cast<int>(H.comp[c][1]);
+    const int hm = static_cast<int>(H.hmax), vm = static_cast<int>(H.vmax);
+    int ss = min_s;
+    while (ss < 8 && (hm * min_s) % (h * ss * 2) == 0 && (vm * min_s) % (v * ss * 2) == 0) ss *= 2;
+    if ((hm * min_s) != h * ss || (vm * min_s) != v * ss) return false;  // would need upsampling
+  }
+  return true;
+}
+
 class JpegCoefDecoder {
  public:
   // Bytes the slot layout of a frame of at most `max_w` x `max_h` pixels needs in the worst case (every coefficient
@@ -426,6 +452,7 @@ class JpegCoefDecoder {
       comp_[c].td = s[2 + 2 * i] >> 4;
       comp_[c].ta = s[2 + 2 * i] & 15;
       if (comp_[c].td > 3 || comp_[c].ta > 3 || !dc_[comp_[c].td].ok || !ac_[comp_[c].ta].ok) return kCorrupt;
+      if (comp_[c].td > 1 || comp_[c].ta > 1) return kUnsupported;  // (the GPU layout carries tables 0 and 1)
     }
     if (s[1 + 2 * ns] != 0 || s[2 + 2 * ns] != 63 || s[3 + 2 * ns] != 0) return kUnsupported;
     p_ += l;
@@ -463,7 +490,7 @@ class JpegCoefDecoder {
     H->mcuy = static_cast<uint32_t>(mcuy_);
     H->bpm = bpm;
     std::memcpy(H->quant, quant_, sizeof(quant_));
-    for (int t = 0; t < 4; ++t) {
+    for (int t = 0; t < 2; ++t) {
       if (dc_[t].ok) gpu_table(dc_[t], false, &H->dc[t]);
       else std::memset(&H->dc[t], 0, sizeof(GpuHuff));
       if (ac_[t].ok) gpu_table(ac_[t], true, &H->ac[t]);

@@ -28,11 +28,32 @@ struct JpegScanHeader {
   uint8_t blk_dx[16];
   uint8_t pad2[16];
   uint16_t quant[4][64];  // natural order
-  GpuHuff dc[4], ac[4];
+  GpuHuff dc[2], ac[2];   // baseline tables 0 and 1 (a scan naming table 2 or 3 is decoded on the CPU)
 };
 static_assert(sizeof(JpegScanHeader) % 16 == 0, "JpegScanHeader alignment");
 static constexpr uint32_t kJpegScanMagic = 0x3153434a;  // "JCS1"
 static constexpr size_t kJpegScanPad = 64;
+
+// A payload-ring slot that holds a prepared frame (instead of decoded pixels) ends with this trailer; `key` is the
+// ring's secret (RingTail, written by the ring's creator), so a raw payload (which always fills its whole slot) can
+// never be taken for one.
+struct JpegSlotTrailer {
+  uint64_t magic;
+  uint64_t key;
+  uint32_t used;  // prepared bytes at the start of the slot
+  uint32_t pad;
+  uint64_t pad2;
+};
+static_assert(sizeof(JpegSlotTrailer) == 32, "JpegSlotTrailer layout");
+static constexpr uint64_t kJpegSlotMagic = 0x3153504a45344941ull;  // "AI4EJPS1"
+// after the ring's slots: magic, key (0: the ring's workers do not decode prepared frames)
+struct RingTail {
+  uint64_t magic;
+  uint64_t key;
+  uint64_t pad[6];
+};
+static_assert(sizeof(RingTail) == 64, "RingTail layout");
+static constexpr uint64_t kRingTailMagic = 0x474e495245344941ull;  // "AI4ERING"
 
 // One frame of a decode batch (built by runtime/jpeg_gpu.py; device addresses).
 struct JpegFrameDesc {

@@ -34,8 +34,8 @@ AI4E_HD inline int jspan_z(uint64_t s) { return static_cast<int>((s >> 32) & 0xF
 AI4E_HD inline int jspan_cp(uint64_t s) { return static_cast<int>((s >> 40) & 0xFF); }
 
 struct JSpanTables {
-  const uint32_t* lut;     // [8][1 << kGpuLook]: DC tables 0-3, AC tables 4-7 (LDS on the GPU)
-  const GpuHuff* huff;     // dc[4], ac[4] of the JpegScanHeader (slow path: codes longer than kGpuLook)
+  const uint32_t* lut;     // [4][1 << kGpuLook]: DC tables 0-1, AC tables 0-1 (LDS on the GPU)
+  const GpuHuff* huff;     // dc[2], ac[2] of the JpegScanHeader (slow path: codes longer than kGpuLook)
   const uint8_t* blk_tab;  // per MCU block: dc table | ac table << 2 | component << 4
   const uint8_t* natural;  // zigzag -> natural order, 80 entries (64..79 -> 63, as libjpeg's jpeg_natural_order)
   const uint32_t* words;   // the unstuffed scan as 32-bit words (big-endian bytes), padded with 0xFF
@@ -87,7 +87,7 @@ AI4E_HD inline void jspan_decode(const JSpanTables& T, uint32_t pos, int z, int 
       nb += 32;
       ++wi;
     }
-    const int dct = bt & 3, act = 4 + ((bt >> 2) & 3), comp = bt >> 4;
+    const int dct = bt & 1, act = 2 + ((bt >> 2) & 1), comp = (bt >> 4) & 3;
     const int tab = z == 0 ? dct : act;
     const uint32_t e = T.lut[(tab << kGpuLook) | static_cast<uint32_t>(buf >> (64 - kGpuLook))];
     int kind = static_cast<int>(e >> 25);

@@ -61,6 +61,7 @@
 #include <openssl/ssl.h>
 
 #include "../core/common.h"
+#include "../core/jpeg_coef.h"
 #include "../core/slot_ring.h"
 
 namespace {
@@ -170,7 +171,11 @@ struct Shard {
   int idx = 0, fd = -1;
   std::string endpoint, endpoint_path, shape_str;
   int64_t nslots = 0, item = 0, base = 0, len = 0;
+  int out_h = 0, out_w = 0, out_c = 0;  // the model input (shape_str)
   uint8_t* ring = nullptr;
+  // the ring's key for slots holding prepared JPEG frames (its tail, csrc/core/jpeg_layout.h RingTail; 0: the ring's
+  // workers do not decode them, JPEG bodies go to the serving process)
+  uint64_t jpeg_key = 0;
   std::unique_ptr<ai4e::SlotRing> slots;
   std::mutex send_mu, ack_mu;
   std::condition_variable ack_cv;
@@ -616,13 +621,23 @@ void parse_config(const char* path) {
         std::perror("ai4e_ingestd: shm_open");
         std::exit(2);
       }
-      void* p = mmap(nullptr, static_cast<size_t>(s->nslots * s->item), PROT_READ | PROT_WRITE, MAP_SHARED, mfd, 0);
+      const size_t ring_bytes = static_cast<size_t>(s->nslots * s->item);
+      struct stat sb{};
+      const bool tail = fstat(mfd, &sb) == 0 && static_cast<size_t>(sb.st_size) >= ring_bytes + sizeof(ai4e::RingTail);
+      const size_t map_bytes = ring_bytes + (tail ? sizeof(ai4e::RingTail) : 0);
+      void* p = mmap(nullptr, map_bytes, PROT_READ | PROT_WRITE, MAP_SHARED, mfd, 0);
       ::close(mfd);
       if (p == MAP_FAILED) {
         std::perror("ai4e_ingestd: mmap");
         std::exit(2);
       }
       s->ring = static_cast<uint8_t*>(p);
+      if (tail) {
+        ai4e::RingTail t;
+        std::memcpy(&t, s->ring + ring_bytes, sizeof(t));
+        if (t.magic == ai4e::kRingTailMagic) s->jpeg_key = t.key;
+      }
+      if (std::sscanf(s->shape_str.c_str(), "(%d,%d,%d)", &s->out_h, &s->out_w, &s->out_c) != 3) s->jpeg_key = 0;
       s->slots = std::make_unique<ai4e::SlotRing>(s->len, s->base);
       g_cfg.shards.push_back(std::move(s));
     } else if (kw == "route") {
@@ -980,12 +995,17 @@ bool too_large(Conn& c, int64_t limit) {  // answered before the body is read: t
   return false;
 }
 
-bool proxy(Conn& c, const Request& r, const Route* route) {
+// `prebody`: the request's body, already read (a JPEG the GPU path does not take, csrc ingest_jpeg)
+bool proxy(Conn& c, const Request& r, const Route* route, const std::string* prebody = nullptr) {
   const int64_t limit = route && route->max_content_length > 0 ? std::min(route->max_content_length, kMaxBody) : kMaxBody;
   std::string body;
-  const int rb = read_body(c, r, body, limit);
-  if (rb == 413) return too_large(c, limit);
-  if (rb != 0) return false;
+  if (prebody) {
+    body = *prebody;
+  } else {
+    const int rb = read_body(c, r, body, limit);
+    if (rb == 413) return too_large(c, limit);
+    if (rb != 0) return false;
+  }
   std::string req = r.method + " " + r.target + " HTTP/1.1\r\n";
   for (auto& kv : r.headers)
     if (!is_hop(kv.first)) req += kv.first + ": " + kv.second + "\r\n";
@@ -1070,7 +1090,10 @@ std::string py_list(const std::vector<std::string>& v) {  // Python's repr of a 
 
 constexpr int64_t kDrainMax = 1 << 20;  // refused bodies read and dropped to keep a non-Expect connection
 
-bool ingest(Conn& c, const Request& r, Route& route, Shard& s, bool batch) {
+// mode: 0 one raw item, 1 a binary batch, 2 one JPEG frame (prepared into its slot for the workers' GPU decode,
+// runtime/jpeg_gpu.py; a frame the GPU path does not take goes to the serving process with its body)
+bool ingest(Conn& c, const Request& r, Route& route, Shard& s, int mode) {
+  const bool batch = mode == 1, jpeg = mode == 2;
   const int64_t nbytes = r.content_length;
   const bool ka = r.keep_alive;
   auto reject = [&](int code, const std::string& msg) {  // answer without reading the body: close after
@@ -1093,10 +1116,10 @@ bool ingest(Conn& c, const Request& r, Route& route, Shard& s, bool batch) {
   if (route.max_content_length > 0 && nbytes > route.max_content_length)
     return reject(413, "Request content too large (" + std::to_string(nbytes) +
                            "). Must be smaller than: " + std::to_string(route.max_content_length));
-  if (nbytes <= 0 || nbytes % s.item)
+  if (!jpeg && (nbytes <= 0 || nbytes % s.item))
     return reject(400, "batch payload must be a multiple of " + std::to_string(s.item) + " bytes (uint8 " +
                            s.shape_str + ")");
-  const int64_t n = nbytes / s.item;
+  const int64_t n = jpeg ? 1 : nbytes / s.item;
   if (n > s.len)
     return reject(413, "batch of " + std::to_string(n) + " items exceeds the ingest partition (" +
                            std::to_string(s.len) + " slots)");
@@ -1163,9 +1186,38 @@ bool ingest(Conn& c, const Request& r, Route& route, Shard& s, bool batch) {
     if (!c.discard(static_cast<size_t>(nbytes))) return false;
     return respond(c, 429, "application/json", message_json("Service is busy, please try again later."), ka);
   }
-  // body -> ring: one recv per contiguous slot run
   const double t_up = ai4e::mono_now();
-  for (size_t i = 0; i < sl.size();) {
+  if (jpeg) {
+    // body -> scratch -> headers + unstuffed scan into the slot (~0.2 ms), marked with the ring's key
+    thread_local std::string jbody;
+    thread_local std::unique_ptr<ai4e::JpegCoefDecoder> dec;
+    if (!dec) dec = std::make_unique<ai4e::JpegCoefDecoder>();
+    jbody.resize(static_cast<size_t>(nbytes));
+    if (!c.body_into(reinterpret_cast<uint8_t*>(jbody.data()), jbody.size())) {
+      s.slots->free(sl);
+      return false;
+    }
+    uint8_t* slot = s.ring + sl[0] * s.item;
+    const size_t cap = static_cast<size_t>(s.item) - sizeof(ai4e::JpegSlotTrailer);
+    size_t used = 0;
+    const bool ok = s.item > static_cast<int64_t>(sizeof(ai4e::JpegScanHeader) + sizeof(ai4e::JpegSlotTrailer)) &&
+                    dec->prepare(reinterpret_cast<const uint8_t*>(jbody.data()), jbody.size(), slot, cap, &used) ==
+                        ai4e::JpegCoefDecoder::kOk &&
+                    ai4e::jpeg_gpu_plan_ok(*reinterpret_cast<const ai4e::JpegScanHeader*>(slot), s.out_h, s.out_w,
+                                           s.out_c);
+    if (!ok) {  // decoded on the CPU by the serving process
+      s.slots->free(sl);
+      return proxy(c, r, &route, &jbody);
+    }
+    ai4e::JpegSlotTrailer tr{ai4e::kJpegSlotMagic, s.jpeg_key, static_cast<uint32_t>(used), 0, 0};
+    std::memcpy(slot + s.item - sizeof(tr), &tr, sizeof(tr));
+    static const bool dbg = std::getenv("AI4E_INGESTD_DEBUG") != nullptr;
+    static std::atomic<int> dbg_n{0};
+    if (dbg && dbg_n.fetch_add(1) < 4) std::fprintf(stderr, "ingestd jpeg: %zu bytes prepared into slot %lld\n", used,
+                                                    static_cast<long long>(sl[0]));
+  }
+  // body -> ring: one recv per contiguous slot run
+  for (size_t i = 0; !jpeg && i < sl.size();) {
     size_t j = i + 1;
     while (j < sl.size() && sl[j] == sl[j - 1] + 1) ++j;
     if (!c.body_into(s.ring + sl[i] * s.item, static_cast<size_t>((j - i) * s.item))) {
@@ -1283,9 +1335,12 @@ void serve_requests(Conn& c) {
     const bool ingestible = s && route->mode == "async" && (r.method == "POST" || r.method == "PUT") &&
                             r.get("taskid").empty() && !r.chunked && r.content_length >= 0;
     if (ingestible && ctype == kBatchType && r.content_length > 0) {
-      ok = ingest(c, r, *route, *s, true);
+      ok = ingest(c, r, *route, *s, 1);
     } else if (ingestible && ctype == kRawType && r.content_length == s->item) {
-      ok = ingest(c, r, *route, *s, false);
+      ok = ingest(c, r, *route, *s, 0);
+    } else if (ingestible && s->jpeg_key && r.content_length > 0 &&
+               (ctype == "image/jpeg" || ctype == "image/jpg" || ctype == "image/pjpeg")) {
+      ok = ingest(c, r, *route, *s, 2);
     } else {
       ok = proxy(c, r, route);  // encoded images, task API, sync routes, ... -> the serving process
     }

@@ -2,7 +2,8 @@
 // from the prepared scan (csrc/core/jpeg_coef.h prepare(): headers, lookup tables, unstuffed entropy-coded bits) to the
 // model's uint8 HWC input with no CPU work beyond that copy:
 //
-//   huff_spec / huff_sync x N / huff_prefix / huff_write   parallel Huffman decoding (csrc/core/jpeg_span.h)
+//   huff_sync x (1 + N) / huff_fixup / huff_prefix / huff_write   parallel Huffman decoding (csrc/core/jpeg_span.h);
+//               huff_fixup finishes, one wave per frame, the spans the N sync passes left unsettled (usually none)
 //   idct        dequantisation + libjpeg's scaled IDCT per 8x8 block (8x8 ISLOW, 4x4 / 2x2 / 1x1 reduced), clearing
 //               the coefficients it read (the array stays zero between batches)
 //   color_h     YCbCr -> RGB (libjpeg's fixed-point tables) fused into PIL's horizontal bilinear pass
@@ -33,27 +34,27 @@ __device__ const uint8_t kNatural[80] = {
 constexpr int kThreads = 256;
 
 struct SpanLds {
-  uint32_t lut[8 << kGpuLook];  // 32 KB: the frame's 4 DC + 4 AC lookahead tables
+  uint32_t lut[4 << kGpuLook];  // 16 KB: the frame's 2 DC + 2 AC lookahead tables
   uint8_t natural[80];
   uint8_t btab[16];
 };
 
-// Stage the frame's lookup tables in LDS (all 256 threads) and build the span decoder's view of the frame.
+// Stage the frame's lookup tables in LDS (every thread of the block) and build the span decoder's view of the frame.
 __device__ __forceinline__ JSpanTables stage_tables(const JpegFrameDesc& D, SpanLds& L) {
   const auto* H = reinterpret_cast<const JpegScanHeader*>(D.scan);
   const uint4* src_dc = reinterpret_cast<const uint4*>(H->dc[0].fast);
   constexpr int kPerTab = (1 << kGpuLook) / 4;                 // uint4 per fast table
   constexpr int kStride = sizeof(GpuHuff) / sizeof(uint4);     // uint4 per GpuHuff
   uint4* dst = reinterpret_cast<uint4*>(L.lut);
-  for (int i = threadIdx.x; i < 8 * kPerTab; i += kThreads) {
+  for (int i = threadIdx.x; i < 4 * kPerTab; i += blockDim.x) {
     const int t = i / kPerTab, j = i - t * kPerTab;
     dst[i] = src_dc[t * kStride + j];
   }
-  if (threadIdx.x < 80) L.natural[threadIdx.x] = kNatural[threadIdx.x];
+  for (int i = threadIdx.x; i < 80; i += blockDim.x) L.natural[i] = kNatural[i];
   if (threadIdx.x < 16) {
     const uint32_t k = threadIdx.x;
-    const int c = k < H->bpm ? H->blk_comp[k] : 0;
-    L.btab[k] = static_cast<uint8_t>(H->comp[c][6] | (H->comp[c][7] << 2) | (c << 4));
+    const int c = k < H->bpm ? min(static_cast<int>(H->blk_comp[k]), 2) : 0;
+    L.btab[k] = static_cast<uint8_t>((H->comp[c][6] & 1) | ((H->comp[c][7] & 1) << 2) | (c << 4));
   }
   __syncthreads();
   JSpanTables T;
@@ -117,6 +118,39 @@ __global__ __launch_bounds__(kThreads) void huff_sync_kernel(const JpegFrameDesc
   store_counts(D, t, r);
 }
 
+// After the sync passes: walk the frame's spans in order and re-decode, sequentially, every span whose entry state is
+// still stale (the predecessor changed in the last pass, or was re-decoded here with a new exit). One wave per frame;
+// the wave skips 64 settled spans per step, so a settled frame costs ~nthreads / 64 loads. Makes every valid frame's
+// states exact however slowly its spans synchronise.
+__global__ __launch_bounds__(64) void huff_fixup_kernel(const JpegFrameDesc* __restrict__ descs, int last) {
+  const JpegFrameDesc& D = descs[blockIdx.y];
+  auto* ex = reinterpret_cast<uint64_t*>(D.exit[last & 1]);
+  auto* chg = reinterpret_cast<uint32_t*>(D.chg[last & 1]);
+  const int n = D.nthreads;
+  int first = -1;
+  for (int b = 0; b < n - 1 && first < 0; b += 64) {
+    const int i = b + static_cast<int>(threadIdx.x);
+    const uint64_t m = __ballot(i < n - 1 && chg[i] != 0);
+    if (m) first = b + __ffsll(static_cast<long long>(m)) - 1;
+  }
+  if (first < 0) return;  // settled (wave-uniform)
+  __shared__ SpanLds L;
+  const JSpanTables T = stage_tables(D, L);
+  if (threadIdx.x != 0) return;
+  bool dirty = false;  // span t-1 was re-decoded here with a different exit
+  for (int t = first + 1; t < n; ++t) {
+    if (!dirty && !chg[t - 1]) continue;
+    chg[t - 1] = 0;
+    const uint64_t s = ex[t - 1];
+    JSpanResult r;
+    ai4e::jspan_decode<false>(T, ai4e::jspan_pos(s), ai4e::jspan_z(s), ai4e::jspan_cp(s), span_end(D, t), r);
+    dirty = r.exit != ex[t];
+    ex[t] = r.exit;
+    store_counts(D, t, r);
+  }
+  if (n >= 1) chg[n - 1] = 0;
+}
+
 // Exclusive prefix over the frame's spans of (blocks completed, DC sums): one workgroup per frame.
 __global__ __launch_bounds__(kThreads) void huff_prefix_kernel(const JpegFrameDesc* __restrict__ descs) {
   const JpegFrameDesc& D = descs[blockIdx.y];
@@ -174,7 +208,7 @@ __global__ __launch_bounds__(kThreads) void huff_write_kernel(const JpegFrameDes
   auto* ex = reinterpret_cast<const uint64_t*>(D.exit[last & 1]);
   auto* chg = reinterpret_cast<const uint32_t*>(D.chg[last & 1]);
   uint32_t* status = reinterpret_cast<uint32_t*>(D.status);
-  if (t > 0 && chg[t - 1]) atomicOr(status, 1u);  // the sync passes did not settle: the frame goes to the CPU path
+  if (t > 0 && chg[t - 1]) atomicOr(status, 1u);  // (cannot happen after the fix-up: kept as a guard)
   const uint64_t s = t ? ex[t - 1] : ai4e::jspan_pack(0, 0, 0);
   const int4 base = reinterpret_cast<const int4*>(D.counts)[t];
   const int32_t pred[3] = {base.y, base.z, base.w};
@@ -472,8 +506,8 @@ __global__ __launch_bounds__(kThreads) void resize_v_kernel(const JpegFrameDesc*
 }  // namespace
 
 // descs: device array of `nframes` JpegFrameDesc. max_threads / max_blocks / max_rows_px (src_h * out_w) / max_out
-// (out_h * out_w * out_c): maxima over the frames (grid sizes). sync_passes: re-decode passes after the speculative
-// one (a frame still changing after them gets status bit 0 and is decoded again on the CPU).
+// (out_h * out_w * out_c): maxima over the frames (grid sizes). sync_passes: parallel re-decode passes after the
+// speculative one; what they leave unsettled the fix-up kernel finishes sequentially.
 AI4E_API int ai4e_jpeg_decode(const void* descs, int nframes, int max_threads, int max_blocks, long max_rows_px,
                               long max_out, int sync_passes, hipStream_t stream) {
   if (nframes <= 0 || nframes > 65535 || max_threads <= 0 || max_blocks <= 0 || sync_passes < 1 || sync_passes > 64)
@@ -482,6 +516,7 @@ AI4E_API int ai4e_jpeg_decode(const void* descs, int nframes, int max_threads, i
   const dim3 blk(kThreads);
   const dim3 gs((max_threads + kThreads - 1) / kThreads, nframes);
   for (int p = 0; p <= sync_passes; ++p) hipLaunchKernelGGL(huff_sync_kernel, gs, blk, 0, stream, d, p);
+  hipLaunchKernelGGL(huff_fixup_kernel, dim3(1, nframes), dim3(64), 0, stream, d, sync_passes);
   hipLaunchKernelGGL(huff_prefix_kernel, dim3(1, nframes), blk, 0, stream, d);
   hipLaunchKernelGGL(huff_write_kernel, gs, blk, 0, stream, d, sync_passes);
   hipLaunchKernelGGL(idct_kernel, dim3((max_blocks + kThreads - 1) / kThreads, nframes), blk, 0, stream, d);

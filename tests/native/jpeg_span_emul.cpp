@@ -2,7 +2,9 @@
 // per-thread span decoder (csrc/core/jpeg_span.h) run thread by thread, pass by pass. Used by tests/test_jpeg_gpu.py to
 // check the parallel decode (speculation, sync passes, prefix, write) against the sequential CPU decoder on any host.
 //
-//   jpeg_span_emul <prepared.bin> <span_bits> <coef_out.bin>   -> prints "passes P unsynced0 U bad B"
+//   jpeg_span_emul <prepared.bin> <span_bits> <coef_out.bin> [sync_passes]
+//     -> prints "passes P unsynced0 U ... fixup F": without sync_passes the passes run until nothing changes; with it,
+//        exactly that many run and the fix-up walk (huff_fixup_kernel) finishes the rest sequentially
 #define AI4E_HD
 #include <cstdio>
 #include <cstdlib>
@@ -27,12 +29,13 @@ int main(int argc, char** argv) {
   while ((n = std::fread(tmp, 1, sizeof(tmp), f)) > 0) buf.insert(buf.end(), tmp, tmp + n);
   std::fclose(f);
   const int S = std::atoi(argv[2]);
+  const int max_passes = argc > 4 ? std::atoi(argv[4]) : 1 << 30;
   const auto* H = reinterpret_cast<const JpegScanHeader*>(buf.data());
   if (H->magic != kJpegScanMagic) return 3;
-  std::vector<uint32_t> lut(8 << kGpuLook);
-  for (int t = 0; t < 4; ++t) {
+  std::vector<uint32_t> lut(4 << kGpuLook);
+  for (int t = 0; t < 2; ++t) {
     std::memcpy(&lut[t << kGpuLook], H->dc[t].fast, sizeof(H->dc[t].fast));
-    std::memcpy(&lut[(4 + t) << kGpuLook], H->ac[t].fast, sizeof(H->ac[t].fast));
+    std::memcpy(&lut[(2 + t) << kGpuLook], H->ac[t].fast, sizeof(H->ac[t].fast));
   }
   uint8_t nat[80], btab[16];
   for (int i = 0; i < 80; ++i) nat[i] = i < 64 ? kZz[i] : 63;
@@ -83,9 +86,26 @@ int main(int argc, char** argv) {
       for (int c = 0; c < 3; ++c) counts[4 * t + 1 + c] = r.dc[c];
     }
     if (pass == 1) unsynced0 = changed;
-    if (!changed || pass > 64) break;
+    if (!changed || pass >= max_passes) break;
   }
   const int last = pass & 1;
+  // fix-up walk (huff_fixup_kernel)
+  int fixed = 0;
+  {
+    bool dirty = false;
+    for (int t = 1; t < nt; ++t) {
+      if (!dirty && !chg[last][t - 1]) continue;
+      chg[last][t - 1] = 0;
+      const uint64_t s = ex[last][t - 1];
+      JSpanResult r;
+      jspan_decode<false>(T, jspan_pos(s), jspan_z(s), jspan_cp(s), end_of(t), r);
+      dirty = r.exit != ex[last][t];
+      ex[last][t] = r.exit;
+      counts[4 * t] = r.nblk;
+      for (int c = 0; c < 3; ++c) counts[4 * t + 1 + c] = r.dc[c];
+      ++fixed;
+    }
+  }
   // exclusive prefix
   int32_t acc[4] = {0, 0, 0, 0};
   for (int t = 0; t < nt; ++t)
@@ -107,7 +127,7 @@ int main(int argc, char** argv) {
   FILE* o = std::fopen(argv[3], "wb");
   std::fwrite(coef.data(), 2, coef.size(), o);
   std::fclose(o);
-  std::printf("passes %d unsynced0 %d threads %d bad %d blocks %d redecoded %ld (%.2f spans/thread)\n", pass, unsynced0,
-              nt, bad, acc[0], redecoded, static_cast<double>(redecoded) / nt);
+  std::printf("passes %d unsynced0 %d threads %d bad %d blocks %d redecoded %ld (%.2f spans/thread) fixup %d\n", pass,
+              unsynced0, nt, bad, acc[0], redecoded, static_cast<double>(redecoded) / nt, fixed);
   return 0;
 }
