@@ -20,6 +20,7 @@ import functools
 import math
 import struct
 import threading
+import time
 from concurrent.futures import ThreadPoolExecutor
 from dataclasses import dataclass
 from typing import List, Optional, Sequence, Tuple
@@ -29,8 +30,9 @@ import numpy as np
 SCAN_MAGIC = 0x3153434A  # "JCS1" (csrc/core/jpeg_layout.h)
 COEF_MAGIC = 0x314F434A  # "JCO1"
 PRECISION_BITS = 22      # PIL Resample.c (32 - 8 - 2)
-DEFAULT_SPAN_BITS = 4096  # bits per decoder thread: ~99 % of speculative spans synchronise inside their own span
-DEFAULT_SYNC_PASSES = 8  # 4096-bit spans settle in <= 4 passes on every frame tested (tests/test_jpeg_gpu.py)
+DEFAULT_SPAN_BITS = 2048  # bits per decoder thread: 85-95 % of speculative spans synchronise inside their own span; a pass
+# costs ~one span's decode latency, so shorter spans finish sooner (4096: 12.8k frames/s, 2048: 15.1k, 1024: 14.8k)
+DEFAULT_SYNC_PASSES = 8  # parallel passes; 2048-bit spans settle in 3-8 on the frames tested, the fix-up kernel finishes the rest
 ST_OK, ST_UNSUPPORTED, ST_CORRUPT, ST_NOROOM = 0, 1, 2, 3
 
 
@@ -583,10 +585,13 @@ class JpegGpuDecoder:
         self._staging: List = [None, None]  # pinned host staging, double-buffered across batches
         self._staging_evt: List = [None, None]
         self._scan: List = [None, None]
+        self._scan_done: List = [None, None]
+        self.copy_stream = torch.cuda.Stream(self.device)
         self._flip = 0
         self._lock = threading.Lock()
         self.errors = {}
         self.stats = dict(frames=0, gpu_frames=0, cpu_frames=0, unsupported=0, failed=0)
+        self.host_s = dict(staging_wait=0.0, prepare=0.0, plan=0.0, launch=0.0, finish=0.0)  # host seconds by step
 
     def _pinned(self, nbytes: int):
         torch = self.torch
@@ -614,7 +619,9 @@ class JpegGpuDecoder:
         # frame i's prepared bytes fit in header + its body + padding: back-to-back offsets known before preparing
         caps = [_align(self.hdr_bytes + len(b) + 128) for b in bodies]
         offs = np.concatenate([[0], np.cumsum(caps)]).astype(np.int64)
+        t0 = time.perf_counter()
         staging = self._pinned(int(offs[-1]))
+        t1 = time.perf_counter()
         base = staging.data_ptr()
         nt = min(self.threads, B)
 
@@ -623,6 +630,7 @@ class JpegGpuDecoder:
 
         parts = list(self.pool.map(chunk, range(nt)))
         results = [parts[i % nt][i // nt] for i in range(B)]
+        t2 = time.perf_counter()
         host = staging.numpy()
         frames, gpu, cpu = [], [], []
         for i, (st, used) in enumerate(results):
@@ -635,31 +643,57 @@ class JpegGpuDecoder:
                     continue
             cpu.append(i)
         pending = Pending(bodies, out, gpu, cpu)
+        t3 = time.perf_counter()
         if gpu:
             k = self._flip
             stream = torch.cuda.current_stream(self.device)
             total = int(offs[gpu[-1] + 1])
-            with torch.cuda.stream(stream):
+            # the batch's bytes go up on a copy stream, under the previous batch's kernels; scan area k is rewritten
+            # only once the decode that read it (two batches ago) is done
+            cs = self.copy_stream
+            with torch.cuda.stream(cs):
+                if self._scan_done[k] is not None:
+                    cs.wait_event(self._scan_done[k])
                 self._scan[k] = self.launcher._buf(self._scan[k], total)
                 self._scan[k][:total].copy_(staging[:total], non_blocking=True)  # the whole batch in one copy
             evt = torch.cuda.Event()
-            evt.record(stream)
+            evt.record(cs)
             self._staging_evt[k] = evt
+            stream.wait_event(evt)
+            self._scan[k].record_stream(stream)
             sbase = self._scan[k].data_ptr()
             frames = [(h, p, sbase + o, dst) for h, p, o, dst in frames]
-            pending.status, keep = self.launcher.launch(frames, stream)
-            pending.keep = (keep, self._scan[k])
+            status, keep = self.launcher.launch(frames, stream)
+            # statuses into pinned memory behind the decode: finish() waits for this batch only, not for batches
+            # submitted after it (a .cpu() on the stream would)
+            host = torch.empty(status.numel(), dtype=torch.int32, pin_memory=True)
+            with torch.cuda.stream(stream):
+                host.copy_(status, non_blocking=True)
+            done = torch.cuda.Event()
+            done.record(stream)
+            self._scan_done[k] = done
+            pending.status = (host, done)
+            pending.keep = (keep, self._scan[k], status)
         self._flip ^= 1
+        t4 = time.perf_counter()
         with self._lock:
             self.stats["frames"] += B
             self.stats["unsupported"] += len(cpu)
+            h = self.host_s
+            h["staging_wait"] += t1 - t0
+            h["prepare"] += t2 - t1
+            h["plan"] += t3 - t2
+            h["launch"] += t4 - t3
         return pending
 
     def finish(self, p: Pending):
         torch = self.torch
+        t0 = time.perf_counter()
         cpu = list(p.cpu)
         if p.status is not None:
-            st = p.status.cpu().numpy()
+            host, done = p.status
+            done.synchronize()
+            st = host.numpy()
             bad = [p.gpu[j] for j in np.nonzero(st)[0]]
             with self._lock:
                 self.stats["failed"] += len(bad)
@@ -682,6 +716,7 @@ class JpegGpuDecoder:
                     p.out[i].copy_(torch.from_numpy(np.require(a, requirements="W")))
             with self._lock:
                 self.stats["cpu_frames"] += len(cpu)
+        self.host_s["finish"] += time.perf_counter() - t0
         return p.out
 
     def close(self):

@@ -60,13 +60,13 @@ def rate(fn, body, shape, threads, seconds):
     return sum(counts) / (time.perf_counter() - t0)
 
 
-def gpu_rate(bodies, shape, threads, batch, seconds):
+def gpu_rate(bodies, shape, threads, batch, seconds, span_bits=0):
     """Frames/s of the on-GPU path over `seconds`, and the max |GPU - decode_image| over the distinct bodies."""
     import torch
 
-    from aiforearth_api_platform_amd.runtime.jpeg_gpu import JpegGpuDecoder
+    from aiforearth_api_platform_amd.runtime.jpeg_gpu import DEFAULT_SPAN_BITS, JpegGpuDecoder
 
-    dec = JpegGpuDecoder(shape, "cuda", threads=threads)
+    dec = JpegGpuDecoder(shape, "cuda", threads=threads, span_bits=span_bits or DEFAULT_SPAN_BITS)
     frames = [bodies[i % len(bodies)] for i in range(batch)]
     out = dec.decode(frames)  # warm-up (allocations, coefficient tables)
     torch.cuda.synchronize()
@@ -90,9 +90,11 @@ def gpu_rate(bodies, shape, threads, batch, seconds):
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     stats = dict(dec.stats)
+    host = {name: round(v / (k + 1) * 1e3, 3) for name, v in dec.host_s.items()}  # ms per batch (k timed + warm-up)
     dec.close()
     return {"frames_per_s": round(n / dt, 1), "batch": batch, "cpu_threads": threads, "max_abs_diff_vs_decode_image":
-            diff, "gpu_frames": stats["gpu_frames"], "cpu_fallback_frames": stats["cpu_frames"]}
+            diff, "gpu_frames": stats["gpu_frames"], "cpu_fallback_frames": stats["cpu_frames"],
+            "span_bits": dec.launcher.span_bits, "host_ms_per_batch": host}
 
 
 def main():
@@ -103,6 +105,7 @@ def main():
     ap.add_argument("--json-out", default="")
     ap.add_argument("--gpu", action="store_true", help="only the on-GPU reconstruction (one GPU)")
     ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--span-bits", type=int, default=0, help="entropy-coded bits per decoder thread (0: default)")
     a = ap.parse_args()
     h, w = (int(v) for v in a.frame.split("x"))
     body = frame_jpeg(h, w)
@@ -111,7 +114,8 @@ def main():
         out = {"metric": "JPEG frames decoded + resized per second (on-GPU reconstruction, 1 GPU)", "frame": [h, w],
                "jpeg_bytes": [len(b) for b in bodies], "threads": a.threads, "results": {}}
         for shape in ((640, 640, 3), (224, 224, 3)):
-            out["results"][f"{shape[0]}x{shape[1]}"] = gpu_rate(bodies, shape, a.threads, a.batch, a.seconds)
+            out["results"][f"{shape[0]}x{shape[1]}"] = gpu_rate(bodies, shape, a.threads, a.batch, a.seconds,
+                                                                 a.span_bits)
         line = json.dumps(out)
         print(line)
         if a.json_out:

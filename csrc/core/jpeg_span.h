@@ -79,13 +79,16 @@ AI4E_HD inline void jspan_decode(const JSpanTables& T, uint32_t pos, int z, int 
   buf |= word(wi) << (32 - nb);
   nb += 32;
   ++wi;
+  // the next word is loaded one refill ahead: its (global-memory) latency overlaps the ~5 symbols decoded from the
+  // current window instead of stalling the refill
+  uint64_t nxt = word(wi);
   int bt = T.blk_tab[cp];
   int32_t q = q0;
   while (pos < end) {
     if (nb < 32) {
-      buf |= word(wi) << (32 - nb);
+      buf |= nxt << (32 - nb);
       nb += 32;
-      ++wi;
+      nxt = word(++wi);
     }
     const int dct = bt & 1, act = 2 + ((bt >> 2) & 1), comp = (bt >> 4) & 3;
     const int tab = z == 0 ? dct : act;
@@ -129,10 +132,10 @@ AI4E_HD inline void jspan_decode(const JSpanTables& T, uint32_t pos, int z, int 
     pos += static_cast<uint32_t>(n);
     if (kind == 1) {
       if (sz) {
-        if (nb < sz) {
-          buf |= word(wi) << (32 - nb);
+        if (nb < sz) {  // (never: >= 16 bits remain after a code of <= 16)
+          buf |= nxt << (32 - nb);
           nb += 32;
-          ++wi;
+          nxt = word(++wi);
         }
         const int v = static_cast<int>(buf >> (64 - sz));
         val = v < (1 << (sz - 1)) ? v - (1 << sz) + 1 : v;

@@ -147,8 +147,10 @@ def test_native_frontend_admission_parity(tmp_path, nfe):
     cfgp = tmp_path / "platform.yaml"
     cfgp.write_text(yaml.safe_dump(doc))
     port = _port()
+    # (no latency budget: the statuses under test are keys / types / sizes, not load refusals, which a busy host
+    # could otherwise add to any request)
     env = dict(os.environ, PYTHONPATH=ROOT, AI4E_FRONTEND_PROCESSES=str(nfe), AI4E_FRONTEND_IMPL="native",
-               AI4E_SUBSCRIPTION_KEYS="gk")
+               AI4E_SUBSCRIPTION_KEYS="gk", AI4E_MAX_QUEUE_MS="0")
     proc = subprocess.Popen([sys.executable, "-m", "aiforearth_api_platform_amd.serve", "--config", str(cfgp),
                              "--port", str(port)], cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
     base = f"http://127.0.0.1:{port}"

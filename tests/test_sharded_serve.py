@@ -61,7 +61,7 @@ def test_sharded_serve_four_workers_every_task_resolvable():
     with tempfile.NamedTemporaryFile("w", suffix=".yaml", delete=False) as f:
         f.write(YAML)
         cfg = f.name
-    env = dict(os.environ, PYTHONPATH=ROOT)
+    env = dict(os.environ, PYTHONPATH=ROOT, AI4E_MAX_QUEUE_MS="0")  # (resolvability, not load refusals, is tested)
     proc = subprocess.Popen([sys.executable, "-m", "aiforearth_api_platform_amd.serve", "--config", cfg, "--port",
                              str(port)], cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
     base = f"http://127.0.0.1:{port}"
