@@ -393,14 +393,14 @@ def slot_frames(ring_u8: np.ndarray, slots: Sequence[int], key: int) -> List[Tup
 
 
 # ----------------------------------------------------------------------------------------------------- GPU decoder
-_DESC_FIELDS = ([("scan", "u8"), ("coef", "u8"), ("exit0", "u8"), ("exit1", "u8"), ("chg0", "u8"), ("chg1", "u8"),
+_DESC_FIELDS = ([("scan", "u8"), ("coef", "u8"), ("blen", "u8"), ("exit0", "u8"), ("exit1", "u8"), ("chg0", "u8"), ("chg1", "u8"),
                  ("counts", "u8"), ("planes", "u8"), ("rows", "u8"), ("out", "u8"), ("hk", "u8"), ("hb", "u8"),
                  ("vk", "u8"), ("vb", "u8"), ("status", "u8"), ("nthreads", "i4"), ("span_bits", "i4"), ("hks", "i4"),
                  ("vks", "i4")] + [(f"ssize{i}", "i4") for i in range(3)] + [(f"plane_off{i}", "i4") for i in range(3)]
                 + [(f"plane_pitch{i}", "i4") for i in range(3)]
                 + [(k, "i4") for k in ("src_w", "src_h", "out_w", "out_h", "out_c", "kbase1", "kbase2")])
 DESC_DTYPE = np.dtype(_DESC_FIELDS)
-assert DESC_DTYPE.itemsize == 200  # sizeof(JpegFrameDesc)
+assert DESC_DTYPE.itemsize == 208  # sizeof(JpegFrameDesc)
 
 
 def _align(n: int, a: int = 256) -> int:
@@ -455,6 +455,7 @@ class JpegLauncher:
         self.sync_passes = int(sync_passes)
         self._work = None
         self._coef = None
+        self._blen = None
         self._coeff_cache = {}
         self._templates = {}
 
@@ -527,6 +528,7 @@ class JpegLauncher:
             cb = np.concatenate([[0], np.cumsum(cbytes)[:-1]])
             self._work = self._buf(self._work, int(per.sum()))
             self._coef = self._buf(self._coef, int(cbytes.sum()), zero=True)
+            self._blen = self._buf(self._blen, int(nblk.sum()) + 2, zero=True)  # (int16 storage, byte offsets)
             status = torch.zeros(n, dtype=torch.int32, device=self.device)
             w = self._work.data_ptr() + fbase
             descs["exit0"], descs["exit1"] = w, w + e8
@@ -535,12 +537,14 @@ class JpegLauncher:
             descs["planes"] = w + 2 * e8 + 2 * c4 + c16
             descs["rows"] = w + 2 * e8 + 2 * c4 + c16 + pl
             descs["coef"] = self._coef.data_ptr() + cb
+            descs["blen"] = self._blen.data_ptr() + np.concatenate([[0], np.cumsum(nblk)[:-1]])
             descs["scan"] = np.array([f[2] for f in frames], np.uint64)
             descs["out"] = np.array([f[3] for f in frames], np.uint64)
             descs["status"] = status.data_ptr() + 4 * np.arange(n, dtype=np.uint64)
             descs["nthreads"] = nthr
             max_rows = int(max(t[0]["src_h"] for t in tmpl)) * int(max(t[0]["out_w"] for t in tmpl))
             max_out = int(max(t[0]["out_h"] * t[0]["out_w"] for t in tmpl)) * 3
+            self.last_descs = descs  # (debugging: device addresses of the last batch's work areas)
             ddesc = torch.from_numpy(descs.view(np.uint8)).pin_memory().to(self.device, non_blocking=True)
             self._ext.call("ai4e_jpeg_decode", ddesc.data_ptr(), n, int(nthr.max()), int(nblk.max()), max_rows, max_out,
                            self.sync_passes, stream.cuda_stream)

@@ -329,7 +329,14 @@ PYBIND11_MODULE(_ai4e_core, m) {
         std::memset(coef, 0, static_cast<size_t>(H->nblocks) * 128);
         const int32_t pred[3] = {0, 0, 0};
         JSpanResult r;
-        jspan_decode<true>(T, 0, 0, 0, H->total_bits, r, coef, 0, pred, static_cast<int32_t>(H->nblocks));
+        std::vector<uint8_t> blen(H->nblocks);
+        jspan_decode<true>(T, 0, 0, 0, H->total_bits, r, coef, 0, pred, static_cast<int32_t>(H->nblocks), blen.data());
+        int16_t blk[64];  // zigzag -> natural order, in place per block
+        for (uint32_t q = 0; q < H->nblocks; ++q) {
+          int16_t* b = coef + static_cast<size_t>(q) * 64;
+          for (int k = 0; k < 64; ++k) blk[zz[k]] = b[k];
+          std::memcpy(b, blk, sizeof(blk));
+        }
         return (r.bad || r.nblk < static_cast<int32_t>(H->nblocks)) ? 2 : 0;
       },
       py::arg("src"), py::arg("size"), py::arg("out"));

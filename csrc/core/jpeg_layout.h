@@ -58,7 +58,8 @@ static constexpr uint64_t kRingTailMagic = 0x474e495245344941ull;  // "AI4ERING"
 // One frame of a decode batch (built by runtime/jpeg_gpu.py; device addresses).
 struct JpegFrameDesc {
   uint64_t scan;          // JpegScanHeader + unstuffed scan (16-byte aligned)
-  uint64_t coef;          // int16 [nblocks][64], MCU order; all zero between batches (the IDCT clears what it reads)
+  uint64_t coef;          // int16 [nblocks][64], MCU order, zigzag order; zero between batches (the IDCT clears it)
+  uint64_t blen;          // uint8 [nblocks]: coefficients written per block (zigzag prefix; 0 between batches)
   uint64_t exit[2];       // uint64 [nthreads] span exit states (ping-pong over the sync passes)
   uint64_t chg[2];        // uint32 [nthreads] exit state changed in that pass
   uint64_t counts;        // int32 [nthreads][4]: blocks completed, DC sums -> exclusive prefixes

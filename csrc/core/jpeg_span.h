@@ -11,8 +11,8 @@
 //           starts at the true state);
 //   prefix: exclusive sums over threads of (blocks completed, DC differences per component) give each thread its
 //           first block index and DC predictors;
-//   write:  every thread decodes its span once more from its (now exact) entry state and stores dequantisation-ready
-//           coefficients (natural order, DC undifferenced) into the dense [block][64] array.
+//   write:  every thread decodes its span once more from its (now exact) entry state and stores the coefficients
+//           (zigzag order, DC undifferenced) into the dense [block][64] array, with each block's written length.
 // Host and device share this code: the CPU build (tests/native/jpeg_span_emul.cpp) runs the same passes sequentially
 // against the CPU decoder's output. Needs AI4E_HD (__host__ __device__ for hipcc, empty for g++) defined by the
 // includer.
@@ -50,12 +50,14 @@ struct JSpanResult {
   int32_t bad;    // invalid codes met (0 for a valid stream decoded from a true state)
 };
 
-// kWrite: store coefficients (coef: int16 [total][64], natural order; q0 = index of the block the span starts in,
-// pred = DC predictors at the span's start); stops after the last block.
+// kWrite: store coefficients (coef: int16 [total][64] in ZIGZAG order, natural positions being the IDCT's business;
+// q0 = index of the block the span starts in, pred = DC predictors at the span's start) and, for every block the span
+// finishes, blen[q] = length of the written zigzag prefix (the span that started the block may have written its first
+// coefficients: the entry state's z bounds them); stops after the last block.
 template <bool kWrite>
 AI4E_HD inline void jspan_decode(const JSpanTables& T, uint32_t pos, int z, int cp, uint32_t end, JSpanResult& r,
                                  int16_t* coef = nullptr, int32_t q0 = 0, const int32_t* pred_in = nullptr,
-                                 int32_t total = 0) {
+                                 int32_t total = 0, uint8_t* blen = nullptr) {
   r.exit = jspan_pack(pos, z, cp);
   if (kWrite && q0 >= total) {  // a span past the last block (the scan's padding)
     r.nblk = 0;
@@ -84,6 +86,7 @@ AI4E_HD inline void jspan_decode(const JSpanTables& T, uint32_t pos, int z, int 
   uint64_t nxt = word(wi);
   int bt = T.blk_tab[cp];
   int32_t q = q0;
+  int lz = z > 0 ? z - 1 : 0;  // highest zigzag index written in the current block (bound for the part before us)
   while (pos < end) {
     if (nb < 32) {
       buf |= nxt << (32 - nb);
@@ -153,6 +156,7 @@ AI4E_HD inline void jspan_decode(const JSpanTables& T, uint32_t pos, int z, int 
       if (kWrite) {
         const int p = comp == 0 ? pred0 + dc0 : (comp == 1 ? pred1 + dc1 : pred2 + dc2);
         coef[static_cast<int64_t>(q) * 64] = static_cast<int16_t>(p);
+        lz = 0;
       }
       z = 1;
     } else if (kind == 2) {
@@ -161,10 +165,14 @@ AI4E_HD inline void jspan_decode(const JSpanTables& T, uint32_t pos, int z, int 
       z += 16;
     } else {
       z += run;
-      if (kWrite) coef[static_cast<int64_t>(q) * 64 + T.natural[z > 79 ? 79 : z]] = static_cast<int16_t>(val);
+      if (kWrite) {  // zigzag positions past 63 land on 63, as libjpeg's jpeg_natural_order[64..79]
+        lz = z > 63 ? 63 : z;
+        coef[static_cast<int64_t>(q) * 64 + lz] = static_cast<int16_t>(val);
+      }
       z += 1;
     }
     if (z >= 64) {
+      if (kWrite) blen[q] = static_cast<uint8_t>(lz + 1);
       z = 0;
       ++r.nblk;
       ++q;

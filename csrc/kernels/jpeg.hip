@@ -33,6 +33,11 @@ __device__ const uint8_t kNatural[80] = {
 
 constexpr int kThreads = 256;
 
+// zigzag -> natural, as a compile-time table (the IDCT's unrolled de-zigzag keeps every index constant)
+constexpr uint8_t kNat64[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,  12, 19, 26, 33, 40, 48,
+                                41, 34, 27, 20, 13, 6,  7,  14, 21, 28, 35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23,
+                                30, 37, 44, 51, 58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
+
 struct SpanLds {
   uint32_t lut[4 << kGpuLook];  // 16 KB: the frame's 2 DC + 2 AC lookahead tables
   uint8_t natural[80];
@@ -214,7 +219,8 @@ __global__ __launch_bounds__(kThreads) void huff_write_kernel(const JpegFrameDes
   const int32_t pred[3] = {base.y, base.z, base.w};
   JSpanResult r;
   ai4e::jspan_decode<true>(T, ai4e::jspan_pos(s), ai4e::jspan_z(s), ai4e::jspan_cp(s), span_end(D, t), r,
-                           reinterpret_cast<int16_t*>(D.coef), base.x, pred, static_cast<int32_t>(H->nblocks));
+                           reinterpret_cast<int16_t*>(D.coef), base.x, pred, static_cast<int32_t>(H->nblocks),
+                           reinterpret_cast<uint8_t*>(D.blen));
   if (r.bad) atomicOr(status, 2u);
 }
 
@@ -402,20 +408,31 @@ __global__ __launch_bounds__(kThreads) void idct_kernel(const JpegFrameDesc* __r
   const int kb = c == 0 ? 0 : (c == 1 ? D.kbase1 : D.kbase2);
   const int k = kb + (row % v) * h + (col % h);
   const int64_t q = static_cast<int64_t>(m) * static_cast<int64_t>(H->bpm) + k;
+  // the block's zigzag prefix only (a frame flagged corrupt: all 64, whatever its spans wrote); cleared behind us
   uint4* src = reinterpret_cast<uint4*>(reinterpret_cast<int16_t*>(D.coef) + q * 64);
+  uint8_t* bl = reinterpret_cast<uint8_t*>(D.blen) + q;
+  const int len = *reinterpret_cast<const uint32_t*>(D.status) ? 64 : *bl;
+  const int nchunk = (len + 7) >> 3;
+  *bl = 0;
   const uint16_t* qt = H->quant[C[5]];
-  int d[64];
+  int zz[64];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    const uint4 w = src[j];
+    uint4 w = make_uint4(0, 0, 0, 0);
+    if (j < nchunk) {
+      w = src[j];
+      src[j] = make_uint4(0, 0, 0, 0);
+    }
     const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
     for (int h2 = 0; h2 < 4; ++h2) {
-      d[8 * j + 2 * h2] = static_cast<int16_t>(ww[h2] & 0xFFFF) * static_cast<int>(qt[8 * j + 2 * h2]);
-      d[8 * j + 2 * h2 + 1] = static_cast<int16_t>(ww[h2] >> 16) * static_cast<int>(qt[8 * j + 2 * h2 + 1]);
+      zz[8 * j + 2 * h2] = static_cast<int16_t>(ww[h2] & 0xFFFF);
+      zz[8 * j + 2 * h2 + 1] = static_cast<int16_t>(ww[h2] >> 16);
     }
-    src[j] = make_uint4(0, 0, 0, 0);
   }
+  int d[64];
+#pragma unroll
+  for (int k = 0; k < 64; ++k) d[kNat64[k]] = zz[k] * static_cast<int>(qt[kNat64[k]]);
   const int ss = D.ssize[c];
   uint8_t* out = reinterpret_cast<uint8_t*>(D.planes) + D.plane_off[c] + static_cast<int64_t>(row) * ss * D.plane_pitch[c] +
                  col * ss;
@@ -487,20 +504,43 @@ __global__ __launch_bounds__(kThreads) void color_h_kernel(const JpegFrameDesc* 
   o[2] = clip22(a2);
 }
 
+// PIL's vertical pass: 4 output bytes per thread (one 32-bit load per tap per lane, the bytes being independent
+// channels / pixels with the same row weights) when a row is a multiple of 4 bytes, else one byte per thread.
 __global__ __launch_bounds__(kThreads) void resize_v_kernel(const JpegFrameDesc* __restrict__ descs) {
   const JpegFrameDesc& D = descs[blockIdx.y];
   const int64_t idx = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x;
   const int64_t per_row = static_cast<int64_t>(D.out_w) * D.out_c;
-  if (idx >= static_cast<int64_t>(D.out_h) * per_row) return;
-  const int yo = static_cast<int>(idx / per_row);
-  const int64_t xc = idx - yo * per_row;
+  const bool quad = (per_row & 3) == 0;
+  const int64_t units = quad ? per_row >> 2 : per_row;
+  if (idx >= static_cast<int64_t>(D.out_h) * units) return;
+  const int yo = static_cast<int>(idx / units);
+  const int64_t xu = idx - yo * units;
   const int* vb = reinterpret_cast<const int*>(D.vb) + 2 * yo;
   const int* vk = reinterpret_cast<const int*>(D.vk) + yo * D.vks;
-  const uint8_t* rows = reinterpret_cast<const uint8_t*>(D.rows) + xc;
-  int acc = 1 << 21;
   const int y0 = vb[0], n = vb[1];
+  if (quad) {
+    const uint32_t* rows = reinterpret_cast<const uint32_t*>(D.rows) + xu;
+    const int64_t pitch = per_row >> 2;
+    int a0 = 1 << 21, a1 = 1 << 21, a2 = 1 << 21, a3 = 1 << 21;
+    for (int j = 0; j < n; ++j) {
+      const uint32_t v = rows[static_cast<int64_t>(y0 + j) * pitch];
+      const int k = vk[j];
+      a0 += k * static_cast<int>(v & 0xFF);
+      a1 += k * static_cast<int>((v >> 8) & 0xFF);
+      a2 += k * static_cast<int>((v >> 16) & 0xFF);
+      a3 += k * static_cast<int>(v >> 24);
+    }
+    // (the empty asm keeps the clamp + pack from being matched to v_ashr_pk_u8_i32: measured, that packing left
+    // the upper half of the word holding stale register bits, i.e. bytes 2-3 of every output word garbage)
+    uint32_t b0 = clip22(a0), b1 = clip22(a1), b2 = clip22(a2), b3 = clip22(a3);
+    asm volatile("" : "+v"(b0), "+v"(b1), "+v"(b2), "+v"(b3));
+    reinterpret_cast<uint32_t*>(D.out)[static_cast<int64_t>(yo) * pitch + xu] = b0 | (b1 << 8) | (b2 << 16) | (b3 << 24);
+    return;
+  }
+  const uint8_t* rows = reinterpret_cast<const uint8_t*>(D.rows) + xu;
+  int acc = 1 << 21;
   for (int j = 0; j < n; ++j) acc += vk[j] * static_cast<int>(rows[static_cast<int64_t>(y0 + j) * per_row]);
-  reinterpret_cast<uint8_t*>(D.out)[idx] = clip22(acc);
+  reinterpret_cast<uint8_t*>(D.out)[static_cast<int64_t>(yo) * per_row + xu] = clip22(acc);
 }
 
 }  // namespace

@@ -116,14 +116,26 @@ int main(int argc, char** argv) {
     }
   const int32_t total = static_cast<int32_t>(H->nblocks);
   std::vector<int16_t> coef(static_cast<size_t>(total) * 64, 0);
+  std::vector<uint8_t> blen(static_cast<size_t>(total), 0);
   int bad = 0;
   for (int t = 0; t < nt; ++t) {
     const uint64_t s = t ? ex[last][t - 1] : jspan_pack(0, 0, 0);
     JSpanResult r;
     jspan_decode<true>(T, jspan_pos(s), jspan_z(s), jspan_cp(s), end_of(t), r, coef.data(), counts[4 * t],
-                       &counts[4 * t + 1], total);
+                       &counts[4 * t + 1], total, blen.data());
     bad += r.bad;
   }
+  // zigzag -> natural (the kernels' IDCT does this on load); every coefficient must lie inside its block's length
+  std::vector<int16_t> natural(coef.size(), 0);
+  int beyond = 0;
+  for (int32_t q = 0; q < total; ++q)
+    for (int k = 0; k < 64; ++k) {
+      const int16_t v = coef[static_cast<size_t>(q) * 64 + k];
+      natural[static_cast<size_t>(q) * 64 + kZz[k]] = v;
+      if (v && k >= blen[q]) ++beyond;
+    }
+  coef.swap(natural);
+  bad += beyond;
   FILE* o = std::fopen(argv[3], "wb");
   std::fwrite(coef.data(), 2, coef.size(), o);
   std::fclose(o);
