@@ -22,6 +22,14 @@
 
 #include "jpeg_layout.h"
 
+// Address space of the decoder's global-memory operands: the kernels define it as the global space, so the scan words,
+// slow-path tables and coefficient stores compile to global_* instructions, which count only in vmcnt. As flat_*
+// operations they also count in lgkmcnt, and every LDS table lookup's lgkmcnt(0) wait then waited for the prefetched
+// scan word too (the prefetch hid nothing). Host builds: the default address space.
+#ifndef AI4E_GAS
+#define AI4E_GAS
+#endif
+
 namespace ai4e {
 
 // exit state: bit position (32) | z (8) | block in MCU (8) | valid (bit 63)
@@ -35,10 +43,10 @@ AI4E_HD inline int jspan_cp(uint64_t s) { return static_cast<int>((s >> 40) & 0x
 
 struct JSpanTables {
   const uint32_t* lut;     // [4][1 << kGpuLook]: DC tables 0-1, AC tables 0-1 (LDS on the GPU)
-  const GpuHuff* huff;     // dc[2], ac[2] of the JpegScanHeader (slow path: codes longer than kGpuLook)
+  const AI4E_GAS GpuHuff* huff;  // dc[2], ac[2] of the JpegScanHeader (slow path: codes longer than kGpuLook)
   const uint8_t* blk_tab;  // per MCU block: dc table | ac table << 2 | component << 4
   const uint8_t* natural;  // zigzag -> natural order, 80 entries (64..79 -> 63, as libjpeg's jpeg_natural_order)
-  const uint32_t* words;   // the unstuffed scan as 32-bit words (big-endian bytes), padded with 0xFF
+  const AI4E_GAS uint32_t* words;  // the unstuffed scan as 32-bit words (big-endian bytes), padded with 0xFF
   uint32_t nwords;
   int bpm;
 };
@@ -56,8 +64,8 @@ struct JSpanResult {
 // coefficients: the entry state's z bounds them); stops after the last block.
 template <bool kWrite>
 AI4E_HD inline void jspan_decode(const JSpanTables& T, uint32_t pos, int z, int cp, uint32_t end, JSpanResult& r,
-                                 int16_t* coef = nullptr, int32_t q0 = 0, const int32_t* pred_in = nullptr,
-                                 int32_t total = 0, uint8_t* blen = nullptr) {
+                                 AI4E_GAS int16_t* coef = nullptr, int32_t q0 = 0, const int32_t* pred_in = nullptr,
+                                 int32_t total = 0, AI4E_GAS uint8_t* blen = nullptr) {
   r.exit = jspan_pack(pos, z, cp);
   if (kWrite && q0 >= total) {  // a span past the last block (the scan's padding)
     r.nblk = 0;
@@ -71,27 +79,27 @@ AI4E_HD inline void jspan_decode(const JSpanTables& T, uint32_t pos, int z, int 
   r.bad = 0;
   // 64-bit window, MSB = the bit at `pos`; nb valid bits
   uint32_t wi = pos >> 5;
-  auto word = [&](uint32_t i) -> uint64_t {
-    const uint32_t w = i < T.nwords ? T.words[i] : 0xFFFFFFFFu;
-    return static_cast<uint64_t>(__builtin_bswap32(w));
-  };
+  // raw (big-endian) scan word; the index is clamped, not the loaded value, so nothing consumes a load before its
+  // bits are needed (reads stay inside the 64-byte 0xFF pad: a span never decodes more than a code past its end)
+  auto raw = [&](uint32_t i) -> uint32_t { return T.words[i < T.nwords ? i : T.nwords - 1]; };
+  auto word = [&](uint32_t i) -> uint64_t { return static_cast<uint64_t>(__builtin_bswap32(raw(i))); };
   uint64_t buf = (word(wi) << 32) << (pos & 31);
   int nb = 32 - static_cast<int>(pos & 31);
   ++wi;
   buf |= word(wi) << (32 - nb);
   nb += 32;
   ++wi;
-  // the next word is loaded one refill ahead: its (global-memory) latency overlaps the ~5 symbols decoded from the
-  // current window instead of stalling the refill
-  uint64_t nxt = word(wi);
+  // the next word is loaded one refill ahead and byte-swapped only when used: its global-memory latency overlaps the
+  // ~5 symbols decoded from the current window instead of stalling the refill
+  uint32_t nxt = raw(wi);
   int bt = T.blk_tab[cp];
   int32_t q = q0;
   int lz = z > 0 ? z - 1 : 0;  // highest zigzag index written in the current block (bound for the part before us)
   while (pos < end) {
     if (nb < 32) {
-      buf |= nxt << (32 - nb);
+      buf |= static_cast<uint64_t>(__builtin_bswap32(nxt)) << (32 - nb);
       nb += 32;
-      nxt = word(++wi);
+      nxt = raw(++wi);
     }
     const int dct = bt & 1, act = 2 + ((bt >> 2) & 1), comp = (bt >> 4) & 3;
     const int tab = z == 0 ? dct : act;
@@ -102,7 +110,7 @@ AI4E_HD inline void jspan_decode(const JSpanTables& T, uint32_t pos, int z, int 
     int val = static_cast<int16_t>(e & 0xFFFF);
     int sz = kind == 1 ? val : 0;
     if (kind == 4 || n == 0) {  // code longer than the lookahead
-      const GpuHuff& h = T.huff[tab];
+      const AI4E_GAS GpuHuff& h = T.huff[tab];
       int len = kGpuLook + 1;
       int code = static_cast<int>(buf >> (64 - len));
       while (len <= 16 && code > h.maxcode[len]) {
@@ -136,9 +144,9 @@ AI4E_HD inline void jspan_decode(const JSpanTables& T, uint32_t pos, int z, int 
     if (kind == 1) {
       if (sz) {
         if (nb < sz) {  // (never: >= 16 bits remain after a code of <= 16)
-          buf |= nxt << (32 - nb);
+          buf |= static_cast<uint64_t>(__builtin_bswap32(nxt)) << (32 - nb);
           nb += 32;
-          nxt = word(++wi);
+          nxt = raw(++wi);
         }
         const int v = static_cast<int>(buf >> (64 - sz));
         val = v < (1 << (sz - 1)) ? v - (1 << sz) + 1 : v;

@@ -14,6 +14,7 @@
 // coefficients (runtime/decode.py decode_image; runtime/jpeg_gpu.py builds the coefficient tables on the host).
 // Frames are independent: blockIdx.y is the frame of the batch (JpegFrameDesc).
 #define AI4E_HD __host__ __device__
+#define AI4E_GAS __attribute__((address_space(1)))
 #include "common.h"
 #include "../core/jpeg_span.h"
 
@@ -64,10 +65,10 @@ __device__ __forceinline__ JSpanTables stage_tables(const JpegFrameDesc& D, Span
   __syncthreads();
   JSpanTables T;
   T.lut = L.lut;
-  T.huff = H->dc;
+  T.huff = (const AI4E_GAS GpuHuff*)(H->dc);  // (generic -> global: a C-style address-space cast)
   T.blk_tab = L.btab;
   T.natural = L.natural;
-  T.words = reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(H) + sizeof(JpegScanHeader));
+  T.words = (const AI4E_GAS uint32_t*)(reinterpret_cast<const uint8_t*>(H) + sizeof(JpegScanHeader));
   T.nwords = static_cast<uint32_t>((H->scan_bytes + ai4e::kJpegScanPad) / 4);
   T.bpm = static_cast<int>(H->bpm);
   return T;
@@ -219,8 +220,8 @@ __global__ __launch_bounds__(kThreads) void huff_write_kernel(const JpegFrameDes
   const int32_t pred[3] = {base.y, base.z, base.w};
   JSpanResult r;
   ai4e::jspan_decode<true>(T, ai4e::jspan_pos(s), ai4e::jspan_z(s), ai4e::jspan_cp(s), span_end(D, t), r,
-                           reinterpret_cast<int16_t*>(D.coef), base.x, pred, static_cast<int32_t>(H->nblocks),
-                           reinterpret_cast<uint8_t*>(D.blen));
+                           reinterpret_cast<AI4E_GAS int16_t*>(D.coef), base.x, pred, static_cast<int32_t>(H->nblocks),
+                           reinterpret_cast<AI4E_GAS uint8_t*>(D.blen));
   if (r.bad) atomicOr(status, 2u);
 }
 
