@@ -244,3 +244,49 @@ def test_gpu_decode_corrupt_frame_reports_and_recovers():
         np.testing.assert_array_equal(out[2].cpu().numpy(), ref)
     finally:
         dec.close()
+
+
+def test_span_decoder_memory_safe_on_mutated_frames(tmp_path):
+    """The kernels' span decoder (compiled for the host with AddressSanitizer + UBSan, tests/native/jpeg_span_emul.cpp)
+    over mutated frames: flipped scan bytes, truncations, a garbage scan. Every run must end (bounded passes) without
+    a memory error, whatever the decode makes of the bits. The same per-thread code runs in the GPU kernels, whose reads
+    are bounded by the same clamps."""
+    from aiforearth_api_platform_amd import _ai4e_core as core
+
+    gxx = shutil.which("g++")
+    if gxx is None:
+        pytest.skip("g++ not available")
+    exe = str(tmp_path / "emul_asan")
+    r = subprocess.run([gxx, "-O1", "-g", "-std=c++17", "-fsanitize=address,undefined", "-fno-sanitize-recover=all",
+                        "-o", exe, os.path.join(ROOT, "tests", "native", "jpeg_span_emul.cpp")], capture_output=True)
+    if r.returncode != 0:
+        pytest.skip("sanitizer build unavailable: " + r.stderr.decode()[-200:])
+    rng = np.random.default_rng(0)
+    base = frame(240, 320, q=85, smooth=2)
+    prep = np.zeros(4 << 20, np.uint8)
+    runs = 0
+    for trial in range(24):
+        b = bytearray(base)
+        kind = trial % 4
+        if kind == 0:  # flip bytes inside the entropy-coded data
+            for _ in range(1 + trial):
+                i = int(rng.integers(len(b) // 3, len(b) - 2))
+                b[i] = int(rng.integers(0, 256))
+        elif kind == 1:  # truncate
+            b = b[:int(rng.integers(len(b) // 2, len(b)))]
+        elif kind == 2:  # replace the scan by noise
+            b = b[:len(b) // 3] + bytes(rng.integers(0, 255, len(b) - len(b) // 3, dtype=np.uint8))
+        else:  # random bytes anywhere (headers included)
+            for _ in range(4):
+                i = int(rng.integers(2, len(b)))
+                b[i] = int(rng.integers(0, 256))
+        st, used = core.jpeg_scan_prepare(bytes(b), prep.ctypes.data, prep.nbytes)
+        if st != 0:
+            continue
+        (tmp_path / "p.bin").write_bytes(prep[:used].tobytes())
+        for span, passes in ((512, 3), (2048, 0)):
+            r = subprocess.run([exe, str(tmp_path / "p.bin"), str(span), str(tmp_path / "c.bin")]
+                               + ([str(passes)] if passes else []), capture_output=True, text=True, timeout=120)
+            assert r.returncode == 0, (trial, r.stderr[-2000:])
+            runs += 1
+    assert runs >= 20
