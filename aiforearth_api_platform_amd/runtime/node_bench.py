@@ -30,7 +30,7 @@ import json
 import os
 import threading
 import time
-from typing import Optional
+from typing import Optional, Sequence
 
 import numpy as np
 import torch
@@ -64,7 +64,8 @@ class Client:
 
 
 def http_phase(cp, pool, seconds: float, batch: int, item_shape, path: str, frontends: int = 0,
-               tls: bool = False, max_queue_ms: float = 0.0) -> dict:
+               tls: bool = False, max_queue_ms: float = 0.0, jpeg: Optional[bytes] = None,
+               phases: Sequence[str] = ("batch_route", "single_image_route")) -> dict:
     """REST ingest on this node: aiohttp gateway (this process) + binary batch route (streamed into the
     payload ring), then single-image requests. ``frontends``: ingest front-end processes sharing the port
     (native C++ ``ai4e_ingestd`` by default, AI4E_FRONTEND_IMPL=python for runtime/frontend.py; the pool needs
@@ -72,7 +73,9 @@ def http_phase(cp, pool, seconds: float, batch: int, item_shape, path: str, fron
     processes; the record carries the client and server CPU seconds, so a reader can see which side was
     the ceiling. ``tls``: the front-ends terminate TLS (OpenSSL in ``ai4e_ingestd``, the test certificate under
     tests/fixtures) and every client connection is an HTTPS session. ``max_queue_ms`` > 0: the front-ends' latency-
-    budgeted admission (429 + Retry-After past the budget; the load generator backs off and retries)."""
+    budgeted admission (429 + Retry-After past the budget; the load generator backs off and retries). ``jpeg``: a
+    JPEG frame for the ``jpeg_route`` phase (single ``image/jpeg`` requests: prepared into ring slots by the native
+    front-ends when the pool's workers decode on the GPU, else proxied and decoded by the serving process)."""
     import asyncio
 
     from aiohttp import web
@@ -169,9 +172,13 @@ def http_phase(cp, pool, seconds: float, batch: int, item_shape, path: str, fron
 
     native = os.environ.get("AI4E_HTTP_CLIENT", "native") == "native"
     out = {}
-    for name, body, ctype, is_batch, procs, conc in (
-            ("batch_route", batch_body, BATCH_CONTENT_TYPE, True, 4, 4),
-            ("single_image_route", img.tobytes(), "application/octet-stream", False, 4, 32)):
+    runs = [("batch_route", batch_body, BATCH_CONTENT_TYPE, True, 4, 4),
+            ("single_image_route", img.tobytes(), "application/octet-stream", False, 4, 32)]
+    if jpeg is not None:
+        runs.append(("jpeg_route", jpeg, "image/jpeg", False, 4, 32))
+    for name, body, ctype, is_batch, procs, conc in runs:
+        if name not in phases:
+            continue
         c0, s0 = server_cpu(), server_cpu(True)
         if native:
             res = run_native_clients(url, seconds / 2, conc, body, ctype, procs=procs)

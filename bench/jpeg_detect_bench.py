@@ -25,6 +25,32 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "bench"))
 
 
+def run_http(mode, body, shape, seconds, batch, frontends, max_queue_ms):
+    """The same detector behind the REST front door: 4 native front-ends, the C++ load generator posting the JPEG
+    frame as ``image/jpeg`` (128 connections). gpu: the front-ends prepare frames into ring slots; cpu: they proxy
+    JPEG bodies to the serving process, which decodes them with PIL."""
+    from aiforearth_api_platform_amd.config import Config
+    from aiforearth_api_platform_amd.gateway.control import ControlPlane
+    from aiforearth_api_platform_amd.runtime.node_bench import http_phase
+    from aiforearth_api_platform_amd.runtime.worker_pool import ModelSpec, WorkerPool
+
+    cp = ControlPlane(Config.load(env={}))
+    spec = ModelSpec("aiforearth_api_platform_amd.models.zoo:megadetector", shape, batch, 5)
+    pool = WorkerPool(cp, "http://127.0.0.1/v1/bench/async", spec, ["cuda:0"], jpeg_slots=(mode == "gpu"),
+                      frontends=frontends)
+    try:
+        pool.start(wait_ready_s=900)
+        res = http_phase(cp, pool, 2 * seconds, batch, shape, "/v1/bench/async", frontends=frontends,
+                         max_queue_ms=max_queue_ms, jpeg=body, phases=("jpeg_route",))
+        r = res["jpeg_route"]
+        return {k: r.get(k) for k in ("images_per_s", "busy_429", "errors", "p50_task_latency_ms",
+                                      "p99_task_latency_ms", "server_cpu_s", "server_cpu_split_s", "client_cpu_s",
+                                      "window_s", "connections", "p50_request_latency_ms", "p99_request_latency_ms")}
+    finally:
+        pool.stop()
+        cp.close()
+
+
 def run(mode, bodies, shape, threads, seconds, outstanding, batch):
     from aiforearth_api_platform_amd.config import Config
     from aiforearth_api_platform_amd.gateway.control import ControlPlane
@@ -82,6 +108,9 @@ def main():
     ap.add_argument("--outstanding", type=int, default=128)
     ap.add_argument("--seconds", type=float, default=10.0)
     ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--http", action="store_true", help="through the REST front door (native front-ends)")
+    ap.add_argument("--frontends", type=int, default=4)
+    ap.add_argument("--max-queue-ms", type=float, default=15.0)
     ap.add_argument("--json-out", default="")
     a = ap.parse_args()
     from jpeg_ingest_bench import frame_jpeg
@@ -90,6 +119,13 @@ def main():
     out = {"metric": "camera-trap detection API images/s with JPEG clients (1 GPU)", "frame": [1536, 2048],
            "model": "megadetector (Faster-RCNN R50-FPN, random init)", "input": [640, 640, 3], "results": {}}
     for mode in a.modes.split(","):
+        if a.http:
+            if mode == "raw":
+                continue
+            out["results"][f"http_{mode}"] = run_http(mode, bodies[0], (640, 640, 3), a.seconds, a.batch, a.frontends,
+                                                      a.max_queue_ms)
+            print(f"http_{mode}", out["results"][f"http_{mode}"], flush=True)
+            continue
         out["results"][mode] = run(mode, bodies, (640, 640, 3), a.threads, a.seconds, a.outstanding, a.batch)
         print(mode, out["results"][mode], flush=True)
     line = json.dumps(out)
