@@ -240,6 +240,7 @@ struct Shard {
       rate_sat = sat;
     } else if (t - rate_t >= 0.05) {
       const double r = static_cast<double>(n - rate_n) / (t - rate_t);
+      const uint64_t nref = refused.exchange(0, std::memory_order_relaxed);
       if (n > rate_n) {
         if (!st) {
           rate = rate == 0.0 ? r : 0.7 * rate + 0.3 * r;
@@ -247,7 +248,14 @@ struct Shard {
           rate = rate == 0.0 ? r : 0.7 * rate + 0.3 * r;
         } else if (r > rate) {
           rate = r;
+        } else if (nref > 0) {
+          rate *= 1.5;  // (below)
         }
+      } else if (nref > 0 && !sat) {
+        // refusing while the workers ran out of queued work: the estimate is below the capacity (e.g. one learned
+        // from the first batches after a start, when the demand set the completion rate) and the refusals keep the
+        // samples unsaturated, so it could never rise; probe upward until samples saturate again
+        rate *= 1.5;
       }
       rate_t = t;
       rate_n = n;
@@ -257,6 +265,7 @@ struct Shard {
     return rate;
   }
   std::atomic<double> rate_seen{0.0};
+  std::atomic<uint64_t> refused{0};  // 429s answered since the last rate sample
 
   // request-body upload rate of this front-end (bytes/s, EWMA over completed bodies): a request's tasks only join
   // the queue once its body has arrived, by when the shard has worked off nbytes / upload_bw of its backlog
@@ -982,7 +991,7 @@ int read_body(Conn& c, const Request& r, std::string& body, int64_t limit) {
 
 bool is_hop(const std::string& k) {
   static const char* hop[] = {"connection", "keep-alive", "proxy-authenticate", "proxy-authorization", "te",
-                              "trailers", "transfer-encoding", "upgrade", "content-length"};
+                              "trailers", "transfer-encoding", "upgrade", "content-length", "expect"};
   std::string l = lower(k);
   for (auto* h : hop)
     if (l == h) return true;
@@ -1002,6 +1011,11 @@ bool proxy(Conn& c, const Request& r, const Route* route, const std::string* pre
   if (prebody) {
     body = *prebody;
   } else {
+    // a client waiting for 100-continue before its body (the load generator from 64 KiB) would otherwise stall
+    // until its own timeout; the body then goes upstream whole, without the Expect header
+    if (lower(r.get("expect")) == "100-continue" && r.content_length > 0 &&
+        !c.send_all("HTTP/1.1 100 Continue\r\n\r\n", 25))
+      return false;
     const int rb = read_body(c, r, body, limit);
     if (rb == 413) return too_large(c, limit);
     if (rb != 0) return false;
@@ -1142,6 +1156,7 @@ bool ingest(Conn& c, const Request& r, Route& route, Shard& s, int mode) {
       wait = s.projected_wait(n, static_cast<double>(nbytes));
     }
     if (wait > g_cfg.max_queue_s) {
+      s.refused.fetch_add(1, std::memory_order_relaxed);
       static const bool dbg = std::getenv("AI4E_INGESTD_DEBUG") != nullptr;
       static std::atomic<int> dbg_n{0};
       if (dbg && s.st && dbg_n.fetch_add(1) % 500 == 0)

@@ -162,6 +162,21 @@ def test_native_frontend_prepares_jpeg_into_slots(tmp_path):
             assert r1.headers.get("Server", "").startswith("ai4e-ingestd")
             pairs.append((r1.json()["TaskId"], r2.json()["TaskId"]))
 
+        # a client that waits for 100-continue before its body, on a body the front-end proxies (progressive JPEG)
+        import socket as _socket
+
+        prog = bodies[-1]
+        with _socket.create_connection(("127.0.0.1", port), timeout=30) as so:
+            so.sendall((f"POST /v1/tiny/async HTTP/1.1\r\nHost: x\r\nContent-Type: image/jpeg\r\n"
+                        f"Content-Length: {len(prog)}\r\nExpect: 100-continue\r\n\r\n").encode())
+            head = so.recv(4096)
+            assert head.startswith(b"HTTP/1.1 100"), head
+            so.sendall(prog)
+            resp = b""
+            while b"\r\n\r\n" not in resp:
+                resp += so.recv(65536)
+            assert resp.startswith(b"HTTP/1.1 200"), resp[:200]
+
         def result(t):
             r = s.get(f"{base}/v1/taskmanagement/task/{t}/result")
             return r.json().get("Result") if r.status_code == 200 else None
