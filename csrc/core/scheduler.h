@@ -154,7 +154,12 @@ class NodeScheduler {
     std::atomic<uint64_t> pending;   // [2] bodies uploading at front-ends without a word of their own
     std::atomic<uint64_t> live;      // [3] dispatch workers that are ready
     std::atomic<uint64_t> inflight;  // [4] items handed to GPU workers, not yet finished or requeued
-    uint64_t pad[3];
+    // [5] microseconds the shard has had items in flight at its workers, closed intervals; [6] CLOCK_MONOTONIC
+    // microseconds at which the open interval began (0: none open). Finished items per busy second is the shard's
+    // capacity at the batches it forms, whatever the load (ingestd admission)
+    std::atomic<uint64_t> busy_us;
+    std::atomic<uint64_t> busy_since_us;
+    uint64_t pad[1];
     std::atomic<uint64_t> fe_pending[kStatFrontends];  // [8 + i] front-end i (scheduler rank kFrontendRank0 + i)
   };
   static_assert(sizeof(ShardStat) == 512, "ShardStat is mapped as 512 bytes by csrc/ingest/ingestd.cpp");
@@ -183,7 +188,7 @@ class NodeScheduler {
   }
   // (tests / stats) the published counters: enq, done, pending (all front-ends), live, inflight
   std::vector<uint64_t> stat_counters() {
-    std::vector<uint64_t> out(5, 0);
+    std::vector<uint64_t> out(6, 0);
     if (!stat_) {
       out[3] = static_cast<uint64_t>(live_.load());
       return out;
@@ -194,6 +199,9 @@ class NodeScheduler {
     for (int i = 0; i < kStatFrontends; ++i) out[2] += stat_->fe_pending[i].load();
     out[3] = stat_->live.load();
     out[4] = stat_->inflight.load();
+    const uint64_t t0 = stat_->busy_since_us.load();
+    const uint64_t now = static_cast<uint64_t>(mono_now() * 1e6);
+    out[5] = stat_->busy_us.load() + (t0 && now > t0 ? now - t0 : 0);
     return out;
   }
 
@@ -737,8 +745,14 @@ class NodeScheduler {
   NodeScheduler& owner(const Outstanding& o) { return o.src ? *o.src : *this; }
   void add_inflight(NodeScheduler& own, size_t n, bool add) {
     if (!own.stat_ || !n) return;
-    if (add) own.stat_->inflight.fetch_add(n);
-    else own.stat_->inflight.fetch_sub(n);
+    std::lock_guard<std::mutex> g(own.busy_mu_);  // (per batch: the 0 <-> busy transitions stay paired)
+    const uint64_t now = static_cast<uint64_t>(mono_now() * 1e6);
+    if (add) {
+      if (own.stat_->inflight.fetch_add(n) == 0) own.stat_->busy_since_us.store(now);
+    } else if (own.stat_->inflight.fetch_sub(n) == n) {
+      const uint64_t t0 = own.stat_->busy_since_us.exchange(0);
+      if (t0 && now > t0) own.stat_->busy_us.fetch_add(now - t0);
+    }
   }
 
   void mark_dead(Worker& w, const char* why, bool report) {
@@ -1209,6 +1223,7 @@ class NodeScheduler {
   std::atomic<uint64_t> next_bid_{1};
   std::atomic<uint64_t> images_done_{0};
   ShardStat* stat_ = nullptr;
+  std::mutex busy_mu_;  // (add_inflight: busy-interval bookkeeping)
   std::string stat_name_;
   char* tags_ = nullptr;
   std::mutex fail_mu_;

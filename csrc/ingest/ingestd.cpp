@@ -228,9 +228,36 @@ struct Shard {
   // a sample from a shard that ran out of work only measures the demand, a lower bound: it can raise the estimate,
   // never lower it. (Round 5 held the smoothed rate's peak and let it decay 10 %/s, so a route whose clients were
   // slower than the GPU — single images — read as a slow GPU and throttled itself to 0.59x.)
+  // Busy time published by the scheduler (words 5-6: microseconds with items in flight at the workers): finished items
+  // per busy second is the capacity at the batches the shard forms, at any load. Used once the workers have been
+  // busy for 20 ms of a sample; the completion-rate rules below are the fallback.
+  double busy_s() const {
+    const uint64_t b = st[5].load(std::memory_order_relaxed), t0 = st[6].load(std::memory_order_relaxed);
+    const uint64_t now = static_cast<uint64_t>(ai4e::mono_now() * 1e6);
+    return static_cast<double>(b + (t0 && now > t0 ? now - t0 : 0)) * 1e-6;
+  }
+  double rate_busy0 = 0.0;
+  int64_t rate_bn = 0;
   double service_rate() {
     std::unique_lock<std::mutex> g(rate_mu, std::try_to_lock);
     if (!g.owns_lock()) return rate_seen.load(std::memory_order_relaxed);  // (another thread is sampling)
+    if (st) {
+      const double b = busy_s();
+      const int64_t n = static_cast<int64_t>(st[1].load(std::memory_order_relaxed));
+      if (rate_busy0 == 0.0 && rate_bn == 0) {
+        rate_busy0 = b;
+        rate_bn = n;
+      } else if (b - rate_busy0 >= 0.02 && n > rate_bn) {
+        const double r = static_cast<double>(n - rate_bn) / (b - rate_busy0);
+        busy_rate = busy_rate == 0.0 ? r : 0.7 * busy_rate + 0.3 * r;
+        rate_busy0 = b;
+        rate_bn = n;
+      }
+      if (busy_rate > 0.0) {
+        rate_seen.store(busy_rate, std::memory_order_relaxed);
+        return busy_rate;
+      }
+    }
     const double t = ai4e::mono_now();
     const int64_t n = st ? static_cast<int64_t>(st[1].load(std::memory_order_relaxed)) : freed.load();
     const bool sat = st ? queued() : false;
@@ -266,6 +293,7 @@ struct Shard {
   }
   std::atomic<double> rate_seen{0.0};
   std::atomic<uint64_t> refused{0};  // 429s answered since the last rate sample
+  double busy_rate = 0.0;            // items per busy second (0: no busy-time sample yet)
 
   // request-body upload rate of this front-end (bytes/s, EWMA over completed bodies): a request's tasks only join
   // the queue once its body has arrived, by when the shard has worked off nbytes / upload_bw of its backlog
