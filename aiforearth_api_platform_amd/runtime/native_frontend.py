@@ -120,8 +120,10 @@ def spawn_native_frontends(n: int, pools: Dict[str, object], routes: List[dict],
                 shard_lines.setdefault(name, []).append(si)
                 digits = pool.mint_digits() if hasattr(pool, "mint_digits") else "-"
                 stat = getattr(pool, "stat_name", "") or "-"  # the shard's load counters (admission)
+                mb = int(getattr(getattr(pool, "spec", None), "max_batch", 0) or 0)  # (admission: full-batch capacity)
                 lines.append(f"shard {si} {child.fileno()} {_token(ep.ring.name)} {int(ep.ring.nslots)} {item} "
-                             f"{int(base)} {int(length)} {_token(ep.endpoint)} {shape} {_token(digits)} {_token(stat)}")
+                             f"{int(base)} {int(length)} {_token(ep.endpoint)} {shape} {_token(digits)} {_token(stat)} "
+                             f"{mb}")
         for r in routes:
             si = ",".join(map(str, shard_lines[r["endpoint"]])) if r.get("endpoint") in pools else "-1"
             types = ",".join(_token(t) for t in r.get("content_types") or []) or "-"

@@ -159,7 +159,7 @@ class NodeScheduler {
     // capacity at the batches it forms, whatever the load (ingestd admission)
     std::atomic<uint64_t> busy_us;
     std::atomic<uint64_t> busy_since_us;
-    uint64_t pad[1];
+    std::atomic<uint64_t> batches;  // [7] batches finished (or returned) by the workers
     std::atomic<uint64_t> fe_pending[kStatFrontends];  // [8 + i] front-end i (scheduler rank kFrontendRank0 + i)
   };
   static_assert(sizeof(ShardStat) == 512, "ShardStat is mapped as 512 bytes by csrc/ingest/ingestd.cpp");
@@ -749,7 +749,10 @@ class NodeScheduler {
     const uint64_t now = static_cast<uint64_t>(mono_now() * 1e6);
     if (add) {
       if (own.stat_->inflight.fetch_add(n) == 0) own.stat_->busy_since_us.store(now);
-    } else if (own.stat_->inflight.fetch_sub(n) == n) {
+      return;
+    }
+    own.stat_->batches.fetch_add(1);
+    if (own.stat_->inflight.fetch_sub(n) == n) {
       const uint64_t t0 = own.stat_->busy_since_us.exchange(0);
       if (t0 && now > t0) own.stat_->busy_us.fetch_add(now - t0);
     }

@@ -172,6 +172,7 @@ struct Shard {
   std::string endpoint, endpoint_path, shape_str;
   int64_t nslots = 0, item = 0, base = 0, len = 0;
   int out_h = 0, out_w = 0, out_c = 0;  // the model input (shape_str)
+  int64_t max_batch = 0;                // the workers' batch size (0: unknown)
   uint8_t* ring = nullptr;
   // the ring's key for slots holding prepared JPEG frames (its tail, csrc/core/jpeg_layout.h RingTail; 0: the ring's
   // workers do not decode them, JPEG bodies go to the serving process)
@@ -237,21 +238,31 @@ struct Shard {
     return static_cast<double>(b + (t0 && now > t0 ? now - t0 : 0)) * 1e-6;
   }
   double rate_busy0 = 0.0;
-  int64_t rate_bn = 0;
+  int64_t rate_bn = 0, rate_bb = 0;
   double service_rate() {
     std::unique_lock<std::mutex> g(rate_mu, std::try_to_lock);
     if (!g.owns_lock()) return rate_seen.load(std::memory_order_relaxed);  // (another thread is sampling)
     if (st) {
+      // a backlog drains in full batches: with the workers' batch size known, the capacity is max_batch batches per
+      // busy second of a batch (a light load forms small batches that each cost about a full one: their items per
+      // busy second understate what a backlog would get); else finished items per busy second
       const double b = busy_s();
       const int64_t n = static_cast<int64_t>(st[1].load(std::memory_order_relaxed));
+      const int64_t nb = static_cast<int64_t>(st[7].load(std::memory_order_relaxed));
       if (rate_busy0 == 0.0 && rate_bn == 0) {
         rate_busy0 = b;
         rate_bn = n;
+        rate_bb = nb;
       } else if (b - rate_busy0 >= 0.02 && n > rate_bn) {
-        const double r = static_cast<double>(n - rate_bn) / (b - rate_busy0);
+        const double r = max_batch > 0 && nb > rate_bb
+                             ? std::max(static_cast<double>(n - rate_bn),
+                                        static_cast<double>(max_batch) * static_cast<double>(nb - rate_bb)) /
+                                   (b - rate_busy0)
+                             : static_cast<double>(n - rate_bn) / (b - rate_busy0);
         busy_rate = busy_rate == 0.0 ? r : 0.7 * busy_rate + 0.3 * r;
         rate_busy0 = b;
         rate_bn = n;
+        rate_bb = nb;
       }
       if (busy_rate > 0.0) {
         rate_seen.store(busy_rate, std::memory_order_relaxed);
@@ -645,7 +656,10 @@ void parse_config(const char* path) {
       ls >> s->idx >> s->fd >> shm >> s->nslots >> s->item >> s->base >> s->len >> s->endpoint >> s->shape_str;
       std::string dg, stat;
       if (ls >> dg && !dg.empty() && dg != "-") s->digits = dg;
-      if (ls >> stat && !stat.empty() && stat != "-") {
+      const bool have_stat = static_cast<bool>(ls >> stat);
+      int64_t mb = 0;
+      if (have_stat && (ls >> mb) && mb > 0) s->max_batch = mb;
+      if (have_stat && !stat.empty() && stat != "-") {
         const int sfd = shm_open(("/" + stat).c_str(), O_RDWR, 0);
         void* sp = sfd >= 0 ? mmap(nullptr, Shard::kStatWords * 8, PROT_READ | PROT_WRITE, MAP_SHARED, sfd, 0)
                             : MAP_FAILED;
