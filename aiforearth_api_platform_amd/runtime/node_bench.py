@@ -65,7 +65,7 @@ class Client:
 
 def http_phase(cp, pool, seconds: float, batch: int, item_shape, path: str, frontends: int = 0,
                tls: bool = False, max_queue_ms: float = 0.0, jpeg: Optional[bytes] = None,
-               phases: Sequence[str] = ("batch_route", "single_image_route")) -> dict:
+               phases: Sequence[str] = ("batch_route", "single_image_route"), jpeg_conc: int = 32) -> dict:
     """REST ingest on this node: aiohttp gateway (this process) + binary batch route (streamed into the
     payload ring), then single-image requests. ``frontends``: ingest front-end processes sharing the port
     (native C++ ``ai4e_ingestd`` by default, AI4E_FRONTEND_IMPL=python for runtime/frontend.py; the pool needs
@@ -174,8 +174,8 @@ def http_phase(cp, pool, seconds: float, batch: int, item_shape, path: str, fron
     out = {}
     runs = [("batch_route", batch_body, BATCH_CONTENT_TYPE, True, 4, 4),
             ("single_image_route", img.tobytes(), "application/octet-stream", False, 4, 32)]
-    if jpeg is not None:
-        runs.append(("jpeg_route", jpeg, "image/jpeg", False, 4, 32))
+    if jpeg is not None:  # (a slower model: ~one budget's worth of requests in flight, 4 x jpeg_conc connections)
+        runs.append(("jpeg_route", jpeg, "image/jpeg", False, 4, jpeg_conc))
     for name, body, ctype, is_batch, procs, conc in runs:
         if name not in phases:
             continue

@@ -25,10 +25,11 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "bench"))
 
 
-def run_http(mode, body, shape, seconds, batch, frontends, max_queue_ms):
+def run_http(mode, body, shape, seconds, batch, frontends, max_queue_ms, conc):
     """The same detector behind the REST front door: 4 native front-ends, the C++ load generator posting the JPEG
-    frame as ``image/jpeg`` (128 connections). gpu: the front-ends prepare frames into ring slots; cpu: they proxy
-    JPEG bodies to the serving process, which decodes them with PIL."""
+    frame as ``image/jpeg`` from 4 processes x ``conc`` connections. gpu: the front-ends prepare frames into ring
+    slots; cpu: they proxy JPEG bodies to the serving process, which decodes them with PIL. (At ~4k images/s a 15 ms
+    budget holds ~60 requests: 128 clients always find it full and back off; 4 x 12 keeps about a budget in flight.)"""
     from aiforearth_api_platform_amd.config import Config
     from aiforearth_api_platform_amd.gateway.control import ControlPlane
     from aiforearth_api_platform_amd.runtime.node_bench import http_phase
@@ -41,7 +42,7 @@ def run_http(mode, body, shape, seconds, batch, frontends, max_queue_ms):
     try:
         pool.start(wait_ready_s=900)
         res = http_phase(cp, pool, 2 * seconds, batch, shape, "/v1/bench/async", frontends=frontends,
-                         max_queue_ms=max_queue_ms, jpeg=body, phases=("jpeg_route",))
+                         max_queue_ms=max_queue_ms, jpeg=body, phases=("jpeg_route",), jpeg_conc=conc)
         r = res["jpeg_route"]
         return {k: r.get(k) for k in ("images_per_s", "busy_429", "errors", "p50_task_latency_ms",
                                       "p99_task_latency_ms", "server_cpu_s", "server_cpu_split_s", "client_cpu_s",
@@ -111,6 +112,7 @@ def main():
     ap.add_argument("--http", action="store_true", help="through the REST front door (native front-ends)")
     ap.add_argument("--frontends", type=int, default=4)
     ap.add_argument("--max-queue-ms", type=float, default=15.0)
+    ap.add_argument("--conc", type=int, default=12, help="connections per load-generator process (4 processes)")
     ap.add_argument("--json-out", default="")
     a = ap.parse_args()
     from jpeg_ingest_bench import frame_jpeg
@@ -123,7 +125,7 @@ def main():
             if mode == "raw":
                 continue
             out["results"][f"http_{mode}"] = run_http(mode, bodies[0], (640, 640, 3), a.seconds, a.batch, a.frontends,
-                                                      a.max_queue_ms)
+                                                      a.max_queue_ms, a.conc)
             print(f"http_{mode}", out["results"][f"http_{mode}"], flush=True)
             continue
         out["results"][mode] = run(mode, bodies, (640, 640, 3), a.threads, a.seconds, a.outstanding, a.batch)
