@@ -30,6 +30,7 @@ _SIGS = {
     "ai4e_conv2d_f16_fwd": [_vp, _vp, _vp, _vp, _vp] + [_c_int] * 19 + [_vp],
     "ai4e_conv2d_gn_fwd": [_vp, _vp, _vp, _vp, _vp] + [_c_int] * 19 + [_vp, _c_int, _vp],
     "ai4e_conv2d_head_fwd": [_vp, _vp, _vp, _vp, _vp] + [_c_int] * 19 + [_vp, _c_int, _vp, _vp, _vp],
+    "ai4e_conv2d_sk_fwd": [_vp, _vp, _vp, _vp, _vp] + [_c_int] * 20 + [_vp, _vp, _vp],
     "ai4e_conv_chain_fwd": [_vp] * 10 + [_c_int] * 11 + [_vp, _c_int, _vp],
     "ai4e_conv_chain_f16_fwd": [_vp] * 10 + [_c_int] * 11 + [_vp, _c_int, _vp],
     "ai4e_conv_pair_fwd": [_vp] * 8 + [_c_int] * 5 + [_vp],

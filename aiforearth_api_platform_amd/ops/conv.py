@@ -130,6 +130,17 @@ def tuned_tile(pc: PackedConv, n: int, h: int, w: int, residual: bool) -> int:
     return int(cfg or 0)
 
 
+def split_cfg(tile_cfg: int) -> Tuple[int, int]:
+    """Tile-table entry -> (K split, tile config): entries ``cfg | ks << 4`` (ks 2..4) run a 256-wide config (6, 9,
+    10) with split-K over ``ks`` workgroups per output tile (``ai4e_conv2d_sk_fwd``): layer4's 3x3 convs at batch 250
+    are 96-128 tiles of K 2304-4608, a quarter to a half of the chip's 256 CUs. Other paths (fp16, fused GroupNorm
+    statistics / head) run the plain config."""
+    ks = tile_cfg >> 4
+    if ks < 2 or (tile_cfg & 15) not in (6, 9, 10):
+        return 1, tile_cfg & 15 if ks else tile_cfg
+    return ks, tile_cfg & 15
+
+
 def conv2d_nhwc(x: torch.Tensor, pc: PackedConv, residual: Optional[torch.Tensor] = None, relu: bool = False,
                 out: Optional[torch.Tensor] = None, out_coff: int = 0, tile_cfg: int = -1,
                 residual_up2: bool = False) -> torch.Tensor:
@@ -180,9 +191,19 @@ def _conv_hip(x, pc, residual, relu, out, out_coff, tile_cfg, residual_up2=False
         if residual.shape != rshape or not residual.is_contiguous() or (residual_up2 and (oh % 2 or ow % 2)):
             raise ValueError(f"residual must be contiguous {list(rshape)}")
         ldres = pc.cout
+    ksplit, tile_cfg = split_cfg(tile_cfg)
     args = (base + 2 * (xoff - xoff % ldx), pc.w_packed.data_ptr(), pc.bias.data_ptr(), _ext.ptr(residual),
             out.data_ptr(), n, h, w, c, ldx, xoff % ldx, pc.kh, pc.kw, pc.stride, pc.pad, oh, ow, pc.cout, pc.kpad, ldy,
             out_coff, ldres, int(relu) | (2 if residual_up2 else 0), tile_cfg)
+    if ksplit > 1 and gn is None and not f16:
+        # split-K workspace per call (stream-ordered allocator; a captured graph keeps its own): the parked fp32
+        # partials and the arrival / ready counters, which must be zero at launch (the kernel leaves them zero)
+        tiles = -(-n * oh * ow // (256 if tile_cfg == 6 else 192)) * -(-pc.cout // 256)
+        park = torch.empty(tiles * (ksplit - 1) * (256 if tile_cfg == 6 else 192) * 256, device=x.device,
+                           dtype=torch.float32)
+        sems = torch.zeros(2 * tiles, device=x.device, dtype=torch.int32)
+        _ext.call("ai4e_conv2d_sk_fwd", *args, ksplit, park.data_ptr(), sems.data_ptr(), _ext.stream_ptr(x.device))
+        return
     if gn is None:
         _ext.call("ai4e_conv2d_f16_fwd" if f16 else "ai4e_conv2d_fwd", *args, _ext.stream_ptr(x.device))
     else:

@@ -98,6 +98,12 @@ struct ConvParams {
   const float* hb;
   uint16_t* hy;
   int hw_ld;
+  // split-K (256-wide configs only; ksplit 1 = off): the K tiles of an output tile are split over ksplit workgroups;
+  // the first ksplit - 1 to finish park their fp32 accumulators in skw, the last adds them and runs the epilogue.
+  // sks [2 x tiles] int32 (zero at launch, zero again when the launch ends): arrivals, then parked partials
+  int ksplit;
+  float* skw;
+  int* sks;
 };
 
 // Row of the residual tensor for output pixel m: m itself, or (relu flag bit 1) the pixel (oh/2, ow/2) of a
@@ -580,12 +586,19 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 2, wc = wave & 3;
 
-  const int t = xcd_remap(blockIdx.x, gridDim.x);
+  // split-K: the ksplit workgroups of one output tile are consecutive logical tiles (one XCD's L2 holds the
+  // parked partials), each running K tiles [kb, kb + nk) of the nk_all
+  int t = xcd_remap(blockIdx.x, gridDim.x);
+  const int ksp = p.ksplit > 1 ? p.ksplit : 1;
+  const int ks = t % ksp;
+  t /= ksp;
   const int mt = t / p.ntiles_n;
   const int nt = t - mt * p.ntiles_n;
   const int m0 = mt * BM;
   const int n0 = nt * 256;
-  const int nk = p.Kpad / 64;
+  const int nk_all = p.Kpad / 64;
+  const int kb = ks * nk_all / ksp;
+  const int nk = (ks + 1) * nk_all / ksp - kb;
   const uint32_t sbase = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(smem));
   if (p.hy) {
     // the oldest DMA of the launch, so every counted ring wait below also covers it; thread tid fills slot tid
@@ -624,11 +637,24 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
         xrow[i][xq] = nullptr;
       }
     }
-    wrow[i] = p.w + static_cast<long>(n0 + (R >> 5) * 64 + (R & 31)) * p.Kpad + 8 * q;
+    wrow[i] = p.w + static_cast<long>(n0 + (R >> 5) * 64 + (R & 31)) * p.Kpad + kb * 64 + 8 * q;
   }
   const uint16_t* const zero = p.zero;
-  // X units are staged tile by tile (XQ0 and XQ1 at different phases): one tap walk per unit kind
+  // X units are staged tile by tile (XQ0 and XQ1 at different phases): one tap walk per unit kind, started at
+  // K element kb * 64 (tap (kh, kw), channel cb: element offset (kh * W + kw) * ldx + cb)
   TapWalk wx[2];
+  const int kx0 = kb * 64;  // pointwise: channel offset of this split's first K tile
+  if (GATHER == GATHER_TAP && kb > 0) {
+    const int tap = kx0 / p.C, cb = kx0 - tap * p.C;
+    const int kh = tap / p.KW, kw = tap - kh * p.KW;
+#pragma unroll
+    for (int xq = 0; xq < 2; ++xq) {
+      wx[xq].kh = kh;
+      wx[xq].kw = kw;
+      wx[xq].cb = cb;
+      wx[xq].off = (kh * p.W + kw) * p.ldx + cb;
+    }
+  }
   const int rowjump = (p.W - p.KW) * p.ldx;
 
   // stage unit u of K tile kt into buffer kt&1 (2 DMAs per lane); X units must be staged in tile order
@@ -639,10 +665,10 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
     constexpr int nl = xq ? L3 : 2;
     const uint32_t xb = (xq && L3 == 1) ? ubase - (8 * wave) * 128 : ubase;
     if constexpr (GATHER == GATHER_POINTWISE) {
-      const bool kok = k0 < p.C;
+      const bool kok = kx0 + k0 < p.C;
 #pragma unroll
       for (int i = 0; i < nl; ++i) {
-        const void* src = (kok && xrow[i][xq] != nullptr) ? static_cast<const void*>(xrow[i][xq] + k0) : zero;
+        const void* src = (kok && xrow[i][xq] != nullptr) ? static_cast<const void*>(xrow[i][xq] + kx0 + k0) : zero;
         glds16(src, xb + i * 8 * 128);
       }
     } else {
@@ -848,6 +874,45 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
   if (wr == 0) __builtin_amdgcn_s_barrier();  // re-align the two groups
   wait_vmcnt<0>();
   __syncthreads();
+
+  if (ksp > 1) {
+    // split-K hand-off. Arrival order decides the roles, so nobody waits on a workgroup that has not started: the
+    // first ksplit - 1 arrivals park their accumulators (thread-contiguous f32x4, one 16-B store per lane and
+    // fragment) in their slot and count themselves ready; the last arrival waits for that count (those workgroups
+    // are already past their arrival, only their stores are outstanding), adds the parked partials, resets both
+    // counters for the next launch and runs the epilogue.
+    __shared__ int sk_arrival;
+    const int ntl = gridDim.x / ksp;
+    constexpr int PSZ = MFR * 4 * 512;  // f32x4 per parked partial
+    if (tid == 0) sk_arrival = atomicAdd(p.sks + t, 1);
+    __syncthreads();
+    const int arrival = sk_arrival;
+    f32x4_t* const park = reinterpret_cast<f32x4_t*>(p.skw) + static_cast<long>(t) * (ksp - 1) * PSZ + tid;
+    if (arrival < ksp - 1) {
+#pragma unroll
+      for (int i = 0; i < MFR; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) park[arrival * PSZ + (i * 4 + j) * 512] = acc[i][j];
+      __threadfence();  // release: the partial is visible device-wide before the ready count moves
+      __syncthreads();
+      if (tid == 0) atomicAdd(p.sks + ntl + t, 1);
+      return;
+    }
+    if (tid == 0) {
+      while (__hip_atomic_load(p.sks + ntl + t, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < ksp - 1)
+        __builtin_amdgcn_s_sleep(2);
+      __hip_atomic_store(p.sks + t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(p.sks + ntl + t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    __threadfence();  // acquire for every thread of the workgroup
+    for (int q = 0; q < ksp - 1; ++q) {
+#pragma unroll
+      for (int i = 0; i < MFR; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] += park[q * PSZ + (i * 4 + j) * 512];
+    }
+  }
 
   // ---- epilogue, one pixel group at a time: fp32 [WROWS][256] tile in LDS (16-B chunk index
   //      XOR (row & 7)), then every thread handles 16-B output chunks: + bias (+ residual), ReLU.
@@ -1074,7 +1139,7 @@ int launch256(const ConvParams& p0, hipStream_t s) {
     return AI4E_EINVAL;
   const int mt = ai4e_cdiv(p.M, BM);
   p.ntiles_n = ai4e_cdiv(p.Kout, 256);
-  const int nb = mt * p.ntiles_n;
+  const int nb = mt * p.ntiles_n * (p.ksplit > 1 ? p.ksplit : 1);
   p.zero = zero_chunk_ptr();
   if (!p.zero) return AI4E_ELAUNCH;
   const unsigned dyn = p.hy ? 16u * 512u : 0u;  // the fused head's weights
@@ -1100,7 +1165,8 @@ template <bool F16>
 int conv2d_impl(const void* x, const void* w, const void* bias, const void* res, void* y, int N, int H, int W, int C,
                 int ldx, int xcoff, int KH, int KW, int stride, int pad, int OH, int OW, int Kout, int Kpad, int ldy,
                 int ycoff, int ldres, int relu, int tile_cfg, float* gnp, int gn_groups, hipStream_t stream,
-                const void* hw = nullptr, int hw_ld = 0, const void* hb = nullptr, void* hy = nullptr) {
+                const void* hw = nullptr, int hw_ld = 0, const void* hb = nullptr, void* hy = nullptr,
+                int ksplit = 1, void* skw = nullptr, void* sks = nullptr) {
   if (C % 8 || ldx % 8 || xcoff % 8 || Kpad % (2 * BK) || Kout % 4 || ldy % 4 || ycoff % 4 || (res && ldres % 4) ||
       Kpad < KH * KW * C)
     return AI4E_EINVAL;
@@ -1127,6 +1193,14 @@ int conv2d_impl(const void* x, const void* w, const void* bias, const void* res,
   } else if (!y) {
     return AI4E_EINVAL;
   }
+  if (ksplit > 1) {
+    // split-K: the 256-wide configs, plain epilogue (no GroupNorm statistics, no fused head), >= 1 K tile per split
+    if (ksplit > 4 || !skw || !sks || hy || !(tile_cfg == 6 || tile_cfg == 9 || tile_cfg == 10) || Kpad / 64 < ksplit)
+      return AI4E_EINVAL;
+    p.ksplit = ksplit;
+    p.skw = static_cast<float*>(skw);
+    p.sks = static_cast<int*>(sks);
+  }
   if (p.M <= 0) return AI4E_OK;
   if (tile_cfg == 0) tile_cfg = Kout <= 64 ? 2 : 1;
   if (gnp) {
@@ -1140,6 +1214,7 @@ int conv2d_impl(const void* x, const void* w, const void* bias, const void* res,
     if (tile_cfg == 3 || gn_groups <= 0 || Kout % gn_groups || (OH * OW) % bm || Kout % 8 || ldy % 8 || ycoff % 8 ||
         (res && ldres % 8) || bn % cgw || (wide && (cgw & (cgw - 1))))
       return AI4E_EINVAL;
+    if (ksplit > 1) return AI4E_EINVAL;
     p.gnp = gnp;
     p.gn_groups = gn_groups;
   }
@@ -1201,6 +1276,20 @@ AI4E_API int ai4e_conv2d_head_fwd(const void* x, const void* w, const void* bias
   if (!head) return AI4E_EINVAL;
   return conv2d_impl<false>(x, w, bias, res, y, N, H, W, C, ldx, xcoff, KH, KW, stride, pad, OH, OW, Kout, Kpad, ldy,
                             ycoff, ldres, relu, tile_cfg, nullptr, 0, stream, hw, hw_ld, hb, head);
+}
+
+// Same conv with split-K over ksplit (2..4) workgroups per output tile, for grids too small to fill the chip (a 256-wide
+// tile config 6, 9 or 10; e.g. ResNet-50 layer4's 3x3 convs: 128 tiles of K = 4608 -> 256 workgroups of 2304).
+// skw: fp32 workspace of tiles * (ksplit - 1) * BM * 256 floats (BM = 256 for config 6, else 192; tiles =
+// ceil(M / BM) * ceil(Kout / 256)); sks: 2 * tiles int32, zero at launch (the launch leaves them zero again).
+AI4E_API int ai4e_conv2d_sk_fwd(const void* x, const void* w, const void* bias, const void* res, void* y, int N, int H,
+                                int W, int C, int ldx, int xcoff, int KH, int KW, int stride, int pad, int OH, int OW,
+                                int Kout, int Kpad, int ldy, int ycoff, int ldres, int relu, int tile_cfg, int ksplit,
+                                void* skw, void* sks, hipStream_t stream) {
+  if (ksplit < 2) return AI4E_EINVAL;
+  return conv2d_impl<false>(x, w, bias, res, y, N, H, W, C, ldx, xcoff, KH, KW, stride, pad, OH, OW, Kout, Kpad, ldy,
+                            ycoff, ldres, relu, tile_cfg, nullptr, 0, stream, nullptr, 0, nullptr, nullptr, ksplit, skw,
+                            sks);
 }
 
 #if AI4E_K256_STAMPS

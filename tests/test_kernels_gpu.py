@@ -125,6 +125,71 @@ def test_conv_tile256(case, epi, tile):
     assert err <= 0.02 * ref.abs().max().item() + 0.02, err
 
 
+SPLITK_CASES = [
+    # n, h, w, cin, cout, k, stride, pad (K tiles of 64: 72, 36, 8, 4, 36)
+    (250, 7, 7, 512, 512, 3, 1, 1),     # ResNet-50 layer4 3x3 at the serving batch
+    (3, 14, 14, 512, 512, 3, 2, 1),     # layer4's strided 3x3
+    (2, 7, 7, 512, 2048, 1, 1, 0),      # pointwise, M < BM
+    (3, 28, 28, 256, 512, 1, 2, 0),     # strided pointwise
+    (1, 33, 17, 256, 264, 3, 1, 1),     # ragged M, Cout = 256 + 8 (masked second channel tile)
+]
+
+
+@pytest.mark.parametrize("ks", [2, 3, 4])
+@pytest.mark.parametrize("tile", [6, 9, 10])
+@pytest.mark.parametrize("case", SPLITK_CASES)
+def test_conv_splitk(case, tile, ks):
+    """Split-K over ks workgroups per output tile (arrival-ordered hand-off through the fp32 park) vs fp32."""
+    n, h, w, cin, cout, k, s, p = case
+    torch.manual_seed(11)
+    wt = torch.randn(cout, cin, k, k) / (cin * k * k) ** 0.5
+    b = torch.randn(cout) * 0.1
+    pc = pack_conv(wt, b, stride=s, pad=p).to(DEV)
+    x = torch.randn(n, h, w, pc.cin_pad, device=DEV).to(torch.bfloat16)
+    oh, ow = pc.out_hw(h, w)
+    res = torch.randn(n, oh, ow, cout, device=DEV).to(torch.bfloat16)
+    y = conv2d_nhwc(x, pc, residual=res, relu=True, tile_cfg=tile | ks << 4)
+    y2 = conv2d_nhwc(x, pc, residual=res, relu=True, tile_cfg=tile | ks << 4)  # counters were left zero
+    torch.cuda.synchronize()
+    wq = pc.w_packed[:cout, :k * k * pc.cin_pad].float().reshape(cout, k, k, pc.cin_pad).permute(0, 3, 1, 2)
+    ref = ref_conv(x, wq, b.to(DEV), s, p, res, True)
+    err = (y.float() - ref).abs().max().item()
+    assert err <= 0.02 * ref.abs().max().item() + 0.02, err
+    assert torch.equal(y, y2)
+
+
+def test_conv_splitk_streams_and_graph():
+    """Concurrent split-K launches on two streams (separate workspaces) and a captured graph's replays."""
+    torch.manual_seed(12)
+    wt = torch.randn(512, 512, 3, 3) / (512 * 9) ** 0.5
+    pc = pack_conv(wt, torch.randn(512) * 0.1, pad=1).to(DEV)
+    xs = [torch.randn(64, 7, 7, 512, device=DEV).to(torch.bfloat16) for _ in range(2)]
+    refs = [conv2d_nhwc(x, pc, relu=True, tile_cfg=9) for x in xs]
+    streams = [torch.cuda.Stream() for _ in range(2)]
+    outs = [[], []]
+    torch.cuda.synchronize()
+    for _ in range(8):
+        for i in range(2):
+            with torch.cuda.stream(streams[i]):
+                outs[i].append(conv2d_nhwc(xs[i], pc, relu=True, tile_cfg=9 | 2 << 4))
+    torch.cuda.synchronize()
+    for i in range(2):
+        for y in outs[i]:
+            assert (y.float() - refs[i].float()).abs().max().item() <= 0.02 * refs[i].float().abs().max().item()
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        conv2d_nhwc(xs[0], pc, relu=True, tile_cfg=9 | 2 << 4)
+    torch.cuda.current_stream().wait_stream(side)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        yg = conv2d_nhwc(xs[0], pc, relu=True, tile_cfg=9 | 2 << 4)
+    for _ in range(3):
+        g.replay()
+        torch.cuda.synchronize()
+        assert (yg.float() - refs[0].float()).abs().max().item() <= 0.02 * refs[0].float().abs().max().item()
+
+
 def test_conv_channel_slices():
     """Write into a channel slice of a concat buffer and read from a channel slice."""
     torch.manual_seed(2)
