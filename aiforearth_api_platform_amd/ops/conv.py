@@ -199,7 +199,7 @@ def _conv_hip(x, pc, residual, relu, out, out_coff, tile_cfg, residual_up2=False
         # split-K workspace per call (stream-ordered allocator; a captured graph keeps its own): the parked fp32
         # partials and the arrival / ready counters, which must be zero at launch (the kernel leaves them zero)
         tiles = -(-n * oh * ow // (256 if tile_cfg == 6 else 192)) * -(-pc.cout // 256)
-        park = torch.empty(tiles * (ksplit - 1) * (256 if tile_cfg == 6 else 192) * 256, device=x.device,
+        park = torch.empty(tiles * ksplit * (256 if tile_cfg == 6 else 192) * 256, device=x.device,
                            dtype=torch.float32)
         sems = torch.zeros(2 * tiles, device=x.device, dtype=torch.int32)
         _ext.call("ai4e_conv2d_sk_fwd", *args, ksplit, park.data_ptr(), sems.data_ptr(), _ext.stream_ptr(x.device))

@@ -99,7 +99,7 @@ struct ConvParams {
   uint16_t* hy;
   int hw_ld;
   // split-K (256-wide configs only; ksplit 1 = off): the K tiles of an output tile are split over ksplit workgroups;
-  // the first ksplit - 1 to finish park their fp32 accumulators in skw, the last adds them and runs the epilogue.
+  // the first ksplit - 1 to finish park their fp32 accumulators in skw, the last sums them and runs the epilogue.
   // sks [2 x tiles] int32 (zero at launch, zero again when the launch ends): arrivals, then parked partials
   int ksplit;
   float* skw;
@@ -877,22 +877,23 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
 
   if (ksp > 1) {
     // split-K hand-off. Arrival order decides the roles, so nobody waits on a workgroup that has not started: the
-    // first ksplit - 1 arrivals park their accumulators (thread-contiguous f32x4, one 16-B store per lane and
-    // fragment) in their slot and count themselves ready; the last arrival waits for that count (those workgroups
-    // are already past their arrival, only their stores are outstanding), adds the parked partials, resets both
-    // counters for the next launch and runs the epilogue.
+    // first ksplit - 1 arrivals park their accumulators in their split's slot (thread-contiguous f32x4, one 16-B
+    // store per lane and fragment) and count themselves ready; the last arrival waits for that count (those
+    // workgroups are already past their arrival, only their stores are outstanding), sums the ksplit partials in
+    // split order (its own from registers: the result does not depend on who arrived last), resets both counters
+    // for the next launch and runs the epilogue.
     __shared__ int sk_arrival;
     const int ntl = gridDim.x / ksp;
     constexpr int PSZ = MFR * 4 * 512;  // f32x4 per parked partial
     if (tid == 0) sk_arrival = atomicAdd(p.sks + t, 1);
     __syncthreads();
     const int arrival = sk_arrival;
-    f32x4_t* const park = reinterpret_cast<f32x4_t*>(p.skw) + static_cast<long>(t) * (ksp - 1) * PSZ + tid;
+    f32x4_t* const park = reinterpret_cast<f32x4_t*>(p.skw) + static_cast<long>(t) * ksp * PSZ + tid;
     if (arrival < ksp - 1) {
 #pragma unroll
       for (int i = 0; i < MFR; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) park[arrival * PSZ + (i * 4 + j) * 512] = acc[i][j];
+        for (int j = 0; j < 4; ++j) park[ks * PSZ + (i * 4 + j) * 512] = acc[i][j];
       __threadfence();  // release: the partial is visible device-wide before the ready count moves
       __syncthreads();
       if (tid == 0) atomicAdd(p.sks + ntl + t, 1);
@@ -906,12 +907,14 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
     }
     __syncthreads();
     __threadfence();  // acquire for every thread of the workgroup
-    for (int q = 0; q < ksp - 1; ++q) {
 #pragma unroll
-      for (int i = 0; i < MFR; ++i)
+    for (int i = 0; i < MFR; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] += park[q * PSZ + (i * 4 + j) * 512];
-    }
+      for (int j = 0; j < 4; ++j) {
+        f32x4_t v = ks == 0 ? acc[i][j] : park[(i * 4 + j) * 512];
+        for (int q = 1; q < ksp; ++q) v += q == ks ? acc[i][j] : park[q * PSZ + (i * 4 + j) * 512];
+        acc[i][j] = v;
+      }
   }
 
   // ---- epilogue, one pixel group at a time: fp32 [WROWS][256] tile in LDS (16-B chunk index
@@ -1280,7 +1283,7 @@ AI4E_API int ai4e_conv2d_head_fwd(const void* x, const void* w, const void* bias
 
 // Same conv with split-K over ksplit (2..4) workgroups per output tile, for grids too small to fill the chip (a 256-wide
 // tile config 6, 9 or 10; e.g. ResNet-50 layer4's 3x3 convs: 128 tiles of K = 4608 -> 256 workgroups of 2304).
-// skw: fp32 workspace of tiles * (ksplit - 1) * BM * 256 floats (BM = 256 for config 6, else 192; tiles =
+// skw: fp32 workspace of tiles * ksplit * BM * 256 floats (BM = 256 for config 6, else 192; tiles =
 // ceil(M / BM) * ceil(Kout / 256)); sks: 2 * tiles int32, zero at launch (the launch leaves them zero again).
 AI4E_API int ai4e_conv2d_sk_fwd(const void* x, const void* w, const void* bias, const void* res, void* y, int N, int H,
                                 int W, int C, int ldx, int xcoff, int KH, int KW, int stride, int pad, int OH, int OW,

@@ -157,3 +157,18 @@ def test_conv_head_cpu_fallback_matches_two_convs():
     ref = conv2d_nhwc(conv2d_nhwc(x, pc, relu=True), head)
     assert y.shape == (1, 6, 5, 16)
     assert torch.equal(y, ref)
+
+
+def test_split_cfg_decoding_and_cpu_conv():
+    """Tile-table entries ``cfg | ks << 4`` select split-K on the 256-wide configs only; the CPU path ignores them."""
+    from aiforearth_api_platform_amd.ops.conv import conv2d_nhwc, pack_conv, split_cfg
+
+    assert split_cfg(9) == (1, 9) and split_cfg(0) == (1, 0)
+    assert split_cfg(9 | 2 << 4) == (2, 9) and split_cfg(6 | 4 << 4) == (4, 6) and split_cfg(10 | 3 << 4) == (3, 10)
+    assert split_cfg(4 | 2 << 4) == (1, 4)  # not a 256-wide config: the plain tile
+    torch.manual_seed(0)
+    pc = pack_conv(torch.randn(32, 16, 3, 3) / 12, torch.zeros(32), pad=1)
+    x = torch.randn(2, 5, 5, pc.cin_pad).bfloat16()
+    a = conv2d_nhwc(x, pc, relu=True, tile_cfg=9 | 2 << 4)
+    b = conv2d_nhwc(x, pc, relu=True, tile_cfg=9)
+    assert torch.equal(a, b)
