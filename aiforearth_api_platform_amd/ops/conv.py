@@ -202,7 +202,8 @@ def _conv_hip(x, pc, residual, relu, out, out_coff, tile_cfg, residual_up2=False
         park = torch.empty(tiles * ksplit * (256 if tile_cfg == 6 else 192) * 256, device=x.device,
                            dtype=torch.float32)
         sems = torch.zeros(2 * tiles, device=x.device, dtype=torch.int32)
-        _ext.call("ai4e_conv2d_sk_fwd", *args, ksplit, park.data_ptr(), sems.data_ptr(), _ext.stream_ptr(x.device))
+        diag = int(os.environ.get("AI4E_SPLITK_DIAG", "0"))  # hand-off A/B variants (timing only)
+        _ext.call("ai4e_conv2d_sk_fwd", *args, ksplit | diag << 8, park.data_ptr(), sems.data_ptr(), _ext.stream_ptr(x.device))
         return
     if gn is None:
         _ext.call("ai4e_conv2d_f16_fwd" if f16 else "ai4e_conv2d_fwd", *args, _ext.stream_ptr(x.device))

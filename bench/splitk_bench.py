@@ -1,5 +1,5 @@
 """Split-K A/B for the small-grid ResNet-50 convs at the serving batch (250): each shape's committed tile config
-against the 256-wide configs with K split over 2-4 workgroups per output tile (``ops.conv.split_cfg``).
+against the 256-wide configs with K split over two workgroups per output tile (``ops.conv.split_cfg``).
 
 Prints one JSON line per shape: microseconds per launch (CUDA events over 20 launches) and the largest deviation
 of each config's output from the committed config's (split-K only reorders the fp32 sums)."""
@@ -23,14 +23,18 @@ SHAPES = [
     ("l4_down", 1024, 2048, 1, 2, 0, 14, 14, False),
     ("l3_c1", 1024, 256, 1, 1, 0, 14, 14, False),
 ]
-CFGS = [6, 9, 10, 6 | 2 << 4, 9 | 2 << 4, 10 | 2 << 4, 6 | 3 << 4, 9 | 3 << 4, 6 | 4 << 4, 9 | 4 << 4]
+CFGS = [6, 9, 10, 6 | 2 << 4, 9 | 2 << 4, 10 | 2 << 4]
 
 
 def main():
     B = int(os.environ.get("B", "250"))
+    cfgs = [int(c) for c in os.environ["SPLITK_CFGS"].split(",")] if os.environ.get("SPLITK_CFGS") else CFGS
+    only = set(os.environ["SPLITK_LAYERS"].split(",")) if os.environ.get("SPLITK_LAYERS") else None
     dev = torch.device("cuda:0")
     torch.manual_seed(0)
     for name, cin, cout, k, s, p, h, w, res in SHAPES:
+        if only and name not in only:
+            continue
         wt = torch.randn(cout, cin, k, k) / (cin * k * k) ** 0.5
         pc = pack_conv(wt, torch.randn(cout) * 0.1, stride=s, pad=p).to(dev)
         x = torch.randn(B, h, w, pc.cin_pad, device=dev).bfloat16()
@@ -39,7 +43,7 @@ def main():
         base = tuned_tile(pc, B, h, w, res)
         ref = conv2d_nhwc(x, pc, residual=r, relu=True, tile_cfg=base).float()
         us, dev_max = {}, {}
-        for cfg in [base] + [c for c in CFGS if c != base]:
+        for cfg in [base] + [c for c in cfgs if c != base]:
             try:
                 y = conv2d_nhwc(x, pc, residual=r, relu=True, tile_cfg=cfg)
             except RuntimeError:

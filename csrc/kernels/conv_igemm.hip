@@ -98,12 +98,13 @@ struct ConvParams {
   const float* hb;
   uint16_t* hy;
   int hw_ld;
-  // split-K (256-wide configs only; ksplit 1 = off): the K tiles of an output tile are split over ksplit workgroups;
-  // the first ksplit - 1 to finish park their fp32 accumulators in skw, the last sums them and runs the epilogue.
+  // split-K (256-wide configs only; ksplit 1 = off, 2 = on): the K tiles of an output tile are split over two
+  // workgroups; the first to finish parks its fp32 accumulators in skw, the other adds them and runs the epilogue.
   // sks [2 x tiles] int32 (zero at launch, zero again when the launch ends): arrivals, then parked partials
   int ksplit;
   float* skw;
   int* sks;
+  int skdiag;  // 1 = split-K without the parked traffic (timing only; wrong sums)
 };
 
 // Row of the residual tensor for output pixel m: m itself, or (relu flag bit 1) the pixel (oh/2, ow/2) of a
@@ -562,7 +563,7 @@ constexpr int U_ROWS = 128, U_BYTES = U_ROWS * 128;
 // Measured and removed (profiles/r3_ph3/, profiles/r3_k256/; the code is in the git history up to commit bc1ff0a):
 // a static priority for the trailing wave group (config 11), the staging DMAs inside the MFMA segment (12 / 13),
 // 32x32x16 MFMAs (14 / 15) and priority on the load segment instead of the MFMAs (16 / 17) — all slower.
-template <int GATHER, int BM, bool F16 = false, bool PH3 = false>
+template <int GATHER, int BM, bool F16 = false, bool PH3 = false, bool SK = false>
 __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) {
   static_assert(GATHER == GATHER_TAP || GATHER == GATHER_POINTWISE, "256 tile needs C % 64 == 0");
   static_assert(BM == 256 || BM == 192, "wave groups of 128 or 96 pixels");
@@ -586,10 +587,10 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 2, wc = wave & 3;
 
-  // split-K: the ksplit workgroups of one output tile are consecutive logical tiles (one XCD's L2 holds the
-  // parked partials), each running K tiles [kb, kb + nk) of the nk_all
+  // split-K (SK): the two workgroups of one output tile are consecutive logical tiles (one XCD's L2 holds the
+  // parked partial), each running K tiles [kb, kb + nk) of the nk_all
   int t = xcd_remap(blockIdx.x, gridDim.x);
-  const int ksp = p.ksplit > 1 ? p.ksplit : 1;
+  constexpr int ksp = SK ? 2 : 1;
   const int ks = t % ksp;
   t /= ksp;
   const int mt = t / p.ntiles_n;
@@ -875,46 +876,58 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
   wait_vmcnt<0>();
   __syncthreads();
 
-  if (ksp > 1) {
+  if constexpr (SK) {
     // split-K hand-off. Arrival order decides the roles, so nobody waits on a workgroup that has not started: the
-    // first ksplit - 1 arrivals park their accumulators in their split's slot (thread-contiguous f32x4, one 16-B
-    // store per lane and fragment) and count themselves ready; the last arrival waits for that count (those
-    // workgroups are already past their arrival, only their stores are outstanding), sums the ksplit partials in
-    // split order (its own from registers: the result does not depend on who arrived last), resets both counters
-    // for the next launch and runs the epilogue.
+    // first arrival parks its accumulators and counts itself ready; the second waits for that count (the first is
+    // already past its arrival, only its stores are outstanding), adds the parked partial (fp32 addition commutes:
+    // the same bits whichever split arrived last), resets both counters for the next launch and runs the epilogue.
+    // The parked values move with agent-coherent (sc1) 16-B buffer stores and loads, ordered by vmcnt and the
+    // barrier: a release / acquire fence would write back / invalidate the whole L2 of the XCD (buffer_wbl2 /
+    // buffer_inv) and every workgroup on it would refetch its operands (measured 1.6-6x slower), and sc1 dword
+    // atomics cost 2x the 16-B form (profiles/r6_splitk/). p.skdiag = 1 (timing only): no parked traffic.
     __shared__ int sk_arrival;
-    const int ntl = gridDim.x / ksp;
-    constexpr int PSZ = MFR * 4 * 512;  // f32x4 per parked partial
+    const int ntl = gridDim.x / 2;
+    constexpr int PSZ = MFR * 4 * 512;  // f32x4 per parked partial: [i][j][thread]
     if (tid == 0) sk_arrival = atomicAdd(p.sks + t, 1);
     __syncthreads();
-    const int arrival = sk_arrival;
-    f32x4_t* const park = reinterpret_cast<f32x4_t*>(p.skw) + static_cast<long>(t) * ksp * PSZ + tid;
-    if (arrival < ksp - 1) {
+    const bool traffic = p.skdiag != 1;
+    const __amdgpu_buffer_rsrc_t park =
+        __builtin_amdgcn_make_buffer_rsrc(p.skw + static_cast<long>(t) * 2 * PSZ * 4, 0, 2 * PSZ * 16, 0x00020000);
+    constexpr int SC1 = 16;  // cache policy: agent coherent
+    if (sk_arrival == 0) {
+      if (traffic) {
 #pragma unroll
-      for (int i = 0; i < MFR; ++i)
+        for (int i = 0; i < MFR; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) park[ks * PSZ + (i * 4 + j) * 512] = acc[i][j];
-      __threadfence();  // release: the partial is visible device-wide before the ready count moves
+          for (int j = 0; j < 4; ++j)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(ai4e_conv::u32x4_t, acc[i][j]), park,
+                                                   ((ks * PSZ + (i * 4 + j) * 512 + tid) * 16), 0, SC1);
+      }
+      wait_vmcnt<0>();  // this thread's partial has reached the coherence point
       __syncthreads();
       if (tid == 0) atomicAdd(p.sks + ntl + t, 1);
       return;
     }
     if (tid == 0) {
-      while (__hip_atomic_load(p.sks + ntl + t, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < ksp - 1)
+      while (__hip_atomic_load(p.sks + ntl + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < 1)
         __builtin_amdgcn_s_sleep(2);
       __hip_atomic_store(p.sks + t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(p.sks + ntl + t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
-    __threadfence();  // acquire for every thread of the workgroup
+    if (traffic) {
+      // two accumulator rows (8 loads) in flight at a time: all of them at once spills the 256-pixel tile
 #pragma unroll
-    for (int i = 0; i < MFR; ++i)
+      for (int i = 0; i < MFR; i += 2) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        f32x4_t v = ks == 0 ? acc[i][j] : park[(i * 4 + j) * 512];
-        for (int q = 1; q < ksp; ++q) v += q == ks ? acc[i][j] : park[q * PSZ + (i * 4 + j) * 512];
-        acc[i][j] = v;
+        for (int ii = i; ii < i + 2 && ii < MFR; ++ii)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[ii][j] += __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(
+                                                          park, ((1 - ks) * PSZ + (ii * 4 + j) * 512 + tid) * 16, 0, SC1));
+        __builtin_amdgcn_sched_barrier(0);
       }
+    }
   }
 
   // ---- epilogue, one pixel group at a time: fp32 [WROWS][256] tile in LDS (16-B chunk index
@@ -1146,10 +1159,17 @@ int launch256(const ConvParams& p0, hipStream_t s) {
   p.zero = zero_chunk_ptr();
   if (!p.zero) return AI4E_ELAUNCH;
   const unsigned dyn = p.hy ? 16u * 512u : 0u;  // the fused head's weights
-  if (p.KH == 1 && p.KW == 1 && p.pad == 0)
+  const bool pw = p.KH == 1 && p.KW == 1 && p.pad == 0;
+  if (p.ksplit > 1) {
+    if (pw)
+      hipLaunchKernelGGL((conv_igemm256_kernel<GATHER_POINTWISE, BM, F16, PH3, true>), dim3(nb), dim3(512), dyn, s, p);
+    else
+      hipLaunchKernelGGL((conv_igemm256_kernel<GATHER_TAP, BM, F16, PH3, true>), dim3(nb), dim3(512), dyn, s, p);
+  } else if (pw) {
     hipLaunchKernelGGL((conv_igemm256_kernel<GATHER_POINTWISE, BM, F16, PH3>), dim3(nb), dim3(512), dyn, s, p);
-  else
+  } else {
     hipLaunchKernelGGL((conv_igemm256_kernel<GATHER_TAP, BM, F16, PH3>), dim3(nb), dim3(512), dyn, s, p);
+  }
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
 }
 
@@ -1198,7 +1218,9 @@ int conv2d_impl(const void* x, const void* w, const void* bias, const void* res,
   }
   if (ksplit > 1) {
     // split-K: the 256-wide configs, plain epilogue (no GroupNorm statistics, no fused head), >= 1 K tile per split
-    if (ksplit > 4 || !skw || !sks || hy || !(tile_cfg == 6 || tile_cfg == 9 || tile_cfg == 10) || Kpad / 64 < ksplit)
+    p.skdiag = ksplit >> 8;  // diagnostic hand-off variant (timing only)
+    ksplit &= 255;
+    if (ksplit != 2 || !skw || !sks || hy || !(tile_cfg == 6 || tile_cfg == 9 || tile_cfg == 10) || Kpad / 64 < ksplit)
       return AI4E_EINVAL;
     p.ksplit = ksplit;
     p.skw = static_cast<float*>(skw);
@@ -1281,7 +1303,7 @@ AI4E_API int ai4e_conv2d_head_fwd(const void* x, const void* w, const void* bias
                             ycoff, ldres, relu, tile_cfg, nullptr, 0, stream, hw, hw_ld, hb, head);
 }
 
-// Same conv with split-K over ksplit (2..4) workgroups per output tile, for grids too small to fill the chip (a 256-wide
+// Same conv with split-K over ksplit (= 2) workgroups per output tile, for grids too small to fill the chip (a 256-wide
 // tile config 6, 9 or 10; e.g. ResNet-50 layer4's 3x3 convs: 128 tiles of K = 4608 -> 256 workgroups of 2304).
 // skw: fp32 workspace of tiles * ksplit * BM * 256 floats (BM = 256 for config 6, else 192; tiles =
 // ceil(M / BM) * ceil(Kout / 256)); sks: 2 * tiles int32, zero at launch (the launch leaves them zero again).

@@ -135,11 +135,12 @@ SPLITK_CASES = [
 ]
 
 
-@pytest.mark.parametrize("ks", [2, 3, 4])
+@pytest.mark.parametrize("ks", [2])
 @pytest.mark.parametrize("tile", [6, 9, 10])
 @pytest.mark.parametrize("case", SPLITK_CASES)
 def test_conv_splitk(case, tile, ks):
-    """Split-K over ks workgroups per output tile (arrival-ordered hand-off through the fp32 park) vs fp32."""
+    """Split-K over two workgroups per output tile (arrival-ordered hand-off through the fp32 park) vs fp32, and
+    bit-identical on a second launch (the counters were left zero; either split may arrive last)."""
     n, h, w, cin, cout, k, s, p = case
     torch.manual_seed(11)
     wt = torch.randn(cout, cin, k, k) / (cin * k * k) ** 0.5
