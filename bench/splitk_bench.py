@@ -22,6 +22,18 @@ SHAPES = [
     ("l4_c3", 512, 2048, 1, 1, 0, 7, 7, True),
     ("l4_down", 1024, 2048, 1, 2, 0, 14, 14, False),
     ("l3_c1", 1024, 256, 1, 1, 0, 14, 14, False),
+    ("l2_down", 256, 512, 1, 2, 0, 56, 56, False),
+    ("l3_down", 512, 1024, 1, 2, 0, 28, 28, False),
+    ("l4_c1_first", 1024, 512, 1, 1, 0, 14, 14, False),
+    ("l2_c1_first", 256, 128, 1, 1, 0, 56, 56, False),
+    # the detector's backbone / FPN (batch 32 at 640^2) and the U-Net's deepest level (16 tiles of 512^2)
+    ("det_l4_c2_s2", 512, 512, 3, 2, 1, 40, 40, False, 32),
+    ("det_l4_c2", 512, 512, 3, 1, 1, 20, 20, False, 32),
+    ("det_fpn_p4", 256, 256, 3, 1, 1, 40, 40, False, 32),
+    ("det_fpn_p5", 256, 256, 3, 1, 1, 20, 20, False, 32),
+    ("det_lat_c4", 1024, 256, 1, 1, 0, 40, 40, True, 32),
+    ("unet_l4", 512, 512, 3, 1, 1, 32, 32, False, 16),
+    ("unet_l3", 512, 512, 3, 1, 1, 64, 64, False, 16),
 ]
 CFGS = [6, 9, 10, 6 | 2 << 4, 9 | 2 << 4, 10 | 2 << 4]
 
@@ -32,9 +44,10 @@ def main():
     only = set(os.environ["SPLITK_LAYERS"].split(",")) if os.environ.get("SPLITK_LAYERS") else None
     dev = torch.device("cuda:0")
     torch.manual_seed(0)
-    for name, cin, cout, k, s, p, h, w, res in SHAPES:
+    for name, cin, cout, k, s, p, h, w, res, *nb in SHAPES:
         if only and name not in only:
             continue
+        B = nb[0] if nb else int(os.environ.get("B", "250"))
         wt = torch.randn(cout, cin, k, k) / (cin * k * k) ** 0.5
         pc = pack_conv(wt, torch.randn(cout) * 0.1, stride=s, pad=p).to(dev)
         x = torch.randn(B, h, w, pc.cin_pad, device=dev).bfloat16()

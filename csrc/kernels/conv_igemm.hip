@@ -901,7 +901,7 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
 #pragma unroll
           for (int j = 0; j < 4; ++j)
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(ai4e_conv::u32x4_t, acc[i][j]), park,
-                                                   ((ks * PSZ + (i * 4 + j) * 512 + tid) * 16), 0, SC1);
+                                                   (ks * PSZ + tid) * 16, (i * 4 + j) * 512 * 16, SC1);
       }
       wait_vmcnt<0>();  // this thread's partial has reached the coherence point
       __syncthreads();
@@ -916,15 +916,17 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
     }
     __syncthreads();
     if (traffic) {
-      // two accumulator rows (8 loads) in flight at a time: all of them at once spills the 256-pixel tile
+      // two accumulator rows (8 loads) in flight at a time (the offsets of a row in SGPRs: VGPR offsets spilled
+      // the 256-pixel tile)
+      constexpr int RB = 2;
 #pragma unroll
-      for (int i = 0; i < MFR; i += 2) {
+      for (int i = 0; i < MFR; i += RB) {
 #pragma unroll
-        for (int ii = i; ii < i + 2 && ii < MFR; ++ii)
+        for (int ii = i; ii < i + RB && ii < MFR; ++ii)
 #pragma unroll
           for (int j = 0; j < 4; ++j)
             acc[ii][j] += __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(
-                                                          park, ((1 - ks) * PSZ + (ii * 4 + j) * 512 + tid) * 16, 0, SC1));
+                                                          park, ((1 - ks) * PSZ + tid) * 16, (ii * 4 + j) * 512 * 16, SC1));
         __builtin_amdgcn_sched_barrier(0);
       }
     }
