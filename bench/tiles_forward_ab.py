@@ -5,7 +5,9 @@ box-to-box and run-to-run drift cancel (a single bench.py run varies by a few % 
     python bench/tiles_forward_ab.py MODEL TABLE_B [rounds 8] [replays 20]
 
 MODEL: resnet (batch 250 at 224^2), detector (batch 32 at 640^2) or unet (16 tiles of 512^2). TABLE_B: a JSON tile
-table (ops/conv_tiles.json format); A is the committed table. Prints one JSON line: median ms per forward of each,
+table (ops/conv_tiles.json format), or ``NAME=VALUE[,NAME=VALUE]`` module switches of ops/conv.py for B (e.g.
+``PAIR_X=1``, ``PAIR_TILE=64``: the values its environment variables would set; ``net.par_down=1``: a model
+attribute); A is the committed state. Prints one JSON line: median ms per forward of each,
 B / A, and the largest output difference (split-K reorders fp32 sums only)."""
 import json
 import os
@@ -63,10 +65,20 @@ def main():
     net, x = build(model, dev)
     convmod._TILES = None
     ga, oa = capture(net, x)  # committed table
-    with open(table_b) as f:
-        convmod._TILES = json.load(f)
+    saved = {}
+    if table_b.endswith(".json"):
+        with open(table_b) as f:
+            convmod._TILES = json.load(f)
+    else:
+        for kv in table_b.split(","):
+            k, v = kv.split("=")
+            obj, k = (net, k[4:]) if k.startswith("net.") else (convmod, k)  # net.X: a model attribute
+            saved[(obj, k)] = getattr(obj, k)
+            setattr(obj, k, type(saved[(obj, k)])(int(v)))
     gb, ob = capture(net, x)
     convmod._TILES = None
+    for (obj, k), v in saved.items():
+        setattr(obj, k, v)
     ga.replay()
     gb.replay()
     torch.cuda.synchronize()
