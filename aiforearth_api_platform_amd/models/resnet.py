@@ -20,7 +20,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops.conv import (PackedConv, chain_supported, conv2d_nhwc, conv_chain, fold_bn, pack_conv, pack_stem_s2d,
-                        pair_route, pair_supported, stem_pool, stem_pool_c1)
+                        pair_route, pair_supported, stem_pool, stem_pool_c1, stem_pool_c1_u8, stem_u8_supported)
 from ..ops.head import softmax_topk
 from ..ops.pool import global_avgpool_nhwc, maxpool2d_nhwc, preprocess_s2d_u8, space_to_depth_shifted
 
@@ -172,6 +172,9 @@ class FusedResNet:
         self.fold_down = os.environ.get("AI4E_RESNET_FOLD_DOWN", "1") not in ("0", "off", "")
         # the first bottleneck's 1x1 c1 fused into the stem kernel (computed from the pooled tile in LDS)
         self.stem_c1 = os.environ.get("AI4E_STEM_C1", "1") not in ("0", "off", "")
+        # with the fused c1: the stem builds its input from the uint8 images itself (no preprocess launch, no s2d
+        # tensor; AI4E_STEM_U8=0: preprocess_s2d_u8 + the stem, the A/B reference)
+        self.stem_u8 = os.environ.get("AI4E_STEM_U8", "1") not in ("0", "off", "")
         # classifier FC on K1 (1x1 conv over the pooled features) by default: parity-or-better with hipBLASLt in
         # the captured forward (80.7/80.7k vs 81.3/80.9k images/s same-box A/B) and no library kernel left
         # stage entry: the downsample projection on a side stream, concurrent with the stage's first c1 (both read
@@ -358,7 +361,11 @@ class FusedResNet:
                     y = self._block(y, self.blocks[i], out=feats[n0:n0 + mb] if i == nblocks - 1 else None)
             y = feats
         elif self.chain:
-            y, t1 = self._stem_t1(pre(x))
+            if (preprocess is preprocess_s2d_u8 and self.stem_c1 and self.stem_u8
+                    and stem_u8_supported(x, self.stem, self.stages[0][0][0])):
+                y, t1 = stem_pool_c1_u8(x, self.stem, self.stages[0][0][0])  # preprocess inside the stem launch
+            else:
+                y, t1 = self._stem_t1(pre(x))
             return self._stages_chained(y, t1=t1)
         else:
             y, nblocks = self._stem(pre(x)), 0

@@ -38,6 +38,7 @@ _SIGS = {
     "ai4e_stem_pool_c1_f16_fwd": [_vp] * 7 + [_c_int] * 5 + [_vp],
     "ai4e_stem_pool_fwd": [_vp] * 4 + [_c_int] * 5 + [_vp],
     "ai4e_stem_pool_c1_fwd": [_vp] * 7 + [_c_int] * 5 + [_vp],
+    "ai4e_stem_pool_c1_u8_fwd": [_vp] * 3 + [_c_float] + [_vp] * 6 + [_c_int] * 5 + [_vp],
     "ai4e_stem_stamps_read": [_vp],
     "ai4e_chain_stamps_read": [_vp],
     "ai4e_k256_stamps_read": [_vp],  # (AI4E_K256_STAMPS diagnostic builds only)

@@ -503,6 +503,37 @@ def stem_pool(x: torch.Tensor, pc: PackedConv, variant: int = -1) -> torch.Tenso
     return y
 
 
+def stem_u8_supported(img: torch.Tensor, pc: PackedConv, c1: PackedConv) -> bool:
+    """Shapes ``stem_pool_c1_u8`` runs as ONE launch from the uint8 images (else: preprocess + ``stem_pool_c1``)."""
+    return (_ext.backend_for(img) == "hip" and img.dtype == torch.uint8 and img.dim() == 4 and img.shape[-1] == 3
+            and img.shape[1] % 2 == 0 and img.shape[2] % 2 == 0 and img.is_contiguous() and pc.cout == 64
+            and (pc.kh, pc.kw, pc.pad, pc.pad_hi) == (4, 4, 1, 2) and pc.cin_pad == 16
+            and (c1.kh, c1.kw, c1.stride, c1.pad, c1.cin_pad, c1.cout) == (1, 1, 1, 0, 64, 64) and STEM_VARIANT == 0
+            and pc.w_packed.dtype == torch.bfloat16 and c1.w_packed.dtype == torch.bfloat16
+            and _ext.has("ai4e_stem_pool_c1_u8_fwd"))
+
+
+def stem_pool_c1_u8(img: torch.Tensor, pc: PackedConv, c1: PackedConv, mean=None, std=None, scale: float = 1.0 / 255.0):
+    """``stem_pool_c1(preprocess_s2d_u8(img, mean, std, scale), pc, c1)`` in ONE launch: the direct stem kernel builds
+    its input footprint from the uint8 RGB images (the same normalization arithmetic, so the result is identical),
+    and the normalized space-to-depth tensor (100 MB bf16 at batch 250) is never written or read."""
+    from .pool import IMAGENET_MEAN, IMAGENET_STD, ctypes_floats, preprocess_s2d_u8
+    mean = IMAGENET_MEAN if mean is None else mean
+    std = IMAGENET_STD if std is None else std
+    if not stem_u8_supported(img, pc, c1):
+        return stem_pool_c1(preprocess_s2d_u8(img, mean, std, scale), pc, c1)
+    import ctypes
+    n, h, w, _ = img.shape
+    ph, pw = (h // 2 - 1) // 2 + 1, (w // 2 - 1) // 2 + 1
+    y = torch.empty(n, ph, pw, 64, device=img.device, dtype=torch.bfloat16)
+    t1 = torch.empty(n, ph, pw, 64, device=img.device, dtype=torch.bfloat16)
+    ma, sa = ctypes_floats(list(mean)[:3]), ctypes_floats(list(std)[:3])
+    _ext.call("ai4e_stem_pool_c1_u8_fwd", img.data_ptr(), ctypes.addressof(ma), ctypes.addressof(sa), scale,
+              pc.w_packed.data_ptr(), pc.bias.data_ptr(), y.data_ptr(), c1.w_packed.data_ptr(), c1.bias.data_ptr(),
+              t1.data_ptr(), c1.kpad, n, h, w, pc.kpad, _ext.stream_ptr(img.device))
+    return y, t1
+
+
 def stem_pool_c1(x: torch.Tensor, pc: PackedConv, c1: PackedConv):
     """K1s followed by the first bottleneck's 1x1 c1 (64 -> 64, + bias, ReLU) computed from the pooled tile
     while it is still in LDS: returns ``(y, relu(c1(y)))`` from ONE launch (no re-read of y). Other backends /

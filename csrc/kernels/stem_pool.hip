@@ -43,6 +43,12 @@ struct StemParams {
   const float* b1;
   uint16_t* t1;
   int kpad1;
+  // U8 (direct kernel): the footprint is built from the uint8 RGB images [N, 2H, 2W, 3] instead of the s2d tensor:
+  // s2d channel (dy * 2 + dx) * 3 + c of pixel (i, j) = (x8[2i + dy - 1, 2j + dx - 1, c] * scale - mean_c) * istd_c
+  // (zero outside the image), exactly the preprocess_s2d_kernel's arithmetic, so the preprocess launch and its
+  // 100 MB bf16 round trip disappear
+  const uint8_t* x8;
+  float pm[3], pis[3], pscale;
 };
 
 typedef unsigned short u16x2_t __attribute__((ext_vector_type(2)));
@@ -227,7 +233,7 @@ __device__ unsigned long long g_stem_stamps[2048 * 4 * STEM_NSEG];
   } while (0)
 #endif
 
-template <bool C1 = false, bool F16 = false>
+template <bool C1 = false, bool F16 = false, bool U8 = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void stem_pool_direct_kernel(const StemParams p, int ntiles) {
 #if AI4E_STEM_STAMPS
@@ -285,7 +291,71 @@ void stem_pool_direct_kernel(const StemParams p, int ntiles) {
              sb + D_FP + (wave + 4 * q) * 1024);
     }
   };
-  if (static_cast<int>(blockIdx.x) < ntiles) issue_fp(blockIdx.x);
+  // U8: the footprint slots from the uint8 images, one byte load per s2d channel (s2d channel k = 8 * plane + e of
+  // footprint pixel (ih, iw) is byte c of image pixel (2 ih + dy - 1, 2 iw + dx - 1), (dy * 2 + dx) * 3 + c = k), then
+  // normalized, packed and written with 16-B LDS stores at the slot the DMA would have filled. Loaded and written in
+  // one go after the epilogue (accumulators dead, footprint free): bytes held in registers across the epilogue, as
+  // the DMA form's prefetch distance would need, spill (24 VGPRs over the 250 the kernel uses)
+  auto build_fp8 = [&](int tt) __attribute__((always_inline)) {
+    const int im = tt / per_img;
+    const int r0 = (tt - im * per_img) / p.tiles_c;
+    const int c0 = tt - im * per_img - r0 * p.tiles_c;
+    const int oh = 2 * r0 * SP_TR - 1, ow = 2 * c0 * SP_TC - 1;
+    const int H8 = 2 * p.H, W8 = 2 * p.W;
+    const uint8_t* const xs = p.x8 + static_cast<long>(im) * H8 * W8 * 3;
+    uint32_t u8r[FP_DMA][8];
+    int u8m[FP_DMA], u8h[FP_DMA];
+    // an opaque zero: the slot geometry below is loop-invariant, and hoisted out of the persistent loop it stays live
+    // across the MFMA loop and spills; recomputed per tile it costs a few VALU ops
+    int opq;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(opq));
+#pragma unroll
+    for (int q = 0; q < FP_DMA; ++q) {
+      const int s = (wave + 4 * q) * 64 + lane + opq;
+      const int h = s >= FP_STRIDE ? 1 : 0, pix = s - h * FP_STRIDE;
+      const int a = pix / FP_C, b = pix - a * FP_C;
+      const int ih = oh - 1 + a, iw = ow - 1 + b;
+      const bool ok = s < FP_SLOTS && pix < FP_PIX && b < SP_RC + 3 && static_cast<unsigned>(ih) < static_cast<unsigned>(p.H) &&
+                      static_cast<unsigned>(iw) < static_cast<unsigned>(p.W);
+      // byte offsets of image rows 2 ih - 1 (o0) and 2 ih (o1) at pixel 2 iw - 1. Plane 0 (channels 0-7) = row o0
+      // bytes 0-5, row o1 bytes 0-1; plane 1 (channels 8-11) = row o1 bytes 2-5: so e < 6 reads ra + e with ra = o0
+      // (plane 0) or o1 + 2 (plane 1), e = 6, 7 read o1 + e - 6 (plane 0 only)
+      const int o0 = ((2 * ih - 1) * W8 + 2 * iw - 1) * 3, o1 = o0 + 3 * W8;
+      const int ra = h ? o1 + 2 : o0;
+      const bool y0 = ih > 0, x0 = iw > 0;  // row 2 ih - 1 / pixel 2 iw - 1 inside the image (2 ih, 2 iw always are)
+      int m = 0;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int k = 8 * h + e, blk = k / 3;
+        const bool v = ok && k < 12 && ((blk >> 1) || y0) && ((blk & 1) || x0);
+        // unconditional loads (a masked-off byte reads the image's first byte): a conditional load becomes a branch
+        // per byte with its own wait
+        const int off = v ? (e < 6 ? ra + e : o1 + e - 6) : 0;
+        u8r[q][e] = xs[off];
+        m |= v ? 1 << e : 0;
+      }
+      u8m[q] = m;
+      u8h[q] = h;
+    }
+#pragma unroll
+    for (int q = 0; q < FP_DMA; ++q) {
+      const int h = u8h[q];
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int c = (8 * h + e) % 3;
+        const float mc = c == 0 ? p.pm[0] : c == 1 ? p.pm[1] : p.pm[2];
+        const float ic = c == 0 ? p.pis[0] : c == 1 ? p.pis[1] : p.pis[2];
+        v[e] = (u8m[q] >> e) & 1 ? (static_cast<float>(u8r[q][e]) * p.pscale - mc) * ic : 0.f;
+      }
+      *reinterpret_cast<uint4*>(dsm + D_FP + (wave + 4 * q) * 1024 + 16 * (lane + opq)) =
+          make_uint4(pack2<F16>(v[0], v[1]), pack2<F16>(v[2], v[3]), pack2<F16>(v[4], v[5]), pack2<F16>(v[6], v[7]));
+    }
+  };
+  if (static_cast<int>(blockIdx.x) < ntiles) {
+    if constexpr (U8) build_fp8(blockIdx.x);
+    else issue_fp(blockIdx.x);
+  }
 
   for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
     const int img = t / per_img;
@@ -331,7 +401,7 @@ void stem_pool_direct_kernel(const StemParams p, int ntiles) {
     }
     STEM_STAMP(1);  // MFMA loop
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // every wave finished reading the footprint
-    if (t + static_cast<int>(gridDim.x) < ntiles) issue_fp(t + gridDim.x);
+    if (!U8 && t + static_cast<int>(gridDim.x) < ntiles) issue_fp(t + gridDim.x);
     STEM_STAMP(2);  // barrier + next footprint DMA issue
     // epilogue: bf16 relu(acc + b) -> tile [256 px][64 ch] (ptile layout)
 #pragma unroll
@@ -351,6 +421,9 @@ void stem_pool_direct_kernel(const StemParams p, int ntiles) {
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    // U8: the next tile's footprint, built here where the accumulators are dead (the MFMA loop's last footprint
+    // read is behind the barrier above it)
+    if (U8 && t + static_cast<int>(gridDim.x) < ntiles) build_fp8(t + gridDim.x);
     STEM_STAMP(3);  // epilogue tile writes + barrier
     // fused c1 operands, issued now so the L2 latency hides under the pooling: W1 fragments (output-channel
     // rows 16j + lane&15, k-chunk lane>>4 of k-step ks; 8 KB, L2-resident) and the bias
@@ -447,11 +520,11 @@ void stem_pool_direct_kernel(const StemParams p, int ntiles) {
 #endif
 }
 
-template <bool C1 = false, bool F16 = false>
+template <bool C1 = false, bool F16 = false, bool U8 = false>
 int launch_direct(const StemParams& p, long nb, hipStream_t stream) {
   static bool attr = false;
   if (!attr) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(stem_pool_direct_kernel<C1, F16>),
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(stem_pool_direct_kernel<C1, F16, U8>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, D_LDS) != hipSuccess)
       return AI4E_ELAUNCH;
     attr = true;
@@ -467,7 +540,7 @@ int launch_direct(const StemParams& p, long nb, hipStream_t stream) {
     return v < 1 ? 1L : v;
   }();
   const long grid = nb < wpc * cus ? nb : wpc * cus;
-  hipLaunchKernelGGL((stem_pool_direct_kernel<C1, F16>), dim3(static_cast<unsigned>(grid)), dim3(256), D_LDS, stream, p,
+  hipLaunchKernelGGL((stem_pool_direct_kernel<C1, F16, U8>), dim3(static_cast<unsigned>(grid)), dim3(256), D_LDS, stream, p,
                      static_cast<int>(nb));
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
 }
@@ -514,6 +587,41 @@ int stem_c1(bool f16, const void* x, const void* w, const void* bias, void* y, c
   return f16 ? launch_direct<true, true>(p, nb, stream) : launch_direct<true>(p, nb, stream);
 }
 }  // namespace
+
+// The same from uint8 RGB images [N, H8, W8, 3] (H8, W8 even; the s2d stem input is their normalized 2x2 space-to-depth,
+// built in the kernel: mean3 / std3 / scale as ai4e_preprocess_s2d_u8), bf16. y, t1: [N, ceil(H8/4), ceil(W8/4), 64].
+AI4E_API int ai4e_stem_pool_c1_u8_fwd(const void* x8, const float* mean3, const float* std3, float scale, const void* w,
+                                      const void* bias, void* y, const void* w1, const void* b1, void* t1, int kpad1,
+                                      int N, int H8, int W8, int kpad, hipStream_t stream) {
+  if (!x8 || !mean3 || !std3 || !w || !bias || !y || !w1 || !b1 || !t1 || kpad < 256 || kpad % 8 || kpad1 < 64 ||
+      kpad1 % 8 || H8 <= 0 || W8 <= 0 || (H8 & 1) || (W8 & 1))
+    return AI4E_EINVAL;
+  StemParams p{};
+  p.x8 = static_cast<const uint8_t*>(x8);
+  for (int c = 0; c < 3; ++c) {
+    p.pm[c] = mean3[c];
+    p.pis[c] = 1.f / std3[c];  // as the preprocess launcher: the same fp32 reciprocal
+  }
+  p.pscale = scale;
+  p.w = static_cast<const uint16_t*>(w);
+  p.bias = static_cast<const float*>(bias);
+  p.y = static_cast<uint16_t*>(y);
+  p.zero = stem_zero_ptr();
+  if (!p.zero) return AI4E_ELAUNCH;
+  p.w1 = static_cast<const uint16_t*>(w1);
+  p.b1 = static_cast<const float*>(b1);
+  p.t1 = static_cast<uint16_t*>(t1);
+  p.kpad1 = kpad1;
+  p.H = H8 / 2; p.W = W8 / 2;
+  p.PH = (p.H - 1) / 2 + 1;
+  p.PW = (p.W - 1) / 2 + 1;
+  p.kpad = kpad;
+  p.tiles_r = ai4e_cdiv(p.PH, SP_TR);
+  p.tiles_c = ai4e_cdiv(p.PW, SP_TC);
+  const long nb = static_cast<long>(N) * p.tiles_r * p.tiles_c;
+  if (nb <= 0) return AI4E_OK;
+  return launch_direct<true, false, true>(p, nb, stream);
+}
 
 AI4E_API int ai4e_stem_pool_c1_fwd(const void* x, const void* w, const void* bias, void* y, const void* w1,
                                    const void* b1, void* t1, int kpad1, int N, int H, int W, int kpad,

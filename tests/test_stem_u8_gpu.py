@@ -1,0 +1,60 @@
+"""The uint8-input stem (K1s building its input footprint from the RGB images: preprocess fused into the stem launch)
+against the two-launch path it replaces (preprocess_s2d_u8 + stem_pool_c1), and the stem against an fp32 PyTorch
+reference of conv 7x7/2 + ReLU + max-pool 3x3/2 + the fused 1x1 (GPU box only)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+from aiforearth_api_platform_amd.ops import _ext
+from aiforearth_api_platform_amd.ops.conv import pack_conv, pack_stem_s2d, stem_pool_c1, stem_pool_c1_u8, stem_u8_supported
+from aiforearth_api_platform_amd.ops.pool import IMAGENET_MEAN, IMAGENET_STD, preprocess_s2d_u8
+
+DEV = "cuda"
+
+
+@pytest.fixture(autouse=True, scope="module")
+def _lib():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from aiforearth_api_platform_amd import _build
+    _build.build_kernels()
+    _ext.lib()
+
+
+def _stem(seed=0):
+    g = torch.Generator().manual_seed(seed)
+    w7 = torch.randn(64, 3, 7, 7, generator=g) / 12
+    b = torch.randn(64, generator=g) * 0.1
+    w1 = torch.randn(64, 64, 1, 1, generator=g) / 8
+    b1 = torch.randn(64, generator=g) * 0.1
+    return w7, b, pack_stem_s2d(w7, b).to(DEV), w1, b1, pack_conv(w1, b1).to(DEV)
+
+
+@pytest.mark.parametrize("shape", [(250, 224, 224), (3, 64, 96), (2, 30, 46), (1, 226, 222)])
+def test_stem_u8_matches_two_launch_path(shape):
+    n, h, w = shape
+    _, _, pc, _, _, c1 = _stem()
+    img = torch.randint(0, 256, (n, h, w, 3), dtype=torch.uint8, device=DEV)
+    assert stem_u8_supported(img, pc, c1)
+    y, t1 = stem_pool_c1_u8(img, pc, c1)
+    y_ref, t1_ref = stem_pool_c1(preprocess_s2d_u8(img), pc, c1)
+    torch.cuda.synchronize()
+    assert torch.equal(y, y_ref)  # the same normalization arithmetic, the same footprint values
+    assert torch.equal(t1, t1_ref)
+
+
+def test_stem_u8_vs_fp32_reference():
+    w7, b, pc, w1, b1, c1 = _stem(1)
+    img = torch.randint(0, 256, (2, 64, 96, 3), dtype=torch.uint8, device=DEV)
+    y, t1 = stem_pool_c1_u8(img, pc, c1)
+    x = (img.float() / 255 - torch.tensor(IMAGENET_MEAN, device=DEV)) / torch.tensor(IMAGENET_STD, device=DEV)
+    xq = x.to(torch.bfloat16).float().permute(0, 3, 1, 2)
+    wq = w7.to(torch.bfloat16).float().to(DEV)
+    ref = F.max_pool2d(F.relu(F.conv2d(xq, wq, b.to(DEV), stride=2, padding=3)), 3, 2, 1)
+    ref1 = F.relu(F.conv2d(ref.to(torch.bfloat16).float(), w1.to(torch.bfloat16).float().to(DEV), b1.to(DEV)))
+    ref = ref.permute(0, 2, 3, 1)
+    ref1 = ref1.permute(0, 2, 3, 1)
+    assert (y.float() - ref).abs().max().item() <= 0.03 * ref.abs().max().item() + 0.03
+    assert (t1.float() - ref1).abs().max().item() <= 0.03 * ref1.abs().max().item() + 0.03
