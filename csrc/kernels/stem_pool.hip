@@ -45,8 +45,8 @@ struct StemParams {
   int kpad1;
   // U8 (direct kernel): the footprint is built from the uint8 RGB images [N, 2H, 2W, 3] instead of the s2d tensor:
   // s2d channel (dy * 2 + dx) * 3 + c of pixel (i, j) = (x8[2i + dy - 1, 2j + dx - 1, c] * scale - mean_c) * istd_c
-  // (zero outside the image), exactly the preprocess_s2d_kernel's arithmetic, so the preprocess launch and its
-  // 100 MB bf16 round trip disappear
+  // (zero outside the image), the preprocess_s2d_kernel's arithmetic, so the preprocess launch and its 100 MB bf16
+  // round trip disappear; pixels i = H / j = W are built as well (the exact 7x7/2 conv at the bottom / right edge)
   const uint8_t* x8;
   float pm[3], pis[3], pscale;
 };
@@ -315,8 +315,11 @@ void stem_pool_direct_kernel(const StemParams p, int ntiles) {
       const int h = s >= FP_STRIDE ? 1 : 0, pix = s - h * FP_STRIDE;
       const int a = pix / FP_C, b = pix - a * FP_C;
       const int ih = oh - 1 + a, iw = ow - 1 + b;
-      const bool ok = s < FP_SLOTS && pix < FP_PIX && b < SP_RC + 3 && static_cast<unsigned>(ih) < static_cast<unsigned>(p.H) &&
-                      static_cast<unsigned>(iw) < static_cast<unsigned>(p.W);
+      // s2d pixels 0..H (W): pixel H holds image rows 2H - 1 (real) and 2H (outside), so the last image row / column
+      // reaches the conv's last output row / column as in the 7x7/2 conv (the [N, H/2, W/2, 16] s2d tensor of the
+      // two-launch path ends at pixel H - 1 and leaves image row / column 2H - 1 out)
+      const bool ok = s < FP_SLOTS && pix < FP_PIX && b < SP_RC + 3 && static_cast<unsigned>(ih) <= static_cast<unsigned>(p.H) &&
+                      static_cast<unsigned>(iw) <= static_cast<unsigned>(p.W);
       // byte offsets of image rows 2 ih - 1 (o0) and 2 ih (o1) at pixel 2 iw - 1. Plane 0 (channels 0-7) = row o0
       // bytes 0-5, row o1 bytes 0-1; plane 1 (channels 8-11) = row o1 bytes 2-5: so e < 6 reads ra + e with ra = o0
       // (plane 0) or o1 + 2 (plane 1), e = 6, 7 read o1 + e - 6 (plane 0 only)

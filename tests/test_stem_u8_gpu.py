@@ -41,13 +41,17 @@ def test_stem_u8_matches_two_launch_path(shape):
     y, t1 = stem_pool_c1_u8(img, pc, c1)
     y_ref, t1_ref = stem_pool_c1(preprocess_s2d_u8(img), pc, c1)
     torch.cuda.synchronize()
-    assert torch.equal(y, y_ref)  # the same normalization arithmetic, the same footprint values
-    assert torch.equal(t1, t1_ref)
+    # the same normalization arithmetic, the same footprint values: bit-identical except the last pooled rows and
+    # columns (one, or two for odd H/2), where the two-launch path's [N, H/2, W/2, 16] s2d tensor leaves the image's
+    # last row / column out (the fp32 test below checks the edge against the 7x7/2 conv)
+    assert torch.equal(y[:, :-2, :-2], y_ref[:, :-2, :-2])
+    assert torch.equal(t1[:, :-2, :-2], t1_ref[:, :-2, :-2])
 
 
-def test_stem_u8_vs_fp32_reference():
+@pytest.mark.parametrize("shape", [(2, 64, 96), (3, 224, 224), (1, 30, 46)])
+def test_stem_u8_vs_fp32_reference(shape):
     w7, b, pc, w1, b1, c1 = _stem(1)
-    img = torch.randint(0, 256, (2, 64, 96, 3), dtype=torch.uint8, device=DEV)
+    img = torch.randint(0, 256, (*shape, 3), dtype=torch.uint8, device=DEV)
     y, t1 = stem_pool_c1_u8(img, pc, c1)
     x = (img.float() / 255 - torch.tensor(IMAGENET_MEAN, device=DEV)) / torch.tensor(IMAGENET_STD, device=DEV)
     xq = x.to(torch.bfloat16).float().permute(0, 3, 1, 2)
@@ -56,5 +60,6 @@ def test_stem_u8_vs_fp32_reference():
     ref1 = F.relu(F.conv2d(ref.to(torch.bfloat16).float(), w1.to(torch.bfloat16).float().to(DEV), b1.to(DEV)))
     ref = ref.permute(0, 2, 3, 1)
     ref1 = ref1.permute(0, 2, 3, 1)
-    assert (y.float() - ref).abs().max().item() <= 0.03 * ref.abs().max().item() + 0.03
-    assert (t1.float() - ref1).abs().max().item() <= 0.03 * ref1.abs().max().item() + 0.03
+    # every output, the bottom / right edge included (the exact 7x7/2, pad 3 conv)
+    assert (y.float() - ref).abs().max().item() <= 0.02 * ref.abs().max().item() + 0.02
+    assert (t1.float() - ref1).abs().max().item() <= 0.02 * ref1.abs().max().item() + 0.02
