@@ -57,9 +57,14 @@ def test_stem_u8_vs_fp32_reference(shape):
     xq = x.to(torch.bfloat16).float().permute(0, 3, 1, 2)
     wq = w7.to(torch.bfloat16).float().to(DEV)
     ref = F.max_pool2d(F.relu(F.conv2d(xq, wq, b.to(DEV), stride=2, padding=3)), 3, 2, 1)
-    ref1 = F.relu(F.conv2d(ref.to(torch.bfloat16).float(), w1.to(torch.bfloat16).float().to(DEV), b1.to(DEV)))
     ref = ref.permute(0, 2, 3, 1)
+    # every output, the bottom / right edge included (the exact 7x7/2, pad 3 conv): the edge is no worse than the
+    # interior (the two-launch path's s2d tensor leaves the image's last row / column out there)
+    err = (y.float() - ref).abs()
+    assert err.max().item() <= 0.02 * ref.abs().max().item() + 0.02
+    edge = torch.cat([err[:, -1].flatten(), err[:, :, -1].flatten()]).max().item()
+    assert edge <= max(2 * err[:, :-1, :-1].max().item(), 0.05), edge
+    # the fused 1x1 on the pooled tile == the 1x1 of the stored pooled values
+    ref1 = F.relu(F.conv2d(y.float().permute(0, 3, 1, 2), w1.to(torch.bfloat16).float().to(DEV), b1.to(DEV)))
     ref1 = ref1.permute(0, 2, 3, 1)
-    # every output, the bottom / right edge included (the exact 7x7/2, pad 3 conv)
-    assert (y.float() - ref).abs().max().item() <= 0.02 * ref.abs().max().item() + 0.02
-    assert (t1.float() - ref1).abs().max().item() <= 0.02 * ref1.abs().max().item() + 0.02
+    assert (t1.float() - ref1).abs().max().item() <= 0.01 * ref1.abs().max().item() + 0.02
