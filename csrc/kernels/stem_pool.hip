@@ -325,12 +325,13 @@ void stem_pool_direct_kernel(const StemParams p, int ntiles) {
       // (plane 0) or o1 + 2 (plane 1), e = 6, 7 read o1 + e - 6 (plane 0 only)
       const int o0 = ((2 * ih - 1) * W8 + 2 * iw - 1) * 3, o1 = o0 + 3 * W8;
       const int ra = h ? o1 + 2 : o0;
-      const bool y0 = ih > 0, x0 = iw > 0;  // row 2 ih - 1 / pixel 2 iw - 1 inside the image (2 ih, 2 iw always are)
+      // row 2 ih - 1 / 2 ih and pixel 2 iw - 1 / 2 iw inside the image (ih and iw run over 0..H / 0..W)
+      const bool y0 = ih > 0, y1 = ih < p.H, x0 = iw > 0, x1 = iw < p.W;
       int m = 0;
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const int k = 8 * h + e, blk = k / 3;
-        const bool v = ok && k < 12 && ((blk >> 1) || y0) && ((blk & 1) || x0);
+        const bool v = ok && k < 12 && ((blk >> 1) ? y1 : y0) && ((blk & 1) ? x1 : x0);
         // unconditional loads (a masked-off byte reads the image's first byte): a conditional load becomes a branch
         // per byte with its own wait
         const int off = v ? (e < 6 ? ra + e : o1 + e - 6) : 0;
