@@ -172,9 +172,11 @@ class FusedResNet:
         self.fold_down = os.environ.get("AI4E_RESNET_FOLD_DOWN", "1") not in ("0", "off", "")
         # the first bottleneck's 1x1 c1 fused into the stem kernel (computed from the pooled tile in LDS)
         self.stem_c1 = os.environ.get("AI4E_STEM_C1", "1") not in ("0", "off", "")
-        # with the fused c1: the stem builds its input from the uint8 images itself (no preprocess launch, no s2d
-        # tensor; AI4E_STEM_U8=0: preprocess_s2d_u8 + the stem, the A/B reference)
-        self.stem_u8 = os.environ.get("AI4E_STEM_U8", "1") not in ("0", "off", "")
+        # opt-in (AI4E_STEM_U8=1): the stem builds its input from the uint8 images itself (no preprocess launch, no
+        # s2d tensor, and the exact 7x7/2 conv at the bottom / right edge, which the [N, H/2, W/2, 16] s2d tensor of
+        # the default path leaves out), but its per-byte footprint loads cost more than they save: 3.306 vs 3.231 ms
+        # per forward, same process (profiles/r6_stem_u8/)
+        self.stem_u8 = os.environ.get("AI4E_STEM_U8", "0") not in ("0", "off", "")
         # classifier FC on K1 (1x1 conv over the pooled features) by default: parity-or-better with hipBLASLt in
         # the captured forward (80.7/80.7k vs 81.3/80.9k images/s same-box A/B) and no library kernel left
         # stage entry: the downsample projection on a side stream, concurrent with the stage's first c1 (both read
