@@ -107,7 +107,19 @@ struct PairParams {
 // (one store chunk and FI / NKC residual loads after each step's MFMAs) instead of a burst between the Y barrier and
 // the C phase: the stamps (profiles/r3_pair/) put 33 % of a wave's life in that burst (vector-memory issue backs up).
 // (Spreading the next pass's B weight fragments over the C steps as well was measured slower: profiles/r3_pair/.)
-template <int MID, int C4, int MIDN, int BM, bool KF = true, bool SP = false, bool F16 = false>
+// YW (bm_cfg 99): the Y epilogue pairs pixel fragments 16 rows apart with v_permlane16_swap (as the K1c chain's
+// patch-mode T2 epilogue), so each lane adds a 16-B residual chunk and writes one 16-B Y chunk per fragment pair
+// instead of 8 B per fragment.
+__device__ __forceinline__ void pswap16(f32x4_t& a, f32x4_t& b) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(a[q]), __float_as_uint(b[q]), false, false);
+    a[q] = __uint_as_float(r[0]);
+    b[q] = __uint_as_float(r[1]);
+  }
+}
+
+template <int MID, int C4, int MIDN, int BM, bool KF = true, bool SP = false, bool F16 = false, bool YW = false>
 __global__ __launch_bounds__(512) void conv_pair_kernel(const PairParams p) {
   constexpr int FI = BM / 16;            // pixel fragments
   constexpr int NKB = MID / 32;          // B K steps
@@ -164,10 +176,16 @@ __global__ __launch_bounds__(512) void conv_pair_kernel(const PairParams p) {
     return *reinterpret_cast<const bf16x8_t*>(w1l + (static_cast<long>((w * JC + j) * (C4 / 32) + pass * NKC + kc) << 9));
   };
   // residual of pass `pass` in the accumulator layout: pixel 16i + frow, channels 128 pass + 16 w + 4 lg .. +3
+  // (YW: in the swapped layout of fragment pair ip: pixel 32 ip + frow + 16 (lg & 1), channels 16 w + 8 (lg >> 1) ..
+  // +7, i.e. entries 0 .. FI/2 - 1)
+  static_assert(!YW || FI % 2 == 0, "YW: pairs of pixel fragments");
+  constexpr int FR = YW ? FI / 2 : FI;  // residual loads per pass
   const uint16_t* resl[FI];
 #pragma unroll
   for (int i = 0; i < FI; ++i)
-    resl[i] = p.res + static_cast<long>(min(m0 + 16 * i + frow, p.M - 1)) * C4 + 16 * w + 4 * lg;
+    resl[i] = YW ? p.res + static_cast<long>(min(m0 + 32 * (i % FR) + frow + 16 * (lg & 1), p.M - 1)) * C4 + 16 * w +
+                       8 * (lg >> 1)
+                 : p.res + static_cast<long>(min(m0 + 16 * i + frow, p.M - 1)) * C4 + 16 * w + 4 * lg;
 
   // T1' accumulators seeded with b1'
   f32x4_t accn[FI][JC];
@@ -184,8 +202,14 @@ __global__ __launch_bounds__(512) void conv_pair_kernel(const PairParams p) {
 #pragma unroll
   for (int k = 0; k < NKB; ++k) wb[k] = w3frag(0, k);
   uint2 rr[FI];
+  uint4 rr4[FR];
+  if constexpr (YW) {
 #pragma unroll
-  for (int i = 0; i < FI; ++i) rr[i] = *reinterpret_cast<const uint2*>(resl[i]);
+    for (int i = 0; i < FR; ++i) rr4[i] = *reinterpret_cast<const uint4*>(resl[i]);
+  } else {
+#pragma unroll
+    for (int i = 0; i < FI; ++i) rr[i] = *reinterpret_cast<const uint2*>(resl[i]);
+  }
 
   pbarrier();  // T2 tile visible
   PAIR_STAMP(0);
@@ -225,12 +249,24 @@ __global__ __launch_bounds__(512) void conv_pair_kernel(const PairParams p) {
 
     PAIR_STAMP(1);
     // ---- epilogue: + residual (registers), ReLU, bf16 -> Y chunk (LDS)
+    if constexpr (YW) {
 #pragma unroll
-    for (int i = 0; i < FI; ++i) {
-      const uint2 rv = rr[i];
-      *reinterpret_cast<uint2*>(ybuf + poff<BM>(16 * i + frow, 16 * w + 4 * lg)) =
-          make_uint2(pack_relu2<F16>(add_lo<F16>(rv.x, accb[i][0]), add_hi<F16>(rv.x, accb[i][1])),
-                     pack_relu2<F16>(add_lo<F16>(rv.y, accb[i][2]), add_hi<F16>(rv.y, accb[i][3])));
+      for (int ip = 0; ip < FR; ++ip) {
+        f32x4_t a = accb[2 * ip], b = accb[2 * ip + 1];
+        pswap16(a, b);
+        const int r = 32 * ip + frow + 16 * (lg & 1), n = 16 * w + 8 * (lg >> 1);
+        const float f[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+        *reinterpret_cast<uint4*>(ybuf + (n >> 5) * KBS + r * 64 + ((((n & 31) >> 3) ^ pswz(r)) << 4)) =
+            epilogue8<F16>(f, true, rr4[ip], true);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < FI; ++i) {
+        const uint2 rv = rr[i];
+        *reinterpret_cast<uint2*>(ybuf + poff<BM>(16 * i + frow, 16 * w + 4 * lg)) =
+            make_uint2(pack_relu2<F16>(add_lo<F16>(rv.x, accb[i][0]), add_hi<F16>(rv.x, accb[i][1])),
+                       pack_relu2<F16>(add_lo<F16>(rv.y, accb[i][2]), add_hi<F16>(rv.y, accb[i][3])));
+      }
     }
     pbarrier();  // Y chunk visible (and every wave is past the chunk buffer's previous readers)
     PAIR_STAMP(2);
@@ -250,7 +286,13 @@ __global__ __launch_bounds__(512) void conv_pair_kernel(const PairParams p) {
     };
     if constexpr (!SP) {
 #pragma unroll
-      for (int i = 0; i < FI; ++i) rr[i] = *reinterpret_cast<const uint2*>(resl[i] + pn * PR_CH);
+      for (int i = 0; i < FI; ++i) {
+        if constexpr (YW) {
+          if (i < FR) rr4[i] = *reinterpret_cast<const uint4*>(resl[i] + pn * PR_CH);
+        } else {
+          rr[i] = *reinterpret_cast<const uint2*>(resl[i] + pn * PR_CH);
+        }
+      }
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int e = 0; e < NS; ++e) copy_out(e);
@@ -276,11 +318,13 @@ __global__ __launch_bounds__(512) void conv_pair_kernel(const PairParams p) {
         for (int j = 0; j < JC; ++j)
           accn[i][j] = mfma_16x16x32<F16>(wc[k][j], fy[k & 1][i], accn[i][j]);
       if constexpr (SP) {
-        constexpr int RPS = (FI + NKC - 1) / NKC;  // residual loads per C step
+        constexpr int RPS = (FR + NKC - 1) / NKC;  // residual loads per C step
         if (k < NS) copy_out(k);
 #pragma unroll
-        for (int i = k * RPS; i < (k + 1) * RPS && i < FI; ++i)
-          rr[i] = *reinterpret_cast<const uint2*>(resl[i] + pn * PR_CH);
+        for (int i = k * RPS; i < (k + 1) * RPS && i < FR; ++i) {
+          if constexpr (YW) rr4[i] = *reinterpret_cast<const uint4*>(resl[i] + pn * PR_CH);
+          else rr[i] = *reinterpret_cast<const uint2*>(resl[i] + pn * PR_CH);
+        }
         static_assert(NS <= NKC, "one Y store chunk per C step");
       }
       if constexpr (KF) __builtin_amdgcn_sched_barrier(0);
@@ -316,17 +360,17 @@ __global__ __launch_bounds__(512) void conv_pair_kernel(const PairParams p) {
 #endif
 }
 
-template <int MID, int C4, int MIDN, int BM, bool KF = true, bool SP = false, bool F16 = false>
+template <int MID, int C4, int MIDN, int BM, bool KF = true, bool SP = false, bool F16 = false, bool YW = false>
 int launch_pair(const PairParams& p, hipStream_t s) {
   constexpr int LDS = (MID / 32 + 2 * PR_CH / 32 > MIDN / 32 ? MID / 32 + 2 * PR_CH / 32 : MIDN / 32) * kbs<BM>();
   static bool attr = false;
   if (!attr) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(conv_pair_kernel<MID, C4, MIDN, BM, KF, SP, F16>),
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(conv_pair_kernel<MID, C4, MIDN, BM, KF, SP, F16, YW>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, LDS) != hipSuccess)
       return AI4E_ELAUNCH;
     attr = true;
   }
-  hipLaunchKernelGGL((conv_pair_kernel<MID, C4, MIDN, BM, KF, SP, F16>), dim3(ai4e_cdiv(p.M, BM)), dim3(512), LDS, s, p);
+  hipLaunchKernelGGL((conv_pair_kernel<MID, C4, MIDN, BM, KF, SP, F16, YW>), dim3(ai4e_cdiv(p.M, BM)), dim3(512), LDS, s, p);
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
 }
 
@@ -394,6 +438,7 @@ AI4E_API int ai4e_conv_pair_fwd(const void* t2, const void* w3p, const void* b3,
       case 96: return launch_pair<256, 1024, 256, 96>(p, stream);  // A/B reference: the burst after the Y barrier
       case 64: return launch_pair<256, 1024, 256, 64>(p, stream);
       case 97: return launch_pair<256, 1024, 256, 96, false>(p, stream);  // A/B: scheduler-placed fragment reads
+      case 99: return launch_pair<256, 1024, 256, 96, true, true, false, true>(p, stream);  // spread + 16-B Y writes
       default: return AI4E_EINVAL;
     }
   }

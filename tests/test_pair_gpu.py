@@ -43,7 +43,22 @@ CASES = [
     (1, 5, 9, 128, 98, 256),
     (2, 7, 7, 512, 98),
     (1, 3, 5, 512, 98),
+    (8, 14, 14, 256, 99),     # 16-B Y writes (fragment pairs swapped with v_permlane16_swap)
+    (1, 5, 7, 256, 99),       # ... with a partial tile
 ]
+
+
+def test_conv_pair_yw_bit_identical():
+    """bm_cfg 99 (16-B Y writes) computes the same bits as the default spread schedule (98)."""
+    torch.manual_seed(12)
+    c3 = pack_conv(torch.randn(1024, 256, 1, 1) / 16, torch.randn(1024) * 0.1).to(DEV)
+    c1n = pack_conv(torch.randn(256, 1024, 1, 1) / 32, torch.randn(256) * 0.1).to(DEV)
+    t2 = torch.randn(9, 14, 14, 256, device=DEV).relu().to(torch.bfloat16)
+    res = torch.randn(9, 14, 14, 1024, device=DEV).to(torch.bfloat16)
+    a = conv_pair(t2, c3, res, c1n, tile_cfg=98)
+    b = conv_pair(t2, c3, res, c1n, tile_cfg=99)
+    torch.cuda.synchronize()
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
 
 
 @pytest.mark.parametrize("case", CASES)
