@@ -433,12 +433,13 @@ AI4E_API int ai4e_conv_pair_fwd(const void* t2, const void* w3p, const void* b3,
   if (M == 0) return AI4E_OK;
   if (mid == 256 && c4 == 1024 && midn == 256) {
     switch (bm_cfg) {
-      case 0:   // default: loads + stores spread over the C phase (profiles/r3_pair/)
-      case 98: return launch_pair<256, 1024, 256, 96, true, true>(p, stream);
+      case 0:   // default: loads + stores spread over the C phase (profiles/r3_pair/), 16-B Y writes (round 6:
+      case 99:  // -0.7 % of the serial forward, bit-identical, profiles/r6_pair_yw/)
+        return launch_pair<256, 1024, 256, 96, true, true, false, true>(p, stream);
+      case 98: return launch_pair<256, 1024, 256, 96, true, true>(p, stream);  // A/B reference: 8-B Y writes
       case 96: return launch_pair<256, 1024, 256, 96>(p, stream);  // A/B reference: the burst after the Y barrier
       case 64: return launch_pair<256, 1024, 256, 64>(p, stream);
       case 97: return launch_pair<256, 1024, 256, 96, false>(p, stream);  // A/B: scheduler-placed fragment reads
-      case 99: return launch_pair<256, 1024, 256, 96, true, true, false, true>(p, stream);  // spread + 16-B Y writes
       default: return AI4E_EINVAL;
     }
   }

@@ -49,7 +49,7 @@ CASES = [
 
 
 def test_conv_pair_yw_bit_identical():
-    """bm_cfg 99 (16-B Y writes) computes the same bits as the default spread schedule (98)."""
+    """bm_cfg 99 (16-B Y writes, the default) computes the same bits as the 8-B-write schedule (98)."""
     torch.manual_seed(12)
     c3 = pack_conv(torch.randn(1024, 256, 1, 1) / 16, torch.randn(1024) * 0.1).to(DEV)
     c1n = pack_conv(torch.randn(256, 1024, 1, 1) / 32, torch.randn(256) * 0.1).to(DEV)
