@@ -119,11 +119,7 @@ __device__ __forceinline__ void pswap16(f32x4_t& a, f32x4_t& b) {
   }
 }
 
-// PL (bm_cfg 100): the T2 tile's prologue copy walks one K block at a time (a wave writes 16 rows x 64 B of one block,
-// 1 KB contiguous) instead of along each 512-B input row across the 8 blocks, whose starts are 0 or 128 B mod 256:
-// the row-major walk put 4 lanes of a ds_write_b128 group on the same banks.
-template <int MID, int C4, int MIDN, int BM, bool KF = true, bool SP = false, bool F16 = false, bool YW = false,
-          bool PL = false>
+template <int MID, int C4, int MIDN, int BM, bool KF = true, bool SP = false, bool F16 = false, bool YW = false>
 __global__ __launch_bounds__(512) void conv_pair_kernel(const PairParams p) {
   constexpr int FI = BM / 16;            // pixel fragments
   constexpr int NKB = MID / 32;          // B K steps
@@ -155,27 +151,16 @@ __global__ __launch_bounds__(512) void conv_pair_kernel(const PairParams p) {
   {
     constexpr int N = BM * MID / 8 / 512;
     uint4 v[N];
-    // thread g -> (row r, 16-B chunk cq of the row): row-major, or (PL) block-major: chunk q = g & 3 of row
-    // (g >> 2) % BM in K block (g >> 2) / BM
-    auto rc = [&](int g, int& r, int& cq) __attribute__((always_inline)) {
-      if constexpr (PL) {
-        r = (g >> 2) % BM;
-        cq = (g >> 2) / BM * 4 + (g & 3);
-      } else {
-        r = g / (MID / 8);
-        cq = g % (MID / 8);
-      }
-    };
 #pragma unroll
     for (int e = 0; e < N; ++e) {
-      int r, cq;
-      rc(tid + 512 * e, r, cq);
+      const int g = tid + 512 * e;
+      const int r = g / (MID / 8), cq = g % (MID / 8);
       v[e] = *reinterpret_cast<const uint4*>(p.t2 + static_cast<long>(min(m0 + r, p.M - 1)) * MID + 8 * cq);
     }
 #pragma unroll
     for (int e = 0; e < N; ++e) {
-      int r, cq;
-      rc(tid + 512 * e, r, cq);
+      const int g = tid + 512 * e;
+      const int r = g / (MID / 8), cq = g % (MID / 8);
       *reinterpret_cast<uint4*>(t2s + (cq >> 2) * KBS + r * 64 + (((cq & 3) ^ pswz(r)) << 4)) = v[e];
     }
   }
@@ -375,18 +360,17 @@ __global__ __launch_bounds__(512) void conv_pair_kernel(const PairParams p) {
 #endif
 }
 
-template <int MID, int C4, int MIDN, int BM, bool KF = true, bool SP = false, bool F16 = false, bool YW = false,
-          bool PL = false>
+template <int MID, int C4, int MIDN, int BM, bool KF = true, bool SP = false, bool F16 = false, bool YW = false>
 int launch_pair(const PairParams& p, hipStream_t s) {
   constexpr int LDS = (MID / 32 + 2 * PR_CH / 32 > MIDN / 32 ? MID / 32 + 2 * PR_CH / 32 : MIDN / 32) * kbs<BM>();
   static bool attr = false;
   if (!attr) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(conv_pair_kernel<MID, C4, MIDN, BM, KF, SP, F16, YW, PL>),
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(conv_pair_kernel<MID, C4, MIDN, BM, KF, SP, F16, YW>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, LDS) != hipSuccess)
       return AI4E_ELAUNCH;
     attr = true;
   }
-  hipLaunchKernelGGL((conv_pair_kernel<MID, C4, MIDN, BM, KF, SP, F16, YW, PL>), dim3(ai4e_cdiv(p.M, BM)), dim3(512), LDS, s, p);
+  hipLaunchKernelGGL((conv_pair_kernel<MID, C4, MIDN, BM, KF, SP, F16, YW>), dim3(ai4e_cdiv(p.M, BM)), dim3(512), LDS, s, p);
   return hipGetLastError() == hipSuccess ? AI4E_OK : AI4E_ELAUNCH;
 }
 
@@ -453,7 +437,6 @@ AI4E_API int ai4e_conv_pair_fwd(const void* t2, const void* w3p, const void* b3,
       case 99:  // -0.7 % of the serial forward, bit-identical, profiles/r6_pair_yw/)
         return launch_pair<256, 1024, 256, 96, true, true, false, true>(p, stream);
       case 98: return launch_pair<256, 1024, 256, 96, true, true>(p, stream);  // A/B reference: 8-B Y writes
-      case 100: return launch_pair<256, 1024, 256, 96, true, true, false, true, true>(p, stream);  // + PL (A/B)
       case 96: return launch_pair<256, 1024, 256, 96>(p, stream);  // A/B reference: the burst after the Y barrier
       case 64: return launch_pair<256, 1024, 256, 64>(p, stream);
       case 97: return launch_pair<256, 1024, 256, 96, false>(p, stream);  // A/B: scheduler-placed fragment reads

@@ -45,8 +45,6 @@ CASES = [
     (1, 3, 5, 512, 98),
     (8, 14, 14, 256, 99),     # 16-B Y writes (fragment pairs swapped with v_permlane16_swap)
     (1, 5, 7, 256, 99),       # ... with a partial tile
-    (8, 14, 14, 256, 100),    # + block-major T2 prologue copy
-    (1, 5, 7, 256, 100),
 ]
 
 
@@ -59,10 +57,8 @@ def test_conv_pair_yw_bit_identical():
     res = torch.randn(9, 14, 14, 1024, device=DEV).to(torch.bfloat16)
     a = conv_pair(t2, c3, res, c1n, tile_cfg=98)
     b = conv_pair(t2, c3, res, c1n, tile_cfg=99)
-    c = conv_pair(t2, c3, res, c1n, tile_cfg=100)
     torch.cuda.synchronize()
     assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
-    assert torch.equal(a[0], c[0]) and torch.equal(a[1], c[1])
 
 
 @pytest.mark.parametrize("case", CASES)
