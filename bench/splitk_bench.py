@@ -26,6 +26,7 @@ SHAPES = [
     ("l3_down", 512, 1024, 1, 2, 0, 28, 28, False),
     ("l4_c1_first", 1024, 512, 1, 1, 0, 14, 14, False),
     ("l2_c1_first", 256, 128, 1, 1, 0, 56, 56, False),
+    ("fc", 2048, 1000, 1, 1, 0, 1, 1, False),          # the classifier (1x1 conv over the pooled features)
     # the detector's backbone / FPN (batch 32 at 640^2) and the U-Net's deepest level (16 tiles of 512^2)
     ("det_l4_c2_s2", 512, 512, 3, 2, 1, 40, 40, False, 32),
     ("det_l4_c2", 512, 512, 3, 1, 1, 20, 20, False, 32),
