@@ -918,7 +918,10 @@ __global__ __launch_bounds__(512) void conv_igemm256_kernel(const ConvParams p) 
     if (traffic) {
       // two accumulator rows (8 loads) in flight at a time (the offsets of a row in SGPRs: VGPR offsets spilled
       // the 256-pixel tile)
-      constexpr int RB = 2;
+#ifndef AI4E_SK_RB
+#define AI4E_SK_RB 2
+#endif
+      constexpr int RB = AI4E_SK_RB < MFR ? AI4E_SK_RB : MFR;
 #pragma unroll
       for (int i = 0; i < MFR; i += RB) {
 #pragma unroll
