@@ -7,7 +7,7 @@ box-to-box and run-to-run drift cancel (a single bench.py run varies by a few % 
 MODEL: resnet (batch 250 at 224^2), detector (batch 32 at 640^2) or unet (16 tiles of 512^2). TABLE_B: a JSON tile
 table (ops/conv_tiles.json format), or ``NAME=VALUE[,NAME=VALUE]`` module switches of ops/conv.py for B (e.g.
 ``PAIR_X=1``, ``PAIR_TILE=64``: the values its environment variables would set; ``net.par_down=1``: a model
-attribute); A is the committed state. Prints one JSON line: median ms per forward of each,
+attribute), comma-separated, a table and switches mixed; A is the committed state. Prints one JSON line: median ms per forward of each,
 B / A, and the largest output difference (split-K reorders fp32 sums only)."""
 import json
 import os
@@ -66,11 +66,11 @@ def main():
     convmod._TILES = None
     ga, oa = capture(net, x)  # committed table
     saved = {}
-    if table_b.endswith(".json"):
-        with open(table_b) as f:
-            convmod._TILES = json.load(f)
-    else:
-        for kv in table_b.split(","):
+    for kv in table_b.split(","):
+        if kv.endswith(".json"):
+            with open(kv) as f:
+                convmod._TILES = json.load(f)
+        else:
             k, v = kv.split("=")
             obj, k = (net, k[4:]) if k.startswith("net.") else (convmod, k)  # net.X: a model attribute
             saved[(obj, k)] = getattr(obj, k)
