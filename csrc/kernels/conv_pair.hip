@@ -413,7 +413,10 @@ AI4E_API int ai4e_conv_pair_f16_fwd(const void* t2, const void* w3p, const void*
   if (!t2 || !w3p || !b3 || !res || !y || !w1p || !b1n || !t1n || M < 0) return AI4E_EINVAL;
   if (mid != 256 || c4 != 1024 || midn != 256 || (bm_cfg != 0 && bm_cfg != 98)) return AI4E_EINVAL;
   if (M == 0) return AI4E_OK;
-  return launch_pair<256, 1024, 256, 96, true, true, true>(pair_params(t2, w3p, b3, res, y, w1p, b1n, t1n, M), stream);
+  // 16-B Y writes (YW) as the bf16 default: epilogue8<true> runs the same fp16 dot2 residual adds, cvt and sign-bit
+  // ReLU as the 8-B form, so the bits are the same
+  return launch_pair<256, 1024, 256, 96, true, true, true, true>(pair_params(t2, w3p, b3, res, y, w1p, b1n, t1n, M),
+                                                                 stream);
 }
 
 AI4E_API int ai4e_conv_pair_fwd(const void* t2, const void* w3p, const void* b3, const void* res, void* y,
