@@ -335,12 +335,26 @@ __global__ __launch_bounds__(512) void conv_pair_kernel(const PairParams p) {
   // ---- T1' epilogue through the T2 region (every wave finished its last B phase before the last barrier);
   // a T1' wider than T2 (layer3 -> layer4's 512-wide c1) also spans the Y buffers: wait for every wave's C phase
   if constexpr (MIDN / 32 * KBS > T2_BYTES) pbarrier();
+  if constexpr (YW && JC == 2) {
+    // the wave's two 16-channel blocks form one 32-channel K block: swapped, each lane holds 8 consecutive channels
+    // (16-B chunk ((lg & 1) << 1) | (lg >> 1) of the block) of one pixel and writes them with one 16-B store
 #pragma unroll
-  for (int i = 0; i < FI; ++i)
+    for (int i = 0; i < FI; ++i) {
+      f32x4_t a = accn[i][0], b = accn[i][1];
+      pswap16(a, b);
+      const int r = 16 * i + frow, q = ((lg & 1) << 1) | (lg >> 1);
+      *reinterpret_cast<uint4*>(t2s + w * KBS + r * 64 + ((q ^ pswz(r)) << 4)) =
+          make_uint4(pack_relu2<F16>(a[0], a[1]), pack_relu2<F16>(a[2], a[3]), pack_relu2<F16>(b[0], b[1]),
+                     pack_relu2<F16>(b[2], b[3]));
+    }
+  } else {
 #pragma unroll
-    for (int j = 0; j < JC; ++j)
-      *reinterpret_cast<uint2*>(t2s + poff<BM>(16 * i + frow, (w * JC + j) * 16 + 4 * lg)) =
-          make_uint2(pack_relu2<F16>(accn[i][j][0], accn[i][j][1]), pack_relu2<F16>(accn[i][j][2], accn[i][j][3]));
+    for (int i = 0; i < FI; ++i)
+#pragma unroll
+      for (int j = 0; j < JC; ++j)
+        *reinterpret_cast<uint2*>(t2s + poff<BM>(16 * i + frow, (w * JC + j) * 16 + 4 * lg)) =
+            make_uint2(pack_relu2<F16>(accn[i][j][0], accn[i][j][1]), pack_relu2<F16>(accn[i][j][2], accn[i][j][3]));
+  }
   pbarrier();
   constexpr int NT = BM * MIDN / 8 / 512;
 #pragma unroll
